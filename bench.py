@@ -1,0 +1,301 @@
+"""Benchmark of the CoDA hot path on MI355X (driver contract: one JSON line from rank 0).
+
+Headline (BASELINE.json configs[1]): ResNet-50 CoDA, bf16 autocast backbone,
+batch 256 per GPU, 224x224 synthetic inputs already resident in HBM, p=0.1,
+fused AUC surrogate + primal-dual update kernels, CoDA averaging every I=16
+steps over RCCL. A step = label map/p_hat + forward + fused loss + backward +
+update (+ the averaging round when t % I == 0). value = images/s of the whole
+job (all ranks), timed over exactly --steps steps between barriers.
+
+Second leg (configs[3]): exact AUC of 2^24 fp32 scores at 1 % positives, the
+pair count sharded by positive blocks over the ranks with one int64 all-reduce.
+
+Kernel timing: HIP events recorded on the stream each kernel is launched on
+(torch's current stream, which is the stream libdauc.so receives), around every
+launch inside the timed region. roofline.achieved = algorithmic bytes per launch
+/ average launch duration.
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parent
+sys.path.insert(0, str(REPO))
+os.environ.setdefault("MIOPEN_FIND_MODE", "FAST")
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+VALU_PAIR_PEAK = 1.97e13     # 256 CU x 2.4 GHz x 64 lanes / 2 compares per pair
+METRIC = "CoDA train imgs/sec + exact-AUC pos×neg pairs/sec at 1/2/4/8 MI355X"
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--arch", default="resnet50")
+    p.add_argument("--batch", type=int, default=256)
+    p.add_argument("--image-size", type=int, default=224)
+    p.add_argument("--I", type=int, default=16)
+    p.add_argument("--pos-ratio", type=float, default=0.1)
+    p.add_argument("--pool", type=int, default=4, help="distinct resident input batches cycled")
+    p.add_argument("--auc-log2n", type=int, default=24)
+    p.add_argument("--auc-pos", type=float, default=0.01)
+    p.add_argument("--auc-reps", type=int, default=3)
+    p.add_argument("--variant", type=int, default=0, help="pair-count kernel variant")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-auc", action="store_true")
+    p.add_argument("--no-train", action="store_true")
+    return p.parse_args()
+
+
+class KernelTimer:
+    """Wraps an ops function: HIP events on the launch stream around every call while enabled."""
+
+    def __init__(self, module, name):
+        self.module, self.name = module, name
+        self.fn = getattr(module, name)
+        self.pairs = []
+        self.enabled = False
+
+        def wrapped(*a, **k):
+            if not self.enabled:
+                return self.fn(*a, **k)
+            s = torch.cuda.current_stream()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(s)
+            r = self.fn(*a, **k)
+            e1.record(s)
+            self.pairs.append((e0, e1))
+            return r
+
+        setattr(module, name, wrapped)
+
+    def mean_ms(self):
+        torch.cuda.synchronize()
+        return float(np.mean([a.elapsed_time(b) for a, b in self.pairs])) if self.pairs else float("nan")
+
+
+def max_over_ranks(x: float, world: int) -> float:
+    if world == 1:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def bench_train(args, world, rank, device):
+    from distributedauc_amd import ops
+    from distributedauc_amd.backbone import build_backbone
+    from distributedauc_amd.coda import CoDA
+    from distributedauc_amd.loader import DeviceLoader, SyntheticImageNet, imagenet_like_labels
+
+    torch.manual_seed(1234)
+    split = 499
+    labels = imagenet_like_labels(1 << 16, 1000, split, pos_ratio=args.pos_ratio, seed=123 + rank)
+    ds = SyntheticImageNet(labels, args.image_size, split)
+    loader = DeviceLoader(ds, np.arange(len(labels)), args.batch, device, seed=1234 + rank,
+                          channels_last=True, pool=args.pool)
+    net = build_backbone(args.arch, num_classes=2).to(device).to(memory_format=torch.channels_last)
+    coda = CoDA(net, lr=0.1, gamma=2000.0, T0=10 ** 9, I=args.I, split_index=split, world=world, rank=rank,
+                autocast_dtype=torch.bfloat16, device=device)
+    it = iter(loader)
+    coda.average_all()            # main.py:141-142
+    coda.begin_stage(1, it)       # alpha estimate + anchors (untimed)
+    upd = KernelTimer(ops, "pd_update")
+    sur = KernelTimer(ops, "surrogate_fwdbwd")
+    for _ in range(args.warmup):
+        x, y = next(it)
+        coda.train_step(x, y)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    upd.enabled = sur.enabled = True
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        x, y = next(it)
+        coda.train_step(x, y)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    upd.enabled = sur.enabled = False
+    dt = max_over_ranks(dt, world)
+    loss = float(coda.last_loss.item())
+    n_params = coda.state.numel()
+    upd_ms = upd.mean_ms()
+    upd_bytes = coda.state.bytes_per_update(True)
+    sur_ms = sur.mean_ms()
+    return {
+        "dt": dt, "imgs": world * args.batch * args.steps, "loss": loss, "n_params": n_params,
+        "update_ms": upd_ms, "update_bytes": upd_bytes, "surrogate_us": sur_ms * 1e3,
+    }
+
+
+def bench_auc(args, world, rank, device):
+    from distributedauc_amd import ops
+    from distributedauc_amd.auc import ExactAUC
+
+    n = 1 << args.auc_log2n
+    g = torch.Generator(device=device).manual_seed(2024)  # same scores on every rank
+    s = torch.rand(n, generator=g, device=device)
+    y = torch.where(torch.rand(n, generator=g, device=device) < args.auc_pos, 1, -1).to(torch.int8)
+    ev = ExactAUC(world=world, rank=rank, variant=args.variant)
+    pc = KernelTimer(ops, "pair_count")
+    c = ev.counts(y, s)  # warm-up (also compiles nothing: AOT code object)
+    times = []
+    pc.enabled = True
+    for _ in range(args.auc_reps):
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        c = ev.counts(y, s)
+        torch.cuda.synchronize()
+        times.append(time.perf_counter() - t0)
+    pc.enabled = False
+    t_eval = max_over_ranks(float(np.median(times)), world)
+    t_count = max_over_ranks(pc.mean_ms() / 1e3, world)
+    pairs = c["P"] * c["N"]
+    return {"n": n, "P": c["P"], "N": c["N"], "wins": c["wins"], "ties": c["ties"],
+            "auc": ExactAUC.from_counts(c), "t_eval": t_eval, "t_count": t_count, "pairs": pairs,
+            "scores": s, "labels": y}
+
+
+def cpu_baseline_train(args):
+    """The reference's CPU path on a bounded sample: torch-CPU ResNet-50 fwd, verbatim loss
+    (main.py:313-317), autograd, per-tensor dppd_sg (main.py:56-64) + running average."""
+    from distributedauc_amd.backbone import build_backbone
+    from oracle import reference_cpu as R
+
+    torch.manual_seed(0)
+    B, steps = 32, 2
+    net = build_backbone(args.arch, num_classes=2)
+    net0 = {k: v.clone() for k, v in net.state_dict().items()}
+    avg = {k: v.clone() for k, v in net.state_dict().items()}
+    a, b, alpha = (torch.zeros(1, requires_grad=True) for _ in range(3))
+    x = torch.randn(B, 3, args.image_size, args.image_size)
+    lab = torch.where(torch.rand(B) < args.pos_ratio, 1, -1)
+    p = torch.tensor([args.pos_ratio])
+
+    def step():
+        h = net(x)[:, 1]
+        loss = R.surrogate_loss(h, lab, a, b, alpha, p)
+        net.zero_grad()
+        loss.backward()
+        with torch.no_grad():
+            for name, prm in net.named_parameters():
+                prm.data = R.pd_step(prm.data, prm.grad.data, net0[name], 0.1, 2000.0)
+                avg[name] = avg[name] + prm.data
+
+    step()  # warm-up
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    dt = time.perf_counter() - t0
+    return {"value": B * steps / dt, "unit": "imgs/sec", "cores": torch.get_num_threads(), "kind": "port",
+            "sample": f"{args.arch} {args.image_size}x{args.image_size} batch {B}, {steps} timed steps "
+                      f"(fwd + reference loss + backward + per-tensor dppd_sg + running average), torch CPU fp32"}
+
+
+def cpu_baseline_auc(auc_res):
+    """sklearn roc_curve + auc (main.py:79-81) on the same scores: the reference CPU path."""
+    from oracle import reference_cpu as R
+
+    s = auc_res["scores"].cpu().numpy()
+    y = auc_res["labels"].cpu().numpy().astype(np.int64)
+    t0 = time.perf_counter()
+    ref = R.auc_sklearn(y, s)
+    dt = time.perf_counter() - t0
+    return {"value": auc_res["pairs"] / dt, "unit": "pairs/sec (effective: P*N / wall)", "cores": 1,
+            "kind": "port", "seconds": dt, "auc": ref,
+            "auc_abs_diff": abs(ref - auc_res["auc"]),
+            "sample": f"full 2^{int(np.log2(auc_res['n']))} scores, sklearn roc_curve+auc (single-threaded sort)"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=device)
+    if args.gpus != world and rank == 0:
+        print(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using {world}", file=sys.stderr)
+
+    res = bench_train(args, world, rank, device) if not args.no_train else None
+    auc = bench_auc(args, world, rank, device) if not args.no_auc else None
+
+    if rank == 0:
+        out = {"metric": METRIC}
+        if res is not None:
+            upd_gbs = res["update_bytes"] / (res["update_ms"] / 1e3) / 1e9
+            out.update({
+                "value": res["imgs"] / res["dt"], "unit": "imgs/sec", "n_gpus": world, "steps": args.steps,
+                "warmup": args.warmup, "ms_per_step": res["dt"] / args.steps * 1e3, "higher_is_better": True,
+                "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+                "config": {"workload": f"{args.arch} CoDA, bf16 autocast backbone, fp32 AUC kernels "
+                                       "(BASELINE configs[1])",
+                           "global_batch": args.batch * world, "image_size": args.image_size, "I": args.I,
+                           "pos_ratio": args.pos_ratio, "parallelism": f"dp{world}", "params": res["n_params"]},
+                "roofline": {"kernel": "dauc_pd_update (fused dppd_sg + running average)", "bound": "hbm",
+                             "achieved": upd_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                             "frac": upd_gbs / HBM_PEAK_GBS, "traffic": load_traffic("pd_update"),
+                             "bytes_per_launch": res["update_bytes"], "avg_launch_us": res["update_ms"] * 1e3},
+                "surrogate_us_per_call": res["surrogate_us"],
+                "final_loss": res["loss"],
+            })
+        if auc is not None:
+            per_gpu = auc["pairs"] / auc["t_count"] / world
+            out["auc_eval"] = {
+                "workload": f"exact AUC, 2^{args.auc_log2n} fp32 scores, {args.auc_pos:.0%} positives "
+                            "(BASELINE configs[3]), pair count sharded by positive blocks",
+                "pairs_per_sec": auc["pairs"] / auc["t_count"], "eval_pairs_per_sec": auc["pairs"] / auc["t_eval"],
+                "eval_ms": auc["t_eval"] * 1e3, "count_ms": auc["t_count"] * 1e3, "P": auc["P"], "N": auc["N"],
+                "wins": auc["wins"], "ties": auc["ties"], "auc": auc["auc"],
+                "roofline": {"kernel": "dauc_pair_count", "bound": "valu", "achieved": per_gpu,
+                             "peak": VALU_PAIR_PEAK, "unit": "pairs/s per GPU", "frac": per_gpu / VALU_PAIR_PEAK},
+            }
+        if world == 1 and not args.no_cpu_baseline:
+            torch.set_num_threads(min(16, os.cpu_count() or 1))
+            if res is not None:
+                out["cpu_baseline"] = cpu_baseline_train(args)
+            if auc is not None:
+                out.setdefault("auc_eval", {})["cpu_baseline"] = cpu_baseline_auc(auc)
+        else:
+            out["cpu_baseline"] = None
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def load_traffic(kernel: str):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/), or None."""
+    f = REPO / "profiles" / "traffic.json"
+    if not f.exists():
+        return None
+    try:
+        return json.loads(f.read_text()).get(kernel)
+    except Exception:
+        return None
+
+
+if __name__ == "__main__":
+    main()

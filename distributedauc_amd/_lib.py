@@ -1,0 +1,96 @@
+"""ctypes binding of libdauc.so — the C ABI declared in include/dauc.h.
+
+The product path has exactly one implementation: the gfx950 HIP kernels in
+this library. If the library is missing or cannot be loaded this module raises
+immediately; there is no CPU fallback anywhere in ``distributedauc_amd``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+from pathlib import Path
+
+PKG_DIR = Path(__file__).resolve().parent
+LIB_PATH = Path(os.environ.get("DAUC_LIB", PKG_DIR / "libdauc.so"))
+HEADER = PKG_DIR.parent / "include" / "dauc.h"
+
+DAUC_OK = 0
+DAUC_EINVAL = -100000
+LABEL_I8, LABEL_I32, LABEL_I64 = 1, 2, 3
+MODE_REFERENCE, MODE_PAPER = 0, 1
+
+
+class DaucError(RuntimeError):
+    """A libdauc.so call returned a non-zero status."""
+
+
+class GradSeg(ctypes.Structure):
+    """dauc_grad_seg: one parameter's gradient and its offset in the flat buffer."""
+
+    _fields_ = [("grad", ctypes.c_void_p), ("offset", ctypes.c_int64), ("numel", ctypes.c_int64)]
+
+
+_vp = ctypes.c_void_p
+_i64 = ctypes.c_int64
+_int = ctypes.c_int
+_f32 = ctypes.c_float
+_sz = ctypes.c_size_t
+
+# name -> (restype, argtypes); must list every function include/dauc.h declares
+SIGNATURES = {
+    "dauc_version": (_int, []),
+    "dauc_strerror": (ctypes.c_char_p, [_int]),
+    "dauc_label_map_phat": (_int, [_vp, _i64, _i64, _vp, _vp, _vp, _vp, _vp]),
+    "dauc_surrogate_workspace_size": (_sz, [_i64]),
+    "dauc_surrogate_fwdbwd": (_int, [_vp, _i64, _vp, _int, _i64, _vp, _vp, _vp, _i64, _vp, _vp, _vp,
+                                     _vp, _sz, _vp]),
+    "dauc_class_sums": (_int, [_vp, _i64, _vp, _int, _i64, _vp, _int, _vp, _sz, _vp]),
+    "dauc_alpha_from_sums": (_int, [_vp, _vp, _vp]),
+    "dauc_pd_update": (_int, [_vp, _vp, _vp, ctypes.POINTER(GradSeg), _int, _vp, _vp, _vp, _f32, _f32,
+                              _int, _vp]),
+    "dauc_pd_update_dense": (_int, [_vp, _vp, _vp, _vp, _i64, _f32, _f32, _vp]),
+    "dauc_coda_finalize": (_int, [_vp, _i64, _int, _vp, _vp, _vp]),
+    "dauc_scale_div": (_int, [_vp, _i64, _f32, _vp]),
+    "dauc_split_workspace_size": (_sz, [_i64]),
+    "dauc_split_scores": (_int, [_vp, _vp, _int, _i64, _vp, _vp, _vp, _vp, _sz, _vp]),
+    "dauc_pair_count": (_int, [_vp, _i64, _vp, _i64, _vp, _vp]),
+    "dauc_pair_count_variant": (_int, [_vp, _i64, _vp, _i64, _vp, _int, _vp]),
+}
+
+_lib = None
+
+
+def header_functions(header: Path = HEADER) -> list[str]:
+    """Names of every function the C header declares (used by the ABI tests)."""
+    text = re.sub(r"/\*.*?\*/", "", header.read_text(), flags=re.S)
+    return sorted(set(re.findall(r"\b(dauc_[a-z0-9_]+)\s*\(", text)) - {"dauc_grad_seg"})
+
+
+def load() -> ctypes.CDLL:
+    """Load libdauc.so and attach the prototypes. Raises if it is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not LIB_PATH.exists():
+        raise ImportError(
+            f"{LIB_PATH} not found: the HIP library must be built first "
+            "(python -c 'import __graft_entry__ as g; g.build()' or python distributedauc_amd/build.py). "
+            "distributedauc_amd has no CPU fallback."
+        )
+    lib = ctypes.CDLL(str(LIB_PATH))
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def strerror(rc: int) -> str:
+    return load().dauc_strerror(rc).decode()
+
+
+def check(rc: int, what: str) -> None:
+    if rc != DAUC_OK:
+        raise DaucError(f"{what} failed: {strerror(rc)} (status {rc})")

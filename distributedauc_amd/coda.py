@@ -1,0 +1,181 @@
+"""CoDA: one rank's proximal primal-dual SGD with periodic model averaging.
+
+Restates the training loop of main.py:83-339 on the flat HBM state
+(flat.FlatState), with the hot path in HIP kernels:
+
+  per step     label map + p_hat          1 launch  (dauc_label_map_phat)     main.py:303-310
+               backbone forward           PyTorch-ROCm (MIOpen), bf16 autocast main.py:311
+               surrogate loss + grads     1 launch  (dauc_surrogate_fwdbwd)   main.py:313-317, 326
+               backbone backward          PyTorch-ROCm
+               dppd_sg + running average  1 launch  (dauc_pd_update)          main.py:327, 333-334
+  every I      all-reduce of flat[:n_reduce] over RCCL (params, a, b, alpha, class counts)
+               + 1 launch (dauc_coda_finalize)                                main.py:292-301, 33-54
+  per stage    alpha estimate: class sums (1 launch per batch), all-reduce,
+               dauc_alpha_from_sums; anchor/average snapshots; stage-end divide main.py:144-208, 338-339
+
+There is no host synchronisation inside a step (the reference syncs for p_hat
+at main.py:309-310 every step). The reference's quirks are the
+default (mode="reference"); mode="paper" applies the intended dual ascent.
+"""
+from __future__ import annotations
+
+import contextlib
+from typing import Callable, Iterator
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+
+from . import ops
+from .flat import FlatState
+from .surrogate import auc_surrogate
+
+
+class CoDA:
+    """CoDA state machine for one rank (main.py:83-339)."""
+
+    def __init__(self, model: nn.Module, *, lr: float = 0.1, gamma: float = 2000.0, T0: int = 5000,
+                 I: int = 2, split_index: int = 4, mode: str = "reference", world: int = 1, rank: int = 0,
+                 group=None, autocast_dtype: torch.dtype | None = None, device=None,
+                 max_exact_count: int = 1 << 24):
+        if I < 1:
+            raise ValueError("averaging period I must be >= 1")
+        ops.mode_code(mode)  # validates
+        self.model = model
+        self.state = FlatState(model, device)
+        self.device = self.state.device
+        self.lr0 = float(lr)
+        self.gamma = float(gamma)
+        self.T0 = int(T0)
+        self.I = int(I)
+        self.split_index = int(split_index)
+        self.mode = mode
+        self.world = int(world)
+        self.rank = int(rank)
+        self.group = group
+        self.autocast_dtype = autocast_dtype
+        self.max_exact_count = max_exact_count
+        self.t_total = 0
+        self.stage = 0
+        self.T = 0
+        self.lr = self.lr0
+        self.end_all = False
+        self._sums4 = torch.zeros(4, dtype=torch.float64, device=self.device)
+        self._scratch = torch.zeros(8, dtype=torch.float32, device=self.device)
+        self._ab_stage = torch.zeros(2, dtype=torch.float32, device=self.device)
+        self.last_loss: torch.Tensor | None = None
+
+    # ---------------------------------------------------------------- plumbing
+    def _autocast(self):
+        if self.autocast_dtype is None:
+            return contextlib.nullcontext()
+        return torch.autocast(device_type="cuda", dtype=self.autocast_dtype)
+
+    def scores(self, x: torch.Tensor) -> torch.Tensor:
+        """h = net(x)[:, 1] (resnet.py:218: column 1 of the softmax), fp32."""
+        with self._autocast():
+            out = self.model(x)
+        h = out[:, 1]
+        return h if h.dtype == torch.float32 else h.float()
+
+    # ---------------------------------------------------------------- a6
+    def average_all(self):
+        """One CoDA round: main.py:40-54 (world > 1) / 297-299 (world == 1), then 300-301."""
+        st = self.state
+        if self.world > 1:
+            dist.all_reduce(st.flat[: st.n_reduce], op=dist.ReduceOp.SUM, group=self.group)
+        ops.coda_finalize(st.flat, st.n_avg, self.world, st.lcounts, st.gcounts)
+
+    # ---------------------------------------------------------------- a7
+    def begin_stage(self, s: int, batches: Iterator):
+        """main.py:148-208: restart point, alpha estimate over 3**s batches, snapshots, T, lr."""
+        st = self.state
+        with torch.no_grad():
+            if s > 1:
+                st.params.copy_(st.avg)                 # main.py:149-150 (avg already / T)
+                st.abalpha[:2].copy_(self._ab_stage)    # main.py:151-152
+            self.model.eval()
+            self._sums4.zero_()
+            for _ in range(3 ** s):                     # main.py:172-188
+                x, labels = next(batches)
+                y8 = st.y8(labels.numel())
+                self._scratch.zero_()
+                ops.label_map_phat(labels, self.split_index, y8, self._scratch[0:2], self._scratch[2:4],
+                                   self._scratch[4:5])
+                ops.class_sums(self.scores(x), y8, self._sums4, accumulate=True)
+            self.model.train()
+            if self.world > 1:
+                dist.all_reduce(self._sums4, op=dist.ReduceOp.SUM, group=self.group)  # main.py:192-195
+            ops.alpha_from_sums(self._sums4, st.alpha)  # main.py:197
+            st.snapshot_anchor()                        # main.py:154 + 199-201
+            self._ab_stage.copy_(st.abalpha[:2])        # a_average, b_average (main.py:207-208)
+            st.reset_average()                          # main.py:206
+        self.stage = s
+        self.T = self.T0 * (3 ** (s - 1))               # main.py:202
+        self.lr = self.lr0 * ((1 / 3) ** (s - 1))       # main.py:203
+
+    def end_stage(self):
+        """main.py:338-339: net_average /= T."""
+        ops.scale_div(self.state.avg, float(self.T))
+
+    # ---------------------------------------------------------------- a1-a5
+    def train_step(self, x: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
+        """main.py:289-334 for one batch already on the device. Returns the loss (device scalar)."""
+        st = self.state
+        B = labels.numel()
+        if self.world * self.I * B >= self.max_exact_count:
+            raise ValueError("world*I*batch must stay below 2^24 so the fp32 count slots stay exact")
+        self.t_total += 1
+        if self.t_total % self.I == 0:
+            with torch.no_grad():
+                self.average_all()
+        y8 = st.y8(B)
+        ops.label_map_phat(labels, self.split_index, y8, st.lcounts, st.gcounts, st.p_hat)
+        h = self.scores(x)
+        loss = auc_surrogate(h, y8, st.abalpha, st.p_hat, st.grad3)
+        loss.backward()
+        st.update(self.lr, self.gamma, self.mode)
+        self.model.zero_grad(set_to_none=True)
+        self.last_loss = loss.detach()
+        return self.last_loss
+
+    # ---------------------------------------------------------------- loop
+    def run(self, batches: Iterator, *, num_stages: int, total_iter: int, test_freq: int | None = None,
+            evaluate: Callable[["CoDA"], None] | None = None,
+            on_step: Callable[["CoDA"], None] | None = None):
+        """The full schedule of main.py:140-339 (stages 1 .. num_stages-1).
+
+        ``on_step`` (optional) is called after every training step (history, tests).
+        """
+        with torch.no_grad():
+            self.average_all()  # main.py:141-142
+        for s in range(1, num_stages):
+            if self.end_all:
+                break
+            self.begin_stage(s, batches)
+            for _ in range(self.T):
+                if test_freq and evaluate is not None and self.t_total % test_freq == 0:
+                    evaluate(self)  # main.py:215-270
+                if self.t_total > total_iter:  # main.py:273-275
+                    self.end_all = True
+                    break
+                x, labels = next(batches)
+                self.train_step(x, labels)
+                if on_step is not None:
+                    on_step(self)
+            self.end_stage()
+
+    def stage_lengths(self, num_stages: int) -> list[int]:
+        return [self.T0 * 3 ** (s - 1) for s in range(1, num_stages)]
+
+    @staticmethod
+    def p_prior(split_index: int, neg_keep_ratio: float, num_classes: int = 1000) -> float:
+        """main.py:86-87: the positive prior used only for the run label."""
+        p_pos = (split_index + 1.0) / num_classes
+        return p_pos / (p_pos + (1 - p_pos) * neg_keep_ratio)
+
+    def __repr__(self):
+        n = self.state.numel()
+        return (f"CoDA(params={n}, I={self.I}, T0={self.T0}, lr0={self.lr0}, gamma={self.gamma}, "
+                f"mode={self.mode}, world={self.world}, rank={self.rank}, flat_MB={4 * n / 2**20:.1f})")
+

@@ -1,0 +1,268 @@
+// Proximal primal-dual SGD update over the flat parameter buffer, fused with
+// the per-step running average; CoDA round finalisation; stage-end division.
+//
+// Reference: imagenet/main.py:56-64 (dppd_sg), main.py:333-334 (running
+// average), main.py:33-54 + 297-301 (average_all / count folding),
+// main.py:338-339 (stage-end division).
+//
+// HBM traffic per parameter: read w, g, w0 (12 B) + write w (4 B) = 16 B, plus
+// read+write of the running average (8 B) = 24 B when fused. Every element is
+// touched exactly once, 16 B per lane per access (float4), one launch for all
+// parameter tensors: the gradients stay where autograd left them and are found
+// through a segment table passed in the kernel arguments.
+//
+// Numerics: the fp32 operation order of main.py:61 with every operation
+// rounded separately (no FMA contraction), so the result is bit-identical to
+// the reference's torch fp32 ops: w' = w - lr*(g + (1/gamma)*(w - w0)).
+
+#include "dauc_internal.h"
+
+namespace dauc {
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kVecPerThread = 4;                                   // float4 per thread
+constexpr int64_t kElemsPerBlock = int64_t(kThreads) * 4 * kVecPerThread;  // 4096 floats
+constexpr int kMaxSeg = 96;                                       // segments per launch
+
+struct SegTable {
+    int nseg;
+    int blk_start[kMaxSeg + 1];  // first block of each segment; blk_start[nseg] = grid
+    const float* grad[kMaxSeg];
+    int64_t offset[kMaxSeg];
+    int64_t numel[kMaxSeg];
+};
+
+__device__ __forceinline__ float pd_step(float w, float g, float w0, float lr, float invg) {
+    const float d = __fsub_rn(w, w0);       // (param.data - model0[name])
+    const float t = __fmul_rn(invg, d);     // 1/gamma * (...)
+    const float gp = __fadd_rn(g, t);       // param.grad.data + ...
+    const float u = __fmul_rn(lr, gp);      // lr * (...)
+    return __fsub_rn(w, u);                 // param.data - ...
+}
+
+__device__ void scalar_update(float* s, const float* g3, const float* a3, float lr, float invg,
+                              int mode) {
+    const float a = s[0], b = s[1], al = s[2];
+    const float a_new = pd_step(a, g3[0], a3[0], lr, invg);   // main.py:58
+    float b_new, al_new;
+    if (mode == DAUC_MODE_PAPER) {
+        b_new = pd_step(b, g3[1], a3[1], lr, invg);           // intended (b - b0)
+        al_new = __fadd_rn(al, __fmul_rn(lr, g3[2]));         // dual ascent
+    } else {
+        // main.py:59 uses the UPDATED a in b's proximal term; main.py:64 only
+        // rebinds a local name, so alpha is left unchanged.
+        const float t = __fmul_rn(invg, __fsub_rn(a_new, a3[0]));
+        b_new = __fsub_rn(b, __fmul_rn(lr, __fadd_rn(g3[1], t)));
+        al_new = al;
+    }
+    s[0] = a_new;
+    s[1] = b_new;
+    s[2] = al_new;
+}
+
+template <bool AVG>
+__global__ __launch_bounds__(kThreads) void pd_update_kernel(
+    float* __restrict__ w, const float* __restrict__ w0, float* __restrict__ wavg, SegTable tab,
+    float lr, float invg, float* __restrict__ scalars, const float* __restrict__ grad3,
+    const float* __restrict__ anchor3, int mode) {
+    const int bid = blockIdx.x;
+    if (scalars != nullptr && bid == 0 && threadIdx.x == 0)
+        scalar_update(scalars, grad3, anchor3, lr, invg, mode);
+
+    // segment owning this block (wave-uniform binary search over kernel args)
+    int lo = 0, hi = tab.nseg - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (tab.blk_start[mid] <= bid) lo = mid;
+        else hi = mid - 1;
+    }
+    const float* __restrict__ g = tab.grad[lo];
+    const int64_t off = tab.offset[lo];
+    const int64_t n = tab.numel[lo];
+    const int64_t e0 = int64_t(bid - tab.blk_start[lo]) * kElemsPerBlock;
+    float* __restrict__ ws = w + off;
+    const float* __restrict__ w0s = w0 + off;
+    float* __restrict__ as = AVG ? wavg + off : nullptr;
+
+    const bool vec_ok = ((off & 3) == 0) && ((reinterpret_cast<uintptr_t>(g) & 15u) == 0);
+    if (vec_ok && e0 + kElemsPerBlock <= n) {
+        // full block: 4 independent float4 streams per thread, all loads issued first
+        f32x4 wv[kVecPerThread], gv[kVecPerThread], zv[kVecPerThread], av[kVecPerThread];
+#pragma unroll
+        for (int v = 0; v < kVecPerThread; ++v) {
+            const int64_t i = e0 + (int64_t(v) * kThreads + threadIdx.x) * 4;
+            wv[v] = *reinterpret_cast<const f32x4*>(ws + i);
+            gv[v] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(g + i));
+            zv[v] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(w0s + i));
+            if (AVG) av[v] = *reinterpret_cast<const f32x4*>(as + i);
+        }
+#pragma unroll
+        for (int v = 0; v < kVecPerThread; ++v) {
+            const int64_t i = e0 + (int64_t(v) * kThreads + threadIdx.x) * 4;
+            f32x4 r;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) r[c] = pd_step(wv[v][c], gv[v][c], zv[v][c], lr, invg);
+            *reinterpret_cast<f32x4*>(ws + i) = r;
+            if (AVG) {
+                f32x4 a;
+#pragma unroll
+                for (int c = 0; c < 4; ++c) a[c] = __fadd_rn(av[v][c], r[c]);
+                *reinterpret_cast<f32x4*>(as + i) = a;
+            }
+        }
+        return;
+    }
+    // partial or unaligned block: scalar loop over this block's element range
+    const int64_t e1 = (e0 + kElemsPerBlock < n) ? e0 + kElemsPerBlock : n;
+    for (int64_t i = e0 + threadIdx.x; i < e1; i += kThreads) {
+        const float r = pd_step(ws[i], g[i], w0s[i], lr, invg);
+        ws[i] = r;
+        if (AVG) as[i] = __fadd_rn(as[i], r);
+    }
+}
+
+// scalars-only launch (used when the tensor list is empty)
+__global__ void scalar_update_kernel(float* s, const float* g3, const float* a3, float lr,
+                                     float invg, int mode) {
+    scalar_update(s, g3, a3, lr, invg, mode);
+}
+
+int launch_table(float* w, const float* w0, float* wavg, const SegTable& tab, float lr, float invg,
+                 float* scalars, const float* grad3, const float* anchor3, int mode,
+                 hipStream_t st) {
+    const int grid = tab.blk_start[tab.nseg];
+    if (grid <= 0) return DAUC_OK;
+    if (wavg)
+        hipLaunchKernelGGL(pd_update_kernel<true>, dim3(grid), dim3(kThreads), 0, st, w, w0, wavg,
+                           tab, lr, invg, scalars, grad3, anchor3, mode);
+    else
+        hipLaunchKernelGGL(pd_update_kernel<false>, dim3(grid), dim3(kThreads), 0, st, w, w0,
+                           wavg, tab, lr, invg, scalars, grad3, anchor3, mode);
+    return launch_status();
+}
+
+// ---- CoDA finalisation and stage-end division ---------------------------------
+
+template <bool DIV_ONLY>
+__global__ __launch_bounds__(kThreads) void div_kernel(float* __restrict__ x, int64_t n, float d,
+                                                       float* __restrict__ lcounts,
+                                                       float* __restrict__ gcounts) {
+    if (!DIV_ONLY && blockIdx.x == 0 && threadIdx.x == 0) {
+        // main.py:46-50 + 300-301: counts were summed by the all-reduce; fold them
+        // into the fp32 global accumulators and restart the local ones.
+        gcounts[0] = __fadd_rn(gcounts[0], lcounts[0]);
+        gcounts[1] = __fadd_rn(gcounts[1], lcounts[1]);
+        lcounts[0] = 0.0f;
+        lcounts[1] = 0.0f;
+    }
+    const int64_t nvec = (reinterpret_cast<uintptr_t>(x) & 15u) ? 0 : n / 4;
+    const int64_t stride = int64_t(gridDim.x) * kThreads;
+    for (int64_t v = int64_t(blockIdx.x) * kThreads + threadIdx.x; v < nvec; v += stride) {
+        float4 a = reinterpret_cast<float4*>(x)[v];
+        a.x = __fdiv_rn(a.x, d);
+        a.y = __fdiv_rn(a.y, d);
+        a.z = __fdiv_rn(a.z, d);
+        a.w = __fdiv_rn(a.w, d);
+        reinterpret_cast<float4*>(x)[v] = a;
+    }
+    for (int64_t i = nvec * 4 + int64_t(blockIdx.x) * kThreads + threadIdx.x; i < n; i += stride)
+        x[i] = __fdiv_rn(x[i], d);
+}
+
+int div_grid(int64_t n) {
+    int64_t g = (n / 4 + kThreads - 1) / kThreads;
+    if (g < 1) g = 1;
+    if (g > 2048) g = 2048;
+    return static_cast<int>(g);
+}
+
+}  // namespace
+}  // namespace dauc
+
+using namespace dauc;
+
+extern "C" {
+
+int dauc_pd_update(float* w, const float* w0, float* w_avg, const dauc_grad_seg* segs, int nseg,
+                   float* scalars, const float* grad3, const float* anchor3, float lr,
+                   float inv_gamma, int mode, dauc_stream_t stream) {
+    if (w == nullptr || w0 == nullptr || nseg < 0 || (nseg > 0 && segs == nullptr))
+        return DAUC_EINVAL;
+    if (scalars != nullptr && (grad3 == nullptr || anchor3 == nullptr)) return DAUC_EINVAL;
+    if (mode != DAUC_MODE_REFERENCE && mode != DAUC_MODE_PAPER) return DAUC_EINVAL;
+    for (int i = 0; i < nseg; ++i)
+        if (segs[i].numel < 0 || segs[i].offset < 0 || (segs[i].numel > 0 && !segs[i].grad))
+            return DAUC_EINVAL;
+    hipStream_t st = as_hip(stream);
+    if (nseg == 0) {
+        if (scalars == nullptr) return DAUC_OK;
+        hipLaunchKernelGGL(scalar_update_kernel, dim3(1), dim3(1), 0, st, scalars, grad3, anchor3,
+                           lr, inv_gamma, mode);
+        return launch_status();
+    }
+    SegTable tab;
+    int i = 0;
+    bool first = true;
+    while (i < nseg) {
+        tab.nseg = 0;
+        int64_t blocks = 0;
+        while (i < nseg && tab.nseg < kMaxSeg) {
+            const dauc_grad_seg& s = segs[i++];
+            if (s.numel == 0) continue;
+            const int64_t nb = (s.numel + kElemsPerBlock - 1) / kElemsPerBlock;
+            if (blocks + nb > 0x7fffffffLL) return DAUC_EINVAL;
+            tab.blk_start[tab.nseg] = static_cast<int>(blocks);
+            tab.grad[tab.nseg] = s.grad;
+            tab.offset[tab.nseg] = s.offset;
+            tab.numel[tab.nseg] = s.numel;
+            blocks += nb;
+            ++tab.nseg;
+        }
+        tab.blk_start[tab.nseg] = static_cast<int>(blocks);
+        if (tab.nseg == 0) continue;
+        // the scalar part rides in the first launch only
+        const int rc = launch_table(w, w0, w_avg, tab, lr, inv_gamma, first ? scalars : nullptr,
+                                    grad3, anchor3, mode, st);
+        if (rc != DAUC_OK) return rc;
+        first = false;
+    }
+    if (first && scalars != nullptr) {  // every segment was empty
+        hipLaunchKernelGGL(scalar_update_kernel, dim3(1), dim3(1), 0, st, scalars, grad3, anchor3,
+                           lr, inv_gamma, mode);
+        return launch_status();
+    }
+    return DAUC_OK;
+}
+
+int dauc_pd_update_dense(float* w, const float* g, const float* w0, float* w_avg, int64_t n,
+                         float lr, float inv_gamma, dauc_stream_t stream) {
+    if (w == nullptr || g == nullptr || w0 == nullptr || n < 0) return DAUC_EINVAL;
+    if (n == 0) return DAUC_OK;
+    // one segment per 2^31 blocks is far beyond any model; a single table suffices
+    dauc_grad_seg seg{g, 0, n};
+    return dauc_pd_update(w, w0, w_avg, &seg, 1, nullptr, nullptr, nullptr, lr, inv_gamma,
+                          DAUC_MODE_REFERENCE, stream);
+}
+
+int dauc_coda_finalize(float* flat, int64_t n_avg, int world, float* lcounts, float* gcounts,
+                       dauc_stream_t stream) {
+    if (flat == nullptr || n_avg < 0 || world < 1 || lcounts == nullptr || gcounts == nullptr)
+        return DAUC_EINVAL;
+    hipStream_t st = as_hip(stream);
+    // world == 1: the reference skips averaging (main.py:297-299) and only folds counts
+    const int64_t n = world == 1 ? 0 : n_avg;
+    hipLaunchKernelGGL(div_kernel<false>, dim3(div_grid(n)), dim3(kThreads), 0, st, flat, n,
+                       static_cast<float>(world), lcounts, gcounts);
+    return launch_status();
+}
+
+int dauc_scale_div(float* x, int64_t n, float divisor, dauc_stream_t stream) {
+    if (x == nullptr || n < 0) return DAUC_EINVAL;
+    if (n == 0) return DAUC_OK;
+    hipLaunchKernelGGL(div_kernel<true>, dim3(div_grid(n)), dim3(kThreads), 0, as_hip(stream), x,
+                       n, divisor, nullptr, nullptr);
+    return launch_status();
+}
+
+}  // extern "C"

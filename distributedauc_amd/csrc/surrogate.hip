@@ -1,0 +1,346 @@
+// Fused min-max square-loss AUC surrogate (forward + backward in one pass),
+// the per-batch label map / p_hat, and the stage-start class sums.
+//
+// Reference: imagenet/main.py:303-317 (label map, counts, p_hat, inline loss),
+// main.py:326 (its autograd backward) and main.py:166-197 (alpha estimate).
+//
+// HBM layout: h is read with an element stride (2 when it is column 1 of the
+// [B,2] softmax output), labels are int8 (+1/-1) on the fast path, dF/dh is
+// written once. Algorithmic traffic: 4 (h) + 1 (int8 y) + 4 (dh) = 9 B/element.
+// The reductions (six fp64 sums + two counts) are reduced wave -> block -> grid
+// in a fixed order, so results are bitwise reproducible run to run.
+
+#include "dauc_internal.h"
+
+namespace dauc {
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kVec = 4;                                // elements per thread per iteration
+constexpr int kMaxBlocks = 2048;                       // partial slots in the workspace
+constexpr int kPerBlockIter = kThreads * kVec;         // 1024 elements
+constexpr int kNumAcc = 8;                             // accumulators per thread
+constexpr size_t kCounterBytes = 256;                  // counter padded to its own lines
+
+// accumulator slots
+enum { S_POS = 0, S_NEG, Q_POS, Q_NEG, H_POS, H_NEG, N_POS, N_NEG };
+
+int grid_for(int64_t B) {
+    int64_t g = (B + 2 * kPerBlockIter - 1) / (2 * kPerBlockIter);  // >= 2 iterations per thread
+    if (g < 1) g = 1;
+    if (g > kMaxBlocks) g = kMaxBlocks;
+    return static_cast<int>(g);
+}
+
+template <typename YT>
+__device__ __forceinline__ int load_label(const YT* __restrict__ y, int64_t i) {
+    return static_cast<int>(y[i]);
+}
+
+struct SurrogateScalars {
+    double a, b, alpha, p;
+    double c_pos, k_pos;  // dF/dh = c_pos * (h - k_pos) for y = +1
+    double c_neg, k_neg;  // dF/dh = c_neg * (h - k_neg) for y = -1
+};
+
+__device__ __forceinline__ SurrogateScalars make_scalars(const float* abalpha, const float* p_hat,
+                                                         int64_t B) {
+    SurrogateScalars s;
+    s.a = abalpha[0];
+    s.b = abalpha[1];
+    s.alpha = abalpha[2];
+    s.p = p_hat[0];
+    const double invB = 1.0 / static_cast<double>(B);
+    s.c_pos = 2.0 * (1.0 - s.p) * invB;
+    s.k_pos = s.a + 1.0 + s.alpha;
+    s.c_neg = 2.0 * s.p * invB;
+    s.k_neg = s.b - 1.0 - s.alpha;
+    return s;
+}
+
+// One element: accumulate its contribution and return dF/dh.
+template <bool CLASS_ONLY>
+__device__ __forceinline__ float visit(float hf, int yv, const SurrogateScalars& s,
+                                       double (&acc)[kNumAcc]) {
+    const double h = hf;
+    const bool pos = (yv == 1);
+    const bool neg = (yv == -1);
+    if (!CLASS_ONLY) {
+        const double dpos = pos ? h - s.a : 0.0;
+        const double dneg = neg ? h - s.b : 0.0;
+        acc[S_POS] += dpos;
+        acc[S_NEG] += dneg;
+        acc[Q_POS] += dpos * dpos;
+        acc[Q_NEG] += dneg * dneg;
+    }
+    acc[H_POS] += pos ? h : 0.0;
+    acc[H_NEG] += neg ? h : 0.0;
+    acc[N_POS] += pos ? 1.0 : 0.0;
+    acc[N_NEG] += neg ? 1.0 : 0.0;
+    if (CLASS_ONLY) return 0.0f;
+    const double c = pos ? s.c_pos : (neg ? s.c_neg : 0.0);
+    const double k = pos ? s.k_pos : s.k_neg;
+    return static_cast<float>(c * (h - k));
+}
+
+// Final scalars from the grid totals (one thread).
+__device__ void finalize(const double (&t)[kNumAcc], const SurrogateScalars& s, int64_t B,
+                         double* out64, float* grad3, float* loss) {
+    const double invB = 1.0 / static_cast<double>(B);
+    const double p = s.p, q = 1.0 - s.p;
+    const double cross = p * t[H_NEG] - q * t[H_POS];  // sum(p h [neg] - (1-p) h [pos])
+    const double F = q * t[Q_POS] * invB + p * t[Q_NEG] * invB +
+                     2.0 * (1.0 + s.alpha) * cross * invB - p * q * s.alpha * s.alpha;
+    const double dA = -2.0 * q * t[S_POS] * invB;
+    const double dB = -2.0 * p * t[S_NEG] * invB;
+    const double dAl = 2.0 * cross * invB - 2.0 * p * q * s.alpha;
+    if (out64) {
+        out64[0] = F;
+        out64[1] = dA;
+        out64[2] = dB;
+        out64[3] = dAl;
+        out64[4] = t[N_POS];
+        out64[5] = t[N_NEG];
+    }
+    if (grad3) {
+        grad3[0] = static_cast<float>(dA);
+        grad3[1] = static_cast<float>(dB);
+        grad3[2] = static_cast<float>(dAl);
+    }
+    if (loss) loss[0] = static_cast<float>(F);
+}
+
+__device__ void emit_class_sums(const double (&t)[kNumAcc], double* sums4, int accumulate) {
+    const double v[4] = {t[H_NEG], t[N_NEG], t[H_POS], t[N_POS]};
+    for (int k = 0; k < 4; ++k) sums4[k] = accumulate ? sums4[k] + v[k] : v[k];
+}
+
+// UNIT: h, y and dh are unit-stride and 4-element aligned (vector loads/stores).
+template <typename YT, bool CLASS_ONLY, bool UNIT>
+__global__ __launch_bounds__(kThreads) void surrogate_kernel(
+    const float* __restrict__ h, int64_t hs, const YT* __restrict__ y, int64_t B,
+    const float* __restrict__ abalpha, const float* __restrict__ p_hat, float* __restrict__ dh,
+    int64_t dhs, double* __restrict__ partials, unsigned* __restrict__ counter,
+    double* __restrict__ out64, float* __restrict__ grad3, float* __restrict__ loss,
+    double* __restrict__ sums4, int accumulate) {
+    __shared__ double scratch[kNumAcc * (kThreads / kWave)];
+    __shared__ int last_flag;
+
+    SurrogateScalars s;
+    if (CLASS_ONLY) {
+        s = SurrogateScalars{};
+    } else {
+        s = make_scalars(abalpha, p_hat, B);
+    }
+    double acc[kNumAcc];
+#pragma unroll
+    for (int k = 0; k < kNumAcc; ++k) acc[k] = 0.0;
+
+    const int64_t stride = static_cast<int64_t>(gridDim.x) * kPerBlockIter;
+    for (int64_t base = static_cast<int64_t>(blockIdx.x) * kPerBlockIter + threadIdx.x * kVec;
+         base < B; base += stride) {
+        if (UNIT && base + kVec <= B) {
+            const float4 hv = *reinterpret_cast<const float4*>(h + base);
+            int yv[kVec];
+            if constexpr (sizeof(YT) == 1) {
+                const char4 c = *reinterpret_cast<const char4*>(y + base);
+                yv[0] = c.x; yv[1] = c.y; yv[2] = c.z; yv[3] = c.w;
+            } else {
+#pragma unroll
+                for (int j = 0; j < kVec; ++j) yv[j] = load_label(y, base + j);
+            }
+            float4 g;
+            g.x = visit<CLASS_ONLY>(hv.x, yv[0], s, acc);
+            g.y = visit<CLASS_ONLY>(hv.y, yv[1], s, acc);
+            g.z = visit<CLASS_ONLY>(hv.z, yv[2], s, acc);
+            g.w = visit<CLASS_ONLY>(hv.w, yv[3], s, acc);
+            if (!CLASS_ONLY && dh) *reinterpret_cast<float4*>(dh + base) = g;
+        } else {
+#pragma unroll
+            for (int j = 0; j < kVec; ++j) {
+                const int64_t i = base + j;
+                if (i < B) {
+                    const float g = visit<CLASS_ONLY>(h[i * hs], load_label(y, i), s, acc);
+                    if (!CLASS_ONLY && dh) dh[i * dhs] = g;
+                }
+            }
+        }
+    }
+
+    block_sum<kNumAcc>(acc, scratch);
+
+    if (gridDim.x == 1) {
+        if (threadIdx.x == 0) {
+            if (CLASS_ONLY) emit_class_sums(acc, sums4, accumulate);
+            else finalize(acc, s, B, out64, grad3, loss);
+        }
+        return;
+    }
+
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int k = 0; k < kNumAcc; ++k) partials[blockIdx.x * kNumAcc + k] = acc[k];
+    }
+    if (!arrive_last(counter, gridDim.x, &last_flag)) return;
+
+    // Last block: reduce all partials in a fixed order.
+#pragma unroll
+    for (int k = 0; k < kNumAcc; ++k) acc[k] = 0.0;
+    for (int b = threadIdx.x; b < static_cast<int>(gridDim.x); b += kThreads) {
+#pragma unroll
+        for (int k = 0; k < kNumAcc; ++k) acc[k] += partials[b * kNumAcc + k];
+    }
+    block_sum<kNumAcc>(acc, scratch);
+    if (threadIdx.x == 0) {
+        if (CLASS_ONLY) emit_class_sums(acc, sums4, accumulate);
+        else finalize(acc, s, B, out64, grad3, loss);
+    }
+}
+
+bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+template <bool CLASS_ONLY, typename YT>
+int launch_surrogate(const float* h, int64_t hs, const YT* y, int64_t B, const float* abalpha,
+                     const float* p_hat, float* dh, int64_t dhs, double* out64, float* grad3,
+                     float* loss, double* sums4, int accumulate, void* ws, size_t ws_bytes,
+                     hipStream_t st) {
+    const int grid = grid_for(B);
+    unsigned* counter = nullptr;
+    double* partials = nullptr;
+    if (grid > 1) {
+        if (ws == nullptr || ws_bytes < dauc_surrogate_workspace_size(B)) return DAUC_EINVAL;
+        counter = static_cast<unsigned*>(ws);
+        partials = reinterpret_cast<double*>(static_cast<char*>(ws) + kCounterBytes);
+    }
+    const bool unit = hs == 1 && aligned16(h) &&
+                      (reinterpret_cast<uintptr_t>(y) % (kVec * sizeof(YT))) == 0 &&
+                      (CLASS_ONLY || dh == nullptr || (dhs == 1 && aligned16(dh)));
+    if (unit) {
+        hipLaunchKernelGGL((surrogate_kernel<YT, CLASS_ONLY, true>), dim3(grid), dim3(kThreads), 0,
+                           st, h, hs, y, B, abalpha, p_hat, dh, dhs, partials, counter, out64,
+                           grad3, loss, sums4, accumulate);
+    } else {
+        hipLaunchKernelGGL((surrogate_kernel<YT, CLASS_ONLY, false>), dim3(grid), dim3(kThreads),
+                           0, st, h, hs, y, B, abalpha, p_hat, dh, dhs, partials, counter, out64,
+                           grad3, loss, sums4, accumulate);
+    }
+    return launch_status();
+}
+
+template <bool CLASS_ONLY>
+int dispatch_labels(const float* h, int64_t hs, const void* y, int yt, int64_t B,
+                    const float* abalpha, const float* p_hat, float* dh, int64_t dhs,
+                    double* out64, float* grad3, float* loss, double* sums4, int accumulate,
+                    void* ws, size_t ws_bytes, hipStream_t st) {
+    switch (yt) {
+        case DAUC_LABEL_I8:
+            return launch_surrogate<CLASS_ONLY>(h, hs, static_cast<const int8_t*>(y), B, abalpha,
+                                                p_hat, dh, dhs, out64, grad3, loss, sums4,
+                                                accumulate, ws, ws_bytes, st);
+        case DAUC_LABEL_I32:
+            return launch_surrogate<CLASS_ONLY>(h, hs, static_cast<const int32_t*>(y), B, abalpha,
+                                                p_hat, dh, dhs, out64, grad3, loss, sums4,
+                                                accumulate, ws, ws_bytes, st);
+        case DAUC_LABEL_I64:
+            return launch_surrogate<CLASS_ONLY>(h, hs, static_cast<const int64_t*>(y), B, abalpha,
+                                                p_hat, dh, dhs, out64, grad3, loss, sums4,
+                                                accumulate, ws, ws_bytes, st);
+        default:
+            return DAUC_EINVAL;
+    }
+}
+
+// ---- a1: label map + class counts + p_hat (one block; B is a training batch) ----
+__global__ __launch_bounds__(kThreads) void label_map_phat_kernel(
+    const int64_t* __restrict__ labels, int64_t B, int64_t split, int8_t* __restrict__ y_out,
+    float* __restrict__ lcounts, const float* __restrict__ gcounts, float* __restrict__ p_hat) {
+    __shared__ unsigned long long part[2][kThreads / kWave];
+    unsigned long long npos = 0, nneg = 0;
+    for (int64_t i = threadIdx.x; i < B; i += kThreads) {
+        const int8_t v = labels[i] <= split ? int8_t(-1) : int8_t(1);
+        if (y_out) y_out[i] = v;
+        npos += (v == 1);
+        nneg += (v == -1);
+    }
+    npos = wave_sum(npos);
+    nneg = wave_sum(nneg);
+    const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+    if (lane == 0) {
+        part[0][wid] = npos;
+        part[1][wid] = nneg;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long tp = 0, tn = 0;
+        for (int w = 0; w < kThreads / kWave; ++w) {
+            tp += part[0][w];
+            tn += part[1][w];
+        }
+        // main.py:307-308: lpos/lneg accumulate (fp32, exact below 2^24)
+        const float lpos = __fadd_rn(lcounts[0], static_cast<float>(tp));
+        const float lneg = __fadd_rn(lcounts[1], static_cast<float>(tn));
+        lcounts[0] = lpos;
+        lcounts[1] = lneg;
+        // main.py:309-310: fp32 tensor sums, float() to double, double divide, fp32 store
+        const float gpos = gcounts[0], gneg = gcounts[1];
+        const float num = __fadd_rn(gpos, lpos);
+        const float den = __fadd_rn(__fadd_rn(num, gneg), lneg);
+        p_hat[0] = static_cast<float>(static_cast<double>(num) / static_cast<double>(den));
+    }
+}
+
+__global__ void alpha_from_sums_kernel(const double* __restrict__ s, float* __restrict__ alpha) {
+    // main.py:197 computes this from fp32 sums; fp64 here, rounded once.
+    alpha[0] = static_cast<float>(s[0] / s[1] - s[2] / s[3]);
+}
+
+}  // namespace
+}  // namespace dauc
+
+using namespace dauc;
+
+extern "C" {
+
+size_t dauc_surrogate_workspace_size(int64_t B) {
+    const int g = grid_for(B < 0 ? 0 : B);
+    return kCounterBytes + static_cast<size_t>(g) * kNumAcc * sizeof(double);
+}
+
+int dauc_surrogate_fwdbwd(const float* h, int64_t h_stride, const void* y, int y_dtype, int64_t B,
+                          const float* abalpha, const float* p_hat, float* dh, int64_t dh_stride,
+                          double* out64, float* grad3, float* loss, void* workspace,
+                          size_t workspace_bytes, dauc_stream_t stream) {
+    if (B <= 0 || h == nullptr || y == nullptr || abalpha == nullptr || p_hat == nullptr ||
+        h_stride <= 0 || (dh != nullptr && dh_stride <= 0))
+        return DAUC_EINVAL;
+    return dispatch_labels<false>(h, h_stride, y, y_dtype, B, abalpha, p_hat, dh, dh_stride, out64,
+                                  grad3, loss, nullptr, 0, workspace, workspace_bytes,
+                                  as_hip(stream));
+}
+
+int dauc_class_sums(const float* h, int64_t h_stride, const void* y, int y_dtype, int64_t B,
+                    double* sums4, int accumulate, void* workspace, size_t workspace_bytes,
+                    dauc_stream_t stream) {
+    if (B <= 0 || h == nullptr || y == nullptr || sums4 == nullptr || h_stride <= 0)
+        return DAUC_EINVAL;
+    return dispatch_labels<true>(h, h_stride, y, y_dtype, B, nullptr, nullptr, nullptr, 1, nullptr,
+                                 nullptr, nullptr, sums4, accumulate, workspace, workspace_bytes,
+                                 as_hip(stream));
+}
+
+int dauc_alpha_from_sums(const double* sums4, float* alpha, dauc_stream_t stream) {
+    if (sums4 == nullptr || alpha == nullptr) return DAUC_EINVAL;
+    hipLaunchKernelGGL(alpha_from_sums_kernel, dim3(1), dim3(1), 0, as_hip(stream), sums4, alpha);
+    return launch_status();
+}
+
+int dauc_label_map_phat(const int64_t* labels, int64_t B, int64_t split_index, int8_t* y_out,
+                        float* lcounts, const float* gcounts, float* p_hat, dauc_stream_t stream) {
+    if (B <= 0 || labels == nullptr || lcounts == nullptr || gcounts == nullptr || p_hat == nullptr)
+        return DAUC_EINVAL;
+    hipLaunchKernelGGL(label_map_phat_kernel, dim3(1), dim3(kThreads), 0, as_hip(stream), labels, B,
+                       split_index, y_out, lcounts, gcounts, p_hat);
+    return launch_status();
+}
+
+}  // extern "C"

@@ -1,0 +1,120 @@
+"""Synthetic ImageNet-shaped data, generated on the device.
+
+The reference reads ImageNet through torchvision (main.py:94-117) with a
+4-worker host DataLoader and copies every batch to the GPU (main.py:285-286).
+This build has no dataset and no network, so training data is synthetic with
+ImageNet's shape: a label per sample index (class 0..num_classes-1) and
+images generated directly in HBM (N(0,1) noise plus a small class-dependent
+signal, so the AUC actually moves). Only the int64 label indices cross PCIe,
+through pinned memory and non-blocking copies.
+"""
+from __future__ import annotations
+
+from typing import Iterator, Sequence
+
+import numpy as np
+import torch
+
+from .data_partitioner import IMAGENET_LEN, IMAGENET_NEG
+
+
+def imagenet_like_labels(n: int = IMAGENET_LEN, num_classes: int = 1000, split_index: int = 499,
+                         pos_ratio: float | None = None, seed: int = 0) -> np.ndarray:
+    """Class index per sample.
+
+    With ``pos_ratio=None`` and n == 1281167 the labels are sorted by class like the
+    ImageNet train folder, consistent with the index ranges data_partitioner.py
+    hard-codes (negatives 0..642288 <= split_index 499). Otherwise classes are
+    drawn so that a fraction ``pos_ratio`` is above ``split_index``.
+    """
+    if pos_ratio is None and n == IMAGENET_LEN and split_index == 499 and num_classes == 1000:
+        i = np.arange(n, dtype=np.int64)
+        n_neg = IMAGENET_NEG[1]
+        neg_cls = i * 500 // n_neg
+        pos_cls = 500 + (i - n_neg) * 500 // (n - n_neg)
+        return np.where(i < n_neg, neg_cls, pos_cls).astype(np.int64)
+    if pos_ratio is None:
+        pos_ratio = (num_classes - 1 - split_index) / num_classes
+    rng = np.random.default_rng(seed)
+    is_pos = rng.random(n) < pos_ratio
+    neg_cls = rng.integers(0, split_index + 1, size=n)
+    pos_cls = rng.integers(split_index + 1, num_classes, size=n)
+    return np.where(is_pos, pos_cls, neg_cls).astype(np.int64)
+
+
+class SyntheticImageNet:
+    """Index -> (image spec, class label). Images are materialised per batch on the device."""
+
+    def __init__(self, labels: np.ndarray, image_size: int = 224, split_index: int = 499):
+        self.labels = np.asarray(labels, dtype=np.int64)
+        self.image_size = image_size
+        self.split_index = split_index
+
+    def __len__(self):
+        return len(self.labels)
+
+    def __getitem__(self, i):
+        return i, int(self.labels[i])
+
+
+class DeviceLoader:
+    """Infinite iterator of (images [B,3,R,R], labels int64 [B]) on ``device``.
+
+    Epochs reshuffle ``indices`` (like DataLoader(shuffle=True)) with a seeded RNG;
+    a final partial batch is kept (drop_last=False, the DataLoader default).
+    ``pool`` > 0 pre-generates that many batches once and cycles them, so a timed
+    loop reads inputs already resident in HBM.
+    """
+
+    def __init__(self, dataset: SyntheticImageNet, indices: Sequence[int], batch_size: int, device,
+                 seed: int = 0, shuffle: bool = True, channels_last: bool = True, signal: float = 0.25,
+                 pool: int = 0, drop_last: bool = False):
+        self.ds = dataset
+        self.indices = np.asarray(indices, dtype=np.int64)
+        if self.indices.size == 0:
+            raise ValueError("empty partition")
+        self.B = int(batch_size)
+        self.device = torch.device(device)
+        self.seed = seed
+        self.shuffle = shuffle
+        self.channels_last = channels_last
+        self.signal = signal
+        self.drop_last = drop_last
+        self.gen = torch.Generator(device=self.device)
+        self.gen.manual_seed(seed)
+        self._pool = [self._make(b) for b in self._index_batches(pool)] if pool else None
+
+    def _index_batches(self, limit: int | None = None) -> Iterator[np.ndarray]:
+        epoch, made = 0, 0
+        while True:
+            order = self.indices
+            if self.shuffle:
+                order = np.random.default_rng(self.seed + epoch).permutation(self.indices)
+            stop = len(order) - (len(order) % self.B if self.drop_last else 0)
+            for s in range(0, stop, self.B):
+                yield order[s:s + self.B]
+                made += 1
+                if limit is not None and made >= limit:
+                    return
+            epoch += 1
+
+    def _make(self, idx: np.ndarray):
+        R = self.ds.image_size
+        lab_host = torch.from_numpy(self.ds.labels[idx]).pin_memory()
+        labels = lab_host.to(self.device, non_blocking=True)
+        x = torch.randn((len(idx), 3, R, R), generator=self.gen, device=self.device, dtype=torch.float32)
+        if self.signal:
+            sign = torch.where(labels > self.ds.split_index, 1.0, -1.0).to(torch.float32)
+            x[:, 0].add_(sign.view(-1, 1, 1), alpha=self.signal)
+        if self.channels_last:
+            x = x.contiguous(memory_format=torch.channels_last)
+        return x, labels
+
+    def __iter__(self):
+        if self._pool is not None:
+            k = 0
+            while True:
+                yield self._pool[k % len(self._pool)]
+                k += 1
+        for idx in self._index_batches():
+            yield self._make(idx)

@@ -1,0 +1,282 @@
+"""Tensor-level wrappers over the libdauc.so C ABI.
+
+Every function takes torch tensors that live on the GPU, validates shapes,
+dtypes and devices on the host (so a kernel never sees an operand its grid does
+not expect), and enqueues the HIP kernel on torch's current stream for that
+device. Nothing here synchronises or allocates on the steady-state path except
+cached, zero-initialised workspaces. CPU tensors are rejected: there is no CPU
+fallback in the product path.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib
+from ._lib import GradSeg, check
+
+_LABEL_CODES = {torch.int8: _lib.LABEL_I8, torch.int32: _lib.LABEL_I32, torch.int64: _lib.LABEL_I64}
+_MODES = {"reference": _lib.MODE_REFERENCE, "paper": _lib.MODE_PAPER}
+
+
+def _require_gpu(t: torch.Tensor, name: str) -> None:
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name} must be a torch.Tensor, got {type(t).__name__}")
+    if t.device.type != "cuda":
+        raise RuntimeError(
+            f"{name}: distributedauc_amd runs its hot path on the MI355X only (HIP kernels in "
+            f"libdauc.so); got a tensor on {t.device}. There is no CPU fallback."
+        )
+
+
+def _require(t: torch.Tensor, name: str, dtype: torch.dtype, device=None) -> None:
+    _require_gpu(t, name)
+    if t.dtype != dtype:
+        raise TypeError(f"{name} must be {dtype}, got {t.dtype}")
+    if device is not None and t.device != device:
+        raise ValueError(f"{name} is on {t.device}, expected {device}")
+
+
+def _ptr(t) -> ctypes.c_void_p:
+    return ctypes.c_void_p(0 if t is None else t.data_ptr())
+
+
+def _stream(device: torch.device) -> ctypes.c_void_p:
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def mode_code(mode: str) -> int:
+    try:
+        return _MODES[mode]
+    except KeyError:
+        raise ValueError(f"mode must be one of {sorted(_MODES)}, got {mode!r}") from None
+
+
+class _Workspaces:
+    """Zero-initialised scratch, one per (device, stream, kind), grown on demand.
+
+    The kernels that need zeroed scratch (the surrogate's last-arriver ticket)
+    leave it zeroed again, so a workspace is cleared only when it is created.
+    """
+
+    def __init__(self):
+        self._ws: dict = {}
+
+    def get(self, device: torch.device, kind: str, nbytes: int) -> torch.Tensor:
+        key = (device.index, torch.cuda.current_stream(device).cuda_stream, kind)
+        t = self._ws.get(key)
+        if t is None or t.numel() < nbytes:
+            t = torch.zeros(max(nbytes, 256), dtype=torch.uint8, device=device)
+            self._ws[key] = t
+        return t
+
+
+workspaces = _Workspaces()
+
+
+def _label_code(y: torch.Tensor, name: str = "y") -> int:
+    _require_gpu(y, name)
+    try:
+        return _LABEL_CODES[y.dtype]
+    except KeyError:
+        raise TypeError(f"{name} must be int8, int32 or int64, got {y.dtype}") from None
+
+
+def _check_vec(h: torch.Tensor, y: torch.Tensor) -> int:
+    _require(h, "h", torch.float32)
+    if h.dim() != 1 or y.dim() != 1 or h.shape[0] != y.shape[0]:
+        raise ValueError(f"h and y must be 1-D of equal length, got {tuple(h.shape)} and {tuple(y.shape)}")
+    if y.stride(0) != 1:
+        raise ValueError("y must be contiguous")
+    if h.device != y.device:
+        raise ValueError("h and y must be on the same device")
+    if h.shape[0] == 0:
+        raise ValueError("empty batch")
+    return h.shape[0]
+
+
+# ----------------------------------------------------------------- a1
+def label_map_phat(labels: torch.Tensor, split_index: int, y_out: torch.Tensor, lcounts: torch.Tensor,
+                   gcounts: torch.Tensor, p_hat: torch.Tensor) -> None:
+    """main.py:303-310 in one launch: y_out = +/-1 (int8), lcounts += counts, p_hat (fp32)."""
+    _require(labels, "labels", torch.int64)
+    dev = labels.device
+    _require(y_out, "y_out", torch.int8, dev)
+    for t, n in ((lcounts, "lcounts"), (gcounts, "gcounts"), (p_hat, "p_hat")):
+        _require(t, n, torch.float32, dev)
+    if labels.dim() != 1 or not labels.is_contiguous() or y_out.shape != labels.shape or not y_out.is_contiguous():
+        raise ValueError("labels and y_out must be contiguous 1-D tensors of equal length")
+    if lcounts.numel() < 2 or gcounts.numel() < 2 or p_hat.numel() < 1 or labels.numel() == 0:
+        raise ValueError("lcounts/gcounts need 2 elements, p_hat 1, labels >= 1")
+    check(_lib.load().dauc_label_map_phat(_ptr(labels), labels.numel(), int(split_index), _ptr(y_out),
+                                          _ptr(lcounts), _ptr(gcounts), _ptr(p_hat), _stream(dev)),
+          "dauc_label_map_phat")
+
+
+# ----------------------------------------------------------------- a2/a3
+def surrogate_fwdbwd(h: torch.Tensor, y: torch.Tensor, abalpha: torch.Tensor, p_hat: torch.Tensor, *,
+                     dh: torch.Tensor | None = None, out64: torch.Tensor | None = None,
+                     grad3: torch.Tensor | None = None, loss: torch.Tensor | None = None) -> None:
+    """Fused loss + gradients of main.py:313-317 (one pass over h and y)."""
+    B = _check_vec(h, y)
+    dev = h.device
+    yc = _label_code(y)
+    _require(abalpha, "abalpha", torch.float32, dev)
+    _require(p_hat, "p_hat", torch.float32, dev)
+    if abalpha.numel() < 3 or not abalpha.is_contiguous() or p_hat.numel() < 1:
+        raise ValueError("abalpha needs 3 contiguous fp32 values, p_hat 1")
+    dh_stride = 1
+    if dh is not None:
+        _require(dh, "dh", torch.float32, dev)
+        if dh.dim() != 1 or dh.shape[0] != B:
+            raise ValueError("dh must be 1-D of length B")
+        dh_stride = dh.stride(0)
+    if out64 is not None:
+        _require(out64, "out64", torch.float64, dev)
+        if out64.numel() < 6 or not out64.is_contiguous():
+            raise ValueError("out64 needs 6 contiguous fp64 slots")
+    if grad3 is not None:
+        _require(grad3, "grad3", torch.float32, dev)
+        if grad3.numel() < 3 or not grad3.is_contiguous():
+            raise ValueError("grad3 needs 3 contiguous fp32 slots")
+    if loss is not None:
+        _require(loss, "loss", torch.float32, dev)
+    L = _lib.load()
+    nbytes = L.dauc_surrogate_workspace_size(B)
+    ws = workspaces.get(dev, "surrogate", nbytes)
+    check(L.dauc_surrogate_fwdbwd(_ptr(h), h.stride(0), _ptr(y), yc, B, _ptr(abalpha), _ptr(p_hat),
+                                  _ptr(dh), dh_stride, _ptr(out64), _ptr(grad3), _ptr(loss), _ptr(ws),
+                                  ws.numel(), _stream(dev)),
+          "dauc_surrogate_fwdbwd")
+
+
+def class_sums(h: torch.Tensor, y: torch.Tensor, sums4: torch.Tensor, accumulate: bool = True) -> None:
+    """main.py:185-188: sums4 (+)= {sum h[y=-1], #neg, sum h[y=1], #pos} (fp64)."""
+    B = _check_vec(h, y)
+    dev = h.device
+    yc = _label_code(y)
+    _require(sums4, "sums4", torch.float64, dev)
+    if sums4.numel() < 4 or not sums4.is_contiguous():
+        raise ValueError("sums4 needs 4 contiguous fp64 slots")
+    L = _lib.load()
+    ws = workspaces.get(dev, "surrogate", L.dauc_surrogate_workspace_size(B))
+    check(L.dauc_class_sums(_ptr(h), h.stride(0), _ptr(y), yc, B, _ptr(sums4), int(bool(accumulate)),
+                            _ptr(ws), ws.numel(), _stream(dev)), "dauc_class_sums")
+
+
+def alpha_from_sums(sums4: torch.Tensor, alpha: torch.Tensor) -> None:
+    """main.py:197 on the device: alpha = h_neg/N_neg - h_pos/N_pos."""
+    _require(sums4, "sums4", torch.float64)
+    _require(alpha, "alpha", torch.float32, sums4.device)
+    check(_lib.load().dauc_alpha_from_sums(_ptr(sums4), _ptr(alpha), _stream(sums4.device)),
+          "dauc_alpha_from_sums")
+
+
+# ----------------------------------------------------------------- a4/a5
+def pd_update(w: torch.Tensor, w0: torch.Tensor, w_avg: torch.Tensor | None, segs, nseg: int, *,
+              scalars: torch.Tensor | None = None, grad3: torch.Tensor | None = None,
+              anchor3: torch.Tensor | None = None, lr: float, gamma: float, mode: str = "reference") -> None:
+    """dppd_sg over the flat buffer + running average, one launch (segs: GradSeg ctypes array).
+
+    The caller guarantees every segment lies inside w / w0 / w_avg (FlatState builds
+    the table from the parameters' own offsets).
+    """
+    _require(w, "w", torch.float32)
+    dev = w.device
+    _require(w0, "w0", torch.float32, dev)
+    if w_avg is not None:
+        _require(w_avg, "w_avg", torch.float32, dev)
+    if scalars is not None:
+        for t, n in ((scalars, "scalars"), (grad3, "grad3"), (anchor3, "anchor3")):
+            _require(t, n, torch.float32, dev)
+    check(_lib.load().dauc_pd_update(_ptr(w), _ptr(w0), _ptr(w_avg), segs, int(nseg), _ptr(scalars),
+                                     _ptr(grad3), _ptr(anchor3), float(lr), float(1 / gamma),
+                                     mode_code(mode), _stream(dev)),
+          "dauc_pd_update")
+
+
+def pd_update_dense(w: torch.Tensor, g: torch.Tensor, w0: torch.Tensor, w_avg: torch.Tensor | None, *,
+                    lr: float, gamma: float) -> None:
+    """main.py:61 (+333-334) over one dense buffer of n parameters."""
+    _require(w, "w", torch.float32)
+    dev = w.device
+    n = w.numel()
+    for t, name in ((g, "g"), (w0, "w0")) + (((w_avg, "w_avg"),) if w_avg is not None else ()):
+        _require(t, name, torch.float32, dev)
+        if t.numel() != n or not t.is_contiguous():
+            raise ValueError(f"{name} must be contiguous with {n} elements")
+    if not w.is_contiguous():
+        raise ValueError("w must be contiguous")
+    check(_lib.load().dauc_pd_update_dense(_ptr(w), _ptr(g), _ptr(w0), _ptr(w_avg), n, float(lr),
+                                           float(1 / gamma), _stream(dev)),
+          "dauc_pd_update_dense")
+
+
+# ----------------------------------------------------------------- a6
+def coda_finalize(flat: torch.Tensor, n_avg: int, world: int, lcounts: torch.Tensor,
+                  gcounts: torch.Tensor) -> None:
+    """Divide the all-reduced flat[:n_avg] by world and fold the class counts."""
+    _require(flat, "flat", torch.float32)
+    dev = flat.device
+    _require(lcounts, "lcounts", torch.float32, dev)
+    _require(gcounts, "gcounts", torch.float32, dev)
+    if not flat.is_contiguous() or n_avg > flat.numel() or n_avg < 0:
+        raise ValueError("flat must be contiguous and hold n_avg elements")
+    check(_lib.load().dauc_coda_finalize(_ptr(flat), int(n_avg), int(world), _ptr(lcounts), _ptr(gcounts),
+                                         _stream(dev)), "dauc_coda_finalize")
+
+
+def scale_div(x: torch.Tensor, divisor: float) -> None:
+    """x /= divisor (fp32 IEEE division), main.py:338-339."""
+    _require(x, "x", torch.float32)
+    if not x.is_contiguous():
+        raise ValueError("x must be contiguous")
+    check(_lib.load().dauc_scale_div(_ptr(x), x.numel(), float(divisor), _stream(x.device)), "dauc_scale_div")
+
+
+# ----------------------------------------------------------------- a8
+def split_scores(scores: torch.Tensor, labels: torch.Tensor):
+    """Stable split into (pos, neg) score buffers plus device stats {P, N, non-finite, other}.
+
+    Returns (pos_buf, neg_buf, stats): pos_buf/neg_buf have capacity n; the valid
+    prefixes are stats[0] and stats[1] long.
+    """
+    _require(scores, "scores", torch.float32)
+    dev = scores.device
+    lc = _label_code(labels, "labels")
+    if scores.dim() != 1 or labels.dim() != 1 or scores.shape != labels.shape:
+        raise ValueError("scores and labels must be 1-D of equal length")
+    if not scores.is_contiguous() or not labels.is_contiguous():
+        raise ValueError("scores and labels must be contiguous")
+    n = scores.numel()
+    if n == 0:
+        raise ValueError("empty score vector")
+    pos = torch.empty(n, dtype=torch.float32, device=dev)
+    neg = torch.empty(n, dtype=torch.float32, device=dev)
+    stats = torch.empty(4, dtype=torch.int64, device=dev)
+    L = _lib.load()
+    ws = workspaces.get(dev, "split", L.dauc_split_workspace_size(n))
+    check(L.dauc_split_scores(_ptr(scores), _ptr(labels), lc, n, _ptr(pos), _ptr(neg), _ptr(stats), _ptr(ws),
+                              ws.numel(), _stream(dev)), "dauc_split_scores")
+    return pos, neg, stats
+
+
+def pair_count(pos: torch.Tensor, neg: torch.Tensor, wins_ties: torch.Tensor, variant: int = 0) -> None:
+    """wins_ties[0] += #{pos > neg}, wins_ties[1] += #{pos == neg} (int64 view of uint64 counters)."""
+    _require(pos, "pos", torch.float32)
+    dev = pos.device
+    _require(neg, "neg", torch.float32, dev)
+    _require(wins_ties, "wins_ties", torch.int64, dev)
+    if pos.dim() != 1 or neg.dim() != 1 or not pos.is_contiguous() or not neg.is_contiguous():
+        raise ValueError("pos and neg must be contiguous 1-D tensors")
+    if wins_ties.numel() < 2 or not wins_ties.is_contiguous():
+        raise ValueError("wins_ties needs 2 contiguous int64 slots")
+    check(_lib.load().dauc_pair_count_variant(_ptr(pos), pos.numel(), _ptr(neg), neg.numel(), _ptr(wins_ties),
+                                              int(variant), _stream(dev)), "dauc_pair_count")
+
+
+__all__ = [
+    "GradSeg", "label_map_phat", "surrogate_fwdbwd", "class_sums", "alpha_from_sums", "pd_update",
+    "pd_update_dense", "coda_finalize", "scale_div", "split_scores", "pair_count", "mode_code", "workspaces",
+]

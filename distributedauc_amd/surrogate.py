@@ -1,0 +1,44 @@
+"""Autograd entry of the fused min-max square-loss AUC surrogate.
+
+Replaces the inline expression of main.py:313-317 and its autograd backward
+(main.py:326). The HIP kernel produces F, dF/dh and the three scalar gradients
+in the forward pass (one read of h and y); backward only hands the stored dF/dh
+to the backbone. The gradients of (a, b, alpha) are written straight into the
+caller's ``grad3`` buffer (the CoDA flat gradient tail), where the update kernel
+reads them, so they never enter autograd.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import ops
+
+
+class AUCSurrogate(torch.autograd.Function):
+    """F(h; a, b, alpha, p) with dF/dh, dF/da, dF/db, dF/dalpha from one kernel pass."""
+
+    @staticmethod
+    def forward(ctx, h, y, abalpha, p_hat, grad3):
+        dh = torch.empty(h.shape[0], dtype=torch.float32, device=h.device)
+        loss = torch.empty((), dtype=torch.float32, device=h.device)
+        g3 = grad3 if grad3 is not None else torch.empty(3, dtype=torch.float32, device=h.device)
+        ops.surrogate_fwdbwd(h, y, abalpha, p_hat, dh=dh, grad3=g3, loss=loss)
+        ctx.save_for_backward(dh, g3)
+        ctx.abalpha_grad = abalpha.requires_grad
+        return loss
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        dh, g3 = ctx.saved_tensors
+        d_ab = g3 * grad_out if ctx.abalpha_grad else None
+        return dh * grad_out, None, d_ab, None, None
+
+
+def auc_surrogate(h: torch.Tensor, y: torch.Tensor, abalpha: torch.Tensor, p_hat: torch.Tensor,
+                  grad3: torch.Tensor | None = None) -> torch.Tensor:
+    """Loss of main.py:313-317 for scores ``h`` (1-D, any stride) and labels ``y`` (+1/-1).
+
+    abalpha: fp32 [3] = (a, b, alpha); p_hat: fp32 [1]. If ``grad3`` is given, the
+    kernel writes (dF/da, dF/db, dF/dalpha) into it during the forward pass.
+    """
+    return AUCSurrogate.apply(h, y, abalpha, p_hat, grad3)

@@ -1,0 +1,197 @@
+/*
+ * dauc.h — C ABI of libdauc.so, the MI355X (gfx950) hot path of CoDA
+ * (communication-efficient distributed AUC maximization).
+ *
+ * This is the drop-in boundary for the data-parallel hot path of the reference
+ * (ZhishuaiGuo/DistributedAUC, imagenet/main.py). The reference has no FFI: its
+ * path is a handful of in-process Python functions and one inline loss
+ * expression. Each entry point below replaces one of them; the citation names
+ * the reference interface it replaces.
+ *
+ * Conventions (all entry points):
+ *   - Every pointer argument is a DEVICE pointer owned by the caller, unless the
+ *     parameter is documented as a host pointer.
+ *   - The library never allocates or synchronises on the hot path. Scratch
+ *     space is sized with the matching *_workspace_size() query and provided by
+ *     the caller, zero-filled before its first use (the library leaves it
+ *     zeroed again after every call).
+ *   - Every call takes a hipStream_t (pass the caller's current stream). Work
+ *     is enqueued on that stream, asynchronously and in stream order.
+ *   - Return value: 0 on success, DAUC_EINVAL on a bad argument (nothing was
+ *     enqueued), or -(hipError_t) if a HIP launch failed. No C++ exception ever
+ *     crosses this boundary. dauc_strerror() turns a status into text.
+ *   - One rank per process, one stream per call site: calls are
+ *     thread-compatible, not thread-safe on one workspace.
+ */
+#ifndef DAUC_H_
+#define DAUC_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ihipStream_t* dauc_stream_t; /* == hipStream_t */
+
+#define DAUC_OK 0
+#define DAUC_EINVAL (-100000)
+
+/* label element types accepted by the surrogate / class-sum kernels */
+#define DAUC_LABEL_I8 1
+#define DAUC_LABEL_I32 2
+#define DAUC_LABEL_I64 3
+
+/* dauc_pd_update modes */
+#define DAUC_MODE_REFERENCE 0 /* main.py:58-64 as written: b prox uses (a_new-a0), alpha unchanged */
+#define DAUC_MODE_PAPER 1     /* b prox uses (b-b0), alpha <- alpha + lr*dF/dalpha              */
+
+/* ---------------------------------------------------------------- misc */
+
+/* Library version as 100*major + minor. */
+int dauc_version(void);
+
+/* Human-readable text for a status returned by any dauc_* call (static storage). */
+const char* dauc_strerror(int status);
+
+/* ------------------------------------------------- a1: label map + p_hat */
+
+/*
+ * Replaces main.py:303-310 (label map, class counts and p_hat, including the
+ * per-step device->host sync the reference pays at 309-310).
+ *   y_out[i]  = (labels[i] <= split_index) ? -1 : +1               (int8)
+ *   lcounts[0] += #{y == +1};  lcounts[1] += #{y == -1}              (fp32 accumulators; exact below 2^24)
+ *   p_hat[0]  = (float)( (double)fp32(gpos+lpos) /
+ *                        (double)fp32(((gpos+lpos)+gneg)+lneg) )    (gcounts = {gpos, gneg}, fp32)
+ * labels: int64 [B] class indices. lcounts is normally the two count slots at
+ * the tail of the CoDA flat buffer (so they ride in the averaging all-reduce).
+ */
+int dauc_label_map_phat(const int64_t* labels, int64_t B, int64_t split_index, int8_t* y_out,
+                        float* lcounts, const float* gcounts, float* p_hat, dauc_stream_t stream);
+
+/* ---------------------------------------------- a2+a3: fused surrogate */
+
+/* Bytes of zero-initialised scratch dauc_surrogate_fwdbwd / dauc_class_sums need for B elements. */
+size_t dauc_surrogate_workspace_size(int64_t B);
+
+/*
+ * Replaces the inline loss of main.py:313-317 and its autograd backward
+ * (main.py:326) in ONE pass over the batch:
+ *   F = (1-p) mean((h-a)^2 [y=1]) + p mean((h-b)^2 [y=-1])
+ *       + 2(1+alpha) mean(p h [y=-1] - (1-p) h [y=1]) - p(1-p) alpha^2      (means divide by B)
+ * Inputs : h [B] fp32 with element stride h_stride (e.g. 2 for column 1 of a [B,2] softmax),
+ *          y [B] of type y_dtype (+1 positive, -1 negative, anything else in neither class),
+ *          abalpha = {a, b, alpha} fp32 [3], p_hat fp32 [1].
+ * Outputs: dh [B] fp32 with element stride dh_stride = dF/dh (nullable: skip),
+ *          out64 [6] fp64 = {F, dF/da, dF/db, dF/dalpha, n_pos, n_neg} (nullable),
+ *          grad3 [3] fp32 = {dF/da, dF/db, dF/dalpha} (nullable; normally the tail of the flat grad),
+ *          loss [1] fp32 = F (nullable).
+ * Reductions accumulate in fp64 in a fixed order: results are bitwise reproducible.
+ */
+int dauc_surrogate_fwdbwd(const float* h, int64_t h_stride, const void* y, int y_dtype, int64_t B,
+                          const float* abalpha, const float* p_hat, float* dh, int64_t dh_stride,
+                          double* out64, float* grad3, float* loss, void* workspace,
+                          size_t workspace_bytes, dauc_stream_t stream);
+
+/*
+ * Replaces the stage-start alpha estimate of main.py:166-188 (per batch):
+ *   sums4 (+)= { sum h[y=-1], #{y=-1}, sum h[y=1], #{y=1} }       (fp64 [4])
+ * accumulate != 0 adds into sums4, otherwise overwrites it.
+ */
+int dauc_class_sums(const float* h, int64_t h_stride, const void* y, int y_dtype, int64_t B,
+                    double* sums4, int accumulate, void* workspace, size_t workspace_bytes,
+                    dauc_stream_t stream);
+
+/*
+ * main.py:197: alpha[0] = (float)(sums4[0]/sums4[1] - sums4[2]/sums4[3]).
+ */
+int dauc_alpha_from_sums(const double* sums4, float* alpha, dauc_stream_t stream);
+
+/* ---------------------------------------- a4+a5: primal-dual update */
+
+/* One parameter tensor's gradient, located at w + offset inside the flat buffer. */
+typedef struct dauc_grad_seg {
+    const float* grad; /* device pointer, dense, same physical element order as the parameter */
+    int64_t offset;    /* element offset of the parameter inside w / w0 / w_avg */
+    int64_t numel;
+} dauc_grad_seg;
+
+/*
+ * Replaces dppd_sg (main.py:56-64) for every named parameter, fused with the
+ * per-step running average (main.py:333-334), over the flat parameter buffer:
+ *   w[i]     <- w[i] - lr*(g[i] + inv_gamma*(w[i] - w0[i]))      (fp32, op order of main.py:61, no FMA)
+ *   w_avg[i] <- w_avg[i] + w[i]                                  (if w_avg != NULL)
+ * The gradients stay where autograd left them: segs (HOST array, nseg entries)
+ * gives each parameter's gradient pointer and its offset in the flat buffer.
+ * If scalars != NULL, the same launch also applies the scalar part:
+ *   scalars = {a, b, alpha} fp32 [3], grad3 = {dF/da, dF/db, dF/dalpha}, anchor3 = {a0, b0, alpha0}
+ *   a <- a - lr*(da + inv_gamma*(a - a0))
+ *   b <- b - lr*(db + inv_gamma*(a_new - a0))     [REFERENCE] / (b - b0) [PAPER]
+ *   alpha unchanged                                [REFERENCE] / alpha + lr*dalpha [PAPER]
+ */
+int dauc_pd_update(float* w, const float* w0, float* w_avg, const dauc_grad_seg* segs, int nseg,
+                   float* scalars, const float* grad3, const float* anchor3, float lr,
+                   float inv_gamma, int mode, dauc_stream_t stream);
+
+/*
+ * Same update over one dense gradient (w, g, w0, w_avg all [n]): the
+ * single-tensor form used by the micro-benchmarks and by callers whose
+ * gradient already lives in one buffer.
+ */
+int dauc_pd_update_dense(float* w, const float* g, const float* w0, float* w_avg, int64_t n,
+                         float lr, float inv_gamma, dauc_stream_t stream);
+
+/* ----------------------------------------------- a6: CoDA averaging */
+
+/*
+ * Completes one CoDA averaging round (main.py:33-54 + 297-301) after the
+ * caller's SUM all-reduce of the flat buffer:
+ *   flat[i] <- flat[i] / world            for i < n_avg        (parameters, a, b, alpha)
+ *   gcounts[k] <- gcounts[k] + lcounts[k]; lcounts[k] <- 0     (k = 0 pos, 1 neg; fp32)
+ * With world == 1 the caller skips the all-reduce and this only folds the counts.
+ */
+int dauc_coda_finalize(float* flat, int64_t n_avg, int world, float* lcounts, float* gcounts,
+                       dauc_stream_t stream);
+
+/* x[i] <- x[i] / divisor (fp32 IEEE division): stage-end average, main.py:338-339. */
+int dauc_scale_div(float* x, int64_t n, float divisor, dauc_stream_t stream);
+
+/* ------------------------------------------------ a8: exact AUC count */
+
+/* Bytes of zero-initialised scratch dauc_split_scores needs for n scores. */
+size_t dauc_split_workspace_size(int64_t n);
+
+/*
+ * Stable split of (scores, labels) into positive (label == 1) and negative
+ * (label != 1) score lists, the sklearn roc_curve(pos_label=1) convention used
+ * by main.py:79-80, in original order:
+ *   pos_out[0..P), neg_out[0..N), each sized n by the caller.
+ *   stats[4] (int64) = { P, N, #non-finite scores, #labels not in {-1, 1} }
+ */
+int dauc_split_scores(const float* scores, const void* labels, int label_dtype, int64_t n,
+                      float* pos_out, float* neg_out, int64_t* stats, void* workspace,
+                      size_t workspace_bytes, dauc_stream_t stream);
+
+/*
+ * Exact pairwise count replacing sklearn roc_curve + auc (main.py:79-81):
+ *   wins_ties[0] += #{(i, j): pos[i] >  neg[j]}
+ *   wins_ties[1] += #{(i, j): pos[i] == neg[j]}      (fp32 equality: -0 == +0)
+ * AUC = (2*wins + ties) / (2*P*N). Integer-exact; scores must be finite.
+ */
+int dauc_pair_count(const float* pos, int64_t P, const float* neg, int64_t N,
+                    unsigned long long* wins_ties, dauc_stream_t stream);
+
+/*
+ * dauc_pair_count with an explicit kernel variant (0 = the default used by
+ * dauc_pair_count; 1, 2 = alternative accumulation schemes kept for tuning).
+ * Every variant returns identical counts.
+ */
+int dauc_pair_count_variant(const float* pos, int64_t P, const float* neg, int64_t N,
+                            unsigned long long* wins_ties, int variant, dauc_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* DAUC_H_ */

@@ -1,0 +1,372 @@
+"""Parity of every HIP kernel against the CPU oracle and the reference's golden vectors.
+
+Tolerances (fp32 path, north_star: "within 1e-5 relative (fp32)"):
+  * surrogate F and scalar gradients: |got - ref| <= 1e-5 * scale, where scale is the
+    sum of magnitudes of the terms that make up the value (a plain relative bound
+    is meaningless when terms cancel to ~0); against the fp64 closed form 1e-6.
+  * dF/dh per element: |got - ref| <= 1e-5 * max(|ref|, c) with c = 2/B * (|h|+|k|) the
+    magnitude of the element's factors.
+  * update kernel, finalise, stage divide, label map / p_hat: bit-exact.
+  * AUC pair counts: bit-exact integers.
+"""
+from __future__ import annotations
+
+import warnings
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import coracle
+from oracle import reference_cpu as R
+
+pytestmark = pytest.mark.gpu
+
+
+def T(a, dev, dtype=None):
+    t = torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    return t if dtype is None else t.to(dtype)
+
+
+# ------------------------------------------------------------------ surrogate
+def _scales(h, y, a, b, al, p):
+    h = np.asarray(h, np.float64)
+    B = h.size
+    pos = (y == 1)
+    neg = (y == -1)
+    q = 1 - p
+    sF = (q * np.sum((h - a) ** 2 * pos) + p * np.sum((h - b) ** 2 * neg)
+          + 2 * abs(1 + al) * np.sum(p * h * neg + q * h * pos)) / B + abs(p * q * al * al)
+    sa = 2 * q * np.sum(np.abs(h - a) * pos) / B
+    sb = 2 * p * np.sum(np.abs(h - b) * neg) / B
+    sal = 2 * np.sum(p * h * neg + q * h * pos) / B + abs(2 * p * q * al)
+    return np.array([sF, sa, sb, sal])
+
+
+def _run_surrogate(ops, dev, h, y, abap, h_stride=1, ydtype=torch.int8):
+    B = h.size
+    if h_stride == 1:
+        th = T(h, dev)
+    else:
+        big = np.zeros((B, h_stride), np.float32)
+        big[:, 1] = h
+        th = T(big, dev)[:, 1]
+    ty = T(y, dev).to(ydtype)
+    out64 = torch.zeros(6, dtype=torch.float64, device=dev)
+    grad3 = torch.zeros(3, device=dev)
+    loss = torch.zeros((), device=dev)
+    dh = torch.empty(B, device=dev)
+    ops.surrogate_fwdbwd(th, ty, T(abap[:3], dev), T(abap[3:4], dev), dh=dh, out64=out64, grad3=grad3,
+                         loss=loss)
+    return out64.cpu().numpy(), dh.cpu().numpy(), grad3.cpu().numpy(), loss.item()
+
+
+def test_surrogate_golden(dev, golden):
+    from distributedauc_amd import ops
+
+    z = np.load(golden / "surrogate_cases.npz")
+    for ci in range(int(z["ncases"])):
+        h, y, abap = z[f"c{ci}_h"], z[f"c{ci}_y"].astype(np.int64), z[f"c{ci}_abap"]
+        out64, dh, g3, loss = _run_surrogate(ops, dev, h, y, abap)
+        ref32, ref64 = z[f"c{ci}_fp32"].astype(np.float64), z[f"c{ci}_fp64"]
+        sc = _scales(h, y, *abap.astype(np.float64))
+        assert np.all(np.abs(out64[:4] - ref32) <= 1e-5 * sc + 1e-12), (ci, out64[:4], ref32)
+        assert np.all(np.abs(out64[:4] - ref64) <= 1e-6 * sc + 1e-12), (ci, out64[:4], ref64)
+        assert np.all(np.abs(g3 - ref32[1:]) <= 1e-5 * sc[1:] + 1e-12)
+        assert abs(loss - ref32[0]) <= 1e-5 * sc[0] + 1e-12
+        assert out64[4] == np.sum(y == 1) and out64[5] == np.sum(y == -1)
+        a, b, al, p = abap.astype(np.float64)
+        k = np.where(y == 1, a + 1 + al, b - 1 - al)
+        c = 2.0 / h.size * (np.abs(h) + np.abs(k))
+        dref = z[f"c{ci}_dh32"].astype(np.float64)
+        assert np.all(np.abs(dh - dref) <= 1e-5 * np.maximum(np.abs(dref), c)), ci
+
+
+@pytest.mark.parametrize("ydtype", [torch.int8, torch.int32, torch.int64])
+@pytest.mark.parametrize("stride", [1, 2, 3])
+def test_surrogate_strides_and_label_types(dev, ydtype, stride):
+    from distributedauc_amd import ops
+
+    rng = np.random.default_rng(stride)
+    for B in (1, 255, 256, 1023, 5000, 70_001):
+        h = rng.random(B, dtype=np.float32)
+        y = np.where(rng.random(B) < 0.2, 1, -1).astype(np.int64)
+        y[rng.random(B) < 0.05] = 0
+        abap = np.array([0.2, -0.3, 0.05, 0.21], np.float32)
+        out64, dh, _, _ = _run_surrogate(ops, dev, h, y, abap, stride, ydtype)
+        F, dh64, da, db, dal = R.surrogate_closed_form(h, y, *abap)
+        sc = _scales(h, y, *abap.astype(np.float64))
+        assert np.all(np.abs(out64[:4] - [F, da, db, dal]) <= 1e-6 * sc + 1e-12), (B, stride)
+        k = np.where(y == 1, 0.2 + 1 + 0.05, -0.3 - 1 - 0.05)
+        c = 2.0 / B * (np.abs(h) + np.abs(k))
+        assert np.all(np.abs(dh - dh64) <= 1e-6 * np.maximum(np.abs(dh64), c))
+        assert np.all(dh[y == 0] == 0)
+
+
+def test_surrogate_large_deterministic(dev):
+    """Multi-block path (last-arriver reduce) at 2^24: fp64 closed form + bitwise run-to-run."""
+    from distributedauc_amd import ops
+
+    B = 1 << 24
+    g = torch.Generator(device=dev).manual_seed(3)
+    h = torch.rand(B, device=dev, generator=g)
+    y = torch.where(torch.rand(B, device=dev, generator=g) < 0.1, 1, -1).to(torch.int8)
+    abap = torch.tensor([0.1, -0.2, 0.3, 0.1], device=dev)
+    outs = []
+    for _ in range(3):
+        o = torch.zeros(6, dtype=torch.float64, device=dev)
+        ops.surrogate_fwdbwd(h, y, abap[:3], abap[3:], out64=o)
+        outs.append(o.cpu().numpy())
+    assert all(np.array_equal(outs[0], o) for o in outs[1:])
+    hn, yn = h.cpu().numpy(), y.cpu().numpy().astype(np.int64)
+    F, _, da, db, dal = R.surrogate_closed_form(hn, yn, 0.1, -0.2, 0.3, 0.1)
+    sc = _scales(hn, yn, 0.1, -0.2, 0.3, float(np.float32(0.1)))
+    assert np.all(np.abs(outs[0][:4] - [F, da, db, dal]) <= 1e-9 * sc + 1e-12)
+    assert outs[0][4] == np.sum(yn == 1)
+
+
+def test_class_sums_and_alpha(dev):
+    from distributedauc_amd import ops
+
+    rng = np.random.default_rng(5)
+    sums = torch.zeros(4, dtype=torch.float64, device=dev)
+    ref = np.zeros(4)
+    for B in (32, 3000, 100_000):
+        h = rng.random(B, dtype=np.float32)
+        y = np.where(rng.random(B) < 0.3, 1, -1).astype(np.int8)
+        ops.class_sums(T(h, dev), T(y, dev), sums, accumulate=True)
+        hd = h.astype(np.float64)
+        ref += [hd[y == -1].sum(), (y == -1).sum(), hd[y == 1].sum(), (y == 1).sum()]
+    got = sums.cpu().numpy()
+    assert np.allclose(got, ref, rtol=1e-12)
+    alpha = torch.zeros(1, device=dev)
+    ops.alpha_from_sums(sums, alpha)
+    assert alpha.item() == np.float32(got[0] / got[1] - got[2] / got[3])
+
+
+def test_label_map_phat_exact(dev):
+    from distributedauc_amd import ops
+
+    rng = np.random.default_rng(9)
+    for split in (4, 499, 0):
+        lab = rng.integers(0, 1000, size=256).astype(np.int64)
+        lc = torch.tensor([3.0, 17.0], device=dev)
+        gc = torch.tensor([120.0, 901.0], device=dev)
+        y8 = torch.empty(256, dtype=torch.int8, device=dev)
+        p = torch.zeros(1, device=dev)
+        ops.label_map_phat(T(lab, dev), split, y8, lc, gc, p)
+        ym = R.label_map(lab, split)
+        assert np.array_equal(y8.cpu().numpy(), ym)
+        lpos, lneg = 3 + (ym == 1).sum(), 17 + (ym == -1).sum()
+        assert lc.cpu().tolist() == [lpos, lneg]
+        assert p.cpu().numpy()[0] == R.phat(120.0, 901.0, lpos, lneg)
+
+
+# ------------------------------------------------------------------ update
+def test_pd_update_dense_bitexact(dev):
+    from distributedauc_amd import ops
+
+    rng = np.random.default_rng(1)
+    for n in (1, 3, 4096, 4097, 1_000_003):
+        w, g, w0, avg = (rng.standard_normal(n).astype(np.float32) for _ in range(4))
+        tw, tavg = T(w, dev), T(avg, dev)
+        ops.pd_update_dense(tw, T(g, dev), T(w0, dev), tavg, lr=0.1 / 3, gamma=2000.0)
+        ew, eavg = coracle.pd_update(w, g, w0, 0.1 / 3, 2000.0, avg)
+        assert np.array_equal(tw.cpu().numpy(), ew), n
+        assert np.array_equal(tavg.cpu().numpy(), eavg), n
+        # the torch-CPU restatement (the reference's own op sequence) agrees bit for bit
+        assert np.array_equal(R.dppd_sg_flat(w, g, w0, 0.1 / 3, 2000.0), ew)
+
+
+def test_dppd_sg_golden_generic_path(dev, golden):
+    """main.dppd_sg parity through the reference-signature wrapper (per-tensor path)."""
+    from distributedauc_amd import main as M
+
+    z = np.load(golden / "dppd_sg.npz")
+    torch.manual_seed(5)
+    net = torch.nn.Sequential(torch.nn.Linear(40, 30), torch.nn.BatchNorm1d(30), torch.nn.Linear(30, 2)).to(dev)
+    names = [n for n, _ in net.named_parameters()]
+    off = 0
+    model0 = {}
+    for (name, p) in net.named_parameters():
+        k = p.numel()
+        p.data.copy_(T(z["w"][off:off + k].reshape(p.shape), dev))
+        p.grad = T(z["g"][off:off + k].reshape(p.shape), dev)
+        model0[name] = T(z["w0"][off:off + k].reshape(p.shape), dev)
+        off += k
+    mk = lambda v: torch.tensor([v], dtype=torch.float32, device=dev)  # noqa: E731
+    a, b, al = (mk(v) for v in z["scalars"])
+    for t, gv in zip((a, b, al), z["grad3"]):
+        t.grad = mk(gv)
+    a0, b0, al0 = (mk(v) for v in z["anchor3"])
+    M.dppd_sg(net, a, b, al, model0, a0, b0, al0, float(z["lr"]), float(z["gamma"]))
+    got = np.concatenate([p.detach().cpu().numpy().reshape(-1) for p in net.parameters()])
+    assert np.array_equal(got, z["w_new"])
+    assert np.array_equal(np.array([a.item(), b.item(), al.item()], np.float32), z["scalars_new"])
+    assert names
+
+
+def test_pd_update_segments_flat(dev):
+    """Flat-buffer update with per-parameter gradient segments of awkward sizes/layouts."""
+    from distributedauc_amd.flat import FlatState
+
+    torch.manual_seed(0)
+    net = torch.nn.Sequential(torch.nn.Conv2d(3, 5, 3), torch.nn.BatchNorm2d(5), torch.nn.Conv2d(5, 7, 1),
+                              torch.nn.Flatten(), torch.nn.Linear(7 * 4 * 4, 2)).to(dev)
+    net = net.to(memory_format=torch.channels_last)
+    st = FlatState(net)
+    st.snapshot_anchor()
+    st.anchor[: st.n_params] += 0.01 * torch.randn(st.n_params, device=dev)
+    st.reset_average()
+    x = torch.randn(4, 3, 6, 6, device=dev).contiguous(memory_format=torch.channels_last)
+    net(x).square().sum().backward()
+    st.grad3.copy_(torch.tensor([0.3, -0.1, 0.2, 0.0]))
+    st.abalpha.copy_(torch.tensor([0.5, 0.25, -0.5]))
+    st.anchor3.copy_(torch.tensor([0.4, 0.2, -0.4]))
+    before = {n: p.detach().clone() for n, p in net.named_parameters()}
+    grads = {n: p.grad.clone() for n, p in net.named_parameters()}
+    w0 = {n: torch.as_strided(st.anchor, p.shape, p.stride(), o).clone() for n, p, o, _ in st.entries}
+    avg0 = st.avg.clone()
+    st.update(0.1, 10.0, "reference")
+    for n, p in net.named_parameters():
+        e = R.pd_step(before[n].cpu(), grads[n].cpu(), w0[n].cpu(), 0.1, 10.0)
+        assert torch.equal(p.detach().cpu(), e), n
+    # running average: avg + w_new over every parameter slot
+    assert torch.equal(st.avg.cpu(), (avg0 + st.params).cpu())
+    ea, eb, eal = R.scalar_update(0.5, 0.25, -0.5, 0.3, -0.1, 0.2, 0.4, 0.2, -0.4, 0.1, 10.0, "reference")
+    assert st.abalpha.cpu().numpy().tolist() == [ea, eb, eal]
+
+
+def test_scalar_update_paper_mode(dev):
+    from distributedauc_amd import ops
+
+    sc = torch.tensor([0.5, 0.25, -0.5], device=dev)
+    ops.pd_update(sc, sc, None, None, 0, scalars=sc, grad3=torch.tensor([0.3, -0.1, 0.2], device=dev),
+                  anchor3=torch.tensor([0.4, 0.2, -0.4], device=dev), lr=0.1, gamma=10.0, mode="paper")
+    e = R.scalar_update(0.5, 0.25, -0.5, 0.3, -0.1, 0.2, 0.4, 0.2, -0.4, 0.1, 10.0, "paper")
+    assert sc.cpu().numpy().tolist() == list(e)
+
+
+def test_coda_finalize_and_scale_div(dev):
+    from distributedauc_amd import ops
+
+    rng = np.random.default_rng(2)
+    for world in (1, 2, 4, 8, 3):
+        n = 10_001
+        x = rng.standard_normal(n + 5).astype(np.float32)
+        x[n + 3:] = [7.0, 29.0]
+        tx = T(x, dev)
+        gc = torch.tensor([100.0, 400.0], device=dev)
+        ops.coda_finalize(tx, n + 3, world, tx[n + 3:n + 5], gc)
+        got = tx.cpu().numpy()
+        exp = x.copy()
+        if world > 1:
+            exp[: n + 3] = (torch.from_numpy(x[: n + 3]) / float(world)).numpy()
+        assert np.array_equal(got[: n + 3], exp[: n + 3])
+        assert got[n + 3:n + 5].tolist() == [0.0, 0.0] and gc.cpu().tolist() == [107.0, 429.0]
+    y = rng.standard_normal(777).astype(np.float32)
+    ty = T(y, dev)
+    ops.scale_div(ty, 15.0)
+    assert np.array_equal(ty.cpu().numpy(), (torch.from_numpy(y) / 15).numpy())
+
+
+# ------------------------------------------------------------------ exact AUC
+def _counts_gpu(dev, y, s, world=1, rank=0, variant=0):
+    from distributedauc_amd.auc import ExactAUC
+
+    return ExactAUC(world=world, rank=rank, variant=variant, reduce=False).counts(T(y, dev), T(s, dev))
+
+
+def test_auc_golden(dev, golden):
+    from distributedauc_amd.auc import ExactAUC
+
+    z = np.load(golden / "auc_cases.npz")
+    for name in z["names"]:
+        y, s = z[f"{name}_y"], z[f"{name}_s"]
+        W, Tt, P, N, two_u = (int(v) for v in z[f"{name}_counts"])
+        for variant in (0, 1, 2):
+            c = _counts_gpu(dev, y, s, variant=variant)
+            assert (c["wins"], c["ties"], c["P"], c["N"]) == (W, Tt, P, N), (name, variant, c)
+            assert 2 * c["wins"] + c["ties"] == two_u
+        auc = ExactAUC.from_counts(c)
+        ref = float(z[f"{name}_auc"])
+        assert abs(auc - ref) <= 4 * np.spacing(ref), (name, auc, ref)
+
+
+@pytest.mark.parametrize("n,p,ties", [(1 << 20, 0.01, False), (1 << 20, 0.3, True), (1 << 24, 0.01, False),
+                                      (1 << 24, 0.01, True)])
+def test_auc_counts_large(dev, n, p, ties):
+    """Full-size parity: 2^24 scores at 1 % positives (configs[3]) vs the C oracle, bit-exact."""
+    rng = np.random.default_rng(n + int(ties))
+    s = rng.random(n, dtype=np.float32)
+    if ties:
+        s = (np.floor(s * 4096) / 4096).astype(np.float32)
+    y = np.where(rng.random(n) < p, 1, -1).astype(np.int8)
+    e = coracle.auc_counts(y.astype(np.int64), s)
+    c = _counts_gpu(dev, y, s)
+    assert (c["wins"], c["ties"], c["P"], c["N"]) == (e["wins"], e["ties"], e["P"], e["N"])
+
+
+def test_auc_sharded_sum_is_invariant(dev):
+    """Positive-block sharding over G ranks sums to the unsharded counts for every G."""
+    rng = np.random.default_rng(4)
+    n = 300_000
+    s = (np.floor(rng.random(n) * 1000) / 1000).astype(np.float32)
+    y = np.where(rng.random(n) < 0.05, 1, -1).astype(np.int8)
+    full = _counts_gpu(dev, y, s)
+    for G in (2, 3, 4, 8):
+        parts = [_counts_gpu(dev, y, s, world=G, rank=r) for r in range(G)]
+        assert sum(c["wins"] for c in parts) == full["wins"]
+        assert sum(c["ties"] for c in parts) == full["ties"]
+
+
+def test_auc_errors_like_sklearn(dev):
+    from distributedauc_amd.auc import AUC
+
+    with pytest.raises(ValueError):
+        AUC(torch.tensor([1, -1, 1], device=dev), torch.tensor([0.1, float("nan"), 0.3], device=dev))
+    with pytest.raises(ValueError):
+        AUC(torch.tensor([1, -1, 1], device=dev), torch.tensor([0.1, float("inf"), 0.3], device=dev))
+    with pytest.raises(ValueError):
+        AUC(torch.tensor([1, -1, 0], device=dev), torch.tensor([0.1, 0.2, 0.3], device=dev))
+    with warnings.catch_warnings(record=True) as rec:
+        warnings.simplefilter("always")
+        v = AUC(torch.tensor([1, 1, 1], device=dev), torch.tensor([0.1, 0.2, 0.3], device=dev))
+    assert np.isnan(v) and rec
+    # {0, 1} labels are binary for sklearn: 0 is the negative class
+    assert AUC(np.array([1, 0, 1, 0]), np.array([0.9, 0.1, 0.8, 0.2], np.float32)) == 1.0
+
+
+def test_split_is_stable(dev):
+    from distributedauc_amd import ops
+
+    rng = np.random.default_rng(8)
+    n = 123_457
+    s = rng.random(n, dtype=np.float32)
+    y = np.where(rng.random(n) < 0.2, 1, -1).astype(np.int8)
+    pos, neg, stats = ops.split_scores(T(s, dev), T(y, dev))
+    P, N, nf, other = stats.cpu().tolist()
+    assert (P, N, nf, other) == ((y == 1).sum(), (y != 1).sum(), 0, 0)
+    assert np.array_equal(pos[:P].cpu().numpy(), s[y == 1])
+    assert np.array_equal(neg[:N].cpu().numpy(), s[y != 1])
+
+
+def test_pair_count_edge_sizes(dev):
+    from distributedauc_amd import ops
+
+    rng = np.random.default_rng(6)
+    for P, N in ((1, 1), (1, 5000), (3000, 1), (2049, 2047), (4097, 9001), (0, 10), (10, 0)):
+        pos = (np.floor(rng.random(P) * 64) / 64).astype(np.float32)
+        neg = (np.floor(rng.random(N) * 64) / 64).astype(np.float32)
+        for variant in (0, 1, 2):
+            wt = torch.zeros(2, dtype=torch.int64, device=dev)
+            ops.pair_count(T(pos, dev), T(neg, dev), wt, variant=variant)
+            assert tuple(wt.cpu().tolist()) == coracle.pair_count_bruteforce(pos, neg), (P, N, variant)
+    # misaligned negative base pointer (sharded slices)
+    pos = rng.random(777, dtype=np.float32)
+    negall = rng.random(10_001, dtype=np.float32)
+    tn = T(negall, dev)
+    wt = torch.zeros(2, dtype=torch.int64, device=dev)
+    ops.pair_count(T(pos, dev), tn[1:], wt)
+    assert tuple(wt.cpu().tolist()) == coracle.pair_count_bruteforce(pos, negall[1:])
+
