@@ -34,6 +34,11 @@ ALIGN = 64  # elements: every parameter view starts on a 256-byte boundary
 TAIL = 8    # a, b, alpha, lpos, lneg + 3 pad (keeps the buffer a multiple of 16 B)
 
 
+def _check_device(dev: torch.device) -> None:
+    if dev.type != "cuda":
+        raise RuntimeError(f"FlatState lives in GPU memory; got device {dev}")
+
+
 def _dense_layout(t: torch.Tensor) -> bool:
     """True if t's elements occupy exactly numel contiguous slots (any dim order)."""
     if t.numel() <= 1:
@@ -55,8 +60,7 @@ class FlatState:
         if not params:
             raise ValueError("model has no parameters")
         dev = torch.device(device) if device is not None else params[0][1].device
-        if dev.type != "cuda":
-            raise RuntimeError(f"FlatState lives in GPU memory; got device {dev}")
+        _check_device(dev)
         self.device = dev
         entries = []
         off = 0

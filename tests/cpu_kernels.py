@@ -1,0 +1,99 @@
+"""CPU stand-ins for the libdauc.so kernels, built on the oracle (TEST INFRASTRUCTURE).
+
+Used only by the CPU (no-GPU) tests of the host orchestration: the CoDA loop,
+its multi-process gloo averaging and the flat-buffer bookkeeping run unchanged
+while each ``distributedauc_amd.ops`` call is served by the oracle's restatement
+of the same reference lines. The product itself has no CPU path; these
+stand-ins are installed only by ``install(monkeypatch)`` inside tests.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from oracle import reference_cpu as R
+
+
+def label_map_phat(labels, split_index, y_out, lcounts, gcounts, p_hat):
+    y = torch.where(labels <= split_index, -1, 1)
+    y_out.copy_(y.to(torch.int8))
+    lcounts[0] += float((y == 1).sum())
+    lcounts[1] += float((y == -1).sum())
+    p_hat[0] = float(R.phat(gcounts[0].item(), gcounts[1].item(), lcounts[0].item(), lcounts[1].item()))
+
+
+def surrogate_fwdbwd(h, y, abalpha, p_hat, *, dh=None, out64=None, grad3=None, loss=None):
+    a, b, al = (float(v) for v in abalpha[:3])
+    F, dh64, da, db, dal = R.surrogate_closed_form(h.detach().numpy(), y.numpy(), a, b, al, float(p_hat[0]))
+    if dh is not None:
+        dh.copy_(torch.from_numpy(dh64.astype(np.float32)))
+    if out64 is not None:
+        out64[:6] = torch.tensor([F, da, db, dal, float((y == 1).sum()), float((y == -1).sum())])
+    if grad3 is not None:
+        grad3[:3] = torch.tensor([da, db, dal], dtype=torch.float32)
+    if loss is not None:
+        loss.fill_(float(F))
+
+
+def class_sums(h, y, sums4, accumulate=True):
+    hd = h.detach().double()
+    v = torch.tensor([hd[y == -1].sum(), (y == -1).sum(), hd[y == 1].sum(), (y == 1).sum()], dtype=torch.float64)
+    if accumulate:
+        sums4 += v
+    else:
+        sums4.copy_(v)
+
+
+def alpha_from_sums(sums4, alpha):
+    s = sums4.tolist()
+    alpha[0] = float(np.float32(s[0] / s[1] - s[2] / s[3]))
+
+
+def coda_finalize(flat, n_avg, world, lcounts, gcounts):
+    if world > 1:
+        flat[:n_avg] /= float(world)
+    gcounts += lcounts
+    lcounts.zero_()
+
+
+def scale_div(x, divisor):
+    x /= float(divisor)
+
+
+def pd_update(w, w0, w_avg, segs, nseg, *, scalars=None, grad3=None, anchor3=None, lr, gamma, mode="reference"):
+    """Walks the same segment table the HIP kernel receives (raw host pointers on CPU)."""
+    if scalars is not None:
+        s = scalars.tolist()
+        g = grad3.tolist()
+        an = anchor3.tolist()
+        scalars[:3] = torch.tensor(R.scalar_update(*s[:3], *g[:3], *an[:3], lr, gamma, mode))
+    for i in range(nseg):
+        sg = segs[i]
+        n, off = sg.numel, sg.offset
+        g = torch.from_numpy(np.ctypeslib.as_array((ctypes.c_float * n).from_address(sg.grad)).copy())
+        new = R.pd_step(w[off:off + n], g, w0[off:off + n], lr, gamma)
+        w[off:off + n] = new
+        if w_avg is not None:
+            w_avg[off:off + n] += new
+
+
+def install(monkeypatch):
+    from distributedauc_amd import flat, ops
+
+    for name in ("label_map_phat", "surrogate_fwdbwd", "class_sums", "alpha_from_sums", "coda_finalize",
+                 "scale_div", "pd_update"):
+        monkeypatch.setattr(ops, name, globals()[name])
+    monkeypatch.setattr(flat, "_check_device", lambda dev: None)
+
+
+class _Patcher:
+    """Minimal monkeypatch for spawned worker processes (no pytest fixture there)."""
+
+    def setattr(self, obj, name, value):
+        setattr(obj, name, value)
+
+
+def install_in_process():
+    install(_Patcher())
