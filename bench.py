@@ -29,7 +29,6 @@ from pathlib import Path
 
 REPO = Path(__file__).resolve().parent
 sys.path.insert(0, str(REPO))
-os.environ.setdefault("MIOPEN_FIND_MODE", "FAST")
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
@@ -88,6 +87,10 @@ class KernelTimer:
         return float(np.mean([a.elapsed_time(b) for a, b in self.pairs])) if self.pairs else float("nan")
 
 
+def log(msg: str):
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def max_over_ranks(x: float, world: int) -> float:
     if world == 1:
         return x
@@ -112,6 +115,7 @@ def bench_train(args, world, rank, device):
     coda = CoDA(net, lr=0.1, gamma=2000.0, T0=10 ** 9, I=args.I, split_index=split, world=world, rank=rank,
                 autocast_dtype=torch.bfloat16, device=device)
     it = iter(loader)
+    log(f"rank {rank}: model + data ready, first steps compile/tune MIOpen kernels")
     coda.average_all()            # main.py:141-142
     coda.begin_stage(1, it)       # alpha estimate + anchors (untimed)
     upd = KernelTimer(ops, "pd_update")
@@ -120,6 +124,7 @@ def bench_train(args, world, rank, device):
         x, y = next(it)
         coda.train_step(x, y)
     torch.cuda.synchronize()
+    log(f"rank {rank}: warm-up done")
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()

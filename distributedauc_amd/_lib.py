@@ -50,6 +50,7 @@ SIGNATURES = {
     "dauc_pd_update": (_int, [_vp, _vp, _vp, ctypes.POINTER(GradSeg), _int, _vp, _vp, _vp, _f32, _f32,
                               _int, _vp]),
     "dauc_pd_update_dense": (_int, [_vp, _vp, _vp, _vp, _i64, _f32, _f32, _vp]),
+    "dauc_pd_update_dense_variant": (_int, [_vp, _vp, _vp, _vp, _i64, _f32, _f32, _int, _vp]),
     "dauc_coda_finalize": (_int, [_vp, _i64, _int, _vp, _vp, _vp]),
     "dauc_scale_div": (_int, [_vp, _i64, _f32, _vp]),
     "dauc_split_workspace_size": (_sz, [_i64]),

@@ -49,33 +49,47 @@ def _needs_build() -> bool:
     return any(p.stat().st_mtime > t for p in deps)
 
 
-def _compile(src: Path) -> Path:
-    obj = OBJ_DIR / (src.stem + ".o")
-    cmd = [HIPCC, *CFLAGS, "-c", str(src), "-o", str(obj)]
+def _compile(src: Path, obj_dir: Path = OBJ_DIR, defines: tuple = ()) -> Path:
+    obj = obj_dir / (src.stem + ".o")
+    cmd = [HIPCC, *CFLAGS, *[f"-D{d}" for d in defines], "-c", str(src), "-o", str(obj)]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src.name}:\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
     return obj
 
 
-def build_library(force: bool = False, verbose: bool = False) -> Path:
-    """Compile every csrc/*.hip for gfx950 and link libdauc.so (incremental)."""
-    if not force and not _needs_build():
+def build_library(force: bool = False, verbose: bool = False, out: Path | None = None,
+                  defines: tuple = ()) -> Path:
+    """Compile every csrc/*.hip for gfx950 and link libdauc.so (incremental).
+
+    ``out``/``defines`` build a tuning variant of the library side by side
+    (e.g. ``defines=("DAUC_SURROGATE_SLOTS=2",)``); the product loads LIB_PATH.
+    """
+    target = Path(out) if out is not None else LIB_PATH
+    if out is None and not defines and not force and not _needs_build():
         return LIB_PATH
-    OBJ_DIR.mkdir(exist_ok=True)
+    obj_dir = OBJ_DIR if out is None else OBJ_DIR / target.stem
+    obj_dir.mkdir(parents=True, exist_ok=True)
     srcs = sources()
     with cf.ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
-        objs = list(ex.map(_compile, srcs))
-    tmp = LIB_PATH.with_suffix(".so.tmp")
+        objs = list(ex.map(lambda s: _compile(s, obj_dir, tuple(defines)), srcs))
+    tmp = target.with_suffix(".so.tmp")
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs), "-o", str(tmp)]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed:\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
-    os.replace(tmp, LIB_PATH)
+    os.replace(tmp, target)
     if verbose:
-        print(f"built {LIB_PATH}", file=sys.stderr)
-    return LIB_PATH
+        print(f"built {target}", file=sys.stderr)
+    return target
 
 
 if __name__ == "__main__":
-    build_library(force="--force" in sys.argv, verbose=True)
+    import argparse
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("--out", default=None, help="write a tuning variant here instead of libdauc.so")
+    ap.add_argument("-D", dest="defines", action="append", default=[])
+    a = ap.parse_args()
+    build_library(force=a.force, verbose=True, out=a.out, defines=tuple(a.defines))

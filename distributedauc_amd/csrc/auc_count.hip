@@ -188,8 +188,6 @@ int launch_split(const float* s, const LT* lab, int64_t n, float* pos_out, float
 
 constexpr int kPcThreads = 256;
 constexpr int kNegTile = 2048;  // negatives per LDS tile (8 KB)
-constexpr int kRP = 8;          // positives held per lane
-constexpr int64_t kPosPerBlock = int64_t(kPcThreads) * kRP;
 constexpr int64_t kTargetBlocks = 8192;
 
 __device__ __forceinline__ float nan_f() { return __builtin_nanf(""); }
@@ -342,38 +340,45 @@ int dauc_pair_count_variant(const float* pos, int64_t P, const float* neg, int64
         (N > 0 && neg == nullptr))
         return DAUC_EINVAL;
     if (P == 0 || N == 0) return DAUC_OK;
-    const int64_t gx = (P + kPosPerBlock - 1) / kPosPerBlock;
+    // variant = mode + 3 * rp_index; mode: accumulation scheme, rp: positives per lane {8, 4, 16}
+    if (variant < 0 || variant >= 9) return DAUC_EINVAL;
+    const int mode = variant % 3;
+    const int rp = variant / 3 == 0 ? 8 : (variant / 3 == 1 ? 4 : 16);
+    const int64_t pos_per_block = int64_t(kPcThreads) * rp;
+    const int64_t gx = (P + pos_per_block - 1) / pos_per_block;
     if (gx > 0x7fffffffLL) return DAUC_EINVAL;
     const int64_t tiles = (N + kNegTile - 1) / kNegTile;
     int64_t gy = (kTargetBlocks + gx - 1) / gx;
     if (gy > tiles) gy = tiles;
-    // per-lane counters are 32-bit: keep each block's negative slice below 2^30
-    const int64_t min_gy = (N + (int64_t(1) << 30) - 1) >> 30;
+    // per-lane counters are 32-bit: keep each block's negative slice below 2^27 (x RP <= 16 per lane)
+    const int64_t cap = int64_t(1) << 27;
+    const int64_t min_gy = (N + cap - 1) / cap;
     if (gy < min_gy) gy = min_gy;
     if (gy > 65535) gy = 65535;
     int64_t per = (N + gy - 1) / gy;
     per = (per + kNegTile - 1) / kNegTile * kNegTile;
     gy = (N + per - 1) / per;
-    if (per > (int64_t(1) << 30) + kNegTile) return DAUC_EINVAL;
+    if (per > cap + kNegTile) return DAUC_EINVAL;
     const int aligned = (reinterpret_cast<uintptr_t>(neg) & 15u) == 0;
     const dim3 grid(static_cast<unsigned>(gx), static_cast<unsigned>(gy));
     hipStream_t st = as_hip(stream);
+#define DAUC_PC_LAUNCH(RPV, MV)                                                                    \
+    hipLaunchKernelGGL((pair_count_kernel<RPV, MV>), grid, dim3(kPcThreads), 0, st, pos, P, neg, N, \
+                       per, aligned, wins_ties)
     switch (variant) {
-        case 0:
-            hipLaunchKernelGGL((pair_count_kernel<kRP, 0>), grid, dim3(kPcThreads), 0, st, pos, P,
-                               neg, N, per, aligned, wins_ties);
-            break;
-        case 1:
-            hipLaunchKernelGGL((pair_count_kernel<kRP, 1>), grid, dim3(kPcThreads), 0, st, pos, P,
-                               neg, N, per, aligned, wins_ties);
-            break;
-        case 2:
-            hipLaunchKernelGGL((pair_count_kernel<kRP, 2>), grid, dim3(kPcThreads), 0, st, pos, P,
-                               neg, N, per, aligned, wins_ties);
-            break;
-        default:
-            return DAUC_EINVAL;
+        case 0: DAUC_PC_LAUNCH(8, 0); break;
+        case 1: DAUC_PC_LAUNCH(8, 1); break;
+        case 2: DAUC_PC_LAUNCH(8, 2); break;
+        case 3: DAUC_PC_LAUNCH(4, 0); break;
+        case 4: DAUC_PC_LAUNCH(4, 1); break;
+        case 5: DAUC_PC_LAUNCH(4, 2); break;
+        case 6: DAUC_PC_LAUNCH(16, 0); break;
+        case 7: DAUC_PC_LAUNCH(16, 1); break;
+        case 8: DAUC_PC_LAUNCH(16, 2); break;
     }
+#undef DAUC_PC_LAUNCH
+    (void)mode;
+    (void)rp;
     return launch_status();
 }
 

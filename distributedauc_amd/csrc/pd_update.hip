@@ -21,17 +21,22 @@ namespace dauc {
 namespace {
 
 constexpr int kThreads = 256;
-constexpr int kVecPerThread = 4;                                   // float4 per thread
-constexpr int64_t kElemsPerBlock = int64_t(kThreads) * 4 * kVecPerThread;  // 4096 floats
-constexpr int kMaxSeg = 96;                                       // segments per launch
+constexpr int kMaxSeg = 176;  // segments per launch (kernel-argument table, < 4 KB)
+
+// Geometry: VPT float4 per thread -> 256*4*VPT elements per block. The default
+// (variant 0) is VPT = 2 with non-temporal g/w0 loads: fastest on MI355X
+// (scripts/micro_kernels.py sweep, 82 us for ResNet-50's 23.5M parameters).
+
+constexpr int64_t elems_per_block(int vpt) { return int64_t(kThreads) * 4 * vpt; }
 
 struct SegTable {
     int nseg;
     int blk_start[kMaxSeg + 1];  // first block of each segment; blk_start[nseg] = grid
     const float* grad[kMaxSeg];
-    int64_t offset[kMaxSeg];
-    int64_t numel[kMaxSeg];
+    int offset[kMaxSeg];         // element offsets / counts fit 31 bits (checked on the host)
+    int numel[kMaxSeg];
 };
+static_assert(sizeof(SegTable) < 4000, "kernel-argument table must stay below 4 KB");
 
 __device__ __forceinline__ float pd_step(float w, float g, float w0, float lr, float invg) {
     const float d = __fsub_rn(w, w0);       // (param.data - model0[name])
@@ -61,7 +66,7 @@ __device__ void scalar_update(float* s, const float* g3, const float* a3, float 
     s[2] = al_new;
 }
 
-template <bool AVG>
+template <bool AVG, int VPT, bool NT>
 __global__ __launch_bounds__(kThreads) void pd_update_kernel(
     float* __restrict__ w, const float* __restrict__ w0, float* __restrict__ wavg, SegTable tab,
     float lr, float invg, float* __restrict__ scalars, const float* __restrict__ grad3,
@@ -80,40 +85,59 @@ __global__ __launch_bounds__(kThreads) void pd_update_kernel(
     const float* __restrict__ g = tab.grad[lo];
     const int64_t off = tab.offset[lo];
     const int64_t n = tab.numel[lo];
+    constexpr int64_t kElemsPerBlock = elems_per_block(VPT);
     const int64_t e0 = int64_t(bid - tab.blk_start[lo]) * kElemsPerBlock;
     float* __restrict__ ws = w + off;
     const float* __restrict__ w0s = w0 + off;
     float* __restrict__ as = AVG ? wavg + off : nullptr;
 
     const bool vec_ok = ((off & 3) == 0) && ((reinterpret_cast<uintptr_t>(g) & 15u) == 0);
-    if (vec_ok && e0 + kElemsPerBlock <= n) {
-        // full block: 4 independent float4 streams per thread, all loads issued first
-        f32x4 wv[kVecPerThread], gv[kVecPerThread], zv[kVecPerThread], av[kVecPerThread];
+    if (vec_ok) {
+        // VPT independent float4 slots per thread, all loads issued before any math.
+        // A segment's last block guards each slot; only its final n % 4 elements go scalar.
+        f32x4 wv[VPT], gv[VPT], zv[VPT], av[VPT];
+        bool full[VPT];
 #pragma unroll
-        for (int v = 0; v < kVecPerThread; ++v) {
+        for (int v = 0; v < VPT; ++v) {
             const int64_t i = e0 + (int64_t(v) * kThreads + threadIdx.x) * 4;
-            wv[v] = *reinterpret_cast<const f32x4*>(ws + i);
-            gv[v] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(g + i));
-            zv[v] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(w0s + i));
-            if (AVG) av[v] = *reinterpret_cast<const f32x4*>(as + i);
+            full[v] = i + 4 <= n;
+            if (full[v]) {
+                wv[v] = *reinterpret_cast<const f32x4*>(ws + i);
+                if (NT) {
+                    gv[v] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(g + i));
+                    zv[v] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(w0s + i));
+                } else {
+                    gv[v] = *reinterpret_cast<const f32x4*>(g + i);
+                    zv[v] = *reinterpret_cast<const f32x4*>(w0s + i);
+                }
+                if (AVG) av[v] = *reinterpret_cast<const f32x4*>(as + i);
+            }
         }
 #pragma unroll
-        for (int v = 0; v < kVecPerThread; ++v) {
+        for (int v = 0; v < VPT; ++v) {
             const int64_t i = e0 + (int64_t(v) * kThreads + threadIdx.x) * 4;
-            f32x4 r;
+            if (full[v]) {
+                f32x4 r;
 #pragma unroll
-            for (int c = 0; c < 4; ++c) r[c] = pd_step(wv[v][c], gv[v][c], zv[v][c], lr, invg);
-            *reinterpret_cast<f32x4*>(ws + i) = r;
-            if (AVG) {
-                f32x4 a;
+                for (int c = 0; c < 4; ++c) r[c] = pd_step(wv[v][c], gv[v][c], zv[v][c], lr, invg);
+                *reinterpret_cast<f32x4*>(ws + i) = r;
+                if (AVG) {
+                    f32x4 a;
 #pragma unroll
-                for (int c = 0; c < 4; ++c) a[c] = __fadd_rn(av[v][c], r[c]);
-                *reinterpret_cast<f32x4*>(as + i) = a;
+                    for (int c = 0; c < 4; ++c) a[c] = __fadd_rn(av[v][c], r[c]);
+                    *reinterpret_cast<f32x4*>(as + i) = a;
+                }
+            } else {
+                for (int64_t j = i; j < n && j < i + 4; ++j) {
+                    const float r = pd_step(ws[j], g[j], w0s[j], lr, invg);
+                    ws[j] = r;
+                    if (AVG) as[j] = __fadd_rn(as[j], r);
+                }
             }
         }
         return;
     }
-    // partial or unaligned block: scalar loop over this block's element range
+    // unaligned gradient: scalar loop over this block's element range
     const int64_t e1 = (e0 + kElemsPerBlock < n) ? e0 + kElemsPerBlock : n;
     for (int64_t i = e0 + threadIdx.x; i < e1; i += kThreads) {
         const float r = pd_step(ws[i], g[i], w0s[i], lr, invg);
@@ -128,18 +152,40 @@ __global__ void scalar_update_kernel(float* s, const float* g3, const float* a3,
     scalar_update(s, g3, a3, lr, invg, mode);
 }
 
-int launch_table(float* w, const float* w0, float* wavg, const SegTable& tab, float lr, float invg,
-                 float* scalars, const float* grad3, const float* anchor3, int mode,
-                 hipStream_t st) {
+template <int VPT, bool NT>
+int launch_table_t(float* w, const float* w0, float* wavg, const SegTable& tab, float lr, float invg,
+                   float* scalars, const float* grad3, const float* anchor3, int mode, hipStream_t st) {
     const int grid = tab.blk_start[tab.nseg];
     if (grid <= 0) return DAUC_OK;
     if (wavg)
-        hipLaunchKernelGGL(pd_update_kernel<true>, dim3(grid), dim3(kThreads), 0, st, w, w0, wavg,
+        hipLaunchKernelGGL((pd_update_kernel<true, VPT, NT>), dim3(grid), dim3(kThreads), 0, st, w, w0, wavg,
                            tab, lr, invg, scalars, grad3, anchor3, mode);
     else
-        hipLaunchKernelGGL(pd_update_kernel<false>, dim3(grid), dim3(kThreads), 0, st, w, w0,
+        hipLaunchKernelGGL((pd_update_kernel<false, VPT, NT>), dim3(grid), dim3(kThreads), 0, st, w, w0,
                            wavg, tab, lr, invg, scalars, grad3, anchor3, mode);
     return launch_status();
+}
+
+// variant = vpt_index + 4 * nt: vpt in {2, 1, 4, 3}, nt = non-temporal g/w0 loads off (1) / on (0)
+int launch_table(int variant, float* w, const float* w0, float* wavg, const SegTable& tab, float lr,
+                 float invg, float* scalars, const float* grad3, const float* anchor3, int mode,
+                 hipStream_t st) {
+    switch (variant) {
+        case 0: return launch_table_t<2, true>(w, w0, wavg, tab, lr, invg, scalars, grad3, anchor3, mode, st);
+        case 1: return launch_table_t<1, true>(w, w0, wavg, tab, lr, invg, scalars, grad3, anchor3, mode, st);
+        case 2: return launch_table_t<4, true>(w, w0, wavg, tab, lr, invg, scalars, grad3, anchor3, mode, st);
+        case 3: return launch_table_t<3, true>(w, w0, wavg, tab, lr, invg, scalars, grad3, anchor3, mode, st);
+        case 4: return launch_table_t<2, false>(w, w0, wavg, tab, lr, invg, scalars, grad3, anchor3, mode, st);
+        case 5: return launch_table_t<1, false>(w, w0, wavg, tab, lr, invg, scalars, grad3, anchor3, mode, st);
+        case 6: return launch_table_t<4, false>(w, w0, wavg, tab, lr, invg, scalars, grad3, anchor3, mode, st);
+        case 7: return launch_table_t<3, false>(w, w0, wavg, tab, lr, invg, scalars, grad3, anchor3, mode, st);
+        default: return DAUC_EINVAL;
+    }
+}
+
+int variant_vpt(int variant) {
+    static const int vpt[4] = {2, 1, 4, 3};
+    return vpt[variant & 3];
 }
 
 // ---- CoDA finalisation and stage-end division ---------------------------------
@@ -184,23 +230,20 @@ using namespace dauc;
 
 extern "C" {
 
-int dauc_pd_update(float* w, const float* w0, float* w_avg, const dauc_grad_seg* segs, int nseg,
-                   float* scalars, const float* grad3, const float* anchor3, float lr,
-                   float inv_gamma, int mode, dauc_stream_t stream) {
+static int pd_update_impl(float* w, const float* w0, float* w_avg, const dauc_grad_seg* segs, int nseg,
+                          float* scalars, const float* grad3, const float* anchor3, float lr,
+                          float inv_gamma, int mode, int variant, dauc_stream_t stream) {
     if (w == nullptr || w0 == nullptr || nseg < 0 || (nseg > 0 && segs == nullptr))
         return DAUC_EINVAL;
     if (scalars != nullptr && (grad3 == nullptr || anchor3 == nullptr)) return DAUC_EINVAL;
     if (mode != DAUC_MODE_REFERENCE && mode != DAUC_MODE_PAPER) return DAUC_EINVAL;
+    if (variant < 0 || variant >= 8) return DAUC_EINVAL;
     for (int i = 0; i < nseg; ++i)
-        if (segs[i].numel < 0 || segs[i].offset < 0 || (segs[i].numel > 0 && !segs[i].grad))
+        if (segs[i].numel < 0 || segs[i].offset < 0 || (segs[i].numel > 0 && !segs[i].grad) ||
+            segs[i].offset + segs[i].numel > 0x7fffffffLL)
             return DAUC_EINVAL;
     hipStream_t st = as_hip(stream);
-    if (nseg == 0) {
-        if (scalars == nullptr) return DAUC_OK;
-        hipLaunchKernelGGL(scalar_update_kernel, dim3(1), dim3(1), 0, st, scalars, grad3, anchor3,
-                           lr, inv_gamma, mode);
-        return launch_status();
-    }
+    const int64_t epb = elems_per_block(variant_vpt(variant));
     SegTable tab;
     int i = 0;
     bool first = true;
@@ -210,39 +253,50 @@ int dauc_pd_update(float* w, const float* w0, float* w_avg, const dauc_grad_seg*
         while (i < nseg && tab.nseg < kMaxSeg) {
             const dauc_grad_seg& s = segs[i++];
             if (s.numel == 0) continue;
-            const int64_t nb = (s.numel + kElemsPerBlock - 1) / kElemsPerBlock;
+            const int64_t nb = (s.numel + epb - 1) / epb;
             if (blocks + nb > 0x7fffffffLL) return DAUC_EINVAL;
             tab.blk_start[tab.nseg] = static_cast<int>(blocks);
             tab.grad[tab.nseg] = s.grad;
-            tab.offset[tab.nseg] = s.offset;
-            tab.numel[tab.nseg] = s.numel;
+            tab.offset[tab.nseg] = static_cast<int>(s.offset);
+            tab.numel[tab.nseg] = static_cast<int>(s.numel);
             blocks += nb;
             ++tab.nseg;
         }
         tab.blk_start[tab.nseg] = static_cast<int>(blocks);
         if (tab.nseg == 0) continue;
         // the scalar part rides in the first launch only
-        const int rc = launch_table(w, w0, w_avg, tab, lr, inv_gamma, first ? scalars : nullptr,
+        const int rc = launch_table(variant, w, w0, w_avg, tab, lr, inv_gamma, first ? scalars : nullptr,
                                     grad3, anchor3, mode, st);
         if (rc != DAUC_OK) return rc;
         first = false;
     }
-    if (first && scalars != nullptr) {  // every segment was empty
-        hipLaunchKernelGGL(scalar_update_kernel, dim3(1), dim3(1), 0, st, scalars, grad3, anchor3,
-                           lr, inv_gamma, mode);
+    if (first && scalars != nullptr) {  // no non-empty segment: scalars only
+        hipLaunchKernelGGL(scalar_update_kernel, dim3(1), dim3(1), 0, st, scalars, grad3, anchor3, lr,
+                           inv_gamma, mode);
         return launch_status();
     }
     return DAUC_OK;
 }
 
-int dauc_pd_update_dense(float* w, const float* g, const float* w0, float* w_avg, int64_t n,
-                         float lr, float inv_gamma, dauc_stream_t stream) {
+int dauc_pd_update(float* w, const float* w0, float* w_avg, const dauc_grad_seg* segs, int nseg,
+                   float* scalars, const float* grad3, const float* anchor3, float lr,
+                   float inv_gamma, int mode, dauc_stream_t stream) {
+    return pd_update_impl(w, w0, w_avg, segs, nseg, scalars, grad3, anchor3, lr, inv_gamma, mode, 0,
+                          stream);
+}
+
+int dauc_pd_update_dense_variant(float* w, const float* g, const float* w0, float* w_avg, int64_t n,
+                                 float lr, float inv_gamma, int variant, dauc_stream_t stream) {
     if (w == nullptr || g == nullptr || w0 == nullptr || n < 0) return DAUC_EINVAL;
     if (n == 0) return DAUC_OK;
-    // one segment per 2^31 blocks is far beyond any model; a single table suffices
     dauc_grad_seg seg{g, 0, n};
-    return dauc_pd_update(w, w0, w_avg, &seg, 1, nullptr, nullptr, nullptr, lr, inv_gamma,
-                          DAUC_MODE_REFERENCE, stream);
+    return pd_update_impl(w, w0, w_avg, &seg, 1, nullptr, nullptr, nullptr, lr, inv_gamma,
+                          DAUC_MODE_REFERENCE, variant, stream);
+}
+
+int dauc_pd_update_dense(float* w, const float* g, const float* w0, float* w_avg, int64_t n,
+                         float lr, float inv_gamma, dauc_stream_t stream) {
+    return dauc_pd_update_dense_variant(w, g, w0, w_avg, n, lr, inv_gamma, 0, stream);
 }
 
 int dauc_coda_finalize(float* flat, int64_t n_avg, int world, float* lcounts, float* gcounts,

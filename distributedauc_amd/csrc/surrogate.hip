@@ -16,17 +16,30 @@ namespace dauc {
 namespace {
 
 constexpr int kThreads = 256;
-constexpr int kVec = 4;                                // elements per thread per iteration
+constexpr int kVec = 4;                                // elements per float4 slot
+#ifndef DAUC_SURROGATE_SLOTS
+#define DAUC_SURROGATE_SLOTS 4
+#endif
+constexpr int kSlots = DAUC_SURROGATE_SLOTS;           // float4 slots per thread per iteration
 constexpr int kMaxBlocks = 2048;                       // partial slots in the workspace
-constexpr int kPerBlockIter = kThreads * kVec;         // 1024 elements
-constexpr int kNumAcc = 8;                             // accumulators per thread
+constexpr int kPerBlockIter = kThreads * kVec * kSlots;  // 4096 elements
+constexpr int kNumAcc = 6;                             // fp64 partials per thread / block
 constexpr size_t kCounterBytes = 256;                  // counter padded to its own lines
 
-// accumulator slots
-enum { S_POS = 0, S_NEG, Q_POS, Q_NEG, H_POS, H_NEG, N_POS, N_NEG };
+// Accumulators. H_pos / H_neg are not accumulated: H = S + a * n (exact in fp64
+// to ~1e-16 relative), reconstructed once in finalize().
+//   S_POS = sum_pos (h - a)      Q_POS = sum_pos (h - a)^2     N_POS = #pos
+//   S_NEG = sum_neg (h - b)      Q_NEG = sum_neg (h - b)^2     N_NEG = #neg
+enum { S_POS = 0, S_NEG, Q_POS, Q_NEG, N_POS, N_NEG };
+
+// Resident-block capacity of the device for the surrogate kernel (queried once, cached):
+// a grid of exactly that many blocks has no partially filled last wave.
+int resident_blocks();
 
 int grid_for(int64_t B) {
-    int64_t g = (B + 2 * kPerBlockIter - 1) / (2 * kPerBlockIter);  // >= 2 iterations per thread
+    int64_t g = (B + kPerBlockIter - 1) / kPerBlockIter;
+    const int64_t cap = resident_blocks();
+    if (g > cap) g = cap;
     if (g < 1) g = 1;
     if (g > kMaxBlocks) g = kMaxBlocks;
     return static_cast<int>(g);
@@ -39,48 +52,67 @@ __device__ __forceinline__ int load_label(const YT* __restrict__ y, int64_t i) {
 
 struct SurrogateScalars {
     double a, b, alpha, p;
-    double c_pos, k_pos;  // dF/dh = c_pos * (h - k_pos) for y = +1
-    double c_neg, k_neg;  // dF/dh = c_neg * (h - k_neg) for y = -1
+    float af, bf;          // fp32 copies for the per-element differences
+    float c_pos, k_pos;    // dF/dh = c_pos * (h - k_pos) for y = +1
+    float c_neg, k_neg;    // dF/dh = c_neg * (h - k_neg) for y = -1
 };
 
 __device__ __forceinline__ SurrogateScalars make_scalars(const float* abalpha, const float* p_hat,
                                                          int64_t B) {
     SurrogateScalars s;
-    s.a = abalpha[0];
-    s.b = abalpha[1];
+    s.af = abalpha[0];
+    s.bf = abalpha[1];
+    s.a = s.af;
+    s.b = s.bf;
     s.alpha = abalpha[2];
     s.p = p_hat[0];
     const double invB = 1.0 / static_cast<double>(B);
-    s.c_pos = 2.0 * (1.0 - s.p) * invB;
-    s.k_pos = s.a + 1.0 + s.alpha;
-    s.c_neg = 2.0 * s.p * invB;
-    s.k_neg = s.b - 1.0 - s.alpha;
+    s.c_pos = static_cast<float>(2.0 * (1.0 - s.p) * invB);
+    s.k_pos = static_cast<float>(s.a + 1.0 + s.alpha);
+    s.c_neg = static_cast<float>(2.0 * s.p * invB);
+    s.k_neg = static_cast<float>(s.b - 1.0 - s.alpha);
     return s;
 }
 
-// One element: accumulate its contribution and return dF/dh.
+// Per-thread state: fp32 partials over one float4 slot, folded into fp64 per slot.
+struct Acc {
+    double s_pos = 0.0, s_neg = 0.0, q_pos = 0.0, q_neg = 0.0;
+    int n_pos = 0, n_neg = 0;
+};
+
+// One float4 slot: accumulate and return dF/dh for its four elements.
 template <bool CLASS_ONLY>
-__device__ __forceinline__ float visit(float hf, int yv, const SurrogateScalars& s,
-                                       double (&acc)[kNumAcc]) {
-    const double h = hf;
-    const bool pos = (yv == 1);
-    const bool neg = (yv == -1);
-    if (!CLASS_ONLY) {
-        const double dpos = pos ? h - s.a : 0.0;
-        const double dneg = neg ? h - s.b : 0.0;
-        acc[S_POS] += dpos;
-        acc[S_NEG] += dneg;
-        acc[Q_POS] += dpos * dpos;
-        acc[Q_NEG] += dneg * dneg;
+__device__ __forceinline__ f32x4 visit4(f32x4 h, const int (&yv)[4], const SurrogateScalars& s,
+                                        Acc& acc) {
+    float sp = 0.f, sn = 0.f, qp = 0.f, qn = 0.f;
+    f32x4 g;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const bool pos = (yv[c] == 1);
+        const bool neg = (yv[c] == -1);
+        const float dp = pos ? h[c] - s.af : 0.f;
+        const float dn = neg ? h[c] - s.bf : 0.f;
+        sp += dp;
+        sn += dn;
+        if (!CLASS_ONLY) {
+            qp += dp * dp;
+            qn += dn * dn;
+        }
+        acc.n_pos += pos;
+        acc.n_neg += neg;
+        if (!CLASS_ONLY) {
+            const float cc = pos ? s.c_pos : (neg ? s.c_neg : 0.f);
+            const float kk = pos ? s.k_pos : s.k_neg;
+            g[c] = cc * (h[c] - kk);
+        }
     }
-    acc[H_POS] += pos ? h : 0.0;
-    acc[H_NEG] += neg ? h : 0.0;
-    acc[N_POS] += pos ? 1.0 : 0.0;
-    acc[N_NEG] += neg ? 1.0 : 0.0;
-    if (CLASS_ONLY) return 0.0f;
-    const double c = pos ? s.c_pos : (neg ? s.c_neg : 0.0);
-    const double k = pos ? s.k_pos : s.k_neg;
-    return static_cast<float>(c * (h - k));
+    acc.s_pos += sp;
+    acc.s_neg += sn;
+    if (!CLASS_ONLY) {
+        acc.q_pos += qp;
+        acc.q_neg += qn;
+    }
+    return g;
 }
 
 // Final scalars from the grid totals (one thread).
@@ -88,7 +120,9 @@ __device__ void finalize(const double (&t)[kNumAcc], const SurrogateScalars& s, 
                          double* out64, float* grad3, float* loss) {
     const double invB = 1.0 / static_cast<double>(B);
     const double p = s.p, q = 1.0 - s.p;
-    const double cross = p * t[H_NEG] - q * t[H_POS];  // sum(p h [neg] - (1-p) h [pos])
+    const double h_pos = t[S_POS] + s.a * t[N_POS];
+    const double h_neg = t[S_NEG] + s.b * t[N_NEG];
+    const double cross = p * h_neg - q * h_pos;  // sum(p h [neg] - (1-p) h [pos])
     const double F = q * t[Q_POS] * invB + p * t[Q_NEG] * invB +
                      2.0 * (1.0 + s.alpha) * cross * invB - p * q * s.alpha * s.alpha;
     const double dA = -2.0 * q * t[S_POS] * invB;
@@ -110,9 +144,24 @@ __device__ void finalize(const double (&t)[kNumAcc], const SurrogateScalars& s, 
     if (loss) loss[0] = static_cast<float>(F);
 }
 
+// class sums (a = b = 0 there, so S_* are the plain score sums)
 __device__ void emit_class_sums(const double (&t)[kNumAcc], double* sums4, int accumulate) {
-    const double v[4] = {t[H_NEG], t[N_NEG], t[H_POS], t[N_POS]};
+    const double v[4] = {t[S_NEG], t[N_NEG], t[S_POS], t[N_POS]};
     for (int k = 0; k < 4; ++k) sums4[k] = accumulate ? sums4[k] + v[k] : v[k];
+}
+
+template <typename YT>
+__device__ __forceinline__ void load_labels4(const YT* __restrict__ y, int64_t base, int (&yv)[4]) {
+    if constexpr (sizeof(YT) == 1) {
+        const char4 c = *reinterpret_cast<const char4*>(y + base);
+        yv[0] = c.x;
+        yv[1] = c.y;
+        yv[2] = c.z;
+        yv[3] = c.w;
+    } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) yv[j] = load_label(y, base + j);
+    }
 }
 
 // UNIT: h, y and dh are unit-stride and 4-element aligned (vector loads/stores).
@@ -132,69 +181,100 @@ __global__ __launch_bounds__(kThreads) void surrogate_kernel(
     } else {
         s = make_scalars(abalpha, p_hat, B);
     }
-    double acc[kNumAcc];
-#pragma unroll
-    for (int k = 0; k < kNumAcc; ++k) acc[k] = 0.0;
+    Acc acc;
+    const bool write_dh = !CLASS_ONLY && dh != nullptr;
 
     const int64_t stride = static_cast<int64_t>(gridDim.x) * kPerBlockIter;
     for (int64_t base = static_cast<int64_t>(blockIdx.x) * kPerBlockIter + threadIdx.x * kVec;
          base < B; base += stride) {
-        if (UNIT && base + kVec <= B) {
-            const float4 hv = *reinterpret_cast<const float4*>(h + base);
-            int yv[kVec];
-            if constexpr (sizeof(YT) == 1) {
-                const char4 c = *reinterpret_cast<const char4*>(y + base);
-                yv[0] = c.x; yv[1] = c.y; yv[2] = c.z; yv[3] = c.w;
-            } else {
+        // kSlots float4 slots, 1024 elements apart; all loads issued first
+        if (UNIT && base + int64_t(kThreads) * kVec * (kSlots - 1) + kVec <= B) {
+            f32x4 hv[kSlots];
+            int yv[kSlots][4];
 #pragma unroll
-                for (int j = 0; j < kVec; ++j) yv[j] = load_label(y, base + j);
+            for (int k = 0; k < kSlots; ++k) {
+                const int64_t b = base + int64_t(k) * kThreads * kVec;
+                hv[k] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(h + b));
+                load_labels4(y, b, yv[k]);
             }
-            float4 g;
-            g.x = visit<CLASS_ONLY>(hv.x, yv[0], s, acc);
-            g.y = visit<CLASS_ONLY>(hv.y, yv[1], s, acc);
-            g.z = visit<CLASS_ONLY>(hv.z, yv[2], s, acc);
-            g.w = visit<CLASS_ONLY>(hv.w, yv[3], s, acc);
-            if (!CLASS_ONLY && dh) *reinterpret_cast<float4*>(dh + base) = g;
+#pragma unroll
+            for (int k = 0; k < kSlots; ++k) {
+                const f32x4 g = visit4<CLASS_ONLY>(hv[k], yv[k], s, acc);
+                if (write_dh)
+                    __builtin_nontemporal_store(g, reinterpret_cast<f32x4*>(dh + base + int64_t(k) * kThreads * kVec));
+            }
         } else {
 #pragma unroll
-            for (int j = 0; j < kVec; ++j) {
-                const int64_t i = base + j;
-                if (i < B) {
-                    const float g = visit<CLASS_ONLY>(h[i * hs], load_label(y, i), s, acc);
-                    if (!CLASS_ONLY && dh) dh[i * dhs] = g;
+            for (int k = 0; k < kSlots; ++k) {
+                const int64_t b = base + int64_t(k) * kThreads * kVec;
+                f32x4 hv = {0.f, 0.f, 0.f, 0.f};
+                int yv[4] = {0, 0, 0, 0};
+#pragma unroll
+                for (int j = 0; j < kVec; ++j) {
+                    if (b + j < B) {
+                        hv[j] = h[(b + j) * hs];
+                        yv[j] = load_label(y, b + j);
+                    }
+                }
+                const f32x4 g = visit4<CLASS_ONLY>(hv, yv, s, acc);
+                if (write_dh) {
+#pragma unroll
+                    for (int j = 0; j < kVec; ++j)
+                        if (b + j < B) dh[(b + j) * dhs] = g[j];
                 }
             }
         }
     }
 
-    block_sum<kNumAcc>(acc, scratch);
+    double tot[kNumAcc] = {acc.s_pos, acc.s_neg, acc.q_pos, acc.q_neg,
+                           static_cast<double>(acc.n_pos), static_cast<double>(acc.n_neg)};
+    block_sum<kNumAcc>(tot, scratch);
 
     if (gridDim.x == 1) {
         if (threadIdx.x == 0) {
-            if (CLASS_ONLY) emit_class_sums(acc, sums4, accumulate);
-            else finalize(acc, s, B, out64, grad3, loss);
+            if (CLASS_ONLY) emit_class_sums(tot, sums4, accumulate);
+            else finalize(tot, s, B, out64, grad3, loss);
         }
         return;
     }
 
     if (threadIdx.x == 0) {
 #pragma unroll
-        for (int k = 0; k < kNumAcc; ++k) partials[blockIdx.x * kNumAcc + k] = acc[k];
+        for (int k = 0; k < kNumAcc; ++k) partials[blockIdx.x * kNumAcc + k] = tot[k];
     }
     if (!arrive_last(counter, gridDim.x, &last_flag)) return;
 
     // Last block: reduce all partials in a fixed order.
 #pragma unroll
-    for (int k = 0; k < kNumAcc; ++k) acc[k] = 0.0;
+    for (int k = 0; k < kNumAcc; ++k) tot[k] = 0.0;
     for (int b = threadIdx.x; b < static_cast<int>(gridDim.x); b += kThreads) {
 #pragma unroll
-        for (int k = 0; k < kNumAcc; ++k) acc[k] += partials[b * kNumAcc + k];
+        for (int k = 0; k < kNumAcc; ++k) tot[k] += partials[b * kNumAcc + k];
     }
-    block_sum<kNumAcc>(acc, scratch);
+    block_sum<kNumAcc>(tot, scratch);
     if (threadIdx.x == 0) {
-        if (CLASS_ONLY) emit_class_sums(acc, sums4, accumulate);
-        else finalize(acc, s, B, out64, grad3, loss);
+        if (CLASS_ONLY) emit_class_sums(tot, sums4, accumulate);
+        else finalize(tot, s, B, out64, grad3, loss);
     }
+}
+
+int resident_blocks() {
+    static int cached = 0;
+    if (cached == 0) {
+        int dev = 0, cus = 0, per_cu = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                &per_cu, reinterpret_cast<const void*>(&surrogate_kernel<int8_t, false, true>), kThreads,
+                0) != hipSuccess ||
+            cus <= 0 || per_cu <= 0) {
+            (void)hipGetLastError();
+            cached = kMaxBlocks;  // no device (e.g. size queries on a build host): upper bound
+        } else {
+            cached = cus * per_cu;
+        }
+    }
+    return cached;
 }
 
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }

@@ -197,7 +197,7 @@ def pd_update(w: torch.Tensor, w0: torch.Tensor, w_avg: torch.Tensor | None, seg
 
 
 def pd_update_dense(w: torch.Tensor, g: torch.Tensor, w0: torch.Tensor, w_avg: torch.Tensor | None, *,
-                    lr: float, gamma: float) -> None:
+                    lr: float, gamma: float, variant: int = 0) -> None:
     """main.py:61 (+333-334) over one dense buffer of n parameters."""
     _require(w, "w", torch.float32)
     dev = w.device
@@ -208,8 +208,8 @@ def pd_update_dense(w: torch.Tensor, g: torch.Tensor, w0: torch.Tensor, w_avg: t
             raise ValueError(f"{name} must be contiguous with {n} elements")
     if not w.is_contiguous():
         raise ValueError("w must be contiguous")
-    check(_lib.load().dauc_pd_update_dense(_ptr(w), _ptr(g), _ptr(w0), _ptr(w_avg), n, float(lr),
-                                           float(1 / gamma), _stream(dev)),
+    check(_lib.load().dauc_pd_update_dense_variant(_ptr(w), _ptr(g), _ptr(w0), _ptr(w_avg), n, float(lr),
+                                                   float(1 / gamma), int(variant), _stream(dev)),
           "dauc_pd_update_dense")
 
 

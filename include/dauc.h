@@ -113,7 +113,7 @@ int dauc_alpha_from_sums(const double* sums4, float* alpha, dauc_stream_t stream
 /* One parameter tensor's gradient, located at w + offset inside the flat buffer. */
 typedef struct dauc_grad_seg {
     const float* grad; /* device pointer, dense, same physical element order as the parameter */
-    int64_t offset;    /* element offset of the parameter inside w / w0 / w_avg */
+    int64_t offset;    /* element offset of the parameter inside w / w0 / w_avg (offset+numel < 2^31) */
     int64_t numel;
 } dauc_grad_seg;
 
@@ -141,6 +141,15 @@ int dauc_pd_update(float* w, const float* w0, float* w_avg, const dauc_grad_seg*
  */
 int dauc_pd_update_dense(float* w, const float* g, const float* w0, float* w_avg, int64_t n,
                          float lr, float inv_gamma, dauc_stream_t stream);
+
+/*
+ * dauc_pd_update_dense with an explicit kernel geometry, for tuning:
+ * variant = v + 4*t, v selects 2 / 1 / 4 / 3 float4 per thread, t = 1 turns the
+ * non-temporal loads of g and w0 off. Variant 0 is the default. Results are
+ * bit-identical across variants.
+ */
+int dauc_pd_update_dense_variant(float* w, const float* g, const float* w0, float* w_avg, int64_t n,
+                                 float lr, float inv_gamma, int variant, dauc_stream_t stream);
 
 /* ----------------------------------------------- a6: CoDA averaging */
 
@@ -183,9 +192,10 @@ int dauc_pair_count(const float* pos, int64_t P, const float* neg, int64_t N,
                     unsigned long long* wins_ties, dauc_stream_t stream);
 
 /*
- * dauc_pair_count with an explicit kernel variant (0 = the default used by
- * dauc_pair_count; 1, 2 = alternative accumulation schemes kept for tuning).
- * Every variant returns identical counts.
+ * dauc_pair_count with an explicit kernel variant, for tuning: variant =
+ * mode + 3*r, mode 0 = per-lane VGPR counters, 1 = wave ballot + scalar
+ * popcount, 2 = mixed; r selects 8 / 4 / 16 positives held per lane.
+ * Variant 0 is what dauc_pair_count uses. Every variant returns identical counts.
  */
 int dauc_pair_count_variant(const float* pos, int64_t P, const float* neg, int64_t N,
                             unsigned long long* wins_ties, int variant, dauc_stream_t stream);

@@ -1,0 +1,125 @@
+"""Micro-benchmarks of the hot kernels (HIP events on the launch stream), one process.
+
+  update     dauc_pd_update_dense, n = 23,512,130 (ResNet-50), 24 B/param, every variant
+  copy       torch D2D copy of 1 GiB: the practical HBM ceiling next to the 8 TB/s spec
+  surrogate  dauc_surrogate_fwdbwd at B = 2^26 (9 B/element) and B = 256 (latency)
+  paircount  dauc_pair_count_variant at 2^24 scores, 1 % positives, every variant (counts must agree)
+
+Prints one JSON object per measurement.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from distributedauc_amd import ops  # noqa: E402
+
+
+def timeit(fn, reps, warm=3):
+    for _ in range(warm):
+        fn()
+    s = torch.cuda.current_stream()
+    ts = []
+    for _ in range(reps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(s)
+        fn()
+        b.record(s)
+        ts.append((a, b))
+    torch.cuda.synchronize()
+    v = [a.elapsed_time(b) for a, b in ts]
+    return float(np.median(v)), float(np.min(v))
+
+
+def emit(**kw):
+    print(json.dumps(kw), flush=True)
+
+
+def bench_update(dev, reps):
+    n = 23_512_130
+    g = torch.Generator(device=dev).manual_seed(0)
+    base = [torch.randn(n, device=dev, generator=g) for _ in range(4)]
+    ref = None
+    for v in range(8):
+        w, gr, w0, avg = (t.clone() for t in base)
+        ops.pd_update_dense(w, gr, w0, avg, lr=0.1, gamma=2000.0, variant=v)
+        if ref is None:
+            ref = (w.clone(), avg.clone())
+        same = bool(torch.equal(ref[0], w) and torch.equal(ref[1], avg))
+        med, mn = timeit(lambda: ops.pd_update_dense(w, gr, w0, avg, lr=0.1, gamma=2000.0, variant=v), reps)
+        emit(kernel="pd_update", variant=v, n=n, us=med * 1e3, us_min=mn * 1e3, GBps=24 * n / med / 1e6,
+             GBps_best=24 * n / mn / 1e6, bitexact_vs_v0=same)
+    for v in (0,):
+        w, gr, w0 = (t.clone() for t in base[:3])
+        med, mn = timeit(lambda: ops.pd_update_dense(w, gr, w0, None, lr=0.1, gamma=2000.0, variant=v), reps)
+        emit(kernel="pd_update_noavg", variant=v, n=n, us=med * 1e3, GBps=16 * n / med / 1e6)
+
+
+def bench_copy(dev, reps):
+    n = 1 << 28  # 1 GiB of fp32
+    a = torch.empty(n, device=dev).normal_()
+    b = torch.empty_like(a)
+    med, mn = timeit(lambda: b.copy_(a), reps)
+    emit(kernel="torch_copy_1GiB", us=med * 1e3, GBps=8 * n / med / 1e6, GBps_best=8 * n / mn / 1e6)
+    n2 = 23_512_130 * 3  # update-sized working set
+    a2, b2 = a[:n2], b[:n2]
+    med, mn = timeit(lambda: b2.copy_(a2), reps)
+    emit(kernel="torch_copy_282MB", us=med * 1e3, GBps=8 * n2 / med / 1e6)
+
+
+def bench_surrogate(dev, reps):
+    for B in (1 << 26, 1 << 20, 256):
+        g = torch.Generator(device=dev).manual_seed(1)
+        h = torch.rand(B, device=dev, generator=g)
+        y = torch.where(torch.rand(B, device=dev, generator=g) < 0.1, 1, -1).to(torch.int8)
+        ab = torch.tensor([0.1, -0.2, 0.3], device=dev)
+        p = torch.tensor([0.1], device=dev)
+        dh = torch.empty(B, device=dev)
+        g3 = torch.empty(3, device=dev)
+        med, mn = timeit(lambda: ops.surrogate_fwdbwd(h, y, ab, p, dh=dh, grad3=g3), reps)
+        emit(kernel="surrogate", B=B, us=med * 1e3, us_min=mn * 1e3, GBps=9 * B / med / 1e6)
+
+
+def bench_paircount(dev, reps, log2n):
+    n = 1 << log2n
+    g = torch.Generator(device=dev).manual_seed(2024)
+    s = torch.rand(n, device=dev, generator=g)
+    y = torch.where(torch.rand(n, device=dev, generator=g) < 0.01, 1, -1).to(torch.int8)
+    pos, neg, st = ops.split_scores(s, y)
+    P, N = st[0].item(), st[1].item()
+    pos, neg = pos[:P].contiguous(), neg[:N].contiguous()
+    med, _ = timeit(lambda: ops.split_scores(s, y), reps)
+    emit(kernel="split_scores", n=n, us=med * 1e3, GBps=(n * 5 * 2 + n * 4) / med / 1e6)
+    ref = None
+    for v in range(9):
+        wt = torch.zeros(2, dtype=torch.int64, device=dev)
+        ops.pair_count(pos, neg, wt, variant=v)
+        c = tuple(wt.tolist())
+        ref = ref or c
+        med, mn = timeit(lambda: ops.pair_count(pos, neg, wt, variant=v), reps, warm=1)
+        emit(kernel="pair_count", variant=v, P=P, N=N, ms=med, pairs_per_s=P * N / med * 1e3,
+             frac_valu=P * N / med * 1e3 / 1.97e13, counts_equal=c == ref)
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--which", default="update,copy,surrogate,paircount")
+    ap.add_argument("--reps", type=int, default=30)
+    ap.add_argument("--log2n", type=int, default=24)
+    a = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    w = a.which.split(",")
+    if "update" in w:
+        bench_update(dev, a.reps)
+    if "copy" in w:
+        bench_copy(dev, a.reps)
+    if "surrogate" in w:
+        bench_surrogate(dev, a.reps)
+    if "paircount" in w:
+        bench_paircount(dev, max(3, a.reps // 10), a.log2n)
