@@ -57,6 +57,9 @@ SIGNATURES = {
     "dauc_split_scores": (_int, [_vp, _vp, _int, _i64, _vp, _vp, _vp, _vp, _sz, _vp]),
     "dauc_pair_count": (_int, [_vp, _i64, _vp, _i64, _vp, _vp]),
     "dauc_pair_count_variant": (_int, [_vp, _i64, _vp, _i64, _vp, _int, _vp]),
+    "dauc_sort_workspace_size": (_sz, [_i64]),
+    "dauc_auc_counts_sorted": (_int, [_vp, _i64, _vp, _i64, _vp, _vp, _sz, _vp]),
+    "dauc_sort_keys": (_int, [_vp, _i64, _vp, _vp, _sz, _vp]),
 }
 
 _lib = None

@@ -7,6 +7,11 @@ T counts tied pairs; the kernels here compute W and T as exact integers, so the
 counts are bit-exact against the reference on identical scores and the returned
 float is within a few ulp of sklearn's trapezoid sum.
 
+Two exact methods give the same integers: ``method="pairs"`` runs the LDS-tiled
+pair-count kernel (O(P*N), the north-star kernel) and ``method="sort"`` (default)
+radix-sorts the negatives and binary-searches every positive (O(N + P log N),
+SURVEY §8f row 1).
+
 Sharding (north star): every rank holds the same score vector; rank
 r compares positives [r*P/G, (r+1)*P/G) of the stable split against ALL
 negatives, and one int64 [2] all-reduce sums (W, T). The result does not depend
@@ -54,12 +59,16 @@ def _as_device_pair(label, scores, device):
 class ExactAUC:
     """Exact AUC evaluator; sharded over a process group when world > 1."""
 
-    def __init__(self, group=None, world: int = 1, rank: int = 0, variant: int = 0, reduce: bool = True):
+    def __init__(self, group=None, world: int = 1, rank: int = 0, variant: int = 0, reduce: bool = True,
+                 method: str = "sort"):
+        if method not in ("sort", "pairs"):
+            raise ValueError("method must be 'sort' (radix sort + search) or 'pairs' (pair-count kernel)")
         self.group = group
         self.world = world
         self.rank = rank
         self.variant = variant
         self.reduce = reduce  # False: return only this rank's share (no collective)
+        self.method = method
 
     def counts(self, label, scores, device=None) -> dict:
         """Exact {wins, ties, P, N} (Python ints). One host sync for the split sizes."""
@@ -79,7 +88,10 @@ class ExactAUC:
             lo = self.rank * P // self.world
             hi = (self.rank + 1) * P // self.world
             if hi > lo:
-                ops.pair_count(pos[lo:hi], neg[:N], wt, variant=self.variant)
+                if self.method == "pairs":
+                    ops.pair_count(pos[lo:hi], neg[:N], wt, variant=self.variant)
+                else:
+                    ops.auc_counts_sorted(pos[lo:hi], neg[:N], wt)
         if self.world > 1 and self.reduce:
             dist.all_reduce(wt, op=dist.ReduceOp.SUM, group=self.group)
         W, T = (int(v) for v in wt.tolist())

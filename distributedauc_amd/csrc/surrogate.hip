@@ -7,8 +7,9 @@
 // HBM layout: h is read with an element stride (2 when it is column 1 of the
 // [B,2] softmax output), labels are int8 (+1/-1) on the fast path, dF/dh is
 // written once. Algorithmic traffic: 4 (h) + 1 (int8 y) + 4 (dh) = 9 B/element.
-// The reductions (six fp64 sums + two counts) are reduced wave -> block -> grid
-// in a fixed order, so results are bitwise reproducible run to run.
+// Per 4-element slot the fp32 partials of sum(h-a), sum(h-b), sum((h-a)^2),
+// sum((h-b)^2) are folded into fp64; with the two class counts they are reduced
+// wave -> block -> grid in a fixed order, so results are bitwise reproducible.
 
 #include "dauc_internal.h"
 
@@ -17,12 +18,21 @@ namespace {
 
 constexpr int kThreads = 256;
 constexpr int kVec = 4;                                // elements per float4 slot
+// Geometry from the MI355X sweep (scripts/gpu_sweep_sur.sh, profiles/r01): 8 float4
+// slots per thread and 2 resident blocks per CU stream best (a narrow, deep window;
+// more resident blocks lose DRAM locality).
 #ifndef DAUC_SURROGATE_SLOTS
-#define DAUC_SURROGATE_SLOTS 4
+#define DAUC_SURROGATE_SLOTS 8
+#endif
+#ifndef DAUC_SURROGATE_BPC
+#define DAUC_SURROGATE_BPC 2
 #endif
 constexpr int kSlots = DAUC_SURROGATE_SLOTS;           // float4 slots per thread per iteration
+#ifndef DAUC_SURROGATE_NTSTORE
+#define DAUC_SURROGATE_NTSTORE 1
+#endif
 constexpr int kMaxBlocks = 2048;                       // partial slots in the workspace
-constexpr int kPerBlockIter = kThreads * kVec * kSlots;  // 4096 elements
+constexpr int kPerBlockIter = kThreads * kVec * kSlots;  // 8192 elements
 constexpr int kNumAcc = 6;                             // fp64 partials per thread / block
 constexpr size_t kCounterBytes = 256;                  // counter padded to its own lines
 
@@ -58,7 +68,7 @@ struct SurrogateScalars {
 };
 
 __device__ __forceinline__ SurrogateScalars make_scalars(const float* abalpha, const float* p_hat,
-                                                         int64_t B) {
+                                                         double invB) {
     SurrogateScalars s;
     s.af = abalpha[0];
     s.bf = abalpha[1];
@@ -66,7 +76,6 @@ __device__ __forceinline__ SurrogateScalars make_scalars(const float* abalpha, c
     s.b = s.bf;
     s.alpha = abalpha[2];
     s.p = p_hat[0];
-    const double invB = 1.0 / static_cast<double>(B);
     s.c_pos = static_cast<float>(2.0 * (1.0 - s.p) * invB);
     s.k_pos = static_cast<float>(s.a + 1.0 + s.alpha);
     s.c_neg = static_cast<float>(2.0 * s.p * invB);
@@ -116,9 +125,8 @@ __device__ __forceinline__ f32x4 visit4(f32x4 h, const int (&yv)[4], const Surro
 }
 
 // Final scalars from the grid totals (one thread).
-__device__ void finalize(const double (&t)[kNumAcc], const SurrogateScalars& s, int64_t B,
+__device__ void finalize(const double (&t)[kNumAcc], const SurrogateScalars& s, double invB,
                          double* out64, float* grad3, float* loss) {
-    const double invB = 1.0 / static_cast<double>(B);
     const double p = s.p, q = 1.0 - s.p;
     const double h_pos = t[S_POS] + s.a * t[N_POS];
     const double h_neg = t[S_NEG] + s.b * t[N_NEG];
@@ -167,7 +175,7 @@ __device__ __forceinline__ void load_labels4(const YT* __restrict__ y, int64_t b
 // UNIT: h, y and dh are unit-stride and 4-element aligned (vector loads/stores).
 template <typename YT, bool CLASS_ONLY, bool UNIT>
 __global__ __launch_bounds__(kThreads) void surrogate_kernel(
-    const float* __restrict__ h, int64_t hs, const YT* __restrict__ y, int64_t B,
+    const float* __restrict__ h, int64_t hs, const YT* __restrict__ y, int64_t B, double invB,
     const float* __restrict__ abalpha, const float* __restrict__ p_hat, float* __restrict__ dh,
     int64_t dhs, double* __restrict__ partials, unsigned* __restrict__ counter,
     double* __restrict__ out64, float* __restrict__ grad3, float* __restrict__ loss,
@@ -179,16 +187,17 @@ __global__ __launch_bounds__(kThreads) void surrogate_kernel(
     if (CLASS_ONLY) {
         s = SurrogateScalars{};
     } else {
-        s = make_scalars(abalpha, p_hat, B);
+        s = make_scalars(abalpha, p_hat, invB);
     }
     Acc acc;
     const bool write_dh = !CLASS_ONLY && dh != nullptr;
 
-    const int64_t stride = static_cast<int64_t>(gridDim.x) * kPerBlockIter;
-    for (int64_t base = static_cast<int64_t>(blockIdx.x) * kPerBlockIter + threadIdx.x * kVec;
-         base < B; base += stride) {
-        // kSlots float4 slots, 1024 elements apart; all loads issued first
-        if (UNIT && base + int64_t(kThreads) * kVec * (kSlots - 1) + kVec <= B) {
+    // 1) vector path: whole block-iterations of kPerBlockIter elements, every slot in range
+    int64_t done = 0;
+    if (UNIT) {
+        const int64_t n_iter = B / kPerBlockIter;
+        for (int64_t it = blockIdx.x; it < n_iter; it += gridDim.x) {
+            const int64_t base = it * kPerBlockIter + threadIdx.x * kVec;
             f32x4 hv[kSlots];
             int yv[kSlots][4];
 #pragma unroll
@@ -200,28 +209,38 @@ __global__ __launch_bounds__(kThreads) void surrogate_kernel(
 #pragma unroll
             for (int k = 0; k < kSlots; ++k) {
                 const f32x4 g = visit4<CLASS_ONLY>(hv[k], yv[k], s, acc);
-                if (write_dh)
-                    __builtin_nontemporal_store(g, reinterpret_cast<f32x4*>(dh + base + int64_t(k) * kThreads * kVec));
-            }
-        } else {
-#pragma unroll
-            for (int k = 0; k < kSlots; ++k) {
-                const int64_t b = base + int64_t(k) * kThreads * kVec;
-                f32x4 hv = {0.f, 0.f, 0.f, 0.f};
-                int yv[4] = {0, 0, 0, 0};
-#pragma unroll
-                for (int j = 0; j < kVec; ++j) {
-                    if (b + j < B) {
-                        hv[j] = h[(b + j) * hs];
-                        yv[j] = load_label(y, b + j);
-                    }
-                }
-                const f32x4 g = visit4<CLASS_ONLY>(hv, yv, s, acc);
                 if (write_dh) {
-#pragma unroll
-                    for (int j = 0; j < kVec; ++j)
-                        if (b + j < B) dh[(b + j) * dhs] = g[j];
+                    f32x4* dst = reinterpret_cast<f32x4*>(dh + base + int64_t(k) * kThreads * kVec);
+                    if (DAUC_SURROGATE_NTSTORE) __builtin_nontemporal_store(g, dst);
+                    else *dst = g;
                 }
+            }
+        }
+        done = n_iter * kPerBlockIter;
+    }
+    // 2) scalar path: the tail of a unit-stride batch, or all of a strided one (training
+    //    batches: column 1 of the [B,2] softmax). One element per thread per step.
+    {
+        for (int64_t i = done + int64_t(blockIdx.x) * kThreads + threadIdx.x; i < B;
+             i += int64_t(gridDim.x) * kThreads) {
+            const float hv = h[i * hs];
+            const int yv = load_label(y, i);
+            const bool pos = (yv == 1), neg = (yv == -1);
+            const float dp = pos ? hv - s.af : 0.f;
+            const float dn = neg ? hv - s.bf : 0.f;
+            // per-element fp64 folding keeps long strided loops exact to fp64 rounding
+            acc.s_pos += dp;
+            acc.s_neg += dn;
+            if (!CLASS_ONLY) {
+                acc.q_pos += dp * dp;
+                acc.q_neg += dn * dn;
+            }
+            acc.n_pos += pos;
+            acc.n_neg += neg;
+            if (write_dh) {
+                const float cc = pos ? s.c_pos : (neg ? s.c_neg : 0.f);
+                const float kk = pos ? s.k_pos : s.k_neg;
+                dh[i * dhs] = cc * (hv - kk);
             }
         }
     }
@@ -233,7 +252,7 @@ __global__ __launch_bounds__(kThreads) void surrogate_kernel(
     if (gridDim.x == 1) {
         if (threadIdx.x == 0) {
             if (CLASS_ONLY) emit_class_sums(tot, sums4, accumulate);
-            else finalize(tot, s, B, out64, grad3, loss);
+            else finalize(tot, s, invB, out64, grad3, loss);
         }
         return;
     }
@@ -254,7 +273,7 @@ __global__ __launch_bounds__(kThreads) void surrogate_kernel(
     block_sum<kNumAcc>(tot, scratch);
     if (threadIdx.x == 0) {
         if (CLASS_ONLY) emit_class_sums(tot, sums4, accumulate);
-        else finalize(tot, s, B, out64, grad3, loss);
+        else finalize(tot, s, invB, out64, grad3, loss);
     }
 }
 
@@ -271,6 +290,7 @@ int resident_blocks() {
             (void)hipGetLastError();
             cached = kMaxBlocks;  // no device (e.g. size queries on a build host): upper bound
         } else {
+            per_cu = per_cu < DAUC_SURROGATE_BPC ? per_cu : DAUC_SURROGATE_BPC;
             cached = cus * per_cu;
         }
     }
@@ -297,12 +317,12 @@ int launch_surrogate(const float* h, int64_t hs, const YT* y, int64_t B, const f
                       (CLASS_ONLY || dh == nullptr || (dhs == 1 && aligned16(dh)));
     if (unit) {
         hipLaunchKernelGGL((surrogate_kernel<YT, CLASS_ONLY, true>), dim3(grid), dim3(kThreads), 0,
-                           st, h, hs, y, B, abalpha, p_hat, dh, dhs, partials, counter, out64,
-                           grad3, loss, sums4, accumulate);
+                           st, h, hs, y, B, 1.0 / static_cast<double>(B), abalpha, p_hat, dh, dhs,
+                           partials, counter, out64, grad3, loss, sums4, accumulate);
     } else {
         hipLaunchKernelGGL((surrogate_kernel<YT, CLASS_ONLY, false>), dim3(grid), dim3(kThreads),
-                           0, st, h, hs, y, B, abalpha, p_hat, dh, dhs, partials, counter, out64,
-                           grad3, loss, sums4, accumulate);
+                           0, st, h, hs, y, B, 1.0 / static_cast<double>(B), abalpha, p_hat, dh,
+                           dhs, partials, counter, out64, grad3, loss, sums4, accumulate);
     }
     return launch_status();
 }

@@ -276,7 +276,38 @@ def pair_count(pos: torch.Tensor, neg: torch.Tensor, wins_ties: torch.Tensor, va
                                               int(variant), _stream(dev)), "dauc_pair_count")
 
 
+def auc_counts_sorted(pos: torch.Tensor, neg: torch.Tensor, wins_ties: torch.Tensor) -> None:
+    """Same (wins, ties) accumulation as pair_count, by radix-sorting neg and binary-searching pos."""
+    _require(pos, "pos", torch.float32)
+    dev = pos.device
+    _require(neg, "neg", torch.float32, dev)
+    _require(wins_ties, "wins_ties", torch.int64, dev)
+    if pos.dim() != 1 or neg.dim() != 1 or not pos.is_contiguous() or not neg.is_contiguous():
+        raise ValueError("pos and neg must be contiguous 1-D tensors")
+    if wins_ties.numel() < 2 or not wins_ties.is_contiguous():
+        raise ValueError("wins_ties needs 2 contiguous int64 slots")
+    L = _lib.load()
+    ws = workspaces.get(dev, "sort", L.dauc_sort_workspace_size(max(neg.numel(), 1)))
+    check(L.dauc_auc_counts_sorted(_ptr(pos), pos.numel(), _ptr(neg), neg.numel(), _ptr(wins_ties), _ptr(ws),
+                                   ws.numel(), _stream(dev)), "dauc_auc_counts_sorted")
+
+
+def sort_keys(scores: torch.Tensor) -> torch.Tensor:
+    """Ascending order-preserving uint32 keys of fp32 scores, returned as int32 bit patterns."""
+    _require(scores, "scores", torch.float32)
+    if scores.dim() != 1 or not scores.is_contiguous() or scores.numel() == 0:
+        raise ValueError("scores must be a non-empty contiguous 1-D tensor")
+    dev = scores.device
+    out = torch.empty(scores.numel(), dtype=torch.int32, device=dev)
+    L = _lib.load()
+    ws = workspaces.get(dev, "sort", L.dauc_sort_workspace_size(scores.numel()))
+    check(L.dauc_sort_keys(_ptr(scores), scores.numel(), _ptr(out), _ptr(ws), ws.numel(), _stream(dev)),
+          "dauc_sort_keys")
+    return out
+
+
 __all__ = [
     "GradSeg", "label_map_phat", "surrogate_fwdbwd", "class_sums", "alpha_from_sums", "pd_update",
-    "pd_update_dense", "coda_finalize", "scale_div", "split_scores", "pair_count", "mode_code", "workspaces",
+    "pd_update_dense", "coda_finalize", "scale_div", "split_scores", "pair_count", "auc_counts_sorted",
+    "sort_keys", "mode_code", "workspaces",
 ]

@@ -200,6 +200,23 @@ int dauc_pair_count(const float* pos, int64_t P, const float* neg, int64_t N,
 int dauc_pair_count_variant(const float* pos, int64_t P, const float* neg, int64_t N,
                             unsigned long long* wins_ties, int variant, dauc_stream_t stream);
 
+/* Bytes of scratch dauc_auc_counts_sorted / dauc_sort_keys need for N negatives (no zeroing needed). */
+size_t dauc_sort_workspace_size(int64_t N);
+
+/*
+ * Same counts as dauc_pair_count by sorting instead of enumerating pairs
+ * (SURVEY §8f row 1): LSD radix sort of the negatives' order-preserving uint32
+ * keys (-0 == +0), then lower/upper-bound searches per positive.
+ * O(N + P log N); wins_ties accumulates like dauc_pair_count.
+ */
+int dauc_auc_counts_sorted(const float* pos, int64_t P, const float* neg, int64_t N,
+                           unsigned long long* wins_ties, void* workspace, size_t workspace_bytes,
+                           dauc_stream_t stream);
+
+/* The radix sort alone: keys_out[0..n) = ascending order-preserving keys of scores (testing). */
+int dauc_sort_keys(const float* scores, int64_t n, unsigned* keys_out, void* workspace,
+                   size_t workspace_bytes, dauc_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -18,7 +18,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
-from distributedauc_amd import ops  # noqa: E402
+from distributedauc_amd import _lib, ops  # noqa: E402
 
 
 def timeit(fn, reps, warm=3):
@@ -41,12 +41,12 @@ def emit(**kw):
     print(json.dumps(kw), flush=True)
 
 
-def bench_update(dev, reps):
+def bench_update(dev, reps, variants=range(8)):
     n = 23_512_130
     g = torch.Generator(device=dev).manual_seed(0)
     base = [torch.randn(n, device=dev, generator=g) for _ in range(4)]
     ref = None
-    for v in range(8):
+    for v in variants:
         w, gr, w0, avg = (t.clone() for t in base)
         ops.pd_update_dense(w, gr, w0, avg, lr=0.1, gamma=2000.0, variant=v)
         if ref is None:
@@ -55,7 +55,7 @@ def bench_update(dev, reps):
         med, mn = timeit(lambda: ops.pd_update_dense(w, gr, w0, avg, lr=0.1, gamma=2000.0, variant=v), reps)
         emit(kernel="pd_update", variant=v, n=n, us=med * 1e3, us_min=mn * 1e3, GBps=24 * n / med / 1e6,
              GBps_best=24 * n / mn / 1e6, bitexact_vs_v0=same)
-    for v in (0,):
+    for v in list(variants)[:1]:
         w, gr, w0 = (t.clone() for t in base[:3])
         med, mn = timeit(lambda: ops.pd_update_dense(w, gr, w0, None, lr=0.1, gamma=2000.0, variant=v), reps)
         emit(kernel="pd_update_noavg", variant=v, n=n, us=med * 1e3, GBps=16 * n / med / 1e6)
@@ -83,7 +83,9 @@ def bench_surrogate(dev, reps):
         dh = torch.empty(B, device=dev)
         g3 = torch.empty(3, device=dev)
         med, mn = timeit(lambda: ops.surrogate_fwdbwd(h, y, ab, p, dh=dh, grad3=g3), reps)
-        emit(kernel="surrogate", B=B, us=med * 1e3, us_min=mn * 1e3, GBps=9 * B / med / 1e6)
+        grid = (_lib.load().dauc_surrogate_workspace_size(B) - 256) // 48
+        emit(kernel="surrogate", B=B, us=med * 1e3, us_min=mn * 1e3, GBps=9 * B / med / 1e6, grid=grid,
+             lib=os.path.basename(str(_lib.LIB_PATH)))
 
 
 def bench_paircount(dev, reps, log2n):
@@ -96,7 +98,13 @@ def bench_paircount(dev, reps, log2n):
     pos, neg = pos[:P].contiguous(), neg[:N].contiguous()
     med, _ = timeit(lambda: ops.split_scores(s, y), reps)
     emit(kernel="split_scores", n=n, us=med * 1e3, GBps=(n * 5 * 2 + n * 4) / med / 1e6)
-    ref = None
+    wt = torch.zeros(2, dtype=torch.int64, device=dev)
+    ops.auc_counts_sorted(pos, neg, wt)
+    sorted_counts = tuple(wt.tolist())
+    med, mn = timeit(lambda: ops.auc_counts_sorted(pos, neg, wt), reps * 5)
+    emit(kernel="auc_counts_sorted", P=P, N=N, us=med * 1e3, us_min=mn * 1e3,
+         effective_pairs_per_s=P * N / med * 1e3, keys_GBps=N * 4 * 12 / med / 1e6)
+    ref = sorted_counts
     for v in range(9):
         wt = torch.zeros(2, dtype=torch.int64, device=dev)
         ops.pair_count(pos, neg, wt, variant=v)
@@ -112,11 +120,12 @@ if __name__ == "__main__":
     ap.add_argument("--which", default="update,copy,surrogate,paircount")
     ap.add_argument("--reps", type=int, default=30)
     ap.add_argument("--log2n", type=int, default=24)
+    ap.add_argument("--variants", default=None, help="comma list of update variants (default: all)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     w = a.which.split(",")
     if "update" in w:
-        bench_update(dev, a.reps)
+        bench_update(dev, a.reps, [int(v) for v in a.variants.split(",")] if a.variants else range(8))
     if "copy" in w:
         bench_copy(dev, a.reps)
     if "surrogate" in w:

@@ -274,10 +274,11 @@ def test_coda_finalize_and_scale_div(dev):
 
 
 # ------------------------------------------------------------------ exact AUC
-def _counts_gpu(dev, y, s, world=1, rank=0, variant=0):
+def _counts_gpu(dev, y, s, world=1, rank=0, variant=0, method="pairs"):
     from distributedauc_amd.auc import ExactAUC
 
-    return ExactAUC(world=world, rank=rank, variant=variant, reduce=False).counts(T(y, dev), T(s, dev))
+    return ExactAUC(world=world, rank=rank, variant=variant, reduce=False, method=method).counts(T(y, dev),
+                                                                                                T(s, dev))
 
 
 def test_auc_golden(dev, golden):
@@ -287,10 +288,12 @@ def test_auc_golden(dev, golden):
     for name in z["names"]:
         y, s = z[f"{name}_y"], z[f"{name}_s"]
         W, Tt, P, N, two_u = (int(v) for v in z[f"{name}_counts"])
-        for variant in (0, 1, 2):
+        for variant in (0, 1, 2, 3, 6):
             c = _counts_gpu(dev, y, s, variant=variant)
             assert (c["wins"], c["ties"], c["P"], c["N"]) == (W, Tt, P, N), (name, variant, c)
             assert 2 * c["wins"] + c["ties"] == two_u
+        c = _counts_gpu(dev, y, s, method="sort")
+        assert (c["wins"], c["ties"], c["P"], c["N"]) == (W, Tt, P, N), (name, "sort", c)
         auc = ExactAUC.from_counts(c)
         ref = float(z[f"{name}_auc"])
         assert abs(auc - ref) <= 4 * np.spacing(ref), (name, auc, ref)
@@ -306,8 +309,9 @@ def test_auc_counts_large(dev, n, p, ties):
         s = (np.floor(s * 4096) / 4096).astype(np.float32)
     y = np.where(rng.random(n) < p, 1, -1).astype(np.int8)
     e = coracle.auc_counts(y.astype(np.int64), s)
-    c = _counts_gpu(dev, y, s)
-    assert (c["wins"], c["ties"], c["P"], c["N"]) == (e["wins"], e["ties"], e["P"], e["N"])
+    for method in ("pairs", "sort"):
+        c = _counts_gpu(dev, y, s, method=method)
+        assert (c["wins"], c["ties"], c["P"], c["N"]) == (e["wins"], e["ties"], e["P"], e["N"]), method
 
 
 def test_auc_sharded_sum_is_invariant(dev):
@@ -317,10 +321,11 @@ def test_auc_sharded_sum_is_invariant(dev):
     s = (np.floor(rng.random(n) * 1000) / 1000).astype(np.float32)
     y = np.where(rng.random(n) < 0.05, 1, -1).astype(np.int8)
     full = _counts_gpu(dev, y, s)
-    for G in (2, 3, 4, 8):
-        parts = [_counts_gpu(dev, y, s, world=G, rank=r) for r in range(G)]
-        assert sum(c["wins"] for c in parts) == full["wins"]
-        assert sum(c["ties"] for c in parts) == full["ties"]
+    for method in ("pairs", "sort"):
+        for G in (2, 3, 4, 8):
+            parts = [_counts_gpu(dev, y, s, world=G, rank=r, method=method) for r in range(G)]
+            assert sum(c["wins"] for c in parts) == full["wins"]
+            assert sum(c["ties"] for c in parts) == full["ties"]
 
 
 def test_auc_errors_like_sklearn(dev):
@@ -373,3 +378,36 @@ def test_pair_count_edge_sizes(dev):
     ops.pair_count(T(pos, dev), tn[1:], wt)
     assert tuple(wt.cpu().tolist()) == coracle.pair_count_bruteforce(pos, negall[1:])
 
+
+
+def test_radix_sort_keys(dev):
+    """The LSD radix sort orders keys exactly like the floats (with -0 == +0)."""
+    from distributedauc_amd import ops
+
+    rng = np.random.default_rng(12)
+    for n in (1, 7, 4096, 4097, 300_001):
+        v = rng.standard_normal(n).astype(np.float32) * rng.choice([1e-40, 1.0, 1e30], n).astype(np.float32)
+        v[rng.random(n) < 0.05] = 0.0
+        v[rng.random(n) < 0.05] = -0.0
+        k = ops.sort_keys(T(v, dev)).cpu().numpy().view(np.uint32)
+        assert np.all(k[1:] >= k[:-1]), n
+        u = np.sort(v.copy()).view(np.uint32)
+        u = np.where(np.sort(v) == 0, np.uint32(0x80000000), np.where(u >> 31, ~u, u | np.uint32(0x80000000)))
+        assert np.array_equal(k, u.astype(np.uint32)), n
+
+
+@pytest.mark.parametrize("P,N", [(1, 1), (5, 100_000), (100_000, 5), (50_000, 50_000), (3, 4096), (4096, 4097)])
+def test_sorted_counts_match_pair_count(dev, P, N):
+    from distributedauc_amd import ops
+
+    rng = np.random.default_rng(P * 7 + N)
+    pos = (np.floor(rng.random(P) * 97) / 97 - 0.5).astype(np.float32)
+    neg = (np.floor(rng.random(N) * 97) / 97 - 0.5).astype(np.float32)
+    neg[rng.random(N) < 0.1] = -0.0
+    a = torch.zeros(2, dtype=torch.int64, device=dev)
+    b = torch.zeros(2, dtype=torch.int64, device=dev)
+    ops.pair_count(T(pos, dev), T(neg, dev), a)
+    ops.auc_counts_sorted(T(pos, dev), T(neg, dev), b)
+    assert a.tolist() == b.tolist()
+    if P * N <= 10_000_000:
+        assert tuple(a.tolist()) == coracle.pair_count_bruteforce(pos, neg)
