@@ -54,6 +54,7 @@ def parse():
     p.add_argument("--auc-pos", type=float, default=0.01)
     p.add_argument("--auc-reps", type=int, default=3)
     p.add_argument("--variant", type=int, default=0, help="pair-count kernel variant")
+    p.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL; gloo for rehearsals)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-auc", action="store_true")
     p.add_argument("--no-train", action="store_true")
@@ -61,26 +62,35 @@ def parse():
 
 
 class KernelTimer:
-    """Wraps an ops function: HIP events on the launch stream around every call while enabled."""
+    """HIP events on the launch stream around every call of one libdauc.so entry point.
 
-    def __init__(self, module, name):
-        self.module, self.name = module, name
-        self.fn = getattr(module, name)
+    The wrapper replaces the ctypes function on the loaded library, so only the C call
+    (host launch + the kernel) sits between the two event records. The stream argument
+    is the last parameter of every dauc_* entry point.
+    """
+
+    def __init__(self, lib, name):
+        self.lib, self.name = lib, name
+        self.fn = getattr(lib, name)
         self.pairs = []
         self.enabled = False
+        fn = self.fn
 
-        def wrapped(*a, **k):
+        def wrapped(*a):
             if not self.enabled:
-                return self.fn(*a, **k)
+                return fn(*a)
             s = torch.cuda.current_stream()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(s)
-            r = self.fn(*a, **k)
+            r = fn(*a)
             e1.record(s)
             self.pairs.append((e0, e1))
             return r
 
-        setattr(module, name, wrapped)
+        setattr(lib, name, wrapped)
+
+    def restore(self):
+        setattr(self.lib, self.name, self.fn)
 
     def mean_ms(self):
         torch.cuda.synchronize()
@@ -100,7 +110,7 @@ def max_over_ranks(x: float, world: int) -> float:
 
 
 def bench_train(args, world, rank, device):
-    from distributedauc_amd import ops
+    from distributedauc_amd import _lib
     from distributedauc_amd.backbone import build_backbone
     from distributedauc_amd.coda import CoDA
     from distributedauc_amd.loader import DeviceLoader, SyntheticImageNet, imagenet_like_labels
@@ -118,8 +128,9 @@ def bench_train(args, world, rank, device):
     log(f"rank {rank}: model + data ready, first steps compile/tune MIOpen kernels")
     coda.average_all()            # main.py:141-142
     coda.begin_stage(1, it)       # alpha estimate + anchors (untimed)
-    upd = KernelTimer(ops, "pd_update")
-    sur = KernelTimer(ops, "surrogate_fwdbwd")
+    lib = _lib.load()
+    upd = KernelTimer(lib, "dauc_pd_update")
+    sur = KernelTimer(lib, "dauc_surrogate_fwdbwd")
     for _ in range(args.warmup):
         x, y = next(it)
         coda.train_step(x, y)
@@ -152,33 +163,41 @@ def bench_train(args, world, rank, device):
 
 
 def bench_auc(args, world, rank, device):
-    from distributedauc_amd import ops
+    """configs[3]: exact AUC of 2^k scores, sharded by positive blocks; both exact methods."""
+    from distributedauc_amd import _lib
     from distributedauc_amd.auc import ExactAUC
 
     n = 1 << args.auc_log2n
     g = torch.Generator(device=device).manual_seed(2024)  # same scores on every rank
     s = torch.rand(n, generator=g, device=device)
     y = torch.where(torch.rand(n, generator=g, device=device) < args.auc_pos, 1, -1).to(torch.int8)
-    ev = ExactAUC(world=world, rank=rank, variant=args.variant)
-    pc = KernelTimer(ops, "pair_count")
-    c = ev.counts(y, s)  # warm-up (also compiles nothing: AOT code object)
-    times = []
-    pc.enabled = True
-    for _ in range(args.auc_reps):
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        t0 = time.perf_counter()
-        c = ev.counts(y, s)
-        torch.cuda.synchronize()
-        times.append(time.perf_counter() - t0)
-    pc.enabled = False
-    t_eval = max_over_ranks(float(np.median(times)), world)
-    t_count = max_over_ranks(pc.mean_ms() / 1e3, world)
-    pairs = c["P"] * c["N"]
-    return {"n": n, "P": c["P"], "N": c["N"], "wins": c["wins"], "ties": c["ties"],
-            "auc": ExactAUC.from_counts(c), "t_eval": t_eval, "t_count": t_count, "pairs": pairs,
-            "scores": s, "labels": y}
+    out = {"n": n, "scores": s, "labels": y}
+    for method, fn in (("sort", "dauc_auc_counts_sorted"), ("pairs", "dauc_pair_count_variant")):
+        ev = ExactAUC(world=world, rank=rank, variant=args.variant, method=method)
+        kt = KernelTimer(_lib.load(), fn)
+        c = ev.counts(y, s)  # warm-up
+        reps = args.auc_reps if method == "pairs" else 5 * args.auc_reps
+        times = []
+        kt.enabled = True
+        for _ in range(reps):
+            torch.cuda.synchronize()
+            if world > 1:
+                dist.barrier()
+            t0 = time.perf_counter()
+            c = ev.counts(y, s)
+            torch.cuda.synchronize()
+            times.append(time.perf_counter() - t0)
+        kt.enabled = False
+        kt.restore()
+        out["m_" + method] = {"t_eval": max_over_ranks(float(np.median(times)), world),
+                              "t_count": max_over_ranks(kt.mean_ms() / 1e3, world), "counts": c}
+        log(f"rank {rank}: auc {method} eval {out['m_' + method]['t_eval'] * 1e3:.2f} ms")
+    a, b = out["m_sort"]["counts"], out["m_pairs"]["counts"]
+    if (a["wins"], a["ties"]) != (b["wins"], b["ties"]):
+        raise RuntimeError(f"exact AUC methods disagree: {a} vs {b}")
+    out.update({"P": a["P"], "N": a["N"], "wins": a["wins"], "ties": a["ties"], "auc": ExactAUC.from_counts(a),
+                "npairs": a["P"] * a["N"]})
+    return out
 
 
 def cpu_baseline_train(args):
@@ -226,7 +245,7 @@ def cpu_baseline_auc(auc_res):
     t0 = time.perf_counter()
     ref = R.auc_sklearn(y, s)
     dt = time.perf_counter() - t0
-    return {"value": auc_res["pairs"] / dt, "unit": "pairs/sec (effective: P*N / wall)", "cores": 1,
+    return {"value": auc_res["npairs"] / dt, "unit": "pairs/sec (effective: P*N / wall)", "cores": 1,
             "kind": "port", "seconds": dt, "auc": ref,
             "auc_abs_diff": abs(ref - auc_res["auc"]),
             "sample": f"full 2^{int(np.log2(auc_res['n']))} scores, sklearn roc_curve+auc (single-threaded sort)"}
@@ -237,10 +256,14 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    device = torch.device("cuda", local)
+    ndev = torch.cuda.device_count()
+    device = torch.device("cuda", local % max(ndev, 1))  # ranks share a device only in rehearsals
     torch.cuda.set_device(device)
     if world > 1:
-        dist.init_process_group("nccl", device_id=device)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group(args.backend)
     if args.gpus != world and rank == 0:
         print(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using {world}", file=sys.stderr)
 
@@ -267,15 +290,22 @@ def main():
                 "final_loss": res["loss"],
             })
         if auc is not None:
-            per_gpu = auc["pairs"] / auc["t_count"] / world
+            pk, sk = auc["m_pairs"], auc["m_sort"]
+            npairs = auc["npairs"]
+            pc_rate = npairs / pk["t_count"]
             out["auc_eval"] = {
                 "workload": f"exact AUC, 2^{args.auc_log2n} fp32 scores, {args.auc_pos:.0%} positives "
-                            "(BASELINE configs[3]), pair count sharded by positive blocks",
-                "pairs_per_sec": auc["pairs"] / auc["t_count"], "eval_pairs_per_sec": auc["pairs"] / auc["t_eval"],
-                "eval_ms": auc["t_eval"] * 1e3, "count_ms": auc["t_count"] * 1e3, "P": auc["P"], "N": auc["N"],
-                "wins": auc["wins"], "ties": auc["ties"], "auc": auc["auc"],
-                "roofline": {"kernel": "dauc_pair_count", "bound": "valu", "achieved": per_gpu,
-                             "peak": VALU_PAIR_PEAK, "unit": "pairs/s per GPU", "frac": per_gpu / VALU_PAIR_PEAK},
+                            "(BASELINE configs[3]), sharded by positive blocks, int64 all-reduce",
+                "pairs_per_sec": npairs / sk["t_eval"],
+                "method": "sort (radix sort of negatives + binary search; default evaluator)",
+                "eval_ms": sk["t_eval"] * 1e3, "sort_count_ms": sk["t_count"] * 1e3,
+                "P": auc["P"], "N": auc["N"], "wins": auc["wins"], "ties": auc["ties"], "auc": auc["auc"],
+                "methods_agree": True,
+                "pair_count_kernel": {
+                    "pairs_per_sec": pc_rate, "eval_ms": pk["t_eval"] * 1e3, "count_ms": pk["t_count"] * 1e3,
+                    "roofline": {"kernel": "dauc_pair_count", "bound": "valu", "achieved": pc_rate / world,
+                                 "peak": VALU_PAIR_PEAK, "unit": "pairs/s per GPU",
+                                 "frac": pc_rate / world / VALU_PAIR_PEAK}},
             }
         if world == 1 and not args.no_cpu_baseline:
             torch.set_num_threads(min(16, os.cpu_count() or 1))

@@ -18,6 +18,7 @@ HEADER = PKG_DIR.parent / "include" / "dauc.h"
 DAUC_OK = 0
 DAUC_EINVAL = -100000
 LABEL_I8, LABEL_I32, LABEL_I64 = 1, 2, 3
+DTYPE_F32, DTYPE_BF16 = 1, 2
 MODE_REFERENCE, MODE_PAPER = 0, 1
 
 
@@ -47,6 +48,9 @@ SIGNATURES = {
                                      _vp, _sz, _vp]),
     "dauc_class_sums": (_int, [_vp, _i64, _vp, _int, _i64, _vp, _int, _vp, _sz, _vp]),
     "dauc_alpha_from_sums": (_int, [_vp, _vp, _vp]),
+    "dauc_surrogate_logits_fwdbwd": (_int, [_vp, _int, _i64, _vp, _int, _i64, _vp, _vp, _vp, _i64, _vp, _vp,
+                                            _vp, _vp, _vp, _sz, _vp]),
+    "dauc_class_sums_logits": (_int, [_vp, _int, _i64, _vp, _int, _i64, _vp, _vp, _int, _vp, _sz, _vp]),
     "dauc_pd_update": (_int, [_vp, _vp, _vp, ctypes.POINTER(GradSeg), _int, _vp, _vp, _vp, _f32, _f32,
                               _int, _vp]),
     "dauc_pd_update_dense": (_int, [_vp, _vp, _vp, _vp, _i64, _f32, _f32, _vp]),

@@ -28,7 +28,7 @@ import torch.nn as nn
 
 from . import ops
 from .flat import FlatState
-from .surrogate import auc_surrogate
+from .surrogate import auc_surrogate, auc_surrogate_logits
 
 
 class CoDA:
@@ -37,10 +37,13 @@ class CoDA:
     def __init__(self, model: nn.Module, *, lr: float = 0.1, gamma: float = 2000.0, T0: int = 5000,
                  I: int = 2, split_index: int = 4, mode: str = "reference", world: int = 1, rank: int = 0,
                  group=None, autocast_dtype: torch.dtype | None = None, device=None,
-                 max_exact_count: int = 1 << 24):
+                 max_exact_count: int = 1 << 24, head: str = "softmax"):
         if I < 1:
             raise ValueError("averaging period I must be >= 1")
         ops.mode_code(mode)  # validates
+        if head not in ("softmax", "logits"):
+            raise ValueError("head must be 'softmax' (model outputs probabilities, resnet.py:218) or 'logits'")
+        self.head = head  # "logits": the model's softmax is folded into the surrogate kernel (§8f row 2)
         self.model = model
         self.state = FlatState(model, device)
         self.device = self.state.device
@@ -71,10 +74,15 @@ class CoDA:
             return contextlib.nullcontext()
         return torch.autocast(device_type="cuda", dtype=self.autocast_dtype)
 
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        with self._autocast():
+            return self.model(x)
+
     def scores(self, x: torch.Tensor) -> torch.Tensor:
         """h = net(x)[:, 1] (resnet.py:218: column 1 of the softmax), fp32."""
-        with self._autocast():
-            out = self.model(x)
+        out = self.forward(x)
+        if self.head == "logits":
+            out = torch.softmax(out.float(), dim=1)
         h = out[:, 1]
         return h if h.dtype == torch.float32 else h.float()
 
@@ -102,7 +110,10 @@ class CoDA:
                 self._scratch.zero_()
                 ops.label_map_phat(labels, self.split_index, y8, self._scratch[0:2], self._scratch[2:4],
                                    self._scratch[4:5])
-                ops.class_sums(self.scores(x), y8, self._sums4, accumulate=True)
+                if self.head == "logits":
+                    ops.class_sums_logits(self.forward(x), y8, self._sums4, accumulate=True)
+                else:
+                    ops.class_sums(self.scores(x), y8, self._sums4, accumulate=True)
             self.model.train()
             if self.world > 1:
                 dist.all_reduce(self._sums4, op=dist.ReduceOp.SUM, group=self.group)  # main.py:192-195
@@ -131,8 +142,10 @@ class CoDA:
                 self.average_all()
         y8 = st.y8(B)
         ops.label_map_phat(labels, self.split_index, y8, st.lcounts, st.gcounts, st.p_hat)
-        h = self.scores(x)
-        loss = auc_surrogate(h, y8, st.abalpha, st.p_hat, st.grad3)
+        if self.head == "logits":
+            loss = auc_surrogate_logits(self.forward(x), y8, st.abalpha, st.p_hat, st.grad3)
+        else:
+            loss = auc_surrogate(self.scores(x), y8, st.abalpha, st.p_hat, st.grad3)
         loss.backward()
         st.update(self.lr, self.gamma, self.mode)
         self.model.zero_grad(set_to_none=True)

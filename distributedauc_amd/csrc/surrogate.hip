@@ -11,6 +11,8 @@
 // sum((h-b)^2) are folded into fp64; with the two class counts they are reduced
 // wave -> block -> grid in a fixed order, so results are bitwise reproducible.
 
+#include <hip/hip_bf16.h>
+
 #include "dauc_internal.h"
 
 namespace dauc {
@@ -45,6 +47,16 @@ enum { S_POS = 0, S_NEG, Q_POS, Q_NEG, N_POS, N_NEG };
 // Resident-block capacity of the device for the surrogate kernel (queried once, cached):
 // a grid of exactly that many blocks has no partially filled last wave.
 int resident_blocks();
+
+// grid of the one-element-per-thread logits kernel (never smaller than grid_for)
+int grid_scalar(int64_t B) {
+    int64_t g = (B + kThreads - 1) / kThreads;
+    const int64_t cap = resident_blocks();
+    if (g > cap) g = cap;
+    if (g < 1) g = 1;
+    if (g > kMaxBlocks) g = kMaxBlocks;
+    return static_cast<int>(g);
+}
 
 int grid_for(int64_t B) {
     int64_t g = (B + kPerBlockIter - 1) / kPerBlockIter;
@@ -172,6 +184,108 @@ __device__ __forceinline__ void load_labels4(const YT* __restrict__ y, int64_t b
     }
 }
 
+// Block reduction, then the grid reduction by the last-arriving block, then the
+// final scalars. Every block of the grid calls this exactly once.
+template <bool CLASS_ONLY>
+__device__ __forceinline__ void reduce_and_finalize(const Acc& acc, const SurrogateScalars& s, double invB,
+                                                    double* __restrict__ partials,
+                                                    unsigned* __restrict__ counter,
+                                                    double* __restrict__ out64, float* __restrict__ grad3,
+                                                    float* __restrict__ loss, double* __restrict__ sums4,
+                                                    int accumulate) {
+    __shared__ double scratch[kNumAcc * (kThreads / kWave)];
+    __shared__ int last_flag;
+    double tot[kNumAcc] = {acc.s_pos, acc.s_neg, acc.q_pos, acc.q_neg,
+                           static_cast<double>(acc.n_pos), static_cast<double>(acc.n_neg)};
+    block_sum<kNumAcc>(tot, scratch);
+
+    if (gridDim.x == 1) {
+        if (threadIdx.x == 0) {
+            if (CLASS_ONLY) emit_class_sums(tot, sums4, accumulate);
+            else finalize(tot, s, invB, out64, grad3, loss);
+        }
+        return;
+    }
+
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int k = 0; k < kNumAcc; ++k) partials[blockIdx.x * kNumAcc + k] = tot[k];
+    }
+    if (!arrive_last(counter, gridDim.x, &last_flag)) return;
+
+    // Last block: reduce all partials in a fixed order.
+#pragma unroll
+    for (int k = 0; k < kNumAcc; ++k) tot[k] = 0.0;
+    for (int b = threadIdx.x; b < static_cast<int>(gridDim.x); b += kThreads) {
+#pragma unroll
+        for (int k = 0; k < kNumAcc; ++k) tot[k] += partials[b * kNumAcc + k];
+    }
+    block_sum<kNumAcc>(tot, scratch);
+    if (threadIdx.x == 0) {
+        if (CLASS_ONLY) emit_class_sums(tot, sums4, accumulate);
+        else finalize(tot, s, invB, out64, grad3, loss);
+    }
+}
+
+// One element: accumulate its contribution (per-element fp64 folding) and return dF/dh.
+template <bool CLASS_ONLY>
+__device__ __forceinline__ float visit1(float hv, int yv, const SurrogateScalars& s, Acc& acc) {
+    const bool pos = (yv == 1), neg = (yv == -1);
+    const float dp = pos ? hv - s.af : 0.f;
+    const float dn = neg ? hv - s.bf : 0.f;
+    acc.s_pos += dp;
+    acc.s_neg += dn;
+    if (!CLASS_ONLY) {
+        acc.q_pos += dp * dp;
+        acc.q_neg += dn * dn;
+    }
+    acc.n_pos += pos;
+    acc.n_neg += neg;
+    if (CLASS_ONLY) return 0.f;
+    const float cc = pos ? s.c_pos : (neg ? s.c_neg : 0.f);
+    const float kk = pos ? s.k_pos : s.k_neg;
+    return cc * (hv - kk);
+}
+
+__device__ __forceinline__ float to_f32(float v) { return v; }
+__device__ __forceinline__ float to_f32(__hip_bfloat16 v) { return __bfloat162float(v); }
+template <typename ZT>
+__device__ __forceinline__ ZT from_f32(float v);
+template <>
+__device__ __forceinline__ float from_f32<float>(float v) { return v; }
+template <>
+__device__ __forceinline__ __hip_bfloat16 from_f32<__hip_bfloat16>(float v) { return __float2bfloat16(v); }
+
+// the loss straight from the 2-way logits z [B, 2] (row stride ldz):
+// h = softmax(z)[:, 1] = 1 / (1 + exp(z0 - z1)) in fp32, and the backward through the
+// softmax column is fused: dF/dz1 = dF/dh * h * (1 - h), dF/dz0 = -dF/dz1 (resnet.py:218).
+// h_out (nullable) receives h in fp32.
+template <typename ZT, typename YT, bool CLASS_ONLY>
+__global__ __launch_bounds__(kThreads) void surrogate_logits_kernel(
+    const ZT* __restrict__ z, int64_t ldz, const YT* __restrict__ y, int64_t B, double invB,
+    const float* __restrict__ abalpha, const float* __restrict__ p_hat, ZT* __restrict__ dz, int64_t lddz,
+    float* __restrict__ h_out, double* __restrict__ partials, unsigned* __restrict__ counter,
+    double* __restrict__ out64, float* __restrict__ grad3, float* __restrict__ loss,
+    double* __restrict__ sums4, int accumulate) {
+    SurrogateScalars s;
+    if (CLASS_ONLY) s = SurrogateScalars{};
+    else s = make_scalars(abalpha, p_hat, invB);
+    Acc acc;
+    for (int64_t i = int64_t(blockIdx.x) * kThreads + threadIdx.x; i < B; i += int64_t(gridDim.x) * kThreads) {
+        const float z0 = to_f32(z[i * ldz]);
+        const float z1 = to_f32(z[i * ldz + 1]);
+        const float h = 1.0f / (1.0f + expf(z0 - z1));
+        if (h_out) h_out[i] = h;
+        const float g = visit1<CLASS_ONLY>(h, load_label(y, i), s, acc);
+        if (!CLASS_ONLY && dz) {
+            const float gz = g * h * (1.0f - h);
+            dz[i * lddz] = from_f32<ZT>(-gz);
+            dz[i * lddz + 1] = from_f32<ZT>(gz);
+        }
+    }
+    reduce_and_finalize<CLASS_ONLY>(acc, s, invB, partials, counter, out64, grad3, loss, sums4, accumulate);
+}
+
 // UNIT: h, y and dh are unit-stride and 4-element aligned (vector loads/stores).
 template <typename YT, bool CLASS_ONLY, bool UNIT>
 __global__ __launch_bounds__(kThreads) void surrogate_kernel(
@@ -180,9 +294,6 @@ __global__ __launch_bounds__(kThreads) void surrogate_kernel(
     int64_t dhs, double* __restrict__ partials, unsigned* __restrict__ counter,
     double* __restrict__ out64, float* __restrict__ grad3, float* __restrict__ loss,
     double* __restrict__ sums4, int accumulate) {
-    __shared__ double scratch[kNumAcc * (kThreads / kWave)];
-    __shared__ int last_flag;
-
     SurrogateScalars s;
     if (CLASS_ONLY) {
         s = SurrogateScalars{};
@@ -223,58 +334,12 @@ __global__ __launch_bounds__(kThreads) void surrogate_kernel(
     {
         for (int64_t i = done + int64_t(blockIdx.x) * kThreads + threadIdx.x; i < B;
              i += int64_t(gridDim.x) * kThreads) {
-            const float hv = h[i * hs];
-            const int yv = load_label(y, i);
-            const bool pos = (yv == 1), neg = (yv == -1);
-            const float dp = pos ? hv - s.af : 0.f;
-            const float dn = neg ? hv - s.bf : 0.f;
-            // per-element fp64 folding keeps long strided loops exact to fp64 rounding
-            acc.s_pos += dp;
-            acc.s_neg += dn;
-            if (!CLASS_ONLY) {
-                acc.q_pos += dp * dp;
-                acc.q_neg += dn * dn;
-            }
-            acc.n_pos += pos;
-            acc.n_neg += neg;
-            if (write_dh) {
-                const float cc = pos ? s.c_pos : (neg ? s.c_neg : 0.f);
-                const float kk = pos ? s.k_pos : s.k_neg;
-                dh[i * dhs] = cc * (hv - kk);
-            }
+            const float g = visit1<CLASS_ONLY>(h[i * hs], load_label(y, i), s, acc);
+            if (write_dh) dh[i * dhs] = g;
         }
     }
 
-    double tot[kNumAcc] = {acc.s_pos, acc.s_neg, acc.q_pos, acc.q_neg,
-                           static_cast<double>(acc.n_pos), static_cast<double>(acc.n_neg)};
-    block_sum<kNumAcc>(tot, scratch);
-
-    if (gridDim.x == 1) {
-        if (threadIdx.x == 0) {
-            if (CLASS_ONLY) emit_class_sums(tot, sums4, accumulate);
-            else finalize(tot, s, invB, out64, grad3, loss);
-        }
-        return;
-    }
-
-    if (threadIdx.x == 0) {
-#pragma unroll
-        for (int k = 0; k < kNumAcc; ++k) partials[blockIdx.x * kNumAcc + k] = tot[k];
-    }
-    if (!arrive_last(counter, gridDim.x, &last_flag)) return;
-
-    // Last block: reduce all partials in a fixed order.
-#pragma unroll
-    for (int k = 0; k < kNumAcc; ++k) tot[k] = 0.0;
-    for (int b = threadIdx.x; b < static_cast<int>(gridDim.x); b += kThreads) {
-#pragma unroll
-        for (int k = 0; k < kNumAcc; ++k) tot[k] += partials[b * kNumAcc + k];
-    }
-    block_sum<kNumAcc>(tot, scratch);
-    if (threadIdx.x == 0) {
-        if (CLASS_ONLY) emit_class_sums(tot, sums4, accumulate);
-        else finalize(tot, s, invB, out64, grad3, loss);
-    }
+    reduce_and_finalize<CLASS_ONLY>(acc, s, invB, partials, counter, out64, grad3, loss, sums4, accumulate);
 }
 
 int resident_blocks() {
@@ -350,6 +415,60 @@ int dispatch_labels(const float* h, int64_t hs, const void* y, int yt, int64_t B
     }
 }
 
+template <bool CLASS_ONLY, typename ZT, typename YT>
+int launch_logits_t(const ZT* z, int64_t ldz, const YT* y, int64_t B, const float* abalpha, const float* p_hat,
+                    ZT* dz, int64_t lddz, float* h_out, double* out64, float* grad3, float* loss, double* sums4,
+                    int accumulate, void* ws, size_t ws_bytes, hipStream_t st) {
+    const int grid = grid_scalar(B);
+    unsigned* counter = nullptr;
+    double* partials = nullptr;
+    if (grid > 1) {
+        if (ws == nullptr || ws_bytes < dauc_surrogate_workspace_size(B)) return DAUC_EINVAL;
+        counter = static_cast<unsigned*>(ws);
+        partials = reinterpret_cast<double*>(static_cast<char*>(ws) + kCounterBytes);
+    }
+    hipLaunchKernelGGL((surrogate_logits_kernel<ZT, YT, CLASS_ONLY>), dim3(grid), dim3(kThreads), 0, st, z, ldz,
+                       y, B, 1.0 / static_cast<double>(B), abalpha, p_hat, dz, lddz, h_out, partials, counter,
+                       out64, grad3, loss, sums4, accumulate);
+    return launch_status();
+}
+
+template <bool CLASS_ONLY, typename ZT>
+int launch_logits_y(const ZT* z, int64_t ldz, const void* y, int yt, int64_t B, const float* abalpha,
+                    const float* p_hat, ZT* dz, int64_t lddz, float* h_out, double* out64, float* grad3,
+                    float* loss, double* sums4, int accumulate, void* ws, size_t ws_bytes, hipStream_t st) {
+    switch (yt) {
+        case DAUC_LABEL_I8:
+            return launch_logits_t<CLASS_ONLY>(z, ldz, static_cast<const int8_t*>(y), B, abalpha, p_hat, dz, lddz,
+                                               h_out, out64, grad3, loss, sums4, accumulate, ws, ws_bytes, st);
+        case DAUC_LABEL_I32:
+            return launch_logits_t<CLASS_ONLY>(z, ldz, static_cast<const int32_t*>(y), B, abalpha, p_hat, dz,
+                                               lddz, h_out, out64, grad3, loss, sums4, accumulate, ws, ws_bytes,
+                                               st);
+        case DAUC_LABEL_I64:
+            return launch_logits_t<CLASS_ONLY>(z, ldz, static_cast<const int64_t*>(y), B, abalpha, p_hat, dz,
+                                               lddz, h_out, out64, grad3, loss, sums4, accumulate, ws, ws_bytes,
+                                               st);
+        default:
+            return DAUC_EINVAL;
+    }
+}
+
+template <bool CLASS_ONLY>
+int launch_logits(const void* z, int zt, int64_t ldz, const void* y, int yt, int64_t B, const float* abalpha,
+                  const float* p_hat, void* dz, int64_t lddz, float* h_out, double* out64, float* grad3,
+                  float* loss, double* sums4, int accumulate, void* ws, size_t ws_bytes, hipStream_t st) {
+    if (zt == DAUC_DTYPE_F32)
+        return launch_logits_y<CLASS_ONLY>(static_cast<const float*>(z), ldz, y, yt, B, abalpha, p_hat,
+                                           static_cast<float*>(dz), lddz, h_out, out64, grad3, loss, sums4,
+                                           accumulate, ws, ws_bytes, st);
+    if (zt == DAUC_DTYPE_BF16)
+        return launch_logits_y<CLASS_ONLY>(static_cast<const __hip_bfloat16*>(z), ldz, y, yt, B, abalpha, p_hat,
+                                           static_cast<__hip_bfloat16*>(dz), lddz, h_out, out64, grad3, loss,
+                                           sums4, accumulate, ws, ws_bytes, st);
+    return DAUC_EINVAL;
+}
+
 // ---- a1: label map + class counts + p_hat (one block; B is a training batch) ----
 __global__ __launch_bounds__(kThreads) void label_map_phat_kernel(
     const int64_t* __restrict__ labels, int64_t B, int64_t split, int8_t* __restrict__ y_out,
@@ -402,7 +521,7 @@ using namespace dauc;
 extern "C" {
 
 size_t dauc_surrogate_workspace_size(int64_t B) {
-    const int g = grid_for(B < 0 ? 0 : B);
+    const int g = grid_scalar(B < 0 ? 0 : B);  // >= grid_for(B): covers every surrogate kernel
     return kCounterBytes + static_cast<size_t>(g) * kNumAcc * sizeof(double);
 }
 
@@ -426,6 +545,25 @@ int dauc_class_sums(const float* h, int64_t h_stride, const void* y, int y_dtype
     return dispatch_labels<true>(h, h_stride, y, y_dtype, B, nullptr, nullptr, nullptr, 1, nullptr,
                                  nullptr, nullptr, sums4, accumulate, workspace, workspace_bytes,
                                  as_hip(stream));
+}
+
+int dauc_surrogate_logits_fwdbwd(const void* z, int z_dtype, int64_t ldz, const void* y, int y_dtype,
+                                 int64_t B, const float* abalpha, const float* p_hat, void* dz, int64_t lddz,
+                                 float* h_out, double* out64, float* grad3, float* loss, void* workspace,
+                                 size_t workspace_bytes, dauc_stream_t stream) {
+    if (B <= 0 || z == nullptr || y == nullptr || abalpha == nullptr || p_hat == nullptr || ldz < 2 ||
+        (dz != nullptr && lddz < 2))
+        return DAUC_EINVAL;
+    return launch_logits<false>(z, z_dtype, ldz, y, y_dtype, B, abalpha, p_hat, dz, lddz, h_out, out64, grad3,
+                                loss, nullptr, 0, workspace, workspace_bytes, as_hip(stream));
+}
+
+int dauc_class_sums_logits(const void* z, int z_dtype, int64_t ldz, const void* y, int y_dtype, int64_t B,
+                           float* h_out, double* sums4, int accumulate, void* workspace, size_t workspace_bytes,
+                           dauc_stream_t stream) {
+    if (B <= 0 || z == nullptr || y == nullptr || sums4 == nullptr || ldz < 2) return DAUC_EINVAL;
+    return launch_logits<true>(z, z_dtype, ldz, y, y_dtype, B, nullptr, nullptr, nullptr, 2, h_out, nullptr,
+                               nullptr, nullptr, sums4, accumulate, workspace, workspace_bytes, as_hip(stream));
 }
 
 int dauc_alpha_from_sums(const double* sums4, float* alpha, dauc_stream_t stream) {

@@ -165,6 +165,74 @@ def class_sums(h: torch.Tensor, y: torch.Tensor, sums4: torch.Tensor, accumulate
                             _ptr(ws), ws.numel(), _stream(dev)), "dauc_class_sums")
 
 
+_Z_CODES = {torch.float32: _lib.DTYPE_F32, torch.bfloat16: _lib.DTYPE_BF16}
+
+
+def _check_logits(z: torch.Tensor, y: torch.Tensor) -> tuple[int, int]:
+    _require_gpu(z, "z")
+    if z.dtype not in _Z_CODES:
+        raise TypeError(f"logits must be fp32 or bf16, got {z.dtype}")
+    if z.dim() != 2 or z.shape[1] != 2 or z.stride(1) != 1:
+        raise ValueError(f"logits must be [B, 2] with unit column stride, got {tuple(z.shape)} {z.stride()}")
+    if y.dim() != 1 or y.shape[0] != z.shape[0] or y.stride(0) != 1 or y.device != z.device:
+        raise ValueError("labels must be contiguous [B] on the logits' device")
+    if z.shape[0] == 0:
+        raise ValueError("empty batch")
+    return z.shape[0], _Z_CODES[z.dtype]
+
+
+def surrogate_logits_fwdbwd(z: torch.Tensor, y: torch.Tensor, abalpha: torch.Tensor, p_hat: torch.Tensor, *,
+                            dz: torch.Tensor | None = None, h_out: torch.Tensor | None = None,
+                            out64: torch.Tensor | None = None, grad3: torch.Tensor | None = None,
+                            loss: torch.Tensor | None = None) -> None:
+    """loss and dF/dz straight from the [B,2] logits (softmax column fused)."""
+    B, zc = _check_logits(z, y)
+    dev = z.device
+    yc = _label_code(y)
+    _require(abalpha, "abalpha", torch.float32, dev)
+    _require(p_hat, "p_hat", torch.float32, dev)
+    if abalpha.numel() < 3 or not abalpha.is_contiguous():
+        raise ValueError("abalpha needs 3 contiguous fp32 values")
+    lddz = 2
+    if dz is not None:
+        _require(dz, "dz", z.dtype, dev)
+        if dz.shape != z.shape or dz.stride(1) != 1:
+            raise ValueError("dz must match the logits' shape with unit column stride")
+        lddz = dz.stride(0)
+    if h_out is not None:
+        _require(h_out, "h_out", torch.float32, dev)
+        if h_out.numel() < B or not h_out.is_contiguous():
+            raise ValueError("h_out needs B contiguous fp32 slots")
+    for t, n, dt, k in ((out64, "out64", torch.float64, 6), (grad3, "grad3", torch.float32, 3)):
+        if t is not None:
+            _require(t, n, dt, dev)
+            if t.numel() < k or not t.is_contiguous():
+                raise ValueError(f"{n} needs {k} contiguous slots")
+    if loss is not None:
+        _require(loss, "loss", torch.float32, dev)
+    L = _lib.load()
+    ws = workspaces.get(dev, "surrogate", L.dauc_surrogate_workspace_size(B))
+    check(L.dauc_surrogate_logits_fwdbwd(_ptr(z), zc, z.stride(0), _ptr(y), yc, B, _ptr(abalpha), _ptr(p_hat),
+                                         _ptr(dz), lddz, _ptr(h_out), _ptr(out64), _ptr(grad3), _ptr(loss),
+                                         _ptr(ws), ws.numel(), _stream(dev)), "dauc_surrogate_logits_fwdbwd")
+
+
+def class_sums_logits(z: torch.Tensor, y: torch.Tensor, sums4: torch.Tensor, accumulate: bool = True,
+                      h_out: torch.Tensor | None = None) -> None:
+    """class_sums with h = softmax(z)[:, 1] computed in the kernel."""
+    B, zc = _check_logits(z, y)
+    dev = z.device
+    yc = _label_code(y)
+    _require(sums4, "sums4", torch.float64, dev)
+    if h_out is not None:
+        _require(h_out, "h_out", torch.float32, dev)
+    L = _lib.load()
+    ws = workspaces.get(dev, "surrogate", L.dauc_surrogate_workspace_size(B))
+    check(L.dauc_class_sums_logits(_ptr(z), zc, z.stride(0), _ptr(y), yc, B, _ptr(h_out), _ptr(sums4),
+                                   int(bool(accumulate)), _ptr(ws), ws.numel(), _stream(dev)),
+          "dauc_class_sums_logits")
+
+
 def alpha_from_sums(sums4: torch.Tensor, alpha: torch.Tensor) -> None:
     """main.py:197 on the device: alpha = h_neg/N_neg - h_pos/N_pos."""
     _require(sums4, "sums4", torch.float64)
@@ -309,5 +377,6 @@ def sort_keys(scores: torch.Tensor) -> torch.Tensor:
 __all__ = [
     "GradSeg", "label_map_phat", "surrogate_fwdbwd", "class_sums", "alpha_from_sums", "pd_update",
     "pd_update_dense", "coda_finalize", "scale_div", "split_scores", "pair_count", "auc_counts_sorted",
+    "surrogate_logits_fwdbwd", "class_sums_logits",
     "sort_keys", "mode_code", "workspaces",
 ]

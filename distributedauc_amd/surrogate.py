@@ -42,3 +42,35 @@ def auc_surrogate(h: torch.Tensor, y: torch.Tensor, abalpha: torch.Tensor, p_hat
     kernel writes (dF/da, dF/db, dF/dalpha) into it during the forward pass.
     """
     return AUCSurrogate.apply(h, y, abalpha, p_hat, grad3)
+
+
+class AUCSurrogateLogits(torch.autograd.Function):
+    """The same loss from the [B, 2] logits with the softmax column fused.
+
+    Backward hands dF/dz (same dtype as z) to the backbone: the softmax forward and
+    backward kernels (resnet.py:159, 218) are not run at all.
+    """
+
+    @staticmethod
+    def forward(ctx, z, y, abalpha, p_hat, grad3):
+        dz = torch.empty_like(z, memory_format=torch.contiguous_format)
+        loss = torch.empty((), dtype=torch.float32, device=z.device)
+        g3 = grad3 if grad3 is not None else torch.empty(3, dtype=torch.float32, device=z.device)
+        ops.surrogate_logits_fwdbwd(z, y, abalpha, p_hat, dz=dz, grad3=g3, loss=loss)
+        ctx.save_for_backward(dz, g3)
+        ctx.abalpha_grad = abalpha.requires_grad
+        return loss
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        dz, g3 = ctx.saved_tensors
+        d_ab = g3 * grad_out if ctx.abalpha_grad else None
+        return dz * grad_out.to(dz.dtype), None, d_ab, None, None
+
+
+def auc_surrogate_logits(z: torch.Tensor, y: torch.Tensor, abalpha: torch.Tensor, p_hat: torch.Tensor,
+                         grad3: torch.Tensor | None = None) -> torch.Tensor:
+    """Loss of main.py:313-317 from 2-way logits z [B, 2] (fp32 or bf16), h = softmax(z)[:, 1]."""
+    if not z.is_contiguous():
+        z = z.contiguous()
+    return AUCSurrogateLogits.apply(z, y, abalpha, p_hat, grad3)

@@ -43,6 +43,10 @@ typedef struct ihipStream_t* dauc_stream_t; /* == hipStream_t */
 #define DAUC_LABEL_I32 2
 #define DAUC_LABEL_I64 3
 
+/* element types of the logits accepted by the fused-softmax surrogate */
+#define DAUC_DTYPE_F32 1
+#define DAUC_DTYPE_BF16 2
+
 /* dauc_pd_update modes */
 #define DAUC_MODE_REFERENCE 0 /* main.py:58-64 as written: b prox uses (a_new-a0), alpha unchanged */
 #define DAUC_MODE_PAPER 1     /* b prox uses (b-b0), alpha <- alpha + lr*dF/dalpha              */
@@ -102,6 +106,24 @@ int dauc_surrogate_fwdbwd(const float* h, int64_t h_stride, const void* y, int y
 int dauc_class_sums(const float* h, int64_t h_stride, const void* y, int y_dtype, int64_t B,
                     double* sums4, int accumulate, void* workspace, size_t workspace_bytes,
                     dauc_stream_t stream);
+
+/*
+ * the same loss straight from the 2-way logits z [B,2] (row stride
+ * ldz, fp32 or bf16), i.e. with the backbone's final softmax (resnet.py:159, 218)
+ * folded into the kernel: h = 1/(1+exp(z0-z1)) in fp32, and the backward through
+ * the softmax column fused: dz[i,1] = dF/dh_i * h_i*(1-h_i), dz[i,0] = -dz[i,1]
+ * (dz same dtype as z, row stride lddz; nullable). h_out [B] fp32 (nullable)
+ * receives the probabilities. Other outputs as dauc_surrogate_fwdbwd.
+ */
+int dauc_surrogate_logits_fwdbwd(const void* z, int z_dtype, int64_t ldz, const void* y, int y_dtype,
+                                 int64_t B, const float* abalpha, const float* p_hat, void* dz, int64_t lddz,
+                                 float* h_out, double* out64, float* grad3, float* loss, void* workspace,
+                                 size_t workspace_bytes, dauc_stream_t stream);
+
+/* dauc_class_sums from the logits (h = softmax(z)[:,1] computed in the kernel; h_out nullable). */
+int dauc_class_sums_logits(const void* z, int z_dtype, int64_t ldz, const void* y, int y_dtype, int64_t B,
+                           float* h_out, double* sums4, int accumulate, void* workspace, size_t workspace_bytes,
+                           dauc_stream_t stream);
 
 /*
  * main.py:197: alpha[0] = (float)(sums4[0]/sums4[1] - sums4[2]/sums4[3]).

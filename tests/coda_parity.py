@@ -31,16 +31,18 @@ def close(got, ref, what, rtol=RTOL, atol=ATOL):
                              f"ref {ref.reshape(-1)[i]!r}")
 
 
-def run_rank(fixture: dict, rank: int, world: int, device, group=None):
+def run_rank(fixture: dict, rank: int, world: int, device, group=None, head: str = "softmax"):
     from distributedauc_amd.coda import CoDA
 
     cfg = json.loads(str(fixture["config"]))
     net = tinynet.TinyNet()
     net.load_state_dict({k[len("init_"):]: torch.from_numpy(v) for k, v in fixture.items()
                          if k.startswith("init_")})
+    if head == "logits":  # fold the softmax into the surrogate kernel
+        net.softmax = torch.nn.Identity()
     net = net.to(device)
     coda = CoDA(net, lr=cfg["lr"], gamma=cfg["gamma"], T0=cfg["T0"], I=cfg["I"], split_index=cfg["split_index"],
-                world=world, rank=rank, group=group, device=device)
+                world=world, rank=rank, group=group, device=device, head=head)
     xs, ys = fixture[f"r{rank}_x"], fixture[f"r{rank}_y"]
 
     def batches():

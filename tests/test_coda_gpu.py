@@ -31,6 +31,13 @@ def test_coda_round_world1(dev, golden):
     coda_parity.compare(fx, 0, rec)
 
 
+def test_coda_round_world1_fused_softmax_head(dev, golden):
+    """Same trajectory with the softmax column folded into the surrogate kernel."""
+    fx = _load(golden, 1)
+    rec, _ = coda_parity.run_rank(fx, 0, 1, dev, head="logits")
+    coda_parity.compare(fx, 0, rec)
+
+
 def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))

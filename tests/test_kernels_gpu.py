@@ -411,3 +411,59 @@ def test_sorted_counts_match_pair_count(dev, P, N):
     assert a.tolist() == b.tolist()
     if P * N <= 10_000_000:
         assert tuple(a.tolist()) == coracle.pair_count_bruteforce(pos, neg)
+
+
+@pytest.mark.parametrize("zdtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("B", [1, 256, 5000])
+def test_surrogate_logits_fused_softmax(dev, zdtype, B):
+    """§8f row 2: loss/grads from logits vs fp64 closed form; dz vs torch autograd through softmax."""
+    from distributedauc_amd import ops
+    from distributedauc_amd.surrogate import auc_surrogate_logits
+
+    rng = np.random.default_rng(B)
+    z = torch.from_numpy(rng.normal(0, 2, (B, 2)).astype(np.float32)).to(dev).to(zdtype)
+    y = np.where(rng.random(B) < 0.3, 1, -1).astype(np.int8)
+    y[rng.random(B) < 0.05] = 0
+    ab = torch.tensor([0.2, -0.1, 0.05], device=dev)
+    p = torch.tensor([0.3], device=dev)
+    out64 = torch.zeros(6, dtype=torch.float64, device=dev)
+    h_out = torch.empty(B, device=dev)
+    dz = torch.empty_like(z)
+    ops.surrogate_logits_fwdbwd(z, T(y, dev), ab, p, dz=dz, h_out=h_out, out64=out64)
+    zf = z.float().cpu().numpy().astype(np.float64)
+    h64 = 1.0 / (1.0 + np.exp(zf[:, 0] - zf[:, 1]))
+    assert np.allclose(h_out.cpu().numpy(), h64, rtol=2e-6, atol=1e-7)
+    F, dh64, da, db, dal = R.surrogate_closed_form(h64.astype(np.float32), y.astype(np.int64), 0.2, -0.1, 0.05,
+                                                   np.float32(0.3))
+    sc = _scales(h64, y, 0.2, -0.1, 0.05, float(np.float32(0.3)))
+    assert np.all(np.abs(out64.cpu().numpy()[:4] - [F, da, db, dal]) <= 1e-5 * sc + 1e-12)
+    # autograd of the reference expression through torch's softmax, fp32
+    zt = z.float().detach().clone().requires_grad_(True)
+    hh = torch.softmax(zt, dim=1)[:, 1]
+    Fr = R.surrogate_loss(hh, T(y.astype(np.int64), dev), ab[0], ab[1], ab[2], p[0])
+    Fr.backward()
+    ref = zt.grad.cpu().numpy()
+    got = dz.float().cpu().numpy()
+    tol = 1e-5 if zdtype == torch.float32 else 8e-3  # bf16 output rounding (8-bit mantissa)
+    scale = np.abs(ref).max() + 1e-12
+    assert np.all(np.abs(got - ref) <= tol * np.maximum(np.abs(ref), 1e-3 * scale) + 1e-9), zdtype
+    # through autograd: loss.backward() delivers dz to the producer of z
+    zz = z.detach().clone().requires_grad_(True)
+    g3 = torch.zeros(3, device=dev)
+    loss = auc_surrogate_logits(zz, T(y, dev), ab, p, g3)
+    loss.backward()
+    assert torch.equal(zz.grad, dz)
+    assert abs(loss.item() - F) <= 1e-5 * sc[0] + 1e-7
+
+
+def test_class_sums_logits(dev):
+    from distributedauc_amd import ops
+
+    rng = np.random.default_rng(3)
+    z = torch.from_numpy(rng.normal(0, 1, (3000, 2)).astype(np.float32)).to(dev)
+    y = np.where(rng.random(3000) < 0.3, 1, -1).astype(np.int8)
+    s4 = torch.zeros(4, dtype=torch.float64, device=dev)
+    ops.class_sums_logits(z, T(y, dev), s4, accumulate=False)
+    h = torch.softmax(z.double(), 1)[:, 1].cpu().numpy()
+    ref = [h[y == -1].sum(), (y == -1).sum(), h[y == 1].sum(), (y == 1).sum()]
+    assert np.allclose(s4.cpu().numpy(), ref, rtol=1e-6)
