@@ -77,8 +77,10 @@ class ResNet(nn.Module):
     """Stem (7x7/2 conv, BN, ReLU, 3x3/2 max-pool) -> 4 stages -> avg-pool -> fc -> softmax."""
 
     def __init__(self, block, layers, num_classes: int = 2, groups: int = 1, width_per_group: int = 64,
-                 zero_init_residual: bool = False):
+                 zero_init_residual: bool = False, head: str = "softmax"):
         super().__init__()
+        if head not in ("softmax", "logits"):
+            raise ValueError("head must be 'softmax' or 'logits'")
         self.groups = groups
         self.base_width = width_per_group
         self.inplanes = 64
@@ -92,7 +94,8 @@ class ResNet(nn.Module):
         self.layer4 = self._stage(block, 512, layers[3], 2)
         self.avgpool = nn.AdaptiveAvgPool2d((1, 1))
         self.fc = nn.Linear(512 * block.expansion, num_classes)
-        self.softmax = nn.Softmax(dim=1)
+        # "logits": the surrogate kernel applies the softmax column itself
+        self.softmax = nn.Softmax(dim=1) if head == "softmax" else nn.Identity()
         for m in self.modules():
             if isinstance(m, nn.Conv2d):
                 nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")

@@ -63,6 +63,7 @@ class CoDA:
         self.T = 0
         self.lr = self.lr0
         self.end_all = False
+        self.t_in_stage = 0
         self._sums4 = torch.zeros(4, dtype=torch.float64, device=self.device)
         self._scratch = torch.zeros(8, dtype=torch.float32, device=self.device)
         self._ab_stage = torch.zeros(2, dtype=torch.float32, device=self.device)
@@ -155,18 +156,29 @@ class CoDA:
     # ---------------------------------------------------------------- loop
     def run(self, batches: Iterator, *, num_stages: int, total_iter: int, test_freq: int | None = None,
             evaluate: Callable[["CoDA"], None] | None = None,
-            on_step: Callable[["CoDA"], None] | None = None):
+            on_step: Callable[["CoDA"], None] | None = None,
+            checkpoint_every: int | None = None, checkpoint_path: str | None = None):
         """The full schedule of main.py:140-339 (stages 1 .. num_stages-1).
 
         ``on_step`` (optional) is called after every training step (history, tests).
+        A CoDA restored with ``load()`` resumes at the saved stage and step (the caller
+        resumes its batch stream); ``checkpoint_every`` saves every that many steps.
         """
-        with torch.no_grad():
-            self.average_all()  # main.py:141-142
-        for s in range(1, num_stages):
+        resuming = self.stage > 0
+        if not resuming:
+            with torch.no_grad():
+                self.average_all()  # main.py:141-142
+        first = self.stage if resuming else 1
+        for s in range(first, num_stages):
             if self.end_all:
                 break
-            self.begin_stage(s, batches)
-            for _ in range(self.T):
+            if resuming and s == first:
+                start = self.t_in_stage
+            else:
+                self.begin_stage(s, batches)
+                start = 0
+            for t in range(start, self.T):
+                self.t_in_stage = t
                 if test_freq and evaluate is not None and self.t_total % test_freq == 0:
                     evaluate(self)  # main.py:215-270
                 if self.t_total > total_iter:  # main.py:273-275
@@ -174,9 +186,56 @@ class CoDA:
                     break
                 x, labels = next(batches)
                 self.train_step(x, labels)
+                self.t_in_stage = t + 1
                 if on_step is not None:
                     on_step(self)
+                if checkpoint_every and checkpoint_path and self.t_total % checkpoint_every == 0:
+                    self.save(checkpoint_path)
             self.end_stage()
+            self.t_in_stage = self.T
+
+    # ---------------------------------------------------------------- checkpoint / resume
+    def state_dict(self) -> dict:
+        """Everything a resumed run needs (the reference has no checkpointing)."""
+        st = self.state
+        return {
+            "flat": st.flat.detach().clone(), "anchor": st.anchor.clone(), "avg": st.avg.clone(),
+            "gcounts": st.gcounts.clone(), "p_hat": st.p_hat.clone(), "ab_stage": self._ab_stage.clone(),
+            "buffers": {n: b.detach().clone() for n, b in self.model.named_buffers()},
+            "counters": torch.tensor([self.t_total, self.stage, self.T, self.t_in_stage, int(self.end_all)],
+                                     dtype=torch.int64),
+            "lr": torch.tensor([self.lr], dtype=torch.float64),
+            "layout": torch.tensor([e[2] for e in st.entries] + [st.n_params], dtype=torch.int64),
+        }
+
+    def load_state_dict(self, sd: dict) -> None:
+        st = self.state
+        layout = torch.tensor([e[2] for e in st.entries] + [st.n_params], dtype=torch.int64)
+        if not torch.equal(sd["layout"].cpu(), layout):
+            raise ValueError("checkpoint was written for a different model layout")
+        with torch.no_grad():
+            st.flat.copy_(sd["flat"])
+            st.anchor.copy_(sd["anchor"])
+            st.avg.copy_(sd["avg"])
+            st.gcounts.copy_(sd["gcounts"])
+            st.p_hat.copy_(sd["p_hat"])
+            self._ab_stage.copy_(sd["ab_stage"])
+            bufs = dict(self.model.named_buffers())
+            for n, b in sd["buffers"].items():
+                bufs[n].copy_(b)
+        self.t_total, self.stage, self.T, self.t_in_stage, end_all = (int(v) for v in sd["counters"].tolist())
+        self.end_all = bool(end_all)
+        self.lr = float(sd["lr"][0])
+
+    def save(self, path: str) -> None:
+        import os
+
+        tmp = f"{path}.tmp"
+        torch.save(self.state_dict(), tmp)
+        os.replace(tmp, path)
+
+    def load(self, path: str) -> None:
+        self.load_state_dict(torch.load(path, map_location=self.device, weights_only=True))
 
     def stage_lengths(self, num_stages: int) -> list[int]:
         return [self.T0 * 3 ** (s - 1) for s in range(1, num_stages)]

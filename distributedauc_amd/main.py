@@ -197,12 +197,13 @@ def train(rank: int, size: int, group=None, para=None):
     train_part = partition.use(rank + 1)
     train_loader = DeviceLoader(dataset, train_part.index, para.local_batchsize, device, seed=para.seed + rank,
                                 channels_last=para.channels_last)
-    net = build_backbone(para.arch, num_classes=2).to(device)
+    head = getattr(para, "head", "softmax")
+    net = build_backbone(para.arch, num_classes=2, head=head).to(device)
     if para.channels_last:
         net = net.to(memory_format=torch.channels_last)
     coda = CoDA(net, lr=para.lr, gamma=para.gamma, T0=para.T0, I=para.I, split_index=para.split_index,
                 mode=para.mode, world=size, rank=rank, group=group,
-                autocast_dtype=torch.bfloat16 if para.bf16 else None, device=device)
+                autocast_dtype=torch.bfloat16 if para.bf16 else None, device=device, head=head)
     evaluate = None
     if len(test_part) > 0:
         test_loader = DeviceLoader(dataset, test_part.index, para.test_batchsize, device, seed=para.seed + 999,

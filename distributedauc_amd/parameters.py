@@ -45,6 +45,9 @@ def get_parser() -> argparse.ArgumentParser:
     p.add_argument("--bf16", action=argparse.BooleanOptionalAction, default=True,
                    help="bf16 autocast for the backbone (fp32 master weights and fp32 AUC kernels)")
     p.add_argument("--channels_last", action=argparse.BooleanOptionalAction, default=True)
+    p.add_argument("--head", choices=["softmax", "logits"], default="softmax",
+                   help="softmax: the model ends in Softmax like resnet.py:159; logits: the softmax column is "
+                        "folded into the fused surrogate kernel")
     p.add_argument("--seed", type=int, default=1234)
     p.add_argument("--history_dir", type=str, default="history")
     p.add_argument("--backend", type=str, default=None, help="torch.distributed backend (default nccl=RCCL)")

@@ -38,6 +38,62 @@ def test_coda_round_world1_fused_softmax_head(dev, golden):
     coda_parity.compare(fx, 0, rec)
 
 
+def test_checkpoint_resume_bitwise(dev, golden, tmp_path):
+    """Stop after step 5 (mid stage 2), save, restore into a fresh CoDA, finish: identical to one run."""
+    import json as _json
+
+    import tinynet
+    from distributedauc_amd.coda import CoDA
+
+    fx = _load(golden, 1)
+    cfg = _json.loads(str(fx["config"]))
+    xs, ys = fx["r0_x"], fx["r0_y"]
+
+    def make():
+        net = tinynet.TinyNet()
+        net.load_state_dict({k[5:]: torch.from_numpy(v) for k, v in fx.items() if k.startswith("init_")})
+        return CoDA(net.to(dev), lr=cfg["lr"], gamma=cfg["gamma"], T0=cfg["T0"], I=cfg["I"],
+                    split_index=cfg["split_index"], device=dev)
+
+    def stream(start=0):
+        for k in range(start, len(xs)):
+            yield torch.from_numpy(xs[k]).to(dev), torch.from_numpy(ys[k]).to(dev)
+
+    full = make()
+    full.run(stream(), num_stages=cfg["numStages"], total_iter=cfg["total_iter"])
+
+    class Stop(Exception):
+        pass
+
+    used = {"n": 0}
+
+    def counting(it):
+        for b in it:
+            used["n"] += 1
+            yield b
+
+    part = make()
+    ck = str(tmp_path / "coda.pt")
+
+    def stop_at(c):
+        if c.t_total == 5:
+            c.save(ck)
+            raise Stop
+
+    try:
+        part.run(counting(stream()), num_stages=cfg["numStages"], total_iter=cfg["total_iter"], on_step=stop_at)
+    except Stop:
+        pass
+    resumed = make()
+    resumed.load(ck)
+    assert resumed.t_total == 5 and resumed.stage == 2
+    resumed.run(stream(used["n"]), num_stages=cfg["numStages"], total_iter=cfg["total_iter"])
+    assert torch.equal(resumed.state.flat, full.state.flat)
+    assert torch.equal(resumed.state.avg, full.state.avg)
+    assert torch.equal(resumed.state.gcounts, full.state.gcounts)
+    assert resumed.t_total == full.t_total
+
+
 def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
