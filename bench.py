@@ -53,11 +53,14 @@ def parse():
     p.add_argument("--auc-log2n", type=int, default=24)
     p.add_argument("--auc-pos", type=float, default=0.01)
     p.add_argument("--auc-reps", type=int, default=3)
+    p.add_argument("--sur-log2b", type=int, default=26, help="surrogate kernel leg: batch of 2^k scores")
+    p.add_argument("--sur-reps", type=int, default=20)
     p.add_argument("--variant", type=int, default=0, help="pair-count kernel variant")
     p.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL; gloo for rehearsals)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-auc", action="store_true")
     p.add_argument("--no-train", action="store_true")
+    p.add_argument("--no-surrogate", action="store_true")
     return p.parse_args()
 
 
@@ -200,6 +203,40 @@ def bench_auc(args, world, rank, device):
     return out
 
 
+def bench_surrogate(args, device):
+    """The fused loss kernel at a streaming size (9 B/element = fp32 h + int8 y + fp32 dh).
+
+    Training batches (B = 256) are launch-latency bound; this leg measures the same kernel where
+    HBM bounds it. Inputs resident in HBM; HIP events on the launch stream around every call."""
+    from distributedauc_amd import _lib, ops
+
+    B = 1 << args.sur_log2b
+    g = torch.Generator(device=device).manual_seed(7)
+    h = torch.rand(B, device=device, generator=g)
+    y = torch.where(torch.rand(B, device=device, generator=g) < args.pos_ratio, 1, -1).to(torch.int8)
+    abalpha = torch.tensor([0.1, -0.2, 0.3], device=device)
+    p_hat = torch.tensor([args.pos_ratio], device=device)
+    dh = torch.empty(B, device=device)
+    grad3 = torch.empty(3, device=device)
+    out64 = torch.zeros(6, dtype=torch.float64, device=device)
+    for _ in range(3):
+        ops.surrogate_fwdbwd(h, y, abalpha, p_hat, dh=dh, grad3=grad3, out64=out64)
+    kt = KernelTimer(_lib.load(), "dauc_surrogate_fwdbwd")
+    kt.enabled = True
+    for _ in range(args.sur_reps):
+        ops.surrogate_fwdbwd(h, y, abalpha, p_hat, dh=dh, grad3=grad3, out64=out64)
+    kt.enabled = False
+    kt.restore()
+    ms = kt.mean_ms()
+    nbytes = 9 * B
+    gbs = nbytes / (ms / 1e3) / 1e9
+    return {"workload": f"fused surrogate fwd+bwd, B = 2^{args.sur_log2b} fp32 scores, int8 labels, p = {args.pos_ratio}",
+            "B": B, "avg_launch_us": ms * 1e3, "loss": float(out64[0].item()),
+            "roofline": {"kernel": "dauc_surrogate_fwdbwd", "bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS, "traffic": load_traffic(f"surrogate_2^{args.sur_log2b}"),
+                         "bytes_per_launch": nbytes}}
+
+
 def cpu_baseline_train(args):
     """The reference's CPU path on a bounded sample: torch-CPU ResNet-50 fwd, verbatim loss
     (main.py:313-317), autograd, per-tensor dppd_sg (main.py:56-64) + running average."""
@@ -269,6 +306,7 @@ def main():
 
     res = bench_train(args, world, rank, device) if not args.no_train else None
     auc = bench_auc(args, world, rank, device) if not args.no_auc else None
+    sur = bench_surrogate(args, device) if (not args.no_surrogate and rank == 0) else None
 
     if rank == 0:
         out = {"metric": METRIC}
@@ -289,6 +327,8 @@ def main():
                 "surrogate_us_per_call": res["surrogate_us"],
                 "final_loss": res["loss"],
             })
+        if sur is not None:
+            out["surrogate_kernel"] = sur
         if auc is not None:
             pk, sk = auc["m_pairs"], auc["m_sort"]
             npairs = auc["npairs"]

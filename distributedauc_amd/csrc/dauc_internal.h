@@ -60,26 +60,40 @@ __device__ __forceinline__ void block_sum(double (&v)[K], double* scratch) {
 }
 
 // ---- inter-workgroup "last arriver" ticket ------------------------------------
-// Producer side of the agent-scope release/acquire hand-off (cdna_hip_programming
-// §6 Guideline 16): the calling block has stored its partial with plain stores
-// from thread 0 only. Returns true in every thread of the block that arrived last;
-// that block may then read every other block's partial with plain loads.
+// The write-through form of the agent-scope hand-off (cdna_hip_programming §6
+// Guideline 16, R1): the payload (one workgroup's fp64 partial row) is stored by
+// thread 0 with sc1 (write-through, agent-scope atomic) stores, drained with
+// s_waitcnt vmcnt(0), and signalled by a relaxed agent-scope ticket add. The last
+// arriver reads every row with sc1 loads (load_sc1), so neither a release fence
+// (an L2 write-back that every workgroup would pay behind its streamed stores) nor
+// an acquire is needed. Tickets start at zero and the last arriver resets them.
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+typedef __attribute__((address_space(1))) unsigned gu32;
+
+__device__ __forceinline__ void store_sc1(double* p, double v) {
+    __hip_atomic_store((gu64*)p, static_cast<unsigned long long>(__double_as_longlong(v)), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ double load_sc1(const double* p) {
+    return __longlong_as_double(static_cast<long long>(
+        __hip_atomic_load((gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
+}
+
+// Called by every thread of the block after thread 0 stored its row with store_sc1.
+// Returns true in every thread of the block that arrived last.
 __device__ __forceinline__ bool arrive_last(unsigned* counter, unsigned nblocks, int* lds_flag) {
     if (threadIdx.x == 0) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        unsigned t = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        int last = (t == nblocks - 1);
-        if (last) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            // leave the workspace zeroed for the next call on this stream
-            __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+        const unsigned t = __hip_atomic_fetch_add((gu32*)counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int last = (t == nblocks - 1);
+        // leave the workspace zeroed for the next call on this stream
+        if (last) __hip_atomic_store((gu32*)counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         *lds_flag = last;
     }
     __syncthreads();
+    // no instruction: keeps the compiler from hoisting the sc1 row loads above the ticket
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     return *lds_flag != 0;
 }
 

@@ -209,7 +209,7 @@ __device__ __forceinline__ void reduce_and_finalize(const Acc& acc, const Surrog
 
     if (threadIdx.x == 0) {
 #pragma unroll
-        for (int k = 0; k < kNumAcc; ++k) partials[blockIdx.x * kNumAcc + k] = tot[k];
+        for (int k = 0; k < kNumAcc; ++k) store_sc1(&partials[blockIdx.x * kNumAcc + k], tot[k]);
     }
     if (!arrive_last(counter, gridDim.x, &last_flag)) return;
 
@@ -218,7 +218,7 @@ __device__ __forceinline__ void reduce_and_finalize(const Acc& acc, const Surrog
     for (int k = 0; k < kNumAcc; ++k) tot[k] = 0.0;
     for (int b = threadIdx.x; b < static_cast<int>(gridDim.x); b += kThreads) {
 #pragma unroll
-        for (int k = 0; k < kNumAcc; ++k) tot[k] += partials[b * kNumAcc + k];
+        for (int k = 0; k < kNumAcc; ++k) tot[k] += load_sc1(&partials[b * kNumAcc + k]);
     }
     block_sum<kNumAcc>(tot, scratch);
     if (threadIdx.x == 0) {
@@ -342,6 +342,145 @@ __global__ __launch_bounds__(kThreads) void surrogate_kernel(
     reduce_and_finalize<CLASS_ONLY>(acc, s, invB, partials, counter, out64, grad3, loss, sums4, accumulate);
 }
 
+// ---- large unit-stride batches: one chunk per workgroup + a two-level ticket ----------
+//
+// A grid-stride (persistent) loop keeps only 2 workgroups per CU busy and walks the
+// whole batch with a large stride, so concurrently open DRAM pages are far apart. Here
+// every workgroup takes ONE contiguous chunk of 256 x 4 x S elements (the dispatcher
+// hands chunks out in address order, like the update kernel's one-shot grid), issues
+// all of its loads before any math, and writes one fp64 partial row. The partials are
+// then reduced deterministically: the last arriver of each group of kGroup workgroups
+// sums its group's rows in a fixed order, and the last group reducer sums the group rows.
+constexpr int kGroup = 256;               // workgroups per first-level reduction group
+constexpr int kMaxGroups = 4096;          // ticket slots: up to 2^20 workgroups per launch
+constexpr size_t kTicketStride = 16;      // bytes between tickets
+
+struct ChunkWs {
+    unsigned* top;        // ticket of the group reducers
+    unsigned* group;      // one ticket per group (kTicketStride apart)
+    double* partials;     // [nblocks][kNumAcc]
+    double* gpartials;    // [ngroups][kNumAcc]
+};
+
+__host__ __device__ constexpr int64_t chunk_elems(int S) { return int64_t(kThreads) * kVec * S; }
+
+inline int64_t chunk_groups(int64_t nblocks) { return (nblocks + kGroup - 1) / kGroup; }
+
+// Workspace layout: [persistent kernel: ticket + kMaxBlocks rows][chunk tickets: top +
+// kMaxGroups][chunk rows][group rows]. Tickets must stay zero between calls, so they
+// sit at a fixed place that no row of any kernel geometry or batch size ever covers.
+constexpr size_t kPersistentBytes = kCounterBytes + size_t(kMaxBlocks) * kNumAcc * sizeof(double);
+constexpr size_t kChunkTicketBytes = kTicketStride * (1 + kMaxGroups);
+
+inline size_t chunk_ws_bytes(int64_t nblocks) {
+    const int64_t ng = chunk_groups(nblocks);
+    return kPersistentBytes + kChunkTicketBytes + static_cast<size_t>(nblocks + ng) * kNumAcc * sizeof(double);
+}
+
+inline ChunkWs chunk_ws(void* ws, int64_t nblocks) {
+    char* base = static_cast<char*>(ws) + kPersistentBytes;
+    ChunkWs w;
+    w.top = reinterpret_cast<unsigned*>(base);
+    w.group = reinterpret_cast<unsigned*>(base + kTicketStride);
+    w.partials = reinterpret_cast<double*>(base + kChunkTicketBytes);
+    w.gpartials = w.partials + nblocks * kNumAcc;
+    return w;
+}
+
+template <typename YT, bool CLASS_ONLY, int S, bool NT_LOAD, bool NT_STORE>
+__global__ __launch_bounds__(kThreads) void surrogate_chunk_kernel(
+    const float* __restrict__ h, const YT* __restrict__ y, int64_t B, double invB,
+    const float* __restrict__ abalpha, const float* __restrict__ p_hat, float* __restrict__ dh,
+    ChunkWs ws, double* __restrict__ out64, float* __restrict__ grad3, float* __restrict__ loss,
+    double* __restrict__ sums4, int accumulate) {
+    SurrogateScalars s;
+    if (CLASS_ONLY) s = SurrogateScalars{};
+    else s = make_scalars(abalpha, p_hat, invB);
+    Acc acc;
+    const bool write_dh = !CLASS_ONLY && dh != nullptr;
+    const int64_t nblocks = gridDim.x;
+    const int64_t base = int64_t(blockIdx.x) * chunk_elems(S);
+
+    if (base + chunk_elems(S) <= B) {
+        f32x4 hv[S];
+        int yv[S][4];
+#pragma unroll
+        for (int k = 0; k < S; ++k) {
+            const int64_t b = base + (int64_t(k) * kThreads + threadIdx.x) * kVec;
+            if (NT_LOAD) hv[k] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(h + b));
+            else hv[k] = *reinterpret_cast<const f32x4*>(h + b);
+            load_labels4(y, b, yv[k]);
+        }
+#pragma unroll
+        for (int k = 0; k < S; ++k) {
+            const f32x4 g = visit4<CLASS_ONLY>(hv[k], yv[k], s, acc);
+            if (write_dh) {
+                f32x4* dst = reinterpret_cast<f32x4*>(dh + base + (int64_t(k) * kThreads + threadIdx.x) * kVec);
+                if (NT_STORE) __builtin_nontemporal_store(g, dst);
+                else *dst = g;
+            }
+        }
+    } else {
+        // the ragged last chunk: one element per thread per step
+        for (int64_t i = base + threadIdx.x; i < B; i += kThreads) {
+            const float g = visit1<CLASS_ONLY>(h[i], load_label(y, i), s, acc);
+            if (write_dh) dh[i] = g;
+        }
+    }
+
+    __shared__ double scratch[kNumAcc * (kThreads / kWave)];
+    __shared__ int last_flag;
+    double tot[kNumAcc] = {acc.s_pos, acc.s_neg, acc.q_pos, acc.q_neg,
+                           static_cast<double>(acc.n_pos), static_cast<double>(acc.n_neg)};
+    block_sum<kNumAcc>(tot, scratch);
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int k = 0; k < kNumAcc; ++k) store_sc1(&ws.partials[blockIdx.x * kNumAcc + k], tot[k]);
+    }
+    // level 1: the last workgroup of the group reduces the group's rows in order
+    const int64_t grp = blockIdx.x / kGroup;
+    const int64_t g0 = grp * kGroup;
+    const int64_t gn = (nblocks - g0) < kGroup ? (nblocks - g0) : kGroup;
+    unsigned* gticket = reinterpret_cast<unsigned*>(reinterpret_cast<char*>(ws.group) + grp * kTicketStride);
+    if (!arrive_last(gticket, static_cast<unsigned>(gn), &last_flag)) return;
+#pragma unroll
+    for (int k = 0; k < kNumAcc; ++k) tot[k] = 0.0;
+    for (int64_t b = g0 + threadIdx.x; b < g0 + gn; b += kThreads) {
+#pragma unroll
+        for (int k = 0; k < kNumAcc; ++k) tot[k] += load_sc1(&ws.partials[b * kNumAcc + k]);
+    }
+    block_sum<kNumAcc>(tot, scratch);
+    const int64_t ngroups = (nblocks + kGroup - 1) / kGroup;
+    if (ngroups > 1) {
+        if (threadIdx.x == 0) {
+#pragma unroll
+            for (int k = 0; k < kNumAcc; ++k) store_sc1(&ws.gpartials[grp * kNumAcc + k], tot[k]);
+        }
+        // level 2: the last group reducer sums the group rows in order
+        if (!arrive_last(ws.top, static_cast<unsigned>(ngroups), &last_flag)) return;
+#pragma unroll
+        for (int k = 0; k < kNumAcc; ++k) tot[k] = 0.0;
+        for (int64_t g = threadIdx.x; g < ngroups; g += kThreads) {
+#pragma unroll
+            for (int k = 0; k < kNumAcc; ++k) tot[k] += load_sc1(&ws.gpartials[g * kNumAcc + k]);
+        }
+        block_sum<kNumAcc>(tot, scratch);
+    }
+    if (threadIdx.x == 0) {
+        if (CLASS_ONLY) emit_class_sums(tot, sums4, accumulate);
+        else finalize(tot, s, invB, out64, grad3, loss);
+    }
+}
+
+// Default chunk geometry (variant sweep: scripts/micro_kernels.py --which surrogate).
+#ifndef DAUC_SURROGATE_CHUNK_SLOTS
+#define DAUC_SURROGATE_CHUNK_SLOTS 8
+#endif
+constexpr int kChunkSlots = DAUC_SURROGATE_CHUNK_SLOTS;
+// Unit-stride batches at least this large take the chunked kernel; smaller ones are
+// latency-bound and stay on the single-ticket persistent kernel.
+constexpr int64_t kChunkMinB = int64_t(1) << 20;
+
 int resident_blocks() {
     static int cached = 0;
     if (cached == 0) {
@@ -364,22 +503,56 @@ int resident_blocks() {
 
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
+template <typename YT, bool CLASS_ONLY, int S, bool NTL, bool NTS>
+int launch_chunk(const float* h, const YT* y, int64_t B, const float* abalpha, const float* p_hat, float* dh,
+                 double* out64, float* grad3, float* loss, double* sums4, int accumulate, void* ws,
+                 size_t ws_bytes, hipStream_t st) {
+    const int64_t nblocks = (B + chunk_elems(S) - 1) / chunk_elems(S);
+    if (chunk_groups(nblocks) > kMaxGroups) return DAUC_EINVAL;
+    if (ws == nullptr || ws_bytes < chunk_ws_bytes(nblocks)) return DAUC_EINVAL;
+    hipLaunchKernelGGL((surrogate_chunk_kernel<YT, CLASS_ONLY, S, NTL, NTS>), dim3(static_cast<unsigned>(nblocks)),
+                       dim3(kThreads), 0, st, h, y, B, 1.0 / static_cast<double>(B), abalpha, p_hat, dh,
+                       chunk_ws(ws, nblocks), out64, grad3, loss, sums4, accumulate);
+    return launch_status();
+}
+
+// variant: 0 = default dispatch, 1 = persistent kernel, 2..7 = chunk kernel geometries
+// (tuning; only for int8 labels with a loss, i.e. the micro-benchmark's configuration).
 template <bool CLASS_ONLY, typename YT>
 int launch_surrogate(const float* h, int64_t hs, const YT* y, int64_t B, const float* abalpha,
                      const float* p_hat, float* dh, int64_t dhs, double* out64, float* grad3,
                      float* loss, double* sums4, int accumulate, void* ws, size_t ws_bytes,
-                     hipStream_t st) {
+                     hipStream_t st, int variant = 0) {
+    const bool unit = hs == 1 && aligned16(h) &&
+                      (reinterpret_cast<uintptr_t>(y) % (kVec * sizeof(YT))) == 0 &&
+                      (CLASS_ONLY || dh == nullptr || (dhs == 1 && aligned16(dh)));
+    if (unit && variant >= 2) {
+        if constexpr (!CLASS_ONLY && sizeof(YT) == 1) {
+            switch (variant) {
+                case 2: return launch_chunk<YT, false, 4, true, true>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, sums4, accumulate, ws, ws_bytes, st);
+                case 3: return launch_chunk<YT, false, 8, true, true>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, sums4, accumulate, ws, ws_bytes, st);
+                case 4: return launch_chunk<YT, false, 16, true, true>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, sums4, accumulate, ws, ws_bytes, st);
+                case 5: return launch_chunk<YT, false, 8, false, true>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, sums4, accumulate, ws, ws_bytes, st);
+                case 6: return launch_chunk<YT, false, 8, true, false>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, sums4, accumulate, ws, ws_bytes, st);
+                case 7: return launch_chunk<YT, false, 2, true, true>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, sums4, accumulate, ws, ws_bytes, st);
+                default: return DAUC_EINVAL;
+            }
+        }
+        return DAUC_EINVAL;
+    }
+    if (unit && variant == 0 && B >= kChunkMinB &&
+        chunk_groups((B + chunk_elems(kChunkSlots) - 1) / chunk_elems(kChunkSlots)) <= kMaxGroups)
+        return launch_chunk<YT, CLASS_ONLY, kChunkSlots, true, true>(h, y, B, abalpha, p_hat, dh, out64, grad3,
+                                                                      loss, sums4, accumulate, ws, ws_bytes, st);
     const int grid = grid_for(B);
     unsigned* counter = nullptr;
     double* partials = nullptr;
     if (grid > 1) {
-        if (ws == nullptr || ws_bytes < dauc_surrogate_workspace_size(B)) return DAUC_EINVAL;
+        if (ws == nullptr || ws_bytes < kCounterBytes + static_cast<size_t>(grid) * kNumAcc * sizeof(double))
+            return DAUC_EINVAL;
         counter = static_cast<unsigned*>(ws);
         partials = reinterpret_cast<double*>(static_cast<char*>(ws) + kCounterBytes);
     }
-    const bool unit = hs == 1 && aligned16(h) &&
-                      (reinterpret_cast<uintptr_t>(y) % (kVec * sizeof(YT))) == 0 &&
-                      (CLASS_ONLY || dh == nullptr || (dhs == 1 && aligned16(dh)));
     if (unit) {
         hipLaunchKernelGGL((surrogate_kernel<YT, CLASS_ONLY, true>), dim3(grid), dim3(kThreads), 0,
                            st, h, hs, y, B, 1.0 / static_cast<double>(B), abalpha, p_hat, dh, dhs,
@@ -396,12 +569,13 @@ template <bool CLASS_ONLY>
 int dispatch_labels(const float* h, int64_t hs, const void* y, int yt, int64_t B,
                     const float* abalpha, const float* p_hat, float* dh, int64_t dhs,
                     double* out64, float* grad3, float* loss, double* sums4, int accumulate,
-                    void* ws, size_t ws_bytes, hipStream_t st) {
+                    void* ws, size_t ws_bytes, hipStream_t st, int variant = 0) {
+    if (variant != 0 && yt != DAUC_LABEL_I8) return DAUC_EINVAL;
     switch (yt) {
         case DAUC_LABEL_I8:
             return launch_surrogate<CLASS_ONLY>(h, hs, static_cast<const int8_t*>(y), B, abalpha,
                                                 p_hat, dh, dhs, out64, grad3, loss, sums4,
-                                                accumulate, ws, ws_bytes, st);
+                                                accumulate, ws, ws_bytes, st, variant);
         case DAUC_LABEL_I32:
             return launch_surrogate<CLASS_ONLY>(h, hs, static_cast<const int32_t*>(y), B, abalpha,
                                                 p_hat, dh, dhs, out64, grad3, loss, sums4,
@@ -521,8 +695,12 @@ using namespace dauc;
 extern "C" {
 
 size_t dauc_surrogate_workspace_size(int64_t B) {
-    const int g = grid_scalar(B < 0 ? 0 : B);  // >= grid_for(B): covers every surrogate kernel
-    return kCounterBytes + static_cast<size_t>(g) * kNumAcc * sizeof(double);
+    if (B < 0) B = 0;
+    const int g = grid_scalar(B);  // >= grid_for(B): covers the persistent kernels
+    const size_t persistent = kCounterBytes + static_cast<size_t>(g) * kNumAcc * sizeof(double);
+    // the chunk kernels (smallest chunk of any variant: S = 2)
+    const size_t chunked = chunk_ws_bytes((B + chunk_elems(2) - 1) / chunk_elems(2));
+    return persistent > chunked ? persistent : chunked;
 }
 
 int dauc_surrogate_fwdbwd(const float* h, int64_t h_stride, const void* y, int y_dtype, int64_t B,
@@ -535,6 +713,18 @@ int dauc_surrogate_fwdbwd(const float* h, int64_t h_stride, const void* y, int y
     return dispatch_labels<false>(h, h_stride, y, y_dtype, B, abalpha, p_hat, dh, dh_stride, out64,
                                   grad3, loss, nullptr, 0, workspace, workspace_bytes,
                                   as_hip(stream));
+}
+
+int dauc_surrogate_fwdbwd_variant(const float* h, int64_t h_stride, const void* y, int y_dtype, int64_t B,
+                                  const float* abalpha, const float* p_hat, float* dh, int64_t dh_stride,
+                                  double* out64, float* grad3, float* loss, void* workspace,
+                                  size_t workspace_bytes, int variant, dauc_stream_t stream) {
+    if (B <= 0 || h == nullptr || y == nullptr || abalpha == nullptr || p_hat == nullptr ||
+        h_stride <= 0 || (dh != nullptr && dh_stride <= 0) || variant < 0 || variant > 7)
+        return DAUC_EINVAL;
+    return dispatch_labels<false>(h, h_stride, y, y_dtype, B, abalpha, p_hat, dh, dh_stride, out64,
+                                  grad3, loss, nullptr, 0, workspace, workspace_bytes,
+                                  as_hip(stream), variant);
 }
 
 int dauc_class_sums(const float* h, int64_t h_stride, const void* y, int y_dtype, int64_t B,

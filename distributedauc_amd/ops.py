@@ -117,8 +117,11 @@ def label_map_phat(labels: torch.Tensor, split_index: int, y_out: torch.Tensor, 
 # ----------------------------------------------------------------- a2/a3
 def surrogate_fwdbwd(h: torch.Tensor, y: torch.Tensor, abalpha: torch.Tensor, p_hat: torch.Tensor, *,
                      dh: torch.Tensor | None = None, out64: torch.Tensor | None = None,
-                     grad3: torch.Tensor | None = None, loss: torch.Tensor | None = None) -> None:
-    """Fused loss + gradients of main.py:313-317 (one pass over h and y)."""
+                     grad3: torch.Tensor | None = None, loss: torch.Tensor | None = None,
+                     variant: int = 0) -> None:
+    """Fused loss + gradients of main.py:313-317 (one pass over h and y).
+
+    ``variant`` != 0 forces a kernel geometry (tuning; see dauc_surrogate_fwdbwd_variant)."""
     B = _check_vec(h, y)
     dev = h.device
     yc = _label_code(y)
@@ -145,10 +148,15 @@ def surrogate_fwdbwd(h: torch.Tensor, y: torch.Tensor, abalpha: torch.Tensor, p_
     L = _lib.load()
     nbytes = L.dauc_surrogate_workspace_size(B)
     ws = workspaces.get(dev, "surrogate", nbytes)
-    check(L.dauc_surrogate_fwdbwd(_ptr(h), h.stride(0), _ptr(y), yc, B, _ptr(abalpha), _ptr(p_hat),
-                                  _ptr(dh), dh_stride, _ptr(out64), _ptr(grad3), _ptr(loss), _ptr(ws),
-                                  ws.numel(), _stream(dev)),
-          "dauc_surrogate_fwdbwd")
+    if variant == 0:
+        rc = L.dauc_surrogate_fwdbwd(_ptr(h), h.stride(0), _ptr(y), yc, B, _ptr(abalpha), _ptr(p_hat),
+                                     _ptr(dh), dh_stride, _ptr(out64), _ptr(grad3), _ptr(loss), _ptr(ws),
+                                     ws.numel(), _stream(dev))
+    else:
+        rc = L.dauc_surrogate_fwdbwd_variant(_ptr(h), h.stride(0), _ptr(y), yc, B, _ptr(abalpha), _ptr(p_hat),
+                                             _ptr(dh), dh_stride, _ptr(out64), _ptr(grad3), _ptr(loss), _ptr(ws),
+                                             ws.numel(), int(variant), _stream(dev))
+    check(rc, "dauc_surrogate_fwdbwd")
 
 
 def class_sums(h: torch.Tensor, y: torch.Tensor, sums4: torch.Tensor, accumulate: bool = True) -> None:

@@ -99,6 +99,20 @@ int dauc_surrogate_fwdbwd(const float* h, int64_t h_stride, const void* y, int y
                           size_t workspace_bytes, dauc_stream_t stream);
 
 /*
+ * dauc_surrogate_fwdbwd with an explicit kernel geometry, for tuning: variant 0 is the
+ * default dispatch (what dauc_surrogate_fwdbwd does), 1 forces the persistent
+ * grid-stride kernel, 2..7 force the one-chunk-per-workgroup kernel (2: 4 float4 slots
+ * per thread, 3: 8, 4: 16, all non-temporal; 5: 8 slots, plain loads; 6: 8 slots, plain
+ * stores; 7: 2 slots, non-temporal). Variants 2..7 need unit strides, 16-byte
+ * aligned h/dh and int8 labels, and B <= 2^31. Every variant returns bitwise-identical dh and counts;
+ * the fp64 sums agree to rounding (their reduction trees differ).
+ */
+int dauc_surrogate_fwdbwd_variant(const float* h, int64_t h_stride, const void* y, int y_dtype, int64_t B,
+                                  const float* abalpha, const float* p_hat, float* dh, int64_t dh_stride,
+                                  double* out64, float* grad3, float* loss, void* workspace,
+                                  size_t workspace_bytes, int variant, dauc_stream_t stream);
+
+/*
  * Replaces the stage-start alpha estimate of main.py:166-188 (per batch):
  *   sums4 (+)= { sum h[y=-1], #{y=-1}, sum h[y=1], #{y=1} }       (fp64 [4])
  * accumulate != 0 adds into sums4, otherwise overwrites it.

@@ -73,8 +73,9 @@ def bench_copy(dev, reps):
     emit(kernel="torch_copy_282MB", us=med * 1e3, GBps=8 * n2 / med / 1e6)
 
 
-def bench_surrogate(dev, reps):
-    for B in (1 << 26, 1 << 20, 256):
+def bench_surrogate(dev, reps, variants=(0,)):
+    """variant 0 = default dispatch; 1 = persistent grid-stride kernel; 2..7 = chunk geometries."""
+    for B in (1 << 26, 1 << 24, 1 << 22, 1 << 20, 256):
         g = torch.Generator(device=dev).manual_seed(1)
         h = torch.rand(B, device=dev, generator=g)
         y = torch.where(torch.rand(B, device=dev, generator=g) < 0.1, 1, -1).to(torch.int8)
@@ -82,10 +83,20 @@ def bench_surrogate(dev, reps):
         p = torch.tensor([0.1], device=dev)
         dh = torch.empty(B, device=dev)
         g3 = torch.empty(3, device=dev)
-        med, mn = timeit(lambda: ops.surrogate_fwdbwd(h, y, ab, p, dh=dh, grad3=g3), reps)
-        grid = (_lib.load().dauc_surrogate_workspace_size(B) - 256) // 48
-        emit(kernel="surrogate", B=B, us=med * 1e3, us_min=mn * 1e3, GBps=9 * B / med / 1e6, grid=grid,
-             lib=os.path.basename(str(_lib.LIB_PATH)))
+        ref = None
+        if B >= (1 << 24):
+            # practical ceilings for this access mix: torch's own streaming kernels
+            med, _ = timeit(lambda: dh.copy_(h), reps)
+            emit(kernel="ceiling_copy_f32", B=B, us=med * 1e3, GBps=8 * B / med / 1e6)
+            med, _ = timeit(lambda: torch.mul(h, y, out=dh), reps)
+            emit(kernel="ceiling_mul_f32_i8", B=B, us=med * 1e3, GBps=9 * B / med / 1e6)
+        for v in (variants if B >= 4096 else (0,)):
+            ops.surrogate_fwdbwd(h, y, ab, p, dh=dh, grad3=g3, variant=v)
+            got = dh.clone()
+            ref = got if ref is None else ref
+            med, mn = timeit(lambda: ops.surrogate_fwdbwd(h, y, ab, p, dh=dh, grad3=g3, variant=v), reps)
+            emit(kernel="surrogate", variant=v, B=B, us=med * 1e3, us_min=mn * 1e3, GBps=9 * B / med / 1e6,
+                 GBps_best=9 * B / mn / 1e6, dh_equal_v0=bool(torch.equal(got, ref)))
 
 
 def bench_paircount(dev, reps, log2n):
@@ -121,6 +132,7 @@ if __name__ == "__main__":
     ap.add_argument("--reps", type=int, default=30)
     ap.add_argument("--log2n", type=int, default=24)
     ap.add_argument("--variants", default=None, help="comma list of update variants (default: all)")
+    ap.add_argument("--sur-variants", default="0", help="comma list of surrogate variants")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     w = a.which.split(",")
@@ -129,6 +141,6 @@ if __name__ == "__main__":
     if "copy" in w:
         bench_copy(dev, a.reps)
     if "surrogate" in w:
-        bench_surrogate(dev, a.reps)
+        bench_surrogate(dev, a.reps, [int(v) for v in a.sur_variants.split(",")])
     if "paircount" in w:
         bench_paircount(dev, max(3, a.reps // 10), a.log2n)

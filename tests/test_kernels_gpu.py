@@ -125,6 +125,47 @@ def test_surrogate_large_deterministic(dev):
     assert outs[0][4] == np.sum(yn == 1)
 
 
+@pytest.mark.parametrize("B", [(1 << 20), (1 << 20) + 37, 3 * (1 << 20) + 4099])
+def test_surrogate_chunked_variants(dev, B):
+    """One-chunk-per-workgroup kernel (default for unit-stride B >= 2^20, two-level ticket)
+    and every tuning variant: fp64 closed form within 1e-6 of term scale, dh and counts
+    bitwise equal across variants (dh is per-element; the sums only differ in tree order),
+    bitwise run-to-run, ragged last chunk, and the workspace left zeroed for the next call."""
+    from distributedauc_amd import ops
+
+    g = torch.Generator(device=dev).manual_seed(B & 0xFFFF)
+    h = torch.rand(B, device=dev, generator=g)
+    y = torch.where(torch.rand(B, device=dev, generator=g) < 0.1, 1, -1).to(torch.int8)
+    y[::97] = 0  # neither class
+    abap = torch.tensor([0.1, -0.2, 0.3, 0.1], device=dev)
+    hn, yn = h.cpu().numpy(), y.cpu().numpy().astype(np.int64)
+    F, dh64, da, db, dal = R.surrogate_closed_form(hn, yn, 0.1, -0.2, 0.3, float(np.float32(0.1)))
+    sc = _scales(hn, yn, 0.1, -0.2, 0.3, float(np.float32(0.1)))
+    k = np.where(yn == 1, 0.1 + 1 + 0.3, -0.2 - 1 - 0.3)
+    c = 2.0 / B * (np.abs(hn) + np.abs(k))
+    ref_dh = None
+    for variant in (0, 0, 1, 2, 3, 4, 5, 6, 7):
+        o = torch.zeros(6, dtype=torch.float64, device=dev)
+        dh = torch.full((B,), float("nan"), device=dev)
+        ops.surrogate_fwdbwd(h, y, abap[:3], abap[3:], dh=dh, out64=o, variant=variant)
+        got, dhn = o.cpu().numpy(), dh.cpu().numpy()
+        assert np.all(np.abs(got[:4] - [F, da, db, dal]) <= 1e-6 * sc + 1e-12), (variant, got, F)
+        assert got[4] == np.sum(yn == 1) and got[5] == np.sum(yn == -1), variant
+        assert np.all(np.abs(dhn - dh64) <= 1e-6 * np.maximum(np.abs(dh64), c)), variant
+        if ref_dh is None:
+            ref_dh, ref0 = dhn, got
+        else:
+            assert np.array_equal(dhn, ref_dh), variant
+        if variant == 0:
+            assert np.array_equal(got, ref0)  # deterministic reduction order
+    sums = torch.zeros(4, dtype=torch.float64, device=dev)
+    ops.class_sums(h, y, sums, accumulate=False)  # chunked CLASS_ONLY path
+    s = sums.cpu().numpy()
+    hd = hn.astype(np.float64)
+    assert np.allclose(s, [hd[yn == -1].sum(), (yn == -1).sum(), hd[yn == 1].sum(), (yn == 1).sum()],
+                       rtol=1e-7, atol=0)
+
+
 def test_class_sums_and_alpha(dev):
     from distributedauc_amd import ops
 
