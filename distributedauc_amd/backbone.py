@@ -16,11 +16,26 @@ from __future__ import annotations
 
 import torch
 import torch.nn as nn
+import torch.nn.functional as F
 
 __all__ = [
     "ResNet", "resnet18", "resnet34", "resnet50", "resnet101", "resnet152", "resnext50_32x4d",
     "resnext101_32x8d", "wide_resnet50_2", "wide_resnet101_2", "build_backbone",
 ]
+
+
+def _bn_act(fused: bool, bn: nn.BatchNorm2d, x: torch.Tensor, relu: bool = True,
+            residual: torch.Tensor | None = None) -> torch.Tensor:
+    """relu?(bn(x) + residual?): one fused HIP node when ``fused`` and training (fused_bn.py),
+    torch's own modules otherwise (eval mode uses the running statistics)."""
+    if fused and bn.training:
+        from .fused_bn import bn_act
+
+        return bn_act(x, bn, relu, residual)
+    y = bn(x)
+    if residual is not None:
+        y = y + residual
+    return F.relu(y, inplace=True) if relu else y
 
 
 def _conv(cin: int, cout: int, k: int, stride: int = 1, groups: int = 1) -> nn.Conv2d:
@@ -40,12 +55,13 @@ class BasicBlock(nn.Module):
         self.bn2 = nn.BatchNorm2d(planes)
         self.relu = nn.ReLU(inplace=True)
         self.downsample = downsample
+        self.fused_bn = False
 
     def forward(self, x):
-        skip = x if self.downsample is None else self.downsample(x)
-        y = self.relu(self.bn1(self.conv1(x)))
-        y = self.bn2(self.conv2(y))
-        return self.relu(y + skip)
+        f = self.fused_bn
+        skip = x if self.downsample is None else _bn_act(f, self.downsample[1], self.downsample[0](x), relu=False)
+        y = _bn_act(f, self.bn1, self.conv1(x))
+        return _bn_act(f, self.bn2, self.conv2(y), residual=skip)
 
 
 class Bottleneck(nn.Module):
@@ -64,13 +80,14 @@ class Bottleneck(nn.Module):
         self.bn3 = nn.BatchNorm2d(planes * self.expansion)
         self.relu = nn.ReLU(inplace=True)
         self.downsample = downsample
+        self.fused_bn = False
 
     def forward(self, x):
-        skip = x if self.downsample is None else self.downsample(x)
-        y = self.relu(self.bn1(self.conv1(x)))
-        y = self.relu(self.bn2(self.conv2(y)))
-        y = self.bn3(self.conv3(y))
-        return self.relu(y + skip)
+        f = self.fused_bn
+        skip = x if self.downsample is None else _bn_act(f, self.downsample[1], self.downsample[0](x), relu=False)
+        y = _bn_act(f, self.bn1, self.conv1(x))
+        y = _bn_act(f, self.bn2, self.conv2(y))
+        return _bn_act(f, self.bn3, self.conv3(y), residual=skip)
 
 
 class ResNet(nn.Module):
@@ -119,8 +136,19 @@ class ResNet(nn.Module):
         mods += [block(cout, planes, 1, None, self.groups, self.base_width) for _ in range(1, blocks)]
         return nn.Sequential(*mods)
 
+    fused_bn = False
+
+    def set_fused_bn(self, enabled: bool = True) -> "ResNet":
+        """Route every training-mode bn (+ add) + relu through the fused HIP kernels (channels-last
+        bf16/fp32 on the GPU; csrc/bn_act.hip). Parameter and buffer names are unchanged."""
+        self.fused_bn = bool(enabled)
+        for m in self.modules():
+            if isinstance(m, (BasicBlock, Bottleneck)):
+                m.fused_bn = self.fused_bn
+        return self
+
     def features(self, x):
-        x = self.maxpool(self.relu(self.bn1(self.conv1(x))))
+        x = self.maxpool(_bn_act(self.fused_bn, self.bn1, self.conv1(x)))
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         return torch.flatten(self.avgpool(x), 1)
 

@@ -253,6 +253,37 @@ int dauc_auc_counts_sorted(const float* pos, int64_t P, const float* neg, int64_
 int dauc_sort_keys(const float* scores, int64_t n, unsigned* keys_out, void* workspace,
                    size_t workspace_bytes, dauc_stream_t stream);
 
+/* ------------------------------------- backbone: fused BatchNorm + add + ReLU */
+
+/*
+ * Training-mode BatchNorm over channels-last activations x [M, C] (M = N*H*W rows,
+ * C contiguous; dtype bf16 or fp32; C a power-of-two multiple of the 16-byte vector,
+ * 16-byte aligned pointers), fused with the residual add and the ReLU that follow it
+ * in the ResNet blocks (resnet.py:47-64, 87-108, 203-206):
+ *   y = relu?( (x - mean) * invstd * gamma + beta  (+ residual) )
+ * with batch mean / biased variance over M, invstd = 1/sqrt(var + eps), and the
+ * running statistics updated as torch does (unbiased variance, momentum). gamma,
+ * beta, running_* are fp32 [C] (nullable: affine off / no running stats);
+ * save_mean, save_invstd fp32 [C] receive the batch statistics for the backward.
+ * Workspace: dauc_bn_workspace_size(M, C) bytes, 16-byte aligned, no zeroing needed.
+ */
+size_t dauc_bn_workspace_size(int64_t M, int C);
+int dauc_bn_act_forward(const void* x, int dtype, int64_t M, int C, const void* residual, int relu,
+                        const float* gamma, const float* beta, float* running_mean, float* running_var,
+                        float momentum, float eps, void* y, float* save_mean, float* save_invstd, void* workspace,
+                        size_t workspace_bytes, dauc_stream_t stream);
+
+/*
+ * Backward of dauc_bn_act_forward. g = dy * [y > 0] (relu; y = the forward output) or dy.
+ *   dres (nullable) <- g: the gradient of the residual input;
+ *   dx <- gamma*invstd*(g - mean(g) - xhat*mean(g*xhat)); dgamma <- sum g*xhat; dbeta <- sum g
+ * (dgamma / dbeta fp32 [C], nullable).
+ */
+int dauc_bn_act_backward(const void* dy, const void* y, const void* x, int dtype, int64_t M, int C, int relu,
+                         const float* gamma, const float* save_mean, const float* save_invstd, void* dres, void* dx,
+                         float* dgamma, float* dbeta, void* workspace, size_t workspace_bytes,
+                         dauc_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif
