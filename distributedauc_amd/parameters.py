@@ -45,6 +45,9 @@ def get_parser() -> argparse.ArgumentParser:
     p.add_argument("--bf16", action=argparse.BooleanOptionalAction, default=True,
                    help="bf16 autocast for the backbone (fp32 master weights and fp32 AUC kernels)")
     p.add_argument("--channels_last", action=argparse.BooleanOptionalAction, default=True)
+    p.add_argument("--fused_bn", action=argparse.BooleanOptionalAction, default=True,
+                   help="training-mode BatchNorm + residual add + ReLU through the fused HIP kernels "
+                        "(needs --channels_last; csrc/bn_act.hip)")
     p.add_argument("--head", choices=["softmax", "logits"], default="softmax",
                    help="softmax: the model ends in Softmax like resnet.py:159; logits: the softmax column is "
                         "folded into the fused surrogate kernel")
