@@ -53,6 +53,8 @@ def parse():
     p.add_argument("--auc-log2n", type=int, default=24)
     p.add_argument("--auc-pos", type=float, default=0.01)
     p.add_argument("--auc-reps", type=int, default=3)
+    p.add_argument("--auc2-log2n", type=int, default=27, help="configs[4] leg (0 = off)")
+    p.add_argument("--auc2-pos", type=float, default=0.001)
     p.add_argument("--sur-log2b", type=int, default=26, help="surrogate kernel leg: batch of 2^k scores")
     p.add_argument("--sur-reps", type=int, default=20)
     p.add_argument("--variant", type=int, default=0, help="pair-count kernel variant")
@@ -167,21 +169,23 @@ def bench_train(args, world, rank, device):
     }
 
 
-def bench_auc(args, world, rank, device):
-    """configs[3]: exact AUC of 2^k scores, sharded by positive blocks; both exact methods."""
+def bench_auc(args, world, rank, device, log2n=None, pos=None, pair_reps=None):
+    """configs[3] (and [4]): exact AUC of 2^k scores, sharded by positive blocks; both exact methods."""
     from distributedauc_amd import _lib
     from distributedauc_amd.auc import ExactAUC
 
-    n = 1 << args.auc_log2n
+    log2n = args.auc_log2n if log2n is None else log2n
+    pos = args.auc_pos if pos is None else pos
+    n = 1 << log2n
     g = torch.Generator(device=device).manual_seed(2024)  # same scores on every rank
     s = torch.rand(n, generator=g, device=device)
-    y = torch.where(torch.rand(n, generator=g, device=device) < args.auc_pos, 1, -1).to(torch.int8)
-    out = {"n": n, "scores": s, "labels": y}
+    y = torch.where(torch.rand(n, generator=g, device=device) < pos, 1, -1).to(torch.int8)
+    out = {"n": n, "log2n": log2n, "pos": pos, "scores": s, "labels": y}
     for method, fn in (("sort", "dauc_auc_counts_sorted"), ("pairs", "dauc_pair_count_variant")):
         ev = ExactAUC(world=world, rank=rank, variant=args.variant, method=method)
         kt = KernelTimer(_lib.load(), fn)
         c = ev.counts(y, s)  # warm-up
-        reps = args.auc_reps if method == "pairs" else 5 * args.auc_reps
+        reps = (args.auc_reps if pair_reps is None else pair_reps) if method == "pairs" else 5 * args.auc_reps
         times = []
         kt.enabled = True
         for _ in range(reps):
@@ -202,7 +206,30 @@ def bench_auc(args, world, rank, device):
         raise RuntimeError(f"exact AUC methods disagree: {a} vs {b}")
     out.update({"P": a["P"], "N": a["N"], "wins": a["wins"], "ties": a["ties"], "auc": ExactAUC.from_counts(a),
                 "npairs": a["P"] * a["N"]})
+    if world == 1 and not args.no_cpu_baseline:
+        out["scores_host"] = (s.cpu().numpy(), y.cpu().numpy().astype(np.int64))
+    del out["scores"], out["labels"]
     return out
+
+
+def auc_record(auc, world, config_name):
+    pk, sk = auc["m_pairs"], auc["m_sort"]
+    npairs = auc["npairs"]
+    pc_rate = npairs / pk["t_count"]
+    return {
+        "workload": f"exact AUC, 2^{auc['log2n']} fp32 scores, {auc['pos']:.1%} positives "
+                    f"(BASELINE {config_name}), sharded by positive blocks, int64 all-reduce",
+        "pairs_per_sec": npairs / sk["t_eval"],
+        "method": "sort (radix sort of negatives + binary search; default evaluator)",
+        "eval_ms": sk["t_eval"] * 1e3, "sort_count_ms": sk["t_count"] * 1e3,
+        "P": auc["P"], "N": auc["N"], "wins": auc["wins"], "ties": auc["ties"], "auc": auc["auc"],
+        "methods_agree": True,
+        "pair_count_kernel": {
+            "pairs_per_sec": pc_rate, "eval_ms": pk["t_eval"] * 1e3, "count_ms": pk["t_count"] * 1e3,
+            "roofline": {"kernel": "dauc_pair_count", "bound": "valu", "achieved": pc_rate / world,
+                         "peak": VALU_PAIR_PEAK, "unit": "pairs/s per GPU",
+                         "frac": pc_rate / world / VALU_PAIR_PEAK}},
+    }
 
 
 def bench_surrogate(args, device):
@@ -275,19 +302,30 @@ def cpu_baseline_train(args):
                       f"(fwd + reference loss + backward + per-tensor dppd_sg + running average), torch CPU fp32"}
 
 
-def cpu_baseline_auc(auc_res):
-    """sklearn roc_curve + auc (main.py:79-81) on the same scores: the reference CPU path."""
+def cpu_baseline_auc(auc_res, max_log2n=None):
+    """sklearn roc_curve + auc (main.py:79-81) on the same scores: the reference CPU path.
+
+    With max_log2n, a bounded sample: the first 2^max_log2n of the scores (the rate is the sample's
+    pairs over its wall time)."""
     from oracle import reference_cpu as R
 
-    s = auc_res["scores"].cpu().numpy()
-    y = auc_res["labels"].cpu().numpy().astype(np.int64)
+    s, y = auc_res["scores_host"]
+    n = s.size
+    if max_log2n is not None and n > (1 << max_log2n):
+        s, y = s[:1 << max_log2n], y[:1 << max_log2n]
+    P = int(np.sum(y == 1))
     t0 = time.perf_counter()
     ref = R.auc_sklearn(y, s)
     dt = time.perf_counter() - t0
-    return {"value": auc_res["npairs"] / dt, "unit": "pairs/sec (effective: P*N / wall)", "cores": 1,
-            "kind": "port", "seconds": dt, "auc": ref,
-            "auc_abs_diff": abs(ref - auc_res["auc"]),
-            "sample": f"full 2^{int(np.log2(auc_res['n']))} scores, sklearn roc_curve+auc (single-threaded sort)"}
+    full = s.size == n
+    rec = {"value": P * (s.size - P) / dt, "unit": "pairs/sec (effective: P*N / wall)", "cores": 1,
+           "kind": "port", "seconds": dt, "auc": ref,
+           "sample": (f"full 2^{int(np.log2(n))} scores" if full else
+                      f"first 2^{int(np.log2(s.size))} of the 2^{int(np.log2(n))} scores") +
+                     ", sklearn roc_curve+auc (single-threaded sort)"}
+    if full:
+        rec["auc_abs_diff"] = abs(ref - auc_res["auc"])
+    return rec
 
 
 def main():
@@ -308,6 +346,9 @@ def main():
 
     res = bench_train(args, world, rank, device) if not args.no_train else None
     auc = bench_auc(args, world, rank, device) if not args.no_auc else None
+    auc2 = None
+    if not args.no_auc and args.auc2_log2n > 0:  # configs[4]: 2^27 scores at 0.1 % positives
+        auc2 = bench_auc(args, world, rank, device, args.auc2_log2n, args.auc2_pos, pair_reps=1)
     sur = bench_surrogate(args, device) if (not args.no_surrogate and rank == 0) else None
 
     if rank == 0:
@@ -333,29 +374,17 @@ def main():
         if sur is not None:
             out["surrogate_kernel"] = sur
         if auc is not None:
-            pk, sk = auc["m_pairs"], auc["m_sort"]
-            npairs = auc["npairs"]
-            pc_rate = npairs / pk["t_count"]
-            out["auc_eval"] = {
-                "workload": f"exact AUC, 2^{args.auc_log2n} fp32 scores, {args.auc_pos:.0%} positives "
-                            "(BASELINE configs[3]), sharded by positive blocks, int64 all-reduce",
-                "pairs_per_sec": npairs / sk["t_eval"],
-                "method": "sort (radix sort of negatives + binary search; default evaluator)",
-                "eval_ms": sk["t_eval"] * 1e3, "sort_count_ms": sk["t_count"] * 1e3,
-                "P": auc["P"], "N": auc["N"], "wins": auc["wins"], "ties": auc["ties"], "auc": auc["auc"],
-                "methods_agree": True,
-                "pair_count_kernel": {
-                    "pairs_per_sec": pc_rate, "eval_ms": pk["t_eval"] * 1e3, "count_ms": pk["t_count"] * 1e3,
-                    "roofline": {"kernel": "dauc_pair_count", "bound": "valu", "achieved": pc_rate / world,
-                                 "peak": VALU_PAIR_PEAK, "unit": "pairs/s per GPU",
-                                 "frac": pc_rate / world / VALU_PAIR_PEAK}},
-            }
+            out["auc_eval"] = auc_record(auc, world, "configs[3]")
+        if auc2 is not None:
+            out["auc_eval_extreme"] = auc_record(auc2, world, "configs[4]")
         if world == 1 and not args.no_cpu_baseline:
             torch.set_num_threads(min(16, os.cpu_count() or 1))
             if res is not None:
                 out["cpu_baseline"] = cpu_baseline_train(args)
             if auc is not None:
                 out.setdefault("auc_eval", {})["cpu_baseline"] = cpu_baseline_auc(auc)
+            if auc2 is not None:
+                out.setdefault("auc_eval_extreme", {})["cpu_baseline"] = cpu_baseline_auc(auc2, max_log2n=24)
         else:
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)
