@@ -64,6 +64,8 @@ def parse():
     p.add_argument("--no-train", action="store_true")
     p.add_argument("--no-surrogate", action="store_true")
     p.add_argument("--fused-bn", type=int, default=1, help="fused BN+add+ReLU HIP kernels in the backbone (1/0)")
+    p.add_argument("--gemm-conv1x1", type=int, default=1,
+                   help="stride-1 1x1 convs as hipBLASLt GEMMs where faster (per-shape timing; 1/0)")
     return p.parse_args()
 
 
@@ -128,7 +130,7 @@ def bench_train(args, world, rank, device):
     loader = DeviceLoader(ds, np.arange(len(labels)), args.batch, device, seed=1234 + rank,
                           channels_last=True, pool=args.pool)
     net = build_backbone(args.arch, num_classes=2).to(device).to(memory_format=torch.channels_last)
-    net.set_fused_bn(bool(args.fused_bn))
+    net.set_fused_bn(bool(args.fused_bn)).set_gemm_conv1x1(bool(args.gemm_conv1x1))
     coda = CoDA(net, lr=0.1, gamma=2000.0, T0=10 ** 9, I=args.I, split_index=split, world=world, rank=rank,
                 autocast_dtype=torch.bfloat16, device=device)
     it = iter(loader)
@@ -360,7 +362,8 @@ def main():
                 "warmup": args.warmup, "ms_per_step": res["dt"] / args.steps * 1e3, "higher_is_better": True,
                 "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
                 "config": {"workload": f"{args.arch} CoDA, bf16 autocast backbone"
-                                       f"{' (fused BN+add+ReLU kernels)' if args.fused_bn else ''}, fp32 AUC kernels "
+                                       f"{' (fused BN+add+ReLU kernels)' if args.fused_bn else ''}"
+                                       f"{' (1x1 convs as GEMMs)' if args.gemm_conv1x1 else ''}, fp32 AUC kernels "
                                        "(BASELINE configs[1])",
                            "global_batch": args.batch * world, "image_size": args.image_size, "I": args.I,
                            "pos_ratio": args.pos_ratio, "parallelism": f"dp{world}", "params": res["n_params"]},

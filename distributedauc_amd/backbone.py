@@ -38,6 +38,15 @@ def _bn_act(fused: bool, bn: nn.BatchNorm2d, x: torch.Tensor, relu: bool = True,
     return F.relu(y, inplace=True) if relu else y
 
 
+def _c1(gemm: bool, conv: nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
+    """A 1x1 conv: through conv1x1.py (GEMM or MIOpen, timed per shape) when ``gemm``, else the module."""
+    if gemm:
+        from .conv1x1 import conv1x1
+
+        return conv1x1(conv, x)
+    return conv(x)
+
+
 def _conv(cin: int, cout: int, k: int, stride: int = 1, groups: int = 1) -> nn.Conv2d:
     return nn.Conv2d(cin, cout, kernel_size=k, stride=stride, padding=k // 2, groups=groups, bias=False)
 
@@ -56,10 +65,13 @@ class BasicBlock(nn.Module):
         self.relu = nn.ReLU(inplace=True)
         self.downsample = downsample
         self.fused_bn = False
+        self.gemm_conv1x1 = False
 
     def forward(self, x):
         f = self.fused_bn
-        skip = x if self.downsample is None else _bn_act(f, self.downsample[1], self.downsample[0](x), relu=False)
+        skip = x if self.downsample is None else _bn_act(f, self.downsample[1], _c1(self.gemm_conv1x1,
+                                                                                  self.downsample[0], x),
+                                                         relu=False)
         y = _bn_act(f, self.bn1, self.conv1(x))
         return _bn_act(f, self.bn2, self.conv2(y), residual=skip)
 
@@ -81,13 +93,15 @@ class Bottleneck(nn.Module):
         self.relu = nn.ReLU(inplace=True)
         self.downsample = downsample
         self.fused_bn = False
+        self.gemm_conv1x1 = False
 
     def forward(self, x):
-        f = self.fused_bn
-        skip = x if self.downsample is None else _bn_act(f, self.downsample[1], self.downsample[0](x), relu=False)
-        y = _bn_act(f, self.bn1, self.conv1(x))
+        f, g = self.fused_bn, self.gemm_conv1x1
+        skip = x if self.downsample is None else _bn_act(f, self.downsample[1], _c1(g, self.downsample[0], x),
+                                                         relu=False)
+        y = _bn_act(f, self.bn1, _c1(g, self.conv1, x))
         y = _bn_act(f, self.bn2, self.conv2(y))
-        return _bn_act(f, self.bn3, self.conv3(y), residual=skip)
+        return _bn_act(f, self.bn3, _c1(g, self.conv3, y), residual=skip)
 
 
 class ResNet(nn.Module):
@@ -145,6 +159,13 @@ class ResNet(nn.Module):
         for m in self.modules():
             if isinstance(m, (BasicBlock, Bottleneck)):
                 m.fused_bn = self.fused_bn
+        return self
+
+    def set_gemm_conv1x1(self, enabled: bool = True) -> "ResNet":
+        """Run the stride-1 1x1 convolutions as GEMMs where that is faster (conv1x1.py; channels-last GPU)."""
+        for m in self.modules():
+            if isinstance(m, (BasicBlock, Bottleneck)):
+                m.gemm_conv1x1 = bool(enabled)
         return self
 
     def features(self, x):

@@ -201,7 +201,7 @@ def train(rank: int, size: int, group=None, para=None):
     net = build_backbone(para.arch, num_classes=2, head=head).to(device)
     if para.channels_last:
         net = net.to(memory_format=torch.channels_last)
-        net.set_fused_bn(para.fused_bn)
+        net.set_fused_bn(para.fused_bn).set_gemm_conv1x1(para.gemm_conv1x1)
     coda = CoDA(net, lr=para.lr, gamma=para.gamma, T0=para.T0, I=para.I, split_index=para.split_index,
                 mode=para.mode, world=size, rank=rank, group=group,
                 autocast_dtype=torch.bfloat16 if para.bf16 else None, device=device, head=head)

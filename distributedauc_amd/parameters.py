@@ -48,6 +48,9 @@ def get_parser() -> argparse.ArgumentParser:
     p.add_argument("--fused_bn", action=argparse.BooleanOptionalAction, default=True,
                    help="training-mode BatchNorm + residual add + ReLU through the fused HIP kernels "
                         "(needs --channels_last; csrc/bn_act.hip)")
+    p.add_argument("--gemm_conv1x1", action=argparse.BooleanOptionalAction, default=True,
+                   help="stride-1 1x1 convolutions as hipBLASLt GEMMs where a per-shape timing says so "
+                        "(needs --channels_last; conv1x1.py)")
     p.add_argument("--head", choices=["softmax", "logits"], default="softmax",
                    help="softmax: the model ends in Softmax like resnet.py:159; logits: the softmax column is "
                         "folded into the fused surrogate kernel")

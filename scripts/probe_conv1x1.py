@@ -56,9 +56,21 @@ for H, cin, cout, cnt in SHAPES:
         dw = torch.mm(g2.t(), x2)
         return y, dx, dw
 
-    tc = timeit(conv_fb)
-    tm = timeit(mm_fb)
+    # per direction: MIOpen via aten.convolution_backward, GEMMs via torch.mm (dW split-K over 16 slabs)
+    xx, ww = x.detach(), w.detach()
+    t_cf = timeit(lambda: F.conv2d(xx, ww))
+    t_cd = timeit(lambda: torch.ops.aten.convolution_backward(gy, xx, ww, None, [1, 1], [0, 0], [1, 1], False,
+                                                             [0, 0], 1, [True, False, False]))
+    t_cw = timeit(lambda: torch.ops.aten.convolution_backward(gy, xx, ww, None, [1, 1], [0, 0], [1, 1], False,
+                                                             [0, 0], 1, [False, True, False]))
+    t_mf = timeit(lambda: torch.mm(x2, w2.t()))
+    t_md = timeit(lambda: torch.mm(g2, w2))
+    S = 16 if M % 16 == 0 else 1
+    t_mw = timeit(lambda: torch.bmm(g2.view(S, M // S, cout).transpose(1, 2), x2.view(S, M // S, cin)).sum(0))
+    tc = t_cf + t_cd + t_cw
+    tm = min(t_cf, t_mf) + min(t_cd, t_md) + min(t_cw, t_mw)
     tot_conv += tc * cnt
     tot_mm += tm * cnt
-    print(f"H={H:3d} {cin:5d}->{cout:5d} x{cnt}: conv {tc:8.1f} us  mm {tm:8.1f} us  ({tc / tm:4.2f}x)", flush=True)
-print(f"TOTAL 1x1 stride-1 per step: conv {tot_conv / 1e3:.2f} ms  mm {tot_mm / 1e3:.2f} ms", flush=True)
+    print(f"H={H:3d} {cin:5d}->{cout:5d} x{cnt}: fwd conv {t_cf:7.1f} mm {t_mf:7.1f} | dgrad conv {t_cd:7.1f} "
+          f"mm {t_md:7.1f} | wgrad conv {t_cw:7.1f} mm(splitK) {t_mw:7.1f} us", flush=True)
+print(f"TOTAL 1x1 stride-1 per step: MIOpen {tot_conv / 1e3:.2f} ms  best-of-each {tot_mm / 1e3:.2f} ms", flush=True)
