@@ -35,7 +35,11 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-VALU_PAIR_PEAK = 1.97e13     # 256 CU x 2.4 GHz x 64 lanes / 2 compares per pair
+# VALU issue ceiling of the cheapest exact per-pair sequence on gfx950: 3 packed-fp32
+# instructions (v_pk_add, v_pk_fma clamp, v_pk_add) per 2 pairs = 1.5 lane-ops per pair;
+# 256 CU x 4 SIMD x 16 lanes x 2.4 GHz = 3.93e13 lane-ops/s -> 2.62e13 pairs/s per GPU.
+# (SURVEY §8d's 1.97e13 assumed 2 fp32 compares per pair.)
+VALU_PAIR_PEAK = 2.62e13
 METRIC = "CoDA train imgs/sec + exact-AUC pos×neg pairs/sec at 1/2/4/8 MI355X"
 
 

@@ -5,13 +5,16 @@
 // is (2W + T) / (2PN) with W = #{pos > neg}, T = #{pos == neg}; this file
 // computes W and T as exact integers, with no sort and no host round trip.
 //
-// Pair count: the kernel is VALU compare-issue bound, not HBM bound. Each
-// workgroup keeps 256*RP positives in registers (RP per lane) and streams a
-// slice of the negatives through LDS in 8 KB tiles; every lane compares its
-// RP positives against each staged negative, which all 64 lanes read from one
-// LDS address (a broadcast, conflict-free ds_read_b128). Out-of-range slots are
-// NaN-padded: ordered compares with NaN are false, so padding counts nothing
-// and the inner loop has no bounds checks.
+// Pair count: the kernel is VALU-issue bound, not HBM bound. Each workgroup
+// keeps 256*RP positives in registers (RP per lane) and streams a slice of the
+// negatives through LDS in 8 KB tiles; every lane counts its RP positives
+// against each staged negative, which all 64 lanes read from one LDS address
+// (a broadcast, conflict-free ds_read_b128). The default counting step is a
+// packed-fp32 difference + clamped fma (3 v_pk instructions per 2 pairs, see
+// pk_clamp_fma); tiles holding infinities or tiny subnormal-range scores fall
+// back to exact compares. Out-of-range slots are NaN-padded: ordered compares
+// with NaN are false and clamp(NaN) = 0, so padding counts nothing and the
+// inner loop has no bounds checks.
 
 #include <math.h>
 
@@ -192,32 +195,70 @@ constexpr int64_t kTargetBlocks = 8192;
 
 __device__ __forceinline__ float nan_f() { return __builtin_nanf(""); }
 
-// MODE selects how a compare result is accumulated:
-//   0: per-lane VGPR counters (v_cmp + v_cndmask/v_addc on the VALU)
-//   1: wave ballot + popcount on the scalar unit (v_cmp -> SGPR mask, s_bcnt1, s_add)
-//   2: mixed: '>' through the scalar unit, '>=' through VGPR counters
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// Packed count step for two positives (p0, p1) against one negative q:
+//   u = (p0 - q, p1 - q)                     v_pk_add_f32 (q broadcast by op_sel)
+//   g = clamp(u * 2^127 + 2^-12, 0, 1)        v_pk_fma_f32 ... clamp
+// g is exactly 1 for a win, 2^-12 for a tie and 0 for a loss (or a NaN pad:
+// clamp maps NaN to 0, dx10_clamp) PROVIDED every nonzero difference is at
+// least 2^-126 in magnitude, so that u * 2^127 >= 2 -- see tile_safe(). The
+// accumulator sum W + T * 2^-12 is exact in fp32 for up to 2048 negatives
+// (W + T <= 2048 < 2^11, a multiple of 2^-12), so it is decoded per LDS tile.
+__device__ __forceinline__ f32x2 pk_clamp_fma(f32x2 u, f32x2 s, f32x2 c) {
+    f32x2 g;
+    asm("v_pk_fma_f32 %0, %1, %2, %3 clamp" : "=v"(g) : "v"(u), "s"(s), "v"(c));
+    return g;
+}
+
+// A score is safe for the packed step when it is NaN, +-0, or finite with
+// |v| >= 2^-103: all such values are integer multiples of 2^-126, so a nonzero
+// difference of two of them is >= 2^-126 (it may overflow to +-inf, which is
+// fine). Unsafe: +-inf (inf - inf = NaN would drop a tie) and |v| in
+// (0, 2^-103). A block that sees an unsafe value uses the exact compare loop.
+__device__ __forceinline__ bool unsafe_score(float v) {
+    const unsigned b = __float_as_uint(v) & 0x7fffffffu;
+    return (b - 1u) < (0x0C000000u - 1u) || b == 0x7f800000u;
+}
+
+// MODE selects how a (pos, neg) pair is counted:
+//   0: packed fp32 difference + clamp (1.5 VALU instructions per pair), with a
+//      per-tile fallback to mode 1 for tiles holding unsafe scores (default)
+//   1: per-lane VGPR counters (v_cmp + v_cndmask/v_addc: ~4 instructions per pair)
+//   2: wave ballot + popcount on the scalar unit (v_cmp -> SGPR mask, s_bcnt1, s_add)
+//   3: mixed: '>' through the scalar unit, '>=' through VGPR counters
 template <int RP, int MODE>
 __global__ __launch_bounds__(kPcThreads) void pair_count_kernel(
     const float* __restrict__ pos, int64_t P, const float* __restrict__ neg, int64_t N,
     int64_t neg_per_block, int neg_aligned, unsigned long long* __restrict__ out) {
+    static_assert(RP % 2 == 0, "positives are processed in pairs");
     __shared__ float4 tile[kNegTile / 4];
     __shared__ unsigned long long red[2][kPcThreads / kWave];
 
     float p[RP];
     const int64_t pb = int64_t(blockIdx.x) * (int64_t(kPcThreads) * RP);
+    bool bad = false;
 #pragma unroll
     for (int r = 0; r < RP; ++r) {
         const int64_t i = pb + int64_t(r) * kPcThreads + threadIdx.x;
         p[r] = i < P ? pos[i] : nan_f();
+        bad |= unsafe_score(p[r]);
     }
+    const bool pos_bad = MODE == 0 ? __syncthreads_or(bad) != 0 : true;
+    f32x2 pp[RP / 2];
+#pragma unroll
+    for (int k = 0; k < RP / 2; ++k) pp[k] = f32x2{p[2 * k], p[2 * k + 1]};
+    const f32x2 kScale = {0x1p127f, 0x1p127f}, kTie = {0x1p-12f, 0x1p-12f};
+
     unsigned gt[RP], ge[RP];
 #pragma unroll
     for (int r = 0; r < RP; ++r) gt[r] = ge[r] = 0u;
-    unsigned long long sgt = 0, sge = 0;  // wave-uniform counters (MODE 1, 2)
+    unsigned long long sgt = 0, sge = 0;  // wave-uniform counters (MODE 2, 3)
 
     const int64_t n0 = int64_t(blockIdx.y) * neg_per_block;
     const int64_t n1 = (n0 + neg_per_block < N) ? n0 + neg_per_block : N;
     for (int64_t t0 = n0; t0 < n1; t0 += kNegTile) {
+        bool tbad = false;
 #pragma unroll
         for (int k = 0; k < kNegTile / 4 / kPcThreads; ++k) {
             const int v = k * kPcThreads + threadIdx.x;
@@ -231,35 +272,70 @@ __global__ __launch_bounds__(kPcThreads) void pair_count_kernel(
                 x.z = i + 2 < n1 ? neg[i + 2] : nan_f();
                 x.w = i + 3 < n1 ? neg[i + 3] : nan_f();
             }
+            if constexpr (MODE == 0)
+                tbad |= unsafe_score(x.x) | unsafe_score(x.y) | unsafe_score(x.z) | unsafe_score(x.w);
             tile[v] = x;
         }
-        __syncthreads();
-#pragma unroll 2
-        for (int j = 0; j < kNegTile / 4; ++j) {
-            const float4 q = tile[j];  // same address in every lane: LDS broadcast
+        bool packed = false;
+        if constexpr (MODE == 0) {
+            // the barrier must run in every case (no short-circuit): it publishes the tile
+            const int any_bad = __syncthreads_or(tbad);
+            packed = !pos_bad && any_bad == 0;  // block-uniform
+        } else {
+            __syncthreads();
+        }
+        if (packed) {
+            f32x2 acc[RP / 2];
 #pragma unroll
-            for (int r = 0; r < RP; ++r) {
-                if constexpr (MODE == 0) {
-                    gt[r] += (p[r] > q.x);
-                    ge[r] += (p[r] >= q.x);
-                    gt[r] += (p[r] > q.y);
-                    ge[r] += (p[r] >= q.y);
-                    gt[r] += (p[r] > q.z);
-                    ge[r] += (p[r] >= q.z);
-                    gt[r] += (p[r] > q.w);
-                    ge[r] += (p[r] >= q.w);
-                } else if constexpr (MODE == 1) {
-                    sgt += __popcll(__ballot(p[r] > q.x)) + __popcll(__ballot(p[r] > q.y)) +
-                           __popcll(__ballot(p[r] > q.z)) + __popcll(__ballot(p[r] > q.w));
-                    sge += __popcll(__ballot(p[r] >= q.x)) + __popcll(__ballot(p[r] >= q.y)) +
-                           __popcll(__ballot(p[r] >= q.z)) + __popcll(__ballot(p[r] >= q.w));
-                } else {
-                    sgt += __popcll(__ballot(p[r] > q.x)) + __popcll(__ballot(p[r] > q.y)) +
-                           __popcll(__ballot(p[r] > q.z)) + __popcll(__ballot(p[r] > q.w));
-                    ge[r] += (p[r] >= q.x);
-                    ge[r] += (p[r] >= q.y);
-                    ge[r] += (p[r] >= q.z);
-                    ge[r] += (p[r] >= q.w);
+            for (int k = 0; k < RP / 2; ++k) acc[k] = f32x2{0.f, 0.f};
+#pragma unroll 2
+            for (int j = 0; j < kNegTile / 4; ++j) {
+                const float4 q = tile[j];  // same address in every lane: LDS broadcast
+#pragma unroll
+                for (int k = 0; k < RP / 2; ++k) {
+                    acc[k] += pk_clamp_fma(pp[k] - f32x2{q.x, q.x}, kScale, kTie);
+                    acc[k] += pk_clamp_fma(pp[k] - f32x2{q.y, q.y}, kScale, kTie);
+                    acc[k] += pk_clamp_fma(pp[k] - f32x2{q.z, q.z}, kScale, kTie);
+                    acc[k] += pk_clamp_fma(pp[k] - f32x2{q.w, q.w}, kScale, kTie);
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < RP / 2; ++k) {
+                const f32x2 x = acc[k] * 4096.f;  // W * 4096 + T, exact, < 2^24
+                const unsigned a0 = static_cast<unsigned>(x.x), a1 = static_cast<unsigned>(x.y);
+                gt[2 * k] += a0 >> 12;
+                ge[2 * k] += (a0 >> 12) + (a0 & 4095u);
+                gt[2 * k + 1] += a1 >> 12;
+                ge[2 * k + 1] += (a1 >> 12) + (a1 & 4095u);
+            }
+        } else {
+#pragma unroll 2
+            for (int j = 0; j < kNegTile / 4; ++j) {
+                const float4 q = tile[j];
+#pragma unroll
+                for (int r = 0; r < RP; ++r) {
+                    if constexpr (MODE <= 1) {
+                        gt[r] += (p[r] > q.x);
+                        ge[r] += (p[r] >= q.x);
+                        gt[r] += (p[r] > q.y);
+                        ge[r] += (p[r] >= q.y);
+                        gt[r] += (p[r] > q.z);
+                        ge[r] += (p[r] >= q.z);
+                        gt[r] += (p[r] > q.w);
+                        ge[r] += (p[r] >= q.w);
+                    } else if constexpr (MODE == 2) {
+                        sgt += __popcll(__ballot(p[r] > q.x)) + __popcll(__ballot(p[r] > q.y)) +
+                               __popcll(__ballot(p[r] > q.z)) + __popcll(__ballot(p[r] > q.w));
+                        sge += __popcll(__ballot(p[r] >= q.x)) + __popcll(__ballot(p[r] >= q.y)) +
+                               __popcll(__ballot(p[r] >= q.z)) + __popcll(__ballot(p[r] >= q.w));
+                    } else {
+                        sgt += __popcll(__ballot(p[r] > q.x)) + __popcll(__ballot(p[r] > q.y)) +
+                               __popcll(__ballot(p[r] > q.z)) + __popcll(__ballot(p[r] > q.w));
+                        ge[r] += (p[r] >= q.x);
+                        ge[r] += (p[r] >= q.y);
+                        ge[r] += (p[r] >= q.z);
+                        ge[r] += (p[r] >= q.w);
+                    }
                 }
             }
         }
@@ -275,8 +351,8 @@ __global__ __launch_bounds__(kPcThreads) void pair_count_kernel(
     }
     tg = wave_sum(tg);
     te = wave_sum(te);
-    if (MODE >= 1) tg = sgt;  // already a per-wave total
-    if (MODE == 1) te = sge;
+    if (MODE >= 2) tg = sgt;  // already a per-wave total
+    if (MODE == 2) te = sge;
     if (lane == 0) {
         red[0][wid] = tg;
         red[1][wid] = te;
@@ -340,10 +416,9 @@ int dauc_pair_count_variant(const float* pos, int64_t P, const float* neg, int64
         (N > 0 && neg == nullptr))
         return DAUC_EINVAL;
     if (P == 0 || N == 0) return DAUC_OK;
-    // variant = mode + 3 * rp_index; mode: accumulation scheme, rp: positives per lane {8, 4, 16}
-    if (variant < 0 || variant >= 9) return DAUC_EINVAL;
-    const int mode = variant % 3;
-    const int rp = variant / 3 == 0 ? 8 : (variant / 3 == 1 ? 4 : 16);
+    // variant = mode + 4 * rp_index; mode: counting scheme, rp: positives per lane {8, 4, 16}
+    if (variant < 0 || variant >= 12) return DAUC_EINVAL;
+    const int rp = variant / 4 == 0 ? 8 : (variant / 4 == 1 ? 4 : 16);
     const int64_t pos_per_block = int64_t(kPcThreads) * rp;
     const int64_t gx = (P + pos_per_block - 1) / pos_per_block;
     if (gx > 0x7fffffffLL) return DAUC_EINVAL;
@@ -369,16 +444,17 @@ int dauc_pair_count_variant(const float* pos, int64_t P, const float* neg, int64
         case 0: DAUC_PC_LAUNCH(8, 0); break;
         case 1: DAUC_PC_LAUNCH(8, 1); break;
         case 2: DAUC_PC_LAUNCH(8, 2); break;
-        case 3: DAUC_PC_LAUNCH(4, 0); break;
-        case 4: DAUC_PC_LAUNCH(4, 1); break;
-        case 5: DAUC_PC_LAUNCH(4, 2); break;
-        case 6: DAUC_PC_LAUNCH(16, 0); break;
-        case 7: DAUC_PC_LAUNCH(16, 1); break;
-        case 8: DAUC_PC_LAUNCH(16, 2); break;
+        case 3: DAUC_PC_LAUNCH(8, 3); break;
+        case 4: DAUC_PC_LAUNCH(4, 0); break;
+        case 5: DAUC_PC_LAUNCH(4, 1); break;
+        case 6: DAUC_PC_LAUNCH(4, 2); break;
+        case 7: DAUC_PC_LAUNCH(4, 3); break;
+        case 8: DAUC_PC_LAUNCH(16, 0); break;
+        case 9: DAUC_PC_LAUNCH(16, 1); break;
+        case 10: DAUC_PC_LAUNCH(16, 2); break;
+        case 11: DAUC_PC_LAUNCH(16, 3); break;
     }
 #undef DAUC_PC_LAUNCH
-    (void)mode;
-    (void)rp;
     return launch_status();
 }
 

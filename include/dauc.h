@@ -229,9 +229,10 @@ int dauc_pair_count(const float* pos, int64_t P, const float* neg, int64_t N,
 
 /*
  * dauc_pair_count with an explicit kernel variant, for tuning: variant =
- * mode + 3*r, mode 0 = per-lane VGPR counters, 1 = wave ballot + scalar
- * popcount, 2 = mixed; r selects 8 / 4 / 16 positives held per lane.
- * Variant 0 is what dauc_pair_count uses. Every variant returns identical counts.
+ * mode + 4*r, mode 0 = packed fp32 difference + clamp (exact-compare fallback
+ * for tiles with infinities or |score| < 2^-103), 1 = per-lane VGPR compare
+ * counters, 2 = wave ballot + scalar popcount, 3 = mixed; r selects 8 / 4 / 16
+ * positives held per lane. Every variant returns identical counts.
  */
 int dauc_pair_count_variant(const float* pos, int64_t P, const float* neg, int64_t N,
                             unsigned long long* wins_ties, int variant, dauc_stream_t stream);

@@ -407,7 +407,7 @@ def test_pair_count_edge_sizes(dev):
     for P, N in ((1, 1), (1, 5000), (3000, 1), (2049, 2047), (4097, 9001), (0, 10), (10, 0)):
         pos = (np.floor(rng.random(P) * 64) / 64).astype(np.float32)
         neg = (np.floor(rng.random(N) * 64) / 64).astype(np.float32)
-        for variant in (0, 1, 2):
+        for variant in range(12):
             wt = torch.zeros(2, dtype=torch.int64, device=dev)
             ops.pair_count(T(pos, dev), T(neg, dev), wt, variant=variant)
             assert tuple(wt.cpu().tolist()) == coracle.pair_count_bruteforce(pos, neg), (P, N, variant)
@@ -420,6 +420,41 @@ def test_pair_count_edge_sizes(dev):
     assert tuple(wt.cpu().tolist()) == coracle.pair_count_bruteforce(pos, negall[1:])
 
 
+
+
+@pytest.mark.parametrize("variant", [0, 4, 8, 1])
+def test_pair_count_packed_fallback_values(dev, variant):
+    """Mode 0 (packed fp32 difference + clamp) must equal exact compares for every value class.
+
+    Tiles are 2048 negatives and blocks 256*RP positives: the unsafe values (+-inf, subnormals,
+    |v| < 2^-103) are placed in some tiles / blocks only, so both the packed loop and the
+    per-tile compare fallback run inside one launch. Bit-exact vs the C brute-force oracle."""
+    from distributedauc_amd import ops
+
+    rng = np.random.default_rng(100 + variant)
+    safe = np.array([0.0, -0.0, 1.0, -1.0, 2.0 ** -103, -(2.0 ** -103), 2.0 ** -102, 3.0e38, -3.0e38,
+                     1.1754944e-38 * 4096, 0.5, 0.25], np.float32)
+    unsafe = np.array([np.inf, -np.inf, 1e-45, -1e-45, 1.1754944e-38, 2.0 ** -104, 1e-40], np.float32)
+    for P, N, frac_bad in ((3000, 9000, 0.0), (3000, 9000, 0.002), (5000, 20_000, 0.0005), (17, 5000, 0.01)):
+        pool = np.concatenate([safe, rng.random(64, dtype=np.float32), -rng.random(64, dtype=np.float32)])
+        pos = rng.choice(pool, P).astype(np.float32)
+        neg = rng.choice(pool, N).astype(np.float32)
+        # unsafe values only in the second half of the negatives and the last positives
+        if frac_bad:
+            k = max(1, int(N * frac_bad))
+            neg[N // 2 + rng.integers(0, N - N // 2, k)] = rng.choice(unsafe, k)
+            pos[-max(1, int(P * frac_bad)):] = rng.choice(unsafe, max(1, int(P * frac_bad)))
+        wt = torch.zeros(2, dtype=torch.int64, device=dev)
+        ops.pair_count(T(pos, dev), T(neg, dev), wt, variant=variant)
+        assert tuple(wt.cpu().tolist()) == coracle.pair_count_bruteforce(pos, neg), (P, N, frac_bad)
+    # tiny-difference neighbours: consecutive floats just above the 2^-103 bound and near 1.0
+    base = np.array([2.0 ** -103, 1.0, 1e-20], np.float32)
+    vals = np.concatenate([np.nextafter(base, np.float32(np.inf)), base])
+    pos = np.tile(vals, 300).astype(np.float32)
+    neg = np.tile(vals[::-1], 700).astype(np.float32)
+    wt = torch.zeros(2, dtype=torch.int64, device=dev)
+    ops.pair_count(T(pos, dev), T(neg, dev), wt, variant=variant)
+    assert tuple(wt.cpu().tolist()) == coracle.pair_count_bruteforce(pos, neg)
 
 def test_radix_sort_keys(dev):
     """The LSD radix sort orders keys exactly like the floats (with -0 == +0)."""
