@@ -35,10 +35,11 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-# VALU issue ceiling of the cheapest exact per-pair sequence on gfx950: 3 packed-fp32
-# instructions (v_pk_add, v_pk_fma clamp, v_pk_add) per 2 pairs = 1.5 lane-ops per pair;
-# 256 CU x 4 SIMD x 16 lanes x 2.4 GHz = 3.93e13 lane-ops/s -> 2.62e13 pairs/s per GPU.
-# (SURVEY §8d's 1.97e13 assumed 2 fp32 compares per pair.)
+# VALU ceiling of the cheapest exact per-pair sequence on gfx950: 3 fp32 lane-ops per pair
+# (v_pk_add_f32, v_pk_fma_f32 clamp, v_pk_add_f32 over 2 pairs; a packed op is 2 lane-ops on
+# the 32-wide CDNA4 SIMD). Vector fp32 rate = 256 CU x 4 SIMD x 32 lanes x 2.4 GHz = 7.86e13
+# lane-ops/s (157.3 TF / 2) -> 2.62e13 pairs/s per GPU. (SURVEY §8d's 1.97e13 assumed 16-wide
+# SIMDs and 2 compares per pair.)
 VALU_PAIR_PEAK = 2.62e13
 METRIC = "CoDA train imgs/sec + exact-AUC pos×neg pairs/sec at 1/2/4/8 MI355X"
 
@@ -267,7 +268,9 @@ def bench_surrogate(args, device):
     gbs = nbytes / (ms / 1e3) / 1e9
     return {"workload": f"fused surrogate fwd+bwd, B = 2^{args.sur_log2b} fp32 scores, int8 labels, p = {args.pos_ratio}",
             "B": B, "avg_launch_us": ms * 1e3, "loss": float(out64[0].item()),
-            "roofline": {"kernel": "dauc_surrogate_fwdbwd", "bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS,
+            "roofline": {"kernel": "dauc_surrogate_fwdbwd", "launches": "surrogate_chunk_kernel (stream) + "
+                         "surrogate_rows_reduce_kernel (fp64 rows), both inside the timed ABI call",
+                         "bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS, "traffic": load_traffic(f"surrogate_2^{args.sur_log2b}"),
                          "bytes_per_launch": nbytes}}
 

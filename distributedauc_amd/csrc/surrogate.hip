@@ -342,67 +342,110 @@ __global__ __launch_bounds__(kThreads) void surrogate_kernel(
     reduce_and_finalize<CLASS_ONLY>(acc, s, invB, partials, counter, out64, grad3, loss, sums4, accumulate);
 }
 
-// ---- large unit-stride batches: one chunk per workgroup + a two-level ticket ----------
+// ---- large unit-stride batches: one chunk per workgroup + a separate row reduction -------
 //
-// A grid-stride (persistent) loop keeps only 2 workgroups per CU busy and walks the
-// whole batch with a large stride, so concurrently open DRAM pages are far apart. Here
-// every workgroup takes ONE contiguous chunk of 256 x 4 x S elements (the dispatcher
-// hands chunks out in address order, like the update kernel's one-shot grid), issues
-// all of its loads before any math, and writes one fp64 partial row. The partials are
-// then reduced deterministically: the last arriver of each group of kGroup workgroups
-// sums its group's rows in a fixed order, and the last group reducer sums the group rows.
-constexpr int kGroup = 256;               // workgroups per first-level reduction group
-constexpr int kMaxGroups = 4096;          // ticket slots: up to 2^20 workgroups per launch
-constexpr size_t kTicketStride = 16;      // bytes between tickets
-
-struct ChunkWs {
-    unsigned* top;        // ticket of the group reducers
-    unsigned* group;      // one ticket per group (kTicketStride apart)
-    double* partials;     // [nblocks][kNumAcc]
-    double* gpartials;    // [ngroups][kNumAcc]
-};
+// A grid-stride (persistent) loop walks the batch with a large stride, so concurrently open
+// DRAM pages are far apart (measured: 6.2 TB/s for this 5:4 read:write mix vs 6.5 TB/s for
+// one chunk per workgroup, scripts/probe_stream.hip). Here every workgroup takes ONE
+// contiguous chunk of 256 x 4 x S elements (the dispatcher hands chunks out roughly in
+// address order, like the update kernel's one-shot grid) and issues all of its loads
+// before any math.
+//
+// No workgroup of the streaming launch waits for anything: every WAVE reduces its 6
+// partials with DPP (no barrier, no LDS) and its lane 63 stores them as one 48-B row with
+// plain 16-B stores, then the wave stores dF/dh and exits. A second, small launch reduces
+// the rows (the kernel boundary publishes them). Measured on MI355X at B = 2^26: any
+// in-launch hand-off stalls the stream -- a per-workgroup ticket (barrier + row drain +
+// returning atomic) cost ~18 % (110 us), last-arriver spinners polling rows ~35 % (128 us),
+// because under a full streaming load every round trip to memory queues behind ~70 MB of
+// loads in flight (10-20 us per hop, scripts/probe_sur_timeline.py); the wait-free stream
+// runs at the streaming ceiling of this access mix (93 us). Fixed summation orders
+// everywhere: bitwise reproducible.
+constexpr int kWaves = kThreads / kWave;          // waves per workgroup
+// 1: one row per wave (no barrier in the stream kernel), 0: one row per workgroup
+#ifndef DAUC_SURROGATE_WAVE_ROWS
+#define DAUC_SURROGATE_WAVE_ROWS 0
+#endif
+constexpr int64_t kRowsPerChunk = DAUC_SURROGATE_WAVE_ROWS ? kWaves : 1;
+constexpr int kRowWords = 6;                      // s_pos, s_neg, q_pos, q_neg, n_pos, n_neg (fp64)
+constexpr int kRowsPerReduceBlock = 512;          // rows one workgroup of the reduce kernel sums
 
 __host__ __device__ constexpr int64_t chunk_elems(int S) { return int64_t(kThreads) * kVec * S; }
 
-inline int64_t chunk_groups(int64_t nblocks) { return (nblocks + kGroup - 1) / kGroup; }
+inline int64_t reduce_blocks(int64_t nrows) { return (nrows + kRowsPerReduceBlock - 1) / kRowsPerReduceBlock; }
 
-// Workspace layout: [persistent kernel: ticket + kMaxBlocks rows][chunk tickets: top +
-// kMaxGroups][chunk rows][group rows]. Tickets must stay zero between calls, so they
-// sit at a fixed place that no row of any kernel geometry or batch size ever covers.
+// Workspace layout: [persistent kernel: ticket + kMaxBlocks rows][chunk rows][reduce hand-off words].
 constexpr size_t kPersistentBytes = kCounterBytes + size_t(kMaxBlocks) * kNumAcc * sizeof(double);
-constexpr size_t kChunkTicketBytes = kTicketStride * (1 + kMaxGroups);
 
 inline size_t chunk_ws_bytes(int64_t nblocks) {
-    const int64_t ng = chunk_groups(nblocks);
-    return kPersistentBytes + kChunkTicketBytes + static_cast<size_t>(nblocks + ng) * kNumAcc * sizeof(double);
+    const int64_t nrows = nblocks * kRowsPerChunk;
+    return kPersistentBytes + static_cast<size_t>(nrows + reduce_blocks(nrows)) * kRowWords * sizeof(double);
 }
 
+struct ChunkWs {
+    double* rows;      // [nblocks * kRowsPerChunk][kRowWords]
+    double* brows;     // [reduce blocks][kRowWords] encoded hand-off words (zero between calls)
+};
+
 inline ChunkWs chunk_ws(void* ws, int64_t nblocks) {
-    char* base = static_cast<char*>(ws) + kPersistentBytes;
     ChunkWs w;
-    w.top = reinterpret_cast<unsigned*>(base);
-    w.group = reinterpret_cast<unsigned*>(base + kTicketStride);
-    w.partials = reinterpret_cast<double*>(base + kChunkTicketBytes);
-    w.gpartials = w.partials + nblocks * kNumAcc;
+    w.rows = reinterpret_cast<double*>(static_cast<char*>(ws) + kPersistentBytes);
+    w.brows = w.rows + nblocks * kRowsPerChunk * kRowWords;
     return w;
+}
+
+// One DPP step: the value of the source lane selected by CTRL (0 where ROWMASK disables the row).
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ double dpp_f64(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp(0, static_cast<int>(b), CTRL, ROWMASK, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, static_cast<int>(b >> 32), CTRL, ROWMASK, 0xF, false);
+    return __longlong_as_double((static_cast<long long>(hi) << 32) | static_cast<unsigned>(lo));
+}
+
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ int dpp_i32(int v) {
+    return __builtin_amdgcn_update_dpp(0, v, CTRL, ROWMASK, 0xF, false);
+}
+
+// Wave sum in a fixed order; the total is valid in lane 63:
+// quad_perm[1,0,3,2], quad_perm[2,3,0,1], row_half_mirror, row_mirror (16-lane row sums in
+// every lane), row_bcast:15 into rows 1 and 3, row_bcast:31 into rows 2 and 3.
+__device__ __forceinline__ double wave_total_dpp(double v) {
+    v += dpp_f64<0xB1, 0xF>(v);
+    v += dpp_f64<0x4E, 0xF>(v);
+    v += dpp_f64<0x141, 0xF>(v);
+    v += dpp_f64<0x140, 0xF>(v);
+    v += dpp_f64<0x142, 0xA>(v);
+    v += dpp_f64<0x143, 0xC>(v);
+    return v;
+}
+
+__device__ __forceinline__ int wave_total_dpp(int v) {
+    v += dpp_i32<0xB1, 0xF>(v);
+    v += dpp_i32<0x4E, 0xF>(v);
+    v += dpp_i32<0x141, 0xF>(v);
+    v += dpp_i32<0x140, 0xF>(v);
+    v += dpp_i32<0x142, 0xA>(v);
+    v += dpp_i32<0x143, 0xC>(v);
+    return v;
 }
 
 template <typename YT, bool CLASS_ONLY, int S, bool NT_LOAD, bool NT_STORE>
 __global__ __launch_bounds__(kThreads) void surrogate_chunk_kernel(
     const float* __restrict__ h, const YT* __restrict__ y, int64_t B, double invB,
     const float* __restrict__ abalpha, const float* __restrict__ p_hat, float* __restrict__ dh,
-    ChunkWs ws, double* __restrict__ out64, float* __restrict__ grad3, float* __restrict__ loss,
-    double* __restrict__ sums4, int accumulate) {
+    double* __restrict__ rows) {
     SurrogateScalars s;
     if (CLASS_ONLY) s = SurrogateScalars{};
     else s = make_scalars(abalpha, p_hat, invB);
     Acc acc;
     const bool write_dh = !CLASS_ONLY && dh != nullptr;
-    const int64_t nblocks = gridDim.x;
     const int64_t base = int64_t(blockIdx.x) * chunk_elems(S);
+    const bool full = base + chunk_elems(S) <= B;
 
-    if (base + chunk_elems(S) <= B) {
-        f32x4 hv[S];
+    f32x4 hv[S];
+    if (full) {
         int yv[S][4];
 #pragma unroll
         for (int k = 0; k < S; ++k) {
@@ -412,14 +455,7 @@ __global__ __launch_bounds__(kThreads) void surrogate_chunk_kernel(
             load_labels4(y, b, yv[k]);
         }
 #pragma unroll
-        for (int k = 0; k < S; ++k) {
-            const f32x4 g = visit4<CLASS_ONLY>(hv[k], yv[k], s, acc);
-            if (write_dh) {
-                f32x4* dst = reinterpret_cast<f32x4*>(dh + base + (int64_t(k) * kThreads + threadIdx.x) * kVec);
-                if (NT_STORE) __builtin_nontemporal_store(g, dst);
-                else *dst = g;
-            }
-        }
+        for (int k = 0; k < S; ++k) hv[k] = visit4<CLASS_ONLY>(hv[k], yv[k], s, acc);
     } else {
         // the ragged last chunk: one element per thread per step
         for (int64_t i = base + threadIdx.x; i < B; i += kThreads) {
@@ -428,58 +464,164 @@ __global__ __launch_bounds__(kThreads) void surrogate_chunk_kernel(
         }
     }
 
-    __shared__ double scratch[kNumAcc * (kThreads / kWave)];
-    __shared__ int last_flag;
-    double tot[kNumAcc] = {acc.s_pos, acc.s_neg, acc.q_pos, acc.q_neg,
-                           static_cast<double>(acc.n_pos), static_cast<double>(acc.n_neg)};
-    block_sum<kNumAcc>(tot, scratch);
-    if (threadIdx.x == 0) {
-#pragma unroll
-        for (int k = 0; k < kNumAcc; ++k) store_sc1(&ws.partials[blockIdx.x * kNumAcc + k], tot[k]);
+    // Wave totals by DPP (lane 63), then the dF/dh stores, then ONE row per workgroup: the
+    // barrier comes after every store of the chunk has been issued, so no wave holds its
+    // stores back for it (stores need not complete before a barrier).
+    const double sp = wave_total_dpp(acc.s_pos), sn = wave_total_dpp(acc.s_neg);
+    const double qp = wave_total_dpp(acc.q_pos), qn = wave_total_dpp(acc.q_neg);
+    const int np = wave_total_dpp(acc.n_pos), nn = wave_total_dpp(acc.n_neg);
+#if DAUC_SURROGATE_WAVE_ROWS
+    if ((threadIdx.x & (kWave - 1)) == kWave - 1) {
+        typedef double f64x2 __attribute__((ext_vector_type(2)));
+        f64x2* row = reinterpret_cast<f64x2*>(rows + (int64_t(blockIdx.x) * kWaves + threadIdx.x / kWave) * kRowWords);
+        row[0] = f64x2{sp, sn};
+        row[1] = f64x2{qp, qn};
+        row[2] = f64x2{static_cast<double>(np), static_cast<double>(nn)};
     }
-    // level 1: the last workgroup of the group reduces the group's rows in order
-    const int64_t grp = blockIdx.x / kGroup;
-    const int64_t g0 = grp * kGroup;
-    const int64_t gn = (nblocks - g0) < kGroup ? (nblocks - g0) : kGroup;
-    unsigned* gticket = reinterpret_cast<unsigned*>(reinterpret_cast<char*>(ws.group) + grp * kTicketStride);
-    if (!arrive_last(gticket, static_cast<unsigned>(gn), &last_flag)) return;
+#endif
+    if (full && write_dh) {
+#pragma unroll
+        for (int k = 0; k < S; ++k) {
+            f32x4* dst = reinterpret_cast<f32x4*>(dh + base + (int64_t(k) * kThreads + threadIdx.x) * kVec);
+            if (NT_STORE) __builtin_nontemporal_store(hv[k], dst);
+            else *dst = hv[k];
+        }
+    }
+#if !DAUC_SURROGATE_WAVE_ROWS
+    __shared__ double wrow[kWaves][kRowWords];
+    const int wid = threadIdx.x / kWave;
+    if ((threadIdx.x & (kWave - 1)) == kWave - 1) {
+        wrow[wid][0] = sp;
+        wrow[wid][1] = sn;
+        wrow[wid][2] = qp;
+        wrow[wid][3] = qn;
+        wrow[wid][4] = static_cast<double>(np);
+        wrow[wid][5] = static_cast<double>(nn);
+    }
+    __syncthreads();
+    if (threadIdx.x < kRowWords) {
+        const int k = threadIdx.x;
+        rows[int64_t(blockIdx.x) * kRowWords + k] = ((wrow[0][k] + wrow[1][k]) + wrow[2][k]) + wrow[3][k];
+    }
+#endif
+}
+
+// Reduce the streaming launch's rows (the kernel boundary published them): workgroup b sums
+// rows [512 b, 512 (b + 1)) in a fixed order (thread t: rows t, t + 256). Workgroups b > 0
+// hand their 6 totals to workgroup 0 as encoded 8-B words stored write-through (sc1): a word
+// is bits ^ kEmptyKey, a signalling-NaN pattern no arithmetic result or count can equal, so a
+// zero word means "not written yet" (cdna_hip_programming.md Guideline 16, R2: the data is
+// the flag, no drain, no ticket). Workgroup 0 polls those words with sc1 loads (bounded; a
+// timeout yields NaN outputs), sums them in a fixed order, zeroes them again for the next
+// call, and writes the scalars. The grid is small (<= 64 workgroups up to B = 2^27) and
+// workgroup 0 is the only one that waits, so every workgroup it waits for can run.
+constexpr unsigned long long kEmptyKey = 0x7FF4DEADBEEF0001ull;  // signalling NaN
+constexpr int kMaxPolls = 1 << 22;
+
+__device__ __forceinline__ unsigned long long enc_word(double v) {
+    return static_cast<unsigned long long>(__double_as_longlong(v)) ^ kEmptyKey;
+}
+
+template <bool CLASS_ONLY>
+__global__ __launch_bounds__(kThreads) void surrogate_rows_reduce_kernel(
+    const double* __restrict__ rows, int64_t nrows, ChunkWs ws, double invB, const float* __restrict__ abalpha,
+    const float* __restrict__ p_hat, double* __restrict__ out64, float* __restrict__ grad3, float* __restrict__ loss,
+    double* __restrict__ sums4, int accumulate) {
+    __shared__ double scratch[kNumAcc * kWaves];
+    double tot[kNumAcc];
 #pragma unroll
     for (int k = 0; k < kNumAcc; ++k) tot[k] = 0.0;
-    for (int64_t b = g0 + threadIdx.x; b < g0 + gn; b += kThreads) {
+    const int64_t r0 = int64_t(blockIdx.x) * kRowsPerReduceBlock;
+    const int64_t r1 = (r0 + kRowsPerReduceBlock < nrows) ? r0 + kRowsPerReduceBlock : nrows;
+    // all of a thread's rows in flight at once (rows t, t + 256, ...: a fixed order)
+    typedef double f64x2 __attribute__((ext_vector_type(2)));
+    constexpr int kPer = kRowsPerReduceBlock / kThreads;
+    f64x2 v[kPer][3];
 #pragma unroll
-        for (int k = 0; k < kNumAcc; ++k) tot[k] += load_sc1(&ws.partials[b * kNumAcc + k]);
+    for (int j = 0; j < kPer; ++j) {
+        const int64_t r = r0 + threadIdx.x + int64_t(j) * kThreads;
+#pragma unroll
+        for (int q = 0; q < 3; ++q)
+            v[j][q] = r < r1 ? reinterpret_cast<const f64x2*>(rows + r * kRowWords)[q] : f64x2{0.0, 0.0};
+    }
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            tot[2 * q] += v[j][q].x;
+            tot[2 * q + 1] += v[j][q].y;
+        }
     }
     block_sum<kNumAcc>(tot, scratch);
-    const int64_t ngroups = (nblocks + kGroup - 1) / kGroup;
-    if (ngroups > 1) {
+    unsigned long long* words = reinterpret_cast<unsigned long long*>(ws.brows);
+    if (blockIdx.x > 0) {
         if (threadIdx.x == 0) {
 #pragma unroll
-            for (int k = 0; k < kNumAcc; ++k) store_sc1(&ws.gpartials[grp * kNumAcc + k], tot[k]);
+            for (int k = 0; k < kNumAcc; ++k)
+                __hip_atomic_store((gu64*)(words + int64_t(blockIdx.x) * kRowWords + k), enc_word(tot[k]),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        // level 2: the last group reducer sums the group rows in order
-        if (!arrive_last(ws.top, static_cast<unsigned>(ngroups), &last_flag)) return;
+        return;
+    }
+    bool ok = true;
+    if (gridDim.x > 1) {
+        double rest[kNumAcc];
 #pragma unroll
-        for (int k = 0; k < kNumAcc; ++k) tot[k] = 0.0;
-        for (int64_t g = threadIdx.x; g < ngroups; g += kThreads) {
+        for (int k = 0; k < kNumAcc; ++k) rest[k] = 0.0;
+        for (int b = 1 + threadIdx.x; b < static_cast<int>(gridDim.x); b += kThreads) {
+            unsigned long long* row = words + int64_t(b) * kRowWords;
+            unsigned long long w[kRowWords];
 #pragma unroll
-            for (int k = 0; k < kNumAcc; ++k) tot[k] += load_sc1(&ws.gpartials[g * kNumAcc + k]);
+            for (int k = 0; k < kRowWords; ++k)
+                w[k] = __hip_atomic_load((gu64*)(row + k), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            for (int polls = 0;; ++polls) {
+                bool missing = false;
+#pragma unroll
+                for (int k = 0; k < kRowWords; ++k) missing |= (w[k] == 0ull);
+                if (!missing) break;
+                if (polls >= kMaxPolls) {
+                    ok = false;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+#pragma unroll
+                for (int k = 0; k < kRowWords; ++k)
+                    if (w[k] == 0ull)
+                        w[k] = __hip_atomic_load((gu64*)(row + k), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+#pragma unroll
+            for (int k = 0; k < kRowWords; ++k) {
+                rest[k] += __longlong_as_double(static_cast<long long>(w[k] ^ kEmptyKey));
+                __hip_atomic_store((gu64*)(row + k), 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
         }
-        block_sum<kNumAcc>(tot, scratch);
+        block_sum<kNumAcc>(rest, scratch);
+        ok = __syncthreads_or(!ok) == 0;
+#pragma unroll
+        for (int k = 0; k < kNumAcc; ++k) tot[k] += rest[k];
     }
     if (threadIdx.x == 0) {
-        if (CLASS_ONLY) emit_class_sums(tot, sums4, accumulate);
-        else finalize(tot, s, invB, out64, grad3, loss);
+        if (!ok) {
+#pragma unroll
+            for (int k = 0; k < kNumAcc; ++k) tot[k] = __builtin_nan("");
+        }
+        if (CLASS_ONLY) {
+            emit_class_sums(tot, sums4, accumulate);
+        } else {
+            const SurrogateScalars s = make_scalars(abalpha, p_hat, invB);
+            finalize(tot, s, invB, out64, grad3, loss);
+        }
     }
 }
 
 // Default chunk geometry (variant sweep: scripts/micro_kernels.py --which surrogate).
 #ifndef DAUC_SURROGATE_CHUNK_SLOTS
-#define DAUC_SURROGATE_CHUNK_SLOTS 8
+#define DAUC_SURROGATE_CHUNK_SLOTS 4
 #endif
 constexpr int kChunkSlots = DAUC_SURROGATE_CHUNK_SLOTS;
 // Unit-stride batches at least this large take the chunked kernel; smaller ones are
 // latency-bound and stay on the single-ticket persistent kernel.
-constexpr int64_t kChunkMinB = int64_t(1) << 20;
+constexpr int64_t kChunkMinB = int64_t(1) << 22;
 
 int resident_blocks() {
     static int cached = 0;
@@ -508,11 +650,18 @@ int launch_chunk(const float* h, const YT* y, int64_t B, const float* abalpha, c
                  double* out64, float* grad3, float* loss, double* sums4, int accumulate, void* ws,
                  size_t ws_bytes, hipStream_t st) {
     const int64_t nblocks = (B + chunk_elems(S) - 1) / chunk_elems(S);
-    if (chunk_groups(nblocks) > kMaxGroups) return DAUC_EINVAL;
+    if (nblocks > 0x7fffffffLL) return DAUC_EINVAL;
     if (ws == nullptr || ws_bytes < chunk_ws_bytes(nblocks)) return DAUC_EINVAL;
+    const ChunkWs w = chunk_ws(ws, nblocks);
+    const double invB = 1.0 / static_cast<double>(B);
     hipLaunchKernelGGL((surrogate_chunk_kernel<YT, CLASS_ONLY, S, NTL, NTS>), dim3(static_cast<unsigned>(nblocks)),
-                       dim3(kThreads), 0, st, h, y, B, 1.0 / static_cast<double>(B), abalpha, p_hat, dh,
-                       chunk_ws(ws, nblocks), out64, grad3, loss, sums4, accumulate);
+                       dim3(kThreads), 0, st, h, y, B, invB, abalpha, p_hat, dh, w.rows);
+    int rc = launch_status();
+    if (rc) return rc;
+    const int64_t nrows = nblocks * kRowsPerChunk;
+    hipLaunchKernelGGL((surrogate_rows_reduce_kernel<CLASS_ONLY>), dim3(static_cast<unsigned>(reduce_blocks(nrows))),
+                       dim3(kThreads), 0, st, w.rows, nrows, w, invB, abalpha, p_hat, out64, grad3, loss, sums4,
+                       accumulate);
     return launch_status();
 }
 
@@ -540,8 +689,7 @@ int launch_surrogate(const float* h, int64_t hs, const YT* y, int64_t B, const f
         }
         return DAUC_EINVAL;
     }
-    if (unit && variant == 0 && B >= kChunkMinB &&
-        chunk_groups((B + chunk_elems(kChunkSlots) - 1) / chunk_elems(kChunkSlots)) <= kMaxGroups)
+    if (unit && variant == 0 && B >= kChunkMinB)
         return launch_chunk<YT, CLASS_ONLY, kChunkSlots, true, true>(h, y, B, abalpha, p_hat, dh, out64, grad3,
                                                                       loss, sums4, accumulate, ws, ws_bytes, st);
     const int grid = grid_for(B);

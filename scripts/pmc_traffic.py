@@ -32,6 +32,8 @@ def rows(pattern):
 def kernel_key(name: str) -> str | None:
     if "pd_update_kernel" in name:
         return "pd_update"
+    if "surrogate_rows_reduce_kernel" in name:
+        return "surrogate_reduce"
     if "surrogate_chunk_kernel" in name or "surrogate_kernel" in name:
         return "surrogate"
     return None
@@ -48,7 +50,7 @@ def per_kernel(rs, counter):
         by.setdefault(k, []).append((int(r["Grid_Size"]), float(r["Counter_Value"]) * 1024.0))
     out = {}
     for k, v in by.items():
-        if k == "surrogate":
+        if k.startswith("surrogate"):
             gmax = max(g for g, _ in v)
             v = [x for x in v if x[0] == gmax]
         out[k] = statistics.median(b for _, b in v)
@@ -61,10 +63,16 @@ def main(src: str, dst: str):
     res = {
         "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes (scripts/gpu_pmc.sh), "
                   "counter-collection CSV per dispatch; KB = 1024 B; FETCH_SIZE doubled for gfx950 wide streaming "
-                  "reads (MI355X_MICROARCH.md §HBM); median over dispatches (surrogate: largest grid = B 2^26); "
+                  "reads (MI355X_MICROARCH.md §HBM); median over dispatches (surrogate: largest grid = B 2^26, chunk kernel + row-reduce kernel); "
                   "scripts/pmc_traffic.py",
         "source": dst,
     }
+    # the surrogate call at large B is two launches: the streaming chunk kernel + the row reduction
+    for key in ("surrogate",):
+        if key + "_reduce" in fetch and key in fetch:
+            fetch[key] += fetch[key + "_reduce"]
+        if key + "_reduce" in write and key in write:
+            write[key] += write[key + "_reduce"]
     for k, name in (("pd_update", "pd_update"), ("surrogate", "surrogate_2^26")):
         if k in fetch and k in write:
             rd, wr = 2.0 * fetch[k], write[k]

@@ -62,30 +62,8 @@ def test_conv1x1_falls_back_for_strided(dev):
 
 def test_resnet_gemm_conv1x1_trains(dev):
     """ResNet-50 step with fused BN + GEMM 1x1 convs (autotuned engines) vs the fp32 torch step:
-    logits and every gradient within 2x the error torch's own bf16 autocast step makes."""
-    from distributedauc_amd.backbone import build_backbone
+    summed over 3 seeds (tests/bf16_step_compare.py), logits and every gradient within 2x the
+    error torch's own bf16 autocast step makes."""
+    from bf16_step_compare import compare
 
-    torch.manual_seed(0)
-    base = build_backbone("resnet50", num_classes=2)
-    x = torch.randn(8, 3, 64, 64, device=dev).contiguous(memory_format=torch.channels_last)
-    runs = {}
-    for name, amp, fast in (("fp32", False, False), ("bf16", True, False), ("fast", True, True)):
-        net = build_backbone("resnet50", num_classes=2)
-        net.load_state_dict(base.state_dict())
-        net = net.to(dev).to(memory_format=torch.channels_last).train()
-        net.set_fused_bn(fast).set_gemm_conv1x1(fast)
-        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
-            out = net(x)
-        out[:, 1].sum().backward()
-        runs[name] = (out.detach().float(), {n: p.grad.detach().float().flatten() for n, p in net.named_parameters()})
-    ref_out, ref_g = runs["fp32"]
-    e_b = float((runs["bf16"][0] - ref_out).abs().max())
-    e_f = float((runs["fast"][0] - ref_out).abs().max())
-    assert e_f <= 2 * e_b + 1e-3, (e_f, e_b)
-    worse = []
-    for n, g in ref_g.items():
-        eb = float((runs["bf16"][1][n] - g).norm())
-        ef = float((runs["fast"][1][n] - g).norm())
-        if ef > 2 * eb + 1e-3 * float(g.norm()) + 1e-12:
-            worse.append((n, ef, eb))
-    assert not worse, worse
+    compare(dev, fused_bn=True, gemm_1x1=True)

@@ -126,38 +126,10 @@ def test_bn_act_rejects_unsupported(dev):
 
 def test_resnet_fused_matches_unfused(dev):
     """A ResNet-50 training step (channels-last) three ways: fp32 torch (the reference), bf16
-    autocast with torch's BN/add/relu, bf16 autocast with the fused kernels. The fused run must be
-    as close to the fp32 reference as torch's own bf16 run is (outputs: max error <= 2x torch's
-    + 1e-3; every parameter gradient: L2 error to the fp32 gradient <= 2x torch bf16's + 1e-3 of
-    its norm), and the same for its BN running statistics (max error)."""
-    from distributedauc_amd.backbone import build_backbone
+    autocast with torch's BN/add/relu, bf16 autocast with the fused kernels. Summed over 3 seeds
+    (tests/bf16_step_compare.py), the fused run must be as close to the fp32 reference as torch's
+    own bf16 run is: logits max error <= 2x torch's + 1e-3; every parameter gradient's L2 error
+    <= 2x torch bf16's + 1e-3 of its norm; every BN running statistic's max error likewise."""
+    from bf16_step_compare import compare
 
-    torch.manual_seed(0)
-    base = build_backbone("resnet50", num_classes=2)
-    x = torch.randn(8, 3, 64, 64, device=dev).contiguous(memory_format=torch.channels_last)
-    runs = {}
-    for name, amp, fused in (("fp32", False, False), ("bf16", True, False), ("fused", True, True)):
-        net = build_backbone("resnet50", num_classes=2)
-        net.load_state_dict(base.state_dict())
-        net = net.to(dev).to(memory_format=torch.channels_last).train()
-        net.set_fused_bn(fused)
-        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
-            out = net(x)
-        out[:, 1].sum().backward()
-        runs[name] = (out.detach().float(), {n: p.grad.detach().float().flatten() for n, p in net.named_parameters()},
-                      {n: b.detach().float() for n, b in net.named_buffers()})
-    ref_out, ref_g, ref_b = runs["fp32"]
-    e_bf16 = float((runs["bf16"][0] - ref_out).abs().max())
-    e_fused = float((runs["fused"][0] - ref_out).abs().max())
-    assert e_fused <= 2 * e_bf16 + 1e-3, (e_fused, e_bf16)
-    worse = []
-    for n, g in ref_g.items():
-        e_b = float((runs["bf16"][1][n] - g).norm())
-        e_f = float((runs["fused"][1][n] - g).norm())
-        if e_f > 2 * e_b + 1e-3 * float(g.norm()) + 1e-12:
-            worse.append((n, e_f, e_b, float(g.norm())))
-    assert not worse, worse
-    for n, b in ref_b.items():
-        e_b = float((runs["bf16"][2][n] - b).abs().max())
-        e_f = float((runs["fused"][2][n] - b).abs().max())
-        assert e_f <= 2 * e_b + 1e-3 * float(b.abs().max()) + 1e-6, (n, e_f, e_b)
+    compare(dev, fused_bn=True, gemm_1x1=False, check_buffers=True)
