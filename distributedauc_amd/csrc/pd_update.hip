@@ -22,6 +22,7 @@ namespace {
 
 constexpr int kThreads = 256;
 constexpr int kMaxSeg = 176;  // segments per launch (kernel-argument table, < 4 KB)
+constexpr int kSearchSlots = 192;  // blk_start entries: kMaxSeg + 1 rounded up to whole waves
 
 // Geometry: VPT float4 per thread -> 256*4*VPT elements per block. The default
 // (variant 0) is VPT = 2 with non-temporal g/w0 loads: fastest on MI355X
@@ -31,7 +32,7 @@ constexpr int64_t elems_per_block(int vpt) { return int64_t(kThreads) * 4 * vpt;
 
 struct SegTable {
     int nseg;
-    int blk_start[kMaxSeg + 1];  // first block of each segment; blk_start[nseg] = grid
+    int blk_start[kSearchSlots];  // first block of each segment; blk_start[nseg] = grid; INT_MAX after
     const float* grad[kMaxSeg];
     int offset[kMaxSeg];         // element offsets / counts fit 31 bits (checked on the host)
     int numel[kMaxSeg];
@@ -66,7 +67,7 @@ __device__ void scalar_update(float* s, const float* g3, const float* a3, float 
     s[2] = al_new;
 }
 
-template <bool AVG, int VPT, bool NT>
+template <bool AVG, int VPT, bool NT, bool NTALL = false>
 __global__ __launch_bounds__(kThreads) void pd_update_kernel(
     float* __restrict__ w, const float* __restrict__ w0, float* __restrict__ wavg, SegTable tab,
     float lr, float invg, float* __restrict__ scalars, const float* __restrict__ grad3,
@@ -75,12 +76,19 @@ __global__ __launch_bounds__(kThreads) void pd_update_kernel(
     if (scalars != nullptr && bid == 0 && threadIdx.x == 0)
         scalar_update(scalars, grad3, anchor3, lr, invg, mode);
 
-    // segment owning this block (wave-uniform binary search over kernel args)
-    int lo = 0, hi = tab.nseg - 1;
-    while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (tab.blk_start[mid] <= bid) lo = mid;
-        else hi = mid - 1;
+    // segment owning this block: every lane tests a few segment starts at once (independent
+    // loads from the kernel-argument table), the count of starts <= bid is the segment + 1.
+    // (A binary search is ~8 dependent scalar loads, ~0.7 us at every block's start.)
+    int lo;
+    {
+        const int lane = threadIdx.x & (kWave - 1);
+        int cnt = 0;
+#pragma unroll
+        for (int base = 0; base < kSearchSlots; base += kWave) {
+            const int start = tab.blk_start[base + lane];  // unconditional: all loads in flight together
+            cnt += __popcll(__ballot(start <= bid));
+        }
+        lo = __builtin_amdgcn_readfirstlane(cnt - 1);
     }
     const float* __restrict__ g = tab.grad[lo];
     const int64_t off = tab.offset[lo];
@@ -102,7 +110,8 @@ __global__ __launch_bounds__(kThreads) void pd_update_kernel(
             const int64_t i = e0 + (int64_t(v) * kThreads + threadIdx.x) * 4;
             full[v] = i + 4 <= n;
             if (full[v]) {
-                wv[v] = *reinterpret_cast<const f32x4*>(ws + i);
+                if (NTALL) wv[v] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(ws + i));
+                else wv[v] = *reinterpret_cast<const f32x4*>(ws + i);
                 if (NT) {
                     gv[v] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(g + i));
                     zv[v] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(w0s + i));
@@ -110,7 +119,10 @@ __global__ __launch_bounds__(kThreads) void pd_update_kernel(
                     gv[v] = *reinterpret_cast<const f32x4*>(g + i);
                     zv[v] = *reinterpret_cast<const f32x4*>(w0s + i);
                 }
-                if (AVG) av[v] = *reinterpret_cast<const f32x4*>(as + i);
+                if (AVG) {
+                    if (NTALL) av[v] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(as + i));
+                    else av[v] = *reinterpret_cast<const f32x4*>(as + i);
+                }
             }
         }
 #pragma unroll
@@ -120,12 +132,14 @@ __global__ __launch_bounds__(kThreads) void pd_update_kernel(
                 f32x4 r;
 #pragma unroll
                 for (int c = 0; c < 4; ++c) r[c] = pd_step(wv[v][c], gv[v][c], zv[v][c], lr, invg);
-                *reinterpret_cast<f32x4*>(ws + i) = r;
+                if (NTALL) __builtin_nontemporal_store(r, reinterpret_cast<f32x4*>(ws + i));
+                else *reinterpret_cast<f32x4*>(ws + i) = r;
                 if (AVG) {
                     f32x4 a;
 #pragma unroll
                     for (int c = 0; c < 4; ++c) a[c] = __fadd_rn(av[v][c], r[c]);
-                    *reinterpret_cast<f32x4*>(as + i) = a;
+                    if (NTALL) __builtin_nontemporal_store(a, reinterpret_cast<f32x4*>(as + i));
+                    else *reinterpret_cast<f32x4*>(as + i) = a;
                 }
             } else {
                 for (int64_t j = i; j < n && j < i + 4; ++j) {
@@ -152,21 +166,22 @@ __global__ void scalar_update_kernel(float* s, const float* g3, const float* a3,
     scalar_update(s, g3, a3, lr, invg, mode);
 }
 
-template <int VPT, bool NT>
+template <int VPT, bool NT, bool NTALL = false>
 int launch_table_t(float* w, const float* w0, float* wavg, const SegTable& tab, float lr, float invg,
                    float* scalars, const float* grad3, const float* anchor3, int mode, hipStream_t st) {
     const int grid = tab.blk_start[tab.nseg];
     if (grid <= 0) return DAUC_OK;
     if (wavg)
-        hipLaunchKernelGGL((pd_update_kernel<true, VPT, NT>), dim3(grid), dim3(kThreads), 0, st, w, w0, wavg,
+        hipLaunchKernelGGL((pd_update_kernel<true, VPT, NT, NTALL>), dim3(grid), dim3(kThreads), 0, st, w, w0, wavg,
                            tab, lr, invg, scalars, grad3, anchor3, mode);
     else
-        hipLaunchKernelGGL((pd_update_kernel<false, VPT, NT>), dim3(grid), dim3(kThreads), 0, st, w, w0,
+        hipLaunchKernelGGL((pd_update_kernel<false, VPT, NT, NTALL>), dim3(grid), dim3(kThreads), 0, st, w, w0,
                            wavg, tab, lr, invg, scalars, grad3, anchor3, mode);
     return launch_status();
 }
 
-// variant = vpt_index + 4 * nt: vpt in {2, 1, 4, 3}, nt = non-temporal g/w0 loads off (1) / on (0)
+// variant = vpt_index + 4 * k: vpt in {2, 1, 4, 3}; k = 0: non-temporal g/w0 loads, 1: all plain,
+// 2: every load and store non-temporal
 int launch_table(int variant, float* w, const float* w0, float* wavg, const SegTable& tab, float lr,
                  float invg, float* scalars, const float* grad3, const float* anchor3, int mode,
                  hipStream_t st) {
@@ -179,6 +194,10 @@ int launch_table(int variant, float* w, const float* w0, float* wavg, const SegT
         case 5: return launch_table_t<1, false>(w, w0, wavg, tab, lr, invg, scalars, grad3, anchor3, mode, st);
         case 6: return launch_table_t<4, false>(w, w0, wavg, tab, lr, invg, scalars, grad3, anchor3, mode, st);
         case 7: return launch_table_t<3, false>(w, w0, wavg, tab, lr, invg, scalars, grad3, anchor3, mode, st);
+        case 8: return launch_table_t<2, true, true>(w, w0, wavg, tab, lr, invg, scalars, grad3, anchor3, mode, st);
+        case 9: return launch_table_t<1, true, true>(w, w0, wavg, tab, lr, invg, scalars, grad3, anchor3, mode, st);
+        case 10: return launch_table_t<4, true, true>(w, w0, wavg, tab, lr, invg, scalars, grad3, anchor3, mode, st);
+        case 11: return launch_table_t<3, true, true>(w, w0, wavg, tab, lr, invg, scalars, grad3, anchor3, mode, st);
         default: return DAUC_EINVAL;
     }
 }
@@ -237,7 +256,7 @@ static int pd_update_impl(float* w, const float* w0, float* w_avg, const dauc_gr
         return DAUC_EINVAL;
     if (scalars != nullptr && (grad3 == nullptr || anchor3 == nullptr)) return DAUC_EINVAL;
     if (mode != DAUC_MODE_REFERENCE && mode != DAUC_MODE_PAPER) return DAUC_EINVAL;
-    if (variant < 0 || variant >= 8) return DAUC_EINVAL;
+    if (variant < 0 || variant >= 12) return DAUC_EINVAL;
     for (int i = 0; i < nseg; ++i)
         if (segs[i].numel < 0 || segs[i].offset < 0 || (segs[i].numel > 0 && !segs[i].grad) ||
             segs[i].offset + segs[i].numel > 0x7fffffffLL)
@@ -263,6 +282,7 @@ static int pd_update_impl(float* w, const float* w0, float* w_avg, const dauc_gr
             ++tab.nseg;
         }
         tab.blk_start[tab.nseg] = static_cast<int>(blocks);
+        for (int j = tab.nseg + 1; j < kSearchSlots; ++j) tab.blk_start[j] = 0x7fffffff;  // never <= a block id
         if (tab.nseg == 0) continue;
         // the scalar part rides in the first launch only
         const int rc = launch_table(variant, w, w0, w_avg, tab, lr, inv_gamma, first ? scalars : nullptr,
