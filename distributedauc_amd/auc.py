@@ -85,12 +85,20 @@ class ExactAUC:
                 raise ValueError("multiclass format is not supported")
         wt = torch.zeros(2, dtype=torch.int64, device=s.device)
         if P and N:
-            lo = self.rank * P // self.world
-            hi = (self.rank + 1) * P // self.world
-            if hi > lo:
-                if self.method == "pairs":
+            if self.method == "pairs":
+                # positive-set blocks: every rank compares its block against all negatives
+                lo, hi = self.rank * P // self.world, (self.rank + 1) * P // self.world
+                if hi > lo:
                     ops.pair_count(pos[lo:hi], neg[:N], wt, variant=self.variant)
-                else:
+            elif P <= N:
+                # the sorted table is the (small) positive class on every rank; the negatives,
+                # which are streamed through the search, are split
+                lo, hi = self.rank * N // self.world, (self.rank + 1) * N // self.world
+                if hi > lo:
+                    ops.auc_counts_sorted(pos[:P], neg[lo:hi], wt)
+            else:
+                lo, hi = self.rank * P // self.world, (self.rank + 1) * P // self.world
+                if hi > lo:
                     ops.auc_counts_sorted(pos[lo:hi], neg[:N], wt)
         if self.world > 1 and self.reduce:
             dist.all_reduce(wt, op=dist.ReduceOp.SUM, group=self.group)

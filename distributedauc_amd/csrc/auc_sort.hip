@@ -1,6 +1,7 @@
-// Exact AUC by sorting: LSD radix sort of the negatives' order-preserving keys,
-// then two binary searches per positive. O(N + P log N) work instead of the
-// pair count's O(P*N); the counts are the same integers (W, T).
+// Exact AUC by sorting: LSD radix sort of the SMALLER class's order-preserving keys,
+// then every score of the larger class is located in it with an LDS-resident search
+// tree. O(M log M + L log M) work (M = min(P, N), L = max(P, N)) instead of the pair
+// count's O(P*N); the counts are the same integers (W, T).
 //
 // Reference: imagenet/main.py:79-81 -> sklearn roc_curve/auc, whose
 // _binary_clf_curve (sklearn/metrics/_ranking.py:826-908) also sorts the scores
@@ -16,8 +17,15 @@
 //             tile's keys with the same digit comes from 8 wave ballots (wave multisplit)
 //             plus per-digit wave/chunk offsets in LDS, so the scatter is STABLE (LSD
 //             correctness needs it); writes to out[offset[digit][tile] + rank].
-// Search: each thread takes one positive key, lower_bound / upper_bound over the sorted
-//   negatives; W += lb, T += ub - lb, reduced per block, one 64-bit atomic per block.
+// Search: every k-th sorted key (k a power of two, so at most 16383 splitters) goes into an
+//   Eytzinger (BFS-order) tree, which every workgroup loads into LDS once; one query key x
+//   walks it twice in lockstep (x and x - 1: the splitters <= x and < x; BFS order puts
+//   each level's nodes side by side, so a level's reads spread over the LDS banks instead
+//   of all landing in one as a sorted array's power-of-two strides do), then one vector
+//   load of its k-key bucket from the (L2-resident) sorted table finishes upper_bound and
+//   lower_bound. The queries are streamed once with float4 loads; per-block integer sums,
+//   one 64-bit atomic each.
+//   table = positives: W += M - ub(x), T += ub - lb;  table = negatives: W += lb(x), T += ub - lb.
 
 #include "dauc_internal.h"
 
@@ -29,6 +37,7 @@ constexpr int kPerThread = 16;
 constexpr int kTile = kSortThreads * kPerThread;  // 4096 keys
 constexpr int kRadix = 256;
 constexpr int kScanBlock = 1024;
+constexpr int64_t kSingleScan = 32768;  // histogram entries one workgroup scans alone (<= 512K keys)
 
 __device__ __forceinline__ unsigned key_of(float f) {
     if (f == 0.0f) f = 0.0f;  // -0 -> +0
@@ -159,49 +168,162 @@ __global__ __launch_bounds__(kSortThreads) void radix_scatter_kernel(const void*
 
 // ---- search ---------------------------------------------------------------------------
 
-__device__ __forceinline__ int64_t lower_bound_u32(const unsigned* __restrict__ a, int64_t n, unsigned k) {
-    int64_t lo = 0, len = n;
+constexpr int kMaxSplit = 16383;          // splitters: a perfect tree of depth <= 14 (64 KB of LDS)
+constexpr int kTreeSlots = kMaxSplit + 1;  // 1-based BFS array
+constexpr size_t kTreeBytes = size_t(kTreeSlots) * 4;
+constexpr int kQueryThreads = 1024;
+constexpr unsigned kPadKey = 0xffffffffu;  // above every finite score's key (max 0xff7fffff)
+
+// tree[i] (BFS index i in [1, 2^h)) = the splitter whose in-order rank is r, i.e.
+// sorted[r * k], or kPadKey past the last splitter.
+__global__ __launch_bounds__(256) void build_tree_kernel(const unsigned* __restrict__ sorted, int64_t M, int k,
+                                                         int S, int h, unsigned* __restrict__ tree) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i == 0 || i >= (1 << h)) return;
+    const int d = 31 - __clz(i);                          // depth of node i
+    const int pidx = i - (1 << d);                        // position within its level
+    const int r = ((2 * pidx + 1) << (h - 1 - d)) - 1;    // in-order rank
+    tree[i] = r < S ? sorted[int64_t(r) * k] : kPadKey;
+}
+
+// #keys of bucket b (keys sorted[b*k .. min(b*k + k, M))) that are <= x, and that are < x;
+// first = the bucket's smallest key (its splitter)
+template <int K>
+__device__ __forceinline__ void bucket_counts(const unsigned* __restrict__ sorted, int64_t M, int64_t b,
+                                              unsigned x, int& le, int& lt, unsigned& first) {
+    const int64_t base = b * K;
+    unsigned v[K];
+    if constexpr (K >= 4) {
+#pragma unroll
+        for (int q = 0; q < K / 4; ++q) {
+            const uint4 u = reinterpret_cast<const uint4*>(sorted + base)[q];
+            v[4 * q] = u.x;
+            v[4 * q + 1] = u.y;
+            v[4 * q + 2] = u.z;
+            v[4 * q + 3] = u.w;
+        }
+    } else if constexpr (K == 2) {
+        const uint2 u = *reinterpret_cast<const uint2*>(sorted + base);
+        v[0] = u.x;
+        v[1] = u.y;
+    } else {
+        v[0] = sorted[base];
+    }
+    first = v[0];
+    le = 0;
+    lt = 0;
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        const bool in = base + j < M;  // the tail bucket reads past M inside the workspace
+        le += in && v[j] <= x;
+        lt += in && v[j] < x;
+    }
+}
+
+// #keys in sorted[lo, hi) that are < x (LT) or <= x (!LT): binary search in global memory
+template <bool LT>
+__device__ __forceinline__ int64_t count_below(const unsigned* __restrict__ a, int64_t lo, int64_t hi, unsigned x) {
+    int64_t len = hi - lo, base = lo;
     while (len > 0) {
         const int64_t half = len >> 1;
-        if (a[lo + half] < k) {
-            lo += half + 1;
+        const unsigned v = a[base + half];
+        if (LT ? v < x : v <= x) {
+            base += half + 1;
             len -= half + 1;
         } else {
             len = half;
         }
     }
-    return lo;
+    return base - lo;
 }
 
-__device__ __forceinline__ int64_t upper_bound_u32(const unsigned* __restrict__ a, int64_t n, unsigned k) {
-    int64_t lo = 0, len = n;
-    while (len > 0) {
-        const int64_t half = len >> 1;
-        if (a[lo + half] <= k) {
-            lo += half + 1;
-            len -= half + 1;
-        } else {
-            len = half;
+// K = 0: buckets of k > 32 keys, finished by binary searches in global memory
+template <int K, bool TABLE_POS>
+__device__ __forceinline__ void count_query(unsigned x, const unsigned* __restrict__ tree, int h, int k,
+                                            const unsigned* __restrict__ sorted, int64_t M,
+                                            unsigned long long& w, unsigned long long& t) {
+    // splitters <= x (walk i) and < x = <= x - 1 (walk j; finite keys are >= 0x00800000, so
+    // x - 1 never wraps)
+    const unsigned xm = x - 1u;
+    int64_t su, sl = 0;
+    if constexpr (K <= 1) {
+        unsigned i = 1, j = 1;
+        for (int d = 0; d < h; ++d) {
+            const unsigned a = tree[i], c = tree[j];
+            i = 2 * i + (a <= x);
+            j = 2 * j + (c <= xm);
+        }
+        su = int64_t(i) - (int64_t(1) << h);
+        sl = int64_t(j) - (int64_t(1) << h);
+    } else {
+        unsigned i = 1;
+        for (int d = 0; d < h; ++d) i = 2 * i + (tree[i] <= x);
+        su = int64_t(i) - (int64_t(1) << h);
+    }
+    int64_t ub, lb;
+    if constexpr (K == 1) {
+        ub = su;
+        lb = sl;
+    } else if constexpr (K == 0) {
+        ub = 0;
+        lb = 0;
+        if (su > 0) {
+            const int64_t b0 = (su - 1) * k, b1 = (b0 + k < M) ? b0 + k : M;
+            ub = b0 + count_below<false>(sorted, b0, b1, x);
+        }
+        if (sl > 0) {
+            const int64_t b0 = (sl - 1) * k, b1 = (b0 + k < M) ? b0 + k : M;
+            lb = b0 + count_below<true>(sorted, b0, b1, x);
+        }
+    } else {
+        // one walk for x; the walk for x - 1 is needed only when the last splitter <= x
+        // equals x (a run of x may then start in an earlier bucket)
+        ub = 0;
+        lb = 0;
+        if (su > 0) {
+            int le = 0, lt = 0;
+            unsigned first = 0;
+            bucket_counts<K>(sorted, M, su - 1, x, le, lt, first);
+            ub = (su - 1) * K + le;
+            if (first < x) {
+                lb = (su - 1) * K + lt;
+            } else {
+                unsigned j = 1;
+                for (int d = 0; d < h; ++d) j = 2 * j + (tree[j] <= xm);
+                const int64_t sl = int64_t(j) - (int64_t(1) << h);
+                if (sl > 0) {
+                    bucket_counts<K>(sorted, M, sl - 1, x, le, lt, first);
+                    lb = (sl - 1) * K + lt;
+                }
+            }
         }
     }
-    return lo;
+    w += TABLE_POS ? static_cast<unsigned long long>(M - ub) : static_cast<unsigned long long>(lb);
+    t += static_cast<unsigned long long>(ub - lb);
 }
 
-__global__ __launch_bounds__(kSortThreads) void search_count_kernel(const float* __restrict__ pos, int64_t P,
-                                                                    const unsigned* __restrict__ sorted,
-                                                                    int64_t N,
-                                                                    unsigned long long* __restrict__ out) {
-    __shared__ unsigned long long red[2][kSortThreads / kWave];
+template <int K, bool TABLE_POS>
+__global__ __launch_bounds__(kQueryThreads) void query_count_kernel(const float* __restrict__ q, int64_t L,
+                                                                   const unsigned* __restrict__ gtree, int h, int k,
+                                                                   const unsigned* __restrict__ sorted, int64_t M,
+                                                                   unsigned long long* __restrict__ out) {
+    extern __shared__ unsigned tree[];
+    for (int i = threadIdx.x; i < (1 << h); i += kQueryThreads) tree[i] = gtree[i];
+    __syncthreads();
     unsigned long long w = 0, t = 0;
-    for (int64_t i = int64_t(blockIdx.x) * kSortThreads + threadIdx.x; i < P;
-         i += int64_t(gridDim.x) * kSortThreads) {
-        const unsigned k = key_of(pos[i]);
-        const int64_t lb = lower_bound_u32(sorted, N, k);
-        // ties: the run of equal keys starts at lb; search only the tail
-        const int64_t ub = lb + upper_bound_u32(sorted + lb, N - lb, k);
-        w += static_cast<unsigned long long>(lb);
-        t += static_cast<unsigned long long>(ub - lb);
+    const bool vec = (reinterpret_cast<uintptr_t>(q) & 15u) == 0;
+    const int64_t nvec = vec ? L / 4 : 0;
+    const int64_t stride = int64_t(gridDim.x) * kQueryThreads;
+    for (int64_t v = int64_t(blockIdx.x) * kQueryThreads + threadIdx.x; v < nvec; v += stride) {
+        const f32x4 f = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(q) + v);
+        count_query<K, TABLE_POS>(key_of(f.x), tree, h, k, sorted, M, w, t);
+        count_query<K, TABLE_POS>(key_of(f.y), tree, h, k, sorted, M, w, t);
+        count_query<K, TABLE_POS>(key_of(f.z), tree, h, k, sorted, M, w, t);
+        count_query<K, TABLE_POS>(key_of(f.w), tree, h, k, sorted, M, w, t);
     }
+    for (int64_t i = nvec * 4 + int64_t(blockIdx.x) * kQueryThreads + threadIdx.x; i < L; i += stride)
+        count_query<K, TABLE_POS>(key_of(q[i]), tree, h, k, sorted, M, w, t);
+    __shared__ unsigned long long red[2][kQueryThreads / kWave];
     w = wave_sum(w);
     t = wave_sum(t);
     const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
@@ -212,13 +334,50 @@ __global__ __launch_bounds__(kSortThreads) void search_count_kernel(const float*
     __syncthreads();
     if (threadIdx.x == 0) {
         unsigned long long bw = 0, bt = 0;
-        for (int i = 0; i < kSortThreads / kWave; ++i) {
+        for (int i = 0; i < kQueryThreads / kWave; ++i) {
             bw += red[0][i];
             bt += red[1][i];
         }
         if (bw) atomicAdd(out + 0, bw);
         if (bt) atomicAdd(out + 1, bt);
     }
+}
+
+int query_grid(int64_t L) {
+    static int cus = 0;
+    if (cus == 0) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) {
+            (void)hipGetLastError();
+            cus = 256;
+        }
+    }
+    int64_t g = (L + 4 * kQueryThreads - 1) / (4 * kQueryThreads);
+    if (g > cus) g = cus;  // one 1024-thread workgroup per CU (64 KB of LDS each)
+    if (g < 1) g = 1;
+    return static_cast<int>(g);
+}
+
+template <bool TABLE_POS>
+int launch_query(int k, const float* q, int64_t L, const unsigned* tree, int h, const unsigned* sorted, int64_t M,
+                 unsigned long long* out, hipStream_t st) {
+    const dim3 grid(query_grid(L)), block(kQueryThreads);
+    const size_t lds = size_t(1) << h << 2;
+    if (k > 32) {
+        hipLaunchKernelGGL((query_count_kernel<0, TABLE_POS>), grid, block, lds, st, q, L, tree, h, k, sorted, M, out);
+        return launch_status();
+    }
+    switch (k) {
+        case 1: hipLaunchKernelGGL((query_count_kernel<1, TABLE_POS>), grid, block, lds, st, q, L, tree, h, k, sorted, M, out); break;
+        case 2: hipLaunchKernelGGL((query_count_kernel<2, TABLE_POS>), grid, block, lds, st, q, L, tree, h, k, sorted, M, out); break;
+        case 4: hipLaunchKernelGGL((query_count_kernel<4, TABLE_POS>), grid, block, lds, st, q, L, tree, h, k, sorted, M, out); break;
+        case 8: hipLaunchKernelGGL((query_count_kernel<8, TABLE_POS>), grid, block, lds, st, q, L, tree, h, k, sorted, M, out); break;
+        case 16: hipLaunchKernelGGL((query_count_kernel<16, TABLE_POS>), grid, block, lds, st, q, L, tree, h, k, sorted, M, out); break;
+        case 32: hipLaunchKernelGGL((query_count_kernel<32, TABLE_POS>), grid, block, lds, st, q, L, tree, h, k, sorted, M, out); break;
+        default: return DAUC_EINVAL;
+    }
+    return launch_status();
 }
 
 struct SortWs {
@@ -265,9 +424,14 @@ int radix_sort_keys(const float* neg, int64_t N, const SortWs& w, hipStream_t st
         else
             hipLaunchKernelGGL(radix_hist_kernel<false>, dim3(w.ntiles), dim3(kSortThreads), 0, st,
                                static_cast<const void*>(src), N, shift, w.hist, w.ntiles);
-        hipLaunchKernelGGL(scan_blocks_kernel, dim3(w.nsum), dim3(kScanBlock), 0, st, w.hist, w.m, w.sums);
-        hipLaunchKernelGGL(scan_sums_kernel, dim3(1), dim3(kScanBlock), 0, st, w.sums, w.nsum);
-        hipLaunchKernelGGL(scan_add_kernel, dim3(w.nsum), dim3(kScanBlock), 0, st, w.hist, w.m, w.sums);
+        if (w.m <= kSingleScan) {
+            // small sorts are launch-bound: one workgroup scans the whole histogram array
+            hipLaunchKernelGGL(scan_sums_kernel, dim3(1), dim3(kScanBlock), 0, st, w.hist, w.m);
+        } else {
+            hipLaunchKernelGGL(scan_blocks_kernel, dim3(w.nsum), dim3(kScanBlock), 0, st, w.hist, w.m, w.sums);
+            hipLaunchKernelGGL(scan_sums_kernel, dim3(1), dim3(kScanBlock), 0, st, w.sums, w.nsum);
+            hipLaunchKernelGGL(scan_add_kernel, dim3(w.nsum), dim3(kScanBlock), 0, st, w.hist, w.m, w.sums);
+        }
         if (pass == 0)
             hipLaunchKernelGGL(radix_scatter_kernel<true>, dim3(w.ntiles), dim3(kSortThreads), 0, st,
                                static_cast<const void*>(neg), N, shift, w.hist, w.ntiles, dst);
@@ -290,7 +454,7 @@ using namespace dauc;
 
 extern "C" {
 
-size_t dauc_sort_workspace_size(int64_t N) { return sort_ws_bytes(N < 1 ? 1 : N); }
+size_t dauc_sort_workspace_size(int64_t n) { return sort_ws_bytes(n < 1 ? 1 : n) + kTreeBytes + 256; }
 
 int dauc_sort_keys(const float* scores, int64_t n, unsigned* keys_out, void* workspace,
                    size_t workspace_bytes, dauc_stream_t stream) {
@@ -312,17 +476,27 @@ int dauc_auc_counts_sorted(const float* pos, int64_t P, const float* neg, int64_
         (N > 0 && neg == nullptr))
         return DAUC_EINVAL;
     if (P == 0 || N == 0) return DAUC_OK;
-    if (workspace == nullptr || workspace_bytes < sort_ws_bytes(N) || N > 0xffffffffLL) return DAUC_EINVAL;
+    // the smaller class is sorted (the table); the larger one streams through the search
+    const bool table_pos = P <= N;
+    const int64_t M = table_pos ? P : N, L = table_pos ? N : P;
+    if (workspace == nullptr || workspace_bytes < dauc_sort_workspace_size(M) || M > 0xffffffffLL) return DAUC_EINVAL;
     hipStream_t st = as_hip(stream);
-    SortWs w = carve(workspace, N);
+    SortWs w = carve(workspace, M);
     const unsigned* sorted = nullptr;
-    int rc = radix_sort_keys(neg, N, w, st, &sorted);
+    int rc = radix_sort_keys(table_pos ? pos : neg, M, w, st, &sorted);
     if (rc) return rc;
-    int64_t grid = (P + kSortThreads - 1) / kSortThreads;
-    if (grid > 4096) grid = 4096;
-    hipLaunchKernelGGL(search_count_kernel, dim3(grid), dim3(kSortThreads), 0, st, pos, P, sorted, N,
-                       wins_ties);
-    return launch_status();
+    int k = 1;
+    while ((M + k - 1) / k > kMaxSplit) k *= 2;
+    const int S = static_cast<int>((M + k - 1) / k);
+    int h = 1;
+    while ((1 << h) - 1 < S) ++h;
+    unsigned* tree = reinterpret_cast<unsigned*>(static_cast<char*>(workspace) + ((sort_ws_bytes(M) + 255) / 256) * 256);
+    hipLaunchKernelGGL(build_tree_kernel, dim3(((1 << h) + 255) / 256), dim3(256), 0, st, sorted, M, k, S, h, tree);
+    rc = launch_status();
+    if (rc) return rc;
+    const float* q = table_pos ? neg : pos;
+    return table_pos ? launch_query<true>(k, q, L, tree, h, sorted, M, wins_ties, st)
+                     : launch_query<false>(k, q, L, tree, h, sorted, M, wins_ties, st);
 }
 
 }  // extern "C"

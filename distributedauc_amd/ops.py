@@ -353,7 +353,8 @@ def pair_count(pos: torch.Tensor, neg: torch.Tensor, wins_ties: torch.Tensor, va
 
 
 def auc_counts_sorted(pos: torch.Tensor, neg: torch.Tensor, wins_ties: torch.Tensor) -> None:
-    """Same (wins, ties) accumulation as pair_count, by radix-sorting neg and binary-searching pos."""
+    """Same (wins, ties) accumulation as pair_count, by radix-sorting the smaller class and
+    locating every score of the larger one in it (LDS search tree + one bucket load)."""
     _require(pos, "pos", torch.float32)
     dev = pos.device
     _require(neg, "neg", torch.float32, dev)
@@ -363,7 +364,7 @@ def auc_counts_sorted(pos: torch.Tensor, neg: torch.Tensor, wins_ties: torch.Ten
     if wins_ties.numel() < 2 or not wins_ties.is_contiguous():
         raise ValueError("wins_ties needs 2 contiguous int64 slots")
     L = _lib.load()
-    ws = workspaces.get(dev, "sort", L.dauc_sort_workspace_size(max(neg.numel(), 1)))
+    ws = workspaces.get(dev, "sort", L.dauc_sort_workspace_size(max(min(pos.numel(), neg.numel()), 1)))
     check(L.dauc_auc_counts_sorted(_ptr(pos), pos.numel(), _ptr(neg), neg.numel(), _ptr(wins_ties), _ptr(ws),
                                    ws.numel(), _stream(dev)), "dauc_auc_counts_sorted")
 

@@ -237,14 +237,19 @@ int dauc_pair_count(const float* pos, int64_t P, const float* neg, int64_t N,
 int dauc_pair_count_variant(const float* pos, int64_t P, const float* neg, int64_t N,
                             unsigned long long* wins_ties, int variant, dauc_stream_t stream);
 
-/* Bytes of scratch dauc_auc_counts_sorted / dauc_sort_keys need for N negatives (no zeroing needed). */
-size_t dauc_sort_workspace_size(int64_t N);
+/*
+ * Bytes of scratch dauc_sort_keys needs for n keys, and dauc_auc_counts_sorted needs for
+ * n = min(P, N) (the smaller class is the one sorted). No zeroing needed.
+ */
+size_t dauc_sort_workspace_size(int64_t n);
 
 /*
  * Same counts as dauc_pair_count by sorting instead of enumerating pairs
- * (SURVEY §8f row 1): LSD radix sort of the negatives' order-preserving uint32
- * keys (-0 == +0), then lower/upper-bound searches per positive.
- * O(N + P log N); wins_ties accumulates like dauc_pair_count.
+ * (SURVEY §8f row 1): LSD radix sort of the smaller class's order-preserving uint32
+ * keys (-0 == +0), then every score of the larger class is located in it through an
+ * LDS-resident search tree of every k-th key plus one bucket load (upper_bound and
+ * lower_bound). O(M log M + L log M), M = min(P, N), L = max(P, N); wins_ties
+ * accumulates like dauc_pair_count. Scores must be finite.
  */
 int dauc_auc_counts_sorted(const float* pos, int64_t P, const float* neg, int64_t N,
                            unsigned long long* wins_ties, void* workspace, size_t workspace_bytes,

@@ -103,7 +103,8 @@ def bench_paircount(dev, reps, log2n):
     n = 1 << log2n
     g = torch.Generator(device=dev).manual_seed(2024)
     s = torch.rand(n, device=dev, generator=g)
-    y = torch.where(torch.rand(n, device=dev, generator=g) < 0.01, 1, -1).to(torch.int8)
+    prate = float(os.environ.get("DAUC_MICRO_POS_RATE", "0.01"))
+    y = torch.where(torch.rand(n, device=dev, generator=g) < prate, 1, -1).to(torch.int8)
     pos, neg, st = ops.split_scores(s, y)
     P, N = st[0].item(), st[1].item()
     pos, neg = pos[:P].contiguous(), neg[:N].contiguous()
@@ -115,6 +116,8 @@ def bench_paircount(dev, reps, log2n):
     med, mn = timeit(lambda: ops.auc_counts_sorted(pos, neg, wt), reps * 5)
     emit(kernel="auc_counts_sorted", P=P, N=N, us=med * 1e3, us_min=mn * 1e3,
          effective_pairs_per_s=P * N / med * 1e3, keys_GBps=N * 4 * 12 / med / 1e6)
+    if os.environ.get("DAUC_MICRO_SORT_ONLY"):
+        return
     ref = sorted_counts
     for v in range(12):
         wt = torch.zeros(2, dtype=torch.int64, device=dev)

@@ -356,7 +356,8 @@ def test_auc_counts_large(dev, n, p, ties):
 
 
 def test_auc_sharded_sum_is_invariant(dev):
-    """Positive-block sharding over G ranks sums to the unsharded counts for every G."""
+    """Sharding over G ranks (pairs: positive blocks; sort: the larger class, the one streamed
+    through the search) sums to the unsharded counts for every G."""
     rng = np.random.default_rng(4)
     n = 300_000
     s = (np.floor(rng.random(n) * 1000) / 1000).astype(np.float32)
@@ -487,6 +488,31 @@ def test_sorted_counts_match_pair_count(dev, P, N):
     assert a.tolist() == b.tolist()
     if P * N <= 10_000_000:
         assert tuple(a.tolist()) == coracle.pair_count_bruteforce(pos, neg)
+
+
+@pytest.mark.parametrize("M,L,table_pos", [(10_000, 300_000, True), (20_000, 50_000, True), (60_000, 70_000, False),
+                                            (100_000, 2_000_000, True), (250_000, 260_000, False),
+                                            (400_000, 1_000_000, True), (600_000, 700_000, True),
+                                            (700_000, 600_000, False)])
+def test_sorted_counts_bucket_sizes(dev, M, L, table_pos):
+    """The search tree holds every k-th key of the sorted smaller class (k = 1 .. 32: one bucket
+    load; k > 32: binary search in global memory). Every k, and both table sides, vs the pair-count
+    kernel on tie-heavy scores (ties at splitter boundaries included), bit-exact."""
+    from distributedauc_amd import ops
+
+    rng = np.random.default_rng(M + L)
+    P, N = (M, L) if table_pos else (L, M)
+    pos = (np.floor(rng.random(P) * 5003) / 5003 - 0.3).astype(np.float32)
+    neg = (np.floor(rng.random(N) * 5003) / 5003 - 0.5).astype(np.float32)
+    neg[rng.random(N) < 0.05] = -0.0
+    pos[rng.random(P) < 0.05] = 0.0
+    a = torch.zeros(2, dtype=torch.int64, device=dev)
+    b = torch.zeros(2, dtype=torch.int64, device=dev)
+    ops.pair_count(T(pos, dev), T(neg, dev), a)
+    ops.auc_counts_sorted(T(pos, dev), T(neg, dev), b)
+    assert a.tolist() == b.tolist()
+    if M <= 20_000 and L <= 300_000:
+        assert tuple(b.tolist()) == coracle.pair_count_bruteforce(pos, neg)
 
 
 @pytest.mark.parametrize("zdtype", [torch.float32, torch.bfloat16])
