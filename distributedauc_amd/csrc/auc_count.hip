@@ -24,33 +24,82 @@ namespace dauc {
 namespace {
 
 // ============================ stable split ====================================
+//
+// Tiles of 8192 scores per workgroup; a thread handles kSlots float4 slots, slot k of thread t
+// covering scores tile0 + (k*256 + t)*4 + [0, 4) (every load instruction of a wave reads 1 KB
+// contiguous). Tile order = k-major, then thread, then the 4 lanes of the float4.
 
 constexpr int kSplitThreads = 256;
-constexpr int kSplitPerThread = 16;
-constexpr int kSplitTile = kSplitThreads * kSplitPerThread;  // 4096 scores per block
+constexpr int kSlots = 8;
+constexpr int kSplitTile = kSplitThreads * 4 * kSlots;  // 8192 scores per block
 constexpr int kScanThreads = 1024;
 
 int64_t split_blocks(int64_t n) { return (n + kSplitTile - 1) / kSplitTile; }
 
+// label class of 4 consecutive scores: 1 (positive), -1 (negative), 2 (other), 0 (past n)
 template <typename LT>
-__device__ __forceinline__ bool is_pos(const LT* __restrict__ lab, int64_t i) {
-    return lab[i] == LT(1);
+__device__ __forceinline__ void load_labels4(const LT* __restrict__ lab, int64_t i, int64_t n, bool full,
+                                             int (&l)[4]) {
+    if (full && sizeof(LT) == 1) {
+        const char4 c = *reinterpret_cast<const char4*>(lab + i);
+        const int r[4] = {c.x, c.y, c.z, c.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) l[q] = r[q] == 1 ? 1 : (r[q] == -1 ? -1 : 2);
+    } else if (full && sizeof(LT) == 4) {
+        const int4 c = *reinterpret_cast<const int4*>(lab + i);
+        const int r[4] = {c.x, c.y, c.z, c.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) l[q] = r[q] == 1 ? 1 : (r[q] == -1 ? -1 : 2);
+    } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            if (i + q < n) {
+                const LT v = lab[i + q];
+                l[q] = v == LT(1) ? 1 : (v == LT(-1) ? -1 : 2);
+            } else {
+                l[q] = 0;
+            }
+        }
+    }
+}
+
+__device__ __forceinline__ void load_scores4(const float* __restrict__ s, int64_t i, int64_t n, bool full,
+                                             float (&v)[4]) {
+    if (full) {
+        const f32x4 x = *reinterpret_cast<const f32x4*>(s + i);
+        v[0] = x.x;
+        v[1] = x.y;
+        v[2] = x.z;
+        v[3] = x.w;
+    } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = i + q < n ? s[i + q] : 0.0f;
+    }
 }
 
 // pass 1: per-block positive count, non-finite scores, labels outside {-1, 1}
 template <typename LT>
 __global__ __launch_bounds__(kSplitThreads) void split_count_kernel(
-    const float* __restrict__ s, const LT* __restrict__ lab, int64_t n, int* __restrict__ blk) {
+    const float* __restrict__ s, const LT* __restrict__ lab, int64_t n, int vec, int* __restrict__ blk) {
     __shared__ int part[3][kSplitThreads / kWave];
     const int64_t base = int64_t(blockIdx.x) * kSplitTile;
     int np = 0, nf = 0, no = 0;
-    for (int k = 0; k < kSplitPerThread; ++k) {
-        const int64_t i = base + int64_t(k) * kSplitThreads + threadIdx.x;
-        if (i < n) {
-            const LT l = lab[i];
-            np += (l == LT(1));
-            no += (l != LT(1) && l != LT(-1));
-            nf += !isfinite(s[i]);
+    float v[kSlots][4];
+    int l[kSlots][4];
+#pragma unroll
+    for (int k = 0; k < kSlots; ++k) {
+        const int64_t i = base + (int64_t(k) * kSplitThreads + threadIdx.x) * 4;
+        const bool full = vec && i + 4 <= n;
+        load_scores4(s, i, n, full, v[k]);
+        load_labels4(lab, i, n, full, l[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < kSlots; ++k) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            np += l[k][q] == 1;
+            no += l[k][q] == 2;
+            nf += l[k][q] != 0 && !isfinite(v[k][q]);
         }
     }
     for (int off = 32; off > 0; off >>= 1) {
@@ -130,41 +179,65 @@ __global__ __launch_bounds__(kScanThreads) void split_scan_kernel(const int* __r
     }
 }
 
-// pass 3: order-preserving scatter, 256 scores at a time per block
+// pass 3: order-preserving scatter of one tile. Each wave ballots its positives per slot and
+// float4 lane, one barrier publishes the per-(slot, wave) counts, and every score's rank among
+// the tile's positives (a negative's: its tile position minus that rank) follows from the
+// counts before it in tile order plus the ballot bits of the lower lanes.
 template <typename LT>
 __global__ __launch_bounds__(kSplitThreads) void split_write_kernel(
-    const float* __restrict__ s, const LT* __restrict__ lab, int64_t n,
-    const int64_t* __restrict__ pos_base, float* __restrict__ pos_out,
-    float* __restrict__ neg_out) {
-    __shared__ int wave_cnt[kSplitThreads / kWave];
+    const float* __restrict__ s, const LT* __restrict__ lab, int64_t n, int vec,
+    const int64_t* __restrict__ pos_base, float* __restrict__ pos_out, float* __restrict__ neg_out) {
+    constexpr int kW = kSplitThreads / kWave;
+    __shared__ int cnt[kSlots * kW];
     const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
     const int64_t tile0 = int64_t(blockIdx.x) * kSplitTile;
     const int64_t pbase = pos_base[blockIdx.x];
     const int64_t nbase = tile0 - pbase;
     const unsigned long long lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    int64_t run_pos = 0;  // positives already written by this block
-    for (int k = 0; k < kSplitPerThread; ++k) {
-        const int64_t t = int64_t(k) * kSplitThreads + threadIdx.x;  // index inside the tile
-        const int64_t i = tile0 + t;
-        const bool valid = i < n;
-        const bool p = valid && is_pos(lab, i);
-        const unsigned long long m = __ballot(p);
-        if (lane == 0) wave_cnt[wid] = __popcll(m);
-        __syncthreads();
-        int before = 0, chunk = 0;
-        for (int w = 0; w < kSplitThreads / kWave; ++w) {
-            const int c = wave_cnt[w];
-            before += (w < wid) ? c : 0;
-            chunk += c;
+    float v[kSlots][4];
+    int l[kSlots][4];
+#pragma unroll
+    for (int k = 0; k < kSlots; ++k) {
+        const int64_t i = tile0 + (int64_t(k) * kSplitThreads + threadIdx.x) * 4;
+        const bool full = vec && i + 4 <= n;
+        load_scores4(s, i, n, full, v[k]);
+        load_labels4(lab, i, n, full, l[k]);
+    }
+    int below[kSlots];  // positives of this wave's lower lanes in slot k
+#pragma unroll
+    for (int k = 0; k < kSlots; ++k) {
+        int tot = 0, low = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const unsigned long long m = __ballot(l[k][q] == 1);
+            tot += __popcll(m);
+            low += __popcll(m & lt_mask);
         }
-        const int64_t pos_rank = run_pos + before + __popcll(m & lt_mask);
-        if (valid) {
-            const float v = s[i];
-            if (p) pos_out[pbase + pos_rank] = v;
-            else neg_out[nbase + (t - pos_rank)] = v;
+        below[k] = low;
+        if (lane == 0) cnt[k * kW + wid] = tot;
+    }
+    __syncthreads();
+    int run = 0;  // positives of the tile before slot k
+#pragma unroll
+    for (int k = 0; k < kSlots; ++k) {
+        int before = run;
+#pragma unroll
+        for (int w = 0; w < kW; ++w) {
+            const int c = cnt[k * kW + w];
+            before += w < wid ? c : 0;
+            run += c;
         }
-        run_pos += chunk;
-        __syncthreads();
+        int r = before + below[k];  // rank of this thread's first score of slot k
+        const int64_t t = (int64_t(k) * kSplitThreads + threadIdx.x) * 4;  // position in the tile
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            if (l[k][q] == 1) {
+                pos_out[pbase + r] = v[k][q];
+                ++r;
+            } else if (l[k][q] != 0) {
+                neg_out[nbase + (t + q - r)] = v[k][q];
+            }
+        }
     }
 }
 
@@ -174,7 +247,9 @@ int launch_split(const float* s, const LT* lab, int64_t n, float* pos_out, float
     const int64_t nblk = split_blocks(n);
     int64_t* pos_base = static_cast<int64_t*>(ws);
     int* blk = reinterpret_cast<int*>(pos_base + nblk);
-    hipLaunchKernelGGL(split_count_kernel<LT>, dim3(nblk), dim3(kSplitThreads), 0, st, s, lab, n,
+    const int vec = (reinterpret_cast<uintptr_t>(s) & 15u) == 0 &&
+                    (reinterpret_cast<uintptr_t>(lab) & (4 * sizeof(LT) - 1)) == 0;
+    hipLaunchKernelGGL(split_count_kernel<LT>, dim3(nblk), dim3(kSplitThreads), 0, st, s, lab, n, vec,
                        blk);
     int rc = launch_status();
     if (rc) return rc;
@@ -182,7 +257,7 @@ int launch_split(const float* s, const LT* lab, int64_t n, float* pos_out, float
                        pos_base, stats);
     rc = launch_status();
     if (rc) return rc;
-    hipLaunchKernelGGL(split_write_kernel<LT>, dim3(nblk), dim3(kSplitThreads), 0, st, s, lab, n,
+    hipLaunchKernelGGL(split_write_kernel<LT>, dim3(nblk), dim3(kSplitThreads), 0, st, s, lab, n, vec,
                        pos_base, pos_out, neg_out);
     return launch_status();
 }
