@@ -9,13 +9,14 @@ float is within a few ulp of sklearn's trapezoid sum.
 
 Two exact methods give the same integers: ``method="pairs"`` runs the LDS-tiled
 pair-count kernel (O(P*N), the north-star kernel) and ``method="sort"`` (default)
-radix-sorts the negatives and binary-searches every positive (O(N + P log N),
-SURVEY §8f row 1).
+radix-sorts the smaller class and locates every score of the larger class in it
+through an LDS search tree (O(M log M + L log M)).
 
-Sharding (north star): every rank holds the same score vector; rank
-r compares positives [r*P/G, (r+1)*P/G) of the stable split against ALL
-negatives, and one int64 [2] all-reduce sums (W, T). The result does not depend
-on G.
+Sharding (north star): every rank holds the same score vector. The
+pair-count method gives rank r the positives [r*P/G, (r+1)*P/G) of the stable
+split against ALL negatives; the sort method gives rank r a slice of the larger
+class against all of the smaller one. One int64 [2] all-reduce sums (W, T); the
+result does not depend on G.
 
 Error behaviour mirrors sklearn: non-finite scores raise ValueError; labels
 with more than two distinct values raise ValueError; a single class returns NaN
