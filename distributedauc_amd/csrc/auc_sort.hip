@@ -17,7 +17,7 @@
 //             tile's keys with the same digit comes from 8 wave ballots (wave multisplit)
 //             plus per-digit wave/chunk offsets in LDS, so the scatter is STABLE (LSD
 //             correctness needs it); writes to out[offset[digit][tile] + rank].
-// Search: every k-th sorted key (k a power of two, so at most 16383 splitters) goes into an
+// Search: every k-th sorted key (k a power of two, so at most 32767 splitters) goes into an
 //   Eytzinger (BFS-order) tree, which every workgroup loads into LDS once; one query key x
 //   walks it twice in lockstep (x and x - 1: the splitters <= x and < x; BFS order puts
 //   each level's nodes side by side, so a level's reads spread over the LDS banks instead
@@ -168,7 +168,14 @@ __global__ __launch_bounds__(kSortThreads) void radix_scatter_kernel(const void*
 
 // ---- search ---------------------------------------------------------------------------
 
-constexpr int kMaxSplit = 16383;          // splitters: a perfect tree of depth <= 14 (64 KB of LDS)
+#ifndef DAUC_QUERY_MAX_DEPTH
+#define DAUC_QUERY_MAX_DEPTH 15
+#endif
+#ifndef DAUC_QUERY_BLOCKS_PER_CU
+#define DAUC_QUERY_BLOCKS_PER_CU 1
+#endif
+// splitters: a perfect tree of depth <= 15 (128 KB of LDS; bucket size k halves per level)
+constexpr int kMaxSplit = (1 << DAUC_QUERY_MAX_DEPTH) - 1;
 constexpr int kTreeSlots = kMaxSplit + 1;  // 1-based BFS array
 constexpr size_t kTreeBytes = size_t(kTreeSlots) * 4;
 constexpr int kQueryThreads = 1024;
@@ -354,7 +361,7 @@ int query_grid(int64_t L) {
         }
     }
     int64_t g = (L + 4 * kQueryThreads - 1) / (4 * kQueryThreads);
-    if (g > cus) g = cus;  // one 1024-thread workgroup per CU (64 KB of LDS each)
+    if (g > DAUC_QUERY_BLOCKS_PER_CU * cus) g = DAUC_QUERY_BLOCKS_PER_CU * cus;  // 1024-thread workgroups
     if (g < 1) g = 1;
     return static_cast<int>(g);
 }

@@ -493,10 +493,11 @@ def test_sorted_counts_match_pair_count(dev, P, N):
 @pytest.mark.parametrize("M,L,table_pos", [(10_000, 300_000, True), (20_000, 50_000, True), (60_000, 70_000, False),
                                             (100_000, 2_000_000, True), (250_000, 260_000, False),
                                             (400_000, 1_000_000, True), (600_000, 700_000, True),
-                                            (700_000, 600_000, False)])
+                                            (700_000, 600_000, False), (1_100_000, 1_300_000, True)])
 def test_sorted_counts_bucket_sizes(dev, M, L, table_pos):
-    """The search tree holds every k-th key of the sorted smaller class (k = 1 .. 32: one bucket
-    load; k > 32: binary search in global memory). Every k, and both table sides, vs the pair-count
+    """The search tree holds every k-th key of the sorted smaller class (<= 32767 splitters, so
+    these sizes give k = 1, 2, 4, 8, 16, 32 (one bucket load) and 64 (k > 32: binary search in
+    global memory)). Every k, and both table sides, vs the pair-count
     kernel on tie-heavy scores (ties at splitter boundaries included), bit-exact."""
     from distributedauc_amd import ops
 
