@@ -188,7 +188,7 @@ def bench_auc(args, world, rank, device, log2n=None, pos=None, pair_reps=None):
     s = torch.rand(n, generator=g, device=device)
     y = torch.where(torch.rand(n, generator=g, device=device) < pos, 1, -1).to(torch.int8)
     out = {"n": n, "log2n": log2n, "pos": pos, "scores": s, "labels": y}
-    for method, fn in (("sort", "dauc_auc_counts_sorted"), ("pairs", "dauc_pair_count_variant")):
+    for method, fn in (("sort", "dauc_auc_counts_sorted_labeled"), ("pairs", "dauc_pair_count_variant")):
         ev = ExactAUC(world=world, rank=rank, variant=args.variant, method=method)
         kt = KernelTimer(_lib.load(), fn)
         c = ev.counts(y, s)  # warm-up
@@ -225,9 +225,11 @@ def auc_record(auc, world, config_name):
     pc_rate = npairs / pk["t_count"]
     return {
         "workload": f"exact AUC, 2^{auc['log2n']} fp32 scores, {auc['pos']:.1%} positives "
-                    f"(BASELINE {config_name}), sharded by positive blocks, int64 all-reduce",
+                    f"(BASELINE {config_name}), sharded over ranks (sort: score-index ranges; pair count: "
+                    "positive blocks), int64 all-reduce",
         "pairs_per_sec": npairs / sk["t_eval"],
-        "method": "sort (radix sort of negatives + binary search; default evaluator)",
+        "method": "sort (default evaluator: split out the positives, radix-sort them, locate every negative "
+                  "through an LDS search tree, read in place)",
         "eval_ms": sk["t_eval"] * 1e3, "sort_count_ms": sk["t_count"] * 1e3,
         "P": auc["P"], "N": auc["N"], "wins": auc["wins"], "ties": auc["ties"], "auc": auc["auc"],
         "methods_agree": True,

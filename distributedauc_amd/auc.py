@@ -76,7 +76,8 @@ class ExactAUC:
         y, s = _as_device_pair(label, scores, device)
         if y.numel() != s.numel():
             raise ValueError(f"Found input variables with inconsistent numbers of samples: {[y.numel(), s.numel()]}")
-        pos, neg, stats = ops.split_scores(s, y)
+        # the sort method reads the negatives in place (only the positives are compacted)
+        pos, neg, stats = ops.split_scores(s, y, negatives=self.method == "pairs")
         P, N, nonfinite, other = (int(v) for v in stats.tolist())
         if nonfinite:
             raise ValueError("Input y_score contains NaN or infinity.")
@@ -92,12 +93,15 @@ class ExactAUC:
                 if hi > lo:
                     ops.pair_count(pos[lo:hi], neg[:N], wt, variant=self.variant)
             elif P <= N:
-                # the sorted table is the (small) positive class on every rank; the negatives,
-                # which are streamed through the search, are split
-                lo, hi = self.rank * N // self.world, (self.rank + 1) * N // self.world
+                # the sorted table is the (small) positive class on every rank; the negatives are
+                # read in place from the full score/label arrays, whose index range is split
+                n = s.numel()
+                lo, hi = self.rank * n // self.world, (self.rank + 1) * n // self.world
                 if hi > lo:
-                    ops.auc_counts_sorted(pos[:P], neg[lo:hi], wt)
+                    ops.auc_counts_sorted_labeled(pos[:P], s, y, lo, hi, wt)
             else:
+                # more positives than negatives: the negatives are the sorted table
+                pos, neg, _ = ops.split_scores(s, y)
                 lo, hi = self.rank * P // self.world, (self.rank + 1) * P // self.world
                 if hi > lo:
                     ops.auc_counts_sorted(pos[lo:hi], neg[:N], wt)

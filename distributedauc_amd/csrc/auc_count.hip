@@ -234,7 +234,7 @@ __global__ __launch_bounds__(kSplitThreads) void split_write_kernel(
             if (l[k][q] == 1) {
                 pos_out[pbase + r] = v[k][q];
                 ++r;
-            } else if (l[k][q] != 0) {
+            } else if (l[k][q] != 0 && neg_out != nullptr) {  // neg_out == NULL: positives only
                 neg_out[nbase + (t + q - r)] = v[k][q];
             }
         }
@@ -460,7 +460,7 @@ int dauc_split_scores(const float* scores, const void* labels, int label_dtype, 
                       float* pos_out, float* neg_out, int64_t* stats, void* workspace,
                       size_t workspace_bytes, dauc_stream_t stream) {
     if (n <= 0 || scores == nullptr || labels == nullptr || pos_out == nullptr ||
-        neg_out == nullptr || stats == nullptr || workspace == nullptr ||
+        stats == nullptr || workspace == nullptr ||
         workspace_bytes < dauc_split_workspace_size(n) ||
         (reinterpret_cast<uintptr_t>(workspace) & 7u))
         return DAUC_EINVAL;

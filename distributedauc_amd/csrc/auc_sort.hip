@@ -350,6 +350,90 @@ __global__ __launch_bounds__(kQueryThreads) void query_count_kernel(const float*
     }
 }
 
+// Labeled queries: the negatives are not materialised. Elements [begin, end) of the full score
+// and label arrays are streamed (float4 + 4 labels per slot); every element whose label is
+// not +1 is a query against the sorted positives (table = positives).
+template <typename LT>
+__device__ __forceinline__ void label4(const LT* __restrict__ lab, int64_t i, bool full, int64_t end, bool (&neg)[4]) {
+    if (full && sizeof(LT) == 1) {
+        const char4 c = *reinterpret_cast<const char4*>(lab + i);
+        neg[0] = c.x != 1;
+        neg[1] = c.y != 1;
+        neg[2] = c.z != 1;
+        neg[3] = c.w != 1;
+    } else if (full && sizeof(LT) == 4) {
+        const int4 c = *reinterpret_cast<const int4*>(lab + i);
+        neg[0] = c.x != 1;
+        neg[1] = c.y != 1;
+        neg[2] = c.z != 1;
+        neg[3] = c.w != 1;
+    } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) neg[q] = i + q < end && lab[i + q] != LT(1);
+    }
+}
+
+template <int K, typename LT>
+__global__ __launch_bounds__(kQueryThreads) void query_labeled_kernel(const float* __restrict__ s,
+                                                                     const LT* __restrict__ lab, int64_t begin,
+                                                                     int64_t end, const unsigned* __restrict__ gtree,
+                                                                     int h, int k, const unsigned* __restrict__ sorted,
+                                                                     int64_t M, unsigned long long* __restrict__ out) {
+    extern __shared__ unsigned tree[];
+    for (int i = threadIdx.x; i < (1 << h); i += kQueryThreads) tree[i] = gtree[i];
+    __syncthreads();
+    unsigned long long w = 0, t = 0;
+    // scalar head up to a 4-element boundary, then float4 slots, then the scalar tail
+    const int64_t a0 = (begin + 3) & ~int64_t(3);
+    const int64_t head = a0 < end ? a0 : end;
+    const int64_t stride = int64_t(gridDim.x) * kQueryThreads;
+    const int64_t tid = int64_t(blockIdx.x) * kQueryThreads + threadIdx.x;
+    for (int64_t i = begin + tid; i < head; i += stride)
+        if (lab[i] != LT(1)) count_query<K, true>(key_of(s[i]), tree, h, k, sorted, M, w, t);
+    const int64_t nvec = end > head ? (end - head) / 4 : 0;
+    const bool aligned = (reinterpret_cast<uintptr_t>(s + head) & 15u) == 0 &&
+                         (reinterpret_cast<uintptr_t>(lab + head) & (4 * sizeof(LT) - 1)) == 0;
+    for (int64_t v = tid; v < nvec; v += stride) {
+        const int64_t i = head + v * 4;
+        float f[4];
+        if (aligned) {
+            const f32x4 x = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(s + i));
+            f[0] = x.x;
+            f[1] = x.y;
+            f[2] = x.z;
+            f[3] = x.w;
+        } else {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) f[q] = s[i + q];
+        }
+        bool neg[4];
+        label4(lab, i, aligned, end, neg);
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            if (neg[q]) count_query<K, true>(key_of(f[q]), tree, h, k, sorted, M, w, t);
+    }
+    for (int64_t i = head + nvec * 4 + tid; i < end; i += stride)
+        if (lab[i] != LT(1)) count_query<K, true>(key_of(s[i]), tree, h, k, sorted, M, w, t);
+    __shared__ unsigned long long red[2][kQueryThreads / kWave];
+    w = wave_sum(w);
+    t = wave_sum(t);
+    const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+    if (lane == 0) {
+        red[0][wid] = w;
+        red[1][wid] = t;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long bw = 0, bt = 0;
+        for (int i = 0; i < kQueryThreads / kWave; ++i) {
+            bw += red[0][i];
+            bt += red[1][i];
+        }
+        if (bw) atomicAdd(out + 0, bw);
+        if (bt) atomicAdd(out + 1, bt);
+    }
+}
+
 int query_grid(int64_t L) {
     static int cus = 0;
     if (cus == 0) {
@@ -454,6 +538,45 @@ int radix_sort_keys(const float* neg, int64_t N, const SortWs& w, hipStream_t st
     return DAUC_OK;
 }
 
+template <typename LT>
+int launch_labeled(int k, const float* s, const LT* lab, int64_t begin, int64_t end, const unsigned* tree, int h,
+                   const unsigned* sorted, int64_t M, unsigned long long* out, hipStream_t st) {
+    const dim3 grid(query_grid(end - begin)), block(kQueryThreads);
+    const size_t lds = size_t(1) << h << 2;
+#define DAUC_QL(KV)                                                                                           \
+    hipLaunchKernelGGL((query_labeled_kernel<KV, LT>), grid, block, lds, st, s, lab, begin, end, tree, h, k, \
+                       sorted, M, out)
+    switch (k) {
+        case 1: DAUC_QL(1); break;
+        case 2: DAUC_QL(2); break;
+        case 4: DAUC_QL(4); break;
+        case 8: DAUC_QL(8); break;
+        case 16: DAUC_QL(16); break;
+        case 32: DAUC_QL(32); break;
+        default: DAUC_QL(0); break;
+    }
+#undef DAUC_QL
+    return launch_status();
+}
+
+// sort the table, build the tree; returns the tree pointer and geometry
+int prepare_table(const float* table, int64_t M, void* workspace, hipStream_t st, const unsigned** sorted,
+                  unsigned** tree, int* k_out, int* h_out) {
+    SortWs w = carve(workspace, M);
+    int rc = radix_sort_keys(table, M, w, st, sorted);
+    if (rc) return rc;
+    int k = 1;
+    while ((M + k - 1) / k > kMaxSplit) k *= 2;
+    const int S = static_cast<int>((M + k - 1) / k);
+    int h = 1;
+    while ((1 << h) - 1 < S) ++h;
+    *tree = reinterpret_cast<unsigned*>(static_cast<char*>(workspace) + ((sort_ws_bytes(M) + 255) / 256) * 256);
+    hipLaunchKernelGGL(build_tree_kernel, dim3(((1 << h) + 255) / 256), dim3(256), 0, st, *sorted, M, k, S, h, *tree);
+    *k_out = k;
+    *h_out = h;
+    return launch_status();
+}
+
 }  // namespace
 }  // namespace dauc
 
@@ -488,22 +611,43 @@ int dauc_auc_counts_sorted(const float* pos, int64_t P, const float* neg, int64_
     const int64_t M = table_pos ? P : N, L = table_pos ? N : P;
     if (workspace == nullptr || workspace_bytes < dauc_sort_workspace_size(M) || M > 0xffffffffLL) return DAUC_EINVAL;
     hipStream_t st = as_hip(stream);
-    SortWs w = carve(workspace, M);
     const unsigned* sorted = nullptr;
-    int rc = radix_sort_keys(table_pos ? pos : neg, M, w, st, &sorted);
-    if (rc) return rc;
-    int k = 1;
-    while ((M + k - 1) / k > kMaxSplit) k *= 2;
-    const int S = static_cast<int>((M + k - 1) / k);
-    int h = 1;
-    while ((1 << h) - 1 < S) ++h;
-    unsigned* tree = reinterpret_cast<unsigned*>(static_cast<char*>(workspace) + ((sort_ws_bytes(M) + 255) / 256) * 256);
-    hipLaunchKernelGGL(build_tree_kernel, dim3(((1 << h) + 255) / 256), dim3(256), 0, st, sorted, M, k, S, h, tree);
-    rc = launch_status();
+    unsigned* tree = nullptr;
+    int k = 1, h = 1;
+    int rc = prepare_table(table_pos ? pos : neg, M, workspace, st, &sorted, &tree, &k, &h);
     if (rc) return rc;
     const float* q = table_pos ? neg : pos;
     return table_pos ? launch_query<true>(k, q, L, tree, h, sorted, M, wins_ties, st)
                      : launch_query<false>(k, q, L, tree, h, sorted, M, wins_ties, st);
+}
+
+int dauc_auc_counts_sorted_labeled(const float* pos, int64_t P, const float* scores, const void* labels,
+                                   int label_dtype, int64_t begin, int64_t end, unsigned long long* wins_ties,
+                                   void* workspace, size_t workspace_bytes, dauc_stream_t stream) {
+    if (P < 0 || begin < 0 || end < begin || wins_ties == nullptr || (P > 0 && pos == nullptr) ||
+        (end > begin && (scores == nullptr || labels == nullptr)))
+        return DAUC_EINVAL;
+    if (label_dtype != DAUC_LABEL_I8 && label_dtype != DAUC_LABEL_I32 && label_dtype != DAUC_LABEL_I64)
+        return DAUC_EINVAL;
+    if (P == 0 || end == begin) return DAUC_OK;
+    if (workspace == nullptr || workspace_bytes < dauc_sort_workspace_size(P) || P > 0xffffffffLL) return DAUC_EINVAL;
+    hipStream_t st = as_hip(stream);
+    const unsigned* sorted = nullptr;
+    unsigned* tree = nullptr;
+    int k = 1, h = 1;
+    int rc = prepare_table(pos, P, workspace, st, &sorted, &tree, &k, &h);
+    if (rc) return rc;
+    switch (label_dtype) {
+        case DAUC_LABEL_I8:
+            return launch_labeled(k, scores, static_cast<const int8_t*>(labels), begin, end, tree, h, sorted, P,
+                                  wins_ties, st);
+        case DAUC_LABEL_I32:
+            return launch_labeled(k, scores, static_cast<const int32_t*>(labels), begin, end, tree, h, sorted, P,
+                                  wins_ties, st);
+        default:
+            return launch_labeled(k, scores, static_cast<const int64_t*>(labels), begin, end, tree, h, sorted, P,
+                                  wins_ties, st);
+    }
 }
 
 }  // extern "C"

@@ -312,11 +312,12 @@ def scale_div(x: torch.Tensor, divisor: float) -> None:
 
 
 # ----------------------------------------------------------------- a8
-def split_scores(scores: torch.Tensor, labels: torch.Tensor):
+def split_scores(scores: torch.Tensor, labels: torch.Tensor, negatives: bool = True):
     """Stable split into (pos, neg) score buffers plus device stats {P, N, non-finite, other}.
 
     Returns (pos_buf, neg_buf, stats): pos_buf/neg_buf have capacity n; the valid
-    prefixes are stats[0] and stats[1] long.
+    prefixes are stats[0] and stats[1] long. negatives=False writes only the
+    positives (neg_buf is None).
     """
     _require(scores, "scores", torch.float32)
     dev = scores.device
@@ -329,12 +330,12 @@ def split_scores(scores: torch.Tensor, labels: torch.Tensor):
     if n == 0:
         raise ValueError("empty score vector")
     pos = torch.empty(n, dtype=torch.float32, device=dev)
-    neg = torch.empty(n, dtype=torch.float32, device=dev)
+    neg = torch.empty(n, dtype=torch.float32, device=dev) if negatives else None
     stats = torch.empty(4, dtype=torch.int64, device=dev)
     L = _lib.load()
     ws = workspaces.get(dev, "split", L.dauc_split_workspace_size(n))
-    check(L.dauc_split_scores(_ptr(scores), _ptr(labels), lc, n, _ptr(pos), _ptr(neg), _ptr(stats), _ptr(ws),
-                              ws.numel(), _stream(dev)), "dauc_split_scores")
+    check(L.dauc_split_scores(_ptr(scores), _ptr(labels), lc, n, _ptr(pos), _ptr(neg) if negatives else None,
+                              _ptr(stats), _ptr(ws), ws.numel(), _stream(dev)), "dauc_split_scores")
     return pos, neg, stats
 
 
@@ -369,6 +370,30 @@ def auc_counts_sorted(pos: torch.Tensor, neg: torch.Tensor, wins_ties: torch.Ten
                                    ws.numel(), _stream(dev)), "dauc_auc_counts_sorted")
 
 
+def auc_counts_sorted_labeled(pos: torch.Tensor, scores: torch.Tensor, labels: torch.Tensor, begin: int, end: int,
+                              wins_ties: torch.Tensor) -> None:
+    """auc_counts_sorted with the negatives read in place: every element of scores[begin:end]
+    whose label is not 1 is counted against the sorted positives."""
+    _require(pos, "pos", torch.float32)
+    dev = pos.device
+    _require(scores, "scores", torch.float32, dev)
+    _require(wins_ties, "wins_ties", torch.int64, dev)
+    lc = _label_code(labels, "labels")
+    if pos.dim() != 1 or not pos.is_contiguous() or scores.dim() != 1 or not scores.is_contiguous():
+        raise ValueError("pos and scores must be contiguous 1-D tensors")
+    if labels.shape != scores.shape or not labels.is_contiguous() or labels.device != dev:
+        raise ValueError("labels must be a contiguous tensor shaped like scores, on the same device")
+    if not 0 <= begin <= end <= scores.numel():
+        raise ValueError("need 0 <= begin <= end <= scores.numel()")
+    if wins_ties.numel() < 2 or not wins_ties.is_contiguous():
+        raise ValueError("wins_ties needs 2 contiguous int64 slots")
+    L = _lib.load()
+    ws = workspaces.get(dev, "sort", L.dauc_sort_workspace_size(max(pos.numel(), 1)))
+    check(L.dauc_auc_counts_sorted_labeled(_ptr(pos), pos.numel(), _ptr(scores), _ptr(labels), lc, int(begin),
+                                           int(end), _ptr(wins_ties), _ptr(ws), ws.numel(), _stream(dev)),
+          "dauc_auc_counts_sorted_labeled")
+
+
 def sort_keys(scores: torch.Tensor) -> torch.Tensor:
     """Ascending order-preserving uint32 keys of fp32 scores, returned as int32 bit patterns."""
     _require(scores, "scores", torch.float32)
@@ -387,5 +412,5 @@ __all__ = [
     "GradSeg", "label_map_phat", "surrogate_fwdbwd", "class_sums", "alpha_from_sums", "pd_update",
     "pd_update_dense", "coda_finalize", "scale_div", "split_scores", "pair_count", "auc_counts_sorted",
     "surrogate_logits_fwdbwd", "class_sums_logits",
-    "sort_keys", "mode_code", "workspaces",
+    "sort_keys", "auc_counts_sorted_labeled", "mode_code", "workspaces",
 ]

@@ -211,7 +211,8 @@ size_t dauc_split_workspace_size(int64_t n);
  * Stable split of (scores, labels) into positive (label == 1) and negative
  * (label != 1) score lists, the sklearn roc_curve(pos_label=1) convention used
  * by main.py:79-80, in original order:
- *   pos_out[0..P), neg_out[0..N), each sized n by the caller.
+ *   pos_out[0..P), neg_out[0..N), each sized n by the caller (neg_out may be NULL:
+ *   only the positives are written).
  *   stats[4] (int64) = { P, N, #non-finite scores, #labels not in {-1, 1} }
  */
 int dauc_split_scores(const float* scores, const void* labels, int label_dtype, int64_t n,
@@ -254,6 +255,16 @@ size_t dauc_sort_workspace_size(int64_t n);
 int dauc_auc_counts_sorted(const float* pos, int64_t P, const float* neg, int64_t N,
                            unsigned long long* wins_ties, void* workspace, size_t workspace_bytes,
                            dauc_stream_t stream);
+
+/*
+ * dauc_auc_counts_sorted without materialised negatives: the sorted table is the
+ * positives pos[0..P); the queries are the elements of scores/labels in [begin, end)
+ * whose label is not 1 (the full arrays, as given to dauc_split_scores). Same
+ * accumulation into wins_ties; workspace >= dauc_sort_workspace_size(P).
+ */
+int dauc_auc_counts_sorted_labeled(const float* pos, int64_t P, const float* scores, const void* labels,
+                                   int label_dtype, int64_t begin, int64_t end, unsigned long long* wins_ties,
+                                   void* workspace, size_t workspace_bytes, dauc_stream_t stream);
 
 /* The radix sort alone: keys_out[0..n) = ascending order-preserving keys of scores (testing). */
 int dauc_sort_keys(const float* scores, int64_t n, unsigned* keys_out, void* workspace,

@@ -44,7 +44,7 @@ def test_workspace_sizes():
     L = _lib.load()
     assert L.dauc_surrogate_workspace_size(1) >= 256
     assert L.dauc_surrogate_workspace_size(1 << 26) > L.dauc_surrogate_workspace_size(4096)
-    assert L.dauc_split_workspace_size(1 << 24) >= (1 << 24) // 4096 * 20
+    assert L.dauc_split_workspace_size(1 << 24) >= (1 << 24) // 8192 * 20  # 8192-score tiles
 
 
 def test_invalid_arguments_return_einval():

@@ -516,6 +516,30 @@ def test_sorted_counts_bucket_sizes(dev, M, L, table_pos):
         assert tuple(b.tolist()) == coracle.pair_count_bruteforce(pos, neg)
 
 
+@pytest.mark.parametrize("ldtype", [np.int8, np.int32, np.int64])
+@pytest.mark.parametrize("n,p,begin,trim", [(1000, 0.3, 0, 0), (300_001, 0.02, 3, 5), (2_000_003, 0.01, 1, 2),
+                                            (150_000, 0.2, 0, 1)])
+def test_sorted_counts_labeled(dev, ldtype, n, p, begin, trim):
+    """Negatives read in place from [begin, end) of the full arrays (labels != 1, including
+    labels outside {-1, 1}) vs the pair-count kernel over the same negatives; unaligned ranges,
+    every label dtype, ties and +-0, bit-exact."""
+    from distributedauc_amd import ops
+
+    rng = np.random.default_rng(n + begin)
+    s = (np.floor(rng.random(n) * 3001) / 3001 - 0.5).astype(np.float32)
+    s[rng.random(n) < 0.03] = -0.0
+    y = np.where(rng.random(n) < p, 1, -1).astype(ldtype)
+    y[rng.random(n) < 0.01] = 0  # not +1: a negative for roc_curve(pos_label=1)
+    end = n - trim
+    pos = s[y == 1]
+    neg = s[begin:end][y[begin:end] != 1]
+    a = torch.zeros(2, dtype=torch.int64, device=dev)
+    b = torch.zeros(2, dtype=torch.int64, device=dev)
+    ops.pair_count(T(pos, dev), T(neg, dev), a)
+    ops.auc_counts_sorted_labeled(T(pos, dev), T(s, dev), T(y, dev), begin, end, b)
+    assert a.tolist() == b.tolist()
+
+
 @pytest.mark.parametrize("zdtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("B", [1, 256, 5000])
 def test_surrogate_logits_fused_softmax(dev, zdtype, B):
