@@ -218,7 +218,10 @@ __device__ __forceinline__ void reduce_and_finalize(const Acc& acc, const Surrog
     for (int k = 0; k < kNumAcc; ++k) tot[k] = 0.0;
     for (int b = threadIdx.x; b < static_cast<int>(gridDim.x); b += kThreads) {
 #pragma unroll
-        for (int k = 0; k < kNumAcc; ++k) tot[k] += load_sc1(&partials[b * kNumAcc + k]);
+        for (int k = 0; k < kNumAcc; ++k) {
+            tot[k] += load_sc1(&partials[b * kNumAcc + k]);
+            partials[b * kNumAcc + k] = 0.0;  // the workspace is left zeroed (dauc.h)
+        }
     }
     block_sum<kNumAcc>(tot, scratch);
     if (threadIdx.x == 0) {
@@ -524,7 +527,7 @@ __device__ __forceinline__ unsigned long long enc_word(double v) {
 
 template <bool CLASS_ONLY>
 __global__ __launch_bounds__(kThreads) void surrogate_rows_reduce_kernel(
-    const double* __restrict__ rows, int64_t nrows, ChunkWs ws, double invB, const float* __restrict__ abalpha,
+    double* __restrict__ rows, int64_t nrows, ChunkWs ws, double invB, const float* __restrict__ abalpha,
     const float* __restrict__ p_hat, double* __restrict__ out64, float* __restrict__ grad3, float* __restrict__ loss,
     double* __restrict__ sums4, int accumulate) {
     __shared__ double scratch[kNumAcc * kWaves];
@@ -546,10 +549,12 @@ __global__ __launch_bounds__(kThreads) void surrogate_rows_reduce_kernel(
     }
 #pragma unroll
     for (int j = 0; j < kPer; ++j) {
+        const int64_t r = r0 + threadIdx.x + int64_t(j) * kThreads;
 #pragma unroll
         for (int q = 0; q < 3; ++q) {
             tot[2 * q] += v[j][q].x;
             tot[2 * q + 1] += v[j][q].y;
+            if (r < r1) reinterpret_cast<f64x2*>(rows + r * kRowWords)[q] = f64x2{0.0, 0.0};
         }
     }
     block_sum<kNumAcc>(tot, scratch);
@@ -614,6 +619,225 @@ __global__ __launch_bounds__(kThreads) void surrogate_rows_reduce_kernel(
     }
 }
 
+// ---- the same stream in ONE launch: start-order tickets ------------------------------------
+//
+// Workgroups are grouped by blockIdx (kTicketGroup consecutive chunks). A workgroup's FIRST
+// instruction is a returning ticket add on its group's counter; the reply travels while the
+// chunk's loads are in flight, so nobody waits for it. The workgroup that draws its group's
+// last ticket is the last one of the group to START: every other member is already resident
+// and waits for nothing, so it may poll their rows (data-as-flag words, as above) after its
+// own chunk without any risk of waiting for a workgroup that cannot run. It sums the group's
+// rows in blockIdx order, zeroes them, publishes the group total as data-as-flag words and
+// draws a ticket on the final counter; the group reducer that draws the last of those (every
+// other group reducer has already published) sums the group totals in group order and writes
+// the scalars. Only ngroups + 1 workgroups ever wait, each near the end of its own life, and
+// the summation order is fixed by blockIdx: bitwise reproducible, same as the two-launch form.
+constexpr int kTicketGroupMin = 64;            // smallest group of any variant (sizes the workspace)
+constexpr int kCtrStrideMax = 16384;           // widest counter spacing of any variant (64 KB)
+
+__host__ __device__ inline int64_t ticket_groups(int64_t nblocks, int G = kTicketGroupMin) { return (nblocks + G - 1) / G; }
+
+struct TicketWs {
+    unsigned* ctr;                 // [ngroups + 1] * kCtrStride; [ngroups * kCtrStride] is the final counter
+    unsigned long long* rows;      // [nblocks][kRowWords] encoded
+    unsigned long long* gwords;    // [ngroups][kRowWords] encoded
+};
+
+inline size_t align256(size_t b) { return (b + 255) / 256 * 256; }
+
+// sized for the smallest group and the widest counter spacing of any variant
+inline size_t ticket_ws_bytes(int64_t nblocks) {
+    const int64_t ng = ticket_groups(nblocks);
+    return kPersistentBytes + align256(size_t(ng + 1) * kCtrStrideMax * 4) +
+           align256(size_t(nblocks) * kRowWords * 8) + size_t(ng) * kRowWords * 8;
+}
+
+inline TicketWs ticket_ws(void* ws, int64_t nblocks) {
+    const int64_t ng = ticket_groups(nblocks);
+    char* p = static_cast<char*>(ws) + kPersistentBytes;
+    TicketWs w;
+    w.ctr = reinterpret_cast<unsigned*>(p);
+    p += align256(size_t(ng + 1) * kCtrStrideMax * 4);
+    w.rows = reinterpret_cast<unsigned long long*>(p);
+    p += align256(size_t(nblocks) * kRowWords * 8);
+    w.gwords = reinterpret_cast<unsigned long long*>(p);
+    return w;
+}
+
+// Take nrows encoded rows (thread t: rows t, t + 256, then the next 512, ...): every word of a
+// pass is loaded before any is examined, only the missing ones are polled again (bounded; a
+// timeout leaves NaN), each is re-zeroed, and tot[] sums them in that fixed order.
+__device__ __forceinline__ void take_rows(unsigned long long* words, int64_t nrows, double (&tot)[kNumAcc],
+                                          bool& ok) {
+    for (int64_t r0 = threadIdx.x; r0 < nrows; r0 += 2 * kThreads) {
+        const int64_t r1 = r0 + kThreads;
+        const bool two = r1 < nrows;
+        unsigned long long w[2][kRowWords];
+#pragma unroll
+        for (int k = 0; k < kRowWords; ++k) {
+            w[0][k] = __hip_atomic_load((gu64*)(words + r0 * kRowWords + k), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            w[1][k] = two ? __hip_atomic_load((gu64*)(words + r1 * kRowWords + k), __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT)
+                          : ~0ull;
+        }
+        for (int polls = 0;; ++polls) {
+            bool missing = false;
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int k = 0; k < kRowWords; ++k) missing |= (w[j][k] == 0ull);
+            if (!missing) break;
+            if (polls >= kMaxPolls) {
+                ok = false;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int k = 0; k < kRowWords; ++k)
+                    if (w[j][k] == 0ull)
+                        w[j][k] = __hip_atomic_load((gu64*)(words + (j ? r1 : r0) * kRowWords + k), __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT);
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            if (j == 1 && !two) break;
+#pragma unroll
+            for (int k = 0; k < kRowWords; ++k) {
+                tot[k] += __longlong_as_double(static_cast<long long>(w[j][k] ^ kEmptyKey));
+                __hip_atomic_store((gu64*)(words + (j ? r1 : r0) * kRowWords + k), 0ull, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+    }
+}
+
+template <typename YT, bool CLASS_ONLY, int S, int kTicketGroup, int kCtrStride, bool TICKET_FIRST>
+__global__ __launch_bounds__(kThreads) void surrogate_ticket_kernel(
+    const float* __restrict__ h, const YT* __restrict__ y, int64_t B, double invB,
+    const float* __restrict__ abalpha, const float* __restrict__ p_hat, float* __restrict__ dh, TicketWs ws,
+    double* __restrict__ out64, float* __restrict__ grad3, float* __restrict__ loss, double* __restrict__ sums4,
+    int accumulate) {
+    const int64_t nblocks = gridDim.x;
+    const int64_t ngroups = ticket_groups(nblocks, kTicketGroup);
+    const int64_t grp = blockIdx.x / kTicketGroup;
+    const int64_t g0 = grp * kTicketGroup;
+    const int64_t gsize = (nblocks - g0 < kTicketGroup) ? nblocks - g0 : kTicketGroup;
+    unsigned ticket = 0;
+    // an opaque per-lane zero keeps the address divergent, so the atomic optimizer does not
+    // rewrite the add into a wave-aggregated form that waits for the reply right away
+    auto draw = [&]() {
+        if (threadIdx.x == 0) {
+            int zero;
+            asm volatile("v_mov_b32 %0, 0" : "=v"(zero));
+            ticket = __hip_atomic_fetch_add((gu32*)(ws.ctr + grp * kCtrStride + zero), 1u, __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_AGENT);
+        }
+    };
+    if (TICKET_FIRST) draw();
+
+    SurrogateScalars s;
+    if (CLASS_ONLY) s = SurrogateScalars{};
+    else s = make_scalars(abalpha, p_hat, invB);
+    Acc acc;
+    const bool write_dh = !CLASS_ONLY && dh != nullptr;
+    const int64_t base = int64_t(blockIdx.x) * chunk_elems(S);
+    const bool full = base + chunk_elems(S) <= B;
+    f32x4 hv[S];
+    if (full) {
+        int yv[S][4];
+#pragma unroll
+        for (int k = 0; k < S; ++k) {
+            const int64_t b = base + (int64_t(k) * kThreads + threadIdx.x) * kVec;
+            hv[k] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(h + b));
+            load_labels4(y, b, yv[k]);
+        }
+        if (!TICKET_FIRST) draw();  // issued behind the loads: waiting for them does not wait for it
+#pragma unroll
+        for (int k = 0; k < S; ++k) hv[k] = visit4<CLASS_ONLY>(hv[k], yv[k], s, acc);
+    } else {
+        if (!TICKET_FIRST) draw();
+        for (int64_t i = base + threadIdx.x; i < B; i += kThreads) {
+            const float g = visit1<CLASS_ONLY>(h[i], load_label(y, i), s, acc);
+            if (write_dh) dh[i] = g;
+        }
+    }
+    const double sp = wave_total_dpp(acc.s_pos), sn = wave_total_dpp(acc.s_neg);
+    const double qp = wave_total_dpp(acc.q_pos), qn = wave_total_dpp(acc.q_neg);
+    const int np = wave_total_dpp(acc.n_pos), nn = wave_total_dpp(acc.n_neg);
+    if (full && write_dh) {
+#pragma unroll
+        for (int k = 0; k < S; ++k)
+            __builtin_nontemporal_store(hv[k], reinterpret_cast<f32x4*>(dh + base + (int64_t(k) * kThreads + threadIdx.x) * kVec));
+    }
+    __shared__ double wrow[kWaves][kRowWords];
+    __shared__ int role;  // 0: done, 1: group reducer
+    const int wid = threadIdx.x / kWave;
+    if ((threadIdx.x & (kWave - 1)) == kWave - 1) {
+        wrow[wid][0] = sp;
+        wrow[wid][1] = sn;
+        wrow[wid][2] = qp;
+        wrow[wid][3] = qn;
+        wrow[wid][4] = static_cast<double>(np);
+        wrow[wid][5] = static_cast<double>(nn);
+    }
+    if (threadIdx.x == 0) role = (ticket == gsize - 1);
+    __syncthreads();
+    if (threadIdx.x < kRowWords) {
+        const int k = threadIdx.x;
+        const double v = ((wrow[0][k] + wrow[1][k]) + wrow[2][k]) + wrow[3][k];
+        __hip_atomic_store((gu64*)(ws.rows + int64_t(blockIdx.x) * kRowWords + k), enc_word(v), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (!role) return;
+
+    // group reducer: rows g0 .. g0 + gsize in blockIdx order
+    __shared__ double scratch[kNumAcc * kWaves];
+    __shared__ int fin;
+    bool ok = true;
+    double tot[kNumAcc];
+#pragma unroll
+    for (int k = 0; k < kNumAcc; ++k) tot[k] = 0.0;
+    take_rows(ws.rows + g0 * kRowWords, gsize, tot, ok);
+    block_sum<kNumAcc>(tot, scratch);
+    if (threadIdx.x < kRowWords) {
+        double v = tot[0];
+#pragma unroll
+        for (int k = 1; k < kNumAcc; ++k)
+            if (threadIdx.x == k) v = tot[k];
+        __hip_atomic_store((gu64*)(ws.gwords + grp * kRowWords + threadIdx.x), enc_word(v), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (threadIdx.x == 0) {
+        // every ticket of this group has been drawn: leave the counter zeroed for the next call
+        __hip_atomic_store((gu32*)(ws.ctr + grp * kCtrStride), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned f = __hip_atomic_fetch_add((gu32*)(ws.ctr + ngroups * kCtrStride), 1u, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
+        fin = (f == ngroups - 1);
+        if (fin)
+            __hip_atomic_store((gu32*)(ws.ctr + ngroups * kCtrStride), 0u, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+    }
+    ok = __syncthreads_or(!ok) == 0;
+    if (!fin) return;
+
+    // final reducer: the group totals in group order
+#pragma unroll
+    for (int k = 0; k < kNumAcc; ++k) tot[k] = 0.0;
+    take_rows(ws.gwords, ngroups, tot, ok);
+    block_sum<kNumAcc>(tot, scratch);
+    ok = __syncthreads_or(!ok) == 0;
+    if (threadIdx.x == 0) {
+        if (!ok) {
+#pragma unroll
+            for (int k = 0; k < kNumAcc; ++k) tot[k] = __builtin_nan("");
+        }
+        if (CLASS_ONLY) emit_class_sums(tot, sums4, accumulate);
+        else finalize(tot, s, invB, out64, grad3, loss);
+    }
+}
+
 // Default chunk geometry (variant sweep: scripts/micro_kernels.py --which surrogate).
 #ifndef DAUC_SURROGATE_CHUNK_SLOTS
 #define DAUC_SURROGATE_CHUNK_SLOTS 4
@@ -665,7 +889,21 @@ int launch_chunk(const float* h, const YT* y, int64_t B, const float* abalpha, c
     return launch_status();
 }
 
-// variant: 0 = default dispatch, 1 = persistent kernel, 2..7 = chunk kernel geometries
+template <typename YT, bool CLASS_ONLY, int S, int G, int CS, bool TF>
+int launch_ticket(const float* h, const YT* y, int64_t B, const float* abalpha, const float* p_hat, float* dh,
+                  double* out64, float* grad3, float* loss, double* sums4, int accumulate, void* ws, size_t ws_bytes,
+                  hipStream_t st) {
+    const int64_t nblocks = (B + chunk_elems(S) - 1) / chunk_elems(S);
+    if (nblocks > 0x7fffffffLL) return DAUC_EINVAL;
+    if (ws == nullptr || ws_bytes < ticket_ws_bytes(nblocks)) return DAUC_EINVAL;
+    hipLaunchKernelGGL((surrogate_ticket_kernel<YT, CLASS_ONLY, S, G, CS, TF>), dim3(static_cast<unsigned>(nblocks)),
+                       dim3(kThreads), 0, st, h, y, B, 1.0 / static_cast<double>(B), abalpha, p_hat, dh,
+                       ticket_ws(ws, nblocks), out64, grad3, loss, sums4, accumulate);
+    return launch_status();
+}
+
+// variant: 0 = default dispatch, 1 = persistent kernel, 2..7 = chunk kernel geometries,
+// 8..14 = single-launch ticket kernel (slots, group size, counter spacing, ticket order)
 // (tuning; only for int8 labels with a loss, i.e. the micro-benchmark's configuration).
 template <bool CLASS_ONLY, typename YT>
 int launch_surrogate(const float* h, int64_t hs, const YT* y, int64_t B, const float* abalpha,
@@ -684,6 +922,15 @@ int launch_surrogate(const float* h, int64_t hs, const YT* y, int64_t B, const f
                 case 5: return launch_chunk<YT, false, 8, false, true>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, sums4, accumulate, ws, ws_bytes, st);
                 case 6: return launch_chunk<YT, false, 8, true, false>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, sums4, accumulate, ws, ws_bytes, st);
                 case 7: return launch_chunk<YT, false, 2, true, true>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, sums4, accumulate, ws, ws_bytes, st);
+#define DAUC_TV(S, G, CS, TF) return launch_ticket<YT, false, S, G, CS, TF>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, sums4, accumulate, ws, ws_bytes, st)
+                case 8: DAUC_TV(4, 512, 1024, true);
+                case 9: DAUC_TV(4, 64, 1024, true);
+                case 10: DAUC_TV(4, 128, 1024, true);
+                case 11: DAUC_TV(4, 256, 1024, true);
+                case 12: DAUC_TV(4, 64, 1024, false);
+                case 13: DAUC_TV(8, 64, 1024, true);
+                case 14: DAUC_TV(8, 256, 1024, true);
+#undef DAUC_TV
                 default: return DAUC_EINVAL;
             }
         }
@@ -847,8 +1094,10 @@ size_t dauc_surrogate_workspace_size(int64_t B) {
     const int g = grid_scalar(B);  // >= grid_for(B): covers the persistent kernels
     const size_t persistent = kCounterBytes + static_cast<size_t>(g) * kNumAcc * sizeof(double);
     // the chunk kernels (smallest chunk of any variant: S = 2)
-    const size_t chunked = chunk_ws_bytes((B + chunk_elems(2) - 1) / chunk_elems(2));
-    return persistent > chunked ? persistent : chunked;
+    const int64_t nb2 = (B + chunk_elems(2) - 1) / chunk_elems(2);
+    const size_t chunked = chunk_ws_bytes(nb2), ticketed = ticket_ws_bytes(nb2);
+    const size_t big = chunked > ticketed ? chunked : ticketed;
+    return persistent > big ? persistent : big;
 }
 
 int dauc_surrogate_fwdbwd(const float* h, int64_t h_stride, const void* y, int y_dtype, int64_t B,
@@ -868,7 +1117,7 @@ int dauc_surrogate_fwdbwd_variant(const float* h, int64_t h_stride, const void* 
                                   double* out64, float* grad3, float* loss, void* workspace,
                                   size_t workspace_bytes, int variant, dauc_stream_t stream) {
     if (B <= 0 || h == nullptr || y == nullptr || abalpha == nullptr || p_hat == nullptr ||
-        h_stride <= 0 || (dh != nullptr && dh_stride <= 0) || variant < 0 || variant > 7)
+        h_stride <= 0 || (dh != nullptr && dh_stride <= 0) || variant < 0 || variant > 14)
         return DAUC_EINVAL;
     return dispatch_labels<false>(h, h_stride, y, y_dtype, B, abalpha, p_hat, dh, dh_stride, out64,
                                   grad3, loss, nullptr, 0, workspace, workspace_bytes,

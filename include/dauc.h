@@ -103,7 +103,9 @@ int dauc_surrogate_fwdbwd(const float* h, int64_t h_stride, const void* y, int y
  * default dispatch (what dauc_surrogate_fwdbwd does), 1 forces the persistent
  * grid-stride kernel, 2..7 force the one-chunk-per-workgroup kernel (2: 4 float4 slots
  * per thread, 3: 8, 4: 16, all non-temporal; 5: 8 slots, plain loads; 6: 8 slots, plain
- * stores; 7: 2 slots, non-temporal). Variants 2..7 need unit strides, 16-byte
+ * stores; 7: 2 slots, non-temporal), 8..14 the single-launch form with start-order tickets
+ * (8..12: 4 slots, groups of 512 / 64 / 128 / 256 chunks, 12: ticket drawn after the loads;
+ * 13, 14: 8 slots, groups of 64 / 256). Variants 2..14 need unit strides, 16-byte
  * aligned h/dh and int8 labels, and B <= 2^31. Every variant returns bitwise-identical dh and counts;
  * the fp64 sums agree to rounding (their reduction trees differ).
  */

@@ -125,12 +125,14 @@ def test_surrogate_large_deterministic(dev):
     assert outs[0][4] == np.sum(yn == 1)
 
 
-@pytest.mark.parametrize("B", [(1 << 20), (1 << 20) + 37, 3 * (1 << 20) + 4099])
+@pytest.mark.parametrize("B", [(1 << 20), (1 << 20) + 37, 3 * (1 << 20) + 4099, (1 << 24) + 5])
 def test_surrogate_chunked_variants(dev, B):
     """One-chunk-per-workgroup kernel (default for unit-stride B >= 2^20, two-level ticket)
     and every tuning variant: fp64 closed form within 1e-6 of term scale, dh and counts
     bitwise equal across variants (dh is per-element; the sums only differ in tree order),
-    bitwise run-to-run, ragged last chunk, and the workspace left zeroed for the next call."""
+    bitwise run-to-run, ragged last chunk, and the workspace left zeroed for the next call.
+    Variants 8..14 (single-launch tickets) run interleaved with the others on the
+    same workspace, 1 to 33 ticket groups."""
     from distributedauc_amd import ops
 
     g = torch.Generator(device=dev).manual_seed(B & 0xFFFF)
@@ -144,7 +146,8 @@ def test_surrogate_chunked_variants(dev, B):
     k = np.where(yn == 1, 0.1 + 1 + 0.3, -0.2 - 1 - 0.3)
     c = 2.0 / B * (np.abs(hn) + np.abs(k))
     ref_dh = None
-    for variant in (0, 0, 1, 2, 3, 4, 5, 6, 7):
+    tick = {}
+    for variant in (0, 0, 1, 2, 3, 4, 5, 6, 7, 8, 8, 9, 10, 11, 12, 13, 14, 2, 8, 1, 12, 14):
         o = torch.zeros(6, dtype=torch.float64, device=dev)
         dh = torch.full((B,), float("nan"), device=dev)
         ops.surrogate_fwdbwd(h, y, abap[:3], abap[3:], dh=dh, out64=o, variant=variant)
@@ -158,6 +161,8 @@ def test_surrogate_chunked_variants(dev, B):
             assert np.array_equal(dhn, ref_dh), variant
         if variant == 0:
             assert np.array_equal(got, ref0)  # deterministic reduction order
+        if variant >= 8:  # fixed blockIdx summation order: bitwise run-to-run
+            assert np.array_equal(got, tick.setdefault(variant, got)), variant
     sums = torch.zeros(4, dtype=torch.float64, device=dev)
     ops.class_sums(h, y, sums, accumulate=False)  # chunked CLASS_ONLY path
     s = sums.cpu().numpy()
