@@ -72,6 +72,10 @@ SIGNATURES = {
                                    _vp, _sz, _vp]),
     "dauc_bn_act_backward": (_int, [_vp, _vp, _vp, _int, _i64, _int, _int, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                     _sz, _vp]),
+    "dauc_maxpool2d_forward": (_int, [_vp, _int, _i64, _int, _int, _int, _int, _int, _int, _vp, _vp, _int, _int,
+                                      _vp]),
+    "dauc_maxpool2d_backward": (_int, [_vp, _vp, _int, _i64, _int, _int, _int, _int, _int, _int, _int, _int, _vp,
+                                       _vp]),
 }
 
 _lib = None

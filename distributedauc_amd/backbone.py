@@ -169,7 +169,13 @@ class ResNet(nn.Module):
         return self
 
     def features(self, x):
-        x = self.maxpool(_bn_act(self.fused_bn, self.bn1, self.conv1(x)))
+        x = _bn_act(self.fused_bn, self.bn1, self.conv1(x))
+        if self.fused_bn and x.is_cuda:  # the stem max-pool with int8 indices (pool.py)
+            from .pool import max_pool2d
+
+            x = max_pool2d(x, self.maxpool)
+        else:
+            x = self.maxpool(x)
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         return torch.flatten(self.avgpool(x), 1)
 

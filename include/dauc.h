@@ -303,6 +303,25 @@ int dauc_bn_act_backward(const void* dy, const void* y, const void* x, int dtype
                          float* dgamma, float* dbeta, void* workspace, size_t workspace_bytes,
                          dauc_stream_t stream);
 
+/* ------------------------------------------------ backbone: stem max-pool */
+
+/*
+ * Max pooling over channels-last x [N, H, W, C] (bf16 or fp32; C a multiple of the
+ * 16-byte vector; 16-byte aligned), square kernel, stride, zero-free padding
+ * (pad <= kernel / 2, kernel^2 <= 127), floor mode: Ho = (H + 2 pad - kernel) / stride + 1.
+ * Replaces torch's max_pool2d_with_indices of resnet.py:205 (the stem). argmax int8
+ * [N, Ho, Wo, C] (8-byte aligned) receives each maximum's position inside its window
+ * (row * kernel + column; -1 = no element compared greater than -inf, torch's index 0).
+ * Output, comparisons (NaN wins) and the backward's fp32 summation order are torch's:
+ * bit-identical results.
+ */
+int dauc_maxpool2d_forward(const void* x, int dtype, int64_t N, int H, int W, int C, int kernel, int stride,
+                           int pad, void* y, int8_t* argmax, int Ho, int Wo, dauc_stream_t stream);
+
+/* dx [N, H, W, C] <- the gradient of dauc_maxpool2d_forward given dy [N, Ho, Wo, C]. */
+int dauc_maxpool2d_backward(const void* dy, const int8_t* argmax, int dtype, int64_t N, int H, int W, int C,
+                            int kernel, int stride, int pad, int Ho, int Wo, void* dx, dauc_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -61,6 +61,13 @@ def test_invalid_arguments_return_einval():
     assert L.dauc_coda_finalize(null, 10, 2, null, null, null) == _lib.DAUC_EINVAL
     assert L.dauc_split_scores(null, null, 1, 10, null, null, null, null, 0, null) == _lib.DAUC_EINVAL
     assert L.dauc_label_map_phat(null, 0, 4, null, null, null, null, null) == _lib.DAUC_EINVAL
+    a = ctypes.c_void_p(256)
+    # max-pool: Ho/Wo must be the floor-mode sizes, C a whole bf16 vector, pad <= kernel / 2
+    assert L.dauc_maxpool2d_forward(a, 2, 2, 112, 112, 64, 3, 2, 1, a, a, 55, 56, null) == _lib.DAUC_EINVAL
+    assert L.dauc_maxpool2d_forward(a, 2, 2, 112, 112, 60, 3, 2, 1, a, a, 56, 56, null) == _lib.DAUC_EINVAL
+    assert L.dauc_maxpool2d_forward(a, 2, 2, 112, 112, 64, 3, 2, 2, a, a, 57, 57, null) == _lib.DAUC_EINVAL
+    assert L.dauc_maxpool2d_backward(a, null, 2, 2, 112, 112, 64, 3, 2, 1, 56, 56, a, null) == _lib.DAUC_EINVAL
+    assert L.dauc_maxpool2d_backward(a, a, 3, 2, 112, 112, 64, 3, 2, 1, 56, 56, a, null) == _lib.DAUC_EINVAL
     with pytest.raises(_lib.DaucError, match="invalid argument"):
         _lib.check(_lib.DAUC_EINVAL, "x")
 
