@@ -97,9 +97,17 @@ class Bottleneck(nn.Module):
 
     def forward(self, x):
         f, g = self.fused_bn, self.gemm_conv1x1
-        skip = x if self.downsample is None else _bn_act(f, self.downsample[1], _c1(g, self.downsample[0], x),
-                                                         relu=False)
-        y = _bn_act(f, self.bn1, _c1(g, self.conv1, x))
+        down = None if self.downsample is None else self.downsample[0]
+        if g and x.is_cuda and (down is None or down.stride == (1, 1)):
+            # conv1 and the skip branch in one node: the gradient sum at x rides in the dgrad GEMM
+            from .conv1x1 import conv1x1_skip
+
+            h, skip = conv1x1_skip(self.conv1, x, down, skip_grad_owned=f and self.training)
+        else:
+            h, skip = _c1(g, self.conv1, x), (x if down is None else _c1(g, down, x))
+        if down is not None:
+            skip = _bn_act(f, self.downsample[1], skip, relu=False)
+        y = _bn_act(f, self.bn1, h)
         y = _bn_act(f, self.bn2, self.conv2(y))
         return _bn_act(f, self.bn3, _c1(g, self.conv3, y), residual=skip)
 

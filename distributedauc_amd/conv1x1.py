@@ -20,7 +20,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-__all__ = ["conv1x1", "Conv1x1Function", "plans"]
+__all__ = ["conv1x1", "conv1x1_skip", "Conv1x1Function", "Conv1x1SkipFunction", "plans"]
 
 plans: dict = {}  # (M, Cin, Cout, dtype, direction) -> engine
 
@@ -66,22 +66,97 @@ def _wgrad_gemm(g2, x2, slabs):
     return part.sum(0)
 
 
+def _fwd(x, weight):
+    """y = conv1x1(x, weight) (bf16 operands as x, fp32 accumulation), engine timed per shape."""
+    N, cin, H, W = x.shape
+    cout = weight.shape[0]
+    M = N * H * W
+    wc = weight.detach().reshape(cout, cin).to(x.dtype)
+    x2 = x.permute(0, 2, 3, 1).reshape(M, cin)  # a view: x is channels-last contiguous
+    with torch.autocast("cuda", enabled=False):
+        key = (M, cin, cout, x.dtype, "fwd")
+        eng = _choose(key, {"gemm": lambda: torch.mm(x2, wc.t()),
+                            "conv": lambda: F.conv2d(x, wc.view(cout, cin, 1, 1))})
+        if eng == "gemm":
+            y = torch.mm(x2, wc.t()).view(N, H, W, cout).permute(0, 3, 1, 2)
+        else:
+            y = F.conv2d(x, wc.view(cout, cin, 1, 1)).contiguous(memory_format=torch.channels_last)
+    return y, wc
+
+
+def _prep_grad(gy, x, cout):
+    N, cin, H, W = x.shape
+    gy = gy.to(x.dtype).contiguous(memory_format=torch.channels_last)
+    return gy, gy.permute(0, 2, 3, 1).reshape(N * H * W, cout)
+
+
+def _conv_dgrad(gy, x, wc):
+    cout, cin = wc.shape
+    return torch.ops.aten.convolution_backward(gy, x, wc.view(cout, cin, 1, 1), None, [1, 1], [0, 0], [1, 1],
+                                               False, [0, 0], 1, [True, False, False])[0]
+
+
+def _dgrad(gy, g2, x, wc):
+    """dx = dy @ W (a new channels-last tensor)."""
+    N, cin, H, W = x.shape
+    cout = wc.shape[0]
+    M = N * H * W
+    with torch.autocast("cuda", enabled=False):
+        eng = _choose((M, cin, cout, x.dtype, "dgrad"),
+                      {"gemm": lambda: torch.mm(g2, wc), "conv": lambda: _conv_dgrad(gy, x, wc)})
+        if eng == "gemm":
+            return torch.mm(g2, wc).view(N, H, W, cin).permute(0, 3, 1, 2)
+        return _conv_dgrad(gy, x, wc).contiguous(memory_format=torch.channels_last)
+
+
+def _dgrad_acc(base, gy, g2, x, wc):
+    """base += dy @ W in place (base: a channels-last tensor shaped like x that this backward owns).
+    GEMM engine: one hipBLASLt launch with beta = 1 (reads base once, writes it once, one rounding),
+    instead of a dgrad output plus autograd's separate add pass (read 2, write 1)."""
+    N, cin, H, W = x.shape
+    cout = wc.shape[0]
+    M = N * H * W
+    b2 = base.permute(0, 2, 3, 1).reshape(M, cin)  # a view of base
+    with torch.autocast("cuda", enabled=False):
+        key = (M, cin, cout, x.dtype, "dgrad_acc")
+        if key not in plans:
+            scratch = base.clone(memory_format=torch.channels_last)
+            s2 = scratch.permute(0, 2, 3, 1).reshape(M, cin)
+            _choose(key, {"gemm": lambda: s2.addmm_(g2, wc), "conv": lambda: scratch.add_(_conv_dgrad(gy, x, wc))})
+            del scratch, s2
+        if plans[key] == "gemm":
+            b2.addmm_(g2, wc)
+        else:
+            base.add_(_conv_dgrad(gy, x, wc))
+    return base
+
+
+def _wgrad(gy, g2, x, wc, wdtype):
+    N, cin, H, W = x.shape
+    cout = wc.shape[0]
+    M = N * H * W
+    x2 = x.permute(0, 2, 3, 1).reshape(M, cin)
+    with torch.autocast("cuda", enabled=False):
+        def conv_w():
+            return torch.ops.aten.convolution_backward(gy, x, wc.view(cout, cin, 1, 1), None, [1, 1], [0, 0], [1, 1],
+                                                       False, [0, 0], 1, [False, True, False])[1]
+
+        cands = {"conv": conv_w}
+        for s in (8, 32, 128):
+            if M % s == 0 and M // s >= 64:
+                cands[f"gemm{s}"] = (lambda s=s: _wgrad_gemm(g2, x2, s))
+        eng = _choose((M, cin, cout, x.dtype, "wgrad"), cands)
+        if eng == "conv":
+            dw = conv_w().reshape(cout, cin).to(wdtype)
+        else:
+            dw = _wgrad_gemm(g2, x2, int(eng[4:])).to(wdtype)
+    return dw.view(cout, cin, 1, 1)
+
+
 class Conv1x1Function(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight):
-        N, cin, H, W = x.shape
-        cout = weight.shape[0]
-        M = N * H * W
-        wc = weight.detach().reshape(cout, cin).to(x.dtype)
-        x2 = x.permute(0, 2, 3, 1).reshape(M, cin)  # a view: x is channels-last contiguous
-        with torch.autocast("cuda", enabled=False):
-            key = (M, cin, cout, x.dtype, "fwd")
-            eng = _choose(key, {"gemm": lambda: torch.mm(x2, wc.t()),
-                                "conv": lambda: F.conv2d(x, wc.view(cout, cin, 1, 1))})
-            if eng == "gemm":
-                y = torch.mm(x2, wc.t()).view(N, H, W, cout).permute(0, 3, 1, 2)
-            else:
-                y = F.conv2d(x, wc.view(cout, cin, 1, 1)).contiguous(memory_format=torch.channels_last)
+        y, wc = _fwd(x, weight)
         ctx.save_for_backward(x, wc)
         ctx.wdtype = weight.dtype
         return y
@@ -89,45 +164,63 @@ class Conv1x1Function(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gy):
         x, wc = ctx.saved_tensors
-        N, cin, H, W = x.shape
-        cout = wc.shape[0]
-        M = N * H * W
-        gy = gy.to(x.dtype).contiguous(memory_format=torch.channels_last)
-        g2 = gy.permute(0, 2, 3, 1).reshape(M, cout)
-        x2 = x.permute(0, 2, 3, 1).reshape(M, cin)
-        w4 = wc.view(cout, cin, 1, 1)
-        dx = dw = None
-        with torch.autocast("cuda", enabled=False):
-            if ctx.needs_input_grad[0]:
-                key = (M, cin, cout, x.dtype, "dgrad")
-
-                def conv_d():
-                    return torch.ops.aten.convolution_backward(gy, x, w4, None, [1, 1], [0, 0], [1, 1], False,
-                                                               [0, 0], 1, [True, False, False])[0]
-
-                eng = _choose(key, {"gemm": lambda: torch.mm(g2, wc), "conv": conv_d})
-                if eng == "gemm":
-                    dx = torch.mm(g2, wc).view(N, H, W, cin).permute(0, 3, 1, 2)
-                else:
-                    dx = conv_d().contiguous(memory_format=torch.channels_last)
-            if ctx.needs_input_grad[1]:
-                key = (M, cin, cout, x.dtype, "wgrad")
-
-                def conv_w():
-                    return torch.ops.aten.convolution_backward(gy, x, w4, None, [1, 1], [0, 0], [1, 1], False,
-                                                               [0, 0], 1, [False, True, False])[1]
-
-                cands = {"conv": conv_w}
-                for s in (8, 32, 128):
-                    if M % s == 0 and M // s >= 64:
-                        cands[f"gemm{s}"] = (lambda s=s: _wgrad_gemm(g2, x2, s))
-                eng = _choose(key, cands)
-                if eng == "conv":
-                    dw = conv_w().reshape(cout, cin).to(ctx.wdtype)
-                else:
-                    dw = _wgrad_gemm(g2, x2, int(eng[4:])).to(ctx.wdtype)
-                dw = dw.view(cout, cin, 1, 1)
+        gy, g2 = _prep_grad(gy, x, wc.shape[0])
+        dx = _dgrad(gy, g2, x, wc) if ctx.needs_input_grad[0] else None
+        dw = _wgrad(gy, g2, x, wc, ctx.wdtype) if ctx.needs_input_grad[1] else None
         return dx, dw
+
+
+class Conv1x1SkipFunction(torch.autograd.Function):
+    """(conv1(x), skip) for a bottleneck block's input x: skip = x (identity) or the stride-1 1x1
+    downsample conv of x (resnet.py:87-108). Backward: dx = dgrad(conv1) + d(skip) with the second
+    GEMM accumulating into the first term in place (beta = 1), so the branch-point gradient sum that
+    autograd would run as a separate add kernel over the block input (ResNet-50 b256: up to 3 x 411
+    MB per block) disappears."""
+
+    @staticmethod
+    def forward(ctx, x, w1, wd, skip_grad_owned):
+        y1, wc1 = _fwd(x, w1)
+        if wd is None:
+            skip, wcd = x, None
+        else:
+            skip, wcd = _fwd(x, wd)
+        ctx.save_for_backward(x, wc1, wcd)
+        ctx.wdtypes = (w1.dtype, None if wd is None else wd.dtype)
+        ctx.skip_grad_owned = bool(skip_grad_owned)
+        return y1, skip
+
+    @staticmethod
+    def backward(ctx, g1, gs):
+        x, wc1, wcd = ctx.saved_tensors
+        dx = dw1 = dwd = None
+        gy1 = g21 = gyd = g2d = None
+        if g1 is not None:
+            gy1, g21 = _prep_grad(g1, x, wc1.shape[0])
+        if gs is not None and wcd is not None:
+            gyd, g2d = _prep_grad(gs, x, wcd.shape[0])
+        if ctx.needs_input_grad[0]:
+            if gs is None:
+                base = None
+            elif wcd is None:
+                # the identity branch's gradient. With the fused BN node as its consumer it is a
+                # fresh tensor (BnActFunction's dres) seen only here, so it is accumulated into in
+                # place; otherwise (e.g. torch's add, which hands one tensor to both operands) a copy
+                base = gs.to(x.dtype).contiguous(memory_format=torch.channels_last)
+                if base is gs and not ctx.skip_grad_owned:
+                    base = base.clone(memory_format=torch.channels_last)
+            else:
+                base = _dgrad(gyd, g2d, x, wcd)
+            if g1 is None:
+                dx = base
+            elif base is None:
+                dx = _dgrad(gy1, g21, x, wc1)
+            else:
+                dx = _dgrad_acc(base, gy1, g21, x, wc1)
+        if ctx.needs_input_grad[1] and g1 is not None:
+            dw1 = _wgrad(gy1, g21, x, wc1, ctx.wdtypes[0])
+        if wcd is not None and ctx.needs_input_grad[2] and gs is not None:
+            dwd = _wgrad(gyd, g2d, x, wcd, ctx.wdtypes[1])
+        return dx, dw1, dwd, None
 
 
 def conv1x1(conv: nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
@@ -140,3 +233,22 @@ def conv1x1(conv: nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
     if torch.is_autocast_enabled("cuda") and x.dtype == torch.float32:
         x = x.to(torch.get_autocast_dtype("cuda"))
     return Conv1x1Function.apply(x, conv.weight)
+
+
+def _gemm_ok(conv: nn.Conv2d | None, x: torch.Tensor) -> bool:
+    return conv is None or (conv.kernel_size == (1, 1) and conv.stride == (1, 1) and conv.groups == 1
+                            and conv.bias is None and conv.padding == (0, 0))
+
+
+def conv1x1_skip(conv: nn.Conv2d, x: torch.Tensor, down: nn.Conv2d | None = None, skip_grad_owned: bool = False):
+    """``(conv(x), x if down is None else down(x))`` for a bottleneck's stride-1 1x1 conv1 and its
+    identity / stride-1 1x1 downsample branch, with the branch-point gradient sum fused into the
+    dgrad GEMM (Conv1x1SkipFunction). ``skip_grad_owned``: the skip's consumer hands back a gradient
+    tensor nobody else holds (the fused BN node does), so it may be accumulated into in place.
+    Other shapes: the two branches separately."""
+    if (x.device.type != "cuda" or not x.is_contiguous(memory_format=torch.channels_last)
+            or not _gemm_ok(conv, x) or not _gemm_ok(down, x)):
+        return conv1x1(conv, x), (x if down is None else conv1x1(down, x))
+    if torch.is_autocast_enabled("cuda") and x.dtype == torch.float32:
+        x = x.to(torch.get_autocast_dtype("cuda"))
+    return Conv1x1SkipFunction.apply(x, conv.weight, None if down is None else down.weight, skip_grad_owned)

@@ -67,3 +67,49 @@ def test_resnet_gemm_conv1x1_trains(dev):
     from bf16_step_compare import compare
 
     compare(dev, fused_bn=True, gemm_1x1=True)
+
+
+@pytest.mark.parametrize("down", [False, True])
+@pytest.mark.parametrize("owned", [False, True])
+@pytest.mark.parametrize("acc_engine", ["gemm", "conv"])
+def test_conv1x1_skip_fuses_branch_gradient(dev, down, owned, acc_engine):
+    """(conv1(x), skip) in one node: dx = dgrad(conv1) + d(skip), the sum accumulated by the GEMM
+    (beta = 1, in place) or by an add after MIOpen's dgrad; vs fp64 autograd of the two branches.
+    Also: the incoming skip gradient is left untouched unless the caller marked it as owned."""
+    from distributedauc_amd import conv1x1 as C
+
+    torch.manual_seed(7 + down + 2 * owned)
+    N, cin, width, H = 4, 256, 64, 14
+    conv = nn.Conv2d(cin, width, 1, bias=False).to(dev).to(memory_format=torch.channels_last)
+    dconv = nn.Conv2d(cin, 4 * width, 1, bias=False).to(dev).to(memory_format=torch.channels_last) if down else None
+    x = torch.randn(N, cin, H, H, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    M = N * H * H
+    C.plans.clear()
+    C.plans[(M, cin, width, torch.bfloat16, "dgrad_acc")] = acc_engine
+    xg = x.clone().requires_grad_(True)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        h, skip = C.conv1x1_skip(conv, xg, dconv, skip_grad_owned=owned)
+    assert h.dtype == skip.dtype == torch.bfloat16
+    if not down:
+        assert torch.equal(skip, x)
+    gh = torch.randn_like(h)
+    gs = torch.randn_like(skip).contiguous(memory_format=torch.channels_last)
+    gs_copy = gs.clone()
+    torch.autograd.backward([h, skip], [gh, gs])
+    if not owned:
+        assert torch.equal(gs, gs_copy), "a gradient the node does not own was modified"
+    xr = x.detach().cpu().double().requires_grad_(True)
+    wr = conv.weight.detach().cpu().double().to(torch.bfloat16).double().requires_grad_(True)
+    hr = F.conv2d(xr, wr)
+    if down:
+        wdr = dconv.weight.detach().cpu().double().to(torch.bfloat16).double().requires_grad_(True)
+        sr = F.conv2d(xr, wdr)
+    else:
+        sr = xr
+    torch.autograd.backward([hr, sr], [gh.cpu().double(), gs_copy.cpu().double()])
+    assert _err(h, hr) <= 2 ** -7 and _err(skip, sr) <= 2 ** -7
+    assert _err(xg.grad, xr.grad) <= 2 ** -7, ("dx", _err(xg.grad, xr.grad))
+    assert _err(conv.weight.grad, wr.grad) <= 1e-2, ("dw1", _err(conv.weight.grad, wr.grad))
+    if down:
+        assert _err(dconv.weight.grad, wdr.grad) <= 1e-2, ("dwd", _err(dconv.weight.grad, wdr.grad))
+    C.plans.clear()
