@@ -159,14 +159,24 @@ class ResNet(nn.Module):
         return nn.Sequential(*mods)
 
     fused_bn = False
+    _counted_bns: list = []
 
     def set_fused_bn(self, enabled: bool = True) -> "ResNet":
         """Route every training-mode bn (+ add) + relu through the fused HIP kernels (channels-last
         bf16/fp32 on the GPU; csrc/bn_act.hip). Parameter and buffer names are unchanged."""
         self.fused_bn = bool(enabled)
+        self._counted_bns = []
         for m in self.modules():
             if isinstance(m, (BasicBlock, Bottleneck)):
                 m.fused_bn = self.fused_bn
+            if isinstance(m, nn.BatchNorm2d):
+                # fused training forwards bump every BN's num_batches_tracked in ONE multi-tensor
+                # launch (features()) instead of one add kernel per layer; momentum=None layers
+                # need the count inside their own node and keep counting there
+                batched = self.fused_bn and m.track_running_stats and m.momentum is not None
+                m._dauc_counted = batched
+                if batched:
+                    self._counted_bns.append(m)
         return self
 
     def set_gemm_conv1x1(self, enabled: bool = True) -> "ResNet":
@@ -177,6 +187,8 @@ class ResNet(nn.Module):
         return self
 
     def features(self, x):
+        if self.fused_bn and self.training and x.is_cuda and self._counted_bns:
+            torch._foreach_add_([m.num_batches_tracked for m in self._counted_bns], 1)
         x = _bn_act(self.fused_bn, self.bn1, self.conv1(x))
         if self.fused_bn and x.is_cuda:  # the stem max-pool with int8 indices (pool.py)
             from .pool import max_pool2d

@@ -101,7 +101,7 @@ def bn_act(x: torch.Tensor, bn: nn.BatchNorm2d, relu: bool = True,
                          f"got {tuple(x.shape)} {x.dtype}")
     momentum = 0.0 if bn.momentum is None else bn.momentum
     rm, rv = (bn.running_mean, bn.running_var) if bn.track_running_stats else (None, None)
-    if bn.track_running_stats and bn.num_batches_tracked is not None:
+    if bn.track_running_stats and bn.num_batches_tracked is not None and not getattr(bn, "_dauc_counted", False):
         bn.num_batches_tracked.add_(1)
         if bn.momentum is None:  # cumulative moving average (torch semantics; syncs once)
             momentum = 1.0 / float(bn.num_batches_tracked.item())

@@ -89,3 +89,15 @@ def test_missing_library_fails_loudly(tmp_path, monkeypatch):
     monkeypatch.setattr(_lib, "LIB_PATH", tmp_path / "libdauc.so")
     with pytest.raises(ImportError, match="no CPU fallback"):
         _lib.load()
+
+
+def test_ctypes_signatures_match_header_arity():
+    """Every ctypes prototype has as many parameters as the C declaration in include/dauc.h."""
+    import re
+
+    text = re.sub(r"/\*.*?\*/", "", _lib.HEADER.read_text(), flags=re.S)
+    decls = dict(re.findall(r"\b(dauc_[a-z0-9_]+)\s*\(([^;{]*?)\)\s*;", text))
+    for name, (_, args) in _lib.SIGNATURES.items():
+        params = decls[name].strip()
+        n = 0 if params in ("", "void") else params.count(",") + 1
+        assert n == len(args), (name, n, len(args))

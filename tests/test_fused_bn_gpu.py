@@ -133,3 +133,18 @@ def test_resnet_fused_matches_unfused(dev):
     from bf16_step_compare import compare
 
     compare(dev, fused_bn=True, gemm_1x1=False, check_buffers=True)
+
+
+def test_resnet_fused_counts_batches_once(dev):
+    """Fused training forwards bump every BN's num_batches_tracked once (one multi-tensor launch)."""
+    from distributedauc_amd.backbone import resnet18
+
+    net = resnet18().to(dev).to(memory_format=torch.channels_last).set_fused_bn(True).train()
+    x = torch.randn(4, 3, 32, 32, device=dev).contiguous(memory_format=torch.channels_last)
+    net(x)
+    net(x)
+    counts = {n: int(b) for n, b in net.named_buffers() if n.endswith("num_batches_tracked")}
+    assert counts and set(counts.values()) == {2}, counts
+    net.eval()
+    net(x)
+    assert {int(b) for n, b in net.named_buffers() if n.endswith("num_batches_tracked")} == {2}
