@@ -98,7 +98,7 @@ class Bottleneck(nn.Module):
     def forward(self, x):
         f, g = self.fused_bn, self.gemm_conv1x1
         down = None if self.downsample is None else self.downsample[0]
-        if g and x.is_cuda and (down is None or down.stride == (1, 1)):
+        if g and x.is_cuda:
             # conv1 and the skip branch in one node: the gradient sum at x rides in the dgrad GEMM
             from .conv1x1 import conv1x1_skip
 

@@ -171,19 +171,25 @@ class Conv1x1Function(torch.autograd.Function):
 
 
 class Conv1x1SkipFunction(torch.autograd.Function):
-    """(conv1(x), skip) for a bottleneck block's input x: skip = x (identity) or the stride-1 1x1
-    downsample conv of x (resnet.py:87-108). Backward: dx = dgrad(conv1) + d(skip) with the second
-    GEMM accumulating into the first term in place (beta = 1), so the branch-point gradient sum that
-    autograd would run as a separate add kernel over the block input (ResNet-50 b256: up to 3 x 411
-    MB per block) disappears."""
+    """(conv1(x), skip) for a bottleneck block's input x: skip = x (identity) or the 1x1 downsample
+    conv of x (resnet.py:87-108; stride 1 as a GEMM, stride 2 through MIOpen). Backward: dx = d(skip)
+    + dgrad(conv1), the conv1 dgrad GEMM accumulating into the skip term in place (beta = 1), so the
+    branch-point gradient sum that autograd would run as a separate add kernel over the block input
+    (ResNet-50 b256: up to 3 x 411 MB per block) disappears."""
 
     @staticmethod
-    def forward(ctx, x, w1, wd, skip_grad_owned):
+    def forward(ctx, x, w1, wd, skip_grad_owned, down_stride=1):
         y1, wc1 = _fwd(x, w1)
+        ctx.down_stride = int(down_stride)
         if wd is None:
             skip, wcd = x, None
-        else:
+        elif down_stride == 1:
             skip, wcd = _fwd(x, wd)
+        else:
+            wcd = wd.detach().reshape(wd.shape[0], wd.shape[1]).to(x.dtype)
+            with torch.autocast("cuda", enabled=False):
+                skip = F.conv2d(x, wcd.view(*wd.shape), stride=down_stride).contiguous(
+                    memory_format=torch.channels_last)
         ctx.save_for_backward(x, wc1, wcd)
         ctx.wdtypes = (w1.dtype, None if wd is None else wd.dtype)
         ctx.skip_grad_owned = bool(skip_grad_owned)
@@ -196,8 +202,18 @@ class Conv1x1SkipFunction(torch.autograd.Function):
         gy1 = g21 = gyd = g2d = None
         if g1 is not None:
             gy1, g21 = _prep_grad(g1, x, wc1.shape[0])
-        if gs is not None and wcd is not None:
+        strided = wcd is not None and ctx.down_stride != 1
+        if gs is not None and wcd is not None and not strided:
             gyd, g2d = _prep_grad(gs, x, wcd.shape[0])
+        dx_down = None
+        if gs is not None and strided:
+            # the strided downsample through MIOpen: input and weight grads in one call
+            gsd = gs.to(x.dtype).contiguous(memory_format=torch.channels_last)
+            cout, cin = wcd.shape
+            with torch.autocast("cuda", enabled=False):
+                dx_down, dwd_s, _ = torch.ops.aten.convolution_backward(
+                    gsd, x, wcd.view(cout, cin, 1, 1), None, [ctx.down_stride] * 2, [0, 0], [1, 1], False, [0, 0], 1,
+                    [bool(ctx.needs_input_grad[0]), bool(ctx.needs_input_grad[2]), False])
         if ctx.needs_input_grad[0]:
             if gs is None:
                 base = None
@@ -208,6 +224,8 @@ class Conv1x1SkipFunction(torch.autograd.Function):
                 base = gs.to(x.dtype).contiguous(memory_format=torch.channels_last)
                 if base is gs and not ctx.skip_grad_owned:
                     base = base.clone(memory_format=torch.channels_last)
+            elif strided:
+                base = dx_down.contiguous(memory_format=torch.channels_last)
             else:
                 base = _dgrad(gyd, g2d, x, wcd)
             if g1 is None:
@@ -219,8 +237,11 @@ class Conv1x1SkipFunction(torch.autograd.Function):
         if ctx.needs_input_grad[1] and g1 is not None:
             dw1 = _wgrad(gy1, g21, x, wc1, ctx.wdtypes[0])
         if wcd is not None and ctx.needs_input_grad[2] and gs is not None:
-            dwd = _wgrad(gyd, g2d, x, wcd, ctx.wdtypes[1])
-        return dx, dw1, dwd, None
+            if strided:
+                dwd = dwd_s.to(ctx.wdtypes[1]).view(cout, cin, 1, 1)
+            else:
+                dwd = _wgrad(gyd, g2d, x, wcd, ctx.wdtypes[1])
+        return dx, dw1, dwd, None, None
 
 
 def conv1x1(conv: nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
@@ -235,20 +256,22 @@ def conv1x1(conv: nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
     return Conv1x1Function.apply(x, conv.weight)
 
 
-def _gemm_ok(conv: nn.Conv2d | None, x: torch.Tensor) -> bool:
-    return conv is None or (conv.kernel_size == (1, 1) and conv.stride == (1, 1) and conv.groups == 1
-                            and conv.bias is None and conv.padding == (0, 0))
+def _gemm_ok(conv: nn.Conv2d | None, x: torch.Tensor, any_stride: bool = False) -> bool:
+    return conv is None or (conv.kernel_size == (1, 1) and conv.groups == 1 and conv.bias is None
+                            and conv.padding == (0, 0) and conv.dilation == (1, 1)
+                            and (conv.stride == (1, 1) or (any_stride and conv.stride[0] == conv.stride[1])))
 
 
 def conv1x1_skip(conv: nn.Conv2d, x: torch.Tensor, down: nn.Conv2d | None = None, skip_grad_owned: bool = False):
     """``(conv(x), x if down is None else down(x))`` for a bottleneck's stride-1 1x1 conv1 and its
-    identity / stride-1 1x1 downsample branch, with the branch-point gradient sum fused into the
+    identity / 1x1 downsample branch (any stride), with the branch-point gradient sum fused into the
     dgrad GEMM (Conv1x1SkipFunction). ``skip_grad_owned``: the skip's consumer hands back a gradient
     tensor nobody else holds (the fused BN node does), so it may be accumulated into in place.
     Other shapes: the two branches separately."""
     if (x.device.type != "cuda" or not x.is_contiguous(memory_format=torch.channels_last)
-            or not _gemm_ok(conv, x) or not _gemm_ok(down, x)):
+            or not _gemm_ok(conv, x) or not _gemm_ok(down, x, any_stride=True)):
         return conv1x1(conv, x), (x if down is None else conv1x1(down, x))
     if torch.is_autocast_enabled("cuda") and x.dtype == torch.float32:
         x = x.to(torch.get_autocast_dtype("cuda"))
-    return Conv1x1SkipFunction.apply(x, conv.weight, None if down is None else down.weight, skip_grad_owned)
+    return Conv1x1SkipFunction.apply(x, conv.weight, None if down is None else down.weight, skip_grad_owned,
+                                     1 if down is None else down.stride[0])

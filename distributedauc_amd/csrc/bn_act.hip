@@ -32,6 +32,7 @@ namespace dauc {
 namespace {
 
 constexpr int kBnThreads = 256;
+constexpr int kDefaultPartThreads = 512;  // profiles/r01/ab_bn_threads.jsonl
 constexpr int kMaxRowBlocks = 2048;  // partial rows per channel (workspace bound)
 constexpr int kFinThreads = 1024;    // finalize: 64 row subsets x 16 channel quads
 constexpr int kFinSubsets = kFinThreads / 16;
@@ -44,6 +45,18 @@ int row_block_target() {
         const char* e = getenv("DAUC_BN_ROWBLOCKS");
         int t = e ? atoi(e) : 256;
         v = (t >= 1 && t <= kMaxRowBlocks) ? t : 256;
+    }
+    return v;
+}
+// threads per workgroup of the partial-sum passes (DAUC_BN_PART_THREADS: 256 | 512 | 1024). With
+// ~256 row blocks the grid is about one workgroup per CU, so the workgroup size sets the bytes
+// in flight per CU.
+int part_threads() {
+    static int v = 0;
+    if (v == 0) {
+        const char* e = getenv("DAUC_BN_PART_THREADS");
+        const int t = e ? atoi(e) : kDefaultPartThreads;
+        v = (t == 256 || t == 512 || t == 1024) ? t : kDefaultPartThreads;
     }
     return v;
 }
@@ -122,7 +135,7 @@ struct Geometry {
     int64_t rows; // rows per row block
 };
 
-int make_geometry(int64_t M, int C, int elem_bytes, Geometry& g) {
+int make_geometry(int64_t M, int C, int elem_bytes, Geometry& g, int threads = kBnThreads) {
     g.N = 16 / elem_bytes;
     if (M <= 0 || C <= 0 || C % g.N != 0) return DAUC_EINVAL;
     const int CV = C / g.N;
@@ -130,7 +143,7 @@ int make_geometry(int64_t M, int C, int elem_bytes, Geometry& g) {
     if (kBnThreads % g.TPR != 0 || CV % g.TPR != 0) return DAUC_EINVAL;  // power-of-two vector counts
     g.CT = g.TPR * g.N;
     g.ctiles = C / g.CT;
-    g.RPB = kBnThreads / g.TPR;
+    g.RPB = threads / g.TPR;
     int64_t target = (row_block_target() + g.ctiles - 1) / g.ctiles;
     const int64_t passes = (M + g.RPB - 1) / g.RPB;
     if (target > passes) target = passes;
@@ -148,14 +161,14 @@ int make_geometry(int64_t M, int C, int elem_bytes, Geometry& g) {
 // factor is (mean - k)^2 / var = O(1)); k is written as a third partial row.
 // Backward: g = dy * [y > 0] (RELU) or dy; s1 = sum g, s2 = sum g * (x - mean); g is
 // written to dz (the residual branch's gradient) when dz != nullptr.
-template <typename T, bool STATS, bool RELU>
-__global__ __launch_bounds__(kBnThreads) void bn_partial_kernel(
+template <typename T, bool STATS, bool RELU, int TH>
+__global__ __launch_bounds__(TH) void bn_partial_kernel(
     const T* __restrict__ x, const T* __restrict__ dy, const T* __restrict__ y, T* __restrict__ dz, int64_t M,
     int C, int CT, int64_t rows_per_block, const float* __restrict__ center, float* __restrict__ partials) {
     constexpr int N = VecT<T>::N;
-    __shared__ float red[2 * kBnThreads * N];
+    __shared__ float red[2 * TH * N];
     const int TPR = CT / N;
-    const int RPB = kBnThreads / TPR;
+    const int RPB = TH / TPR;
     const int cl = (threadIdx.x % TPR) * N;  // channel offset within the tile
     const int c0 = blockIdx.y * CT + cl;
     const int r0 = threadIdx.x / TPR;
@@ -245,14 +258,14 @@ __global__ __launch_bounds__(kBnThreads) void bn_partial_kernel(
 
     // fixed-order reduction over the RPB rows of the pass
     float* r1 = red;
-    float* r2 = red + kBnThreads * N;
+    float* r2 = red + TH * N;
 #pragma unroll
     for (int i = 0; i < N; ++i) {
         r1[r0 * CT + cl + i] = s1[i];
         r2[r0 * CT + cl + i] = s2[i];
     }
     __syncthreads();
-    for (int j = threadIdx.x; j < 2 * CT; j += kBnThreads) {
+    for (int j = threadIdx.x; j < 2 * CT; j += TH) {
         const int stat = j / CT, c = j % CT;
         const float* src = stat ? r2 : r1;
         float acc = 0.f;
@@ -480,17 +493,32 @@ int launch_elementwise(const T* x, const T* g_in, const T* aux, T* out, int64_t 
     return launch_status();
 }
 
+template <typename T, bool STATS, bool RELU>
+void launch_partial(int th, const Geometry& g, const T* x, const T* dy, const T* y, T* dz, int64_t M, int C,
+                    const float* center, float* partials, hipStream_t st) {
+    const dim3 grid(g.nrb, g.ctiles);
+    if (th == 1024)
+        hipLaunchKernelGGL((bn_partial_kernel<T, STATS, RELU, 1024>), grid, dim3(1024), 0, st, x, dy, y, dz, M, C,
+                           g.CT, g.rows, center, partials);
+    else if (th == 512)
+        hipLaunchKernelGGL((bn_partial_kernel<T, STATS, RELU, 512>), grid, dim3(512), 0, st, x, dy, y, dz, M, C,
+                           g.CT, g.rows, center, partials);
+    else
+        hipLaunchKernelGGL((bn_partial_kernel<T, STATS, RELU, 256>), grid, dim3(256), 0, st, x, dy, y, dz, M, C,
+                           g.CT, g.rows, center, partials);
+}
+
 template <typename T>
 int bn_forward_t(const T* x, int64_t M, int C, const T* res, int relu, const float* gamma, const float* beta,
                  float* running_mean, float* running_var, float momentum, float eps, T* y, float* save_mean,
                  float* save_invstd, void* ws, size_t ws_bytes, hipStream_t st) {
     Geometry g;
-    if (make_geometry(M, C, sizeof(T), g) != DAUC_OK) return DAUC_EINVAL;
+    const int th = part_threads();
+    if (make_geometry(M, C, sizeof(T), g, th) != DAUC_OK) return DAUC_EINVAL;
     if (ws == nullptr || ws_bytes < ws_bytes_for(C) || !aligned16p(ws)) return DAUC_EINVAL;
     if ((running_mean == nullptr) != (running_var == nullptr)) return DAUC_EINVAL;
     const BnWs w = carve(ws, C);
-    hipLaunchKernelGGL((bn_partial_kernel<T, true, false>), dim3(g.nrb, g.ctiles), dim3(kBnThreads), 0, st, x,
-                       nullptr, nullptr, nullptr, M, C, g.CT, g.rows, nullptr, w.partials);
+    launch_partial<T, true, false>(th, g, x, nullptr, nullptr, nullptr, M, C, nullptr, w.partials, st);
     hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((C + 63) / 64), dim3(kFinThreads), 0, st, w.partials, g.nrb,
                        g.rows, M, C, gamma, beta, running_mean, running_var, momentum, eps, save_mean, save_invstd, w.c0, w.c1, w.c3);
     int rc = launch_status();
@@ -507,16 +535,15 @@ int bn_backward_t(const T* dy, const T* y, const T* x, int64_t M, int C, int rel
                   const float* save_mean, const float* save_invstd, T* dres, T* dx, float* dgamma, float* dbeta,
                   void* ws, size_t ws_bytes, hipStream_t st) {
     Geometry g;
-    if (make_geometry(M, C, sizeof(T), g) != DAUC_OK) return DAUC_EINVAL;
+    const int th = part_threads();
+    if (make_geometry(M, C, sizeof(T), g, th) != DAUC_OK) return DAUC_EINVAL;
     if (ws == nullptr || ws_bytes < ws_bytes_for(C) || !aligned16p(ws)) return DAUC_EINVAL;
     if (relu && y == nullptr) return DAUC_EINVAL;
     const BnWs w = carve(ws, C);
     if (relu)
-        hipLaunchKernelGGL((bn_partial_kernel<T, false, true>), dim3(g.nrb, g.ctiles), dim3(kBnThreads), 0, st, x, dy,
-                           y, dres, M, C, g.CT, g.rows, save_mean, w.partials);
+        launch_partial<T, false, true>(th, g, x, dy, y, dres, M, C, save_mean, w.partials, st);
     else
-        hipLaunchKernelGGL((bn_partial_kernel<T, false, false>), dim3(g.nrb, g.ctiles), dim3(kBnThreads), 0, st, x,
-                           dy, nullptr, dres, M, C, g.CT, g.rows, save_mean, w.partials);
+        launch_partial<T, false, false>(th, g, x, dy, nullptr, dres, M, C, save_mean, w.partials, st);
     hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(kFinThreads), 0, st, w.partials, g.nrb, M, C,
                        gamma, save_mean, save_invstd, dgamma, dbeta, w.c0, w.c1, w.c2, w.c3);
     int rc = launch_status();

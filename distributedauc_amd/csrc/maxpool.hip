@@ -113,15 +113,16 @@ __global__ __launch_bounds__(kPoolThreads) void maxpool_fwd_kernel(const T* __re
     constexpr int V = PoolVec<T>::N;
     typedef typename PoolVec<T>::Raw Raw;
     typedef typename PoolVec<T>::Idx Idx;
+    // blockIdx.y = image: 32-bit index arithmetic within one image (checked on the host)
     const int cv = g.C / V;
-    const int64_t total = g.N * g.Ho * g.Wo * cv;
-    const int64_t t = int64_t(blockIdx.x) * kPoolThreads + threadIdx.x;
-    if (t >= total) return;
-    const int c = static_cast<int>(t % cv) * V;
-    const int64_t pix = t / cv;  // output pixel (n, oh, ow)
-    const int ow = static_cast<int>(pix % g.Wo);
-    const int oh = static_cast<int>((pix / g.Wo) % g.Ho);
-    const int64_t n = pix / (int64_t(g.Wo) * g.Ho);
+    const int t = blockIdx.x * kPoolThreads + threadIdx.x;
+    if (t >= g.Ho * g.Wo * cv) return;
+    const int c = (t % cv) * V;
+    const int q = t / cv;  // output pixel (oh, ow) of image n
+    const int ow = q % g.Wo;
+    const int oh = q / g.Wo;
+    const int64_t n = blockIdx.y;
+    const int64_t pix = n * g.Ho * g.Wo + q;
     const int hs = oh * g.s - g.p, ws = ow * g.s - g.p;
     const int h0 = hs > 0 ? hs : 0, w0 = ws > 0 ? ws : 0;
     const int h1 = hs + g.k < g.H ? hs + g.k : g.H, w1 = ws + g.k < g.W ? ws + g.k : g.W;
@@ -159,14 +160,14 @@ __global__ __launch_bounds__(kPoolThreads) void maxpool_bwd_kernel(const T* __re
     typedef typename PoolVec<T>::Raw Raw;
     typedef typename PoolVec<T>::Idx Idx;
     const int cv = g.C / V;
-    const int64_t total = g.N * g.H * g.W * cv;
-    const int64_t t = int64_t(blockIdx.x) * kPoolThreads + threadIdx.x;
-    if (t >= total) return;
-    const int c = static_cast<int>(t % cv) * V;
-    const int64_t pix = t / cv;  // input pixel (n, ih, iw)
-    const int iw = static_cast<int>(pix % g.W);
-    const int ih = static_cast<int>((pix / g.W) % g.H);
-    const int64_t n = pix / (int64_t(g.W) * g.H);
+    const int t = blockIdx.x * kPoolThreads + threadIdx.x;
+    if (t >= g.H * g.W * cv) return;
+    const int c = (t % cv) * V;
+    const int q = t / cv;  // input pixel (ih, iw) of image n
+    const int iw = q % g.W;
+    const int ih = q / g.W;
+    const int64_t n = blockIdx.y;
+    const int64_t pix = n * g.H * g.W + q;
     // torch's p_start / p_end (dilation 1)
     const int ph0 = (ih + g.p < g.k) ? 0 : (ih + g.p - g.k) / g.s + 1;
     const int pw0 = (iw + g.p < g.k) ? 0 : (iw + g.p - g.k) / g.s + 1;
@@ -207,10 +208,10 @@ bool pool_args_ok(const void* a, const void* b, const void* c, int dtype, int64_
     return true;
 }
 
-int pool_grid(int64_t threads, unsigned* grid) {
-    const int64_t g = (threads + kPoolThreads - 1) / kPoolThreads;
-    if (g < 1 || g > 0x7fffffffLL) return DAUC_EINVAL;
-    *grid = static_cast<unsigned>(g);
+// grid: x covers one image's (pixel, vector) pairs, y the images
+int pool_grid(int64_t per_image, int64_t N, dim3* grid) {
+    if (per_image < 1 || per_image > 0x7fffffffLL - kPoolThreads || N < 1 || N > 65535) return DAUC_EINVAL;
+    *grid = dim3(static_cast<unsigned>((per_image + kPoolThreads - 1) / kPoolThreads), static_cast<unsigned>(N));
     return DAUC_OK;
 }
 
@@ -226,14 +227,14 @@ int dauc_maxpool2d_forward(const void* x, int dtype, int64_t N, int H, int W, in
     if (!pool_args_ok(x, argmax, y, dtype, N, H, W, C, kernel, stride, pad, Ho, Wo)) return DAUC_EINVAL;
     const PoolGeom g{N, H, W, C, kernel, stride, pad, Ho, Wo};
     const int V = dtype == DAUC_DTYPE_BF16 ? 8 : 4;
-    unsigned grid;
-    if (pool_grid(N * Ho * Wo * (C / V), &grid)) return DAUC_EINVAL;
+    dim3 grid;
+    if (pool_grid(int64_t(Ho) * Wo * (C / V), N, &grid)) return DAUC_EINVAL;
     hipStream_t st = as_hip(stream);
     if (dtype == DAUC_DTYPE_BF16)
-        hipLaunchKernelGGL(maxpool_fwd_kernel<__hip_bfloat16>, dim3(grid), dim3(kPoolThreads), 0, st,
+        hipLaunchKernelGGL(maxpool_fwd_kernel<__hip_bfloat16>, grid, dim3(kPoolThreads), 0, st,
                            static_cast<const __hip_bfloat16*>(x), g, static_cast<__hip_bfloat16*>(y), argmax);
     else
-        hipLaunchKernelGGL(maxpool_fwd_kernel<float>, dim3(grid), dim3(kPoolThreads), 0, st,
+        hipLaunchKernelGGL(maxpool_fwd_kernel<float>, grid, dim3(kPoolThreads), 0, st,
                            static_cast<const float*>(x), g, static_cast<float*>(y), argmax);
     return launch_status();
 }
@@ -243,14 +244,14 @@ int dauc_maxpool2d_backward(const void* dy, const int8_t* argmax, int dtype, int
     if (!pool_args_ok(dy, argmax, dx, dtype, N, H, W, C, kernel, stride, pad, Ho, Wo)) return DAUC_EINVAL;
     const PoolGeom g{N, H, W, C, kernel, stride, pad, Ho, Wo};
     const int V = dtype == DAUC_DTYPE_BF16 ? 8 : 4;
-    unsigned grid;
-    if (pool_grid(N * H * W * (C / V), &grid)) return DAUC_EINVAL;
+    dim3 grid;
+    if (pool_grid(int64_t(H) * W * (C / V), N, &grid)) return DAUC_EINVAL;
     hipStream_t st = as_hip(stream);
     if (dtype == DAUC_DTYPE_BF16)
-        hipLaunchKernelGGL(maxpool_bwd_kernel<__hip_bfloat16>, dim3(grid), dim3(kPoolThreads), 0, st,
+        hipLaunchKernelGGL(maxpool_bwd_kernel<__hip_bfloat16>, grid, dim3(kPoolThreads), 0, st,
                            static_cast<const __hip_bfloat16*>(dy), argmax, g, static_cast<__hip_bfloat16*>(dx));
     else
-        hipLaunchKernelGGL(maxpool_bwd_kernel<float>, dim3(grid), dim3(kPoolThreads), 0, st,
+        hipLaunchKernelGGL(maxpool_bwd_kernel<float>, grid, dim3(kPoolThreads), 0, st,
                            static_cast<const float*>(dy), argmax, g, static_cast<float*>(dx));
     return launch_status();
 }

@@ -307,7 +307,7 @@ int dauc_bn_act_backward(const void* dy, const void* y, const void* x, int dtype
 
 /*
  * Max pooling over channels-last x [N, H, W, C] (bf16 or fp32; C a multiple of the
- * 16-byte vector; 16-byte aligned), square kernel, stride, zero-free padding
+ * 16-byte vector; 16-byte aligned; N <= 65535), square kernel, stride, zero-free padding
  * (pad <= kernel / 2, kernel^2 <= 127), floor mode: Ho = (H + 2 pad - kernel) / stride + 1.
  * Replaces torch's max_pool2d_with_indices of resnet.py:205 (the stem). argmax int8
  * [N, Ho, Wo, C] (8-byte aligned) receives each maximum's position inside its window

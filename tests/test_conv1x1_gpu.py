@@ -69,19 +69,21 @@ def test_resnet_gemm_conv1x1_trains(dev):
     compare(dev, fused_bn=True, gemm_1x1=True)
 
 
-@pytest.mark.parametrize("down", [False, True])
+@pytest.mark.parametrize("down", [0, 1, 2])
 @pytest.mark.parametrize("owned", [False, True])
 @pytest.mark.parametrize("acc_engine", ["gemm", "conv"])
 def test_conv1x1_skip_fuses_branch_gradient(dev, down, owned, acc_engine):
     """(conv1(x), skip) in one node: dx = dgrad(conv1) + d(skip), the sum accumulated by the GEMM
-    (beta = 1, in place) or by an add after MIOpen's dgrad; vs fp64 autograd of the two branches.
+    (beta = 1, in place) or by an add after MIOpen's dgrad; skip = identity (down 0) or a 1x1
+    downsample of stride 1 (GEMM) / 2 (MIOpen); vs fp64 autograd of the two branches.
     Also: the incoming skip gradient is left untouched unless the caller marked it as owned."""
     from distributedauc_amd import conv1x1 as C
 
     torch.manual_seed(7 + down + 2 * owned)
     N, cin, width, H = 4, 256, 64, 14
     conv = nn.Conv2d(cin, width, 1, bias=False).to(dev).to(memory_format=torch.channels_last)
-    dconv = nn.Conv2d(cin, 4 * width, 1, bias=False).to(dev).to(memory_format=torch.channels_last) if down else None
+    dconv = (nn.Conv2d(cin, 4 * width, 1, stride=down, bias=False).to(dev).to(memory_format=torch.channels_last)
+             if down else None)
     x = torch.randn(N, cin, H, H, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
     M = N * H * H
     C.plans.clear()
@@ -103,7 +105,7 @@ def test_conv1x1_skip_fuses_branch_gradient(dev, down, owned, acc_engine):
     hr = F.conv2d(xr, wr)
     if down:
         wdr = dconv.weight.detach().cpu().double().to(torch.bfloat16).double().requires_grad_(True)
-        sr = F.conv2d(xr, wdr)
+        sr = F.conv2d(xr, wdr, stride=down)
     else:
         sr = xr
     torch.autograd.backward([hr, sr], [gh.cpu().double(), gs_copy.cpu().double()])
