@@ -74,6 +74,7 @@ SIGNATURES = {
                                     _sz, _vp]),
     "dauc_maxpool2d_forward": (_int, [_vp, _int, _i64, _int, _int, _int, _int, _int, _int, _vp, _vp, _int, _int,
                                       _vp]),
+    "dauc_slab_sum": (_int, [_vp, _i64, _i64, _vp, _vp]),
     "dauc_maxpool2d_backward": (_int, [_vp, _vp, _int, _i64, _int, _int, _int, _int, _int, _int, _int, _int, _vp,
                                        _vp]),
 }

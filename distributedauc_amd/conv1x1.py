@@ -25,6 +25,30 @@ __all__ = ["conv1x1", "conv1x1_skip", "Conv1x1Function", "Conv1x1SkipFunction", 
 plans: dict = {}  # (M, Cin, Cout, dtype, direction) -> engine
 
 
+def _L():
+    from . import _lib
+
+    return _lib.load()
+
+
+def _ptr(t):
+    from .ops import _ptr as p
+
+    return p(t)
+
+
+def _stream(dev):
+    from .ops import _stream as st
+
+    return st(dev)
+
+
+def _check(rc, what):
+    from .ops import check
+
+    check(rc, what)
+
+
 def _timed(fn, reps=3):
     torch.cuda.synchronize()
     best = float("inf")
@@ -63,7 +87,11 @@ def _wgrad_gemm(g2, x2, slabs):
         return torch.mm(g2.t(), x2, out_dtype=torch.float32)
     part = torch.bmm(g2.view(slabs, M // slabs, cout).transpose(1, 2), x2.view(slabs, M // slabs, cin),
                      out_dtype=torch.float32)
-    return part.sum(0)
+    if (cout * cin) % 4:
+        return part.sum(0)
+    out = torch.empty((cout, cin), dtype=torch.float32, device=part.device)
+    _check(_L().dauc_slab_sum(_ptr(part), slabs, cout * cin, _ptr(out), _stream(part.device)), "dauc_slab_sum")
+    return out
 
 
 def _fwd(x, weight):

@@ -322,6 +322,15 @@ int dauc_maxpool2d_forward(const void* x, int dtype, int64_t N, int H, int W, in
 int dauc_maxpool2d_backward(const void* dy, const int8_t* argmax, int dtype, int64_t N, int H, int W, int C,
                             int kernel, int stride, int pad, int Ho, int Wo, void* dx, dauc_stream_t stream);
 
+/* ---------------------------------- backbone: split-K weight-gradient sum */
+
+/*
+ * out[i] = sum over s = 0 .. S-1 (ascending) of part[s * n + i], fp32; n % 4 == 0, 16-byte
+ * aligned pointers. The last step of the 1x1 convolutions' split-K weight gradient
+ * (conv1x1.py: S slab GEMMs over the N*H*W rows). Bitwise reproducible.
+ */
+int dauc_slab_sum(const float* part, int64_t S, int64_t n, float* out, dauc_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -115,3 +115,21 @@ def test_conv1x1_skip_fuses_branch_gradient(dev, down, owned, acc_engine):
     if down:
         assert _err(dconv.weight.grad, wdr.grad) <= 1e-2, ("dwd", _err(dconv.weight.grad, wdr.grad))
     C.plans.clear()
+
+
+@pytest.mark.parametrize("S,n", [(1, 4), (8, 64 * 256), (32, 2048 * 512), (13, 1028), (128, 256 * 64)])
+def test_slab_sum_matches_sequential_fp32(dev, S, n):
+    """dauc_slab_sum: out = sum of S slabs in ascending slab order, bit-identical to sequential
+    fp32 adds (the split-K weight-gradient reduction of the 1x1 convolutions)."""
+    from distributedauc_amd import _lib
+    from distributedauc_amd.ops import _ptr, _stream, check
+
+    g = torch.Generator(device=dev).manual_seed(S * 7 + n)
+    part = torch.randn((S, n), device=dev, generator=g) * torch.rand((S, 1), device=dev, generator=g) * 100
+    out = torch.empty(n, device=dev)
+    check(_lib.load().dauc_slab_sum(_ptr(part), S, n, _ptr(out), _stream(dev)), "dauc_slab_sum")
+    ref = torch.zeros(n, device=dev)
+    for s in range(S):
+        ref += part[s]
+    assert torch.equal(out, ref)
+    assert _lib.load().dauc_slab_sum(_ptr(part), S, n - 2, _ptr(out), _stream(dev)) == _lib.DAUC_EINVAL
