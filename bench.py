@@ -41,6 +41,7 @@ HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # lane-ops/s (157.3 TF / 2) -> 2.62e13 pairs/s per GPU. (SURVEY §8d's 1.97e13 assumed 16-wide
 # SIMDs and 2 compares per pair.)
 VALU_PAIR_PEAK = 2.62e13
+XGMI_PEAK_GBS = 7 * 153.0   # one GPU's 7 xGMI links x ~153 GB/s (the ring all-reduce's bus-bandwidth ceiling)
 METRIC = "CoDA train imgs/sec + exact-AUC pos×neg pairs/sec at 1/2/4/8 MI355X"
 
 
@@ -170,10 +171,36 @@ def bench_train(args, world, rank, device):
     upd_ms = upd.mean_ms()
     upd_bytes = coda.state.bytes_per_update(True)
     sur_ms = sur.mean_ms()
-    return {
+    out = {
         "dt": dt, "imgs": world * args.batch * args.steps, "loss": loss, "n_params": n_params,
         "update_ms": upd_ms, "update_bytes": upd_bytes, "surrogate_us": sur_ms * 1e3,
     }
+    if world > 1:
+        out["coda_round"] = bench_coda_round(coda, world)
+    return out
+
+
+def bench_coda_round(coda, world, reps=5):
+    """One CoDA round (main.py:33-54) after the timed steps: the all-reduce of flat[:n_reduce]
+    (parameters, a, b, alpha, class counts) + the finalise launch, HIP events on the current stream
+    around `reps` rounds (the collective's stream is joined to it), max over ranks. Bus bytes per
+    round = 2 (G-1)/G x payload."""
+    nbytes = coda.state.n_reduce * 4
+    torch.cuda.synchronize()
+    dist.barrier()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    with torch.no_grad():
+        e0.record()
+        for _ in range(reps):
+            coda.average_all()
+        e1.record()
+    e1.synchronize()
+    ms = max_over_ranks(e0.elapsed_time(e1) / reps, world)
+    bus = 2 * (world - 1) / world * nbytes / (ms / 1e3) / 1e9
+    return {"workload": f"all-reduce of {nbytes} B (params + a, b, alpha + class counts) + finalise, {world} ranks",
+            "ms_per_round": ms, "payload_bytes": nbytes, "rounds_per_step": 1.0 / coda.I,
+            "roofline": {"bound": "xgmi", "achieved": bus, "peak": XGMI_PEAK_GBS, "unit": "GB/s (bus)",
+                         "frac": bus / XGMI_PEAK_GBS}}
 
 
 def bench_auc(args, world, rank, device, log2n=None, pos=None, pair_reps=None):
@@ -395,6 +422,7 @@ def main():
                              "frac": upd_gbs / HBM_PEAK_GBS, "traffic": load_traffic("pd_update"),
                              "bytes_per_launch": res["update_bytes"], "avg_launch_us": res["update_ms"] * 1e3},
                 "surrogate_us_per_call": res["surrogate_us"],
+                **({"coda_round": res["coda_round"]} if "coda_round" in res else {}),
                 "final_loss": res["loss"],
             })
         if sur is not None:
