@@ -20,33 +20,13 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from . import _lib
+from .ops import _ptr, _stream, check
+
 __all__ = ["conv1x1", "conv1x1_skip", "Conv1x1Function", "Conv1x1SkipFunction", "plans"]
 
 plans: dict = {}  # (M, Cin, Cout, dtype, direction) -> engine
 
-
-def _L():
-    from . import _lib
-
-    return _lib.load()
-
-
-def _ptr(t):
-    from .ops import _ptr as p
-
-    return p(t)
-
-
-def _stream(dev):
-    from .ops import _stream as st
-
-    return st(dev)
-
-
-def _check(rc, what):
-    from .ops import check
-
-    check(rc, what)
 
 
 def _timed(fn, reps=3):
@@ -90,7 +70,8 @@ def _wgrad_gemm(g2, x2, slabs):
     if (cout * cin) % 4:
         return part.sum(0)
     out = torch.empty((cout, cin), dtype=torch.float32, device=part.device)
-    _check(_L().dauc_slab_sum(_ptr(part), slabs, cout * cin, _ptr(out), _stream(part.device)), "dauc_slab_sum")
+    check(_lib.load().dauc_slab_sum(_ptr(part), slabs, cout * cin, _ptr(out), _stream(part.device)),
+          "dauc_slab_sum")
     return out
 
 
