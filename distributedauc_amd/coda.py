@@ -141,7 +141,15 @@ class CoDA:
         if self.t_total % self.I == 0:
             with torch.no_grad():
                 self.average_all()
-        y8 = st.y8(B)
+        self.last_loss = self.step_body(x, labels)
+        return self.last_loss
+
+    def step_body(self, x: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
+        """main.py:303-334 without the round trigger: label map + p_hat, forward, surrogate,
+        backward, pd_update, zero_grad. Stream-ordered with no host sync, so it can be
+        captured in a HIP graph (the lr it bakes in changes only at a stage start)."""
+        st = self.state
+        y8 = st.y8(labels.numel())
         ops.label_map_phat(labels, self.split_index, y8, st.lcounts, st.gcounts, st.p_hat)
         if self.head == "logits":
             loss = auc_surrogate_logits(self.forward(x), y8, st.abalpha, st.p_hat, st.grad3)
@@ -150,8 +158,7 @@ class CoDA:
         loss.backward()
         st.update(self.lr, self.gamma, self.mode)
         self.model.zero_grad(set_to_none=True)
-        self.last_loss = loss.detach()
-        return self.last_loss
+        return loss.detach()
 
     # ---------------------------------------------------------------- loop
     def run(self, batches: Iterator, *, num_stages: int, total_iter: int, test_freq: int | None = None,
