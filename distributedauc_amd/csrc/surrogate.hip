@@ -79,20 +79,23 @@ struct SurrogateScalars {
     float c_neg, k_neg;    // dF/dh = c_neg * (h - k_neg) for y = -1
 };
 
-__device__ __forceinline__ SurrogateScalars make_scalars(const float* abalpha, const float* p_hat,
-                                                         double invB) {
+__device__ __forceinline__ SurrogateScalars make_scalars_v(float a, float b, float alpha, float p, double invB) {
     SurrogateScalars s;
-    s.af = abalpha[0];
-    s.bf = abalpha[1];
+    s.af = a;
+    s.bf = b;
     s.a = s.af;
     s.b = s.bf;
-    s.alpha = abalpha[2];
-    s.p = p_hat[0];
+    s.alpha = alpha;
+    s.p = p;
     s.c_pos = static_cast<float>(2.0 * (1.0 - s.p) * invB);
     s.k_pos = static_cast<float>(s.a + 1.0 + s.alpha);
     s.c_neg = static_cast<float>(2.0 * s.p * invB);
     s.k_neg = static_cast<float>(s.b - 1.0 - s.alpha);
     return s;
+}
+
+__device__ __forceinline__ SurrogateScalars make_scalars(const float* abalpha, const float* p_hat, double invB) {
+    return make_scalars_v(abalpha[0], abalpha[1], abalpha[2], p_hat[0], invB);
 }
 
 // Per-thread state: fp32 partials over one float4 slot, folded into fp64 per slot.
@@ -531,6 +534,17 @@ __global__ __launch_bounds__(kThreads) void surrogate_rows_reduce_kernel(
     const float* __restrict__ p_hat, double* __restrict__ out64, float* __restrict__ grad3, float* __restrict__ loss,
     double* __restrict__ sums4, int accumulate) {
     __shared__ double scratch[kNumAcc * kWaves];
+    // Workgroup 0's scalar inputs are read up front: after the hand-off they would be one more
+    // dependent round trip to memory at the very end of the call.
+    __shared__ int bad;
+    if (threadIdx.x == 0) bad = 0;  // ordered before any write by block_sum's barriers
+    float sc[4] = {0.f, 0.f, 0.f, 0.f};
+    if (!CLASS_ONLY && blockIdx.x == 0) {
+        sc[0] = abalpha[0];
+        sc[1] = abalpha[1];
+        sc[2] = abalpha[2];
+        sc[3] = p_hat[0];
+    }
     double tot[kNumAcc];
 #pragma unroll
     for (int k = 0; k < kNumAcc; ++k) tot[k] = 0.0;
@@ -549,15 +563,26 @@ __global__ __launch_bounds__(kThreads) void surrogate_rows_reduce_kernel(
     }
 #pragma unroll
     for (int j = 0; j < kPer; ++j) {
-        const int64_t r = r0 + threadIdx.x + int64_t(j) * kThreads;
 #pragma unroll
         for (int q = 0; q < 3; ++q) {
             tot[2 * q] += v[j][q].x;
             tot[2 * q + 1] += v[j][q].y;
-            if (r < r1) reinterpret_cast<f64x2*>(rows + r * kRowWords)[q] = f64x2{0.0, 0.0};
         }
     }
     block_sum<kNumAcc>(tot, scratch);
+    // The rows are zeroed again for the next call only after the totals are on their way:
+    // stores count in vmcnt, so zeroing before the sums would put their write acks on the
+    // critical path.
+    auto zero_rows = [&]() {
+#pragma unroll
+        for (int j = 0; j < kPer; ++j) {
+            const int64_t r = r0 + threadIdx.x + int64_t(j) * kThreads;
+            if (r < r1) {
+#pragma unroll
+                for (int q = 0; q < 3; ++q) reinterpret_cast<f64x2*>(rows + r * kRowWords)[q] = f64x2{0.0, 0.0};
+            }
+        }
+    };
     unsigned long long* words = reinterpret_cast<unsigned long long*>(ws.brows);
     if (blockIdx.x > 0) {
         if (threadIdx.x == 0) {
@@ -566,8 +591,10 @@ __global__ __launch_bounds__(kThreads) void surrogate_rows_reduce_kernel(
                 __hip_atomic_store((gu64*)(words + int64_t(blockIdx.x) * kRowWords + k), enc_word(tot[k]),
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
+        zero_rows();
         return;
     }
+    zero_rows();
     bool ok = true;
     if (gridDim.x > 1) {
         double rest[kNumAcc];
@@ -600,8 +627,11 @@ __global__ __launch_bounds__(kThreads) void surrogate_rows_reduce_kernel(
                 __hip_atomic_store((gu64*)(row + k), 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
         }
+        // a timed-out poll in any thread: an LDS flag (block_sum's barriers order it) instead of
+        // __syncthreads_or, whose block-size read would be one more memory trip at the end
+        if (!ok) bad = 1;
         block_sum<kNumAcc>(rest, scratch);
-        ok = __syncthreads_or(!ok) == 0;
+        ok = bad == 0;
 #pragma unroll
         for (int k = 0; k < kNumAcc; ++k) tot[k] += rest[k];
     }
@@ -613,7 +643,7 @@ __global__ __launch_bounds__(kThreads) void surrogate_rows_reduce_kernel(
         if (CLASS_ONLY) {
             emit_class_sums(tot, sums4, accumulate);
         } else {
-            const SurrogateScalars s = make_scalars(abalpha, p_hat, invB);
+            const SurrogateScalars s = make_scalars_v(sc[0], sc[1], sc[2], sc[3], invB);
             finalize(tot, s, invB, out64, grad3, loss);
         }
     }
