@@ -29,6 +29,9 @@ from pathlib import Path
 
 REPO = Path(__file__).resolve().parent
 sys.path.insert(0, str(REPO))
+from distributedauc_amd import use_tuned_miopen_db  # noqa: E402
+
+use_tuned_miopen_db()  # before any convolution: the shipped MI355X find/perf db
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402

@@ -7,9 +7,22 @@ RCCL, and exact AUC evaluation. The AUC-specific work runs in hand-written
 gfx950 HIP kernels behind the C ABI of include/dauc.h (libdauc.so); the ResNet
 backbone stays on PyTorch-ROCm.
 """
+import os
+
 from . import _lib
 
 __version__ = "1.0.0"
+
+MIOPEN_DB = os.path.join(os.path.dirname(os.path.abspath(__file__)), "miopen_db")
+
+
+def use_tuned_miopen_db() -> str:
+    """Point MIOpen at the shipped MI355X find + perf db unless the caller already chose one
+    (MIOPEN_USER_DB_PATH). The db holds the ResNet-50 b256 channels-last bf16 convolutions of
+    bench.py tuned by exhaustive search (torch.backends.cudnn.benchmark, scripts/gpu_miopen_tune.sh):
+    27.2 vs 28.5 ms per backbone step, and ~1 s instead of ~60 s of first-step solver search.
+    Call before the first convolution; returns the db path in effect."""
+    return os.environ.setdefault("MIOPEN_USER_DB_PATH", MIOPEN_DB)
 
 __all__ = ["_lib", "ops", "auc", "coda", "flat", "surrogate", "backbone", "main", "parameters",
            "data_partitioner", "loader"]

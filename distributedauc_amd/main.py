@@ -181,6 +181,9 @@ class Evaluator:
 def train(rank: int, size: int, group=None, para=None):
     """main.py:83-339 with synthetic on-device data; returns the CoDA object."""
     para = para or parse([])
+    from . import use_tuned_miopen_db
+
+    use_tuned_miopen_db()  # before the first convolution
     device = torch.device("cuda", para.local_rank)
     torch.cuda.set_device(device)
     _seed_everything(para.seed)
