@@ -7,8 +7,20 @@ steps over RCCL. A step = label map/p_hat + forward + fused loss + backward +
 update (+ the averaging round when t % I == 0). value = images/s of the whole
 job (all ranks), timed over exactly --steps steps between barriers.
 
-Second leg (configs[3]): exact AUC of 2^24 fp32 scores at 1 % positives, the
-pair count sharded by positive blocks over the ranks with one int64 all-reduce.
+Other BASELINE configs, as sub-records of the same line:
+  configs[2]  the averaging-period sweep I in {1, 8, 16, 32} of the same step (``period_sweep``)
+              and one timed CoDA round (``coda_round``: the RCCL all-reduce + finalise, xGMI share)
+  configs[0]  ResNet-18 b32 224^2 I=8 on the GPUs (``configs0.gpu``) next to the reference CPU
+              path on 4 gloo worker processes (``configs0.cpu``: restated step + average_all)
+  configs[3]  exact AUC of 2^24 scores at 1 % positives (``auc_eval``)
+  configs[4]  exact AUC of 2^27 scores at 0.1 % positives (``auc_eval_extreme``), with the C
+              oracle's counts on the full vector in its cpu_baseline
+plus the loss kernel at a streaming size (``surrogate_kernel``).
+
+Launch: ``python bench.py --gpus N`` with no launcher starts N rank processes itself (a
+torch.distributed.run child, before this process touches the GPU) and exits with its code;
+under a launcher (WORLD_SIZE set) it runs as one rank. The run fails if the process group's
+size differs from --gpus.
 
 Kernel timing: HIP events recorded on the stream each kernel is launched on
 (torch's current stream, which is the stream libdauc.so receives), around every
@@ -16,14 +28,16 @@ launch inside the timed region. roofline.achieved = algorithmic bytes per launch
 / average launch duration.
 
     python bench.py [--gpus N --steps K --warmup W]
-    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
+import tempfile
 import time
 from pathlib import Path
 
@@ -38,17 +52,18 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-# VALU ceiling of the cheapest exact per-pair sequence on gfx950: 3 fp32 lane-ops per pair
-# (v_pk_add_f32, v_pk_fma_f32 clamp, v_pk_add_f32 over 2 pairs; a packed op is 2 lane-ops on
-# the 32-wide CDNA4 SIMD). Vector fp32 rate = 256 CU x 4 SIMD x 32 lanes x 2.4 GHz = 7.86e13
-# lane-ops/s (157.3 TF / 2) -> 2.62e13 pairs/s per GPU. (SURVEY §8d's 1.97e13 assumed 16-wide
-# SIMDs and 2 compares per pair.)
+# VALU ceilings of the pair count (pairs/s per GPU). Vector fp32 rate = 256 CU x 4 SIMD x 32
+# lanes x 2.4 GHz = 7.86e13 lane-ops/s (157.3 TF / 2).
+#   packed: the cheapest exact sequence on gfx950, 3 fp32 lane-ops per pair (v_pk_add_f32,
+#           v_pk_fma_f32 clamp, v_pk_add_f32 over 2 pairs) -> 2.62e13
+#   survey: SURVEY §8(d)'s bar, 2 compares per pair on 16-wide SIMDs -> 1.97e13
 VALU_PAIR_PEAK = 2.62e13
+SURVEY_PAIR_PEAK = 1.97e13
 XGMI_PEAK_GBS = 7 * 153.0   # one GPU's 7 xGMI links x ~153 GB/s (the ring all-reduce's bus-bandwidth ceiling)
 METRIC = "CoDA train imgs/sec + exact-AUC pos×neg pairs/sec at 1/2/4/8 MI355X"
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
@@ -59,6 +74,9 @@ def parse():
     p.add_argument("--I", type=int, default=16)
     p.add_argument("--pos-ratio", type=float, default=0.1)
     p.add_argument("--pool", type=int, default=4, help="distinct resident input batches cycled")
+    p.add_argument("--sweep-I", default="1,8,16,32", help="configs[2] averaging periods ('' = off)")
+    p.add_argument("--sweep-steps", type=int, default=32, help="timed steps per period (a multiple of every I)")
+    p.add_argument("--r18-steps", type=int, default=16, help="configs[0] GPU leg: timed ResNet-18 b32 steps (0 = off)")
     p.add_argument("--auc-log2n", type=int, default=24)
     p.add_argument("--auc-pos", type=float, default=0.01)
     p.add_argument("--auc-reps", type=int, default=3)
@@ -69,15 +87,47 @@ def parse():
     p.add_argument("--variant", type=int, default=0, help="pair-count kernel variant")
     p.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL; gloo for rehearsals)")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-workers", type=int, default=4, help="configs[0] CPU leg: gloo worker processes")
+    p.add_argument("--cpu-steps", type=int, default=8, help="configs[0] CPU leg: timed steps (one round at I=8)")
+    p.add_argument("--cpu-sklearn-full", type=int, default=1,
+                   help="time sklearn on the full configs[4] vector (1) or its first 2^24 scores (0)")
     p.add_argument("--no-auc", action="store_true")
     p.add_argument("--no-train", action="store_true")
     p.add_argument("--no-surrogate", action="store_true")
     p.add_argument("--fused-bn", type=int, default=1, help="fused BN+add+ReLU HIP kernels in the backbone (1/0)")
     p.add_argument("--gemm-conv1x1", type=int, default=1,
                    help="stride-1 1x1 convs as hipBLASLt GEMMs where faster (per-shape timing; 1/0)")
-    return p.parse_args()
+    # internal: one process of the configs[0] CPU baseline (never touches the GPU)
+    p.add_argument("--cpu-coda-worker", action="store_true", help=argparse.SUPPRESS)
+    p.add_argument("--cw-rank", type=int, default=0, help=argparse.SUPPRESS)
+    p.add_argument("--cw-port", type=int, default=0, help=argparse.SUPPRESS)
+    p.add_argument("--cw-threads", type=int, default=1, help=argparse.SUPPRESS)
+    p.add_argument("--cw-out", default="", help=argparse.SUPPRESS)
+    return p.parse_args(argv)
 
 
+def log(msg: str):
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
+def free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def host_info() -> dict:
+    """The host CPU share this run may use (north_star: the core count must be stated)."""
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except AttributeError:
+        affinity = os.cpu_count() or 1
+    omp = os.environ.get("OMP_NUM_THREADS")
+    budget = min(affinity, int(omp)) if omp and omp.isdigit() and int(omp) > 0 else affinity
+    return {"nproc": os.cpu_count(), "affinity_cpus": affinity, "omp_num_threads": omp, "cpu_budget": budget}
+
+
+# ----------------------------------------------------------------------------- timing helpers
 class KernelTimer:
     """HIP events on the launch stream around every call of one libdauc.so entry point.
 
@@ -114,10 +164,6 @@ class KernelTimer:
         return float(np.mean([a.elapsed_time(b) for a, b in self.pairs])) if self.pairs else float("nan")
 
 
-def log(msg: str):
-    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
-
-
 def max_over_ranks(x: float, world: int) -> float:
     if world == 1:
         return x
@@ -126,26 +172,50 @@ def max_over_ranks(x: float, world: int) -> float:
     return float(t.item())
 
 
-def bench_train(args, world, rank, device):
-    from distributedauc_amd import _lib
+def timed_steps(coda, it, steps: int, world: int) -> float:
+    """Exactly `steps` CoDA steps between barrier + synchronize on both sides; max over ranks (s)."""
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        x, y = next(it)
+        coda.train_step(x, y)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    return max_over_ranks(time.perf_counter() - t0, world)
+
+
+# ----------------------------------------------------------------------------- training legs
+def make_coda(arch, batch, image_size, I, pos_ratio, pool, world, rank, device, fused_bn=True, gemm_conv1x1=True):
     from distributedauc_amd.backbone import build_backbone
     from distributedauc_amd.coda import CoDA
     from distributedauc_amd.loader import DeviceLoader, SyntheticImageNet, imagenet_like_labels
 
     torch.manual_seed(1234)
     split = 499
-    labels = imagenet_like_labels(1 << 16, 1000, split, pos_ratio=args.pos_ratio, seed=123 + rank)
-    ds = SyntheticImageNet(labels, args.image_size, split)
-    loader = DeviceLoader(ds, np.arange(len(labels)), args.batch, device, seed=1234 + rank,
-                          channels_last=True, pool=args.pool)
-    net = build_backbone(args.arch, num_classes=2).to(device).to(memory_format=torch.channels_last)
-    net.set_fused_bn(bool(args.fused_bn)).set_gemm_conv1x1(bool(args.gemm_conv1x1))
-    coda = CoDA(net, lr=0.1, gamma=2000.0, T0=10 ** 9, I=args.I, split_index=split, world=world, rank=rank,
+    labels = imagenet_like_labels(1 << 16, 1000, split, pos_ratio=pos_ratio, seed=123 + rank)
+    ds = SyntheticImageNet(labels, image_size, split)
+    loader = DeviceLoader(ds, np.arange(len(labels)), batch, device, seed=1234 + rank, channels_last=True, pool=pool)
+    net = build_backbone(arch, num_classes=2).to(device).to(memory_format=torch.channels_last)
+    net.set_fused_bn(bool(fused_bn)).set_gemm_conv1x1(bool(gemm_conv1x1))
+    coda = CoDA(net, lr=0.1, gamma=2000.0, T0=10 ** 9, I=I, split_index=split, world=world, rank=rank,
                 autocast_dtype=torch.bfloat16, device=device)
     it = iter(loader)
-    log(f"rank {rank}: model + data ready, first steps compile/tune MIOpen kernels")
     coda.average_all()            # main.py:141-142
     coda.begin_stage(1, it)       # alpha estimate + anchors (untimed)
+    return coda, it
+
+
+def bench_train(args, world, rank, device):
+    from distributedauc_amd import _lib
+
+    coda, it = make_coda(args.arch, args.batch, args.image_size, args.I, args.pos_ratio, args.pool, world, rank,
+                         device, args.fused_bn, args.gemm_conv1x1)
+    log(f"rank {rank}: model + data ready, first steps compile/tune MIOpen kernels")
     lib = _lib.load()
     upd = KernelTimer(lib, "dauc_pd_update")
     sur = KernelTimer(lib, "dauc_surrogate_fwdbwd")
@@ -154,33 +224,42 @@ def bench_train(args, world, rank, device):
         coda.train_step(x, y)
     torch.cuda.synchronize()
     log(f"rank {rank}: warm-up done")
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
     upd.enabled = sur.enabled = True
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        x, y = next(it)
-        coda.train_step(x, y)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
+    dt = timed_steps(coda, it, args.steps, world)
     upd.enabled = sur.enabled = False
-    dt = max_over_ranks(dt, world)
+    upd.restore()
+    sur.restore()
     loss = float(coda.last_loss.item())
-    n_params = coda.state.numel()
-    upd_ms = upd.mean_ms()
-    upd_bytes = coda.state.bytes_per_update(True)
-    sur_ms = sur.mean_ms()
     out = {
-        "dt": dt, "imgs": world * args.batch * args.steps, "loss": loss, "n_params": n_params,
-        "update_ms": upd_ms, "update_bytes": upd_bytes, "surrogate_us": sur_ms * 1e3,
+        "dt": dt, "imgs": world * args.batch * args.steps, "loss": loss, "n_params": coda.state.numel(),
+        "update_ms": upd.mean_ms(), "update_bytes": coda.state.bytes_per_update(True),
+        "surrogate_us": sur.mean_ms() * 1e3, "payload_bytes": coda.state.n_reduce * 4,
     }
+    if args.sweep_I:
+        out["period_sweep"] = bench_period_sweep(coda, it, args, world)
     if world > 1:
         out["coda_round"] = bench_coda_round(coda, world)
+    del coda, it
+    torch.cuda.empty_cache()
     return out
+
+
+def bench_period_sweep(coda, it, args, world):
+    """configs[2]: the same step at each averaging period I (main.py:292-301). Every window is
+    --sweep-steps consecutive steps, a multiple of every I, so it holds exactly steps/I rounds."""
+    recs = []
+    I0 = coda.I
+    for I in (int(v) for v in args.sweep_I.split(",") if v.strip()):
+        if args.sweep_steps % I:
+            raise ValueError(f"--sweep-steps {args.sweep_steps} is not a multiple of I={I}")
+        coda.I = I
+        dt = timed_steps(coda, it, args.sweep_steps, world)
+        recs.append({"I": I, "imgs_per_sec": world * args.batch * args.sweep_steps / dt,
+                     "ms_per_step": dt / args.sweep_steps * 1e3, "steps": args.sweep_steps,
+                     "rounds_per_step": 1.0 / I, "rounds_in_window": args.sweep_steps // I})
+        log(f"rank {coda.rank}: period sweep I={I}: {recs[-1]['ms_per_step']:.2f} ms/step")
+    coda.I = I0
+    return recs
 
 
 def bench_coda_round(coda, world, reps=5):
@@ -193,6 +272,7 @@ def bench_coda_round(coda, world, reps=5):
     dist.barrier()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     with torch.no_grad():
+        coda.average_all()  # warm
         e0.record()
         for _ in range(reps):
             coda.average_all()
@@ -202,22 +282,43 @@ def bench_coda_round(coda, world, reps=5):
     bus = 2 * (world - 1) / world * nbytes / (ms / 1e3) / 1e9
     return {"workload": f"all-reduce of {nbytes} B (params + a, b, alpha + class counts) + finalise, {world} ranks",
             "ms_per_round": ms, "payload_bytes": nbytes, "rounds_per_step": 1.0 / coda.I,
+            "backend": dist.get_backend(),
             "roofline": {"bound": "xgmi", "achieved": bus, "peak": XGMI_PEAK_GBS, "unit": "GB/s (bus)",
                          "frac": bus / XGMI_PEAK_GBS}}
 
 
+def bench_r18(args, world, rank, device):
+    """configs[0] on the GPUs: ResNet-18 CoDA, batch 32 per rank, 224^2, I = 8 (the CPU path of
+    the same config is cpu_baseline_configs0)."""
+    coda, it = make_coda("resnet18", 32, args.image_size, 8, args.pos_ratio, args.pool, world, rank, device,
+                         args.fused_bn, args.gemm_conv1x1)
+    for _ in range(max(args.warmup, 8)):
+        x, y = next(it)
+        coda.train_step(x, y)
+    torch.cuda.synchronize()
+    steps = max(8, args.r18_steps // 8 * 8)
+    dt = timed_steps(coda, it, steps, world)
+    rec = {"workload": "resnet18 CoDA, batch 32 per rank, 224x224, I=8, bf16 autocast backbone, fp32 AUC kernels "
+                       "(BASELINE configs[0] on the GPUs)",
+           "imgs_per_sec": world * 32 * steps / dt, "ms_per_step": dt / steps * 1e3, "steps": steps,
+           "n_gpus": world, "params": coda.state.numel(), "final_loss": float(coda.last_loss.item())}
+    del coda, it
+    torch.cuda.empty_cache()
+    return rec
+
+
+# ----------------------------------------------------------------------------- exact AUC legs
 def bench_auc(args, world, rank, device, log2n=None, pos=None, pair_reps=None):
-    """configs[3] (and [4]): exact AUC of 2^k scores, sharded by positive blocks; both exact methods."""
+    """configs[3] (and [4]): exact AUC of 2^k scores, sharded over the ranks; both exact methods."""
     from distributedauc_amd import _lib
     from distributedauc_amd.auc import ExactAUC
+    from distributedauc_amd.loader import synthetic_scores
 
     log2n = args.auc_log2n if log2n is None else log2n
     pos = args.auc_pos if pos is None else pos
     n = 1 << log2n
-    g = torch.Generator(device=device).manual_seed(2024)  # same scores on every rank
-    s = torch.rand(n, generator=g, device=device)
-    y = torch.where(torch.rand(n, generator=g, device=device) < pos, 1, -1).to(torch.int8)
-    out = {"n": n, "log2n": log2n, "pos": pos, "scores": s, "labels": y}
+    s, y = synthetic_scores(n, pos, device)  # same scores on every rank
+    out = {"n": n, "log2n": log2n, "pos": pos}
     for method, fn in (("sort", "dauc_auc_counts_sorted_labeled"), ("pairs", "dauc_pair_count_variant")):
         ev = ExactAUC(world=world, rank=rank, variant=args.variant, method=method)
         kt = KernelTimer(_lib.load(), fn)
@@ -237,15 +338,14 @@ def bench_auc(args, world, rank, device, log2n=None, pos=None, pair_reps=None):
         kt.restore()
         out["m_" + method] = {"t_eval": max_over_ranks(float(np.median(times)), world),
                               "t_count": max_over_ranks(kt.mean_ms() / 1e3, world), "counts": c}
-        log(f"rank {rank}: auc {method} eval {out['m_' + method]['t_eval'] * 1e3:.2f} ms")
+        log(f"rank {rank}: auc 2^{log2n} {method} eval {out['m_' + method]['t_eval'] * 1e3:.2f} ms")
     a, b = out["m_sort"]["counts"], out["m_pairs"]["counts"]
     if (a["wins"], a["ties"]) != (b["wins"], b["ties"]):
         raise RuntimeError(f"exact AUC methods disagree: {a} vs {b}")
     out.update({"P": a["P"], "N": a["N"], "wins": a["wins"], "ties": a["ties"], "auc": ExactAUC.from_counts(a),
                 "npairs": a["P"] * a["N"]})
-    if world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and not args.no_cpu_baseline:
         out["scores_host"] = (s.cpu().numpy(), y.cpu().numpy().astype(np.int64))
-    del out["scores"], out["labels"]
     return out
 
 
@@ -253,29 +353,42 @@ def auc_record(auc, world, config_name):
     pk, sk = auc["m_pairs"], auc["m_sort"]
     npairs = auc["npairs"]
     pc_rate = npairs / pk["t_count"]
+    n = auc["n"]
+    # the sort method's HBM floor: labels read twice by the compaction, scores + labels once by
+    # the query pass (the positives' scores and the sorted table are ~0.1-1 % of that)
+    eval_bytes = n * (2 * 1 + 4 + 1) // world
     return {
         "workload": f"exact AUC, 2^{auc['log2n']} fp32 scores, {auc['pos']:.1%} positives "
-                    f"(BASELINE {config_name}), sharded over ranks (sort: score-index ranges; pair count: "
+                    f"(BASELINE {config_name}), sharded over {world} rank(s) (sort: score-index ranges; pair count: "
                     "positive blocks), int64 all-reduce",
         "pairs_per_sec": npairs / sk["t_eval"],
-        "method": "sort (default evaluator: split out the positives, radix-sort them, locate every negative "
-                  "through an LDS search tree, read in place)",
+        "method": "sort (default evaluator: compact the positives reading labels only, radix-sort them, locate "
+                  "every negative through an LDS search tree, read in place)",
         "eval_ms": sk["t_eval"] * 1e3, "sort_count_ms": sk["t_count"] * 1e3,
+        "eval_roofline": {"bound": "hbm", "bytes_per_rank": eval_bytes,
+                          "achieved": eval_bytes / sk["t_eval"] / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                          "frac": eval_bytes / sk["t_eval"] / 1e9 / HBM_PEAK_GBS,
+                          "note": "bytes = 2 label passes + 1 score/label pass over this rank's share"},
         "P": auc["P"], "N": auc["N"], "wins": auc["wins"], "ties": auc["ties"], "auc": auc["auc"],
         "methods_agree": True,
         "pair_count_kernel": {
             "pairs_per_sec": pc_rate, "eval_ms": pk["t_eval"] * 1e3, "count_ms": pk["t_count"] * 1e3,
             "roofline": {"kernel": "dauc_pair_count", "bound": "valu", "achieved": pc_rate / world,
                          "peak": VALU_PAIR_PEAK, "unit": "pairs/s per GPU",
-                         "frac": pc_rate / world / VALU_PAIR_PEAK}},
+                         "frac": pc_rate / world / VALU_PAIR_PEAK,
+                         "peak_note": "packed-issue ceiling: 3 fp32 lane-ops per pair on 32-wide SIMDs",
+                         "survey_peak": SURVEY_PAIR_PEAK, "frac_vs_survey_peak": pc_rate / world / SURVEY_PAIR_PEAK,
+                         "survey_peak_note": "SURVEY §8(d): 2 compares per pair on 16-wide SIMDs"}},
     }
 
 
+# ----------------------------------------------------------------------------- loss kernel leg
 def bench_surrogate(args, device):
     """The fused loss kernel at a streaming size (9 B/element = fp32 h + int8 y + fp32 dh).
 
     Training batches (B = 256) are launch-latency bound; this leg measures the same kernel where
-    HBM bounds it. Inputs resident in HBM; HIP events on the launch stream around every call."""
+    HBM bounds it. Inputs resident in HBM. Reported separately: the whole ABI call (streaming
+    kernel + the small row-reduce launch) and the streaming kernel alone (variant 15)."""
     from distributedauc_amd import _lib, ops
 
     B = 1 << args.sur_log2b
@@ -287,18 +400,24 @@ def bench_surrogate(args, device):
     dh = torch.empty(B, device=device)
     grad3 = torch.empty(3, device=device)
     out64 = torch.zeros(6, dtype=torch.float64, device=device)
-    for _ in range(3):
-        ops.surrogate_fwdbwd(h, y, abalpha, p_hat, dh=dh, grad3=grad3, out64=out64)
+
+    def b2b(variant):
+        for _ in range(3):
+            ops.surrogate_fwdbwd(h, y, abalpha, p_hat, dh=dh, grad3=grad3, out64=out64, variant=variant)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(args.sur_reps):
+            ops.surrogate_fwdbwd(h, y, abalpha, p_hat, dh=dh, grad3=grad3, out64=out64, variant=variant)
+        e1.record()
+        e1.synchronize()
+        return e0.elapsed_time(e1) / args.sur_reps
+
     # (1) HIP events over the timed region: one pair around sur_reps back-to-back calls on the
     #     launch stream (the average includes the gaps between calls, not per-call event packets)
-    torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(args.sur_reps):
-        ops.surrogate_fwdbwd(h, y, abalpha, p_hat, dh=dh, grad3=grad3, out64=out64)
-    e1.record()
-    e1.synchronize()
-    ms = e0.elapsed_time(e1) / args.sur_reps
+    ms = b2b(0)
+    loss = float(out64[0].item())
+    stream_ms = b2b(15)  # the streaming kernel alone (no row reduce)
     # (2) an event pair around every call (each pair adds its own marker packets to the stream)
     kt = KernelTimer(_lib.load(), "dauc_surrogate_fwdbwd")
     kt.enabled = True
@@ -309,35 +428,44 @@ def bench_surrogate(args, device):
     per_call_ms = kt.mean_ms()
     nbytes = 9 * B
     gbs = nbytes / (ms / 1e3) / 1e9
+    sgbs = nbytes / (stream_ms / 1e3) / 1e9
     return {"workload": f"fused surrogate fwd+bwd, B = 2^{args.sur_log2b} fp32 scores, int8 labels, p = {args.pos_ratio}",
             "B": B, "avg_launch_us": ms * 1e3, "per_call_events_us": per_call_ms * 1e3,
             "timing": f"HIP events around {args.sur_reps} back-to-back calls on the launch stream, divided by the "
                       "call count (per_call_events_us: an event pair around every call instead)",
-            "loss": float(out64[0].item()),
-            "roofline": {"kernel": "dauc_surrogate_fwdbwd", "launches": "surrogate_chunk_kernel (stream) + "
+            "loss": loss,
+            "roofline": {"kernel": "dauc_surrogate_fwdbwd (whole call)", "launches": "surrogate_chunk_kernel (stream) + "
                          "surrogate_rows_reduce_kernel (fp64 rows), both inside every timed ABI call",
                          "bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS, "traffic": load_traffic(f"surrogate_2^{args.sur_log2b}"),
-                         "bytes_per_launch": nbytes}}
+                         "bytes_per_launch": nbytes},
+            "stream_kernel": {"kernel": "surrogate_chunk_kernel alone (variant 15: no row reduce, no scalars)",
+                              "avg_launch_us": stream_ms * 1e3, "bound": "hbm", "achieved": sgbs,
+                              "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": sgbs / HBM_PEAK_GBS,
+                              "bytes_per_launch": nbytes},
+            "row_reduce_us": (ms - stream_ms) * 1e3}
 
 
-def cpu_baseline_train(args):
-    """The reference's CPU path on a bounded sample: torch-CPU ResNet-50 fwd, verbatim loss
-    (main.py:313-317), autograd, per-tensor dppd_sg (main.py:56-64) + running average."""
+# ----------------------------------------------------------------------------- CPU baselines
+def cpu_baseline_train(args, threads):
+    """The reference's CPU path for the headline config: torch-CPU ResNet-50 fwd at the GPU's batch
+    (256, 224^2), verbatim loss (main.py:313-317), autograd, per-tensor dppd_sg (main.py:56-64)
+    + running average (main.py:333-334). One warm-up step at batch 32, one timed step at 256."""
     from distributedauc_amd.backbone import build_backbone
     from oracle import reference_cpu as R
 
+    torch.set_num_threads(threads)
     torch.manual_seed(0)
-    B, steps = 32, 2
+    B = args.batch
     net = build_backbone(args.arch, num_classes=2)
     net0 = {k: v.clone() for k, v in net.state_dict().items()}
     avg = {k: v.clone() for k, v in net.state_dict().items()}
     a, b, alpha = (torch.zeros(1, requires_grad=True) for _ in range(3))
-    x = torch.randn(B, 3, args.image_size, args.image_size)
-    lab = torch.where(torch.rand(B) < args.pos_ratio, 1, -1)
     p = torch.tensor([args.pos_ratio])
 
-    def step():
+    def step(nb):
+        x = torch.randn(nb, 3, args.image_size, args.image_size)
+        lab = torch.where(torch.rand(nb) < args.pos_ratio, 1, -1)
         h = net(x)[:, 1]
         loss = R.surrogate_loss(h, lab, a, b, alpha, p)
         net.zero_grad()
@@ -347,25 +475,147 @@ def cpu_baseline_train(args):
                 prm.data = R.pd_step(prm.data, prm.grad.data, net0[name], 0.1, 2000.0)
                 avg[name] = avg[name] + prm.data
 
-    step()  # warm-up
+    step(32)  # warm-up
     t0 = time.perf_counter()
-    for _ in range(steps):
-        step()
+    step(B)
     dt = time.perf_counter() - t0
-    return {"value": B * steps / dt, "unit": "imgs/sec", "cores": torch.get_num_threads(), "kind": "port",
-            "sample": f"{args.arch} {args.image_size}x{args.image_size} batch {B}, {steps} timed steps "
-                      f"(fwd + reference loss + backward + per-tensor dppd_sg + running average), torch CPU fp32"}
+    return {"value": B / dt, "unit": "imgs/sec", "cores": threads, "kind": "port",
+            "sample": f"{args.arch} {args.image_size}x{args.image_size}, one timed step at batch {B} (the GPU's "
+                      "batch; warm-up at 32): fwd + reference loss + backward + per-tensor dppd_sg + running "
+                      f"average, torch CPU fp32, {threads} threads", "seconds": dt}
 
 
-def cpu_baseline_auc(auc_res, max_log2n=None):
-    """sklearn roc_curve + auc (main.py:79-81) on the same scores: the reference CPU path.
+def cpu_coda_worker(args):
+    """One rank of the configs[0] CPU baseline (ResNet-18 b32 224^2, I=8): the reference's step
+    restated by the oracle (main.py:303-334) with average_all over gloo (main.py:33-54, 292-301).
+    Never touches the GPU. Rank 0 writes the timings as JSON to --cw-out."""
+    from distributedauc_amd.backbone import build_backbone
+    from oracle import reference_cpu as R
 
-    With max_log2n, a bounded sample: the first 2^max_log2n of the scores (the rate is the sample's
-    pairs over its wall time)."""
+    torch.set_num_threads(max(1, args.cw_threads))
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(args.cw_port)
+    world = args.cpu_workers
+    dist.init_process_group("gloo", rank=args.cw_rank, world_size=world)
+    torch.manual_seed(1234)
+    net = build_backbone("resnet18", num_classes=2)
+    net0 = {k: v.clone() for k, v in net.state_dict().items()}
+    avg = {k: v.clone() for k, v in net.state_dict().items()}
+    a, b, alpha = (torch.zeros(1, requires_grad=True) for _ in range(3))
+    gpos, gneg = torch.zeros(1), torch.zeros(1)
+    lpos, lneg = torch.zeros(1), torch.zeros(1)
+    gen = torch.Generator().manual_seed(1234 + args.cw_rank)
+    B, I = 32, 8
+
+    def step(t_total):
+        nonlocal lpos, lneg
+        if t_total % I == 0:  # main.py:292-301
+            with torch.no_grad():
+                R.average_all_dist(net, a, b, alpha, gpos, gneg, lpos, lneg, world)
+            lpos, lneg = torch.zeros(1), torch.zeros(1)
+        x = torch.randn(B, 3, args.image_size, args.image_size, generator=gen)
+        lab = torch.where(torch.rand(B, generator=gen) < args.pos_ratio, 1, -1)
+        lpos += float((lab == 1).sum())
+        lneg += float((lab == -1).sum())
+        p = torch.tensor([float(gpos + lpos) / float(gpos + lpos + gneg + lneg)])  # main.py:309-310
+        h = net(x)[:, 1]
+        loss = R.surrogate_loss(h, lab, a, b, alpha, p)
+        net.zero_grad()
+        a.grad = b.grad = alpha.grad = None
+        loss.backward()
+        with torch.no_grad():
+            for name, prm in net.named_parameters():
+                prm.data = R.pd_step(prm.data, prm.grad.data, net0[name], 0.1, 2000.0)
+                avg[name] = avg[name] + prm.data
+
+    with torch.no_grad():
+        R.average_all_dist(net, a, b, alpha, gpos, gneg, lpos, lneg, world)  # main.py:141-142
+    t = 1
+    step(t)  # warm-up
+    t += 1
+    while t % I:  # align so the timed window holds exactly steps / I rounds
+        t += 1
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.cpu_steps):
+        step(t)
+        t += 1
+    dist.barrier()
+    dt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+    dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+    # the averaging round alone (the survey measured 127.9 ms for R-18 on 4 ranks)
+    rounds = 3
+    dist.barrier()
+    t0 = time.perf_counter()
+    with torch.no_grad():
+        for _ in range(rounds):
+            R.average_all_dist(net, a, b, alpha, gpos, gneg, lpos, lneg, world)
+    dist.barrier()
+    dr = torch.tensor([(time.perf_counter() - t0) / rounds], dtype=torch.float64)
+    dist.all_reduce(dr, op=dist.ReduceOp.MAX)
+    if args.cw_rank == 0 and args.cw_out:
+        nparams = sum(p.numel() for p in net.parameters())
+        Path(args.cw_out).write_text(json.dumps({
+            "dt": float(dt), "steps": args.cpu_steps, "imgs": world * B * args.cpu_steps,
+            "round_ms": float(dr) * 1e3, "params": nparams,
+            "params_finite": all(bool(torch.isfinite(p).all()) for p in net.parameters())}))
+    dist.destroy_process_group()
+
+
+def cpu_baseline_configs0(args, host):
+    """configs[0]: 4 gloo CPU worker processes x (budget / 4) threads, ResNet-18 b32 224^2, I = 8
+    ("4 processes x nproc/4 threads"). Child processes of this one (they never touch
+    the GPU); their rank 0 reports the max-over-ranks time of exactly --cpu-steps steps."""
+    W = args.cpu_workers
+    threads = max(1, host["cpu_budget"] // W)
+    port = free_port()
+    with tempfile.TemporaryDirectory() as td:
+        out = Path(td) / "cw.json"
+        env = dict(os.environ, HIP_VISIBLE_DEVICES="", CUDA_VISIBLE_DEVICES="", ROCR_VISIBLE_DEVICES="",
+                   OMP_NUM_THREADS=str(threads))
+        procs = [subprocess.Popen([sys.executable, str(Path(__file__).resolve()), "--cpu-coda-worker",
+                                   "--cpu-workers", str(W), "--cw-rank", str(r), "--cw-port", str(port),
+                                   "--cw-threads", str(threads), "--cw-out", str(out),
+                                   "--cpu-steps", str(args.cpu_steps), "--image-size", str(args.image_size),
+                                   "--pos-ratio", str(args.pos_ratio)], env=env)
+                 for r in range(W)]
+        try:
+            rcs = [p.wait(timeout=600) for p in procs]
+        finally:
+            for p in procs:
+                if p.poll() is None:
+                    p.kill()
+        if any(rcs) or not out.exists():
+            return {"error": f"cpu workers exited with {rcs}"}
+        r = json.loads(out.read_text())
+    return {"value": r["imgs"] / r["dt"], "unit": "imgs/sec", "cores": W * threads, "kind": "port",
+            "workers": W, "threads_per_worker": threads, "ms_per_step": r["dt"] / r["steps"] * 1e3,
+            "averaging_round_ms": r["round_ms"], "params": r["params"], "params_finite": r["params_finite"],
+            "sample": f"resnet18 {args.image_size}x{args.image_size} batch 32 per worker, I=8, {W} gloo worker processes x {threads} threads, "
+                      f"{r['steps']} timed steps (one averaging round inside: per-parameter all_reduce + /= size, "
+                      "main.py:33-54), fwd + reference loss + backward + per-tensor dppd_sg + running average, "
+                      "torch CPU fp32"}
+
+
+def cpu_baseline_auc(auc_res, max_log2n=None, oracle_check=False):
+    """sklearn roc_curve + auc (main.py:79-81) on the same scores: the reference CPU path, and
+    (oracle_check) the C oracle's integer counts on the full vector vs the GPU's."""
     from oracle import reference_cpu as R
 
     s, y = auc_res["scores_host"]
     n = s.size
+    rec = {}
+    if oracle_check:
+        from oracle import coracle
+
+        t0 = time.perf_counter()
+        e = coracle.auc_counts(y, s)
+        rec["oracle_counts"] = {"wins": e["wins"], "ties": e["ties"], "P": e["P"], "N": e["N"],
+                                "seconds": time.perf_counter() - t0,
+                                "match": (e["wins"], e["ties"], e["P"], e["N"]) ==
+                                         (auc_res["wins"], auc_res["ties"], auc_res["P"], auc_res["N"]),
+                                "what": "C restatement of sklearn _binary_clf_curve's integer counts "
+                                        "(oracle/auc_oracle.c) on the full vector, vs the GPU counts"}
     if max_log2n is not None and n > (1 << max_log2n):
         s, y = s[:1 << max_log2n], y[:1 << max_log2n]
     P = int(np.sum(y == 1))
@@ -373,41 +623,75 @@ def cpu_baseline_auc(auc_res, max_log2n=None):
     ref = R.auc_sklearn(y, s)
     dt = time.perf_counter() - t0
     full = s.size == n
-    rec = {"value": P * (s.size - P) / dt, "unit": "pairs/sec (effective: P*N / wall)", "cores": 1,
-           "kind": "port", "seconds": dt, "auc": ref,
-           "sample": (f"full 2^{int(np.log2(n))} scores" if full else
-                      f"first 2^{int(np.log2(s.size))} of the 2^{int(np.log2(n))} scores") +
-                     ", sklearn roc_curve+auc (single-threaded sort)"}
+    rec.update({"value": P * (s.size - P) / dt, "unit": "pairs/sec (effective: P*N / wall)", "cores": 1,
+                "kind": "port", "seconds": dt, "auc": ref,
+                "sample": (f"full 2^{int(np.log2(n))} scores" if full else
+                           f"first 2^{int(np.log2(s.size))} of the 2^{int(np.log2(n))} scores") +
+                          ", sklearn roc_curve+auc (single-threaded sort)"})
     if full:
         rec["auc_abs_diff"] = abs(ref - auc_res["auc"])
     return rec
 
 
+# ----------------------------------------------------------------------------- launch
+def self_launch(args) -> int | None:
+    """--gpus N without a launcher: start N ranks as a torch.distributed.run child process (this
+    process has not touched the GPU) and return its exit code."""
+    if args.cpu_coda_worker or "WORLD_SIZE" in os.environ or args.gpus <= 1:
+        return None
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}", str(Path(__file__).resolve()), *sys.argv[1:]]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    log(f"launching {args.gpus} ranks: {' '.join(cmd[1:5])} ...")
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     args = parse()
+    if args.cpu_coda_worker:
+        cpu_coda_worker(args)
+        return
+    rc = self_launch(args)
+    if rc is not None:
+        sys.exit(rc)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+    if world != args.gpus:
+        print(f"error: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks", file=sys.stderr)
+        sys.exit(2)
     ndev = torch.cuda.device_count()
-    device = torch.device("cuda", local % max(ndev, 1))  # ranks share a device only in rehearsals
+    if args.backend == "nccl" and world > 1 and ndev < local_world:
+        print(f"error: the nccl (RCCL) backend needs one GPU per rank: {local_world} ranks on this node, "
+              f"{ndev} GPU(s) visible (use --backend gloo for a shared-GPU rehearsal)", file=sys.stderr)
+        sys.exit(3)
+    device = torch.device("cuda", local % max(ndev, 1))  # ranks share a device only in gloo rehearsals
     torch.cuda.set_device(device)
+    quiet = None
     if world > 1:
         if args.backend == "nccl":
             dist.init_process_group("nccl", device_id=device)
         else:
             dist.init_process_group(args.backend)
-    if args.gpus != world and rank == 0:
-        print(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using {world}", file=sys.stderr)
+        if dist.get_world_size() != args.gpus:
+            print(f"error: process group has {dist.get_world_size()} ranks, --gpus {args.gpus}", file=sys.stderr)
+            sys.exit(2)
+        quiet = dist.new_group(backend="gloo")  # waits without spinning a core (CPU baseline runs on rank 0)
+    host = host_info()
 
     res = bench_train(args, world, rank, device) if not args.no_train else None
+    r18 = bench_r18(args, world, rank, device) if (not args.no_train and args.r18_steps > 0) else None
     auc = bench_auc(args, world, rank, device) if not args.no_auc else None
     auc2 = None
     if not args.no_auc and args.auc2_log2n > 0:  # configs[4]: 2^27 scores at 0.1 % positives
         auc2 = bench_auc(args, world, rank, device, args.auc2_log2n, args.auc2_pos, pair_reps=1)
     sur = bench_surrogate(args, device) if (not args.no_surrogate and rank == 0) else None
+    torch.cuda.synchronize()
 
     if rank == 0:
-        out = {"metric": METRIC}
+        out = {"metric": METRIC, "n_gpus": world}
         if res is not None:
             upd_gbs = res["update_bytes"] / (res["update_ms"] / 1e3) / 1e9
             out.update({
@@ -425,28 +709,48 @@ def main():
                              "frac": upd_gbs / HBM_PEAK_GBS, "traffic": load_traffic("pd_update"),
                              "bytes_per_launch": res["update_bytes"], "avg_launch_us": res["update_ms"] * 1e3},
                 "surrogate_us_per_call": res["surrogate_us"],
-                **({"coda_round": res["coda_round"]} if "coda_round" in res else {}),
                 "final_loss": res["loss"],
             })
+            if "period_sweep" in res:
+                out["period_sweep"] = {"workload": "BASELINE configs[2]: the headline step at each averaging period",
+                                       "records": res["period_sweep"]}
+            if "coda_round" in res:
+                out["coda_round"] = res["coda_round"]
+        out["process_group"] = {"world_size": dist.get_world_size() if world > 1 else 1,
+                                "backend": dist.get_backend() if world > 1 else None,
+                                "rccl_version": ".".join(map(str, torch.cuda.nccl.version()))
+                                if torch.cuda.is_available() and hasattr(torch.cuda, "nccl") else None,
+                                "devices_visible": torch.cuda.device_count()}
+        out["host"] = host
         if sur is not None:
             out["surrogate_kernel"] = sur
+        if r18 is not None:
+            out["configs0"] = {"gpu": r18}
         if auc is not None:
             out["auc_eval"] = auc_record(auc, world, "configs[3]")
         if auc2 is not None:
             out["auc_eval_extreme"] = auc_record(auc2, world, "configs[4]")
-        if world == 1 and not args.no_cpu_baseline:
-            torch.set_num_threads(min(16, os.cpu_count() or 1))
+        if not args.no_cpu_baseline:
+            threads = host["cpu_budget"]
             if res is not None:
-                out["cpu_baseline"] = cpu_baseline_train(args)
+                log("cpu baseline: resnet50 step")
+                out["cpu_baseline"] = cpu_baseline_train(args, threads)
+            if r18 is not None and args.cpu_workers > 0:
+                log("cpu baseline: configs[0] gloo workers")
+                out.setdefault("configs0", {})["cpu"] = cpu_baseline_configs0(args, host)
+            torch.set_num_threads(threads)
             if auc is not None:
-                out.setdefault("auc_eval", {})["cpu_baseline"] = cpu_baseline_auc(auc)
+                log("cpu baseline: sklearn configs[3]")
+                out["auc_eval"]["cpu_baseline"] = cpu_baseline_auc(auc)
             if auc2 is not None:
-                out.setdefault("auc_eval_extreme", {})["cpu_baseline"] = cpu_baseline_auc(auc2, max_log2n=24)
+                log("cpu baseline: oracle + sklearn configs[4]")
+                out["auc_eval_extreme"]["cpu_baseline"] = cpu_baseline_auc(
+                    auc2, max_log2n=None if args.cpu_sklearn_full else 24, oracle_check=True)
         else:
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)
     if world > 1:
-        dist.barrier()
+        dist.barrier(group=quiet)
         dist.destroy_process_group()
 
 

@@ -65,7 +65,8 @@ SIGNATURES = {
     "dauc_pair_count_variant": (_int, [_vp, _i64, _vp, _i64, _vp, _int, _vp]),
     "dauc_sort_workspace_size": (_sz, [_i64]),
     "dauc_auc_counts_sorted": (_int, [_vp, _i64, _vp, _i64, _vp, _vp, _sz, _vp]),
-    "dauc_auc_counts_sorted_labeled": (_int, [_vp, _i64, _vp, _vp, _int, _i64, _i64, _vp, _vp, _sz, _vp]),
+    "dauc_auc_counts_sorted_labeled": (_int, [_vp, _i64, _vp, _vp, _int, _i64, _i64, _vp, _vp, _vp, _sz, _vp]),
+    "dauc_compact_positives": (_int, [_vp, _vp, _int, _i64, _vp, _vp, _vp, _sz, _vp]),
     "dauc_sort_keys": (_int, [_vp, _i64, _vp, _vp, _sz, _vp]),
     "dauc_bn_workspace_size": (_sz, [_i64, _int]),
     "dauc_bn_act_forward": (_int, [_vp, _int, _i64, _int, _vp, _int, _vp, _vp, _vp, _vp, _f32, _f32, _vp, _vp, _vp,

@@ -76,8 +76,13 @@ class ExactAUC:
         y, s = _as_device_pair(label, scores, device)
         if y.numel() != s.numel():
             raise ValueError(f"Found input variables with inconsistent numbers of samples: {[y.numel(), s.numel()]}")
-        # the sort method reads the negatives in place (only the positives are compacted)
-        pos, neg, stats = ops.split_scores(s, y, negatives=self.method == "pairs")
+        if self.method == "pairs":
+            # stable split: every rank sees the positives in the same order, so positive blocks shard
+            pos, neg, stats = ops.split_scores(s, y)
+        else:
+            # the sort method reads the negatives in place: only the labels and the positives' scores
+            # are read here; the negatives' finiteness is checked by the query kernel
+            pos, stats = ops.compact_positives(s, y)
         P, N, nonfinite, other = (int(v) for v in stats.tolist())
         if nonfinite:
             raise ValueError("Input y_score contains NaN or infinity.")
@@ -85,7 +90,14 @@ class ExactAUC:
             distinct = torch.unique(y)
             if distinct.numel() > 2:
                 raise ValueError("multiclass format is not supported")
-        wt = torch.zeros(2, dtype=torch.int64, device=s.device)
+        # wins, ties, non-finite queried scores (sort method, P <= N)
+        wt = torch.zeros(3, dtype=torch.int64, device=s.device)
+        if self.method == "sort" and (P == 0 or N == 0 or P > N):
+            # no query pass over the negatives (one class empty) or the negatives are the sorted table:
+            # materialise both classes; the split checks every score
+            pos, neg, stats = ops.split_scores(s, y)
+            if int(stats[2].item()):
+                raise ValueError("Input y_score contains NaN or infinity.")
         if P and N:
             if self.method == "pairs":
                 # positive-set blocks: every rank compares its block against all negatives
@@ -98,16 +110,17 @@ class ExactAUC:
                 n = s.numel()
                 lo, hi = self.rank * n // self.world, (self.rank + 1) * n // self.world
                 if hi > lo:
-                    ops.auc_counts_sorted_labeled(pos[:P], s, y, lo, hi, wt)
+                    ops.auc_counts_sorted_labeled(pos[:P], s, y, lo, hi, wt, nonfinite=wt[2:])
             else:
                 # more positives than negatives: the negatives are the sorted table
-                pos, neg, _ = ops.split_scores(s, y)
                 lo, hi = self.rank * P // self.world, (self.rank + 1) * P // self.world
                 if hi > lo:
                     ops.auc_counts_sorted(pos[lo:hi], neg[:N], wt)
         if self.world > 1 and self.reduce:
             dist.all_reduce(wt, op=dist.ReduceOp.SUM, group=self.group)
-        W, T = (int(v) for v in wt.tolist())
+        W, T, bad = (int(v) for v in wt.tolist())
+        if bad:
+            raise ValueError("Input y_score contains NaN or infinity.")
         return {"wins": W, "ties": T, "P": P, "N": N}
 
     @staticmethod

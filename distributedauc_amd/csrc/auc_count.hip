@@ -262,6 +262,178 @@ int launch_split(const float* s, const LT* lab, int64_t n, float* pos_out, float
     return launch_status();
 }
 
+// ============================ positive compaction =============================
+//
+// The sort method only needs the positives as a table (every negative is read in place by the
+// query kernel, which also checks it is finite), so this pass reads the LABELS of every score
+// (1 B each at int8) and the SCORE of each positive only: at 2^27 scores with 0.1 % positives it
+// moves 2 x 134 MB of labels instead of the stable split's 2 x 671 MB of scores + labels. The
+// output keeps the original order (a stable compaction: count, scan, write), so every rank that
+// compacts the same vector gets the same list.
+//
+// Block tile: 256 threads x kCmpSlots groups of 16 labels; group k of thread t covers labels
+// tile0 + (k * 256 + t) * 16 + [0, 16) (each wave load instruction reads 1 KB contiguous at int8).
+
+constexpr int kCmpThreads = 256;
+constexpr int kCmpSlots = 4;
+constexpr int kCmpTile = kCmpThreads * 16 * kCmpSlots;  // 16384 labels per block
+static_assert(kCmpTile >= kSplitTile, "split_workspace_size() also sizes the compaction");
+
+int64_t compact_blocks(int64_t n) { return (n + kCmpTile - 1) / kCmpTile; }
+
+// bytes == 0 -> 0x80 in that byte, 0 elsewhere (exact, no carries between bytes)
+__device__ __forceinline__ unsigned zero_bytes(unsigned v) {
+    return ~(((v & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | v | 0x7F7F7F7Fu);
+}
+
+// the 4 byte flags (0x80 per byte) of zero_bytes() as a 4-bit mask
+__device__ __forceinline__ unsigned byte_flags4(unsigned f) { return (((f >> 7) * 0x00204081u) >> 21) & 0xFu; }
+
+// 16 labels from i: bit j of pos = (label[i + j] == 1); nother += #labels not in {-1, 1}
+template <typename LT>
+__device__ __forceinline__ unsigned label_masks16(const LT* __restrict__ lab, int64_t i, int64_t n, bool vec,
+                                                  int& nother) {
+    unsigned pos = 0;
+    if (vec && i + 16 <= n) {
+        if constexpr (sizeof(LT) == 1) {
+            const int4 v = *reinterpret_cast<const int4*>(lab + i);
+            const unsigned w[4] = {unsigned(v.x), unsigned(v.y), unsigned(v.z), unsigned(v.w)};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const unsigned p = zero_bytes(w[q] ^ 0x01010101u), m = zero_bytes(~w[q]);
+                pos |= byte_flags4(p) << (4 * q);
+                nother += 4 - __popc(p | m);
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < 16; q += 16 / sizeof(LT)) {
+                LT c[16 / sizeof(LT)];
+                *reinterpret_cast<int4*>(c) = *reinterpret_cast<const int4*>(lab + i + q);
+#pragma unroll
+                for (int j = 0; j < int(16 / sizeof(LT)); ++j) {
+                    pos |= unsigned(c[j] == LT(1)) << (q + j);
+                    nother += c[j] != LT(1) && c[j] != LT(-1);
+                }
+            }
+        }
+    } else {
+        for (int j = 0; j < 16; ++j) {
+            if (i + j < n) {
+                const LT c = lab[i + j];
+                pos |= unsigned(c == LT(1)) << j;
+                nother += c != LT(1) && c != LT(-1);
+            }
+        }
+    }
+    return pos;
+}
+
+// pass 1: per-block positive and other-label counts (blk[3b + 1], the non-finite slot, stays 0:
+// the positives' scores are checked by the write pass, the negatives' by the query kernel)
+template <typename LT>
+__global__ __launch_bounds__(kCmpThreads) void compact_count_kernel(const LT* __restrict__ lab, int64_t n,
+                                                                    int vec, int* __restrict__ blk) {
+    __shared__ int part[2][kCmpThreads / kWave];
+    const int64_t base = int64_t(blockIdx.x) * kCmpTile;
+    int np = 0, no = 0;
+    unsigned m[kCmpSlots];
+#pragma unroll
+    for (int k = 0; k < kCmpSlots; ++k)
+        m[k] = label_masks16(lab, base + (int64_t(k) * kCmpThreads + threadIdx.x) * 16, n, vec, no);
+#pragma unroll
+    for (int k = 0; k < kCmpSlots; ++k) np += __popc(m[k]);
+    for (int off = 32; off > 0; off >>= 1) {
+        np += __shfl_xor(np, off, kWave);
+        no += __shfl_xor(no, off, kWave);
+    }
+    const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+    if (lane == 0) {
+        part[0][wid] = np;
+        part[1][wid] = no;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int t0 = 0, t2 = 0;
+        for (int w = 0; w < kCmpThreads / kWave; ++w) {
+            t0 += part[0][w];
+            t2 += part[1][w];
+        }
+        blk[3 * blockIdx.x + 0] = t0;
+        blk[3 * blockIdx.x + 1] = 0;
+        blk[3 * blockIdx.x + 2] = t2;
+    }
+}
+
+// pass 3: every positive's score goes to pos_out[pos_base[block] + its rank in the tile]; rank
+// order = group k, then thread, then the 16 labels of the group (original order).
+template <typename LT>
+__global__ __launch_bounds__(kCmpThreads) void compact_write_kernel(
+    const float* __restrict__ s, const LT* __restrict__ lab, int64_t n, int vec,
+    const int64_t* __restrict__ pos_base, float* __restrict__ pos_out, unsigned long long* __restrict__ nonfinite) {
+    constexpr int kW = kCmpThreads / kWave;
+    __shared__ int cnt[kCmpSlots][kW];
+    const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+    const int64_t base = int64_t(blockIdx.x) * kCmpTile;
+    int no = 0;
+    unsigned m[kCmpSlots];
+#pragma unroll
+    for (int k = 0; k < kCmpSlots; ++k)
+        m[k] = label_masks16(lab, base + (int64_t(k) * kCmpThreads + threadIdx.x) * 16, n, vec, no);
+    int excl[kCmpSlots];
+#pragma unroll
+    for (int k = 0; k < kCmpSlots; ++k) {
+        const int c = __popc(m[k]);
+        int incl = c;  // inclusive scan over the wave's lanes
+#pragma unroll
+        for (int off = 1; off < kWave; off <<= 1) {
+            const int v = __shfl_up(incl, off, kWave);
+            if (lane >= off) incl += v;
+        }
+        excl[k] = incl - c;
+        if (lane == kWave - 1) cnt[k][wid] = incl;
+    }
+    __syncthreads();
+    const int64_t pbase = pos_base[blockIdx.x];
+    int run = 0, nf = 0;
+#pragma unroll
+    for (int k = 0; k < kCmpSlots; ++k) {
+        int before = run;
+#pragma unroll
+        for (int w = 0; w < kW; ++w) {
+            const int c = cnt[k][w];
+            before += w < wid ? c : 0;
+            run += c;
+        }
+        int64_t r = pbase + before + excl[k];
+        const int64_t i = base + (int64_t(k) * kCmpThreads + threadIdx.x) * 16;
+        for (unsigned b = m[k]; b != 0u; b &= b - 1u) {
+            const float v = s[i + __ffs(b) - 1];
+            nf += !isfinite(v);
+            pos_out[r++] = v;
+        }
+    }
+    if (nf) atomicAdd(nonfinite, static_cast<unsigned long long>(nf));
+}
+
+template <typename LT>
+int launch_compact(const float* s, const LT* lab, int64_t n, float* pos_out, int64_t* stats, void* ws,
+                   hipStream_t st) {
+    const int64_t nblk = compact_blocks(n);
+    int64_t* pos_base = static_cast<int64_t*>(ws);
+    int* blk = reinterpret_cast<int*>(pos_base + nblk);
+    const int vec = (reinterpret_cast<uintptr_t>(lab) & 15u) == 0;
+    hipLaunchKernelGGL(compact_count_kernel<LT>, dim3(nblk), dim3(kCmpThreads), 0, st, lab, n, vec, blk);
+    int rc = launch_status();
+    if (rc) return rc;
+    // stats = {P, n - P, 0, #other}; the write pass adds the non-finite positives into stats[2]
+    hipLaunchKernelGGL(split_scan_kernel, dim3(1), dim3(kScanThreads), 0, st, blk, nblk, n, pos_base, stats);
+    rc = launch_status();
+    if (rc) return rc;
+    hipLaunchKernelGGL(compact_write_kernel<LT>, dim3(nblk), dim3(kCmpThreads), 0, st, s, lab, n, vec, pos_base,
+                       pos_out, reinterpret_cast<unsigned long long*>(stats + 2));
+    return launch_status();
+}
+
 // ============================ pair count ======================================
 
 constexpr int kPcThreads = 256;
@@ -475,6 +647,26 @@ int dauc_split_scores(const float* scores, const void* labels, int label_dtype, 
         case DAUC_LABEL_I64:
             return launch_split(scores, static_cast<const int64_t*>(labels), n, pos_out, neg_out,
                                 stats, workspace, st);
+        default:
+            return DAUC_EINVAL;
+    }
+}
+
+int dauc_compact_positives(const float* scores, const void* labels, int label_dtype, int64_t n,
+                           float* pos_out, int64_t* stats, void* workspace, size_t workspace_bytes,
+                           dauc_stream_t stream) {
+    if (n <= 0 || scores == nullptr || labels == nullptr || pos_out == nullptr || stats == nullptr ||
+        workspace == nullptr || workspace_bytes < dauc_split_workspace_size(n) ||
+        (reinterpret_cast<uintptr_t>(workspace) & 7u) || (reinterpret_cast<uintptr_t>(stats) & 7u))
+        return DAUC_EINVAL;
+    hipStream_t st = as_hip(stream);
+    switch (label_dtype) {
+        case DAUC_LABEL_I8:
+            return launch_compact(scores, static_cast<const int8_t*>(labels), n, pos_out, stats, workspace, st);
+        case DAUC_LABEL_I32:
+            return launch_compact(scores, static_cast<const int32_t*>(labels), n, pos_out, stats, workspace, st);
+        case DAUC_LABEL_I64:
+            return launch_compact(scores, static_cast<const int64_t*>(labels), n, pos_out, stats, workspace, st);
         default:
             return DAUC_EINVAL;
     }

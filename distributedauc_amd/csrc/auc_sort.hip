@@ -168,29 +168,58 @@ __global__ __launch_bounds__(kSortThreads) void radix_scatter_kernel(const void*
 
 // ---- search ---------------------------------------------------------------------------
 
-#ifndef DAUC_QUERY_MAX_DEPTH
-#define DAUC_QUERY_MAX_DEPTH 15
+#ifndef DAUC_QUERY_MAX_SPLIT
+#define DAUC_QUERY_MAX_SPLIT 40000
 #endif
 #ifndef DAUC_QUERY_BLOCKS_PER_CU
 #define DAUC_QUERY_BLOCKS_PER_CU 1
 #endif
-// splitters: a perfect tree of depth <= 15 (128 KB of LDS; bucket size k halves per level)
-constexpr int kMaxSplit = (1 << DAUC_QUERY_MAX_DEPTH) - 1;
-constexpr int kTreeSlots = kMaxSplit + 1;  // 1-based BFS array
-constexpr size_t kTreeBytes = size_t(kTreeSlots) * 4;
+#ifndef DAUC_QUERY_LOCKSTEP
+#define DAUC_QUERY_LOCKSTEP 0  // 0: by bucket size (lockstep_queries), else 1 / 2 / 4 keys in lockstep
+#endif
+// Splitters (every k-th sorted key, k a power of two) kept in LDS: at most kMaxSplit of them
+// (4 B each: 40000 -> 156 KB of the CU's 160 KB), so a bucket holds k <= 4 keys -- ONE 16-byte
+// load -- up to M = 160,000 table keys (2^27 scores at 0.1 % positives: M = 134,447 -> k = 4).
+constexpr int kMaxSplit = DAUC_QUERY_MAX_SPLIT;
+constexpr size_t kTreeBytes = size_t(kMaxSplit) * 4;
 constexpr int kQueryThreads = 1024;
 constexpr unsigned kPadKey = 0xffffffffu;  // above every finite score's key (max 0xff7fffff)
 
-// tree[i] (BFS index i in [1, 2^h)) = the splitter whose in-order rank is r, i.e.
-// sorted[r * k], or kPadKey past the last splitter.
-__global__ __launch_bounds__(256) void build_tree_kernel(const unsigned* __restrict__ sorted, int64_t M, int k,
-                                                         int S, int h, unsigned* __restrict__ tree) {
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i == 0 || i >= (1 << h)) return;
-    const int d = 31 - __clz(i);                          // depth of node i
-    const int pidx = i - (1 << d);                        // position within its level
-    const int r = ((2 * pidx + 1) << (h - 1 - d)) - 1;    // in-order rank
-    tree[i] = r < S ? sorted[int64_t(r) * k] : kPadKey;
+// The S splitters form the in-order ranks of a perfect BFS tree of height h (2^(h-1) <= S <
+// 2^h): node (depth d, position p) has rank ((2p + 1) << (h - 1 - d)) - 1; nodes whose rank is
+// >= S are padding (+inf) and form a suffix of every level, so only the first
+// level_nodes(S, h, d) nodes of each level are stored, level after level: S words in all.
+__host__ __device__ __forceinline__ int level_nodes(int S, int h, int d) { return ((S >> (h - 1 - d)) + 1) >> 1; }
+
+__global__ __launch_bounds__(256) void build_tree_kernel(const unsigned* __restrict__ sorted, int k, int S, int h,
+                                                         unsigned* __restrict__ tree) {
+    const int c = blockIdx.x * 256 + threadIdx.x;
+    if (c >= S) return;
+    int d = 0, off = 0;
+    while (c >= off + level_nodes(S, h, d)) off += level_nodes(S, h, d++);
+    const int r = ((2 * (c - off) + 1) << (h - 1 - d)) - 1;  // in-order rank (< S)
+    tree[c] = sorted[int64_t(r) * k];
+}
+
+// Q walks of the tree in lockstep: i[q] ends as 2^h + #splitters <= x[q]. The level geometry is
+// wave-uniform (scalar registers); a position past the stored prefix of its level is padding.
+template <int Q>
+__device__ __forceinline__ void tree_walk(const unsigned (&x)[Q], unsigned (&i)[Q], const unsigned* __restrict__ tree,
+                                          int S, int h) {
+#pragma unroll
+    for (int q = 0; q < Q; ++q) i[q] = 1;
+    int off = 0;
+    for (int d = 0; d < h; ++d) {
+        const unsigned nd = static_cast<unsigned>(level_nodes(S, h, d)), lvl = 1u << d;
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            const unsigned p = i[q] - lvl;
+            const bool in = p < nd;
+            const unsigned v = tree[off + (in ? p : nd - 1)];
+            i[q] = 2 * i[q] + ((in ? v : kPadKey) <= x[q]);
+        }
+        off += static_cast<int>(nd);
+    }
 }
 
 // #keys of bucket b (keys sorted[b*k .. min(b*k + k, M))) that are <= x, and that are < x;
@@ -244,49 +273,40 @@ __device__ __forceinline__ int64_t count_below(const unsigned* __restrict__ a, i
     return base - lo;
 }
 
-// K = 0: buckets of k > 32 keys, finished by binary searches in global memory
+// One query (K = 0: buckets of k > 32 keys, finished by binary searches in global memory).
 template <int K, bool TABLE_POS>
-__device__ __forceinline__ void count_query(unsigned x, const unsigned* __restrict__ tree, int h, int k,
+__device__ __forceinline__ void count_query(unsigned x, const unsigned* __restrict__ tree, int S, int h, int k,
                                             const unsigned* __restrict__ sorted, int64_t M,
                                             unsigned long long& w, unsigned long long& t) {
-    // splitters <= x (walk i) and < x = <= x - 1 (walk j; finite keys are >= 0x00800000, so
+    // splitters <= x (walk 0) and < x = <= x - 1 (walk 1; finite keys are >= 0x00800000, so
     // x - 1 never wraps)
-    const unsigned xm = x - 1u;
-    int64_t su, sl = 0;
+    const int64_t leaves = int64_t(1) << h;
+    int64_t ub = 0, lb = 0;
     if constexpr (K <= 1) {
-        unsigned i = 1, j = 1;
-        for (int d = 0; d < h; ++d) {
-            const unsigned a = tree[i], c = tree[j];
-            i = 2 * i + (a <= x);
-            j = 2 * j + (c <= xm);
-        }
-        su = int64_t(i) - (int64_t(1) << h);
-        sl = int64_t(j) - (int64_t(1) << h);
-    } else {
-        unsigned i = 1;
-        for (int d = 0; d < h; ++d) i = 2 * i + (tree[i] <= x);
-        su = int64_t(i) - (int64_t(1) << h);
-    }
-    int64_t ub, lb;
-    if constexpr (K == 1) {
-        ub = su;
-        lb = sl;
-    } else if constexpr (K == 0) {
-        ub = 0;
-        lb = 0;
-        if (su > 0) {
-            const int64_t b0 = (su - 1) * k, b1 = (b0 + k < M) ? b0 + k : M;
-            ub = b0 + count_below<false>(sorted, b0, b1, x);
-        }
-        if (sl > 0) {
-            const int64_t b0 = (sl - 1) * k, b1 = (b0 + k < M) ? b0 + k : M;
-            lb = b0 + count_below<true>(sorted, b0, b1, x);
+        const unsigned xs[2] = {x, x - 1u};
+        unsigned i[2];
+        tree_walk<2>(xs, i, tree, S, h);
+        const int64_t su = int64_t(i[0]) - leaves, sl = int64_t(i[1]) - leaves;
+        if constexpr (K == 1) {
+            ub = su;
+            lb = sl;
+        } else {
+            if (su > 0) {
+                const int64_t b0 = (su - 1) * k, b1 = (b0 + k < M) ? b0 + k : M;
+                ub = b0 + count_below<false>(sorted, b0, b1, x);
+            }
+            if (sl > 0) {
+                const int64_t b0 = (sl - 1) * k, b1 = (b0 + k < M) ? b0 + k : M;
+                lb = b0 + count_below<true>(sorted, b0, b1, x);
+            }
         }
     } else {
         // one walk for x; the walk for x - 1 is needed only when the last splitter <= x
         // equals x (a run of x may then start in an earlier bucket)
-        ub = 0;
-        lb = 0;
+        const unsigned xs[1] = {x};
+        unsigned i[1];
+        tree_walk<1>(xs, i, tree, S, h);
+        const int64_t su = int64_t(i[0]) - leaves;
         if (su > 0) {
             int le = 0, lt = 0;
             unsigned first = 0;
@@ -295,9 +315,9 @@ __device__ __forceinline__ void count_query(unsigned x, const unsigned* __restri
             if (first < x) {
                 lb = (su - 1) * K + lt;
             } else {
-                unsigned j = 1;
-                for (int d = 0; d < h; ++d) j = 2 * j + (tree[j] <= xm);
-                const int64_t sl = int64_t(j) - (int64_t(1) << h);
+                const unsigned xm[1] = {x - 1u};
+                tree_walk<1>(xm, i, tree, S, h);
+                const int64_t sl = int64_t(i[0]) - leaves;
                 if (sl > 0) {
                     bucket_counts<K>(sorted, M, sl - 1, x, le, lt, first);
                     lb = (sl - 1) * K + lt;
@@ -309,27 +329,123 @@ __device__ __forceinline__ void count_query(unsigned x, const unsigned* __restri
     t += static_cast<unsigned long long>(ub - lb);
 }
 
+// Q queries walked in lockstep (K = 1 .. 32): Q independent chains of LDS reads (and then Q
+// bucket loads) in flight per lane. use[q] = false: the slot is walked but not counted.
+template <int K>
+constexpr int lockstep_queries() {
+    return DAUC_QUERY_LOCKSTEP ? (DAUC_QUERY_LOCKSTEP * K > 32 ? 1 : DAUC_QUERY_LOCKSTEP)
+                               : (K <= 8 ? 4 : (K == 16 ? 2 : 1));
+}
+
+template <int K, int Q, bool TABLE_POS>
+__device__ __forceinline__ void count_queries(const unsigned (&x)[Q], const bool (&use)[Q],
+                                              const unsigned* __restrict__ tree, int S, int h,
+                                              const unsigned* __restrict__ sorted, int64_t M,
+                                              unsigned long long& w, unsigned long long& t) {
+    static_assert(K >= 1 && K <= 32, "bucketed lockstep walk");
+    const int64_t leaves = int64_t(1) << h;
+    if constexpr (K == 1) {
+        // the tree holds every key: splitters <= x and <= x - 1 directly
+        unsigned xs[2 * Q], i[2 * Q];
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            xs[q] = x[q];
+            xs[Q + q] = x[q] - 1u;
+        }
+        tree_walk<2 * Q>(xs, i, tree, S, h);
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            if (!use[q]) continue;
+            const int64_t ub = int64_t(i[q]) - leaves, lb = int64_t(i[Q + q]) - leaves;
+            w += TABLE_POS ? static_cast<unsigned long long>(M - ub) : static_cast<unsigned long long>(lb);
+            t += static_cast<unsigned long long>(ub - lb);
+        }
+    } else {
+        unsigned i[Q];
+        tree_walk<Q>(x, i, tree, S, h);
+        // every bucket load issued before any is examined (su = 0: bucket 0 is read, unused)
+        int le[Q], lt[Q];
+        unsigned first[Q];
+        int64_t su[Q];
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            su[q] = int64_t(i[q]) - leaves;
+            bucket_counts<K>(sorted, M, su[q] > 0 ? su[q] - 1 : 0, x[q], le[q], lt[q], first[q]);
+        }
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            if (!use[q]) continue;
+            int64_t ub = 0, lb = 0;
+            if (su[q] > 0) {
+                ub = (su[q] - 1) * K + le[q];
+                if (first[q] < x[q]) {
+                    lb = (su[q] - 1) * K + lt[q];
+                } else {
+                    // the bucket starts with x: a run of x may begin in an earlier bucket (rare)
+                    const unsigned xm[1] = {x[q] - 1u};
+                    unsigned j[1];
+                    tree_walk<1>(xm, j, tree, S, h);
+                    const int64_t sl = int64_t(j[0]) - leaves;
+                    if (sl > 0) {
+                        int le2 = 0, lt2 = 0;
+                        unsigned f2 = 0;
+                        bucket_counts<K>(sorted, M, sl - 1, x[q], le2, lt2, f2);
+                        lb = (sl - 1) * K + lt2;
+                    }
+                }
+            }
+            w += TABLE_POS ? static_cast<unsigned long long>(M - ub) : static_cast<unsigned long long>(lb);
+            t += static_cast<unsigned long long>(ub - lb);
+        }
+    }
+}
+
+// Four keys (one float4 slot) with per-key use flags, through count_queries in groups of Q
+// (K = 0, buckets > 32 keys finished in global memory: one key at a time).
+template <int K, bool TABLE_POS>
+__device__ __forceinline__ void count4(const unsigned (&x)[4], const bool (&use)[4], const unsigned* __restrict__ tree,
+                                       int S, int h, int k, const unsigned* __restrict__ sorted, int64_t M,
+                                       unsigned long long& w, unsigned long long& t) {
+    if constexpr (K == 0) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            if (use[q]) count_query<0, TABLE_POS>(x[q], tree, S, h, k, sorted, M, w, t);
+    } else {
+        constexpr int Q = lockstep_queries<K>();
+#pragma unroll
+        for (int g = 0; g < 4; g += Q) {
+            unsigned xs[Q];
+            bool us[Q];
+#pragma unroll
+            for (int q = 0; q < Q; ++q) {
+                xs[q] = x[g + q];
+                us[q] = use[g + q];
+            }
+            count_queries<K, Q, TABLE_POS>(xs, us, tree, S, h, sorted, M, w, t);
+        }
+    }
+}
+
 template <int K, bool TABLE_POS>
 __global__ __launch_bounds__(kQueryThreads) void query_count_kernel(const float* __restrict__ q, int64_t L,
-                                                                   const unsigned* __restrict__ gtree, int h, int k,
-                                                                   const unsigned* __restrict__ sorted, int64_t M,
-                                                                   unsigned long long* __restrict__ out) {
+                                                                   const unsigned* __restrict__ gtree, int S, int h,
+                                                                   int k, const unsigned* __restrict__ sorted,
+                                                                   int64_t M, unsigned long long* __restrict__ out) {
     extern __shared__ unsigned tree[];
-    for (int i = threadIdx.x; i < (1 << h); i += kQueryThreads) tree[i] = gtree[i];
+    for (int i = threadIdx.x; i < S; i += kQueryThreads) tree[i] = gtree[i];
     __syncthreads();
     unsigned long long w = 0, t = 0;
     const bool vec = (reinterpret_cast<uintptr_t>(q) & 15u) == 0;
     const int64_t nvec = vec ? L / 4 : 0;
     const int64_t stride = int64_t(gridDim.x) * kQueryThreads;
+    const bool all[4] = {true, true, true, true};
     for (int64_t v = int64_t(blockIdx.x) * kQueryThreads + threadIdx.x; v < nvec; v += stride) {
         const f32x4 f = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(q) + v);
-        count_query<K, TABLE_POS>(key_of(f.x), tree, h, k, sorted, M, w, t);
-        count_query<K, TABLE_POS>(key_of(f.y), tree, h, k, sorted, M, w, t);
-        count_query<K, TABLE_POS>(key_of(f.z), tree, h, k, sorted, M, w, t);
-        count_query<K, TABLE_POS>(key_of(f.w), tree, h, k, sorted, M, w, t);
+        const unsigned x[4] = {key_of(f.x), key_of(f.y), key_of(f.z), key_of(f.w)};
+        count4<K, TABLE_POS>(x, all, tree, S, h, k, sorted, M, w, t);
     }
     for (int64_t i = nvec * 4 + int64_t(blockIdx.x) * kQueryThreads + threadIdx.x; i < L; i += stride)
-        count_query<K, TABLE_POS>(key_of(q[i]), tree, h, k, sorted, M, w, t);
+        count_query<K, TABLE_POS>(key_of(q[i]), tree, S, h, k, sorted, M, w, t);
     __shared__ unsigned long long red[2][kQueryThreads / kWave];
     w = wave_sum(w);
     t = wave_sum(t);
@@ -373,23 +489,33 @@ __device__ __forceinline__ void label4(const LT* __restrict__ lab, int64_t i, bo
     }
 }
 
+// Every queried score is also checked to be finite (sklearn rejects NaN / inf scores,
+// _ranking.py:868-869): nonfinite (nullable) += #queried non-finite scores. The negatives are
+// never materialised, so this is the only pass that reads their scores.
 template <int K, typename LT>
 __global__ __launch_bounds__(kQueryThreads) void query_labeled_kernel(const float* __restrict__ s,
                                                                      const LT* __restrict__ lab, int64_t begin,
                                                                      int64_t end, const unsigned* __restrict__ gtree,
-                                                                     int h, int k, const unsigned* __restrict__ sorted,
-                                                                     int64_t M, unsigned long long* __restrict__ out) {
+                                                                     int S, int h, int k,
+                                                                     const unsigned* __restrict__ sorted,
+                                                                     int64_t M, unsigned long long* __restrict__ out,
+                                                                     unsigned long long* __restrict__ nonfinite) {
     extern __shared__ unsigned tree[];
-    for (int i = threadIdx.x; i < (1 << h); i += kQueryThreads) tree[i] = gtree[i];
+    for (int i = threadIdx.x; i < S; i += kQueryThreads) tree[i] = gtree[i];
     __syncthreads();
     unsigned long long w = 0, t = 0;
+    unsigned nf = 0;
     // scalar head up to a 4-element boundary, then float4 slots, then the scalar tail
     const int64_t a0 = (begin + 3) & ~int64_t(3);
     const int64_t head = a0 < end ? a0 : end;
     const int64_t stride = int64_t(gridDim.x) * kQueryThreads;
     const int64_t tid = int64_t(blockIdx.x) * kQueryThreads + threadIdx.x;
-    for (int64_t i = begin + tid; i < head; i += stride)
-        if (lab[i] != LT(1)) count_query<K, true>(key_of(s[i]), tree, h, k, sorted, M, w, t);
+    for (int64_t i = begin + tid; i < head; i += stride) {
+        if (lab[i] != LT(1)) {
+            nf += !isfinite(s[i]);
+            count_query<K, true>(key_of(s[i]), tree, S, h, k, sorted, M, w, t);
+        }
+    }
     const int64_t nvec = end > head ? (end - head) / 4 : 0;
     const bool aligned = (reinterpret_cast<uintptr_t>(s + head) & 15u) == 0 &&
                          (reinterpret_cast<uintptr_t>(lab + head) & (4 * sizeof(LT) - 1)) == 0;
@@ -408,29 +534,41 @@ __global__ __launch_bounds__(kQueryThreads) void query_labeled_kernel(const floa
         }
         bool neg[4];
         label4(lab, i, aligned, end, neg);
+        unsigned x[4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
-            if (neg[q]) count_query<K, true>(key_of(f[q]), tree, h, k, sorted, M, w, t);
+        for (int q = 0; q < 4; ++q) {
+            x[q] = key_of(f[q]);
+            nf += neg[q] && !isfinite(f[q]);
+        }
+        count4<K, true>(x, neg, tree, S, h, k, sorted, M, w, t);
     }
-    for (int64_t i = head + nvec * 4 + tid; i < end; i += stride)
-        if (lab[i] != LT(1)) count_query<K, true>(key_of(s[i]), tree, h, k, sorted, M, w, t);
-    __shared__ unsigned long long red[2][kQueryThreads / kWave];
+    for (int64_t i = head + nvec * 4 + tid; i < end; i += stride) {
+        if (lab[i] != LT(1)) {
+            nf += !isfinite(s[i]);
+            count_query<K, true>(key_of(s[i]), tree, S, h, k, sorted, M, w, t);
+        }
+    }
+    __shared__ unsigned long long red[3][kQueryThreads / kWave];
     w = wave_sum(w);
     t = wave_sum(t);
+    const unsigned long long nfw = wave_sum(static_cast<unsigned long long>(nf));
     const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
     if (lane == 0) {
         red[0][wid] = w;
         red[1][wid] = t;
+        red[2][wid] = nfw;
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-        unsigned long long bw = 0, bt = 0;
+        unsigned long long bw = 0, bt = 0, bn = 0;
         for (int i = 0; i < kQueryThreads / kWave; ++i) {
             bw += red[0][i];
             bt += red[1][i];
+            bn += red[2][i];
         }
         if (bw) atomicAdd(out + 0, bw);
         if (bt) atomicAdd(out + 1, bt);
+        if (bn && nonfinite) atomicAdd(nonfinite, bn);
     }
 }
 
@@ -451,23 +589,22 @@ int query_grid(int64_t L) {
 }
 
 template <bool TABLE_POS>
-int launch_query(int k, const float* q, int64_t L, const unsigned* tree, int h, const unsigned* sorted, int64_t M,
-                 unsigned long long* out, hipStream_t st) {
+int launch_query(int k, const float* q, int64_t L, const unsigned* tree, int S, int h, const unsigned* sorted,
+                 int64_t M, unsigned long long* out, hipStream_t st) {
     const dim3 grid(query_grid(L)), block(kQueryThreads);
-    const size_t lds = size_t(1) << h << 2;
-    if (k > 32) {
-        hipLaunchKernelGGL((query_count_kernel<0, TABLE_POS>), grid, block, lds, st, q, L, tree, h, k, sorted, M, out);
-        return launch_status();
-    }
+    const size_t lds = size_t(S) * 4;
+#define DAUC_QC(KV) \
+    hipLaunchKernelGGL((query_count_kernel<KV, TABLE_POS>), grid, block, lds, st, q, L, tree, S, h, k, sorted, M, out)
     switch (k) {
-        case 1: hipLaunchKernelGGL((query_count_kernel<1, TABLE_POS>), grid, block, lds, st, q, L, tree, h, k, sorted, M, out); break;
-        case 2: hipLaunchKernelGGL((query_count_kernel<2, TABLE_POS>), grid, block, lds, st, q, L, tree, h, k, sorted, M, out); break;
-        case 4: hipLaunchKernelGGL((query_count_kernel<4, TABLE_POS>), grid, block, lds, st, q, L, tree, h, k, sorted, M, out); break;
-        case 8: hipLaunchKernelGGL((query_count_kernel<8, TABLE_POS>), grid, block, lds, st, q, L, tree, h, k, sorted, M, out); break;
-        case 16: hipLaunchKernelGGL((query_count_kernel<16, TABLE_POS>), grid, block, lds, st, q, L, tree, h, k, sorted, M, out); break;
-        case 32: hipLaunchKernelGGL((query_count_kernel<32, TABLE_POS>), grid, block, lds, st, q, L, tree, h, k, sorted, M, out); break;
-        default: return DAUC_EINVAL;
+        case 1: DAUC_QC(1); break;
+        case 2: DAUC_QC(2); break;
+        case 4: DAUC_QC(4); break;
+        case 8: DAUC_QC(8); break;
+        case 16: DAUC_QC(16); break;
+        case 32: DAUC_QC(32); break;
+        default: DAUC_QC(0); break;
     }
+#undef DAUC_QC
     return launch_status();
 }
 
@@ -539,13 +676,14 @@ int radix_sort_keys(const float* neg, int64_t N, const SortWs& w, hipStream_t st
 }
 
 template <typename LT>
-int launch_labeled(int k, const float* s, const LT* lab, int64_t begin, int64_t end, const unsigned* tree, int h,
-                   const unsigned* sorted, int64_t M, unsigned long long* out, hipStream_t st) {
+int launch_labeled(int k, const float* s, const LT* lab, int64_t begin, int64_t end, const unsigned* tree, int S,
+                   int h, const unsigned* sorted, int64_t M, unsigned long long* out, unsigned long long* nonfinite,
+                   hipStream_t st) {
     const dim3 grid(query_grid(end - begin)), block(kQueryThreads);
-    const size_t lds = size_t(1) << h << 2;
-#define DAUC_QL(KV)                                                                                           \
-    hipLaunchKernelGGL((query_labeled_kernel<KV, LT>), grid, block, lds, st, s, lab, begin, end, tree, h, k, \
-                       sorted, M, out)
+    const size_t lds = size_t(S) * 4;
+#define DAUC_QL(KV)                                                                                              \
+    hipLaunchKernelGGL((query_labeled_kernel<KV, LT>), grid, block, lds, st, s, lab, begin, end, tree, S, h, k, \
+                       sorted, M, out, nonfinite)
     switch (k) {
         case 1: DAUC_QL(1); break;
         case 2: DAUC_QL(2); break;
@@ -561,7 +699,7 @@ int launch_labeled(int k, const float* s, const LT* lab, int64_t begin, int64_t 
 
 // sort the table, build the tree; returns the tree pointer and geometry
 int prepare_table(const float* table, int64_t M, void* workspace, hipStream_t st, const unsigned** sorted,
-                  unsigned** tree, int* k_out, int* h_out) {
+                  unsigned** tree, int* k_out, int* S_out, int* h_out) {
     SortWs w = carve(workspace, M);
     int rc = radix_sort_keys(table, M, w, st, sorted);
     if (rc) return rc;
@@ -571,8 +709,9 @@ int prepare_table(const float* table, int64_t M, void* workspace, hipStream_t st
     int h = 1;
     while ((1 << h) - 1 < S) ++h;
     *tree = reinterpret_cast<unsigned*>(static_cast<char*>(workspace) + ((sort_ws_bytes(M) + 255) / 256) * 256);
-    hipLaunchKernelGGL(build_tree_kernel, dim3(((1 << h) + 255) / 256), dim3(256), 0, st, *sorted, M, k, S, h, *tree);
+    hipLaunchKernelGGL(build_tree_kernel, dim3((S + 255) / 256), dim3(256), 0, st, *sorted, k, S, h, *tree);
     *k_out = k;
+    *S_out = S;
     *h_out = h;
     return launch_status();
 }
@@ -613,17 +752,18 @@ int dauc_auc_counts_sorted(const float* pos, int64_t P, const float* neg, int64_
     hipStream_t st = as_hip(stream);
     const unsigned* sorted = nullptr;
     unsigned* tree = nullptr;
-    int k = 1, h = 1;
-    int rc = prepare_table(table_pos ? pos : neg, M, workspace, st, &sorted, &tree, &k, &h);
+    int k = 1, S = 1, h = 1;
+    int rc = prepare_table(table_pos ? pos : neg, M, workspace, st, &sorted, &tree, &k, &S, &h);
     if (rc) return rc;
     const float* q = table_pos ? neg : pos;
-    return table_pos ? launch_query<true>(k, q, L, tree, h, sorted, M, wins_ties, st)
-                     : launch_query<false>(k, q, L, tree, h, sorted, M, wins_ties, st);
+    return table_pos ? launch_query<true>(k, q, L, tree, S, h, sorted, M, wins_ties, st)
+                     : launch_query<false>(k, q, L, tree, S, h, sorted, M, wins_ties, st);
 }
 
 int dauc_auc_counts_sorted_labeled(const float* pos, int64_t P, const float* scores, const void* labels,
                                    int label_dtype, int64_t begin, int64_t end, unsigned long long* wins_ties,
-                                   void* workspace, size_t workspace_bytes, dauc_stream_t stream) {
+                                   unsigned long long* nonfinite, void* workspace, size_t workspace_bytes,
+                                   dauc_stream_t stream) {
     if (P < 0 || begin < 0 || end < begin || wins_ties == nullptr || (P > 0 && pos == nullptr) ||
         (end > begin && (scores == nullptr || labels == nullptr)))
         return DAUC_EINVAL;
@@ -634,19 +774,19 @@ int dauc_auc_counts_sorted_labeled(const float* pos, int64_t P, const float* sco
     hipStream_t st = as_hip(stream);
     const unsigned* sorted = nullptr;
     unsigned* tree = nullptr;
-    int k = 1, h = 1;
-    int rc = prepare_table(pos, P, workspace, st, &sorted, &tree, &k, &h);
+    int k = 1, S = 1, h = 1;
+    int rc = prepare_table(pos, P, workspace, st, &sorted, &tree, &k, &S, &h);
     if (rc) return rc;
     switch (label_dtype) {
         case DAUC_LABEL_I8:
-            return launch_labeled(k, scores, static_cast<const int8_t*>(labels), begin, end, tree, h, sorted, P,
-                                  wins_ties, st);
+            return launch_labeled(k, scores, static_cast<const int8_t*>(labels), begin, end, tree, S, h, sorted, P,
+                                  wins_ties, nonfinite, st);
         case DAUC_LABEL_I32:
-            return launch_labeled(k, scores, static_cast<const int32_t*>(labels), begin, end, tree, h, sorted, P,
-                                  wins_ties, st);
+            return launch_labeled(k, scores, static_cast<const int32_t*>(labels), begin, end, tree, S, h, sorted, P,
+                                  wins_ties, nonfinite, st);
         default:
-            return launch_labeled(k, scores, static_cast<const int64_t*>(labels), begin, end, tree, h, sorted, P,
-                                  wins_ties, st);
+            return launch_labeled(k, scores, static_cast<const int64_t*>(labels), begin, end, tree, S, h, sorted, P,
+                                  wins_ties, nonfinite, st);
     }
 }
 

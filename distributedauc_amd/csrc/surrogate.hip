@@ -512,6 +512,99 @@ __global__ __launch_bounds__(kThreads) void surrogate_chunk_kernel(
 #endif
 }
 
+// The same stream with SPAN consecutive chunks per workgroup (one contiguous span of
+// SPAN x 4096 elements): the chunk after the current one is loaded while the current one is
+// reduced and stored (two chunks of loads in flight per thread), and the launch writes SPAN
+// times fewer rows, so the row reduce shrinks to one workgroup (<= 512 rows) with no hand-off.
+// Only whole spans; the ragged tail (< SPAN chunks) is handled element-wise by the last
+// workgroup.
+template <typename YT, bool CLASS_ONLY, int S, int SPAN>
+__global__ __launch_bounds__(kThreads) void surrogate_span_kernel(
+    const float* __restrict__ h, const YT* __restrict__ y, int64_t B, double invB,
+    const float* __restrict__ abalpha, const float* __restrict__ p_hat, float* __restrict__ dh,
+    double* __restrict__ rows) {
+    SurrogateScalars s;
+    if (CLASS_ONLY) s = SurrogateScalars{};
+    else s = make_scalars(abalpha, p_hat, invB);
+    Acc acc;
+    const bool write_dh = !CLASS_ONLY && dh != nullptr;
+    constexpr int64_t kChunk = chunk_elems(S);
+    const int64_t base = int64_t(blockIdx.x) * SPAN * kChunk;
+    const int64_t whole = B / (SPAN * kChunk);  // workgroups with a full span
+    if (int64_t(blockIdx.x) < whole) {
+        f32x4 cur[S], nxt[S];
+        int ycur[S][4], ynxt[S][4];
+#pragma unroll
+        for (int k = 0; k < S; ++k) {
+            const int64_t b = base + (int64_t(k) * kThreads + threadIdx.x) * kVec;
+            cur[k] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(h + b));
+            load_labels4(y, b, ycur[k]);
+        }
+        for (int c = 0; c < SPAN; ++c) {
+            const int64_t cb = base + c * kChunk;
+            if (c + 1 < SPAN) {
+#pragma unroll
+                for (int k = 0; k < S; ++k) {
+                    const int64_t b = cb + kChunk + (int64_t(k) * kThreads + threadIdx.x) * kVec;
+                    nxt[k] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(h + b));
+                    load_labels4(y, b, ynxt[k]);
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < S; ++k) {
+                const f32x4 g = visit4<CLASS_ONLY>(cur[k], ycur[k], s, acc);
+                if (write_dh)
+                    __builtin_nontemporal_store(
+                        g, reinterpret_cast<f32x4*>(dh + cb + (int64_t(k) * kThreads + threadIdx.x) * kVec));
+            }
+#pragma unroll
+            for (int k = 0; k < S; ++k) {
+                cur[k] = nxt[k];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) ycur[k][q] = ynxt[k][q];
+            }
+        }
+    } else {
+        // after the whole spans: one chunk per workgroup (vector path), the ragged last chunk
+        // element-wise
+        const int64_t cb = whole * SPAN * kChunk + (int64_t(blockIdx.x) - whole) * kChunk;
+        if (cb + kChunk <= B) {
+#pragma unroll
+            for (int k = 0; k < S; ++k) {
+                const int64_t b = cb + (int64_t(k) * kThreads + threadIdx.x) * kVec;
+                int yv[4];
+                load_labels4(y, b, yv);
+                const f32x4 g = visit4<CLASS_ONLY>(
+                    __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(h + b)), yv, s, acc);
+                if (write_dh) __builtin_nontemporal_store(g, reinterpret_cast<f32x4*>(dh + b));
+            }
+        } else {
+            for (int64_t i = cb + threadIdx.x; i < B; i += kThreads) {
+                const float g = visit1<CLASS_ONLY>(h[i], load_label(y, i), s, acc);
+                if (write_dh) dh[i] = g;
+            }
+        }
+    }
+    const double sp = wave_total_dpp(acc.s_pos), sn = wave_total_dpp(acc.s_neg);
+    const double qp = wave_total_dpp(acc.q_pos), qn = wave_total_dpp(acc.q_neg);
+    const int np = wave_total_dpp(acc.n_pos), nn = wave_total_dpp(acc.n_neg);
+    __shared__ double wrow[kWaves][kRowWords];
+    const int wid = threadIdx.x / kWave;
+    if ((threadIdx.x & (kWave - 1)) == kWave - 1) {
+        wrow[wid][0] = sp;
+        wrow[wid][1] = sn;
+        wrow[wid][2] = qp;
+        wrow[wid][3] = qn;
+        wrow[wid][4] = static_cast<double>(np);
+        wrow[wid][5] = static_cast<double>(nn);
+    }
+    __syncthreads();
+    if (threadIdx.x < kRowWords) {
+        const int k = threadIdx.x;
+        rows[int64_t(blockIdx.x) * kRowWords + k] = ((wrow[0][k] + wrow[1][k]) + wrow[2][k]) + wrow[3][k];
+    }
+}
+
 // Reduce the streaming launch's rows (the kernel boundary published them): workgroup b sums
 // rows [512 b, 512 (b + 1)) in a fixed order (thread t: rows t, t + 256). Workgroups b > 0
 // hand their 6 totals to workgroup 0 as encoded 8-B words stored write-through (sc1): a word
@@ -919,6 +1012,27 @@ int launch_chunk(const float* h, const YT* y, int64_t B, const float* abalpha, c
     return launch_status();
 }
 
+template <typename YT, bool CLASS_ONLY, int S, int SPAN>
+int launch_span(const float* h, const YT* y, int64_t B, const float* abalpha, const float* p_hat, float* dh,
+                double* out64, float* grad3, float* loss, double* sums4, int accumulate, void* ws, size_t ws_bytes,
+                hipStream_t st) {
+    constexpr int64_t kChunk = chunk_elems(S);
+    const int64_t whole = B / (SPAN * kChunk);
+    const int64_t nblocks = whole + (B - whole * SPAN * kChunk + kChunk - 1) / kChunk;
+    if (nblocks > 0x7fffffffLL) return DAUC_EINVAL;
+    if (ws == nullptr || ws_bytes < chunk_ws_bytes(nblocks)) return DAUC_EINVAL;
+    const ChunkWs w = chunk_ws(ws, nblocks);
+    const double invB = 1.0 / static_cast<double>(B);
+    hipLaunchKernelGGL((surrogate_span_kernel<YT, CLASS_ONLY, S, SPAN>), dim3(static_cast<unsigned>(nblocks)),
+                       dim3(kThreads), 0, st, h, y, B, invB, abalpha, p_hat, dh, w.rows);
+    int rc = launch_status();
+    if (rc) return rc;
+    hipLaunchKernelGGL((surrogate_rows_reduce_kernel<CLASS_ONLY>), dim3(static_cast<unsigned>(reduce_blocks(nblocks))),
+                       dim3(kThreads), 0, st, w.rows, nblocks, w, invB, abalpha, p_hat, out64, grad3, loss, sums4,
+                       accumulate);
+    return launch_status();
+}
+
 template <typename YT, bool CLASS_ONLY, int S, int G, int CS, bool TF>
 int launch_ticket(const float* h, const YT* y, int64_t B, const float* abalpha, const float* p_hat, float* dh,
                   double* out64, float* grad3, float* loss, double* sums4, int accumulate, void* ws, size_t ws_bytes,
@@ -961,6 +1075,20 @@ int launch_surrogate(const float* h, int64_t hs, const YT* y, int64_t B, const f
                 case 13: DAUC_TV(8, 64, 1024, true);
                 case 14: DAUC_TV(8, 256, 1024, true);
 #undef DAUC_TV
+                case 15: {
+                    // the default streaming kernel alone (no row reduce, no scalars): timing only. It
+                    // leaves its rows in the workspace, so it must not share one with the other variants.
+                    const int64_t nblocks = (B + chunk_elems(kChunkSlots) - 1) / chunk_elems(kChunkSlots);
+                    if (ws == nullptr || ws_bytes < chunk_ws_bytes(nblocks)) return DAUC_EINVAL;
+                    hipLaunchKernelGGL((surrogate_chunk_kernel<YT, false, kChunkSlots, true, true>),
+                                       dim3(static_cast<unsigned>(nblocks)), dim3(kThreads), 0, st, h, y, B,
+                                       1.0 / static_cast<double>(B), abalpha, p_hat, dh, chunk_ws(ws, nblocks).rows);
+                    return launch_status();
+                }
+                case 16: return launch_span<YT, false, 4, 4>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, sums4, accumulate, ws, ws_bytes, st);
+                case 17: return launch_span<YT, false, 4, 8>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, sums4, accumulate, ws, ws_bytes, st);
+                case 18: return launch_span<YT, false, 4, 16>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, sums4, accumulate, ws, ws_bytes, st);
+                case 19: return launch_span<YT, false, 4, 32>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, sums4, accumulate, ws, ws_bytes, st);
                 default: return DAUC_EINVAL;
             }
         }
@@ -1147,7 +1275,7 @@ int dauc_surrogate_fwdbwd_variant(const float* h, int64_t h_stride, const void* 
                                   double* out64, float* grad3, float* loss, void* workspace,
                                   size_t workspace_bytes, int variant, dauc_stream_t stream) {
     if (B <= 0 || h == nullptr || y == nullptr || abalpha == nullptr || p_hat == nullptr ||
-        h_stride <= 0 || (dh != nullptr && dh_stride <= 0) || variant < 0 || variant > 14)
+        h_stride <= 0 || (dh != nullptr && dh_stride <= 0) || variant < 0 || variant > 19)
         return DAUC_EINVAL;
     return dispatch_labels<false>(h, h_stride, y, y_dtype, B, abalpha, p_hat, dh, dh_stride, out64,
                                   grad3, loss, nullptr, 0, workspace, workspace_bytes,

@@ -118,3 +118,14 @@ class DeviceLoader:
                 k += 1
         for idx in self._index_batches():
             yield self._make(idx)
+
+
+def synthetic_scores(n: int, pos_ratio: float, device, seed: int = 2024) -> tuple[torch.Tensor, torch.Tensor]:
+    """The exact-AUC workloads of BASELINE configs[3] / [4]: scores ~ U(0,1) fp32
+    and int8 labels +1 with probability ``pos_ratio`` (else -1), drawn in HBM from one seeded
+    device generator, so every rank (and every test) that asks for the same (n, p, seed) gets
+    the same vectors."""
+    g = torch.Generator(device=device).manual_seed(seed)
+    s = torch.rand(n, generator=g, device=device)
+    y = torch.where(torch.rand(n, generator=g, device=device) < pos_ratio, 1, -1).to(torch.int8)
+    return s, y

@@ -147,7 +147,8 @@ def surrogate_fwdbwd(h: torch.Tensor, y: torch.Tensor, abalpha: torch.Tensor, p_
         _require(loss, "loss", torch.float32, dev)
     L = _lib.load()
     nbytes = L.dauc_surrogate_workspace_size(B)
-    ws = workspaces.get(dev, "surrogate", nbytes)
+    # variant 15 (the streaming kernel alone) leaves its rows behind: a workspace of its own
+    ws = workspaces.get(dev, "surrogate_stream_only" if variant == 15 else "surrogate", nbytes)
     if variant == 0:
         rc = L.dauc_surrogate_fwdbwd(_ptr(h), h.stride(0), _ptr(y), yc, B, _ptr(abalpha), _ptr(p_hat),
                                      _ptr(dh), dh_stride, _ptr(out64), _ptr(grad3), _ptr(loss), _ptr(ws),
@@ -339,6 +340,31 @@ def split_scores(scores: torch.Tensor, labels: torch.Tensor, negatives: bool = T
     return pos, neg, stats
 
 
+def compact_positives(scores: torch.Tensor, labels: torch.Tensor):
+    """Positive scores (label == 1) in original order, reading only the labels and the positives' scores.
+
+    Returns (pos_buf, stats): pos_buf has capacity n, its valid prefix is stats[0] long;
+    stats (device int64 [4]) = {P, n - P, #non-finite positive scores, #labels not in {-1, 1}}.
+    """
+    _require(scores, "scores", torch.float32)
+    dev = scores.device
+    lc = _label_code(labels, "labels")
+    if scores.dim() != 1 or labels.dim() != 1 or scores.shape != labels.shape:
+        raise ValueError("scores and labels must be 1-D of equal length")
+    if not scores.is_contiguous() or not labels.is_contiguous():
+        raise ValueError("scores and labels must be contiguous")
+    n = scores.numel()
+    if n == 0:
+        raise ValueError("empty score vector")
+    pos = torch.empty(n, dtype=torch.float32, device=dev)
+    stats = torch.empty(4, dtype=torch.int64, device=dev)
+    L = _lib.load()
+    ws = workspaces.get(dev, "split", L.dauc_split_workspace_size(n))
+    check(L.dauc_compact_positives(_ptr(scores), _ptr(labels), lc, n, _ptr(pos), _ptr(stats), _ptr(ws),
+                                   ws.numel(), _stream(dev)), "dauc_compact_positives")
+    return pos, stats
+
+
 def pair_count(pos: torch.Tensor, neg: torch.Tensor, wins_ties: torch.Tensor, variant: int = 0) -> None:
     """wins_ties[0] += #{pos > neg}, wins_ties[1] += #{pos == neg} (int64 view of uint64 counters)."""
     _require(pos, "pos", torch.float32)
@@ -371,9 +397,10 @@ def auc_counts_sorted(pos: torch.Tensor, neg: torch.Tensor, wins_ties: torch.Ten
 
 
 def auc_counts_sorted_labeled(pos: torch.Tensor, scores: torch.Tensor, labels: torch.Tensor, begin: int, end: int,
-                              wins_ties: torch.Tensor) -> None:
+                              wins_ties: torch.Tensor, nonfinite: torch.Tensor | None = None) -> None:
     """auc_counts_sorted with the negatives read in place: every element of scores[begin:end]
-    whose label is not 1 is counted against the sorted positives."""
+    whose label is not 1 is counted against the sorted positives; nonfinite (int64 [1],
+    optional) += the number of those scores that are NaN or infinite."""
     _require(pos, "pos", torch.float32)
     dev = pos.device
     _require(scores, "scores", torch.float32, dev)
@@ -387,10 +414,15 @@ def auc_counts_sorted_labeled(pos: torch.Tensor, scores: torch.Tensor, labels: t
         raise ValueError("need 0 <= begin <= end <= scores.numel()")
     if wins_ties.numel() < 2 or not wins_ties.is_contiguous():
         raise ValueError("wins_ties needs 2 contiguous int64 slots")
+    if nonfinite is not None:
+        _require(nonfinite, "nonfinite", torch.int64, dev)
+        if nonfinite.numel() < 1:
+            raise ValueError("nonfinite needs 1 int64 slot")
     L = _lib.load()
     ws = workspaces.get(dev, "sort", L.dauc_sort_workspace_size(max(pos.numel(), 1)))
     check(L.dauc_auc_counts_sorted_labeled(_ptr(pos), pos.numel(), _ptr(scores), _ptr(labels), lc, int(begin),
-                                           int(end), _ptr(wins_ties), _ptr(ws), ws.numel(), _stream(dev)),
+                                           int(end), _ptr(wins_ties), _ptr(nonfinite), _ptr(ws), ws.numel(),
+                                           _stream(dev)),
           "dauc_auc_counts_sorted_labeled")
 
 
@@ -412,5 +444,5 @@ __all__ = [
     "GradSeg", "label_map_phat", "surrogate_fwdbwd", "class_sums", "alpha_from_sums", "pd_update",
     "pd_update_dense", "coda_finalize", "scale_div", "split_scores", "pair_count", "auc_counts_sorted",
     "surrogate_logits_fwdbwd", "class_sums_logits",
-    "sort_keys", "auc_counts_sorted_labeled", "mode_code", "workspaces",
+    "sort_keys", "auc_counts_sorted_labeled", "compact_positives", "mode_code", "workspaces",
 ]

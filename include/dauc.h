@@ -105,7 +105,11 @@ int dauc_surrogate_fwdbwd(const float* h, int64_t h_stride, const void* y, int y
  * per thread, 3: 8, 4: 16, all non-temporal; 5: 8 slots, plain loads; 6: 8 slots, plain
  * stores; 7: 2 slots, non-temporal), 8..14 the single-launch form with start-order tickets
  * (8..12: 4 slots, groups of 512 / 64 / 128 / 256 chunks, 12: ticket drawn after the loads;
- * 13, 14: 8 slots, groups of 64 / 256). Variants 2..14 need unit strides, 16-byte
+ * 13, 14: 8 slots, groups of 64 / 256), 15 the default streaming kernel ALONE (dh only: no
+ * row reduce, no scalar outputs; it leaves its rows in the workspace, so give it a workspace of
+ * its own: timing of the stream without the reduce launch), 16..19 one contiguous span of
+ * 4 / 8 / 16 / 32 chunks (4 slots) per workgroup, next chunk's loads in flight, so the row
+ * reduce is one small workgroup. Variants 2..19 need unit strides, 16-byte
  * aligned h/dh and int8 labels, and B <= 2^31. Every variant returns bitwise-identical dh and counts;
  * the fp64 sums agree to rounding (their reduction trees differ).
  */
@@ -222,6 +226,20 @@ int dauc_split_scores(const float* scores, const void* labels, int label_dtype, 
                       size_t workspace_bytes, dauc_stream_t stream);
 
 /*
+ * Stable compaction of the positive scores (label == 1) for the sort method of main.py:79-81
+ * (sklearn roc_curve(pos_label=1) -> _binary_clf_curve, _ranking.py:826-908): every label is
+ * read once and only the positives' scores are read, so a vector with few positives costs
+ * about one label pass (1 B per score at int8) instead of a full split.
+ *   pos_out[0..P) = the positive scores in original order (capacity n)
+ *   stats[4] (int64) = { P, n - P, #non-finite POSITIVE scores, #labels not in {-1, 1} }
+ * The negatives' scores are checked by dauc_auc_counts_sorted_labeled (its nonfinite count).
+ * workspace >= dauc_split_workspace_size(n), zero-initialised.
+ */
+int dauc_compact_positives(const float* scores, const void* labels, int label_dtype, int64_t n,
+                           float* pos_out, int64_t* stats, void* workspace, size_t workspace_bytes,
+                           dauc_stream_t stream);
+
+/*
  * Exact pairwise count replacing sklearn roc_curve + auc (main.py:79-81):
  *   wins_ties[0] += #{(i, j): pos[i] >  neg[j]}
  *   wins_ties[1] += #{(i, j): pos[i] == neg[j]}      (fp32 equality: -0 == +0)
@@ -261,12 +279,15 @@ int dauc_auc_counts_sorted(const float* pos, int64_t P, const float* neg, int64_
 /*
  * dauc_auc_counts_sorted without materialised negatives: the sorted table is the
  * positives pos[0..P); the queries are the elements of scores/labels in [begin, end)
- * whose label is not 1 (the full arrays, as given to dauc_split_scores). Same
- * accumulation into wins_ties; workspace >= dauc_sort_workspace_size(P).
+ * whose label is not 1 (the full arrays, as given to dauc_compact_positives). Same
+ * accumulation into wins_ties; nonfinite (device uint64 [1], nullable) += the number of
+ * queried scores that are NaN or +-inf (the only check the negatives get: sklearn's
+ * _ranking.py:868-869 rejects them). workspace >= dauc_sort_workspace_size(P).
  */
 int dauc_auc_counts_sorted_labeled(const float* pos, int64_t P, const float* scores, const void* labels,
                                    int label_dtype, int64_t begin, int64_t end, unsigned long long* wins_ties,
-                                   void* workspace, size_t workspace_bytes, dauc_stream_t stream);
+                                   unsigned long long* nonfinite, void* workspace, size_t workspace_bytes,
+                                   dauc_stream_t stream);
 
 /* The radix sort alone: keys_out[0..n) = ascending order-preserving keys of scores (testing). */
 int dauc_sort_keys(const float* scores, int64_t n, unsigned* keys_out, void* workspace,

@@ -167,6 +167,25 @@ def coda_average(per_rank: list[np.ndarray]) -> np.ndarray:
     return acc.numpy()
 
 
+def average_all_dist(model, a, b, alpha, gpos, gneg, lpos, lneg, world: int) -> None:
+    """main.py:33-54 over a live torch.distributed group (gloo on the CPU baseline):
+    one blocking all_reduce(SUM) + ``/= size`` per parameter tensor (buffers untouched,
+    main.py:35-38), then a, b, alpha and the local counts (43-47), the global counts
+    accumulate the summed locals (49-50), and a, b, alpha are divided (52-54). The caller
+    zeroes the locals afterwards (main.py:300-301)."""
+    import torch.distributed as dist
+
+    for param in model.parameters():
+        dist.all_reduce(param.data, op=dist.ReduceOp.SUM)
+        param.data /= float(world)
+    for t in (a, b, alpha, lpos, lneg):
+        dist.all_reduce(t.data, op=dist.ReduceOp.SUM)
+    gpos += lpos
+    gneg += lneg
+    for t in (a, b, alpha):
+        t.data /= float(world)
+
+
 def alpha_from_sums(h_neg, n_neg, h_pos, n_pos) -> np.float32:
     """main.py:197: ``alpha = h_neg/N_neg - h_pos/N_pos``."""
     return np.float32(h_neg / n_neg - h_pos / n_pos)

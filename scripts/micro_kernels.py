@@ -99,6 +99,70 @@ def bench_surrogate(dev, reps, variants=(0,)):
                  GBps_best=9 * B / mn / 1e6, dh_equal_v0=bool(torch.equal(got, ref)))
 
 
+def timeit_b2b(fn, reps, warm=3):
+    """One event pair around reps back-to-back calls (no per-call marker packets): ms per call."""
+    for _ in range(warm):
+        fn()
+    s = torch.cuda.current_stream()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    a.record(s)
+    for _ in range(reps):
+        fn()
+    b.record(s)
+    b.synchronize()
+    return a.elapsed_time(b) / reps
+
+
+def bench_surrogate_b2b(dev, reps, variants):
+    """B = 2^26: each variant timed over reps back-to-back calls (what the bench line reports)."""
+    B = 1 << 26
+    g = torch.Generator(device=dev).manual_seed(7)
+    h = torch.rand(B, device=dev, generator=g)
+    y = torch.where(torch.rand(B, device=dev, generator=g) < 0.1, 1, -1).to(torch.int8)
+    ab = torch.tensor([0.1, -0.2, 0.3], device=dev)
+    p = torch.tensor([0.1], device=dev)
+    dh = torch.empty(B, device=dev)
+    g3 = torch.empty(3, device=dev)
+    o = torch.zeros(6, dtype=torch.float64, device=dev)
+    for v in variants:
+        ms = timeit_b2b(lambda: ops.surrogate_fwdbwd(h, y, ab, p, dh=dh, grad3=g3, out64=o, variant=v), reps)
+        emit(kernel="surrogate_b2b", variant=v, B=B, us=ms * 1e3, GBps=9 * B / ms / 1e6, frac=9 * B / ms / 1e6 / 8000)
+
+
+def bench_aucsort(dev, reps):
+    """The sort-method evaluation by stage: compaction (labels + positives' scores), the
+    whole ExactAUC call, at configs[3] (2^24 @ 1 %) and configs[4] (2^27 @ 0.1 %)."""
+    from distributedauc_amd.auc import ExactAUC
+    from distributedauc_amd.loader import synthetic_scores
+
+    for log2n, pr in ((24, 0.01), (27, 0.001)):
+        n = 1 << log2n
+        s, y = synthetic_scores(n, pr, dev)
+        ms = timeit_b2b(lambda: ops.compact_positives(s, y), reps)
+        emit(kernel="compact_positives", log2n=log2n, us=ms * 1e3, label_GBps=n / ms / 1e6)
+        ms = timeit_b2b(lambda: ops.split_scores(s, y, negatives=False), reps)
+        emit(kernel="split_scores_posonly", log2n=log2n, us=ms * 1e3)
+        pos, st = ops.compact_positives(s, y)
+        P = int(st[0].item())
+        wt = torch.zeros(3, dtype=torch.int64, device=dev)
+        ms = timeit_b2b(lambda: ops.auc_counts_sorted_labeled(pos[:P], s, y, 0, n, wt, nonfinite=wt[2:]), reps)
+        emit(kernel="sort_plus_query", log2n=log2n, P=P, us=ms * 1e3)
+        ev = ExactAUC(method="sort")
+        c = ev.counts(y, s)
+        ts = []
+        for _ in range(reps):
+            torch.cuda.synchronize()
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            ev.counts(y, s)
+            b.record()
+            b.synchronize()
+            ts.append(a.elapsed_time(b))
+        emit(kernel="exact_auc_sort_eval", log2n=log2n, ms=float(np.median(ts)), ms_min=float(np.min(ts)),
+             wins=c["wins"], ties=c["ties"], P=c["P"], N=c["N"])
+
+
 def bench_paircount(dev, reps, log2n):
     n = 1 << log2n
     g = torch.Generator(device=dev).manual_seed(2024)
@@ -145,5 +209,9 @@ if __name__ == "__main__":
         bench_copy(dev, a.reps)
     if "surrogate" in w:
         bench_surrogate(dev, a.reps, [int(v) for v in a.sur_variants.split(",")])
+    if "surrogate_b2b" in w:
+        bench_surrogate_b2b(dev, a.reps, [int(v) for v in a.sur_variants.split(",")])
+    if "aucsort" in w:
+        bench_aucsort(dev, a.reps)
     if "paircount" in w:
         bench_paircount(dev, max(3, a.reps // 10), a.log2n)

@@ -8,6 +8,11 @@ REPO = Path(__file__).resolve().parent.parent
 sys.path.insert(0, str(REPO))
 sys.path.insert(0, str(REPO / "tests"))
 os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+# the shipped MI355X MIOpen find/perf db (ResNet-50 b256 convolutions), set before any GPU test
+# runs a convolution, as bench.py and main.train do
+from distributedauc_amd import use_tuned_miopen_db  # noqa: E402
+
+use_tuned_miopen_db()
 
 GOLDEN = REPO / "tests" / "golden"
 

@@ -1,0 +1,61 @@
+"""bench.py's host logic (CPU): the launch contract and the configs[0] CPU baseline leg.
+
+The N-rank GPU path itself is exercised on the GPU box (tests/test_bench_gpu.py); here only
+what runs before any GPU call, and the gloo worker processes of the CPU baseline, which never
+touch a GPU."""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+import pytest
+
+REPO = Path(__file__).resolve().parents[1]
+
+
+def _bench():
+    sys.path.insert(0, str(REPO))
+    import bench
+
+    return bench
+
+
+def test_defaults_cover_the_baseline_configs():
+    b = _bench()
+    a = b.parse([])
+    assert a.gpus == 1 and a.arch == "resnet50" and a.batch == 256 and a.I == 16  # configs[1]
+    periods = [int(v) for v in a.sweep_I.split(",")]
+    assert {1, 8, 32} <= set(periods)                                                 # configs[2]
+    assert all(a.sweep_steps % I == 0 for I in periods)
+    assert (a.auc_log2n, a.auc_pos) == (24, 0.01)                                     # configs[3]
+    assert (a.auc2_log2n, a.auc2_pos) == (27, 0.001)                                  # configs[4]
+    assert a.r18_steps > 0 and a.cpu_workers == 4                                     # configs[0]
+
+
+def test_world_size_mismatch_fails_before_touching_the_gpu():
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, str(REPO / "bench.py"), "--gpus", "4", "--no-train", "--no-auc",
+                        "--no-surrogate", "--no-cpu-baseline"], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 2, r.stderr
+    assert "WORLD_SIZE=2" in r.stderr
+
+
+def test_host_info_states_core_counts():
+    h = _bench().host_info()
+    assert h["nproc"] >= 1 and 1 <= h["cpu_budget"] <= h["affinity_cpus"]
+
+
+@pytest.mark.timeout(300)
+def test_configs0_cpu_baseline_gloo_workers():
+    """configs[0]'s CPU path: gloo worker processes running the restated step with one
+    average_all round (main.py:33-54) inside the timed window (small images to stay fast)."""
+    b = _bench()
+    args = b.parse(["--cpu-steps", "8", "--image-size", "32", "--cpu-workers", "2"])
+    host = dict(b.host_info(), cpu_budget=2)
+    r = b.cpu_baseline_configs0(args, host)
+    assert "error" not in r, r
+    assert r["workers"] == 2 and r["cores"] == 2 and r["value"] > 0
+    assert r["params"] == 11_177_538 and r["params_finite"]
+    assert r["averaging_round_ms"] > 0

@@ -147,7 +147,8 @@ def test_surrogate_chunked_variants(dev, B):
     c = 2.0 / B * (np.abs(hn) + np.abs(k))
     ref_dh = None
     tick = {}
-    for variant in (0, 0, 1, 2, 3, 4, 5, 6, 7, 8, 8, 9, 10, 11, 12, 13, 14, 2, 8, 1, 12, 14):
+    for variant in (0, 0, 1, 2, 3, 4, 5, 6, 7, 8, 8, 9, 10, 11, 12, 13, 14, 2, 8, 1, 12, 14, 16, 17, 18, 19, 19,
+                    0, 16):
         o = torch.zeros(6, dtype=torch.float64, device=dev)
         dh = torch.full((B,), float("nan"), device=dev)
         ops.surrogate_fwdbwd(h, y, abap[:3], abap[3:], dh=dh, out64=o, variant=variant)
@@ -163,6 +164,14 @@ def test_surrogate_chunked_variants(dev, B):
             assert np.array_equal(got, ref0)  # deterministic reduction order
         if variant >= 8:  # fixed blockIdx summation order: bitwise run-to-run
             assert np.array_equal(got, tick.setdefault(variant, got)), variant
+    # variant 15: the streaming kernel alone (own workspace): the same dh, no scalar outputs
+    dh = torch.full((B,), float("nan"), device=dev)
+    o = torch.zeros(6, dtype=torch.float64, device=dev)
+    ops.surrogate_fwdbwd(h, y, abap[:3], abap[3:], dh=dh, out64=o, variant=15)
+    assert np.array_equal(dh.cpu().numpy(), ref_dh) and not o.any()
+    o = torch.zeros(6, dtype=torch.float64, device=dev)
+    ops.surrogate_fwdbwd(h, y, abap[:3], abap[3:], dh=dh, out64=o)  # the shared workspace is still clean
+    assert np.array_equal(o.cpu().numpy(), ref0)
     sums = torch.zeros(4, dtype=torch.float64, device=dev)
     ops.class_sums(h, y, sums, accumulate=False)  # chunked CLASS_ONLY path
     s = sums.cpu().numpy()
@@ -404,6 +413,72 @@ def test_split_is_stable(dev):
     assert (P, N, nf, other) == ((y == 1).sum(), (y != 1).sum(), 0, 0)
     assert np.array_equal(pos[:P].cpu().numpy(), s[y == 1])
     assert np.array_equal(neg[:N].cpu().numpy(), s[y != 1])
+
+
+@pytest.mark.parametrize("ldtype", [np.int8, np.int32, np.int64])
+def test_compact_positives(dev, ldtype):
+    """Stable positive compaction (labels read once, positives' scores only): same list as
+    s[y == 1], stats = {P, n - P, #non-finite positives, #labels not in {-1, 1}}; ragged sizes
+    around the 16-label groups and the 16384-label tile, misaligned label slices, p = 0 / 1."""
+    from distributedauc_amd import ops
+
+    rng = np.random.default_rng(31)
+    for n, p, off in ((1, 1.0, 0), (15, 0.5, 0), (16, 0.5, 1), (17, 0.3, 0), (16384, 0.01, 0), (16385, 0.0, 0),
+                      (16387, 1.0, 3), (300_001, 0.02, 1), (2_000_003, 0.001, 0), (1 << 20, 0.5, 0)):
+        sall = rng.standard_normal(n + off).astype(np.float32)
+        yall = np.where(rng.random(n + off) < p, 1, -1).astype(ldtype)
+        if n > 100:
+            yall[rng.random(n + off) < 0.003] = 0  # a negative for roc_curve(pos_label=1), counted as "other"
+            sall[rng.integers(0, n + off, 5)] = np.nan
+        ts, ty = T(sall, dev)[off:], T(yall, dev)[off:]
+        s, y = sall[off:], yall[off:]
+        pos, stats = ops.compact_positives(ts, ty)
+        P = int((y == 1).sum())
+        nf = int((~np.isfinite(s[y == 1])).sum())
+        other = int(((y != 1) & (y != -1)).sum())
+        assert stats.cpu().tolist() == [P, n - P, nf, other], (n, p, off)
+        assert np.array_equal(pos[:P].cpu().numpy(), s[y == 1], equal_nan=True), (n, p, off)
+
+
+def test_auc_sort_rejects_nonfinite_negatives(dev):
+    """The sort method never materialises the negatives: the query kernel's finiteness count
+    must still reject a NaN / inf negative (sklearn _ranking.py:868-869), sharded or not."""
+    from distributedauc_amd.auc import ExactAUC
+
+    rng = np.random.default_rng(5)
+    n = 200_003
+    for bad in (np.nan, np.inf, -np.inf):
+        s = rng.random(n, dtype=np.float32)
+        y = np.where(rng.random(n) < 0.01, 1, -1).astype(np.int8)
+        j = int(np.flatnonzero(y == -1)[-7])
+        s[j] = bad
+        with pytest.raises(ValueError):
+            ExactAUC(method="sort")(T(y, dev), T(s, dev))
+        # two shards: only the rank whose slice holds the bad score sees it before the reduce
+        hits = 0
+        for r in range(2):
+            try:
+                ExactAUC(world=2, rank=r, reduce=False, method="sort").counts(T(y, dev), T(s, dev))
+            except ValueError:
+                hits += 1
+        assert hits == 1
+
+
+def test_auc_counts_extreme_configs4(dev):
+    """BASELINE configs[4] at full size: 2^27 fp32 scores at 0.1 % positives, drawn by the
+    bench's own generator (loader.synthetic_scores), both exact methods, bit-exact vs the C
+    oracle's O(n log n) integer counts; sort-method shards over 8 ranks sum to the same."""
+    from distributedauc_amd.auc import ExactAUC
+    from distributedauc_amd.loader import synthetic_scores
+
+    ts, ty = synthetic_scores(1 << 27, 0.001, dev)
+    e = coracle.auc_counts(ty.cpu().numpy().astype(np.int64), ts.cpu().numpy())
+    ref = (e["wins"], e["ties"], e["P"], e["N"])
+    for method in ("sort", "pairs"):
+        c = ExactAUC(method=method).counts(ty, ts)
+        assert (c["wins"], c["ties"], c["P"], c["N"]) == ref, method
+    parts = [ExactAUC(world=8, rank=r, reduce=False).counts(ty, ts) for r in range(8)]
+    assert (sum(c["wins"] for c in parts), sum(c["ties"] for c in parts)) == ref[:2]
 
 
 def test_pair_count_edge_sizes(dev):
