@@ -27,6 +27,8 @@
 //   one 64-bit atomic each.
 //   table = positives: W += M - ub(x), T += ub - lb;  table = negatives: W += lb(x), T += ub - lb.
 
+#include <type_traits>
+
 #include "dauc_internal.h"
 
 namespace dauc {
@@ -118,7 +120,12 @@ __global__ __launch_bounds__(kScanBlock) void scan_add_kernel(unsigned* __restri
     if (i < m) a[i] += sums[blockIdx.x];
 }
 
-template <bool FROM_FLOAT>
+// FUSED_SCAN: offs is the raw digit-major histogram; every workgroup derives its own output
+// offsets from it (its digit's count in the tiles before it + the exclusive scan of the digit
+// totals): a small sort (<= kFusedScanTiles tiles) then needs no scan launches at all.
+constexpr int64_t kFusedScanTiles = 128;
+
+template <bool FROM_FLOAT, bool FUSED_SCAN>
 __global__ __launch_bounds__(kSortThreads) void radix_scatter_kernel(const void* __restrict__ in, int64_t n,
                                                                      int shift,
                                                                      const unsigned* __restrict__ offs,
@@ -127,7 +134,30 @@ __global__ __launch_bounds__(kSortThreads) void radix_scatter_kernel(const void*
     __shared__ unsigned base[kRadix];                       // running output position per digit
     __shared__ unsigned wcnt[kSortThreads / kWave][kRadix];  // per-wave digit counts of a chunk
     const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
-    base[threadIdx.x] = offs[int64_t(threadIdx.x) * ntiles + blockIdx.x];
+    if constexpr (FUSED_SCAN) {
+        static_assert(kSortThreads == kRadix, "one thread per digit");
+        const unsigned* h = offs + int64_t(threadIdx.x) * ntiles;
+        unsigned before = 0, total = 0;
+        for (int64_t b = 0; b < ntiles; ++b) {
+            const unsigned c = h[b];
+            before += b < blockIdx.x ? c : 0u;
+            total += c;
+        }
+        // exclusive scan of the digit totals (Hillis-Steele over the 256 digits, in wcnt[0])
+        unsigned* sc = wcnt[0];
+        sc[threadIdx.x] = total;
+        __syncthreads();
+        for (int d = 1; d < kRadix; d <<= 1) {
+            const unsigned v = threadIdx.x >= d ? sc[threadIdx.x - d] : 0u;
+            __syncthreads();
+            sc[threadIdx.x] += v;
+            __syncthreads();
+        }
+        base[threadIdx.x] = sc[threadIdx.x] - total + before;
+        __syncthreads();
+    } else {
+        base[threadIdx.x] = offs[int64_t(threadIdx.x) * ntiles + blockIdx.x];
+    }
     const unsigned long long lt = lane ? (~0ull >> (64 - lane)) : 0ull;
     const int64_t t0 = int64_t(blockIdx.x) * kTile;
     for (int k = 0; k < kPerThread; ++k) {
@@ -174,6 +204,9 @@ __global__ __launch_bounds__(kSortThreads) void radix_scatter_kernel(const void*
 #ifndef DAUC_QUERY_BLOCKS_PER_CU
 #define DAUC_QUERY_BLOCKS_PER_CU 1
 #endif
+#ifndef DAUC_ABLATE
+#define DAUC_ABLATE 0  // timing ablations only (wrong counts): 1 = no bucket load, 2 = no tree walk
+#endif
 #ifndef DAUC_QUERY_LOCKSTEP
 #define DAUC_QUERY_LOCKSTEP 0  // 0: by bucket size (lockstep_queries), else 1 / 2 / 4 keys in lockstep
 #endif
@@ -181,44 +214,133 @@ __global__ __launch_bounds__(kSortThreads) void radix_scatter_kernel(const void*
 // (4 B each: 40000 -> 156 KB of the CU's 160 KB), so a bucket holds k <= 4 keys -- ONE 16-byte
 // load -- up to M = 160,000 table keys (2^27 scores at 0.1 % positives: M = 134,447 -> k = 4).
 constexpr int kMaxSplit = DAUC_QUERY_MAX_SPLIT;
-constexpr size_t kTreeBytes = size_t(kMaxSplit) * 4;
+constexpr size_t kTreeBytes = (size_t(kMaxSplit) + 64) * 4;  // nodes of 4 keys + per-level padding nodes
 constexpr int kQueryThreads = 1024;
 constexpr unsigned kPadKey = 0xffffffffu;  // above every finite score's key (max 0xff7fffff)
 
-// The S splitters form the in-order ranks of a perfect BFS tree of height h (2^(h-1) <= S <
-// 2^h): node (depth d, position p) has rank ((2p + 1) << (h - 1 - d)) - 1; nodes whose rank is
-// >= S are padding (+inf) and form a suffix of every level, so only the first
-// level_nodes(S, h, d) nodes of each level are stored, level after level: S words in all.
-__host__ __device__ __forceinline__ int level_nodes(int S, int h, int d) { return ((S >> (h - 1 - d)) + 1) >> 1; }
+// The S splitters are the in-order keys of a perfect 5-ary search tree of height H (5^(H-1) <= S
+// + 1 <= 5^H): a node is 4 keys (16 B, one ds_read_b128) and routes a query to child
+// #(keys <= x), so a walk is H <= 7 dependent LDS reads (a binary tree needs ~16). Key i of node
+// j on level d has in-order rank (5j + i + 1) * 5^(H-1-d) - 1; keys of rank >= S are padding
+// (+inf). The nodes holding at least one real key form a prefix of every level (n_d nodes),
+// stored level after level and followed by ONE all-padding node: a walk at position p of level
+// d reads node off_d + min(p, n_d), and p <- 5p + #(node keys <= x); after H levels p =
+// #splitters <= x. The sorted table is padded with kPadKey to a whole number of buckets.
+#ifndef DAUC_TREE_ARITY
+#define DAUC_TREE_ARITY 5
+#endif
+constexpr int kTreeArity = DAUC_TREE_ARITY;      // 3: 2-key nodes (ds_read_b64), 5: 4-key nodes (ds_read_b128)
+static_assert(kTreeArity == 3 || kTreeArity == 5, "tree nodes are 8 or 16 bytes");
+constexpr int kNodeKeys = kTreeArity - 1;
+constexpr int kMaxTreeH = kTreeArity == 5 ? 7 : 10;  // 5^7 - 1, 3^10 - 1 >= kMaxSplit
+static_assert(kMaxSplit <= (kTreeArity == 5 ? 78124 : 59048), "tree height bound");
+typedef typename std::conditional<kTreeArity == 5, uint4, uint2>::type TreeNode;
 
-__global__ __launch_bounds__(256) void build_tree_kernel(const unsigned* __restrict__ sorted, int k, int S, int h,
-                                                         unsigned* __restrict__ tree) {
-    const int c = blockIdx.x * 256 + threadIdx.x;
-    if (c >= S) return;
-    int d = 0, off = 0;
-    while (c >= off + level_nodes(S, h, d)) off += level_nodes(S, h, d++);
-    const int r = ((2 * (c - off) + 1) << (h - 1 - d)) - 1;  // in-order rank (< S)
-    tree[c] = sorted[int64_t(r) * k];
+struct TreeGeom {
+    int S, H;
+    int nd[kMaxTreeH];   // stored real nodes of level d
+    int off[kMaxTreeH];  // first node of level d
+    int nodes;           // total stored nodes (incl. the per-level padding nodes)
+};
+
+TreeGeom tree_geom(int S) {
+    TreeGeom g{};
+    g.S = S;
+    int64_t pw = 1;
+    g.H = 0;
+    while (pw * kTreeArity - 1 < S) {
+        pw *= kTreeArity;
+        ++g.H;
+    }
+    ++g.H;  // A^(H-1) <= S + 1 <= A^H
+    int off = 0;
+    int64_t div = pw;  // A^(H-1-d)
+    for (int d = 0; d < g.H; ++d) {
+        const int64_t t = S / div;
+        g.nd[d] = static_cast<int>((t + kTreeArity - 1) / kTreeArity);  // j with A j + 1 <= t
+        g.off[d] = off;
+        off += g.nd[d] + 1;
+        div /= kTreeArity;
+    }
+    g.nodes = off;
+    return g;
 }
 
-// Q walks of the tree in lockstep: i[q] ends as 2^h + #splitters <= x[q]. The level geometry is
-// wave-uniform (scalar registers); a position past the stored prefix of its level is padding.
-template <int Q>
-__device__ __forceinline__ void tree_walk(const unsigned (&x)[Q], unsigned (&i)[Q], const unsigned* __restrict__ tree,
-                                          int S, int h) {
+__device__ __forceinline__ void store_node(uint4* t, int64_t c, const unsigned (&k)[4]) { t[c] = uint4{k[0], k[1], k[2], k[3]}; }
+__device__ __forceinline__ void store_node(uint2* t, int64_t c, const unsigned (&k)[4]) { t[c] = uint2{k[0], k[1]}; }
+
+__global__ __launch_bounds__(256) void build_tree_kernel(unsigned* __restrict__ sorted, int64_t M, int64_t pad, int k,
+                                                         TreeGeom g, TreeNode* __restrict__ tree) {
+    const int64_t c = int64_t(blockIdx.x) * 256 + threadIdx.x;
+    if (c < g.nodes) {
+        int d = 0;
+        while (d + 1 < g.H && c >= g.off[d + 1]) ++d;
+        const int j = static_cast<int>(c) - g.off[d];
+        int64_t pw = 1;
+        for (int e = d + 1; e < g.H; ++e) pw *= kTreeArity;
+        unsigned key[4] = {kPadKey, kPadKey, kPadKey, kPadKey};
 #pragma unroll
-    for (int q = 0; q < Q; ++q) i[q] = 1;
-    int off = 0;
-    for (int d = 0; d < h; ++d) {
-        const unsigned nd = static_cast<unsigned>(level_nodes(S, h, d)), lvl = 1u << d;
-#pragma unroll
-        for (int q = 0; q < Q; ++q) {
-            const unsigned p = i[q] - lvl;
-            const bool in = p < nd;
-            const unsigned v = tree[off + (in ? p : nd - 1)];
-            i[q] = 2 * i[q] + ((in ? v : kPadKey) <= x[q]);
+        for (int i = 0; i < kNodeKeys; ++i) {
+            const int64_t r = (int64_t(kTreeArity) * j + i + 1) * pw - 1;  // in-order rank
+            key[i] = (j < g.nd[d] && r < g.S) ? sorted[r * k] : kPadKey;
         }
-        off += static_cast<int>(nd);
+        store_node(tree, c, key);
+    }
+    // keys M .. S*k of the last bucket: +inf, so bucket compares need no bounds
+    if (c < pad) sorted[M + c] = kPadKey;
+}
+
+// p <- A p + #(node keys <= x): the compares' carries feed the adds.
+__device__ __forceinline__ unsigned tree_step(unsigned p, uint4 n, unsigned x) {
+    unsigned r = p * 5u;
+    asm("v_cmp_le_u32_e32 vcc, %1, %5\n\t"
+        "v_addc_co_u32_e32 %0, vcc, 0, %0, vcc\n\t"
+        "v_cmp_le_u32_e32 vcc, %2, %5\n\t"
+        "v_addc_co_u32_e32 %0, vcc, 0, %0, vcc\n\t"
+        "v_cmp_le_u32_e32 vcc, %3, %5\n\t"
+        "v_addc_co_u32_e32 %0, vcc, 0, %0, vcc\n\t"
+        "v_cmp_le_u32_e32 vcc, %4, %5\n\t"
+        "v_addc_co_u32_e32 %0, vcc, 0, %0, vcc"
+        : "+v"(r)
+        : "v"(n.x), "v"(n.y), "v"(n.z), "v"(n.w), "v"(x)
+        : "vcc");
+    return r;
+}
+
+__device__ __forceinline__ unsigned tree_step(unsigned p, uint2 n, unsigned x) {
+    unsigned r = p * 3u;
+    asm("v_cmp_le_u32_e32 vcc, %1, %3\n\t"
+        "v_addc_co_u32_e32 %0, vcc, 0, %0, vcc\n\t"
+        "v_cmp_le_u32_e32 vcc, %2, %3\n\t"
+        "v_addc_co_u32_e32 %0, vcc, 0, %0, vcc"
+        : "+v"(r)
+        : "v"(n.x), "v"(n.y), "v"(x)
+        : "vcc");
+    return r;
+}
+
+// Q walks of the tree in lockstep: p[q] ends as #splitters <= x[q]. The level geometry is
+// wave-uniform (kernel arguments, scalar registers).
+template <int Q>
+__device__ __forceinline__ void tree_walk(const unsigned (&x)[Q], unsigned (&p)[Q], const TreeNode* __restrict__ tree,
+                                          const TreeGeom& g) {
+#pragma unroll
+    for (int q = 0; q < Q; ++q) p[q] = 0;
+    if (DAUC_ABLATE == 2) {
+#pragma unroll
+        for (int q = 0; q < Q; ++q) p[q] = (x[q] * 2654435761u) % static_cast<unsigned>(g.S);
+        return;
+    }
+#pragma unroll
+    for (int d = 0; d < kMaxTreeH; ++d) {
+        if (d < g.H) {
+            const unsigned nd = static_cast<unsigned>(g.nd[d]), off = static_cast<unsigned>(g.off[d]);
+            TreeNode v[Q];
+#pragma unroll
+            for (int q = 0; q < Q; ++q) v[q] = tree[off + (p[q] < nd ? p[q] : nd)];
+#pragma unroll
+            for (int q = 0; q < Q; ++q) p[q] = tree_step(p[q], v[q], x[q]);
+        }
     }
 }
 
@@ -227,6 +349,11 @@ __device__ __forceinline__ void tree_walk(const unsigned (&x)[Q], unsigned (&i)[
 template <int K>
 __device__ __forceinline__ void bucket_counts(const unsigned* __restrict__ sorted, int64_t M, int64_t b,
                                               unsigned x, int& le, int& lt, unsigned& first) {
+    if (DAUC_ABLATE == 1) {
+        le = lt = static_cast<int>(b & 3);
+        first = 0;
+        return;
+    }
     const int64_t base = b * K;
     unsigned v[K];
     if constexpr (K >= 4) {
@@ -249,10 +376,9 @@ __device__ __forceinline__ void bucket_counts(const unsigned* __restrict__ sorte
     le = 0;
     lt = 0;
 #pragma unroll
-    for (int j = 0; j < K; ++j) {
-        const bool in = base + j < M;  // the tail bucket reads past M inside the workspace
-        le += in && v[j] <= x;
-        lt += in && v[j] < x;
+    for (int j = 0; j < K; ++j) {  // the tail bucket is padded with kPadKey (> every finite key)
+        le += v[j] <= x;
+        lt += v[j] < x;
     }
 }
 
@@ -275,18 +401,17 @@ __device__ __forceinline__ int64_t count_below(const unsigned* __restrict__ a, i
 
 // One query (K = 0: buckets of k > 32 keys, finished by binary searches in global memory).
 template <int K, bool TABLE_POS>
-__device__ __forceinline__ void count_query(unsigned x, const unsigned* __restrict__ tree, int S, int h, int k,
+__device__ __forceinline__ void count_query(unsigned x, const TreeNode* __restrict__ tree, const TreeGeom& g, int k,
                                             const unsigned* __restrict__ sorted, int64_t M,
                                             unsigned long long& w, unsigned long long& t) {
     // splitters <= x (walk 0) and < x = <= x - 1 (walk 1; finite keys are >= 0x00800000, so
     // x - 1 never wraps)
-    const int64_t leaves = int64_t(1) << h;
     int64_t ub = 0, lb = 0;
     if constexpr (K <= 1) {
         const unsigned xs[2] = {x, x - 1u};
         unsigned i[2];
-        tree_walk<2>(xs, i, tree, S, h);
-        const int64_t su = int64_t(i[0]) - leaves, sl = int64_t(i[1]) - leaves;
+        tree_walk<2>(xs, i, tree, g);
+        const int64_t su = i[0], sl = i[1];
         if constexpr (K == 1) {
             ub = su;
             lb = sl;
@@ -305,8 +430,8 @@ __device__ __forceinline__ void count_query(unsigned x, const unsigned* __restri
         // equals x (a run of x may then start in an earlier bucket)
         const unsigned xs[1] = {x};
         unsigned i[1];
-        tree_walk<1>(xs, i, tree, S, h);
-        const int64_t su = int64_t(i[0]) - leaves;
+        tree_walk<1>(xs, i, tree, g);
+        const int64_t su = i[0];
         if (su > 0) {
             int le = 0, lt = 0;
             unsigned first = 0;
@@ -316,8 +441,8 @@ __device__ __forceinline__ void count_query(unsigned x, const unsigned* __restri
                 lb = (su - 1) * K + lt;
             } else {
                 const unsigned xm[1] = {x - 1u};
-                tree_walk<1>(xm, i, tree, S, h);
-                const int64_t sl = int64_t(i[0]) - leaves;
+                tree_walk<1>(xm, i, tree, g);
+                const int64_t sl = i[0];
                 if (sl > 0) {
                     bucket_counts<K>(sorted, M, sl - 1, x, le, lt, first);
                     lb = (sl - 1) * K + lt;
@@ -339,11 +464,10 @@ constexpr int lockstep_queries() {
 
 template <int K, int Q, bool TABLE_POS>
 __device__ __forceinline__ void count_queries(const unsigned (&x)[Q], const bool (&use)[Q],
-                                              const unsigned* __restrict__ tree, int S, int h,
+                                              const TreeNode* __restrict__ tree, const TreeGeom& g,
                                               const unsigned* __restrict__ sorted, int64_t M,
                                               unsigned long long& w, unsigned long long& t) {
     static_assert(K >= 1 && K <= 32, "bucketed lockstep walk");
-    const int64_t leaves = int64_t(1) << h;
     if constexpr (K == 1) {
         // the tree holds every key: splitters <= x and <= x - 1 directly
         unsigned xs[2 * Q], i[2 * Q];
@@ -352,24 +476,24 @@ __device__ __forceinline__ void count_queries(const unsigned (&x)[Q], const bool
             xs[q] = x[q];
             xs[Q + q] = x[q] - 1u;
         }
-        tree_walk<2 * Q>(xs, i, tree, S, h);
+        tree_walk<2 * Q>(xs, i, tree, g);
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
             if (!use[q]) continue;
-            const int64_t ub = int64_t(i[q]) - leaves, lb = int64_t(i[Q + q]) - leaves;
+            const int64_t ub = i[q], lb = i[Q + q];
             w += TABLE_POS ? static_cast<unsigned long long>(M - ub) : static_cast<unsigned long long>(lb);
             t += static_cast<unsigned long long>(ub - lb);
         }
     } else {
         unsigned i[Q];
-        tree_walk<Q>(x, i, tree, S, h);
+        tree_walk<Q>(x, i, tree, g);
         // every bucket load issued before any is examined (su = 0: bucket 0 is read, unused)
         int le[Q], lt[Q];
         unsigned first[Q];
         int64_t su[Q];
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
-            su[q] = int64_t(i[q]) - leaves;
+            su[q] = i[q];
             bucket_counts<K>(sorted, M, su[q] > 0 ? su[q] - 1 : 0, x[q], le[q], lt[q], first[q]);
         }
 #pragma unroll
@@ -384,8 +508,8 @@ __device__ __forceinline__ void count_queries(const unsigned (&x)[Q], const bool
                     // the bucket starts with x: a run of x may begin in an earlier bucket (rare)
                     const unsigned xm[1] = {x[q] - 1u};
                     unsigned j[1];
-                    tree_walk<1>(xm, j, tree, S, h);
-                    const int64_t sl = int64_t(j[0]) - leaves;
+                    tree_walk<1>(xm, j, tree, g);
+                    const int64_t sl = j[0];
                     if (sl > 0) {
                         int le2 = 0, lt2 = 0;
                         unsigned f2 = 0;
@@ -403,36 +527,36 @@ __device__ __forceinline__ void count_queries(const unsigned (&x)[Q], const bool
 // Four keys (one float4 slot) with per-key use flags, through count_queries in groups of Q
 // (K = 0, buckets > 32 keys finished in global memory: one key at a time).
 template <int K, bool TABLE_POS>
-__device__ __forceinline__ void count4(const unsigned (&x)[4], const bool (&use)[4], const unsigned* __restrict__ tree,
-                                       int S, int h, int k, const unsigned* __restrict__ sorted, int64_t M,
+__device__ __forceinline__ void count4(const unsigned (&x)[4], const bool (&use)[4], const TreeNode* __restrict__ tree,
+                                       const TreeGeom& g, int k, const unsigned* __restrict__ sorted, int64_t M,
                                        unsigned long long& w, unsigned long long& t) {
     if constexpr (K == 0) {
 #pragma unroll
         for (int q = 0; q < 4; ++q)
-            if (use[q]) count_query<0, TABLE_POS>(x[q], tree, S, h, k, sorted, M, w, t);
+            if (use[q]) count_query<0, TABLE_POS>(x[q], tree, g, k, sorted, M, w, t);
     } else {
         constexpr int Q = lockstep_queries<K>();
 #pragma unroll
-        for (int g = 0; g < 4; g += Q) {
+        for (int b = 0; b < 4; b += Q) {
             unsigned xs[Q];
             bool us[Q];
 #pragma unroll
             for (int q = 0; q < Q; ++q) {
-                xs[q] = x[g + q];
-                us[q] = use[g + q];
+                xs[q] = x[b + q];
+                us[q] = use[b + q];
             }
-            count_queries<K, Q, TABLE_POS>(xs, us, tree, S, h, sorted, M, w, t);
+            count_queries<K, Q, TABLE_POS>(xs, us, tree, g, sorted, M, w, t);
         }
     }
 }
 
 template <int K, bool TABLE_POS>
 __global__ __launch_bounds__(kQueryThreads) void query_count_kernel(const float* __restrict__ q, int64_t L,
-                                                                   const unsigned* __restrict__ gtree, int S, int h,
+                                                                   const TreeNode* __restrict__ gtree, TreeGeom g,
                                                                    int k, const unsigned* __restrict__ sorted,
                                                                    int64_t M, unsigned long long* __restrict__ out) {
-    extern __shared__ unsigned tree[];
-    for (int i = threadIdx.x; i < S; i += kQueryThreads) tree[i] = gtree[i];
+    extern __shared__ TreeNode tree[];
+    for (int i = threadIdx.x; i < g.nodes; i += kQueryThreads) tree[i] = gtree[i];
     __syncthreads();
     unsigned long long w = 0, t = 0;
     const bool vec = (reinterpret_cast<uintptr_t>(q) & 15u) == 0;
@@ -442,10 +566,10 @@ __global__ __launch_bounds__(kQueryThreads) void query_count_kernel(const float*
     for (int64_t v = int64_t(blockIdx.x) * kQueryThreads + threadIdx.x; v < nvec; v += stride) {
         const f32x4 f = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(q) + v);
         const unsigned x[4] = {key_of(f.x), key_of(f.y), key_of(f.z), key_of(f.w)};
-        count4<K, TABLE_POS>(x, all, tree, S, h, k, sorted, M, w, t);
+        count4<K, TABLE_POS>(x, all, tree, g, k, sorted, M, w, t);
     }
     for (int64_t i = nvec * 4 + int64_t(blockIdx.x) * kQueryThreads + threadIdx.x; i < L; i += stride)
-        count_query<K, TABLE_POS>(key_of(q[i]), tree, S, h, k, sorted, M, w, t);
+        count_query<K, TABLE_POS>(key_of(q[i]), tree, g, k, sorted, M, w, t);
     __shared__ unsigned long long red[2][kQueryThreads / kWave];
     w = wave_sum(w);
     t = wave_sum(t);
@@ -495,13 +619,13 @@ __device__ __forceinline__ void label4(const LT* __restrict__ lab, int64_t i, bo
 template <int K, typename LT>
 __global__ __launch_bounds__(kQueryThreads) void query_labeled_kernel(const float* __restrict__ s,
                                                                      const LT* __restrict__ lab, int64_t begin,
-                                                                     int64_t end, const unsigned* __restrict__ gtree,
-                                                                     int S, int h, int k,
+                                                                     int64_t end, const TreeNode* __restrict__ gtree,
+                                                                     TreeGeom g, int k,
                                                                      const unsigned* __restrict__ sorted,
                                                                      int64_t M, unsigned long long* __restrict__ out,
                                                                      unsigned long long* __restrict__ nonfinite) {
-    extern __shared__ unsigned tree[];
-    for (int i = threadIdx.x; i < S; i += kQueryThreads) tree[i] = gtree[i];
+    extern __shared__ TreeNode tree[];
+    for (int i = threadIdx.x; i < g.nodes; i += kQueryThreads) tree[i] = gtree[i];
     __syncthreads();
     unsigned long long w = 0, t = 0;
     unsigned nf = 0;
@@ -513,39 +637,97 @@ __global__ __launch_bounds__(kQueryThreads) void query_labeled_kernel(const floa
     for (int64_t i = begin + tid; i < head; i += stride) {
         if (lab[i] != LT(1)) {
             nf += !isfinite(s[i]);
-            count_query<K, true>(key_of(s[i]), tree, S, h, k, sorted, M, w, t);
+            count_query<K, true>(key_of(s[i]), tree, g, k, sorted, M, w, t);
         }
     }
     const int64_t nvec = end > head ? (end - head) / 4 : 0;
     const bool aligned = (reinterpret_cast<uintptr_t>(s + head) & 15u) == 0 &&
                          (reinterpret_cast<uintptr_t>(lab + head) & (4 * sizeof(LT) - 1)) == 0;
-    for (int64_t v = tid; v < nvec; v += stride) {
-        const int64_t i = head + v * 4;
-        float f[4];
-        if (aligned) {
-            const f32x4 x = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(s + i));
-            f[0] = x.x;
-            f[1] = x.y;
-            f[2] = x.z;
-            f[3] = x.w;
-        } else {
+    if (aligned) {
+        // U float4 slots (4 queries each) per iteration, and the NEXT iteration's loads issued
+        // before this one's walks: each walk is a chain of dependent LDS reads and a bucket load,
+        // so without this the stream's HBM latency sits between every two iterations of a wave.
+        constexpr int U = sizeof(LT) == 8 ? 2 : 4;
+        f32x4 fc[U], fn[U];
+        LT lc[U][4], ln[U][4];
+        auto load = [&](int64_t v0, f32x4 (&f)[U], LT (&l)[U][4]) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int64_t v = v0 + int64_t(u) * stride;
+                if (v < nvec) {
+                    const int64_t i = head + v * 4;
+                    f[u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(s + i));
+                    if constexpr (sizeof(LT) == 1) {
+                        const char4 c = *reinterpret_cast<const char4*>(lab + i);
+                        l[u][0] = c.x;
+                        l[u][1] = c.y;
+                        l[u][2] = c.z;
+                        l[u][3] = c.w;
+                    } else if constexpr (sizeof(LT) == 4) {
+                        const int4 c = *reinterpret_cast<const int4*>(lab + i);
+                        l[u][0] = c.x;
+                        l[u][1] = c.y;
+                        l[u][2] = c.z;
+                        l[u][3] = c.w;
+                    } else {
+                        const longlong2 c0 = reinterpret_cast<const longlong2*>(lab + i)[0];
+                        const longlong2 c1 = reinterpret_cast<const longlong2*>(lab + i)[1];
+                        l[u][0] = c0.x;
+                        l[u][1] = c0.y;
+                        l[u][2] = c1.x;
+                        l[u][3] = c1.y;
+                    }
+                } else {
+                    f[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) l[u][q] = LT(1);  // past the end: no query
+                }
+            }
+        };
+        load(tid, fc, lc);
+        for (int64_t v0 = tid; v0 < nvec; v0 += int64_t(U) * stride) {
+            load(v0 + int64_t(U) * stride, fn, ln);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const float f[4] = {fc[u].x, fc[u].y, fc[u].z, fc[u].w};
+                bool neg[4];
+                unsigned x[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    neg[q] = lc[u][q] != LT(1);
+                    x[q] = key_of(f[q]);
+                    nf += neg[q] && !isfinite(f[q]);
+                }
+                count4<K, true>(x, neg, tree, g, k, sorted, M, w, t);
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                fc[u] = fn[u];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) lc[u][q] = ln[u][q];
+            }
+        }
+    } else {
+        for (int64_t v = tid; v < nvec; v += stride) {
+            const int64_t i = head + v * 4;
+            float f[4];
 #pragma unroll
             for (int q = 0; q < 4; ++q) f[q] = s[i + q];
-        }
-        bool neg[4];
-        label4(lab, i, aligned, end, neg);
-        unsigned x[4];
+            bool neg[4];
+            label4(lab, i, false, end, neg);
+            unsigned x[4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            x[q] = key_of(f[q]);
-            nf += neg[q] && !isfinite(f[q]);
+            for (int q = 0; q < 4; ++q) {
+                x[q] = key_of(f[q]);
+                nf += neg[q] && !isfinite(f[q]);
+            }
+            count4<K, true>(x, neg, tree, g, k, sorted, M, w, t);
         }
-        count4<K, true>(x, neg, tree, S, h, k, sorted, M, w, t);
     }
     for (int64_t i = head + nvec * 4 + tid; i < end; i += stride) {
         if (lab[i] != LT(1)) {
             nf += !isfinite(s[i]);
-            count_query<K, true>(key_of(s[i]), tree, S, h, k, sorted, M, w, t);
+            count_query<K, true>(key_of(s[i]), tree, g, k, sorted, M, w, t);
         }
     }
     __shared__ unsigned long long red[3][kQueryThreads / kWave];
@@ -589,12 +771,12 @@ int query_grid(int64_t L) {
 }
 
 template <bool TABLE_POS>
-int launch_query(int k, const float* q, int64_t L, const unsigned* tree, int S, int h, const unsigned* sorted,
+int launch_query(int k, const float* q, int64_t L, const TreeNode* tree, const TreeGeom& g, const unsigned* sorted,
                  int64_t M, unsigned long long* out, hipStream_t st) {
     const dim3 grid(query_grid(L)), block(kQueryThreads);
-    const size_t lds = size_t(S) * 4;
+    const size_t lds = size_t(g.nodes) * sizeof(TreeNode);
 #define DAUC_QC(KV) \
-    hipLaunchKernelGGL((query_count_kernel<KV, TABLE_POS>), grid, block, lds, st, q, L, tree, S, h, k, sorted, M, out)
+    hipLaunchKernelGGL((query_count_kernel<KV, TABLE_POS>), grid, block, lds, st, q, L, tree, g, k, sorted, M, out)
     switch (k) {
         case 1: DAUC_QC(1); break;
         case 2: DAUC_QC(2); break;
@@ -627,8 +809,8 @@ SortWs carve(void* ws, int64_t n) {
         p += ((count * 4 + 255) / 256) * 256;
         return r;
     };
-    w.keys_a = take(n);
-    w.keys_b = take(n);
+    w.keys_a = take(n + 64);  // + room for the last bucket's kPadKey tail
+    w.keys_b = take(n + 64);
     w.hist = take(w.m);
     w.sums = take(w.nsum);
     return w;
@@ -637,7 +819,7 @@ SortWs carve(void* ws, int64_t n) {
 size_t sort_ws_bytes(int64_t n) {
     const int64_t nt = tiles_for(n), m = int64_t(kRadix) * nt, ns = (m + kScanBlock - 1) / kScanBlock;
     auto rnd = [](int64_t c) { return ((c * 4 + 255) / 256) * 256; };
-    return static_cast<size_t>(rnd(n) * 2 + rnd(m) + rnd(ns));
+    return static_cast<size_t>(rnd(n + 64) * 2 + rnd(m) + rnd(ns));
 }
 
 // Sorts the keys of neg[0..N) into the workspace; returns the sorted array.
@@ -652,20 +834,30 @@ int radix_sort_keys(const float* neg, int64_t N, const SortWs& w, hipStream_t st
         else
             hipLaunchKernelGGL(radix_hist_kernel<false>, dim3(w.ntiles), dim3(kSortThreads), 0, st,
                                static_cast<const void*>(src), N, shift, w.hist, w.ntiles);
-        if (w.m <= kSingleScan) {
-            // small sorts are launch-bound: one workgroup scans the whole histogram array
-            hipLaunchKernelGGL(scan_sums_kernel, dim3(1), dim3(kScanBlock), 0, st, w.hist, w.m);
+        const void* in = pass == 0 ? static_cast<const void*>(neg) : static_cast<const void*>(src);
+        if (w.ntiles <= kFusedScanTiles) {
+            // small sorts are launch-bound: the scatter workgroups scan the histogram themselves
+            if (pass == 0)
+                hipLaunchKernelGGL((radix_scatter_kernel<true, true>), dim3(w.ntiles), dim3(kSortThreads), 0, st,
+                                   in, N, shift, w.hist, w.ntiles, dst);
+            else
+                hipLaunchKernelGGL((radix_scatter_kernel<false, true>), dim3(w.ntiles), dim3(kSortThreads), 0, st,
+                                   in, N, shift, w.hist, w.ntiles, dst);
         } else {
-            hipLaunchKernelGGL(scan_blocks_kernel, dim3(w.nsum), dim3(kScanBlock), 0, st, w.hist, w.m, w.sums);
-            hipLaunchKernelGGL(scan_sums_kernel, dim3(1), dim3(kScanBlock), 0, st, w.sums, w.nsum);
-            hipLaunchKernelGGL(scan_add_kernel, dim3(w.nsum), dim3(kScanBlock), 0, st, w.hist, w.m, w.sums);
+            if (w.m <= kSingleScan) {
+                hipLaunchKernelGGL(scan_sums_kernel, dim3(1), dim3(kScanBlock), 0, st, w.hist, w.m);
+            } else {
+                hipLaunchKernelGGL(scan_blocks_kernel, dim3(w.nsum), dim3(kScanBlock), 0, st, w.hist, w.m, w.sums);
+                hipLaunchKernelGGL(scan_sums_kernel, dim3(1), dim3(kScanBlock), 0, st, w.sums, w.nsum);
+                hipLaunchKernelGGL(scan_add_kernel, dim3(w.nsum), dim3(kScanBlock), 0, st, w.hist, w.m, w.sums);
+            }
+            if (pass == 0)
+                hipLaunchKernelGGL((radix_scatter_kernel<true, false>), dim3(w.ntiles), dim3(kSortThreads), 0, st,
+                                   in, N, shift, w.hist, w.ntiles, dst);
+            else
+                hipLaunchKernelGGL((radix_scatter_kernel<false, false>), dim3(w.ntiles), dim3(kSortThreads), 0, st,
+                                   in, N, shift, w.hist, w.ntiles, dst);
         }
-        if (pass == 0)
-            hipLaunchKernelGGL(radix_scatter_kernel<true>, dim3(w.ntiles), dim3(kSortThreads), 0, st,
-                               static_cast<const void*>(neg), N, shift, w.hist, w.ntiles, dst);
-        else
-            hipLaunchKernelGGL(radix_scatter_kernel<false>, dim3(w.ntiles), dim3(kSortThreads), 0, st,
-                               static_cast<const void*>(src), N, shift, w.hist, w.ntiles, dst);
         const int rc = launch_status();
         if (rc) return rc;
         src = dst;
@@ -676,13 +868,13 @@ int radix_sort_keys(const float* neg, int64_t N, const SortWs& w, hipStream_t st
 }
 
 template <typename LT>
-int launch_labeled(int k, const float* s, const LT* lab, int64_t begin, int64_t end, const unsigned* tree, int S,
-                   int h, const unsigned* sorted, int64_t M, unsigned long long* out, unsigned long long* nonfinite,
+int launch_labeled(int k, const float* s, const LT* lab, int64_t begin, int64_t end, const TreeNode* tree,
+                   const TreeGeom& g, const unsigned* sorted, int64_t M, unsigned long long* out, unsigned long long* nonfinite,
                    hipStream_t st) {
     const dim3 grid(query_grid(end - begin)), block(kQueryThreads);
-    const size_t lds = size_t(S) * 4;
+    const size_t lds = size_t(g.nodes) * sizeof(TreeNode);
 #define DAUC_QL(KV)                                                                                              \
-    hipLaunchKernelGGL((query_labeled_kernel<KV, LT>), grid, block, lds, st, s, lab, begin, end, tree, S, h, k, \
+    hipLaunchKernelGGL((query_labeled_kernel<KV, LT>), grid, block, lds, st, s, lab, begin, end, tree, g, k, \
                        sorted, M, out, nonfinite)
     switch (k) {
         case 1: DAUC_QL(1); break;
@@ -699,20 +891,23 @@ int launch_labeled(int k, const float* s, const LT* lab, int64_t begin, int64_t 
 
 // sort the table, build the tree; returns the tree pointer and geometry
 int prepare_table(const float* table, int64_t M, void* workspace, hipStream_t st, const unsigned** sorted,
-                  unsigned** tree, int* k_out, int* S_out, int* h_out) {
+                  TreeNode** tree, int* k_out, TreeGeom* g_out) {
     SortWs w = carve(workspace, M);
     int rc = radix_sort_keys(table, M, w, st, sorted);
     if (rc) return rc;
     int k = 1;
     while ((M + k - 1) / k > kMaxSplit) k *= 2;
     const int S = static_cast<int>((M + k - 1) / k);
-    int h = 1;
-    while ((1 << h) - 1 < S) ++h;
-    *tree = reinterpret_cast<unsigned*>(static_cast<char*>(workspace) + ((sort_ws_bytes(M) + 255) / 256) * 256);
-    hipLaunchKernelGGL(build_tree_kernel, dim3((S + 255) / 256), dim3(256), 0, st, *sorted, k, S, h, *tree);
+    const TreeGeom g = tree_geom(S);
+    *tree = reinterpret_cast<TreeNode*>(static_cast<char*>(workspace) + ((sort_ws_bytes(M) + 255) / 256) * 256);
+    // buckets of <= 32 keys are read whole (one vector load), so their tail is padded; larger
+    // ones are binary-searched with bounds (k - 1 < 64 keys of slack in the sort workspace)
+    const int64_t pad = k <= 32 ? int64_t(S) * k - M : 0;
+    const int64_t nthreads = (g.nodes > pad) ? g.nodes : pad;
+    hipLaunchKernelGGL(build_tree_kernel, dim3(static_cast<unsigned>((nthreads + 255) / 256)), dim3(256), 0, st,
+                       const_cast<unsigned*>(*sorted), M, pad, k, g, *tree);
     *k_out = k;
-    *S_out = S;
-    *h_out = h;
+    *g_out = g;
     return launch_status();
 }
 
@@ -751,13 +946,14 @@ int dauc_auc_counts_sorted(const float* pos, int64_t P, const float* neg, int64_
     if (workspace == nullptr || workspace_bytes < dauc_sort_workspace_size(M) || M > 0xffffffffLL) return DAUC_EINVAL;
     hipStream_t st = as_hip(stream);
     const unsigned* sorted = nullptr;
-    unsigned* tree = nullptr;
-    int k = 1, S = 1, h = 1;
-    int rc = prepare_table(table_pos ? pos : neg, M, workspace, st, &sorted, &tree, &k, &S, &h);
+    TreeNode* tree = nullptr;
+    int k = 1;
+    TreeGeom g{};
+    int rc = prepare_table(table_pos ? pos : neg, M, workspace, st, &sorted, &tree, &k, &g);
     if (rc) return rc;
     const float* q = table_pos ? neg : pos;
-    return table_pos ? launch_query<true>(k, q, L, tree, S, h, sorted, M, wins_ties, st)
-                     : launch_query<false>(k, q, L, tree, S, h, sorted, M, wins_ties, st);
+    return table_pos ? launch_query<true>(k, q, L, tree, g, sorted, M, wins_ties, st)
+                     : launch_query<false>(k, q, L, tree, g, sorted, M, wins_ties, st);
 }
 
 int dauc_auc_counts_sorted_labeled(const float* pos, int64_t P, const float* scores, const void* labels,
@@ -773,19 +969,20 @@ int dauc_auc_counts_sorted_labeled(const float* pos, int64_t P, const float* sco
     if (workspace == nullptr || workspace_bytes < dauc_sort_workspace_size(P) || P > 0xffffffffLL) return DAUC_EINVAL;
     hipStream_t st = as_hip(stream);
     const unsigned* sorted = nullptr;
-    unsigned* tree = nullptr;
-    int k = 1, S = 1, h = 1;
-    int rc = prepare_table(pos, P, workspace, st, &sorted, &tree, &k, &S, &h);
+    TreeNode* tree = nullptr;
+    int k = 1;
+    TreeGeom g{};
+    int rc = prepare_table(pos, P, workspace, st, &sorted, &tree, &k, &g);
     if (rc) return rc;
     switch (label_dtype) {
         case DAUC_LABEL_I8:
-            return launch_labeled(k, scores, static_cast<const int8_t*>(labels), begin, end, tree, S, h, sorted, P,
+            return launch_labeled(k, scores, static_cast<const int8_t*>(labels), begin, end, tree, g, sorted, P,
                                   wins_ties, nonfinite, st);
         case DAUC_LABEL_I32:
-            return launch_labeled(k, scores, static_cast<const int32_t*>(labels), begin, end, tree, S, h, sorted, P,
+            return launch_labeled(k, scores, static_cast<const int32_t*>(labels), begin, end, tree, g, sorted, P,
                                   wins_ties, nonfinite, st);
         default:
-            return launch_labeled(k, scores, static_cast<const int64_t*>(labels), begin, end, tree, S, h, sorted, P,
+            return launch_labeled(k, scores, static_cast<const int64_t*>(labels), begin, end, tree, g, sorted, P,
                                   wins_ties, nonfinite, st);
     }
 }

@@ -374,7 +374,11 @@ constexpr int kWaves = kThreads / kWave;          // waves per workgroup
 #endif
 constexpr int64_t kRowsPerChunk = DAUC_SURROGATE_WAVE_ROWS ? kWaves : 1;
 constexpr int kRowWords = 6;                      // s_pos, s_neg, q_pos, q_neg, n_pos, n_neg (fp64)
-constexpr int kRowsPerReduceBlock = 512;          // rows one workgroup of the reduce kernel sums
+#ifndef DAUC_SURROGATE_REDUCE_ROWS
+#define DAUC_SURROGATE_REDUCE_ROWS 512
+#endif
+constexpr int kRowsPerReduceBlock = DAUC_SURROGATE_REDUCE_ROWS;  // rows one workgroup of the reduce kernel sums
+static_assert(kRowsPerReduceBlock % 256 == 0, "whole rows per thread");
 
 __host__ __device__ constexpr int64_t chunk_elems(int S) { return int64_t(kThreads) * kVec * S; }
 

@@ -59,3 +59,21 @@ def test_configs0_cpu_baseline_gloo_workers():
     assert r["workers"] == 2 and r["cores"] == 2 and r["value"] > 0
     assert r["params"] == 11_177_538 and r["params_finite"]
     assert r["averaging_round_ms"] > 0
+
+
+def test_shipped_conv1x1_plans_load():
+    """The shipped engine plan (measured once on MI355X) parses into fixed choices for the bench
+    shapes, so no rank times engines at run time for them."""
+    from distributedauc_amd import conv1x1 as C
+
+    saved = dict(C.plans)
+    try:
+        C.plans.clear()
+        C._load_plans()
+        assert len(C.plans) >= 30
+        key = (200704, 512, 128, __import__("torch").bfloat16, "dgrad_acc")  # ResNet-50 layer1 conv1 + skip
+        assert key in C.plans
+        assert all(v in ("gemm", "conv") or v.startswith("gemm") for v in C.plans.values())
+    finally:
+        C.plans.clear()
+        C.plans.update(saved)
