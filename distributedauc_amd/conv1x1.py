@@ -156,20 +156,31 @@ def _dgrad(gy, g2, x, wc):
 
 
 def _dgrad_acc(base, gy, g2, x, wc):
-    """base + dy @ W (base: a channels-last tensor shaped like x). GEMM engine: ONE GEMM launch with
-    beta = 1 (reads base once, writes the sum once, one rounding) instead of a dgrad output plus
-    autograd's separate add pass (read 2, write 1). The sum goes to a NEW tensor (C and D of the
-    GEMM never alias), so no engine or tuned solution ever sees an in-place C == D operand."""
+    """base += dy @ W in place (base: a channels-last tensor shaped like x that this backward owns).
+    GEMM engine: one launch with beta = 1 (reads base once, writes it once, one rounding), instead
+    of a dgrad output plus autograd's separate add pass (read 2, write 1). C aliases D here; on
+    MI355X every engine / tuned solution of these shapes returns the same bits for the aliased
+    in-place form as for the out-of-place one (profiles/r02/tunableop/tunableop_probe.jsonl), and
+    out-of-place torch.addmm would first copy C into D (2 x 411 MB more traffic at layer 1)."""
     N, cin, H, W = x.shape
     cout = wc.shape[0]
     M = N * H * W
     b2 = base.permute(0, 2, 3, 1).reshape(M, cin)  # a view of base
     with torch.autocast("cuda", enabled=False):
-        eng = _choose((M, cin, cout, x.dtype, "dgrad_acc"),
-                      {"gemm": lambda: torch.addmm(b2, g2, wc), "conv": lambda: base + _conv_dgrad(gy, x, wc)})
-        if eng == "gemm":
-            return torch.addmm(b2, g2, wc).view(N, H, W, cin).permute(0, 3, 1, 2)
-        return (base + _conv_dgrad(gy, x, wc)).contiguous(memory_format=torch.channels_last)
+        key = (M, cin, cout, x.dtype, "dgrad_acc")
+        if not _loaded:
+            _load_plans()
+            _loaded.append(True)
+        if key not in plans:
+            scratch = base.clone(memory_format=torch.channels_last)
+            s2 = scratch.permute(0, 2, 3, 1).reshape(M, cin)
+            _choose(key, {"gemm": lambda: s2.addmm_(g2, wc), "conv": lambda: scratch.add_(_conv_dgrad(gy, x, wc))})
+            del scratch, s2
+        if plans[key] == "gemm":
+            b2.addmm_(g2, wc)
+        else:
+            base.add_(_conv_dgrad(gy, x, wc))
+    return base
 
 
 def _wgrad(gy, g2, x, wc, wdtype):
@@ -259,9 +270,9 @@ class Conv1x1SkipFunction(torch.autograd.Function):
             if gs is None:
                 base = None
             elif wcd is None:
-                # the identity branch's gradient: the accumulate GEMM only reads it; a tensor another
-                # consumer also holds (e.g. torch's add hands one tensor to both operands) is copied
-                # before it can be returned as dx
+                # the identity branch's gradient. With the fused BN node as its consumer it is a
+                # fresh tensor (BnActFunction's dres) seen only here, so it is accumulated into in
+                # place; otherwise (e.g. torch's add, which hands one tensor to both operands) a copy
                 base = gs.to(x.dtype).contiguous(memory_format=torch.channels_last)
                 if base is gs and not ctx.skip_grad_owned:
                     base = base.clone(memory_format=torch.channels_last)

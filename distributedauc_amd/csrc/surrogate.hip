@@ -965,6 +965,123 @@ __global__ __launch_bounds__(kThreads) void surrogate_ticket_kernel(
     }
 }
 
+// ---- the stream with its row reduce in the same launch: the LAST R workgroups reduce ---------
+//
+// Every workgroup streams its chunk (as surrogate_chunk_kernel) and stores its 48-B row as
+// data-as-flag words (bits ^ kEmptyKey, agent-scope stores; no drain, no ticket). The last R
+// workgroups by blockIdx are the reducers: reducer r, after its own chunk and row, takes the rows
+// of group r (a contiguous range of ceil(nblocks / R) rows; take_rows: polls only words still
+// zero, bounded, re-zeroes what it consumed, fixed summation order), and publishes the group total
+// the same way; reducer R-1 then takes the R group totals in group order and writes the scalars.
+// Nothing waits on a workgroup that waits: the rows every reducer needs come from workgroups that
+// never wait (and from the reducers' own rows, stored before they reduce), and at most R of the
+// grid's resident slots are ever held by waiting workgroups. Bitwise reproducible.
+template <typename YT, int S, int R>
+__global__ __launch_bounds__(kThreads) void surrogate_tail_kernel(
+    const float* __restrict__ h, const YT* __restrict__ y, int64_t B, double invB,
+    const float* __restrict__ abalpha, const float* __restrict__ p_hat, float* __restrict__ dh,
+    unsigned long long* __restrict__ rows, unsigned long long* __restrict__ gwords,
+    double* __restrict__ out64, float* __restrict__ grad3, float* __restrict__ loss) {
+    const SurrogateScalars s = make_scalars(abalpha, p_hat, invB);
+    Acc acc;
+    const bool write_dh = dh != nullptr;
+    const int64_t base = int64_t(blockIdx.x) * chunk_elems(S);
+    const bool full = base + chunk_elems(S) <= B;
+    f32x4 hv[S];
+    if (full) {
+        int yv[S][4];
+#pragma unroll
+        for (int k = 0; k < S; ++k) {
+            const int64_t b = base + (int64_t(k) * kThreads + threadIdx.x) * kVec;
+            hv[k] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(h + b));
+            load_labels4(y, b, yv[k]);
+        }
+#pragma unroll
+        for (int k = 0; k < S; ++k) hv[k] = visit4<false>(hv[k], yv[k], s, acc);
+    } else {
+        for (int64_t i = base + threadIdx.x; i < B; i += kThreads) {
+            const float g = visit1<false>(h[i], load_label(y, i), s, acc);
+            if (write_dh) dh[i] = g;
+        }
+    }
+    const double sp = wave_total_dpp(acc.s_pos), sn = wave_total_dpp(acc.s_neg);
+    const double qp = wave_total_dpp(acc.q_pos), qn = wave_total_dpp(acc.q_neg);
+    const int np = wave_total_dpp(acc.n_pos), nn = wave_total_dpp(acc.n_neg);
+    if (full && write_dh) {
+#pragma unroll
+        for (int k = 0; k < S; ++k)
+            __builtin_nontemporal_store(hv[k], reinterpret_cast<f32x4*>(dh + base + (int64_t(k) * kThreads + threadIdx.x) * kVec));
+    }
+    __shared__ double wrow[kWaves][kRowWords];
+    const int wid = threadIdx.x / kWave;
+    if ((threadIdx.x & (kWave - 1)) == kWave - 1) {
+        wrow[wid][0] = sp;
+        wrow[wid][1] = sn;
+        wrow[wid][2] = qp;
+        wrow[wid][3] = qn;
+        wrow[wid][4] = static_cast<double>(np);
+        wrow[wid][5] = static_cast<double>(nn);
+    }
+    __syncthreads();
+    if (threadIdx.x < kRowWords) {
+        const int k = threadIdx.x;
+        const double v = ((wrow[0][k] + wrow[1][k]) + wrow[2][k]) + wrow[3][k];
+        __hip_atomic_store((gu64*)(rows + int64_t(blockIdx.x) * kRowWords + k), enc_word(v), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    }
+    const int64_t nblocks = gridDim.x;
+    const int64_t nred = nblocks < R ? nblocks : R;
+    const int64_t r = int64_t(blockIdx.x) - (nblocks - nred);
+    if (r < 0) return;
+
+    // reducer r: the rows of group r, then (reducer nred - 1) the group totals
+    __shared__ double scratch[kNumAcc * kWaves];
+    const int64_t G = (nblocks + nred - 1) / nred;
+    const int64_t g0 = r * G, g1 = (g0 + G < nblocks) ? g0 + G : nblocks;
+    bool ok = true;
+    double tot[kNumAcc];
+#pragma unroll
+    for (int k = 0; k < kNumAcc; ++k) tot[k] = 0.0;
+    if (g1 > g0) take_rows(rows + g0 * kRowWords, g1 - g0, tot, ok);
+    block_sum<kNumAcc>(tot, scratch);
+    if (threadIdx.x < kRowWords) {
+        double v = tot[0];
+#pragma unroll
+        for (int k = 1; k < kNumAcc; ++k)
+            if (threadIdx.x == k) v = tot[k];
+        __hip_atomic_store((gu64*)(gwords + r * kRowWords + threadIdx.x), enc_word(v), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    }
+    ok = __syncthreads_or(!ok) == 0;
+    if (r != nred - 1) return;
+#pragma unroll
+    for (int k = 0; k < kNumAcc; ++k) tot[k] = 0.0;
+    take_rows(gwords, nred, tot, ok);
+    block_sum<kNumAcc>(tot, scratch);
+    ok = __syncthreads_or(!ok) == 0;
+    if (threadIdx.x == 0) {
+        if (!ok) {
+#pragma unroll
+            for (int k = 0; k < kNumAcc; ++k) tot[k] = __builtin_nan("");
+        }
+        finalize(tot, s, invB, out64, grad3, loss);
+    }
+}
+
+template <typename YT, int S, int R>
+int launch_tail(const float* h, const YT* y, int64_t B, const float* abalpha, const float* p_hat, float* dh,
+                double* out64, float* grad3, float* loss, void* ws, size_t ws_bytes, hipStream_t st) {
+    const int64_t nblocks = (B + chunk_elems(S) - 1) / chunk_elems(S);
+    if (nblocks > 0x7fffffffLL) return DAUC_EINVAL;
+    const size_t need = kPersistentBytes + static_cast<size_t>(nblocks + R) * kRowWords * 8;
+    if (ws == nullptr || ws_bytes < need) return DAUC_EINVAL;
+    auto* rows = reinterpret_cast<unsigned long long*>(static_cast<char*>(ws) + kPersistentBytes);
+    hipLaunchKernelGGL((surrogate_tail_kernel<YT, S, R>), dim3(static_cast<unsigned>(nblocks)), dim3(kThreads), 0, st,
+                       h, y, B, 1.0 / static_cast<double>(B), abalpha, p_hat, dh, rows, rows + nblocks * kRowWords,
+                       out64, grad3, loss);
+    return launch_status();
+}
+
 // Default chunk geometry (variant sweep: scripts/micro_kernels.py --which surrogate).
 #ifndef DAUC_SURROGATE_CHUNK_SLOTS
 #define DAUC_SURROGATE_CHUNK_SLOTS 4
@@ -1093,6 +1210,9 @@ int launch_surrogate(const float* h, int64_t hs, const YT* y, int64_t B, const f
                 case 17: return launch_span<YT, false, 4, 8>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, sums4, accumulate, ws, ws_bytes, st);
                 case 18: return launch_span<YT, false, 4, 16>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, sums4, accumulate, ws, ws_bytes, st);
                 case 19: return launch_span<YT, false, 4, 32>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, sums4, accumulate, ws, ws_bytes, st);
+                case 20: return launch_tail<YT, 4, 32>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, ws, ws_bytes, st);
+                case 21: return launch_tail<YT, 4, 16>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, ws, ws_bytes, st);
+                case 22: return launch_tail<YT, 4, 64>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, ws, ws_bytes, st);
                 default: return DAUC_EINVAL;
             }
         }
@@ -1279,7 +1399,7 @@ int dauc_surrogate_fwdbwd_variant(const float* h, int64_t h_stride, const void* 
                                   double* out64, float* grad3, float* loss, void* workspace,
                                   size_t workspace_bytes, int variant, dauc_stream_t stream) {
     if (B <= 0 || h == nullptr || y == nullptr || abalpha == nullptr || p_hat == nullptr ||
-        h_stride <= 0 || (dh != nullptr && dh_stride <= 0) || variant < 0 || variant > 19)
+        h_stride <= 0 || (dh != nullptr && dh_stride <= 0) || variant < 0 || variant > 22)
         return DAUC_EINVAL;
     return dispatch_labels<false>(h, h_stride, y, y_dtype, B, abalpha, p_hat, dh, dh_stride, out64,
                                   grad3, loss, nullptr, 0, workspace, workspace_bytes,

@@ -74,7 +74,7 @@ def test_resnet_gemm_conv1x1_trains(dev):
 @pytest.mark.parametrize("acc_engine", ["gemm", "conv"])
 def test_conv1x1_skip_fuses_branch_gradient(dev, down, owned, acc_engine):
     """(conv1(x), skip) in one node: dx = dgrad(conv1) + d(skip), the sum accumulated by the GEMM
-    (beta = 1, into a new tensor: C and D never alias) or by an add after MIOpen's dgrad; skip = identity (down 0) or a 1x1
+    (beta = 1, in place) or by an add after MIOpen's dgrad; skip = identity (down 0) or a 1x1
     downsample of stride 1 (GEMM) / 2 (MIOpen); vs fp64 autograd of the two branches.
     Also: the incoming skip gradient is left untouched unless the caller marked it as owned."""
     from distributedauc_amd import conv1x1 as C
