@@ -14,9 +14,10 @@ through an LDS search tree (O(M log M + L log M)).
 
 Sharding (north star): every rank holds the same score vector. The
 pair-count method gives rank r the positives [r*P/G, (r+1)*P/G) of the stable
-split against ALL negatives; the sort method gives rank r a slice of the larger
-class against all of the smaller one. One int64 [2] all-reduce sums (W, T); the
-result does not depend on G.
+split against ALL negatives; the sort method has rank r compact the positives of
+its index slice (all ranks then all-gather them, in order) and stream its slice
+of the scores through the search over ALL positives. One int64 [3] all-reduce
+sums (W, T, non-finite); the result does not depend on G.
 
 Error behaviour mirrors sklearn: non-finite scores raise ValueError; labels
 with more than two distinct values raise ValueError; a single class returns NaN
@@ -79,11 +80,16 @@ class ExactAUC:
         if self.method == "pairs":
             # stable split: every rank sees the positives in the same order, so positive blocks shard
             pos, neg, stats = ops.split_scores(s, y)
+            P, N, nonfinite, other = (int(v) for v in stats.tolist())
+        elif self.world > 1 and self.reduce:
+            # the sort method over ranks: each rank compacts the positives of its own index slice,
+            # then every rank gathers all of them (in index order, so every rank holds the same list)
+            pos, (P, N, nonfinite, other) = self._compact_sharded(s, y)
         else:
             # the sort method reads the negatives in place: only the labels and the positives' scores
             # are read here; the negatives' finiteness is checked by the query kernel
             pos, stats = ops.compact_positives(s, y)
-        P, N, nonfinite, other = (int(v) for v in stats.tolist())
+            P, N, nonfinite, other = (int(v) for v in stats.tolist())
         if nonfinite:
             raise ValueError("Input y_score contains NaN or infinity.")
         if other:
@@ -122,6 +128,30 @@ class ExactAUC:
         if bad:
             raise ValueError("Input y_score contains NaN or infinity.")
         return {"wins": W, "ties": T, "P": P, "N": N}
+
+    def _compact_sharded(self, s: torch.Tensor, y: torch.Tensor):
+        """dauc_compact_positives over this rank's index slice, then an all-gather of the per-rank
+        stats (one host sync) and of the positives (padded to the largest share): every rank ends
+        with all the positive scores in original order and the global {P, N, non-finite, other}."""
+        n, G, r = s.numel(), self.world, self.rank
+        lo, hi = r * n // G, (r + 1) * n // G
+        if hi > lo:
+            pos_r, st_r = ops.compact_positives(s[lo:hi], y[lo:hi])
+        else:
+            pos_r, st_r = s.new_empty(0), torch.zeros(4, dtype=torch.int64, device=s.device)
+        st_all = [torch.empty_like(st_r) for _ in range(G)]
+        dist.all_gather(st_all, st_r, group=self.group)
+        st = torch.stack(st_all).cpu()
+        sizes = st[:, 0].tolist()
+        P, N, nonfinite, other = (int(v) for v in st.sum(0).tolist())
+        width = max(sizes)
+        if width == 0:
+            return s.new_empty(0), (P, N, nonfinite, other)
+        send = s.new_empty(width)
+        send[:sizes[r]] = pos_r[:sizes[r]]
+        parts = [torch.empty_like(send) for _ in range(G)]
+        dist.all_gather(parts, send, group=self.group)
+        return torch.cat([parts[q][:sizes[q]] for q in range(G) if sizes[q]]), (P, N, nonfinite, other)
 
     @staticmethod
     def from_counts(c: dict) -> float:

@@ -1,9 +1,11 @@
 #!/bin/bash
-# round-2 evidence: kernel trace of the bench, PMC traffic (update, surrogate, compaction, query),
-# and a longer interleaved surrogate A/B (default two-launch call vs the in-launch reduce variants)
+# round-2 evidence: sharded-compaction smoke (2 gloo ranks through bench.py), kernel trace of the
+# bench, PMC traffic (update, surrogate, compaction, query), and an interleaved surrogate A/B
 set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out/r02_prof gpurun_out/pmc_r02
+timeout -k 10 600 python -u -m pytest -x -q --timeout 550 --timeout-method thread tests/test_bench_gpu.py \
+    tests/test_kernels_gpu.py -k "bench or auc" > gpurun_out/r02_prof/tests.log 2>&1 || exit 1
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r02_prof -o bench -- \
     python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline > gpurun_out/r02_prof/bench.log 2>&1 || exit 1
 for c in FETCH_SIZE WRITE_SIZE; do

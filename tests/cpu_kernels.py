@@ -79,11 +79,38 @@ def pd_update(w, w0, w_avg, segs, nseg, *, scalars=None, grad3=None, anchor3=Non
             w_avg[off:off + n] += new
 
 
+def compact_positives(scores, labels):
+    """Stable compaction stand-in: (pos buffer of capacity n, stats {P, n - P, non-finite pos, other})."""
+    s, y = scores.detach(), labels
+    pos = torch.empty_like(s)
+    m = y == 1
+    P = int(m.sum())
+    pos[:P] = s[m]
+    other = int(((y != 1) & (y != -1)).sum())
+    return pos, torch.tensor([P, s.numel() - P, int((~torch.isfinite(s[m])).sum()), other], dtype=torch.int64)
+
+
+def auc_counts_sorted_labeled(pos, scores, labels, begin, end, wins_ties, nonfinite=None):
+    """(wins, ties) of every label != 1 in [begin, end) against pos, by the C oracle's brute force."""
+    neg = scores[begin:end][labels[begin:end] != 1].numpy()
+    W, T = coracle_pair_count(pos.numpy(), neg)
+    wins_ties[0] += W
+    wins_ties[1] += T
+    if nonfinite is not None:
+        nonfinite[0] += int((~np.isfinite(neg)).sum())
+
+
+def coracle_pair_count(pos, neg):
+    from oracle import coracle
+
+    return coracle.pair_count_bruteforce(pos, neg)
+
+
 def install(monkeypatch):
     from distributedauc_amd import flat, ops
 
     for name in ("label_map_phat", "surrogate_fwdbwd", "class_sums", "alpha_from_sums", "coda_finalize",
-                 "scale_div", "pd_update"):
+                 "scale_div", "pd_update", "compact_positives", "auc_counts_sorted_labeled"):
         monkeypatch.setattr(ops, name, globals()[name])
     monkeypatch.setattr(flat, "_check_device", lambda dev: None)
 

@@ -1,0 +1,75 @@
+"""The sharded exact-AUC orchestration on CPU (gloo, world 2 and 3): each rank compacts the
+positives of its own index slice, all ranks all-gather them (in order) and stream their slice of
+the scores through the count; one all-reduce of (wins, ties, non-finite). The kernels are served
+by the oracle (tests/cpu_kernels.py); the GPU form runs in bench.py --gpus 2 (tests/test_bench_gpu.py)."""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import cpu_kernels
+from test_coda_gloo import _free_port
+
+
+def _worker(rank, world, port, q):
+    import traceback
+
+    import torch.distributed as dist
+
+    try:
+        torch.set_num_threads(1)
+        cpu_kernels.install_in_process()
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from distributedauc_amd.auc import ExactAUC
+        from oracle import coracle
+
+        rng = np.random.default_rng(5)
+        n = 20_011
+        s = (np.floor(rng.random(n) * 997) / 997).astype(np.float32)
+        y = np.where(rng.random(n) < 0.03, 1, -1).astype(np.int8)
+        ev = ExactAUC(world=world, rank=rank, method="sort")
+        c = ev.counts(torch.from_numpy(y), torch.from_numpy(s), device="cpu")
+        e = coracle.auc_counts(y.astype(np.int64), s)
+        assert (c["wins"], c["ties"], c["P"], c["N"]) == (e["wins"], e["ties"], e["P"], e["N"]), (c, e)
+        # a non-finite negative in one rank's slice is seen by every rank after the reduce
+        s2 = s.copy()
+        s2[np.flatnonzero(y == -1)[-3]] = np.nan
+        try:
+            ev.counts(torch.from_numpy(y), torch.from_numpy(s2), device="cpu")
+            raised = False
+        except ValueError:
+            raised = True
+        assert raised
+        dist.destroy_process_group()
+        q.put((rank, None))
+    except BaseException:
+        q.put((rank, traceback.format_exc()))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.timeout(300)
+def test_sharded_sort_auc_gloo(world):
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(240)
+    res = []
+    while not q.empty():
+        res.append(q.get())
+    for p in procs:
+        if p.is_alive():
+            p.kill()
+    errs = [e for _, e in res if e]
+    assert not errs, "\n".join(errs)
+    assert sorted(r for r, _ in res) == list(range(world))
