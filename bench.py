@@ -83,7 +83,7 @@ def parse(argv=None):
     p.add_argument("--auc2-log2n", type=int, default=27, help="configs[4] leg (0 = off)")
     p.add_argument("--auc2-pos", type=float, default=0.001)
     p.add_argument("--sur-log2b", type=int, default=26, help="surrogate kernel leg: batch of 2^k scores")
-    p.add_argument("--sur-reps", type=int, default=20)
+    p.add_argument("--sur-reps", type=int, default=100)
     p.add_argument("--variant", type=int, default=0, help="pair-count kernel variant")
     p.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL; gloo for rehearsals)")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -402,7 +402,7 @@ def bench_surrogate(args, device):
     out64 = torch.zeros(6, dtype=torch.float64, device=device)
 
     def b2b(variant):
-        for _ in range(3):
+        for _ in range(max(10, args.sur_reps)):  # warm: the first calls after other work run ~2-3 us slower
             ops.surrogate_fwdbwd(h, y, abalpha, p_hat, dh=dh, grad3=grad3, out64=out64, variant=variant)
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -434,8 +434,8 @@ def bench_surrogate(args, device):
             "timing": f"HIP events around {args.sur_reps} back-to-back calls on the launch stream, divided by the "
                       "call count (per_call_events_us: an event pair around every call instead)",
             "loss": loss,
-            "roofline": {"kernel": "dauc_surrogate_fwdbwd (whole call)", "launches": "surrogate_chunk_kernel (stream) + "
-                         "surrogate_rows_reduce_kernel (fp64 rows), both inside every timed ABI call",
+            "roofline": {"kernel": "dauc_surrogate_fwdbwd (whole call)", "launches": "surrogate_tail_kernel: the stream "
+                         "and its fp64 row reduce (by the last 64 workgroups) in ONE launch",
                          "bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS, "traffic": load_traffic(f"surrogate_2^{args.sur_log2b}"),
                          "bytes_per_launch": nbytes},

@@ -35,8 +35,11 @@ namespace dauc {
 namespace {
 
 constexpr int kSortThreads = 256;
-constexpr int kPerThread = 16;
-constexpr int kTile = kSortThreads * kPerThread;  // 4096 keys
+#ifndef DAUC_SORT_PER_THREAD
+#define DAUC_SORT_PER_THREAD 8
+#endif
+constexpr int kPerThread = DAUC_SORT_PER_THREAD;  // keys per thread per pass tile
+constexpr int kTile = kSortThreads * kPerThread;  // 2048 keys (8 per thread: the hist pass 4.9 vs 6.1 us at 134k keys)
 constexpr int kRadix = 256;
 constexpr int kScanBlock = 1024;
 constexpr int64_t kSingleScan = 32768;  // histogram entries one workgroup scans alone (<= 512K keys)
@@ -123,7 +126,7 @@ __global__ __launch_bounds__(kScanBlock) void scan_add_kernel(unsigned* __restri
 // FUSED_SCAN: offs is the raw digit-major histogram; every workgroup derives its own output
 // offsets from it (its digit's count in the tiles before it + the exclusive scan of the digit
 // totals): a small sort (<= kFusedScanTiles tiles) then needs no scan launches at all.
-constexpr int64_t kFusedScanTiles = 128;
+constexpr int64_t kFusedScanTiles = 256;
 
 template <bool FROM_FLOAT, bool FUSED_SCAN>
 __global__ __launch_bounds__(kSortThreads) void radix_scatter_kernel(const void* __restrict__ in, int64_t n,
@@ -485,41 +488,44 @@ __device__ __forceinline__ void count_queries(const unsigned (&x)[Q], const bool
             t += static_cast<unsigned long long>(ub - lb);
         }
     } else {
-        unsigned i[Q];
-        tree_walk<Q>(x, i, tree, g);
+        unsigned su[Q];
+        tree_walk<Q>(x, su, tree, g);
         // every bucket load issued before any is examined (su = 0: bucket 0 is read, unused)
         int le[Q], lt[Q];
         unsigned first[Q];
-        int64_t su[Q];
+#pragma unroll
+        for (int q = 0; q < Q; ++q) bucket_counts<K>(sorted, M, su[q] ? su[q] - 1u : 0u, x[q], le[q], lt[q], first[q]);
+        // 32-bit and branch-free: lb below is exact unless the bucket starts with x itself (then
+        // a run of x may begin in an earlier bucket); those rare queries are fixed up after
+        bool slow = false;
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
-            su[q] = i[q];
-            bucket_counts<K>(sorted, M, su[q] > 0 ? su[q] - 1 : 0, x[q], le[q], lt[q], first[q]);
+            const unsigned base = su[q] ? (su[q] - 1u) * static_cast<unsigned>(K) : 0u;
+            const unsigned ub = su[q] ? base + static_cast<unsigned>(le[q]) : 0u;
+            const unsigned lb = su[q] ? base + static_cast<unsigned>(lt[q]) : 0u;
+            const unsigned wq = TABLE_POS ? static_cast<unsigned>(M) - ub : lb;
+            w += use[q] ? wq : 0u;
+            t += use[q] ? ub - lb : 0u;
+            slow |= use[q] && su[q] != 0u && first[q] >= x[q];
         }
+        if (slow) {
 #pragma unroll
-        for (int q = 0; q < Q; ++q) {
-            if (!use[q]) continue;
-            int64_t ub = 0, lb = 0;
-            if (su[q] > 0) {
-                ub = (su[q] - 1) * K + le[q];
-                if (first[q] < x[q]) {
-                    lb = (su[q] - 1) * K + lt[q];
-                } else {
-                    // the bucket starts with x: a run of x may begin in an earlier bucket (rare)
-                    const unsigned xm[1] = {x[q] - 1u};
-                    unsigned j[1];
-                    tree_walk<1>(xm, j, tree, g);
-                    const int64_t sl = j[0];
-                    if (sl > 0) {
-                        int le2 = 0, lt2 = 0;
-                        unsigned f2 = 0;
-                        bucket_counts<K>(sorted, M, sl - 1, x[q], le2, lt2, f2);
-                        lb = (sl - 1) * K + lt2;
-                    }
+            for (int q = 0; q < Q; ++q) {
+                if (!(use[q] && su[q] != 0u && first[q] >= x[q])) continue;
+                const unsigned xm[1] = {x[q] - 1u};
+                unsigned j[1];
+                tree_walk<1>(xm, j, tree, g);
+                unsigned lb_true = 0u;
+                if (j[0] != 0u) {
+                    int le2 = 0, lt2 = 0;
+                    unsigned f2 = 0;
+                    bucket_counts<K>(sorted, M, j[0] - 1u, x[q], le2, lt2, f2);
+                    lb_true = (j[0] - 1u) * static_cast<unsigned>(K) + static_cast<unsigned>(lt2);
                 }
+                const unsigned lb_fast = (su[q] - 1u) * static_cast<unsigned>(K);  // lt = 0: the bucket starts with x
+                t += lb_fast - lb_true;                                             // ties: ub - lb_true
+                if (!TABLE_POS) w -= lb_fast - lb_true;                             // wins: lb_true
             }
-            w += TABLE_POS ? static_cast<unsigned long long>(M - ub) : static_cast<unsigned long long>(lb);
-            t += static_cast<unsigned long long>(ub - lb);
         }
     }
 }

@@ -1087,6 +1087,12 @@ int launch_tail(const float* h, const YT* y, int64_t B, const float* abalpha, co
 #define DAUC_SURROGATE_CHUNK_SLOTS 4
 #endif
 constexpr int kChunkSlots = DAUC_SURROGATE_CHUNK_SLOTS;
+// reducers of the one-launch loss (variants 20-24 measured at B = 2^26: 16 / 32 / 64 / 128 / 256;
+// profiles/r02/surrogate_ab.jsonl)
+#ifndef DAUC_SURROGATE_TAIL_REDUCERS
+#define DAUC_SURROGATE_TAIL_REDUCERS 64
+#endif
+constexpr int kTailReducers = DAUC_SURROGATE_TAIL_REDUCERS;
 // Unit-stride batches at least this large take the chunked kernel; smaller ones are
 // latency-bound and stay on the single-ticket persistent kernel.
 constexpr int64_t kChunkMinB = int64_t(1) << 22;
@@ -1213,14 +1219,24 @@ int launch_surrogate(const float* h, int64_t hs, const YT* y, int64_t B, const f
                 case 20: return launch_tail<YT, 4, 32>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, ws, ws_bytes, st);
                 case 21: return launch_tail<YT, 4, 16>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, ws, ws_bytes, st);
                 case 22: return launch_tail<YT, 4, 64>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, ws, ws_bytes, st);
+                case 23: return launch_tail<YT, 4, 128>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, ws, ws_bytes, st);
+                case 24: return launch_tail<YT, 4, 256>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, ws, ws_bytes, st);
+                case 25: return launch_chunk<YT, false, kChunkSlots, true, true>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, sums4, accumulate, ws, ws_bytes, st);
                 default: return DAUC_EINVAL;
             }
         }
         return DAUC_EINVAL;
     }
-    if (unit && variant == 0 && B >= kChunkMinB)
-        return launch_chunk<YT, CLASS_ONLY, kChunkSlots, true, true>(h, y, B, abalpha, p_hat, dh, out64, grad3,
-                                                                      loss, sums4, accumulate, ws, ws_bytes, st);
+    if (unit && variant == 0 && B >= kChunkMinB) {
+        // the loss: the stream with its row reduce done by its last kTailReducers workgroups (one
+        // launch); the class sums keep the two-launch form
+        if constexpr (!CLASS_ONLY)
+            return launch_tail<YT, kChunkSlots, kTailReducers>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, ws,
+                                                               ws_bytes, st);
+        else
+            return launch_chunk<YT, CLASS_ONLY, kChunkSlots, true, true>(h, y, B, abalpha, p_hat, dh, out64, grad3,
+                                                                          loss, sums4, accumulate, ws, ws_bytes, st);
+    }
     const int grid = grid_for(B);
     unsigned* counter = nullptr;
     double* partials = nullptr;
@@ -1399,7 +1415,7 @@ int dauc_surrogate_fwdbwd_variant(const float* h, int64_t h_stride, const void* 
                                   double* out64, float* grad3, float* loss, void* workspace,
                                   size_t workspace_bytes, int variant, dauc_stream_t stream) {
     if (B <= 0 || h == nullptr || y == nullptr || abalpha == nullptr || p_hat == nullptr ||
-        h_stride <= 0 || (dh != nullptr && dh_stride <= 0) || variant < 0 || variant > 22)
+        h_stride <= 0 || (dh != nullptr && dh_stride <= 0) || variant < 0 || variant > 25)
         return DAUC_EINVAL;
     return dispatch_labels<false>(h, h_stride, y, y_dtype, B, abalpha, p_hat, dh, dh_stride, out64,
                                   grad3, loss, nullptr, 0, workspace, workspace_bytes,

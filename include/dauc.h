@@ -109,8 +109,10 @@ int dauc_surrogate_fwdbwd(const float* h, int64_t h_stride, const void* y, int y
  * row reduce, no scalar outputs; it leaves its rows in the workspace, so give it a workspace of
  * its own: timing of the stream without the reduce launch), 16..19 one contiguous span of
  * 4 / 8 / 16 / 32 chunks (4 slots) per workgroup, next chunk's loads in flight, so the row
- * reduce is one small workgroup; 20..22 the row reduce inside the streaming launch, by its last
- * 32 / 16 / 64 workgroups (data-as-flag rows, no second launch). Variants 2..22 need unit strides, 16-byte
+ * reduce is one small workgroup; 20..24 the row reduce inside the streaming launch, by its last
+ * 32 / 16 / 64 / 128 / 256 workgroups (data-as-flag rows, no second launch; 64 is what variant 0
+ * runs for unit-stride B >= 2^22), 25 the two-launch form (stream + row-reduce kernel). Variants
+ * 2..25 need unit strides, 16-byte
  * aligned h/dh and int8 labels, and B <= 2^31. Every variant returns bitwise-identical dh and counts;
  * the fp64 sums agree to rounding (their reduction trees differ).
  */

@@ -37,7 +37,7 @@ def kernel_key(name: str) -> str | None:
         return "pd_update"
     if "surrogate_rows_reduce_kernel" in name:
         return "surrogate_reduce"
-    if "surrogate_chunk_kernel" in name or "surrogate_kernel" in name:
+    if "surrogate_chunk_kernel" in name or "surrogate_kernel" in name or "surrogate_tail_kernel" in name:
         return "surrogate"
     if "compact_count_kernel" in name:
         return "compact_count_2^27"
@@ -72,7 +72,7 @@ def main(src: str, dst: str):
     res = {
         "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes (scripts/gpu_pmc.sh), "
                   "counter-collection CSV per dispatch; KB = 1024 B; FETCH_SIZE doubled for gfx950 wide streaming "
-                  "reads (MI355X_MICROARCH.md §HBM); median over dispatches (surrogate: largest grid = B 2^26, chunk kernel + row-reduce kernel); "
+                  "reads (MI355X_MICROARCH.md §HBM); median over dispatches (surrogate: largest grid = B 2^26, the one-launch tail kernel, or chunk kernel + row-reduce kernel); "
                   "scripts/pmc_traffic.py",
         "source": dst,
     }
@@ -99,8 +99,8 @@ def main(src: str, dst: str):
             res[k + "_algorithmic"] = ALGORITHMIC[k]
     os.makedirs(dst, exist_ok=True)
     for f in glob.glob(os.path.join(src, "**", "*counter_collection.csv"), recursive=True):
-        counter = "FETCH_SIZE" if "FETCH_SIZE" in f else "WRITE_SIZE"
-        with open(f) as fh, open(os.path.join(dst, f"pmc_{counter}_dauc.csv"), "w", newline="") as oh:
+        stem = os.path.basename(f).replace("_counter_collection.csv", "")
+        with open(f) as fh, open(os.path.join(dst, f"{stem}_dauc.csv"), "w", newline="") as oh:
             rd = csv.DictReader(fh)
             w = csv.DictWriter(oh, fieldnames=rd.fieldnames)
             w.writeheader()
