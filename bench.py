@@ -655,6 +655,11 @@ def main():
     rc = self_launch(args)
     if rc is not None:
         sys.exit(rc)
+    # Only the JSON record goes to stdout: everything else written to fd 1 (gloo's C++ connection
+    # messages, CPU worker children, library chatter) is sent to stderr for the rest of the run.
+    json_fd = os.dup(1)
+    sys.stdout.flush()
+    os.dup2(2, 1)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -748,7 +753,8 @@ def main():
                     auc2, max_log2n=None if args.cpu_sklearn_full else 24, oracle_check=True)
         else:
             out["cpu_baseline"] = None
-        print(json.dumps(out), flush=True)
+        sys.stdout.flush()
+        os.write(json_fd, (json.dumps(out) + "\n").encode())
     if world > 1:
         dist.barrier(group=quiet)
         dist.destroy_process_group()

@@ -25,8 +25,9 @@ def test_bench_self_launches_two_ranks():
                         "--no-surrogate", "--no-cpu-baseline", "--auc-log2n", "18", "--auc2-log2n", "0",
                         "--auc-reps", "1"], env=env, capture_output=True, text=True, timeout=540)
     assert r.returncode == 0, r.stderr[-3000:]
-    line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
-    out = json.loads(line)
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout[-3000:]  # stdout carries the JSON record and nothing else
+    out = json.loads(lines[0])
     assert out["n_gpus"] == 2
     assert out["process_group"]["world_size"] == 2 and out["process_group"]["backend"] == "gloo"
     assert out["auc_eval"]["methods_agree"] and out["auc_eval"]["P"] > 0
