@@ -840,6 +840,39 @@ __device__ __forceinline__ void take_rows(unsigned long long* words, int64_t nro
     }
 }
 
+// take_rows with one row per thread per pass: 12 fewer live VGPRs, which keeps a kernel that
+// also streams (surrogate_tail_kernel) at the stream's own occupancy
+__device__ __forceinline__ void take_rows_narrow(unsigned long long* words, int64_t nrows, double (&tot)[kNumAcc],
+                                                 bool& ok) {
+    for (int64_t r0 = threadIdx.x; r0 < nrows; r0 += kThreads) {
+        unsigned long long w[kRowWords];
+#pragma unroll
+        for (int k = 0; k < kRowWords; ++k)
+            w[k] = __hip_atomic_load((gu64*)(words + r0 * kRowWords + k), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (int polls = 0;; ++polls) {
+            bool missing = false;
+#pragma unroll
+            for (int k = 0; k < kRowWords; ++k) missing |= (w[k] == 0ull);
+            if (!missing) break;
+            if (polls >= kMaxPolls) {
+                ok = false;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+#pragma unroll
+            for (int k = 0; k < kRowWords; ++k)
+                if (w[k] == 0ull)
+                    w[k] = __hip_atomic_load((gu64*)(words + r0 * kRowWords + k), __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+        }
+#pragma unroll
+        for (int k = 0; k < kRowWords; ++k) {
+            tot[k] += __longlong_as_double(static_cast<long long>(w[k] ^ kEmptyKey));
+            __hip_atomic_store((gu64*)(words + r0 * kRowWords + k), 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
 template <typename YT, bool CLASS_ONLY, int S, int kTicketGroup, int kCtrStride, bool TICKET_FIRST>
 __global__ __launch_bounds__(kThreads) void surrogate_ticket_kernel(
     const float* __restrict__ h, const YT* __restrict__ y, int64_t B, double invB,
@@ -972,7 +1005,8 @@ __global__ __launch_bounds__(kThreads) void surrogate_ticket_kernel(
 // workgroups by blockIdx are the reducers: reducer r, after its own chunk and row, takes the rows
 // of group r (a contiguous range of ceil(nblocks / R) rows; take_rows: polls only words still
 // zero, bounded, re-zeroes what it consumed, fixed summation order), and publishes the group total
-// the same way; reducer R-1 then takes the R group totals in group order and writes the scalars.
+// the same way; reducer R-1 takes the other R-1 group totals (in group order, then its own) and
+// writes the scalars.
 // Nothing waits on a workgroup that waits: the rows every reducer needs come from workgroups that
 // never wait (and from the reducers' own rows, stored before they reduce), and at most R of the
 // grid's resident slots are ever held by waiting workgroups. Bitwise reproducible.
@@ -1034,36 +1068,70 @@ __global__ __launch_bounds__(kThreads) void surrogate_tail_kernel(
     const int64_t r = int64_t(blockIdx.x) - (nblocks - nred);
     if (r < 0) return;
 
-    // reducer r: the rows of group r, then (reducer nred - 1) the group totals
+    // reducer r: the rows of group r; reducer nred - 1 (whose group holds the grid's last rows)
+    // also takes the other group totals, loaded before its own group so that their trip overlaps
+    // its wait, and adds its own total from registers: one memory trip after the last row lands
     __shared__ double scratch[kNumAcc * kWaves];
     const int64_t G = (nblocks + nred - 1) / nred;
     const int64_t g0 = r * G, g1 = (g0 + G < nblocks) ? g0 + G : nblocks;
+    const bool final_red = r == nred - 1;
+    const bool holds = final_red && threadIdx.x < nred - 1;  // thread t: group total t
+    unsigned long long gw[kRowWords];
+    if (holds) {
+#pragma unroll
+        for (int k = 0; k < kRowWords; ++k)
+            gw[k] = __hip_atomic_load((gu64*)(gwords + threadIdx.x * kRowWords + k), __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_AGENT);
+    }
     bool ok = true;
     double tot[kNumAcc];
 #pragma unroll
     for (int k = 0; k < kNumAcc; ++k) tot[k] = 0.0;
-    if (g1 > g0) take_rows(rows + g0 * kRowWords, g1 - g0, tot, ok);
+    if (g1 > g0) take_rows_narrow(rows + g0 * kRowWords, g1 - g0, tot, ok);
     block_sum<kNumAcc>(tot, scratch);
-    if (threadIdx.x < kRowWords) {
-        double v = tot[0];
+    if (!final_red) {
+        if (threadIdx.x < kRowWords) {
+            double v = tot[0];
 #pragma unroll
-        for (int k = 1; k < kNumAcc; ++k)
-            if (threadIdx.x == k) v = tot[k];
-        __hip_atomic_store((gu64*)(gwords + r * kRowWords + threadIdx.x), enc_word(v), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
+            for (int k = 1; k < kNumAcc; ++k)
+                if (threadIdx.x == k) v = tot[k];
+            __hip_atomic_store((gu64*)(gwords + r * kRowWords + threadIdx.x), enc_word(v), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        }
+        return;
     }
-    ok = __syncthreads_or(!ok) == 0;
-    if (r != nred - 1) return;
+    double rest[kNumAcc];
 #pragma unroll
-    for (int k = 0; k < kNumAcc; ++k) tot[k] = 0.0;
-    take_rows(gwords, nred, tot, ok);
-    block_sum<kNumAcc>(tot, scratch);
+    for (int k = 0; k < kNumAcc; ++k) rest[k] = 0.0;
+    if (holds) {
+        for (int polls = 0;; ++polls) {
+            bool missing = false;
+#pragma unroll
+            for (int k = 0; k < kRowWords; ++k) missing |= (gw[k] == 0ull);
+            if (!missing) break;
+            if (polls >= kMaxPolls) {
+                ok = false;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+#pragma unroll
+            for (int k = 0; k < kRowWords; ++k)
+                if (gw[k] == 0ull)
+                    gw[k] = __hip_atomic_load((gu64*)(gwords + threadIdx.x * kRowWords + k), __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+        }
+#pragma unroll
+        for (int k = 0; k < kRowWords; ++k) {
+            rest[k] = __longlong_as_double(static_cast<long long>(gw[k] ^ kEmptyKey));
+            __hip_atomic_store((gu64*)(gwords + threadIdx.x * kRowWords + k), 0ull, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    block_sum<kNumAcc>(rest, scratch);
     ok = __syncthreads_or(!ok) == 0;
     if (threadIdx.x == 0) {
-        if (!ok) {
 #pragma unroll
-            for (int k = 0; k < kNumAcc; ++k) tot[k] = __builtin_nan("");
-        }
+        for (int k = 0; k < kNumAcc; ++k) tot[k] = ok ? rest[k] + tot[k] : __builtin_nan("");
         finalize(tot, s, invB, out64, grad3, loss);
     }
 }
