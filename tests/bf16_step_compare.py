@@ -11,12 +11,12 @@ import torch
 SEEDS = (0, 1, 2)
 
 
-def _step(dev, seed, amp: bool, fused_bn: bool, gemm_1x1: bool):
+def _step(dev, seed, amp: bool, fused_bn: bool, gemm_1x1: bool, batch: int = 8, size: int = 64):
     from distributedauc_amd.backbone import build_backbone
 
     torch.manual_seed(seed)
     net = build_backbone("resnet50", num_classes=2)
-    x = torch.randn(8, 3, 64, 64, device=dev).contiguous(memory_format=torch.channels_last)
+    x = torch.randn(batch, 3, size, size, device=dev).contiguous(memory_format=torch.channels_last)
     net = net.to(dev).to(memory_format=torch.channels_last).train()
     net.set_fused_bn(fused_bn)
     if gemm_1x1:
@@ -28,16 +28,17 @@ def _step(dev, seed, amp: bool, fused_bn: bool, gemm_1x1: bool):
             {n: b.detach().float() for n, b in net.named_buffers()})
 
 
-def compare(dev, fused_bn: bool, gemm_1x1: bool, check_buffers: bool = False) -> None:
+def compare(dev, fused_bn: bool, gemm_1x1: bool, check_buffers: bool = False, batch: int = 8, size: int = 64,
+            seeds=SEEDS) -> None:
     e_out = [0.0, 0.0]
     e_grad: dict = {}
     g_norm: dict = {}
     e_buf: dict = {}
     b_max: dict = {}
-    for seed in SEEDS:
-        ref_out, ref_g, ref_b = _step(dev, seed, False, False, False)
-        tb = _step(dev, seed, True, False, False)
-        fa = _step(dev, seed, True, fused_bn, gemm_1x1)
+    for seed in seeds:
+        ref_out, ref_g, ref_b = _step(dev, seed, False, False, False, batch, size)
+        tb = _step(dev, seed, True, False, False, batch, size)
+        fa = _step(dev, seed, True, fused_bn, gemm_1x1, batch, size)
         e_out[0] += float((tb[0] - ref_out).abs().max())
         e_out[1] += float((fa[0] - ref_out).abs().max())
         for n, g in ref_g.items():
@@ -48,7 +49,7 @@ def compare(dev, fused_bn: bool, gemm_1x1: bool, check_buffers: bool = False) ->
             eb, ef = e_buf.get(n, (0.0, 0.0))
             e_buf[n] = (eb + float((tb[2][n] - b).abs().max()), ef + float((fa[2][n] - b).abs().max()))
             b_max[n] = b_max.get(n, 0.0) + float(b.abs().max())
-    assert e_out[1] <= 2 * e_out[0] + 1e-3 * len(SEEDS), ("logits", e_out)
+    assert e_out[1] <= 2 * e_out[0] + 1e-3 * len(seeds), ("logits", e_out)
     worse = [(n, ef, eb, g_norm[n]) for n, (eb, ef) in e_grad.items() if ef > 2 * eb + 1e-3 * g_norm[n] + 1e-12]
     assert not worse, worse
     if check_buffers:

@@ -69,6 +69,17 @@ def test_resnet_gemm_conv1x1_trains(dev):
     compare(dev, fused_bn=True, gemm_1x1=True)
 
 
+@pytest.mark.timeout(900)
+def test_resnet_fast_paths_at_bench_shape(dev):
+    """The shipped default backbone (fused BN+add+ReLU, GEMM 1x1 convs on the shipped engine plan)
+    at the bench's own shape, ResNet-50 b256 224x224 (BASELINE configs[1]), vs the fp32 torch
+    step: logits, every gradient and the BN running stats within 2x the error of torch's own
+    bf16 autocast step (2 seeds)."""
+    from bf16_step_compare import compare
+
+    compare(dev, fused_bn=True, gemm_1x1=True, check_buffers=True, batch=256, size=224, seeds=(0, 1))
+
+
 @pytest.mark.parametrize("down", [0, 1, 2])
 @pytest.mark.parametrize("owned", [False, True])
 @pytest.mark.parametrize("acc_engine", ["gemm", "conv"])
