@@ -17,6 +17,7 @@ Output (small .npz / .json data files, inputs and expected outputs only):
   auc_cases.npz        main.AUC + sklearn integer counts on tie-heavy cases
   partitions.json      sha256 of DataPartitioner index lists
   coda_w{1,2,4}.npz    per-rank trajectory of a 2-stage CoDA run on TinyNet
+  coda_w8_I*.npz       8 ranks at I = 1 (2 stages), 8 and 32 (3 stages): BASELINE configs[2]'s periods
 """
 from __future__ import annotations
 
@@ -173,7 +174,7 @@ def gen_partitions(dp):
 
 
 # ---------------------------------------------------------------- CoDA trajectory
-def _coda_rank(rank, world, port, outdir):
+def _coda_rank(rank, world, port, outdir, overrides=None, nbatches=32):
     import torch.distributed as dist
 
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -182,11 +183,11 @@ def _coda_rank(rank, world, port, outdir):
     torch.set_num_threads(1)
     main, _ = import_reference()
     main.size = world  # average_all reads the module-global `size` (main.py:52-54)
-    cfg = tinynet.CONFIG
+    cfg = dict(tinynet.CONFIG, **(overrides or {}))
     net = tinynet.TinyNet()
     net.load_state_dict(tinynet.initial_state())
-    xs, ys = tinynet.make_batches(rank, 32)
-    it = iter(range(32))
+    xs, ys = tinynet.make_batches(rank, nbatches)
+    it = iter(range(nbatches))
 
     def next_batch():
         k = next(it)
@@ -299,13 +300,15 @@ def _coda_rank(rank, world, port, outdir):
     dist.destroy_process_group()
 
 
-def gen_coda(world, port):
+def gen_coda(world, port, overrides=None, suffix="", nbatches=32):
+    """coda_w{world}{suffix}.npz; overrides replace tinynet.CONFIG entries (e.g. the averaging
+    period I and the stage count, for BASELINE configs[2]'s I sweep at 8 ranks)."""
     import tempfile
 
     import torch.multiprocessing as mp
 
     with tempfile.TemporaryDirectory() as td:
-        mp.spawn(_coda_rank, args=(world, port, td), nprocs=world, join=True)
+        mp.spawn(_coda_rank, args=(world, port, td, overrides, nbatches), nprocs=world, join=True)
         merged = {}
         for r in range(world):
             with np.load(Path(td) / f"rank{r}.npz") as z:
@@ -315,11 +318,24 @@ def gen_coda(world, port):
     for k, v in init.items():
         merged[f"init_{k}"] = v.numpy()
     merged["world"] = np.array(world)
-    merged["config"] = np.array(json.dumps(tinynet.CONFIG))
-    np.savez_compressed(HERE / f"coda_w{world}.npz", **merged)
+    merged["config"] = np.array(json.dumps(dict(tinynet.CONFIG, **(overrides or {}))))
+    np.savez_compressed(HERE / f"coda_w{world}{suffix}.npz", **merged)
+
+
+# BASELINE configs[2] (8 ranks, I in {1, 8, 32}) on TinyNet: 4 stages = 3 + 9 + 27 = 39 steps, so
+# I = 8 averages 4 times and I = 32 once; the stage-s alpha estimate reads 3^s batches per rank
+CODA_W8 = (("_I1", dict(I=1), 32), ("_I8_s4", dict(I=8, numStages=4), 80), ("_I32_s4", dict(I=32, numStages=4), 80))
 
 
 if __name__ == "__main__":
+    import sys
+
+    if sys.argv[1:] == ["coda8"]:  # only the 8-rank period fixtures
+        import_reference()
+        for i, (suffix, ov, nb) in enumerate(CODA_W8):
+            gen_coda(8, 29620 + i, ov, suffix, nb)
+        print("8-rank CoDA fixtures written to", HERE)
+        sys.exit(0)
     main, dp = import_reference()
     gen_surrogate()
     gen_dppd(main)
@@ -327,4 +343,6 @@ if __name__ == "__main__":
     gen_partitions(dp)
     for w, port in ((1, 29611), (2, 29612), (4, 29614)):
         gen_coda(w, port)
+    for i, (suffix, ov, nb) in enumerate(CODA_W8):
+        gen_coda(8, 29620 + i, ov, suffix, nb)
     print("golden fixtures written to", HERE)

@@ -1,4 +1,7 @@
-"""Multi-rank CoDA orchestration on CPU (gloo, world 1/2/4) vs the reference trajectory.
+"""Multi-rank CoDA orchestration on CPU (gloo, world 1/2/4/8) vs the reference trajectory.
+
+World 8 runs BASELINE configs[2]'s averaging periods I = 1, 8, 32 (coda_w8_I*.npz, made by the
+reference's own main.average_all over gloo at 8 ranks).
 
 The product's CoDA loop, FlatState bookkeeping (segment table, count slots in the
 all-reduced buffer, anchors, stage restarts) and its torch.distributed calls run
@@ -19,8 +22,8 @@ import coda_parity
 import cpu_kernels
 
 
-def _load(golden, world):
-    with np.load(golden / f"coda_w{world}.npz") as z:
+def _load(golden, world, suffix=""):
+    with np.load(golden / f"coda_w{world}{suffix}.npz") as z:
         return {k: z[k] for k in z.files}
 
 
@@ -41,7 +44,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, golden_dir, q):
+def _worker(rank, world, port, golden_dir, q, suffix=""):
     import traceback
     from pathlib import Path
 
@@ -53,7 +56,7 @@ def _worker(rank, world, port, golden_dir, q):
         os.environ["MASTER_ADDR"] = "127.0.0.1"
         os.environ["MASTER_PORT"] = str(port)
         dist.init_process_group("gloo", rank=rank, world_size=world)
-        fx = _load(Path(golden_dir), world)
+        fx = _load(Path(golden_dir), world, suffix)
         rec, coda = coda_parity.run_rank(fx, rank, world, torch.device("cpu"))
         coda_parity.compare(fx, rank, rec)
         # BN buffers are local (main.py:35): ranks must still differ after averaging
@@ -63,15 +66,15 @@ def _worker(rank, world, port, golden_dir, q):
         q.put((rank, traceback.format_exc()))
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world,suffix", [(2, ""), (4, ""), (8, "_I1"), (8, "_I8_s4"), (8, "_I32_s4")])
 @pytest.mark.timeout(300)
-def test_coda_multirank_gloo(golden, world):
+def test_coda_multirank_gloo(golden, world, suffix):
     import torch.multiprocessing as mp
 
     ctx = mp.get_context("spawn")
     q = ctx.SimpleQueue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, str(golden), q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, str(golden), q, suffix)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
@@ -85,5 +88,11 @@ def test_coda_multirank_gloo(golden, world):
     errs = [e for _, e in res if e]
     assert not errs, "\n".join(errs)
     assert sorted(r for r, _ in res) == list(range(world))
-    fx = _load(golden, world)
+    fx = _load(golden, world, suffix)
     assert not np.allclose(fx["r0_bn"][-1], fx["r1_bn"][-1])  # reference keeps BN buffers local
+    if world == 8:  # the period really varies the number of averaging rounds
+        import json
+
+        cfg = json.loads(str(fx["config"]))
+        steps = len(fx["r0_t_total"])
+        assert steps == (12 if cfg["numStages"] == 3 else 39) and steps // cfg["I"] >= 1

@@ -20,8 +20,8 @@ import coda_parity
 pytestmark = pytest.mark.gpu
 
 
-def _load(golden, world):
-    with np.load(golden / f"coda_w{world}.npz") as z:
+def _load(golden, world, suffix=""):
+    with np.load(golden / f"coda_w{world}{suffix}.npz") as z:
         return {k: z[k] for k in z.files}
 
 
@@ -152,7 +152,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, golden_dir, errq):
+def _worker(rank, world, port, golden_dir, errq, suffix=""):
     import torch.distributed as dist
     from pathlib import Path
 
@@ -160,7 +160,7 @@ def _worker(rank, world, port, golden_dir, errq):
         os.environ["MASTER_ADDR"] = "127.0.0.1"
         os.environ["MASTER_PORT"] = str(port)
         dist.init_process_group("gloo", rank=rank, world_size=world)
-        fx = _load(Path(golden_dir), world)
+        fx = _load(Path(golden_dir), world, suffix)
         rec, _ = coda_parity.run_rank(fx, rank, world, torch.device("cuda", 0))
         coda_parity.compare(fx, rank, rec)
         dist.destroy_process_group()
@@ -172,18 +172,21 @@ def _worker(rank, world, port, golden_dir, errq):
         raise SystemExit(1) from e
 
 
-@pytest.mark.timeout(240)
-def test_coda_round_world2_gloo_on_device(dev, golden):
+@pytest.mark.parametrize("world,suffix", [(2, ""), (8, "_I8_s4")])
+@pytest.mark.timeout(300)
+def test_coda_round_gloo_on_device(dev, golden, world, suffix):
+    """world ranks as gloo processes sharing cuda:0, the HIP kernels doing every step, vs the
+    reference's trajectory at that world size (8 ranks, I = 8: BASELINE configs[2]'s shape)."""
     import torch.multiprocessing as mp
 
     ctx = mp.get_context("spawn")
     q = ctx.SimpleQueue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, str(golden), q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, str(golden), q, suffix)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
-        p.join(200)
+        p.join(260)
     errs = []
     while not q.empty():
         errs.append(q.get())
@@ -192,4 +195,4 @@ def test_coda_round_world2_gloo_on_device(dev, golden):
             p.kill()
     bad = [e for _, e in errs if e]
     assert not bad, "\n".join(bad)
-    assert len(errs) == 2 and all(p.exitcode == 0 for p in procs)
+    assert len(errs) == world and all(p.exitcode == 0 for p in procs)
