@@ -562,6 +562,10 @@ def cpu_coda_worker(args):
     dist.destroy_process_group()
 
 
+_LAUNCH_VARS = ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK", "GROUP_WORLD_SIZE",
+                "ROLE_RANK", "ROLE_WORLD_SIZE", "ROLE_NAME", "MASTER_ADDR", "MASTER_PORT")
+
+
 def cpu_baseline_configs0(args, host):
     """configs[0]: 4 gloo CPU worker processes x (budget / 4) threads, ResNet-18 b32 224^2, I = 8
     ("4 processes x nproc/4 threads"). Child processes of this one (they never touch
@@ -571,8 +575,12 @@ def cpu_baseline_configs0(args, host):
     port = free_port()
     with tempfile.TemporaryDirectory() as td:
         out = Path(td) / "cw.json"
-        env = dict(os.environ, HIP_VISIBLE_DEVICES="", CUDA_VISIBLE_DEVICES="", ROCR_VISIBLE_DEVICES="",
-                   OMP_NUM_THREADS=str(threads))
+        # a job of their own: none of this rank's launcher variables (under torch.distributed.run,
+        # TORCHELASTIC_USE_AGENT_STORE would make their rendezvous wait for the agent's store)
+        env = {k: v for k, v in os.environ.items()
+               if not (k.startswith("TORCHELASTIC_") or k in _LAUNCH_VARS)}
+        env.update(HIP_VISIBLE_DEVICES="", CUDA_VISIBLE_DEVICES="", ROCR_VISIBLE_DEVICES="",
+                   OMP_NUM_THREADS=str(threads), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs = [subprocess.Popen([sys.executable, str(Path(__file__).resolve()), "--cpu-coda-worker",
                                    "--cpu-workers", str(W), "--cw-rank", str(r), "--cw-port", str(port),
                                    "--cw-threads", str(threads), "--cw-out", str(out),

@@ -47,10 +47,23 @@ def test_host_info_states_core_counts():
     assert h["nproc"] >= 1 and 1 <= h["cpu_budget"] <= h["affinity_cpus"]
 
 
+@pytest.mark.parametrize("under_launcher", [False, True])
 @pytest.mark.timeout(300)
-def test_configs0_cpu_baseline_gloo_workers():
+def test_configs0_cpu_baseline_gloo_workers(monkeypatch, under_launcher):
     """configs[0]'s CPU path: gloo worker processes running the restated step with one
-    average_all round (main.py:33-54) inside the timed window (small images to stay fast)."""
+    average_all round (main.py:33-54) inside the timed window (small images to stay fast).
+    under_launcher: called from rank 0 of a torch.distributed.run job (its env: the agent store,
+    another job's MASTER_PORT and world size), as at N > 1 — the workers must form their own job."""
+    if under_launcher:
+        import socket
+
+        with socket.socket() as s:
+            s.bind(("127.0.0.1", 0))
+            dead = s.getsockname()[1]
+        for k, v in dict(TORCHELASTIC_USE_AGENT_STORE="True", TORCHELASTIC_RUN_ID="none", MASTER_ADDR="127.0.0.1",
+                         MASTER_PORT=str(dead), RANK="0", WORLD_SIZE="8", LOCAL_RANK="0",
+                         LOCAL_WORLD_SIZE="8").items():
+            monkeypatch.setenv(k, v)
     b = _bench()
     args = b.parse(["--cpu-steps", "8", "--image-size", "32", "--cpu-workers", "2"])
     host = dict(b.host_info(), cpu_budget=2)
