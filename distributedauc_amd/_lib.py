@@ -66,6 +66,9 @@ SIGNATURES = {
     "dauc_sort_workspace_size": (_sz, [_i64]),
     "dauc_auc_counts_sorted": (_int, [_vp, _i64, _vp, _i64, _vp, _vp, _sz, _vp]),
     "dauc_auc_counts_sorted_labeled": (_int, [_vp, _i64, _vp, _vp, _int, _i64, _i64, _vp, _vp, _vp, _sz, _vp]),
+    "dauc_compact_workspace_size": (_sz, [_i64]),
+    "dauc_auc_eval_workspace_size": (_sz, [_i64]),
+    "dauc_auc_eval_counts": (_int, [_vp, _vp, _int, _i64, _vp, _vp, _sz, _vp]),
     "dauc_compact_positives": (_int, [_vp, _vp, _int, _i64, _vp, _vp, _vp, _sz, _vp]),
     "dauc_sort_keys": (_int, [_vp, _i64, _vp, _vp, _sz, _vp]),
     "dauc_bn_workspace_size": (_sz, [_i64, _int]),

@@ -77,6 +77,14 @@ class ExactAUC:
         y, s = _as_device_pair(label, scores, device)
         if y.numel() != s.numel():
             raise ValueError(f"Found input variables with inconsistent numbers of samples: {[y.numel(), s.numel()]}")
+        if self.method == "sort" and self.world == 1:
+            # one GPU: the whole evaluation is one blocking C call (same stages, no host work between)
+            W, T, P, N, nonfinite, other = ops.auc_eval_counts(s, y)
+            if nonfinite:
+                raise ValueError("Input y_score contains NaN or infinity.")
+            if other and torch.unique(y).numel() > 2:
+                raise ValueError("multiclass format is not supported")
+            return {"wins": W, "ties": T, "P": P, "N": N}
         if self.method == "pairs":
             # stable split: every rank sees the positives in the same order, so positive blocks shard
             pos, neg, stats = ops.split_scores(s, y)

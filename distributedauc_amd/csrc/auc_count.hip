@@ -267,19 +267,21 @@ int launch_split(const float* s, const LT* lab, int64_t n, float* pos_out, float
 // The sort method only needs the positives as a table (every negative is read in place by the
 // query kernel, which also checks it is finite), so this pass reads the LABELS of every score
 // (1 B each at int8) and the SCORE of each positive only: at 2^27 scores with 0.1 % positives it
-// moves 2 x 134 MB of labels instead of the stable split's 2 x 671 MB of scores + labels. The
-// output keeps the original order (a stable compaction: count, scan, write), so every rank that
-// compacts the same vector gets the same list.
+// moves 134 MB of labels instead of the stable split's 2 x 671 MB of scores + labels. The
+// output keeps the original order (a stable compaction), so every rank that compacts the same
+// vector gets the same list.
 //
 // Block tile: 256 threads x kCmpSlots groups of 16 labels; group k of thread t covers labels
 // tile0 + (k * 256 + t) * 16 + [0, 16) (each wave load instruction reads 1 KB contiguous at int8).
 
 constexpr int kCmpThreads = 256;
-constexpr int kCmpSlots = 4;
-constexpr int kCmpTile = kCmpThreads * 16 * kCmpSlots;  // 16384 labels per block
-static_assert(kCmpTile >= kSplitTile, "split_workspace_size() also sizes the compaction");
+constexpr int kCmpSlots = 8;
+constexpr int kCmpTile = kCmpThreads * 16 * kCmpSlots;  // 32768 labels per block
 
 int64_t compact_blocks(int64_t n) { return (n + kCmpTile - 1) / kCmpTile; }
+
+// per tile: positives, labels outside {-1, 1}
+inline size_t compact_ws_bytes(int64_t n) { return 64 + static_cast<size_t>(compact_blocks(n)) * 2 * sizeof(int); }
 
 // bytes == 0 -> 0x80 in that byte, 0 elsewhere (exact, no carries between bytes)
 __device__ __forceinline__ unsigned zero_bytes(unsigned v) {
@@ -328,13 +330,20 @@ __device__ __forceinline__ unsigned label_masks16(const LT* __restrict__ lab, in
     return pos;
 }
 
-// pass 1: per-block positive and other-label counts (blk[3b + 1], the non-finite slot, stays 0:
-// the positives' scores are checked by the write pass, the negatives' by the query kernel)
+// Two launches. (1) count: per tile, its positives and its labels outside {-1, 1}. (2) write:
+// every tile first sums the positive counts of the tiles before it (its 256 threads read them
+// strided from L2 and reduce: no scan launch, no inter-workgroup wait), then writes its positives'
+// scores at that offset in tile order; the last tile also sums every tile's counts into stats[].
+// A single-launch decoupled look-back was built and measured: with ~1 µs of work per tile and
+// ~2 µs per cross-XCD round trip its prefix frontier advances one 64-tile window per round trip
+// (2^27 labels: 298 µs against this form's count + write).
 template <typename LT>
 __global__ __launch_bounds__(kCmpThreads) void compact_count_kernel(const LT* __restrict__ lab, int64_t n,
-                                                                    int vec, int* __restrict__ blk) {
+                                                                    int vec, int* __restrict__ blk,
+                                                                    int64_t* __restrict__ stats) {
     __shared__ int part[2][kCmpThreads / kWave];
     const int64_t base = int64_t(blockIdx.x) * kCmpTile;
+    if (blockIdx.x == 0 && threadIdx.x == 0) stats[2] = 0;  // the write pass adds the non-finite positives
     int np = 0, no = 0;
     unsigned m[kCmpSlots];
 #pragma unroll
@@ -353,32 +362,66 @@ __global__ __launch_bounds__(kCmpThreads) void compact_count_kernel(const LT* __
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-        int t0 = 0, t2 = 0;
+        int t0 = 0, t1 = 0;
         for (int w = 0; w < kCmpThreads / kWave; ++w) {
             t0 += part[0][w];
-            t2 += part[1][w];
+            t1 += part[1][w];
         }
-        blk[3 * blockIdx.x + 0] = t0;
-        blk[3 * blockIdx.x + 1] = 0;
-        blk[3 * blockIdx.x + 2] = t2;
+        blk[blockIdx.x] = t0;
+        blk[gridDim.x + blockIdx.x] = t1;
     }
 }
 
-// pass 3: every positive's score goes to pos_out[pos_base[block] + its rank in the tile]; rank
-// order = group k, then thread, then the 16 labels of the group (original order).
+// sum of v[0..count) over the block (every thread gets it); count <= 2^31 entries of <= 2^15
+__device__ __forceinline__ long long block_sum_ints(const int* __restrict__ v, int64_t count, long long* red) {
+    long long acc = 0;
+    int64_t i0 = 0;
+    if ((reinterpret_cast<uintptr_t>(v) & 15u) == 0) {
+        // int4 loads, 4 in flight per thread per round: 4096 counts in one round
+        const int4* v4 = reinterpret_cast<const int4*>(v);
+        const int64_t nv = count / 4;
+        for (int64_t j = threadIdx.x; j < nv; j += 4 * kCmpThreads) {
+            int4 q[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int64_t jj = j + u * kCmpThreads;
+                q[u] = jj < nv ? v4[jj] : make_int4(0, 0, 0, 0);
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) acc += (long long)q[u].x + q[u].y + q[u].z + q[u].w;
+        }
+        i0 = nv * 4;
+    }
+    for (int64_t i = i0 + threadIdx.x; i < count; i += kCmpThreads) acc += v[i];
+    for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, kWave);
+    const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+    if (lane == 0) red[wid] = acc;
+    __syncthreads();
+    long long t = 0;
+#pragma unroll
+    for (int w = 0; w < kCmpThreads / kWave; ++w) t += red[w];
+    __syncthreads();
+    return t;
+}
+
+// every positive's score goes to pos_out[(positives of earlier tiles) + its rank in the tile]; rank
+// order = group k, then thread, then the 16 labels of the group (original order)
 template <typename LT>
 __global__ __launch_bounds__(kCmpThreads) void compact_write_kernel(
-    const float* __restrict__ s, const LT* __restrict__ lab, int64_t n, int vec,
-    const int64_t* __restrict__ pos_base, float* __restrict__ pos_out, unsigned long long* __restrict__ nonfinite) {
+    const float* __restrict__ s, const LT* __restrict__ lab, int64_t n, int vec, int* __restrict__ blk,
+    float* __restrict__ pos_out, int64_t* __restrict__ stats) {
     constexpr int kW = kCmpThreads / kWave;
     __shared__ int cnt[kCmpSlots][kW];
+    __shared__ long long red[kW];
     const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+    const int64_t nblk = gridDim.x;
     const int64_t base = int64_t(blockIdx.x) * kCmpTile;
     int no = 0;
     unsigned m[kCmpSlots];
 #pragma unroll
     for (int k = 0; k < kCmpSlots; ++k)
         m[k] = label_masks16(lab, base + (int64_t(k) * kCmpThreads + threadIdx.x) * 16, n, vec, no);
+    const int64_t pbase = block_sum_ints(blk, blockIdx.x, red);  // loads overlap the label loads above
     int excl[kCmpSlots];
 #pragma unroll
     for (int k = 0; k < kCmpSlots; ++k) {
@@ -393,7 +436,6 @@ __global__ __launch_bounds__(kCmpThreads) void compact_write_kernel(
         if (lane == kWave - 1) cnt[k][wid] = incl;
     }
     __syncthreads();
-    const int64_t pbase = pos_base[blockIdx.x];
     int run = 0, nf = 0;
 #pragma unroll
     for (int k = 0; k < kCmpSlots; ++k) {
@@ -412,25 +454,31 @@ __global__ __launch_bounds__(kCmpThreads) void compact_write_kernel(
             pos_out[r++] = v;
         }
     }
-    if (nf) atomicAdd(nonfinite, static_cast<unsigned long long>(nf));
+    if (nf) atomicAdd(reinterpret_cast<unsigned long long*>(stats + 2), static_cast<unsigned long long>(nf));
+    if (blockIdx.x == nblk - 1) {
+        // P = the positives before this tile + its own; the other-label total over every tile
+        const long long other = block_sum_ints(blk + nblk, nblk, red);
+        if (threadIdx.x == 0) {
+            stats[0] = pbase + run;
+            stats[1] = n - (pbase + run);
+            stats[3] = other;
+        }
+    }
 }
 
 template <typename LT>
 int launch_compact(const float* s, const LT* lab, int64_t n, float* pos_out, int64_t* stats, void* ws,
                    hipStream_t st) {
     const int64_t nblk = compact_blocks(n);
-    int64_t* pos_base = static_cast<int64_t*>(ws);
-    int* blk = reinterpret_cast<int*>(pos_base + nblk);
+    if (nblk > 0x7fffffffLL) return DAUC_EINVAL;
+    int* blk = static_cast<int*>(ws);
     const int vec = (reinterpret_cast<uintptr_t>(lab) & 15u) == 0;
-    hipLaunchKernelGGL(compact_count_kernel<LT>, dim3(nblk), dim3(kCmpThreads), 0, st, lab, n, vec, blk);
+    hipLaunchKernelGGL(compact_count_kernel<LT>, dim3(static_cast<unsigned>(nblk)), dim3(kCmpThreads), 0, st, lab, n,
+                       vec, blk, stats);
     int rc = launch_status();
     if (rc) return rc;
-    // stats = {P, n - P, 0, #other}; the write pass adds the non-finite positives into stats[2]
-    hipLaunchKernelGGL(split_scan_kernel, dim3(1), dim3(kScanThreads), 0, st, blk, nblk, n, pos_base, stats);
-    rc = launch_status();
-    if (rc) return rc;
-    hipLaunchKernelGGL(compact_write_kernel<LT>, dim3(nblk), dim3(kCmpThreads), 0, st, s, lab, n, vec, pos_base,
-                       pos_out, reinterpret_cast<unsigned long long*>(stats + 2));
+    hipLaunchKernelGGL(compact_write_kernel<LT>, dim3(static_cast<unsigned>(nblk)), dim3(kCmpThreads), 0, st, s, lab,
+                       n, vec, blk, pos_out, stats);
     return launch_status();
 }
 
@@ -652,11 +700,13 @@ int dauc_split_scores(const float* scores, const void* labels, int label_dtype, 
     }
 }
 
+size_t dauc_compact_workspace_size(int64_t n) { return compact_ws_bytes(n < 0 ? 0 : n); }
+
 int dauc_compact_positives(const float* scores, const void* labels, int label_dtype, int64_t n,
                            float* pos_out, int64_t* stats, void* workspace, size_t workspace_bytes,
                            dauc_stream_t stream) {
     if (n <= 0 || scores == nullptr || labels == nullptr || pos_out == nullptr || stats == nullptr ||
-        workspace == nullptr || workspace_bytes < dauc_split_workspace_size(n) ||
+        workspace == nullptr || workspace_bytes < dauc_compact_workspace_size(n) ||
         (reinterpret_cast<uintptr_t>(workspace) & 7u) || (reinterpret_cast<uintptr_t>(stats) & 7u))
         return DAUC_EINVAL;
     hipStream_t st = as_hip(stream);

@@ -1,0 +1,132 @@
+// One-call exact AUC counts on one GPU (the sort method), host orchestration in C++.
+//
+// Reference: imagenet/main.py:79-81, AUC(label, scores) = sklearn roc_curve(pos_label=1) + auc,
+// a blocking host call. This entry point is its blocking counterpart: it enqueues the
+// compaction, reads the class sizes back (the sort needs the table size), enqueues the sort,
+// the tree and the query pass, and reads the integer counts back. The stages are the ABI calls
+// dauc_compact_positives and dauc_auc_counts_sorted_labeled (or, when the positives outnumber
+// the negatives, dauc_split_scores and dauc_auc_counts_sorted), so it returns exactly their
+// integers; what it removes is the host work between them: on the Python path each readback
+// was followed by ~45 us of interpreter work and small torch launches before the sort began
+// (profiles/r02/final/bench_kernel_trace gaps), here it is a few HIP calls.
+
+#include <hip/hip_runtime.h>
+
+#include "dauc.h"
+#include "dauc_internal.h"
+
+namespace dauc {
+namespace {
+
+inline size_t align256(size_t b) { return (b + 255) / 256 * 256; }
+
+// pinned host words for the two readbacks (one set per host thread, allocated on first use)
+int64_t* pinned_words() {
+    static thread_local int64_t* p = nullptr;
+    if (p == nullptr) {
+        void* q = nullptr;
+        if (hipHostMalloc(&q, 64 * sizeof(int64_t), hipHostMallocDefault) != hipSuccess) return nullptr;
+        p = static_cast<int64_t*>(q);
+    }
+    return p;
+}
+
+struct EvalWs {
+    float* pos;                   // [n]   positive scores (P <= n)
+    float* neg;                   // [n/2] negative scores (only when P > N, so N < n/2)
+    int64_t* stats;               // [4]   compaction / split stats
+    unsigned long long* wt;       // [3]   wins, ties, non-finite queried scores
+    void* cws;                    // compaction workspace
+    void* sws;                    // split workspace
+    void* tws;                    // sort + tree workspace (table of at most n/2 keys)
+    size_t cws_bytes, sws_bytes, tws_bytes;
+};
+
+EvalWs eval_ws(void* ws, int64_t n) {
+    char* p = static_cast<char*>(ws);
+    EvalWs w;
+    w.stats = reinterpret_cast<int64_t*>(p);
+    w.wt = reinterpret_cast<unsigned long long*>(p + 64);
+    p += 256;
+    w.pos = reinterpret_cast<float*>(p);
+    p += align256(size_t(n) * 4);
+    w.neg = reinterpret_cast<float*>(p);
+    p += align256(size_t(n / 2 + 1) * 4);
+    w.cws_bytes = dauc_compact_workspace_size(n);
+    w.cws = p;
+    p += align256(w.cws_bytes);
+    w.sws_bytes = dauc_split_workspace_size(n);
+    w.sws = p;
+    p += align256(w.sws_bytes);
+    w.tws_bytes = dauc_sort_workspace_size(n / 2 + 1);
+    w.tws = p;
+    return w;
+}
+
+size_t eval_ws_bytes(int64_t n) {
+    return 256 + align256(size_t(n) * 4) + align256(size_t(n / 2 + 1) * 4) + align256(dauc_compact_workspace_size(n)) +
+           align256(dauc_split_workspace_size(n)) + align256(dauc_sort_workspace_size(n / 2 + 1));
+}
+
+}  // namespace
+}  // namespace dauc
+
+using namespace dauc;
+
+extern "C" {
+
+size_t dauc_auc_eval_workspace_size(int64_t n) { return eval_ws_bytes(n < 1 ? 1 : n); }
+
+int dauc_auc_eval_counts(const float* scores, const void* labels, int label_dtype, int64_t n, int64_t* out,
+                         void* workspace, size_t workspace_bytes, dauc_stream_t stream) {
+    if (n <= 0 || scores == nullptr || labels == nullptr || out == nullptr || workspace == nullptr ||
+        workspace_bytes < eval_ws_bytes(n) || (reinterpret_cast<uintptr_t>(workspace) & 255u))
+        return DAUC_EINVAL;
+    if (label_dtype != DAUC_LABEL_I8 && label_dtype != DAUC_LABEL_I32 && label_dtype != DAUC_LABEL_I64)
+        return DAUC_EINVAL;
+    int64_t* host = pinned_words();
+    if (host == nullptr) return -static_cast<int>(hipErrorOutOfMemory);
+    hipStream_t st = as_hip(stream);
+    const EvalWs w = eval_ws(workspace, n);
+    hipError_t e = hipMemsetAsync(w.wt, 0, 3 * sizeof(unsigned long long), st);  // ahead of the compaction
+    if (e != hipSuccess) return -static_cast<int>(e);
+    int rc = dauc_compact_positives(scores, labels, label_dtype, n, w.pos, w.stats, w.cws, w.cws_bytes, stream);
+    if (rc) return rc;
+    if ((e = hipMemcpyAsync(host, w.stats, 4 * sizeof(int64_t), hipMemcpyDeviceToHost, st)) != hipSuccess ||
+        (e = hipStreamSynchronize(st)) != hipSuccess)
+        return -static_cast<int>(e);
+    int64_t P = host[0], N = host[1], nonfinite = host[2];
+    const int64_t other = host[3];
+    if (P > 0 && N > 0 && nonfinite == 0) {
+        if (P <= N) {
+            // the positives are the table; every other score is a query read in place
+            rc = dauc_auc_counts_sorted_labeled(w.pos, P, scores, labels, label_dtype, 0, n, w.wt, w.wt + 2, w.tws,
+                                                w.tws_bytes, stream);
+        } else {
+            // the negatives are the smaller class: materialise both (the split checks every score)
+            rc = dauc_split_scores(scores, labels, label_dtype, n, w.pos, w.neg, w.stats, w.sws, w.sws_bytes, stream);
+            if (rc) return rc;
+            if ((e = hipMemcpyAsync(host, w.stats, 4 * sizeof(int64_t), hipMemcpyDeviceToHost, st)) != hipSuccess ||
+                (e = hipStreamSynchronize(st)) != hipSuccess)
+                return -static_cast<int>(e);
+            P = host[0];
+            N = host[1];
+            nonfinite = host[2];
+            if (nonfinite == 0)
+                rc = dauc_auc_counts_sorted(w.pos, P, w.neg, N, w.wt, w.tws, w.tws_bytes, stream);
+        }
+        if (rc) return rc;
+    }
+    if ((e = hipMemcpyAsync(host + 8, w.wt, 3 * sizeof(unsigned long long), hipMemcpyDeviceToHost, st)) != hipSuccess ||
+        (e = hipStreamSynchronize(st)) != hipSuccess)
+        return -static_cast<int>(e);
+    out[0] = host[8];
+    out[1] = host[9];
+    out[2] = P;
+    out[3] = N;
+    out[4] = nonfinite + host[10];
+    out[5] = other;
+    return DAUC_OK;
+}
+
+}  // extern "C"

@@ -128,74 +128,110 @@ __global__ __launch_bounds__(kScanBlock) void scan_add_kernel(unsigned* __restri
 // totals): a small sort (<= kFusedScanTiles tiles) then needs no scan launches at all.
 constexpr int64_t kFusedScanTiles = 256;
 
+// exclusive scan of v over the block's 256 threads (thread t holds digit t): wave scans by
+// shuffles, then the wave totals through LDS (one barrier); returns the exclusive prefix
+__device__ __forceinline__ unsigned block_excl_scan256(unsigned v, unsigned* wtot) {
+    static_assert(kSortThreads == 256, "4 waves");
+    const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+    unsigned incl = v;
+#pragma unroll
+    for (int off = 1; off < kWave; off <<= 1) {
+        const unsigned t = __shfl_up(incl, off, kWave);
+        if (lane >= off) incl += t;
+    }
+    if (lane == kWave - 1) wtot[wid] = incl;
+    __syncthreads();
+    unsigned before = 0;
+#pragma unroll
+    for (int w = 0; w < kSortThreads / kWave; ++w) before += w < wid ? wtot[w] : 0u;
+    return before + incl - v;
+}
+
+// Stable scatter of one tile. Wave w owns the tile's contiguous keys [w * 512, (w + 1) * 512),
+// read as 8 chunks of 64 (one per lane). A key's rank among its wave's keys with the same digit
+// = the wave's running count of that digit (wave-private LDS row: a wave's LDS reads and writes
+// are ordered, so no barrier) + the same-digit lanes below it in its chunk (8 ballots: wave
+// multisplit). One barrier, then per digit the waves' counts become offsets, and every key goes
+// to base[digit] + offset[wave][digit] + rank: 2 barriers per pass instead of 4 per chunk.
 template <bool FROM_FLOAT, bool FUSED_SCAN>
 __global__ __launch_bounds__(kSortThreads) void radix_scatter_kernel(const void* __restrict__ in, int64_t n,
                                                                      int shift,
                                                                      const unsigned* __restrict__ offs,
                                                                      int64_t ntiles,
                                                                      unsigned* __restrict__ out) {
-    __shared__ unsigned base[kRadix];                       // running output position per digit
-    __shared__ unsigned wcnt[kSortThreads / kWave][kRadix];  // per-wave digit counts of a chunk
+    constexpr int kWaves = kSortThreads / kWave;
+    constexpr int kChunks = kTile / kSortThreads;  // chunks of 64 keys per wave
+    __shared__ unsigned base[kRadix];             // output start of each digit for this tile
+    __shared__ unsigned wcnt[kWaves][kRadix];     // per-wave running digit counts, then offsets
+    __shared__ unsigned wtot[kWaves];
     const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+    const unsigned long long lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+    const int64_t t0 = int64_t(blockIdx.x) * kTile + int64_t(wid) * (kChunks * kWave);
+    unsigned key[kChunks];
+#pragma unroll
+    for (int c = 0; c < kChunks; ++c) {
+        const int64_t i = t0 + c * kWave + lane;
+        key[c] = 0u;
+        if (i < n)
+            key[c] = FROM_FLOAT ? key_of(static_cast<const float*>(in)[i]) : static_cast<const unsigned*>(in)[i];
+    }
+    // this tile's digit bases (thread t = digit t)
     if constexpr (FUSED_SCAN) {
         static_assert(kSortThreads == kRadix, "one thread per digit");
         const unsigned* h = offs + int64_t(threadIdx.x) * ntiles;
         unsigned before = 0, total = 0;
-        for (int64_t b = 0; b < ntiles; ++b) {
+        int64_t b = 0;
+        for (; b + 4 <= ntiles; b += 4) {
+            const unsigned c0 = h[b], c1 = h[b + 1], c2 = h[b + 2], c3 = h[b + 3];
+            before += (b < blockIdx.x ? c0 : 0u) + (b + 1 < blockIdx.x ? c1 : 0u) + (b + 2 < blockIdx.x ? c2 : 0u) +
+                      (b + 3 < blockIdx.x ? c3 : 0u);
+            total += c0 + c1 + c2 + c3;
+        }
+        for (; b < ntiles; ++b) {
             const unsigned c = h[b];
             before += b < blockIdx.x ? c : 0u;
             total += c;
         }
-        // exclusive scan of the digit totals (Hillis-Steele over the 256 digits, in wcnt[0])
-        unsigned* sc = wcnt[0];
-        sc[threadIdx.x] = total;
-        __syncthreads();
-        for (int d = 1; d < kRadix; d <<= 1) {
-            const unsigned v = threadIdx.x >= d ? sc[threadIdx.x - d] : 0u;
-            __syncthreads();
-            sc[threadIdx.x] += v;
-            __syncthreads();
-        }
-        base[threadIdx.x] = sc[threadIdx.x] - total + before;
-        __syncthreads();
+        base[threadIdx.x] = block_excl_scan256(total, wtot) + before;
     } else {
         base[threadIdx.x] = offs[int64_t(threadIdx.x) * ntiles + blockIdx.x];
     }
-    const unsigned long long lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-    const int64_t t0 = int64_t(blockIdx.x) * kTile;
-    for (int k = 0; k < kPerThread; ++k) {
-        const int64_t i = t0 + int64_t(k) * kSortThreads + threadIdx.x;
-        const bool valid = i < n;
-        unsigned key = 0;
-        if (valid)
-            key = FROM_FLOAT ? key_of(static_cast<const float*>(in)[i]) : static_cast<const unsigned*>(in)[i];
-        const unsigned d = (key >> shift) & 0xffu;
-        // lanes of this wave holding the same digit (wave multisplit)
+#pragma unroll
+    for (int q = 0; q < kRadix / kWave; ++q) wcnt[wid][q * kWave + lane] = 0u;
+    unsigned rank[kChunks];
+#pragma unroll
+    for (int c = 0; c < kChunks; ++c) {
+        const bool valid = t0 + c * kWave + lane < n;
+        const unsigned d = (key[c] >> shift) & 0xffu;
         unsigned long long same = __ballot(valid);
 #pragma unroll
-        for (int b = 0; b < 8; ++b) {
-            const unsigned long long m = __ballot((d >> b) & 1u);
-            same &= ((d >> b) & 1u) ? m : ~m;
+        for (int bit = 0; bit < 8; ++bit) {
+            const unsigned long long m = __ballot((d >> bit) & 1u);
+            same &= ((d >> bit) & 1u) ? m : ~m;
         }
-        // clear this chunk's wave counts, then publish each digit's count from its first lane
+        const unsigned below = __popcll(same & lt);
+        const unsigned run = valid ? wcnt[wid][d] : 0u;  // every same-digit lane reads before the leader writes
+        rank[c] = run + below;
+        if (valid && below == 0) wcnt[wid][d] = run + __popcll(same);
+    }
+    __syncthreads();
+    {
+        // offsets of the waves within each digit (thread t = digit t)
+        unsigned run = 0;
 #pragma unroll
-        for (int w = 0; w < kSortThreads / kWave; ++w) wcnt[w][threadIdx.x] = 0;
-        __syncthreads();
-        const unsigned rank_in_wave = __popcll(same & lt);
-        if (valid && rank_in_wave == 0) wcnt[wid][d] = __popcll(same);
-        __syncthreads();
-        if (valid) {
-            unsigned before = 0;
-            for (int w = 0; w < wid; ++w) before += wcnt[w][d];
-            out[base[d] + before + rank_in_wave] = key;
+        for (int w = 0; w < kWaves; ++w) {
+            const unsigned c = wcnt[w][threadIdx.x];
+            wcnt[w][threadIdx.x] = run;
+            run += c;
         }
-        __syncthreads();
-        // advance the running base of every digit by this chunk's count
-        unsigned tot = 0;
+    }
+    __syncthreads();
 #pragma unroll
-        for (int w = 0; w < kSortThreads / kWave; ++w) tot += wcnt[w][threadIdx.x];
-        base[threadIdx.x] += tot;
-        __syncthreads();
+    for (int c = 0; c < kChunks; ++c) {
+        if (t0 + c * kWave + lane < n) {
+            const unsigned d = (key[c] >> shift) & 0xffu;
+            out[base[d] + wcnt[wid][d] + rank[c]] = key[c];
+        }
     }
 }
 

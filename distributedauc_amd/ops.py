@@ -340,6 +340,27 @@ def split_scores(scores: torch.Tensor, labels: torch.Tensor, negatives: bool = T
     return pos, neg, stats
 
 
+def auc_eval_counts(scores: torch.Tensor, labels: torch.Tensor) -> tuple:
+    """The single-GPU sort-method evaluation in one blocking ABI call (dauc_auc_eval_counts):
+    (W, T, P, N, #non-finite scores, #labels not in {-1, 1}) as Python ints."""
+    _require(scores, "scores", torch.float32)
+    dev = scores.device
+    lc = _label_code(labels, "labels")
+    if scores.dim() != 1 or labels.dim() != 1 or scores.shape != labels.shape:
+        raise ValueError("scores and labels must be 1-D of equal length")
+    if not scores.is_contiguous() or not labels.is_contiguous():
+        raise ValueError("scores and labels must be contiguous")
+    n = scores.numel()
+    if n == 0:
+        raise ValueError("empty score vector")
+    L = _lib.load()
+    ws = workspaces.get(dev, "auc_eval", L.dauc_auc_eval_workspace_size(n))
+    out = (ctypes.c_int64 * 6)()
+    check(L.dauc_auc_eval_counts(_ptr(scores), _ptr(labels), lc, n, ctypes.cast(out, ctypes.c_void_p), _ptr(ws),
+                                 ws.numel(), _stream(dev)), "dauc_auc_eval_counts")
+    return tuple(int(v) for v in out)
+
+
 def compact_positives(scores: torch.Tensor, labels: torch.Tensor):
     """Positive scores (label == 1) in original order, reading only the labels and the positives' scores.
 
@@ -359,7 +380,7 @@ def compact_positives(scores: torch.Tensor, labels: torch.Tensor):
     pos = torch.empty(n, dtype=torch.float32, device=dev)
     stats = torch.empty(4, dtype=torch.int64, device=dev)
     L = _lib.load()
-    ws = workspaces.get(dev, "split", L.dauc_split_workspace_size(n))
+    ws = workspaces.get(dev, "compact", L.dauc_compact_workspace_size(n))
     check(L.dauc_compact_positives(_ptr(scores), _ptr(labels), lc, n, _ptr(pos), _ptr(stats), _ptr(ws),
                                    ws.numel(), _stream(dev)), "dauc_compact_positives")
     return pos, stats

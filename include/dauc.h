@@ -232,12 +232,14 @@ int dauc_split_scores(const float* scores, const void* labels, int label_dtype, 
  * Stable compaction of the positive scores (label == 1) for the sort method of main.py:79-81
  * (sklearn roc_curve(pos_label=1) -> _binary_clf_curve, _ranking.py:826-908): every label is
  * read once and only the positives' scores are read, so a vector with few positives costs
- * about one label pass (1 B per score at int8) instead of a full split.
+ * about two label passes (1 B per score at int8) instead of a full split. Two launches (per-tile
+ * counts; a write pass in which every tile sums the counts before it itself).
  *   pos_out[0..P) = the positive scores in original order (capacity n)
  *   stats[4] (int64) = { P, n - P, #non-finite POSITIVE scores, #labels not in {-1, 1} }
  * The negatives' scores are checked by dauc_auc_counts_sorted_labeled (its nonfinite count).
- * workspace >= dauc_split_workspace_size(n), zero-initialised.
+ * workspace >= dauc_compact_workspace_size(n) bytes, 8-byte aligned; no zeroing needed.
  */
+size_t dauc_compact_workspace_size(int64_t n);
 int dauc_compact_positives(const float* scores, const void* labels, int label_dtype, int64_t n,
                            float* pos_out, int64_t* stats, void* workspace, size_t workspace_bytes,
                            dauc_stream_t stream);
@@ -291,6 +293,21 @@ int dauc_auc_counts_sorted_labeled(const float* pos, int64_t P, const float* sco
                                    int label_dtype, int64_t begin, int64_t end, unsigned long long* wins_ties,
                                    unsigned long long* nonfinite, void* workspace, size_t workspace_bytes,
                                    dauc_stream_t stream);
+
+/*
+ * The whole single-GPU exact-AUC evaluation of main.py:79-81 in ONE blocking call (sklearn's
+ * roc_curve + auc is a blocking host call too): positive compaction, a readback of the class
+ * sizes, the radix sort of the smaller class, the tree and the query pass, a readback of the
+ * counts. Same integers as the stage-by-stage calls it chains. The exception to the
+ * conventions above: it synchronises `stream` (twice; three times when P > N) and keeps one
+ * small pinned host buffer per calling thread, allocated on first use.
+ *   out[6] (HOST int64) = { W, T, P, N, #non-finite scores, #labels not in {-1, 1} }
+ *   (W = T = 0 when a class is empty or a score is non-finite: the caller raises like sklearn)
+ * workspace >= dauc_auc_eval_workspace_size(n) bytes, 256-byte aligned; no zeroing needed.
+ */
+size_t dauc_auc_eval_workspace_size(int64_t n);
+int dauc_auc_eval_counts(const float* scores, const void* labels, int label_dtype, int64_t n, int64_t* out,
+                         void* workspace, size_t workspace_bytes, dauc_stream_t stream);
 
 /* The radix sort alone: keys_out[0..n) = ascending order-preserving keys of scores (testing). */
 int dauc_sort_keys(const float* scores, int64_t n, unsigned* keys_out, void* workspace,

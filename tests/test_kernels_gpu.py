@@ -419,12 +419,15 @@ def test_split_is_stable(dev):
 def test_compact_positives(dev, ldtype):
     """Stable positive compaction (labels read once, positives' scores only): same list as
     s[y == 1], stats = {P, n - P, #non-finite positives, #labels not in {-1, 1}}; ragged sizes
-    around the 16-label groups and the 16384-label tile, misaligned label slices, p = 0 / 1."""
+    around the 16-label groups and the 32768-label tile, misaligned label slices, p = 0 / 1,
+    growing and shrinking n on one workspace (2^24 + 5: 513 tiles, each summing the counts of
+    the tiles before it)."""
     from distributedauc_amd import ops
 
     rng = np.random.default_rng(31)
-    for n, p, off in ((1, 1.0, 0), (15, 0.5, 0), (16, 0.5, 1), (17, 0.3, 0), (16384, 0.01, 0), (16385, 0.0, 0),
-                      (16387, 1.0, 3), (300_001, 0.02, 1), (2_000_003, 0.001, 0), (1 << 20, 0.5, 0)):
+    for n, p, off in ((1, 1.0, 0), (15, 0.5, 0), (16, 0.5, 1), (17, 0.3, 0), (16384, 0.01, 0), (32768, 0.01, 0), (32769, 0.0, 0),
+                      (32771, 1.0, 3), (300_001, 0.02, 1), (2_000_003, 0.001, 0), (1 << 20, 0.5, 0),
+                      ((1 << 24) + 5, 0.3, 0), (40_000, 0.9, 2), (1 << 22, 1.0, 0)):
         sall = rng.standard_normal(n + off).astype(np.float32)
         yall = np.where(rng.random(n + off) < p, 1, -1).astype(ldtype)
         if n > 100:
@@ -438,6 +441,40 @@ def test_compact_positives(dev, ldtype):
         other = int(((y != 1) & (y != -1)).sum())
         assert stats.cpu().tolist() == [P, n - P, nf, other], (n, p, off)
         assert np.array_equal(pos[:P].cpu().numpy(), s[y == 1], equal_nan=True), (n, p, off)
+
+
+@pytest.mark.parametrize("ldtype", [np.int8, np.int32, np.int64])
+def test_auc_eval_counts_one_call(dev, ldtype):
+    """dauc_auc_eval_counts (the single-GPU evaluation in one blocking call) vs the C oracle:
+    P < N (positives are the table), P > N (split, negatives are the table), P == N, one class
+    empty, labels 0 counted as negatives and as "other", a non-finite positive or negative
+    reported (and no counts), ragged sizes; and the workspace reused across sizes."""
+    from distributedauc_amd import ops
+
+    rng = np.random.default_rng(77)
+    cases = [(1, 1.0), (2, 0.5), (1000, 0.0), (1000, 1.0), (4097, 0.5), (300_001, 0.02), (300_001, 0.9),
+             (1 << 20, 0.5), (2_000_003, 0.001), (65_536, 0.75)]
+    for n, p in cases:
+        s = (np.floor(rng.random(n) * 3000) / 3000).astype(np.float32)
+        y = np.where(rng.random(n) < p, 1, -1).astype(ldtype)
+        if n > 100:
+            y[rng.random(n) < 0.002] = 0
+        W, Tt, P, N, bad, other = ops.auc_eval_counts(T(s, dev), T(y, dev))
+        e = coracle.auc_counts(y.astype(np.int64), s)
+        assert (P, N, bad, other) == (e["P"], e["N"], 0, int((y == 0).sum())), (n, p)
+        if P and N:
+            assert (W, Tt) == (e["wins"], e["ties"]), (n, p)
+        else:
+            assert (W, Tt) == (0, 0)
+    for where in ("pos", "neg"):
+        for p in (0.01, 0.99):  # both table sides
+            n = 100_003
+            s = rng.random(n, dtype=np.float32)
+            y = np.where(rng.random(n) < p, 1, -1).astype(ldtype)
+            j = int(np.flatnonzero(y == (1 if where == "pos" else -1))[3])
+            s[j] = np.inf if where == "pos" else np.nan
+            W, Tt, P, N, bad, other = ops.auc_eval_counts(T(s, dev), T(y, dev))
+            assert bad >= 1, (where, p)
 
 
 def test_auc_sort_rejects_nonfinite_negatives(dev):
