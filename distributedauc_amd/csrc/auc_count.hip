@@ -340,10 +340,14 @@ __device__ __forceinline__ unsigned label_masks16(const LT* __restrict__ lab, in
 template <typename LT>
 __global__ __launch_bounds__(kCmpThreads) void compact_count_kernel(const LT* __restrict__ lab, int64_t n,
                                                                     int vec, int* __restrict__ blk,
-                                                                    int64_t* __restrict__ stats) {
+                                                                    int64_t* __restrict__ stats,
+                                                                    unsigned long long* __restrict__ zero3) {
     __shared__ int part[2][kCmpThreads / kWave];
     const int64_t base = int64_t(blockIdx.x) * kCmpTile;
-    if (blockIdx.x == 0 && threadIdx.x == 0) stats[2] = 0;  // the write pass adds the non-finite positives
+    if (blockIdx.x == 0 && threadIdx.x < 4) {
+        if (threadIdx.x == 0) stats[2] = 0;  // the write pass adds the non-finite positives
+        else if (zero3 != nullptr) zero3[threadIdx.x - 1] = 0;  // a later stage's counters (dauc_auc_eval_counts)
+    }
     int np = 0, no = 0;
     unsigned m[kCmpSlots];
 #pragma unroll
@@ -468,13 +472,13 @@ __global__ __launch_bounds__(kCmpThreads) void compact_write_kernel(
 
 template <typename LT>
 int launch_compact(const float* s, const LT* lab, int64_t n, float* pos_out, int64_t* stats, void* ws,
-                   hipStream_t st) {
+                   hipStream_t st, unsigned long long* zero3 = nullptr) {
     const int64_t nblk = compact_blocks(n);
     if (nblk > 0x7fffffffLL) return DAUC_EINVAL;
     int* blk = static_cast<int*>(ws);
     const int vec = (reinterpret_cast<uintptr_t>(lab) & 15u) == 0;
     hipLaunchKernelGGL(compact_count_kernel<LT>, dim3(static_cast<unsigned>(nblk)), dim3(kCmpThreads), 0, st, lab, n,
-                       vec, blk, stats);
+                       vec, blk, stats, zero3);
     int rc = launch_status();
     if (rc) return rc;
     hipLaunchKernelGGL(compact_write_kernel<LT>, dim3(static_cast<unsigned>(nblk)), dim3(kCmpThreads), 0, st, s, lab,
@@ -702,24 +706,37 @@ int dauc_split_scores(const float* scores, const void* labels, int label_dtype, 
 
 size_t dauc_compact_workspace_size(int64_t n) { return compact_ws_bytes(n < 0 ? 0 : n); }
 
-int dauc_compact_positives(const float* scores, const void* labels, int label_dtype, int64_t n,
-                           float* pos_out, int64_t* stats, void* workspace, size_t workspace_bytes,
-                           dauc_stream_t stream) {
+}  // extern "C"
+
+namespace dauc {
+// dauc_compact_positives that also zeroes 3 counters of a later stage in its first launch
+int compact_positives_zeroing(const float* scores, const void* labels, int label_dtype, int64_t n, float* pos_out,
+                              int64_t* stats, void* workspace, size_t workspace_bytes, unsigned long long* zero3,
+                              hipStream_t st) {
     if (n <= 0 || scores == nullptr || labels == nullptr || pos_out == nullptr || stats == nullptr ||
         workspace == nullptr || workspace_bytes < dauc_compact_workspace_size(n) ||
         (reinterpret_cast<uintptr_t>(workspace) & 7u) || (reinterpret_cast<uintptr_t>(stats) & 7u))
         return DAUC_EINVAL;
-    hipStream_t st = as_hip(stream);
     switch (label_dtype) {
         case DAUC_LABEL_I8:
-            return launch_compact(scores, static_cast<const int8_t*>(labels), n, pos_out, stats, workspace, st);
+            return launch_compact(scores, static_cast<const int8_t*>(labels), n, pos_out, stats, workspace, st, zero3);
         case DAUC_LABEL_I32:
-            return launch_compact(scores, static_cast<const int32_t*>(labels), n, pos_out, stats, workspace, st);
+            return launch_compact(scores, static_cast<const int32_t*>(labels), n, pos_out, stats, workspace, st, zero3);
         case DAUC_LABEL_I64:
-            return launch_compact(scores, static_cast<const int64_t*>(labels), n, pos_out, stats, workspace, st);
+            return launch_compact(scores, static_cast<const int64_t*>(labels), n, pos_out, stats, workspace, st, zero3);
         default:
             return DAUC_EINVAL;
     }
+}
+}  // namespace dauc
+
+extern "C" {
+
+int dauc_compact_positives(const float* scores, const void* labels, int label_dtype, int64_t n,
+                           float* pos_out, int64_t* stats, void* workspace, size_t workspace_bytes,
+                           dauc_stream_t stream) {
+    return compact_positives_zeroing(scores, labels, label_dtype, n, pos_out, stats, workspace, workspace_bytes,
+                                     nullptr, as_hip(stream));
 }
 
 int dauc_pair_count(const float* pos, int64_t P, const float* neg, int64_t N,

@@ -63,6 +63,18 @@ EvalWs eval_ws(void* ws, int64_t n) {
     return w;
 }
 
+// the last evaluation's table size for its length and label type (one per host thread)
+struct EvalMemo {
+    int64_t n;
+    int dtype;
+    int64_t P;
+};
+
+EvalMemo& eval_memo() {
+    static thread_local EvalMemo m{0, 0, 0};
+    return m;
+}
+
 size_t eval_ws_bytes(int64_t n) {
     return 256 + align256(size_t(n) * 4) + align256(size_t(n / 2 + 1) * 4) + align256(dauc_compact_workspace_size(n)) +
            align256(dauc_split_workspace_size(n)) + align256(dauc_sort_workspace_size(n / 2 + 1));
@@ -88,43 +100,60 @@ int dauc_auc_eval_counts(const float* scores, const void* labels, int label_dtyp
     if (host == nullptr) return -static_cast<int>(hipErrorOutOfMemory);
     hipStream_t st = as_hip(stream);
     const EvalWs w = eval_ws(workspace, n);
-    hipError_t e = hipMemsetAsync(w.wt, 0, 3 * sizeof(unsigned long long), st);  // ahead of the compaction
-    if (e != hipSuccess) return -static_cast<int>(e);
-    int rc = dauc_compact_positives(scores, labels, label_dtype, n, w.pos, w.stats, w.cws, w.cws_bytes, stream);
+    hipError_t e;
+    // stats [0, 32) and the counts [64, 88) come back in one copy
+    auto readback = [&]() -> int {
+        if ((e = hipMemcpyAsync(host, w.stats, 88, hipMemcpyDeviceToHost, st)) != hipSuccess ||
+            (e = hipStreamSynchronize(st)) != hipSuccess)
+            return -static_cast<int>(e);
+        return DAUC_OK;
+    };
+    auto query = [&](int64_t P) {
+        return dauc_auc_counts_sorted_labeled(w.pos, P, scores, labels, label_dtype, 0, n, w.wt, w.wt + 2, w.tws,
+                                              w.tws_bytes, stream);
+    };
+    // The table size P is known only after the compaction. An evaluation repeats on the same
+    // test set (main.py evaluates it after every stage), so the last call's P for this n is
+    // taken as the size and the sort and query are enqueued behind the compaction WITHOUT a
+    // readback in between; the one readback at the end returns the real P with the counts, and a
+    // different P (other data of the same length) re-runs the sort and query at the real size.
+    EvalMemo& memo = eval_memo();
+    const bool speculate = memo.n == n && memo.dtype == label_dtype && memo.P > 0 && memo.P <= n - memo.P;
+    // the compaction's first launch also zeroes the query's counters
+    int rc = compact_positives_zeroing(scores, labels, label_dtype, n, w.pos, w.stats, w.cws, w.cws_bytes, w.wt, st);
     if (rc) return rc;
-    if ((e = hipMemcpyAsync(host, w.stats, 4 * sizeof(int64_t), hipMemcpyDeviceToHost, st)) != hipSuccess ||
-        (e = hipStreamSynchronize(st)) != hipSuccess)
-        return -static_cast<int>(e);
+    if (speculate && (rc = query(memo.P))) return rc;
+    if ((rc = readback())) return rc;
     int64_t P = host[0], N = host[1], nonfinite = host[2];
     const int64_t other = host[3];
-    if (P > 0 && N > 0 && nonfinite == 0) {
+    bool counted = speculate && P == memo.P;
+    memo = EvalMemo{n, label_dtype, P};
+    if (!counted && P > 0 && N > 0 && nonfinite == 0) {
+        if ((e = hipMemsetAsync(w.wt, 0, 3 * sizeof(unsigned long long), st)) != hipSuccess)
+            return -static_cast<int>(e);
         if (P <= N) {
             // the positives are the table; every other score is a query read in place
-            rc = dauc_auc_counts_sorted_labeled(w.pos, P, scores, labels, label_dtype, 0, n, w.wt, w.wt + 2, w.tws,
-                                                w.tws_bytes, stream);
+            rc = query(P);
         } else {
             // the negatives are the smaller class: materialise both (the split checks every score)
             rc = dauc_split_scores(scores, labels, label_dtype, n, w.pos, w.neg, w.stats, w.sws, w.sws_bytes, stream);
             if (rc) return rc;
-            if ((e = hipMemcpyAsync(host, w.stats, 4 * sizeof(int64_t), hipMemcpyDeviceToHost, st)) != hipSuccess ||
-                (e = hipStreamSynchronize(st)) != hipSuccess)
-                return -static_cast<int>(e);
+            if ((rc = readback())) return rc;
             P = host[0];
             N = host[1];
             nonfinite = host[2];
-            if (nonfinite == 0)
-                rc = dauc_auc_counts_sorted(w.pos, P, w.neg, N, w.wt, w.tws, w.tws_bytes, stream);
+            if (nonfinite == 0) rc = dauc_auc_counts_sorted(w.pos, P, w.neg, N, w.wt, w.tws, w.tws_bytes, stream);
         }
         if (rc) return rc;
+        if ((rc = readback())) return rc;
+        counted = true;
     }
-    if ((e = hipMemcpyAsync(host + 8, w.wt, 3 * sizeof(unsigned long long), hipMemcpyDeviceToHost, st)) != hipSuccess ||
-        (e = hipStreamSynchronize(st)) != hipSuccess)
-        return -static_cast<int>(e);
-    out[0] = host[8];
-    out[1] = host[9];
+    const bool have = counted && P > 0 && N > 0 && nonfinite == 0;
+    out[0] = have ? host[8] : 0;
+    out[1] = have ? host[9] : 0;
     out[2] = P;
     out[3] = N;
-    out[4] = nonfinite + host[10];
+    out[4] = nonfinite + (have ? host[10] : 0);
     out[5] = other;
     return DAUC_OK;
 }

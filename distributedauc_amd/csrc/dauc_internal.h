@@ -97,4 +97,9 @@ __device__ __forceinline__ bool arrive_last(unsigned* counter, unsigned nblocks,
     return *lds_flag != 0;
 }
 
+// auc_count.hip: dauc_compact_positives that also zeroes zero3[0..3) (used by auc_eval.hip)
+int compact_positives_zeroing(const float* scores, const void* labels, int label_dtype, int64_t n, float* pos_out,
+                              int64_t* stats, void* workspace, size_t workspace_bytes, unsigned long long* zero3,
+                              hipStream_t st);
+
 }  // namespace dauc

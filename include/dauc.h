@@ -299,8 +299,12 @@ int dauc_auc_counts_sorted_labeled(const float* pos, int64_t P, const float* sco
  * roc_curve + auc is a blocking host call too): positive compaction, a readback of the class
  * sizes, the radix sort of the smaller class, the tree and the query pass, a readback of the
  * counts. Same integers as the stage-by-stage calls it chains. The exception to the
- * conventions above: it synchronises `stream` (twice; three times when P > N) and keeps one
- * small pinned host buffer per calling thread, allocated on first use.
+ * conventions above: it synchronises `stream` and keeps one small pinned host buffer per
+ * calling thread, allocated on first use. The table size is known only after the compaction;
+ * when the calling thread's previous call had the same n and label type, its P is used to
+ * enqueue the sort and the query right behind the compaction and the call synchronises ONCE
+ * (repeated evaluation of one test set); if the real P differs, the sort and the query are
+ * re-run at the real size (2 synchronisations; 3 when P > N).
  *   out[6] (HOST int64) = { W, T, P, N, #non-finite scores, #labels not in {-1, 1} }
  *   (W = T = 0 when a class is empty or a score is non-finite: the caller raises like sklearn)
  * workspace >= dauc_auc_eval_workspace_size(n) bytes, 256-byte aligned; no zeroing needed.

@@ -466,6 +466,18 @@ def test_auc_eval_counts_one_call(dev, ldtype):
             assert (W, Tt) == (e["wins"], e["ties"]), (n, p)
         else:
             assert (W, Tt) == (0, 0)
+    # repeated length: the previous call's P is used before the real one is known (a hit when the
+    # data repeat, a re-run at the real size when the class sizes differ), both table sides
+    n = 300_001
+    data = []
+    for p in (0.02, 0.03, 0.02, 0.7, 0.02):
+        s = rng.random(n, dtype=np.float32)
+        data.append((s, np.where(rng.random(n) < p, 1, -1).astype(ldtype)))
+    for k in (0, 0, 1, 1, 0, 2, 3, 3, 4, 0):
+        s, y = data[k]
+        W, Tt, P, N, bad, other = ops.auc_eval_counts(T(s, dev), T(y, dev))
+        e = coracle.auc_counts(y.astype(np.int64), s)
+        assert (W, Tt, P, N, bad) == (e["wins"], e["ties"], e["P"], e["N"], 0), k
     for where in ("pos", "neg"):
         for p in (0.01, 0.99):  # both table sides
             n = 100_003
