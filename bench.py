@@ -33,6 +33,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import socket
 import subprocess
@@ -319,7 +320,10 @@ def bench_auc(args, world, rank, device, log2n=None, pos=None, pair_reps=None):
     n = 1 << log2n
     s, y = synthetic_scores(n, pos, device)  # same scores on every rank
     out = {"n": n, "log2n": log2n, "pos": pos}
-    for method, fn in (("sort", "dauc_auc_counts_sorted_labeled"), ("pairs", "dauc_pair_count_variant")):
+    # the sort method on one GPU is ONE blocking C call (dauc_auc_eval_counts); over ranks the
+    # compaction, the all-gathers and dauc_auc_counts_sorted_labeled are separate
+    sort_fn = "dauc_auc_eval_counts" if world == 1 else "dauc_auc_counts_sorted_labeled"
+    for method, fn in (("sort", sort_fn), ("pairs", "dauc_pair_count_variant")):
         ev = ExactAUC(world=world, rank=rank, variant=args.variant, method=method)
         kt = KernelTimer(_lib.load(), fn)
         c = ev.counts(y, s)  # warm-up
@@ -337,7 +341,7 @@ def bench_auc(args, world, rank, device, log2n=None, pos=None, pair_reps=None):
         kt.enabled = False
         kt.restore()
         out["m_" + method] = {"t_eval": max_over_ranks(float(np.median(times)), world),
-                              "t_count": max_over_ranks(kt.mean_ms() / 1e3, world), "counts": c}
+                              "t_count": max_over_ranks(kt.mean_ms() / 1e3, world), "count_fn": fn, "counts": c}
         log(f"rank {rank}: auc 2^{log2n} {method} eval {out['m_' + method]['t_eval'] * 1e3:.2f} ms")
     a, b = out["m_sort"]["counts"], out["m_pairs"]["counts"]
     if (a["wins"], a["ties"]) != (b["wins"], b["ties"]):
@@ -365,6 +369,9 @@ def auc_record(auc, world, config_name):
         "method": "sort (default evaluator: compact the positives reading labels only, radix-sort them, locate "
                   "every negative through an LDS search tree, read in place)",
         "eval_ms": sk["t_eval"] * 1e3, "sort_count_ms": sk["t_count"] * 1e3,
+        "sort_count_what": f"HIP events around every {sk['count_fn']} call"
+                           + (" (the whole one-call evaluation: compaction, sort, query, readback)"
+                              if sk["count_fn"] == "dauc_auc_eval_counts" else " (sort + tree + query)"),
         "eval_roofline": {"bound": "hbm", "bytes_per_rank": eval_bytes,
                           "achieved": eval_bytes / sk["t_eval"] / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                           "frac": eval_bytes / sk["t_eval"] / 1e9 / HBM_PEAK_GBS,
@@ -762,10 +769,21 @@ def main():
         else:
             out["cpu_baseline"] = None
         sys.stdout.flush()
-        os.write(json_fd, (json.dumps(out) + "\n").encode())
+        os.write(json_fd, (json.dumps(_finite(out)) + "\n").encode())
     if world > 1:
         dist.barrier(group=quiet)
         dist.destroy_process_group()
+
+
+def _finite(x):
+    """NaN / inf (an unmeasured figure) as null: the record stays strict JSON."""
+    if isinstance(x, float):
+        return x if math.isfinite(x) else None
+    if isinstance(x, dict):
+        return {k: _finite(v) for k, v in x.items()}
+    if isinstance(x, (list, tuple)):
+        return [_finite(v) for v in x]
+    return x
 
 
 def load_traffic(kernel: str):
