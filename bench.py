@@ -367,7 +367,9 @@ def auc_record(auc, world, config_name):
                     "positive blocks), int64 all-reduce",
         "pairs_per_sec": npairs / sk["t_eval"],
         "method": "sort (default evaluator: compact the positives reading labels only, radix-sort them, locate "
-                  "every negative through an LDS search tree, read in place)",
+                  "every negative through an LDS search tree, read in place; on one GPU one blocking C call that "
+                  "sizes the sort by the previous call's P for this length and re-runs it if P differs, so a "
+                  "repeated test set costs one readback)",
         "eval_ms": sk["t_eval"] * 1e3, "sort_count_ms": sk["t_count"] * 1e3,
         "sort_count_what": f"HIP events around every {sk['count_fn']} call"
                            + (" (the whole one-call evaluation: compaction, sort, query, readback)"
@@ -376,6 +378,7 @@ def auc_record(auc, world, config_name):
                           "achieved": eval_bytes / sk["t_eval"] / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                           "frac": eval_bytes / sk["t_eval"] / 1e9 / HBM_PEAK_GBS,
                           "note": "bytes = 2 label passes + 1 score/label pass over this rank's share"},
+        "query_kernel": load_profile("query_valu.json", f"2^{auc['log2n']}"),
         "P": auc["P"], "N": auc["N"], "wins": auc["wins"], "ties": auc["ties"], "auc": auc["auc"],
         "methods_agree": True,
         "pair_count_kernel": {
@@ -409,7 +412,9 @@ def bench_surrogate(args, device):
     out64 = torch.zeros(6, dtype=torch.float64, device=device)
 
     def b2b(variant):
-        for _ in range(max(10, args.sur_reps)):  # warm: the first calls after other work run ~2-3 us slower
+        # warm: the first ~200-300 calls of a streaming kernel run 2-4 us slower than the steady
+        # state (profiles/r02/surrogate_tail/sur_order_effect.jsonl); 400 calls is ~40 ms
+        for _ in range(max(400, 4 * args.sur_reps)):
             ops.surrogate_fwdbwd(h, y, abalpha, p_hat, dh=dh, grad3=grad3, out64=out64, variant=variant)
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -786,15 +791,23 @@ def _finite(x):
     return x
 
 
-def load_traffic(kernel: str):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/), or None."""
-    f = REPO / "profiles" / "traffic.json"
+def load_profile(name: str, key: str):
+    """One entry of a committed rocprofv3 PMC summary (profiles/<name>), or None."""
+    f = REPO / "profiles" / name
     if not f.exists():
         return None
     try:
-        return json.loads(f.read_text()).get(kernel)
+        rec = json.loads(f.read_text()).get(key)
     except Exception:
         return None
+    if isinstance(rec, dict):
+        rec = dict(rec, source=f"profiles/{name} (scripts/query_valu.py; rocprofv3 PMC + kernel trace, not this run)")
+    return rec
+
+
+def load_traffic(kernel: str):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/), or None."""
+    return load_profile("traffic.json", kernel)
 
 
 if __name__ == "__main__":

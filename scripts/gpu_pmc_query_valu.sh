@@ -1,0 +1,16 @@
+#!/bin/bash
+# VALU-issue roofline of the labeled query kernel (2^27 @ 0.1 %): instruction counters in one PMC
+# pass, kernel durations in a separate trace pass
+set -o pipefail
+export TMPDIR=/tmp
+O=gpurun_out/pmc_valu
+mkdir -p $O
+timeout -k 10 -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_WAVES \
+    SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d $O -o valu -- \
+    python3 scripts/probe_query.py 27 0.001 3 > $O/log_valu.txt 2>&1 || exit 1
+timeout -k 10 -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVES GRBM_GUI_ACTIVE --output-format csv \
+    -d $O -o valu24 -- python3 scripts/probe_query.py 24 0.01 3 > $O/log_valu24.txt 2>&1 || exit 1
+timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $O -o trace -- \
+    python3 scripts/probe_query.py 27 0.001 5 > $O/log_trace.txt 2>&1 || exit 1
+timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $O -o trace24 -- \
+    python3 scripts/probe_query.py 24 0.01 5 > $O/log_trace24.txt 2>&1 || exit 1
