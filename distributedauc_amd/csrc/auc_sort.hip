@@ -282,6 +282,20 @@ struct TreeGeom {
     int nodes;           // total stored nodes (incl. the per-level padding nodes)
 };
 
+// The top levels of the tree as wave-uniform registers (SGPRs): level 0 (4 keys) or levels 0-1
+// (the 24 splitters of the first two levels — #(those <= x) is the position after two levels).
+// Each level held here is one dependent LDS read fewer per query; 24 uniform compares cost more
+// VALU than two node reads, so which is faster is measured (DAUC_TREE_TOP_LEVELS 0 / 1 / 2).
+#ifndef DAUC_TREE_TOP_LEVELS
+#define DAUC_TREE_TOP_LEVELS 0
+#endif
+constexpr int kTopLevels = kTreeArity == 5 ? DAUC_TREE_TOP_LEVELS : 0;
+constexpr int kTopKeys = kTopLevels == 2 ? 24 : (kTopLevels == 1 ? 4 : 1);
+struct TopKeys {
+    unsigned k[kTopKeys];
+    bool on;  // the tree has at least kTopLevels levels
+};
+
 TreeGeom tree_geom(int S) {
     TreeGeom g{};
     g.S = S;
@@ -362,7 +376,7 @@ __device__ __forceinline__ unsigned tree_step(unsigned p, uint2 n, unsigned x) {
 // wave-uniform (kernel arguments, scalar registers).
 template <int Q>
 __device__ __forceinline__ void tree_walk(const unsigned (&x)[Q], unsigned (&p)[Q], const TreeNode* __restrict__ tree,
-                                          const TreeGeom& g) {
+                                          const TreeGeom& g, const TopKeys& top) {
 #pragma unroll
     for (int q = 0; q < Q; ++q) p[q] = 0;
     if (DAUC_ABLATE == 2) {
@@ -370,9 +384,20 @@ __device__ __forceinline__ void tree_walk(const unsigned (&x)[Q], unsigned (&p)[
         for (int q = 0; q < Q; ++q) p[q] = (x[q] * 2654435761u) % static_cast<unsigned>(g.S);
         return;
     }
+    int d0 = 0;
+    if (kTopLevels > 0 && top.on) {
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            unsigned c = 0;
+#pragma unroll
+            for (int m = 0; m < kTopKeys; ++m) c += top.k[m] <= x[q];
+            p[q] = c;
+        }
+        d0 = kTopLevels;
+    }
 #pragma unroll
     for (int d = 0; d < kMaxTreeH; ++d) {
-        if (d < g.H) {
+        if (d >= d0 && d < g.H) {
             const unsigned nd = static_cast<unsigned>(g.nd[d]), off = static_cast<unsigned>(g.off[d]);
             TreeNode v[Q];
 #pragma unroll
@@ -440,7 +465,8 @@ __device__ __forceinline__ int64_t count_below(const unsigned* __restrict__ a, i
 
 // One query (K = 0: buckets of k > 32 keys, finished by binary searches in global memory).
 template <int K, bool TABLE_POS>
-__device__ __forceinline__ void count_query(unsigned x, const TreeNode* __restrict__ tree, const TreeGeom& g, int k,
+__device__ __forceinline__ void count_query(unsigned x, const TreeNode* __restrict__ tree, const TreeGeom& g,
+                                            const TopKeys& top, int k,
                                             const unsigned* __restrict__ sorted, int64_t M,
                                             unsigned long long& w, unsigned long long& t) {
     // splitters <= x (walk 0) and < x = <= x - 1 (walk 1; finite keys are >= 0x00800000, so
@@ -449,7 +475,7 @@ __device__ __forceinline__ void count_query(unsigned x, const TreeNode* __restri
     if constexpr (K <= 1) {
         const unsigned xs[2] = {x, x - 1u};
         unsigned i[2];
-        tree_walk<2>(xs, i, tree, g);
+        tree_walk<2>(xs, i, tree, g, top);
         const int64_t su = i[0], sl = i[1];
         if constexpr (K == 1) {
             ub = su;
@@ -469,7 +495,7 @@ __device__ __forceinline__ void count_query(unsigned x, const TreeNode* __restri
         // equals x (a run of x may then start in an earlier bucket)
         const unsigned xs[1] = {x};
         unsigned i[1];
-        tree_walk<1>(xs, i, tree, g);
+        tree_walk<1>(xs, i, tree, g, top);
         const int64_t su = i[0];
         if (su > 0) {
             int le = 0, lt = 0;
@@ -480,7 +506,7 @@ __device__ __forceinline__ void count_query(unsigned x, const TreeNode* __restri
                 lb = (su - 1) * K + lt;
             } else {
                 const unsigned xm[1] = {x - 1u};
-                tree_walk<1>(xm, i, tree, g);
+                tree_walk<1>(xm, i, tree, g, top);
                 const int64_t sl = i[0];
                 if (sl > 0) {
                     bucket_counts<K>(sorted, M, sl - 1, x, le, lt, first);
@@ -504,6 +530,7 @@ constexpr int lockstep_queries() {
 template <int K, int Q, bool TABLE_POS>
 __device__ __forceinline__ void count_queries(const unsigned (&x)[Q], const bool (&use)[Q],
                                               const TreeNode* __restrict__ tree, const TreeGeom& g,
+                                              const TopKeys& top,
                                               const unsigned* __restrict__ sorted, int64_t M,
                                               unsigned long long& w, unsigned long long& t) {
     static_assert(K >= 1 && K <= 32, "bucketed lockstep walk");
@@ -515,7 +542,7 @@ __device__ __forceinline__ void count_queries(const unsigned (&x)[Q], const bool
             xs[q] = x[q];
             xs[Q + q] = x[q] - 1u;
         }
-        tree_walk<2 * Q>(xs, i, tree, g);
+        tree_walk<2 * Q>(xs, i, tree, g, top);
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
             if (!use[q]) continue;
@@ -525,7 +552,7 @@ __device__ __forceinline__ void count_queries(const unsigned (&x)[Q], const bool
         }
     } else {
         unsigned su[Q];
-        tree_walk<Q>(x, su, tree, g);
+        tree_walk<Q>(x, su, tree, g, top);
         // every bucket load issued before any is examined (su = 0: bucket 0 is read, unused)
         int le[Q], lt[Q];
         unsigned first[Q];
@@ -533,24 +560,28 @@ __device__ __forceinline__ void count_queries(const unsigned (&x)[Q], const bool
         for (int q = 0; q < Q; ++q) bucket_counts<K>(sorted, M, su[q] ? su[q] - 1u : 0u, x[q], le[q], lt[q], first[q]);
         // 32-bit and branch-free: lb below is exact unless the bucket starts with x itself (then
         // a run of x may begin in an earlier bucket); those rare queries are fixed up after
+        // the Q queries' counts summed in 32 bits (Q * M < 2^32), one 64-bit add each
         bool slow = false;
+        unsigned wl = 0u, tl = 0u;
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
             const unsigned base = su[q] ? (su[q] - 1u) * static_cast<unsigned>(K) : 0u;
             const unsigned ub = su[q] ? base + static_cast<unsigned>(le[q]) : 0u;
             const unsigned lb = su[q] ? base + static_cast<unsigned>(lt[q]) : 0u;
             const unsigned wq = TABLE_POS ? static_cast<unsigned>(M) - ub : lb;
-            w += use[q] ? wq : 0u;
-            t += use[q] ? ub - lb : 0u;
+            wl += use[q] ? wq : 0u;
+            tl += use[q] ? ub - lb : 0u;
             slow |= use[q] && su[q] != 0u && first[q] >= x[q];
         }
+        w += wl;
+        t += tl;
         if (slow) {
 #pragma unroll
             for (int q = 0; q < Q; ++q) {
                 if (!(use[q] && su[q] != 0u && first[q] >= x[q])) continue;
                 const unsigned xm[1] = {x[q] - 1u};
                 unsigned j[1];
-                tree_walk<1>(xm, j, tree, g);
+                tree_walk<1>(xm, j, tree, g, top);
                 unsigned lb_true = 0u;
                 if (j[0] != 0u) {
                     int le2 = 0, lt2 = 0;
@@ -570,12 +601,12 @@ __device__ __forceinline__ void count_queries(const unsigned (&x)[Q], const bool
 // (K = 0, buckets > 32 keys finished in global memory: one key at a time).
 template <int K, bool TABLE_POS>
 __device__ __forceinline__ void count4(const unsigned (&x)[4], const bool (&use)[4], const TreeNode* __restrict__ tree,
-                                       const TreeGeom& g, int k, const unsigned* __restrict__ sorted, int64_t M,
+                                       const TreeGeom& g, const TopKeys& top, int k, const unsigned* __restrict__ sorted, int64_t M,
                                        unsigned long long& w, unsigned long long& t) {
     if constexpr (K == 0) {
 #pragma unroll
         for (int q = 0; q < 4; ++q)
-            if (use[q]) count_query<0, TABLE_POS>(x[q], tree, g, k, sorted, M, w, t);
+            if (use[q]) count_query<0, TABLE_POS>(x[q], tree, g, top, k, sorted, M, w, t);
     } else {
         constexpr int Q = lockstep_queries<K>();
 #pragma unroll
@@ -587,9 +618,35 @@ __device__ __forceinline__ void count4(const unsigned (&x)[4], const bool (&use)
                 xs[q] = x[b + q];
                 us[q] = use[b + q];
             }
-            count_queries<K, Q, TABLE_POS>(xs, us, tree, g, sorted, M, w, t);
+            count_queries<K, Q, TABLE_POS>(xs, us, tree, g, top, sorted, M, w, t);
         }
     }
+}
+
+// the top levels' keys, read once per workgroup with uniform (scalar) loads
+__device__ __forceinline__ TopKeys load_top(const TreeNode* __restrict__ gtree, const TreeGeom& g) {
+    TopKeys t{};
+    t.on = kTopLevels > 0 && g.H >= kTopLevels;
+    if constexpr (kTopLevels > 0) {
+        if (t.on) {
+            const uint4 n0 = gtree[g.off[0]];
+            t.k[0] = n0.x;
+            t.k[1] = n0.y;
+            t.k[2] = n0.z;
+            t.k[3] = n0.w;
+            if constexpr (kTopLevels == 2) {
+#pragma unroll
+                for (int j = 0; j < 5; ++j) {
+                    const uint4 n = gtree[g.off[1] + (j < g.nd[1] ? j : g.nd[1])];
+                    t.k[4 + 4 * j] = n.x;
+                    t.k[5 + 4 * j] = n.y;
+                    t.k[6 + 4 * j] = n.z;
+                    t.k[7 + 4 * j] = n.w;
+                }
+            }
+        }
+    }
+    return t;
 }
 
 template <int K, bool TABLE_POS>
@@ -599,6 +656,7 @@ __global__ __launch_bounds__(kQueryThreads) void query_count_kernel(const float*
                                                                    int64_t M, unsigned long long* __restrict__ out) {
     extern __shared__ TreeNode tree[];
     for (int i = threadIdx.x; i < g.nodes; i += kQueryThreads) tree[i] = gtree[i];
+    const TopKeys top = load_top(gtree, g);
     __syncthreads();
     unsigned long long w = 0, t = 0;
     const bool vec = (reinterpret_cast<uintptr_t>(q) & 15u) == 0;
@@ -608,10 +666,10 @@ __global__ __launch_bounds__(kQueryThreads) void query_count_kernel(const float*
     for (int64_t v = int64_t(blockIdx.x) * kQueryThreads + threadIdx.x; v < nvec; v += stride) {
         const f32x4 f = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(q) + v);
         const unsigned x[4] = {key_of(f.x), key_of(f.y), key_of(f.z), key_of(f.w)};
-        count4<K, TABLE_POS>(x, all, tree, g, k, sorted, M, w, t);
+        count4<K, TABLE_POS>(x, all, tree, g, top, k, sorted, M, w, t);
     }
     for (int64_t i = nvec * 4 + int64_t(blockIdx.x) * kQueryThreads + threadIdx.x; i < L; i += stride)
-        count_query<K, TABLE_POS>(key_of(q[i]), tree, g, k, sorted, M, w, t);
+        count_query<K, TABLE_POS>(key_of(q[i]), tree, g, top, k, sorted, M, w, t);
     __shared__ unsigned long long red[2][kQueryThreads / kWave];
     w = wave_sum(w);
     t = wave_sum(t);
@@ -668,6 +726,7 @@ __global__ __launch_bounds__(kQueryThreads) void query_labeled_kernel(const floa
                                                                      unsigned long long* __restrict__ nonfinite) {
     extern __shared__ TreeNode tree[];
     for (int i = threadIdx.x; i < g.nodes; i += kQueryThreads) tree[i] = gtree[i];
+    const TopKeys top = load_top(gtree, g);
     __syncthreads();
     unsigned long long w = 0, t = 0;
     unsigned nf = 0;
@@ -679,7 +738,7 @@ __global__ __launch_bounds__(kQueryThreads) void query_labeled_kernel(const floa
     for (int64_t i = begin + tid; i < head; i += stride) {
         if (lab[i] != LT(1)) {
             nf += !isfinite(s[i]);
-            count_query<K, true>(key_of(s[i]), tree, g, k, sorted, M, w, t);
+            count_query<K, true>(key_of(s[i]), tree, g, top, k, sorted, M, w, t);
         }
     }
     const int64_t nvec = end > head ? (end - head) / 4 : 0;
@@ -740,7 +799,7 @@ __global__ __launch_bounds__(kQueryThreads) void query_labeled_kernel(const floa
                     x[q] = key_of(f[q]);
                     nf += neg[q] && !isfinite(f[q]);
                 }
-                count4<K, true>(x, neg, tree, g, k, sorted, M, w, t);
+                count4<K, true>(x, neg, tree, g, top, k, sorted, M, w, t);
             }
 #pragma unroll
             for (int u = 0; u < U; ++u) {
@@ -763,13 +822,13 @@ __global__ __launch_bounds__(kQueryThreads) void query_labeled_kernel(const floa
                 x[q] = key_of(f[q]);
                 nf += neg[q] && !isfinite(f[q]);
             }
-            count4<K, true>(x, neg, tree, g, k, sorted, M, w, t);
+            count4<K, true>(x, neg, tree, g, top, k, sorted, M, w, t);
         }
     }
     for (int64_t i = head + nvec * 4 + tid; i < end; i += stride) {
         if (lab[i] != LT(1)) {
             nf += !isfinite(s[i]);
-            count_query<K, true>(key_of(s[i]), tree, g, k, sorted, M, w, t);
+            count_query<K, true>(key_of(s[i]), tree, g, top, k, sorted, M, w, t);
         }
     }
     __shared__ unsigned long long red[3][kQueryThreads / kWave];
