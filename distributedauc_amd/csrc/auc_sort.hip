@@ -293,7 +293,8 @@ constexpr int kTopLevels = kTreeArity == 5 ? DAUC_TREE_TOP_LEVELS : 0;
 constexpr int kTopKeys = kTopLevels == 2 ? 24 : (kTopLevels == 1 ? 4 : 1);
 struct TopKeys {
     unsigned k[kTopKeys];
-    bool on;  // the tree has at least kTopLevels levels
+    bool on;        // the tree has at least kTopLevels levels
+    unsigned last;  // the largest splitter (a finite score's key, so >= 0x007fffff > 0)
 };
 
 TreeGeom tree_geom(int S) {
@@ -384,13 +385,20 @@ __device__ __forceinline__ void tree_walk(const unsigned (&x)[Q], unsigned (&p)[
         for (int q = 0; q < Q; ++q) p[q] = (x[q] * 2654435761u) % static_cast<unsigned>(g.S);
         return;
     }
+    // A walk for x below the largest splitter only visits stored nodes: its node at level d is
+    // floor(r / 5^(H-d)) for r = #splitters <= x <= S - 1, at most the level's one padding node
+    // (n_d). So x is clamped below the largest splitter (no per-level index clamp) and the
+    // queries at or above it get p = S.
+    unsigned xc[Q];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) xc[q] = x[q] < top.last ? x[q] : top.last - 1u;
     int d0 = 0;
     if (kTopLevels > 0 && top.on) {
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
             unsigned c = 0;
 #pragma unroll
-            for (int m = 0; m < kTopKeys; ++m) c += top.k[m] <= x[q];
+            for (int m = 0; m < kTopKeys; ++m) c += top.k[m] <= xc[q];
             p[q] = c;
         }
         d0 = kTopLevels;
@@ -398,14 +406,16 @@ __device__ __forceinline__ void tree_walk(const unsigned (&x)[Q], unsigned (&p)[
 #pragma unroll
     for (int d = 0; d < kMaxTreeH; ++d) {
         if (d >= d0 && d < g.H) {
-            const unsigned nd = static_cast<unsigned>(g.nd[d]), off = static_cast<unsigned>(g.off[d]);
+            const unsigned off = static_cast<unsigned>(g.off[d]);
             TreeNode v[Q];
 #pragma unroll
-            for (int q = 0; q < Q; ++q) v[q] = tree[off + (p[q] < nd ? p[q] : nd)];
+            for (int q = 0; q < Q; ++q) v[q] = tree[off + p[q]];
 #pragma unroll
-            for (int q = 0; q < Q; ++q) p[q] = tree_step(p[q], v[q], x[q]);
+            for (int q = 0; q < Q; ++q) p[q] = tree_step(p[q], v[q], xc[q]);
         }
     }
+#pragma unroll
+    for (int q = 0; q < Q; ++q) p[q] = x[q] < top.last ? p[q] : static_cast<unsigned>(g.S);
 }
 
 // #keys of bucket b (keys sorted[b*k .. min(b*k + k, M))) that are <= x, and that are < x;
@@ -624,8 +634,10 @@ __device__ __forceinline__ void count4(const unsigned (&x)[4], const bool (&use)
 }
 
 // the top levels' keys, read once per workgroup with uniform (scalar) loads
-__device__ __forceinline__ TopKeys load_top(const TreeNode* __restrict__ gtree, const TreeGeom& g) {
+__device__ __forceinline__ TopKeys load_top(const TreeNode* __restrict__ gtree, const TreeGeom& g,
+                                           const unsigned* __restrict__ sorted, int k) {
     TopKeys t{};
+    t.last = sorted[int64_t(g.S - 1) * k];
     t.on = kTopLevels > 0 && g.H >= kTopLevels;
     if constexpr (kTopLevels > 0) {
         if (t.on) {
@@ -656,7 +668,7 @@ __global__ __launch_bounds__(kQueryThreads) void query_count_kernel(const float*
                                                                    int64_t M, unsigned long long* __restrict__ out) {
     extern __shared__ TreeNode tree[];
     for (int i = threadIdx.x; i < g.nodes; i += kQueryThreads) tree[i] = gtree[i];
-    const TopKeys top = load_top(gtree, g);
+    const TopKeys top = load_top(gtree, g, sorted, k);
     __syncthreads();
     unsigned long long w = 0, t = 0;
     const bool vec = (reinterpret_cast<uintptr_t>(q) & 15u) == 0;
@@ -726,7 +738,7 @@ __global__ __launch_bounds__(kQueryThreads) void query_labeled_kernel(const floa
                                                                      unsigned long long* __restrict__ nonfinite) {
     extern __shared__ TreeNode tree[];
     for (int i = threadIdx.x; i < g.nodes; i += kQueryThreads) tree[i] = gtree[i];
-    const TopKeys top = load_top(gtree, g);
+    const TopKeys top = load_top(gtree, g, sorted, k);
     __syncthreads();
     unsigned long long w = 0, t = 0;
     unsigned nf = 0;
