@@ -1,6 +1,6 @@
 """The reference-side ctypes binding shown in INTEGRATION.md §2, executed verbatim against libdauc.so:
-its AUC() (dauc_compact_positives + dauc_auc_counts_sorted_labeled) must give the C oracle's exact
-counts, and its dppd_sg_param() the oracle's bit-exact update (main.py:61)."""
+its AUC() (the one blocking call dauc_auc_eval_counts) must give the C oracle's exact counts, and
+its dppd_sg_param() the oracle's bit-exact update (main.py:61)."""
 from __future__ import annotations
 
 import re
@@ -29,7 +29,7 @@ def _stub():
 def test_integration_stub_auc_and_update(dev):
     ns = _stub()
     rng = np.random.default_rng(11)
-    for n, p, q in ((1000, 0.1, 0), (300_007, 0.01, 1024), (2_000_000, 0.002, 0)):
+    for n, p, q in ((1000, 0.1, 0), (300_007, 0.01, 1024), (300_007, 0.9, 1024), (2_000_000, 0.002, 0)):
         s = rng.random(n, dtype=np.float32)
         if q:
             s = (np.floor(s * q) / q).astype(np.float32)
