@@ -78,6 +78,7 @@ def parse(argv=None):
     p.add_argument("--sweep-I", default="1,8,16,32", help="configs[2] averaging periods ('' = off)")
     p.add_argument("--sweep-steps", type=int, default=32, help="timed steps per period (a multiple of every I)")
     p.add_argument("--r18-steps", type=int, default=16, help="configs[0] GPU leg: timed ResNet-18 b32 steps (0 = off)")
+    p.add_argument("--r18-graph", type=int, default=1, help="configs[0] GPU leg: replay the step body as a HIP graph (1/0)")
     p.add_argument("--auc-log2n", type=int, default=24)
     p.add_argument("--auc-pos", type=float, default=0.01)
     p.add_argument("--auc-reps", type=int, default=3)
@@ -191,7 +192,8 @@ def timed_steps(coda, it, steps: int, world: int) -> float:
 
 
 # ----------------------------------------------------------------------------- training legs
-def make_coda(arch, batch, image_size, I, pos_ratio, pool, world, rank, device, fused_bn=True, gemm_conv1x1=True):
+def make_coda(arch, batch, image_size, I, pos_ratio, pool, world, rank, device, fused_bn=True, gemm_conv1x1=True,
+              graph=False):
     from distributedauc_amd.backbone import build_backbone
     from distributedauc_amd.coda import CoDA
     from distributedauc_amd.loader import DeviceLoader, SyntheticImageNet, imagenet_like_labels
@@ -208,6 +210,7 @@ def make_coda(arch, batch, image_size, I, pos_ratio, pool, world, rank, device, 
     it = iter(loader)
     coda.average_all()            # main.py:141-142
     coda.begin_stage(1, it)       # alpha estimate + anchors (untimed)
+    coda.use_graph(graph)         # step bodies replayed from one HIP graph (captured at the first step)
     return coda, it
 
 
@@ -292,7 +295,7 @@ def bench_r18(args, world, rank, device):
     """configs[0] on the GPUs: ResNet-18 CoDA, batch 32 per rank, 224^2, I = 8 (the CPU path of
     the same config is cpu_baseline_configs0)."""
     coda, it = make_coda("resnet18", 32, args.image_size, 8, args.pos_ratio, args.pool, world, rank, device,
-                         args.fused_bn, args.gemm_conv1x1)
+                         args.fused_bn, args.gemm_conv1x1, graph=bool(args.r18_graph))
     for _ in range(max(args.warmup, 8)):
         x, y = next(it)
         coda.train_step(x, y)
@@ -300,7 +303,9 @@ def bench_r18(args, world, rank, device):
     steps = max(8, args.r18_steps // 8 * 8)
     dt = timed_steps(coda, it, steps, world)
     rec = {"workload": "resnet18 CoDA, batch 32 per rank, 224x224, I=8, bf16 autocast backbone, fp32 AUC kernels "
-                       "(BASELINE configs[0] on the GPUs)",
+                       "(BASELINE configs[0] on the GPUs)"
+                       + (", step bodies replayed from one HIP graph (averaging rounds eager)" if args.r18_graph else ""),
+           "graph": bool(args.r18_graph),
            "imgs_per_sec": world * 32 * steps / dt, "ms_per_step": dt / steps * 1e3, "steps": steps,
            "n_gpus": world, "params": coda.state.numel(), "final_loss": float(coda.last_loss.item())}
     del coda, it

@@ -68,6 +68,9 @@ class CoDA:
         self._scratch = torch.zeros(8, dtype=torch.float32, device=self.device)
         self._ab_stage = torch.zeros(2, dtype=torch.float32, device=self.device)
         self.last_loss: torch.Tensor | None = None
+        self._graph_on = False
+        self._graph = None
+        self._graph_key = None
 
     # ---------------------------------------------------------------- plumbing
     def _autocast(self):
@@ -141,7 +144,7 @@ class CoDA:
         if self.t_total % self.I == 0:
             with torch.no_grad():
                 self.average_all()
-        self.last_loss = self.step_body(x, labels)
+        self.last_loss = self._graphed_body(x, labels) if self._graph_on else self.step_body(x, labels)
         return self.last_loss
 
     def step_body(self, x: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
@@ -159,6 +162,50 @@ class CoDA:
         st.update(self.lr, self.gamma, self.mode)
         self.model.zero_grad(set_to_none=True)
         return loss.detach()
+
+    # ---------------------------------------------------------------- HIP graph replay
+    def use_graph(self, enable: bool = True) -> "CoDA":
+        """Replay step_body (label map, forward, surrogate, backward, pd_update, zero_grad) as ONE
+        HIP graph: a small batch's step is bound by the ~200 kernel launches of the backbone, not
+        by the GPU. The averaging round stays outside the graph (RCCL, every I steps), so the
+        schedule is the reference's. The graph is captured at the first step of each (input
+        shape, dtype, lr) — lr changes only at a stage start — after two warm-up bodies on a
+        side stream whose effect on the state is undone; every replay reads the batch from the
+        graph's own input buffers, so the caller's tensors are copied in first."""
+        self._graph_on = bool(enable)
+        self._graph = self._graph_key = None
+        return self
+
+    def _graphed_body(self, x: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
+        key = (tuple(x.shape), x.dtype, x.stride(), tuple(labels.shape), labels.dtype, self.lr)
+        if self._graph is None or self._graph_key != key:
+            self._capture(x, labels, key)
+        self._gx.copy_(x)
+        self._gy.copy_(labels)
+        self._graph.replay()
+        return self._gloss
+
+    def _capture(self, x: torch.Tensor, labels: torch.Tensor, key) -> None:
+        st = self.state
+        state = [st.flat, st.avg, st.lcounts, st.gcounts, st.p_hat, *self.model.buffers()]
+        self._graph = None
+        with torch.no_grad():
+            snap = [t.clone() for t in state]
+            self._gx, self._gy = x.clone(), labels.clone()
+        cur = torch.cuda.current_stream(self.device)
+        side = torch.cuda.Stream(self.device)
+        side.wait_stream(cur)
+        with torch.cuda.stream(side):
+            for _ in range(2):  # lazy initialisation (engine choices, workspaces) before capture
+                self.step_body(self._gx, self._gy)
+        cur.wait_stream(side)
+        with torch.no_grad():
+            for t, s in zip(state, snap):
+                t.copy_(s)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            self._gloss = self.step_body(self._gx, self._gy)
+        self._graph, self._graph_key = graph, key
 
     # ---------------------------------------------------------------- loop
     def run(self, batches: Iterator, *, num_stages: int, total_iter: int, test_freq: int | None = None,

@@ -94,6 +94,19 @@ def test_checkpoint_resume_bitwise(dev, golden, tmp_path):
     assert resumed.t_total == full.t_total
 
 
+def test_coda_graph_replay_matches_eager_and_reference(dev, golden):
+    """CoDA.use_graph(): every step body replayed from one HIP graph (re-captured when the stage
+    changes lr) gives the eager run's trajectory bit for bit — parameters, a/b/alpha, counts,
+    p_hat, losses, BN buffers — and so the reference's, over 2 stages with averaging rounds."""
+    fx = _load(golden, 1)
+    eager, _ = coda_parity.run_rank(fx, 0, 1, dev)
+    graphed, coda = coda_parity.run_rank(fx, 0, 1, dev, graph=True)
+    assert coda._graph is not None
+    for k in eager:
+        assert np.array_equal(eager[k], graphed[k]), k
+    coda_parity.compare(fx, 0, graphed)
+
+
 def test_step_body_hip_graph_bitwise(dev, golden):
     """CoDA.step_body (label map, forward, surrogate, backward, pd_update, zero_grad) captured in a
     HIP graph and replayed 3 times from a saved state gives the same parameters, running average,
