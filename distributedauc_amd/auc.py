@@ -74,7 +74,14 @@ class ExactAUC:
 
     def counts(self, label, scores, device=None) -> dict:
         """Exact {wins, ties, P, N} (Python ints). One host sync for the split sizes."""
-        y, s = _as_device_pair(label, scores, device)
+        if (device is None and isinstance(scores, torch.Tensor) and isinstance(label, torch.Tensor)
+                and scores.is_cuda and scores.dtype == torch.float32 and scores.dim() == 1
+                and scores.is_contiguous() and label.device == scores.device and label.dim() == 1
+                and label.dtype in (torch.int8, torch.int32, torch.int64) and label.is_contiguous()
+                and not scores.requires_grad):
+            y, s = label, scores  # already what the kernels read: no conversion ops
+        else:
+            y, s = _as_device_pair(label, scores, device)
         if y.numel() != s.numel():
             raise ValueError(f"Found input variables with inconsistent numbers of samples: {[y.numel(), s.numel()]}")
         if self.method == "sort" and self.world == 1:

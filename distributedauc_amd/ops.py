@@ -63,8 +63,8 @@ class _Workspaces:
     def __init__(self):
         self._ws: dict = {}
 
-    def get(self, device: torch.device, kind: str, nbytes: int) -> torch.Tensor:
-        key = (device.index, torch.cuda.current_stream(device).cuda_stream, kind)
+    def get(self, device: torch.device, kind: str, nbytes: int, stream: int | None = None) -> torch.Tensor:
+        key = (device.index, torch.cuda.current_stream(device).cuda_stream if stream is None else stream, kind)
         t = self._ws.get(key)
         if t is None or t.numel() < nbytes:
             t = torch.zeros(max(nbytes, 256), dtype=torch.uint8, device=device)
@@ -354,11 +354,18 @@ def auc_eval_counts(scores: torch.Tensor, labels: torch.Tensor) -> tuple:
     if n == 0:
         raise ValueError("empty score vector")
     L = _lib.load()
-    ws = workspaces.get(dev, "auc_eval", L.dauc_auc_eval_workspace_size(n))
+    nbytes = _eval_ws_bytes.get(n)
+    if nbytes is None:
+        nbytes = _eval_ws_bytes[n] = L.dauc_auc_eval_workspace_size(n)
+    st = torch.cuda.current_stream(dev).cuda_stream
+    ws = workspaces.get(dev, "auc_eval", nbytes, st)
     out = (ctypes.c_int64 * 6)()
-    check(L.dauc_auc_eval_counts(_ptr(scores), _ptr(labels), lc, n, ctypes.cast(out, ctypes.c_void_p), _ptr(ws),
-                                 ws.numel(), _stream(dev)), "dauc_auc_eval_counts")
-    return tuple(int(v) for v in out)
+    check(L.dauc_auc_eval_counts(scores.data_ptr(), labels.data_ptr(), lc, n, ctypes.addressof(out), ws.data_ptr(),
+                                 ws.numel(), st), "dauc_auc_eval_counts")
+    return tuple(out)
+
+
+_eval_ws_bytes: dict = {}  # dauc_auc_eval_workspace_size per length (a pure function of n)
 
 
 def compact_positives(scores: torch.Tensor, labels: torch.Tensor):
