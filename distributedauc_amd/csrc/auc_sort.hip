@@ -344,8 +344,28 @@ __global__ __launch_bounds__(256) void build_tree_kernel(unsigned* __restrict__ 
     if (c < pad) sorted[M + c] = kPadKey;
 }
 
-// p <- A p + #(node keys <= x): the compares' carries feed the adds.
+// p <- A p + #(node keys <= x): the compares' carries feed the adds (DAUC_TREE_STEP 0), or
+// (1) without the carry flag: sat(k - x) (unsigned saturating subtract) is 0 iff k <= x, so
+// #(keys <= x) = 4 - sum(min(sat(k_i - x), 1)) — 12 VALU, none writing VCC.
+#ifndef DAUC_TREE_STEP
+#define DAUC_TREE_STEP 0
+#endif
 __device__ __forceinline__ unsigned tree_step(unsigned p, uint4 n, unsigned x) {
+    if (DAUC_TREE_STEP == 1) {
+        unsigned d0, d1, d2, d3, gt;
+        asm("v_sub_u32_e64 %0, %5, %9 clamp\n\t"
+            "v_sub_u32_e64 %1, %6, %9 clamp\n\t"
+            "v_sub_u32_e64 %2, %7, %9 clamp\n\t"
+            "v_sub_u32_e64 %3, %8, %9 clamp\n\t"
+            "v_min_u32_e32 %0, 1, %0\n\t"
+            "v_min_u32_e32 %1, 1, %1\n\t"
+            "v_min_u32_e32 %2, 1, %2\n\t"
+            "v_min_u32_e32 %3, 1, %3\n\t"
+            "v_add3_u32 %4, %0, %1, %2"
+            : "=&v"(d0), "=&v"(d1), "=&v"(d2), "=&v"(d3), "=&v"(gt)
+            : "v"(n.x), "v"(n.y), "v"(n.z), "v"(n.w), "v"(x));
+        return p * 5u + 4u - (gt + d3);
+    }
     unsigned r = p * 5u;
     asm("v_cmp_le_u32_e32 vcc, %1, %5\n\t"
         "v_addc_co_u32_e32 %0, vcc, 0, %0, vcc\n\t"
