@@ -1010,13 +1010,16 @@ __global__ __launch_bounds__(kThreads) void surrogate_ticket_kernel(
 // Nothing waits on a workgroup that waits: the rows every reducer needs come from workgroups that
 // never wait (and from the reducers' own rows, stored before they reduce), and at most R of the
 // grid's resident slots are ever held by waiting workgroups. Bitwise reproducible.
-template <typename YT, int S, int R>
+// EXTRA: the R reducers are R extra workgroups after the nstream streaming ones (they stream
+// nothing; a streaming workgroup never waits) instead of the last R streaming workgroups.
+template <typename YT, int S, int R, bool EXTRA, bool NO_REDUCE = false>
 __global__ __launch_bounds__(kThreads) void surrogate_tail_kernel(
     const float* __restrict__ h, const YT* __restrict__ y, int64_t B, double invB,
     const float* __restrict__ abalpha, const float* __restrict__ p_hat, float* __restrict__ dh,
     unsigned long long* __restrict__ rows, unsigned long long* __restrict__ gwords,
-    double* __restrict__ out64, float* __restrict__ grad3, float* __restrict__ loss) {
+    double* __restrict__ out64, float* __restrict__ grad3, float* __restrict__ loss, int64_t nstream) {
     const SurrogateScalars s = make_scalars(abalpha, p_hat, invB);
+    if (!EXTRA || int64_t(blockIdx.x) < nstream) {
     Acc acc;
     const bool write_dh = dh != nullptr;
     const int64_t base = int64_t(blockIdx.x) * chunk_elems(S);
@@ -1063,10 +1066,11 @@ __global__ __launch_bounds__(kThreads) void surrogate_tail_kernel(
         __hip_atomic_store((gu64*)(rows + int64_t(blockIdx.x) * kRowWords + k), enc_word(v), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
     }
-    const int64_t nblocks = gridDim.x;
+    }
+    const int64_t nblocks = EXTRA ? nstream : int64_t(gridDim.x);  // rows
     const int64_t nred = nblocks < R ? nblocks : R;
-    const int64_t r = int64_t(blockIdx.x) - (nblocks - nred);
-    if (r < 0) return;
+    const int64_t r = EXTRA ? int64_t(blockIdx.x) - nstream : int64_t(blockIdx.x) - (nblocks - nred);
+    if (r < 0 || r >= nred || NO_REDUCE) return;
 
     // reducer r: the rows of group r; reducer nred - 1 (whose group holds the grid's last rows)
     // also takes the other group totals, loaded before its own group so that their trip overlaps
@@ -1136,17 +1140,18 @@ __global__ __launch_bounds__(kThreads) void surrogate_tail_kernel(
     }
 }
 
-template <typename YT, int S, int R>
+template <typename YT, int S, int R, bool EXTRA = false, bool NO_REDUCE = false>
 int launch_tail(const float* h, const YT* y, int64_t B, const float* abalpha, const float* p_hat, float* dh,
                 double* out64, float* grad3, float* loss, void* ws, size_t ws_bytes, hipStream_t st) {
     const int64_t nblocks = (B + chunk_elems(S) - 1) / chunk_elems(S);
-    if (nblocks > 0x7fffffffLL) return DAUC_EINVAL;
+    if (nblocks + R > 0x7fffffffLL) return DAUC_EINVAL;
     const size_t need = kPersistentBytes + static_cast<size_t>(nblocks + R) * kRowWords * 8;
     if (ws == nullptr || ws_bytes < need) return DAUC_EINVAL;
     auto* rows = reinterpret_cast<unsigned long long*>(static_cast<char*>(ws) + kPersistentBytes);
-    hipLaunchKernelGGL((surrogate_tail_kernel<YT, S, R>), dim3(static_cast<unsigned>(nblocks)), dim3(kThreads), 0, st,
-                       h, y, B, 1.0 / static_cast<double>(B), abalpha, p_hat, dh, rows, rows + nblocks * kRowWords,
-                       out64, grad3, loss);
+    const int64_t grid = EXTRA ? nblocks + R : nblocks;
+    hipLaunchKernelGGL((surrogate_tail_kernel<YT, S, R, EXTRA, NO_REDUCE>), dim3(static_cast<unsigned>(grid)), dim3(kThreads), 0,
+                       st, h, y, B, 1.0 / static_cast<double>(B), abalpha, p_hat, dh, rows, rows + nblocks * kRowWords,
+                       out64, grad3, loss, nblocks);
     return launch_status();
 }
 
@@ -1290,6 +1295,12 @@ int launch_surrogate(const float* h, int64_t hs, const YT* y, int64_t B, const f
                 case 23: return launch_tail<YT, 4, 128>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, ws, ws_bytes, st);
                 case 24: return launch_tail<YT, 4, 256>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, ws, ws_bytes, st);
                 case 25: return launch_chunk<YT, false, kChunkSlots, true, true>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, sums4, accumulate, ws, ws_bytes, st);
+                case 26: return launch_tail<YT, 4, 64, true>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, ws, ws_bytes, st);
+                case 27: return launch_tail<YT, 4, 32, true>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, ws, ws_bytes, st);
+                case 28: return launch_tail<YT, 4, 128, true>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, ws, ws_bytes, st);
+                // timing only: the one-launch stream with its data-as-flag row stores, nobody reducing
+                // (rows are left in the workspace: give it one of its own, like variant 15)
+                case 29: return launch_tail<YT, 4, 64, false, true>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, ws, ws_bytes, st);
                 default: return DAUC_EINVAL;
             }
         }
@@ -1483,7 +1494,7 @@ int dauc_surrogate_fwdbwd_variant(const float* h, int64_t h_stride, const void* 
                                   double* out64, float* grad3, float* loss, void* workspace,
                                   size_t workspace_bytes, int variant, dauc_stream_t stream) {
     if (B <= 0 || h == nullptr || y == nullptr || abalpha == nullptr || p_hat == nullptr ||
-        h_stride <= 0 || (dh != nullptr && dh_stride <= 0) || variant < 0 || variant > 25)
+        h_stride <= 0 || (dh != nullptr && dh_stride <= 0) || variant < 0 || variant > 29)
         return DAUC_EINVAL;
     return dispatch_labels<false>(h, h_stride, y, y_dtype, B, abalpha, p_hat, dh, dh_stride, out64,
                                   grad3, loss, nullptr, 0, workspace, workspace_bytes,

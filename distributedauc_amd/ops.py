@@ -148,7 +148,7 @@ def surrogate_fwdbwd(h: torch.Tensor, y: torch.Tensor, abalpha: torch.Tensor, p_
     L = _lib.load()
     nbytes = L.dauc_surrogate_workspace_size(B)
     # variant 15 (the streaming kernel alone) leaves its rows behind: a workspace of its own
-    ws = workspaces.get(dev, "surrogate_stream_only" if variant == 15 else "surrogate", nbytes)
+    ws = workspaces.get(dev, "surrogate_stream_only" if variant in (15, 29) else "surrogate", nbytes)
     if variant == 0:
         rc = L.dauc_surrogate_fwdbwd(_ptr(h), h.stride(0), _ptr(y), yc, B, _ptr(abalpha), _ptr(p_hat),
                                      _ptr(dh), dh_stride, _ptr(out64), _ptr(grad3), _ptr(loss), _ptr(ws),

@@ -111,8 +111,9 @@ int dauc_surrogate_fwdbwd(const float* h, int64_t h_stride, const void* y, int y
  * 4 / 8 / 16 / 32 chunks (4 slots) per workgroup, next chunk's loads in flight, so the row
  * reduce is one small workgroup; 20..24 the row reduce inside the streaming launch, by its last
  * 32 / 16 / 64 / 128 / 256 workgroups (data-as-flag rows, no second launch; 64 is what variant 0
- * runs for unit-stride B >= 2^22), 25 the two-launch form (stream + row-reduce kernel). Variants
- * 2..25 need unit strides, 16-byte
+ * runs for unit-stride B >= 2^22), 25 the two-launch form (stream + row-reduce kernel), 26..28
+ * the reduce by 64 / 32 / 128 EXTRA workgroups appended to the grid (they stream nothing). Variants
+ * 2..28 need unit strides, 16-byte
  * aligned h/dh and int8 labels, and B <= 2^31. Every variant returns bitwise-identical dh and counts;
  * the fp64 sums agree to rounding (their reduction trees differ).
  */

@@ -148,7 +148,7 @@ def test_surrogate_chunked_variants(dev, B):
     ref_dh = None
     tick = {}
     for variant in (0, 0, 1, 2, 3, 4, 5, 6, 7, 8, 8, 9, 10, 11, 12, 13, 14, 2, 8, 1, 12, 14, 16, 17, 18, 19, 19,
-                    0, 16, 20, 20, 21, 22, 0, 20, 8, 21, 23, 24, 25, 0, 25, 24):
+                    0, 16, 20, 20, 21, 22, 0, 20, 8, 21, 23, 24, 25, 0, 25, 24, 26, 27, 28, 26, 0, 28):
         o = torch.zeros(6, dtype=torch.float64, device=dev)
         dh = torch.full((B,), float("nan"), device=dev)
         ops.surrogate_fwdbwd(h, y, abap[:3], abap[3:], dh=dh, out64=o, variant=variant)
