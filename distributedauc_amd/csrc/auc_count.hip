@@ -281,7 +281,9 @@ constexpr int kCmpTile = kCmpThreads * 16 * kCmpSlots;  // 32768 labels per bloc
 int64_t compact_blocks(int64_t n) { return (n + kCmpTile - 1) / kCmpTile; }
 
 // per tile: positives, labels outside {-1, 1}
-inline size_t compact_ws_bytes(int64_t n) { return 64 + static_cast<size_t>(compact_blocks(n)) * 2 * sizeof(int); }
+// then the positive bit masks of every tile (1 bit per label: 4 KB per 32768-label tile)
+inline size_t compact_masks_offset(int64_t n) { return (64 + static_cast<size_t>(compact_blocks(n)) * 2 * sizeof(int) + 255) / 256 * 256; }
+inline size_t compact_ws_bytes(int64_t n) { return compact_masks_offset(n) + static_cast<size_t>(compact_blocks(n)) * kCmpThreads * 16; }
 
 // bytes == 0 -> 0x80 in that byte, 0 elsewhere (exact, no carries between bytes)
 __device__ __forceinline__ unsigned zero_bytes(unsigned v) {
@@ -330,18 +332,22 @@ __device__ __forceinline__ unsigned label_masks16(const LT* __restrict__ lab, in
     return pos;
 }
 
-// Two launches. (1) count: per tile, its positives and its labels outside {-1, 1}. (2) write:
-// every tile first sums the positive counts of the tiles before it (its 256 threads read them
-// strided from L2 and reduce: no scan launch, no inter-workgroup wait), then writes its positives'
-// scores at that offset in tile order; the last tile also sums every tile's counts into stats[].
+// Two launches. (1) count: per tile, its positives and its labels outside {-1, 1}, and the
+// positive bit masks (1 bit per label, one 16-B store per thread). (2) write: every tile first
+// sums the positive counts of the tiles before it (its 256 threads read them strided from L2 and
+// reduce: no scan launch, no inter-workgroup wait), then reads its masks — not the labels again:
+// 1/8 of the bytes at int8 — and writes its positives' scores at that offset in tile order; the
+// last tile also sums every tile's counts into stats[].
 // A single-launch decoupled look-back was built and measured: with ~1 µs of work per tile and
 // ~2 µs per cross-XCD round trip its prefix frontier advances one 64-tile window per round trip
 // (2^27 labels: 298 µs against this form's count + write).
 template <typename LT>
 __global__ __launch_bounds__(kCmpThreads) void compact_count_kernel(const LT* __restrict__ lab, int64_t n,
                                                                     int vec, int* __restrict__ blk,
+                                                                    uint4* __restrict__ masks,
                                                                     int64_t* __restrict__ stats,
                                                                     unsigned long long* __restrict__ zero3) {
+    static_assert(kCmpSlots == 8, "8 16-bit group masks = one uint4 per thread");
     __shared__ int part[2][kCmpThreads / kWave];
     const int64_t base = int64_t(blockIdx.x) * kCmpTile;
     if (blockIdx.x == 0 && threadIdx.x < 4) {
@@ -355,6 +361,8 @@ __global__ __launch_bounds__(kCmpThreads) void compact_count_kernel(const LT* __
         m[k] = label_masks16(lab, base + (int64_t(k) * kCmpThreads + threadIdx.x) * 16, n, vec, no);
 #pragma unroll
     for (int k = 0; k < kCmpSlots; ++k) np += __popc(m[k]);
+    masks[int64_t(blockIdx.x) * kCmpThreads + threadIdx.x] =
+        uint4{m[0] | (m[1] << 16), m[2] | (m[3] << 16), m[4] | (m[5] << 16), m[6] | (m[7] << 16)};
     for (int off = 32; off > 0; off >>= 1) {
         np += __shfl_xor(np, off, kWave);
         no += __shfl_xor(no, off, kWave);
@@ -410,9 +418,8 @@ __device__ __forceinline__ long long block_sum_ints(const int* __restrict__ v, i
 
 // every positive's score goes to pos_out[(positives of earlier tiles) + its rank in the tile]; rank
 // order = group k, then thread, then the 16 labels of the group (original order)
-template <typename LT>
 __global__ __launch_bounds__(kCmpThreads) void compact_write_kernel(
-    const float* __restrict__ s, const LT* __restrict__ lab, int64_t n, int vec, int* __restrict__ blk,
+    const float* __restrict__ s, int64_t n, const int* __restrict__ blk, const uint4* __restrict__ masks,
     float* __restrict__ pos_out, int64_t* __restrict__ stats) {
     constexpr int kW = kCmpThreads / kWave;
     __shared__ int cnt[kCmpSlots][kW];
@@ -420,12 +427,10 @@ __global__ __launch_bounds__(kCmpThreads) void compact_write_kernel(
     const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
     const int64_t nblk = gridDim.x;
     const int64_t base = int64_t(blockIdx.x) * kCmpTile;
-    int no = 0;
-    unsigned m[kCmpSlots];
-#pragma unroll
-    for (int k = 0; k < kCmpSlots; ++k)
-        m[k] = label_masks16(lab, base + (int64_t(k) * kCmpThreads + threadIdx.x) * 16, n, vec, no);
-    const int64_t pbase = block_sum_ints(blk, blockIdx.x, red);  // loads overlap the label loads above
+    const uint4 mq = masks[int64_t(blockIdx.x) * kCmpThreads + threadIdx.x];
+    const unsigned m[kCmpSlots] = {mq.x & 0xffffu, mq.x >> 16, mq.y & 0xffffu, mq.y >> 16,
+                                   mq.z & 0xffffu, mq.z >> 16, mq.w & 0xffffu, mq.w >> 16};
+    const int64_t pbase = block_sum_ints(blk, blockIdx.x, red);
     int excl[kCmpSlots];
 #pragma unroll
     for (int k = 0; k < kCmpSlots; ++k) {
@@ -476,13 +481,14 @@ int launch_compact(const float* s, const LT* lab, int64_t n, float* pos_out, int
     const int64_t nblk = compact_blocks(n);
     if (nblk > 0x7fffffffLL) return DAUC_EINVAL;
     int* blk = static_cast<int*>(ws);
+    auto* masks = reinterpret_cast<uint4*>(static_cast<char*>(ws) + compact_masks_offset(n));
     const int vec = (reinterpret_cast<uintptr_t>(lab) & 15u) == 0;
     hipLaunchKernelGGL(compact_count_kernel<LT>, dim3(static_cast<unsigned>(nblk)), dim3(kCmpThreads), 0, st, lab, n,
-                       vec, blk, stats, zero3);
+                       vec, blk, masks, stats, zero3);
     int rc = launch_status();
     if (rc) return rc;
-    hipLaunchKernelGGL(compact_write_kernel<LT>, dim3(static_cast<unsigned>(nblk)), dim3(kCmpThreads), 0, st, s, lab,
-                       n, vec, blk, pos_out, stats);
+    hipLaunchKernelGGL(compact_write_kernel, dim3(static_cast<unsigned>(nblk)), dim3(kCmpThreads), 0, st, s, n, blk,
+                       masks, pos_out, stats);
     return launch_status();
 }
 
@@ -715,7 +721,7 @@ int compact_positives_zeroing(const float* scores, const void* labels, int label
                               hipStream_t st) {
     if (n <= 0 || scores == nullptr || labels == nullptr || pos_out == nullptr || stats == nullptr ||
         workspace == nullptr || workspace_bytes < dauc_compact_workspace_size(n) ||
-        (reinterpret_cast<uintptr_t>(workspace) & 7u) || (reinterpret_cast<uintptr_t>(stats) & 7u))
+        (reinterpret_cast<uintptr_t>(workspace) & 15u) || (reinterpret_cast<uintptr_t>(stats) & 7u))
         return DAUC_EINVAL;
     switch (label_dtype) {
         case DAUC_LABEL_I8:

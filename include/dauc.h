@@ -233,12 +233,13 @@ int dauc_split_scores(const float* scores, const void* labels, int label_dtype, 
  * Stable compaction of the positive scores (label == 1) for the sort method of main.py:79-81
  * (sklearn roc_curve(pos_label=1) -> _binary_clf_curve, _ranking.py:826-908): every label is
  * read once and only the positives' scores are read, so a vector with few positives costs
- * about two label passes (1 B per score at int8) instead of a full split. Two launches (per-tile
- * counts; a write pass in which every tile sums the counts before it itself).
+ * about one label pass (1 B per score at int8) instead of a full split. Two launches (per-tile
+ * counts and 1-bit positive masks; a write pass in which every tile sums the counts before it
+ * itself and reads its masks instead of the labels).
  *   pos_out[0..P) = the positive scores in original order (capacity n)
  *   stats[4] (int64) = { P, n - P, #non-finite POSITIVE scores, #labels not in {-1, 1} }
  * The negatives' scores are checked by dauc_auc_counts_sorted_labeled (its nonfinite count).
- * workspace >= dauc_compact_workspace_size(n) bytes, 8-byte aligned; no zeroing needed.
+ * workspace >= dauc_compact_workspace_size(n) bytes, 16-byte aligned; no zeroing needed.
  */
 size_t dauc_compact_workspace_size(int64_t n);
 int dauc_compact_positives(const float* scores, const void* labels, int label_dtype, int64_t n,
