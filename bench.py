@@ -78,7 +78,9 @@ def parse(argv=None):
     p.add_argument("--sweep-I", default="1,8,16,32", help="configs[2] averaging periods ('' = off)")
     p.add_argument("--sweep-steps", type=int, default=32, help="timed steps per period (a multiple of every I)")
     p.add_argument("--r18-steps", type=int, default=16, help="configs[0] GPU leg: timed ResNet-18 b32 steps (0 = off)")
-    p.add_argument("--r18-graph", type=int, default=1, help="configs[0] GPU leg: replay the step body as a HIP graph (1/0)")
+    p.add_argument("--r18-graph", type=int, default=1,
+                   help="configs[0] GPU leg at N=1: replay the step body as a HIP graph (1/0); N>1 runs eager "
+                        "(2 gloo ranks sharing one GPU replayed slower than eager: profiles/r02/graph/)")
     p.add_argument("--auc-log2n", type=int, default=24)
     p.add_argument("--auc-pos", type=float, default=0.01)
     p.add_argument("--auc-reps", type=int, default=3)
@@ -295,7 +297,7 @@ def bench_r18(args, world, rank, device):
     """configs[0] on the GPUs: ResNet-18 CoDA, batch 32 per rank, 224^2, I = 8 (the CPU path of
     the same config is cpu_baseline_configs0)."""
     coda, it = make_coda("resnet18", 32, args.image_size, 8, args.pos_ratio, args.pool, world, rank, device,
-                         args.fused_bn, args.gemm_conv1x1, graph=bool(args.r18_graph))
+                         args.fused_bn, args.gemm_conv1x1, graph=bool(args.r18_graph) and world == 1)
     for _ in range(max(args.warmup, 8)):
         x, y = next(it)
         coda.train_step(x, y)
@@ -304,8 +306,8 @@ def bench_r18(args, world, rank, device):
     dt = timed_steps(coda, it, steps, world)
     rec = {"workload": "resnet18 CoDA, batch 32 per rank, 224x224, I=8, bf16 autocast backbone, fp32 AUC kernels "
                        "(BASELINE configs[0] on the GPUs)"
-                       + (", step bodies replayed from one HIP graph (averaging rounds eager)" if args.r18_graph else ""),
-           "graph": bool(args.r18_graph),
+                       + (", step bodies replayed from one HIP graph (averaging rounds eager)" if coda._graph_on else ""),
+           "graph": coda._graph_on, "graph_captures": coda.graph_captures,
            "imgs_per_sec": world * 32 * steps / dt, "ms_per_step": dt / steps * 1e3, "steps": steps,
            "n_gpus": world, "params": coda.state.numel(), "final_loss": float(coda.last_loss.item())}
     del coda, it

@@ -71,6 +71,7 @@ class CoDA:
         self._graph_on = False
         self._graph = None
         self._graph_key = None
+        self.graph_captures = 0
 
     # ---------------------------------------------------------------- plumbing
     def _autocast(self):
@@ -203,9 +204,12 @@ class CoDA:
             for t, s in zip(state, snap):
                 t.copy_(s)
         graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
+        # thread_local: a communicator's helper threads (RCCL's proxy) may touch the runtime while
+        # this thread captures; only this thread's calls must be capturable
+        with torch.cuda.graph(graph, capture_error_mode="thread_local"):
             self._gloss = self.step_body(self._gx, self._gy)
         self._graph, self._graph_key = graph, key
+        self.graph_captures += 1
 
     # ---------------------------------------------------------------- loop
     def run(self, batches: Iterator, *, num_stages: int, total_iter: int, test_freq: int | None = None,
