@@ -20,7 +20,8 @@ import sys
 
 ALGORITHMIC = {"pd_update": 24 * 23_512_130, "surrogate_2^26": 9 * (1 << 26),
                # configs[4] sort-method passes at 2^27 scores, 0.1 % positives (134,447 of them)
-               "compact_count_2^27": 1 << 27, "compact_write_2^27": (1 << 27) + 8 * 134_447,
+               "compact_count_2^27": (1 << 27) + (1 << 27) // 8,          # labels + 1-bit masks
+               "compact_write_2^27": (1 << 27) // 8 + 8 * 134_447,        # masks + positives read & written
                "query_labeled_2^27": 5 * (1 << 27)}
 
 
