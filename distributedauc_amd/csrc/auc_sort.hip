@@ -10,21 +10,21 @@
 // Keys: an fp32 score maps to a uint32 that orders like the float, with -0 and
 // +0 on one key (fp32 equality semantics): k = bits ^ (sign ? 0xffffffff : 0x80000000).
 //
-// Sort (per 8-bit digit, 4 passes, keys only):
-//   hist    : one block per 4096-key tile, 256-bin LDS histogram -> hist[digit][tile]
-//   scan    : exclusive scan over the digit-major hist array (decoupled 3-step scan)
-//   scatter : each tile re-reads its keys in 16 chunks of 256; a key's rank among the
-//             tile's keys with the same digit comes from 8 wave ballots (wave multisplit)
-//             plus per-digit wave/chunk offsets in LDS, so the scatter is STABLE (LSD
-//             correctness needs it); writes to out[offset[digit][tile] + rank].
-// Search: every k-th sorted key (k a power of two, so at most 32767 splitters) goes into an
-//   Eytzinger (BFS-order) tree, which every workgroup loads into LDS once; one query key x
-//   walks it twice in lockstep (x and x - 1: the splitters <= x and < x; BFS order puts
-//   each level's nodes side by side, so a level's reads spread over the LDS banks instead
-//   of all landing in one as a sorted array's power-of-two strides do), then one vector
-//   load of its k-key bucket from the (L2-resident) sorted table finishes upper_bound and
-//   lower_bound. The queries are streamed once with float4 loads; per-block integer sums,
-//   one 64-bit atomic each.
+// Sort (per 8-bit digit, 4 passes, keys only; 2048-key tiles, one 256-thread workgroup each):
+//   hist    : LDS histogram of the tile's digit -> hist[digit][tile] (digit-major)
+//   scan    : small sorts (<= 256 tiles) have none — every scatter workgroup derives its own
+//             offsets from the raw histogram; larger sorts scan it in 1 or 3 launches
+//   scatter : wave w owns the tile's keys [512w, 512w + 512); a key's stable rank among its
+//             wave's keys with the same digit = the wave's running count of that digit (a
+//             wave-private LDS row) + the same-digit lanes below it (8 ballots); one barrier turns
+//             the per-wave counts into offsets; writes to out[offset[digit][tile] + rank].
+// Search: every k-th sorted key (k a power of two, at most kMaxSplit splitters) is a key of a
+//   5-ary search tree of 16-byte nodes (4 keys, one ds_read_b128 per level) that every query
+//   workgroup copies into LDS; each level stores only its real prefix plus one all-padding
+//   node. A query x, clamped below the largest splitter, walks <= 7 levels (p <- 5p + #(node
+//   keys <= x)), then one 16-byte load of its k-key bucket from the (L2-resident) sorted table
+//   finishes upper_bound and lower_bound. The queries are streamed once with float4 loads;
+//   per-block integer sums, one 64-bit atomic each.
 //   table = positives: W += M - ub(x), T += ub - lb;  table = negatives: W += lb(x), T += ub - lb.
 
 #include <type_traits>

@@ -10,6 +10,13 @@
 // Per 4-element slot the fp32 partials of sum(h-a), sum(h-b), sum((h-a)^2),
 // sum((h-b)^2) are folded into fp64; with the two class counts they are reduced
 // wave -> block -> grid in a fixed order, so results are bitwise reproducible.
+//
+// Two geometries: unit-stride batches >= 2^22 (the streaming size) take ONE launch of
+// surrogate_tail_kernel — one 4096-element chunk per workgroup, rows handed to the last 64
+// workgroups as data-as-flag words, which reduce them (see the comment at that kernel); smaller
+// or strided batches (training, B = 256) take the persistent kernel with one last-arriver
+// ticket. The other kernels below are tuning variants kept measurable through
+// dauc_surrogate_fwdbwd_variant (include/dauc.h).
 
 #include <hip/hip_bf16.h>
 
