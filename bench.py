@@ -329,7 +329,8 @@ def bench_auc(args, world, rank, device, log2n=None, pos=None, pair_reps=None):
     out = {"n": n, "log2n": log2n, "pos": pos}
     # the sort method on one GPU is ONE blocking C call (dauc_auc_eval_counts); over ranks the
     # compaction, the all-gathers and dauc_auc_counts_sorted_labeled are separate
-    sort_fn = "dauc_auc_eval_counts" if world == 1 else "dauc_auc_counts_sorted_labeled"
+    sort_fn = ("dauc_auc_eval_counts" if world == 1 or n < ExactAUC.SHARD_MIN
+               else "dauc_auc_counts_sorted_labeled")
     for method, fn in (("sort", sort_fn), ("pairs", "dauc_pair_count_variant")):
         ev = ExactAUC(world=world, rank=rank, variant=args.variant, method=method)
         kt = KernelTimer(_lib.load(), fn)
@@ -348,7 +349,8 @@ def bench_auc(args, world, rank, device, log2n=None, pos=None, pair_reps=None):
         kt.enabled = False
         kt.restore()
         out["m_" + method] = {"t_eval": max_over_ranks(float(np.median(times)), world),
-                              "t_count": max_over_ranks(kt.mean_ms() / 1e3, world), "count_fn": fn, "counts": c}
+                              "t_count": max_over_ranks(kt.mean_ms() / 1e3, world), "count_fn": fn, "counts": c,
+                              "mode": ev.last_mode}
         log(f"rank {rank}: auc 2^{log2n} {method} eval {out['m_' + method]['t_eval'] * 1e3:.2f} ms")
     a, b = out["m_sort"]["counts"], out["m_pairs"]["counts"]
     if (a["wins"], a["ties"]) != (b["wins"], b["ties"]):
@@ -370,8 +372,10 @@ def auc_record(auc, world, config_name):
     eval_bytes = n * (2 * 1 + 4 + 1) // world
     return {
         "workload": f"exact AUC, 2^{auc['log2n']} fp32 scores, {auc['pos']:.1%} positives "
-                    f"(BASELINE {config_name}), sharded over {world} rank(s) (sort: score-index ranges; pair count: "
-                    "positive blocks), int64 all-reduce",
+                    f"(BASELINE {config_name}), {world} rank(s); sort method {sk['mode']} "
+                    "(sharded = score-index ranges + int64 all-reduce; replicated = every rank evaluates the whole "
+                    "vector, below 2^25 scores); pair count: positive blocks, int64 all-reduce",
+        "sort_mode": sk["mode"],
         "pairs_per_sec": npairs / sk["t_eval"],
         "method": "sort (default evaluator: compact the positives reading labels only, radix-sort them, locate "
                   "every negative through an LDS search tree, read in place; on one GPU one blocking C call that "

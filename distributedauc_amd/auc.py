@@ -61,8 +61,13 @@ def _as_device_pair(label, scores, device):
 class ExactAUC:
     """Exact AUC evaluator; sharded over a process group when world > 1."""
 
+    # Below this many scores the sort method does not shard: every rank evaluates the whole vector
+    # (same integers, no collective). Sharding saves ~5 ns per query per rank but costs two small
+    # all-gathers with a host sync and an all-reduce (~150-200 us), so it pays from ~2^25 scores.
+    SHARD_MIN = 1 << 25
+
     def __init__(self, group=None, world: int = 1, rank: int = 0, variant: int = 0, reduce: bool = True,
-                 method: str = "sort"):
+                 method: str = "sort", shard_min: int | None = None):
         if method not in ("sort", "pairs"):
             raise ValueError("method must be 'sort' (radix sort + search) or 'pairs' (pair-count kernel)")
         self.group = group
@@ -71,6 +76,8 @@ class ExactAUC:
         self.variant = variant
         self.reduce = reduce  # False: return only this rank's share (no collective)
         self.method = method
+        self.shard_min = self.SHARD_MIN if shard_min is None else int(shard_min)
+        self.last_mode = None  # "single", "replicated" or "sharded" (the last call's)
 
     def counts(self, label, scores, device=None) -> dict:
         """Exact {wins, ties, P, N} (Python ints). One host sync for the split sizes."""
@@ -84,14 +91,17 @@ class ExactAUC:
             y, s = _as_device_pair(label, scores, device)
         if y.numel() != s.numel():
             raise ValueError(f"Found input variables with inconsistent numbers of samples: {[y.numel(), s.numel()]}")
-        if self.method == "sort" and self.world == 1:
-            # one GPU: the whole evaluation is one blocking C call (same stages, no host work between)
+        if self.method == "sort" and (self.world == 1 or (self.reduce and s.numel() < self.shard_min)):
+            # one GPU (or a vector too small to be worth sharding: every rank evaluates all of it):
+            # the whole evaluation is one blocking C call (same stages, no host work between)
+            self.last_mode = "single" if self.world == 1 else "replicated"
             W, T, P, N, nonfinite, other = ops.auc_eval_counts(s, y)
             if nonfinite:
                 raise ValueError("Input y_score contains NaN or infinity.")
             if other and torch.unique(y).numel() > 2:
                 raise ValueError("multiclass format is not supported")
             return {"wins": W, "ties": T, "P": P, "N": N}
+        self.last_mode = "sharded" if self.world > 1 else "single"
         if self.method == "pairs":
             # stable split: every rank sees the positives in the same order, so positive blocks shard
             pos, neg, stats = ops.split_scores(s, y)

@@ -100,6 +100,20 @@ def auc_counts_sorted_labeled(pos, scores, labels, begin, end, wins_ties, nonfin
         nonfinite[0] += int((~np.isfinite(neg)).sum())
 
 
+def auc_eval_counts(scores, labels):
+    """The one-call evaluation stand-in: (W, T, P, N, non-finite, other) by the C oracle."""
+    from oracle import coracle
+
+    s, y = scores.detach().numpy(), labels.numpy().astype(np.int64)
+    P = int((y == 1).sum())
+    bad = int((~np.isfinite(s)).sum())
+    other = int(((y != 1) & (y != -1)).sum())
+    if bad or P == 0 or P == s.size:
+        return 0, 0, P, s.size - P, bad, other
+    e = coracle.auc_counts(np.where(y == 1, 1, -1), s)
+    return e["wins"], e["ties"], P, s.size - P, 0, other
+
+
 def coracle_pair_count(pos, neg):
     from oracle import coracle
 
@@ -110,7 +124,7 @@ def install(monkeypatch):
     from distributedauc_amd import flat, ops
 
     for name in ("label_map_phat", "surrogate_fwdbwd", "class_sums", "alpha_from_sums", "coda_finalize",
-                 "scale_div", "pd_update", "compact_positives", "auc_counts_sorted_labeled"):
+                 "scale_div", "pd_update", "compact_positives", "auc_counts_sorted_labeled", "auc_eval_counts"):
         monkeypatch.setattr(ops, name, globals()[name])
     monkeypatch.setattr(flat, "_check_device", lambda dev: None)
 

@@ -1,7 +1,9 @@
 """The sharded exact-AUC orchestration on CPU (gloo, world 2 and 3): each rank compacts the
 positives of its own index slice, all ranks all-gather them (in order) and stream their slice of
-the scores through the count; one all-reduce of (wins, ties, non-finite). The kernels are served
-by the oracle (tests/cpu_kernels.py); the GPU form runs in bench.py --gpus 2 (tests/test_bench_gpu.py)."""
+the scores through the count; one all-reduce of (wins, ties, non-finite). Below
+ExactAUC.SHARD_MIN scores every rank evaluates the whole vector instead (same integers, no
+collective); both modes run here. The kernels are served by the oracle (tests/cpu_kernels.py);
+the GPU form runs in bench.py --gpus 2 (tests/test_bench_gpu.py)."""
 from __future__ import annotations
 
 import os
@@ -14,7 +16,7 @@ import cpu_kernels
 from test_coda_gloo import _free_port
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, shard_min):
     import traceback
 
     import torch.distributed as dist
@@ -32,8 +34,9 @@ def _worker(rank, world, port, q):
         n = 20_011
         s = (np.floor(rng.random(n) * 997) / 997).astype(np.float32)
         y = np.where(rng.random(n) < 0.03, 1, -1).astype(np.int8)
-        ev = ExactAUC(world=world, rank=rank, method="sort")
+        ev = ExactAUC(world=world, rank=rank, method="sort", shard_min=shard_min)
         c = ev.counts(torch.from_numpy(y), torch.from_numpy(s), device="cpu")
+        assert ev.last_mode == ("sharded" if n >= shard_min else "replicated"), ev.last_mode
         e = coracle.auc_counts(y.astype(np.int64), s)
         assert (c["wins"], c["ties"], c["P"], c["N"]) == (e["wins"], e["ties"], e["P"], e["N"]), (c, e)
         # a non-finite negative in one rank's slice is seen by every rank after the reduce
@@ -51,15 +54,16 @@ def _worker(rank, world, port, q):
         q.put((rank, traceback.format_exc()))
 
 
+@pytest.mark.parametrize("shard_min", [0, 1 << 25])
 @pytest.mark.parametrize("world", [2, 3])
 @pytest.mark.timeout(300)
-def test_sharded_sort_auc_gloo(world):
+def test_sharded_sort_auc_gloo(world, shard_min):
     import torch.multiprocessing as mp
 
     ctx = mp.get_context("spawn")
     q = ctx.SimpleQueue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, shard_min)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
