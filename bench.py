@@ -127,8 +127,13 @@ def host_info() -> dict:
     except AttributeError:
         affinity = os.cpu_count() or 1
     omp = os.environ.get("OMP_NUM_THREADS")
-    budget = min(affinity, int(omp)) if omp and omp.isdigit() and int(omp) > 0 else affinity
-    return {"nproc": os.cpu_count(), "affinity_cpus": affinity, "omp_num_threads": omp, "cpu_budget": budget}
+    if omp == "1" and int(os.environ.get("LOCAL_WORLD_SIZE", "1")) > 1:
+        # torch.distributed.run exports OMP_NUM_THREADS=1 when the environment had none; the CPU
+        # baselines run on rank 0 alone while the other ranks wait, so use the default share
+        omp = None
+    budget = min(affinity, int(omp)) if omp and omp.isdigit() and int(omp) > 0 else min(affinity, 16)
+    return {"nproc": os.cpu_count(), "affinity_cpus": affinity, "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
+            "cpu_budget": budget}
 
 
 # ----------------------------------------------------------------------------- timing helpers
