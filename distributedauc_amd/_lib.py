@@ -71,6 +71,7 @@ SIGNATURES = {
     "dauc_auc_eval_counts": (_int, [_vp, _vp, _int, _i64, _vp, _vp, _sz, _vp]),
     "dauc_compact_positives": (_int, [_vp, _vp, _int, _i64, _vp, _vp, _vp, _sz, _vp]),
     "dauc_sort_keys": (_int, [_vp, _i64, _vp, _vp, _sz, _vp]),
+    "dauc_set_search_mode": (_int, [_int]),
     "dauc_bn_workspace_size": (_sz, [_i64, _int]),
     "dauc_bn_act_forward": (_int, [_vp, _int, _i64, _int, _vp, _int, _vp, _vp, _vp, _vp, _f32, _f32, _vp, _vp, _vp,
                                    _vp, _sz, _vp]),

@@ -627,6 +627,99 @@ __device__ __forceinline__ void count_queries(const unsigned (&x)[Q], const bool
     }
 }
 
+// Two-phase form of count_queries for Q = 4 lockstep queries and K = 2, 4, 8 (the labeled
+// kernel's hot loop), a measured variant (DAUC_QUERY_PIPE=1): phase A walks the tree and
+// issues the bucket loads of every slot of an iteration, then the next iteration's stream loads
+// are issued, then phase B compares and counts -- so no wait for a bucket load also waits out a
+// streaming load's HBM latency (vmcnt retires in issue order). Same speed as the one-phase loop
+// (2^27 @ 0.1 %: 699 vs 684 us per sort + query; 2^24 @ 1 %: 165 vs 170 us;
+// profiles/r02/query_tuning/micro_pipe.jsonl): the query pass is not bound by load latency.
+#ifndef DAUC_QUERY_PIPE
+#define DAUC_QUERY_PIPE 0
+#endif
+#ifndef DAUC_QUERY_PIPE_U
+#define DAUC_QUERY_PIPE_U 2  // float4 slots per iteration of the batched loop (int8 labels)
+#endif
+template <int K>
+constexpr bool pipelined() {
+    return DAUC_QUERY_PIPE != 0 && (K == 2 || K == 4 || K == 8) && lockstep_queries<K>() == 4;
+}
+
+template <int K>
+__device__ __forceinline__ void load_bucket(const unsigned* __restrict__ sorted, unsigned b, unsigned (&v)[K]) {
+    const unsigned* p = sorted + size_t(b) * K;
+    if constexpr (K == 2) {
+        const uint2 u = *reinterpret_cast<const uint2*>(p);
+        v[0] = u.x;
+        v[1] = u.y;
+    } else {
+#pragma unroll
+        for (int q = 0; q < K / 4; ++q) {
+            const uint4 u = reinterpret_cast<const uint4*>(p)[q];
+            v[4 * q] = u.x;
+            v[4 * q + 1] = u.y;
+            v[4 * q + 2] = u.z;
+            v[4 * q + 3] = u.w;
+        }
+    }
+}
+
+template <int K>
+__device__ __forceinline__ void walk_and_load(const unsigned (&x)[4], unsigned (&su)[4], unsigned (&v)[4][K],
+                                              const TreeNode* __restrict__ tree, const TreeGeom& g,
+                                              const TopKeys& top, const unsigned* __restrict__ sorted) {
+    tree_walk<4>(x, su, tree, g, top);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) load_bucket<K>(sorted, su[q] ? su[q] - 1u : 0u, v[q]);
+}
+
+template <int K, bool TABLE_POS>
+__device__ __forceinline__ void finish_counts(const unsigned (&x)[4], const bool (&use)[4], const unsigned (&su)[4],
+                                              const unsigned (&v)[4][K], const TreeNode* __restrict__ tree,
+                                              const TreeGeom& g, const TopKeys& top,
+                                              const unsigned* __restrict__ sorted, int64_t M,
+                                              unsigned long long& w, unsigned long long& t) {
+    bool slow = false;
+    unsigned wl = 0u, tl = 0u;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        int le = 0, lt = 0;
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            le += v[q][j] <= x[q];
+            lt += v[q][j] < x[q];
+        }
+        const unsigned base = su[q] ? (su[q] - 1u) * static_cast<unsigned>(K) : 0u;
+        const unsigned ub = su[q] ? base + static_cast<unsigned>(le) : 0u;
+        const unsigned lb = su[q] ? base + static_cast<unsigned>(lt) : 0u;
+        const unsigned wq = TABLE_POS ? static_cast<unsigned>(M) - ub : lb;
+        wl += use[q] ? wq : 0u;
+        tl += use[q] ? ub - lb : 0u;
+        slow |= use[q] && su[q] != 0u && v[q][0] >= x[q];
+    }
+    w += wl;
+    t += tl;
+    if (slow) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            if (!(use[q] && su[q] != 0u && v[q][0] >= x[q])) continue;
+            const unsigned xm[1] = {x[q] - 1u};
+            unsigned j[1];
+            tree_walk<1>(xm, j, tree, g, top);
+            unsigned lb_true = 0u;
+            if (j[0] != 0u) {
+                int le2 = 0, lt2 = 0;
+                unsigned f2 = 0;
+                bucket_counts<K>(sorted, M, j[0] - 1u, x[q], le2, lt2, f2);
+                lb_true = (j[0] - 1u) * static_cast<unsigned>(K) + static_cast<unsigned>(lt2);
+            }
+            const unsigned lb_fast = (su[q] - 1u) * static_cast<unsigned>(K);
+            t += lb_fast - lb_true;
+            if (!TABLE_POS) w -= lb_fast - lb_true;
+        }
+    }
+}
+
 // Four keys (one float4 slot) with per-key use flags, through count_queries in groups of Q
 // (K = 0, buckets > 32 keys finished in global memory: one key at a time).
 template <int K, bool TABLE_POS>
@@ -722,6 +815,38 @@ __global__ __launch_bounds__(kQueryThreads) void query_count_kernel(const float*
     }
 }
 
+// One float4 slot's 4 labels as loaded (int8: ONE 32-bit word, unpacked where used, so the
+// next iteration's prefetched labels cost 1 VGPR per slot instead of 4)
+template <typename LT>
+struct LabelWords {
+    LT v[4];
+    __device__ __forceinline__ void load(const LT* p) {
+        if constexpr (sizeof(LT) == 4) {
+            const int4 c = *reinterpret_cast<const int4*>(p);
+            v[0] = c.x;
+            v[1] = c.y;
+            v[2] = c.z;
+            v[3] = c.w;
+        } else {
+            const longlong2 c0 = reinterpret_cast<const longlong2*>(p)[0];
+            const longlong2 c1 = reinterpret_cast<const longlong2*>(p)[1];
+            v[0] = c0.x;
+            v[1] = c0.y;
+            v[2] = c1.x;
+            v[3] = c1.y;
+        }
+    }
+    __device__ __forceinline__ void set_positive() { v[0] = v[1] = v[2] = v[3] = LT(1); }
+    __device__ __forceinline__ bool not_positive(int q) const { return v[q] != LT(1); }
+};
+template <>
+struct LabelWords<int8_t> {
+    unsigned w;
+    __device__ __forceinline__ void load(const int8_t* p) { w = *reinterpret_cast<const unsigned*>(p); }
+    __device__ __forceinline__ void set_positive() { w = 0x01010101u; }
+    __device__ __forceinline__ bool not_positive(int q) const { return ((w >> (8 * q)) & 0xffu) != 1u; }
+};
+
 // Labeled queries: the negatives are not materialised. Elements [begin, end) of the full score
 // and label arrays are streamed (float4 + 4 labels per slot); every element whose label is
 // not +1 is a query against the sorted positives (table = positives).
@@ -745,42 +870,374 @@ __device__ __forceinline__ void label4(const LT* __restrict__ lab, int64_t i, bo
     }
 }
 
-// Every queried score is also checked to be finite (sklearn rejects NaN / inf scores,
-// _ranking.py:868-869): nonfinite (nullable) += #queried non-finite scores. The negatives are
-// never materialised, so this is the only pass that reads their scores.
-template <int K, typename LT>
-__global__ __launch_bounds__(kQueryThreads) void query_labeled_kernel(const float* __restrict__ s,
-                                                                     const LT* __restrict__ lab, int64_t begin,
-                                                                     int64_t end, const TreeNode* __restrict__ gtree,
-                                                                     TreeGeom g, int k,
-                                                                     const unsigned* __restrict__ sorted,
-                                                                     int64_t M, unsigned long long* __restrict__ out,
-                                                                     unsigned long long* __restrict__ nonfinite) {
-    extern __shared__ TreeNode tree[];
-    for (int i = threadIdx.x; i < g.nodes; i += kQueryThreads) tree[i] = gtree[i];
-    const TopKeys top = load_top(gtree, g, sorted, k);
+// ---- radix cell index (a measured alternative to the tree: dauc_set_search_mode(2)) --------
+//
+// The tree walk above is a chain of 7 dependent LDS reads and ~60 VALU per query. The cell
+// index replaces it by arithmetic: the key's top 12 bits (sign, exponent, 3 mantissa bits) pick
+// a top bucket t, whose C_t cells split its 2^20 low key values evenly; C_t = ceil(n_t / mu)
+// for the n_t table keys in the bucket, so a cell holds mu keys on average (mu = 4 for the
+// 2^27 @ 0.1 % table). LDS holds l1[t] = first cell | C_t << 16 and base[c] = #table keys below
+// cell c; global memory (L2-resident) holds every cell's first 16 keys, padded with +inf, as
+// one 64-byte slot. A query is: one LDS read (l1), a multiply-high for its cell, one LDS read2
+// (base[c], base[c+1]) in parallel with the 64-byte slot load, and 16 compares for
+// #(keys < x) and #(keys <= x) -- keys before the cell are all < x, keys after it all > x.
+// Cells with more than 16 keys finish with a binary search of the table beyond the slot.
+// Measured SLOWER than the tree (2^27 @ 0.1 %: 1,176 vs 710 us per sort + query; 2^24 @ 1 %:
+// 273 vs 179 us; profiles/r02/query_tuning/micro_cells.jsonl): a 64-byte slot is four 16-byte
+// lane gathers, and each 16-byte gather per query costs as much as the whole LDS walk (the
+// tree's one bucket gather: ~200 us of its 700 at 2^27). The 4-key-group form of the compares
+// (DAUC_CELL_COUNT=1) was slower still. Kept, tested bit-exact, as the record of that result.
+// The builder also records whether the table is skewed (more than 1/64 of the keys beyond
+// their slot: clustered or tie-heavy keys) in a device word that both query kernels read.
+constexpr int kTopBits = 12;
+constexpr int kTop = 1 << kTopBits;
+constexpr int kLowBits = 32 - kTopBits;
+constexpr int kCellSlot = 16;                                 // keys per cell slot (64 B)
+constexpr int kMaxCells = 35840;                              // LDS: 4 * (4096 + 35842) B + reduce scratch <= 160 KB
+constexpr int kCellMuAuto = 6, kCellMuForced = 16;            // largest mean keys per cell tried
+constexpr int64_t kCellMaxM = int64_t(kMaxCells) * kCellMuAuto;
+constexpr int kCellPlanThreads = 1024;
+// meta words: [0] cells built (mu found), [1] number of cells, [2] keys beyond the slots, [3] mu
+constexpr int kMetaOk = 0, kMetaCells = 1, kMetaOverflow = 2, kMetaMu = 3;
+
+struct CellWs {
+    unsigned* meta;   // [64]
+    unsigned* l1;     // [kTop]
+    unsigned* base;   // [kMaxCells + 2]
+    uint4* slots;     // [(kMaxCells + 1) * 4]
+};
+
+constexpr size_t kCellBytes = 256 + size_t(kTop) * 4 + ((size_t(kMaxCells) + 2) * 4 + 255) / 256 * 256 +
+                              (size_t(kMaxCells) + 1) * kCellSlot * 4;
+
+// search structure set by dauc_set_search_mode (tests, measurements): 0, 1 = tree, 2 = cells
+int g_search_mode = 0;
+
+__device__ __forceinline__ unsigned cell_of(unsigned key, unsigned e) {
+    return (e & 0xffffu) + __umulhi(key << kTopBits, e >> 16);
+}
+
+__device__ __forceinline__ bool cells_in_use(const unsigned* __restrict__ meta, int64_t M, int force) {
+    return meta[kMetaOk] != 0u && (force || int64_t(meta[kMetaOverflow]) * 64 <= M);
+}
+
+// inclusive scan over the 1024 threads of a workgroup (wave shuffles, one barrier for the wave
+// totals); op is min or +, v the thread's value
+template <bool MIN>
+__device__ __forceinline__ unsigned block_incl_scan1024(unsigned v, unsigned* wtot) {
+    const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+    unsigned incl = v;
+#pragma unroll
+    for (int off = 1; off < kWave; off <<= 1) {
+        const unsigned t = __shfl_up(incl, off, kWave);
+        if (lane >= off) incl = MIN ? (t < incl ? t : incl) : incl + t;
+    }
+    if (lane == kWave - 1) wtot[wid] = incl;
     __syncthreads();
+    unsigned before = MIN ? ~0u : 0u;
+    for (int w = 0; w < wid; ++w) before = MIN ? (wtot[w] < before ? wtot[w] : before) : before + wtot[w];
+    __syncthreads();
+    return MIN ? (before < incl ? before : incl) : before + incl;
+}
+
+// One workgroup: per top bucket the first table index (every key compared with its
+// predecessor), the bucket sizes n_t (suffix minimum of the first indices), the smallest
+// mu in [4, mu_max] whose sum of ceil(n_t / mu) fits kMaxCells, and the cell offsets (prefix sum).
+// Thread i owns the buckets t = 4095 - 4i - j (j = 0..3): descending, so suffix minima over t
+// are prefix minima over the threads.
+__global__ __launch_bounds__(kCellPlanThreads) void cell_plan_kernel(const unsigned* __restrict__ sorted, int64_t M,
+                                                                     int mu_max, unsigned* __restrict__ l1,
+                                                                     unsigned* __restrict__ meta) {
+    static_assert(kTop == 4 * kCellPlanThreads, "four top buckets per thread");
+    __shared__ unsigned first[kTop];
+    __shared__ unsigned wtot[kCellPlanThreads / kWave];
+    const unsigned m32 = static_cast<unsigned>(M);
+    for (int t = threadIdx.x; t < kTop; t += kCellPlanThreads) first[t] = m32;
+    __syncthreads();
+    for (int64_t i = threadIdx.x; i < M; i += kCellPlanThreads) {
+        const unsigned t = sorted[i] >> kLowBits;
+        if (i == 0 || (sorted[i - 1] >> kLowBits) != t) first[t] = static_cast<unsigned>(i);
+    }
+    __syncthreads();
+    int tj[4];
+    unsigned st[4], run = ~0u;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        tj[j] = kTop - 1 - 4 * static_cast<int>(threadIdx.x) - j;
+        const unsigned f = first[tj[j]];
+        run = f < run ? f : run;
+        st[j] = run;  // min of first[] over this thread's buckets >= tj[j]
+    }
+    const unsigned incl = block_incl_scan1024<true>(run, wtot);
+    // start of the bucket above this thread's highest one: the previous threads' minimum (M past
+    // the top bucket); first[] is free again, so it carries the inclusive minima
+    first[threadIdx.x] = incl;
+    __syncthreads();
+    unsigned n[4];
+    {
+        const unsigned above = threadIdx.x == 0 ? m32 : first[threadIdx.x - 1];
+        unsigned hi = above < m32 ? above : m32;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const unsigned s0 = st[j] < hi ? st[j] : hi;  // start of bucket tj[j]
+            n[j] = hi - s0;
+            hi = s0;
+        }
+    }
+    unsigned mu = 0, total = 0;
+    __shared__ unsigned bsum[kCellPlanThreads / kWave];
+    for (unsigned m = 4; m <= static_cast<unsigned>(mu_max); ++m) {
+        unsigned c = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) c += (n[j] + m - 1) / m;
+        unsigned long long cw = wave_sum(static_cast<unsigned long long>(c));
+        if ((threadIdx.x & (kWave - 1)) == 0) bsum[threadIdx.x / kWave] = static_cast<unsigned>(cw);
+        __syncthreads();
+        unsigned tot = 0;
+        for (int w = 0; w < kCellPlanThreads / kWave; ++w) tot += bsum[w];
+        __syncthreads();
+        if (tot <= static_cast<unsigned>(kMaxCells)) {
+            mu = m;
+            total = tot;
+            break;
+        }
+    }
+    if (threadIdx.x == 0) {
+        meta[kMetaOk] = mu != 0u;
+        meta[kMetaCells] = total;
+        meta[kMetaOverflow] = 0u;
+        meta[kMetaMu] = mu;
+    }
+    if (mu == 0u) return;  // uniform: every thread saw the same totals
+    unsigned C[4], csum = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        C[j] = (n[j] + mu - 1) / mu;
+        csum += C[j];
+    }
+    // cells of the buckets >= tj[j] (descending prefix), so off_t = total - that
+    const unsigned incl_c = block_incl_scan1024<false>(csum, wtot);
+    unsigned upto = incl_c - csum;  // cells of the buckets above this thread's
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        upto += C[j];
+        l1[tj[j]] = (total - upto) | (C[j] << 16);
+    }
+}
+
+// One thread per table index i in [0, M] (i = M: a virtual key past every cell). Cells
+// (c(i-1), c(i)] start at i; the cells strictly between are empty (+inf slots); the first key
+// of each cell copies its cell's first 16 keys into the slot; keys of rank >= 16 in their
+// cell are counted as overflow.
+__global__ __launch_bounds__(256) void cell_fill_kernel(const unsigned* __restrict__ sorted, int64_t M,
+                                                        const unsigned* __restrict__ l1, unsigned* __restrict__ meta,
+                                                        unsigned* __restrict__ base, uint4* __restrict__ slots) {
+    if (meta[kMetaOk] == 0u) return;
+    const int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x;
+    unsigned ov = 0;
+    if (i <= M) {
+        const unsigned ncells = meta[kMetaCells];
+        auto cell = [&](int64_t j) -> unsigned {
+            const unsigned key = sorted[j];
+            return cell_of(key, l1[key >> kLowBits]);
+        };
+        const int64_t ci = i < M ? int64_t(cell(i)) : int64_t(ncells) + 1;
+        const int64_t cp = i > 0 ? int64_t(cell(i - 1)) : -1;
+        const uint4 pad4 = uint4{kPadKey, kPadKey, kPadKey, kPadKey};
+        for (int64_t c = cp + 1; c <= ci; ++c) {
+            base[c] = static_cast<unsigned>(i);
+            if (c < ci) {
+#pragma unroll
+                for (int m = 0; m < kCellSlot / 4; ++m) slots[c * (kCellSlot / 4) + m] = pad4;
+            }
+        }
+        if (i < M && ci != cp) {
+            unsigned kk[kCellSlot];
+#pragma unroll
+            for (int j = 0; j < kCellSlot; ++j) {
+                const int64_t idx = i + j;
+                unsigned v = kPadKey;
+                if (idx < M) {
+                    const unsigned key = sorted[idx];
+                    if (int64_t(cell_of(key, l1[key >> kLowBits])) == ci) v = key;
+                }
+                kk[j] = v;
+            }
+#pragma unroll
+            for (int m = 0; m < kCellSlot / 4; ++m)
+                slots[ci * (kCellSlot / 4) + m] = uint4{kk[4 * m], kk[4 * m + 1], kk[4 * m + 2], kk[4 * m + 3]};
+        }
+        if (i < M && i >= kCellSlot && int64_t(cell(i - kCellSlot)) == ci) ov = 1u;
+    }
+    const unsigned long long w = wave_sum(static_cast<unsigned long long>(ov));
+    if ((threadIdx.x & (kWave - 1)) == 0 && w) atomicAdd(meta + kMetaOverflow, static_cast<unsigned>(w));
+}
+
+// #(slot keys < x) and #(slot keys <= x) for Q queries, every load issued before any compare
+#ifndef DAUC_CELL_Q
+#define DAUC_CELL_Q 4
+#endif
+#ifndef DAUC_CELL_U
+#define DAUC_CELL_U 2
+#endif
+// 0: 16 compares per bound; 1: the slot's 4-key group holding the first key >= x (3 compares
+// with the group ends, a 4-way select), then 4 compares per bound
+#ifndef DAUC_CELL_COUNT
+#define DAUC_CELL_COUNT 0
+#endif
+constexpr int kCellQ = DAUC_CELL_Q;
+
+__device__ __forceinline__ void count16(const uint4 (&k)[4], unsigned x, unsigned& lt, unsigned& le) {
+    unsigned a = 0, b = 0;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        a += (k[m].x < x) + (k[m].y < x) + (k[m].z < x) + (k[m].w < x);
+        b += (k[m].x <= x) + (k[m].y <= x) + (k[m].z <= x) + (k[m].w <= x);
+    }
+    lt = a;
+    le = b;
+}
+
+// Exact unless a group's last key equals x and a later group starts with x too (exact = false:
+// the caller recounts the whole slot)
+__device__ __forceinline__ void count16_group(const uint4 (&k)[4], unsigned x, unsigned& lt, unsigned& le,
+                                              bool& exact) {
+    const unsigned g = (k[0].w < x) + (k[1].w < x) + (k[2].w < x);
+    const unsigned g2 = (k[0].w <= x) + (k[1].w <= x) + (k[2].w <= x);
+    const uint4 lo2 = (g & 1u) ? k[1] : k[0];
+    const uint4 hi2 = (g & 1u) ? k[3] : k[2];
+    const uint4 a = (g & 2u) ? hi2 : lo2;
+    lt = 4u * g + (a.x < x) + (a.y < x) + (a.z < x) + (a.w < x);
+    le = 4u * g + (a.x <= x) + (a.y <= x) + (a.z <= x) + (a.w <= x);
+    exact = g2 == g;
+}
+
+// Q queries (use[q] false: computed, not counted) against the cell index; W += M - ub,
+// T += ub - lb (table = positives), summed per group in 32 bits (Q * M < 2^32)
+template <int Q>
+__device__ __forceinline__ void cell_queries(const unsigned (&x)[Q], const bool (&use)[Q],
+                                             const unsigned* __restrict__ l1s, const unsigned* __restrict__ bases,
+                                             const uint4* __restrict__ slots, const unsigned* __restrict__ sorted,
+                                             unsigned M, unsigned long long& w, unsigned long long& t) {
+    unsigned c[Q], lo[Q], hi[Q], lbf[Q], ubf[Q];
+    bool redo[Q];
+    uint4 k[Q][4];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) c[q] = cell_of(x[q], l1s[x[q] >> kLowBits]);
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+        const uint4* sl = slots + size_t(c[q]) * (kCellSlot / 4);
+#pragma unroll
+        for (int m = 0; m < 4; ++m) k[q][m] = sl[m];
+    }
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+        lo[q] = bases[c[q]];
+        hi[q] = bases[c[q] + 1];
+    }
+    unsigned wl = 0u, tl = 0u;
+    bool slow = false;
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+        unsigned lt, le;
+        bool exact = true;
+        if (DAUC_CELL_COUNT == 1)
+            count16_group(k[q], x[q], lt, le, exact);
+        else
+            count16(k[q], x[q], lt, le);
+        lbf[q] = lo[q] + lt;
+        ubf[q] = lo[q] + le;
+        wl += use[q] ? M - ubf[q] : 0u;
+        tl += use[q] ? ubf[q] - lbf[q] : 0u;
+        // the cell continues past its slot and x reaches the slot's last key, or the group
+        // count was not exact: recount below
+        redo[q] = use[q] && ((hi[q] - lo[q] > static_cast<unsigned>(kCellSlot) && k[q][3].w <= x[q]) || !exact);
+        slow |= redo[q];
+    }
+    w += wl;
+    t += tl;
+    if (slow) {
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            if (!redo[q]) continue;
+            unsigned lt, le;
+            count16(k[q], x[q], lt, le);
+            int64_t lb = int64_t(lo[q]) + lt, ub = int64_t(lo[q]) + le;
+            if (hi[q] - lo[q] > static_cast<unsigned>(kCellSlot) && k[q][3].w <= x[q]) {
+                // the rest of the cell from the sorted table (ub always; lb unless the slot's last key is x)
+                const int64_t b0 = int64_t(lo[q]) + kCellSlot, b1 = hi[q];
+                ub = b0 + count_below<false>(sorted, b0, b1, x[q]);
+                if (k[q][3].w < x[q]) lb = b0 + count_below<true>(sorted, b0, b1, x[q]);
+            }
+            // replace the fast counts: W -= ub - ubf, T += (ub - lb) - (ubf - lbf)
+            w -= static_cast<unsigned long long>(ub - int64_t(ubf[q]));
+            t += static_cast<unsigned long long>((ub - lb) - (int64_t(ubf[q]) - int64_t(lbf[q])));
+        }
+    }
+}
+
+template <int Q>
+__device__ __forceinline__ void cell_count4(const unsigned (&x)[4], const bool (&use)[4], const unsigned* l1s,
+                                            const unsigned* bases, const uint4* slots, const unsigned* sorted,
+                                            unsigned M, unsigned long long& w, unsigned long long& t) {
+#pragma unroll
+    for (int b = 0; b < 4; b += Q) {
+        unsigned xs[Q];
+        bool us[Q];
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            xs[q] = x[b + q];
+            us[q] = use[b + q];
+        }
+        cell_queries<Q>(xs, us, l1s, bases, slots, sorted, M, w, t);
+    }
+}
+
+// The labeled query pass over the cell index: the same stream as query_labeled_kernel (every
+// label != +1 is a query against the sorted positives; queried scores checked for finiteness).
+// Returns at once when the builder kept the tree (meta), so it is enqueued unconditionally.
+template <typename LT>
+__global__ __launch_bounds__(kQueryThreads) void query_cells_kernel(const float* __restrict__ s,
+                                                                   const LT* __restrict__ lab, int64_t begin,
+                                                                   int64_t end, const unsigned* __restrict__ meta,
+                                                                   int force, const unsigned* __restrict__ l1g,
+                                                                   const unsigned* __restrict__ baseg,
+                                                                   const uint4* __restrict__ slots,
+                                                                   const unsigned* __restrict__ sorted, int64_t M,
+                                                                   unsigned long long* __restrict__ out,
+                                                                   unsigned long long* __restrict__ nonfinite) {
+    if (!cells_in_use(meta, M, force)) return;
+    extern __shared__ unsigned cells_lds[];
+    unsigned* l1s = cells_lds;
+    unsigned* bases = cells_lds + kTop;
+    {
+        const int nb = static_cast<int>(meta[kMetaCells]) + 2;
+        const uint4* l1v = reinterpret_cast<const uint4*>(l1g);
+        for (int i = threadIdx.x; i < kTop / 4; i += kQueryThreads) reinterpret_cast<uint4*>(l1s)[i] = l1v[i];
+        for (int i = threadIdx.x; i < nb; i += kQueryThreads) bases[i] = baseg[i];
+    }
+    __syncthreads();
+    const unsigned M32 = static_cast<unsigned>(M);
     unsigned long long w = 0, t = 0;
     unsigned nf = 0;
-    // scalar head up to a 4-element boundary, then float4 slots, then the scalar tail
     const int64_t a0 = (begin + 3) & ~int64_t(3);
     const int64_t head = a0 < end ? a0 : end;
     const int64_t stride = int64_t(gridDim.x) * kQueryThreads;
     const int64_t tid = int64_t(blockIdx.x) * kQueryThreads + threadIdx.x;
-    for (int64_t i = begin + tid; i < head; i += stride) {
+    auto one = [&](int64_t i) {
         if (lab[i] != LT(1)) {
             nf += !isfinite(s[i]);
-            count_query<K, true>(key_of(s[i]), tree, g, top, k, sorted, M, w, t);
+            const unsigned x[1] = {key_of(s[i])};
+            const bool u[1] = {true};
+            cell_queries<1>(x, u, l1s, bases, slots, sorted, M32, w, t);
         }
-    }
+    };
+    for (int64_t i = begin + tid; i < head; i += stride) one(i);
     const int64_t nvec = end > head ? (end - head) / 4 : 0;
     const bool aligned = (reinterpret_cast<uintptr_t>(s + head) & 15u) == 0 &&
                          (reinterpret_cast<uintptr_t>(lab + head) & (4 * sizeof(LT) - 1)) == 0;
     if (aligned) {
-        // U float4 slots (4 queries each) per iteration, and the NEXT iteration's loads issued
-        // before this one's walks: each walk is a chain of dependent LDS reads and a bucket load,
-        // so without this the stream's HBM latency sits between every two iterations of a wave.
-        constexpr int U = sizeof(LT) == 8 ? 2 : 4;
+        constexpr int U = DAUC_CELL_U;
         f32x4 fc[U], fn[U];
         LT lc[U][4], ln[U][4];
         auto load = [&](int64_t v0, f32x4 (&f)[U], LT (&l)[U][4]) {
@@ -831,13 +1288,140 @@ __global__ __launch_bounds__(kQueryThreads) void query_labeled_kernel(const floa
                     x[q] = key_of(f[q]);
                     nf += neg[q] && !isfinite(f[q]);
                 }
-                count4<K, true>(x, neg, tree, g, top, k, sorted, M, w, t);
+                cell_count4<kCellQ>(x, neg, l1s, bases, slots, sorted, M32, w, t);
             }
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 fc[u] = fn[u];
 #pragma unroll
                 for (int q = 0; q < 4; ++q) lc[u][q] = ln[u][q];
+            }
+        }
+    } else {
+        for (int64_t v = tid; v < nvec; v += stride)
+            for (int q = 0; q < 4; ++q) one(head + v * 4 + q);
+    }
+    for (int64_t i = head + nvec * 4 + tid; i < end; i += stride) one(i);
+    __shared__ unsigned long long red[3][kQueryThreads / kWave];
+    w = wave_sum(w);
+    t = wave_sum(t);
+    const unsigned long long nfw = wave_sum(static_cast<unsigned long long>(nf));
+    const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+    if (lane == 0) {
+        red[0][wid] = w;
+        red[1][wid] = t;
+        red[2][wid] = nfw;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long bw = 0, bt = 0, bn = 0;
+        for (int i = 0; i < kQueryThreads / kWave; ++i) {
+            bw += red[0][i];
+            bt += red[1][i];
+            bn += red[2][i];
+        }
+        if (bw) atomicAdd(out + 0, bw);
+        if (bt) atomicAdd(out + 1, bt);
+        if (bn && nonfinite) atomicAdd(nonfinite, bn);
+    }
+}
+
+// Every queried score is also checked to be finite (sklearn rejects NaN / inf scores,
+// _ranking.py:868-869): nonfinite (nullable) += #queried non-finite scores. The negatives are
+// never materialised, so this is the only pass that reads their scores. With a cell index
+// built (meta != nullptr) the kernel returns at once unless the builder kept the tree.
+template <int K, typename LT>
+__global__ __launch_bounds__(kQueryThreads) void query_labeled_kernel(const float* __restrict__ s,
+                                                                     const LT* __restrict__ lab, int64_t begin,
+                                                                     int64_t end, const TreeNode* __restrict__ gtree,
+                                                                     TreeGeom g, int k,
+                                                                     const unsigned* __restrict__ sorted,
+                                                                     int64_t M, unsigned long long* __restrict__ out,
+                                                                     unsigned long long* __restrict__ nonfinite,
+                                                                     const unsigned* __restrict__ meta, int force) {
+    if (meta != nullptr && cells_in_use(meta, M, force)) return;
+    extern __shared__ TreeNode tree[];
+    for (int i = threadIdx.x; i < g.nodes; i += kQueryThreads) tree[i] = gtree[i];
+    const TopKeys top = load_top(gtree, g, sorted, k);
+    __syncthreads();
+    unsigned long long w = 0, t = 0;
+    unsigned nf = 0;
+    // scalar head up to a 4-element boundary, then float4 slots, then the scalar tail
+    const int64_t a0 = (begin + 3) & ~int64_t(3);
+    const int64_t head = a0 < end ? a0 : end;
+    const int64_t stride = int64_t(gridDim.x) * kQueryThreads;
+    const int64_t tid = int64_t(blockIdx.x) * kQueryThreads + threadIdx.x;
+    for (int64_t i = begin + tid; i < head; i += stride) {
+        if (lab[i] != LT(1)) {
+            nf += !isfinite(s[i]);
+            count_query<K, true>(key_of(s[i]), tree, g, top, k, sorted, M, w, t);
+        }
+    }
+    const int64_t nvec = end > head ? (end - head) / 4 : 0;
+    const bool aligned = (reinterpret_cast<uintptr_t>(s + head) & 15u) == 0 &&
+                         (reinterpret_cast<uintptr_t>(lab + head) & (4 * sizeof(LT) - 1)) == 0;
+    if (aligned) {
+        // U float4 slots (4 queries each) per iteration, and the NEXT iteration's loads issued
+        // before this one's walks: each walk is a chain of dependent LDS reads and a bucket load,
+        // so without this the stream's HBM latency sits between every two iterations of a wave.
+        // slots per iteration (prefetched one iteration ahead): register-bound
+        constexpr int U = sizeof(LT) == 8 ? 2 : (pipelined<K>() ? (sizeof(LT) == 1 ? DAUC_QUERY_PIPE_U : 2) : 4);
+        f32x4 fc[U], fn[U];
+        LabelWords<LT> lc[U], ln[U];
+        auto load = [&](int64_t v0, f32x4 (&f)[U], LabelWords<LT> (&l)[U]) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int64_t v = v0 + int64_t(u) * stride;
+                if (v < nvec) {
+                    const int64_t i = head + v * 4;
+                    f[u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(s + i));
+                    l[u].load(lab + i);
+                } else {
+                    f[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+                    l[u].set_positive();  // past the end: no query
+                }
+            }
+        };
+        load(tid, fc, lc);
+        for (int64_t v0 = tid; v0 < nvec; v0 += int64_t(U) * stride) {
+            auto keys = [&](int u, unsigned (&x)[4], bool (&neg)[4]) {
+                const float f[4] = {fc[u].x, fc[u].y, fc[u].z, fc[u].w};
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    neg[q] = lc[u].not_positive(q);
+                    x[q] = key_of(f[q]);
+                    nf += neg[q] && !isfinite(f[q]);
+                }
+            };
+            if constexpr (pipelined<K>()) {
+                // every slot's walk and bucket load first, THEN the next iteration's stream loads,
+                // then the compares: vmcnt retires loads in issue order, so a wait for a bucket
+                // load issued after a streaming load would also wait out that load's HBM latency
+                bool neg[U][4];
+                unsigned x[U][4], su[U][4], bv[U][4][K > 0 ? K : 1];
+#pragma unroll
+                for (int u = 0; u < U; ++u) keys(u, x[u], neg[u]);
+#pragma unroll
+                for (int u = 0; u < U; ++u) walk_and_load<K>(x[u], su[u], bv[u], tree, g, top, sorted);
+                asm volatile("" ::: "memory");
+                load(v0 + int64_t(U) * stride, fn, ln);
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+                    finish_counts<K, true>(x[u], neg[u], su[u], bv[u], tree, g, top, sorted, M, w, t);
+            } else {
+                load(v0 + int64_t(U) * stride, fn, ln);
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    bool neg[4];
+                    unsigned x[4];
+                    keys(u, x, neg);
+                    count4<K, true>(x, neg, tree, g, top, k, sorted, M, w, t);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                fc[u] = fn[u];
+                lc[u] = ln[u];
             }
         }
     } else {
@@ -1000,15 +1584,47 @@ int radix_sort_keys(const float* neg, int64_t N, const SortWs& w, hipStream_t st
     return DAUC_OK;
 }
 
+CellWs carve_cells(void* p) {
+    char* c = static_cast<char*>(p);
+    CellWs w;
+    w.meta = reinterpret_cast<unsigned*>(c);
+    c += 256;
+    w.l1 = reinterpret_cast<unsigned*>(c);
+    c += size_t(kTop) * 4;
+    w.base = reinterpret_cast<unsigned*>(c);
+    c += ((size_t(kMaxCells) + 2) * 4 + 255) / 256 * 256;
+    w.slots = reinterpret_cast<uint4*>(c);
+    return w;
+}
+
+// plan + fill of the cell index behind the sort (2 launches; the verdict stays on the device)
+int prepare_cells(const unsigned* sorted, int64_t M, const CellWs& cw, int mu_max, hipStream_t st) {
+    hipLaunchKernelGGL(cell_plan_kernel, dim3(1), dim3(kCellPlanThreads), 0, st, sorted, M, mu_max, cw.l1, cw.meta);
+    hipLaunchKernelGGL(cell_fill_kernel, dim3(static_cast<unsigned>((M + 1 + 255) / 256)), dim3(256), 0, st, sorted, M,
+                       cw.l1, cw.meta, cw.base, cw.slots);
+    return launch_status();
+}
+
+template <typename LT>
+int launch_cells(const float* s, const LT* lab, int64_t begin, int64_t end, const CellWs& cw, int force,
+                 const unsigned* sorted, int64_t M, unsigned long long* out, unsigned long long* nonfinite,
+                 hipStream_t st) {
+    const dim3 grid(query_grid(end - begin)), block(kQueryThreads);
+    const size_t lds = (size_t(kTop) + kMaxCells + 2) * 4;
+    hipLaunchKernelGGL((query_cells_kernel<LT>), grid, block, lds, st, s, lab, begin, end, cw.meta, force, cw.l1,
+                       cw.base, cw.slots, sorted, M, out, nonfinite);
+    return launch_status();
+}
+
 template <typename LT>
 int launch_labeled(int k, const float* s, const LT* lab, int64_t begin, int64_t end, const TreeNode* tree,
                    const TreeGeom& g, const unsigned* sorted, int64_t M, unsigned long long* out, unsigned long long* nonfinite,
-                   hipStream_t st) {
+                   const unsigned* meta, int force, hipStream_t st) {
     const dim3 grid(query_grid(end - begin)), block(kQueryThreads);
     const size_t lds = size_t(g.nodes) * sizeof(TreeNode);
 #define DAUC_QL(KV)                                                                                              \
     hipLaunchKernelGGL((query_labeled_kernel<KV, LT>), grid, block, lds, st, s, lab, begin, end, tree, g, k, \
-                       sorted, M, out, nonfinite)
+                       sorted, M, out, nonfinite, meta, force)
     switch (k) {
         case 1: DAUC_QL(1); break;
         case 2: DAUC_QL(2); break;
@@ -1051,7 +1667,13 @@ using namespace dauc;
 
 extern "C" {
 
-size_t dauc_sort_workspace_size(int64_t n) { return sort_ws_bytes(n < 1 ? 1 : n) + kTreeBytes + 256; }
+size_t dauc_sort_workspace_size(int64_t n) { return sort_ws_bytes(n < 1 ? 1 : n) + kTreeBytes + 256 + kCellBytes + 256; }
+
+int dauc_set_search_mode(int mode) {
+    if (mode < 0 || mode > 2) return DAUC_EINVAL;
+    g_search_mode = mode;
+    return DAUC_OK;
+}
 
 int dauc_sort_keys(const float* scores, int64_t n, unsigned* keys_out, void* workspace,
                    size_t workspace_bytes, dauc_stream_t stream) {
@@ -1107,16 +1729,26 @@ int dauc_auc_counts_sorted_labeled(const float* pos, int64_t P, const float* sco
     TreeGeom g{};
     int rc = prepare_table(pos, P, workspace, st, &sorted, &tree, &k, &g);
     if (rc) return rc;
+    // the cell index for tables it can hold; the tree pass returns at once unless the cell
+    // builder kept the tree (skewed keys), and the cell pass returns at once if it did
+    const int mode = g_search_mode;
+    const int force = mode == 2;
+    const bool cells = mode == 2 && P <= int64_t(kMaxCells) * kCellMuForced;
+    CellWs cw{};
+    if (cells) {
+        cw = carve_cells(reinterpret_cast<char*>(tree) + ((kTreeBytes + 255) / 256) * 256);
+        if ((rc = prepare_cells(sorted, P, cw, force ? kCellMuForced : kCellMuAuto, st))) return rc;
+    }
+    const unsigned* meta = cells ? cw.meta : nullptr;
+    auto run = [&](auto* lab) {
+        int r = launch_labeled(k, scores, lab, begin, end, tree, g, sorted, P, wins_ties, nonfinite, meta, force, st);
+        if (r == DAUC_OK && cells) r = launch_cells(scores, lab, begin, end, cw, force, sorted, P, wins_ties, nonfinite, st);
+        return r;
+    };
     switch (label_dtype) {
-        case DAUC_LABEL_I8:
-            return launch_labeled(k, scores, static_cast<const int8_t*>(labels), begin, end, tree, g, sorted, P,
-                                  wins_ties, nonfinite, st);
-        case DAUC_LABEL_I32:
-            return launch_labeled(k, scores, static_cast<const int32_t*>(labels), begin, end, tree, g, sorted, P,
-                                  wins_ties, nonfinite, st);
-        default:
-            return launch_labeled(k, scores, static_cast<const int64_t*>(labels), begin, end, tree, g, sorted, P,
-                                  wins_ties, nonfinite, st);
+        case DAUC_LABEL_I8: return run(static_cast<const int8_t*>(labels));
+        case DAUC_LABEL_I32: return run(static_cast<const int32_t*>(labels));
+        default: return run(static_cast<const int64_t*>(labels));
     }
 }
 

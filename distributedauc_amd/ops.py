@@ -468,9 +468,16 @@ def sort_keys(scores: torch.Tensor) -> torch.Tensor:
     return out
 
 
+def set_search_mode(mode: int) -> None:
+    """Search structure of the sort method (dauc_set_search_mode): 0 / 1 the LDS search tree (the
+    default), 2 the radix cell index wherever it fits (a measured, slower alternative). Same
+    integers in every mode; for tests and measurements."""
+    check(_lib.load().dauc_set_search_mode(int(mode)), "dauc_set_search_mode")
+
+
 __all__ = [
     "GradSeg", "label_map_phat", "surrogate_fwdbwd", "class_sums", "alpha_from_sums", "pd_update",
     "pd_update_dense", "coda_finalize", "scale_div", "split_scores", "pair_count", "auc_counts_sorted",
     "surrogate_logits_fwdbwd", "class_sums_logits",
-    "sort_keys", "auc_counts_sorted_labeled", "compact_positives", "mode_code", "workspaces",
+    "sort_keys", "auc_counts_sorted_labeled", "compact_positives", "mode_code", "workspaces", "set_search_mode",
 ]

@@ -315,6 +315,17 @@ size_t dauc_auc_eval_workspace_size(int64_t n);
 int dauc_auc_eval_counts(const float* scores, const void* labels, int label_dtype, int64_t n, int64_t* out,
                          void* workspace, size_t workspace_bytes, dauc_stream_t stream);
 
+/*
+ * Search structure of dauc_auc_counts_sorted_labeled (and so of dauc_auc_eval_counts), for
+ * tests and measurements; process-wide, default 0. Same integers in every mode.
+ *   0, 1: the LDS search tree (the default, the faster);
+ *   2: a radix cell index wherever it fits (tables of up to 573,440 keys): the key's top 12 bits
+ *      pick a bucket, a multiply-high its cell of ~4 keys, one 64-byte slot load and 16 compares
+ *      finish. Measured slower than the tree on MI355X (four lane gathers per query instead of
+ *      one); kept as a tested alternative.
+ */
+int dauc_set_search_mode(int mode);
+
 /* The radix sort alone: keys_out[0..n) = ascending order-preserving keys of scores (testing). */
 int dauc_sort_keys(const float* scores, int64_t n, unsigned* keys_out, void* workspace,
                    size_t workspace_bytes, dauc_stream_t stream);

@@ -1,0 +1,188 @@
+"""The radix cell index of the sort method (auc_sort.hip, dauc_set_search_mode) vs the C oracle.
+
+The labeled query pass (dauc_auc_counts_sorted_labeled, and through it dauc_auc_eval_counts)
+locates every negative among the sorted positives either through the LDS search tree (the
+default) or through the cell index (top 12 key bits -> bucket, multiply-high -> cell of ~mu keys,
+a 16-key slot plus a binary search beyond it; mode 2, a measured alternative). Every case here
+runs in all three modes: 0 (default: the tree), 1 (tree), 2 (cells wherever they fit). Bar: the integers (W, T) bit-exact against oracle/auc_oracle.c (sklearn's
+_binary_clf_curve counts, main.py:79-81) on the same scores.
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import coracle
+
+pytestmark = pytest.mark.gpu
+
+MODES = (0, 1, 2)
+
+
+def T(a, dev):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+
+
+@pytest.fixture
+def ops(dev):
+    from distributedauc_amd import ops as o
+
+    yield o
+    o.set_search_mode(0)
+
+
+def _oracle_slice(s, y, begin, end):
+    """(W, T) of all positives against the slice's non-positives (labels != 1)."""
+    pos = s[y == 1]
+    neg = s[begin:end][y[begin:end] != 1]
+    yy = np.concatenate([np.ones(pos.size, np.int64), -np.ones(neg.size, np.int64)])
+    e = coracle.auc_counts(yy, np.concatenate([pos, neg]))
+    return e["wins"], e["ties"]
+
+
+def _check(ops, dev, s, y, begin=0, end=None, modes=MODES, what=""):
+    end = s.size if end is None else end
+    ref = _oracle_slice(s, y, begin, end)
+    ts, ty = T(s, dev), T(y, dev)
+    tpos = T(s[y == 1], dev)
+    for m in modes:
+        ops.set_search_mode(m)
+        wt = torch.zeros(3, dtype=torch.int64, device=dev)
+        ops.auc_counts_sorted_labeled(tpos, ts, ty, begin, end, wt, nonfinite=wt[2:])
+        got = tuple(wt[:2].cpu().tolist())
+        assert got == ref, (what, m, got, ref)
+        assert int(wt[2]) == 0, (what, m)
+
+
+def _labels(rng, n, p, dtype=np.int8):
+    return np.where(rng.random(n) < p, 1, -1).astype(dtype)
+
+
+def test_cells_uniform_scores(dev, ops):
+    """The bench's distribution (U(0,1) fp32, loader.synthetic_scores) at table sizes that need
+    mu = 4, 5 and 6 keys per cell (134k, 168k, 200k positives) and a few small tables."""
+    rng = np.random.default_rng(1)
+    for n, P in ((1 << 20, 1), (1 << 20, 2), (1 << 20, 17), (1 << 20, 4_000), (1 << 21, 134_447),
+                 (1 << 21, 168_478), (1 << 21, 200_000)):
+        s = rng.random(n, dtype=np.float32)
+        y = -np.ones(n, np.int8)
+        y[rng.choice(n, P, replace=False)] = 1
+        _check(ops, dev, s, y, what=(n, P))
+
+
+def test_cells_signed_wide_and_special_values(dev, ops):
+    """Normal scores of both signs over 60 binades, +-0, subnormals, the largest finite values:
+    keys spread over many top buckets, empty buckets between them, ties between -0 and +0."""
+    rng = np.random.default_rng(2)
+    n = 1 << 20
+    s = (rng.standard_normal(n) * np.exp2(rng.integers(-30, 30, n))).astype(np.float32)
+    special = np.array([0.0, -0.0, 1e-45, -1e-45, 1e-40, -1e-40, 3.4e38, -3.4e38, 1.0, -1.0], np.float32)
+    k = rng.random(n) < 0.02
+    s[k] = rng.choice(special, int(k.sum()))
+    y = _labels(rng, n, 0.03)
+    _check(ops, dev, s, y, what="wide")
+    # all positives at the two extremes of the key range (first and last top buckets)
+    s2 = rng.random(n, dtype=np.float32) - 0.5
+    y2 = _labels(rng, n, 0.0)
+    y2[:50] = 1
+    s2[:25] = -3.4e38
+    s2[25:50] = 3.4e38
+    _check(ops, dev, s2, y2, what="extremes")
+
+
+def test_cells_ties_and_overflowing_cells(dev, ops):
+    """Quantised scores: runs of equal keys longer than a 16-key slot (the cell pass searches
+    the rest of the cell in global memory), and a run of 20 equal keys in one cell with the
+    rest of the table uniform (the slow path for that cell only), ties across cell edges."""
+    rng = np.random.default_rng(3)
+    n = 1 << 20
+    for levels, p in ((3001, 0.01), (97, 0.05), (5, 0.2), (1, 0.01)):
+        s = (np.floor(rng.random(n) * levels) / levels).astype(np.float32)
+        y = _labels(rng, n, p)
+        _check(ops, dev, s, y, what=("levels", levels))
+    s = rng.random(n, dtype=np.float32)
+    y = _labels(rng, n, 0.02)
+    pos_idx = np.flatnonzero(y == 1)
+    s[pos_idx[:20]] = np.float32(0.625)        # one cell holds a 20-key run of 0.625
+    neg_idx = np.flatnonzero(y == -1)
+    s[neg_idx[:1000]] = np.float32(0.625)      # negatives tied with it
+    s[neg_idx[1000:2000]] = np.nextafter(np.float32(0.625), np.float32(1))
+    s[neg_idx[2000:3000]] = np.nextafter(np.float32(0.625), np.float32(0))
+    _check(ops, dev, s, y, what="run of 20")
+
+
+def test_cells_clustered_table(dev, ops):
+    """90 % of the positives inside a 1e-4-wide interval: the cells of their top bucket hold
+    hundreds of keys each (slot + binary search in the cell pass)."""
+    rng = np.random.default_rng(4)
+    n = 1 << 20
+    s = rng.random(n, dtype=np.float32)
+    y = _labels(rng, n, 0.01)
+    pos_idx = np.flatnonzero(y == 1)
+    c = pos_idx[: int(0.9 * pos_idx.size)]
+    s[c] = (0.7 + 1e-4 * rng.random(c.size)).astype(np.float32)
+    neg_idx = np.flatnonzero(y == -1)
+    s[neg_idx[:50_000]] = (0.7 + 1e-4 * rng.random(50_000)).astype(np.float32)
+    _check(ops, dev, s, y, what="cluster")
+
+
+@pytest.mark.parametrize("ldtype", [np.int8, np.int32, np.int64])
+def test_cells_label_types_and_ranges(dev, ops, ldtype):
+    """Unaligned [begin, end) slices (the sharded evaluation's index ranges), labels 0 (a
+    negative for pos_label=1), every label dtype."""
+    rng = np.random.default_rng(5)
+    n = 300_001
+    s = rng.random(n, dtype=np.float32)
+    y = _labels(rng, n, 0.02, ldtype)
+    y[rng.random(n) < 0.01] = 0
+    for begin, end in ((0, n), (3, n - 5), (1, 2), (n // 3, 2 * n // 3 + 1), (7, 7)):
+        _check(ops, dev, s, y, begin, end, what=(begin, end))
+
+
+def test_cells_table_size_limits(dev, ops):
+    """Tables needing 6 keys per cell (215,040) and more, up to the cell index's limit of
+    16 keys per cell (573,440) and one key past it (the tree runs in every mode)."""
+    rng = np.random.default_rng(6)
+    n = 1 << 22
+    for P in (215_040, 215_041, 400_000, 573_440, 573_441):
+        s = rng.random(n, dtype=np.float32)
+        y = -np.ones(n, np.int8)
+        y[rng.choice(n, P, replace=False)] = 1
+        _check(ops, dev, s, y, what=P)
+
+
+def test_cells_one_call_eval(dev, ops):
+    """dauc_auc_eval_counts in every mode, the speculative table size included (the same data
+    twice, then other data of the same length)."""
+    rng = np.random.default_rng(7)
+    n = 1 << 21
+    data = [(rng.random(n, dtype=np.float32), _labels(rng, n, p)) for p in (0.001, 0.01, 0.001)]
+    for m in MODES:
+        ops.set_search_mode(m)
+        for s, y in (data[0], data[0], data[1], data[2], data[2]):
+            W, Tt, P, N, bad, other = ops.auc_eval_counts(T(s, dev), T(y, dev))
+            e = coracle.auc_counts(y.astype(np.int64), s)
+            assert (W, Tt, P, N, bad) == (e["wins"], e["ties"], e["P"], e["N"], 0), m
+
+
+def test_cells_rejects_nonfinite_queries(dev, ops):
+    """A NaN / inf negative is counted by the cell pass too (sklearn _ranking.py:868-869)."""
+    rng = np.random.default_rng(8)
+    n = 100_003
+    for m in MODES:
+        ops.set_search_mode(m)
+        for bad in (np.nan, np.inf, -np.inf):
+            s = rng.random(n, dtype=np.float32)
+            y = _labels(rng, n, 0.01)
+            s[int(np.flatnonzero(y == -1)[5])] = bad
+            wt = torch.zeros(3, dtype=torch.int64, device=dev)
+            ops.auc_counts_sorted_labeled(T(s[y == 1], dev), T(s, dev), T(y, dev), 0, n, wt, nonfinite=wt[2:])
+            assert int(wt[2]) == 1, (m, bad)
+
+
+def test_search_mode_rejects_unknown(dev, ops):
+    from distributedauc_amd._lib import DaucError
+
+    with pytest.raises(DaucError):
+        ops.set_search_mode(3)
