@@ -383,7 +383,8 @@ def auc_record(auc, world, config_name):
         "sort_mode": sk["mode"],
         "pairs_per_sec": npairs / sk["t_eval"],
         "method": "sort (default evaluator: compact the positives reading labels only, radix-sort them, locate "
-                  "every negative through an LDS search tree, read in place; on one GPU one blocking C call that "
+                  "every negative, read in place, through the LDS count index (the LDS search tree for tables it "
+                  "does not fit or finds skewed); on one GPU one blocking C call that "
                   "sizes the sort by the previous call's P for this length and re-runs it if P differs, so a "
                   "repeated test set costs one readback)",
         "eval_ms": sk["t_eval"] * 1e3, "sort_count_ms": sk["t_count"] * 1e3,

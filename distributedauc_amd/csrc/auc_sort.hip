@@ -324,7 +324,8 @@ __device__ __forceinline__ void store_node(uint4* t, int64_t c, const unsigned (
 __device__ __forceinline__ void store_node(uint2* t, int64_t c, const unsigned (&k)[4]) { t[c] = uint2{k[0], k[1]}; }
 
 __global__ __launch_bounds__(256) void build_tree_kernel(unsigned* __restrict__ sorted, int64_t M, int64_t pad, int k,
-                                                         TreeGeom g, TreeNode* __restrict__ tree) {
+                                                         TreeGeom g, TreeNode* __restrict__ tree,
+                                                         unsigned* __restrict__ ci_first, int n_first) {
     const int64_t c = int64_t(blockIdx.x) * 256 + threadIdx.x;
     if (c < g.nodes) {
         int d = 0;
@@ -340,8 +341,10 @@ __global__ __launch_bounds__(256) void build_tree_kernel(unsigned* __restrict__ 
         }
         store_node(tree, c, key);
     }
-    // keys M .. S*k of the last bucket: +inf, so bucket compares need no bounds
-    if (c < pad) sorted[M + c] = kPadKey;
+    // keys M .. S*k of the last bucket (and at least 8 past M, for the count index's windows):
+    // +inf, so bucket compares need no bounds
+    if (c < pad || c < 8) sorted[M + c] = kPadKey;
+    if (c < n_first) ci_first[c] = static_cast<unsigned>(M);  // count index: "no key in this bucket"
 }
 
 // p <- A p + #(node keys <= x): the compares' carries feed the adds (DAUC_TREE_STEP 0), or
@@ -894,8 +897,7 @@ constexpr int kTop = 1 << kTopBits;
 constexpr int kLowBits = 32 - kTopBits;
 constexpr int kCellSlot = 16;                                 // keys per cell slot (64 B)
 constexpr int kMaxCells = 35840;                              // LDS: 4 * (4096 + 35842) B + reduce scratch <= 160 KB
-constexpr int kCellMuAuto = 6, kCellMuForced = 16;            // largest mean keys per cell tried
-constexpr int64_t kCellMaxM = int64_t(kMaxCells) * kCellMuAuto;
+constexpr int kCellMuForced = 16;                            // largest mean keys per cell tried
 constexpr int kCellPlanThreads = 1024;
 // meta words: [0] cells built (mu found), [1] number of cells, [2] keys beyond the slots, [3] mu
 constexpr int kMetaOk = 0, kMetaCells = 1, kMetaOverflow = 2, kMetaMu = 3;
@@ -1326,6 +1328,367 @@ __global__ __launch_bounds__(kQueryThreads) void query_cells_kernel(const float*
     }
 }
 
+// ---- count index (the default search where it fits: dauc_set_search_mode 0) -----------------
+//
+// The tree's cost per query is its one 16-byte bucket gather from L2 plus 7 dependent LDS reads
+// and ~140 VALU. The count index answers ~40 % of the queries with no gather at all and the rest
+// with one, from 2 LDS reads and ~60 VALU:
+//   * the key's top 11 bits pick a top bucket t (sign, exponent, 2 mantissa bits); its n_t table
+//     keys get C_t = ceil(n_t * R) cells that split its 2^21 low key values evenly
+//     (cell = off_t + mulhi(low21 << 11, C_t)), R = cells per table key (~1.1 for the 2^27 @
+//     0.1 % table, so ~40 % of the cells -- and of the queries -- are empty);
+//   * LDS holds {off_t, C_t} (2048 x 8 B) and, per block of 8 cells, {the table keys before the
+//     block, the 8 cells' key counts as nibbles} (8 B): 1 B per cell, 146,559 cells;
+//   * rank_lo = block base + the nibbles below the cell = #(table keys < the cell) and cnt = the
+//     cell's nibble: the aligned 16-byte window of the sorted table at rank_lo & ~3 (loaded only
+//     by the lanes with cnt > 0; a second one when the cell runs past it, a binary search past 8
+//     keys) gives lb and ub by counting its keys < x and <= x -- keys before the cell are < x,
+//     keys after it > x or the +inf padding; cnt = 0 gives lb = ub = rank_lo.
+// The builder keeps the tree (a device word both query kernels read) when the table needs more
+// than 1.5 keys per cell or a cell holds 15 or more keys (a nibble): clustered or tie-heavy
+// tables, for which the tree's cost does not depend on the key distribution.
+constexpr int kCiTopBits = 11;
+constexpr int kCiTop = 1 << kCiTopBits;
+constexpr int kCiLowBits = 32 - kCiTopBits;
+constexpr int kCiBlock = 8;                                    // cells per block word
+constexpr int kCiMaxBlocks = 18320;                            // LDS: 16 KB + 8 B per block + 384 B < 160 KB
+constexpr int kCiMaxCells = kCiMaxBlocks * kCiBlock - 1;       // + the virtual cell past the last
+constexpr int kCiPlanThreads = 1024;
+// meta words (after the cell-slot index's): [8] usable, [9] cells, [10] blocks, [11] skewed
+constexpr int kCiOk = 8, kCiCells = 9, kCiBlocks = 10, kCiSkew = 11;
+
+struct CountWs {
+    unsigned* meta;    // [16]
+    unsigned* first;   // [kCiTop]      first table index of every top bucket (M = none)
+    uint2* l1;         // [kCiTop]      {first cell, cells} of every top bucket
+    unsigned* cstart;  // [kCiMaxCells + 2] first table index of every cell
+    uint2* blk;        // [kCiMaxBlocks] {keys before the block, 8 nibble counts}
+};
+
+constexpr size_t kCountBytes = 256 + 3 * size_t(kCiTop) * 4 + ((size_t(kCiMaxCells) + 2) * 4 + 255) / 256 * 256 +
+                               size_t(kCiMaxBlocks) * 8 + 256;
+
+__device__ __forceinline__ unsigned ci_cell(unsigned key, uint2 e) { return e.x + __umulhi(key << kCiTopBits, e.y); }
+
+__device__ __forceinline__ bool count_index_in_use(const unsigned* __restrict__ meta) {
+    return meta[kCiOk] != 0u && meta[kCiSkew] == 0u;
+}
+
+// first[t] = the first table index of top bucket t, for the buckets holding keys (first[] was set
+// to M by build_tree_kernel)
+__global__ __launch_bounds__(256) void ci_first_kernel(const unsigned* __restrict__ sorted, int64_t M,
+                                                       unsigned* __restrict__ first) {
+    const int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x;
+    if (i >= M) return;
+    const unsigned t = sorted[i] >> kCiLowBits;
+    if (i == 0 || (sorted[i - 1] >> kCiLowBits) != t) first[t] = static_cast<unsigned>(i);
+}
+
+// One workgroup: n_t from the suffix minima of first[] (thread i owns the buckets 2047 - 2i and
+// 2046 - 2i: descending, so the suffix minima are prefix minima over the threads), the cells per
+// bucket C_t = ceil(n_t * num / M), num = min(cells left after one per used bucket, 2 M) (so
+// sum C_t fits), and the first cell of every bucket (prefix sum).
+__global__ __launch_bounds__(kCiPlanThreads) void ci_plan_kernel(int64_t M, const unsigned* __restrict__ first,
+                                                                 uint2* __restrict__ l1,
+                                                                 unsigned* __restrict__ meta) {
+    static_assert(kCiTop == 2 * kCiPlanThreads, "two top buckets per thread");
+    __shared__ unsigned wtot[kCiPlanThreads / kWave];
+    __shared__ unsigned incl_min[kCiPlanThreads];
+    __shared__ unsigned totals[2];
+    const unsigned m32 = static_cast<unsigned>(M);
+    int tj[2];
+    unsigned st[2], run = ~0u;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        tj[j] = kCiTop - 1 - 2 * static_cast<int>(threadIdx.x) - j;
+        const unsigned f = first[tj[j]];
+        run = f < run ? f : run;
+        st[j] = run;
+    }
+    const unsigned incl = block_incl_scan1024<true>(run, wtot);
+    incl_min[threadIdx.x] = incl;
+    __syncthreads();
+    unsigned n[2];
+    {
+        const unsigned above = threadIdx.x == 0 ? m32 : incl_min[threadIdx.x - 1];
+        unsigned hi = above < m32 ? above : m32;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const unsigned s0 = st[j] < hi ? st[j] : hi;
+            n[j] = hi - s0;
+            hi = s0;
+        }
+    }
+    const unsigned used = block_incl_scan1024<false>((n[0] != 0u) + (n[1] != 0u), wtot);
+    if (threadIdx.x == kCiPlanThreads - 1) totals[0] = used;
+    __syncthreads();
+    const int64_t avail = int64_t(kCiMaxCells) - int64_t(totals[0]);
+    const int64_t num = avail < 2 * M ? avail : 2 * M;
+    unsigned C[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) C[j] = n[j] ? static_cast<unsigned>((int64_t(n[j]) * num + M - 1) / M) : 0u;
+    const unsigned csum = C[0] + C[1];
+    const unsigned incl_c = block_incl_scan1024<false>(csum, wtot);
+    if (threadIdx.x == kCiPlanThreads - 1) totals[1] = incl_c;
+    __syncthreads();
+    const unsigned total = totals[1];
+    unsigned upto = incl_c - csum;  // cells of the buckets above this thread's
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        upto += C[j];
+        l1[tj[j]] = uint2{total - upto, C[j]};
+    }
+    if (threadIdx.x == 0) {
+        meta[kCiOk] = (3 * num >= 2 * M && total <= static_cast<unsigned>(kCiMaxCells)) ? 1u : 0u;  // <= 1.5 keys/cell
+        meta[kCiCells] = total;
+        meta[kCiBlocks] = (total + 1 + kCiBlock - 1) / kCiBlock;
+        meta[kCiSkew] = 0u;
+    }
+}
+
+// One thread per table index i in [0, M] (i = M: past the last cell): cells (c(i-1), c(i)] start at i
+__global__ __launch_bounds__(256) void ci_cells_kernel(const unsigned* __restrict__ sorted, int64_t M,
+                                                       const uint2* __restrict__ l1, const unsigned* __restrict__ meta,
+                                                       unsigned* __restrict__ cstart) {
+    if (meta[kCiOk] == 0u) return;
+    const int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x;
+    if (i > M) return;
+    auto cell = [&](int64_t j) -> int64_t {
+        const unsigned key = sorted[j];
+        return ci_cell(key, l1[key >> kCiLowBits]);
+    };
+    const int64_t ci = i < M ? cell(i) : int64_t(meta[kCiCells]) + 1;
+    const int64_t cp = i > 0 ? cell(i - 1) : -1;
+    for (int64_t c = cp + 1; c <= ci; ++c) cstart[c] = static_cast<unsigned>(i);
+}
+
+// One thread per block of 8 cells: the table keys before the block and the cells' counts as
+// nibbles; a count of 15 or more marks the table skewed (the tree is used)
+__global__ __launch_bounds__(256) void ci_blocks_kernel(const unsigned* __restrict__ cstart,
+                                                        unsigned* __restrict__ meta, uint2* __restrict__ blk) {
+    if (meta[kCiOk] == 0u) return;
+    const int b = blockIdx.x * 256 + threadIdx.x;
+    const int nb = static_cast<int>(meta[kCiBlocks]);
+    const int last = static_cast<int>(meta[kCiCells]) + 1;  // cstart[0 .. last] are written
+    bool skew = false;
+    if (b < nb) {
+        unsigned w = 0;
+        const int c0 = b * kCiBlock;
+        unsigned prev = cstart[c0 < last ? c0 : last];
+        const unsigned base = prev;
+#pragma unroll
+        for (int j = 0; j < kCiBlock; ++j) {
+            const int c = c0 + j + 1;
+            const unsigned nxt = cstart[c < last ? c : last];
+            const unsigned cnt = nxt - prev;
+            skew |= cnt >= 15u;
+            w |= (cnt < 15u ? cnt : 15u) << (4 * j);
+            prev = nxt;
+        }
+        blk[b] = uint2{base, w};
+    }
+    if (__ballot(skew) != 0ull && (threadIdx.x & (kWave - 1)) == 0) atomicOr(meta + kCiSkew, 1u);
+}
+
+// the order-preserving key (-0 -> +0 by adding +0)
+__device__ __forceinline__ unsigned key_fast(float f) {
+    const unsigned u = __float_as_uint(f + 0.0f);
+    return u ^ (static_cast<unsigned>(static_cast<int>(u) >> 31) | 0x80000000u);
+}
+
+// Phase 1 of one query: cell, rank_lo, count and (lanes with cnt > 0) the window load
+#ifndef DAUC_CI_ABLATE
+#define DAUC_CI_ABLATE 0  // timing ablations only (wrong counts): 1 no window load, 2 no LDS, 3 neither
+#endif
+__device__ __forceinline__ void ci_locate(unsigned x, const uint2* __restrict__ l1, const uint2* __restrict__ blk,
+                                          const unsigned* __restrict__ sorted, unsigned& rl, unsigned& cnt,
+                                          uint4& k) {
+    if (DAUC_CI_ABLATE >= 2) {
+        rl = (x * 2654435761u) % 100000u;
+        cnt = (x >> 7) & 1u;
+        k = uint4{kPadKey, kPadKey, kPadKey, kPadKey};
+        if (DAUC_CI_ABLATE == 2 && cnt) k = *reinterpret_cast<const uint4*>(sorted + (rl & ~3u));
+        return;
+    }
+    const unsigned c = ci_cell(x, l1[x >> kCiLowBits]);
+    const uint2 b = blk[c / kCiBlock];
+    const unsigned sh = 4u * (c % kCiBlock);
+    const unsigned below = __builtin_amdgcn_ubfe(b.y, 0u, sh);           // nibbles of the cells before
+    const unsigned bytes = (below & 0x0f0f0f0fu) + ((below >> 4) & 0x0f0f0f0fu);
+    rl = b.x + __builtin_amdgcn_sad_u8(bytes, 0u, 0u);
+    cnt = __builtin_amdgcn_ubfe(b.y, sh, 4u);
+    k = uint4{kPadKey, kPadKey, kPadKey, kPadKey};
+    if (DAUC_CI_ABLATE == 0 && cnt) k = *reinterpret_cast<const uint4*>(sorted + (rl & ~3u));
+}
+
+// Phase 2: lb, ub from the window (W += M - ub, T += ub - lb for use); returns whether the cell
+// runs past the window (then ci_fix recounts it)
+__device__ __forceinline__ bool ci_count(unsigned x, bool use, unsigned rl, unsigned cnt, const uint4& k, unsigned M,
+                                         unsigned& wl, unsigned& tl) {
+    const unsigned base = cnt ? (rl & ~3u) : rl;
+    const unsigned lt = (k.x < x) + (k.y < x) + (k.z < x) + (k.w < x);
+    const unsigned le = (k.x <= x) + (k.y <= x) + (k.z <= x) + (k.w <= x);
+    wl += use ? M - (base + le) : 0u;
+    tl += use ? le - lt : 0u;
+    return use && (rl & 3u) + cnt > 4u;
+}
+
+// a cell past its window: the next 4 keys (or a binary search past 8); corrects W and T
+__device__ __forceinline__ void ci_fix(unsigned x, unsigned rl, unsigned cnt, const uint4& k,
+                                       const unsigned* __restrict__ sorted, unsigned long long& w,
+                                       unsigned long long& t) {
+    const unsigned a = rl & ~3u;
+    const unsigned lt0 = (k.x < x) + (k.y < x) + (k.z < x) + (k.w < x);
+    const unsigned le0 = (k.x <= x) + (k.y <= x) + (k.z <= x) + (k.w <= x);
+    int64_t lb, ub;
+    if ((rl & 3u) + cnt <= 8u) {
+        const uint4 k2 = *reinterpret_cast<const uint4*>(sorted + a + 4);
+        lb = int64_t(a) + lt0 + (k2.x < x) + (k2.y < x) + (k2.z < x) + (k2.w < x);
+        ub = int64_t(a) + le0 + (k2.x <= x) + (k2.y <= x) + (k2.z <= x) + (k2.w <= x);
+    } else {
+        const int64_t b0 = rl, b1 = int64_t(rl) + cnt;
+        lb = b0 + count_below<true>(sorted, b0, b1, x);
+        ub = b0 + count_below<false>(sorted, b0, b1, x);
+    }
+    const int64_t lbf = int64_t(a) + lt0, ubf = int64_t(a) + le0;
+    w -= static_cast<unsigned long long>(ub - ubf);
+    t += static_cast<unsigned long long>((ub - lb) - (ubf - lbf));
+}
+
+#ifndef DAUC_CI_U
+#define DAUC_CI_U 2
+#endif
+
+// The labeled query pass over the count index (same stream and checks as query_labeled_kernel);
+// returns at once when the builder kept the tree, so it is enqueued unconditionally. Per
+// iteration every slot's window loads are issued BEFORE the next iteration's stream loads:
+// vmcnt retires loads in issue order, so a wait for a window would otherwise also wait out a
+// streaming load's HBM latency.
+template <typename LT>
+__global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __restrict__ s,
+                                                                const LT* __restrict__ lab, int64_t begin,
+                                                                int64_t end, const unsigned* __restrict__ meta,
+                                                                const uint2* __restrict__ l1g,
+                                                                const uint2* __restrict__ blkg,
+                                                                const unsigned* __restrict__ sorted, int64_t M,
+                                                                unsigned long long* __restrict__ out,
+                                                                unsigned long long* __restrict__ nonfinite) {
+    if (!count_index_in_use(meta)) return;
+    extern __shared__ uint2 ci_lds[];
+    const int nb = static_cast<int>(meta[kCiBlocks]);
+    uint2* l1 = ci_lds;          // [2048]
+    uint2* blk = ci_lds + kCiTop;  // [nb]
+    for (int i = threadIdx.x; i < kCiTop; i += kQueryThreads) l1[i] = l1g[i];
+    for (int i = threadIdx.x; i < nb; i += kQueryThreads) blk[i] = blkg[i];
+    __syncthreads();
+    const unsigned M32 = static_cast<unsigned>(M);
+    unsigned long long w = 0, t = 0;
+    unsigned nf = 0;
+    const int64_t a0 = (begin + 3) & ~int64_t(3);
+    const int64_t head = a0 < end ? a0 : end;
+    const int64_t stride = int64_t(gridDim.x) * kQueryThreads;
+    const int64_t tid = int64_t(blockIdx.x) * kQueryThreads + threadIdx.x;
+    auto one = [&](int64_t i) {
+        if (lab[i] != LT(1)) {
+            nf += !isfinite(s[i]);
+            const unsigned x = key_fast(s[i]);
+            unsigned rl, cnt, wl = 0u, tl = 0u;
+            uint4 k;
+            ci_locate(x, l1, blk, sorted, rl, cnt, k);
+            const bool more = ci_count(x, true, rl, cnt, k, M32, wl, tl);
+            w += wl;
+            t += tl;
+            if (more) ci_fix(x, rl, cnt, k, sorted, w, t);
+        }
+    };
+    for (int64_t i = begin + tid; i < head; i += stride) one(i);
+    const int64_t nvec = end > head ? (end - head) / 4 : 0;
+    const bool aligned = (reinterpret_cast<uintptr_t>(s + head) & 15u) == 0 &&
+                         (reinterpret_cast<uintptr_t>(lab + head) & (4 * sizeof(LT) - 1)) == 0;
+    if (aligned) {
+        constexpr int U = sizeof(LT) == 1 ? DAUC_CI_U : 1;
+        constexpr int NQ = 4 * U;
+        f32x4 fc[U], fn[U];
+        LabelWords<LT> lc[U], ln[U];
+        auto load = [&](int64_t v0, f32x4 (&f)[U], LabelWords<LT> (&l)[U]) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int64_t v = v0 + int64_t(u) * stride;
+                if (v < nvec) {
+                    const int64_t i = head + v * 4;
+                    f[u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(s + i));
+                    l[u].load(lab + i);
+                } else {
+                    f[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+                    l[u].set_positive();
+                }
+            }
+        };
+        load(tid, fc, lc);
+        for (int64_t v0 = tid; v0 < nvec; v0 += int64_t(U) * stride) {
+            unsigned x[NQ], rl[NQ], cnt[NQ];
+            bool use[NQ];
+            uint4 k[NQ];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const float f[4] = {fc[u].x, fc[u].y, fc[u].z, fc[u].w};
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    use[4 * u + q] = lc[u].not_positive(q);
+                    x[4 * u + q] = key_fast(f[q]);
+                    nf += use[4 * u + q] && !isfinite(f[q]);
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) ci_locate(x[q], l1, blk, sorted, rl[q], cnt[q], k[q]);
+            asm volatile("" ::: "memory");
+            load(v0 + int64_t(U) * stride, fn, ln);
+            unsigned wl = 0u, tl = 0u;
+            bool more = false;
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) more |= ci_count(x[q], use[q], rl[q], cnt[q], k[q], M32, wl, tl);
+            w += wl;
+            t += tl;
+            if (more) {
+#pragma unroll
+                for (int q = 0; q < NQ; ++q)
+                    if (use[q] && (rl[q] & 3u) + cnt[q] > 4u) ci_fix(x[q], rl[q], cnt[q], k[q], sorted, w, t);
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                fc[u] = fn[u];
+                lc[u] = ln[u];
+            }
+        }
+    } else {
+        for (int64_t v = tid; v < nvec; v += stride)
+            for (int q = 0; q < 4; ++q) one(head + v * 4 + q);
+    }
+    for (int64_t i = head + nvec * 4 + tid; i < end; i += stride) one(i);
+    __shared__ unsigned long long red[3][kQueryThreads / kWave];
+    w = wave_sum(w);
+    t = wave_sum(t);
+    const unsigned long long nfw = wave_sum(static_cast<unsigned long long>(nf));
+    const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+    if (lane == 0) {
+        red[0][wid] = w;
+        red[1][wid] = t;
+        red[2][wid] = nfw;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long bw = 0, bt = 0, bn = 0;
+        for (int i = 0; i < kQueryThreads / kWave; ++i) {
+            bw += red[0][i];
+            bt += red[1][i];
+            bn += red[2][i];
+        }
+        if (bw) atomicAdd(out + 0, bw);
+        if (bt) atomicAdd(out + 1, bt);
+        if (bn && nonfinite) atomicAdd(nonfinite, bn);
+    }
+}
+
 // Every queried score is also checked to be finite (sklearn rejects NaN / inf scores,
 // _ranking.py:868-869): nonfinite (nullable) += #queried non-finite scores. The negatives are
 // never materialised, so this is the only pass that reads their scores. With a cell index
@@ -1339,7 +1702,8 @@ __global__ __launch_bounds__(kQueryThreads) void query_labeled_kernel(const floa
                                                                      int64_t M, unsigned long long* __restrict__ out,
                                                                      unsigned long long* __restrict__ nonfinite,
                                                                      const unsigned* __restrict__ meta, int force) {
-    if (meta != nullptr && cells_in_use(meta, M, force)) return;
+    // meta: the slot-cell index's (force = 1) or the count index's (force = 0) builder verdict
+    if (meta != nullptr && (force ? cells_in_use(meta, M, 1) : count_index_in_use(meta))) return;
     extern __shared__ TreeNode tree[];
     for (int i = threadIdx.x; i < g.nodes; i += kQueryThreads) tree[i] = gtree[i];
     const TopKeys top = load_top(gtree, g, sorted, k);
@@ -1616,6 +1980,44 @@ int launch_cells(const float* s, const LT* lab, int64_t begin, int64_t end, cons
     return launch_status();
 }
 
+CountWs carve_count(void* p) {
+    char* c = static_cast<char*>(p);
+    CountWs w;
+    w.meta = reinterpret_cast<unsigned*>(c);
+    c += 256;
+    w.first = reinterpret_cast<unsigned*>(c);
+    c += size_t(kCiTop) * 4;
+    w.l1 = reinterpret_cast<uint2*>(c);
+    c += size_t(kCiTop) * 8;
+    w.cstart = reinterpret_cast<unsigned*>(c);
+    c += ((size_t(kCiMaxCells) + 2) * 4 + 255) / 256 * 256;
+    w.blk = reinterpret_cast<uint2*>(c);
+    return w;
+}
+
+// the count index behind the sort and the tree (first[] was reset by build_tree_kernel): 4 small
+// launches; the verdict (usable, skewed) stays on the device
+int prepare_count(const unsigned* sorted, int64_t M, const CountWs& cw, hipStream_t st) {
+    hipLaunchKernelGGL(ci_first_kernel, dim3(static_cast<unsigned>((M + 255) / 256)), dim3(256), 0, st, sorted, M,
+                       cw.first);
+    hipLaunchKernelGGL(ci_plan_kernel, dim3(1), dim3(kCiPlanThreads), 0, st, M, cw.first, cw.l1, cw.meta);
+    hipLaunchKernelGGL(ci_cells_kernel, dim3(static_cast<unsigned>((M + 1 + 255) / 256)), dim3(256), 0, st, sorted, M,
+                       cw.l1, cw.meta, cw.cstart);
+    hipLaunchKernelGGL(ci_blocks_kernel, dim3((kCiMaxBlocks + 255) / 256), dim3(256), 0, st, cw.cstart, cw.meta,
+                       cw.blk);
+    return launch_status();
+}
+
+template <typename LT>
+int launch_ci(const float* s, const LT* lab, int64_t begin, int64_t end, const CountWs& cw, const unsigned* sorted,
+              int64_t M, unsigned long long* out, unsigned long long* nonfinite, hipStream_t st) {
+    const dim3 grid(query_grid(end - begin)), block(kQueryThreads);
+    const size_t lds = (size_t(kCiTop) + kCiMaxBlocks) * 8;
+    hipLaunchKernelGGL((query_ci_kernel<LT>), grid, block, lds, st, s, lab, begin, end, cw.meta, cw.l1, cw.blk, sorted,
+                       M, out, nonfinite);
+    return launch_status();
+}
+
 template <typename LT>
 int launch_labeled(int k, const float* s, const LT* lab, int64_t begin, int64_t end, const TreeNode* tree,
                    const TreeGeom& g, const unsigned* sorted, int64_t M, unsigned long long* out, unsigned long long* nonfinite,
@@ -1640,7 +2042,7 @@ int launch_labeled(int k, const float* s, const LT* lab, int64_t begin, int64_t 
 
 // sort the table, build the tree; returns the tree pointer and geometry
 int prepare_table(const float* table, int64_t M, void* workspace, hipStream_t st, const unsigned** sorted,
-                  TreeNode** tree, int* k_out, TreeGeom* g_out) {
+                  TreeNode** tree, int* k_out, TreeGeom* g_out, unsigned* ci_first = nullptr) {
     SortWs w = carve(workspace, M);
     int rc = radix_sort_keys(table, M, w, st, sorted);
     if (rc) return rc;
@@ -1652,9 +2054,12 @@ int prepare_table(const float* table, int64_t M, void* workspace, hipStream_t st
     // buckets of <= 32 keys are read whole (one vector load), so their tail is padded; larger
     // ones are binary-searched with bounds (k - 1 < 64 keys of slack in the sort workspace)
     const int64_t pad = k <= 32 ? int64_t(S) * k - M : 0;
-    const int64_t nthreads = (g.nodes > pad) ? g.nodes : pad;
+    const int n_first = ci_first ? kCiTop : 0;
+    int64_t nthreads = (g.nodes > pad) ? g.nodes : pad;
+    if (nthreads < 8) nthreads = 8;
+    if (nthreads < n_first) nthreads = n_first;
     hipLaunchKernelGGL(build_tree_kernel, dim3(static_cast<unsigned>((nthreads + 255) / 256)), dim3(256), 0, st,
-                       const_cast<unsigned*>(*sorted), M, pad, k, g, *tree);
+                       const_cast<unsigned*>(*sorted), M, pad, k, g, *tree, ci_first, n_first);
     *k_out = k;
     *g_out = g;
     return launch_status();
@@ -1667,7 +2072,9 @@ using namespace dauc;
 
 extern "C" {
 
-size_t dauc_sort_workspace_size(int64_t n) { return sort_ws_bytes(n < 1 ? 1 : n) + kTreeBytes + 256 + kCellBytes + 256; }
+size_t dauc_sort_workspace_size(int64_t n) {
+    return sort_ws_bytes(n < 1 ? 1 : n) + kTreeBytes + 256 + kCellBytes + 256 + kCountBytes + 256;
+}
 
 int dauc_set_search_mode(int mode) {
     if (mode < 0 || mode > 2) return DAUC_EINVAL;
@@ -1727,22 +2134,26 @@ int dauc_auc_counts_sorted_labeled(const float* pos, int64_t P, const float* sco
     TreeNode* tree = nullptr;
     int k = 1;
     TreeGeom g{};
-    int rc = prepare_table(pos, P, workspace, st, &sorted, &tree, &k, &g);
-    if (rc) return rc;
-    // the cell index for tables it can hold; the tree pass returns at once unless the cell
-    // builder kept the tree (skewed keys), and the cell pass returns at once if it did
+    // the search structure: mode 0 the count index where the table can use it (the device keeps
+    // the tree for skewed tables), 1 the tree, 2 the slot-cell index (a measured alternative)
     const int mode = g_search_mode;
-    const int force = mode == 2;
-    const bool cells = mode == 2 && P <= int64_t(kMaxCells) * kCellMuForced;
-    CellWs cw{};
-    if (cells) {
-        cw = carve_cells(reinterpret_cast<char*>(tree) + ((kTreeBytes + 255) / 256) * 256);
-        if ((rc = prepare_cells(sorted, P, cw, force ? kCellMuForced : kCellMuAuto, st))) return rc;
-    }
-    const unsigned* meta = cells ? cw.meta : nullptr;
+    const bool slot_cells = mode == 2 && P <= int64_t(kMaxCells) * kCellMuForced;
+    const bool count = mode == 0 && 2 * P <= 3 * int64_t(kCiMaxCells);
+    char* after_tree = static_cast<char*>(workspace) + ((sort_ws_bytes(P) + 255) / 256) * 256 +
+                       ((kTreeBytes + 255) / 256) * 256;
+    const CellWs cw = carve_cells(after_tree);
+    const CountWs nw = carve_count(after_tree + ((kCellBytes + 255) / 256) * 256);
+    int rc = prepare_table(pos, P, workspace, st, &sorted, &tree, &k, &g, count ? nw.first : nullptr);
+    if (rc) return rc;
+    if (slot_cells && (rc = prepare_cells(sorted, P, cw, kCellMuForced, st))) return rc;
+    if (count && (rc = prepare_count(sorted, P, nw, st))) return rc;
+    const unsigned* meta = slot_cells ? cw.meta : (count ? nw.meta : nullptr);
     auto run = [&](auto* lab) {
-        int r = launch_labeled(k, scores, lab, begin, end, tree, g, sorted, P, wins_ties, nonfinite, meta, force, st);
-        if (r == DAUC_OK && cells) r = launch_cells(scores, lab, begin, end, cw, force, sorted, P, wins_ties, nonfinite, st);
+        int r = launch_labeled(k, scores, lab, begin, end, tree, g, sorted, P, wins_ties, nonfinite, meta,
+                               slot_cells ? 1 : 0, st);
+        if (r == DAUC_OK && slot_cells)
+            r = launch_cells(scores, lab, begin, end, cw, 1, sorted, P, wins_ties, nonfinite, st);
+        if (r == DAUC_OK && count) r = launch_ci(scores, lab, begin, end, nw, sorted, P, wins_ties, nonfinite, st);
         return r;
     };
     switch (label_dtype) {

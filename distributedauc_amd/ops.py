@@ -469,9 +469,10 @@ def sort_keys(scores: torch.Tensor) -> torch.Tensor:
 
 
 def set_search_mode(mode: int) -> None:
-    """Search structure of the sort method (dauc_set_search_mode): 0 / 1 the LDS search tree (the
-    default), 2 the radix cell index wherever it fits (a measured, slower alternative). Same
-    integers in every mode; for tests and measurements."""
+    """Search structure of the sort method (dauc_set_search_mode): 0 automatic (the count index
+    where the table fits it and is not skewed, else the LDS search tree), 1 the tree, 2 the
+    16-key-slot cell index (a measured, slower alternative). Same integers in every mode; for
+    tests and measurements."""
     check(_lib.load().dauc_set_search_mode(int(mode)), "dauc_set_search_mode")
 
 

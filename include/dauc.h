@@ -318,11 +318,14 @@ int dauc_auc_eval_counts(const float* scores, const void* labels, int label_dtyp
 /*
  * Search structure of dauc_auc_counts_sorted_labeled (and so of dauc_auc_eval_counts), for
  * tests and measurements; process-wide, default 0. Same integers in every mode.
- *   0, 1: the LDS search tree (the default, the faster);
- *   2: a radix cell index wherever it fits (tables of up to 573,440 keys): the key's top 12 bits
- *      pick a bucket, a multiply-high its cell of ~4 keys, one 64-byte slot load and 16 compares
- *      finish. Measured slower than the tree on MI355X (four lane gathers per query instead of
- *      one); kept as a tested alternative.
+ *   0: automatic -- the count index for tables of up to 219,838 keys (the key's top 11 bits pick
+ *      a bucket, a multiply-high its cell; an LDS word per 8 cells holds the keys before them and
+ *      the cells' counts, so a query in an empty cell needs no table read and the others one
+ *      16-byte window), unless the device finds the table skewed (a cell of 15+ keys, or more
+ *      than 1.5 keys per cell): then, and for larger tables, the LDS search tree;
+ *   1: the LDS search tree always;
+ *   2: a 16-key-slot cell index wherever it fits (tables of up to 573,440 keys), a measured
+ *      alternative (four lane gathers per query: slower than the tree), kept tested.
  */
 int dauc_set_search_mode(int mode);
 

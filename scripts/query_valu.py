@@ -1,11 +1,13 @@
-"""VALU-issue roofline of the labeled query kernel from committed rocprofv3 data.
+"""VALU-issue roofline of the labeled query pass from committed rocprofv3 data.
 
-Inputs (profiles/r02/pmc_query/): SQ_INSTS_VALU / SQ_INSTS_LDS per dispatch (one --pmc pass,
-scripts/gpu_pmc_query_valu.sh) and the kernel's average duration from a separate
---kernel-trace --stats pass over the same command; LDS bank-conflict and wait counters
-(scripts/gpu_pmc_query_lds.sh). Peak: 256 CUs x 4 SIMD-32 x 2.4 GHz / 2 cycles per wave64 VALU
-instruction = 1.2288e12 wave-instructions/s (MI355X_MICROARCH.md, execution model).
-Writes profiles/query_valu.json, which bench.py attaches to the AUC records."""
+Inputs (profiles/r02/pmc_count_index/, or the directory given as argv[1]): SQ_INSTS_VALU /
+SQ_INSTS_LDS per dispatch (one --pmc pass, scripts/gpu_pmc_ci.sh) and the kernel's average
+duration from a separate --kernel-trace --stats pass over the same command; LDS bank-conflict,
+wait and in-flight counters. The query pass is the count-index kernel (query_ci_kernel) where the
+table fits it, else the tree kernel (query_labeled_kernel); every dispatch of either is counted.
+Peak: 256 CUs x 4 SIMD-32 x 2.4 GHz / 2 cycles per wave64 VALU instruction = 1.2288e12
+wave-instructions/s (MI355X_MICROARCH.md, execution model). Writes profiles/query_valu.json,
+which bench.py attaches to the AUC records."""
 from __future__ import annotations
 
 import collections
@@ -15,24 +17,34 @@ import sys
 from pathlib import Path
 
 REPO = Path(__file__).resolve().parents[1]
-SRC = REPO / "profiles" / "r02" / "pmc_query"
+SRC = Path(sys.argv[1]) if len(sys.argv) > 1 else REPO / "profiles" / "r02" / "pmc_count_index"
+QUERY_KERNELS = ("query_ci_kernel", "query_labeled_kernel")
 PEAK = 256 * 4 * 2.4e9 / 2
 
 
 def counters(f):
+    """Per-dispatch counter sums of the query kernel that did the work (the other one of the pair
+    returns at once), averaged over its dispatches."""
     agg = collections.defaultdict(lambda: collections.defaultdict(float))
     for r in csv.DictReader(open(f)):
-        if "query_labeled" in r["Kernel_Name"]:
-            agg[r["Dispatch_Id"]][r["Counter_Name"]] += float(r["Counter_Value"])
-    vals = list(agg.values())
+        if any(k in r["Kernel_Name"] for k in QUERY_KERNELS):
+            agg[(r["Kernel_Name"].split("(")[0], r["Dispatch_Id"])][r["Counter_Name"]] += float(r["Counter_Value"])
+    by_kernel = collections.defaultdict(list)
+    for (name, _), v in agg.items():
+        by_kernel[name].append(v)
+    vals = max(by_kernel.values(), key=lambda vs: sum(sum(v.values()) for v in vs) / len(vs))
     return {k: sum(v[k] for v in vals) / len(vals) for k in vals[0]}
 
 
 def avg_us(f):
+    best = None
     for r in csv.DictReader(open(f)):
-        if "query_labeled" in r["Name"]:
-            return float(r["AverageNs"]) / 1e3
-    raise SystemExit(f"no query kernel in {f}")
+        if any(k in r["Name"] for k in QUERY_KERNELS):
+            us = float(r["AverageNs"]) / 1e3
+            best = us if best is None or us > best else best
+    if best is None:
+        raise SystemExit(f"no query kernel in {f}")
+    return best
 
 
 def main():
@@ -49,6 +61,10 @@ def main():
             cyc = us * 1e-6 * 2.4e9
             rec["lds_bank_conflict_frac"] = lds["SQ_LDS_BANK_CONFLICT"] / 256 / cyc
             rec["wave_wait_dependency_frac"] = lds["SQ_WAIT_INST_ANY"] / lds["SQ_WAVE_CYCLES"]
+            if "SQ_INST_LEVEL_LDS" in lds and c.get("SQ_INSTS_LDS"):
+                # Little's law over the kernel: average LDS / vector-memory instructions in flight
+                rec["lds_in_flight_per_wave"] = lds["SQ_INST_LEVEL_LDS"] / lds["SQ_WAVE_CYCLES"]
+                rec["vmem_in_flight_per_wave"] = lds["SQ_INST_LEVEL_VMEM"] / lds["SQ_WAVE_CYCLES"]
         out[f"2^{tag}"] = rec
     dst = REPO / "profiles" / "query_valu.json"
     dst.write_text(json.dumps(out, indent=1) + "\n")

@@ -1,10 +1,12 @@
-"""The radix cell index of the sort method (auc_sort.hip, dauc_set_search_mode) vs the C oracle.
+"""The search structures of the sort method (auc_sort.hip, dauc_set_search_mode) vs the C oracle.
 
 The labeled query pass (dauc_auc_counts_sorted_labeled, and through it dauc_auc_eval_counts)
-locates every negative among the sorted positives either through the LDS search tree (the
-default) or through the cell index (top 12 key bits -> bucket, multiply-high -> cell of ~mu keys,
-a 16-key slot plus a binary search beyond it; mode 2, a measured alternative). Every case here
-runs in all three modes: 0 (default: the tree), 1 (tree), 2 (cells wherever they fit). Bar: the integers (W, T) bit-exact against oracle/auc_oracle.c (sklearn's
+locates every negative among the sorted positives through one of: the count index (mode 0, the
+default where it fits: top 11 key bits -> bucket, multiply-high -> cell, per-8-cell LDS words of
+base + nibble counts, one 16-byte window for non-empty cells; the device falls back to the tree
+for skewed tables), the LDS search tree (mode 1), or the 16-key-slot cell index (mode 2, a
+measured alternative). Every case here runs in all three modes, so the skewed cases also cover
+mode 0's device-side fallback. Bar: the integers (W, T) bit-exact against oracle/auc_oracle.c (sklearn's
 _binary_clf_curve counts, main.py:79-81) on the same scores.
 """
 from __future__ import annotations
@@ -92,9 +94,10 @@ def test_cells_signed_wide_and_special_values(dev, ops):
 
 
 def test_cells_ties_and_overflowing_cells(dev, ops):
-    """Quantised scores: runs of equal keys longer than a 16-key slot (the cell pass searches
-    the rest of the cell in global memory), and a run of 20 equal keys in one cell with the
-    rest of the table uniform (the slow path for that cell only), ties across cell edges."""
+    """Quantised scores: runs of equal keys longer than a 16-key slot (the slot-cell pass
+    searches the rest of the cell in global memory; the count index finds a cell of 15+ keys
+    and keeps the tree), and a run of 20 equal keys in one cell with the rest of the table
+    uniform, ties across cell edges."""
     rng = np.random.default_rng(3)
     n = 1 << 20
     for levels, p in ((3001, 0.01), (97, 0.05), (5, 0.2), (1, 0.01)):
@@ -141,8 +144,9 @@ def test_cells_label_types_and_ranges(dev, ops, ldtype):
 
 
 def test_cells_table_size_limits(dev, ops):
-    """Tables needing 6 keys per cell (215,040) and more, up to the cell index's limit of
-    16 keys per cell (573,440) and one key past it (the tree runs in every mode)."""
+    """Table sizes around the limits: the count index up to 1.5 keys per cell (215,040 uses it,
+    400,000 is past it: the tree), the slot-cell index up to 16 keys per cell (573,440) and one
+    key past it (the tree in every mode)."""
     rng = np.random.default_rng(6)
     n = 1 << 22
     for P in (215_040, 215_041, 400_000, 573_440, 573_441):
