@@ -61,10 +61,7 @@ def main():
             cyc = us * 1e-6 * 2.4e9
             rec["lds_bank_conflict_frac"] = lds["SQ_LDS_BANK_CONFLICT"] / 256 / cyc
             rec["wave_wait_dependency_frac"] = lds["SQ_WAIT_INST_ANY"] / lds["SQ_WAVE_CYCLES"]
-            if "SQ_INST_LEVEL_LDS" in lds and c.get("SQ_INSTS_LDS"):
-                # Little's law over the kernel: average LDS / vector-memory instructions in flight
-                rec["lds_in_flight_per_wave"] = lds["SQ_INST_LEVEL_LDS"] / lds["SQ_WAVE_CYCLES"]
-                rec["vmem_in_flight_per_wave"] = lds["SQ_INST_LEVEL_VMEM"] / lds["SQ_WAVE_CYCLES"]
+
         out[f"2^{tag}"] = rec
     dst = REPO / "profiles" / "query_valu.json"
     dst.write_text(json.dumps(out, indent=1) + "\n")
