@@ -332,10 +332,11 @@ def bench_auc(args, world, rank, device, log2n=None, pos=None, pair_reps=None):
     n = 1 << log2n
     s, y = synthetic_scores(n, pos, device)  # same scores on every rank
     out = {"n": n, "log2n": log2n, "pos": pos}
-    # the sort method on one GPU is ONE blocking C call (dauc_auc_eval_counts); over ranks the
-    # compaction, the all-gathers and dauc_auc_counts_sorted_labeled are separate
+    # the sort method is ONE blocking C call per rank: the whole evaluation on one GPU (or below
+    # SHARD_MIN) is dauc_auc_eval_counts; over ranks each runs dauc_auc_eval_counts_part for its
+    # share of the queries, then one int64 [3] all-reduce
     sort_fn = ("dauc_auc_eval_counts" if world == 1 or n < ExactAUC.SHARD_MIN
-               else "dauc_auc_counts_sorted_labeled")
+               else "dauc_auc_eval_counts_part")
     for method, fn in (("sort", sort_fn), ("pairs", "dauc_pair_count_variant")):
         ev = ExactAUC(world=world, rank=rank, variant=args.variant, method=method)
         kt = KernelTimer(_lib.load(), fn)
@@ -372,14 +373,17 @@ def auc_record(auc, world, config_name):
     npairs = auc["npairs"]
     pc_rate = npairs / pk["t_count"]
     n = auc["n"]
-    # the sort method's HBM floor: labels read twice by the compaction, scores + labels once by
-    # the query pass (the positives' scores and the sorted table are ~0.1-1 % of that)
-    eval_bytes = n * (2 * 1 + 4 + 1) // world
+    # the sort method's HBM floor: labels read twice by the compaction (every rank compacts the
+    # whole vector), scores + labels once by the query pass over the rank's share (the positives'
+    # scores and the sorted table are ~0.1-1 % of that)
+    shard = world if sk["mode"] == "sharded" else 1
+    eval_bytes = n * 2 * 1 + n * (4 + 1) // shard
     return {
         "workload": f"exact AUC, 2^{auc['log2n']} fp32 scores, {auc['pos']:.1%} positives "
                     f"(BASELINE {config_name}), {world} rank(s); sort method {sk['mode']} "
-                    "(sharded = score-index ranges + int64 all-reduce; replicated = every rank evaluates the whole "
-                    "vector, below 2^25 scores); pair count: positive blocks, int64 all-reduce",
+                    "(sharded = every rank compacts and sorts all positives, queries its score-index range, int64 "
+                    "all-reduce; replicated = every rank evaluates the whole vector, below 2^24 scores); pair count: "
+                    "positive blocks, int64 all-reduce",
         "sort_mode": sk["mode"],
         "pairs_per_sec": npairs / sk["t_eval"],
         "method": "sort (default evaluator: compact the positives reading labels only, radix-sort them, locate "
@@ -390,11 +394,12 @@ def auc_record(auc, world, config_name):
         "eval_ms": sk["t_eval"] * 1e3, "sort_count_ms": sk["t_count"] * 1e3,
         "sort_count_what": f"HIP events around every {sk['count_fn']} call"
                            + (" (the whole one-call evaluation: compaction, sort, query, readback)"
-                              if sk["count_fn"] == "dauc_auc_eval_counts" else " (sort + tree + query)"),
+                              if sk["count_fn"] == "dauc_auc_eval_counts" else
+                              " (this rank's one-call part: compaction, sort, its query share, readback)"),
         "eval_roofline": {"bound": "hbm", "bytes_per_rank": eval_bytes,
                           "achieved": eval_bytes / sk["t_eval"] / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                           "frac": eval_bytes / sk["t_eval"] / 1e9 / HBM_PEAK_GBS,
-                          "note": "bytes = 2 label passes + 1 score/label pass over this rank's share"},
+                          "note": "bytes = 2 label passes over all n + 1 score/label pass over this rank's query share"},
         "query_kernel": load_profile("query_valu.json", f"2^{auc['log2n']}"),
         "P": auc["P"], "N": auc["N"], "wins": auc["wins"], "ties": auc["ties"], "auc": auc["auc"],
         "methods_agree": True,

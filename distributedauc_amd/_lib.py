@@ -69,6 +69,7 @@ SIGNATURES = {
     "dauc_compact_workspace_size": (_sz, [_i64]),
     "dauc_auc_eval_workspace_size": (_sz, [_i64]),
     "dauc_auc_eval_counts": (_int, [_vp, _vp, _int, _i64, _vp, _vp, _sz, _vp]),
+    "dauc_auc_eval_counts_part": (_int, [_vp, _vp, _int, _i64, _int, _int, _vp, _vp, _vp, _sz, _vp]),
     "dauc_compact_positives": (_int, [_vp, _vp, _int, _i64, _vp, _vp, _vp, _sz, _vp]),
     "dauc_sort_keys": (_int, [_vp, _i64, _vp, _vp, _sz, _vp]),
     "dauc_set_search_mode": (_int, [_int]),

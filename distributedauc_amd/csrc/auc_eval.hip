@@ -89,11 +89,25 @@ extern "C" {
 
 size_t dauc_auc_eval_workspace_size(int64_t n) { return eval_ws_bytes(n < 1 ? 1 : n); }
 
-int dauc_auc_eval_counts(const float* scores, const void* labels, int label_dtype, int64_t n, int64_t* out,
-                         void* workspace, size_t workspace_bytes, dauc_stream_t stream) {
+}  // extern "C"
+
+namespace dauc {
+namespace {
+
+// The evaluation of part `part` of `parts` (part 0 of 1 = the whole vector). Every part compacts
+// ALL the positives (each rank holds the same scores: main.py:237-250 evaluates one test set), so
+// the table is identical on every rank with no collective; only the queries are split -- the
+// score-index range [part*n/parts, (part+1)*n/parts) when the positives are the table, the
+// positive range [part*P/parts, (part+1)*P/parts) against the sorted negatives otherwise.
+//   out[7] = { W_part, T_part, P, N, #non-finite (global checks), #labels not in {-1, 1},
+//              #non-finite queried scores of this part }
+int eval_counts_part(const float* scores, const void* labels, int label_dtype, int64_t n, int part, int parts,
+                     int64_t* out, int64_t* part_counts, void* workspace, size_t workspace_bytes,
+                     dauc_stream_t stream) {
     if (n <= 0 || scores == nullptr || labels == nullptr || out == nullptr || workspace == nullptr ||
         workspace_bytes < eval_ws_bytes(n) || (reinterpret_cast<uintptr_t>(workspace) & 255u))
         return DAUC_EINVAL;
+    if (parts < 1 || part < 0 || part >= parts) return DAUC_EINVAL;
     if (label_dtype != DAUC_LABEL_I8 && label_dtype != DAUC_LABEL_I32 && label_dtype != DAUC_LABEL_I64)
         return DAUC_EINVAL;
     int64_t* host = pinned_words();
@@ -108,8 +122,10 @@ int dauc_auc_eval_counts(const float* scores, const void* labels, int label_dtyp
             return -static_cast<int>(e);
         return DAUC_OK;
     };
+    const int64_t qlo = n * part / parts, qhi = n * (part + 1) / parts;
     auto query = [&](int64_t P) {
-        return dauc_auc_counts_sorted_labeled(w.pos, P, scores, labels, label_dtype, 0, n, w.wt, w.wt + 2, w.tws,
+        if (qhi <= qlo) return static_cast<int>(DAUC_OK);
+        return dauc_auc_counts_sorted_labeled(w.pos, P, scores, labels, label_dtype, qlo, qhi, w.wt, w.wt + 2, w.tws,
                                               w.tws_bytes, stream);
     };
     // The table size P is known only after the compaction. An evaluation repeats on the same
@@ -142,20 +158,50 @@ int dauc_auc_eval_counts(const float* scores, const void* labels, int label_dtyp
             P = host[0];
             N = host[1];
             nonfinite = host[2];
-            if (nonfinite == 0) rc = dauc_auc_counts_sorted(w.pos, P, w.neg, N, w.wt, w.tws, w.tws_bytes, stream);
+            const int64_t plo = P * part / parts, phi = P * (part + 1) / parts;
+            if (nonfinite == 0 && phi > plo)
+                rc = dauc_auc_counts_sorted(w.pos + plo, phi - plo, w.neg, N, w.wt, w.tws, w.tws_bytes, stream);
         }
         if (rc) return rc;
         if ((rc = readback())) return rc;
         counted = true;
     }
     const bool have = counted && P > 0 && N > 0 && nonfinite == 0;
+    // this part's counts stay on the device too, for the caller's all-reduce (same stream: no sync)
+    if (have && part_counts != nullptr &&
+        (e = hipMemcpyAsync(part_counts, w.wt, 3 * sizeof(int64_t), hipMemcpyDeviceToDevice, st)) != hipSuccess)
+        return -static_cast<int>(e);
     out[0] = have ? host[8] : 0;
     out[1] = have ? host[9] : 0;
     out[2] = P;
     out[3] = N;
-    out[4] = nonfinite + (have ? host[10] : 0);
+    out[4] = nonfinite;
     out[5] = other;
+    out[6] = have ? host[10] : 0;
     return DAUC_OK;
+}
+
+}  // namespace
+}  // namespace dauc
+
+extern "C" {
+
+int dauc_auc_eval_counts(const float* scores, const void* labels, int label_dtype, int64_t n, int64_t* out,
+                         void* workspace, size_t workspace_bytes, dauc_stream_t stream) {
+    if (out == nullptr) return DAUC_EINVAL;
+    int64_t o[7];
+    const int rc = eval_counts_part(scores, labels, label_dtype, n, 0, 1, o, nullptr, workspace, workspace_bytes, stream);
+    if (rc) return rc;
+    for (int i = 0; i < 6; ++i) out[i] = o[i];
+    out[4] += o[6];
+    return DAUC_OK;
+}
+
+int dauc_auc_eval_counts_part(const float* scores, const void* labels, int label_dtype, int64_t n, int part,
+                              int parts, int64_t* out, int64_t* part_counts, void* workspace, size_t workspace_bytes,
+                              dauc_stream_t stream) {
+    return eval_counts_part(scores, labels, label_dtype, n, part, parts, out, part_counts, workspace, workspace_bytes,
+                            stream);
 }
 
 }  // extern "C"

@@ -365,6 +365,40 @@ def auc_eval_counts(scores: torch.Tensor, labels: torch.Tensor) -> tuple:
     return tuple(out)
 
 
+def auc_eval_counts_part(scores: torch.Tensor, labels: torch.Tensor, part: int, parts: int,
+                         part_counts: torch.Tensor) -> tuple:
+    """Part `part` of `parts` of the one-call evaluation (dauc_auc_eval_counts_part): every part
+    compacts and sorts all the positives, only the queries are split. Returns (W_part, T_part, P,
+    N, #non-finite by the global checks, #labels not in {-1, 1}, #non-finite queried scores of
+    this part); `part_counts` (int64 [3] on the device) receives (W_part, T_part, that last count)
+    on the current stream for an all-reduce, when both classes are present and the global checks
+    passed."""
+    _require(scores, "scores", torch.float32)
+    dev = scores.device
+    lc = _label_code(labels, "labels")
+    if scores.dim() != 1 or labels.dim() != 1 or scores.shape != labels.shape:
+        raise ValueError("scores and labels must be 1-D of equal length")
+    if not scores.is_contiguous() or not labels.is_contiguous():
+        raise ValueError("scores and labels must be contiguous")
+    _require(part_counts, "part_counts", torch.int64)
+    if part_counts.numel() < 3 or not part_counts.is_contiguous() or part_counts.device != dev:
+        raise ValueError("part_counts must be a contiguous int64 tensor of >= 3 elements on the scores' device")
+    n = scores.numel()
+    if n == 0:
+        raise ValueError("empty score vector")
+    L = _lib.load()
+    nbytes = _eval_ws_bytes.get(n)
+    if nbytes is None:
+        nbytes = _eval_ws_bytes[n] = L.dauc_auc_eval_workspace_size(n)
+    st = torch.cuda.current_stream(dev).cuda_stream
+    ws = workspaces.get(dev, "auc_eval", nbytes, st)
+    out = (ctypes.c_int64 * 7)()
+    check(L.dauc_auc_eval_counts_part(scores.data_ptr(), labels.data_ptr(), lc, n, int(part), int(parts),
+                                      ctypes.addressof(out), part_counts.data_ptr(), ws.data_ptr(), ws.numel(), st),
+          "dauc_auc_eval_counts_part")
+    return tuple(out)
+
+
 _eval_ws_bytes: dict = {}  # dauc_auc_eval_workspace_size per length (a pure function of n)
 
 

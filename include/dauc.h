@@ -316,6 +316,25 @@ int dauc_auc_eval_counts(const float* scores, const void* labels, int label_dtyp
                          void* workspace, size_t workspace_bytes, dauc_stream_t stream);
 
 /*
+ * Part `part` of `parts` of the same evaluation, for ranks that all hold the same test set
+ * (the reference evaluates one test set, main.py:237-250, and its sharded counterpart, SURVEY
+ * §8e). Every part compacts and sorts ALL the positives itself (the compaction reads only the
+ * labels and the positives' scores: no collective is needed to give every rank the same table);
+ * only the queries are split: scores [part*n/parts, (part+1)*n/parts) when P <= N, positives
+ * [part*P/parts, (part+1)*P/parts) against the sorted negatives when P > N. The parts' counts
+ * sum to dauc_auc_eval_counts's for every `parts`.
+ *   out[7] (HOST int64) = { W_part, T_part, P, N, #non-finite scores found by the global checks,
+ *                           #labels not in {-1, 1}, #non-finite queried scores of this part }
+ *   part_counts (DEVICE int64[3], may be NULL): receives { W_part, T_part, out[6] } on `stream`
+ *   (enqueued, not synchronised) when P > 0, N > 0 and out[4] == 0 -- the buffer the caller
+ *   all-reduces; out[2..5] are the same on every part, so every rank takes the same branch.
+ * Same workspace, synchronisation and speculative table size as dauc_auc_eval_counts.
+ */
+int dauc_auc_eval_counts_part(const float* scores, const void* labels, int label_dtype, int64_t n, int part,
+                              int parts, int64_t* out, int64_t* part_counts, void* workspace, size_t workspace_bytes,
+                              dauc_stream_t stream);
+
+/*
  * Search structure of dauc_auc_counts_sorted_labeled (and so of dauc_auc_eval_counts), for
  * tests and measurements; process-wide, default 0. Same integers in every mode.
  *   0: automatic -- the count index for tables of up to 219,838 keys (the key's top 11 bits pick

@@ -1,0 +1,50 @@
+"""Per-rank cost of the sharded sort-method evaluation on ONE GPU: dauc_auc_eval_counts_part for
+part 0 and part G-1 of G (what one rank of a G-GPU job runs before its all-reduce), next to the
+whole-vector dauc_auc_eval_counts, at configs[3] (2^24 @ 1 %) and configs[4] (2^27 @ 0.1 %).
+Wall time of the blocking call (median of `reps`), and the parts' counts summed against the
+whole call's. One JSON line per (n, G)."""
+from __future__ import annotations
+
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from distributedauc_amd import ops  # noqa: E402
+from distributedauc_amd.loader import synthetic_scores  # noqa: E402
+
+reps = int(sys.argv[1]) if len(sys.argv) > 1 else 30
+dev = torch.device("cuda", 0)
+pc = torch.zeros(3, dtype=torch.int64, device=dev)
+
+
+def wall(fn):
+    fn()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        fn()
+        ts.append(time.perf_counter() - t0)
+    return float(np.median(ts)) * 1e3
+
+
+for log2n, pr in ((24, 0.01), (27, 0.001)):
+    s, y = synthetic_scores(1 << log2n, pr, dev)
+    whole = ops.auc_eval_counts(s, y)
+    t_whole = wall(lambda: ops.auc_eval_counts(s, y))
+    print(json.dumps({"log2n": log2n, "G": 1, "fn": "dauc_auc_eval_counts", "ms": t_whole, "W": whole[0],
+                      "T": whole[1]}), flush=True)
+    for G in (2, 4, 8):
+        W = T = 0
+        for r in range(G):
+            o = ops.auc_eval_counts_part(s, y, r, G, pc)
+            W, T = W + o[0], T + o[1]
+        t0 = wall(lambda: ops.auc_eval_counts_part(s, y, 0, G, pc))
+        tl = wall(lambda: ops.auc_eval_counts_part(s, y, G - 1, G, pc))
+        print(json.dumps({"log2n": log2n, "G": G, "fn": "dauc_auc_eval_counts_part", "ms_part0": t0,
+                          "ms_last": tl, "sum_matches_whole": (W, T) == (whole[0], whole[1])}), flush=True)

@@ -114,6 +114,34 @@ def auc_eval_counts(scores, labels):
     return e["wins"], e["ties"], P, s.size - P, 0, other
 
 
+def auc_eval_counts_part(scores, labels, part, parts, part_counts):
+    """dauc_auc_eval_counts_part's stand-in: every part sees all positives, queries its slice."""
+    s, y = scores.detach().numpy(), labels.numpy().astype(np.int64)
+    n = s.size
+    ispos = y == 1
+    P, N = int(ispos.sum()), n - int(ispos.sum())
+    other = int(((y != 1) & (y != -1)).sum())
+    fin = np.isfinite(s)
+    if P <= N:
+        bad = int((~fin[ispos]).sum())  # the compaction checks the positives' scores
+    else:
+        bad = int((~fin).sum())  # the split checks every score
+    if bad or P == 0 or N == 0:
+        return 0, 0, P, N, bad, other, 0
+    pos, negs = s[ispos], s[~ispos]
+    if P <= N:
+        lo, hi = n * part // parts, n * (part + 1) // parts
+        q = s[lo:hi][y[lo:hi] != 1]
+        qbad = int((~np.isfinite(q)).sum())
+        W, T = coracle_pair_count(pos, q[np.isfinite(q)]) if q.size else (0, 0)
+    else:
+        lo, hi = P * part // parts, P * (part + 1) // parts
+        qbad = 0
+        W, T = coracle_pair_count(pos[lo:hi], negs) if hi > lo else (0, 0)
+    part_counts[0], part_counts[1], part_counts[2] = W, T, qbad
+    return W, T, P, N, bad, other, qbad
+
+
 def coracle_pair_count(pos, neg):
     from oracle import coracle
 
@@ -124,7 +152,8 @@ def install(monkeypatch):
     from distributedauc_amd import flat, ops
 
     for name in ("label_map_phat", "surrogate_fwdbwd", "class_sums", "alpha_from_sums", "coda_finalize",
-                 "scale_div", "pd_update", "compact_positives", "auc_counts_sorted_labeled", "auc_eval_counts"):
+                 "scale_div", "pd_update", "compact_positives", "auc_counts_sorted_labeled", "auc_eval_counts",
+                 "auc_eval_counts_part"):
         monkeypatch.setattr(ops, name, globals()[name])
     monkeypatch.setattr(flat, "_check_device", lambda dev: None)
 

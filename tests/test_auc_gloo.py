@@ -1,6 +1,6 @@
-"""The sharded exact-AUC orchestration on CPU (gloo, world 2 and 3): each rank compacts the
-positives of its own index slice, all ranks all-gather them (in order) and stream their slice of
-the scores through the count; one all-reduce of (wins, ties, non-finite). Below
+"""The sharded exact-AUC orchestration on CPU (gloo, world 2 and 3): every rank runs the
+part-wise evaluation (all positives compacted and sorted locally, its slice of the scores
+streamed through the search) and one all-reduce sums (wins, ties, non-finite). Below
 ExactAUC.SHARD_MIN scores every rank evaluates the whole vector instead (same integers, no
 collective); both modes run here. The kernels are served by the oracle (tests/cpu_kernels.py);
 the GPU form runs in bench.py --gpus 2 (tests/test_bench_gpu.py)."""

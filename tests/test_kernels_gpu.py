@@ -489,6 +489,42 @@ def test_auc_eval_counts_one_call(dev, ldtype):
             assert bad >= 1, (where, p)
 
 
+def test_auc_eval_counts_part(dev):
+    """dauc_auc_eval_counts_part (the sharded evaluation's per-rank call): for G = 1, 2, 3, 8 the
+    parts' (W, T) sum to the C oracle's on both table sides (P < N: score ranges; P > N: positive
+    ranges), including G larger than a tiny n (empty parts); the device part_counts equal the host
+    ones; P, N and the global checks are the same on every part; a non-finite negative shows up
+    in exactly the part whose range holds it; speculation hits and misses (parts re-use the
+    previous call's P)."""
+    from distributedauc_amd import ops
+
+    rng = np.random.default_rng(91)
+    for n, p in ((300_001, 0.02), (300_001, 0.8), (5, 0.4), (2_000_003, 0.001), (300_001, 0.03)):
+        s = (np.floor(rng.random(n) * 2000) / 2000).astype(np.float32)
+        y = np.where(rng.random(n) < p, 1, -1).astype(np.int8)
+        e = coracle.auc_counts(y.astype(np.int64), s)
+        for G in (1, 2, 3, 8):
+            W = Tt = 0
+            for r in range(G):
+                pc = torch.full((3,), -7, dtype=torch.int64, device=dev)
+                o = ops.auc_eval_counts_part(T(s, dev), T(y, dev), r, G, pc)
+                assert o[2:6] == (e["P"], e["N"], 0, 0) and o[6] == 0, (n, p, G, r, o)
+                if e["P"] and e["N"]:
+                    assert pc.cpu().tolist() == [o[0], o[1], 0], (n, p, G, r)
+                W += o[0]
+                Tt += o[1]
+            if e["P"] and e["N"]:
+                assert (W, Tt) == (e["wins"], e["ties"]), (n, p, G)
+    n = 100_003
+    s = rng.random(n, dtype=np.float32)
+    y = np.where(rng.random(n) < 0.05, 1, -1).astype(np.int8)
+    j = int(np.flatnonzero(y == -1)[-2])  # in the last part's range
+    s[j] = np.nan
+    pc = torch.zeros(3, dtype=torch.int64, device=dev)
+    seen = [ops.auc_eval_counts_part(T(s, dev), T(y, dev), r, 4, pc)[6] for r in range(4)]
+    assert seen == [0, 0, 0, 1], seen
+
+
 def test_auc_sort_rejects_nonfinite_negatives(dev):
     """The sort method never materialises the negatives: the query kernel's finiteness count
     must still reject a NaN / inf negative (sklearn _ranking.py:868-869), sharded or not."""
