@@ -346,7 +346,8 @@ __global__ __launch_bounds__(kCmpThreads) void compact_count_kernel(const LT* __
                                                                     int vec, int* __restrict__ blk,
                                                                     uint4* __restrict__ masks,
                                                                     int64_t* __restrict__ stats,
-                                                                    unsigned long long* __restrict__ zero3) {
+                                                                    unsigned long long* __restrict__ zero3,
+                                                                    unsigned* __restrict__ zero_w, int nzero_w) {
     static_assert(kCmpSlots == 8, "8 16-bit group masks = one uint4 per thread");
     __shared__ int part[2][kCmpThreads / kWave];
     const int64_t base = int64_t(blockIdx.x) * kCmpTile;
@@ -354,6 +355,8 @@ __global__ __launch_bounds__(kCmpThreads) void compact_count_kernel(const LT* __
         if (threadIdx.x == 0) stats[2] = 0;  // the write pass adds the non-finite positives
         else if (zero3 != nullptr) zero3[threadIdx.x - 1] = 0;  // a later stage's counters (dauc_auc_eval_counts)
     }
+    if (blockIdx.x == 0)  // a later stage's histogram (the eval's direct count-index build)
+        for (int i = threadIdx.x; i < nzero_w; i += kCmpThreads) zero_w[i] = 0u;
     int np = 0, no = 0;
     unsigned m[kCmpSlots];
 #pragma unroll
@@ -477,14 +480,15 @@ __global__ __launch_bounds__(kCmpThreads) void compact_write_kernel(
 
 template <typename LT>
 int launch_compact(const float* s, const LT* lab, int64_t n, float* pos_out, int64_t* stats, void* ws,
-                   hipStream_t st, unsigned long long* zero3 = nullptr) {
+                   hipStream_t st, unsigned long long* zero3 = nullptr, unsigned* zero_w = nullptr,
+                   int nzero_w = 0) {
     const int64_t nblk = compact_blocks(n);
     if (nblk > 0x7fffffffLL) return DAUC_EINVAL;
     int* blk = static_cast<int*>(ws);
     auto* masks = reinterpret_cast<uint4*>(static_cast<char*>(ws) + compact_masks_offset(n));
     const int vec = (reinterpret_cast<uintptr_t>(lab) & 15u) == 0;
     hipLaunchKernelGGL(compact_count_kernel<LT>, dim3(static_cast<unsigned>(nblk)), dim3(kCmpThreads), 0, st, lab, n,
-                       vec, blk, masks, stats, zero3);
+                       vec, blk, masks, stats, zero3, zero_w, nzero_w);
     int rc = launch_status();
     if (rc) return rc;
     hipLaunchKernelGGL(compact_write_kernel, dim3(static_cast<unsigned>(nblk)), dim3(kCmpThreads), 0, st, s, n, blk,
@@ -715,21 +719,25 @@ size_t dauc_compact_workspace_size(int64_t n) { return compact_ws_bytes(n < 0 ? 
 }  // extern "C"
 
 namespace dauc {
-// dauc_compact_positives that also zeroes 3 counters of a later stage in its first launch
+// dauc_compact_positives that also zeroes 3 counters and nzero_w words of later stages in its
+// first launch
 int compact_positives_zeroing(const float* scores, const void* labels, int label_dtype, int64_t n, float* pos_out,
                               int64_t* stats, void* workspace, size_t workspace_bytes, unsigned long long* zero3,
-                              hipStream_t st) {
+                              hipStream_t st, unsigned* zero_w, int nzero_w) {
     if (n <= 0 || scores == nullptr || labels == nullptr || pos_out == nullptr || stats == nullptr ||
         workspace == nullptr || workspace_bytes < dauc_compact_workspace_size(n) ||
         (reinterpret_cast<uintptr_t>(workspace) & 15u) || (reinterpret_cast<uintptr_t>(stats) & 7u))
         return DAUC_EINVAL;
     switch (label_dtype) {
         case DAUC_LABEL_I8:
-            return launch_compact(scores, static_cast<const int8_t*>(labels), n, pos_out, stats, workspace, st, zero3);
+            return launch_compact(scores, static_cast<const int8_t*>(labels), n, pos_out, stats, workspace, st, zero3,
+                                  zero_w, nzero_w);
         case DAUC_LABEL_I32:
-            return launch_compact(scores, static_cast<const int32_t*>(labels), n, pos_out, stats, workspace, st, zero3);
+            return launch_compact(scores, static_cast<const int32_t*>(labels), n, pos_out, stats, workspace, st, zero3,
+                                  zero_w, nzero_w);
         case DAUC_LABEL_I64:
-            return launch_compact(scores, static_cast<const int64_t*>(labels), n, pos_out, stats, workspace, st, zero3);
+            return launch_compact(scores, static_cast<const int64_t*>(labels), n, pos_out, stats, workspace, st, zero3,
+                                  zero_w, nzero_w);
         default:
             return DAUC_EINVAL;
     }

@@ -68,10 +68,11 @@ struct EvalMemo {
     int64_t n;
     int dtype;
     int64_t P;
+    bool direct_ok;  // the count index built from the unsorted table was usable last time
 };
 
 EvalMemo& eval_memo() {
-    static thread_local EvalMemo m{0, 0, 0};
+    static thread_local EvalMemo m{0, 0, 0, true};
     return m;
 }
 
@@ -115,41 +116,74 @@ int eval_counts_part(const float* scores, const void* labels, int label_dtype, i
     hipStream_t st = as_hip(stream);
     const EvalWs w = eval_ws(workspace, n);
     hipError_t e;
-    // stats [0, 32) and the counts [64, 88) come back in one copy
+    // the direct build's verdict word (1 = the count index was usable, 2 = re-run sorted)
+    unsigned* verdict = reinterpret_cast<unsigned*>(w.wt + 3);
+    // stats [0, 32), the counts [64, 88) and the verdict [88, 92) come back in one copy
     auto readback = [&]() -> int {
-        if ((e = hipMemcpyAsync(host, w.stats, 88, hipMemcpyDeviceToHost, st)) != hipSuccess ||
+        if ((e = hipMemcpyAsync(host, w.stats, 96, hipMemcpyDeviceToHost, st)) != hipSuccess ||
             (e = hipStreamSynchronize(st)) != hipSuccess)
             return -static_cast<int>(e);
         return DAUC_OK;
     };
     const int64_t qlo = n * part / parts, qhi = n * (part + 1) / parts;
+    // the sorted path: radix sort of the positives, the tree, the count index behind them
     auto query = [&](int64_t P) {
         if (qhi <= qlo) return static_cast<int>(DAUC_OK);
         return dauc_auc_counts_sorted_labeled(w.pos, P, scores, labels, label_dtype, qlo, qhi, w.wt, w.wt + 2, w.tws,
                                               w.tws_bytes, stream);
     };
+    // the direct path: the count index straight from the unsorted positives (no sort, no tree);
+    // its verdict says whether the table was usable (else the sorted path re-runs)
+    auto direct = [&](int64_t P) {
+        return counts_labeled_direct(w.pos, P, scores, labels, label_dtype, qlo, qhi, w.wt, w.wt + 2, verdict, w.tws,
+                                     w.tws_bytes, st);
+    };
+    auto direct_verdict_ok = [&]() { return qhi <= qlo || static_cast<unsigned>(host[11] & 0xffffffffLL) == 1u; };
     // The table size P is known only after the compaction. An evaluation repeats on the same
     // test set (main.py evaluates it after every stage), so the last call's P for this n is
-    // taken as the size and the sort and query are enqueued behind the compaction WITHOUT a
+    // taken as the size and the build and query are enqueued behind the compaction WITHOUT a
     // readback in between; the one readback at the end returns the real P with the counts, and a
-    // different P (other data of the same length) re-runs the sort and query at the real size.
+    // different P (other data of the same length) re-runs them at the real size.
     EvalMemo& memo = eval_memo();
-    const bool speculate = memo.n == n && memo.dtype == label_dtype && memo.P > 0 && memo.P <= n - memo.P;
-    // the compaction's first launch also zeroes the query's counters
-    int rc = compact_positives_zeroing(scores, labels, label_dtype, n, w.pos, w.stats, w.cws, w.cws_bytes, w.wt, st);
+    const bool same = memo.n == n && memo.dtype == label_dtype;
+    bool direct_ok = same ? memo.direct_ok : true;
+    const bool speculate = same && memo.P > 0 && memo.P <= n - memo.P;
+    const bool spec_direct = speculate && direct_ok && direct_fits(memo.P);
+    // the compaction's first launch also zeroes the query's counters (and the direct build's
+    // top-bucket histogram)
+    int rc = compact_positives_zeroing(
+        scores, labels, label_dtype, n, w.pos, w.stats, w.cws, w.cws_bytes, w.wt, st,
+        spec_direct ? reinterpret_cast<unsigned*>(static_cast<char*>(w.tws) + direct_hist_offset(memo.P)) : nullptr,
+        spec_direct ? direct_hist_words() : 0);
     if (rc) return rc;
-    if (speculate && (rc = query(memo.P))) return rc;
+    if (speculate && (rc = spec_direct ? direct(memo.P) : query(memo.P))) return rc;
     if ((rc = readback())) return rc;
     int64_t P = host[0], N = host[1], nonfinite = host[2];
     const int64_t other = host[3];
-    bool counted = speculate && P == memo.P;
-    memo = EvalMemo{n, label_dtype, P};
+    bool counted = false;
+    if (speculate && P == memo.P) {
+        if (!spec_direct || direct_verdict_ok()) counted = true;
+        else direct_ok = false;  // a skewed table: the sorted path below
+    }
     if (!counted && P > 0 && N > 0 && nonfinite == 0) {
         if ((e = hipMemsetAsync(w.wt, 0, 3 * sizeof(unsigned long long), st)) != hipSuccess)
             return -static_cast<int>(e);
         if (P <= N) {
             // the positives are the table; every other score is a query read in place
-            rc = query(P);
+            if (direct_ok && direct_fits(P)) {
+                unsigned* hist = reinterpret_cast<unsigned*>(static_cast<char*>(w.tws) + direct_hist_offset(P));
+                if ((e = hipMemsetAsync(hist, 0, size_t(direct_hist_words()) * 4, st)) != hipSuccess)
+                    return -static_cast<int>(e);
+                if ((rc = direct(P)) || (rc = readback())) return rc;
+                if (direct_verdict_ok()) {
+                    counted = true;
+                } else {
+                    direct_ok = false;
+                    if ((e = hipMemsetAsync(w.wt, 0, 3 * sizeof(unsigned long long), st)) != hipSuccess)
+                        return -static_cast<int>(e);
+                }
+            }
+            if (!counted) rc = query(P);
         } else {
             // the negatives are the smaller class: materialise both (the split checks every score)
             rc = dauc_split_scores(scores, labels, label_dtype, n, w.pos, w.neg, w.stats, w.sws, w.sws_bytes, stream);
@@ -163,9 +197,10 @@ int eval_counts_part(const float* scores, const void* labels, int label_dtype, i
                 rc = dauc_auc_counts_sorted(w.pos + plo, phi - plo, w.neg, N, w.wt, w.tws, w.tws_bytes, stream);
         }
         if (rc) return rc;
-        if ((rc = readback())) return rc;
+        if (!counted && (rc = readback())) return rc;
         counted = true;
     }
+    memo = EvalMemo{n, label_dtype, P, direct_ok};
     const bool have = counted && P > 0 && N > 0 && nonfinite == 0;
     // this part's counts stay on the device too, for the caller's all-reduce (same stream: no sync)
     if (have && part_counts != nullptr &&

@@ -1533,7 +1533,7 @@ __device__ __forceinline__ bool ci_count(unsigned x, bool use, unsigned rl, unsi
     return use && (rl & 3u) + cnt > 4u;
 }
 
-// a cell past its window: the next 4 keys (or a binary search past 8); corrects W and T
+// a cell past its window: the next 4 keys (or, past 8, every key of the cell); corrects W and T
 __device__ __forceinline__ void ci_fix(unsigned x, unsigned rl, unsigned cnt, const uint4& k,
                                        const unsigned* __restrict__ sorted, unsigned long long& w,
                                        unsigned long long& t) {
@@ -1546,9 +1546,15 @@ __device__ __forceinline__ void ci_fix(unsigned x, unsigned rl, unsigned cnt, co
         lb = int64_t(a) + lt0 + (k2.x < x) + (k2.y < x) + (k2.z < x) + (k2.w < x);
         ub = int64_t(a) + le0 + (k2.x <= x) + (k2.y <= x) + (k2.z <= x) + (k2.w <= x);
     } else {
-        const int64_t b0 = rl, b1 = int64_t(rl) + cnt;
-        lb = b0 + count_below<true>(sorted, b0, b1, x);
-        ub = b0 + count_below<false>(sorted, b0, b1, x);
+        // <= 14 keys (a cell of 15+ keys marks the table skewed): counted one by one, so the order
+        // of the keys inside the cell does not matter (the direct build orders the table by cell only)
+        lb = rl;
+        ub = rl;
+        for (unsigned j = rl; j < rl + cnt; ++j) {
+            const unsigned v = sorted[j];
+            lb += v < x;
+            ub += v <= x;
+        }
     }
     const int64_t lbf = int64_t(a) + lt0, ubf = int64_t(a) + le0;
     w -= static_cast<unsigned long long>(ub - ubf);
@@ -1572,8 +1578,11 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
                                                                 const uint2* __restrict__ blkg,
                                                                 const unsigned* __restrict__ sorted, int64_t M,
                                                                 unsigned long long* __restrict__ out,
-                                                                unsigned long long* __restrict__ nonfinite) {
-    if (!count_index_in_use(meta)) return;
+                                                                unsigned long long* __restrict__ nonfinite,
+                                                                unsigned* __restrict__ verdict) {
+    const bool in_use = count_index_in_use(meta);
+    if (verdict != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *verdict = in_use ? 1u : 2u;
+    if (!in_use) return;
     extern __shared__ uint2 ci_lds[];
     const int nb = static_cast<int>(meta[kCiBlocks]);
     uint2* l1 = ci_lds;          // [2048]
@@ -1686,6 +1695,178 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
         if (bw) atomicAdd(out + 0, bw);
         if (bt) atomicAdd(out + 1, bt);
         if (bn && nonfinite) atomicAdd(nonfinite, bn);
+    }
+}
+
+// ---- the count index built straight from the unsorted table (the one-call evaluation) -------
+//
+// The count index needs the table ordered by CELL only: ci_count and ci_fix count a cell's keys
+// whatever their order (keys of earlier cells are < x, of later cells > x). So the one-call
+// evaluation skips the radix sort and the tree: a top-bucket histogram, the plan, per-cell counts,
+// the block words and their prefix, and a scatter of every key into its cell's range -- 6 small
+// launches over the table instead of 8 sort launches + the tree + the 4-launch build behind a
+// sort. The table is not sorted inside a cell, so the tree cannot fall back on it: when the plan
+// or the block pass finds the table unusable (more than 1.5 keys per cell, a cell of 15+ keys)
+// the query kernel reports it (*verdict = 2) and the caller re-runs the sorted path.
+constexpr int64_t kCiCntWords = ((int64_t(kCiMaxCells) + 2) * 4 + 255) / 256 * 64;  // the cstart region
+constexpr int kDirectPerThread = 8;
+
+// top-bucket histogram (LDS, then one global add per used bucket; `hist` zeroed by the caller);
+// also zeroes the per-cell counters the count pass adds into
+__global__ __launch_bounds__(256) void direct_hist_kernel(const float* __restrict__ pos, int64_t M,
+                                                          unsigned* __restrict__ hist, unsigned* __restrict__ cnt,
+                                                          int64_t ncnt) {
+    __shared__ unsigned h[kCiTop];
+    for (int i = threadIdx.x; i < kCiTop; i += 256) h[i] = 0u;
+    __syncthreads();
+    const int64_t gid = int64_t(blockIdx.x) * 256 + threadIdx.x, stride = int64_t(gridDim.x) * 256;
+    for (int64_t i = gid; i < ncnt; i += stride) cnt[i] = 0u;
+    for (int64_t i = gid; i < M; i += stride) atomicAdd(&h[key_fast(pos[i]) >> kCiLowBits], 1u);
+    __syncthreads();
+    for (int i = threadIdx.x; i < kCiTop; i += 256)
+        if (h[i]) atomicAdd(hist + i, h[i]);
+}
+
+// One workgroup, the plan of ci_plan_kernel from the bucket sizes themselves: C_t = ceil(n_t *
+// num / M) cells per used bucket, num = min(cells left after one per used bucket, 2 M), the
+// first cell of every bucket (ascending), and the verdict words
+__global__ __launch_bounds__(kCiPlanThreads) void direct_plan_kernel(int64_t M, const unsigned* __restrict__ hist,
+                                                                     uint2* __restrict__ l1,
+                                                                     unsigned* __restrict__ meta) {
+    static_assert(kCiTop == 2 * kCiPlanThreads, "two top buckets per thread");
+    __shared__ unsigned wtot[kCiPlanThreads / kWave];
+    __shared__ unsigned totals[2];
+    const uint2 n = reinterpret_cast<const uint2*>(hist)[threadIdx.x];  // buckets 2i, 2i + 1
+    const unsigned used = block_incl_scan1024<false>((n.x != 0u) + (n.y != 0u), wtot);
+    if (threadIdx.x == kCiPlanThreads - 1) totals[0] = used;
+    __syncthreads();
+    const int64_t avail = int64_t(kCiMaxCells) - int64_t(totals[0]);
+    const int64_t num = avail < 2 * M ? avail : 2 * M;
+    const unsigned c0 = n.x ? static_cast<unsigned>((int64_t(n.x) * num + M - 1) / M) : 0u;
+    const unsigned c1 = n.y ? static_cast<unsigned>((int64_t(n.y) * num + M - 1) / M) : 0u;
+    const unsigned incl = block_incl_scan1024<false>(c0 + c1, wtot);
+    if (threadIdx.x == kCiPlanThreads - 1) totals[1] = incl;
+    __syncthreads();
+    const unsigned excl = incl - c0 - c1, total = totals[1];
+    reinterpret_cast<uint4*>(l1)[threadIdx.x] = uint4{excl, c0, excl + c0, c1};
+    if (threadIdx.x == 0) {
+        meta[kCiOk] = (num > 0 && 3 * num >= 2 * M && total <= static_cast<unsigned>(kCiMaxCells)) ? 1u : 0u;
+        meta[kCiCells] = total;
+        meta[kCiBlocks] = (total + 1 + kCiBlock - 1) / kCiBlock;
+        meta[kCiSkew] = 0u;
+    }
+}
+
+// per-cell key counts (a wave whose keys all fall in one cell adds once: tie-heavy tables)
+__global__ __launch_bounds__(256) void direct_count_kernel(const float* __restrict__ pos, int64_t M,
+                                                           const uint2* __restrict__ l1,
+                                                           const unsigned* __restrict__ meta,
+                                                           unsigned* __restrict__ cnt, unsigned* __restrict__ cell) {
+    if (meta[kCiOk] == 0u) return;
+    const int64_t gid = int64_t(blockIdx.x) * 256 + threadIdx.x, stride = int64_t(gridDim.x) * 256;
+    const int lane = threadIdx.x & (kWave - 1);
+    for (int64_t i0 = gid - lane; i0 < M; i0 += stride) {  // wave-uniform trip count
+        const int64_t i = i0 + lane;
+        const bool live = i < M;
+        unsigned c = 0u;
+        if (live) {
+            const unsigned x = key_fast(pos[i]);
+            c = ci_cell(x, l1[x >> kCiLowBits]);
+            cell[i] = c;  // the scatter's cell, so it does not walk pos -> key -> l1 again
+        }
+        const unsigned long long act = __ballot(live);
+        const int first = __ffsll(static_cast<long long>(act)) - 1;
+        const unsigned cf = __shfl(c, first, kWave);
+        if (__ballot(live && c == cf) == act) {
+            if (lane == first) atomicAdd(cnt + cf, static_cast<unsigned>(__popcll(act)));
+        } else if (live) {
+            atomicAdd(cnt + c, 1u);
+        }
+    }
+}
+
+// One thread per block of 8 cells: {the block's key count, the cells' counts as nibbles}; a count
+// of 15 or more marks the table skewed. The block counts become prefixes in direct_scan_kernel.
+__global__ __launch_bounds__(256) void direct_blocks_kernel(const unsigned* __restrict__ cnt,
+                                                            unsigned* __restrict__ meta, uint2* __restrict__ blk) {
+    if (meta[kCiOk] == 0u) return;
+    const int b = blockIdx.x * 256 + threadIdx.x;
+    bool skew = false;
+    if (b < static_cast<int>(meta[kCiBlocks])) {
+        const uint4 lo = reinterpret_cast<const uint4*>(cnt)[2 * b], hi = reinterpret_cast<const uint4*>(cnt)[2 * b + 1];
+        const unsigned c[kCiBlock] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+        unsigned w = 0u, sum = 0u;
+#pragma unroll
+        for (int j = 0; j < kCiBlock; ++j) {
+            skew |= c[j] >= 15u;
+            w |= (c[j] < 15u ? c[j] : 15u) << (4 * j);
+            sum += c[j];
+        }
+        blk[b] = uint2{sum, w};
+    }
+    if (__ballot(skew) != 0ull && (threadIdx.x & (kWave - 1)) == 0) atomicOr(meta + kCiSkew, 1u);
+}
+
+// One workgroup: blk[b].x = the table keys before block b (exclusive prefix of the block counts);
+// the counts are staged through LDS so the global reads and writes stay coalesced while every
+// thread scans a contiguous run of blocks
+__global__ __launch_bounds__(kCiPlanThreads) void direct_scan_kernel(const unsigned* __restrict__ meta,
+                                                                     uint2* __restrict__ blk) {
+    if (meta[kCiOk] == 0u || meta[kCiSkew] != 0u) return;
+    constexpr int kPer = (kCiMaxBlocks + kCiPlanThreads - 1) / kCiPlanThreads;  // 18
+    __shared__ unsigned wtot[kCiPlanThreads / kWave];
+    __shared__ unsigned xs[kPer * kCiPlanThreads];
+    const int nb = static_cast<int>(meta[kCiBlocks]);
+    {
+        unsigned v[kPer];  // every load in flight before the first LDS store
+#pragma unroll
+        for (int j = 0; j < kPer; ++j) {
+            const int i = j * kCiPlanThreads + threadIdx.x;
+            v[j] = i < nb ? blk[i].x : 0u;
+        }
+#pragma unroll
+        for (int j = 0; j < kPer; ++j) xs[j * kCiPlanThreads + threadIdx.x] = v[j];
+    }
+    __syncthreads();
+    const int b0 = threadIdx.x * kPer;
+    unsigned sum = 0u;
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) sum += xs[b0 + j];
+    unsigned run = block_incl_scan1024<false>(sum, wtot) - sum;
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+        const unsigned v = xs[b0 + j];
+        xs[b0 + j] = run;
+        run += v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+        const int i = j * kCiPlanThreads + threadIdx.x;
+        if (i < nb) blk[i].x = xs[i];
+    }
+}
+
+// every key into its cell's range of the table (the counters are counted back down to zero);
+// the table's tail is padded with +inf keys for the 16-byte windows
+__global__ __launch_bounds__(256) void direct_scatter_kernel(const float* __restrict__ pos, int64_t M,
+                                                             const uint2* __restrict__ l1,
+                                                             const uint2* __restrict__ blk,
+                                                             const unsigned* __restrict__ meta,
+                                                             unsigned* __restrict__ cnt,
+                                                             const unsigned* __restrict__ cell,
+                                                             unsigned* __restrict__ table) {
+    if (meta[kCiOk] == 0u || meta[kCiSkew] != 0u) return;
+    const int64_t gid = int64_t(blockIdx.x) * 256 + threadIdx.x, stride = int64_t(gridDim.x) * 256;
+    if (gid < 16) table[M + gid] = kPadKey;
+    for (int64_t i = gid; i < M; i += stride) {
+        const unsigned x = key_fast(pos[i]);
+        const unsigned c = cell[i];
+        const uint2 b = blk[c / kCiBlock];
+        const unsigned below = __builtin_amdgcn_ubfe(b.y, 0u, 4u * (c % kCiBlock));
+        const unsigned bytes = (below & 0x0f0f0f0fu) + ((below >> 4) & 0x0f0f0f0fu);
+        const unsigned slot = atomicSub(cnt + c, 1u) - 1u;
+        table[b.x + __builtin_amdgcn_sad_u8(bytes, 0u, 0u) + slot] = x;
     }
 }
 
@@ -2010,12 +2191,21 @@ int prepare_count(const unsigned* sorted, int64_t M, const CountWs& cw, hipStrea
 
 template <typename LT>
 int launch_ci(const float* s, const LT* lab, int64_t begin, int64_t end, const CountWs& cw, const unsigned* sorted,
-              int64_t M, unsigned long long* out, unsigned long long* nonfinite, hipStream_t st) {
+              int64_t M, unsigned long long* out, unsigned long long* nonfinite, hipStream_t st,
+              unsigned* verdict = nullptr) {
     const dim3 grid(query_grid(end - begin)), block(kQueryThreads);
     const size_t lds = (size_t(kCiTop) + kCiMaxBlocks) * 8;
     hipLaunchKernelGGL((query_ci_kernel<LT>), grid, block, lds, st, s, lab, begin, end, cw.meta, cw.l1, cw.blk, sorted,
-                       M, out, nonfinite);
+                       M, out, nonfinite, verdict);
     return launch_status();
+}
+
+char* after_tree_of(void* workspace, int64_t P) {
+    return static_cast<char*>(workspace) + ((sort_ws_bytes(P) + 255) / 256) * 256 + ((kTreeBytes + 255) / 256) * 256;
+}
+
+CountWs count_ws_of(void* workspace, int64_t P) {
+    return carve_count(after_tree_of(workspace, P) + ((kCellBytes + 255) / 256) * 256);
 }
 
 template <typename LT>
@@ -2066,6 +2256,56 @@ int prepare_table(const float* table, int64_t M, void* workspace, hipStream_t st
 }
 
 }  // namespace
+
+bool direct_fits(int64_t P) { return g_search_mode == 0 && P > 0 && 2 * P <= 3 * int64_t(kCiMaxCells); }
+
+int direct_hist_words() { return kCiTop; }
+
+int64_t direct_hist_offset(int64_t P) {  // carve_count(...).first, relative to the workspace
+    return int64_t(((sort_ws_bytes(P) + 255) / 256) * 256 + ((kTreeBytes + 255) / 256) * 256 +
+                   ((kCellBytes + 255) / 256) * 256 + 256);
+}
+
+int counts_labeled_direct(const float* pos, int64_t P, const float* scores, const void* labels, int label_dtype,
+                          int64_t begin, int64_t end, unsigned long long* wins_ties, unsigned long long* nonfinite,
+                          unsigned* verdict, void* workspace, size_t workspace_bytes, hipStream_t st) {
+    if (!direct_fits(P) || pos == nullptr || begin < 0 || end < begin || wins_ties == nullptr ||
+        (end > begin && (scores == nullptr || labels == nullptr)) || workspace == nullptr ||
+        workspace_bytes < dauc_sort_workspace_size(P))
+        return DAUC_EINVAL;
+    if (label_dtype != DAUC_LABEL_I8 && label_dtype != DAUC_LABEL_I32 && label_dtype != DAUC_LABEL_I64)
+        return DAUC_EINVAL;
+    const SortWs w = carve(workspace, P);
+    const CountWs nw = count_ws_of(workspace, P);
+    unsigned* table = w.keys_a;  // P + 64 words: room for the +inf tail
+    const int64_t ncnt = (2 * P + kCiTop + 16) < kCiCntWords ? (2 * P + kCiTop + 16) : kCiCntWords;
+    // the histogram aggregates 8 keys per thread in LDS; the count and scatter passes are chains of
+    // dependent loads per key, so they take one key per thread (every chain in flight at once)
+    const dim3 g8(static_cast<unsigned>((P + 256 * kDirectPerThread - 1) / (256 * kDirectPerThread)));
+    const dim3 g1(static_cast<unsigned>((P + 255) / 256));
+    hipLaunchKernelGGL(direct_hist_kernel, g8, dim3(256), 0, st, pos, P, nw.first, nw.cstart, ncnt);
+    hipLaunchKernelGGL(direct_plan_kernel, dim3(1), dim3(kCiPlanThreads), 0, st, P, nw.first, nw.l1, nw.meta);
+    hipLaunchKernelGGL(direct_count_kernel, g1, dim3(256), 0, st, pos, P, nw.l1, nw.meta, nw.cstart, w.keys_b);
+    hipLaunchKernelGGL(direct_blocks_kernel, dim3((kCiMaxBlocks + 255) / 256), dim3(256), 0, st, nw.cstart, nw.meta,
+                       nw.blk);
+    hipLaunchKernelGGL(direct_scan_kernel, dim3(1), dim3(kCiPlanThreads), 0, st, nw.meta, nw.blk);
+    hipLaunchKernelGGL(direct_scatter_kernel, g1, dim3(256), 0, st, pos, P, nw.l1, nw.blk, nw.meta, nw.cstart,
+                       w.keys_b, table);
+    int rc = launch_status();
+    if (rc || end == begin) return rc;
+    switch (label_dtype) {
+        case DAUC_LABEL_I8:
+            return launch_ci(scores, static_cast<const int8_t*>(labels), begin, end, nw, table, P, wins_ties, nonfinite,
+                             st, verdict);
+        case DAUC_LABEL_I32:
+            return launch_ci(scores, static_cast<const int32_t*>(labels), begin, end, nw, table, P, wins_ties,
+                             nonfinite, st, verdict);
+        default:
+            return launch_ci(scores, static_cast<const int64_t*>(labels), begin, end, nw, table, P, wins_ties,
+                             nonfinite, st, verdict);
+    }
+}
+
 }  // namespace dauc
 
 using namespace dauc;
@@ -2139,10 +2379,8 @@ int dauc_auc_counts_sorted_labeled(const float* pos, int64_t P, const float* sco
     const int mode = g_search_mode;
     const bool slot_cells = mode == 2 && P <= int64_t(kMaxCells) * kCellMuForced;
     const bool count = mode == 0 && 2 * P <= 3 * int64_t(kCiMaxCells);
-    char* after_tree = static_cast<char*>(workspace) + ((sort_ws_bytes(P) + 255) / 256) * 256 +
-                       ((kTreeBytes + 255) / 256) * 256;
-    const CellWs cw = carve_cells(after_tree);
-    const CountWs nw = carve_count(after_tree + ((kCellBytes + 255) / 256) * 256);
+    const CellWs cw = carve_cells(after_tree_of(workspace, P));
+    const CountWs nw = count_ws_of(workspace, P);
     int rc = prepare_table(pos, P, workspace, st, &sorted, &tree, &k, &g, count ? nw.first : nullptr);
     if (rc) return rc;
     if (slot_cells && (rc = prepare_cells(sorted, P, cw, kCellMuForced, st))) return rc;

@@ -97,9 +97,21 @@ __device__ __forceinline__ bool arrive_last(unsigned* counter, unsigned nblocks,
     return *lds_flag != 0;
 }
 
-// auc_count.hip: dauc_compact_positives that also zeroes zero3[0..3) (used by auc_eval.hip)
+// auc_count.hip: dauc_compact_positives that also zeroes zero3[0..3) and zero_w[0..nzero_w)
+// (used by auc_eval.hip)
 int compact_positives_zeroing(const float* scores, const void* labels, int label_dtype, int64_t n, float* pos_out,
                               int64_t* stats, void* workspace, size_t workspace_bytes, unsigned long long* zero3,
-                              hipStream_t st);
+                              hipStream_t st, unsigned* zero_w = nullptr, int nzero_w = 0);
+
+// auc_sort.hip: the count index built straight from the unsorted positives (no radix sort, no
+// tree) and the labeled query pass over scores [begin, end); the table is ordered by cell only.
+// `hist` (kCiTop words, direct_hist_words()) must be zero on entry. *verdict (device) = 1 when
+// the count index was usable, 2 when the caller must re-run the sorted path (skewed table).
+int64_t direct_hist_offset(int64_t P);  // byte offset of `hist` in the sort workspace
+int direct_hist_words();
+bool direct_fits(int64_t P);  // the search mode is automatic (0) and the count index can hold P keys
+int counts_labeled_direct(const float* pos, int64_t P, const float* scores, const void* labels, int label_dtype,
+                          int64_t begin, int64_t end, unsigned long long* wins_ties, unsigned long long* nonfinite,
+                          unsigned* verdict, void* workspace, size_t workspace_bytes, hipStream_t st);
 
 }  // namespace dauc

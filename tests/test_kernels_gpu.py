@@ -478,6 +478,25 @@ def test_auc_eval_counts_one_call(dev, ldtype):
         W, Tt, P, N, bad, other = ops.auc_eval_counts(T(s, dev), T(y, dev))
         e = coracle.auc_counts(y.astype(np.int64), s)
         assert (W, Tt, P, N, bad) == (e["wins"], e["ties"], e["P"], e["N"], 0), k
+    # the direct count-index build (no sort) and its fallback to the sorted path: tie-heavy and
+    # clustered positive tables (a cell of 15+ keys, too many keys per cell) alternate with
+    # spread ones of the same length, so the speculative size hits and misses on both paths
+    n = 200_003
+    base = rng.random(n, dtype=np.float32)
+    yb = np.where(rng.random(n) < 0.03, 1, -1).astype(ldtype)
+    skew = {
+        "spread": base,
+        "all_equal": np.where(yb == 1, np.float32(0.25), base).astype(np.float32),
+        "ten_levels": np.where(yb == 1, np.floor(base * 10) / 10, base).astype(np.float32),
+        "cluster": np.where(yb == 1, np.float32(0.5) + base * np.float32(1e-6), base).astype(np.float32),
+        "neg_zero": np.where(yb == 1, np.float32(-0.0), np.where(base < 0.5, np.float32(0.0), base)).astype(np.float32),
+    }
+    for name in ("spread", "all_equal", "all_equal", "spread", "spread", "ten_levels", "cluster", "spread",
+                 "neg_zero", "spread"):
+        s = skew[name]
+        W, Tt, P, N, bad, other = ops.auc_eval_counts(T(s, dev), T(yb, dev))
+        e = coracle.auc_counts(yb.astype(np.int64), s)
+        assert (W, Tt, P, N, bad) == (e["wins"], e["ties"], e["P"], e["N"], 0), name
     for where in ("pos", "neg"):
         for p in (0.01, 0.99):  # both table sides
             n = 100_003
