@@ -1374,6 +1374,33 @@ __device__ __forceinline__ bool count_index_in_use(const unsigned* __restrict__ 
     return meta[kCiOk] != 0u && meta[kCiSkew] == 0u;
 }
 
+// the direct build (below): workgroup size, and groups of 256 block words whose prefixes the
+// consumers add (group_prefix)
+constexpr int kDirectThreads = 256;
+constexpr int kDirectGroup = 256;
+constexpr int kDirectMaxGroups = (kCiMaxBlocks + kDirectGroup - 1) / kDirectGroup;  // 72
+static_assert(kDirectMaxGroups <= 2 * kWave, "group_prefix handles up to 128 groups");
+
+// wave 0 of the calling workgroup: pre[g] = sum of grp[0 .. g) for g < kDirectMaxGroups
+// (groups >= ng count nothing)
+__device__ __forceinline__ void group_prefix(const unsigned* __restrict__ grp, int ng, unsigned* pre) {
+    if (threadIdx.x >= kWave) return;
+    const int lane = threadIdx.x;
+    const unsigned v0 = lane < ng ? grp[lane] : 0u, v1 = lane + kWave < ng ? grp[lane + kWave] : 0u;
+    unsigned i0 = v0, i1 = v1;
+#pragma unroll
+    for (int off = 1; off < kWave; off <<= 1) {
+        const unsigned t0 = __shfl_up(i0, off, kWave), t1 = __shfl_up(i1, off, kWave);
+        if (lane >= off) {
+            i0 += t0;
+            i1 += t1;
+        }
+    }
+    const unsigned tot0 = __shfl(i0, kWave - 1, kWave);
+    if (lane < kDirectMaxGroups) pre[lane] = i0 - v0;
+    if (lane + kWave < kDirectMaxGroups) pre[lane + kWave] = tot0 + i1 - v1;
+}
+
 // first[t] = the first table index of top bucket t, for the buckets holding keys (first[] was set
 // to M by build_tree_kernel)
 __global__ __launch_bounds__(256) void ci_first_kernel(const unsigned* __restrict__ sorted, int64_t M,
@@ -1579,7 +1606,8 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
                                                                 const unsigned* __restrict__ sorted, int64_t M,
                                                                 unsigned long long* __restrict__ out,
                                                                 unsigned long long* __restrict__ nonfinite,
-                                                                unsigned* __restrict__ verdict) {
+                                                                unsigned* __restrict__ verdict,
+                                                                const unsigned* __restrict__ grp) {
     const bool in_use = count_index_in_use(meta);
     if (verdict != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *verdict = in_use ? 1u : 2u;
     if (!in_use) return;
@@ -1588,7 +1616,18 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
     uint2* l1 = ci_lds;          // [2048]
     uint2* blk = ci_lds + kCiTop;  // [nb]
     for (int i = threadIdx.x; i < kCiTop; i += kQueryThreads) l1[i] = l1g[i];
-    for (int i = threadIdx.x; i < nb; i += kQueryThreads) blk[i] = blkg[i];
+    if (grp != nullptr) {
+        // the direct build's block words hold prefixes within groups of 256 blocks: add the groups'
+        unsigned* pre = reinterpret_cast<unsigned*>(blk + kCiMaxBlocks);
+        group_prefix(grp, (nb + kDirectGroup - 1) / kDirectGroup, pre);
+        __syncthreads();
+        for (int i = threadIdx.x; i < nb; i += kQueryThreads) {
+            const uint2 v = blkg[i];
+            blk[i] = uint2{v.x + pre[i / kDirectGroup], v.y};
+        }
+    } else {
+        for (int i = threadIdx.x; i < nb; i += kQueryThreads) blk[i] = blkg[i];
+    }
     __syncthreads();
     const unsigned M32 = static_cast<unsigned>(M);
     unsigned long long w = 0, t = 0;
@@ -1727,147 +1766,135 @@ __global__ __launch_bounds__(256) void direct_hist_kernel(const float* __restric
         if (h[i]) atomicAdd(hist + i, h[i]);
 }
 
-// One workgroup, the plan of ci_plan_kernel from the bucket sizes themselves: C_t = ceil(n_t *
-// num / M) cells per used bucket, num = min(cells left after one per used bucket, 2 M), the
-// first cell of every bucket (ascending), and the verdict words
-__global__ __launch_bounds__(kCiPlanThreads) void direct_plan_kernel(int64_t M, const unsigned* __restrict__ hist,
-                                                                     uint2* __restrict__ l1,
-                                                                     unsigned* __restrict__ meta) {
-    static_assert(kCiTop == 2 * kCiPlanThreads, "two top buckets per thread");
-    __shared__ unsigned wtot[kCiPlanThreads / kWave];
+// The plan of ci_plan_kernel from the bucket sizes themselves, computed by EVERY workgroup of the
+// count pass in LDS (2048 buckets, 8 per thread: cheaper than a one-workgroup launch between the
+// histogram and the counts): C_t = ceil(n_t * num / M) cells per used bucket, num = min(cells left
+// after one per used bucket, 2 M), the first cell of every bucket (ascending). Workgroup 0 also
+// writes the plan and the verdict words for the later passes. Then the per-cell key counts (a wave
+// whose keys all fall in one cell adds once: tie-heavy tables) and every key's cell.
+
+__global__ __launch_bounds__(kDirectThreads) void direct_count_kernel(const float* __restrict__ pos, int64_t M,
+                                                                      const unsigned* __restrict__ hist,
+                                                                      uint2* __restrict__ l1g,
+                                                                      unsigned* __restrict__ meta,
+                                                                      unsigned* __restrict__ cnt,
+                                                                      unsigned* __restrict__ cell) {
+    static_assert(kCiTop == 8 * kDirectThreads, "eight top buckets per thread");
+    __shared__ uint2 l1[kCiTop];
+    __shared__ unsigned wtot[kDirectThreads / kWave];
     __shared__ unsigned totals[2];
-    const uint2 n = reinterpret_cast<const uint2*>(hist)[threadIdx.x];  // buckets 2i, 2i + 1
-    const unsigned used = block_incl_scan1024<false>((n.x != 0u) + (n.y != 0u), wtot);
-    if (threadIdx.x == kCiPlanThreads - 1) totals[0] = used;
+    const uint4 h0 = reinterpret_cast<const uint4*>(hist)[2 * threadIdx.x];
+    const uint4 h1 = reinterpret_cast<const uint4*>(hist)[2 * threadIdx.x + 1];
+    const unsigned n[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+    unsigned used = 0u;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) used += n[j] != 0u;
+    used = block_incl_scan1024<false>(used, wtot);
+    if (threadIdx.x == kDirectThreads - 1) totals[0] = used;
     __syncthreads();
     const int64_t avail = int64_t(kCiMaxCells) - int64_t(totals[0]);
     const int64_t num = avail < 2 * M ? avail : 2 * M;
-    const unsigned c0 = n.x ? static_cast<unsigned>((int64_t(n.x) * num + M - 1) / M) : 0u;
-    const unsigned c1 = n.y ? static_cast<unsigned>((int64_t(n.y) * num + M - 1) / M) : 0u;
-    const unsigned incl = block_incl_scan1024<false>(c0 + c1, wtot);
-    if (threadIdx.x == kCiPlanThreads - 1) totals[1] = incl;
+    unsigned C[8], csum = 0u;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        C[j] = n[j] ? static_cast<unsigned>((int64_t(n[j]) * num + M - 1) / M) : 0u;
+        csum += C[j];
+    }
+    const unsigned incl = block_incl_scan1024<false>(csum, wtot);
+    if (threadIdx.x == kDirectThreads - 1) totals[1] = incl;
+    unsigned run = incl - csum;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        l1[8 * threadIdx.x + j] = uint2{run, C[j]};
+        run += C[j];
+    }
     __syncthreads();
-    const unsigned excl = incl - c0 - c1, total = totals[1];
-    reinterpret_cast<uint4*>(l1)[threadIdx.x] = uint4{excl, c0, excl + c0, c1};
-    if (threadIdx.x == 0) {
-        meta[kCiOk] = (num > 0 && 3 * num >= 2 * M && total <= static_cast<unsigned>(kCiMaxCells)) ? 1u : 0u;
-        meta[kCiCells] = total;
-        meta[kCiBlocks] = (total + 1 + kCiBlock - 1) / kCiBlock;
-        meta[kCiSkew] = 0u;
+    const unsigned total = totals[1];
+    const bool ok = num > 0 && 3 * num >= 2 * M && total <= static_cast<unsigned>(kCiMaxCells);
+    if (blockIdx.x == 0) {
+        for (int t = threadIdx.x; t < kCiTop; t += kDirectThreads) l1g[t] = l1[t];
+        if (threadIdx.x == 0) {
+            meta[kCiOk] = ok ? 1u : 0u;
+            meta[kCiCells] = total;
+            meta[kCiBlocks] = (total + 1 + kCiBlock - 1) / kCiBlock;
+            meta[kCiSkew] = 0u;
+        }
     }
-}
-
-// per-cell key counts (a wave whose keys all fall in one cell adds once: tie-heavy tables)
-__global__ __launch_bounds__(256) void direct_count_kernel(const float* __restrict__ pos, int64_t M,
-                                                           const uint2* __restrict__ l1,
-                                                           const unsigned* __restrict__ meta,
-                                                           unsigned* __restrict__ cnt, unsigned* __restrict__ cell) {
-    if (meta[kCiOk] == 0u) return;
-    const int64_t gid = int64_t(blockIdx.x) * 256 + threadIdx.x, stride = int64_t(gridDim.x) * 256;
+    if (!ok) return;
     const int lane = threadIdx.x & (kWave - 1);
-    for (int64_t i0 = gid - lane; i0 < M; i0 += stride) {  // wave-uniform trip count
-        const int64_t i = i0 + lane;
-        const bool live = i < M;
-        unsigned c = 0u;
-        if (live) {
-            const unsigned x = key_fast(pos[i]);
-            c = ci_cell(x, l1[x >> kCiLowBits]);
-            cell[i] = c;  // the scatter's cell, so it does not walk pos -> key -> l1 again
-        }
-        const unsigned long long act = __ballot(live);
-        const int first = __ffsll(static_cast<long long>(act)) - 1;
-        const unsigned cf = __shfl(c, first, kWave);
-        if (__ballot(live && c == cf) == act) {
-            if (lane == first) atomicAdd(cnt + cf, static_cast<unsigned>(__popcll(act)));
-        } else if (live) {
-            atomicAdd(cnt + c, 1u);
-        }
+    const int64_t i = int64_t(blockIdx.x) * kDirectThreads + threadIdx.x;
+    const bool live = i < M;
+    unsigned c = 0u;
+    if (live) {
+        const unsigned x = key_fast(pos[i]);
+        c = ci_cell(x, l1[x >> kCiLowBits]);
+        cell[i] = c;  // the scatter's cell, so it does not walk pos -> key -> plan again
+    }
+    const unsigned long long act = __ballot(live);
+    if (act == 0ull) return;
+    const int first = __ffsll(static_cast<long long>(act)) - 1;
+    const unsigned cf = __shfl(c, first, kWave);
+    if (__ballot(live && c == cf) == act) {
+        if (lane == first) atomicAdd(cnt + cf, static_cast<unsigned>(__popcll(act)));
+    } else if (live) {
+        atomicAdd(cnt + c, 1u);
     }
 }
 
-// One thread per block of 8 cells: {the block's key count, the cells' counts as nibbles}; a count
-// of 15 or more marks the table skewed. The block counts become prefixes in direct_scan_kernel.
-__global__ __launch_bounds__(256) void direct_blocks_kernel(const unsigned* __restrict__ cnt,
-                                                            unsigned* __restrict__ meta, uint2* __restrict__ blk) {
+// One thread per block of 8 cells, one workgroup per group of 256 blocks: blk[b] = {the table
+// keys before block b within its group, the 8 cells' counts as nibbles}, grp[g] = the group's
+// keys; a count of 15 or more marks the table skewed. The consumers add the groups' prefix
+// (group_prefix), so no one-workgroup scan launch sits between this pass and the scatter.
+__global__ __launch_bounds__(kDirectGroup) void direct_blocks_kernel(const unsigned* __restrict__ cnt,
+                                                                     unsigned* __restrict__ meta,
+                                                                     uint2* __restrict__ blk,
+                                                                     unsigned* __restrict__ grp) {
     if (meta[kCiOk] == 0u) return;
-    const int b = blockIdx.x * 256 + threadIdx.x;
+    __shared__ unsigned wtot[kDirectGroup / kWave];
+    const int b = blockIdx.x * kDirectGroup + threadIdx.x;
+    const bool live = b < static_cast<int>(meta[kCiBlocks]);
     bool skew = false;
-    if (b < static_cast<int>(meta[kCiBlocks])) {
+    unsigned w = 0u, sum = 0u;
+    if (live) {
         const uint4 lo = reinterpret_cast<const uint4*>(cnt)[2 * b], hi = reinterpret_cast<const uint4*>(cnt)[2 * b + 1];
         const unsigned c[kCiBlock] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
-        unsigned w = 0u, sum = 0u;
 #pragma unroll
         for (int j = 0; j < kCiBlock; ++j) {
             skew |= c[j] >= 15u;
             w |= (c[j] < 15u ? c[j] : 15u) << (4 * j);
             sum += c[j];
         }
-        blk[b] = uint2{sum, w};
     }
+    const unsigned incl = block_incl_scan1024<false>(sum, wtot);
+    if (live) blk[b] = uint2{incl - sum, w};
+    if (threadIdx.x == kDirectGroup - 1) grp[blockIdx.x] = incl;
     if (__ballot(skew) != 0ull && (threadIdx.x & (kWave - 1)) == 0) atomicOr(meta + kCiSkew, 1u);
-}
-
-// One workgroup: blk[b].x = the table keys before block b (exclusive prefix of the block counts);
-// the counts are staged through LDS so the global reads and writes stay coalesced while every
-// thread scans a contiguous run of blocks
-__global__ __launch_bounds__(kCiPlanThreads) void direct_scan_kernel(const unsigned* __restrict__ meta,
-                                                                     uint2* __restrict__ blk) {
-    if (meta[kCiOk] == 0u || meta[kCiSkew] != 0u) return;
-    constexpr int kPer = (kCiMaxBlocks + kCiPlanThreads - 1) / kCiPlanThreads;  // 18
-    __shared__ unsigned wtot[kCiPlanThreads / kWave];
-    __shared__ unsigned xs[kPer * kCiPlanThreads];
-    const int nb = static_cast<int>(meta[kCiBlocks]);
-    {
-        unsigned v[kPer];  // every load in flight before the first LDS store
-#pragma unroll
-        for (int j = 0; j < kPer; ++j) {
-            const int i = j * kCiPlanThreads + threadIdx.x;
-            v[j] = i < nb ? blk[i].x : 0u;
-        }
-#pragma unroll
-        for (int j = 0; j < kPer; ++j) xs[j * kCiPlanThreads + threadIdx.x] = v[j];
-    }
-    __syncthreads();
-    const int b0 = threadIdx.x * kPer;
-    unsigned sum = 0u;
-#pragma unroll
-    for (int j = 0; j < kPer; ++j) sum += xs[b0 + j];
-    unsigned run = block_incl_scan1024<false>(sum, wtot) - sum;
-#pragma unroll
-    for (int j = 0; j < kPer; ++j) {
-        const unsigned v = xs[b0 + j];
-        xs[b0 + j] = run;
-        run += v;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < kPer; ++j) {
-        const int i = j * kCiPlanThreads + threadIdx.x;
-        if (i < nb) blk[i].x = xs[i];
-    }
 }
 
 // every key into its cell's range of the table (the counters are counted back down to zero);
 // the table's tail is padded with +inf keys for the 16-byte windows
-__global__ __launch_bounds__(256) void direct_scatter_kernel(const float* __restrict__ pos, int64_t M,
-                                                             const uint2* __restrict__ l1,
-                                                             const uint2* __restrict__ blk,
-                                                             const unsigned* __restrict__ meta,
-                                                             unsigned* __restrict__ cnt,
-                                                             const unsigned* __restrict__ cell,
-                                                             unsigned* __restrict__ table) {
+__global__ __launch_bounds__(kDirectThreads) void direct_scatter_kernel(const float* __restrict__ pos, int64_t M,
+                                                                        const uint2* __restrict__ blk,
+                                                                        const unsigned* __restrict__ grp,
+                                                                        const unsigned* __restrict__ meta,
+                                                                        unsigned* __restrict__ cnt,
+                                                                        const unsigned* __restrict__ cell,
+                                                                        unsigned* __restrict__ table) {
     if (meta[kCiOk] == 0u || meta[kCiSkew] != 0u) return;
-    const int64_t gid = int64_t(blockIdx.x) * 256 + threadIdx.x, stride = int64_t(gridDim.x) * 256;
-    if (gid < 16) table[M + gid] = kPadKey;
-    for (int64_t i = gid; i < M; i += stride) {
-        const unsigned x = key_fast(pos[i]);
-        const unsigned c = cell[i];
-        const uint2 b = blk[c / kCiBlock];
-        const unsigned below = __builtin_amdgcn_ubfe(b.y, 0u, 4u * (c % kCiBlock));
-        const unsigned bytes = (below & 0x0f0f0f0fu) + ((below >> 4) & 0x0f0f0f0fu);
-        const unsigned slot = atomicSub(cnt + c, 1u) - 1u;
-        table[b.x + __builtin_amdgcn_sad_u8(bytes, 0u, 0u) + slot] = x;
-    }
+    __shared__ unsigned pre[kDirectMaxGroups];
+    group_prefix(grp, (static_cast<int>(meta[kCiBlocks]) + kDirectGroup - 1) / kDirectGroup, pre);
+    __syncthreads();
+    const int64_t i = int64_t(blockIdx.x) * kDirectThreads + threadIdx.x;
+    if (i < 16) table[M + i] = kPadKey;
+    if (i >= M) return;
+    const unsigned x = key_fast(pos[i]);
+    const unsigned c = cell[i];
+    const unsigned bi = c / kCiBlock;
+    const uint2 b = blk[bi];
+    const unsigned below = __builtin_amdgcn_ubfe(b.y, 0u, 4u * (c % kCiBlock));
+    const unsigned bytes = (below & 0x0f0f0f0fu) + ((below >> 4) & 0x0f0f0f0fu);
+    const unsigned slot = atomicSub(cnt + c, 1u) - 1u;
+    table[pre[bi / kDirectGroup] + b.x + __builtin_amdgcn_sad_u8(bytes, 0u, 0u) + slot] = x;
 }
 
 // Every queried score is also checked to be finite (sklearn rejects NaN / inf scores,
@@ -2192,11 +2219,11 @@ int prepare_count(const unsigned* sorted, int64_t M, const CountWs& cw, hipStrea
 template <typename LT>
 int launch_ci(const float* s, const LT* lab, int64_t begin, int64_t end, const CountWs& cw, const unsigned* sorted,
               int64_t M, unsigned long long* out, unsigned long long* nonfinite, hipStream_t st,
-              unsigned* verdict = nullptr) {
+              unsigned* verdict = nullptr, const unsigned* grp = nullptr) {
     const dim3 grid(query_grid(end - begin)), block(kQueryThreads);
-    const size_t lds = (size_t(kCiTop) + kCiMaxBlocks) * 8;
+    const size_t lds = (size_t(kCiTop) + kCiMaxBlocks) * 8 + (grp ? size_t(kDirectMaxGroups) * 4 : 0);
     hipLaunchKernelGGL((query_ci_kernel<LT>), grid, block, lds, st, s, lab, begin, end, cw.meta, cw.l1, cw.blk, sorted,
-                       M, out, nonfinite, verdict);
+                       M, out, nonfinite, verdict, grp);
     return launch_status();
 }
 
@@ -2281,28 +2308,28 @@ int counts_labeled_direct(const float* pos, int64_t P, const float* scores, cons
     const int64_t ncnt = (2 * P + kCiTop + 16) < kCiCntWords ? (2 * P + kCiTop + 16) : kCiCntWords;
     // the histogram aggregates 8 keys per thread in LDS; the count and scatter passes are chains of
     // dependent loads per key, so they take one key per thread (every chain in flight at once)
+    unsigned* grp = carve_cells(after_tree_of(workspace, P)).l1;  // the slot-cell index is unused here
     const dim3 g8(static_cast<unsigned>((P + 256 * kDirectPerThread - 1) / (256 * kDirectPerThread)));
-    const dim3 g1(static_cast<unsigned>((P + 255) / 256));
+    const dim3 g1(static_cast<unsigned>((P + kDirectThreads - 1) / kDirectThreads));
     hipLaunchKernelGGL(direct_hist_kernel, g8, dim3(256), 0, st, pos, P, nw.first, nw.cstart, ncnt);
-    hipLaunchKernelGGL(direct_plan_kernel, dim3(1), dim3(kCiPlanThreads), 0, st, P, nw.first, nw.l1, nw.meta);
-    hipLaunchKernelGGL(direct_count_kernel, g1, dim3(256), 0, st, pos, P, nw.l1, nw.meta, nw.cstart, w.keys_b);
-    hipLaunchKernelGGL(direct_blocks_kernel, dim3((kCiMaxBlocks + 255) / 256), dim3(256), 0, st, nw.cstart, nw.meta,
-                       nw.blk);
-    hipLaunchKernelGGL(direct_scan_kernel, dim3(1), dim3(kCiPlanThreads), 0, st, nw.meta, nw.blk);
-    hipLaunchKernelGGL(direct_scatter_kernel, g1, dim3(256), 0, st, pos, P, nw.l1, nw.blk, nw.meta, nw.cstart,
-                       w.keys_b, table);
+    hipLaunchKernelGGL(direct_count_kernel, g1, dim3(kDirectThreads), 0, st, pos, P, nw.first, nw.l1, nw.meta,
+                       nw.cstart, w.keys_b);
+    hipLaunchKernelGGL(direct_blocks_kernel, dim3(kDirectMaxGroups), dim3(kDirectGroup), 0, st, nw.cstart, nw.meta,
+                       nw.blk, grp);
+    hipLaunchKernelGGL(direct_scatter_kernel, g1, dim3(kDirectThreads), 0, st, pos, P, nw.blk, grp, nw.meta,
+                       nw.cstart, w.keys_b, table);
     int rc = launch_status();
     if (rc || end == begin) return rc;
     switch (label_dtype) {
         case DAUC_LABEL_I8:
             return launch_ci(scores, static_cast<const int8_t*>(labels), begin, end, nw, table, P, wins_ties, nonfinite,
-                             st, verdict);
+                             st, verdict, grp);
         case DAUC_LABEL_I32:
             return launch_ci(scores, static_cast<const int32_t*>(labels), begin, end, nw, table, P, wins_ties,
-                             nonfinite, st, verdict);
+                             nonfinite, st, verdict, grp);
         default:
             return launch_ci(scores, static_cast<const int64_t*>(labels), begin, end, nw, table, P, wins_ties,
-                             nonfinite, st, verdict);
+                             nonfinite, st, verdict, grp);
     }
 }
 
