@@ -386,11 +386,11 @@ def auc_record(auc, world, config_name):
                     "positive blocks, int64 all-reduce",
         "sort_mode": sk["mode"],
         "pairs_per_sec": npairs / sk["t_eval"],
-        "method": "sort (default evaluator: compact the positives reading labels only, radix-sort them, locate "
-                  "every negative, read in place, through the LDS count index (the LDS search tree for tables it "
-                  "does not fit or finds skewed); on one GPU one blocking C call that "
-                  "sizes the sort by the previous call's P for this length and re-runs it if P differs, so a "
-                  "repeated test set costs one readback)",
+        "method": "sort (default evaluator: compact the positives reading labels only, build the LDS count index "
+                  "straight from them (cell-ordered table, no sort; the radix sort + LDS search tree for tables it "
+                  "does not fit or finds skewed), locate every negative, read in place, through it; one blocking C "
+                  "call per rank that sizes the build by the previous call's P for this length and re-runs it if P "
+                  "differs, so a repeated test set costs one readback)",
         "eval_ms": sk["t_eval"] * 1e3, "sort_count_ms": sk["t_count"] * 1e3,
         "sort_count_what": f"HIP events around every {sk['count_fn']} call"
                            + (" (the whole one-call evaluation: compaction, sort, query, readback)"
