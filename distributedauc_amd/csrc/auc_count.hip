@@ -18,6 +18,8 @@
 
 #include <math.h>
 
+#include <type_traits>
+
 #include "dauc_internal.h"
 
 namespace dauc {
@@ -478,6 +480,79 @@ __global__ __launch_bounds__(kCmpThreads) void compact_write_kernel(
     }
 }
 
+// The one-call evaluation's compaction, in ONE pass and without order: the positives' scores are
+// only ever counted against (the direct count-index build scatters them into cells by atomics
+// anyway), so a tile reserves its range of pos_out with one returning atomic instead of waiting
+// for the earlier tiles' counts (no mask pass, no second launch). stats[0] (positives, the
+// reservation counter), stats[2] (non-finite positives) and stats[3] (labels outside {-1, 1})
+// must be zero on entry; stats[1] is not written (N = n - P). Block 0 zeroes `zero_next` (the
+// next call's stats) and the first `nzero_w` words of `zero_w`, and zero3[0..3).
+// SLOTS groups of 16 labels per thread: 8 (a 32768-label tile) for small inputs; 32 (131072) for
+// large ones, where the reservation atomics of 4096 tiles on one address serialise (2^27 labels:
+// 65 us at 8 slots).
+template <typename LT, int SLOTS>
+__global__ __launch_bounds__(kCmpThreads) void compact_unordered_kernel(
+    const float* __restrict__ s, const LT* __restrict__ lab, int64_t n, int vec, float* __restrict__ pos_out,
+    unsigned long long* __restrict__ stats, unsigned long long* __restrict__ zero_next,
+    unsigned long long* __restrict__ zero3, unsigned* __restrict__ zero_w, int nzero_w) {
+    constexpr int kW = kCmpThreads / kWave;
+    constexpr int64_t kTileU = int64_t(kCmpThreads) * 16 * SLOTS;
+    __shared__ int wtot[2][kW];
+    __shared__ unsigned long long base_s;
+    if (blockIdx.x == 0) {
+        if (threadIdx.x < 4) zero_next[threadIdx.x] = 0ull;
+        else if (threadIdx.x < 7 && zero3 != nullptr) zero3[threadIdx.x - 4] = 0ull;
+        for (int i = threadIdx.x; i < nzero_w; i += kCmpThreads) zero_w[i] = 0u;
+    }
+    const int64_t base = int64_t(blockIdx.x) * kTileU;
+    int no = 0;
+    unsigned m[SLOTS];
+#pragma unroll
+    for (int k = 0; k < SLOTS; ++k)
+        m[k] = label_masks16(lab, base + (int64_t(k) * kCmpThreads + threadIdx.x) * 16, n, vec, no);
+    int np = 0;
+#pragma unroll
+    for (int k = 0; k < SLOTS; ++k) np += __popc(m[k]);
+    const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+    int incl = np;  // inclusive scan of the positives over the wave's lanes
+#pragma unroll
+    for (int off = 1; off < kWave; off <<= 1) {
+        const int v = __shfl_up(incl, off, kWave);
+        if (lane >= off) incl += v;
+    }
+    for (int off = 32; off > 0; off >>= 1) no += __shfl_xor(no, off, kWave);
+    if (lane == kWave - 1) wtot[0][wid] = incl;
+    if (lane == 0) wtot[1][wid] = no;
+    __syncthreads();
+    int before = 0, tile = 0;
+#pragma unroll
+    for (int w = 0; w < kW; ++w) {
+        before += w < wid ? wtot[0][w] : 0;
+        tile += wtot[0][w];
+    }
+    if (threadIdx.x == 0) {
+        int other = 0;
+#pragma unroll
+        for (int w = 0; w < kW; ++w) other += wtot[1][w];
+        if (other) atomicAdd(stats + 3, static_cast<unsigned long long>(other));
+        base_s = tile ? atomicAdd(stats + 0, static_cast<unsigned long long>(tile)) : 0ull;
+    }
+    __syncthreads();
+    if (tile == 0) return;
+    int64_t r = int64_t(base_s) + before + incl - np;
+    int nf = 0;
+#pragma unroll
+    for (int k = 0; k < SLOTS; ++k) {
+        const int64_t i = base + (int64_t(k) * kCmpThreads + threadIdx.x) * 16;
+        for (unsigned b = m[k]; b != 0u; b &= b - 1u) {
+            const float v = s[i + __ffs(b) - 1];
+            nf += !isfinite(v);
+            pos_out[r++] = v;
+        }
+    }
+    if (nf) atomicAdd(stats + 2, static_cast<unsigned long long>(nf));
+}
+
 template <typename LT>
 int launch_compact(const float* s, const LT* lab, int64_t n, float* pos_out, int64_t* stats, void* ws,
                    hipStream_t st, unsigned long long* zero3 = nullptr, unsigned* zero_w = nullptr,
@@ -740,6 +815,35 @@ int compact_positives_zeroing(const float* scores, const void* labels, int label
                                   zero_w, nzero_w);
         default:
             return DAUC_EINVAL;
+    }
+}
+int compact_unordered(const float* scores, const void* labels, int label_dtype, int64_t n, float* pos_out,
+                      unsigned long long* stats, unsigned long long* zero_next, unsigned long long* zero3,
+                      unsigned* zero_w, int nzero_w, hipStream_t st) {
+    if (n <= 0 || scores == nullptr || labels == nullptr || pos_out == nullptr || stats == nullptr ||
+        zero_next == nullptr)
+        return DAUC_EINVAL;
+    const bool wide = n >= (int64_t(1) << 25);
+    const int64_t tile = int64_t(kCmpThreads) * 16 * (wide ? 32 : kCmpSlots);
+    const int64_t nblk = (n + tile - 1) / tile;
+    if (nblk > 0x7fffffffLL) return DAUC_EINVAL;
+    const int vec = (reinterpret_cast<uintptr_t>(labels) & 15u) == 0;
+    const dim3 grid(static_cast<unsigned>(nblk)), block(kCmpThreads);
+    auto go = [&](auto* lab) {
+        using LT = std::remove_const_t<std::remove_pointer_t<decltype(lab)>>;
+        if (wide)
+            hipLaunchKernelGGL((compact_unordered_kernel<LT, 32>), grid, block, 0, st, scores, lab, n, vec, pos_out,
+                               stats, zero_next, zero3, zero_w, nzero_w);
+        else
+            hipLaunchKernelGGL((compact_unordered_kernel<LT, kCmpSlots>), grid, block, 0, st, scores, lab, n, vec,
+                               pos_out, stats, zero_next, zero3, zero_w, nzero_w);
+        return launch_status();
+    };
+    switch (label_dtype) {
+        case DAUC_LABEL_I8: return go(static_cast<const int8_t*>(labels));
+        case DAUC_LABEL_I32: return go(static_cast<const int32_t*>(labels));
+        case DAUC_LABEL_I64: return go(static_cast<const int64_t*>(labels));
+        default: return DAUC_EINVAL;
     }
 }
 }  // namespace dauc

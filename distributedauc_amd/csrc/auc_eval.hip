@@ -76,6 +76,21 @@ EvalMemo& eval_memo() {
     return m;
 }
 
+// The compaction's counters alternate between two 32-byte slots of the workspace header: a call
+// uses slot epoch & 1 and its compaction zeroes the other one for the next call, so no memset
+// launch precedes the compaction; a workspace seen for the first time is zeroed once.
+struct EvalRing {
+    const void* ws;
+    unsigned epoch;
+};
+
+EvalRing& eval_ring() {
+    static thread_local EvalRing r{nullptr, 0};
+    return r;
+}
+
+constexpr size_t kRingOffset = 128;  // header bytes [128, 192): two slots of 4 counters
+
 size_t eval_ws_bytes(int64_t n) {
     return 256 + align256(size_t(n) * 4) + align256(size_t(n / 2 + 1) * 4) + align256(dauc_compact_workspace_size(n)) +
            align256(dauc_split_workspace_size(n)) + align256(dauc_sort_workspace_size(n / 2 + 1));
@@ -118,9 +133,10 @@ int eval_counts_part(const float* scores, const void* labels, int label_dtype, i
     hipError_t e;
     // the direct build's verdict word (1 = the count index was usable, 2 = re-run sorted)
     unsigned* verdict = reinterpret_cast<unsigned*>(w.wt + 3);
-    // stats [0, 32), the counts [64, 88) and the verdict [88, 92) come back in one copy
+    // the split's stats [0, 32), the counts [64, 88), the verdict [88, 92) and the compaction's
+    // counter slots [128, 192) come back in one copy
     auto readback = [&]() -> int {
-        if ((e = hipMemcpyAsync(host, w.stats, 96, hipMemcpyDeviceToHost, st)) != hipSuccess ||
+        if ((e = hipMemcpyAsync(host, w.stats, 192, hipMemcpyDeviceToHost, st)) != hipSuccess ||
             (e = hipStreamSynchronize(st)) != hipSuccess)
             return -static_cast<int>(e);
         return DAUC_OK;
@@ -149,17 +165,29 @@ int eval_counts_part(const float* scores, const void* labels, int label_dtype, i
     bool direct_ok = same ? memo.direct_ok : true;
     const bool speculate = same && memo.P > 0 && memo.P <= n - memo.P;
     const bool spec_direct = speculate && direct_ok && direct_fits(memo.P);
-    // the compaction's first launch also zeroes the query's counters (and the direct build's
-    // top-bucket histogram)
-    int rc = compact_positives_zeroing(
-        scores, labels, label_dtype, n, w.pos, w.stats, w.cws, w.cws_bytes, w.wt, st,
+    // the one-pass compaction (positives in no particular order: everything after it counts) also
+    // zeroes the query's counters, the next call's counter slot and the direct build's histogram
+    EvalRing& ring = eval_ring();
+    auto* slots = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(w.stats) + kRingOffset);
+    if (ring.ws != workspace) {
+        if ((e = hipMemsetAsync(slots, 0, 64, st)) != hipSuccess) return -static_cast<int>(e);
+        ring = EvalRing{workspace, 0u};
+    }
+    const unsigned slot = ring.epoch & 1u;
+    int rc = compact_unordered(
+        scores, labels, label_dtype, n, w.pos, slots + 4 * slot, slots + 4 * (slot ^ 1u), w.wt,
         spec_direct ? reinterpret_cast<unsigned*>(static_cast<char*>(w.tws) + direct_hist_offset(memo.P)) : nullptr,
-        spec_direct ? direct_hist_words() : 0);
-    if (rc) return rc;
+        spec_direct ? direct_hist_words() : 0, st);
+    if (rc) {
+        ring.ws = nullptr;  // the slots' state is unknown: zero them again next time
+        return rc;
+    }
+    ++ring.epoch;
     if (speculate && (rc = spec_direct ? direct(memo.P) : query(memo.P))) return rc;
     if ((rc = readback())) return rc;
-    int64_t P = host[0], N = host[1], nonfinite = host[2];
-    const int64_t other = host[3];
+    const int64_t* cst = host + (kRingOffset / 8) + 4 * slot;
+    int64_t P = cst[0], N = n - cst[0], nonfinite = cst[2];
+    const int64_t other = cst[3];
     bool counted = false;
     if (speculate && P == memo.P) {
         if (!spec_direct || direct_verdict_ok()) counted = true;
