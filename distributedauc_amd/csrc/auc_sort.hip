@@ -1615,18 +1615,34 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
     const int nb = static_cast<int>(meta[kCiBlocks]);
     uint2* l1 = ci_lds;          // [2048]
     uint2* blk = ci_lds + kCiTop;  // [nb]
-    for (int i = threadIdx.x; i < kCiTop; i += kQueryThreads) l1[i] = l1g[i];
-    if (grp != nullptr) {
-        // the direct build's block words hold prefixes within groups of 256 blocks: add the groups'
-        unsigned* pre = reinterpret_cast<unsigned*>(blk + kCiMaxBlocks);
-        group_prefix(grp, (nb + kDirectGroup - 1) / kDirectGroup, pre);
-        __syncthreads();
-        for (int i = threadIdx.x; i < nb; i += kQueryThreads) {
-            const uint2 v = blkg[i];
-            blk[i] = uint2{v.x + pre[i / kDirectGroup], v.y};
+    {
+        // the index into LDS with every load of a thread in flight before its first LDS store (a
+        // load-store loop waits out one L2 round trip per iteration: 18 of them per thread)
+        constexpr int kL1Per = kCiTop / kQueryThreads;                                 // 2
+        constexpr int kBlkPer = (kCiMaxBlocks + kQueryThreads - 1) / kQueryThreads;  // 18
+        uint2 a[kL1Per], v[kBlkPer];
+#pragma unroll
+        for (int j = 0; j < kL1Per; ++j) a[j] = l1g[j * kQueryThreads + threadIdx.x];
+#pragma unroll
+        for (int j = 0; j < kBlkPer; ++j) {
+            const int i = j * kQueryThreads + threadIdx.x;
+            v[j] = i < nb ? blkg[i] : uint2{0u, 0u};
         }
-    } else {
-        for (int i = threadIdx.x; i < nb; i += kQueryThreads) blk[i] = blkg[i];
+        if (grp != nullptr) {
+            // the direct build's block words hold prefixes within groups of 256 blocks: add the groups'
+            unsigned* pre = reinterpret_cast<unsigned*>(blk + kCiMaxBlocks);
+            group_prefix(grp, (nb + kDirectGroup - 1) / kDirectGroup, pre);
+            __syncthreads();
+#pragma unroll
+            for (int j = 0; j < kBlkPer; ++j) v[j].x += pre[(j * kQueryThreads + threadIdx.x) / kDirectGroup];
+        }
+#pragma unroll
+        for (int j = 0; j < kL1Per; ++j) l1[j * kQueryThreads + threadIdx.x] = a[j];
+#pragma unroll
+        for (int j = 0; j < kBlkPer; ++j) {
+            const int i = j * kQueryThreads + threadIdx.x;
+            if (i < nb) blk[i] = v[j];
+        }
     }
     __syncthreads();
     const unsigned M32 = static_cast<unsigned>(M);
