@@ -379,11 +379,11 @@ def auc_record(auc, world, config_name):
     npairs = auc["npairs"]
     pc_rate = npairs / pk["t_count"]
     n = auc["n"]
-    # the sort method's HBM floor: labels read twice by the compaction (every rank compacts the
-    # whole vector), scores + labels once by the query pass over the rank's share (the positives'
-    # scores and the sorted table are ~0.1-1 % of that)
+    # the sort method's HBM floor: labels read once by the one-pass compaction (every rank
+    # compacts the whole vector), scores + labels once by the query pass over the rank's share (the
+    # positives' scores and the count index are ~0.1-1 % of that)
     shard = world if sk["mode"] == "sharded" else 1
-    eval_bytes = n * 2 * 1 + n * (4 + 1) // shard
+    eval_bytes = n * 1 + n * (4 + 1) // shard
     return {
         "workload": f"exact AUC, 2^{auc['log2n']} fp32 scores, {auc['pos']:.1%} positives "
                     f"(BASELINE {config_name}), {world} rank(s); sort method {sk['mode']} "
@@ -405,7 +405,7 @@ def auc_record(auc, world, config_name):
         "eval_roofline": {"bound": "hbm", "bytes_per_rank": eval_bytes,
                           "achieved": eval_bytes / sk["t_eval"] / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                           "frac": eval_bytes / sk["t_eval"] / 1e9 / HBM_PEAK_GBS,
-                          "note": "bytes = 2 label passes over all n + 1 score/label pass over this rank's query share"},
+                          "note": "bytes = 1 label pass over all n + 1 score/label pass over this rank's query share"},
         "query_kernel": load_profile("query_valu.json", f"2^{auc['log2n']}"),
         "P": auc["P"], "N": auc["N"], "wins": auc["wins"], "ties": auc["ties"], "auc": auc["auc"],
         "methods_agree": True,
