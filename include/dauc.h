@@ -298,9 +298,11 @@ int dauc_auc_counts_sorted_labeled(const float* pos, int64_t P, const float* sco
 
 /*
  * The whole single-GPU exact-AUC evaluation of main.py:79-81 in ONE blocking call (sklearn's
- * roc_curve + auc is a blocking host call too): positive compaction, a readback of the class
- * sizes, the radix sort of the smaller class, the tree and the query pass, a readback of the
- * counts. Same integers as the stage-by-stage calls it chains. The exception to the
+ * roc_curve + auc is a blocking host call too): a one-pass positive compaction, the count index
+ * built straight from the (unsorted) positives and the query pass, a readback of the class sizes
+ * and the counts; a table the count index cannot hold (skewed, or more than 219,838 positives)
+ * runs the stable compaction, the radix sort, the tree and the query pass instead. Same
+ * integers as the stage-by-stage calls. The exception to the
  * conventions above: it synchronises `stream` and keeps one small pinned host buffer per
  * calling thread, allocated on first use. The table size is known only after the compaction;
  * when the calling thread's previous call had the same n and label type, its P is used to
