@@ -28,7 +28,7 @@ import torch.nn as nn
 
 from . import ops
 from .flat import FlatState
-from .surrogate import auc_surrogate, auc_surrogate_logits
+from .surrogate import auc_surrogate, auc_surrogate_logits, unit_seed
 
 
 class CoDA:
@@ -159,7 +159,7 @@ class CoDA:
             loss = auc_surrogate_logits(self.forward(x), y8, st.abalpha, st.p_hat, st.grad3)
         else:
             loss = auc_surrogate(self.scores(x), y8, st.abalpha, st.p_hat, st.grad3)
-        loss.backward()
+        loss.backward(unit_seed(loss.device))  # no ones_like fill, no dF/dh * 1 pass
         st.update(self.lr, self.gamma, self.mode)
         self.model.zero_grad(set_to_none=True)
         return loss.detach()

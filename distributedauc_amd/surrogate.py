@@ -13,6 +13,23 @@ import torch
 
 from . import ops
 
+_UNIT: dict = {}  # device -> 0-dim fp32 tensor 1.0, never written (the backward seed of a training step)
+
+
+def unit_seed(device: torch.device) -> torch.Tensor:
+    """The gradient seed ``loss.backward(unit_seed(loss.device))`` passes instead of a fresh
+    ``ones_like(loss)``: the surrogate's backward recognises it by its storage and hands its
+    stored dF/dh on without the ``* grad_out`` pass (the same bits: x * 1.0 == x)."""
+    t = _UNIT.get(device)
+    if t is None:
+        t = _UNIT[device] = torch.ones((), dtype=torch.float32, device=device)
+    return t
+
+
+def _is_unit(grad_out: torch.Tensor) -> bool:
+    t = _UNIT.get(grad_out.device)
+    return t is not None and grad_out.dim() == 0 and grad_out.data_ptr() == t.data_ptr()
+
 
 class AUCSurrogate(torch.autograd.Function):
     """F(h; a, b, alpha, p) with dF/dh, dF/da, dF/db, dF/dalpha from one kernel pass."""
@@ -30,8 +47,9 @@ class AUCSurrogate(torch.autograd.Function):
     @staticmethod
     def backward(ctx, grad_out):
         dh, g3 = ctx.saved_tensors
-        d_ab = g3 * grad_out if ctx.abalpha_grad else None
-        return dh * grad_out, None, d_ab, None, None
+        unit = _is_unit(grad_out)
+        d_ab = (g3 if unit else g3 * grad_out) if ctx.abalpha_grad else None
+        return dh if unit else dh * grad_out, None, d_ab, None, None
 
 
 def auc_surrogate(h: torch.Tensor, y: torch.Tensor, abalpha: torch.Tensor, p_hat: torch.Tensor,
@@ -64,8 +82,9 @@ class AUCSurrogateLogits(torch.autograd.Function):
     @staticmethod
     def backward(ctx, grad_out):
         dz, g3 = ctx.saved_tensors
-        d_ab = g3 * grad_out if ctx.abalpha_grad else None
-        return dz * grad_out.to(dz.dtype), None, d_ab, None, None
+        unit = _is_unit(grad_out)
+        d_ab = (g3 if unit else g3 * grad_out) if ctx.abalpha_grad else None
+        return dz if unit else dz * grad_out.to(dz.dtype), None, d_ab, None, None
 
 
 def auc_surrogate_logits(z: torch.Tensor, y: torch.Tensor, abalpha: torch.Tensor, p_hat: torch.Tensor,
