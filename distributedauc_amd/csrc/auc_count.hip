@@ -493,17 +493,22 @@ __global__ __launch_bounds__(kCmpThreads) void compact_write_kernel(
 template <typename LT, int SLOTS>
 __global__ __launch_bounds__(kCmpThreads) void compact_unordered_kernel(
     const float* __restrict__ s, const LT* __restrict__ lab, int64_t n, int vec, float* __restrict__ pos_out,
-    unsigned long long* __restrict__ stats, unsigned long long* __restrict__ zero_next,
-    unsigned long long* __restrict__ zero3, unsigned* __restrict__ zero_w, int nzero_w) {
+    unsigned long long* __restrict__ stats, unsigned long long tag, unsigned long long* __restrict__ zero_next,
+    unsigned long long next_tag, unsigned long long* __restrict__ zero3, unsigned* __restrict__ zero_w,
+    int nzero_w) {
     constexpr int kW = kCmpThreads / kWave;
     constexpr int64_t kTileU = int64_t(kCmpThreads) * 16 * SLOTS;
     __shared__ int wtot[2][kW];
     __shared__ unsigned long long base_s;
     if (blockIdx.x == 0) {
-        if (threadIdx.x < 4) zero_next[threadIdx.x] = 0ull;
+        if (threadIdx.x < 4) zero_next[threadIdx.x] = threadIdx.x == 1 ? next_tag : 0ull;
         else if (threadIdx.x < 7 && zero3 != nullptr) zero3[threadIdx.x - 4] = 0ull;
         for (int i = threadIdx.x; i < nzero_w; i += kCmpThreads) zero_w[i] = 0u;
     }
+    // the slot's tag (written with the zeroes by the previous call): a workspace whose slot was
+    // not left by this thread's previous call holds stale counters, so no tile reserves from it
+    // (the caller sees the tag and starts over with zeroed slots)
+    const unsigned long long seen = stats[1];
     const int64_t base = int64_t(blockIdx.x) * kTileU;
     int no = 0;
     unsigned m[SLOTS];
@@ -530,6 +535,7 @@ __global__ __launch_bounds__(kCmpThreads) void compact_unordered_kernel(
         before += w < wid ? wtot[0][w] : 0;
         tile += wtot[0][w];
     }
+    if (seen != tag) return;  // uniform across the workgroup
     if (threadIdx.x == 0) {
         int other = 0;
 #pragma unroll
@@ -818,8 +824,9 @@ int compact_positives_zeroing(const float* scores, const void* labels, int label
     }
 }
 int compact_unordered(const float* scores, const void* labels, int label_dtype, int64_t n, float* pos_out,
-                      unsigned long long* stats, unsigned long long* zero_next, unsigned long long* zero3,
-                      unsigned* zero_w, int nzero_w, hipStream_t st) {
+                      unsigned long long* stats, unsigned long long tag, unsigned long long* zero_next,
+                      unsigned long long next_tag, unsigned long long* zero3, unsigned* zero_w, int nzero_w,
+                      hipStream_t st) {
     if (n <= 0 || scores == nullptr || labels == nullptr || pos_out == nullptr || stats == nullptr ||
         zero_next == nullptr)
         return DAUC_EINVAL;
@@ -833,10 +840,10 @@ int compact_unordered(const float* scores, const void* labels, int label_dtype, 
         using LT = std::remove_const_t<std::remove_pointer_t<decltype(lab)>>;
         if (wide)
             hipLaunchKernelGGL((compact_unordered_kernel<LT, 32>), grid, block, 0, st, scores, lab, n, vec, pos_out,
-                               stats, zero_next, zero3, zero_w, nzero_w);
+                               stats, tag, zero_next, next_tag, zero3, zero_w, nzero_w);
         else
             hipLaunchKernelGGL((compact_unordered_kernel<LT, kCmpSlots>), grid, block, 0, st, scores, lab, n, vec,
-                               pos_out, stats, zero_next, zero3, zero_w, nzero_w);
+                               pos_out, stats, tag, zero_next, next_tag, zero3, zero_w, nzero_w);
         return launch_status();
     };
     switch (label_dtype) {

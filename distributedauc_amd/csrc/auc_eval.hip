@@ -91,6 +91,12 @@ EvalRing& eval_ring() {
 
 constexpr size_t kRingOffset = 128;  // header bytes [128, 192): two slots of 4 counters
 
+// slot word 1: the epoch that may use the slot (0 after the first-use memset). A workspace
+// pointer this thread saw before but whose contents changed since (freed and reallocated at the
+// same address) shows a different tag: the compaction then writes nothing and the call starts
+// over with zeroed slots.
+inline unsigned long long slot_tag(unsigned epoch) { return epoch ? (0xDA0C000000000000ull | epoch) : 0ull; }
+
 size_t eval_ws_bytes(int64_t n) {
     return 256 + align256(size_t(n) * 4) + align256(size_t(n / 2 + 1) * 4) + align256(dauc_compact_workspace_size(n)) +
            align256(dauc_split_workspace_size(n)) + align256(dauc_sort_workspace_size(n / 2 + 1));
@@ -119,7 +125,7 @@ namespace {
 //              #non-finite queried scores of this part }
 int eval_counts_part(const float* scores, const void* labels, int label_dtype, int64_t n, int part, int parts,
                      int64_t* out, int64_t* part_counts, void* workspace, size_t workspace_bytes,
-                     dauc_stream_t stream) {
+                     dauc_stream_t stream, bool retry = false) {
     if (n <= 0 || scores == nullptr || labels == nullptr || out == nullptr || workspace == nullptr ||
         workspace_bytes < eval_ws_bytes(n) || (reinterpret_cast<uintptr_t>(workspace) & 255u))
         return DAUC_EINVAL;
@@ -173,9 +179,10 @@ int eval_counts_part(const float* scores, const void* labels, int label_dtype, i
         if ((e = hipMemsetAsync(slots, 0, 64, st)) != hipSuccess) return -static_cast<int>(e);
         ring = EvalRing{workspace, 0u};
     }
-    const unsigned slot = ring.epoch & 1u;
+    const unsigned slot = ring.epoch & 1u, epoch = ring.epoch;
     int rc = compact_unordered(
-        scores, labels, label_dtype, n, w.pos, slots + 4 * slot, slots + 4 * (slot ^ 1u), w.wt,
+        scores, labels, label_dtype, n, w.pos, slots + 4 * slot, slot_tag(epoch), slots + 4 * (slot ^ 1u),
+        slot_tag(epoch + 1), w.wt,
         spec_direct ? reinterpret_cast<unsigned*>(static_cast<char*>(w.tws) + direct_hist_offset(memo.P)) : nullptr,
         spec_direct ? direct_hist_words() : 0, st);
     if (rc) {
@@ -186,6 +193,13 @@ int eval_counts_part(const float* scores, const void* labels, int label_dtype, i
     if (speculate && (rc = spec_direct ? direct(memo.P) : query(memo.P))) return rc;
     if ((rc = readback())) return rc;
     const int64_t* cst = host + (kRingOffset / 8) + 4 * slot;
+    if (static_cast<unsigned long long>(cst[1]) != slot_tag(epoch)) {
+        // stale slots (see slot_tag): nothing was compacted; zero them and start over, once
+        ring.ws = nullptr;
+        if (retry) return DAUC_EINVAL;
+        return eval_counts_part(scores, labels, label_dtype, n, part, parts, out, part_counts, workspace,
+                                workspace_bytes, stream, true);
+    }
     int64_t P = cst[0], N = n - cst[0], nonfinite = cst[2];
     const int64_t other = cst[3];
     bool counted = false;

@@ -104,11 +104,14 @@ int compact_positives_zeroing(const float* scores, const void* labels, int label
                               hipStream_t st, unsigned* zero_w = nullptr, int nzero_w = 0);
 
 // auc_count.hip: the one-call evaluation's single-pass, unordered positive compaction. stats[0]
-// (P), stats[2] (non-finite positives), stats[3] (labels outside {-1, 1}) must be zero on entry;
-// block 0 zeroes zero_next[0..4), zero3[0..3) (nullable) and zero_w[0..nzero_w).
+// (P), stats[2] (non-finite positives), stats[3] (labels outside {-1, 1}) must be zero on entry
+// and stats[1] must hold `tag` (else no tile reserves or writes anything); block 0 zeroes
+// zero_next[0, 2, 3], sets zero_next[1] = next_tag, and zeroes zero3[0..3) (nullable) and
+// zero_w[0..nzero_w).
 int compact_unordered(const float* scores, const void* labels, int label_dtype, int64_t n, float* pos_out,
-                      unsigned long long* stats, unsigned long long* zero_next, unsigned long long* zero3,
-                      unsigned* zero_w, int nzero_w, hipStream_t st);
+                      unsigned long long* stats, unsigned long long tag, unsigned long long* zero_next,
+                      unsigned long long next_tag, unsigned long long* zero3, unsigned* zero_w, int nzero_w,
+                      hipStream_t st);
 
 // auc_sort.hip: the count index built straight from the unsorted positives (no radix sort, no
 // tree) and the labeled query pass over scores [begin, end); the table is ordered by cell only.

@@ -508,6 +508,31 @@ def test_auc_eval_counts_one_call(dev, ldtype):
             assert bad >= 1, (where, p)
 
 
+def test_auc_eval_counts_stale_workspace(dev):
+    """The one-call evaluation keeps its compaction counters in the workspace between calls on a
+    thread; a workspace whose contents changed since (here: overwritten with garbage, as a
+    freed-and-reallocated buffer at the same address would be) must be detected by the slot tag
+    and the call must still return the C oracle's counts (and never write out of bounds)."""
+    from distributedauc_amd import _lib, ops
+
+    rng = np.random.default_rng(12)
+    n = 300_001
+    s = rng.random(n, dtype=np.float32)
+    y = np.where(rng.random(n) < 0.02, 1, -1).astype(np.int8)
+    e = coracle.auc_counts(y.astype(np.int64), s)
+    st, sy = T(s, dev), T(y, dev)
+    want = (e["wins"], e["ties"], e["P"], e["N"], 0, 0)
+    assert ops.auc_eval_counts(st, sy) == want
+    ws = ops.workspaces.get(dev, "auc_eval", _lib.load().dauc_auc_eval_workspace_size(n),
+                            torch.cuda.current_stream(dev).cuda_stream)
+    for fill in (0xAB, 0x00, 0xFF):
+        assert ops.auc_eval_counts(st, sy) == want
+        ws.fill_(fill)
+        assert ops.auc_eval_counts(st, sy) == want, fill
+        assert ops.auc_eval_counts(st, sy) == want, fill
+    torch.cuda.synchronize()
+
+
 def test_auc_eval_counts_part(dev):
     """dauc_auc_eval_counts_part (the sharded evaluation's per-rank call): for G = 1, 2, 3, 8 the
     parts' (W, T) sum to the C oracle's on both table sides (P < N: score ranges; P > N: positive
