@@ -311,7 +311,10 @@ int dauc_auc_counts_sorted_labeled(const float* pos, int64_t P, const float* sco
  * re-run at the real size (2 synchronisations; 3 when P > N).
  *   out[6] (HOST int64) = { W, T, P, N, #non-finite scores, #labels not in {-1, 1} }
  *   (W = T = 0 when a class is empty or a score is non-finite: the caller raises like sklearn)
- * workspace >= dauc_auc_eval_workspace_size(n) bytes, 256-byte aligned; no zeroing needed.
+ * workspace >= dauc_auc_eval_workspace_size(n) bytes, 256-byte aligned; no zeroing needed. The
+ * call keeps the compaction's counters in the workspace between calls of one thread, tagged
+ * with the call's epoch: a workspace that changed in between (or is new to the thread) is
+ * detected and the call starts over with fresh counters, so any buffer may be passed.
  */
 size_t dauc_auc_eval_workspace_size(int64_t n);
 int dauc_auc_eval_counts(const float* scores, const void* labels, int label_dtype, int64_t n, int64_t* out,
