@@ -77,6 +77,8 @@ def parse(argv=None):
     p.add_argument("--pool", type=int, default=4, help="distinct resident input batches cycled")
     p.add_argument("--sweep-I", default="1,8,16,32", help="configs[2] averaging periods ('' = off)")
     p.add_argument("--sweep-steps", type=int, default=32, help="timed steps per period (a multiple of every I)")
+    p.add_argument("--eval-images", type=int, default=8192,
+                   help="in-training evaluation leg: test images scored with rank 0's model (0 = off)")
     p.add_argument("--r18-steps", type=int, default=16, help="configs[0] GPU leg: timed ResNet-18 b32 steps (0 = off)")
     p.add_argument("--r18-graph", type=int, default=1,
                    help="configs[0] GPU leg at N=1: replay the step body as a HIP graph (1/0); N>1 runs eager "
@@ -250,6 +252,8 @@ def bench_train(args, world, rank, device):
         out["period_sweep"] = bench_period_sweep(coda, it, args, world)
     if world > 1:
         out["coda_round"] = bench_coda_round(coda, world)
+    if args.eval_images > 0:
+        out["training_eval"] = bench_training_eval(coda, args, world, rank, device)
     del coda, it
     torch.cuda.empty_cache()
     return out
@@ -271,6 +275,51 @@ def bench_period_sweep(coda, it, args, world):
         log(f"rank {coda.rank}: period sweep I={I}: {recs[-1]['ms_per_step']:.2f} ms/step")
     coda.I = I0
     return recs
+
+
+def bench_training_eval(coda, args, world, rank, device, reps=3):
+    """The in-training evaluation (main.py:215-270): the test set scored with rank 0's model, then
+    the exact AUC. Split: every rank scores 1/world of the batches after a broadcast of rank 0's
+    parameters and BN statistics, all-gather of the scores, sharded count (main.Evaluator). At
+    world > 1 the reference's rank-0 scoring is timed beside it; both give the same AUC."""
+    from distributedauc_amd.loader import DeviceLoader, SyntheticImageNet, imagenet_like_labels
+    from distributedauc_amd.main import Evaluator
+
+    n = args.eval_images
+    tb = args.batch
+    labels = imagenet_like_labels(n, 1000, 499, pos_ratio=args.pos_ratio, seed=777)  # same on every rank
+    ds = SyntheticImageNet(labels, args.image_size, 499)
+    it = iter(DeviceLoader(ds, np.arange(n), tb, device, seed=777, shuffle=False, channels_last=True))
+    batches = [next(it) for _ in range((n + tb - 1) // tb)]
+
+    def timed(split):
+        ev = Evaluator(batches, n, 499, device, None, world, rank, None, split=split)
+        ev(coda)  # warm (workspaces, MIOpen eval-mode kernels)
+        ts, auc = [], None
+        for _ in range(reps):
+            if world > 1:
+                dist.barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            a = ev(coda)
+            torch.cuda.synchronize()
+            ts.append(time.perf_counter() - t0)
+            assert auc is None or a == auc
+            auc = a
+        return max_over_ranks(float(np.median(ts)), world), auc
+
+    ms_split, auc_split = timed(True)
+    rec = {"workload": f"{n} test images {args.image_size}^2 scored by {args.arch} (eval mode, bf16 autocast), "
+                       f"test batch {tb}, then the exact AUC; {world} rank(s)",
+           "ms": ms_split * 1e3, "imgs_per_sec": n / ms_split, "auc": auc_split,
+           "method": "split" if world > 1 else "one rank"}
+    if world > 1:
+        ms0, auc0 = timed(False)
+        if auc0 != auc_split:
+            raise RuntimeError(f"split scoring AUC {auc_split!r} != rank-0 scoring AUC {auc0!r}")
+        rec.update({"ms_rank0_scoring": ms0 * 1e3, "speedup_vs_rank0_scoring": ms0 / ms_split})
+    log(f"rank {rank}: in-training eval of {n} images {ms_split * 1e3:.1f} ms")
+    return rec
 
 
 def bench_coda_round(coda, world, reps=5):
@@ -332,14 +381,25 @@ def bench_auc(args, world, rank, device, log2n=None, pos=None, pair_reps=None):
     n = 1 << log2n
     s, y = synthetic_scores(n, pos, device)  # same scores on every rank
     out = {"n": n, "log2n": log2n, "pos": pos}
-    # the sort method is ONE blocking C call per rank: the whole evaluation on one GPU (or below
-    # SHARD_MIN) is dauc_auc_eval_counts; over ranks each runs dauc_auc_eval_counts_part for its
-    # share of the queries, then one int64 [3] all-reduce
+    # the sort method: the whole evaluation on one GPU (or below SHARD_MIN) is ONE blocking C call,
+    # dauc_auc_eval_counts; over ranks each enqueues its part with no host synchronisation
+    # (dauc_auc_eval_enqueue), then one all-gather of the 8-word records and one host read
     sort_fn = ("dauc_auc_eval_counts" if world == 1 or n < ExactAUC.SHARD_MIN
-               else "dauc_auc_eval_counts_part")
-    for method, fn in (("sort", sort_fn), ("pairs", "dauc_pair_count_variant")):
+               else "dauc_auc_eval_enqueue")
+    for method, fn in (("sort", sort_fn), ("pairs", "dauc_pair_count")):
         ev = ExactAUC(world=world, rank=rank, variant=args.variant, method=method)
         kt = KernelTimer(_lib.load(), fn)
+        cold = None
+        if method == "sort":
+            # the first call ever on this device and stream: the evaluator's workspace and the
+            # page-locked readback words are allocated inside it
+            torch.cuda.synchronize()
+            if world > 1:
+                dist.barrier()
+            t0 = time.perf_counter()
+            ev.counts(y, s)
+            torch.cuda.synchronize()
+            cold = max_over_ranks(time.perf_counter() - t0, world)
         c = ev.counts(y, s)  # warm-up
         reps = (args.auc_reps if pair_reps is None else pair_reps) if method == "pairs" else 5 * args.auc_reps
         # wall time without the event wrapper (its event creation and records are host work of
@@ -363,6 +423,24 @@ def bench_auc(args, world, rank, device, log2n=None, pos=None, pair_reps=None):
         out["m_" + method] = {"t_eval": max_over_ranks(float(np.median(times)), world),
                               "t_count": max_over_ranks(kt.mean_ms() / 1e3, world), "count_fn": fn, "counts": c,
                               "mode": ev.last_mode}
+        if method == "sort":
+            # another test set of the same length (other P) alternating with this one: the
+            # evaluation keeps no state between calls, so every call does the same work
+            g2 = torch.Generator(device=device).manual_seed(4242)
+            s2 = torch.rand(n, device=device, generator=g2)
+            y2 = torch.where(torch.rand(n, device=device, generator=g2) < pos * 1.1, 1, -1).to(torch.int8)
+            alt = []
+            for k in range(reps):
+                torch.cuda.synchronize()
+                if world > 1:
+                    dist.barrier()
+                t0 = time.perf_counter()
+                ev.counts(y2, s2) if k % 2 == 0 else ev.counts(y, s)
+                torch.cuda.synchronize()
+                alt.append(time.perf_counter() - t0)
+            out["m_sort"]["t_cold"] = cold
+            out["m_sort"]["t_alternating"] = max_over_ranks(float(np.median(alt)), world)
+            del s2, y2
         log(f"rank {rank}: auc 2^{log2n} {method} eval {out['m_' + method]['t_eval'] * 1e3:.2f} ms")
     a, b = out["m_sort"]["counts"], out["m_pairs"]["counts"]
     if (a["wins"], a["ties"]) != (b["wins"], b["ties"]):
@@ -387,21 +465,26 @@ def auc_record(auc, world, config_name):
     return {
         "workload": f"exact AUC, 2^{auc['log2n']} fp32 scores, {auc['pos']:.1%} positives "
                     f"(BASELINE {config_name}), {world} rank(s); sort method {sk['mode']} "
-                    "(sharded = every rank compacts and sorts all positives, queries its score-index range, int64 "
-                    "all-reduce; replicated = every rank evaluates the whole vector, below 2^24 scores); pair count: "
-                    "positive blocks, int64 all-reduce",
+                    "(sharded = every rank compacts all positives and builds the index itself, enqueues its "
+                    "score-index range with no host sync, one all-gather of the 8-word part records; replicated = "
+                    "every rank evaluates the whole vector, below 2^24 scores); pair count: positive blocks, int64 "
+                    "all-reduce",
         "sort_mode": sk["mode"],
         "pairs_per_sec": npairs / sk["t_eval"],
         "method": "sort (default evaluator: compact the positives reading labels only, build the LDS count index "
-                  "straight from them (cell-ordered table, no sort; the radix sort + LDS search tree for tables it "
-                  "does not fit or finds skewed), locate every negative, read in place, through it; one blocking C "
-                  "call per rank that sizes the build by the previous call's P for this length and re-runs it if P "
-                  "differs, so a repeated test set costs one readback)",
+                  "straight from them with the table size read on the device (cell-ordered table, no sort), locate "
+                  "every negative, read in place, through it -- all enqueued with no host sync; one readback per "
+                  "call; the radix sort + LDS search tree only for tables the index does not fit or finds skewed)",
         "eval_ms": sk["t_eval"] * 1e3, "sort_count_ms": sk["t_count"] * 1e3,
+        "eval_ms_cold": sk["t_cold"] * 1e3,
+        "eval_ms_cold_what": "the first call on this device/stream: workspace + page-locked readback words allocated",
+        "eval_ms_other_data": sk["t_alternating"] * 1e3,
+        "eval_ms_other_data_what": "median over calls alternating with another test set of the same length and a "
+                                   "different P (no state between calls: no speculation, no miss path)",
         "sort_count_what": f"HIP events around every {sk['count_fn']} call"
-                           + (" (the whole one-call evaluation: compaction, sort, query, readback)"
+                           + (" (the whole one-call evaluation: compaction, index build, query, readback)"
                               if sk["count_fn"] == "dauc_auc_eval_counts" else
-                              " (this rank's one-call part: compaction, sort, its query share, readback)"),
+                              " (this rank's enqueued part: compaction, index build, its query share, record copy)"),
         "eval_roofline": {"bound": "hbm", "bytes_per_rank": eval_bytes,
                           "achieved": eval_bytes / sk["t_eval"] / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                           "frac": eval_bytes / sk["t_eval"] / 1e9 / HBM_PEAK_GBS,
@@ -425,8 +508,9 @@ def bench_surrogate(args, device):
     """The fused loss kernel at a streaming size (9 B/element = fp32 h + int8 y + fp32 dh).
 
     Training batches (B = 256) are launch-latency bound; this leg measures the same kernel where
-    HBM bounds it. Inputs resident in HBM. Reported separately: the whole ABI call (streaming
-    kernel + the small row-reduce launch) and the streaming kernel alone (variant 15)."""
+    HBM bounds it. Inputs resident in HBM. Reported separately: the whole ABI call (ONE launch:
+    the stream and its row reduce), and from the tuning build the streaming kernel alone and the
+    same launch's stream without its reduce (include/dauc_tuning.h variants 3 and 4)."""
     from distributedauc_amd import _lib, ops
 
     B = 1 << args.sur_log2b
@@ -457,7 +541,10 @@ def bench_surrogate(args, device):
     #     launch stream (the average includes the gaps between calls, not per-call event packets)
     ms = b2b(0)
     loss = float(out64[0].item())
-    stream_ms = b2b(15)  # the streaming kernel alone (no row reduce)
+    # the tuning build's stream alone (variant 3: no hand-off, no reduce) and the one-launch
+    # kernel's stream with its tagged row stores but nobody reducing (variant 4)
+    stream_ms = b2b(3)
+    tail_stream_ms = b2b(4)
     # (2) an event pair around every call (each pair adds its own marker packets to the stream)
     kt = KernelTimer(_lib.load(), "dauc_surrogate_fwdbwd")
     kt.enabled = True
@@ -475,15 +562,18 @@ def bench_surrogate(args, device):
                       "call count (per_call_events_us: an event pair around every call instead)",
             "loss": loss,
             "roofline": {"kernel": "dauc_surrogate_fwdbwd (whole call)", "launches": "surrogate_tail_kernel: the stream "
-                         "and its fp64 row reduce (by the last 64 workgroups) in ONE launch",
+                         "and its fp64 row reduce (by the last 64 workgroups, epoch-tagged granules) in ONE launch",
                          "bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS, "traffic": load_traffic(f"surrogate_2^{args.sur_log2b}"),
                          "bytes_per_launch": nbytes},
-            "stream_kernel": {"kernel": "surrogate_chunk_kernel alone (variant 15: no row reduce, no scalars)",
+            "stream_kernel": {"kernel": "surrogate_chunk_kernel alone (tuning variant 3: no row reduce, no scalars)",
                               "avg_launch_us": stream_ms * 1e3, "bound": "hbm", "achieved": sgbs,
                               "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": sgbs / HBM_PEAK_GBS,
                               "bytes_per_launch": nbytes},
-            "row_reduce_us": (ms - stream_ms) * 1e3}
+            "tail_stream_us": tail_stream_ms * 1e3,
+            "tail_stream_what": "the one-launch kernel's stream with its tagged row stores, nobody reducing (variant 4)",
+            "row_reduce_us": (ms - tail_stream_ms) * 1e3,
+            "row_reduce_what": "whole call - variant 4: the in-launch hand-off chain after the last row lands"}
 
 
 # ----------------------------------------------------------------------------- CPU baselines
@@ -769,6 +859,8 @@ def main():
                                        "records": res["period_sweep"]}
             if "coda_round" in res:
                 out["coda_round"] = res["coda_round"]
+            if "training_eval" in res:
+                out["training_eval"] = res["training_eval"]
         out["process_group"] = {"world_size": dist.get_world_size() if world > 1 else 1,
                                 "backend": dist.get_backend() if world > 1 else None,
                                 "rccl_version": ".".join(map(str, torch.cuda.nccl.version()))

@@ -6,6 +6,7 @@ immediately; there is no CPU fallback anywhere in ``distributedauc_amd``.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import os
 import re
@@ -46,8 +47,6 @@ SIGNATURES = {
     "dauc_surrogate_workspace_size": (_sz, [_i64]),
     "dauc_surrogate_fwdbwd": (_int, [_vp, _i64, _vp, _int, _i64, _vp, _vp, _vp, _i64, _vp, _vp, _vp,
                                      _vp, _sz, _vp]),
-    "dauc_surrogate_fwdbwd_variant": (_int, [_vp, _i64, _vp, _int, _i64, _vp, _vp, _vp, _i64, _vp, _vp, _vp,
-                                             _vp, _sz, _int, _vp]),
     "dauc_class_sums": (_int, [_vp, _i64, _vp, _int, _i64, _vp, _int, _vp, _sz, _vp]),
     "dauc_alpha_from_sums": (_int, [_vp, _vp, _vp]),
     "dauc_surrogate_logits_fwdbwd": (_int, [_vp, _int, _i64, _vp, _int, _i64, _vp, _vp, _vp, _i64, _vp, _vp,
@@ -56,23 +55,21 @@ SIGNATURES = {
     "dauc_pd_update": (_int, [_vp, _vp, _vp, ctypes.POINTER(GradSeg), _int, _vp, _vp, _vp, _f32, _f32,
                               _int, _vp]),
     "dauc_pd_update_dense": (_int, [_vp, _vp, _vp, _vp, _i64, _f32, _f32, _vp]),
-    "dauc_pd_update_dense_variant": (_int, [_vp, _vp, _vp, _vp, _i64, _f32, _f32, _int, _vp]),
     "dauc_coda_finalize": (_int, [_vp, _i64, _int, _vp, _vp, _vp]),
     "dauc_scale_div": (_int, [_vp, _i64, _f32, _vp]),
     "dauc_split_workspace_size": (_sz, [_i64]),
     "dauc_split_scores": (_int, [_vp, _vp, _int, _i64, _vp, _vp, _vp, _vp, _sz, _vp]),
     "dauc_pair_count": (_int, [_vp, _i64, _vp, _i64, _vp, _vp]),
-    "dauc_pair_count_variant": (_int, [_vp, _i64, _vp, _i64, _vp, _int, _vp]),
     "dauc_sort_workspace_size": (_sz, [_i64]),
     "dauc_auc_counts_sorted": (_int, [_vp, _i64, _vp, _i64, _vp, _vp, _sz, _vp]),
     "dauc_auc_counts_sorted_labeled": (_int, [_vp, _i64, _vp, _vp, _int, _i64, _i64, _vp, _vp, _vp, _sz, _vp]),
     "dauc_compact_workspace_size": (_sz, [_i64]),
     "dauc_auc_eval_workspace_size": (_sz, [_i64]),
-    "dauc_auc_eval_counts": (_int, [_vp, _vp, _int, _i64, _vp, _vp, _sz, _vp]),
-    "dauc_auc_eval_counts_part": (_int, [_vp, _vp, _int, _i64, _int, _int, _vp, _vp, _vp, _sz, _vp]),
+    "dauc_auc_eval_enqueue": (_int, [_vp, _vp, _int, _i64, _int, _int, _vp, _vp, _sz, _vp]),
+    "dauc_auc_eval_counts": (_int, [_vp, _vp, _int, _i64, _vp, _vp, _vp, _sz, _vp]),
+    "dauc_auc_eval_counts_part": (_int, [_vp, _vp, _int, _i64, _int, _int, _vp, _vp, _vp, _vp, _sz, _vp]),
     "dauc_compact_positives": (_int, [_vp, _vp, _int, _i64, _vp, _vp, _vp, _sz, _vp]),
     "dauc_sort_keys": (_int, [_vp, _i64, _vp, _vp, _sz, _vp]),
-    "dauc_set_search_mode": (_int, [_int]),
     "dauc_bn_workspace_size": (_sz, [_i64, _int]),
     "dauc_bn_act_forward": (_int, [_vp, _int, _i64, _int, _vp, _int, _vp, _vp, _vp, _vp, _f32, _f32, _vp, _vp, _vp,
                                    _vp, _sz, _vp]),
@@ -85,7 +82,31 @@ SIGNATURES = {
                                        _vp]),
 }
 
+# tuning builds only (tuning/libdauc_tuning.so, -DDAUC_TUNING; include/dauc_tuning.h): measured
+# alternatives of the product kernels, selectable by number
+TUNING_SIGNATURES = {
+    "dauc_surrogate_fwdbwd_variant": (_int, [_vp, _i64, _vp, _int, _i64, _vp, _vp, _vp, _i64, _vp, _vp, _vp,
+                                             _vp, _sz, _int, _vp]),
+    "dauc_pd_update_dense_variant": (_int, [_vp, _vp, _vp, _vp, _i64, _f32, _f32, _int, _vp]),
+    "dauc_pair_count_variant": (_int, [_vp, _i64, _vp, _i64, _vp, _int, _vp]),
+    "dauc_set_search_mode": (_int, [_int]),
+}
+TUNING_LIB_PATH = Path(os.environ.get("DAUC_TUNING_LIB", PKG_DIR.parent / "tuning" / "libdauc_tuning.so"))
+
 _lib = None
+_tuning = None
+
+
+@contextlib.contextmanager
+def using(lib: ctypes.CDLL):
+    """Run the ops against another loaded build of the library (tests: the tuning build)."""
+    global _lib
+    prev = load()
+    _lib = lib
+    try:
+        yield lib
+    finally:
+        _lib = prev
 
 
 def header_functions(header: Path = HEADER) -> list[str]:
@@ -105,13 +126,36 @@ def load() -> ctypes.CDLL:
             "(python -c 'import __graft_entry__ as g; g.build()' or python distributedauc_amd/build.py). "
             "distributedauc_amd has no CPU fallback."
         )
-    lib = ctypes.CDLL(str(LIB_PATH))
+    _lib = _attach(ctypes.CDLL(str(LIB_PATH)))
+    return _lib
+
+
+def _attach(lib: ctypes.CDLL) -> ctypes.CDLL:
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    _lib = lib
+    for name, (res, args) in TUNING_SIGNATURES.items():
+        if hasattr(lib, name):
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
     return lib
+
+
+def tuning() -> ctypes.CDLL:
+    """The library that exports the tuning entry points: the loaded one if it is a tuning build
+    (DAUC_LIB), else tuning/libdauc_tuning.so (built by build.py next to the product library).
+    Tests and micro-benchmarks only; the product path never calls it."""
+    global _tuning
+    lib = load()
+    if all(hasattr(lib, n) for n in TUNING_SIGNATURES):
+        return lib
+    if _tuning is None:
+        if not TUNING_LIB_PATH.exists():
+            raise ImportError(f"{TUNING_LIB_PATH} not found: build it with python distributedauc_amd/build.py")
+        _tuning = _attach(ctypes.CDLL(str(TUNING_LIB_PATH)))
+    return _tuning
 
 
 def strerror(rc: int) -> str:

@@ -14,10 +14,13 @@ through an LDS search tree (O(M log M + L log M)).
 
 Sharding (north star): every rank holds the same score vector. The
 pair-count method gives rank r the positives [r*P/G, (r+1)*P/G) of the stable
-split against ALL negatives; the sort method has every rank compact and sort ALL
-the positives itself (a labels-only pass: no collective builds the table) and
-stream its index slice of the scores through the search. One int64 [3]
-all-reduce sums (W, T, non-finite); the result does not depend on G.
+split against ALL negatives, then one int64 [3] all-reduce sums (W, T, non-finite);
+the sort method has every rank compact ALL the positives and build the count index
+from them itself (a labels-only pass: no collective builds the table), stream its
+index slice of the scores through the search with no host synchronisation, and
+all-gather the parts' 8-word records (one collective, one host read). The result
+does not depend on G. Every rank must pass the same vector: the gathered records
+are checked for that, and a mismatch raises on every rank together.
 
 Error behaviour mirrors sklearn: non-finite scores raise ValueError; labels
 with more than two distinct values raise ValueError; a single class returns NaN
@@ -79,7 +82,7 @@ class ExactAUC:
         self.method = method
         self.shard_min = self.SHARD_MIN if shard_min is None else int(shard_min)
         self.last_mode = None  # "single", "replicated" or "sharded" (the last call's)
-        self._part_counts: dict = {}  # device -> int64 [3], the sharded sort method's all-reduce buffer
+        self._part_counts: dict = {}  # device -> int64 [8 (1 + world)]: this part's record + the gathered ones
 
     def counts(self, label, scores, device=None) -> dict:
         """Exact {wins, ties, P, N} (Python ints). One host sync for the split sizes."""
@@ -120,11 +123,13 @@ class ExactAUC:
 
     def _counts_sort(self, y: torch.Tensor, s: torch.Tensor) -> dict:
         """The sort method. One GPU (or a vector below ``shard_min``, which every rank evaluates
-        whole: same integers, no collective): ONE blocking C call. Over ranks: every rank runs the
-        same call for its part (dauc_auc_eval_counts_part) -- it compacts and sorts ALL the
-        positives itself (labels plus the positives' scores only; each rank holds the same scores,
-        so no collective builds the table) and streams its index slice of the scores through the
-        search -- then one int64 [3] all-reduce of (wins, ties, non-finite queried scores)."""
+        whole: same integers, no collective): ONE blocking C call (dauc_auc_eval_counts). Over
+        ranks: every rank enqueues its part (dauc_auc_eval_enqueue: it builds the table from ALL
+        the positives itself -- each rank holds the same scores -- and streams its index slice of
+        the scores through the search, with no host synchronisation), one all-gather of the
+        parts' 8-word records, and ONE host read of the gathered records: the counts are summed
+        on the host, and P, the non-finite / label checks and the verdict must agree on every rank
+        (ranks holding different vectors raise together instead of mixing counts)."""
         if self.world == 1 or (self.reduce and s.numel() < self.shard_min):
             self.last_mode = "single" if self.world == 1 else "replicated"
             W, T, P, N, nonfinite, other = ops.auc_eval_counts(s, y)
@@ -133,16 +138,39 @@ class ExactAUC:
             self._check_labels(other, y)
             return {"wins": W, "ties": T, "P": P, "N": N}
         self.last_mode = "sharded"
-        wt = self._part_counts.get(s.device)
-        if wt is None:
-            wt = self._part_counts[s.device] = torch.zeros(3, dtype=torch.int64, device=s.device)
-        W, T, P, N, nonfinite, other, qbad = ops.auc_eval_counts_part(s, y, self.rank, self.world, wt)
-        # P, N and the global checks are the same on every rank: all take the same branch
-        if nonfinite:
+        n = s.numel()
+        rec = self._part_counts.get(s.device)
+        if rec is None:
+            rec = self._part_counts[s.device] = torch.zeros(8 * (self.world + 1), dtype=torch.int64, device=s.device)
+        mine, gathered = rec[:8], rec[8:]
+        ops.auc_eval_enqueue(s, y, self.rank, self.world, out=mine)
+        if not self.reduce:
+            vals = [mine.tolist()]
+        else:
+            dist.all_gather_into_tensor(gathered, mine, group=self.group)
+            vals = gathered.view(self.world, 8).tolist()  # the one host synchronisation
+        shared = {(v[3], v[5], v[6]) for v in vals}
+        verdicts = {v[7] for v in vals} - {0}
+        if len(shared) != 1 or len(verdicts) > 1:
+            raise RuntimeError("ExactAUC: the ranks' parts disagree on the test set (positives, non-finite or "
+                               "label counts): every rank must pass the same scores and labels")
+        P, nonfinite, other = shared.pop()
+        N = n - P
+        if nonfinite or sum(v[2] for v in vals):
             raise ValueError("Input y_score contains NaN or infinity.")
         self._check_labels(other, y)
         if P == 0 or N == 0:
             return {"wins": 0, "ties": 0, "P": P, "N": N}
+        if verdicts == {2}:
+            return self._counts_sort_sorted_path(y, s)
+        return {"wins": sum(v[0] for v in vals), "ties": sum(v[1] for v in vals), "P": P, "N": N}
+
+    def _counts_sort_sorted_path(self, y: torch.Tensor, s: torch.Tensor) -> dict:
+        """A table the count index cannot hold (more than 219,838 positives, or clustered ones):
+        every rank runs the blocking part (the sorted path) and one int64 [3] all-reduce sums the
+        parts' counts. Every rank reached here with the same verdict, so all take this branch."""
+        wt = torch.zeros(3, dtype=torch.int64, device=s.device)
+        W, T, P, N, nonfinite, other, qbad = ops.auc_eval_counts_part(s, y, self.rank, self.world, wt)
         if self.reduce:
             dist.all_reduce(wt, op=dist.ReduceOp.SUM, group=self.group)
             W, T, qbad = (int(v) for v in wt.tolist())

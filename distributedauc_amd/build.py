@@ -18,6 +18,9 @@ REPO = PKG_DIR.parent
 CSRC = PKG_DIR / "csrc"
 OBJ_DIR = PKG_DIR / "build"
 LIB_PATH = PKG_DIR / "libdauc.so"
+# the tuning build: the same sources with -DDAUC_TUNING, which adds the measured alternatives'
+# entry points (include/dauc_tuning.h); tests and micro-benchmarks load it, the product never does
+TUNING_LIB_PATH = REPO / "tuning" / "libdauc_tuning.so"
 ARCH = os.environ.get("DAUC_OFFLOAD_ARCH", "gfx950")
 
 HIPCC = os.environ.get("HIPCC", shutil.which("hipcc") or "/opt/rocm/bin/hipcc")
@@ -41,11 +44,11 @@ def sources() -> list[Path]:
     return sorted(CSRC.glob("*.hip"))
 
 
-def _needs_build() -> bool:
-    if not LIB_PATH.exists():
+def _needs_build(target: Path = LIB_PATH) -> bool:
+    if not target.exists():
         return True
-    t = LIB_PATH.stat().st_mtime
-    deps = sources() + sorted(CSRC.glob("*.h")) + [REPO / "include" / "dauc.h", Path(__file__)]
+    t = target.stat().st_mtime
+    deps = sources() + sorted(CSRC.glob("*.h")) + sorted((REPO / "include").glob("*.h")) + [Path(__file__)]
     return any(p.stat().st_mtime > t for p in deps)
 
 
@@ -68,8 +71,11 @@ def build_library(force: bool = False, verbose: bool = False, out: Path | None =
     target = Path(out) if out is not None else LIB_PATH
     if out is None and not defines and not force and not _needs_build():
         return LIB_PATH
+    if target == TUNING_LIB_PATH and tuple(defines) == ("DAUC_TUNING",) and not force and not _needs_build(target):
+        return target
     obj_dir = OBJ_DIR if out is None else OBJ_DIR / target.stem
     obj_dir.mkdir(parents=True, exist_ok=True)
+    target.parent.mkdir(parents=True, exist_ok=True)
     srcs = sources()
     with cf.ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
         objs = list(ex.map(lambda s: _compile(s, obj_dir, tuple(defines)), srcs))
@@ -84,6 +90,11 @@ def build_library(force: bool = False, verbose: bool = False, out: Path | None =
     return target
 
 
+def build_tuning(force: bool = False, verbose: bool = False) -> Path:
+    """tuning/libdauc_tuning.so: the product sources with -DDAUC_TUNING."""
+    return build_library(force=force, verbose=verbose, out=TUNING_LIB_PATH, defines=("DAUC_TUNING",))
+
+
 if __name__ == "__main__":
     import argparse
 
@@ -91,5 +102,8 @@ if __name__ == "__main__":
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--out", default=None, help="write a tuning variant here instead of libdauc.so")
     ap.add_argument("-D", dest="defines", action="append", default=[])
+    ap.add_argument("--tuning", action="store_true", help="also build tuning/libdauc_tuning.so")
     a = ap.parse_args()
     build_library(force=a.force, verbose=True, out=a.out, defines=tuple(a.defines))
+    if a.tuning:
+        build_tuning(force=a.force, verbose=True)

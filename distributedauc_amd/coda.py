@@ -184,7 +184,8 @@ class CoDA:
         self._gx.copy_(x)
         self._gy.copy_(labels)
         self._graph.replay()
-        return self._gloss
+        # the graph's loss buffer is overwritten by the next replay: hand out a copy, as eager does
+        return self._gloss.clone()
 
     def _capture(self, x: torch.Tensor, labels: torch.Tensor, key) -> None:
         st = self.state

@@ -14,6 +14,7 @@ so autocast's cast-back kernel disappears too).
 """
 from __future__ import annotations
 
+import contextlib
 import os
 
 import torch
@@ -39,6 +40,11 @@ def _plan_key(key) -> str:
     return f"{M},{cin},{cout},{str(dtype).replace('torch.', '')},{direction}"
 
 
+def _arch() -> str:
+    """gcnArchName of the current device without its feature suffixes (e.g. "gfx950")."""
+    return torch.cuda.get_device_properties(torch.cuda.current_device()).gcnArchName.split(":")[0]
+
+
 def _load_plans() -> None:
     if not PLANS_FILE or not os.path.exists(PLANS_FILE):
         return
@@ -46,9 +52,13 @@ def _load_plans() -> None:
 
     dtypes = {"bfloat16": torch.bfloat16, "float16": torch.float16, "float32": torch.float32}
     with open(PLANS_FILE) as f:
-        for k, eng in json.load(f).get("plans", {}).items():
-            M, cin, cout, dt, direction = k.split(",")
-            plans.setdefault((int(M), int(cin), int(cout), dtypes[dt], direction), eng)
+        doc = json.load(f)
+    # the plan was measured on one GPU architecture: on any other the engines are timed again
+    if doc.get("arch") and torch.cuda.is_available() and doc["arch"] != _arch():
+        return
+    for k, eng in doc.get("plans", {}).items():
+        M, cin, cout, dt, direction = k.split(",")
+        plans.setdefault((int(M), int(cin), int(cout), dtypes[dt], direction), eng)
 
 
 def dump_plans(path: str) -> None:
@@ -57,6 +67,7 @@ def dump_plans(path: str) -> None:
 
     with open(path, "w") as f:
         json.dump({"device": torch.cuda.get_device_name(0) if torch.cuda.is_available() else None,
+                   "arch": _arch() if torch.cuda.is_available() else None,
                    "plans": {_plan_key(k): v for k, v in sorted(plans.items(), key=lambda kv: _plan_key(kv[0]))}},
                   f, indent=1)
 
@@ -77,13 +88,33 @@ def _timed(fn, reps=3):
 
 _FORCE = os.environ.get("DAUC_CONV1X1", "auto")  # auto | gemm | conv (fixed engine: reproducible runs)
 _loaded: list = []
+_fixed: list = []  # fixed_engine() stack
+
+
+@contextlib.contextmanager
+def fixed_engine(name: str = "gemm"):
+    """Inside: every 1x1 convolution runs on engine `name` (gemm | conv), untimed and ignoring the
+    plans. For results that must not depend on a timing: the split evaluation scores the test set
+    on every rank and needs the same bits as one rank scoring it all (main.Evaluator)."""
+    _fixed.append(name)
+    try:
+        yield
+    finally:
+        _fixed.pop()
 
 
 def _choose(key, candidates: dict):
+    if _fixed:
+        eng = next((n for n in candidates if n.startswith(_fixed[-1])), None)
+        if eng == "gemm8" and "gemm32" in candidates:
+            eng = "gemm32"
+        if eng is not None:
+            return eng
     if not _loaded:
         _load_plans()
         _loaded.append(True)
-    eng = plans.get(key)
+    # a forced engine (DAUC_CONV1X1=gemm|conv) wins over the shipped plan
+    eng = plans.get(key) if _FORCE == "auto" else None
     if eng is None and _FORCE != "auto":
         eng = next((n for n in candidates if n.startswith(_FORCE)), None)
         if eng == "gemm8" and "gemm32" in candidates:

@@ -864,13 +864,23 @@ int dauc_compact_positives(const float* scores, const void* labels, int label_dt
                                      nullptr, as_hip(stream));
 }
 
+static int pair_count_impl(const float* pos, int64_t P, const float* neg, int64_t N,
+                           unsigned long long* wins_ties, int variant, dauc_stream_t stream);
+
 int dauc_pair_count(const float* pos, int64_t P, const float* neg, int64_t N,
                     unsigned long long* wins_ties, dauc_stream_t stream) {
-    return dauc_pair_count_variant(pos, P, neg, N, wins_ties, 0, stream);
+    return pair_count_impl(pos, P, neg, N, wins_ties, 0, stream);
 }
 
+#ifdef DAUC_TUNING
 int dauc_pair_count_variant(const float* pos, int64_t P, const float* neg, int64_t N,
                             unsigned long long* wins_ties, int variant, dauc_stream_t stream) {
+    return pair_count_impl(pos, P, neg, N, wins_ties, variant, stream);
+}
+#endif
+
+static int pair_count_impl(const float* pos, int64_t P, const float* neg, int64_t N,
+                           unsigned long long* wins_ties, int variant, dauc_stream_t stream) {
     if (P < 0 || N < 0 || wins_ties == nullptr || (P > 0 && pos == nullptr) ||
         (N > 0 && neg == nullptr))
         return DAUC_EINVAL;
@@ -901,6 +911,7 @@ int dauc_pair_count_variant(const float* pos, int64_t P, const float* neg, int64
                        per, aligned, wins_ties)
     switch (variant) {
         case 0: DAUC_PC_LAUNCH(8, 0); break;
+#ifdef DAUC_TUNING
         case 1: DAUC_PC_LAUNCH(8, 1); break;
         case 2: DAUC_PC_LAUNCH(8, 2); break;
         case 3: DAUC_PC_LAUNCH(8, 3); break;
@@ -912,6 +923,8 @@ int dauc_pair_count_variant(const float* pos, int64_t P, const float* neg, int64
         case 9: DAUC_PC_LAUNCH(16, 1); break;
         case 10: DAUC_PC_LAUNCH(16, 2); break;
         case 11: DAUC_PC_LAUNCH(16, 3); break;
+#endif
+        default: return DAUC_EINVAL;
     }
 #undef DAUC_PC_LAUNCH
     return launch_status();

@@ -913,8 +913,13 @@ constexpr size_t kCellBytes = 256 + size_t(kTop) * 4 + ((size_t(kMaxCells) + 2) 
                               (size_t(kMaxCells) + 1) * kCellSlot * 4;
 
 // search structure set by dauc_set_search_mode (tests, measurements): 0, 1 = tree, 2 = cells
-int g_search_mode = 0;
+#ifdef DAUC_TUNING
+int g_search_mode = 0;  // dauc_set_search_mode (tuning builds): 0 automatic, 1 tree, 2 slot cells
+#else
+constexpr int g_search_mode = 0;
+#endif
 
+#ifdef DAUC_TUNING
 __device__ __forceinline__ unsigned cell_of(unsigned key, unsigned e) {
     return (e & 0xffffu) + __umulhi(key << kTopBits, e >> 16);
 }
@@ -925,6 +930,8 @@ __device__ __forceinline__ bool cells_in_use(const unsigned* __restrict__ meta, 
 
 // inclusive scan over the 1024 threads of a workgroup (wave shuffles, one barrier for the wave
 // totals); op is min or +, v the thread's value
+#endif
+
 template <bool MIN>
 __device__ __forceinline__ unsigned block_incl_scan1024(unsigned v, unsigned* wtot) {
     const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
@@ -947,6 +954,7 @@ __device__ __forceinline__ unsigned block_incl_scan1024(unsigned v, unsigned* wt
 // mu in [4, mu_max] whose sum of ceil(n_t / mu) fits kMaxCells, and the cell offsets (prefix sum).
 // Thread i owns the buckets t = 4095 - 4i - j (j = 0..3): descending, so suffix minima over t
 // are prefix minima over the threads.
+#ifdef DAUC_TUNING
 __global__ __launch_bounds__(kCellPlanThreads) void cell_plan_kernel(const unsigned* __restrict__ sorted, int64_t M,
                                                                      int mu_max, unsigned* __restrict__ l1,
                                                                      unsigned* __restrict__ meta) {
@@ -1328,6 +1336,8 @@ __global__ __launch_bounds__(kQueryThreads) void query_cells_kernel(const float*
     }
 }
 
+#endif  // DAUC_TUNING
+
 // ---- count index (the default search where it fits: dauc_set_search_mode 0) -----------------
 //
 // The tree's cost per query is its one 16-byte bucket gather from L2 plus 7 dependent LDS reads
@@ -1588,8 +1598,14 @@ __device__ __forceinline__ void ci_fix(unsigned x, unsigned rl, unsigned cnt, co
     t += static_cast<unsigned long long>((ub - lb) - (ubf - lbf));
 }
 
+#ifndef DAUC_CI_PIPE
+#define DAUC_CI_PIPE 1  // 1: software-pipelined query loop (LDS lookups overlap the window loads)
+#endif
+#ifndef DAUC_CI_PHASED
+#define DAUC_CI_PHASED 1  // the unpipelined loop: every query's LDS reads of a phase issued together
+#endif
 #ifndef DAUC_CI_U
-#define DAUC_CI_U 2
+#define DAUC_CI_U (DAUC_CI_PIPE ? 1 : 2)  // float4 slots per thread per group (int8 labels)
 #endif
 
 // The labeled query pass over the count index (same stream and checks as query_labeled_kernel);
@@ -1607,8 +1623,10 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
                                                                 unsigned long long* __restrict__ out,
                                                                 unsigned long long* __restrict__ nonfinite,
                                                                 unsigned* __restrict__ verdict,
-                                                                const unsigned* __restrict__ grp) {
+                                                                const unsigned* __restrict__ grp,
+                                                                const unsigned long long* __restrict__ Mp) {
     const bool in_use = count_index_in_use(meta);
+    if (Mp != nullptr) M = static_cast<int64_t>(*Mp);  // the direct build: the table size on the device
     if (verdict != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *verdict = in_use ? 1u : 2u;
     if (!in_use) return;
     extern __shared__ uint2 ci_lds[];
@@ -1669,6 +1687,142 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
     const int64_t nvec = end > head ? (end - head) / 4 : 0;
     const bool aligned = (reinterpret_cast<uintptr_t>(s + head) & 15u) == 0 &&
                          (reinterpret_cast<uintptr_t>(lab + head) & (4 * sizeof(LT) - 1)) == 0;
+#if DAUC_CI_PIPE
+    if (aligned) {
+        // Software-pipelined over groups of NQ queries (U float4 slots per thread): the LDS lookups
+        // of group g run while group g-1's window loads and group g+1's stream loads are in
+        // flight, and group g-1 is counted after group g's windows are issued. Per group, in
+        // issue order: keys(g) [waits for the stream loads issued one group earlier], stream
+        // loads of g+1, LDS lookups of g, window loads of g, count of g-1 [waits for the windows
+        // issued one group earlier; the younger loads stay in flight: vmcnt retires in order].
+        constexpr int U = sizeof(LT) == 1 ? DAUC_CI_U : 1;
+        constexpr int NQ = 4 * U;
+        const int64_t step = int64_t(U) * stride;
+        // two sets of every per-group register (A and B, used alternately by an unrolled pair of
+        // iterations): a loop that rotated one set into the other would copy loaded registers at
+        // its back-edge, i.e. wait there for the loads it had just issued
+        struct Stream {
+            f32x4 f[U];
+            LabelWords<LT> l[U];
+        };
+        // Every load of the loop is issued unconditionally (out-of-range slots re-read slot 0 and are
+        // masked; a lane without a window reads the table's first one): a load under a branch
+        // leaves the number of younger loads in flight unknown, and the compiler then waits with
+        // vmcnt(0) -- for every load in flight -- instead of a counted wait.
+        auto load = [&](Stream& sg, int64_t v0) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int64_t v = v0 + int64_t(u) * stride;
+                const int64_t i = head + (v < nvec ? v : 0) * 4;
+                sg.f[u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(s + i));
+                sg.l[u].load(lab + i);
+                if (v >= nvec) sg.l[u].set_positive();
+            }
+        };
+        // one group in flight: its keys, rank_lo | count << 28 (rank_lo < 2^28: M <= 2^27 here),
+        // window and query mask
+        struct Group {
+            unsigned x[NQ], rc[NQ];
+            uint4 k[NQ];
+            unsigned use;
+        };
+        auto keys = [&](Group& g, const Stream& sg) {
+            g.use = 0u;
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const float f[4] = {sg.f[u].x, sg.f[u].y, sg.f[u].z, sg.f[u].w};
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const bool use = sg.l[u].not_positive(q);
+                    g.use |= unsigned(use) << (4 * u + q);
+                    g.x[4 * u + q] = key_fast(f[q]);
+                    nf += use && !isfinite(f[q]);
+                }
+            }
+        };
+        // phase by phase over the group, so that every query's LDS read of a phase is issued before
+        // the first wait (a per-query chain with its conditional window load in between keeps the
+        // compiler from interleaving the queries: one LDS round trip per read per query)
+        auto locate = [&](Group& g) {
+            uint2 e[NQ];
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) e[q] = l1[g.x[q] >> kCiLowBits];
+            unsigned c[NQ];
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) c[q] = ci_cell(g.x[q], e[q]);
+            uint2 b[NQ];
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) b[q] = blk[c[q] / kCiBlock];
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                const unsigned sh = 4u * (c[q] % kCiBlock);
+                const unsigned below = __builtin_amdgcn_ubfe(b[q].y, 0u, sh);
+                const unsigned bytes = (below & 0x0f0f0f0fu) + ((below >> 4) & 0x0f0f0f0fu);
+                const unsigned rl = b[q].x + __builtin_amdgcn_sad_u8(bytes, 0u, 0u);
+                const unsigned cnt = __builtin_amdgcn_ubfe(b[q].y, sh, 4u);
+                g.rc[q] = rl | (cnt << 28);
+            }
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                const unsigned rl = g.rc[q] & 0x0fffffffu;
+                g.k[q] = *reinterpret_cast<const uint4*>(sorted + ((g.rc[q] >> 28) ? rl & ~3u : 0u));
+            }
+        };
+        auto count = [&](const Group& g) {
+            unsigned wl = 0u, tl = 0u;
+            bool more = false;
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                // an empty cell's lane loaded the table's first window: counted as +inf padding
+                const uint4 k = (g.rc[q] >> 28) ? g.k[q] : uint4{kPadKey, kPadKey, kPadKey, kPadKey};
+                more |= ci_count(g.x[q], (g.use >> q) & 1u, g.rc[q] & 0x0fffffffu, g.rc[q] >> 28, k, M32, wl, tl);
+            }
+            w += wl;
+            t += tl;
+            if (more) {
+#pragma unroll
+                for (int q = 0; q < NQ; ++q) {
+                    const unsigned rl = g.rc[q] & 0x0fffffffu, cnt = g.rc[q] >> 28;
+                    if (((g.use >> q) & 1u) && (rl & 3u) + cnt > 4u) ci_fix(g.x[q], rl, cnt, g.k[q], sorted, w, t);
+                }
+            }
+        };
+        // per group g: keys(g) [its stream loads were issued one group earlier], stream loads of
+        // g + 1, LDS lookups + window loads of g, count of g - 1 [its windows were issued one group
+        // earlier; the younger loads stay in flight: vmcnt retires in order]
+        Stream sa, sb;
+        Group ga, gb;
+        load(sa, tid);
+        keys(ga, sa);
+        load(sb, tid + step);
+        locate(ga);
+        for (int64_t v = tid + step;;) {
+            if (v >= nvec) {
+                count(ga);
+                break;
+            }
+            keys(gb, sb);
+            load(sa, v + step);
+            asm volatile("" ::: "memory");  // the stream loads stay older than this group's windows
+            locate(gb);
+            count(ga);
+            v += step;
+            if (v >= nvec) {
+                count(gb);
+                break;
+            }
+            keys(ga, sa);
+            load(sb, v + step);
+            asm volatile("" ::: "memory");
+            locate(ga);
+            count(gb);
+            v += step;
+        }
+    } else {
+        for (int64_t v = tid; v < nvec; v += stride)
+            for (int q = 0; q < 4; ++q) one(head + v * 4 + q);
+    }
+#else
     if (aligned) {
         constexpr int U = sizeof(LT) == 1 ? DAUC_CI_U : 1;
         constexpr int NQ = 4 * U;
@@ -1703,8 +1857,34 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
                     nf += use[4 * u + q] && !isfinite(f[q]);
                 }
             }
+#if DAUC_CI_PHASED
+            {
+                uint2 e[NQ], b[NQ];
+                unsigned c[NQ];
+#pragma unroll
+                for (int q = 0; q < NQ; ++q) e[q] = l1[x[q] >> kCiLowBits];
+#pragma unroll
+                for (int q = 0; q < NQ; ++q) c[q] = ci_cell(x[q], e[q]);
+#pragma unroll
+                for (int q = 0; q < NQ; ++q) b[q] = blk[c[q] / kCiBlock];
+#pragma unroll
+                for (int q = 0; q < NQ; ++q) {
+                    const unsigned sh = 4u * (c[q] % kCiBlock);
+                    const unsigned below = __builtin_amdgcn_ubfe(b[q].y, 0u, sh);
+                    const unsigned bytes = (below & 0x0f0f0f0fu) + ((below >> 4) & 0x0f0f0f0fu);
+                    rl[q] = b[q].x + __builtin_amdgcn_sad_u8(bytes, 0u, 0u);
+                    cnt[q] = __builtin_amdgcn_ubfe(b[q].y, sh, 4u);
+                }
+#pragma unroll
+                for (int q = 0; q < NQ; ++q) {
+                    const uint4 kk = *reinterpret_cast<const uint4*>(sorted + (cnt[q] ? rl[q] & ~3u : 0u));
+                    k[q] = cnt[q] ? kk : uint4{kPadKey, kPadKey, kPadKey, kPadKey};
+                }
+            }
+#else
 #pragma unroll
             for (int q = 0; q < NQ; ++q) ci_locate(x[q], l1, blk, sorted, rl[q], cnt[q], k[q]);
+#endif
             asm volatile("" ::: "memory");
             load(v0 + int64_t(U) * stride, fn, ln);
             unsigned wl = 0u, tl = 0u;
@@ -1728,6 +1908,7 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
         for (int64_t v = tid; v < nvec; v += stride)
             for (int q = 0; q < 4; ++q) one(head + v * 4 + q);
     }
+#endif
     for (int64_t i = head + nvec * 4 + tid; i < end; i += stride) one(i);
     __shared__ unsigned long long red[3][kQueryThreads / kWave];
     w = wave_sum(w);
@@ -1768,9 +1949,13 @@ constexpr int kDirectPerThread = 8;
 
 // top-bucket histogram (LDS, then one global add per used bucket; `hist` zeroed by the caller);
 // also zeroes the per-cell counters the count pass adds into
-__global__ __launch_bounds__(256) void direct_hist_kernel(const float* __restrict__ pos, int64_t M,
+// The table size M is read from the device (the compaction's count), so the whole build and query
+// are enqueued without the host knowing M: the grids are sized for the index's capacity and loop.
+__global__ __launch_bounds__(256) void direct_hist_kernel(const float* __restrict__ pos,
+                                                          const unsigned long long* __restrict__ Mp,
                                                           unsigned* __restrict__ hist, unsigned* __restrict__ cnt,
                                                           int64_t ncnt) {
+    const int64_t M = static_cast<int64_t>(*Mp);
     __shared__ unsigned h[kCiTop];
     for (int i = threadIdx.x; i < kCiTop; i += 256) h[i] = 0u;
     __syncthreads();
@@ -1789,7 +1974,7 @@ __global__ __launch_bounds__(256) void direct_hist_kernel(const float* __restric
 // writes the plan and the verdict words for the later passes. Then the per-cell key counts (a wave
 // whose keys all fall in one cell adds once: tie-heavy tables) and every key's cell.
 
-__global__ __launch_bounds__(kDirectThreads) void direct_count_kernel(const float* __restrict__ pos, int64_t M,
+__global__ __launch_bounds__(kDirectThreads) void direct_count_kernel(const float* __restrict__ pos, int64_t mcap,
                                                                       const unsigned* __restrict__ hist,
                                                                       uint2* __restrict__ l1g,
                                                                       unsigned* __restrict__ meta,
@@ -1798,16 +1983,22 @@ __global__ __launch_bounds__(kDirectThreads) void direct_count_kernel(const floa
     static_assert(kCiTop == 8 * kDirectThreads, "eight top buckets per thread");
     __shared__ uint2 l1[kCiTop];
     __shared__ unsigned wtot[kDirectThreads / kWave];
-    __shared__ unsigned totals[2];
+    __shared__ unsigned totals[3];
     const uint4 h0 = reinterpret_cast<const uint4*>(hist)[2 * threadIdx.x];
     const uint4 h1 = reinterpret_cast<const uint4*>(hist)[2 * threadIdx.x + 1];
     const unsigned n[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
-    unsigned used = 0u;
+    unsigned used = 0u, keys = 0u;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) used += n[j] != 0u;
+    for (int j = 0; j < 8; ++j) {
+        used += n[j] != 0u;
+        keys += n[j];
+    }
     used = block_incl_scan1024<false>(used, wtot);
     if (threadIdx.x == kDirectThreads - 1) totals[0] = used;
+    keys = block_incl_scan1024<false>(keys, wtot);  // M = the histogram's total (< 2^32: M <= n / 2)
+    if (threadIdx.x == kDirectThreads - 1) totals[2] = keys;
     __syncthreads();
+    const int64_t M = totals[2];
     const int64_t avail = int64_t(kCiMaxCells) - int64_t(totals[0]);
     const int64_t num = avail < 2 * M ? avail : 2 * M;
     unsigned C[8], csum = 0u;
@@ -1826,7 +2017,8 @@ __global__ __launch_bounds__(kDirectThreads) void direct_count_kernel(const floa
     }
     __syncthreads();
     const unsigned total = totals[1];
-    const bool ok = num > 0 && 3 * num >= 2 * M && total <= static_cast<unsigned>(kCiMaxCells);
+    // usable: at most 1.5 keys per cell, and the table fits the workspace (M <= mcap)
+    const bool ok = num > 0 && 3 * num >= 2 * M && total <= static_cast<unsigned>(kCiMaxCells) && M <= mcap;
     if (blockIdx.x == 0) {
         for (int t = threadIdx.x; t < kCiTop; t += kDirectThreads) l1g[t] = l1[t];
         if (threadIdx.x == 0) {
@@ -1838,22 +2030,24 @@ __global__ __launch_bounds__(kDirectThreads) void direct_count_kernel(const floa
     }
     if (!ok) return;
     const int lane = threadIdx.x & (kWave - 1);
-    const int64_t i = int64_t(blockIdx.x) * kDirectThreads + threadIdx.x;
-    const bool live = i < M;
-    unsigned c = 0u;
-    if (live) {
-        const unsigned x = key_fast(pos[i]);
-        c = ci_cell(x, l1[x >> kCiLowBits]);
-        cell[i] = c;  // the scatter's cell, so it does not walk pos -> key -> plan again
-    }
-    const unsigned long long act = __ballot(live);
-    if (act == 0ull) return;
-    const int first = __ffsll(static_cast<long long>(act)) - 1;
-    const unsigned cf = __shfl(c, first, kWave);
-    if (__ballot(live && c == cf) == act) {
-        if (lane == first) atomicAdd(cnt + cf, static_cast<unsigned>(__popcll(act)));
-    } else if (live) {
-        atomicAdd(cnt + c, 1u);
+    for (int64_t i0 = int64_t(blockIdx.x) * kDirectThreads; i0 < M; i0 += int64_t(gridDim.x) * kDirectThreads) {
+        const int64_t i = i0 + threadIdx.x;
+        const bool live = i < M;
+        unsigned c = 0u;
+        if (live) {
+            const unsigned x = key_fast(pos[i]);
+            c = ci_cell(x, l1[x >> kCiLowBits]);
+            cell[i] = c;  // the scatter's cell, so it does not walk pos -> key -> plan again
+        }
+        const unsigned long long act = __ballot(live);
+        if (act == 0ull) continue;
+        const int first = __ffsll(static_cast<long long>(act)) - 1;
+        const unsigned cf = __shfl(c, first, kWave);
+        if (__ballot(live && c == cf) == act) {
+            if (lane == first) atomicAdd(cnt + cf, static_cast<unsigned>(__popcll(act)));
+        } else if (live) {
+            atomicAdd(cnt + c, 1u);
+        }
     }
 }
 
@@ -1889,7 +2083,8 @@ __global__ __launch_bounds__(kDirectGroup) void direct_blocks_kernel(const unsig
 
 // every key into its cell's range of the table (the counters are counted back down to zero);
 // the table's tail is padded with +inf keys for the 16-byte windows
-__global__ __launch_bounds__(kDirectThreads) void direct_scatter_kernel(const float* __restrict__ pos, int64_t M,
+__global__ __launch_bounds__(kDirectThreads) void direct_scatter_kernel(const float* __restrict__ pos,
+                                                                        const unsigned long long* __restrict__ Mp,
                                                                         const uint2* __restrict__ blk,
                                                                         const unsigned* __restrict__ grp,
                                                                         const unsigned* __restrict__ meta,
@@ -1897,20 +2092,22 @@ __global__ __launch_bounds__(kDirectThreads) void direct_scatter_kernel(const fl
                                                                         const unsigned* __restrict__ cell,
                                                                         unsigned* __restrict__ table) {
     if (meta[kCiOk] == 0u || meta[kCiSkew] != 0u) return;
+    const int64_t M = static_cast<int64_t>(*Mp);
     __shared__ unsigned pre[kDirectMaxGroups];
     group_prefix(grp, (static_cast<int>(meta[kCiBlocks]) + kDirectGroup - 1) / kDirectGroup, pre);
     __syncthreads();
-    const int64_t i = int64_t(blockIdx.x) * kDirectThreads + threadIdx.x;
-    if (i < 16) table[M + i] = kPadKey;
-    if (i >= M) return;
-    const unsigned x = key_fast(pos[i]);
-    const unsigned c = cell[i];
-    const unsigned bi = c / kCiBlock;
-    const uint2 b = blk[bi];
-    const unsigned below = __builtin_amdgcn_ubfe(b.y, 0u, 4u * (c % kCiBlock));
-    const unsigned bytes = (below & 0x0f0f0f0fu) + ((below >> 4) & 0x0f0f0f0fu);
-    const unsigned slot = atomicSub(cnt + c, 1u) - 1u;
-    table[pre[bi / kDirectGroup] + b.x + __builtin_amdgcn_sad_u8(bytes, 0u, 0u) + slot] = x;
+    const int64_t gid = int64_t(blockIdx.x) * kDirectThreads + threadIdx.x;
+    if (gid < 16) table[M + gid] = kPadKey;
+    for (int64_t i = gid; i < M; i += int64_t(gridDim.x) * kDirectThreads) {
+        const unsigned x = key_fast(pos[i]);
+        const unsigned c = cell[i];
+        const unsigned bi = c / kCiBlock;
+        const uint2 b = blk[bi];
+        const unsigned below = __builtin_amdgcn_ubfe(b.y, 0u, 4u * (c % kCiBlock));
+        const unsigned bytes = (below & 0x0f0f0f0fu) + ((below >> 4) & 0x0f0f0f0fu);
+        const unsigned slot = atomicSub(cnt + c, 1u) - 1u;
+        table[pre[bi / kDirectGroup] + b.x + __builtin_amdgcn_sad_u8(bytes, 0u, 0u) + slot] = x;
+    }
 }
 
 // Every queried score is also checked to be finite (sklearn rejects NaN / inf scores,
@@ -1926,8 +2123,14 @@ __global__ __launch_bounds__(kQueryThreads) void query_labeled_kernel(const floa
                                                                      int64_t M, unsigned long long* __restrict__ out,
                                                                      unsigned long long* __restrict__ nonfinite,
                                                                      const unsigned* __restrict__ meta, int force) {
-    // meta: the slot-cell index's (force = 1) or the count index's (force = 0) builder verdict
+    // meta: the slot-cell index's (force = 1, tuning builds) or the count index's (force = 0)
+    // builder verdict
+#ifdef DAUC_TUNING
     if (meta != nullptr && (force ? cells_in_use(meta, M, 1) : count_index_in_use(meta))) return;
+#else
+    (void)force;
+    if (meta != nullptr && count_index_in_use(meta)) return;
+#endif
     extern __shared__ TreeNode tree[];
     for (int i = threadIdx.x; i < g.nodes; i += kQueryThreads) tree[i] = gtree[i];
     const TopKeys top = load_top(gtree, g, sorted, k);
@@ -2185,6 +2388,7 @@ CellWs carve_cells(void* p) {
     return w;
 }
 
+#ifdef DAUC_TUNING
 // plan + fill of the cell index behind the sort (2 launches; the verdict stays on the device)
 int prepare_cells(const unsigned* sorted, int64_t M, const CellWs& cw, int mu_max, hipStream_t st) {
     hipLaunchKernelGGL(cell_plan_kernel, dim3(1), dim3(kCellPlanThreads), 0, st, sorted, M, mu_max, cw.l1, cw.meta);
@@ -2203,6 +2407,8 @@ int launch_cells(const float* s, const LT* lab, int64_t begin, int64_t end, cons
                        cw.base, cw.slots, sorted, M, out, nonfinite);
     return launch_status();
 }
+
+#endif
 
 CountWs carve_count(void* p) {
     char* c = static_cast<char*>(p);
@@ -2235,11 +2441,11 @@ int prepare_count(const unsigned* sorted, int64_t M, const CountWs& cw, hipStrea
 template <typename LT>
 int launch_ci(const float* s, const LT* lab, int64_t begin, int64_t end, const CountWs& cw, const unsigned* sorted,
               int64_t M, unsigned long long* out, unsigned long long* nonfinite, hipStream_t st,
-              unsigned* verdict = nullptr, const unsigned* grp = nullptr) {
+              unsigned* verdict = nullptr, const unsigned* grp = nullptr, const unsigned long long* Mp = nullptr) {
     const dim3 grid(query_grid(end - begin)), block(kQueryThreads);
     const size_t lds = (size_t(kCiTop) + kCiMaxBlocks) * 8 + (grp ? size_t(kDirectMaxGroups) * 4 : 0);
     hipLaunchKernelGGL((query_ci_kernel<LT>), grid, block, lds, st, s, lab, begin, end, cw.meta, cw.l1, cw.blk, sorted,
-                       M, out, nonfinite, verdict, grp);
+                       M, out, nonfinite, verdict, grp, Mp);
     return launch_status();
 }
 
@@ -2300,52 +2506,62 @@ int prepare_table(const float* table, int64_t M, void* workspace, hipStream_t st
 
 }  // namespace
 
-bool direct_fits(int64_t P) { return g_search_mode == 0 && P > 0 && 2 * P <= 3 * int64_t(kCiMaxCells); }
+bool direct_enabled() { return g_search_mode == 0; }
+
+int64_t direct_capacity(int64_t n) {
+    // the plan's bound (2 M <= 3 cells), and the smaller class of n scores (the evaluation's
+    // workspace holds a table of n / 2 + 1 keys)
+    const int64_t cap = 3 * int64_t(kCiMaxCells) / 2, half = n / 2 + 1;
+    return half < cap ? half : cap;
+}
 
 int direct_hist_words() { return kCiTop; }
 
-int64_t direct_hist_offset(int64_t P) {  // carve_count(...).first, relative to the workspace
-    return int64_t(((sort_ws_bytes(P) + 255) / 256) * 256 + ((kTreeBytes + 255) / 256) * 256 +
+int64_t direct_hist_offset(int64_t Mcap) {  // carve_count(...).first, relative to the workspace
+    return int64_t(((sort_ws_bytes(Mcap) + 255) / 256) * 256 + ((kTreeBytes + 255) / 256) * 256 +
                    ((kCellBytes + 255) / 256) * 256 + 256);
 }
 
-int counts_labeled_direct(const float* pos, int64_t P, const float* scores, const void* labels, int label_dtype,
-                          int64_t begin, int64_t end, unsigned long long* wins_ties, unsigned long long* nonfinite,
-                          unsigned* verdict, void* workspace, size_t workspace_bytes, hipStream_t st) {
-    if (!direct_fits(P) || pos == nullptr || begin < 0 || end < begin || wins_ties == nullptr ||
+int counts_labeled_direct(const float* pos, const unsigned long long* Mp, int64_t Mcap, const float* scores,
+                          const void* labels, int label_dtype, int64_t begin, int64_t end,
+                          unsigned long long* wins_ties, unsigned long long* nonfinite, unsigned* verdict,
+                          void* workspace, size_t workspace_bytes, hipStream_t st) {
+    if (pos == nullptr || Mp == nullptr || Mcap < 1 || begin < 0 || end < begin || wins_ties == nullptr ||
         (end > begin && (scores == nullptr || labels == nullptr)) || workspace == nullptr ||
-        workspace_bytes < dauc_sort_workspace_size(P))
+        workspace_bytes < dauc_sort_workspace_size(Mcap))
         return DAUC_EINVAL;
     if (label_dtype != DAUC_LABEL_I8 && label_dtype != DAUC_LABEL_I32 && label_dtype != DAUC_LABEL_I64)
         return DAUC_EINVAL;
-    const SortWs w = carve(workspace, P);
-    const CountWs nw = count_ws_of(workspace, P);
-    unsigned* table = w.keys_a;  // P + 64 words: room for the +inf tail
-    const int64_t ncnt = (2 * P + kCiTop + 16) < kCiCntWords ? (2 * P + kCiTop + 16) : kCiCntWords;
+    const SortWs w = carve(workspace, Mcap);
+    const CountWs nw = count_ws_of(workspace, Mcap);
+    unsigned* table = w.keys_a;  // Mcap + 64 words: room for the +inf tail
     // the histogram aggregates 8 keys per thread in LDS; the count and scatter passes are chains of
-    // dependent loads per key, so they take one key per thread (every chain in flight at once)
-    unsigned* grp = carve_cells(after_tree_of(workspace, P)).l1;  // the slot-cell index is unused here
-    const dim3 g8(static_cast<unsigned>((P + 256 * kDirectPerThread - 1) / (256 * kDirectPerThread)));
-    const dim3 g1(static_cast<unsigned>((P + kDirectThreads - 1) / kDirectThreads));
-    hipLaunchKernelGGL(direct_hist_kernel, g8, dim3(256), 0, st, pos, P, nw.first, nw.cstart, ncnt);
-    hipLaunchKernelGGL(direct_count_kernel, g1, dim3(kDirectThreads), 0, st, pos, P, nw.first, nw.l1, nw.meta,
-                       nw.cstart, w.keys_b);
+    // dependent loads per key, so they take one key per thread per step (every chain in flight)
+    unsigned* grp = carve_cells(after_tree_of(workspace, Mcap)).l1;  // the slot-cell index is unused here
+    const auto blocks = [](int64_t keys, int64_t per, int64_t cap) {
+        const int64_t b = (keys + per - 1) / per;
+        return dim3(static_cast<unsigned>(b < cap ? b : cap));
+    };
+    hipLaunchKernelGGL(direct_hist_kernel, blocks(Mcap, 256 * kDirectPerThread, 256), dim3(256), 0, st, pos, Mp,
+                       nw.first, nw.cstart, kCiCntWords);
+    hipLaunchKernelGGL(direct_count_kernel, blocks(Mcap, kDirectThreads, 1024), dim3(kDirectThreads), 0, st, pos,
+                       Mcap, nw.first, nw.l1, nw.meta, nw.cstart, w.keys_b);
     hipLaunchKernelGGL(direct_blocks_kernel, dim3(kDirectMaxGroups), dim3(kDirectGroup), 0, st, nw.cstart, nw.meta,
                        nw.blk, grp);
-    hipLaunchKernelGGL(direct_scatter_kernel, g1, dim3(kDirectThreads), 0, st, pos, P, nw.blk, grp, nw.meta,
-                       nw.cstart, w.keys_b, table);
+    hipLaunchKernelGGL(direct_scatter_kernel, blocks(Mcap, kDirectThreads, 1024), dim3(kDirectThreads), 0, st, pos,
+                       Mp, nw.blk, grp, nw.meta, nw.cstart, w.keys_b, table);
     int rc = launch_status();
     if (rc || end == begin) return rc;
     switch (label_dtype) {
         case DAUC_LABEL_I8:
-            return launch_ci(scores, static_cast<const int8_t*>(labels), begin, end, nw, table, P, wins_ties, nonfinite,
-                             st, verdict, grp);
+            return launch_ci(scores, static_cast<const int8_t*>(labels), begin, end, nw, table, 0, wins_ties,
+                             nonfinite, st, verdict, grp, Mp);
         case DAUC_LABEL_I32:
-            return launch_ci(scores, static_cast<const int32_t*>(labels), begin, end, nw, table, P, wins_ties,
-                             nonfinite, st, verdict, grp);
+            return launch_ci(scores, static_cast<const int32_t*>(labels), begin, end, nw, table, 0, wins_ties,
+                             nonfinite, st, verdict, grp, Mp);
         default:
-            return launch_ci(scores, static_cast<const int64_t*>(labels), begin, end, nw, table, P, wins_ties,
-                             nonfinite, st, verdict, grp);
+            return launch_ci(scores, static_cast<const int64_t*>(labels), begin, end, nw, table, 0, wins_ties,
+                             nonfinite, st, verdict, grp, Mp);
     }
 }
 
@@ -2359,11 +2575,13 @@ size_t dauc_sort_workspace_size(int64_t n) {
     return sort_ws_bytes(n < 1 ? 1 : n) + kTreeBytes + 256 + kCellBytes + 256 + kCountBytes + 256;
 }
 
+#ifdef DAUC_TUNING
 int dauc_set_search_mode(int mode) {
     if (mode < 0 || mode > 2) return DAUC_EINVAL;
     g_search_mode = mode;
     return DAUC_OK;
 }
+#endif
 
 int dauc_sort_keys(const float* scores, int64_t n, unsigned* keys_out, void* workspace,
                    size_t workspace_bytes, dauc_stream_t stream) {
@@ -2420,23 +2638,31 @@ int dauc_auc_counts_sorted_labeled(const float* pos, int64_t P, const float* sco
     // the search structure: mode 0 the count index where the table can use it (the device keeps
     // the tree for skewed tables), 1 the tree, 2 the slot-cell index (a measured alternative)
     const int mode = g_search_mode;
-    const bool slot_cells = mode == 2 && P <= int64_t(kMaxCells) * kCellMuForced;
     const bool count = mode == 0 && 2 * P <= 3 * int64_t(kCiMaxCells);
-    const CellWs cw = carve_cells(after_tree_of(workspace, P));
     const CountWs nw = count_ws_of(workspace, P);
     int rc = prepare_table(pos, P, workspace, st, &sorted, &tree, &k, &g, count ? nw.first : nullptr);
     if (rc) return rc;
-    if (slot_cells && (rc = prepare_cells(sorted, P, cw, kCellMuForced, st))) return rc;
     if (count && (rc = prepare_count(sorted, P, nw, st))) return rc;
-    const unsigned* meta = slot_cells ? cw.meta : (count ? nw.meta : nullptr);
+#ifdef DAUC_TUNING
+    const bool slot_cells = mode == 2 && P <= int64_t(kMaxCells) * kCellMuForced;
+    const CellWs cw = carve_cells(after_tree_of(workspace, P));
+    if (slot_cells && (rc = prepare_cells(sorted, P, cw, kCellMuForced, st))) return rc;
+#else
+    constexpr bool slot_cells = false;
+#endif
+    const unsigned* meta = count ? nw.meta : nullptr;
     auto run = [&](auto* lab) {
-        int r = launch_labeled(k, scores, lab, begin, end, tree, g, sorted, P, wins_ties, nonfinite, meta,
-                               slot_cells ? 1 : 0, st);
-        if (r == DAUC_OK && slot_cells)
-            r = launch_cells(scores, lab, begin, end, cw, 1, sorted, P, wins_ties, nonfinite, st);
+#ifdef DAUC_TUNING
+        if (slot_cells) {
+            int r = launch_labeled(k, scores, lab, begin, end, tree, g, sorted, P, wins_ties, nonfinite, cw.meta, 1, st);
+            return r ? r : launch_cells(scores, lab, begin, end, cw, 1, sorted, P, wins_ties, nonfinite, st);
+        }
+#endif
+        int r = launch_labeled(k, scores, lab, begin, end, tree, g, sorted, P, wins_ties, nonfinite, meta, 0, st);
         if (r == DAUC_OK && count) r = launch_ci(scores, lab, begin, end, nw, sorted, P, wins_ties, nonfinite, st);
         return r;
     };
+    (void)slot_cells;
     switch (label_dtype) {
         case DAUC_LABEL_I8: return run(static_cast<const int8_t*>(labels));
         case DAUC_LABEL_I32: return run(static_cast<const int32_t*>(labels));

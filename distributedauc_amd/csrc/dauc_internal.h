@@ -115,13 +115,17 @@ int compact_unordered(const float* scores, const void* labels, int label_dtype, 
 
 // auc_sort.hip: the count index built straight from the unsorted positives (no radix sort, no
 // tree) and the labeled query pass over scores [begin, end); the table is ordered by cell only.
-// `hist` (kCiTop words, direct_hist_words()) must be zero on entry. *verdict (device) = 1 when
-// the count index was usable, 2 when the caller must re-run the sorted path (skewed table).
-int64_t direct_hist_offset(int64_t P);  // byte offset of `hist` in the sort workspace
+// The table size M is read from the device (*Mp, the compaction's count), so nothing waits for the
+// host; the workspace is carved for Mcap = direct_capacity(n) keys. `hist` (kCiTop words at
+// direct_hist_offset(Mcap)) must be zero on entry. *verdict (device) = 1 when the count index held
+// the table, 2 when the caller must run the sorted path (M > Mcap, or a skewed table).
+bool direct_enabled();  // the search mode is automatic (always, except in a tuning build's mode 1 / 2)
+int64_t direct_capacity(int64_t n);
+int64_t direct_hist_offset(int64_t Mcap);  // byte offset of `hist` in the sort workspace
 int direct_hist_words();
-bool direct_fits(int64_t P);  // the search mode is automatic (0) and the count index can hold P keys
-int counts_labeled_direct(const float* pos, int64_t P, const float* scores, const void* labels, int label_dtype,
-                          int64_t begin, int64_t end, unsigned long long* wins_ties, unsigned long long* nonfinite,
-                          unsigned* verdict, void* workspace, size_t workspace_bytes, hipStream_t st);
+int counts_labeled_direct(const float* pos, const unsigned long long* Mp, int64_t Mcap, const float* scores,
+                          const void* labels, int label_dtype, int64_t begin, int64_t end,
+                          unsigned long long* wins_ties, unsigned long long* nonfinite, unsigned* verdict,
+                          void* workspace, size_t workspace_bytes, hipStream_t st);
 
 }  // namespace dauc

@@ -187,6 +187,7 @@ int launch_table(int variant, float* w, const float* w0, float* wavg, const SegT
                  hipStream_t st) {
     switch (variant) {
         case 0: return launch_table_t<2, true>(w, w0, wavg, tab, lr, invg, scalars, grad3, anchor3, mode, st);
+#ifdef DAUC_TUNING
         case 1: return launch_table_t<1, true>(w, w0, wavg, tab, lr, invg, scalars, grad3, anchor3, mode, st);
         case 2: return launch_table_t<4, true>(w, w0, wavg, tab, lr, invg, scalars, grad3, anchor3, mode, st);
         case 3: return launch_table_t<3, true>(w, w0, wavg, tab, lr, invg, scalars, grad3, anchor3, mode, st);
@@ -198,6 +199,7 @@ int launch_table(int variant, float* w, const float* w0, float* wavg, const SegT
         case 9: return launch_table_t<1, true, true>(w, w0, wavg, tab, lr, invg, scalars, grad3, anchor3, mode, st);
         case 10: return launch_table_t<4, true, true>(w, w0, wavg, tab, lr, invg, scalars, grad3, anchor3, mode, st);
         case 11: return launch_table_t<3, true, true>(w, w0, wavg, tab, lr, invg, scalars, grad3, anchor3, mode, st);
+#endif
         default: return DAUC_EINVAL;
     }
 }
@@ -305,8 +307,8 @@ int dauc_pd_update(float* w, const float* w0, float* w_avg, const dauc_grad_seg*
                           stream);
 }
 
-int dauc_pd_update_dense_variant(float* w, const float* g, const float* w0, float* w_avg, int64_t n,
-                                 float lr, float inv_gamma, int variant, dauc_stream_t stream) {
+static int pd_update_dense_impl(float* w, const float* g, const float* w0, float* w_avg, int64_t n, float lr,
+                                float inv_gamma, int variant, dauc_stream_t stream) {
     if (w == nullptr || g == nullptr || w0 == nullptr || n < 0) return DAUC_EINVAL;
     if (n == 0) return DAUC_OK;
     dauc_grad_seg seg{g, 0, n};
@@ -314,9 +316,16 @@ int dauc_pd_update_dense_variant(float* w, const float* g, const float* w0, floa
                           DAUC_MODE_REFERENCE, variant, stream);
 }
 
+#ifdef DAUC_TUNING
+int dauc_pd_update_dense_variant(float* w, const float* g, const float* w0, float* w_avg, int64_t n,
+                                 float lr, float inv_gamma, int variant, dauc_stream_t stream) {
+    return pd_update_dense_impl(w, g, w0, w_avg, n, lr, inv_gamma, variant, stream);
+}
+#endif
+
 int dauc_pd_update_dense(float* w, const float* g, const float* w0, float* w_avg, int64_t n,
                          float lr, float inv_gamma, dauc_stream_t stream) {
-    return dauc_pd_update_dense_variant(w, g, w0, w_avg, n, lr, inv_gamma, 0, stream);
+    return pd_update_dense_impl(w, g, w0, w_avg, n, lr, inv_gamma, 0, stream);
 }
 
 int dauc_coda_finalize(float* flat, int64_t n_avg, int world, float* lcounts, float* gcounts,

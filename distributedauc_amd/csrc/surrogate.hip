@@ -12,11 +12,11 @@
 // wave -> block -> grid in a fixed order, so results are bitwise reproducible.
 //
 // Two geometries: unit-stride batches >= 2^22 (the streaming size) take ONE launch of
-// surrogate_tail_kernel — one 4096-element chunk per workgroup, rows handed to the last 64
-// workgroups as data-as-flag words, which reduce them (see the comment at that kernel); smaller
+// surrogate_tail_kernel -- one 4096-element chunk per workgroup, rows handed to the last 64
+// workgroups as epoch-tagged granules, which reduce them (see the comment at that kernel); smaller
 // or strided batches (training, B = 256) take the persistent kernel with one last-arriver
-// ticket. The other kernels below are tuning variants kept measurable through
-// dauc_surrogate_fwdbwd_variant (include/dauc.h).
+// ticket. Tuning builds (-DDAUC_TUNING, build.py) add dauc_surrogate_fwdbwd_variant: the
+// persistent kernel at any size, the two-launch form, the stream alone, and a stamped tail.
 
 #include <hip/hip_bf16.h>
 
@@ -116,7 +116,7 @@ template <bool CLASS_ONLY>
 __device__ __forceinline__ f32x4 visit4(f32x4 h, const int (&yv)[4], const SurrogateScalars& s,
                                         Acc& acc) {
     float sp = 0.f, sn = 0.f, qp = 0.f, qn = 0.f;
-    f32x4 g;
+    f32x4 g = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
         const bool pos = (yv[c] == 1);
@@ -355,61 +355,24 @@ __global__ __launch_bounds__(kThreads) void surrogate_kernel(
     reduce_and_finalize<CLASS_ONLY>(acc, s, invB, partials, counter, out64, grad3, loss, sums4, accumulate);
 }
 
-// ---- large unit-stride batches: one chunk per workgroup + a separate row reduction -------
+// ---- large unit-stride batches: one chunk per workgroup -------------------------------------
 //
 // A grid-stride (persistent) loop walks the batch with a large stride, so concurrently open
 // DRAM pages are far apart (measured: 6.2 TB/s for this 5:4 read:write mix vs 6.5 TB/s for
 // one chunk per workgroup, scripts/probe_stream.hip). Here every workgroup takes ONE
 // contiguous chunk of 256 x 4 x S elements (the dispatcher hands chunks out roughly in
 // address order, like the update kernel's one-shot grid) and issues all of its loads
-// before any math.
-//
-// No workgroup of the streaming launch waits for anything: every WAVE reduces its 6
-// partials with DPP (no barrier, no LDS) and its lane 63 stores them as one 48-B row with
-// plain 16-B stores, then the wave stores dF/dh and exits. A second, small launch reduces
-// the rows (the kernel boundary publishes them). Measured on MI355X at B = 2^26: any
-// in-launch hand-off stalls the stream -- a per-workgroup ticket (barrier + row drain +
-// returning atomic) cost ~18 % (110 us), last-arriver spinners polling rows ~35 % (128 us),
-// because under a full streaming load every round trip to memory queues behind ~70 MB of
-// loads in flight (10-20 us per hop, scripts/probe_sur_timeline.py); the wait-free stream
-// runs at the streaming ceiling of this access mix (93 us). Fixed summation orders
-// everywhere: bitwise reproducible.
+// before any math; every WAVE reduces its 6 partials with DPP (no barrier, no LDS), the dF/dh
+// stores are issued, and ONE barrier combines the 4 wave totals into the workgroup's row.
+// Fixed summation orders everywhere: bitwise reproducible.
 constexpr int kWaves = kThreads / kWave;          // waves per workgroup
-// 1: one row per wave (no barrier in the stream kernel), 0: one row per workgroup
-#ifndef DAUC_SURROGATE_WAVE_ROWS
-#define DAUC_SURROGATE_WAVE_ROWS 0
-#endif
-constexpr int64_t kRowsPerChunk = DAUC_SURROGATE_WAVE_ROWS ? kWaves : 1;
 constexpr int kRowWords = 6;                      // s_pos, s_neg, q_pos, q_neg, n_pos, n_neg (fp64)
-#ifndef DAUC_SURROGATE_REDUCE_ROWS
-#define DAUC_SURROGATE_REDUCE_ROWS 512
-#endif
-constexpr int kRowsPerReduceBlock = DAUC_SURROGATE_REDUCE_ROWS;  // rows one workgroup of the reduce kernel sums
-static_assert(kRowsPerReduceBlock % 256 == 0, "whole rows per thread");
+constexpr int kRowsPerReduceBlock = 512;          // rows one workgroup of the two-launch reduce sums
+constexpr size_t kPersistentBytes = kCounterBytes + size_t(kMaxBlocks) * kNumAcc * sizeof(double);
 
 __host__ __device__ constexpr int64_t chunk_elems(int S) { return int64_t(kThreads) * kVec * S; }
 
 inline int64_t reduce_blocks(int64_t nrows) { return (nrows + kRowsPerReduceBlock - 1) / kRowsPerReduceBlock; }
-
-// Workspace layout: [persistent kernel: ticket + kMaxBlocks rows][chunk rows][reduce hand-off words].
-constexpr size_t kPersistentBytes = kCounterBytes + size_t(kMaxBlocks) * kNumAcc * sizeof(double);
-
-inline size_t chunk_ws_bytes(int64_t nblocks) {
-    const int64_t nrows = nblocks * kRowsPerChunk;
-    return kPersistentBytes + static_cast<size_t>(nrows + reduce_blocks(nrows)) * kRowWords * sizeof(double);
-}
-
-struct ChunkWs {
-    double* rows;      // [nblocks * kRowsPerChunk][kRowWords]
-    double* brows;     // [reduce blocks][kRowWords] encoded hand-off words (zero between calls)
-};
-
-inline ChunkWs chunk_ws(void* ws, int64_t nblocks) {
-    ChunkWs w;
-    w.rows = reinterpret_cast<double*>(static_cast<char*>(ws) + kPersistentBytes);
-    w.brows = w.rows + nblocks * kRowsPerChunk * kRowWords;
-    return w;
-}
 
 // One DPP step: the value of the source lane selected by CTRL (0 where ROWMASK disables the row).
 template <int CTRL, int ROWMASK>
@@ -448,27 +411,23 @@ __device__ __forceinline__ int wave_total_dpp(int v) {
     return v;
 }
 
-template <typename YT, bool CLASS_ONLY, int S, bool NT_LOAD, bool NT_STORE>
-__global__ __launch_bounds__(kThreads) void surrogate_chunk_kernel(
-    const float* __restrict__ h, const YT* __restrict__ y, int64_t B, double invB,
-    const float* __restrict__ abalpha, const float* __restrict__ p_hat, float* __restrict__ dh,
-    double* __restrict__ rows) {
-    SurrogateScalars s;
-    if (CLASS_ONLY) s = SurrogateScalars{};
-    else s = make_scalars(abalpha, p_hat, invB);
+// The chunk of workgroup blockIdx.x: loads, dF/dh stores, and the workgroup's row total j
+// (0..5: s_pos, s_neg, q_pos, q_neg, n_pos, n_neg; the counts as exact doubles) for each thread's
+// own j. Every thread calls it.
+template <typename YT, bool CLASS_ONLY, int S>
+__device__ __forceinline__ double stream_chunk(const float* __restrict__ h, const YT* __restrict__ y, int64_t B,
+                                               const SurrogateScalars& s, float* __restrict__ dh, int j) {
     Acc acc;
     const bool write_dh = !CLASS_ONLY && dh != nullptr;
     const int64_t base = int64_t(blockIdx.x) * chunk_elems(S);
     const bool full = base + chunk_elems(S) <= B;
-
     f32x4 hv[S];
     if (full) {
         int yv[S][4];
 #pragma unroll
         for (int k = 0; k < S; ++k) {
             const int64_t b = base + (int64_t(k) * kThreads + threadIdx.x) * kVec;
-            if (NT_LOAD) hv[k] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(h + b));
-            else hv[k] = *reinterpret_cast<const f32x4*>(h + b);
+            hv[k] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(h + b));
             load_labels4(y, b, yv[k]);
         }
 #pragma unroll
@@ -480,31 +439,17 @@ __global__ __launch_bounds__(kThreads) void surrogate_chunk_kernel(
             if (write_dh) dh[i] = g;
         }
     }
-
-    // Wave totals by DPP (lane 63), then the dF/dh stores, then ONE row per workgroup: the
-    // barrier comes after every store of the chunk has been issued, so no wave holds its
-    // stores back for it (stores need not complete before a barrier).
+    // wave totals by DPP (lane 63), then the dF/dh stores, then ONE barrier: it comes after every
+    // store of the chunk has been issued, so no wave holds its stores back for it
     const double sp = wave_total_dpp(acc.s_pos), sn = wave_total_dpp(acc.s_neg);
     const double qp = wave_total_dpp(acc.q_pos), qn = wave_total_dpp(acc.q_neg);
     const int np = wave_total_dpp(acc.n_pos), nn = wave_total_dpp(acc.n_neg);
-#if DAUC_SURROGATE_WAVE_ROWS
-    if ((threadIdx.x & (kWave - 1)) == kWave - 1) {
-        typedef double f64x2 __attribute__((ext_vector_type(2)));
-        f64x2* row = reinterpret_cast<f64x2*>(rows + (int64_t(blockIdx.x) * kWaves + threadIdx.x / kWave) * kRowWords);
-        row[0] = f64x2{sp, sn};
-        row[1] = f64x2{qp, qn};
-        row[2] = f64x2{static_cast<double>(np), static_cast<double>(nn)};
-    }
-#endif
     if (full && write_dh) {
 #pragma unroll
-        for (int k = 0; k < S; ++k) {
-            f32x4* dst = reinterpret_cast<f32x4*>(dh + base + (int64_t(k) * kThreads + threadIdx.x) * kVec);
-            if (NT_STORE) __builtin_nontemporal_store(hv[k], dst);
-            else *dst = hv[k];
-        }
+        for (int k = 0; k < S; ++k)
+            __builtin_nontemporal_store(hv[k],
+                                        reinterpret_cast<f32x4*>(dh + base + (int64_t(k) * kThreads + threadIdx.x) * kVec));
     }
-#if !DAUC_SURROGATE_WAVE_ROWS
     __shared__ double wrow[kWaves][kRowWords];
     const int wid = threadIdx.x / kWave;
     if ((threadIdx.x & (kWave - 1)) == kWave - 1) {
@@ -516,666 +461,481 @@ __global__ __launch_bounds__(kThreads) void surrogate_chunk_kernel(
         wrow[wid][5] = static_cast<double>(nn);
     }
     __syncthreads();
-    if (threadIdx.x < kRowWords) {
-        const int k = threadIdx.x;
-        rows[int64_t(blockIdx.x) * kRowWords + k] = ((wrow[0][k] + wrow[1][k]) + wrow[2][k]) + wrow[3][k];
-    }
-#endif
+    return ((wrow[0][j] + wrow[1][j]) + wrow[2][j]) + wrow[3][j];
 }
 
-// The same stream with SPAN consecutive chunks per workgroup (one contiguous span of
-// SPAN x 4096 elements): the chunk after the current one is loaded while the current one is
-// reduced and stored (two chunks of loads in flight per thread), and the launch writes SPAN
-// times fewer rows, so the row reduce shrinks to one workgroup (<= 512 rows) with no hand-off.
-// Only whole spans; the ragged tail (< SPAN chunks) is handled element-wise by the last
-// workgroup.
-template <typename YT, bool CLASS_ONLY, int S, int SPAN>
-__global__ __launch_bounds__(kThreads) void surrogate_span_kernel(
+// ---- the two-launch form: plain rows, then a small reduce launch -----------------------------
+// The stage-start class sums at large B take it (a few calls per stage); the loss takes the
+// one-launch tail kernel below. The kernel boundary publishes the rows.
+template <typename YT, bool CLASS_ONLY, int S>
+__global__ __launch_bounds__(kThreads) void surrogate_chunk_kernel(
     const float* __restrict__ h, const YT* __restrict__ y, int64_t B, double invB,
     const float* __restrict__ abalpha, const float* __restrict__ p_hat, float* __restrict__ dh,
     double* __restrict__ rows) {
     SurrogateScalars s;
     if (CLASS_ONLY) s = SurrogateScalars{};
     else s = make_scalars(abalpha, p_hat, invB);
-    Acc acc;
-    const bool write_dh = !CLASS_ONLY && dh != nullptr;
-    constexpr int64_t kChunk = chunk_elems(S);
-    const int64_t base = int64_t(blockIdx.x) * SPAN * kChunk;
-    const int64_t whole = B / (SPAN * kChunk);  // workgroups with a full span
-    if (int64_t(blockIdx.x) < whole) {
-        f32x4 cur[S], nxt[S];
-        int ycur[S][4], ynxt[S][4];
-#pragma unroll
-        for (int k = 0; k < S; ++k) {
-            const int64_t b = base + (int64_t(k) * kThreads + threadIdx.x) * kVec;
-            cur[k] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(h + b));
-            load_labels4(y, b, ycur[k]);
-        }
-        for (int c = 0; c < SPAN; ++c) {
-            const int64_t cb = base + c * kChunk;
-            if (c + 1 < SPAN) {
-#pragma unroll
-                for (int k = 0; k < S; ++k) {
-                    const int64_t b = cb + kChunk + (int64_t(k) * kThreads + threadIdx.x) * kVec;
-                    nxt[k] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(h + b));
-                    load_labels4(y, b, ynxt[k]);
-                }
-            }
-#pragma unroll
-            for (int k = 0; k < S; ++k) {
-                const f32x4 g = visit4<CLASS_ONLY>(cur[k], ycur[k], s, acc);
-                if (write_dh)
-                    __builtin_nontemporal_store(
-                        g, reinterpret_cast<f32x4*>(dh + cb + (int64_t(k) * kThreads + threadIdx.x) * kVec));
-            }
-#pragma unroll
-            for (int k = 0; k < S; ++k) {
-                cur[k] = nxt[k];
-#pragma unroll
-                for (int q = 0; q < 4; ++q) ycur[k][q] = ynxt[k][q];
-            }
-        }
-    } else {
-        // after the whole spans: one chunk per workgroup (vector path), the ragged last chunk
-        // element-wise
-        const int64_t cb = whole * SPAN * kChunk + (int64_t(blockIdx.x) - whole) * kChunk;
-        if (cb + kChunk <= B) {
-#pragma unroll
-            for (int k = 0; k < S; ++k) {
-                const int64_t b = cb + (int64_t(k) * kThreads + threadIdx.x) * kVec;
-                int yv[4];
-                load_labels4(y, b, yv);
-                const f32x4 g = visit4<CLASS_ONLY>(
-                    __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(h + b)), yv, s, acc);
-                if (write_dh) __builtin_nontemporal_store(g, reinterpret_cast<f32x4*>(dh + b));
-            }
-        } else {
-            for (int64_t i = cb + threadIdx.x; i < B; i += kThreads) {
-                const float g = visit1<CLASS_ONLY>(h[i], load_label(y, i), s, acc);
-                if (write_dh) dh[i] = g;
-            }
-        }
-    }
-    const double sp = wave_total_dpp(acc.s_pos), sn = wave_total_dpp(acc.s_neg);
-    const double qp = wave_total_dpp(acc.q_pos), qn = wave_total_dpp(acc.q_neg);
-    const int np = wave_total_dpp(acc.n_pos), nn = wave_total_dpp(acc.n_neg);
-    __shared__ double wrow[kWaves][kRowWords];
-    const int wid = threadIdx.x / kWave;
-    if ((threadIdx.x & (kWave - 1)) == kWave - 1) {
-        wrow[wid][0] = sp;
-        wrow[wid][1] = sn;
-        wrow[wid][2] = qp;
-        wrow[wid][3] = qn;
-        wrow[wid][4] = static_cast<double>(np);
-        wrow[wid][5] = static_cast<double>(nn);
-    }
-    __syncthreads();
-    if (threadIdx.x < kRowWords) {
-        const int k = threadIdx.x;
-        rows[int64_t(blockIdx.x) * kRowWords + k] = ((wrow[0][k] + wrow[1][k]) + wrow[2][k]) + wrow[3][k];
-    }
+    const int j = threadIdx.x < kRowWords ? threadIdx.x : 0;
+    const double v = stream_chunk<YT, CLASS_ONLY, S>(h, y, B, s, dh, j);
+    if (threadIdx.x < kRowWords) rows[int64_t(blockIdx.x) * kRowWords + threadIdx.x] = v;
 }
 
-// Reduce the streaming launch's rows (the kernel boundary published them): workgroup b sums
-// rows [512 b, 512 (b + 1)) in a fixed order (thread t: rows t, t + 256). Workgroups b > 0
-// hand their 6 totals to workgroup 0 as encoded 8-B words stored write-through (sc1): a word
-// is bits ^ kEmptyKey, a signalling-NaN pattern no arithmetic result or count can equal, so a
-// zero word means "not written yet" (cdna_hip_programming.md Guideline 16, R2: the data is
-// the flag, no drain, no ticket). Workgroup 0 polls those words with sc1 loads (bounded; a
-// timeout yields NaN outputs), sums them in a fixed order, zeroes them again for the next
-// call, and writes the scalars. The grid is small (<= 64 workgroups up to B = 2^27) and
-// workgroup 0 is the only one that waits, so every workgroup it waits for can run.
-constexpr unsigned long long kEmptyKey = 0x7FF4DEADBEEF0001ull;  // signalling NaN
-constexpr int kMaxPolls = 1 << 22;
-
-__device__ __forceinline__ unsigned long long enc_word(double v) {
-    return static_cast<unsigned long long>(__double_as_longlong(v)) ^ kEmptyKey;
-}
-
+// Workgroup b sums rows [512 b, 512 (b + 1)) in a fixed order (thread t: rows t, t + 256); the
+// partial totals go to a slot per workgroup and the last arriver (ticket) sums the slots in
+// workgroup order and writes the scalars.
 template <bool CLASS_ONLY>
 __global__ __launch_bounds__(kThreads) void surrogate_rows_reduce_kernel(
-    double* __restrict__ rows, int64_t nrows, ChunkWs ws, double invB, const float* __restrict__ abalpha,
-    const float* __restrict__ p_hat, double* __restrict__ out64, float* __restrict__ grad3, float* __restrict__ loss,
-    double* __restrict__ sums4, int accumulate) {
+    double* __restrict__ rows, int64_t nrows, double* __restrict__ partials, unsigned* __restrict__ counter,
+    double invB, const float* __restrict__ abalpha, const float* __restrict__ p_hat, double* __restrict__ out64,
+    float* __restrict__ grad3, float* __restrict__ loss, double* __restrict__ sums4, int accumulate) {
     __shared__ double scratch[kNumAcc * kWaves];
-    // Workgroup 0's scalar inputs are read up front: after the hand-off they would be one more
-    // dependent round trip to memory at the very end of the call.
-    __shared__ int bad;
-    if (threadIdx.x == 0) bad = 0;  // ordered before any write by block_sum's barriers
-    float sc[4] = {0.f, 0.f, 0.f, 0.f};
-    if (!CLASS_ONLY && blockIdx.x == 0) {
-        sc[0] = abalpha[0];
-        sc[1] = abalpha[1];
-        sc[2] = abalpha[2];
-        sc[3] = p_hat[0];
-    }
+    __shared__ int last_flag;
     double tot[kNumAcc];
 #pragma unroll
     for (int k = 0; k < kNumAcc; ++k) tot[k] = 0.0;
     const int64_t r0 = int64_t(blockIdx.x) * kRowsPerReduceBlock;
     const int64_t r1 = (r0 + kRowsPerReduceBlock < nrows) ? r0 + kRowsPerReduceBlock : nrows;
-    // all of a thread's rows in flight at once (rows t, t + 256, ...: a fixed order)
-    typedef double f64x2 __attribute__((ext_vector_type(2)));
-    constexpr int kPer = kRowsPerReduceBlock / kThreads;
-    f64x2 v[kPer][3];
+    for (int64_t r = r0 + threadIdx.x; r < r1; r += kThreads) {
 #pragma unroll
-    for (int j = 0; j < kPer; ++j) {
-        const int64_t r = r0 + threadIdx.x + int64_t(j) * kThreads;
-#pragma unroll
-        for (int q = 0; q < 3; ++q)
-            v[j][q] = r < r1 ? reinterpret_cast<const f64x2*>(rows + r * kRowWords)[q] : f64x2{0.0, 0.0};
-    }
-#pragma unroll
-    for (int j = 0; j < kPer; ++j) {
-#pragma unroll
-        for (int q = 0; q < 3; ++q) {
-            tot[2 * q] += v[j][q].x;
-            tot[2 * q + 1] += v[j][q].y;
-        }
+        for (int k = 0; k < kNumAcc; ++k) tot[k] += rows[r * kRowWords + k];
     }
     block_sum<kNumAcc>(tot, scratch);
-    // The rows are zeroed again for the next call only after the totals are on their way:
-    // stores count in vmcnt, so zeroing before the sums would put their write acks on the
-    // critical path.
-    auto zero_rows = [&]() {
-#pragma unroll
-        for (int j = 0; j < kPer; ++j) {
-            const int64_t r = r0 + threadIdx.x + int64_t(j) * kThreads;
-            if (r < r1) {
-#pragma unroll
-                for (int q = 0; q < 3; ++q) reinterpret_cast<f64x2*>(rows + r * kRowWords)[q] = f64x2{0.0, 0.0};
-            }
-        }
-    };
-    unsigned long long* words = reinterpret_cast<unsigned long long*>(ws.brows);
-    if (blockIdx.x > 0) {
+    if (gridDim.x > 1) {
         if (threadIdx.x == 0) {
 #pragma unroll
-            for (int k = 0; k < kNumAcc; ++k)
-                __hip_atomic_store((gu64*)(words + int64_t(blockIdx.x) * kRowWords + k), enc_word(tot[k]),
-                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            for (int k = 0; k < kNumAcc; ++k) store_sc1(&partials[blockIdx.x * kNumAcc + k], tot[k]);
         }
-        zero_rows();
-        return;
-    }
-    zero_rows();
-    bool ok = true;
-    if (gridDim.x > 1) {
-        double rest[kNumAcc];
+        if (!arrive_last(counter, gridDim.x, &last_flag)) return;
 #pragma unroll
-        for (int k = 0; k < kNumAcc; ++k) rest[k] = 0.0;
-        for (int b = 1 + threadIdx.x; b < static_cast<int>(gridDim.x); b += kThreads) {
-            unsigned long long* row = words + int64_t(b) * kRowWords;
-            unsigned long long w[kRowWords];
+        for (int k = 0; k < kNumAcc; ++k) tot[k] = 0.0;
+        for (int b = threadIdx.x; b < static_cast<int>(gridDim.x); b += kThreads) {
 #pragma unroll
-            for (int k = 0; k < kRowWords; ++k)
-                w[k] = __hip_atomic_load((gu64*)(row + k), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            for (int polls = 0;; ++polls) {
-                bool missing = false;
-#pragma unroll
-                for (int k = 0; k < kRowWords; ++k) missing |= (w[k] == 0ull);
-                if (!missing) break;
-                if (polls >= kMaxPolls) {
-                    ok = false;
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(2);
-#pragma unroll
-                for (int k = 0; k < kRowWords; ++k)
-                    if (w[k] == 0ull)
-                        w[k] = __hip_atomic_load((gu64*)(row + k), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-#pragma unroll
-            for (int k = 0; k < kRowWords; ++k) {
-                rest[k] += __longlong_as_double(static_cast<long long>(w[k] ^ kEmptyKey));
-                __hip_atomic_store((gu64*)(row + k), 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
+            for (int k = 0; k < kNumAcc; ++k) tot[k] += load_sc1(&partials[b * kNumAcc + k]);
         }
-        // a timed-out poll in any thread: an LDS flag (block_sum's barriers order it) instead of
-        // __syncthreads_or, whose block-size read would be one more memory trip at the end
-        if (!ok) bad = 1;
-        block_sum<kNumAcc>(rest, scratch);
-        ok = bad == 0;
-#pragma unroll
-        for (int k = 0; k < kNumAcc; ++k) tot[k] += rest[k];
+        block_sum<kNumAcc>(tot, scratch);
     }
     if (threadIdx.x == 0) {
-        if (!ok) {
-#pragma unroll
-            for (int k = 0; k < kNumAcc; ++k) tot[k] = __builtin_nan("");
-        }
         if (CLASS_ONLY) {
             emit_class_sums(tot, sums4, accumulate);
         } else {
-            const SurrogateScalars s = make_scalars_v(sc[0], sc[1], sc[2], sc[3], invB);
+            const SurrogateScalars s = make_scalars(abalpha, p_hat, invB);
             finalize(tot, s, invB, out64, grad3, loss);
         }
     }
 }
 
-// ---- the same stream in ONE launch: start-order tickets ------------------------------------
+// ---- the loss in ONE launch: the stream, its rows reduced by the LAST R workgroups ---------
 //
-// Workgroups are grouped by blockIdx (kTicketGroup consecutive chunks). A workgroup's FIRST
-// instruction is a returning ticket add on its group's counter; the reply travels while the
-// chunk's loads are in flight, so nobody waits for it. The workgroup that draws its group's
-// last ticket is the last one of the group to START: every other member is already resident
-// and waits for nothing, so it may poll their rows (data-as-flag words, as above) after its
-// own chunk without any risk of waiting for a workgroup that cannot run. It sums the group's
-// rows in blockIdx order, zeroes them, publishes the group total as data-as-flag words and
-// draws a ticket on the final counter; the group reducer that draws the last of those (every
-// other group reducer has already published) sums the group totals in group order and writes
-// the scalars. Only ngroups + 1 workgroups ever wait, each near the end of its own life, and
-// the summation order is fixed by blockIdx: bitwise reproducible, same as the two-launch form.
-constexpr int kTicketGroupMin = 64;            // smallest group of any variant (sizes the workspace)
-constexpr int kCtrStrideMax = 16384;           // widest counter spacing of any variant (64 KB)
+// Every workgroup streams its chunk and publishes its row as tagged 8-byte granules (Guideline
+// 16, R2: the data is the flag; ONE write-through store per granule, no drain, no ticket):
+// granule = {tag (32 bits), payload (32 bits)}, a row = the hi and lo halves of its 4 fp64 sums
+// and its 2 counts = 10 granules. The tag is the call's epoch: every workgroup reads the epoch
+// word of the workspace header at its start, and the final reducer advances it as its very last
+// action (when every row of the call has arrived, so every workgroup has read it). A granule
+// left over from an earlier call -- even one written after that call gave up waiting for it --
+// carries an older tag and is never taken for a current one, and nothing is re-zeroed between
+// calls (tag = epoch | 2^31, so a zeroed workspace holds no valid granule either).
+//
+// The last R workgroups by blockIdx are the reducers: reducer r, after its own chunk and row,
+// takes the rows of group r (a contiguous range of ceil(nblocks / R) rows; one row per thread,
+// only granules not yet current are polled, bounded) and publishes the group total the same way;
+// reducer R-1 (whose group holds the grid's last rows) loads the other R-1 group totals BEFORE
+// waiting on its own group (their trip overlaps its wait), adds them in group order and writes
+// the scalars. A poll that times out makes the outputs NaN (a group reducer then publishes NaN
+// totals), and the epoch still advances. Nothing waits on a workgroup that waits: every row a
+// reducer needs comes from a workgroup that never waits (or from a reducer's own row, stored
+// before it waits). Fixed summation order: bitwise reproducible.
+constexpr int kGran = 10;                   // granules per row / group total
+constexpr int kMaxPolls = 1 << 22;
 
-__host__ __device__ inline int64_t ticket_groups(int64_t nblocks, int G = kTicketGroupMin) { return (nblocks + G - 1) / G; }
-
-struct TicketWs {
-    unsigned* ctr;                 // [ngroups + 1] * kCtrStride; [ngroups * kCtrStride] is the final counter
-    unsigned long long* rows;      // [nblocks][kRowWords] encoded
-    unsigned long long* gwords;    // [ngroups][kRowWords] encoded
+struct TailWs {
+    unsigned* epoch;               // header word
+    unsigned long long* rows;      // [nblocks][kGran]
+    unsigned long long* gtot;      // [R][kGran]
+    unsigned long long* stamps;    // tuning builds: [nblocks + 8 R] s_memrealtime stamps (nullable)
 };
 
-inline size_t align256(size_t b) { return (b + 255) / 256 * 256; }
+constexpr size_t kTailHeader = 256;
 
-// sized for the smallest group and the widest counter spacing of any variant
-inline size_t ticket_ws_bytes(int64_t nblocks) {
-    const int64_t ng = ticket_groups(nblocks);
-    return kPersistentBytes + align256(size_t(ng + 1) * kCtrStrideMax * 4) +
-           align256(size_t(nblocks) * kRowWords * 8) + size_t(ng) * kRowWords * 8;
+inline size_t tail_ws_bytes(int64_t nblocks, int R, bool stamps = false) {
+    return kTailHeader + size_t(nblocks + R) * kGran * 8 + (stamps ? size_t(nblocks + 8 * R) * 8 : 0);
 }
 
-inline TicketWs ticket_ws(void* ws, int64_t nblocks) {
-    const int64_t ng = ticket_groups(nblocks);
-    char* p = static_cast<char*>(ws) + kPersistentBytes;
-    TicketWs w;
-    w.ctr = reinterpret_cast<unsigned*>(p);
-    p += align256(size_t(ng + 1) * kCtrStrideMax * 4);
-    w.rows = reinterpret_cast<unsigned long long*>(p);
-    p += align256(size_t(nblocks) * kRowWords * 8);
-    w.gwords = reinterpret_cast<unsigned long long*>(p);
+inline TailWs tail_ws(void* ws, int64_t nblocks, int R, bool stamps = false) {
+    char* p = static_cast<char*>(ws);
+    TailWs w;
+    w.epoch = reinterpret_cast<unsigned*>(p);
+    w.rows = reinterpret_cast<unsigned long long*>(p + kTailHeader);
+    w.gtot = w.rows + nblocks * kGran;
+    w.stamps = stamps ? w.gtot + int64_t(R) * kGran : nullptr;
     return w;
 }
 
-// Take nrows encoded rows (thread t: rows t, t + 256, then the next 512, ...): every word of a
-// pass is loaded before any is examined, only the missing ones are polled again (bounded; a
-// timeout leaves NaN), each is re-zeroed, and tot[] sums them in that fixed order.
-__device__ __forceinline__ void take_rows(unsigned long long* words, int64_t nrows, double (&tot)[kNumAcc],
-                                          bool& ok) {
-    for (int64_t r0 = threadIdx.x; r0 < nrows; r0 += 2 * kThreads) {
-        const int64_t r1 = r0 + kThreads;
-        const bool two = r1 < nrows;
-        unsigned long long w[2][kRowWords];
-#pragma unroll
-        for (int k = 0; k < kRowWords; ++k) {
-            w[0][k] = __hip_atomic_load((gu64*)(words + r0 * kRowWords + k), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            w[1][k] = two ? __hip_atomic_load((gu64*)(words + r1 * kRowWords + k), __ATOMIC_RELAXED,
-                                              __HIP_MEMORY_SCOPE_AGENT)
-                          : ~0ull;
-        }
-        for (int polls = 0;; ++polls) {
-            bool missing = false;
-#pragma unroll
-            for (int j = 0; j < 2; ++j)
-#pragma unroll
-                for (int k = 0; k < kRowWords; ++k) missing |= (w[j][k] == 0ull);
-            if (!missing) break;
-            if (polls >= kMaxPolls) {
-                ok = false;
-                break;
-            }
-            __builtin_amdgcn_s_sleep(2);
-#pragma unroll
-            for (int j = 0; j < 2; ++j)
-#pragma unroll
-                for (int k = 0; k < kRowWords; ++k)
-                    if (w[j][k] == 0ull)
-                        w[j][k] = __hip_atomic_load((gu64*)(words + (j ? r1 : r0) * kRowWords + k), __ATOMIC_RELAXED,
-                                                    __HIP_MEMORY_SCOPE_AGENT);
-        }
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            if (j == 1 && !two) break;
-#pragma unroll
-            for (int k = 0; k < kRowWords; ++k) {
-                tot[k] += __longlong_as_double(static_cast<long long>(w[j][k] ^ kEmptyKey));
-                __hip_atomic_store((gu64*)(words + (j ? r1 : r0) * kRowWords + k), 0ull, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-            }
-        }
-    }
+__device__ __forceinline__ unsigned long long gran(unsigned tag, unsigned payload) {
+    return (static_cast<unsigned long long>(tag) << 32) | payload;
 }
 
-// take_rows with one row per thread per pass: 12 fewer live VGPRs, which keeps a kernel that
-// also streams (surrogate_tail_kernel) at the stream's own occupancy
-__device__ __forceinline__ void take_rows_narrow(unsigned long long* words, int64_t nrows, double (&tot)[kNumAcc],
-                                                 bool& ok) {
-    for (int64_t r0 = threadIdx.x; r0 < nrows; r0 += kThreads) {
-        unsigned long long w[kRowWords];
-#pragma unroll
-        for (int k = 0; k < kRowWords; ++k)
-            w[k] = __hip_atomic_load((gu64*)(words + r0 * kRowWords + k), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        for (int polls = 0;; ++polls) {
-            bool missing = false;
-#pragma unroll
-            for (int k = 0; k < kRowWords; ++k) missing |= (w[k] == 0ull);
-            if (!missing) break;
-            if (polls >= kMaxPolls) {
-                ok = false;
-                break;
-            }
-            __builtin_amdgcn_s_sleep(2);
-#pragma unroll
-            for (int k = 0; k < kRowWords; ++k)
-                if (w[k] == 0ull)
-                    w[k] = __hip_atomic_load((gu64*)(words + r0 * kRowWords + k), __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_AGENT);
-        }
-#pragma unroll
-        for (int k = 0; k < kRowWords; ++k) {
-            tot[k] += __longlong_as_double(static_cast<long long>(w[k] ^ kEmptyKey));
-            __hip_atomic_store((gu64*)(words + r0 * kRowWords + k), 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
+// Granule k of a row: k = 0..3 the hi halves, 4..7 the lo halves of sums 0..3, 8..9 the counts.
+// The total granule k carries:
+__device__ __forceinline__ int gran_total(int k) { return k < 8 ? (k & 3) : k - 4; }
+
+// thread k < kGran stores granule k of a row; v = the thread's total gran_total(k)
+__device__ __forceinline__ void publish_granule(unsigned long long* row, unsigned tag, double v) {
+    const int k = threadIdx.x;
+    if (k >= kGran) return;
+    const unsigned long long b = static_cast<unsigned long long>(__double_as_longlong(v));
+    // counts: exact integers < 2^32
+    const unsigned payload = k < 4 ? static_cast<unsigned>(b >> 32) : (k < 8 ? static_cast<unsigned>(b) : static_cast<unsigned>(v));
+    __hip_atomic_store((gu64*)(row + k), gran(tag, payload), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <typename YT, bool CLASS_ONLY, int S, int kTicketGroup, int kCtrStride, bool TICKET_FIRST>
-__global__ __launch_bounds__(kThreads) void surrogate_ticket_kernel(
+// a row's 10 payloads (tags already checked) added to its 6 totals
+__device__ __forceinline__ void add_row(const unsigned (&p)[kGran], double (&t)[kRowWords]) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        t[k] += __longlong_as_double(static_cast<long long>((static_cast<unsigned long long>(p[k]) << 32) | p[k + 4]));
+    t[4] += static_cast<double>(p[8]);
+    t[5] += static_cast<double>(p[9]);
+}
+
+// All granules of one row, loaded together (every load in flight before any is examined): their
+// payloads, and a bit per granule that does not carry `tag` yet.
+__device__ __forceinline__ unsigned poll_row(const unsigned long long* row, unsigned tag, unsigned (&p)[kGran]) {
+    unsigned long long g[kGran];
+#pragma unroll
+    for (int k = 0; k < kGran; ++k)
+        g[k] = __hip_atomic_load((gu64*)(row + k), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned missing = 0u;
+#pragma unroll
+    for (int k = 0; k < kGran; ++k) {
+        p[k] = static_cast<unsigned>(g[k]);
+        missing |= unsigned(static_cast<unsigned>(g[k] >> 32) != tag) << k;
+    }
+    return missing;
+}
+
+// Poll until every granule of `row` carries `tag` (bounded; the whole row is re-read each time);
+// false on timeout.
+__device__ __forceinline__ bool wait_row(const unsigned long long* row, unsigned tag, unsigned missing,
+                                         unsigned (&p)[kGran]) {
+    for (int polls = 0; missing; ++polls) {
+        if (polls >= kMaxPolls) return false;
+        __builtin_amdgcn_s_sleep(2);
+        missing = poll_row(row, tag, p);
+    }
+    return true;
+}
+
+__device__ __forceinline__ unsigned long long realtime() { return __builtin_amdgcn_s_memrealtime(); }
+
+// REDUCE = false: the stream with its row stores and nobody reducing (a timing variant).
+// Waves per SIMD the register allocation must allow: the streaming chunk kernel alone runs at 8.
+#ifndef DAUC_TAIL_WAVES
+#define DAUC_TAIL_WAVES 1
+#endif
+// 1: the final reducer loads the other group totals before it waits on its own group
+#ifndef DAUC_TAIL_PREPOLL
+#define DAUC_TAIL_PREPOLL 0
+#endif
+template <typename YT, int S, int R, bool REDUCE, bool STAMPS>
+__global__ __launch_bounds__(kThreads, DAUC_TAIL_WAVES) void surrogate_tail_kernel(
     const float* __restrict__ h, const YT* __restrict__ y, int64_t B, double invB,
-    const float* __restrict__ abalpha, const float* __restrict__ p_hat, float* __restrict__ dh, TicketWs ws,
-    double* __restrict__ out64, float* __restrict__ grad3, float* __restrict__ loss, double* __restrict__ sums4,
-    int accumulate) {
+    const float* __restrict__ abalpha, const float* __restrict__ p_hat, float* __restrict__ dh, TailWs ws,
+    double* __restrict__ out64, float* __restrict__ grad3, float* __restrict__ loss) {
+    const unsigned epoch = __builtin_amdgcn_readfirstlane(
+        __hip_atomic_load((gu32*)ws.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    const unsigned tag = epoch | 0x80000000u;
+    // uniform scalar inputs (scalar registers); the final reducer rebuilds its fp64 scalars from
+    // them at the end instead of keeping them live through the stream and the reduce
+    const float sa = abalpha[0], sb = abalpha[1], sal = abalpha[2], sp = p_hat[0];
     const int64_t nblocks = gridDim.x;
-    const int64_t ngroups = ticket_groups(nblocks, kTicketGroup);
-    const int64_t grp = blockIdx.x / kTicketGroup;
-    const int64_t g0 = grp * kTicketGroup;
-    const int64_t gsize = (nblocks - g0 < kTicketGroup) ? nblocks - g0 : kTicketGroup;
-    unsigned ticket = 0;
-    // an opaque per-lane zero keeps the address divergent, so the atomic optimizer does not
-    // rewrite the add into a wave-aggregated form that waits for the reply right away
-    auto draw = [&]() {
-        if (threadIdx.x == 0) {
-            int zero;
-            asm volatile("v_mov_b32 %0, 0" : "=v"(zero));
-            ticket = __hip_atomic_fetch_add((gu32*)(ws.ctr + grp * kCtrStride + zero), 1u, __ATOMIC_RELAXED,
-                                            __HIP_MEMORY_SCOPE_AGENT);
-        }
-    };
-    if (TICKET_FIRST) draw();
-
-    SurrogateScalars s;
-    if (CLASS_ONLY) s = SurrogateScalars{};
-    else s = make_scalars(abalpha, p_hat, invB);
-    Acc acc;
-    const bool write_dh = !CLASS_ONLY && dh != nullptr;
-    const int64_t base = int64_t(blockIdx.x) * chunk_elems(S);
-    const bool full = base + chunk_elems(S) <= B;
-    f32x4 hv[S];
-    if (full) {
-        int yv[S][4];
-#pragma unroll
-        for (int k = 0; k < S; ++k) {
-            const int64_t b = base + (int64_t(k) * kThreads + threadIdx.x) * kVec;
-            hv[k] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(h + b));
-            load_labels4(y, b, yv[k]);
-        }
-        if (!TICKET_FIRST) draw();  // issued behind the loads: waiting for them does not wait for it
-#pragma unroll
-        for (int k = 0; k < S; ++k) hv[k] = visit4<CLASS_ONLY>(hv[k], yv[k], s, acc);
-    } else {
-        if (!TICKET_FIRST) draw();
-        for (int64_t i = base + threadIdx.x; i < B; i += kThreads) {
-            const float g = visit1<CLASS_ONLY>(h[i], load_label(y, i), s, acc);
-            if (write_dh) dh[i] = g;
-        }
+    {
+        const SurrogateScalars s = make_scalars_v(sa, sb, sal, sp, invB);
+        const double v = stream_chunk<YT, false, S>(h, y, B, s, dh, gran_total(threadIdx.x < kGran ? threadIdx.x : 0));
+        publish_granule(ws.rows + int64_t(blockIdx.x) * kGran, tag, v);
+        if (STAMPS && threadIdx.x == 0) ws.stamps[blockIdx.x] = realtime();
     }
-    const double sp = wave_total_dpp(acc.s_pos), sn = wave_total_dpp(acc.s_neg);
-    const double qp = wave_total_dpp(acc.q_pos), qn = wave_total_dpp(acc.q_neg);
-    const int np = wave_total_dpp(acc.n_pos), nn = wave_total_dpp(acc.n_neg);
-    if (full && write_dh) {
-#pragma unroll
-        for (int k = 0; k < S; ++k)
-            __builtin_nontemporal_store(hv[k], reinterpret_cast<f32x4*>(dh + base + (int64_t(k) * kThreads + threadIdx.x) * kVec));
-    }
-    __shared__ double wrow[kWaves][kRowWords];
-    __shared__ int role;  // 0: done, 1: group reducer
-    const int wid = threadIdx.x / kWave;
-    if ((threadIdx.x & (kWave - 1)) == kWave - 1) {
-        wrow[wid][0] = sp;
-        wrow[wid][1] = sn;
-        wrow[wid][2] = qp;
-        wrow[wid][3] = qn;
-        wrow[wid][4] = static_cast<double>(np);
-        wrow[wid][5] = static_cast<double>(nn);
-    }
-    if (threadIdx.x == 0) role = (ticket == gsize - 1);
-    __syncthreads();
-    if (threadIdx.x < kRowWords) {
-        const int k = threadIdx.x;
-        const double v = ((wrow[0][k] + wrow[1][k]) + wrow[2][k]) + wrow[3][k];
-        __hip_atomic_store((gu64*)(ws.rows + int64_t(blockIdx.x) * kRowWords + k), enc_word(v), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-    }
-    if (!role) return;
-
-    // group reducer: rows g0 .. g0 + gsize in blockIdx order
-    __shared__ double scratch[kNumAcc * kWaves];
-    __shared__ int fin;
-    bool ok = true;
-    double tot[kNumAcc];
-#pragma unroll
-    for (int k = 0; k < kNumAcc; ++k) tot[k] = 0.0;
-    take_rows(ws.rows + g0 * kRowWords, gsize, tot, ok);
-    block_sum<kNumAcc>(tot, scratch);
-    if (threadIdx.x < kRowWords) {
-        double v = tot[0];
-#pragma unroll
-        for (int k = 1; k < kNumAcc; ++k)
-            if (threadIdx.x == k) v = tot[k];
-        __hip_atomic_store((gu64*)(ws.gwords + grp * kRowWords + threadIdx.x), enc_word(v), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-    }
-    if (threadIdx.x == 0) {
-        // every ticket of this group has been drawn: leave the counter zeroed for the next call
-        __hip_atomic_store((gu32*)(ws.ctr + grp * kCtrStride), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const unsigned f = __hip_atomic_fetch_add((gu32*)(ws.ctr + ngroups * kCtrStride), 1u, __ATOMIC_RELAXED,
-                                                  __HIP_MEMORY_SCOPE_AGENT);
-        fin = (f == ngroups - 1);
-        if (fin)
-            __hip_atomic_store((gu32*)(ws.ctr + ngroups * kCtrStride), 0u, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-    }
-    ok = __syncthreads_or(!ok) == 0;
-    if (!fin) return;
-
-    // final reducer: the group totals in group order
-#pragma unroll
-    for (int k = 0; k < kNumAcc; ++k) tot[k] = 0.0;
-    take_rows(ws.gwords, ngroups, tot, ok);
-    block_sum<kNumAcc>(tot, scratch);
-    ok = __syncthreads_or(!ok) == 0;
-    if (threadIdx.x == 0) {
-        if (!ok) {
-#pragma unroll
-            for (int k = 0; k < kNumAcc; ++k) tot[k] = __builtin_nan("");
-        }
-        if (CLASS_ONLY) emit_class_sums(tot, sums4, accumulate);
-        else finalize(tot, s, invB, out64, grad3, loss);
-    }
-}
-
-// ---- the stream with its row reduce in the same launch: the LAST R workgroups reduce ---------
-//
-// Every workgroup streams its chunk (as surrogate_chunk_kernel) and stores its 48-B row as
-// data-as-flag words (bits ^ kEmptyKey, agent-scope stores; no drain, no ticket). The last R
-// workgroups by blockIdx are the reducers: reducer r, after its own chunk and row, takes the rows
-// of group r (a contiguous range of ceil(nblocks / R) rows; take_rows: polls only words still
-// zero, bounded, re-zeroes what it consumed, fixed summation order), and publishes the group total
-// the same way; reducer R-1 takes the other R-1 group totals (in group order, then its own) and
-// writes the scalars.
-// Nothing waits on a workgroup that waits: the rows every reducer needs come from workgroups that
-// never wait (and from the reducers' own rows, stored before they reduce), and at most R of the
-// grid's resident slots are ever held by waiting workgroups. Bitwise reproducible.
-// EXTRA: the R reducers are R extra workgroups after the nstream streaming ones (they stream
-// nothing; a streaming workgroup never waits) instead of the last R streaming workgroups.
-template <typename YT, int S, int R, bool EXTRA, bool NO_REDUCE = false>
-__global__ __launch_bounds__(kThreads) void surrogate_tail_kernel(
-    const float* __restrict__ h, const YT* __restrict__ y, int64_t B, double invB,
-    const float* __restrict__ abalpha, const float* __restrict__ p_hat, float* __restrict__ dh,
-    unsigned long long* __restrict__ rows, unsigned long long* __restrict__ gwords,
-    double* __restrict__ out64, float* __restrict__ grad3, float* __restrict__ loss, int64_t nstream) {
-    const SurrogateScalars s = make_scalars(abalpha, p_hat, invB);
-    if (!EXTRA || int64_t(blockIdx.x) < nstream) {
-    Acc acc;
-    const bool write_dh = dh != nullptr;
-    const int64_t base = int64_t(blockIdx.x) * chunk_elems(S);
-    const bool full = base + chunk_elems(S) <= B;
-    f32x4 hv[S];
-    if (full) {
-        int yv[S][4];
-#pragma unroll
-        for (int k = 0; k < S; ++k) {
-            const int64_t b = base + (int64_t(k) * kThreads + threadIdx.x) * kVec;
-            hv[k] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(h + b));
-            load_labels4(y, b, yv[k]);
-        }
-#pragma unroll
-        for (int k = 0; k < S; ++k) hv[k] = visit4<false>(hv[k], yv[k], s, acc);
-    } else {
-        for (int64_t i = base + threadIdx.x; i < B; i += kThreads) {
-            const float g = visit1<false>(h[i], load_label(y, i), s, acc);
-            if (write_dh) dh[i] = g;
-        }
-    }
-    const double sp = wave_total_dpp(acc.s_pos), sn = wave_total_dpp(acc.s_neg);
-    const double qp = wave_total_dpp(acc.q_pos), qn = wave_total_dpp(acc.q_neg);
-    const int np = wave_total_dpp(acc.n_pos), nn = wave_total_dpp(acc.n_neg);
-    if (full && write_dh) {
-#pragma unroll
-        for (int k = 0; k < S; ++k)
-            __builtin_nontemporal_store(hv[k], reinterpret_cast<f32x4*>(dh + base + (int64_t(k) * kThreads + threadIdx.x) * kVec));
-    }
-    __shared__ double wrow[kWaves][kRowWords];
-    const int wid = threadIdx.x / kWave;
-    if ((threadIdx.x & (kWave - 1)) == kWave - 1) {
-        wrow[wid][0] = sp;
-        wrow[wid][1] = sn;
-        wrow[wid][2] = qp;
-        wrow[wid][3] = qn;
-        wrow[wid][4] = static_cast<double>(np);
-        wrow[wid][5] = static_cast<double>(nn);
-    }
-    __syncthreads();
-    if (threadIdx.x < kRowWords) {
-        const int k = threadIdx.x;
-        const double v = ((wrow[0][k] + wrow[1][k]) + wrow[2][k]) + wrow[3][k];
-        __hip_atomic_store((gu64*)(rows + int64_t(blockIdx.x) * kRowWords + k), enc_word(v), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-    }
-    }
-    const int64_t nblocks = EXTRA ? nstream : int64_t(gridDim.x);  // rows
     const int64_t nred = nblocks < R ? nblocks : R;
-    const int64_t r = EXTRA ? int64_t(blockIdx.x) - nstream : int64_t(blockIdx.x) - (nblocks - nred);
-    if (r < 0 || r >= nred || NO_REDUCE) return;
+    const int64_t r = int64_t(blockIdx.x) - (nblocks - nred);
+    if (!REDUCE || r < 0) return;
 
-    // reducer r: the rows of group r; reducer nred - 1 (whose group holds the grid's last rows)
-    // also takes the other group totals, loaded before its own group so that their trip overlaps
-    // its wait, and adds its own total from registers: one memory trip after the last row lands
     __shared__ double scratch[kNumAcc * kWaves];
     const int64_t G = (nblocks + nred - 1) / nred;
     const int64_t g0 = r * G, g1 = (g0 + G < nblocks) ? g0 + G : nblocks;
     const bool final_red = r == nred - 1;
     const bool holds = final_red && threadIdx.x < nred - 1;  // thread t: group total t
-    unsigned long long gw[kRowWords];
-    if (holds) {
-#pragma unroll
-        for (int k = 0; k < kRowWords; ++k)
-            gw[k] = __hip_atomic_load((gu64*)(gwords + threadIdx.x * kRowWords + k), __ATOMIC_RELAXED,
-                                      __HIP_MEMORY_SCOPE_AGENT);
-    }
+    unsigned long long* st = STAMPS ? ws.stamps + nblocks + 8 * r : nullptr;
+    if (STAMPS && threadIdx.x == 0) st[0] = realtime();
+#if DAUC_TAIL_PREPOLL
+    unsigned gp[kGran], gmiss = 0u;
+    if (holds) gmiss = poll_row(ws.gtot + threadIdx.x * kGran, tag, gp);
+#endif
     bool ok = true;
     double tot[kNumAcc];
 #pragma unroll
     for (int k = 0; k < kNumAcc; ++k) tot[k] = 0.0;
-    if (g1 > g0) take_rows_narrow(rows + g0 * kRowWords, g1 - g0, tot, ok);
-    block_sum<kNumAcc>(tot, scratch);
-    if (!final_red) {
-        if (threadIdx.x < kRowWords) {
-            double v = tot[0];
-#pragma unroll
-            for (int k = 1; k < kNumAcc; ++k)
-                if (threadIdx.x == k) v = tot[k];
-            __hip_atomic_store((gu64*)(gwords + r * kRowWords + threadIdx.x), enc_word(v), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
+    for (int64_t i = g0 + threadIdx.x; i < g1; i += kThreads) {
+        unsigned p[kGran];
+        const unsigned miss = poll_row(ws.rows + i * kGran, tag, p);
+        if (!wait_row(ws.rows + i * kGran, tag, miss, p)) {
+            ok = false;
+            break;
         }
+        add_row(p, tot);
+    }
+    if (STAMPS && threadIdx.x == 0) st[1] = realtime();
+    __shared__ int bad;
+    if (threadIdx.x == 0) bad = 0;
+    __syncthreads();
+    if (!ok) bad = 1;
+    block_sum<kNumAcc>(tot, scratch);  // its barriers order the flag
+    ok = bad == 0;
+    if (STAMPS && threadIdx.x == 0) st[2] = realtime();
+    if (!final_red) {
+        if (!ok) {
+#pragma unroll
+            for (int k = 0; k < kNumAcc; ++k) tot[k] = __builtin_nan("");
+        }
+        double v = tot[0];
+#pragma unroll
+        for (int k = 1; k < kNumAcc; ++k)
+            if (threadIdx.x < kGran && gran_total(threadIdx.x) == k) v = tot[k];
+        publish_granule(ws.gtot + r * kGran, tag, v);
+        if (STAMPS && threadIdx.x == 0) st[3] = realtime();
         return;
     }
     double rest[kNumAcc];
 #pragma unroll
     for (int k = 0; k < kNumAcc; ++k) rest[k] = 0.0;
     if (holds) {
-        for (int polls = 0;; ++polls) {
-            bool missing = false;
-#pragma unroll
-            for (int k = 0; k < kRowWords; ++k) missing |= (gw[k] == 0ull);
-            if (!missing) break;
-            if (polls >= kMaxPolls) {
-                ok = false;
-                break;
-            }
-            __builtin_amdgcn_s_sleep(2);
-#pragma unroll
-            for (int k = 0; k < kRowWords; ++k)
-                if (gw[k] == 0ull)
-                    gw[k] = __hip_atomic_load((gu64*)(gwords + threadIdx.x * kRowWords + k), __ATOMIC_RELAXED,
-                                              __HIP_MEMORY_SCOPE_AGENT);
-        }
-#pragma unroll
-        for (int k = 0; k < kRowWords; ++k) {
-            rest[k] = __longlong_as_double(static_cast<long long>(gw[k] ^ kEmptyKey));
-            __hip_atomic_store((gu64*)(gwords + threadIdx.x * kRowWords + k), 0ull, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-        }
+#if !DAUC_TAIL_PREPOLL
+        unsigned gp[kGran];
+        const unsigned gmiss = poll_row(ws.gtot + threadIdx.x * kGran, tag, gp);
+#endif
+        if (wait_row(ws.gtot + threadIdx.x * kGran, tag, gmiss, gp)) add_row(gp, rest);
+        else ok = false;
     }
+    if (STAMPS && threadIdx.x == 0) st[4] = realtime();
+    if (!ok) bad = 1;
     block_sum<kNumAcc>(rest, scratch);
-    ok = __syncthreads_or(!ok) == 0;
+    ok = bad == 0;
     if (threadIdx.x == 0) {
 #pragma unroll
         for (int k = 0; k < kNumAcc; ++k) tot[k] = ok ? rest[k] + tot[k] : __builtin_nan("");
-        finalize(tot, s, invB, out64, grad3, loss);
+        finalize(tot, make_scalars_v(sa, sb, sal, sp, invB), invB, out64, grad3, loss);
+        // the call's last action: every workgroup has read the epoch (its row has arrived)
+        __hip_atomic_store((gu32*)ws.epoch, epoch + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (STAMPS) st[5] = realtime();
     }
 }
 
-template <typename YT, int S, int R, bool EXTRA = false, bool NO_REDUCE = false>
-int launch_tail(const float* h, const YT* y, int64_t B, const float* abalpha, const float* p_hat, float* dh,
-                double* out64, float* grad3, float* loss, void* ws, size_t ws_bytes, hipStream_t st) {
-    const int64_t nblocks = (B + chunk_elems(S) - 1) / chunk_elems(S);
-    if (nblocks + R > 0x7fffffffLL) return DAUC_EINVAL;
-    const size_t need = kPersistentBytes + static_cast<size_t>(nblocks + R) * kRowWords * 8;
-    if (ws == nullptr || ws_bytes < need) return DAUC_EINVAL;
-    auto* rows = reinterpret_cast<unsigned long long*>(static_cast<char*>(ws) + kPersistentBytes);
-    const int64_t grid = EXTRA ? nblocks + R : nblocks;
-    hipLaunchKernelGGL((surrogate_tail_kernel<YT, S, R, EXTRA, NO_REDUCE>), dim3(static_cast<unsigned>(grid)), dim3(kThreads), 0,
-                       st, h, y, B, 1.0 / static_cast<double>(B), abalpha, p_hat, dh, rows, rows + nblocks * kRowWords,
-                       out64, grad3, loss, nblocks);
-    return launch_status();
+// ---- the same one-launch loss with EARLY group reducers ------------------------------------
+//
+// The stamps of the kernel above (variant 5, scripts/probe_tail_stamps.py) show its tail after
+// the last row store (6.3 us at B = 2^26): the reducers are the last 64 workgroups, so the last
+// of them START at the very end, stream their own chunk, and only then take their (long finished)
+// group and publish its total (+3.8 us); the final reducer then polls the totals (+4.4) and
+// combines them with a second block sum (+6.3). Here groups of G rows get a reducer dispatched
+// L workgroups AFTER the group's last row (by blockIdx; dispatch runs roughly in blockIdx order,
+// so with L >= the resident workgroups the group is finished when its reducer starts -- speed
+// only: a reducer that starts early waits for rows of workgroups that never wait). Only the
+// groups too close to the end for that (the last L rows) are reduced by the last workgroups, the
+// very last one taking the last group and adding every other group's total to its own rows
+// before ONE block sum (thread t: its rows, then group total t: a fixed order, bitwise
+// reproducible). Same granules, epochs, timeouts and stamps as the kernel above.
+struct TailPlan {
+    int64_t G;        // rows per group (ngroups <= 256: the final reducer's threads hold one total each)
+    int64_t ngroups;
+    int64_t L;        // lag: early reducer of group r = workgroup (r + 1) G - 1 + L
+    int64_t r_late0;  // groups r >= r_late0 are reduced by the last nlate workgroups
+    int64_t nlate;
+};
+
+inline TailPlan tail_plan(int64_t nblocks, int64_t L) {
+    TailPlan p;
+    p.G = (nblocks + 255) / 256 > 256 ? (nblocks + 255) / 256 : 256;
+    p.ngroups = (nblocks + p.G - 1) / p.G;
+    p.L = L;
+    p.r_late0 = p.ngroups - 1;
+    for (int64_t r = 0; r < p.ngroups - 1; ++r) {
+        // the late workgroups of groups r .. ngroups-1 are the last (ngroups - r) of the grid
+        if ((r + 1) * p.G - 1 + L >= nblocks - (p.ngroups - r)) {
+            p.r_late0 = r;
+            break;
+        }
+    }
+    p.nlate = p.ngroups - p.r_late0;
+    return p;
 }
 
-// Default chunk geometry (variant sweep: scripts/micro_kernels.py --which surrogate).
-#ifndef DAUC_SURROGATE_CHUNK_SLOTS
-#define DAUC_SURROGATE_CHUNK_SLOTS 4
-#endif
-constexpr int kChunkSlots = DAUC_SURROGATE_CHUNK_SLOTS;
-// reducers of the one-launch loss (variants 20-24 measured at B = 2^26: 16 / 32 / 64 / 128 / 256;
-// profiles/r02/surrogate_ab.jsonl)
+template <typename YT, int S, bool STAMPS>
+__global__ __launch_bounds__(kThreads, DAUC_TAIL_WAVES) void surrogate_tail_early_kernel(
+    const float* __restrict__ h, const YT* __restrict__ y, int64_t B, double invB,
+    const float* __restrict__ abalpha, const float* __restrict__ p_hat, float* __restrict__ dh, TailWs ws,
+    TailPlan plan, double* __restrict__ out64, float* __restrict__ grad3, float* __restrict__ loss) {
+    const unsigned epoch = __builtin_amdgcn_readfirstlane(
+        __hip_atomic_load((gu32*)ws.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    const unsigned tag = epoch | 0x80000000u;
+    const float sa = abalpha[0], sb = abalpha[1], sal = abalpha[2], sp = p_hat[0];
+    const int64_t nblocks = gridDim.x, b = blockIdx.x;
+    {
+        const SurrogateScalars s = make_scalars_v(sa, sb, sal, sp, invB);
+        const double v = stream_chunk<YT, false, S>(h, y, B, s, dh, gran_total(threadIdx.x < kGran ? threadIdx.x : 0));
+        publish_granule(ws.rows + b * kGran, tag, v);
+        if (STAMPS && threadIdx.x == 0) ws.stamps[b] = realtime();
+    }
+    int64_t r = -1;
+    if (b >= nblocks - plan.nlate) {
+        r = plan.r_late0 + (b - (nblocks - plan.nlate));
+    } else {
+        const int64_t e = b + 1 - plan.L;
+        if (e >= plan.G && e % plan.G == 0 && e / plan.G - 1 < plan.r_late0) r = e / plan.G - 1;
+    }
+    if (r < 0) return;
+
+    __shared__ double scratch[kNumAcc * kWaves];
+    __shared__ int bad;
+    const int64_t g0 = r * plan.G, g1 = (g0 + plan.G < nblocks) ? g0 + plan.G : nblocks;
+    const bool final_red = b == nblocks - 1;
+    unsigned long long* st = STAMPS ? ws.stamps + nblocks + 8 * (r < 255 ? r : 255) : nullptr;
+    if (STAMPS && threadIdx.x == 0) st[0] = realtime();
+    if (threadIdx.x == 0) bad = 0;
+    bool ok = true;
+    double tot[kNumAcc];
+#pragma unroll
+    for (int k = 0; k < kNumAcc; ++k) tot[k] = 0.0;
+    for (int64_t i = g0 + threadIdx.x; i < g1; i += kThreads) {
+        unsigned p[kGran];
+        const unsigned miss = poll_row(ws.rows + i * kGran, tag, p);
+        if (!wait_row(ws.rows + i * kGran, tag, miss, p)) {
+            ok = false;
+            break;
+        }
+        add_row(p, tot);
+    }
+    if (STAMPS && threadIdx.x == 0) st[1] = realtime();
+    if (final_red && threadIdx.x < plan.ngroups - 1) {
+        // the other groups' totals, added to this thread's rows (early groups were published long ago)
+        unsigned p[kGran];
+        const unsigned miss = poll_row(ws.gtot + threadIdx.x * kGran, tag, p);
+        if (wait_row(ws.gtot + threadIdx.x * kGran, tag, miss, p)) add_row(p, tot);
+        else ok = false;
+    }
+    if (STAMPS && threadIdx.x == 0) st[4] = realtime();
+    __syncthreads();  // orders bad = 0 before any thread's bad = 1
+    if (!ok) bad = 1;
+    block_sum<kNumAcc>(tot, scratch);  // its barriers order the flag
+    ok = bad == 0;
+    if (STAMPS && threadIdx.x == 0) st[2] = realtime();
+    if (!final_red) {
+        if (!ok) {
+#pragma unroll
+            for (int k = 0; k < kNumAcc; ++k) tot[k] = __builtin_nan("");
+        }
+        double v = tot[0];
+#pragma unroll
+        for (int k = 1; k < kNumAcc; ++k)
+            if (threadIdx.x < kGran && gran_total(threadIdx.x) == k) v = tot[k];
+        publish_granule(ws.gtot + r * kGran, tag, v);
+        if (STAMPS && threadIdx.x == 0) st[3] = realtime();
+        return;
+    }
+    if (threadIdx.x == 0) {
+        if (!ok) {
+#pragma unroll
+            for (int k = 0; k < kNumAcc; ++k) tot[k] = __builtin_nan("");
+        }
+        finalize(tot, make_scalars_v(sa, sb, sal, sp, invB), invB, out64, grad3, loss);
+        // the call's last action: every workgroup has read the epoch (its row has arrived)
+        __hip_atomic_store((gu32*)ws.epoch, epoch + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (STAMPS) st[5] = realtime();
+    }
+}
+
+// Default chunk geometry (scripts/micro_kernels.py --which surrogate, profiles/r01-r02).
+constexpr int kChunkSlots = 4;
+// reducers of the one-launch loss (16 / 32 / 64 / 128 / 256 measured at B = 2^26:
+// profiles/r02/surrogate_ab.jsonl; 64 and 128 tie, 16 is 3 us slower)
 #ifndef DAUC_SURROGATE_TAIL_REDUCERS
 #define DAUC_SURROGATE_TAIL_REDUCERS 64
 #endif
 constexpr int kTailReducers = DAUC_SURROGATE_TAIL_REDUCERS;
-// Unit-stride batches at least this large take the chunked kernel; smaller ones are
+// Unit-stride batches at least this large take the chunked kernels; smaller ones are
 // latency-bound and stay on the single-ticket persistent kernel.
 constexpr int64_t kChunkMinB = int64_t(1) << 22;
+
+inline int64_t chunk_blocks(int64_t B) { return (B + chunk_elems(kChunkSlots) - 1) / chunk_elems(kChunkSlots); }
+
+// workspace regions after the persistent kernel's: the two-launch form's rows + reduce slots, then
+// the tail kernel's header, granule rows and (tuning builds) stamps
+inline size_t chunk_region_bytes(int64_t nblocks) {
+    return size_t(nblocks) * kRowWords * 8 + kCounterBytes + size_t(reduce_blocks(nblocks)) * kNumAcc * 8;
+}
+
+inline size_t tail_offset(int64_t nblocks) {
+    return kPersistentBytes + (chunk_region_bytes(nblocks) + 255) / 256 * 256;
+}
+
+#ifdef DAUC_TUNING
+constexpr bool kStampRegion = true;
+#else
+constexpr bool kStampRegion = false;
+#endif
+
+template <typename YT, int R, bool REDUCE = true, bool STAMPS = false>
+int launch_tail(const float* h, const YT* y, int64_t B, const float* abalpha, const float* p_hat, float* dh,
+                double* out64, float* grad3, float* loss, void* ws, size_t ws_bytes, hipStream_t st) {
+    const int64_t nblocks = chunk_blocks(B);
+    if (nblocks > 0x7fffffffLL) return DAUC_EINVAL;
+    if (ws == nullptr || ws_bytes < tail_offset(nblocks) + tail_ws_bytes(nblocks, R, STAMPS)) return DAUC_EINVAL;
+    const TailWs w = tail_ws(static_cast<char*>(ws) + tail_offset(nblocks), nblocks, R, STAMPS);
+    hipLaunchKernelGGL((surrogate_tail_kernel<YT, kChunkSlots, R, REDUCE, STAMPS>), dim3(static_cast<unsigned>(nblocks)),
+                       dim3(kThreads), 0, st, h, y, B, 1.0 / static_cast<double>(B), abalpha, p_hat, dh, w, out64,
+                       grad3, loss);
+    return launch_status();
+}
+
+// the lag of the early reducers: 2 x the resident workgroups (8 per CU on 256 CUs)
+#ifndef DAUC_TAIL_LAG
+#define DAUC_TAIL_LAG 4096
+#endif
+
+template <typename YT, bool STAMPS = false>
+int launch_tail_early(const float* h, const YT* y, int64_t B, const float* abalpha, const float* p_hat, float* dh,
+                      double* out64, float* grad3, float* loss, void* ws, size_t ws_bytes, hipStream_t st,
+                      int64_t lag = DAUC_TAIL_LAG) {
+    const int64_t nblocks = chunk_blocks(B);
+    if (nblocks > 0x7fffffffLL) return DAUC_EINVAL;
+    const TailPlan plan = tail_plan(nblocks, lag);
+    // group totals: ngroups <= 256 granule rows (the workspace holds kTailReducers... size for 256)
+    if (ws == nullptr || ws_bytes < tail_offset(nblocks) + tail_ws_bytes(nblocks, 256, STAMPS)) return DAUC_EINVAL;
+    const TailWs w = tail_ws(static_cast<char*>(ws) + tail_offset(nblocks), nblocks, 256, STAMPS);
+    hipLaunchKernelGGL((surrogate_tail_early_kernel<YT, kChunkSlots, STAMPS>), dim3(static_cast<unsigned>(nblocks)),
+                       dim3(kThreads), 0, st, h, y, B, 1.0 / static_cast<double>(B), abalpha, p_hat, dh, w, plan,
+                       out64, grad3, loss);
+    return launch_status();
+}
+
+template <typename YT, bool CLASS_ONLY>
+int launch_chunk(const float* h, const YT* y, int64_t B, const float* abalpha, const float* p_hat, float* dh,
+                 double* out64, float* grad3, float* loss, double* sums4, int accumulate, void* ws, size_t ws_bytes,
+                 hipStream_t st, bool reduce = true) {
+    const int64_t nblocks = chunk_blocks(B);
+    if (nblocks > 0x7fffffffLL) return DAUC_EINVAL;
+    if (ws == nullptr || ws_bytes < kPersistentBytes + chunk_region_bytes(nblocks)) return DAUC_EINVAL;
+    double* rows = reinterpret_cast<double*>(static_cast<char*>(ws) + kPersistentBytes);
+    unsigned* counter = reinterpret_cast<unsigned*>(rows + nblocks * kRowWords);
+    double* partials = reinterpret_cast<double*>(reinterpret_cast<char*>(counter) + kCounterBytes);
+    const double invB = 1.0 / static_cast<double>(B);
+    hipLaunchKernelGGL((surrogate_chunk_kernel<YT, CLASS_ONLY, kChunkSlots>), dim3(static_cast<unsigned>(nblocks)),
+                       dim3(kThreads), 0, st, h, y, B, invB, abalpha, p_hat, dh, rows);
+    int rc = launch_status();
+    if (rc || !reduce) return rc;
+    hipLaunchKernelGGL((surrogate_rows_reduce_kernel<CLASS_ONLY>), dim3(static_cast<unsigned>(reduce_blocks(nblocks))),
+                       dim3(kThreads), 0, st, rows, nblocks, partials, counter, invB, abalpha, p_hat, out64, grad3,
+                       loss, sums4, accumulate);
+    return launch_status();
+}
 
 int resident_blocks() {
     static int cached = 0;
@@ -1199,63 +959,10 @@ int resident_blocks() {
 
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
-template <typename YT, bool CLASS_ONLY, int S, bool NTL, bool NTS>
-int launch_chunk(const float* h, const YT* y, int64_t B, const float* abalpha, const float* p_hat, float* dh,
-                 double* out64, float* grad3, float* loss, double* sums4, int accumulate, void* ws,
-                 size_t ws_bytes, hipStream_t st) {
-    const int64_t nblocks = (B + chunk_elems(S) - 1) / chunk_elems(S);
-    if (nblocks > 0x7fffffffLL) return DAUC_EINVAL;
-    if (ws == nullptr || ws_bytes < chunk_ws_bytes(nblocks)) return DAUC_EINVAL;
-    const ChunkWs w = chunk_ws(ws, nblocks);
-    const double invB = 1.0 / static_cast<double>(B);
-    hipLaunchKernelGGL((surrogate_chunk_kernel<YT, CLASS_ONLY, S, NTL, NTS>), dim3(static_cast<unsigned>(nblocks)),
-                       dim3(kThreads), 0, st, h, y, B, invB, abalpha, p_hat, dh, w.rows);
-    int rc = launch_status();
-    if (rc) return rc;
-    const int64_t nrows = nblocks * kRowsPerChunk;
-    hipLaunchKernelGGL((surrogate_rows_reduce_kernel<CLASS_ONLY>), dim3(static_cast<unsigned>(reduce_blocks(nrows))),
-                       dim3(kThreads), 0, st, w.rows, nrows, w, invB, abalpha, p_hat, out64, grad3, loss, sums4,
-                       accumulate);
-    return launch_status();
-}
-
-template <typename YT, bool CLASS_ONLY, int S, int SPAN>
-int launch_span(const float* h, const YT* y, int64_t B, const float* abalpha, const float* p_hat, float* dh,
-                double* out64, float* grad3, float* loss, double* sums4, int accumulate, void* ws, size_t ws_bytes,
-                hipStream_t st) {
-    constexpr int64_t kChunk = chunk_elems(S);
-    const int64_t whole = B / (SPAN * kChunk);
-    const int64_t nblocks = whole + (B - whole * SPAN * kChunk + kChunk - 1) / kChunk;
-    if (nblocks > 0x7fffffffLL) return DAUC_EINVAL;
-    if (ws == nullptr || ws_bytes < chunk_ws_bytes(nblocks)) return DAUC_EINVAL;
-    const ChunkWs w = chunk_ws(ws, nblocks);
-    const double invB = 1.0 / static_cast<double>(B);
-    hipLaunchKernelGGL((surrogate_span_kernel<YT, CLASS_ONLY, S, SPAN>), dim3(static_cast<unsigned>(nblocks)),
-                       dim3(kThreads), 0, st, h, y, B, invB, abalpha, p_hat, dh, w.rows);
-    int rc = launch_status();
-    if (rc) return rc;
-    hipLaunchKernelGGL((surrogate_rows_reduce_kernel<CLASS_ONLY>), dim3(static_cast<unsigned>(reduce_blocks(nblocks))),
-                       dim3(kThreads), 0, st, w.rows, nblocks, w, invB, abalpha, p_hat, out64, grad3, loss, sums4,
-                       accumulate);
-    return launch_status();
-}
-
-template <typename YT, bool CLASS_ONLY, int S, int G, int CS, bool TF>
-int launch_ticket(const float* h, const YT* y, int64_t B, const float* abalpha, const float* p_hat, float* dh,
-                  double* out64, float* grad3, float* loss, double* sums4, int accumulate, void* ws, size_t ws_bytes,
-                  hipStream_t st) {
-    const int64_t nblocks = (B + chunk_elems(S) - 1) / chunk_elems(S);
-    if (nblocks > 0x7fffffffLL) return DAUC_EINVAL;
-    if (ws == nullptr || ws_bytes < ticket_ws_bytes(nblocks)) return DAUC_EINVAL;
-    hipLaunchKernelGGL((surrogate_ticket_kernel<YT, CLASS_ONLY, S, G, CS, TF>), dim3(static_cast<unsigned>(nblocks)),
-                       dim3(kThreads), 0, st, h, y, B, 1.0 / static_cast<double>(B), abalpha, p_hat, dh,
-                       ticket_ws(ws, nblocks), out64, grad3, loss, sums4, accumulate);
-    return launch_status();
-}
-
-// variant: 0 = default dispatch, 1 = persistent kernel, 2..7 = chunk kernel geometries,
-// 8..14 = single-launch ticket kernel (slots, group size, counter spacing, ticket order)
-// (tuning; only for int8 labels with a loss, i.e. the micro-benchmark's configuration).
+// variant (tuning builds only; int8 labels with a loss): 0 = default dispatch, 1 = the persistent
+// kernel at any B, 2 = the two-launch form (stream + row-reduce launch), 3 = the streaming kernel
+// alone (no reduce, no scalars), 4 = the one-launch tail kernel's stream with its row stores and
+// nobody reducing, 5 = the tail kernel recording s_memrealtime stamps in the workspace
 template <bool CLASS_ONLY, typename YT>
 int launch_surrogate(const float* h, int64_t hs, const YT* y, int64_t B, const float* abalpha,
                      const float* p_hat, float* dh, int64_t dhs, double* out64, float* grad3,
@@ -1264,64 +971,34 @@ int launch_surrogate(const float* h, int64_t hs, const YT* y, int64_t B, const f
     const bool unit = hs == 1 && aligned16(h) &&
                       (reinterpret_cast<uintptr_t>(y) % (kVec * sizeof(YT))) == 0 &&
                       (CLASS_ONLY || dh == nullptr || (dhs == 1 && aligned16(dh)));
+#ifdef DAUC_TUNING
     if (unit && variant >= 2) {
         if constexpr (!CLASS_ONLY && sizeof(YT) == 1) {
             switch (variant) {
-                case 2: return launch_chunk<YT, false, 4, true, true>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, sums4, accumulate, ws, ws_bytes, st);
-                case 3: return launch_chunk<YT, false, 8, true, true>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, sums4, accumulate, ws, ws_bytes, st);
-                case 4: return launch_chunk<YT, false, 16, true, true>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, sums4, accumulate, ws, ws_bytes, st);
-                case 5: return launch_chunk<YT, false, 8, false, true>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, sums4, accumulate, ws, ws_bytes, st);
-                case 6: return launch_chunk<YT, false, 8, true, false>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, sums4, accumulate, ws, ws_bytes, st);
-                case 7: return launch_chunk<YT, false, 2, true, true>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, sums4, accumulate, ws, ws_bytes, st);
-#define DAUC_TV(S, G, CS, TF) return launch_ticket<YT, false, S, G, CS, TF>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, sums4, accumulate, ws, ws_bytes, st)
-                case 8: DAUC_TV(4, 512, 1024, true);
-                case 9: DAUC_TV(4, 64, 1024, true);
-                case 10: DAUC_TV(4, 128, 1024, true);
-                case 11: DAUC_TV(4, 256, 1024, true);
-                case 12: DAUC_TV(4, 64, 1024, false);
-                case 13: DAUC_TV(8, 64, 1024, true);
-                case 14: DAUC_TV(8, 256, 1024, true);
-#undef DAUC_TV
-                case 15: {
-                    // the default streaming kernel alone (no row reduce, no scalars): timing only. It
-                    // leaves its rows in the workspace, so it must not share one with the other variants.
-                    const int64_t nblocks = (B + chunk_elems(kChunkSlots) - 1) / chunk_elems(kChunkSlots);
-                    if (ws == nullptr || ws_bytes < chunk_ws_bytes(nblocks)) return DAUC_EINVAL;
-                    hipLaunchKernelGGL((surrogate_chunk_kernel<YT, false, kChunkSlots, true, true>),
-                                       dim3(static_cast<unsigned>(nblocks)), dim3(kThreads), 0, st, h, y, B,
-                                       1.0 / static_cast<double>(B), abalpha, p_hat, dh, chunk_ws(ws, nblocks).rows);
-                    return launch_status();
-                }
-                case 16: return launch_span<YT, false, 4, 4>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, sums4, accumulate, ws, ws_bytes, st);
-                case 17: return launch_span<YT, false, 4, 8>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, sums4, accumulate, ws, ws_bytes, st);
-                case 18: return launch_span<YT, false, 4, 16>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, sums4, accumulate, ws, ws_bytes, st);
-                case 19: return launch_span<YT, false, 4, 32>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, sums4, accumulate, ws, ws_bytes, st);
-                case 20: return launch_tail<YT, 4, 32>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, ws, ws_bytes, st);
-                case 21: return launch_tail<YT, 4, 16>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, ws, ws_bytes, st);
-                case 22: return launch_tail<YT, 4, 64>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, ws, ws_bytes, st);
-                case 23: return launch_tail<YT, 4, 128>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, ws, ws_bytes, st);
-                case 24: return launch_tail<YT, 4, 256>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, ws, ws_bytes, st);
-                case 25: return launch_chunk<YT, false, kChunkSlots, true, true>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, sums4, accumulate, ws, ws_bytes, st);
-                case 26: return launch_tail<YT, 4, 64, true>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, ws, ws_bytes, st);
-                case 27: return launch_tail<YT, 4, 32, true>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, ws, ws_bytes, st);
-                case 28: return launch_tail<YT, 4, 128, true>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, ws, ws_bytes, st);
-                // timing only: the one-launch stream with its data-as-flag row stores, nobody reducing
-                // (rows are left in the workspace: give it one of its own, like variant 15)
-                case 29: return launch_tail<YT, 4, 64, false, true>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, ws, ws_bytes, st);
+                case 2: return launch_chunk<YT, false>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, sums4, accumulate, ws, ws_bytes, st);
+                case 3: return launch_chunk<YT, false>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, sums4, accumulate, ws, ws_bytes, st, false);
+                case 4: return launch_tail<YT, kTailReducers, false>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, ws, ws_bytes, st);
+                case 5: return launch_tail<YT, kTailReducers, true, true>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, ws, ws_bytes, st);
+                case 6: return launch_tail_early<YT>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, ws, ws_bytes, st);
+                case 7: return launch_tail_early<YT, true>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, ws, ws_bytes, st);
+                case 8: return launch_tail_early<YT>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, ws, ws_bytes, st, 2048);
+                case 9: return launch_tail_early<YT>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, ws, ws_bytes, st, 8192);
                 default: return DAUC_EINVAL;
             }
         }
         return DAUC_EINVAL;
     }
+#else
+    (void)variant;
+#endif
     if (unit && variant == 0 && B >= kChunkMinB) {
         // the loss: the stream with its row reduce done by its last kTailReducers workgroups (one
         // launch); the class sums keep the two-launch form
         if constexpr (!CLASS_ONLY)
-            return launch_tail<YT, kChunkSlots, kTailReducers>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, ws,
-                                                               ws_bytes, st);
+            return launch_tail<YT, kTailReducers>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, ws, ws_bytes, st);
         else
-            return launch_chunk<YT, CLASS_ONLY, kChunkSlots, true, true>(h, y, B, abalpha, p_hat, dh, out64, grad3,
-                                                                          loss, sums4, accumulate, ws, ws_bytes, st);
+            return launch_chunk<YT, true>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, sums4, accumulate, ws,
+                                          ws_bytes, st);
     }
     const int grid = grid_for(B);
     unsigned* counter = nullptr;
@@ -1477,11 +1154,10 @@ size_t dauc_surrogate_workspace_size(int64_t B) {
     if (B < 0) B = 0;
     const int g = grid_scalar(B);  // >= grid_for(B): covers the persistent kernels
     const size_t persistent = kCounterBytes + static_cast<size_t>(g) * kNumAcc * sizeof(double);
-    // the chunk kernels (smallest chunk of any variant: S = 2)
-    const int64_t nb2 = (B + chunk_elems(2) - 1) / chunk_elems(2);
-    const size_t chunked = chunk_ws_bytes(nb2), ticketed = ticket_ws_bytes(nb2);
-    const size_t big = chunked > ticketed ? chunked : ticketed;
-    return persistent > big ? persistent : big;
+    // the chunked kernels: the two-launch form's region, then the tail kernel's
+    const int64_t nb = chunk_blocks(B);
+    const size_t chunked = tail_offset(nb) + tail_ws_bytes(nb, 256, kStampRegion);  // <= 256 group totals
+    return persistent > chunked ? persistent : chunked;
 }
 
 int dauc_surrogate_fwdbwd(const float* h, int64_t h_stride, const void* y, int y_dtype, int64_t B,
@@ -1496,17 +1172,19 @@ int dauc_surrogate_fwdbwd(const float* h, int64_t h_stride, const void* y, int y
                                   as_hip(stream));
 }
 
+#ifdef DAUC_TUNING
 int dauc_surrogate_fwdbwd_variant(const float* h, int64_t h_stride, const void* y, int y_dtype, int64_t B,
                                   const float* abalpha, const float* p_hat, float* dh, int64_t dh_stride,
                                   double* out64, float* grad3, float* loss, void* workspace,
                                   size_t workspace_bytes, int variant, dauc_stream_t stream) {
     if (B <= 0 || h == nullptr || y == nullptr || abalpha == nullptr || p_hat == nullptr ||
-        h_stride <= 0 || (dh != nullptr && dh_stride <= 0) || variant < 0 || variant > 29)
+        h_stride <= 0 || (dh != nullptr && dh_stride <= 0) || variant < 0 || variant > 9)
         return DAUC_EINVAL;
     return dispatch_labels<false>(h, h_stride, y, y_dtype, B, abalpha, p_hat, dh, dh_stride, out64,
                                   grad3, loss, nullptr, 0, workspace, workspace_bytes,
                                   as_hip(stream), variant);
 }
+#endif
 
 int dauc_class_sums(const float* h, int64_t h_stride, const void* y, int y_dtype, int64_t B,
                     double* sums4, int accumulate, void* workspace, size_t workspace_bytes,

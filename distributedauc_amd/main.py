@@ -126,13 +126,23 @@ def run_label(para, size: int) -> str:
 
 
 class Evaluator:
-    """main.py:215-270: rank 0 scores the test partition; the exact pair count is sharded."""
+    """main.py:215-270: the test-set AUC of rank 0's model, written to the history CSV.
+
+    The reference scores the whole test partition on rank 0 (main.py:232) while the other ranks
+    wait. Here (``split=True``, the default over ranks) every rank scores a contiguous share of the
+    test batches with rank 0's model: rank 0's parameters and BatchNorm running statistics are
+    broadcast into every rank's model for the evaluation (ranks hold different parameters between
+    averaging rounds, and BN buffers are never averaged, main.py:35) and each rank's own state is
+    restored afterwards. The shares are all-gathered, so every rank holds rank 0's scores in the
+    test-set order, and the exact count is sharded (ExactAUC). Same scores, same AUC as rank-0
+    scoring (tests/test_main_gpu.py); ``split=False`` is the reference's rank-0 scoring."""
 
     def __init__(self, test_batches, n_test: int, split_index: int, device, group, world: int, rank: int,
-                 history_path: str | None = None):
+                 history_path: str | None = None, split: bool = True):
         self.batches = test_batches
         self.n = n_test
         self.split = split_index
+        self.split_scoring = bool(split) and world > 1
         self.device = device
         self.world, self.rank = world, rank
         self.auc = ExactAUC(group, world, rank)
@@ -140,26 +150,70 @@ class Evaluator:
         self.history_path = history_path
         self.rows: list[tuple[int, float, float]] = []
         self.train_seconds = 0.0
+        self.last_eval_seconds = 0.0
         self._mark = time.perf_counter()
+        sizes = [lab.numel() for _, lab in test_batches]
+        nb = len(sizes)
+        self._share = [(r * nb // world, (r + 1) * nb // world) for r in range(world)]
+        self._counts = [sum(sizes[lo:hi]) for lo, hi in self._share]
+        self._labels = None
+
+    def _test_labels(self) -> torch.Tensor:
+        if self._labels is None:
+            self._labels = torch.cat([torch.where(lab > self.split, 1, -1).to(torch.int8) for _, lab in self.batches])
+        return self._labels
+
+    def _score(self, coda: CoDA, lo: int, hi: int, out: torch.Tensor) -> None:
+        from .conv1x1 import fixed_engine
+
+        coda.model.eval()
+        # no per-rank timed engine choice: every rank's scores are the bits rank 0 would compute
+        with torch.no_grad(), fixed_engine("gemm"):
+            k = 0
+            for x, lab in self.batches[lo:hi]:
+                out[k:k + lab.numel()] = coda.scores(x)
+                k += lab.numel()
+        coda.model.train()
+
+    def _scores_split(self, coda: CoDA) -> torch.Tensor:
+        """Every rank scores its share of the batches with rank 0's model; all-gather."""
+        st = coda.state
+        bufs = [b for b in coda.model.buffers() if b.dtype == torch.float32]
+        saved = st.flat[: st.n_params].clone(), [b.clone() for b in bufs]
+        packed = torch.cat([b.reshape(-1) for b in bufs]) if bufs else None
+        dist.broadcast(st.flat[: st.n_params], 0, group=self.group)  # rank 0's parameters
+        if packed is not None:
+            dist.broadcast(packed, 0, group=self.group)              # rank 0's BN running statistics
+            off = 0
+            for b in bufs:
+                b.copy_(packed[off:off + b.numel()].view_as(b))
+                off += b.numel()
+        seg = max(self._counts)
+        mine = torch.zeros(seg, dtype=torch.float32, device=self.device)
+        lo, hi = self._share[self.rank]
+        self._score(coda, lo, hi, mine)
+        gathered = torch.empty(seg * self.world, dtype=torch.float32, device=self.device)
+        dist.all_gather_into_tensor(gathered, mine, group=self.group)
+        with torch.no_grad():  # this rank's own model back
+            st.flat[: st.n_params].copy_(saved[0])
+            for b, s in zip(bufs, saved[1]):
+                b.copy_(s)
+        parts = gathered.view(self.world, seg)
+        return torch.cat([parts[r, : self._counts[r]] for r in range(self.world)])
 
     def __call__(self, coda: CoDA):
         torch.cuda.synchronize(self.device)
-        self.train_seconds += time.perf_counter() - self._mark
-        scores = torch.empty(self.n, dtype=torch.float32, device=self.device)
-        labels = torch.empty(self.n, dtype=torch.int8, device=self.device)
-        if self.rank == 0:
-            coda.model.eval()
-            with torch.no_grad():
-                k = 0
-                for x, lab in self.batches:
-                    B = lab.numel()
-                    scores[k:k + B] = coda.scores(x)
-                    labels[k:k + B] = torch.where(lab > self.split, 1, -1).to(torch.int8)
-                    k += B
-            coda.model.train()
-        if self.world > 1:
-            dist.broadcast(scores, 0, group=self.group)
-            dist.broadcast(labels, 0, group=self.group)
+        t0 = time.perf_counter()
+        self.train_seconds += t0 - self._mark
+        labels = self._test_labels()
+        if self.split_scoring:
+            scores = self._scores_split(coda)
+        else:
+            scores = torch.empty(self.n, dtype=torch.float32, device=self.device)
+            if self.rank == 0:
+                self._score(coda, 0, len(self.batches), scores)
+            if self.world > 1:
+                dist.broadcast(scores, 0, group=self.group)
         auc = self.auc(labels, scores)
         if self.rank == 0:
             p_hat = float(coda.state.p_hat.item())
@@ -175,6 +229,8 @@ class Evaluator:
                 pd.DataFrame({"total_iteration": it, "time": tm, col: au}).to_csv(self.history_path)
         torch.cuda.synchronize(self.device)
         self._mark = time.perf_counter()
+        self.last_eval_seconds = self._mark - t0
+        self.last_scores = scores
         return auc
 
 
@@ -216,7 +272,8 @@ def train(rank: int, size: int, group=None, para=None):
         it = iter(test_loader)
         test_batches = [next(it) for _ in range((n_test + para.test_batchsize - 1) // para.test_batchsize)]
         hist = os.path.join(para.history_dir, "history" + label + ".csv") if para.history_dir else None
-        evaluate = Evaluator(test_batches, n_test, para.split_index, device, group, size, rank, hist)
+        evaluate = Evaluator(test_batches, n_test, para.split_index, device, group, size, rank, hist,
+                             split=getattr(para, "split_eval", 1) != 0)
     coda.run(iter(train_loader), num_stages=para.numStages, total_iter=para.total_iter,
              test_freq=para.test_freq, evaluate=evaluate)
     return coda

@@ -10,6 +10,7 @@ fallback in the product path.
 from __future__ import annotations
 
 import ctypes
+import threading
 
 import torch
 
@@ -54,21 +55,33 @@ def mode_code(mode: str) -> int:
 
 
 class _Workspaces:
-    """Zero-initialised scratch, one per (device, stream, kind), grown on demand.
+    """Zero-initialised scratch, one per (device, stream, host thread, kind), grown on demand.
 
     The kernels that need zeroed scratch (the surrogate's last-arriver ticket)
-    leave it zeroed again, so a workspace is cleared only when it is created.
+    leave it zeroed again, so a workspace is cleared only when it is created. Keyed by
+    the host thread too: two threads enqueueing on one stream must not share scratch
+    (their launches would interleave on it).
     """
 
     def __init__(self):
         self._ws: dict = {}
+        self._pinned: dict = {}
 
     def get(self, device: torch.device, kind: str, nbytes: int, stream: int | None = None) -> torch.Tensor:
-        key = (device.index, torch.cuda.current_stream(device).cuda_stream if stream is None else stream, kind)
+        key = (device.index, torch.cuda.current_stream(device).cuda_stream if stream is None else stream,
+               threading.get_ident(), kind)
         t = self._ws.get(key)
         if t is None or t.numel() < nbytes:
             t = torch.zeros(max(nbytes, 256), dtype=torch.uint8, device=device)
             self._ws[key] = t
+        return t
+
+    def pinned(self, device: torch.device, stream: int) -> torch.Tensor:
+        """16 page-locked int64 host words (the blocking evaluation's readback), same keying."""
+        key = (device.index, stream, threading.get_ident())
+        t = self._pinned.get(key)
+        if t is None:
+            t = self._pinned[key] = torch.zeros(16, dtype=torch.int64, pin_memory=True)
         return t
 
 
@@ -121,7 +134,9 @@ def surrogate_fwdbwd(h: torch.Tensor, y: torch.Tensor, abalpha: torch.Tensor, p_
                      variant: int = 0) -> None:
     """Fused loss + gradients of main.py:313-317 (one pass over h and y).
 
-    ``variant`` != 0 forces a kernel geometry (tuning; see dauc_surrogate_fwdbwd_variant)."""
+    ``variant`` != 0 runs a measured alternative from the tuning build (include/dauc_tuning.h:
+    1 persistent kernel, 2 two-launch form, 3 stream alone, 4 tail stream without its reduce,
+    5 tail kernel with s_memrealtime stamps)."""
     B = _check_vec(h, y)
     dev = h.device
     yc = _label_code(y)
@@ -145,10 +160,10 @@ def surrogate_fwdbwd(h: torch.Tensor, y: torch.Tensor, abalpha: torch.Tensor, p_
             raise ValueError("grad3 needs 3 contiguous fp32 slots")
     if loss is not None:
         _require(loss, "loss", torch.float32, dev)
-    L = _lib.load()
+    # variants run in the tuning build, whose workspace also holds the stamp region
+    L = _lib.load() if variant == 0 else _lib.tuning()
     nbytes = L.dauc_surrogate_workspace_size(B)
-    # variant 15 (the streaming kernel alone) leaves its rows behind: a workspace of its own
-    ws = workspaces.get(dev, "surrogate_stream_only" if variant in (15, 29) else "surrogate", nbytes)
+    ws = workspaces.get(dev, "surrogate" if variant == 0 else "surrogate_tuning", nbytes)
     if variant == 0:
         rc = L.dauc_surrogate_fwdbwd(_ptr(h), h.stride(0), _ptr(y), yc, B, _ptr(abalpha), _ptr(p_hat),
                                      _ptr(dh), dh_stride, _ptr(out64), _ptr(grad3), _ptr(loss), _ptr(ws),
@@ -285,9 +300,13 @@ def pd_update_dense(w: torch.Tensor, g: torch.Tensor, w0: torch.Tensor, w_avg: t
             raise ValueError(f"{name} must be contiguous with {n} elements")
     if not w.is_contiguous():
         raise ValueError("w must be contiguous")
-    check(_lib.load().dauc_pd_update_dense_variant(_ptr(w), _ptr(g), _ptr(w0), _ptr(w_avg), n, float(lr),
-                                                   float(1 / gamma), int(variant), _stream(dev)),
-          "dauc_pd_update_dense")
+    if variant == 0:
+        rc = _lib.load().dauc_pd_update_dense(_ptr(w), _ptr(g), _ptr(w0), _ptr(w_avg), n, float(lr),
+                                              float(1 / gamma), _stream(dev))
+    else:  # a measured alternative geometry (tuning build)
+        rc = _lib.tuning().dauc_pd_update_dense_variant(_ptr(w), _ptr(g), _ptr(w0), _ptr(w_avg), n, float(lr),
+                                                        float(1 / gamma), int(variant), _stream(dev))
+    check(rc, "dauc_pd_update_dense")
 
 
 # ----------------------------------------------------------------- a6
@@ -340,9 +359,7 @@ def split_scores(scores: torch.Tensor, labels: torch.Tensor, negatives: bool = T
     return pos, neg, stats
 
 
-def auc_eval_counts(scores: torch.Tensor, labels: torch.Tensor) -> tuple:
-    """The single-GPU sort-method evaluation in one blocking ABI call (dauc_auc_eval_counts):
-    (W, T, P, N, #non-finite scores, #labels not in {-1, 1}) as Python ints."""
+def _eval_args(scores: torch.Tensor, labels: torch.Tensor):
     _require(scores, "scores", torch.float32)
     dev = scores.device
     lc = _label_code(labels, "labels")
@@ -358,44 +375,52 @@ def auc_eval_counts(scores: torch.Tensor, labels: torch.Tensor) -> tuple:
     if nbytes is None:
         nbytes = _eval_ws_bytes[n] = L.dauc_auc_eval_workspace_size(n)
     st = torch.cuda.current_stream(dev).cuda_stream
-    ws = workspaces.get(dev, "auc_eval", nbytes, st)
+    return L, dev, lc, n, st, workspaces.get(dev, "auc_eval", nbytes, st)
+
+
+def auc_eval_counts(scores: torch.Tensor, labels: torch.Tensor) -> tuple:
+    """The single-GPU sort-method evaluation in one blocking ABI call (dauc_auc_eval_counts):
+    (W, T, P, N, #non-finite scores, #labels not in {-1, 1}) as Python ints."""
+    L, dev, lc, n, st, ws = _eval_args(scores, labels)
+    pin = workspaces.pinned(dev, st)
     out = (ctypes.c_int64 * 6)()
-    check(L.dauc_auc_eval_counts(scores.data_ptr(), labels.data_ptr(), lc, n, ctypes.addressof(out), ws.data_ptr(),
-                                 ws.numel(), st), "dauc_auc_eval_counts")
+    check(L.dauc_auc_eval_counts(scores.data_ptr(), labels.data_ptr(), lc, n, ctypes.addressof(out), pin.data_ptr(),
+                                 ws.data_ptr(), ws.numel(), st), "dauc_auc_eval_counts")
     return tuple(out)
+
+
+def auc_eval_enqueue(scores: torch.Tensor, labels: torch.Tensor, part: int, parts: int,
+                     out: torch.Tensor | None = None) -> torch.Tensor:
+    """Part `part` of `parts` of the evaluation, enqueued with no host synchronisation
+    (dauc_auc_eval_enqueue). Returns the device int64 [8] record: W_part, T_part, #non-finite
+    queried scores (sum these over the parts), P, 0, #non-finite positives, #labels not in
+    {-1, 1}, verdict (1 counted, 0 empty part, 2 run the blocking sorted path)."""
+    L, dev, lc, n, st, ws = _eval_args(scores, labels)
+    if out is None:
+        out = torch.empty(8, dtype=torch.int64, device=dev)
+    elif out.dtype != torch.int64 or out.numel() < 8 or not out.is_contiguous() or out.device != dev:
+        raise ValueError("out must be a contiguous int64 tensor of >= 8 elements on the scores' device")
+    check(L.dauc_auc_eval_enqueue(scores.data_ptr(), labels.data_ptr(), lc, n, int(part), int(parts), out.data_ptr(),
+                                  ws.data_ptr(), ws.numel(), st), "dauc_auc_eval_enqueue")
+    return out
 
 
 def auc_eval_counts_part(scores: torch.Tensor, labels: torch.Tensor, part: int, parts: int,
                          part_counts: torch.Tensor) -> tuple:
-    """Part `part` of `parts` of the one-call evaluation (dauc_auc_eval_counts_part): every part
-    compacts and sorts all the positives, only the queries are split. Returns (W_part, T_part, P,
-    N, #non-finite by the global checks, #labels not in {-1, 1}, #non-finite queried scores of
-    this part); `part_counts` (int64 [3] on the device) receives (W_part, T_part, that last count)
-    on the current stream for an all-reduce, when both classes are present and the global checks
-    passed."""
-    _require(scores, "scores", torch.float32)
-    dev = scores.device
-    lc = _label_code(labels, "labels")
-    if scores.dim() != 1 or labels.dim() != 1 or scores.shape != labels.shape:
-        raise ValueError("scores and labels must be 1-D of equal length")
-    if not scores.is_contiguous() or not labels.is_contiguous():
-        raise ValueError("scores and labels must be contiguous")
+    """Part `part` of `parts` of the blocking evaluation (dauc_auc_eval_counts_part): every part
+    builds the table from all the positives, only the queries are split. Returns (W_part, T_part,
+    P, N, #non-finite positives, #labels not in {-1, 1}, #non-finite queried scores of this part);
+    `part_counts` (int64 [3] on the device) receives (W_part, T_part, that last count) on the
+    current stream for an all-reduce."""
     _require(part_counts, "part_counts", torch.int64)
+    L, dev, lc, n, st, ws = _eval_args(scores, labels)
     if part_counts.numel() < 3 or not part_counts.is_contiguous() or part_counts.device != dev:
         raise ValueError("part_counts must be a contiguous int64 tensor of >= 3 elements on the scores' device")
-    n = scores.numel()
-    if n == 0:
-        raise ValueError("empty score vector")
-    L = _lib.load()
-    nbytes = _eval_ws_bytes.get(n)
-    if nbytes is None:
-        nbytes = _eval_ws_bytes[n] = L.dauc_auc_eval_workspace_size(n)
-    st = torch.cuda.current_stream(dev).cuda_stream
-    ws = workspaces.get(dev, "auc_eval", nbytes, st)
+    pin = workspaces.pinned(dev, st)
     out = (ctypes.c_int64 * 7)()
     check(L.dauc_auc_eval_counts_part(scores.data_ptr(), labels.data_ptr(), lc, n, int(part), int(parts),
-                                      ctypes.addressof(out), part_counts.data_ptr(), ws.data_ptr(), ws.numel(), st),
-          "dauc_auc_eval_counts_part")
+                                      ctypes.addressof(out), part_counts.data_ptr(), pin.data_ptr(), ws.data_ptr(),
+                                      ws.numel(), st), "dauc_auc_eval_counts_part")
     return tuple(out)
 
 
@@ -437,8 +462,13 @@ def pair_count(pos: torch.Tensor, neg: torch.Tensor, wins_ties: torch.Tensor, va
         raise ValueError("pos and neg must be contiguous 1-D tensors")
     if wins_ties.numel() < 2 or not wins_ties.is_contiguous():
         raise ValueError("wins_ties needs 2 contiguous int64 slots")
-    check(_lib.load().dauc_pair_count_variant(_ptr(pos), pos.numel(), _ptr(neg), neg.numel(), _ptr(wins_ties),
-                                              int(variant), _stream(dev)), "dauc_pair_count")
+    if variant == 0:
+        rc = _lib.load().dauc_pair_count(_ptr(pos), pos.numel(), _ptr(neg), neg.numel(), _ptr(wins_ties),
+                                         _stream(dev))
+    else:  # a measured alternative counting scheme (tuning build)
+        rc = _lib.tuning().dauc_pair_count_variant(_ptr(pos), pos.numel(), _ptr(neg), neg.numel(), _ptr(wins_ties),
+                                                   int(variant), _stream(dev))
+    check(rc, "dauc_pair_count")
 
 
 def auc_counts_sorted(pos: torch.Tensor, neg: torch.Tensor, wins_ties: torch.Tensor) -> None:
@@ -507,7 +537,7 @@ def set_search_mode(mode: int) -> None:
     where the table fits it and is not skewed, else the LDS search tree), 1 the tree, 2 the
     16-key-slot cell index (a measured, slower alternative). Same integers in every mode; for
     tests and measurements."""
-    check(_lib.load().dauc_set_search_mode(int(mode)), "dauc_set_search_mode")
+    check(_lib.tuning().dauc_set_search_mode(int(mode)), "dauc_set_search_mode")
 
 
 __all__ = [
@@ -515,4 +545,5 @@ __all__ = [
     "pd_update_dense", "coda_finalize", "scale_div", "split_scores", "pair_count", "auc_counts_sorted",
     "surrogate_logits_fwdbwd", "class_sums_logits",
     "sort_keys", "auc_counts_sorted_labeled", "compact_positives", "mode_code", "workspaces", "set_search_mode",
+    "auc_eval_enqueue",
 ]

@@ -54,6 +54,9 @@ def get_parser() -> argparse.ArgumentParser:
     p.add_argument("--head", choices=["softmax", "logits"], default="softmax",
                    help="softmax: the model ends in Softmax like resnet.py:159; logits: the softmax column is "
                         "folded into the fused surrogate kernel")
+    p.add_argument("--split_eval", type=int, default=1,
+                   help="1: every rank scores a share of the test set with rank 0's model (same AUC); "
+                        "0: rank 0 scores it all (main.py:232)")
     p.add_argument("--seed", type=int, default=1234)
     p.add_argument("--history_dir", type=str, default="history")
     p.add_argument("--backend", type=str, default=None, help="torch.distributed backend (default nccl=RCCL)")

@@ -99,30 +99,6 @@ int dauc_surrogate_fwdbwd(const float* h, int64_t h_stride, const void* y, int y
                           size_t workspace_bytes, dauc_stream_t stream);
 
 /*
- * dauc_surrogate_fwdbwd with an explicit kernel geometry, for tuning: variant 0 is the
- * default dispatch (what dauc_surrogate_fwdbwd does), 1 forces the persistent
- * grid-stride kernel, 2..7 force the one-chunk-per-workgroup kernel (2: 4 float4 slots
- * per thread, 3: 8, 4: 16, all non-temporal; 5: 8 slots, plain loads; 6: 8 slots, plain
- * stores; 7: 2 slots, non-temporal), 8..14 the single-launch form with start-order tickets
- * (8..12: 4 slots, groups of 512 / 64 / 128 / 256 chunks, 12: ticket drawn after the loads;
- * 13, 14: 8 slots, groups of 64 / 256), 15 the default streaming kernel ALONE (dh only: no
- * row reduce, no scalar outputs; it leaves its rows in the workspace, so give it a workspace of
- * its own: timing of the stream without the reduce launch), 16..19 one contiguous span of
- * 4 / 8 / 16 / 32 chunks (4 slots) per workgroup, next chunk's loads in flight, so the row
- * reduce is one small workgroup; 20..24 the row reduce inside the streaming launch, by its last
- * 32 / 16 / 64 / 128 / 256 workgroups (data-as-flag rows, no second launch; 64 is what variant 0
- * runs for unit-stride B >= 2^22), 25 the two-launch form (stream + row-reduce kernel), 26..28
- * the reduce by 64 / 32 / 128 EXTRA workgroups appended to the grid (they stream nothing). Variants
- * 2..28 need unit strides, 16-byte
- * aligned h/dh and int8 labels, and B <= 2^31. Every variant returns bitwise-identical dh and counts;
- * the fp64 sums agree to rounding (their reduction trees differ).
- */
-int dauc_surrogate_fwdbwd_variant(const float* h, int64_t h_stride, const void* y, int y_dtype, int64_t B,
-                                  const float* abalpha, const float* p_hat, float* dh, int64_t dh_stride,
-                                  double* out64, float* grad3, float* loss, void* workspace,
-                                  size_t workspace_bytes, int variant, dauc_stream_t stream);
-
-/*
  * Replaces the stage-start alpha estimate of main.py:166-188 (per batch):
  *   sums4 (+)= { sum h[y=-1], #{y=-1}, sum h[y=1], #{y=1} }       (fp64 [4])
  * accumulate != 0 adds into sums4, otherwise overwrites it.
@@ -188,15 +164,6 @@ int dauc_pd_update(float* w, const float* w0, float* w_avg, const dauc_grad_seg*
 int dauc_pd_update_dense(float* w, const float* g, const float* w0, float* w_avg, int64_t n,
                          float lr, float inv_gamma, dauc_stream_t stream);
 
-/*
- * dauc_pd_update_dense with an explicit kernel geometry, for tuning:
- * variant = v + 4*t, v selects 2 / 1 / 4 / 3 float4 per thread, t = 1 turns the
- * non-temporal loads of g and w0 off. Variant 0 is the default. Results are
- * bit-identical across variants.
- */
-int dauc_pd_update_dense_variant(float* w, const float* g, const float* w0, float* w_avg, int64_t n,
-                                 float lr, float inv_gamma, int variant, dauc_stream_t stream);
-
 /* ----------------------------------------------- a6: CoDA averaging */
 
 /*
@@ -256,16 +223,6 @@ int dauc_pair_count(const float* pos, int64_t P, const float* neg, int64_t N,
                     unsigned long long* wins_ties, dauc_stream_t stream);
 
 /*
- * dauc_pair_count with an explicit kernel variant, for tuning: variant =
- * mode + 4*r, mode 0 = packed fp32 difference + clamp (exact-compare fallback
- * for tiles with infinities or |score| < 2^-103), 1 = per-lane VGPR compare
- * counters, 2 = wave ballot + scalar popcount, 3 = mixed; r selects 8 / 4 / 16
- * positives held per lane. Every variant returns identical counts.
- */
-int dauc_pair_count_variant(const float* pos, int64_t P, const float* neg, int64_t N,
-                            unsigned long long* wins_ties, int variant, dauc_stream_t stream);
-
-/*
  * Bytes of scratch dauc_sort_keys needs for n keys, and dauc_auc_counts_sorted needs for
  * n = min(P, N) (the smaller class is the one sorted). No zeroing needed.
  */
@@ -297,61 +254,52 @@ int dauc_auc_counts_sorted_labeled(const float* pos, int64_t P, const float* sco
                                    dauc_stream_t stream);
 
 /*
- * The whole single-GPU exact-AUC evaluation of main.py:79-81 in ONE blocking call (sklearn's
- * roc_curve + auc is a blocking host call too): a one-pass positive compaction, the count index
- * built straight from the (unsorted) positives and the query pass, a readback of the class sizes
- * and the counts; a table the count index cannot hold (skewed, or more than 219,838 positives)
- * runs the stable compaction, the radix sort, the tree and the query pass instead. Same
- * integers as the stage-by-stage calls. The exception to the
- * conventions above: it synchronises `stream` and keeps one small pinned host buffer per
- * calling thread, allocated on first use. The table size is known only after the compaction;
- * when the calling thread's previous call had the same n and label type, its P is used to
- * enqueue the sort and the query right behind the compaction and the call synchronises ONCE
- * (repeated evaluation of one test set); if the real P differs, the sort and the query are
- * re-run at the real size (2 synchronisations; 3 when P > N).
- *   out[6] (HOST int64) = { W, T, P, N, #non-finite scores, #labels not in {-1, 1} }
- *   (W = T = 0 when a class is empty or a score is non-finite: the caller raises like sklearn)
- * workspace >= dauc_auc_eval_workspace_size(n) bytes, 256-byte aligned; no zeroing needed. The
- * call keeps the compaction's counters in the workspace between calls of one thread, tagged
- * with the call's epoch: a workspace that changed in between (or is new to the thread) is
- * detected and the call starts over with fresh counters, so any buffer may be passed.
+ * The exact-AUC evaluation of main.py:79-81 (sklearn roc_curve + auc over one test set), as ONE
+ * stream-ordered sequence with no host synchronisation and no allocation: a memset of the
+ * workspace header, a one-pass positive compaction (labels read once, P counted on the device),
+ * the count index built straight from the unsorted positives with the table size read on the
+ * device, and the query pass over this part's scores [part*n/parts, (part+1)*n/parts), whose
+ * labels are not 1 (every part builds the index over ALL the positives itself: ranks holding the
+ * same test set need no collective to share the table). Then one 64-byte device copy:
+ *   part_out (DEVICE int64[8]) = { W_part, T_part, #non-finite queried scores of this part,
+ *                                  P, 0, #non-finite positives, #labels not in {-1, 1}, verdict }
+ * The first three sum over the parts (the caller's all-reduce); the rest are the same on every
+ * part. verdict (low 32 bits): 0 = nothing to query (empty part), 1 = counted, 2 = the count index
+ * cannot hold this table (more than 219,838 positives or n/2 + 1, or clustered / tie-heavy
+ * positives): take dauc_auc_eval_counts(_part), which then runs the sorted path. N = n - P.
+ * workspace >= dauc_auc_eval_workspace_size(n) bytes, 256-byte aligned; its contents need no
+ * initialisation and are not used after the call (one workspace per stream at a time).
  */
 size_t dauc_auc_eval_workspace_size(int64_t n);
-int dauc_auc_eval_counts(const float* scores, const void* labels, int label_dtype, int64_t n, int64_t* out,
-                         void* workspace, size_t workspace_bytes, dauc_stream_t stream);
+int dauc_auc_eval_enqueue(const float* scores, const void* labels, int label_dtype, int64_t n, int part, int parts,
+                          int64_t* part_out, void* workspace, size_t workspace_bytes, dauc_stream_t stream);
 
 /*
- * Part `part` of `parts` of the same evaluation, for ranks that all hold the same test set
- * (the reference evaluates one test set, main.py:237-250, and its sharded counterpart, SURVEY
- * §8e). Every part compacts and sorts ALL the positives itself (the compaction reads only the
- * labels and the positives' scores: no collective is needed to give every rank the same table);
- * only the queries are split: scores [part*n/parts, (part+1)*n/parts) when P <= N, positives
- * [part*P/parts, (part+1)*P/parts) against the sorted negatives when P > N. The parts' counts
- * sum to dauc_auc_eval_counts's for every `parts`.
- *   out[7] (HOST int64) = { W_part, T_part, P, N, #non-finite scores found by the global checks,
- *                           #labels not in {-1, 1}, #non-finite queried scores of this part }
+ * The whole single-GPU evaluation as ONE blocking call (sklearn's roc_curve + auc is a blocking
+ * host call too): the sequence above, ONE readback of its record into `pinned` (caller-owned
+ * page-locked host memory of >= 8 int64, e.g. hipHostMalloc; the call writes and reads it) and a
+ * synchronisation of `stream`; for verdict 2 the sorted path (radix sort of the positives + the
+ * LDS search tree or the count index; or, when the negatives are the smaller class, both classes
+ * split and the negatives sorted) and one more readback. Stateless: same inputs, same work.
+ *   out[6] (HOST int64) = { W, T, P, N, #non-finite scores, #labels not in {-1, 1} }
+ *   (W = T = 0 when a class is empty or a score is non-finite: the caller raises like sklearn)
+ */
+int dauc_auc_eval_counts(const float* scores, const void* labels, int label_dtype, int64_t n, int64_t* out,
+                         int64_t* pinned, void* workspace, size_t workspace_bytes, dauc_stream_t stream);
+
+/*
+ * Part `part` of `parts` of the blocking evaluation (the sorted path of a verdict-2 test set,
+ * sharded: scores [part*n/parts, (part+1)*n/parts) when P <= N, positives [part*P/parts,
+ * (part+1)*P/parts) against the sorted negatives when P > N). The parts' counts sum to
+ * dauc_auc_eval_counts's for every `parts`.
+ *   out[7] (HOST int64) = { W_part, T_part, P, N, #non-finite positives, #labels not in {-1, 1},
+ *                           #non-finite queried scores of this part }
  *   part_counts (DEVICE int64[3], may be NULL): receives { W_part, T_part, out[6] } on `stream`
- *   (enqueued, not synchronised) when P > 0, N > 0 and out[4] == 0 -- the buffer the caller
- *   all-reduces; out[2..5] are the same on every part, so every rank takes the same branch.
- * Same workspace, synchronisation and speculative table size as dauc_auc_eval_counts.
+ *   (enqueued, not synchronised) -- the buffer the caller all-reduces.
  */
 int dauc_auc_eval_counts_part(const float* scores, const void* labels, int label_dtype, int64_t n, int part,
-                              int parts, int64_t* out, int64_t* part_counts, void* workspace, size_t workspace_bytes,
-                              dauc_stream_t stream);
-
-/*
- * Search structure of dauc_auc_counts_sorted_labeled (and so of dauc_auc_eval_counts), for
- * tests and measurements; process-wide, default 0. Same integers in every mode.
- *   0: automatic -- the count index for tables of up to 219,838 keys (the key's top 11 bits pick
- *      a bucket, a multiply-high its cell; an LDS word per 8 cells holds the keys before them and
- *      the cells' counts, so a query in an empty cell needs no table read and the others one
- *      16-byte window), unless the device finds the table skewed (a cell of 15+ keys, or more
- *      than 1.5 keys per cell): then, and for larger tables, the LDS search tree;
- *   1: the LDS search tree always;
- *   2: a 16-key-slot cell index wherever it fits (tables of up to 573,440 keys), a measured
- *      alternative (four lane gathers per query: slower than the tree), kept tested.
- */
-int dauc_set_search_mode(int mode);
+                              int parts, int64_t* out, int64_t* part_counts, int64_t* pinned, void* workspace,
+                              size_t workspace_bytes, dauc_stream_t stream);
 
 /* The radix sort alone: keys_out[0..n) = ascending order-preserving keys of scores (testing). */
 int dauc_sort_keys(const float* scores, int64_t n, unsigned* keys_out, void* workspace,

@@ -1,0 +1,73 @@
+/*
+ * dauc_tuning.h -- entry points of the TUNING build of the library (tuning/libdauc_tuning.so:
+ * the product sources compiled with -DDAUC_TUNING by distributedauc_amd/build.py).
+ *
+ * These are measured alternatives of the product kernels, kept selectable by number so the
+ * measurements behind the product's choices can be repeated (scripts/micro_kernels.py) and so the
+ * tests can check that every alternative gives the product's integers. The product library
+ * (libdauc.so, include/dauc.h) exports none of them and runs the default of each.
+ */
+#ifndef DAUC_TUNING_H
+#define DAUC_TUNING_H
+
+#include "dauc.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/*
+ * dauc_surrogate_fwdbwd with an explicit kernel: 0 the product's dispatch, 1 the persistent
+ * grid-stride kernel (the small-batch path) at any B, 2 the two-launch form (the streaming kernel
+ * writes one fp64 row per workgroup, a second launch reduces them), 3 the streaming kernel alone
+ * (dh only: no reduce, no scalar outputs), 4 the one-launch tail kernel's stream with its tagged
+ * row stores and nobody reducing (no scalar outputs), 5 the one-launch tail kernel recording
+ * s_memrealtime stamps in the workspace's stamp region (dauc_surrogate_workspace_size of this
+ * build includes it): per workgroup the time its row was stored, per reducer r the start,
+ * own-group-done, block-sum-done, publish (group reducers) / group-totals-done, finalize (the final
+ * reducer) times; 6 the same one-launch loss with EARLY group reducers (the reducer of a group of
+ * rows is the workgroup dispatched 4096 after the group's last row; only the groups too close to
+ * the end are reduced by the last workgroups), 7 = 6 with the stamps, 8 / 9 = 6 with a lag of 2048
+ * / 8192 workgroups (measured 5 / 3.5 us slower than 0 at B = 2^26: profiles/r03/surrogate_ab.jsonl).
+ * Variants 2..9 need unit strides, 16-byte aligned h/dh and int8 labels.
+ * Every variant returns bitwise-identical dh and counts; the fp64 sums agree to rounding.
+ */
+int dauc_surrogate_fwdbwd_variant(const float* h, int64_t h_stride, const void* y, int y_dtype, int64_t B,
+                                  const float* abalpha, const float* p_hat, float* dh, int64_t dh_stride,
+                                  double* out64, float* grad3, float* loss, void* workspace,
+                                  size_t workspace_bytes, int variant, dauc_stream_t stream);
+
+/*
+ * dauc_pd_update_dense with an explicit kernel geometry: variant = v + 4*t, v selects
+ * 2 / 1 / 4 / 3 float4 per thread, t = 1 turns the non-temporal loads of g and w0 off, t = 2 makes
+ * every load and store non-temporal. Variant 0 is the product's. Results are bit-identical.
+ */
+int dauc_pd_update_dense_variant(float* w, const float* g, const float* w0, float* w_avg, int64_t n,
+                                 float lr, float inv_gamma, int variant, dauc_stream_t stream);
+
+/*
+ * dauc_pair_count with an explicit kernel variant: variant = mode + 4*r, mode 0 = packed fp32
+ * difference + clamp (exact-compare fallback for tiles with infinities or |score| < 2^-103; the
+ * product's), 1 = per-lane VGPR compare counters, 2 = wave ballot + scalar popcount, 3 = mixed;
+ * r selects 8 / 4 / 16 positives held per lane. Every variant returns identical counts.
+ */
+int dauc_pair_count_variant(const float* pos, int64_t P, const float* neg, int64_t N,
+                            unsigned long long* wins_ties, int variant, dauc_stream_t stream);
+
+/*
+ * Search structure of dauc_auc_counts_sorted_labeled in THIS library (process-wide, default 0).
+ * Same integers in every mode.
+ *   0: the product's choice -- the count index for tables of up to 219,838 keys, unless the
+ *      device finds the table skewed (a cell of 15+ keys, or more than 1.5 keys per cell): then,
+ *      and for larger tables, the LDS search tree;
+ *   1: the LDS search tree always;
+ *   2: a 16-key-slot cell index wherever it fits (tables of up to 573,440 keys): measured slower
+ *      than the tree (four lane gathers per query).
+ */
+int dauc_set_search_mode(int mode);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* DAUC_TUNING_H */

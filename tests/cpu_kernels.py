@@ -142,6 +142,32 @@ def auc_eval_counts_part(scores, labels, part, parts, part_counts):
     return W, T, P, N, bad, other, qbad
 
 
+def auc_eval_enqueue(scores, labels, part, parts, out=None):
+    """dauc_auc_eval_enqueue's stand-in: the part's 8-word record (W, T, #non-finite queried,
+    P, 0, #non-finite positives, #labels not in {-1, 1}, verdict). The index holds the table when
+    P <= n / 2 + 1 (verdict 1); larger tables get verdict 2 (the blocking sorted path)."""
+    s, y = scores.detach().numpy(), labels.numpy().astype(np.int64)
+    n = s.size
+    ispos = y == 1
+    P = int(ispos.sum())
+    other = int(((y != 1) & (y != -1)).sum())
+    nfpos = int((~np.isfinite(s[ispos])).sum())
+    lo, hi = n * part // parts, n * (part + 1) // parts
+    rec = torch.zeros(8, dtype=torch.int64) if out is None else out
+    rec.zero_()
+    rec[3], rec[5], rec[6] = P, nfpos, other
+    if hi <= lo:
+        return rec
+    verdict = 1 if P <= n // 2 + 1 else 2
+    rec[7] = verdict
+    q = s[lo:hi][y[lo:hi] != 1]
+    rec[2] = int((~np.isfinite(q)).sum())
+    if verdict == 1 and P and not nfpos:
+        W, T = coracle_pair_count(s[ispos], q[np.isfinite(q)]) if q.size else (0, 0)
+        rec[0], rec[1] = W, T
+    return rec
+
+
 def coracle_pair_count(pos, neg):
     from oracle import coracle
 
@@ -153,7 +179,7 @@ def install(monkeypatch):
 
     for name in ("label_map_phat", "surrogate_fwdbwd", "class_sums", "alpha_from_sums", "coda_finalize",
                  "scale_div", "pd_update", "compact_positives", "auc_counts_sorted_labeled", "auc_eval_counts",
-                 "auc_eval_counts_part"):
+                 "auc_eval_counts_part", "auc_eval_enqueue"):
         monkeypatch.setattr(ops, name, globals()[name])
     monkeypatch.setattr(flat, "_check_device", lambda dev: None)
 

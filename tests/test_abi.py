@@ -20,12 +20,31 @@ def test_library_loads_and_exports_header():
     assert set(declared) == set(_lib.SIGNATURES), "Python prototypes out of sync with include/dauc.h"
 
 
-def test_exported_symbols_are_c_linkage():
-    out = subprocess.run(["nm", "-D", "--defined-only", str(_lib.LIB_PATH)], capture_output=True, text=True,
+def _exports(path):
+    out = subprocess.run(["nm", "-D", "--defined-only", str(path)], capture_output=True, text=True,
                          check=True).stdout
-    syms = {line.split()[-1] for line in out.splitlines() if line.strip()}
-    for name in _lib.header_functions():
-        assert name in syms, f"{name} not exported with C linkage"
+    return {line.split()[-1] for line in out.splitlines() if line.strip() and line.split()[-1].startswith("dauc_")}
+
+
+def test_exported_symbols_are_c_linkage():
+    """libdauc.so exports exactly the product header's entry points (no tuning variants)."""
+    syms = _exports(_lib.LIB_PATH)
+    assert syms == set(_lib.header_functions()), syms ^ set(_lib.header_functions())
+    assert not (syms & set(_lib.TUNING_SIGNATURES))
+
+
+def test_tuning_library_exports_tuning_header():
+    """tuning/libdauc_tuning.so (-DDAUC_TUNING) = the product entry points + include/dauc_tuning.h's."""
+    tuning_header = _lib.HEADER.parent / "dauc_tuning.h"
+    declared = set(_lib.header_functions(tuning_header))
+    assert declared == set(_lib.TUNING_SIGNATURES)
+    syms = _exports(_lib.TUNING_LIB_PATH)
+    assert syms == set(_lib.header_functions()) | declared
+    lib = _lib.tuning()
+    null = ctypes.c_void_p(0)
+    assert lib.dauc_pair_count_variant(null, 0, null, 0, ctypes.c_void_p(8), 7, null) == _lib.DAUC_OK  # empty: no-op
+    assert lib.dauc_pair_count_variant(null, 5, null, 5, ctypes.c_void_p(8), 12, null) == _lib.DAUC_EINVAL
+    assert lib.dauc_set_search_mode(3) == _lib.DAUC_EINVAL
 
 
 def test_library_is_gfx950_code_object():
@@ -52,7 +71,7 @@ def test_invalid_arguments_return_einval():
     null = ctypes.c_void_p(0)
     assert L.dauc_pair_count(null, -1, null, 5, null, null) == _lib.DAUC_EINVAL
     assert L.dauc_pair_count(null, 5, null, 5, ctypes.c_void_p(8), null) == _lib.DAUC_EINVAL
-    assert L.dauc_pair_count_variant(null, 0, null, 0, ctypes.c_void_p(8), 7, null) == _lib.DAUC_OK  # empty: no-op
+    assert L.dauc_pair_count(null, 0, null, 0, ctypes.c_void_p(8), null) == _lib.DAUC_OK  # empty: no-op
     assert L.dauc_surrogate_fwdbwd(null, 1, null, 1, 0, null, null, null, 1, null, null, null, null, 0,
                                    null) == _lib.DAUC_EINVAL
     assert L.dauc_pd_update(null, null, null, None, 0, null, null, null, 0.1, 0.1, 0, null) == _lib.DAUC_EINVAL
@@ -97,7 +116,9 @@ def test_ctypes_signatures_match_header_arity():
 
     text = re.sub(r"/\*.*?\*/", "", _lib.HEADER.read_text(), flags=re.S)
     decls = dict(re.findall(r"\b(dauc_[a-z0-9_]+)\s*\(([^;{]*?)\)\s*;", text))
-    for name, (_, args) in _lib.SIGNATURES.items():
+    text = re.sub(r"/\*.*?\*/", "", (_lib.HEADER.parent / "dauc_tuning.h").read_text(), flags=re.S)
+    decls.update(re.findall(r"\b(dauc_[a-z0-9_]+)\s*\(([^;{]*?)\)\s*;", text))
+    for name, (_, args) in list(_lib.SIGNATURES.items()) + list(_lib.TUNING_SIGNATURES.items()):
         params = decls[name].strip()
         n = 0 if params in ("", "void") else params.count(",") + 1
         assert n == len(args), (name, n, len(args))

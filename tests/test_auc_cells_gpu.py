@@ -1,4 +1,5 @@
-"""The search structures of the sort method (auc_sort.hip, dauc_set_search_mode) vs the C oracle.
+"""The search structures of the sort method (auc_sort.hip; dauc_set_search_mode of the tuning build,
+include/dauc_tuning.h) vs the C oracle.
 
 The labeled query pass (dauc_auc_counts_sorted_labeled, and through it dauc_auc_eval_counts)
 locates every negative among the sorted positives through one of: the count index (mode 0, the
@@ -28,10 +29,13 @@ def T(a, dev):
 
 @pytest.fixture
 def ops(dev):
+    """The ops run against the tuning build of the library, where the search mode is selectable."""
+    from distributedauc_amd import _lib
     from distributedauc_amd import ops as o
 
-    yield o
-    o.set_search_mode(0)
+    with _lib.using(_lib.tuning()):
+        yield o
+        o.set_search_mode(0)
 
 
 def _oracle_slice(s, y, begin, end):

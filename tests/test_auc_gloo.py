@@ -1,6 +1,7 @@
-"""The sharded exact-AUC orchestration on CPU (gloo, world 2 and 3): every rank runs the
-part-wise evaluation (all positives compacted and sorted locally, its slice of the scores
-streamed through the search) and one all-reduce sums (wins, ties, non-finite). Below
+"""The sharded exact-AUC orchestration on CPU (gloo, world 2 and 3): every rank enqueues its
+part (all positives compacted and indexed locally, its slice of the scores streamed through
+the search), one all-gather of the 8-word part records, counts summed on the host, and the
+ranks' records checked to agree (a rank with another test set raises on every rank). Below
 ExactAUC.SHARD_MIN scores every rank evaluates the whole vector instead (same integers, no
 collective); both modes run here. The kernels are served by the oracle (tests/cpu_kernels.py);
 the GPU form runs in bench.py --gpus 2 (tests/test_bench_gpu.py)."""
@@ -31,6 +32,7 @@ def _worker(rank, world, port, q, shard_min):
         from oracle import coracle
 
         rng = np.random.default_rng(5)
+        rng2 = np.random.default_rng(9)
         n = 20_011
         s = (np.floor(rng.random(n) * 997) / 997).astype(np.float32)
         y = np.where(rng.random(n) < 0.03, 1, -1).astype(np.int8)
@@ -48,6 +50,18 @@ def _worker(rank, world, port, q, shard_min):
         except ValueError:
             raised = True
         assert raised
+        if ev.last_mode == "sharded":
+            # ranks holding different vectors: every rank raises (no hang, no mixed counts)
+            y3 = y.copy()
+            if rank == 1:
+                y3[np.flatnonzero(y == -1)[:5]] = 1
+            with pytest.raises(RuntimeError, match="disagree"):
+                ev.counts(torch.from_numpy(y3), torch.from_numpy(s), device="cpu")
+            # a table the index cannot hold (positives > n / 2 + 1 here): the sorted path, same integers
+            y4 = np.where(rng2.random(n) < 0.7, 1, -1).astype(np.int8)
+            c4 = ev.counts(torch.from_numpy(y4), torch.from_numpy(s), device="cpu")
+            e4 = coracle.auc_counts(y4.astype(np.int64), s)
+            assert (c4["wins"], c4["ties"], c4["P"]) == (e4["wins"], e4["ties"], e4["P"])
         dist.destroy_process_group()
         q.put((rank, None))
     except BaseException:

@@ -16,22 +16,13 @@ from __future__ import annotations
 import sys
 from pathlib import Path
 
-import numpy as np
 import pytest
 import torch
 
-from oracle import coracle
-from oracle import reference_cpu as R
+import update_check
 
 pytestmark = pytest.mark.gpu
 sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
-
-
-def _dense(t: torch.Tensor, like: torch.Tensor) -> np.ndarray:
-    """t's elements in `like`'s physical order (the flat buffer's order)."""
-    if t.stride() != like.stride():
-        t = torch.empty_like(like).copy_(t)
-    return torch.as_strided(t, (t.numel(),), (1,)).detach().cpu().numpy()
 
 
 def _run(arch, batch, I, steps, expect_tensors, expect_params, dev):
@@ -41,29 +32,7 @@ def _run(arch, batch, I, steps, expect_tensors, expect_params, dev):
     st = coda.state
     assert len(st.entries) == expect_tensors and st.numel() == expect_params
     assert st.n_reduce * 4 == (st.n_params + 5) * 4 and st.n_params >= expect_params
-    checks = {"updates": 0}
-    orig_update = st.update
-
-    def checked_update(lr, gamma, mode="reference", running_average=True):
-        # everything the launch reads, captured before it runs
-        torch.cuda.synchronize()
-        w = np.concatenate([st.flat[o:o + n].cpu().numpy() for _, _, o, n in st.entries])
-        w0 = np.concatenate([st.anchor[o:o + n].cpu().numpy() for _, _, o, n in st.entries])
-        avg = np.concatenate([st.avg[o:o + n].cpu().numpy() for _, _, o, n in st.entries])
-        g = np.concatenate([_dense(p.grad, p) for _, p, _, _ in st.entries])
-        sc, g3, an = st.abalpha.cpu().numpy(), st.grad3.cpu().numpy(), st.anchor3.cpu().numpy()
-        orig_update(lr, gamma, mode, running_average)
-        torch.cuda.synchronize()
-        ew, eavg = coracle.pd_update(w, g, w0, lr, gamma, avg)
-        got_w = np.concatenate([st.flat[o:o + n].cpu().numpy() for _, _, o, n in st.entries])
-        got_avg = np.concatenate([st.avg[o:o + n].cpu().numpy() for _, _, o, n in st.entries])
-        assert np.array_equal(got_w, ew), f"{arch}: parameters differ from the oracle at step {coda.t_total}"
-        assert np.array_equal(got_avg, eavg), f"{arch}: running average differs at step {coda.t_total}"
-        ea, eb, eal = R.scalar_update(*sc[:3], *g3[:3], *an[:3], lr, gamma, mode)
-        assert st.abalpha.cpu().numpy().tolist() == [ea, eb, eal]
-        checks["updates"] += 1
-
-    st.update = checked_update
+    checks = update_check.install(coda, arch)
     pos = neg = 0
     for _ in range(steps):
         x, labels = next(it)

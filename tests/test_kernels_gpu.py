@@ -125,14 +125,15 @@ def test_surrogate_large_deterministic(dev):
     assert outs[0][4] == np.sum(yn == 1)
 
 
-@pytest.mark.parametrize("B", [(1 << 20), (1 << 20) + 37, 3 * (1 << 20) + 4099, (1 << 24) + 5])
+@pytest.mark.parametrize("B", [(1 << 20), (1 << 22), (1 << 22) + 37, 3 * (1 << 22) + 4099, (1 << 24) + 5])
 def test_surrogate_chunked_variants(dev, B):
-    """One-chunk-per-workgroup kernel (default for unit-stride B >= 2^20, two-level ticket)
-    and every tuning variant: fp64 closed form within 1e-6 of term scale, dh and counts
-    bitwise equal across variants (dh is per-element; the sums only differ in tree order),
-    bitwise run-to-run, ragged last chunk, and the workspace left zeroed for the next call.
-    Variants 8..14 (single-launch tickets) run interleaved with the others on the
-    same workspace, 1 to 33 ticket groups."""
+    """The one-launch tail kernel (the default for unit-stride B >= 2^22) and the tuning build's
+    alternatives (include/dauc_tuning.h: 1 persistent, 2 two-launch, 3 stream alone, 4 tail stream
+    without its reduce, 5 stamped tail, 6..9 early group reducers): fp64 closed form within 1e-6 of
+    term scale, dh and counts
+    bitwise equal across variants (dh is per-element; the sums only differ in tree order), bitwise
+    run-to-run, ragged last chunk; the default and the variants interleave on one workspace (the
+    epoch-tagged granules need no cleanup between calls)."""
     from distributedauc_amd import ops
 
     g = torch.Generator(device=dev).manual_seed(B & 0xFFFF)
@@ -146,38 +147,76 @@ def test_surrogate_chunked_variants(dev, B):
     k = np.where(yn == 1, 0.1 + 1 + 0.3, -0.2 - 1 - 0.3)
     c = 2.0 / B * (np.abs(hn) + np.abs(k))
     ref_dh = None
-    tick = {}
-    for variant in (0, 0, 1, 2, 3, 4, 5, 6, 7, 8, 8, 9, 10, 11, 12, 13, 14, 2, 8, 1, 12, 14, 16, 17, 18, 19, 19,
-                    0, 16, 20, 20, 21, 22, 0, 20, 8, 21, 23, 24, 25, 0, 25, 24, 26, 27, 28, 26, 0, 28):
+    seen = {}
+    for variant in (0, 0, 1, 2, 3, 0, 4, 0, 5, 5, 2, 0, 1, 4, 5, 6, 7, 0, 8, 9, 6, 0):
         o = torch.zeros(6, dtype=torch.float64, device=dev)
         dh = torch.full((B,), float("nan"), device=dev)
         ops.surrogate_fwdbwd(h, y, abap[:3], abap[3:], dh=dh, out64=o, variant=variant)
         got, dhn = o.cpu().numpy(), dh.cpu().numpy()
+        if ref_dh is None:
+            ref_dh = dhn
+        assert np.array_equal(dhn, ref_dh), variant
+        assert np.all(np.abs(dhn - dh64) <= 1e-6 * np.maximum(np.abs(dh64), c)), variant
+        if variant in (3, 4):  # the stream without its reduce: no scalar outputs
+            assert not o.any(), variant
+            continue
         assert np.all(np.abs(got[:4] - [F, da, db, dal]) <= 1e-6 * sc + 1e-12), (variant, got, F)
         assert got[4] == np.sum(yn == 1) and got[5] == np.sum(yn == -1), variant
-        assert np.all(np.abs(dhn - dh64) <= 1e-6 * np.maximum(np.abs(dh64), c)), variant
-        if ref_dh is None:
-            ref_dh, ref0 = dhn, got
-        else:
-            assert np.array_equal(dhn, ref_dh), variant
-        if variant == 0:
-            assert np.array_equal(got, ref0)  # deterministic reduction order
-        if variant >= 8:  # fixed blockIdx summation order: bitwise run-to-run
-            assert np.array_equal(got, tick.setdefault(variant, got)), variant
-    # variant 15: the streaming kernel alone (own workspace): the same dh, no scalar outputs
-    dh = torch.full((B,), float("nan"), device=dev)
-    o = torch.zeros(6, dtype=torch.float64, device=dev)
-    ops.surrogate_fwdbwd(h, y, abap[:3], abap[3:], dh=dh, out64=o, variant=15)
-    assert np.array_equal(dh.cpu().numpy(), ref_dh) and not o.any()
-    o = torch.zeros(6, dtype=torch.float64, device=dev)
-    ops.surrogate_fwdbwd(h, y, abap[:3], abap[3:], dh=dh, out64=o)  # the shared workspace is still clean
-    assert np.array_equal(o.cpu().numpy(), ref0)
+        # fixed summation orders: bitwise run-to-run per variant (5 = 0's kernel with stamps; 6..9 =
+        # the early-reducer kernel: stamps and the lag change which workgroup reduces, not the order)
+        key = {5: 0, 7: 6, 8: 6, 9: 6}.get(variant, variant)
+        assert np.array_equal(got, seen.setdefault(key, got)), variant
     sums = torch.zeros(4, dtype=torch.float64, device=dev)
     ops.class_sums(h, y, sums, accumulate=False)  # chunked CLASS_ONLY path
     s = sums.cpu().numpy()
     hd = hn.astype(np.float64)
     assert np.allclose(s, [hd[yn == -1].sum(), (yn == -1).sum(), hd[yn == 1].sum(), (yn == 1).sum()],
                        rtol=1e-7, atol=0)
+
+
+def test_surrogate_tail_ignores_stale_granules(dev):
+    """The one-launch loss hands rows over as epoch-tagged granules (surrogate.hip, tail kernel):
+    a granule written by a workgroup of an EARLIER call -- e.g. one that stored its row after that
+    call's reducer gave up waiting -- carries an older tag and is never taken for a current one.
+    Here every row and group-total granule of the workspace is overwritten between calls with the
+    previous call's tag (and, once, with random tags) and garbage payloads: the next call is
+    bit-identical to a clean one, and the epoch word advances by one per call."""
+    from distributedauc_amd import _lib, ops
+
+    B = (1 << 22) + 4099
+    g = torch.Generator(device=dev).manual_seed(11)
+    h = torch.rand(B, device=dev, generator=g)
+    y = torch.where(torch.rand(B, device=dev, generator=g) < 0.1, 1, -1).to(torch.int8)
+    abap = torch.tensor([0.1, -0.2, 0.3, 0.1], device=dev)
+
+    def call():
+        o = torch.zeros(6, dtype=torch.float64, device=dev)
+        ops.surrogate_fwdbwd(h, y, abap[:3], abap[3:], out64=o)
+        torch.cuda.synchronize()
+        return o.cpu().numpy()
+
+    ref = call()
+    ws = ops.workspaces.get(dev, "surrogate", _lib.load().dauc_surrogate_workspace_size(B))
+    # the tail region's offset (surrogate.hip: tail_offset): the persistent kernel's region
+    # (256 + 2048 * 6 * 8 B), then the two-launch form's rows + reduce slots, 256-B aligned
+    nb = -(-B // 4096)
+    chunk = nb * 48 + 256 + -(-nb // 512) * 48
+    off = 256 + 2048 * 48 + -(-chunk // 256) * 256
+    words = ws[off: off + 256 + (nb + 64) * 80].view(torch.int64)
+    epoch = int(words[0].item()) & 0xFFFFFFFF
+    gran = words[32:]  # the 256-B header, then the granules
+    rng = torch.Generator(device=dev).manual_seed(5)
+    for k in range(3):
+        assert int(words[0].item()) & 0xFFFFFFFF == epoch
+        garbage = torch.randint(0, 1 << 31, gran.shape, device=dev, generator=rng)
+        if k < 2:
+            stale_tag = ((epoch - 1) & 0xFFFFFFFF) | 0x80000000
+            hi = (stale_tag << 32) - (1 << 64)  # the tag in the high word, as a signed int64
+            gran.copy_(garbage + hi)
+        else:
+            gran.copy_(garbage * (1 << 32) + garbage)  # random tags (bit 31 clear: never current)
+        assert np.array_equal(call(), ref), k
+        epoch = (epoch + 1) & 0xFFFFFFFF
 
 
 def test_class_sums_and_alpha(dev):
@@ -466,8 +505,8 @@ def test_auc_eval_counts_one_call(dev, ldtype):
             assert (W, Tt) == (e["wins"], e["ties"]), (n, p)
         else:
             assert (W, Tt) == (0, 0)
-    # repeated length: the previous call's P is used before the real one is known (a hit when the
-    # data repeat, a re-run at the real size when the class sizes differ), both table sides
+    # repeated length, other class sizes (the calls keep no state: each does the same work), both
+    # table sides
     n = 300_001
     data = []
     for p in (0.02, 0.03, 0.02, 0.7, 0.02):
@@ -480,7 +519,7 @@ def test_auc_eval_counts_one_call(dev, ldtype):
         assert (W, Tt, P, N, bad) == (e["wins"], e["ties"], e["P"], e["N"], 0), k
     # the direct count-index build (no sort) and its fallback to the sorted path: tie-heavy and
     # clustered positive tables (a cell of 15+ keys, too many keys per cell) alternate with
-    # spread ones of the same length, so the speculative size hits and misses on both paths
+    # spread ones of the same length
     n = 200_003
     base = rng.random(n, dtype=np.float32)
     yb = np.where(rng.random(n) < 0.03, 1, -1).astype(ldtype)
@@ -509,10 +548,10 @@ def test_auc_eval_counts_one_call(dev, ldtype):
 
 
 def test_auc_eval_counts_stale_workspace(dev):
-    """The one-call evaluation keeps its compaction counters in the workspace between calls on a
-    thread; a workspace whose contents changed since (here: overwritten with garbage, as a
-    freed-and-reallocated buffer at the same address would be) must be detected by the slot tag
-    and the call must still return the C oracle's counts (and never write out of bounds)."""
+    """The evaluation re-initialises every byte of state it reads (one memset of the workspace
+    header per call): a workspace overwritten with garbage between calls (as a freed-and-
+    reallocated buffer would be) still gives the C oracle's counts, and nothing is written out of
+    bounds."""
     from distributedauc_amd import _lib, ops
 
     rng = np.random.default_rng(12)
@@ -538,8 +577,7 @@ def test_auc_eval_counts_part(dev):
     parts' (W, T) sum to the C oracle's on both table sides (P < N: score ranges; P > N: positive
     ranges), including G larger than a tiny n (empty parts); the device part_counts equal the host
     ones; P, N and the global checks are the same on every part; a non-finite negative shows up
-    in exactly the part whose range holds it; speculation hits and misses (parts re-use the
-    previous call's P)."""
+    in exactly the part whose range holds it."""
     from distributedauc_amd import ops
 
     rng = np.random.default_rng(91)
@@ -566,6 +604,58 @@ def test_auc_eval_counts_part(dev):
     s[j] = np.nan
     pc = torch.zeros(3, dtype=torch.int64, device=dev)
     seen = [ops.auc_eval_counts_part(T(s, dev), T(y, dev), r, 4, pc)[6] for r in range(4)]
+    assert seen == [0, 0, 0, 1], seen
+
+
+def test_auc_eval_enqueue_records(dev):
+    """dauc_auc_eval_enqueue (the sharded evaluation's per-rank part, no host synchronisation): for
+    G = 1, 2, 3, 8 the parts' W, T sum to the C oracle's; P, the non-finite and label counts are
+    the same in every part's record; verdict 1 where the count index holds the table, 0 for an
+    empty part (G > n), and 2 on EVERY part for tables it cannot hold (more positives than
+    n / 2 + 1, a tie-heavy or clustered table) -- the blocking part then gives the oracle's
+    integers; a NaN negative is counted in exactly the part that queries it."""
+    from distributedauc_amd import ops
+
+    rng = np.random.default_rng(93)
+    base = rng.random(300_001, dtype=np.float32)
+    cases = []
+    for p in (0.02, 0.001, 0.6):
+        cases.append(("spread", p, base, np.where(rng.random(base.size) < p, 1, -1).astype(np.int8)))
+    yb = np.where(rng.random(base.size) < 0.03, 1, -1).astype(np.int8)
+    cases.append(("all_equal", 0.03, np.where(yb == 1, np.float32(0.25), base).astype(np.float32), yb))
+    cases.append(("cluster", 0.03, np.where(yb == 1, np.float32(0.5) + base * np.float32(1e-6), base).astype(np.float32), yb))
+    cases.append(("tiny", 0.4, base[:5].copy(), np.array([1, -1, -1, 1, -1], np.int8)))
+    for name, p, s, y in cases:
+        e = coracle.auc_counts(y.astype(np.int64), s)
+        for G in (1, 2, 3, 8):
+            recs = []
+            for r in range(G):
+                out = torch.full((8,), -7, dtype=torch.int64, device=dev)
+                ops.auc_eval_enqueue(T(s, dev), T(y, dev), r, G, out=out)
+                recs.append(out.cpu().tolist())
+            assert {(v[3], v[4], v[5], v[6]) for v in recs} == {(e["P"], 0, 0, 0)}, (name, G, recs)
+            verdicts = {v[7] for v in recs} - {0}
+            assert len(verdicts) == 1, (name, G, recs)
+            n = s.size
+            if G > n:
+                assert any(v[7] == 0 and v[0] == v[1] == 0 for v in recs)
+            fits = name in ("spread", "tiny") and e["P"] <= n // 2 + 1
+            if name != "cluster":  # a clustered table may or may not overflow a cell: either is exact
+                assert verdicts == ({1} if fits else {2}), (name, G, verdicts)
+            if verdicts == {1}:
+                assert (sum(v[0] for v in recs), sum(v[1] for v in recs)) == (e["wins"], e["ties"]), (name, G)
+                assert sum(v[2] for v in recs) == 0
+            else:
+                W = Tt = 0
+                for r in range(G):
+                    pc = torch.zeros(3, dtype=torch.int64, device=dev)
+                    o = ops.auc_eval_counts_part(T(s, dev), T(y, dev), r, G, pc)
+                    W, Tt = W + o[0], Tt + o[1]
+                assert (W, Tt) == (e["wins"], e["ties"]), (name, G)
+    s = rng.random(100_003, dtype=np.float32)
+    y = np.where(rng.random(s.size) < 0.05, 1, -1).astype(np.int8)
+    s[int(np.flatnonzero(y == -1)[-2])] = np.nan  # in the last part's range
+    seen = [ops.auc_eval_enqueue(T(s, dev), T(y, dev), r, 4)[2].item() for r in range(4)]
     assert seen == [0, 0, 0, 1], seen
 
 
