@@ -1607,6 +1607,12 @@ __device__ __forceinline__ void ci_fix(unsigned x, unsigned rl, unsigned cnt, co
 #ifndef DAUC_CI_U
 #define DAUC_CI_U (DAUC_CI_PIPE ? 1 : 2)  // float4 slots per thread per group (int8 labels)
 #endif
+#ifndef DAUC_CI_COUNT3
+#define DAUC_CI_COUNT3 0  // 1: branch-free window counts by min/max (no compare into SGPRs)
+#endif
+#ifndef DAUC_CI_DEPTH
+#define DAUC_CI_DEPTH 1  // groups of stream loads in flight ahead of the group being located
+#endif
 
 // The labeled query pass over the count index (same stream and checks as query_labeled_kernel);
 // returns at once when the builder kept the tree, so it is enqueued unconditionally. Per
@@ -1765,9 +1771,49 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
 #pragma unroll
             for (int q = 0; q < NQ; ++q) {
                 const unsigned rl = g.rc[q] & 0x0fffffffu;
+#if DAUC_CI_COUNT3
+                // every lane loads the window at rank_lo & ~3, an empty cell's too: its keys before
+                // rank_lo are of earlier cells (< x), the others of later cells or padding (> x)
+                g.k[q] = *reinterpret_cast<const uint4*>(sorted + (rl & ~3u));
+#else
                 g.k[q] = *reinterpret_cast<const uint4*>(sorted + ((g.rc[q] >> 28) ? rl & ~3u : 0u));
+#endif
             }
         };
+#if DAUC_CI_COUNT3
+        // Branch-free counts, no compare results in scalar registers: with med(k, lo, hi) =
+        // min(max(k, lo), hi), med(k, x, x+1) - x = [k > x] and med(k, x-1, x) - (x-1) = [k >= x],
+        // so s1 = sum med(k, x, x+1) = 4x + #(> x), s2 = sum med(k, x-1, x) = 4x - 4 + #(>= x) and
+        // W += M - (a + #(<= x)) = M - 4 - a - 4x + s1, T += #(<= x) - #(< x) = s2 - s1 + 4 (mod 2^32;
+        // a NaN query's key may wrap x +- 1, and a NaN makes the evaluation an error anyway).
+        // Positive-label queries are masked out (m = 0).
+        auto count = [&](const Group& g) {
+            unsigned wl = 0u, tl = 0u;
+            bool more = false;
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                const unsigned x = g.x[q], xp = x + 1u, xm = x - 1u;
+                const unsigned rl = g.rc[q] & 0x0fffffffu, cnt = g.rc[q] >> 28, a = rl & ~3u;
+                const uint4 k = g.k[q];
+                auto med = [](unsigned v, unsigned lo, unsigned hi) { return min(max(v, lo), hi); };
+                const unsigned s1 = (med(k.x, x, xp) + med(k.y, x, xp)) + (med(k.z, x, xp) + med(k.w, x, xp));
+                const unsigned s2 = (med(k.x, xm, x) + med(k.y, xm, x)) + (med(k.z, xm, x) + med(k.w, xm, x));
+                const unsigned m = 0u - ((g.use >> q) & 1u);
+                wl += (M32 - 4u - a - 4u * x + s1) & m;
+                tl += (s2 - s1 + 4u) & m;
+                more |= ((g.use >> q) & 1u) && (rl & 3u) + cnt > 4u;
+            }
+            w += wl;
+            t += tl;
+            if (more) {
+#pragma unroll
+                for (int q = 0; q < NQ; ++q) {
+                    const unsigned rl = g.rc[q] & 0x0fffffffu, cnt = g.rc[q] >> 28;
+                    if (((g.use >> q) & 1u) && (rl & 3u) + cnt > 4u) ci_fix(g.x[q], rl, cnt, g.k[q], sorted, w, t);
+                }
+            }
+        };
+#else
         auto count = [&](const Group& g) {
             unsigned wl = 0u, tl = 0u;
             bool more = false;
@@ -1787,37 +1833,42 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
                 }
             }
         };
-        // per group g: keys(g) [its stream loads were issued one group earlier], stream loads of
-        // g + 1, LDS lookups + window loads of g, count of g - 1 [its windows were issued one group
-        // earlier; the younger loads stay in flight: vmcnt retires in order]
-        Stream sa, sb;
-        Group ga, gb;
-        load(sa, tid);
-        keys(ga, sa);
-        load(sb, tid + step);
-        locate(ga);
-        for (int64_t v = tid + step;;) {
-            if (v >= nvec) {
-                count(ga);
-                break;
+#endif
+        // per group g: keys(g) [its stream loads were issued D groups earlier], stream loads of
+        // g + D into the buffer just read, LDS lookups + window loads of g, count of g - 1 [its
+        // windows were issued one group earlier; the younger loads stay in flight: vmcnt retires
+        // in order]. D stream buffers keep D groups of score/label loads in flight per lane: with
+        // one (D = 1) a wave holds 20 B per lane in flight, 5 MB over the chip, which at HBM's
+        // loaded latency caps the stream far below the bandwidth.
+        constexpr int D = DAUC_CI_DEPTH;
+        constexpr int L = D % 2 == 0 ? D : 2 * D;  // unroll: every buffer index compile-time
+        Stream sbuf[D];
+        Group gbuf[2];
+#pragma unroll
+        for (int j = 0; j < D; ++j) load(sbuf[j], tid + int64_t(j) * step);
+        keys(gbuf[0], sbuf[0]);
+        load(sbuf[0], tid + int64_t(D) * step);
+        locate(gbuf[0]);
+        int64_t v = tid + step;
+        for (;;) {
+#pragma unroll
+            for (int j = 0; j < L; ++j) {
+                // group v sits in stream buffer (j + 1) % D and group slot (j + 1) % 2
+                Group& gc = gbuf[(j + 1) % 2];
+                Group& gp = gbuf[j % 2];
+                if (v >= nvec) {
+                    count(gp);
+                    goto ci_stream_done;
+                }
+                keys(gc, sbuf[(j + 1) % D]);
+                load(sbuf[(j + 1) % D], v + int64_t(D) * step);
+                asm volatile("" ::: "memory");  // the stream loads stay older than this group's windows
+                locate(gc);
+                count(gp);
+                v += step;
             }
-            keys(gb, sb);
-            load(sa, v + step);
-            asm volatile("" ::: "memory");  // the stream loads stay older than this group's windows
-            locate(gb);
-            count(ga);
-            v += step;
-            if (v >= nvec) {
-                count(gb);
-                break;
-            }
-            keys(ga, sa);
-            load(sb, v + step);
-            asm volatile("" ::: "memory");
-            locate(ga);
-            count(gb);
-            v += step;
         }
+    ci_stream_done:;
     } else {
         for (int64_t v = tid; v < nvec; v += stride)
             for (int q = 0; q < 4; ++q) one(head + v * 4 + q);

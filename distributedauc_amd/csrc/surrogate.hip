@@ -729,6 +729,118 @@ __global__ __launch_bounds__(kThreads, DAUC_TAIL_WAVES) void surrogate_tail_kern
     }
 }
 
+// ---- the one-launch loss with R EXTRA reducer workgroups that stream nothing ----------------
+//
+// The stamps of the kernel above put its tail (6.3-6.6 us after the last row store) in the
+// reducers: they are the last 64 STREAMING workgroups, so every group total waits for its
+// reducer's own chunk, and the groups next to the end hold the grid's last rows -- two hops
+// (row -> group reducer -> final) after the last row, each a write-through store and a poll.
+// Here the grid is nblocks + R: the R reducers come after every streaming workgroup and stream
+// nothing, so they are polling as soon as the last streaming workgroups are dispatched. The
+// final reducer (the grid's last workgroup) takes the last K rows itself (K / 256 per thread) and
+// the R - 1 group totals of rows [0, nblocks - K), which complete K rows' streaming time (~K / 190
+// us at 2^26) before the last row: after the last row lands one hop is left. PLAIN: the epoch is
+// read with a plain load (every read of it precedes the final's store; a later call reads it across
+// the kernel boundary). Same granules, epochs, bounded polls and fixed summation order as above.
+template <typename YT, int S, int R, int K, bool PLAIN, bool STAMPS, int WAVES = DAUC_TAIL_WAVES>
+__global__ __launch_bounds__(kThreads, WAVES) void surrogate_tail_x_kernel(
+    const float* __restrict__ h, const YT* __restrict__ y, int64_t B, int64_t nblocks, double invB,
+    const float* __restrict__ abalpha, const float* __restrict__ p_hat, float* __restrict__ dh, TailWs ws,
+    double* __restrict__ out64, float* __restrict__ grad3, float* __restrict__ loss) {
+    static_assert(K % kThreads == 0 && R <= kThreads, "final reducer: K / 256 rows and one group total per thread");
+    const unsigned epoch = __builtin_amdgcn_readfirstlane(
+        PLAIN ? *ws.epoch : __hip_atomic_load((gu32*)ws.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    const unsigned tag = epoch | 0x80000000u;
+    const float sa = abalpha[0], sb = abalpha[1], sal = abalpha[2], sp = p_hat[0];
+    const int64_t b = blockIdx.x;
+    if (b < nblocks) {
+        const SurrogateScalars s = make_scalars_v(sa, sb, sal, sp, invB);
+        const double v = stream_chunk<YT, false, S>(h, y, B, s, dh, gran_total(threadIdx.x < kGran ? threadIdx.x : 0));
+        publish_granule(ws.rows + b * kGran, tag, v);
+        if (STAMPS && threadIdx.x == 0) ws.stamps[b] = realtime();
+        return;
+    }
+    const int64_t r = b - nblocks;
+    const bool final_red = r == R - 1;
+    // the final's direct rows: [k0, nblocks); groups split [0, k0) into R - 1 contiguous ranges
+    const int64_t k0 = nblocks > K ? nblocks - K : 0;
+    const int64_t G = (k0 + R - 2) / (R - 1);
+    __shared__ double scratch[kNumAcc * kWaves];
+    __shared__ int bad;
+    unsigned long long* st = STAMPS ? ws.stamps + nblocks + 8 * r : nullptr;
+    if (STAMPS && threadIdx.x == 0) st[0] = realtime();
+    if (threadIdx.x == 0) bad = 0;
+    bool ok = true;
+    double tot[kNumAcc];
+#pragma unroll
+    for (int k = 0; k < kNumAcc; ++k) tot[k] = 0.0;
+    if (!final_red) {
+        const int64_t g0 = r * G < k0 ? r * G : k0, g1 = g0 + G < k0 ? g0 + G : k0;
+        for (int64_t i = g0 + threadIdx.x; i < g1; i += kThreads) {
+            unsigned p[kGran];
+            const unsigned miss = poll_row(ws.rows + i * kGran, tag, p);
+            if (!wait_row(ws.rows + i * kGran, tag, miss, p)) {
+                ok = false;
+                break;
+            }
+            add_row(p, tot);
+        }
+    } else {
+        // every poll of the thread in flight before any wait: its K / 256 rows and group total t
+        constexpr int KR = K / kThreads;
+        unsigned p[KR + 1][kGran], miss[KR + 1];
+#pragma unroll
+        for (int j = 0; j < KR; ++j) {
+            const int64_t i = k0 + int64_t(j) * kThreads + threadIdx.x;
+            miss[j] = i < nblocks ? poll_row(ws.rows + i * kGran, tag, p[j]) : 0u;
+            if (i >= nblocks) {
+#pragma unroll
+                for (int k = 0; k < kGran; ++k) p[j][k] = 0u;
+            }
+        }
+        const bool holds = threadIdx.x < R - 1;
+        miss[KR] = holds ? poll_row(ws.gtot + threadIdx.x * kGran, tag, p[KR]) : 0u;
+        if (!holds) {
+#pragma unroll
+            for (int k = 0; k < kGran; ++k) p[KR][k] = 0u;
+        }
+#pragma unroll
+        for (int j = 0; j < KR; ++j) {
+            const int64_t i = k0 + int64_t(j) * kThreads + threadIdx.x;
+            if (i < nblocks && !wait_row(ws.rows + i * kGran, tag, miss[j], p[j])) ok = false;
+        }
+        if (holds && !wait_row(ws.gtot + threadIdx.x * kGran, tag, miss[KR], p[KR])) ok = false;
+        // fixed order per thread: its rows by index, then its group total
+#pragma unroll
+        for (int j = 0; j <= KR; ++j) add_row(p[j], tot);
+    }
+    if (STAMPS && threadIdx.x == 0) st[1] = realtime();
+    __syncthreads();  // orders bad = 0 before any thread's bad = 1
+    if (!ok) bad = 1;
+    block_sum<kNumAcc>(tot, scratch);  // its barriers order the flag
+    ok = bad == 0;
+    if (STAMPS && threadIdx.x == 0) st[2] = realtime();
+    if (!ok) {
+#pragma unroll
+        for (int k = 0; k < kNumAcc; ++k) tot[k] = __builtin_nan("");
+    }
+    if (!final_red) {
+        double v = tot[0];
+#pragma unroll
+        for (int k = 1; k < kNumAcc; ++k)
+            if (threadIdx.x < kGran && gran_total(threadIdx.x) == k) v = tot[k];
+        publish_granule(ws.gtot + r * kGran, tag, v);
+        if (STAMPS && threadIdx.x == 0) st[3] = realtime();
+        return;
+    }
+    if (threadIdx.x == 0) {
+        finalize(tot, make_scalars_v(sa, sb, sal, sp, invB), invB, out64, grad3, loss);
+        // the call's last action: every workgroup has read the epoch (its row or total has arrived)
+        __hip_atomic_store((gu32*)ws.epoch, epoch + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (STAMPS) st[5] = realtime();
+    }
+}
+
 // ---- the same one-launch loss with EARLY group reducers ------------------------------------
 //
 // The stamps of the kernel above (variant 5, scripts/probe_tail_stamps.py) show its tail after
@@ -895,6 +1007,19 @@ int launch_tail(const float* h, const YT* y, int64_t B, const float* abalpha, co
     return launch_status();
 }
 
+template <typename YT, int R, int K, bool PLAIN, bool STAMPS = false, int WAVES = DAUC_TAIL_WAVES>
+int launch_tail_x(const float* h, const YT* y, int64_t B, const float* abalpha, const float* p_hat, float* dh,
+                  double* out64, float* grad3, float* loss, void* ws, size_t ws_bytes, hipStream_t st) {
+    const int64_t nblocks = chunk_blocks(B);
+    if (nblocks + R > 0x7fffffffLL) return DAUC_EINVAL;
+    if (ws == nullptr || ws_bytes < tail_offset(nblocks) + tail_ws_bytes(nblocks, R, STAMPS)) return DAUC_EINVAL;
+    const TailWs w = tail_ws(static_cast<char*>(ws) + tail_offset(nblocks), nblocks, R, STAMPS);
+    hipLaunchKernelGGL((surrogate_tail_x_kernel<YT, kChunkSlots, R, K, PLAIN, STAMPS, WAVES>),
+                       dim3(static_cast<unsigned>(nblocks + R)), dim3(kThreads), 0, st, h, y, B, nblocks,
+                       1.0 / static_cast<double>(B), abalpha, p_hat, dh, w, out64, grad3, loss);
+    return launch_status();
+}
+
 // the lag of the early reducers: 2 x the resident workgroups (8 per CU on 256 CUs)
 #ifndef DAUC_TAIL_LAG
 #define DAUC_TAIL_LAG 4096
@@ -983,6 +1108,18 @@ int launch_surrogate(const float* h, int64_t hs, const YT* y, int64_t B, const f
                 case 7: return launch_tail_early<YT, true>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, ws, ws_bytes, st);
                 case 8: return launch_tail_early<YT>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, ws, ws_bytes, st, 2048);
                 case 9: return launch_tail_early<YT>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, ws, ws_bytes, st, 8192);
+                case 10: return launch_tail_x<YT, kTailReducers, 512, false>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, ws, ws_bytes, st);
+                case 11: return launch_tail_x<YT, kTailReducers, 512, true>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, ws, ws_bytes, st);
+                case 12: return launch_tail_x<YT, kTailReducers, 256, true>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, ws, ws_bytes, st);
+                case 13: return launch_tail_x<YT, kTailReducers, 1024, true>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, ws, ws_bytes, st);
+                case 14: return launch_tail_x<YT, kTailReducers, 512, true, true>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, ws, ws_bytes, st);
+                case 15: return launch_tail_x<YT, 32, 512, true>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, ws, ws_bytes, st);
+                case 16: return launch_tail_x<YT, 128, 512, true>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, ws, ws_bytes, st);
+                case 17: return launch_tail_x<YT, 128, 1024, true, false, 8>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, ws, ws_bytes, st);
+                case 18: return launch_tail_x<YT, 128, 1536, true, false, 8>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, ws, ws_bytes, st);
+                case 19: return launch_tail_x<YT, 256, 1024, true, false, 8>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, ws, ws_bytes, st);
+                case 20: return launch_tail_x<YT, 128, 512, true, false, 8>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, ws, ws_bytes, st);
+                case 21: return launch_tail_x<YT, 128, 512, true, true>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, ws, ws_bytes, st);
                 default: return DAUC_EINVAL;
             }
         }
@@ -1178,7 +1315,7 @@ int dauc_surrogate_fwdbwd_variant(const float* h, int64_t h_stride, const void* 
                                   double* out64, float* grad3, float* loss, void* workspace,
                                   size_t workspace_bytes, int variant, dauc_stream_t stream) {
     if (B <= 0 || h == nullptr || y == nullptr || abalpha == nullptr || p_hat == nullptr ||
-        h_stride <= 0 || (dh != nullptr && dh_stride <= 0) || variant < 0 || variant > 9)
+        h_stride <= 0 || (dh != nullptr && dh_stride <= 0) || variant < 0 || variant > 21)
         return DAUC_EINVAL;
     return dispatch_labels<false>(h, h_stride, y, y_dtype, B, abalpha, p_hat, dh, dh_stride, out64,
                                   grad3, loss, nullptr, 0, workspace, workspace_bytes,

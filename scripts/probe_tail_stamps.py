@@ -21,7 +21,7 @@ calls = int(sys.argv[1]) if len(sys.argv) > 1 else 20
 variant = int(sys.argv[2]) if len(sys.argv) > 2 else 5
 dev = torch.device("cuda", 0)
 B = 1 << 26
-R = 64 if variant == 5 else 256  # group-total rows the kernel's workspace layout reserves
+R = {5: 64, 14: 64, 21: 128}.get(variant, 256)  # group-total rows the kernel's workspace layout reserves
 g = torch.Generator(device=dev).manual_seed(7)
 h = torch.rand(B, device=dev, generator=g)
 y = torch.where(torch.rand(B, device=dev, generator=g) < 0.1, 1, -1).to(torch.int8)
@@ -47,7 +47,7 @@ for c in range(calls):
     rows, red = s[:nb], s[nb:].reshape(R, 8)
     t_last, first = rows.max(), rows.min()
     used = red[:, 0] > 0
-    fin = 63 if variant == 5 else int(np.flatnonzero(used).max())
+    fin = R - 1 if variant in (5, 14, 21) else int(np.flatnonzero(used).max())
     others = [i for i in np.flatnonzero(used) if i != fin]
     pub = red[others, 3] - t_last
     rec = {"call": c, "stream_us": t_last - first, "rows_last_1pct_us": float(t_last - np.percentile(rows, 99)),
