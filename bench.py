@@ -541,10 +541,10 @@ def bench_surrogate(args, device):
     #     launch stream (the average includes the gaps between calls, not per-call event packets)
     ms = b2b(0)
     loss = float(out64[0].item())
-    # the tuning build's stream alone (variant 3: no hand-off, no reduce) and the one-launch
-    # kernel's stream with its tagged row stores but nobody reducing (variant 4)
+    # the tuning build's stream alone (variant 3: no hand-off, no reduce) and the product
+    # kernel's stream with its tagged row stores but nobody reducing (variant 22)
     stream_ms = b2b(3)
-    tail_stream_ms = b2b(4)
+    tail_stream_ms = b2b(22)
     # (2) an event pair around every call (each pair adds its own marker packets to the stream)
     kt = KernelTimer(_lib.load(), "dauc_surrogate_fwdbwd")
     kt.enabled = True
@@ -561,8 +561,9 @@ def bench_surrogate(args, device):
             "timing": f"HIP events around {args.sur_reps} back-to-back calls on the launch stream, divided by the "
                       "call count (per_call_events_us: an event pair around every call instead)",
             "loss": loss,
-            "roofline": {"kernel": "dauc_surrogate_fwdbwd (whole call)", "launches": "surrogate_tail_kernel: the stream "
-                         "and its fp64 row reduce (by the last 64 workgroups, epoch-tagged granules) in ONE launch",
+            "roofline": {"kernel": "dauc_surrogate_fwdbwd (whole call)", "launches": "surrogate_tail_x_kernel: the stream "
+                         "and its fp64 row reduce (by 128 extra workgroups that stream nothing, the last one taking "
+                         "the grid's last 512 rows itself; epoch-tagged granules) in ONE launch",
                          "bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS, "traffic": load_traffic(f"surrogate_2^{args.sur_log2b}"),
                          "bytes_per_launch": nbytes},
@@ -571,9 +572,10 @@ def bench_surrogate(args, device):
                               "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": sgbs / HBM_PEAK_GBS,
                               "bytes_per_launch": nbytes},
             "tail_stream_us": tail_stream_ms * 1e3,
-            "tail_stream_what": "the one-launch kernel's stream with its tagged row stores, nobody reducing (variant 4)",
+            "tail_stream_what": "the product kernel's stream with its tagged row stores, its reducers returning at "
+                                "once (variant 22)",
             "row_reduce_us": (ms - tail_stream_ms) * 1e3,
-            "row_reduce_what": "whole call - variant 4: the in-launch hand-off chain after the last row lands"}
+            "row_reduce_what": "whole call - variant 22: the in-launch hand-off chain after the last row lands"}
 
 
 # ----------------------------------------------------------------------------- CPU baselines

@@ -1607,6 +1607,13 @@ __device__ __forceinline__ void ci_fix(unsigned x, unsigned rl, unsigned cnt, co
 #ifndef DAUC_CI_U
 #define DAUC_CI_U (DAUC_CI_PIPE ? 1 : 2)  // float4 slots per thread per group (int8 labels)
 #endif
+#ifndef DAUC_CI_ABLATE2
+#define DAUC_CI_ABLATE2 0  // timing ablations only (wrong counts): 1 every window at the table's start,
+                           // 2 the LDS lookups at lane-uniform addresses (same dependency chain), 3 both
+#endif
+#ifndef DAUC_CI_W2
+#define DAUC_CI_W2 1  // 1: the second window of a cell past its first loaded with the first (no branch)
+#endif
 #ifndef DAUC_CI_COUNT3
 #define DAUC_CI_COUNT3 0  // 1: branch-free window counts by min/max (no compare into SGPRs)
 #endif
@@ -1730,6 +1737,9 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
         struct Group {
             unsigned x[NQ], rc[NQ];
             uint4 k[NQ];
+#if DAUC_CI_W2
+            uint4 k2[NQ];  // the next window, for cells that run past the first
+#endif
             unsigned use;
         };
         auto keys = [&](Group& g, const Stream& sg) {
@@ -1752,13 +1762,13 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
         auto locate = [&](Group& g) {
             uint2 e[NQ];
 #pragma unroll
-            for (int q = 0; q < NQ; ++q) e[q] = l1[g.x[q] >> kCiLowBits];
+            for (int q = 0; q < NQ; ++q) e[q] = l1[(DAUC_CI_ABLATE2 & 2) ? (g.x[q] >> 31) : (g.x[q] >> kCiLowBits)];
             unsigned c[NQ];
 #pragma unroll
             for (int q = 0; q < NQ; ++q) c[q] = ci_cell(g.x[q], e[q]);
             uint2 b[NQ];
 #pragma unroll
-            for (int q = 0; q < NQ; ++q) b[q] = blk[c[q] / kCiBlock];
+            for (int q = 0; q < NQ; ++q) b[q] = blk[(DAUC_CI_ABLATE2 & 2) ? (c[q] & 1u) : (c[q] / kCiBlock)];
 #pragma unroll
             for (int q = 0; q < NQ; ++q) {
                 const unsigned sh = 4u * (c[q] % kCiBlock);
@@ -1767,6 +1777,8 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
                 const unsigned rl = b[q].x + __builtin_amdgcn_sad_u8(bytes, 0u, 0u);
                 const unsigned cnt = __builtin_amdgcn_ubfe(b[q].y, sh, 4u);
                 g.rc[q] = rl | (cnt << 28);
+                if (DAUC_CI_ABLATE2 & 2)  // keep ~half the lanes gathering at spread positions
+                    g.rc[q] = ((g.x[q] * 2654435761u) % (M32 + 1u)) | ((((g.x[q] >> 7) & 1u) | (rl >> 31)) << 28);
             }
 #pragma unroll
             for (int q = 0; q < NQ; ++q) {
@@ -1776,9 +1788,22 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
                 // rank_lo are of earlier cells (< x), the others of later cells or padding (> x)
                 g.k[q] = *reinterpret_cast<const uint4*>(sorted + (rl & ~3u));
 #else
-                g.k[q] = *reinterpret_cast<const uint4*>(sorted + ((g.rc[q] >> 28) ? rl & ~3u : 0u));
+                g.k[q] = *reinterpret_cast<const uint4*>(
+                    sorted + (((g.rc[q] >> 28) && !(DAUC_CI_ABLATE2 & 1)) ? rl & ~3u : 0u));
 #endif
             }
+#if DAUC_CI_W2
+            // A cell that runs past its first window ((rank_lo & 3) + count > 4: ~7 % of the queries
+            // at 1.1 cells per key) also loads the next one here, in the same straight-line issue: as
+            // a branch after the count it was waited for with vmcnt(0) -- every load in flight,
+            // the stream's included -- in nearly every iteration of every wave. Lanes that do not
+            // need it load the table's first window (one shared line).
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                const unsigned rl = g.rc[q] & 0x0fffffffu, cnt = g.rc[q] >> 28;
+                g.k2[q] = *reinterpret_cast<const uint4*>(sorted + ((rl & 3u) + cnt > 4u ? (rl & ~3u) + 4u : 0u));
+            }
+#endif
         };
 #if DAUC_CI_COUNT3
         // Branch-free counts, no compare results in scalar registers: with med(k, lo, hi) =
@@ -1823,6 +1848,41 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
                 const uint4 k = (g.rc[q] >> 28) ? g.k[q] : uint4{kPadKey, kPadKey, kPadKey, kPadKey};
                 more |= ci_count(g.x[q], (g.use >> q) & 1u, g.rc[q] & 0x0fffffffu, g.rc[q] >> 28, k, M32, wl, tl);
             }
+#if DAUC_CI_W2
+            // the second window's keys (those of the cell and of later cells; past the cell they
+            // are > x): W -= #(<= x), T += #(<= x) - #(< x); a lane without one adds nothing
+            bool more8 = false;
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                const unsigned x = g.x[q], rl = g.rc[q] & 0x0fffffffu, cnt = g.rc[q] >> 28;
+                const unsigned span = (rl & 3u) + cnt;
+                const unsigned m = 0u - (((g.use >> q) & 1u) & unsigned(span > 4u));
+                const uint4 k2 = g.k2[q];
+                const unsigned lt = (k2.x < x) + (k2.y < x) + (k2.z < x) + (k2.w < x);
+                const unsigned le = (k2.x <= x) + (k2.y <= x) + (k2.z <= x) + (k2.w <= x);
+                wl -= le & m;
+                tl += (le - lt) & m;
+                more8 |= ((g.use >> q) & 1u) && span > 8u;
+            }
+            w += wl;
+            t += tl;
+            if (more8) {  // a cell of 6+ keys across both windows: rare (the nibble caps it at 14)
+#pragma unroll
+                for (int q = 0; q < NQ; ++q) {
+                    const unsigned rl = g.rc[q] & 0x0fffffffu, cnt = g.rc[q] >> 28;
+                    if (((g.use >> q) & 1u) && (rl & 3u) + cnt > 8u) {
+                        // undo the two windows' counts, then count the cell key by key (ci_fix)
+                        const unsigned x = g.x[q];
+                        const uint4 k2 = g.k2[q];
+                        w += (k2.x <= x) + (k2.y <= x) + (k2.z <= x) + (k2.w <= x);
+                        t -= ((k2.x <= x) + (k2.y <= x) + (k2.z <= x) + (k2.w <= x)) -
+                             ((k2.x < x) + (k2.y < x) + (k2.z < x) + (k2.w < x));
+                        ci_fix(x, rl, cnt, g.k[q], sorted, w, t);
+                    }
+                }
+            }
+            (void)more;
+#else
             w += wl;
             t += tl;
             if (more) {
@@ -1832,8 +1892,116 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
                     if (((g.use >> q) & 1u) && (rl & 3u) + cnt > 4u) ci_fix(g.x[q], rl, cnt, g.k[q], sorted, w, t);
                 }
             }
+#endif
         };
 #endif
+#if DAUC_CI_PIPE == 2
+        // Four stages, each group one stage further per iteration, so that no LDS read or window
+        // load is waited for in the iteration that issues it. Per iteration j, in this order:
+        // D(j-1) the count [its windows were issued 3/4 of an iteration earlier], C(j) the block
+        // word decode + the window loads [block words read 3/4 earlier], B(j+1) the cells + the
+        // block-word reads [l1 entries read 3/4 earlier], A(j+2) the keys + the l1 reads [stream
+        // loads issued D groups earlier]. Every stage reads its input slot before the stage
+        // before it refills the slot: one slot per stage. Groups past the lane's last are
+        // bubbles (their loads re-read slot 0, labels positive).
+        struct SA {
+            unsigned x[NQ], use;
+            uint2 e[NQ];
+        };
+        struct SB {
+            unsigned x[NQ], use, c[NQ];
+            uint2 b[NQ];
+        };
+        struct SC {
+            unsigned x[NQ], use, rc[NQ];
+            uint4 k[NQ];
+        };
+        auto stA = [&](SA& a, const Stream& sg) {
+            Group g;
+            keys(g, sg);
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                a.x[q] = g.x[q];
+                a.e[q] = l1[(DAUC_CI_ABLATE2 & 2) ? (a.x[q] >> 31) : (a.x[q] >> kCiLowBits)];
+            }
+            a.use = g.use;
+        };
+        auto stB = [&](SB& b, const SA& a) {
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                b.x[q] = a.x[q];
+                b.c[q] = ci_cell(a.x[q], a.e[q]);
+                b.b[q] = blk[(DAUC_CI_ABLATE2 & 2) ? (b.c[q] & 1u) : (b.c[q] / kCiBlock)];
+            }
+            b.use = a.use;
+        };
+        auto stC = [&](SC& c, const SB& b) {
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                c.x[q] = b.x[q];
+                const unsigned sh = 4u * (b.c[q] % kCiBlock);
+                const unsigned below = __builtin_amdgcn_ubfe(b.b[q].y, 0u, sh);
+                const unsigned bytes = (below & 0x0f0f0f0fu) + ((below >> 4) & 0x0f0f0f0fu);
+                const unsigned rl = b.b[q].x + __builtin_amdgcn_sad_u8(bytes, 0u, 0u);
+                const unsigned cnt = __builtin_amdgcn_ubfe(b.b[q].y, sh, 4u);
+                c.rc[q] = rl | (cnt << 28);
+            }
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                const unsigned rl = c.rc[q] & 0x0fffffffu;
+                c.k[q] = *reinterpret_cast<const uint4*>(sorted + (((c.rc[q] >> 28) && !(DAUC_CI_ABLATE2 & 1)) ? rl & ~3u : 0u));
+            }
+            c.use = b.use;
+        };
+        auto stD = [&](const SC& c) {
+            Group g;
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                g.x[q] = c.x[q];
+                g.rc[q] = c.rc[q];
+                g.k[q] = c.k[q];
+            }
+            g.use = c.use;
+            count(g);
+        };
+        constexpr int D = DAUC_CI_DEPTH;
+        const int64_t ng = nvec > tid ? (nvec - tid + step - 1) / step : 0;  // this lane's groups
+        Stream sbuf[D];
+        SA sa;
+        SB sb;
+        SC sc;
+        auto vof = [&](int64_t g) { return tid + g * step; };
+#pragma unroll
+        for (int g = 0; g < D; ++g) load(sbuf[g], vof(g));
+        // prologue: A(0); B(0) A(1); C(0) B(1) A(2)
+        stA(sa, sbuf[0]);
+        load(sbuf[0], vof(D));
+        asm volatile("" ::: "memory");
+        stB(sb, sa);
+        stA(sa, sbuf[1 % D]);
+        load(sbuf[1 % D], vof(1 + D));
+        asm volatile("" ::: "memory");
+        stC(sc, sb);
+        stB(sb, sa);
+        stA(sa, sbuf[2 % D]);
+        load(sbuf[2 % D], vof(2 + D));
+        asm volatile("" ::: "memory");
+        int64_t j = 1;
+        for (;;) {
+#pragma unroll
+            for (int u = 0; u < D; ++u) {
+                // j = 1 + u (mod D): the stream buffer of group j + 2 is (3 + u) % D
+                if (j > ng) goto ci_stream_done;
+                stD(sc);
+                stC(sc, sb);
+                stB(sb, sa);
+                stA(sa, sbuf[(3 + u) % D]);
+                load(sbuf[(3 + u) % D], vof(j + 2 + D));
+                asm volatile("" ::: "memory");
+                ++j;
+            }
+        }
+#else
         // per group g: keys(g) [its stream loads were issued D groups earlier], stream loads of
         // g + D into the buffer just read, LDS lookups + window loads of g, count of g - 1 [its
         // windows were issued one group earlier; the younger loads stay in flight: vmcnt retires
@@ -1868,6 +2036,7 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
                 v += step;
             }
         }
+#endif
     ci_stream_done:;
     } else {
         for (int64_t v = tid; v < nvec; v += stride)

@@ -525,6 +525,8 @@ __global__ __launch_bounds__(kThreads) void surrogate_rows_reduce_kernel(
 }
 
 // ---- the loss in ONE launch: the stream, its rows reduced by the LAST R workgroups ---------
+// (round 2's product form; since round 3 the tuning build's variants 4 / 5 -- the product takes
+// surrogate_tail_x_kernel below, which shares this section's granules, epochs and polls)
 //
 // Every workgroup streams its chunk and publishes its row as tagged 8-byte granules (Guideline
 // 16, R2: the data is the flag; ONE write-through store per granule, no drain, no ticket):
@@ -729,7 +731,7 @@ __global__ __launch_bounds__(kThreads, DAUC_TAIL_WAVES) void surrogate_tail_kern
     }
 }
 
-// ---- the one-launch loss with R EXTRA reducer workgroups that stream nothing ----------------
+// ---- the one-launch loss with R EXTRA reducer workgroups that stream nothing (the product) ---
 //
 // The stamps of the kernel above put its tail (6.3-6.6 us after the last row store) in the
 // reducers: they are the last 64 STREAMING workgroups, so every group total waits for its
@@ -742,7 +744,7 @@ __global__ __launch_bounds__(kThreads, DAUC_TAIL_WAVES) void surrogate_tail_kern
 // us at 2^26) before the last row: after the last row lands one hop is left. PLAIN: the epoch is
 // read with a plain load (every read of it precedes the final's store; a later call reads it across
 // the kernel boundary). Same granules, epochs, bounded polls and fixed summation order as above.
-template <typename YT, int S, int R, int K, bool PLAIN, bool STAMPS, int WAVES = DAUC_TAIL_WAVES>
+template <typename YT, int S, int R, int K, bool PLAIN, bool STAMPS, int WAVES = DAUC_TAIL_WAVES, bool REDUCE = true>
 __global__ __launch_bounds__(kThreads, WAVES) void surrogate_tail_x_kernel(
     const float* __restrict__ h, const YT* __restrict__ y, int64_t B, int64_t nblocks, double invB,
     const float* __restrict__ abalpha, const float* __restrict__ p_hat, float* __restrict__ dh, TailWs ws,
@@ -760,6 +762,7 @@ __global__ __launch_bounds__(kThreads, WAVES) void surrogate_tail_x_kernel(
         if (STAMPS && threadIdx.x == 0) ws.stamps[b] = realtime();
         return;
     }
+    if (!REDUCE) return;  // a timing variant: the stream with its row stores, nobody reducing
     const int64_t r = b - nblocks;
     const bool final_red = r == R - 1;
     // the final's direct rows: [k0, nblocks); groups split [0, k0) into R - 1 contiguous ranges
@@ -972,6 +975,11 @@ constexpr int kChunkSlots = 4;
 #define DAUC_SURROGATE_TAIL_REDUCERS 64
 #endif
 constexpr int kTailReducers = DAUC_SURROGATE_TAIL_REDUCERS;
+// the product's extra-reducer tail (surrogate_tail_x_kernel): 128 reducer workgroups, the final one
+// taking the grid's last 512 rows itself; at B = 2^26 (tuning variants 10-21, profiles/r03/a):
+// 92.3 us vs 94.4 for the 64 streaming reducers above, 88.2 for the stream with its row stores alone
+constexpr int kTailXReducers = 128;
+constexpr int kTailFinalRows = 512;
 // Unit-stride batches at least this large take the chunked kernels; smaller ones are
 // latency-bound and stay on the single-ticket persistent kernel.
 constexpr int64_t kChunkMinB = int64_t(1) << 22;
@@ -1007,14 +1015,14 @@ int launch_tail(const float* h, const YT* y, int64_t B, const float* abalpha, co
     return launch_status();
 }
 
-template <typename YT, int R, int K, bool PLAIN, bool STAMPS = false, int WAVES = DAUC_TAIL_WAVES>
+template <typename YT, int R, int K, bool PLAIN, bool STAMPS = false, int WAVES = DAUC_TAIL_WAVES, bool REDUCE = true>
 int launch_tail_x(const float* h, const YT* y, int64_t B, const float* abalpha, const float* p_hat, float* dh,
                   double* out64, float* grad3, float* loss, void* ws, size_t ws_bytes, hipStream_t st) {
     const int64_t nblocks = chunk_blocks(B);
     if (nblocks + R > 0x7fffffffLL) return DAUC_EINVAL;
     if (ws == nullptr || ws_bytes < tail_offset(nblocks) + tail_ws_bytes(nblocks, R, STAMPS)) return DAUC_EINVAL;
     const TailWs w = tail_ws(static_cast<char*>(ws) + tail_offset(nblocks), nblocks, R, STAMPS);
-    hipLaunchKernelGGL((surrogate_tail_x_kernel<YT, kChunkSlots, R, K, PLAIN, STAMPS, WAVES>),
+    hipLaunchKernelGGL((surrogate_tail_x_kernel<YT, kChunkSlots, R, K, PLAIN, STAMPS, WAVES, REDUCE>),
                        dim3(static_cast<unsigned>(nblocks + R)), dim3(kThreads), 0, st, h, y, B, nblocks,
                        1.0 / static_cast<double>(B), abalpha, p_hat, dh, w, out64, grad3, loss);
     return launch_status();
@@ -1120,6 +1128,7 @@ int launch_surrogate(const float* h, int64_t hs, const YT* y, int64_t B, const f
                 case 19: return launch_tail_x<YT, 256, 1024, true, false, 8>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, ws, ws_bytes, st);
                 case 20: return launch_tail_x<YT, 128, 512, true, false, 8>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, ws, ws_bytes, st);
                 case 21: return launch_tail_x<YT, 128, 512, true, true>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, ws, ws_bytes, st);
+                case 22: return launch_tail_x<YT, kTailXReducers, kTailFinalRows, true, false, 8, false>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, ws, ws_bytes, st);
                 default: return DAUC_EINVAL;
             }
         }
@@ -1129,10 +1138,12 @@ int launch_surrogate(const float* h, int64_t hs, const YT* y, int64_t B, const f
     (void)variant;
 #endif
     if (unit && variant == 0 && B >= kChunkMinB) {
-        // the loss: the stream with its row reduce done by its last kTailReducers workgroups (one
-        // launch); the class sums keep the two-launch form
+        // the loss: the stream with its row reduce done by kTailXReducers extra workgroups that
+        // stream nothing (one launch); the class sums keep the two-launch form
         if constexpr (!CLASS_ONLY)
-            return launch_tail<YT, kTailReducers>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, ws, ws_bytes, st);
+            // int8 labels: the register bound of 8 waves per SIMD costs no spill (wider labels would spill)
+            return launch_tail_x<YT, kTailXReducers, kTailFinalRows, true, false, sizeof(YT) == 1 ? 8 : DAUC_TAIL_WAVES>(
+                h, y, B, abalpha, p_hat, dh, out64, grad3, loss, ws, ws_bytes, st);
         else
             return launch_chunk<YT, true>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, sums4, accumulate, ws,
                                           ws_bytes, st);
@@ -1315,7 +1326,7 @@ int dauc_surrogate_fwdbwd_variant(const float* h, int64_t h_stride, const void* 
                                   double* out64, float* grad3, float* loss, void* workspace,
                                   size_t workspace_bytes, int variant, dauc_stream_t stream) {
     if (B <= 0 || h == nullptr || y == nullptr || abalpha == nullptr || p_hat == nullptr ||
-        h_stride <= 0 || (dh != nullptr && dh_stride <= 0) || variant < 0 || variant > 21)
+        h_stride <= 0 || (dh != nullptr && dh_stride <= 0) || variant < 0 || variant > 22)
         return DAUC_EINVAL;
     return dispatch_labels<false>(h, h_stride, y, y_dtype, B, abalpha, p_hat, dh, dh_stride, out64,
                                   grad3, loss, nullptr, 0, workspace, workspace_bytes,

@@ -167,12 +167,21 @@ class Evaluator:
         from .conv1x1 import fixed_engine
 
         coda.model.eval()
-        # no per-rank timed engine choice: every rank's scores are the bits rank 0 would compute
-        with torch.no_grad(), fixed_engine("gemm"):
-            k = 0
-            for x, lab in self.batches[lo:hi]:
-                out[k:k + lab.numel()] = coda.scores(x)
-                k += lab.numel()
+        # no per-rank timed engine choice and no run-to-run variation: every rank's scores are the
+        # bits rank 0 would compute. MIOpen's default forward solver for some 3x3 stride-2 shapes
+        # (ResNet-18 layer2.0.conv2 at 32x32, batch 48) changes low bits from call to call;
+        # deterministic mode picks repeatable solvers (scripts/probe_eval_determinism.py,
+        # profiles/r03/determinism/)
+        det, bench = torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark
+        torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = True, False
+        try:
+            with torch.no_grad(), fixed_engine("gemm"):
+                k = 0
+                for x, lab in self.batches[lo:hi]:
+                    out[k:k + lab.numel()] = coda.scores(x)
+                    k += lab.numel()
+        finally:
+            torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = det, bench
         coda.model.train()
 
     def _scores_split(self, coda: CoDA) -> torch.Tensor:

@@ -29,7 +29,15 @@ extern "C" {
  * rows is the workgroup dispatched 4096 after the group's last row; only the groups too close to
  * the end are reduced by the last workgroups), 7 = 6 with the stamps, 8 / 9 = 6 with a lag of 2048
  * / 8192 workgroups (measured 5 / 3.5 us slower than 0 at B = 2^26: profiles/r03/surrogate_ab.jsonl).
- * Variants 2..9 need unit strides, 16-byte aligned h/dh and int8 labels.
+ * 4..9 are round 2's one-launch kernel (64 STREAMING reducers at the grid's end). 10..22 the
+ * extra-reducer kernel (the product since round 3: R reducer workgroups after the streaming ones,
+ * streaming nothing; the final reducer takes the last K rows itself): 10 R = 64, K = 512 with an
+ * atomic epoch load, 11 the same with a plain epoch load, 12 K = 256, 13 K = 1024, 14 = 11 with
+ * stamps, 15 R = 32, 16 R = 128, 17 R = 128 K = 1024, 18 R = 128 K = 1536, 19 R = 256 K = 1024
+ * (17-19 with an 8-waves-per-SIMD register bound), 20 R = 128 K = 512 with that bound (= the
+ * product for int8 labels), 21 = 16 with stamps, 22 = 20 with its reducers returning at once (the
+ * stream and its row stores alone). profiles/r03/a: 10 94.7, 11 93.1, 16 92.4, 20 92.3 us vs 4 88.2.
+ * Variants 2..22 need unit strides, 16-byte aligned h/dh and int8 labels.
  * Every variant returns bitwise-identical dh and counts; the fp64 sums agree to rounding.
  */
 int dauc_surrogate_fwdbwd_variant(const float* h, int64_t h_stride, const void* y, int y_dtype, int64_t B,

@@ -18,6 +18,13 @@ from distributedauc_amd.backbone import build_backbone  # noqa: E402
 from distributedauc_amd.conv1x1 import fixed_engine  # noqa: E402
 
 bs = int(sys.argv[1]) if len(sys.argv) > 1 else 48
+mode = sys.argv[2] if len(sys.argv) > 2 else "default"
+if mode == "det":
+    torch.backends.cudnn.deterministic = True
+    torch.backends.cudnn.benchmark = False
+elif mode == "algos":
+    torch.use_deterministic_algorithms(True, warn_only=True)
+print(json.dumps({"mode": mode}), flush=True)
 use_tuned_miopen_db()
 dev = torch.device("cuda", 0)
 torch.manual_seed(0)

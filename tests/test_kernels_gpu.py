@@ -175,7 +175,7 @@ def test_surrogate_chunked_variants(dev, B):
 
 
 def test_surrogate_tail_ignores_stale_granules(dev):
-    """The one-launch loss hands rows over as epoch-tagged granules (surrogate.hip, tail kernel):
+    """The one-launch loss hands rows over as epoch-tagged granules (surrogate.hip, tail_x kernel):
     a granule written by a workgroup of an EARLIER call -- e.g. one that stored its row after that
     call's reducer gave up waiting -- carries an older tag and is never taken for a current one.
     Here every row and group-total granule of the workspace is overwritten between calls with the
@@ -202,7 +202,7 @@ def test_surrogate_tail_ignores_stale_granules(dev):
     nb = -(-B // 4096)
     chunk = nb * 48 + 256 + -(-nb // 512) * 48
     off = 256 + 2048 * 48 + -(-chunk // 256) * 256
-    words = ws[off: off + 256 + (nb + 64) * 80].view(torch.int64)
+    words = ws[off: off + 256 + (nb + 128) * 80].view(torch.int64)  # rows + the 128 reducers' totals
     epoch = int(words[0].item()) & 0xFFFFFFFF
     gran = words[32:]  # the 256-B header, then the granules
     rng = torch.Generator(device=dev).manual_seed(5)
