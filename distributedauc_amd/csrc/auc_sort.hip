@@ -1611,6 +1611,12 @@ __device__ __forceinline__ void ci_fix(unsigned x, unsigned rl, unsigned cnt, co
 #define DAUC_CI_ABLATE2 0  // timing ablations only (wrong counts): 1 every window at the table's start,
                            // 2 the LDS lookups at lane-uniform addresses (same dependency chain), 3 both
 #endif
+#ifndef DAUC_CI_LATEWIN
+#define DAUC_CI_LATEWIN 0  // 1: count the previous group before issuing this group's window loads
+#endif
+#ifndef DAUC_CI_MED3
+#define DAUC_CI_MED3 0  // 1 (with W2): the window counts by v_med3_u32, branch-free
+#endif
 #ifndef DAUC_CI_W2
 #define DAUC_CI_W2 1  // 1: the second window of a cell past its first loaded with the first (no branch)
 #endif
@@ -1759,7 +1765,7 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
         // phase by phase over the group, so that every query's LDS read of a phase is issued before
         // the first wait (a per-query chain with its conditional window load in between keeps the
         // compiler from interleaving the queries: one LDS round trip per read per query)
-        auto locate = [&](Group& g) {
+        auto locate_lds = [&](Group& g) {
             uint2 e[NQ];
 #pragma unroll
             for (int q = 0; q < NQ; ++q) e[q] = l1[(DAUC_CI_ABLATE2 & 2) ? (g.x[q] >> 31) : (g.x[q] >> kCiLowBits)];
@@ -1780,6 +1786,8 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
                 if (DAUC_CI_ABLATE2 & 2)  // keep ~half the lanes gathering at spread positions
                     g.rc[q] = ((g.x[q] * 2654435761u) % (M32 + 1u)) | ((((g.x[q] >> 7) & 1u) | (rl >> 31)) << 28);
             }
+        };
+        auto locate_win = [&](Group& g) {
 #pragma unroll
             for (int q = 0; q < NQ; ++q) {
                 const unsigned rl = g.rc[q] & 0x0fffffffu;
@@ -1801,9 +1809,14 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
 #pragma unroll
             for (int q = 0; q < NQ; ++q) {
                 const unsigned rl = g.rc[q] & 0x0fffffffu, cnt = g.rc[q] >> 28;
-                g.k2[q] = *reinterpret_cast<const uint4*>(sorted + ((rl & 3u) + cnt > 4u ? (rl & ~3u) + 4u : 0u));
+                g.k2[q] = *reinterpret_cast<const uint4*>(
+                    sorted + ((rl & 3u) + cnt > 4u && !(DAUC_CI_ABLATE2 & 1) ? (rl & ~3u) + 4u : 0u));
             }
 #endif
+        };
+        auto locate = [&](Group& g) {
+            locate_lds(g);
+            locate_win(g);
         };
 #if DAUC_CI_COUNT3
         // Branch-free counts, no compare results in scalar registers: with med(k, lo, hi) =
@@ -1835,6 +1848,59 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
                 for (int q = 0; q < NQ; ++q) {
                     const unsigned rl = g.rc[q] & 0x0fffffffu, cnt = g.rc[q] >> 28;
                     if (((g.use >> q) & 1u) && (rl & 3u) + cnt > 4u) ci_fix(g.x[q], rl, cnt, g.k[q], sorted, w, t);
+                }
+            }
+        };
+#elif DAUC_CI_MED3 && DAUC_CI_W2
+        // The counts of both windows by v_med3_u32 (no compare into a scalar register, no hazard
+        // wait, no branch): med3(k, x, x+1) - x = [k > x], med3(k, x-1, x) - (x-1) = [k >= x]
+        // (x +- 1 wraps only for a NaN query's key, and a NaN makes the evaluation an error).
+        // Masks as 0 / ~0 words: m0 the cell holds keys (else window 1 is the table's first, read
+        // as padding: base = rank_lo, no keys counted), m2 the cell runs into window 2, mu a
+        // negative-label query.
+        auto count = [&](const Group& g) {
+            auto med3 = [](unsigned v, unsigned lo, unsigned hi) {
+                unsigned r;
+                asm("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(v), "v"(lo), "v"(hi));
+                return r;
+            };
+            unsigned wl = 0u, tl = 0u;
+            bool more8 = false;
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                const unsigned x = g.x[q], xp = x + 1u, xm = x - 1u, x4 = x << 2;
+                const unsigned rl = g.rc[q] & 0x0fffffffu, cnt = g.rc[q] >> 28, span = (rl & 3u) + cnt;
+                const uint4 k = g.k[q], k2 = g.k2[q];
+                // #(> x) and #(>= x) of each window
+                const unsigned gt1 = med3(k.x, x, xp) + med3(k.y, x, xp) + med3(k.z, x, xp) + med3(k.w, x, xp) - x4;
+                const unsigned ge1 = med3(k.x, xm, x) + med3(k.y, xm, x) + med3(k.z, xm, x) + med3(k.w, xm, x) - x4 + 4u;
+                const unsigned gt2 = med3(k2.x, x, xp) + med3(k2.y, x, xp) + med3(k2.z, x, xp) + med3(k2.w, x, xp) - x4;
+                const unsigned ge2 = med3(k2.x, xm, x) + med3(k2.y, xm, x) + med3(k2.z, xm, x) + med3(k2.w, xm, x) - x4 + 4u;
+                const unsigned m0 = 0u - min(cnt, 1u);
+                const unsigned m2 = 0u - min((span + 3u) >> 3, 1u);
+                const unsigned mu = 0u - ((g.use >> q) & 1u);
+                // #(<= x) = 4 - gt, #(< x) = 4 - ge; W = M - base - #(<= x), T = #(<= x) - #(< x) = ge - gt
+                const unsigned base = rl - ((rl & 3u) & m0);
+                const unsigned le = ((4u - gt1) & m0) + ((4u - gt2) & m2);
+                const unsigned tie = ((ge1 - gt1) & m0) + ((ge2 - gt2) & m2);
+                wl += (M32 - base - le) & mu;
+                tl += tie & mu;
+                more8 |= ((g.use >> q) & 1u) && span > 8u;
+            }
+            w += wl;
+            t += tl;
+            if (more8) {  // a cell of 6+ keys across both windows: rare (the nibble caps it at 14)
+#pragma unroll
+                for (int q = 0; q < NQ; ++q) {
+                    const unsigned rl = g.rc[q] & 0x0fffffffu, cnt = g.rc[q] >> 28;
+                    if (((g.use >> q) & 1u) && (rl & 3u) + cnt > 8u) {
+                        const unsigned x = g.x[q];
+                        const uint4 k2 = g.k2[q];
+                        w += (k2.x <= x) + (k2.y <= x) + (k2.z <= x) + (k2.w <= x);
+                        t -= ((k2.x <= x) + (k2.y <= x) + (k2.z <= x) + (k2.w <= x)) -
+                             ((k2.x < x) + (k2.y < x) + (k2.z < x) + (k2.w < x));
+                        ci_fix(x, rl, cnt, g.k[q], sorted, w, t);
+                    }
                 }
             }
         };
@@ -2031,8 +2097,17 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
                 keys(gc, sbuf[(j + 1) % D]);
                 load(sbuf[(j + 1) % D], v + int64_t(D) * step);
                 asm volatile("" ::: "memory");  // the stream loads stay older than this group's windows
+#if DAUC_CI_LATEWIN
+                // the previous group is counted before this group's windows are issued: one group's
+                // windows in registers at a time (they were issued 3/4 of an iteration earlier)
+                locate_lds(gc);
+                count(gp);
+                asm volatile("" ::: "memory");
+                locate_win(gc);
+#else
                 locate(gc);
                 count(gp);
+#endif
                 v += step;
             }
         }

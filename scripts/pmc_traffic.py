@@ -40,7 +40,8 @@ def kernel_key(name: str) -> str | None:
         return "pd_update"
     if "surrogate_rows_reduce_kernel" in name:
         return "surrogate_reduce"
-    if "surrogate_chunk_kernel" in name or "surrogate_kernel" in name or "surrogate_tail_kernel" in name:
+    if ("surrogate_chunk_kernel" in name or "surrogate_kernel" in name or "surrogate_tail_kernel" in name
+            or "surrogate_tail_x_kernel" in name):
         return "surrogate"
     if "compact_count_kernel" in name:
         return "compact_count_2^27"
