@@ -134,15 +134,19 @@ class Evaluator:
     broadcast into every rank's model for the evaluation (ranks hold different parameters between
     averaging rounds, and BN buffers are never averaged, main.py:35) and each rank's own state is
     restored afterwards. The shares are all-gathered, so every rank holds rank 0's scores in the
-    test-set order, and the exact count is sharded (ExactAUC). Same scores, same AUC as rank-0
-    scoring (tests/test_main_gpu.py); ``split=False`` is the reference's rank-0 scoring."""
+    test-set order, and the exact count is sharded (ExactAUC). With ``deterministic=True``
+    (``--deterministic_eval 1``) the scores and the AUC are bit-identical to rank-0 scoring
+    (tests/test_main_gpu.py); without it they differ from it only as much as two rank-0 scorings
+    do (MIOpen's default solvers vary in low bits from call to call). ``split=False`` is the
+    reference's rank-0 scoring."""
 
     def __init__(self, test_batches, n_test: int, split_index: int, device, group, world: int, rank: int,
-                 history_path: str | None = None, split: bool = True):
+                 history_path: str | None = None, split: bool = True, deterministic: bool = False):
         self.batches = test_batches
         self.n = n_test
         self.split = split_index
         self.split_scoring = bool(split) and world > 1
+        self.deterministic = bool(deterministic)
         self.device = device
         self.world, self.rank = world, rank
         self.auc = ExactAUC(group, world, rank)
@@ -167,13 +171,15 @@ class Evaluator:
         from .conv1x1 import fixed_engine
 
         coda.model.eval()
-        # no per-rank timed engine choice and no run-to-run variation: every rank's scores are the
-        # bits rank 0 would compute. MIOpen's default forward solver for some 3x3 stride-2 shapes
-        # (ResNet-18 layer2.0.conv2 at 32x32, batch 48) changes low bits from call to call;
-        # deterministic mode picks repeatable solvers (scripts/probe_eval_determinism.py,
-        # profiles/r03/determinism/)
+        # no per-rank timed 1x1 engine choice. MIOpen's default forward solvers are not repeatable
+        # bit for bit (ResNet-18 layer2.0.conv2 at 32x32, batch 48, changes low bits from call to
+        # call: scripts/probe_eval_determinism.py, profiles/r03/determinism/), so rank 0 scoring the
+        # same test set twice differs in low bits as much as split scoring does; `deterministic`
+        # selects repeatable solvers, making split and rank-0 scoring bit-identical (the GPU test),
+        # at a large cost for 224^2 bf16 (ResNet-50, 8192 images: 61 s vs 0.48 s)
         det, bench = torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark
-        torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = True, False
+        if self.deterministic:
+            torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = True, False
         try:
             with torch.no_grad(), fixed_engine("gemm"):
                 k = 0
@@ -282,7 +288,8 @@ def train(rank: int, size: int, group=None, para=None):
         test_batches = [next(it) for _ in range((n_test + para.test_batchsize - 1) // para.test_batchsize)]
         hist = os.path.join(para.history_dir, "history" + label + ".csv") if para.history_dir else None
         evaluate = Evaluator(test_batches, n_test, para.split_index, device, group, size, rank, hist,
-                             split=getattr(para, "split_eval", 1) != 0)
+                             split=getattr(para, "split_eval", 1) != 0,
+                             deterministic=getattr(para, "deterministic_eval", 0) != 0)
     coda.run(iter(train_loader), num_stages=para.numStages, total_iter=para.total_iter,
              test_freq=para.test_freq, evaluate=evaluate)
     return coda

@@ -57,6 +57,10 @@ def get_parser() -> argparse.ArgumentParser:
     p.add_argument("--split_eval", type=int, default=1,
                    help="1: every rank scores a share of the test set with rank 0's model (same AUC); "
                         "0: rank 0 scores it all (main.py:232)")
+    p.add_argument("--deterministic_eval", type=int, default=0,
+                   help="1: score the test set with repeatable convolution solvers (cudnn.deterministic), so "
+                        "split and rank-0 scoring give the same bits; MIOpen's deterministic choices for "
+                        "ResNet-50 224^2 bf16 are ~100x slower than its default ones")
     p.add_argument("--seed", type=int, default=1234)
     p.add_argument("--history_dir", type=str, default="history")
     p.add_argument("--backend", type=str, default=None, help="torch.distributed backend (default nccl=RCCL)")

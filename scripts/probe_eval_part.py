@@ -48,3 +48,14 @@ for log2n, pr in ((24, 0.01), (27, 0.001)):
         tl = wall(lambda: ops.auc_eval_counts_part(s, y, G - 1, G, pc))
         print(json.dumps({"log2n": log2n, "G": G, "fn": "dauc_auc_eval_counts_part", "ms_part0": t0,
                           "ms_last": tl, "sum_matches_whole": (W, T) == (whole[0], whole[1])}), flush=True)
+        # the sharded path's own call: the part enqueued with no host sync, then the one read of its
+        # 64-byte record (ExactAUC reads the all-gathered records instead)
+        rec = torch.zeros(8, dtype=torch.int64, device=dev)
+        W = T = 0
+        for r in range(G):
+            v = ops.auc_eval_enqueue(s, y, r, G, out=rec).tolist()
+            W, T = W + v[0], T + v[1]
+        e0 = wall(lambda: ops.auc_eval_enqueue(s, y, 0, G, out=rec).tolist())
+        el = wall(lambda: ops.auc_eval_enqueue(s, y, G - 1, G, out=rec).tolist())
+        print(json.dumps({"log2n": log2n, "G": G, "fn": "dauc_auc_eval_enqueue + record read", "ms_part0": e0,
+                          "ms_last": el, "sum_matches_whole": (W, T) == (whole[0], whole[1])}), flush=True)

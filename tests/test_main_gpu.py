@@ -93,7 +93,8 @@ def _split_eval_worker(rank, world, port, errq):
         para = parse(["--arch", "resnet18", "--image_size", "32", "--dataset_size", "6000", "--num_classes", "10",
                       "--split_index", "6", "--pos_ratio", "0.3", "--T0", "4", "--numStages", "3", "--I", "3",
                       "--local_batchsize", "16", "--test_batchsize", "48", "--test_freq", "5", "--total_iter", "100",
-                      "--test_ratio", "0.1", "--history_dir", "", "--neg_keep_ratio", "0.5"])
+                      "--test_ratio", "0.1", "--history_dir", "", "--neg_keep_ratio", "0.5",
+                      "--deterministic_eval", "1"])
         coda = M.train(rank, world, None, para)
         assert checked["n"] >= 2, checked
         dist.barrier()
