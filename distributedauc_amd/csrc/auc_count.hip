@@ -277,6 +277,9 @@ int launch_split(const float* s, const LT* lab, int64_t n, float* pos_out, float
 // tile0 + (k * 256 + t) * 16 + [0, 16) (each wave load instruction reads 1 KB contiguous at int8).
 
 constexpr int kCmpThreads = 256;
+#ifndef DAUC_COMPACT_WIDE_THREADS
+#define DAUC_COMPACT_WIDE_THREADS 256
+#endif
 constexpr int kCmpSlots = 8;
 constexpr int kCmpTile = kCmpThreads * 16 * kCmpSlots;  // 32768 labels per block
 
@@ -490,20 +493,20 @@ __global__ __launch_bounds__(kCmpThreads) void compact_write_kernel(
 // SLOTS groups of 16 labels per thread: 8 (a 32768-label tile) for small inputs; 32 (131072) for
 // large ones, where the reservation atomics of 4096 tiles on one address serialise (2^27 labels:
 // 65 us at 8 slots).
-template <typename LT, int SLOTS>
-__global__ __launch_bounds__(kCmpThreads) void compact_unordered_kernel(
+template <typename LT, int SLOTS, int THREADS = kCmpThreads>
+__global__ __launch_bounds__(THREADS) void compact_unordered_kernel(
     const float* __restrict__ s, const LT* __restrict__ lab, int64_t n, int vec, float* __restrict__ pos_out,
     unsigned long long* __restrict__ stats, unsigned long long tag, unsigned long long* __restrict__ zero_next,
     unsigned long long next_tag, unsigned long long* __restrict__ zero3, unsigned* __restrict__ zero_w,
     int nzero_w) {
-    constexpr int kW = kCmpThreads / kWave;
-    constexpr int64_t kTileU = int64_t(kCmpThreads) * 16 * SLOTS;
+    constexpr int kW = THREADS / kWave;
+    constexpr int64_t kTileU = int64_t(THREADS) * 16 * SLOTS;
     __shared__ int wtot[2][kW];
     __shared__ unsigned long long base_s;
     if (blockIdx.x == 0) {
         if (threadIdx.x < 4) zero_next[threadIdx.x] = threadIdx.x == 1 ? next_tag : 0ull;
         else if (threadIdx.x < 7 && zero3 != nullptr) zero3[threadIdx.x - 4] = 0ull;
-        for (int i = threadIdx.x; i < nzero_w; i += kCmpThreads) zero_w[i] = 0u;
+        for (int i = threadIdx.x; i < nzero_w; i += THREADS) zero_w[i] = 0u;
     }
     // the slot's tag (written with the zeroes by the previous call): a workspace whose slot was
     // not left by this thread's previous call holds stale counters, so no tile reserves from it
@@ -514,7 +517,7 @@ __global__ __launch_bounds__(kCmpThreads) void compact_unordered_kernel(
     unsigned m[SLOTS];
 #pragma unroll
     for (int k = 0; k < SLOTS; ++k)
-        m[k] = label_masks16(lab, base + (int64_t(k) * kCmpThreads + threadIdx.x) * 16, n, vec, no);
+        m[k] = label_masks16(lab, base + (int64_t(k) * THREADS + threadIdx.x) * 16, n, vec, no);
     int np = 0;
 #pragma unroll
     for (int k = 0; k < SLOTS; ++k) np += __popc(m[k]);
@@ -549,7 +552,7 @@ __global__ __launch_bounds__(kCmpThreads) void compact_unordered_kernel(
     int nf = 0;
 #pragma unroll
     for (int k = 0; k < SLOTS; ++k) {
-        const int64_t i = base + (int64_t(k) * kCmpThreads + threadIdx.x) * 16;
+        const int64_t i = base + (int64_t(k) * THREADS + threadIdx.x) * 16;
         for (unsigned b = m[k]; b != 0u; b &= b - 1u) {
             const float v = s[i + __ffs(b) - 1];
             nf += !isfinite(v);
@@ -831,16 +834,20 @@ int compact_unordered(const float* scores, const void* labels, int label_dtype, 
         zero_next == nullptr)
         return DAUC_EINVAL;
     const bool wide = n >= (int64_t(1) << 25);
-    const int64_t tile = int64_t(kCmpThreads) * 16 * (wide ? 32 : kCmpSlots);
+    // wide inputs: 1024-thread workgroups of 32 label groups per thread (524,288-label tiles: 256
+    // reservations at 2^27 instead of 1024 on the one counter address) -- DAUC_COMPACT_WIDE_THREADS
+    constexpr int kWideThreads = DAUC_COMPACT_WIDE_THREADS;
+    const int threads = wide ? kWideThreads : kCmpThreads;
+    const int64_t tile = int64_t(threads) * 16 * (wide ? 32 : kCmpSlots);
     const int64_t nblk = (n + tile - 1) / tile;
     if (nblk > 0x7fffffffLL) return DAUC_EINVAL;
     const int vec = (reinterpret_cast<uintptr_t>(labels) & 15u) == 0;
-    const dim3 grid(static_cast<unsigned>(nblk)), block(kCmpThreads);
+    const dim3 grid(static_cast<unsigned>(nblk)), block(threads);
     auto go = [&](auto* lab) {
         using LT = std::remove_const_t<std::remove_pointer_t<decltype(lab)>>;
         if (wide)
-            hipLaunchKernelGGL((compact_unordered_kernel<LT, 32>), grid, block, 0, st, scores, lab, n, vec, pos_out,
-                               stats, tag, zero_next, next_tag, zero3, zero_w, nzero_w);
+            hipLaunchKernelGGL((compact_unordered_kernel<LT, 32, kWideThreads>), grid, block, 0, st, scores, lab, n, vec,
+                               pos_out, stats, tag, zero_next, next_tag, zero3, zero_w, nzero_w);
         else
             hipLaunchKernelGGL((compact_unordered_kernel<LT, kCmpSlots>), grid, block, 0, st, scores, lab, n, vec,
                                pos_out, stats, tag, zero_next, next_tag, zero3, zero_w, nzero_w);
