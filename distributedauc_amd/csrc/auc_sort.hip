@@ -1527,6 +1527,19 @@ __global__ __launch_bounds__(256) void ci_blocks_kernel(const unsigned* __restri
     if (__ballot(skew) != 0ull && (threadIdx.x & (kWave - 1)) == 0) atomicOr(meta + kCiSkew, 1u);
 }
 
+// a 16-byte window of the L2-resident table (DAUC_CI_WIN_NT: with the non-temporal hint)
+#ifndef DAUC_CI_WIN_NT
+#define DAUC_CI_WIN_NT 0
+#endif
+__device__ __forceinline__ uint4 win_load(const unsigned* p) {
+    if (DAUC_CI_WIN_NT) {
+        typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+        const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+        return uint4{v.x, v.y, v.z, v.w};
+    }
+    return *reinterpret_cast<const uint4*>(p);
+}
+
 // the order-preserving key (-0 -> +0 by adding +0)
 __device__ __forceinline__ unsigned key_fast(float f) {
     const unsigned u = __float_as_uint(f + 0.0f);
@@ -1796,8 +1809,7 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
                 // rank_lo are of earlier cells (< x), the others of later cells or padding (> x)
                 g.k[q] = *reinterpret_cast<const uint4*>(sorted + (rl & ~3u));
 #else
-                g.k[q] = *reinterpret_cast<const uint4*>(
-                    sorted + (((g.rc[q] >> 28) && !(DAUC_CI_ABLATE2 & 1)) ? rl & ~3u : 0u));
+                g.k[q] = win_load(sorted + (((g.rc[q] >> 28) && !(DAUC_CI_ABLATE2 & 1)) ? rl & ~3u : 0u));
 #endif
             }
 #if DAUC_CI_W2
@@ -1809,8 +1821,7 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
 #pragma unroll
             for (int q = 0; q < NQ; ++q) {
                 const unsigned rl = g.rc[q] & 0x0fffffffu, cnt = g.rc[q] >> 28;
-                g.k2[q] = *reinterpret_cast<const uint4*>(
-                    sorted + ((rl & 3u) + cnt > 4u && !(DAUC_CI_ABLATE2 & 1) ? (rl & ~3u) + 4u : 0u));
+                g.k2[q] = win_load(sorted + ((rl & 3u) + cnt > 4u && !(DAUC_CI_ABLATE2 & 1) ? (rl & ~3u) + 4u : 0u));
             }
 #endif
         };
@@ -1908,6 +1919,18 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
         auto count = [&](const Group& g) {
             unsigned wl = 0u, tl = 0u;
             bool more = false;
+            if (DAUC_CI_ABLATE2 & 4) {  // timing ablation: the windows consumed, nothing counted
+#pragma unroll
+                for (int q = 0; q < NQ; ++q) {
+                    wl += g.k[q].x ^ g.k[q].w;
+#if DAUC_CI_W2
+                    tl += g.k2[q].y ^ g.k2[q].z;
+#endif
+                }
+                w += wl;
+                t += tl;
+                return;
+            }
 #pragma unroll
             for (int q = 0; q < NQ; ++q) {
                 // an empty cell's lane loaded the table's first window: counted as +inf padding

@@ -646,7 +646,9 @@ __global__ __launch_bounds__(kThreads, DAUC_TAIL_WAVES) void surrogate_tail_kern
     double* __restrict__ out64, float* __restrict__ grad3, float* __restrict__ loss) {
     const unsigned epoch = __builtin_amdgcn_readfirstlane(
         __hip_atomic_load((gu32*)ws.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    const unsigned tag = epoch | 0x80000000u;
+    // a variant that reduces nothing never advances the epoch: its rows carry a tag no call
+    // expects (bit 30 set), so a later call cannot take them for its own
+    const unsigned tag = (epoch | 0x80000000u) ^ (REDUCE ? 0u : 0x40000000u);
     // uniform scalar inputs (scalar registers); the final reducer rebuilds its fp64 scalars from
     // them at the end instead of keeping them live through the stream and the reduce
     const float sa = abalpha[0], sb = abalpha[1], sal = abalpha[2], sp = p_hat[0];
@@ -752,7 +754,9 @@ __global__ __launch_bounds__(kThreads, WAVES) void surrogate_tail_x_kernel(
     static_assert(K % kThreads == 0 && R <= kThreads, "final reducer: K / 256 rows and one group total per thread");
     const unsigned epoch = __builtin_amdgcn_readfirstlane(
         PLAIN ? *ws.epoch : __hip_atomic_load((gu32*)ws.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    const unsigned tag = epoch | 0x80000000u;
+    // a variant that reduces nothing never advances the epoch: its rows carry a tag no call
+    // expects (bit 30 set), so a later call cannot take them for its own
+    const unsigned tag = (epoch | 0x80000000u) ^ (REDUCE ? 0u : 0x40000000u);
     const float sa = abalpha[0], sb = abalpha[1], sal = abalpha[2], sp = p_hat[0];
     const int64_t b = blockIdx.x;
     if (b < nblocks) {

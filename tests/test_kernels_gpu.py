@@ -127,10 +127,12 @@ def test_surrogate_large_deterministic(dev):
 
 @pytest.mark.parametrize("B", [(1 << 20), (1 << 22), (1 << 22) + 37, 3 * (1 << 22) + 4099, (1 << 24) + 5])
 def test_surrogate_chunked_variants(dev, B):
-    """The one-launch tail kernel (the default for unit-stride B >= 2^22) and the tuning build's
-    alternatives (include/dauc_tuning.h: 1 persistent, 2 two-launch, 3 stream alone, 4 tail stream
-    without its reduce, 5 stamped tail, 6..9 early group reducers): fp64 closed form within 1e-6 of
-    term scale, dh and counts
+    """The one-launch tail kernel (the default for unit-stride B >= 2^22: since round 3 the
+    extra-reducer kernel) and the tuning build's alternatives (include/dauc_tuning.h: 1 persistent,
+    2 two-launch, 3 stream alone, 4 round 2's tail stream without its reduce, 5 round 2's tail with
+    stamps, 6..9 early group reducers, 11 / 16 / 20 extra reducers (R = 64 / 128, 20 = the product's
+    kernel), 21 = 16 with stamps, 22 = the product's stream without its reduce): fp64 closed form
+    within 1e-6 of term scale, dh and counts
     bitwise equal across variants (dh is per-element; the sums only differ in tree order), bitwise
     run-to-run, ragged last chunk; the default and the variants interleave on one workspace (the
     epoch-tagged granules need no cleanup between calls)."""
@@ -148,7 +150,7 @@ def test_surrogate_chunked_variants(dev, B):
     c = 2.0 / B * (np.abs(hn) + np.abs(k))
     ref_dh = None
     seen = {}
-    for variant in (0, 0, 1, 2, 3, 0, 4, 0, 5, 5, 2, 0, 1, 4, 5, 6, 7, 0, 8, 9, 6, 0):
+    for variant in (0, 0, 1, 2, 3, 0, 4, 0, 5, 5, 2, 0, 1, 4, 5, 6, 7, 0, 8, 9, 6, 0, 11, 16, 20, 21, 22, 0, 20):
         o = torch.zeros(6, dtype=torch.float64, device=dev)
         dh = torch.full((B,), float("nan"), device=dev)
         ops.surrogate_fwdbwd(h, y, abap[:3], abap[3:], dh=dh, out64=o, variant=variant)
@@ -157,14 +159,17 @@ def test_surrogate_chunked_variants(dev, B):
             ref_dh = dhn
         assert np.array_equal(dhn, ref_dh), variant
         assert np.all(np.abs(dhn - dh64) <= 1e-6 * np.maximum(np.abs(dh64), c)), variant
-        if variant in (3, 4):  # the stream without its reduce: no scalar outputs
+        if variant in (3, 4, 22):  # the stream without its reduce: no scalar outputs
             assert not o.any(), variant
             continue
         assert np.all(np.abs(got[:4] - [F, da, db, dal]) <= 1e-6 * sc + 1e-12), (variant, got, F)
         assert got[4] == np.sum(yn == 1) and got[5] == np.sum(yn == -1), variant
-        # fixed summation orders: bitwise run-to-run per variant (5 = 0's kernel with stamps; 6..9 =
-        # the early-reducer kernel: stamps and the lag change which workgroup reduces, not the order)
-        key = {5: 0, 7: 6, 8: 6, 9: 6}.get(variant, variant)
+        # fixed summation orders: bitwise run-to-run per kernel (6..9 = the early-reducer kernel:
+        # stamps and the lag change which workgroup reduces, not the order; 21 = 16 with stamps; the
+        # product at B >= 2^22 is variant 20's kernel)
+        key = {7: 6, 8: 6, 9: 6, 21: 16}.get(variant, variant)
+        if variant == 0 and B >= (1 << 22):
+            key = 20
         assert np.array_equal(got, seen.setdefault(key, got)), variant
     sums = torch.zeros(4, dtype=torch.float64, device=dev)
     ops.class_sums(h, y, sums, accumulate=False)  # chunked CLASS_ONLY path
@@ -217,6 +222,33 @@ def test_surrogate_tail_ignores_stale_granules(dev):
             gran.copy_(garbage * (1 << 32) + garbage)  # random tags (bit 31 clear: never current)
         assert np.array_equal(call(), ref), k
         epoch = (epoch + 1) & 0xFFFFFFFF
+
+
+def test_surrogate_timing_variants_leave_no_current_rows(dev):
+    """The tuning build's stream-only variants of the tail kernels (4, 22) store their rows but
+    reduce nothing, so the epoch does not advance: their rows carry a tag no call expects. A
+    product call on OTHER data right after one is bit-identical to the same call after a product
+    call (a stale row taken for a current one would change the sums)."""
+    from distributedauc_amd import ops
+
+    B = (1 << 22) + 4099
+    g = torch.Generator(device=dev).manual_seed(23)
+    h1, h2 = torch.rand(B, device=dev, generator=g), torch.rand(B, device=dev, generator=g) * 3.0 - 1.0
+    y1 = torch.where(torch.rand(B, device=dev, generator=g) < 0.1, 1, -1).to(torch.int8)
+    y2 = torch.where(torch.rand(B, device=dev, generator=g) < 0.4, 1, -1).to(torch.int8)
+    abap = torch.tensor([0.1, -0.2, 0.3, 0.1], device=dev)
+
+    def call(h, y, variant=0):
+        o = torch.zeros(6, dtype=torch.float64, device=dev)
+        ops.surrogate_fwdbwd(h, y, abap[:3], abap[3:], out64=o, variant=variant)
+        torch.cuda.synchronize()
+        return o.cpu().numpy()
+
+    call(h1, y1)
+    ref = call(h2, y2)
+    for v in (22, 4):
+        call(h1, y1, v)
+        assert np.array_equal(call(h2, y2), ref), v
 
 
 def test_class_sums_and_alpha(dev):
