@@ -1366,9 +1366,6 @@ constexpr int kCiMaxCells = kCiMaxBlocks * kCiBlock - 1;       // + the virtual 
 constexpr int kCiPlanThreads = 1024;
 // meta words (after the cell-slot index's): [8] usable, [9] cells, [10] blocks, [11] skewed
 constexpr int kCiOk = 8, kCiCells = 9, kCiBlocks = 10, kCiSkew = 11;
-// the fingerprint form of the direct build (DAUC_CI_FP): [12] 1 when the table's keys carry 4-bit
-// fingerprints in LDS (fewer cells, ~0.6 per key), [13] the fingerprint words (u32, 8 per word)
-constexpr int kCiFp = 12, kCiFpWords = 13;
 
 struct CountWs {
     unsigned* meta;    // [16]
@@ -1380,22 +1377,8 @@ struct CountWs {
 
 constexpr size_t kCountBytes = 256 + 3 * size_t(kCiTop) * 4 + ((size_t(kCiMaxCells) + 2) * 4 + 255) / 256 * 256 +
                                size_t(kCiMaxBlocks) * 8 + 256;
-#ifndef DAUC_CI_FP
-#define DAUC_CI_FP 0  // > 0: the direct build's fingerprint form, taken at <= DAUC_CI_FP keys per cell
-#endif
-// The fingerprint form's LDS: l1 (16 KB), nb block words, then the fingerprint words, within the
-// count index's own allocation (kCiTop + kCiMaxBlocks uint2). In global memory the fingerprint
-// words follow the block words in the blk region (word offset 2 nb), which the histogram pass zeroes.
-constexpr int kFpLdsUnits = kCiMaxBlocks;  // uint2 units for blocks + fingerprints
-// fingerprint words a table of M keys needs: 8 per word, + 2 so that the word after the last
-// one read (rank_lo >> 3) + 1 exists
-__host__ __device__ inline int64_t fp_words(int64_t M) { return (M + 7) / 8 + 2; }
 
 __device__ __forceinline__ unsigned ci_cell(unsigned key, uint2 e) { return e.x + __umulhi(key << kCiTopBits, e.y); }
-// the key's position inside its cell to 1/16: the top 4 bits of the fraction the cell map drops
-// (monotone in the key within a cell: a smaller fingerprint means a smaller key, equal ones decide
-// nothing)
-__device__ __forceinline__ unsigned ci_fp(unsigned key, unsigned C) { return ((key << kCiTopBits) * C) >> 28; }
 
 __device__ __forceinline__ bool count_index_in_use(const unsigned* __restrict__ meta) {
     return meta[kCiOk] != 0u && meta[kCiSkew] == 0u;
@@ -1497,8 +1480,6 @@ __global__ __launch_bounds__(kCiPlanThreads) void ci_plan_kernel(int64_t M, cons
         meta[kCiCells] = total;
         meta[kCiBlocks] = (total + 1 + kCiBlock - 1) / kCiBlock;
         meta[kCiSkew] = 0u;
-        meta[kCiFp] = 0u;
-        meta[kCiFpWords] = 0u;
     }
 }
 
@@ -1659,15 +1640,6 @@ __device__ __forceinline__ void ci_fix(unsigned x, unsigned rl, unsigned cnt, co
 #define DAUC_CI_DEPTH 1  // groups of stream loads in flight ahead of the group being located
 #endif
 
-#if DAUC_CI_FP
-#if DAUC_CI_MED3 || DAUC_CI_COUNT3 || DAUC_CI_PIPE != 1
-#error "the fingerprint form is implemented in the default pipelined query loop only"
-#endif
-#define FR_AMB(g, q) ((g).fr[q] == ~0u)
-#else
-#define FR_AMB(g, q) true
-#endif
-
 // The labeled query pass over the count index (same stream and checks as query_labeled_kernel);
 // returns at once when the builder kept the tree, so it is enqueued unconditionally. Per
 // iteration every slot's window loads are issued BEFORE the next iteration's stream loads:
@@ -1693,9 +1665,6 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
     const int nb = static_cast<int>(meta[kCiBlocks]);
     uint2* l1 = ci_lds;          // [2048]
     uint2* blk = ci_lds + kCiTop;  // [nb]
-    // the fingerprint form: its words follow the block words, here as in global memory
-    const bool fpm = DAUC_CI_FP && meta[kCiFp] != 0u;
-    const int nfill = nb + (fpm ? static_cast<int>((meta[kCiFpWords] + 1u) / 2u) : 0);
     {
         // the index into LDS with every load of a thread in flight before its first LDS store (a
         // load-store loop waits out one L2 round trip per iteration: 18 of them per thread)
@@ -1707,7 +1676,7 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
 #pragma unroll
         for (int j = 0; j < kBlkPer; ++j) {
             const int i = j * kQueryThreads + threadIdx.x;
-            v[j] = i < nfill ? blkg[i] : uint2{0u, 0u};
+            v[j] = i < nb ? blkg[i] : uint2{0u, 0u};
         }
         if (grp != nullptr) {
             // the direct build's block words hold prefixes within groups of 256 blocks: add the groups'
@@ -1715,21 +1684,17 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
             group_prefix(grp, (nb + kDirectGroup - 1) / kDirectGroup, pre);
             __syncthreads();
 #pragma unroll
-            for (int j = 0; j < kBlkPer; ++j) {
-                const int i = j * kQueryThreads + threadIdx.x;
-                if (i < nb) v[j].x += pre[i / kDirectGroup];
-            }
+            for (int j = 0; j < kBlkPer; ++j) v[j].x += pre[(j * kQueryThreads + threadIdx.x) / kDirectGroup];
         }
 #pragma unroll
         for (int j = 0; j < kL1Per; ++j) l1[j * kQueryThreads + threadIdx.x] = a[j];
 #pragma unroll
         for (int j = 0; j < kBlkPer; ++j) {
             const int i = j * kQueryThreads + threadIdx.x;
-            if (i < nfill) blk[i] = v[j];
+            if (i < nb) blk[i] = v[j];
         }
     }
     __syncthreads();
-    const unsigned* fpl = reinterpret_cast<const unsigned*>(blk + (fpm ? nb : 0));
     const unsigned M32 = static_cast<unsigned>(M);
     unsigned long long w = 0, t = 0;
     unsigned nf = 0;
@@ -1794,9 +1759,6 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
 #if DAUC_CI_W2
             uint4 k2[NQ];  // the next window, for cells that run past the first
 #endif
-#if DAUC_CI_FP
-            unsigned fr[NQ];  // the fingerprint form: the cell's keys < x, or ~0 (the windows decide)
-#endif
             unsigned use;
         };
         auto keys = [&](Group& g, const Stream& sg) {
@@ -1820,11 +1782,6 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
             uint2 e[NQ];
 #pragma unroll
             for (int q = 0; q < NQ; ++q) e[q] = l1[(DAUC_CI_ABLATE2 & 2) ? (g.x[q] >> 31) : (g.x[q] >> kCiLowBits)];
-#if DAUC_CI_FP
-            unsigned fx[NQ];
-#pragma unroll
-            for (int q = 0; q < NQ; ++q) fx[q] = ci_fp(g.x[q], e[q].y);
-#endif
             unsigned c[NQ];
 #pragma unroll
             for (int q = 0; q < NQ; ++q) c[q] = ci_cell(g.x[q], e[q]);
@@ -1842,35 +1799,6 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
                 if (DAUC_CI_ABLATE2 & 2)  // keep ~half the lanes gathering at spread positions
                     g.rc[q] = ((g.x[q] * 2654435761u) % (M32 + 1u)) | ((((g.x[q] >> 7) & 1u) | (rl >> 31)) << 28);
             }
-#if DAUC_CI_FP
-            // The cell's keys sit at table positions [rank_lo, rank_lo + count), their fingerprints
-            // at the same nibble positions: with the two words around rank_lo / 8 aligned, nibble j
-            // is the cell's j-th key (count <= 8). Per byte lane e + 0x80 - fx has bit 7 set iff
-            // e >= fx, e + 0x7f - fx iff e > fx (no carry between bytes: 0 <= e, fx <= 15). The
-            // nibbles past the cell are masked to 0 (>= fx only for fx = 0: subtracted). No key
-            // with x's fingerprint: the keys below x are counted (no ties); else ~0: the windows.
-            unsigned f0[NQ], f1[NQ];
-#pragma unroll
-            for (int q = 0; q < NQ; ++q) {
-                const unsigned wi = fpm ? (g.rc[q] & 0x0fffffffu) >> 3 : 0u;
-                f0[q] = fpl[wi];
-                f1[q] = fpl[wi + 1];
-            }
-#pragma unroll
-            for (int q = 0; q < NQ; ++q) {
-                const unsigned rl = g.rc[q] & 0x0fffffffu, cnt = g.rc[q] >> 28;
-                const unsigned n = cnt < 8u ? cnt : 8u;
-                const unsigned h = __builtin_amdgcn_alignbit(f1[q], f0[q], 4u * (rl & 7u)) &
-                                   (n == 8u ? ~0u : (1u << (4u * n)) - 1u);
-                const unsigned ev = h & 0x0f0f0f0fu, od = (h >> 4) & 0x0f0f0f0fu;
-                const unsigned kge = (0x80u - fx[q]) * 0x01010101u, kgt = (0x7fu - fx[q]) * 0x01010101u;
-                const unsigned ge = __builtin_popcount((ev + kge) & 0x80808080u) +
-                                    __builtin_popcount((od + kge) & 0x80808080u) - (fx[q] == 0u ? 8u - n : 0u);
-                const unsigned gt = __builtin_popcount((ev + kgt) & 0x80808080u) +
-                                    __builtin_popcount((od + kgt) & 0x80808080u);
-                g.fr[q] = (!fpm || cnt > 8u || ge != gt) ? ~0u : cnt - ge;
-            }
-#endif
         };
         auto locate_win = [&](Group& g) {
 #pragma unroll
@@ -1881,8 +1809,7 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
                 // rank_lo are of earlier cells (< x), the others of later cells or padding (> x)
                 g.k[q] = *reinterpret_cast<const uint4*>(sorted + (rl & ~3u));
 #else
-                const bool amb = !DAUC_CI_FP || FR_AMB(g, q);
-                g.k[q] = win_load(sorted + (((g.rc[q] >> 28) && amb && !(DAUC_CI_ABLATE2 & 1)) ? rl & ~3u : 0u));
+                g.k[q] = win_load(sorted + (((g.rc[q] >> 28) && !(DAUC_CI_ABLATE2 & 1)) ? rl & ~3u : 0u));
 #endif
             }
 #if DAUC_CI_W2
@@ -1894,8 +1821,7 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
 #pragma unroll
             for (int q = 0; q < NQ; ++q) {
                 const unsigned rl = g.rc[q] & 0x0fffffffu, cnt = g.rc[q] >> 28;
-                const bool amb = !DAUC_CI_FP || FR_AMB(g, q);
-                g.k2[q] = win_load(sorted + ((rl & 3u) + cnt > 4u && amb && !(DAUC_CI_ABLATE2 & 1) ? (rl & ~3u) + 4u : 0u));
+                g.k2[q] = win_load(sorted + ((rl & 3u) + cnt > 4u && !(DAUC_CI_ABLATE2 & 1) ? (rl & ~3u) + 4u : 0u));
             }
 #endif
         };
@@ -2008,13 +1934,8 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
 #pragma unroll
             for (int q = 0; q < NQ; ++q) {
                 // an empty cell's lane loaded the table's first window: counted as +inf padding
-                const bool amb = !DAUC_CI_FP || FR_AMB(g, q);
-                const uint4 k = ((g.rc[q] >> 28) && amb) ? g.k[q] : uint4{kPadKey, kPadKey, kPadKey, kPadKey};
-                more |= ci_count(g.x[q], ((g.use >> q) & 1u) && amb, g.rc[q] & 0x0fffffffu, g.rc[q] >> 28, k, M32, wl, tl);
-#if DAUC_CI_FP
-                // decided by the fingerprints: keys < x = rank_lo + fr, none equal
-                if (((g.use >> q) & 1u) && !amb) wl += M32 - (g.rc[q] & 0x0fffffffu) - g.fr[q];
-#endif
+                const uint4 k = (g.rc[q] >> 28) ? g.k[q] : uint4{kPadKey, kPadKey, kPadKey, kPadKey};
+                more |= ci_count(g.x[q], (g.use >> q) & 1u, g.rc[q] & 0x0fffffffu, g.rc[q] >> 28, k, M32, wl, tl);
             }
 #if DAUC_CI_W2
             // the second window's keys (those of the cell and of later cells; past the cell they
@@ -2024,14 +1945,13 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
             for (int q = 0; q < NQ; ++q) {
                 const unsigned x = g.x[q], rl = g.rc[q] & 0x0fffffffu, cnt = g.rc[q] >> 28;
                 const unsigned span = (rl & 3u) + cnt;
-                const bool amb = !DAUC_CI_FP || FR_AMB(g, q);
-                const unsigned m = 0u - (((g.use >> q) & 1u) & unsigned(span > 4u) & unsigned(amb));
+                const unsigned m = 0u - (((g.use >> q) & 1u) & unsigned(span > 4u));
                 const uint4 k2 = g.k2[q];
                 const unsigned lt = (k2.x < x) + (k2.y < x) + (k2.z < x) + (k2.w < x);
                 const unsigned le = (k2.x <= x) + (k2.y <= x) + (k2.z <= x) + (k2.w <= x);
                 wl -= le & m;
                 tl += (le - lt) & m;
-                more8 |= ((g.use >> q) & 1u) && span > 8u && amb;
+                more8 |= ((g.use >> q) & 1u) && span > 8u;
             }
             w += wl;
             t += tl;
@@ -2039,7 +1959,7 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
 #pragma unroll
                 for (int q = 0; q < NQ; ++q) {
                     const unsigned rl = g.rc[q] & 0x0fffffffu, cnt = g.rc[q] >> 28;
-                    if (((g.use >> q) & 1u) && (rl & 3u) + cnt > 8u && (!DAUC_CI_FP || FR_AMB(g, q))) {
+                    if (((g.use >> q) & 1u) && (rl & 3u) + cnt > 8u) {
                         // undo the two windows' counts, then count the cell key by key (ci_fix)
                         const unsigned x = g.x[q];
                         const uint4 k2 = g.k2[q];
@@ -2058,8 +1978,7 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
 #pragma unroll
                 for (int q = 0; q < NQ; ++q) {
                     const unsigned rl = g.rc[q] & 0x0fffffffu, cnt = g.rc[q] >> 28;
-                    if (((g.use >> q) & 1u) && (rl & 3u) + cnt > 4u && FR_AMB(g, q))
-                        ci_fix(g.x[q], rl, cnt, g.k[q], sorted, w, t);
+                    if (((g.use >> q) & 1u) && (rl & 3u) + cnt > 4u) ci_fix(g.x[q], rl, cnt, g.k[q], sorted, w, t);
                 }
             }
 #endif
@@ -2353,14 +2272,13 @@ constexpr int kDirectPerThread = 8;
 __global__ __launch_bounds__(256) void direct_hist_kernel(const float* __restrict__ pos,
                                                           const unsigned long long* __restrict__ Mp,
                                                           unsigned* __restrict__ hist, unsigned* __restrict__ cnt,
-                                                          int64_t ncnt, unsigned* __restrict__ blkw, int64_t nblkw) {
+                                                          int64_t ncnt) {
     const int64_t M = static_cast<int64_t>(*Mp);
     __shared__ unsigned h[kCiTop];
     for (int i = threadIdx.x; i < kCiTop; i += 256) h[i] = 0u;
     __syncthreads();
     const int64_t gid = int64_t(blockIdx.x) * 256 + threadIdx.x, stride = int64_t(gridDim.x) * 256;
     for (int64_t i = gid; i < ncnt; i += stride) cnt[i] = 0u;
-    for (int64_t i = gid; i < nblkw; i += stride) blkw[i] = 0u;  // block + fingerprint words
     for (int64_t i = gid; i < M; i += stride) atomicAdd(&h[key_fast(pos[i]) >> kCiLowBits], 1u);
     __syncthreads();
     for (int i = threadIdx.x; i < kCiTop; i += 256)
@@ -2400,20 +2318,7 @@ __global__ __launch_bounds__(kDirectThreads) void direct_count_kernel(const floa
     __syncthreads();
     const int64_t M = totals[2];
     const int64_t avail = int64_t(kCiMaxCells) - int64_t(totals[0]);
-    int64_t num = avail < 2 * M ? avail : 2 * M;
-    // the fingerprint form (DAUC_CI_FP): the block words and M / 8 fingerprint words share the
-    // count index's LDS, so the table gets fewer cells (~0.6 per key at 134k keys); it is taken
-    // when that still leaves at least one cell per DAUC_CI_FP keys
-    bool fp = false;
-    if (DAUC_CI_FP) {
-        const int64_t nb_max = int64_t(kFpLdsUnits) - (fp_words(M) + 1) / 2;
-        const int64_t avail_fp = 8 * nb_max - 8 - int64_t(totals[0]);
-        const int64_t num_fp = avail_fp < 2 * M ? avail_fp : 2 * M;
-        if (num_fp > 0 && int64_t(DAUC_CI_FP) * num_fp >= M) {
-            fp = true;
-            num = num_fp;
-        }
-    }
+    const int64_t num = avail < 2 * M ? avail : 2 * M;
     unsigned C[8], csum = 0u;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -2430,10 +2335,8 @@ __global__ __launch_bounds__(kDirectThreads) void direct_count_kernel(const floa
     }
     __syncthreads();
     const unsigned total = totals[1];
-    // usable: at most 1.5 keys per cell (the fingerprint form: 4), and the table fits the
-    // workspace (M <= mcap)
-    const bool ok = num > 0 && (fp ? int64_t(DAUC_CI_FP) * num >= M : 3 * num >= 2 * M) &&
-                    total <= static_cast<unsigned>(kCiMaxCells) && M <= mcap;
+    // usable: at most 1.5 keys per cell, and the table fits the workspace (M <= mcap)
+    const bool ok = num > 0 && 3 * num >= 2 * M && total <= static_cast<unsigned>(kCiMaxCells) && M <= mcap;
     if (blockIdx.x == 0) {
         for (int t = threadIdx.x; t < kCiTop; t += kDirectThreads) l1g[t] = l1[t];
         if (threadIdx.x == 0) {
@@ -2441,8 +2344,6 @@ __global__ __launch_bounds__(kDirectThreads) void direct_count_kernel(const floa
             meta[kCiCells] = total;
             meta[kCiBlocks] = (total + 1 + kCiBlock - 1) / kCiBlock;
             meta[kCiSkew] = 0u;
-            meta[kCiFp] = fp ? 1u : 0u;
-            meta[kCiFpWords] = fp ? static_cast<unsigned>(fp_words(M)) : 0u;
         }
     }
     if (!ok) return;
@@ -2507,13 +2408,9 @@ __global__ __launch_bounds__(kDirectThreads) void direct_scatter_kernel(const fl
                                                                         const unsigned* __restrict__ meta,
                                                                         unsigned* __restrict__ cnt,
                                                                         const unsigned* __restrict__ cell,
-                                                                        unsigned* __restrict__ table,
-                                                                        const uint2* __restrict__ l1g) {
+                                                                        unsigned* __restrict__ table) {
     if (meta[kCiOk] == 0u || meta[kCiSkew] != 0u) return;
     const int64_t M = static_cast<int64_t>(*Mp);
-    const bool fp = meta[kCiFp] != 0u;
-    // the fingerprint words follow the block words (zeroed by the histogram pass)
-    unsigned* fpw = reinterpret_cast<unsigned*>(const_cast<uint2*>(blk) + meta[kCiBlocks]);
     __shared__ unsigned pre[kDirectMaxGroups];
     group_prefix(grp, (static_cast<int>(meta[kCiBlocks]) + kDirectGroup - 1) / kDirectGroup, pre);
     __syncthreads();
@@ -2527,9 +2424,7 @@ __global__ __launch_bounds__(kDirectThreads) void direct_scatter_kernel(const fl
         const unsigned below = __builtin_amdgcn_ubfe(b.y, 0u, 4u * (c % kCiBlock));
         const unsigned bytes = (below & 0x0f0f0f0fu) + ((below >> 4) & 0x0f0f0f0fu);
         const unsigned slot = atomicSub(cnt + c, 1u) - 1u;
-        const unsigned at = pre[bi / kDirectGroup] + b.x + __builtin_amdgcn_sad_u8(bytes, 0u, 0u) + slot;
-        table[at] = x;
-        if (fp) atomicOr(fpw + (at >> 3), ci_fp(x, l1g[x >> kCiLowBits].y) << (4u * (at & 7u)));
+        table[pre[bi / kDirectGroup] + b.x + __builtin_amdgcn_sad_u8(bytes, 0u, 0u) + slot] = x;
     }
 }
 
@@ -2966,14 +2861,13 @@ int counts_labeled_direct(const float* pos, const unsigned long long* Mp, int64_
         return dim3(static_cast<unsigned>(b < cap ? b : cap));
     };
     hipLaunchKernelGGL(direct_hist_kernel, blocks(Mcap, 256 * kDirectPerThread, 256), dim3(256), 0, st, pos, Mp,
-                       nw.first, nw.cstart, kCiCntWords, reinterpret_cast<unsigned*>(nw.blk),
-                       DAUC_CI_FP ? int64_t(kCiMaxBlocks) * 2 : int64_t(0));
+                       nw.first, nw.cstart, kCiCntWords);
     hipLaunchKernelGGL(direct_count_kernel, blocks(Mcap, kDirectThreads, 1024), dim3(kDirectThreads), 0, st, pos,
                        Mcap, nw.first, nw.l1, nw.meta, nw.cstart, w.keys_b);
     hipLaunchKernelGGL(direct_blocks_kernel, dim3(kDirectMaxGroups), dim3(kDirectGroup), 0, st, nw.cstart, nw.meta,
                        nw.blk, grp);
     hipLaunchKernelGGL(direct_scatter_kernel, blocks(Mcap, kDirectThreads, 1024), dim3(kDirectThreads), 0, st, pos,
-                       Mp, nw.blk, grp, nw.meta, nw.cstart, w.keys_b, table, nw.l1);
+                       Mp, nw.blk, grp, nw.meta, nw.cstart, w.keys_b, table);
     int rc = launch_status();
     if (rc || end == begin) return rc;
     switch (label_dtype) {
