@@ -337,6 +337,40 @@ __device__ __forceinline__ unsigned label_masks16(const LT* __restrict__ lab, in
     return pos;
 }
 
+#ifndef DAUC_COMPACT_BATCH
+#define DAUC_COMPACT_BATCH 8  // > 0: the compactions load a tile's labels this many 16-B loads at a time
+                              // (0: one group per bounds-checked branch, round 2's form)
+#endif
+
+// the positive mask and the labels outside {-1, 1} of 16 labels already in registers (the bounds-
+// and alignment-checked case of label_masks16)
+template <typename LT>
+__device__ __forceinline__ unsigned masks16_of(const int4 (&v)[sizeof(LT)], int& nother) {
+    unsigned pos = 0;
+    if constexpr (sizeof(LT) == 1) {
+        const unsigned w[4] = {unsigned(v[0].x), unsigned(v[0].y), unsigned(v[0].z), unsigned(v[0].w)};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const unsigned p = zero_bytes(w[q] ^ 0x01010101u), m = zero_bytes(~w[q]);
+            pos |= byte_flags4(p) << (4 * q);
+            nother += 4 - __popc(p | m);
+        }
+    } else {
+        constexpr int kPer = 16 / sizeof(LT);  // labels per int4
+#pragma unroll
+        for (int q = 0; q < int(sizeof(LT)); ++q) {
+            LT c[kPer];
+            *reinterpret_cast<int4*>(c) = v[q];
+#pragma unroll
+            for (int j = 0; j < kPer; ++j) {
+                pos |= unsigned(c[j] == LT(1)) << (q * kPer + j);
+                nother += c[j] != LT(1) && c[j] != LT(-1);
+            }
+        }
+    }
+    return pos;
+}
+
 // Two launches. (1) count: per tile, its positives and its labels outside {-1, 1}, and the
 // positive bit masks (1 bit per label, one 16-B store per thread). (2) write: every tile first
 // sums the positive counts of the tiles before it (its 256 threads read them strided from L2 and
@@ -364,9 +398,24 @@ __global__ __launch_bounds__(kCmpThreads) void compact_count_kernel(const LT* __
         for (int i = threadIdx.x; i < nzero_w; i += kCmpThreads) zero_w[i] = 0u;
     int np = 0, no = 0;
     unsigned m[kCmpSlots];
+    if (DAUC_COMPACT_BATCH && vec && base + kCmpTile <= n) {
+        // a tile wholly in range and aligned (uniform): every group's loads in straight-line code,
+        // not one bounds-checked branch (and so one memory latency) per group
+        constexpr int kPer = int(sizeof(LT));
+        int4 v[kCmpSlots][kPer];
 #pragma unroll
-    for (int k = 0; k < kCmpSlots; ++k)
-        m[k] = label_masks16(lab, base + (int64_t(k) * kCmpThreads + threadIdx.x) * 16, n, vec, no);
+        for (int k = 0; k < kCmpSlots; ++k) {
+            const int4* src = reinterpret_cast<const int4*>(lab + base + (int64_t(k) * kCmpThreads + threadIdx.x) * 16);
+#pragma unroll
+            for (int q = 0; q < kPer; ++q) v[k][q] = src[q];
+        }
+#pragma unroll
+        for (int k = 0; k < kCmpSlots; ++k) m[k] = masks16_of<LT>(v[k], no);
+    } else {
+#pragma unroll
+        for (int k = 0; k < kCmpSlots; ++k)
+            m[k] = label_masks16(lab, base + (int64_t(k) * kCmpThreads + threadIdx.x) * 16, n, vec, no);
+    }
 #pragma unroll
     for (int k = 0; k < kCmpSlots; ++k) np += __popc(m[k]);
     masks[int64_t(blockIdx.x) * kCmpThreads + threadIdx.x] =
@@ -514,13 +563,54 @@ __global__ __launch_bounds__(THREADS) void compact_unordered_kernel(
     const unsigned long long seen = stats[1];
     const int64_t base = int64_t(blockIdx.x) * kTileU;
     int no = 0;
+    int np = 0;
+#if DAUC_COMPACT_BATCH
+    // label_masks16's bounds check is a branch per group, and a load consumed inside a branch is
+    // waited for at once (vmcnt(0)): the groups' loads went out one memory latency apart. A tile
+    // wholly in range and aligned (uniform) issues them DAUC_COMPACT_BATCH at a time in straight-
+    // line code; the masks wait in LDS (16 bits per group) for the write phase, so no batch's
+    // registers stay live across the next (a rolled loop: nothing hoisted past it)
+    __shared__ unsigned short msk[SLOTS][THREADS];
+    if (vec && base + kTileU <= n) {
+        constexpr int kPer = int(sizeof(LT));  // 16-B loads per group
+        constexpr int kB = DAUC_COMPACT_BATCH / kPer > 0 ? DAUC_COMPACT_BATCH / kPer : 1;
+        constexpr int kBatch = kB < SLOTS ? kB : SLOTS;
+        static_assert(SLOTS % kBatch == 0, "whole batches");
+        const char* tb = reinterpret_cast<const char*>(lab + base);  // uniform
+        const unsigned lane_off = threadIdx.x * 16u * unsigned(sizeof(LT));
+        constexpr unsigned kSlotBytes = unsigned(THREADS) * 16u * unsigned(sizeof(LT));
+#pragma unroll 1
+        for (int k0 = 0; k0 < SLOTS; k0 += kBatch) {
+            int4 v[kBatch][kPer];
+#pragma unroll
+            for (int j = 0; j < kBatch; ++j) {
+                const int4* src = reinterpret_cast<const int4*>(tb + (lane_off + unsigned(k0 + j) * kSlotBytes));
+#pragma unroll
+                for (int q = 0; q < kPer; ++q) v[j][q] = src[q];
+            }
+#pragma unroll
+            for (int j = 0; j < kBatch; ++j) {
+                const unsigned mm = masks16_of<LT>(v[j], no);
+                np += __popc(mm);
+                msk[k0 + j][threadIdx.x] = static_cast<unsigned short>(mm);
+            }
+        }
+    } else {
+#pragma unroll 1
+        for (int k = 0; k < SLOTS; ++k) {
+            const unsigned mm = label_masks16(lab, base + (int64_t(k) * THREADS + threadIdx.x) * 16, n, vec, no);
+            np += __popc(mm);
+            msk[k][threadIdx.x] = static_cast<unsigned short>(mm);
+        }
+    }
+#else
     unsigned m[SLOTS];
 #pragma unroll
     for (int k = 0; k < SLOTS; ++k)
         m[k] = label_masks16(lab, base + (int64_t(k) * THREADS + threadIdx.x) * 16, n, vec, no);
-    int np = 0;
 #pragma unroll
     for (int k = 0; k < SLOTS; ++k) np += __popc(m[k]);
+#endif
     const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
     int incl = np;  // inclusive scan of the positives over the wave's lanes
 #pragma unroll
@@ -550,10 +640,19 @@ __global__ __launch_bounds__(THREADS) void compact_unordered_kernel(
     if (tile == 0) return;
     int64_t r = int64_t(base_s) + before + incl - np;
     int nf = 0;
+#if DAUC_COMPACT_BATCH
+#pragma unroll 1
+#else
 #pragma unroll
+#endif
     for (int k = 0; k < SLOTS; ++k) {
         const int64_t i = base + (int64_t(k) * THREADS + threadIdx.x) * 16;
-        for (unsigned b = m[k]; b != 0u; b &= b - 1u) {
+#if DAUC_COMPACT_BATCH
+        const unsigned mk = msk[k][threadIdx.x];  // this thread's own word: no barrier needed
+#else
+        const unsigned mk = m[k];
+#endif
+        for (unsigned b = mk; b != 0u; b &= b - 1u) {
             const float v = s[i + __ffs(b) - 1];
             nf += !isfinite(v);
             pos_out[r++] = v;
