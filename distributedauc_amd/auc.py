@@ -103,17 +103,28 @@ class ExactAUC:
         # and positive blocks shard
         pos, neg, stats = ops.split_scores(s, y)
         P, N, nonfinite, other = (int(v) for v in stats.tolist())
-        if nonfinite:
-            raise ValueError("Input y_score contains NaN or infinity.")
-        self._check_labels(other, y)
         wt = torch.zeros(3, dtype=torch.int64, device=s.device)
-        if P and N:
+        if P and N and not nonfinite:
             lo, hi = self.rank * P // self.world, (self.rank + 1) * P // self.world
             if hi > lo:
                 ops.pair_count(pos[lo:hi], neg[:N], wt, variant=self.variant)
         if self.world > 1 and self.reduce:
-            dist.all_reduce(wt, op=dist.ReduceOp.SUM, group=self.group)
-        W, T, _ = (int(v) for v in wt.tolist())
+            # one all-gather of every rank's (W, T, P, N, non-finite, other): the split's figures
+            # must agree (ranks holding different test sets raise together), and no rank raises
+            # before the collective, so a bad input cannot leave the others waiting in it
+            mine = torch.cat((wt[:2], stats.to(device=wt.device, dtype=torch.int64)))
+            gathered = torch.empty(6 * self.world, dtype=torch.int64, device=wt.device)
+            dist.all_gather_into_tensor(gathered, mine, group=self.group)
+            vals = gathered.view(self.world, 6).tolist()
+            if len({tuple(v[2:]) for v in vals}) != 1:
+                raise RuntimeError("ExactAUC: the ranks' parts disagree on the test set (positives, non-finite or "
+                                   "label counts): every rank must pass the same scores and labels")
+            W, T = sum(v[0] for v in vals), sum(v[1] for v in vals)
+        else:
+            W, T, _ = (int(v) for v in wt.tolist())
+        if nonfinite:
+            raise ValueError("Input y_score contains NaN or infinity.")
+        self._check_labels(other, y)
         return {"wins": W, "ties": T, "P": P, "N": N}
 
     @staticmethod

@@ -168,6 +168,27 @@ def auc_eval_enqueue(scores, labels, part, parts, out=None):
     return rec
 
 
+def split_scores(scores, labels, negatives=True):
+    """dauc_split_scores' stand-in: stable (pos, neg) buffers of capacity n and the stats
+    {P, N, #non-finite scores, #labels not in {-1, 1}} (N counts every label != 1)."""
+    s, y = scores.detach(), labels
+    m = y == 1
+    P = int(m.sum())
+    pos, neg = torch.empty_like(s), torch.empty_like(s) if negatives else None
+    pos[:P] = s[m]
+    if negatives:
+        neg[: s.numel() - P] = s[~m]
+    other = int(((y != 1) & (y != -1)).sum())
+    return pos, neg, torch.tensor([P, s.numel() - P, int((~torch.isfinite(s)).sum()), other], dtype=torch.int64)
+
+
+def pair_count(pos, neg, wins_ties, variant=0):
+    """dauc_pair_count's stand-in: wins_ties[0:2] += the brute-force (wins, ties) of pos x neg."""
+    W, T = coracle_pair_count(pos.detach().numpy(), neg.detach().numpy())
+    wins_ties[0] += W
+    wins_ties[1] += T
+
+
 def coracle_pair_count(pos, neg):
     from oracle import coracle
 
@@ -179,7 +200,7 @@ def install(monkeypatch):
 
     for name in ("label_map_phat", "surrogate_fwdbwd", "class_sums", "alpha_from_sums", "coda_finalize",
                  "scale_div", "pd_update", "compact_positives", "auc_counts_sorted_labeled", "auc_eval_counts",
-                 "auc_eval_counts_part", "auc_eval_enqueue"):
+                 "auc_eval_counts_part", "auc_eval_enqueue", "split_scores", "pair_count"):
         monkeypatch.setattr(ops, name, globals()[name])
     monkeypatch.setattr(flat, "_check_device", lambda dev: None)
 

@@ -91,3 +91,72 @@ def test_sharded_sort_auc_gloo(world, shard_min):
     errs = [e for _, e in res if e]
     assert not errs, "\n".join(errs)
     assert sorted(r for r, _ in res) == list(range(world))
+
+
+def _pairs_worker(rank, world, port, q):
+    import traceback
+
+    import torch.distributed as dist
+
+    try:
+        torch.set_num_threads(1)
+        cpu_kernels.install_in_process()
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from distributedauc_amd.auc import ExactAUC
+        from oracle import coracle
+
+        rng = np.random.default_rng(11)
+        n = 3_001
+        s = (np.floor(rng.random(n) * 211) / 211).astype(np.float32)
+        y = np.where(rng.random(n) < 0.05, 1, -1).astype(np.int8)
+        ev = ExactAUC(world=world, rank=rank, method="pairs")
+        c = ev.counts(torch.from_numpy(y), torch.from_numpy(s), device="cpu")
+        e = coracle.auc_counts(y.astype(np.int64), s)
+        assert (c["wins"], c["ties"], c["P"], c["N"]) == (e["wins"], e["ties"], e["P"], e["N"]), (c, e)
+        # a non-finite score: every rank raises after the gather (none is left in the collective)
+        s2 = s.copy()
+        s2[7] = np.inf
+        with pytest.raises(ValueError, match="NaN or infinity"):
+            ev.counts(torch.from_numpy(y), torch.from_numpy(s2), device="cpu")
+        # ranks holding different vectors: every rank raises
+        y3 = y.copy()
+        if rank == 1:
+            y3[np.flatnonzero(y == -1)[:4]] = 1
+        with pytest.raises(RuntimeError, match="disagree"):
+            ev.counts(torch.from_numpy(y3), torch.from_numpy(s), device="cpu")
+        # and the group is still usable afterwards: the same exact counts
+        c2 = ev.counts(torch.from_numpy(y), torch.from_numpy(s), device="cpu")
+        assert c2 == c, (c2, c)
+        dist.destroy_process_group()
+        q.put((rank, None))
+    except BaseException:
+        q.put((rank, traceback.format_exc()))
+
+
+@pytest.mark.timeout(300)
+def test_sharded_pairs_auc_gloo():
+    """The pair-count method over world 2: positive blocks sharded, one all-gather of the
+    per-rank (W, T, P, N, non-finite, other) records; inconsistent or non-finite inputs raise on
+    every rank together (no rank may raise while the others wait in the collective)."""
+    import torch.multiprocessing as mp
+
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    port = _free_port()
+    procs = [ctx.Process(target=_pairs_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(240)
+    res = []
+    while not q.empty():
+        res.append(q.get())
+    for p in procs:
+        if p.is_alive():
+            p.kill()
+    errs = [e for _, e in res if e]
+    assert not errs, "\n".join(errs)
+    assert sorted(r for r, _ in res) == list(range(world))
