@@ -579,6 +579,26 @@ def test_auc_eval_counts_one_call(dev, ldtype):
             assert bad >= 1, (where, p)
 
 
+@pytest.mark.parametrize("ldtype", [np.int8, np.int32, np.int64])
+def test_auc_eval_counts_wide_tiles(dev, ldtype):
+    """From 2^25 labels the one-pass compaction takes 131072-label tiles whose label loads go out
+    in straight-line batches when the tile is wholly in range and aligned (DAUC_COMPACT_BATCH);
+    a ragged last tile and a misaligned label slice take the per-group bounds-checked path. Both,
+    for every label width, against the C oracle (2^25 + 7 labels, 0.1 % positives)."""
+    from distributedauc_amd import ops
+
+    rng = np.random.default_rng(2025)
+    n = (1 << 25) + 7
+    for off in (0, 1):
+        sall = (np.floor(rng.random(n + off) * 50_000) / 50_000).astype(np.float32)
+        yall = np.where(rng.random(n + off) < 0.001, 1, -1).astype(ldtype)
+        yall[rng.random(n + off) < 1e-5] = 0  # counted as a negative and as "other"
+        s, y = sall[off:], yall[off:]
+        W, Tt, P, N, bad, other = ops.auc_eval_counts(T(sall, dev)[off:], T(yall, dev)[off:])
+        e = coracle.auc_counts(y.astype(np.int64), s)
+        assert (W, Tt, P, N, bad, other) == (e["wins"], e["ties"], e["P"], e["N"], 0, int((y == 0).sum())), off
+
+
 def test_auc_eval_counts_stale_workspace(dev):
     """The evaluation re-initialises every byte of state it reads (one memset of the workspace
     header per call): a workspace overwritten with garbage between calls (as a freed-and-
