@@ -74,6 +74,11 @@ def parse(argv=None):
     p.add_argument("--image-size", type=int, default=224)
     p.add_argument("--I", type=int, default=16)
     p.add_argument("--pos-ratio", type=float, default=0.1)
+    p.add_argument("--lr", type=float, default=0.01,
+                   help="CoDA step size. The reference runs lr 0.1 on a PRETRAINED ResNet-50 (node0.sh); from "
+                        "random init at 0.1 its own loop saturates the softmax column within 5 steps (the CPU "
+                        "oracle loop too: profiles/r04/direction/), so the in-training AUC is meaningless there. "
+                        "0.01 learns the synthetic signal. The step's kernels and bytes do not depend on lr")
     p.add_argument("--pool", type=int, default=4, help="distinct resident input batches cycled")
     p.add_argument("--sweep-I", default="1,8,16,32", help="configs[2] averaging periods ('' = off)")
     p.add_argument("--sweep-steps", type=int, default=32, help="timed steps per period (a multiple of every I)")
@@ -86,6 +91,9 @@ def parse(argv=None):
     p.add_argument("--auc-log2n", type=int, default=24)
     p.add_argument("--auc-pos", type=float, default=0.01)
     p.add_argument("--auc-reps", type=int, default=3)
+    p.add_argument("--auc-shard-min", type=int, default=None,
+                   help="scores below which N > 1 ranks evaluate the whole vector instead of sharding "
+                        "(default ExactAUC.SHARD_MIN = 2^24; 0 shards every size, for rehearsals)")
     p.add_argument("--auc2-log2n", type=int, default=27, help="configs[4] leg (0 = off)")
     p.add_argument("--auc2-pos", type=float, default=0.001)
     p.add_argument("--sur-log2b", type=int, default=26, help="surrogate kernel leg: batch of 2^k scores")
@@ -202,7 +210,7 @@ def timed_steps(coda, it, steps: int, world: int) -> float:
 
 # ----------------------------------------------------------------------------- training legs
 def make_coda(arch, batch, image_size, I, pos_ratio, pool, world, rank, device, fused_bn=True, gemm_conv1x1=True,
-              graph=False):
+              graph=False, lr=0.1):
     from distributedauc_amd.backbone import build_backbone
     from distributedauc_amd.coda import CoDA
     from distributedauc_amd.loader import DeviceLoader, SyntheticImageNet, imagenet_like_labels
@@ -214,7 +222,7 @@ def make_coda(arch, batch, image_size, I, pos_ratio, pool, world, rank, device, 
     loader = DeviceLoader(ds, np.arange(len(labels)), batch, device, seed=1234 + rank, channels_last=True, pool=pool)
     net = build_backbone(arch, num_classes=2).to(device).to(memory_format=torch.channels_last)
     net.set_fused_bn(bool(fused_bn)).set_gemm_conv1x1(bool(gemm_conv1x1))
-    coda = CoDA(net, lr=0.1, gamma=2000.0, T0=10 ** 9, I=I, split_index=split, world=world, rank=rank,
+    coda = CoDA(net, lr=lr, gamma=2000.0, T0=10 ** 9, I=I, split_index=split, world=world, rank=rank,
                 autocast_dtype=torch.bfloat16, device=device)
     it = iter(loader)
     coda.average_all()            # main.py:141-142
@@ -227,7 +235,7 @@ def bench_train(args, world, rank, device):
     from distributedauc_amd import _lib
 
     coda, it = make_coda(args.arch, args.batch, args.image_size, args.I, args.pos_ratio, args.pool, world, rank,
-                         device, args.fused_bn, args.gemm_conv1x1)
+                         device, args.fused_bn, args.gemm_conv1x1, lr=args.lr)
     log(f"rank {rank}: model + data ready, first steps compile/tune MIOpen kernels")
     lib = _lib.load()
     upd = KernelTimer(lib, "dauc_pd_update")
@@ -281,7 +289,15 @@ def bench_training_eval(coda, args, world, rank, device, reps=3):
     """The in-training evaluation (main.py:215-270): the test set scored with rank 0's model, then
     the exact AUC. Split: every rank scores 1/world of the batches after a broadcast of rank 0's
     parameters and BN statistics, all-gather of the scores, sharded count (main.Evaluator). At
-    world > 1 the reference's rank-0 scoring is timed beside it; both give the same AUC."""
+    world > 1 the reference's rank-0 scoring is timed beside it.
+
+    MIOpen's default (fast) solvers are not bit-repeatable from call to call, so two scorings of
+    the same test set -- split or rank 0, or two repetitions of either -- may differ in the low
+    bits of a few scores and flip a near-tie. Bit-identical scoring needs --deterministic_eval
+    (61 s for ResNet-50 224^2 bf16 at 8192 images, profiles/r03/final): too slow for the bench.
+    So the AUCs of every repetition and of both scoring modes are REPORTED (with their largest
+    difference), never asserted equal; tests/test_main_gpu.py checks bit-identity under
+    deterministic solvers."""
     from distributedauc_amd.loader import DeviceLoader, SyntheticImageNet, imagenet_like_labels
     from distributedauc_amd.main import Evaluator
 
@@ -295,30 +311,30 @@ def bench_training_eval(coda, args, world, rank, device, reps=3):
     def timed(split):
         ev = Evaluator(batches, n, 499, device, None, world, rank, None, split=split)
         ev(coda)  # warm (workspaces, MIOpen eval-mode kernels)
-        ts, auc = [], None
+        ts, aucs = [], []
         for _ in range(reps):
             if world > 1:
                 dist.barrier()
             torch.cuda.synchronize()
             t0 = time.perf_counter()
-            a = ev(coda)
+            aucs.append(ev(coda))
             torch.cuda.synchronize()
             ts.append(time.perf_counter() - t0)
-            assert auc is None or a == auc
-            auc = a
-        return max_over_ranks(float(np.median(ts)), world), auc
+        return max_over_ranks(float(np.median(ts)), world), aucs
 
-    ms_split, auc_split = timed(True)
+    ms_split, aucs = timed(True)
     rec = {"workload": f"{n} test images {args.image_size}^2 scored by {args.arch} (eval mode, bf16 autocast), "
                        f"test batch {tb}, then the exact AUC; {world} rank(s)",
-           "ms": ms_split * 1e3, "imgs_per_sec": n / ms_split, "auc": auc_split,
-           "method": "split" if world > 1 else "one rank"}
+           "ms": ms_split * 1e3, "imgs_per_sec": n / ms_split, "auc": aucs[-1], "auc_reps": aucs,
+           "method": "split" if world > 1 else "one rank",
+           "auc_note": "AUCs are reported, not asserted equal: MIOpen's fast solvers change low bits between "
+                       "scorings (bit-identity needs --deterministic_eval, tested in tests/test_main_gpu.py)"}
     if world > 1:
-        ms0, auc0 = timed(False)
-        if auc0 != auc_split:
-            raise RuntimeError(f"split scoring AUC {auc_split!r} != rank-0 scoring AUC {auc0!r}")
-        rec.update({"ms_rank0_scoring": ms0 * 1e3, "speedup_vs_rank0_scoring": ms0 / ms_split})
-    log(f"rank {rank}: in-training eval of {n} images {ms_split * 1e3:.1f} ms")
+        ms0, aucs0 = timed(False)
+        rec.update({"ms_rank0_scoring": ms0 * 1e3, "speedup_vs_rank0_scoring": ms0 / ms_split,
+                    "auc_rank0_scoring": aucs0[-1],
+                    "auc_max_abs_diff_split_vs_rank0": max(abs(a - b) for a in aucs for b in aucs0)})
+    log(f"rank {rank}: in-training eval of {n} images {ms_split * 1e3:.1f} ms, auc {aucs[-1]:.4f}")
     return rec
 
 
@@ -848,6 +864,7 @@ def main():
                                        f"{' (1x1 convs as GEMMs)' if args.gemm_conv1x1 else ''}, fp32 AUC kernels "
                                        "(BASELINE configs[1])",
                            "global_batch": args.batch * world, "image_size": args.image_size, "I": args.I,
+                           "lr": args.lr, "gamma": 2000.0,
                            "pos_ratio": args.pos_ratio, "parallelism": f"dp{world}", "params": res["n_params"]},
                 "roofline": {"kernel": "dauc_pd_update (fused dppd_sg + running average)", "bound": "hbm",
                              "achieved": upd_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",

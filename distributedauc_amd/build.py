@@ -18,6 +18,8 @@ REPO = PKG_DIR.parent
 CSRC = PKG_DIR / "csrc"
 OBJ_DIR = PKG_DIR / "build"
 LIB_PATH = PKG_DIR / "libdauc.so"
+# linker version script: only the dauc_* C entry points are exported (no C++ internals)
+EXPORTS = CSRC / "exports.map"
 # the tuning build: the same sources with -DDAUC_TUNING, which adds the measured alternatives'
 # entry points (include/dauc_tuning.h); tests and micro-benchmarks load it, the product never does
 TUNING_LIB_PATH = REPO / "tuning" / "libdauc_tuning.so"
@@ -48,7 +50,7 @@ def _needs_build(target: Path = LIB_PATH) -> bool:
     if not target.exists():
         return True
     t = target.stat().st_mtime
-    deps = sources() + sorted(CSRC.glob("*.h")) + sorted((REPO / "include").glob("*.h")) + [Path(__file__)]
+    deps = sources() + sorted(CSRC.glob("*.h")) + sorted((REPO / "include").glob("*.h")) + [Path(__file__), EXPORTS]
     return any(p.stat().st_mtime > t for p in deps)
 
 
@@ -80,7 +82,8 @@ def build_library(force: bool = False, verbose: bool = False, out: Path | None =
     with cf.ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
         objs = list(ex.map(lambda s: _compile(s, obj_dir, tuple(defines)), srcs))
     tmp = target.with_suffix(".so.tmp")
-    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs), "-o", str(tmp)]
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", f"-Wl,--version-script={EXPORTS}", *map(str, objs),
+           "-o", str(tmp)]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed:\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")

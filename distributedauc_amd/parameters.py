@@ -55,7 +55,8 @@ def get_parser() -> argparse.ArgumentParser:
                    help="softmax: the model ends in Softmax like resnet.py:159; logits: the softmax column is "
                         "folded into the fused surrogate kernel")
     p.add_argument("--split_eval", type=int, default=1,
-                   help="1: every rank scores a share of the test set with rank 0's model (same AUC); "
+                   help="1: every rank scores a share of the test set with rank 0's model (the same AUC "
+                        "bit for bit only with --deterministic_eval 1; otherwise as close as two rank-0 scorings); "
                         "0: rank 0 scores it all (main.py:232)")
     p.add_argument("--deterministic_eval", type=int, default=0,
                    help="1: score the test set with repeatable convolution solvers (cudnn.deterministic), so "

@@ -273,3 +273,63 @@ def partition_indices(sizes, seed: int = 123, neg_keep_ratio: float = 1.0,
         out.append(idx[:k])
         idx = idx[k:]
     return out
+
+
+# --------------------------------------------------------------- the loop (main.py:140-334, size == 1)
+def train_stage1_world1(net, batches, steps: int, lr: float, gamma: float, split_index: int, I: int = 16):
+    """One rank's stage 1 of the reference's training loop, restated with the functions above.
+
+    main.py:141-142 the pre-training average (size == 1: nothing to average; the counts fold);
+    main.py:154-158 the anchor; main.py:170-197 alpha over 3 batches of ``batches`` in eval mode
+    (the reference forwards each batch twice, 185 and 187; under no_grad in eval mode both
+    passes give the same scores, so one is taken); main.py:210-327 ``steps`` training steps:
+    the count fold every I steps (297-301), the label map and counts (303-308), p_hat (309-310),
+    the verbatim loss (313-317), zero_grad + backward (318-326) and dppd_sg (327, reference
+    quirks). ``batches`` yields CPU (x, class-label) pairs and is consumed exactly as the
+    reference consumes ``train_iter``. Returns the per-step losses; ``net`` is trained in place
+    and (a, b, alpha) are returned with them."""
+    gpos, gneg = torch.zeros(1), torch.zeros(1)
+    lpos, lneg = torch.zeros(1), torch.zeros(1)
+    a, b, alpha = (torch.zeros(1, requires_grad=True) for _ in range(3))
+    net0 = {k: v.clone() for k, v in net.state_dict().items()}
+    a0, b0 = a.detach().clone(), b.detach().clone()
+    sums = [0.0, 0.0, 0.0, 0.0]
+    net.eval()
+    with torch.no_grad():
+        for _ in range(3):
+            x, lab = next(batches)
+            y = torch.where(lab <= split_index, -1, 1)
+            h = net(x)[:, 1]
+            sums[0] += float(torch.sum(h * (y == -1).float()))
+            sums[1] += float(torch.sum(y == -1))
+            sums[2] += float(torch.sum(h * (y == 1).float()))
+            sums[3] += float(torch.sum(y == 1))
+    net.train()
+    alpha.data = torch.tensor([alpha_from_sums(*sums)], dtype=torch.float32)
+    alpha0 = alpha.detach().clone()
+    losses = []
+    for t_total in range(1, steps + 1):
+        x, lab = next(batches)
+        if t_total % I == 0:
+            gneg += lneg
+            gpos += lpos
+            lpos, lneg = torch.zeros(1), torch.zeros(1)
+        y = torch.where(lab <= split_index, -1, 1)
+        lpos += float(torch.sum(y == 1))
+        lneg += float(torch.sum(y == -1))
+        p = torch.tensor([float(phat(float(gpos), float(gneg), float(lpos), float(lneg)))])
+        h = net(x)[:, 1]
+        loss = surrogate_loss(h, y, a, b, alpha, p)
+        net.zero_grad()
+        a.grad = b.grad = alpha.grad = None
+        loss.backward()
+        with torch.no_grad():
+            for name, prm in net.named_parameters():
+                prm.data = pd_step(prm.data, prm.grad.data, net0[name], lr, gamma)
+            na, nb, nal = scalar_update(float(a), float(b), float(alpha), float(a.grad), float(b.grad),
+                                        float(alpha.grad), float(a0), float(b0), float(alpha0), lr, gamma)
+            a.data.fill_(float(na))
+            b.data.fill_(float(nb))
+            alpha.data.fill_(float(nal))
+        losses.append(float(loss.detach()))
+    return losses, (float(a), float(b), float(alpha))

@@ -33,6 +33,44 @@ def test_bench_self_launches_two_ranks():
     assert out["auc_eval"]["methods_agree"] and out["auc_eval"]["P"] > 0
 
 
+@pytest.mark.timeout(900)
+def test_bench_full_two_ranks_gloo(tmp_path):
+    """Every leg the driver's N > 1 run takes, at reduced sizes, as 2 gloo ranks on cuda:0 (VERDICT
+    r03 #2): training + the period sweep, coda_round, the split in-training evaluation, the
+    configs[0] GPU leg, both exact-AUC legs (sharded sort method and pair count), the loss kernel
+    leg and the CPU baselines. One JSON line on stdout, world size 2."""
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    cmd = [sys.executable, str(REPO / "bench.py"), "--gpus", "2", "--backend", "gloo",
+           "--arch", "resnet18", "--batch", "32", "--image-size", "64", "--steps", "4", "--warmup", "2",
+           "--sweep-I", "1,2", "--sweep-steps", "2", "--eval-images", "256", "--r18-steps", "8",
+           "--auc-log2n", "20", "--auc2-log2n", "21", "--auc-reps", "1", "--auc-shard-min", "0", "--sur-log2b", "16", "--sur-reps", "5",
+           "--cpu-workers", "2", "--cpu-steps", "2", "--cpu-sklearn-full", "0"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=840)
+    (tmp_path / "stderr.log").write_text(r.stderr)
+    assert r.returncode == 0, r.stderr[-4000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout[-3000:]
+    out = json.loads(lines[0])
+    out_dir = os.environ.get("DAUC_BENCH_RECORD_DIR")
+    if out_dir:  # the GPU runner keeps the line (profiles/r04/)
+        Path(out_dir).mkdir(parents=True, exist_ok=True)
+        (Path(out_dir) / "bench_n2_gloo_full.json").write_text(lines[0] + "\n")
+    assert out["n_gpus"] == 2 and out["process_group"]["world_size"] == 2
+    assert out["value"] > 0 and out["config"]["parallelism"] == "dp2"
+    assert out["coda_round"]["ms_per_round"] > 0
+    te = out["training_eval"]
+    assert te["method"] == "split" and 0.0 <= te["auc"] <= 1.0 and "auc_rank0_scoring" in te
+    assert [rec["I"] for rec in out["period_sweep"]["records"]] == [1, 2]
+    for k in ("auc_eval", "auc_eval_extreme"):
+        assert out[k]["methods_agree"] and out[k]["sort_mode"] == "sharded"
+    assert out["auc_eval_extreme"]["cpu_baseline"]["oracle_counts"]["match"]
+    assert out["configs0"]["gpu"]["n_gpus"] == 2 and out["configs0"]["cpu"]["params_finite"]
+    assert out["surrogate_kernel"]["roofline"]["achieved"] > 0
+    assert out["cpu_baseline"]["value"] > 0
+
+
 @pytest.mark.timeout(300)
 def test_bench_refuses_rccl_with_fewer_gpus_than_ranks():
     import torch
