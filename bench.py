@@ -400,10 +400,10 @@ def bench_auc(args, world, rank, device, log2n=None, pos=None, pair_reps=None):
     # the sort method: the whole evaluation on one GPU (or below SHARD_MIN) is ONE blocking C call,
     # dauc_auc_eval_counts; over ranks each enqueues its part with no host synchronisation
     # (dauc_auc_eval_enqueue), then one all-gather of the 8-word records and one host read
-    sort_fn = ("dauc_auc_eval_counts" if world == 1 or n < ExactAUC.SHARD_MIN
-               else "dauc_auc_eval_enqueue")
+    shard_min = ExactAUC.SHARD_MIN if args.auc_shard_min is None else args.auc_shard_min
+    sort_fn = "dauc_auc_eval_counts" if world == 1 or n < shard_min else "dauc_auc_eval_enqueue"
     for method, fn in (("sort", sort_fn), ("pairs", "dauc_pair_count")):
-        ev = ExactAUC(world=world, rank=rank, variant=args.variant, method=method)
+        ev = ExactAUC(world=world, rank=rank, variant=args.variant, method=method, shard_min=shard_min)
         kt = KernelTimer(_lib.load(), fn)
         cold = None
         if method == "sort":

@@ -25,7 +25,7 @@
 #include <hip/hip_runtime.h>
 
 #include "dauc.h"
-#include "dauc_internal.h"
+#include "count_index.h"
 
 namespace dauc {
 namespace {
@@ -48,7 +48,8 @@ struct EvalWs {
     int64_t* split_stats;         // [4]   the split's stats (sorted fallback)
     void* sws;                    // split workspace
     void* tws;                    // sort + tree + count-index workspace (a table of at most n/2 keys)
-    size_t sws_bytes, tws_bytes;
+    void* bws;                    // the bucketed count's (auc_bucket.hip): the split queries, tile runs
+    size_t sws_bytes, tws_bytes, bws_bytes;
 };
 
 EvalWs eval_ws(void* ws, int64_t n) {
@@ -69,12 +70,15 @@ EvalWs eval_ws(void* ws, int64_t n) {
     p += align256(w.sws_bytes);
     w.tws_bytes = dauc_sort_workspace_size(n / 2 + 1);
     w.tws = p;
+    p += align256(w.tws_bytes);
+    w.bws_bytes = bucket_workspace_size(n);
+    w.bws = p;
     return w;
 }
 
 size_t eval_ws_bytes(int64_t n) {
     return kHdr + align256(size_t(n) * 4) + align256(size_t(n / 2 + 1) * 4) + align256(dauc_split_workspace_size(n)) +
-           align256(dauc_sort_workspace_size(n / 2 + 1));
+           align256(dauc_sort_workspace_size(n / 2 + 1)) + align256(bucket_workspace_size(n));
 }
 
 bool valid_args(const float* scores, const void* labels, int label_dtype, int64_t n, int part, int parts,
@@ -102,8 +106,15 @@ int enqueue(const float* scores, const void* labels, int label_dtype, int64_t n,
         // a tuning build forcing another search structure: straight to the sorted path
         return -static_cast<int>(hipMemsetAsync(w.verdict, 2, 1, st));
     }
+#if defined(DAUC_BUCKETED) && DAUC_BUCKETED
+    DirectIndex ix{};
+    if ((rc = build_direct_index(w.pos, w.slot, mcap, w.tws, w.tws_bytes, st, &ix))) return rc;
+    return counts_bucketed(ix, w.slot, scores, labels, label_dtype, qlo, qhi, w.wt, w.wt + 2, w.verdict, w.bws,
+                           w.bws_bytes, st);
+#else
     return counts_labeled_direct(w.pos, w.slot, mcap, scores, labels, label_dtype, qlo, qhi, w.wt, w.wt + 2,
                                  w.verdict, w.tws, w.tws_bytes, st);
+#endif
 }
 
 // The sorted path for a verdict-2 evaluation (P, N known): counts of part `part` into w.wt.
@@ -175,7 +186,7 @@ int counts_part_blocking(const float* scores, const void* labels, int label_dtyp
     out[3] = N;
     out[4] = nonfinite;
     out[5] = other;
-    out[6] = need ? pinned[2] : 0;
+    out[6] = pinned[2];  // non-finite queried scores: counted whatever the verdict, one class included
     return DAUC_OK;
 }
 

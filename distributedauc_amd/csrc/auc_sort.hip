@@ -29,7 +29,7 @@
 
 #include <type_traits>
 
-#include "dauc_internal.h"
+#include "count_index.h"
 
 namespace dauc {
 namespace {
@@ -255,7 +255,6 @@ __global__ __launch_bounds__(kSortThreads) void radix_scatter_kernel(const void*
 constexpr int kMaxSplit = DAUC_QUERY_MAX_SPLIT;
 constexpr size_t kTreeBytes = (size_t(kMaxSplit) + 64) * 4;  // nodes of 4 keys + per-level padding nodes
 constexpr int kQueryThreads = 1024;
-constexpr unsigned kPadKey = 0xffffffffu;  // above every finite score's key (max 0xff7fffff)
 
 // The S splitters are the in-order keys of a perfect 5-ary search tree of height H (5^(H-1) <= S
 // + 1 <= 5^H): a node is 4 keys (16 B, one ds_read_b128) and routes a query to child
@@ -818,37 +817,6 @@ __global__ __launch_bounds__(kQueryThreads) void query_count_kernel(const float*
     }
 }
 
-// One float4 slot's 4 labels as loaded (int8: ONE 32-bit word, unpacked where used, so the
-// next iteration's prefetched labels cost 1 VGPR per slot instead of 4)
-template <typename LT>
-struct LabelWords {
-    LT v[4];
-    __device__ __forceinline__ void load(const LT* p) {
-        if constexpr (sizeof(LT) == 4) {
-            const int4 c = *reinterpret_cast<const int4*>(p);
-            v[0] = c.x;
-            v[1] = c.y;
-            v[2] = c.z;
-            v[3] = c.w;
-        } else {
-            const longlong2 c0 = reinterpret_cast<const longlong2*>(p)[0];
-            const longlong2 c1 = reinterpret_cast<const longlong2*>(p)[1];
-            v[0] = c0.x;
-            v[1] = c0.y;
-            v[2] = c1.x;
-            v[3] = c1.y;
-        }
-    }
-    __device__ __forceinline__ void set_positive() { v[0] = v[1] = v[2] = v[3] = LT(1); }
-    __device__ __forceinline__ bool not_positive(int q) const { return v[q] != LT(1); }
-};
-template <>
-struct LabelWords<int8_t> {
-    unsigned w;
-    __device__ __forceinline__ void load(const int8_t* p) { w = *reinterpret_cast<const unsigned*>(p); }
-    __device__ __forceinline__ void set_positive() { w = 0x01010101u; }
-    __device__ __forceinline__ bool not_positive(int q) const { return ((w >> (8 * q)) & 0xffu) != 1u; }
-};
 
 // Labeled queries: the negatives are not materialised. Elements [begin, end) of the full score
 // and label arrays are streamed (float4 + 4 labels per slot); every element whose label is
@@ -932,22 +900,6 @@ __device__ __forceinline__ bool cells_in_use(const unsigned* __restrict__ meta, 
 // totals); op is min or +, v the thread's value
 #endif
 
-template <bool MIN>
-__device__ __forceinline__ unsigned block_incl_scan1024(unsigned v, unsigned* wtot) {
-    const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
-    unsigned incl = v;
-#pragma unroll
-    for (int off = 1; off < kWave; off <<= 1) {
-        const unsigned t = __shfl_up(incl, off, kWave);
-        if (lane >= off) incl = MIN ? (t < incl ? t : incl) : incl + t;
-    }
-    if (lane == kWave - 1) wtot[wid] = incl;
-    __syncthreads();
-    unsigned before = MIN ? ~0u : 0u;
-    for (int w = 0; w < wid; ++w) before = MIN ? (wtot[w] < before ? wtot[w] : before) : before + wtot[w];
-    __syncthreads();
-    return MIN ? (before < incl ? before : incl) : before + incl;
-}
 
 // One workgroup: per top bucket the first table index (every key compared with its
 // predecessor), the bucket sizes n_t (suffix minimum of the first indices), the smallest
@@ -1357,15 +1309,8 @@ __global__ __launch_bounds__(kQueryThreads) void query_cells_kernel(const float*
 // The builder keeps the tree (a device word both query kernels read) when the table needs more
 // than 1.5 keys per cell or a cell holds 15 or more keys (a nibble): clustered or tie-heavy
 // tables, for which the tree's cost does not depend on the key distribution.
-constexpr int kCiTopBits = 11;
-constexpr int kCiTop = 1 << kCiTopBits;
-constexpr int kCiLowBits = 32 - kCiTopBits;
-constexpr int kCiBlock = 8;                                    // cells per block word
-constexpr int kCiMaxBlocks = 18320;                            // LDS: 16 KB + 8 B per block + 384 B < 160 KB
-constexpr int kCiMaxCells = kCiMaxBlocks * kCiBlock - 1;       // + the virtual cell past the last
+
 constexpr int kCiPlanThreads = 1024;
-// meta words (after the cell-slot index's): [8] usable, [9] cells, [10] blocks, [11] skewed
-constexpr int kCiOk = 8, kCiCells = 9, kCiBlocks = 10, kCiSkew = 11;
 
 struct CountWs {
     unsigned* meta;    // [16]
@@ -1378,38 +1323,7 @@ struct CountWs {
 constexpr size_t kCountBytes = 256 + 3 * size_t(kCiTop) * 4 + ((size_t(kCiMaxCells) + 2) * 4 + 255) / 256 * 256 +
                                size_t(kCiMaxBlocks) * 8 + 256;
 
-__device__ __forceinline__ unsigned ci_cell(unsigned key, uint2 e) { return e.x + __umulhi(key << kCiTopBits, e.y); }
 
-__device__ __forceinline__ bool count_index_in_use(const unsigned* __restrict__ meta) {
-    return meta[kCiOk] != 0u && meta[kCiSkew] == 0u;
-}
-
-// the direct build (below): workgroup size, and groups of 256 block words whose prefixes the
-// consumers add (group_prefix)
-constexpr int kDirectThreads = 256;
-constexpr int kDirectGroup = 256;
-constexpr int kDirectMaxGroups = (kCiMaxBlocks + kDirectGroup - 1) / kDirectGroup;  // 72
-static_assert(kDirectMaxGroups <= 2 * kWave, "group_prefix handles up to 128 groups");
-
-// wave 0 of the calling workgroup: pre[g] = sum of grp[0 .. g) for g < kDirectMaxGroups
-// (groups >= ng count nothing)
-__device__ __forceinline__ void group_prefix(const unsigned* __restrict__ grp, int ng, unsigned* pre) {
-    if (threadIdx.x >= kWave) return;
-    const int lane = threadIdx.x;
-    const unsigned v0 = lane < ng ? grp[lane] : 0u, v1 = lane + kWave < ng ? grp[lane + kWave] : 0u;
-    unsigned i0 = v0, i1 = v1;
-#pragma unroll
-    for (int off = 1; off < kWave; off <<= 1) {
-        const unsigned t0 = __shfl_up(i0, off, kWave), t1 = __shfl_up(i1, off, kWave);
-        if (lane >= off) {
-            i0 += t0;
-            i1 += t1;
-        }
-    }
-    const unsigned tot0 = __shfl(i0, kWave - 1, kWave);
-    if (lane < kDirectMaxGroups) pre[lane] = i0 - v0;
-    if (lane + kWave < kDirectMaxGroups) pre[lane + kWave] = tot0 + i1 - v1;
-}
 
 // first[t] = the first table index of top bucket t, for the buckets holding keys (first[] was set
 // to M by build_tree_kernel)
@@ -1540,11 +1454,6 @@ __device__ __forceinline__ uint4 win_load(const unsigned* p) {
     return *reinterpret_cast<const uint4*>(p);
 }
 
-// the order-preserving key (-0 -> +0 by adding +0)
-__device__ __forceinline__ unsigned key_fast(float f) {
-    const unsigned u = __float_as_uint(f + 0.0f);
-    return u ^ (static_cast<unsigned>(static_cast<int>(u) >> 31) | 0x80000000u);
-}
 
 // Phase 1 of one query: cell, rank_lo, count and (lanes with cnt > 0) the window load
 #ifndef DAUC_CI_ABLATE
@@ -2405,7 +2314,7 @@ __global__ __launch_bounds__(kDirectThreads) void direct_scatter_kernel(const fl
                                                                         const unsigned long long* __restrict__ Mp,
                                                                         const uint2* __restrict__ blk,
                                                                         const unsigned* __restrict__ grp,
-                                                                        const unsigned* __restrict__ meta,
+                                                                        unsigned* __restrict__ meta,
                                                                         unsigned* __restrict__ cnt,
                                                                         const unsigned* __restrict__ cell,
                                                                         unsigned* __restrict__ table) {
@@ -2416,16 +2325,35 @@ __global__ __launch_bounds__(kDirectThreads) void direct_scatter_kernel(const fl
     __syncthreads();
     const int64_t gid = int64_t(blockIdx.x) * kDirectThreads + threadIdx.x;
     if (gid < 16) table[M + gid] = kPadKey;
+    // Every index is checked before it is used (a producer bug must become a verdict-2 fallback,
+    // never an out-of-bounds store): the cell must be one of the plan's, and its counter must still
+    // hold a slot (the count pass counted exactly this many keys into it). A failed check marks the
+    // index skewed, so the query passes return at once and the caller takes the sorted path.
+    const unsigned ncells = meta[kCiCells];
+    bool bad = false;
     for (int64_t i = gid; i < M; i += int64_t(gridDim.x) * kDirectThreads) {
         const unsigned x = key_fast(pos[i]);
         const unsigned c = cell[i];
+        if (c >= ncells) {
+            bad = true;
+            continue;
+        }
         const unsigned bi = c / kCiBlock;
-        const uint2 b = blk[bi];
-        const unsigned below = __builtin_amdgcn_ubfe(b.y, 0u, 4u * (c % kCiBlock));
-        const unsigned bytes = (below & 0x0f0f0f0fu) + ((below >> 4) & 0x0f0f0f0fu);
-        const unsigned slot = atomicSub(cnt + c, 1u) - 1u;
-        table[pre[bi / kDirectGroup] + b.x + __builtin_amdgcn_sad_u8(bytes, 0u, 0u) + slot] = x;
+        unsigned rl, ccount;
+        ci_decode(c, blk[bi], rl, ccount);
+        const unsigned left = atomicSub(cnt + c, 1u);  // slots of the cell not yet taken, before this one
+        if (left == 0u || left > ccount) {
+            bad = true;
+            continue;
+        }
+        const unsigned pos_in_table = pre[bi / kDirectGroup] + rl + (left - 1u);
+        if (pos_in_table >= static_cast<unsigned>(M)) {
+            bad = true;
+            continue;
+        }
+        table[pos_in_table] = x;
     }
+    if (__ballot(bad) != 0ull && (threadIdx.x & (kWave - 1)) == 0) atomicOr(meta + kCiSkew, 1u);
 }
 
 // Every queried score is also checked to be finite (sklearn rejects NaN / inf scores,
@@ -2840,15 +2768,10 @@ int64_t direct_hist_offset(int64_t Mcap) {  // carve_count(...).first, relative 
                    ((kCellBytes + 255) / 256) * 256 + 256);
 }
 
-int counts_labeled_direct(const float* pos, const unsigned long long* Mp, int64_t Mcap, const float* scores,
-                          const void* labels, int label_dtype, int64_t begin, int64_t end,
-                          unsigned long long* wins_ties, unsigned long long* nonfinite, unsigned* verdict,
-                          void* workspace, size_t workspace_bytes, hipStream_t st) {
-    if (pos == nullptr || Mp == nullptr || Mcap < 1 || begin < 0 || end < begin || wins_ties == nullptr ||
-        (end > begin && (scores == nullptr || labels == nullptr)) || workspace == nullptr ||
+int build_direct_index(const float* pos, const unsigned long long* Mp, int64_t Mcap, void* workspace,
+                       size_t workspace_bytes, hipStream_t st, DirectIndex* ix) {
+    if (pos == nullptr || Mp == nullptr || Mcap < 1 || workspace == nullptr || ix == nullptr ||
         workspace_bytes < dauc_sort_workspace_size(Mcap))
-        return DAUC_EINVAL;
-    if (label_dtype != DAUC_LABEL_I8 && label_dtype != DAUC_LABEL_I32 && label_dtype != DAUC_LABEL_I64)
         return DAUC_EINVAL;
     const SortWs w = carve(workspace, Mcap);
     const CountWs nw = count_ws_of(workspace, Mcap);
@@ -2868,18 +2791,32 @@ int counts_labeled_direct(const float* pos, const unsigned long long* Mp, int64_
                        nw.blk, grp);
     hipLaunchKernelGGL(direct_scatter_kernel, blocks(Mcap, kDirectThreads, 1024), dim3(kDirectThreads), 0, st, pos,
                        Mp, nw.blk, grp, nw.meta, nw.cstart, w.keys_b, table);
-    int rc = launch_status();
+    *ix = DirectIndex{table, nw.l1, nw.blk, grp, nw.meta};
+    return launch_status();
+}
+
+int counts_labeled_direct(const float* pos, const unsigned long long* Mp, int64_t Mcap, const float* scores,
+                          const void* labels, int label_dtype, int64_t begin, int64_t end,
+                          unsigned long long* wins_ties, unsigned long long* nonfinite, unsigned* verdict,
+                          void* workspace, size_t workspace_bytes, hipStream_t st) {
+    if (begin < 0 || end < begin || wins_ties == nullptr || (end > begin && (scores == nullptr || labels == nullptr)))
+        return DAUC_EINVAL;
+    if (label_dtype != DAUC_LABEL_I8 && label_dtype != DAUC_LABEL_I32 && label_dtype != DAUC_LABEL_I64)
+        return DAUC_EINVAL;
+    DirectIndex ix{};
+    int rc = build_direct_index(pos, Mp, Mcap, workspace, workspace_bytes, st, &ix);
     if (rc || end == begin) return rc;
+    const CountWs nw = count_ws_of(workspace, Mcap);
     switch (label_dtype) {
         case DAUC_LABEL_I8:
-            return launch_ci(scores, static_cast<const int8_t*>(labels), begin, end, nw, table, 0, wins_ties,
-                             nonfinite, st, verdict, grp, Mp);
+            return launch_ci(scores, static_cast<const int8_t*>(labels), begin, end, nw, ix.table, 0, wins_ties,
+                             nonfinite, st, verdict, ix.grp, Mp);
         case DAUC_LABEL_I32:
-            return launch_ci(scores, static_cast<const int32_t*>(labels), begin, end, nw, table, 0, wins_ties,
-                             nonfinite, st, verdict, grp, Mp);
+            return launch_ci(scores, static_cast<const int32_t*>(labels), begin, end, nw, ix.table, 0, wins_ties,
+                             nonfinite, st, verdict, ix.grp, Mp);
         default:
-            return launch_ci(scores, static_cast<const int64_t*>(labels), begin, end, nw, table, 0, wins_ties,
-                             nonfinite, st, verdict, grp, Mp);
+            return launch_ci(scores, static_cast<const int64_t*>(labels), begin, end, nw, ix.table, 0, wins_ties,
+                             nonfinite, st, verdict, ix.grp, Mp);
     }
 }
 

@@ -123,6 +123,19 @@ bool direct_enabled();  // the search mode is automatic (always, except in a tun
 int64_t direct_capacity(int64_t n);
 int64_t direct_hist_offset(int64_t Mcap);  // byte offset of `hist` in the sort workspace
 int direct_hist_words();
+struct DirectIndex;  // count_index.h
+// the direct build alone (4 launches): fills *ix with the index's device pointers
+int build_direct_index(const float* pos, const unsigned long long* Mp, int64_t Mcap, void* workspace,
+                       size_t workspace_bytes, hipStream_t st, DirectIndex* ix);
+// auc_bucket.hip: the labeled queries [begin, end) counted through the direct index by range
+// (split + count passes); workspace of bucket_workspace_size(end - begin) bytes, 256-B aligned.
+// *verdict = 1 (counted) or 2 (the index cannot hold the table: the caller's sorted path);
+// nonfinite += the non-finite queried scores (also when the table is empty).
+size_t bucket_workspace_size(int64_t queries);
+int counts_bucketed(const DirectIndex& ix, const unsigned long long* Mp, const float* scores, const void* labels,
+                    int label_dtype, int64_t begin, int64_t end, unsigned long long* wins_ties,
+                    unsigned long long* nonfinite, unsigned* verdict, void* workspace, size_t workspace_bytes,
+                    hipStream_t st);
 int counts_labeled_direct(const float* pos, const unsigned long long* Mp, int64_t Mcap, const float* scores,
                           const void* labels, int label_dtype, int64_t begin, int64_t end,
                           unsigned long long* wins_ties, unsigned long long* nonfinite, unsigned* verdict,

@@ -711,6 +711,82 @@ def test_auc_eval_enqueue_records(dev):
     assert seen == [0, 0, 0, 1], seen
 
 
+@pytest.mark.parametrize("ldtype", [np.int8, np.int32, np.int64])
+def test_auc_eval_bucketed_ranges(dev, ldtype):
+    """The range-bucketed count (auc_bucket.hip: plan -> split -> prefix -> count) against the C
+    oracle where its bookkeeping is stressed: one range (few positives) and the most ranges the
+    index allows (~220 k positives, 18+ ranges); every query in ONE range (negatives packed into a
+    narrow interval: one range's runs carry all the work, many count chunks of one range); queries
+    in top buckets with no positive at all (their cell is the next used bucket's first); queries
+    below / above every positive; a misaligned score slice (scalar split path) and misaligned
+    labels; parts with ragged bounds (G = 3, 7)."""
+    from distributedauc_amd import ops
+
+    rng = np.random.default_rng(404)
+    n = 1_000_003
+    u = rng.random(n, dtype=np.float32)
+    cases = {
+        "one_range": (u, np.where(rng.random(n) < 0.002, 1, -1)),
+        "max_ranges": (u, np.where(rng.random(n) < 0.21, 1, -1)),
+        "queries_one_range": None,
+        "apart": None,
+        "outside": None,
+    }
+    y = np.where(rng.random(n) < 0.05, 1, -1)
+    s = np.where(y == 1, u, np.float32(0.6) + u * np.float32(1e-4)).astype(np.float32)
+    cases["queries_one_range"] = (s, y)
+    s = np.where(y == 1, np.float32(0.5) + u * np.float32(0.5), u * np.float32(1e-3)).astype(np.float32)
+    cases["apart"] = (s, y)  # negatives in top buckets with no positive
+    s = np.where(y == 1, np.float32(0.4) + u * np.float32(0.2), np.where(u < 0.5, -u, np.float32(1) + u))
+    cases["outside"] = (s.astype(np.float32), y)
+    for name, (s, y) in cases.items():
+        y = y.astype(ldtype)
+        e = coracle.auc_counts(y.astype(np.int64), s)
+        W, Tt, P, N, bad, other = ops.auc_eval_counts(T(s, dev), T(y, dev))
+        assert (W, Tt, P, N, bad, other) == (e["wins"], e["ties"], e["P"], e["N"], 0, 0), name
+        for G in (3, 7):
+            Wp = Tp = 0
+            for r in range(G):
+                out = torch.zeros(8, dtype=torch.int64, device=dev)
+                ops.auc_eval_enqueue(T(s, dev), T(y, dev), r, G, out=out)
+                v = out.cpu().tolist()
+                assert v[7] in (0, 1), (name, G, r, v)
+                Wp, Tp = Wp + v[0], Tp + v[1]
+            assert (Wp, Tp) == (e["wins"], e["ties"]), (name, G)
+    # misaligned slices: scores off by 1 element (4 B: the split's scalar path), labels by 1
+    s, y = cases["max_ranges"][0], cases["max_ranges"][1].astype(ldtype)
+    for so, yo in ((1, 0), (0, 1), (3, 2)):
+        sall = np.concatenate([np.zeros(so, np.float32), s])
+        yall = np.concatenate([np.zeros(yo, ldtype), y])
+        e = coracle.auc_counts(y.astype(np.int64), s)
+        W, Tt, P, N, bad, other = ops.auc_eval_counts(T(sall, dev)[so:], T(yall, dev)[yo:])
+        assert (W, Tt, P, N, bad) == (e["wins"], e["ties"], e["P"], e["N"], 0), (so, yo)
+
+
+def test_auc_one_class_rejects_nonfinite(dev):
+    """with one class empty, a non-finite score must still raise like sklearn
+    (roc_curve checks finiteness before its one-class warning), one GPU and sharded."""
+    from distributedauc_amd.auc import ExactAUC
+
+    n = 50_003
+    rng = np.random.default_rng(17)
+    for fill in (-1, 1):
+        s = rng.random(n, dtype=np.float32)
+        y = np.full(n, fill, np.int8)
+        s[n // 3] = np.nan
+        with pytest.raises(ValueError):
+            ExactAUC(method="sort")(T(y, dev), T(s, dev))
+        hits = 0
+        for r in range(3):
+            try:
+                ExactAUC(world=3, rank=r, reduce=False, method="sort", shard_min=0).counts(T(y, dev), T(s, dev))
+            except ValueError:
+                hits += 1
+        # a non-finite negative is seen by the part that queries it; a non-finite positive by the
+        # compaction, i.e. by every part that compacts it
+        assert hits >= 1, fill
+
+
 def test_auc_sort_rejects_nonfinite_negatives(dev):
     """The sort method never materialises the negatives: the query kernel's finiteness count
     must still reject a NaN / inf negative (sklearn _ranking.py:868-869), sharded or not."""
