@@ -398,10 +398,11 @@ def bench_auc(args, world, rank, device, log2n=None, pos=None, pair_reps=None):
     s, y = synthetic_scores(n, pos, device)  # same scores on every rank
     out = {"n": n, "log2n": log2n, "pos": pos}
     # the sort method: the whole evaluation on one GPU (or below SHARD_MIN) is ONE blocking C call,
-    # dauc_auc_eval_counts; over ranks each enqueues its part with no host synchronisation
-    # (dauc_auc_eval_enqueue), then one all-gather of the 8-word records and one host read
+    # dauc_auc_eval_counts; over ranks each compacts its slice of the labels
+    # (dauc_auc_eval_compact_part), one all-gather of the slots, each counts its query range
+    # (dauc_auc_eval_query_part, timed here), one all-gather of the records and one host read
     shard_min = ExactAUC.SHARD_MIN if args.auc_shard_min is None else args.auc_shard_min
-    sort_fn = "dauc_auc_eval_counts" if world == 1 or n < shard_min else "dauc_auc_eval_enqueue"
+    sort_fn = "dauc_auc_eval_counts" if world == 1 or n < shard_min else "dauc_auc_eval_query_part"
     for method, fn in (("sort", sort_fn), ("pairs", "dauc_pair_count")):
         ev = ExactAUC(world=world, rank=rank, variant=args.variant, method=method, shard_min=shard_min)
         kt = KernelTimer(_lib.load(), fn)
@@ -473,18 +474,18 @@ def auc_record(auc, world, config_name):
     npairs = auc["npairs"]
     pc_rate = npairs / pk["t_count"]
     n = auc["n"]
-    # the sort method's HBM floor: labels read once by the one-pass compaction (every rank
-    # compacts the whole vector), scores + labels once by the query pass over the rank's share (the
-    # positives' scores and the count index are ~0.1-1 % of that)
+    # the sort method's HBM floor: labels read once by the compaction, scores + labels once by the
+    # query pass, each over the rank's share when sharded (the positives' scores, the gathered
+    # slots and the count index are ~0.1-1 % of that)
     shard = world if sk["mode"] == "sharded" else 1
-    eval_bytes = n * 1 + n * (4 + 1) // shard
+    eval_bytes = n * 1 // shard + n * (4 + 1) // shard
     return {
         "workload": f"exact AUC, 2^{auc['log2n']} fp32 scores, {auc['pos']:.1%} positives "
                     f"(BASELINE {config_name}), {world} rank(s); sort method {sk['mode']} "
-                    "(sharded = every rank compacts all positives and builds the index itself, enqueues its "
-                    "score-index range with no host sync, one all-gather of the 8-word part records; replicated = "
-                    "every rank evaluates the whole vector, below 2^24 scores); pair count: positive blocks, int64 "
-                    "all-reduce",
+                    "(sharded = every rank compacts the positives of its slice of the labels, one all-gather of "
+                    "the slots, every rank builds the index from the gathered positives and counts its score-index "
+                    "range, one all-gather of the 8-word part records; replicated = every rank evaluates the whole "
+                    "vector, below 2^24 scores); pair count: positive blocks, int64 all-reduce",
         "sort_mode": sk["mode"],
         "pairs_per_sec": npairs / sk["t_eval"],
         "method": "sort (default evaluator: compact the positives reading labels only, build the LDS count index "
@@ -500,11 +501,12 @@ def auc_record(auc, world, config_name):
         "sort_count_what": f"HIP events around every {sk['count_fn']} call"
                            + (" (the whole one-call evaluation: compaction, index build, query, readback)"
                               if sk["count_fn"] == "dauc_auc_eval_counts" else
-                              " (this rank's enqueued part: compaction, index build, its query share, record copy)"),
+                              " (this rank's step 2: the gathered slots' table, index build, its query share, record "
+                              "copy; its slice's compaction and the two all-gathers are in eval_ms)"),
         "eval_roofline": {"bound": "hbm", "bytes_per_rank": eval_bytes,
                           "achieved": eval_bytes / sk["t_eval"] / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                           "frac": eval_bytes / sk["t_eval"] / 1e9 / HBM_PEAK_GBS,
-                          "note": "bytes = 1 label pass over all n + 1 score/label pass over this rank's query share"},
+                          "note": "bytes = 1 label pass + 1 score/label pass over this rank's share (all n at N=1)"},
         "query_kernel": load_profile("query_valu.json", f"2^{auc['log2n']}"),
         "P": auc["P"], "N": auc["N"], "wins": auc["wins"], "ties": auc["ties"], "auc": auc["auc"],
         "methods_agree": True,

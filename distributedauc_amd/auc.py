@@ -15,12 +15,14 @@ through an LDS search tree (O(M log M + L log M)).
 Sharding (north star): every rank holds the same score vector. The
 pair-count method gives rank r the positives [r*P/G, (r+1)*P/G) of the stable
 split against ALL negatives, then one int64 [3] all-reduce sums (W, T, non-finite);
-the sort method has every rank compact ALL the positives and build the count index
-from them itself (a labels-only pass: no collective builds the table), stream its
-index slice of the scores through the search with no host synchronisation, and
-all-gather the parts' 8-word records (one collective, one host read). The result
-does not depend on G. Every rank must pass the same vector: the gathered records
-are checked for that, and a mismatch raises on every rank together.
+the sort method has every rank compact the positives of its slice of the labels
+into a slot, all-gathers the slots (every rank then holds the whole positive
+table), builds the count index from them, counts its index slice of the scores,
+and all-gathers the parts' 8-word records (two collectives, one host read, no host
+synchronisation before the read). The result does not depend on G. The gathered
+records' label counts (P, non-finite positives, labels outside {-1, 1}) and
+verdicts must agree, and a mismatch raises on every rank together; the scores
+themselves are not compared across ranks.
 
 Error behaviour mirrors sklearn: non-finite scores raise ValueError; labels
 with more than two distinct values raise ValueError; a single class returns NaN
@@ -83,6 +85,7 @@ class ExactAUC:
         self.shard_min = self.SHARD_MIN if shard_min is None else int(shard_min)
         self.last_mode = None  # "single", "replicated" or "sharded" (the last call's)
         self._part_counts: dict = {}  # device -> int64 [8 (1 + world)]: this part's record + the gathered ones
+        self._slots: dict = {}        # (device, n) -> (this rank's slot, the gathered slots)
 
     def counts(self, label, scores, device=None) -> dict:
         """Exact {wins, ties, P, N} (Python ints). One host sync for the split sizes."""
@@ -135,12 +138,13 @@ class ExactAUC:
     def _counts_sort(self, y: torch.Tensor, s: torch.Tensor) -> dict:
         """The sort method. One GPU (or a vector below ``shard_min``, which every rank evaluates
         whole: same integers, no collective): ONE blocking C call (dauc_auc_eval_counts). Over
-        ranks: every rank enqueues its part (dauc_auc_eval_enqueue: it builds the table from ALL
-        the positives itself -- each rank holds the same scores -- and streams its index slice of
-        the scores through the search, with no host synchronisation), one all-gather of the
+        ranks: every rank compacts its slice of the labels into a slot (dauc_auc_eval_compact_part),
+        one all-gather of the slots, every rank builds the index from the gathered positives and
+        counts its index slice of the scores (dauc_auc_eval_query_part), one all-gather of the
         parts' 8-word records, and ONE host read of the gathered records: the counts are summed
-        on the host, and P, the non-finite / label checks and the verdict must agree on every rank
-        (ranks holding different vectors raise together instead of mixing counts)."""
+        on the host, and the label counts and the verdict must agree on every rank (ranks whose
+        label counts differ raise together instead of mixing counts; the scores are not compared).
+        With reduce=False each rank evaluates its part against all the positives itself."""
         if self.world == 1 or (self.reduce and s.numel() < self.shard_min):
             self.last_mode = "single" if self.world == 1 else "replicated"
             W, T, P, N, nonfinite, other = ops.auc_eval_counts(s, y)
@@ -154,10 +158,19 @@ class ExactAUC:
         if rec is None:
             rec = self._part_counts[s.device] = torch.zeros(8 * (self.world + 1), dtype=torch.int64, device=s.device)
         mine, gathered = rec[:8], rec[8:]
-        ops.auc_eval_enqueue(s, y, self.rank, self.world, out=mine)
         if not self.reduce:
+            # no collective: this rank's part with the table built from ALL the positives itself
+            ops.auc_eval_enqueue(s, y, self.rank, self.world, out=mine)
             vals = [mine.tolist()]
         else:
+            # each rank compacts only its slice of the labels; one all-gather of the slots gives
+            # every rank the whole positive table; each rank counts its query range; one
+            # all-gather of the 8-word records (no whole-vector pass per rank)
+            slots = self._slots_of(s.device, n)
+            nb = ops.auc_slot_bytes(n, self.world)
+            ops.auc_eval_compact_part(s, y, self.rank, self.world, slots[0])
+            dist.all_gather_into_tensor(slots[1], slots[0], group=self.group)
+            ops.auc_eval_query_part(s, y, self.rank, self.world, slots[1][: nb * self.world], out=mine)
             dist.all_gather_into_tensor(gathered, mine, group=self.group)
             vals = gathered.view(self.world, 8).tolist()  # the one host synchronisation
         shared = {(v[3], v[5], v[6]) for v in vals}
@@ -175,6 +188,18 @@ class ExactAUC:
         if verdicts == {2}:
             return self._counts_sort_sorted_path(y, s)
         return {"wins": sum(v[0] for v in vals), "ties": sum(v[1] for v in vals), "P": P, "N": N}
+
+    def _slots_of(self, device, n: int):
+        """(this rank's slot, the gathered slots) for n scores: uint8 device buffers, 256-byte
+        aligned (auc_slot_bytes(n, world) bytes per rank), cached per (device, n)."""
+        key = (device, n)
+        got = self._slots.get(key)
+        if got is None:
+            nb = ops.auc_slot_bytes(n, self.world)
+            # torch allocations are 256-byte aligned; nb is a multiple of 256
+            got = self._slots[key] = (torch.empty(nb, dtype=torch.uint8, device=device),
+                                      torch.empty(nb * self.world, dtype=torch.uint8, device=device))
+        return got
 
     def _counts_sort_sorted_path(self, y: torch.Tensor, s: torch.Tensor) -> dict:
         """A table the count index cannot hold (more than 219,838 positives, or clustered ones):

@@ -277,9 +277,6 @@ int launch_split(const float* s, const LT* lab, int64_t n, float* pos_out, float
 // tile0 + (k * 256 + t) * 16 + [0, 16) (each wave load instruction reads 1 KB contiguous at int8).
 
 constexpr int kCmpThreads = 256;
-#ifndef DAUC_COMPACT_WIDE_THREADS
-#define DAUC_COMPACT_WIDE_THREADS 256
-#endif
 constexpr int kCmpSlots = 8;
 constexpr int kCmpTile = kCmpThreads * 16 * kCmpSlots;  // 32768 labels per block
 
@@ -337,10 +334,9 @@ __device__ __forceinline__ unsigned label_masks16(const LT* __restrict__ lab, in
     return pos;
 }
 
-#ifndef DAUC_COMPACT_BATCH
-#define DAUC_COMPACT_BATCH 8  // > 0: the compactions load a tile's labels this many 16-B loads at a time
-                              // (0: one group per bounds-checked branch, round 2's form)
-#endif
+// the compactions load a tile's labels this many 16-B loads at a time (round 2's form, one group
+// per bounds-checked branch, waited out one memory latency per group; 4 and 16 measured equal / slower)
+constexpr int kCompactBatch = 8;
 
 // the positive mask and the labels outside {-1, 1} of 16 labels already in registers (the bounds-
 // and alignment-checked case of label_masks16)
@@ -398,7 +394,7 @@ __global__ __launch_bounds__(kCmpThreads) void compact_count_kernel(const LT* __
         for (int i = threadIdx.x; i < nzero_w; i += kCmpThreads) zero_w[i] = 0u;
     int np = 0, no = 0;
     unsigned m[kCmpSlots];
-    if (DAUC_COMPACT_BATCH && vec && base + kCmpTile <= n) {
+    if (vec && base + kCmpTile <= n) {
         // a tile wholly in range and aligned (uniform): every group's loads in straight-line code,
         // not one bounds-checked branch (and so one memory latency) per group
         constexpr int kPer = int(sizeof(LT));
@@ -547,7 +543,7 @@ __global__ __launch_bounds__(THREADS) void compact_unordered_kernel(
     const float* __restrict__ s, const LT* __restrict__ lab, int64_t n, int vec, float* __restrict__ pos_out,
     unsigned long long* __restrict__ stats, unsigned long long tag, unsigned long long* __restrict__ zero_next,
     unsigned long long next_tag, unsigned long long* __restrict__ zero3, unsigned* __restrict__ zero_w,
-    int nzero_w) {
+    int nzero_w, int64_t cap) {
     constexpr int kW = THREADS / kWave;
     constexpr int64_t kTileU = int64_t(THREADS) * 16 * SLOTS;
     __shared__ int wtot[2][kW];
@@ -564,16 +560,15 @@ __global__ __launch_bounds__(THREADS) void compact_unordered_kernel(
     const int64_t base = int64_t(blockIdx.x) * kTileU;
     int no = 0;
     int np = 0;
-#if DAUC_COMPACT_BATCH
     // label_masks16's bounds check is a branch per group, and a load consumed inside a branch is
     // waited for at once (vmcnt(0)): the groups' loads went out one memory latency apart. A tile
-    // wholly in range and aligned (uniform) issues them DAUC_COMPACT_BATCH at a time in straight-
+    // wholly in range and aligned (uniform) issues them kCompactBatch at a time in straight-
     // line code; the masks wait in LDS (16 bits per group) for the write phase, so no batch's
     // registers stay live across the next (a rolled loop: nothing hoisted past it)
     __shared__ unsigned short msk[SLOTS][THREADS];
     if (vec && base + kTileU <= n) {
         constexpr int kPer = int(sizeof(LT));  // 16-B loads per group
-        constexpr int kB = DAUC_COMPACT_BATCH / kPer > 0 ? DAUC_COMPACT_BATCH / kPer : 1;
+        constexpr int kB = kCompactBatch / kPer > 0 ? kCompactBatch / kPer : 1;
         constexpr int kBatch = kB < SLOTS ? kB : SLOTS;
         static_assert(SLOTS % kBatch == 0, "whole batches");
         const char* tb = reinterpret_cast<const char*>(lab + base);  // uniform
@@ -603,14 +598,6 @@ __global__ __launch_bounds__(THREADS) void compact_unordered_kernel(
             msk[k][threadIdx.x] = static_cast<unsigned short>(mm);
         }
     }
-#else
-    unsigned m[SLOTS];
-#pragma unroll
-    for (int k = 0; k < SLOTS; ++k)
-        m[k] = label_masks16(lab, base + (int64_t(k) * THREADS + threadIdx.x) * 16, n, vec, no);
-#pragma unroll
-    for (int k = 0; k < SLOTS; ++k) np += __popc(m[k]);
-#endif
     const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
     int incl = np;  // inclusive scan of the positives over the wave's lanes
 #pragma unroll
@@ -640,22 +627,15 @@ __global__ __launch_bounds__(THREADS) void compact_unordered_kernel(
     if (tile == 0) return;
     int64_t r = int64_t(base_s) + before + incl - np;
     int nf = 0;
-#if DAUC_COMPACT_BATCH
 #pragma unroll 1
-#else
-#pragma unroll
-#endif
     for (int k = 0; k < SLOTS; ++k) {
         const int64_t i = base + (int64_t(k) * THREADS + threadIdx.x) * 16;
-#if DAUC_COMPACT_BATCH
         const unsigned mk = msk[k][threadIdx.x];  // this thread's own word: no barrier needed
-#else
-        const unsigned mk = m[k];
-#endif
         for (unsigned b = mk; b != 0u; b &= b - 1u) {
             const float v = s[i + __ffs(b) - 1];
             nf += !isfinite(v);
-            pos_out[r++] = v;
+            if (r < cap) pos_out[r] = v;  // past `cap`: counted in stats[0], not stored (the caller's overflow)
+            ++r;
         }
     }
     if (nf) atomicAdd(stats + 2, static_cast<unsigned long long>(nf));
@@ -928,14 +908,14 @@ int compact_positives_zeroing(const float* scores, const void* labels, int label
 int compact_unordered(const float* scores, const void* labels, int label_dtype, int64_t n, float* pos_out,
                       unsigned long long* stats, unsigned long long tag, unsigned long long* zero_next,
                       unsigned long long next_tag, unsigned long long* zero3, unsigned* zero_w, int nzero_w,
-                      hipStream_t st) {
+                      hipStream_t st, int64_t cap) {
     if (n <= 0 || scores == nullptr || labels == nullptr || pos_out == nullptr || stats == nullptr ||
         zero_next == nullptr)
         return DAUC_EINVAL;
     const bool wide = n >= (int64_t(1) << 25);
     // wide inputs: 1024-thread workgroups of 32 label groups per thread (524,288-label tiles: 256
-    // reservations at 2^27 instead of 1024 on the one counter address) -- DAUC_COMPACT_WIDE_THREADS
-    constexpr int kWideThreads = DAUC_COMPACT_WIDE_THREADS;
+    // reservations at 2^27 instead of 1024 on the one counter address) -- 256
+    constexpr int kWideThreads = 256;
     const int threads = wide ? kWideThreads : kCmpThreads;
     const int64_t tile = int64_t(threads) * 16 * (wide ? 32 : kCmpSlots);
     const int64_t nblk = (n + tile - 1) / tile;
@@ -946,10 +926,10 @@ int compact_unordered(const float* scores, const void* labels, int label_dtype, 
         using LT = std::remove_const_t<std::remove_pointer_t<decltype(lab)>>;
         if (wide)
             hipLaunchKernelGGL((compact_unordered_kernel<LT, 32, kWideThreads>), grid, block, 0, st, scores, lab, n, vec,
-                               pos_out, stats, tag, zero_next, next_tag, zero3, zero_w, nzero_w);
+                               pos_out, stats, tag, zero_next, next_tag, zero3, zero_w, nzero_w, cap);
         else
             hipLaunchKernelGGL((compact_unordered_kernel<LT, kCmpSlots>), grid, block, 0, st, scores, lab, n, vec,
-                               pos_out, stats, tag, zero_next, next_tag, zero3, zero_w, nzero_w);
+                               pos_out, stats, tag, zero_next, next_tag, zero3, zero_w, nzero_w, cap);
         return launch_status();
     };
     switch (label_dtype) {

@@ -190,6 +190,80 @@ int counts_part_blocking(const float* scores, const void* labels, int label_dtyp
     return DAUC_OK;
 }
 
+// ---- the sharded evaluation in two steps: each rank compacts only its slice -----------------
+//
+// Step 1 (dauc_auc_eval_compact_part): rank r compacts the positives of ITS slice of the labels
+// into a slot: a 256-byte header {P_r, #non-finite positives, #labels outside {-1, 1}} (u64) and
+// room for `cap` scores. The caller all-gathers the slots (one collective). Step 2
+// (dauc_auc_eval_query_part): the gathered slots are concatenated into the evaluation's positive
+// table on the device (their headers summed), the count index is built from it and the rank's
+// query range is counted; the record is dauc_auc_eval_enqueue's. A slot holds an even share of
+// the index's capacity plus 25 %: a rank whose slice holds more positives (unshuffled test sets)
+// overflows, and the evaluation reports verdict 2 (the caller's blocking sorted path), as it does
+// for tables the index cannot hold.
+constexpr size_t kSlotHdr = 256;
+
+int64_t slot_cap(int64_t n, int parts) {
+    const int64_t share = (n + parts - 1) / parts;
+    const int64_t fair = (direct_capacity(n) + parts - 1) / parts;
+    const int64_t c = fair + fair / 4 + 64;
+    return share < c ? share : c;
+}
+
+size_t slot_bytes(int64_t n, int parts) { return kSlotHdr + align256(size_t(slot_cap(n, parts)) * 4); }
+
+// the slice of the labels rank `part` compacts: boundaries on 256-label multiples (int8 label
+// loads stay 16-byte aligned for every slice of an aligned array)
+int64_t slice_lo(int64_t n, int part, int parts) {
+    return part == 0 ? 0 : part >= parts ? n : ((n * part / parts) & ~int64_t(255));
+}
+
+// One workgroup per slot: the slot's keys to table[sum of the earlier slots' P, ...); workgroup 0
+// sums the headers into the evaluation's counters. m_eff = P, or (any slot overflowed) a size the
+// index refuses, so the build reports verdict 2.
+__global__ __launch_bounds__(256) void gather_slots_kernel(const unsigned char* __restrict__ slots, size_t sbytes,
+                                                           int parts, int64_t cap, int64_t mcap,
+                                                           float* __restrict__ table,
+                                                           unsigned long long* __restrict__ stats,
+                                                           unsigned long long* __restrict__ m_eff) {
+    __shared__ unsigned long long off_s;
+    auto hdr = [&](int r) { return reinterpret_cast<const unsigned long long*>(slots + size_t(r) * sbytes); };
+    if (threadIdx.x < kWave) {
+        // wave 0: the prefix of the slots' P before this one, and (workgroup 0) the totals
+        unsigned long long before = 0, P = 0, nf = 0, other = 0;
+        bool over = false;
+        for (int r = threadIdx.x; r < parts; r += kWave) {
+            const unsigned long long* h = hdr(r);
+            before += r < static_cast<int>(blockIdx.x) ? h[0] : 0ull;
+            P += h[0];
+            nf += h[2];
+            other += h[3];
+            over |= h[0] > static_cast<unsigned long long>(cap);
+        }
+        before = wave_sum(before);
+        P = wave_sum(P);
+        nf = wave_sum(nf);
+        other = wave_sum(other);
+        over = __ballot(over) != 0ull;
+        if (threadIdx.x == 0) {
+            off_s = before;
+            if (blockIdx.x == 0) {
+                stats[0] = P;
+                stats[1] = 0ull;
+                stats[2] = nf;
+                stats[3] = other;
+                *m_eff = over ? static_cast<unsigned long long>(mcap) + 1ull : P;
+            }
+        }
+    }
+    __syncthreads();
+    const unsigned long long Pr = hdr(blockIdx.x)[0];
+    const unsigned long long off = off_s;
+    if (Pr > static_cast<unsigned long long>(cap) || off + Pr > static_cast<unsigned long long>(mcap)) return;
+    const float* src = reinterpret_cast<const float*>(slots + size_t(blockIdx.x) * sbytes + kSlotHdr);
+    for (unsigned long long i = threadIdx.x; i < Pr; i += 256) table[off + i] = src[i];
+}
+
 }  // namespace
 }  // namespace dauc
 
@@ -207,6 +281,54 @@ int dauc_auc_eval_enqueue(const float* scores, const void* labels, int label_dty
     const EvalWs w = eval_ws(workspace, n);
     const int rc = enqueue(scores, labels, label_dtype, n, part, parts, w, st);
     if (rc) return rc;
+    return -static_cast<int>(hipMemcpyAsync(part_out, w.wt, kRecord, hipMemcpyDeviceToDevice, st));
+}
+
+size_t dauc_auc_slot_bytes(int64_t n, int parts) { return n < 1 || parts < 1 ? 0 : slot_bytes(n, parts); }
+
+int dauc_auc_eval_compact_part(const float* scores, const void* labels, int label_dtype, int64_t n, int part,
+                               int parts, void* slot, void* workspace, size_t workspace_bytes, dauc_stream_t stream) {
+    if (slot == nullptr || (reinterpret_cast<uintptr_t>(slot) & 255u) != 0 ||
+        !valid_args(scores, labels, label_dtype, n, part, parts, workspace, workspace_bytes))
+        return DAUC_EINVAL;
+    hipStream_t st = as_hip(stream);
+    const EvalWs w = eval_ws(workspace, n);
+    auto* hdr = static_cast<unsigned long long*>(slot);
+    hipError_t e;
+    if ((e = hipMemsetAsync(hdr, 0, 32, st)) != hipSuccess) return -static_cast<int>(e);
+    const int64_t lo = slice_lo(n, part, parts), hi = slice_lo(n, part + 1, parts);
+    if (hi <= lo) return DAUC_OK;  // an empty slice: P_r = 0
+    const size_t lsz = label_dtype == DAUC_LABEL_I8 ? 1 : label_dtype == DAUC_LABEL_I32 ? 4 : 8;
+    return compact_unordered(scores + lo, static_cast<const char*>(labels) + size_t(lo) * lsz, label_dtype, hi - lo,
+                             reinterpret_cast<float*>(static_cast<char*>(slot) + kSlotHdr), hdr, 0ull, w.spare, 0ull,
+                             nullptr, nullptr, 0, st, slot_cap(n, parts));
+}
+
+int dauc_auc_eval_query_part(const float* scores, const void* labels, int label_dtype, int64_t n, int part, int parts,
+                             const void* slots, int64_t* part_out, void* workspace, size_t workspace_bytes,
+                             dauc_stream_t stream) {
+    if (slots == nullptr || part_out == nullptr || (reinterpret_cast<uintptr_t>(slots) & 255u) != 0 ||
+        !valid_args(scores, labels, label_dtype, n, part, parts, workspace, workspace_bytes))
+        return DAUC_EINVAL;
+    hipStream_t st = as_hip(stream);
+    const EvalWs w = eval_ws(workspace, n);
+    hipError_t e;
+    if ((e = hipMemsetAsync(w.wt, 0, kZeroed, st)) != hipSuccess) return -static_cast<int>(e);
+    const int64_t mcap = direct_capacity(n);
+    unsigned* hist = reinterpret_cast<unsigned*>(static_cast<char*>(w.tws) + direct_hist_offset(mcap));
+    if ((e = hipMemsetAsync(hist, 0, size_t(direct_hist_words()) * 4, st)) != hipSuccess) return -static_cast<int>(e);
+    hipLaunchKernelGGL(gather_slots_kernel, dim3(static_cast<unsigned>(parts)), dim3(256), 0, st,
+                       static_cast<const unsigned char*>(slots), slot_bytes(n, parts), parts, slot_cap(n, parts), mcap,
+                       w.pos, w.slot, w.spare);
+    int rc = launch_status();
+    if (rc) return rc;
+    const int64_t qlo = n * part / parts, qhi = n * (part + 1) / parts;
+    if (qhi > qlo) {
+        // the build and the query see m_eff (w.spare[0]): P, or past the index's capacity on overflow
+        rc = counts_labeled_direct(w.pos, w.spare, mcap, scores, labels, label_dtype, qlo, qhi, w.wt, w.wt + 2,
+                                   w.verdict, w.tws, w.tws_bytes, st);
+        if (rc) return rc;
+    }
     return -static_cast<int>(hipMemcpyAsync(part_out, w.wt, kRecord, hipMemcpyDeviceToDevice, st));
 }
 

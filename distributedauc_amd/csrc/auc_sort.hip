@@ -35,10 +35,7 @@ namespace dauc {
 namespace {
 
 constexpr int kSortThreads = 256;
-#ifndef DAUC_SORT_PER_THREAD
-#define DAUC_SORT_PER_THREAD 8
-#endif
-constexpr int kPerThread = DAUC_SORT_PER_THREAD;  // keys per thread per pass tile
+constexpr int kPerThread = 8;  // keys per thread per pass tile
 constexpr int kTile = kSortThreads * kPerThread;  // 2048 keys (8 per thread: the hist pass 4.9 vs 6.1 us at 134k keys)
 constexpr int kRadix = 256;
 constexpr int kScanBlock = 1024;
@@ -237,22 +234,10 @@ __global__ __launch_bounds__(kSortThreads) void radix_scatter_kernel(const void*
 
 // ---- search ---------------------------------------------------------------------------
 
-#ifndef DAUC_QUERY_MAX_SPLIT
-#define DAUC_QUERY_MAX_SPLIT 40000
-#endif
-#ifndef DAUC_QUERY_BLOCKS_PER_CU
-#define DAUC_QUERY_BLOCKS_PER_CU 1
-#endif
-#ifndef DAUC_ABLATE
-#define DAUC_ABLATE 0  // timing ablations only (wrong counts): 1 = no bucket load, 2 = no tree walk
-#endif
-#ifndef DAUC_QUERY_LOCKSTEP
-#define DAUC_QUERY_LOCKSTEP 0  // 0: by bucket size (lockstep_queries), else 1 / 2 / 4 keys in lockstep
-#endif
 // Splitters (every k-th sorted key, k a power of two) kept in LDS: at most kMaxSplit of them
 // (4 B each: 40000 -> 156 KB of the CU's 160 KB), so a bucket holds k <= 4 keys -- ONE 16-byte
 // load -- up to M = 160,000 table keys (2^27 scores at 0.1 % positives: M = 134,447 -> k = 4).
-constexpr int kMaxSplit = DAUC_QUERY_MAX_SPLIT;
+constexpr int kMaxSplit = 40000;
 constexpr size_t kTreeBytes = (size_t(kMaxSplit) + 64) * 4;  // nodes of 4 keys + per-level padding nodes
 constexpr int kQueryThreads = 1024;
 
@@ -264,15 +249,11 @@ constexpr int kQueryThreads = 1024;
 // stored level after level and followed by ONE all-padding node: a walk at position p of level
 // d reads node off_d + min(p, n_d), and p <- 5p + #(node keys <= x); after H levels p =
 // #splitters <= x. The sorted table is padded with kPadKey to a whole number of buckets.
-#ifndef DAUC_TREE_ARITY
-#define DAUC_TREE_ARITY 5
-#endif
-constexpr int kTreeArity = DAUC_TREE_ARITY;      // 3: 2-key nodes (ds_read_b64), 5: 4-key nodes (ds_read_b128)
-static_assert(kTreeArity == 3 || kTreeArity == 5, "tree nodes are 8 or 16 bytes");
+constexpr int kTreeArity = 5;  // 4-key nodes, one ds_read_b128 (3-ary 8-byte nodes measured the same)
 constexpr int kNodeKeys = kTreeArity - 1;
-constexpr int kMaxTreeH = kTreeArity == 5 ? 7 : 10;  // 5^7 - 1, 3^10 - 1 >= kMaxSplit
-static_assert(kMaxSplit <= (kTreeArity == 5 ? 78124 : 59048), "tree height bound");
-typedef typename std::conditional<kTreeArity == 5, uint4, uint2>::type TreeNode;
+constexpr int kMaxTreeH = 7;  // 5^7 - 1 >= kMaxSplit
+static_assert(kMaxSplit <= 78124, "tree height bound");
+typedef uint4 TreeNode;
 
 struct TreeGeom {
     int S, H;
@@ -281,18 +262,8 @@ struct TreeGeom {
     int nodes;           // total stored nodes (incl. the per-level padding nodes)
 };
 
-// The top levels of the tree as wave-uniform registers (SGPRs): level 0 (4 keys) or levels 0-1
-// (the 24 splitters of the first two levels — #(those <= x) is the position after two levels).
-// Each level held here is one dependent LDS read fewer per query; 24 uniform compares cost more
-// VALU than two node reads, so which is faster is measured (DAUC_TREE_TOP_LEVELS 0 / 1 / 2).
-#ifndef DAUC_TREE_TOP_LEVELS
-#define DAUC_TREE_TOP_LEVELS 0
-#endif
-constexpr int kTopLevels = kTreeArity == 5 ? DAUC_TREE_TOP_LEVELS : 0;
-constexpr int kTopKeys = kTopLevels == 2 ? 24 : (kTopLevels == 1 ? 4 : 1);
+// (round 2 measured the tree's top levels held in SGPRs instead of LDS: no faster)
 struct TopKeys {
-    unsigned k[kTopKeys];
-    bool on;        // the tree has at least kTopLevels levels
     unsigned last;  // the largest splitter (a finite score's key, so >= 0x007fffff > 0)
 };
 
@@ -320,7 +291,6 @@ TreeGeom tree_geom(int S) {
 }
 
 __device__ __forceinline__ void store_node(uint4* t, int64_t c, const unsigned (&k)[4]) { t[c] = uint4{k[0], k[1], k[2], k[3]}; }
-__device__ __forceinline__ void store_node(uint2* t, int64_t c, const unsigned (&k)[4]) { t[c] = uint2{k[0], k[1]}; }
 
 __global__ __launch_bounds__(256) void build_tree_kernel(unsigned* __restrict__ sorted, int64_t M, int64_t pad, int k,
                                                          TreeGeom g, TreeNode* __restrict__ tree,
@@ -346,28 +316,9 @@ __global__ __launch_bounds__(256) void build_tree_kernel(unsigned* __restrict__ 
     if (c < n_first) ci_first[c] = static_cast<unsigned>(M);  // count index: "no key in this bucket"
 }
 
-// p <- A p + #(node keys <= x): the compares' carries feed the adds (DAUC_TREE_STEP 0), or
-// (1) without the carry flag: sat(k - x) (unsigned saturating subtract) is 0 iff k <= x, so
-// #(keys <= x) = 4 - sum(min(sat(k_i - x), 1)) — 12 VALU, none writing VCC.
-#ifndef DAUC_TREE_STEP
-#define DAUC_TREE_STEP 0
-#endif
+// p <- 5 p + #(node keys <= x): the compares' carries feed the adds (a carry-free form with
+// saturating subtracts, 12 VALU instead of 8, measured 5 % slower in round 2)
 __device__ __forceinline__ unsigned tree_step(unsigned p, uint4 n, unsigned x) {
-    if (DAUC_TREE_STEP == 1) {
-        unsigned d0, d1, d2, d3, gt;
-        asm("v_sub_u32_e64 %0, %5, %9 clamp\n\t"
-            "v_sub_u32_e64 %1, %6, %9 clamp\n\t"
-            "v_sub_u32_e64 %2, %7, %9 clamp\n\t"
-            "v_sub_u32_e64 %3, %8, %9 clamp\n\t"
-            "v_min_u32_e32 %0, 1, %0\n\t"
-            "v_min_u32_e32 %1, 1, %1\n\t"
-            "v_min_u32_e32 %2, 1, %2\n\t"
-            "v_min_u32_e32 %3, 1, %3\n\t"
-            "v_add3_u32 %4, %0, %1, %2"
-            : "=&v"(d0), "=&v"(d1), "=&v"(d2), "=&v"(d3), "=&v"(gt)
-            : "v"(n.x), "v"(n.y), "v"(n.z), "v"(n.w), "v"(x));
-        return p * 5u + 4u - (gt + d3);
-    }
     unsigned r = p * 5u;
     asm("v_cmp_le_u32_e32 vcc, %1, %5\n\t"
         "v_addc_co_u32_e32 %0, vcc, 0, %0, vcc\n\t"
@@ -383,18 +334,6 @@ __device__ __forceinline__ unsigned tree_step(unsigned p, uint4 n, unsigned x) {
     return r;
 }
 
-__device__ __forceinline__ unsigned tree_step(unsigned p, uint2 n, unsigned x) {
-    unsigned r = p * 3u;
-    asm("v_cmp_le_u32_e32 vcc, %1, %3\n\t"
-        "v_addc_co_u32_e32 %0, vcc, 0, %0, vcc\n\t"
-        "v_cmp_le_u32_e32 vcc, %2, %3\n\t"
-        "v_addc_co_u32_e32 %0, vcc, 0, %0, vcc"
-        : "+v"(r)
-        : "v"(n.x), "v"(n.y), "v"(x)
-        : "vcc");
-    return r;
-}
-
 // Q walks of the tree in lockstep: p[q] ends as #splitters <= x[q]. The level geometry is
 // wave-uniform (kernel arguments, scalar registers).
 template <int Q>
@@ -402,11 +341,6 @@ __device__ __forceinline__ void tree_walk(const unsigned (&x)[Q], unsigned (&p)[
                                           const TreeGeom& g, const TopKeys& top) {
 #pragma unroll
     for (int q = 0; q < Q; ++q) p[q] = 0;
-    if (DAUC_ABLATE == 2) {
-#pragma unroll
-        for (int q = 0; q < Q; ++q) p[q] = (x[q] * 2654435761u) % static_cast<unsigned>(g.S);
-        return;
-    }
     // A walk for x below the largest splitter only visits stored nodes: its node at level d is
     // floor(r / 5^(H-d)) for r = #splitters <= x <= S - 1, at most the level's one padding node
     // (n_d). So x is clamped below the largest splitter (no per-level index clamp) and the
@@ -414,20 +348,9 @@ __device__ __forceinline__ void tree_walk(const unsigned (&x)[Q], unsigned (&p)[
     unsigned xc[Q];
 #pragma unroll
     for (int q = 0; q < Q; ++q) xc[q] = x[q] < top.last ? x[q] : top.last - 1u;
-    int d0 = 0;
-    if (kTopLevels > 0 && top.on) {
-#pragma unroll
-        for (int q = 0; q < Q; ++q) {
-            unsigned c = 0;
-#pragma unroll
-            for (int m = 0; m < kTopKeys; ++m) c += top.k[m] <= xc[q];
-            p[q] = c;
-        }
-        d0 = kTopLevels;
-    }
 #pragma unroll
     for (int d = 0; d < kMaxTreeH; ++d) {
-        if (d >= d0 && d < g.H) {
+        if (d < g.H) {
             const unsigned off = static_cast<unsigned>(g.off[d]);
             TreeNode v[Q];
 #pragma unroll
@@ -445,11 +368,6 @@ __device__ __forceinline__ void tree_walk(const unsigned (&x)[Q], unsigned (&p)[
 template <int K>
 __device__ __forceinline__ void bucket_counts(const unsigned* __restrict__ sorted, int64_t M, int64_t b,
                                               unsigned x, int& le, int& lt, unsigned& first) {
-    if (DAUC_ABLATE == 1) {
-        le = lt = static_cast<int>(b & 3);
-        first = 0;
-        return;
-    }
     const int64_t base = b * K;
     unsigned v[K];
     if constexpr (K >= 4) {
@@ -555,8 +473,7 @@ __device__ __forceinline__ void count_query(unsigned x, const TreeNode* __restri
 // bucket loads) in flight per lane. use[q] = false: the slot is walked but not counted.
 template <int K>
 constexpr int lockstep_queries() {
-    return DAUC_QUERY_LOCKSTEP ? (DAUC_QUERY_LOCKSTEP * K > 32 ? 1 : DAUC_QUERY_LOCKSTEP)
-                               : (K <= 8 ? 4 : (K == 16 ? 2 : 1));
+    return K <= 8 ? 4 : (K == 16 ? 2 : 1);
 }
 
 template <int K, int Q, bool TABLE_POS>
@@ -629,99 +546,6 @@ __device__ __forceinline__ void count_queries(const unsigned (&x)[Q], const bool
     }
 }
 
-// Two-phase form of count_queries for Q = 4 lockstep queries and K = 2, 4, 8 (the labeled
-// kernel's hot loop), a measured variant (DAUC_QUERY_PIPE=1): phase A walks the tree and
-// issues the bucket loads of every slot of an iteration, then the next iteration's stream loads
-// are issued, then phase B compares and counts -- so no wait for a bucket load also waits out a
-// streaming load's HBM latency (vmcnt retires in issue order). Same speed as the one-phase loop
-// (2^27 @ 0.1 %: 699 vs 684 us per sort + query; 2^24 @ 1 %: 165 vs 170 us;
-// profiles/r02/query_tuning/micro_pipe.jsonl): the query pass is not bound by load latency.
-#ifndef DAUC_QUERY_PIPE
-#define DAUC_QUERY_PIPE 0
-#endif
-#ifndef DAUC_QUERY_PIPE_U
-#define DAUC_QUERY_PIPE_U 2  // float4 slots per iteration of the batched loop (int8 labels)
-#endif
-template <int K>
-constexpr bool pipelined() {
-    return DAUC_QUERY_PIPE != 0 && (K == 2 || K == 4 || K == 8) && lockstep_queries<K>() == 4;
-}
-
-template <int K>
-__device__ __forceinline__ void load_bucket(const unsigned* __restrict__ sorted, unsigned b, unsigned (&v)[K]) {
-    const unsigned* p = sorted + size_t(b) * K;
-    if constexpr (K == 2) {
-        const uint2 u = *reinterpret_cast<const uint2*>(p);
-        v[0] = u.x;
-        v[1] = u.y;
-    } else {
-#pragma unroll
-        for (int q = 0; q < K / 4; ++q) {
-            const uint4 u = reinterpret_cast<const uint4*>(p)[q];
-            v[4 * q] = u.x;
-            v[4 * q + 1] = u.y;
-            v[4 * q + 2] = u.z;
-            v[4 * q + 3] = u.w;
-        }
-    }
-}
-
-template <int K>
-__device__ __forceinline__ void walk_and_load(const unsigned (&x)[4], unsigned (&su)[4], unsigned (&v)[4][K],
-                                              const TreeNode* __restrict__ tree, const TreeGeom& g,
-                                              const TopKeys& top, const unsigned* __restrict__ sorted) {
-    tree_walk<4>(x, su, tree, g, top);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) load_bucket<K>(sorted, su[q] ? su[q] - 1u : 0u, v[q]);
-}
-
-template <int K, bool TABLE_POS>
-__device__ __forceinline__ void finish_counts(const unsigned (&x)[4], const bool (&use)[4], const unsigned (&su)[4],
-                                              const unsigned (&v)[4][K], const TreeNode* __restrict__ tree,
-                                              const TreeGeom& g, const TopKeys& top,
-                                              const unsigned* __restrict__ sorted, int64_t M,
-                                              unsigned long long& w, unsigned long long& t) {
-    bool slow = false;
-    unsigned wl = 0u, tl = 0u;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        int le = 0, lt = 0;
-#pragma unroll
-        for (int j = 0; j < K; ++j) {
-            le += v[q][j] <= x[q];
-            lt += v[q][j] < x[q];
-        }
-        const unsigned base = su[q] ? (su[q] - 1u) * static_cast<unsigned>(K) : 0u;
-        const unsigned ub = su[q] ? base + static_cast<unsigned>(le) : 0u;
-        const unsigned lb = su[q] ? base + static_cast<unsigned>(lt) : 0u;
-        const unsigned wq = TABLE_POS ? static_cast<unsigned>(M) - ub : lb;
-        wl += use[q] ? wq : 0u;
-        tl += use[q] ? ub - lb : 0u;
-        slow |= use[q] && su[q] != 0u && v[q][0] >= x[q];
-    }
-    w += wl;
-    t += tl;
-    if (slow) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            if (!(use[q] && su[q] != 0u && v[q][0] >= x[q])) continue;
-            const unsigned xm[1] = {x[q] - 1u};
-            unsigned j[1];
-            tree_walk<1>(xm, j, tree, g, top);
-            unsigned lb_true = 0u;
-            if (j[0] != 0u) {
-                int le2 = 0, lt2 = 0;
-                unsigned f2 = 0;
-                bucket_counts<K>(sorted, M, j[0] - 1u, x[q], le2, lt2, f2);
-                lb_true = (j[0] - 1u) * static_cast<unsigned>(K) + static_cast<unsigned>(lt2);
-            }
-            const unsigned lb_fast = (su[q] - 1u) * static_cast<unsigned>(K);
-            t += lb_fast - lb_true;
-            if (!TABLE_POS) w -= lb_fast - lb_true;
-        }
-    }
-}
-
 // Four keys (one float4 slot) with per-key use flags, through count_queries in groups of Q
 // (K = 0, buckets > 32 keys finished in global memory: one key at a time).
 template <int K, bool TABLE_POS>
@@ -751,28 +575,10 @@ __device__ __forceinline__ void count4(const unsigned (&x)[4], const bool (&use)
 // the top levels' keys, read once per workgroup with uniform (scalar) loads
 __device__ __forceinline__ TopKeys load_top(const TreeNode* __restrict__ gtree, const TreeGeom& g,
                                            const unsigned* __restrict__ sorted, int k) {
+    (void)gtree;
+    (void)g;
     TopKeys t{};
     t.last = sorted[int64_t(g.S - 1) * k];
-    t.on = kTopLevels > 0 && g.H >= kTopLevels;
-    if constexpr (kTopLevels > 0) {
-        if (t.on) {
-            const uint4 n0 = gtree[g.off[0]];
-            t.k[0] = n0.x;
-            t.k[1] = n0.y;
-            t.k[2] = n0.z;
-            t.k[3] = n0.w;
-            if constexpr (kTopLevels == 2) {
-#pragma unroll
-                for (int j = 0; j < 5; ++j) {
-                    const uint4 n = gtree[g.off[1] + (j < g.nd[1] ? j : g.nd[1])];
-                    t.k[4 + 4 * j] = n.x;
-                    t.k[5 + 4 * j] = n.y;
-                    t.k[6 + 4 * j] = n.z;
-                    t.k[7 + 4 * j] = n.w;
-                }
-            }
-        }
-    }
     return t;
 }
 
@@ -841,454 +647,16 @@ __device__ __forceinline__ void label4(const LT* __restrict__ lab, int64_t i, bo
     }
 }
 
-// ---- radix cell index (a measured alternative to the tree: dauc_set_search_mode(2)) --------
-//
-// The tree walk above is a chain of 7 dependent LDS reads and ~60 VALU per query. The cell
-// index replaces it by arithmetic: the key's top 12 bits (sign, exponent, 3 mantissa bits) pick
-// a top bucket t, whose C_t cells split its 2^20 low key values evenly; C_t = ceil(n_t / mu)
-// for the n_t table keys in the bucket, so a cell holds mu keys on average (mu = 4 for the
-// 2^27 @ 0.1 % table). LDS holds l1[t] = first cell | C_t << 16 and base[c] = #table keys below
-// cell c; global memory (L2-resident) holds every cell's first 16 keys, padded with +inf, as
-// one 64-byte slot. A query is: one LDS read (l1), a multiply-high for its cell, one LDS read2
-// (base[c], base[c+1]) in parallel with the 64-byte slot load, and 16 compares for
-// #(keys < x) and #(keys <= x) -- keys before the cell are all < x, keys after it all > x.
-// Cells with more than 16 keys finish with a binary search of the table beyond the slot.
-// Measured SLOWER than the tree (2^27 @ 0.1 %: 1,176 vs 710 us per sort + query; 2^24 @ 1 %:
-// 273 vs 179 us; profiles/r02/query_tuning/micro_cells.jsonl): a 64-byte slot is four 16-byte
-// lane gathers, and each 16-byte gather per query costs as much as the whole LDS walk (the
-// tree's one bucket gather: ~200 us of its 700 at 2^27). The 4-key-group form of the compares
-// (DAUC_CELL_COUNT=1) was slower still. Kept, tested bit-exact, as the record of that result.
-// The builder also records whether the table is skewed (more than 1/64 of the keys beyond
-// their slot: clustered or tie-heavy keys) in a device word that both query kernels read.
-constexpr int kTopBits = 12;
-constexpr int kTop = 1 << kTopBits;
-constexpr int kLowBits = 32 - kTopBits;
-constexpr int kCellSlot = 16;                                 // keys per cell slot (64 B)
-constexpr int kMaxCells = 35840;                              // LDS: 4 * (4096 + 35842) B + reduce scratch <= 160 KB
-constexpr int kCellMuForced = 16;                            // largest mean keys per cell tried
-constexpr int kCellPlanThreads = 1024;
-// meta words: [0] cells built (mu found), [1] number of cells, [2] keys beyond the slots, [3] mu
-constexpr int kMetaOk = 0, kMetaCells = 1, kMetaOverflow = 2, kMetaMu = 3;
+// Region of the sort workspace that holds the direct build's 72 group totals (grp)
+constexpr size_t kGrpBytes = 512;
 
-struct CellWs {
-    unsigned* meta;   // [64]
-    unsigned* l1;     // [kTop]
-    unsigned* base;   // [kMaxCells + 2]
-    uint4* slots;     // [(kMaxCells + 1) * 4]
-};
-
-constexpr size_t kCellBytes = 256 + size_t(kTop) * 4 + ((size_t(kMaxCells) + 2) * 4 + 255) / 256 * 256 +
-                              (size_t(kMaxCells) + 1) * kCellSlot * 4;
-
-// search structure set by dauc_set_search_mode (tests, measurements): 0, 1 = tree, 2 = cells
+// search structure: 0 automatic (the count index where it holds the table, else the tree); the
+// tuning build can force the tree (dauc_set_search_mode(1)) to test it on any table
 #ifdef DAUC_TUNING
-int g_search_mode = 0;  // dauc_set_search_mode (tuning builds): 0 automatic, 1 tree, 2 slot cells
+int g_search_mode = 0;
 #else
 constexpr int g_search_mode = 0;
 #endif
-
-#ifdef DAUC_TUNING
-__device__ __forceinline__ unsigned cell_of(unsigned key, unsigned e) {
-    return (e & 0xffffu) + __umulhi(key << kTopBits, e >> 16);
-}
-
-__device__ __forceinline__ bool cells_in_use(const unsigned* __restrict__ meta, int64_t M, int force) {
-    return meta[kMetaOk] != 0u && (force || int64_t(meta[kMetaOverflow]) * 64 <= M);
-}
-
-// inclusive scan over the 1024 threads of a workgroup (wave shuffles, one barrier for the wave
-// totals); op is min or +, v the thread's value
-#endif
-
-
-// One workgroup: per top bucket the first table index (every key compared with its
-// predecessor), the bucket sizes n_t (suffix minimum of the first indices), the smallest
-// mu in [4, mu_max] whose sum of ceil(n_t / mu) fits kMaxCells, and the cell offsets (prefix sum).
-// Thread i owns the buckets t = 4095 - 4i - j (j = 0..3): descending, so suffix minima over t
-// are prefix minima over the threads.
-#ifdef DAUC_TUNING
-__global__ __launch_bounds__(kCellPlanThreads) void cell_plan_kernel(const unsigned* __restrict__ sorted, int64_t M,
-                                                                     int mu_max, unsigned* __restrict__ l1,
-                                                                     unsigned* __restrict__ meta) {
-    static_assert(kTop == 4 * kCellPlanThreads, "four top buckets per thread");
-    __shared__ unsigned first[kTop];
-    __shared__ unsigned wtot[kCellPlanThreads / kWave];
-    const unsigned m32 = static_cast<unsigned>(M);
-    for (int t = threadIdx.x; t < kTop; t += kCellPlanThreads) first[t] = m32;
-    __syncthreads();
-    for (int64_t i = threadIdx.x; i < M; i += kCellPlanThreads) {
-        const unsigned t = sorted[i] >> kLowBits;
-        if (i == 0 || (sorted[i - 1] >> kLowBits) != t) first[t] = static_cast<unsigned>(i);
-    }
-    __syncthreads();
-    int tj[4];
-    unsigned st[4], run = ~0u;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        tj[j] = kTop - 1 - 4 * static_cast<int>(threadIdx.x) - j;
-        const unsigned f = first[tj[j]];
-        run = f < run ? f : run;
-        st[j] = run;  // min of first[] over this thread's buckets >= tj[j]
-    }
-    const unsigned incl = block_incl_scan1024<true>(run, wtot);
-    // start of the bucket above this thread's highest one: the previous threads' minimum (M past
-    // the top bucket); first[] is free again, so it carries the inclusive minima
-    first[threadIdx.x] = incl;
-    __syncthreads();
-    unsigned n[4];
-    {
-        const unsigned above = threadIdx.x == 0 ? m32 : first[threadIdx.x - 1];
-        unsigned hi = above < m32 ? above : m32;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const unsigned s0 = st[j] < hi ? st[j] : hi;  // start of bucket tj[j]
-            n[j] = hi - s0;
-            hi = s0;
-        }
-    }
-    unsigned mu = 0, total = 0;
-    __shared__ unsigned bsum[kCellPlanThreads / kWave];
-    for (unsigned m = 4; m <= static_cast<unsigned>(mu_max); ++m) {
-        unsigned c = 0;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) c += (n[j] + m - 1) / m;
-        unsigned long long cw = wave_sum(static_cast<unsigned long long>(c));
-        if ((threadIdx.x & (kWave - 1)) == 0) bsum[threadIdx.x / kWave] = static_cast<unsigned>(cw);
-        __syncthreads();
-        unsigned tot = 0;
-        for (int w = 0; w < kCellPlanThreads / kWave; ++w) tot += bsum[w];
-        __syncthreads();
-        if (tot <= static_cast<unsigned>(kMaxCells)) {
-            mu = m;
-            total = tot;
-            break;
-        }
-    }
-    if (threadIdx.x == 0) {
-        meta[kMetaOk] = mu != 0u;
-        meta[kMetaCells] = total;
-        meta[kMetaOverflow] = 0u;
-        meta[kMetaMu] = mu;
-    }
-    if (mu == 0u) return;  // uniform: every thread saw the same totals
-    unsigned C[4], csum = 0;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        C[j] = (n[j] + mu - 1) / mu;
-        csum += C[j];
-    }
-    // cells of the buckets >= tj[j] (descending prefix), so off_t = total - that
-    const unsigned incl_c = block_incl_scan1024<false>(csum, wtot);
-    unsigned upto = incl_c - csum;  // cells of the buckets above this thread's
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        upto += C[j];
-        l1[tj[j]] = (total - upto) | (C[j] << 16);
-    }
-}
-
-// One thread per table index i in [0, M] (i = M: a virtual key past every cell). Cells
-// (c(i-1), c(i)] start at i; the cells strictly between are empty (+inf slots); the first key
-// of each cell copies its cell's first 16 keys into the slot; keys of rank >= 16 in their
-// cell are counted as overflow.
-__global__ __launch_bounds__(256) void cell_fill_kernel(const unsigned* __restrict__ sorted, int64_t M,
-                                                        const unsigned* __restrict__ l1, unsigned* __restrict__ meta,
-                                                        unsigned* __restrict__ base, uint4* __restrict__ slots) {
-    if (meta[kMetaOk] == 0u) return;
-    const int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x;
-    unsigned ov = 0;
-    if (i <= M) {
-        const unsigned ncells = meta[kMetaCells];
-        auto cell = [&](int64_t j) -> unsigned {
-            const unsigned key = sorted[j];
-            return cell_of(key, l1[key >> kLowBits]);
-        };
-        const int64_t ci = i < M ? int64_t(cell(i)) : int64_t(ncells) + 1;
-        const int64_t cp = i > 0 ? int64_t(cell(i - 1)) : -1;
-        const uint4 pad4 = uint4{kPadKey, kPadKey, kPadKey, kPadKey};
-        for (int64_t c = cp + 1; c <= ci; ++c) {
-            base[c] = static_cast<unsigned>(i);
-            if (c < ci) {
-#pragma unroll
-                for (int m = 0; m < kCellSlot / 4; ++m) slots[c * (kCellSlot / 4) + m] = pad4;
-            }
-        }
-        if (i < M && ci != cp) {
-            unsigned kk[kCellSlot];
-#pragma unroll
-            for (int j = 0; j < kCellSlot; ++j) {
-                const int64_t idx = i + j;
-                unsigned v = kPadKey;
-                if (idx < M) {
-                    const unsigned key = sorted[idx];
-                    if (int64_t(cell_of(key, l1[key >> kLowBits])) == ci) v = key;
-                }
-                kk[j] = v;
-            }
-#pragma unroll
-            for (int m = 0; m < kCellSlot / 4; ++m)
-                slots[ci * (kCellSlot / 4) + m] = uint4{kk[4 * m], kk[4 * m + 1], kk[4 * m + 2], kk[4 * m + 3]};
-        }
-        if (i < M && i >= kCellSlot && int64_t(cell(i - kCellSlot)) == ci) ov = 1u;
-    }
-    const unsigned long long w = wave_sum(static_cast<unsigned long long>(ov));
-    if ((threadIdx.x & (kWave - 1)) == 0 && w) atomicAdd(meta + kMetaOverflow, static_cast<unsigned>(w));
-}
-
-// #(slot keys < x) and #(slot keys <= x) for Q queries, every load issued before any compare
-#ifndef DAUC_CELL_Q
-#define DAUC_CELL_Q 4
-#endif
-#ifndef DAUC_CELL_U
-#define DAUC_CELL_U 2
-#endif
-// 0: 16 compares per bound; 1: the slot's 4-key group holding the first key >= x (3 compares
-// with the group ends, a 4-way select), then 4 compares per bound
-#ifndef DAUC_CELL_COUNT
-#define DAUC_CELL_COUNT 0
-#endif
-constexpr int kCellQ = DAUC_CELL_Q;
-
-__device__ __forceinline__ void count16(const uint4 (&k)[4], unsigned x, unsigned& lt, unsigned& le) {
-    unsigned a = 0, b = 0;
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {
-        a += (k[m].x < x) + (k[m].y < x) + (k[m].z < x) + (k[m].w < x);
-        b += (k[m].x <= x) + (k[m].y <= x) + (k[m].z <= x) + (k[m].w <= x);
-    }
-    lt = a;
-    le = b;
-}
-
-// Exact unless a group's last key equals x and a later group starts with x too (exact = false:
-// the caller recounts the whole slot)
-__device__ __forceinline__ void count16_group(const uint4 (&k)[4], unsigned x, unsigned& lt, unsigned& le,
-                                              bool& exact) {
-    const unsigned g = (k[0].w < x) + (k[1].w < x) + (k[2].w < x);
-    const unsigned g2 = (k[0].w <= x) + (k[1].w <= x) + (k[2].w <= x);
-    const uint4 lo2 = (g & 1u) ? k[1] : k[0];
-    const uint4 hi2 = (g & 1u) ? k[3] : k[2];
-    const uint4 a = (g & 2u) ? hi2 : lo2;
-    lt = 4u * g + (a.x < x) + (a.y < x) + (a.z < x) + (a.w < x);
-    le = 4u * g + (a.x <= x) + (a.y <= x) + (a.z <= x) + (a.w <= x);
-    exact = g2 == g;
-}
-
-// Q queries (use[q] false: computed, not counted) against the cell index; W += M - ub,
-// T += ub - lb (table = positives), summed per group in 32 bits (Q * M < 2^32)
-template <int Q>
-__device__ __forceinline__ void cell_queries(const unsigned (&x)[Q], const bool (&use)[Q],
-                                             const unsigned* __restrict__ l1s, const unsigned* __restrict__ bases,
-                                             const uint4* __restrict__ slots, const unsigned* __restrict__ sorted,
-                                             unsigned M, unsigned long long& w, unsigned long long& t) {
-    unsigned c[Q], lo[Q], hi[Q], lbf[Q], ubf[Q];
-    bool redo[Q];
-    uint4 k[Q][4];
-#pragma unroll
-    for (int q = 0; q < Q; ++q) c[q] = cell_of(x[q], l1s[x[q] >> kLowBits]);
-#pragma unroll
-    for (int q = 0; q < Q; ++q) {
-        const uint4* sl = slots + size_t(c[q]) * (kCellSlot / 4);
-#pragma unroll
-        for (int m = 0; m < 4; ++m) k[q][m] = sl[m];
-    }
-#pragma unroll
-    for (int q = 0; q < Q; ++q) {
-        lo[q] = bases[c[q]];
-        hi[q] = bases[c[q] + 1];
-    }
-    unsigned wl = 0u, tl = 0u;
-    bool slow = false;
-#pragma unroll
-    for (int q = 0; q < Q; ++q) {
-        unsigned lt, le;
-        bool exact = true;
-        if (DAUC_CELL_COUNT == 1)
-            count16_group(k[q], x[q], lt, le, exact);
-        else
-            count16(k[q], x[q], lt, le);
-        lbf[q] = lo[q] + lt;
-        ubf[q] = lo[q] + le;
-        wl += use[q] ? M - ubf[q] : 0u;
-        tl += use[q] ? ubf[q] - lbf[q] : 0u;
-        // the cell continues past its slot and x reaches the slot's last key, or the group
-        // count was not exact: recount below
-        redo[q] = use[q] && ((hi[q] - lo[q] > static_cast<unsigned>(kCellSlot) && k[q][3].w <= x[q]) || !exact);
-        slow |= redo[q];
-    }
-    w += wl;
-    t += tl;
-    if (slow) {
-#pragma unroll
-        for (int q = 0; q < Q; ++q) {
-            if (!redo[q]) continue;
-            unsigned lt, le;
-            count16(k[q], x[q], lt, le);
-            int64_t lb = int64_t(lo[q]) + lt, ub = int64_t(lo[q]) + le;
-            if (hi[q] - lo[q] > static_cast<unsigned>(kCellSlot) && k[q][3].w <= x[q]) {
-                // the rest of the cell from the sorted table (ub always; lb unless the slot's last key is x)
-                const int64_t b0 = int64_t(lo[q]) + kCellSlot, b1 = hi[q];
-                ub = b0 + count_below<false>(sorted, b0, b1, x[q]);
-                if (k[q][3].w < x[q]) lb = b0 + count_below<true>(sorted, b0, b1, x[q]);
-            }
-            // replace the fast counts: W -= ub - ubf, T += (ub - lb) - (ubf - lbf)
-            w -= static_cast<unsigned long long>(ub - int64_t(ubf[q]));
-            t += static_cast<unsigned long long>((ub - lb) - (int64_t(ubf[q]) - int64_t(lbf[q])));
-        }
-    }
-}
-
-template <int Q>
-__device__ __forceinline__ void cell_count4(const unsigned (&x)[4], const bool (&use)[4], const unsigned* l1s,
-                                            const unsigned* bases, const uint4* slots, const unsigned* sorted,
-                                            unsigned M, unsigned long long& w, unsigned long long& t) {
-#pragma unroll
-    for (int b = 0; b < 4; b += Q) {
-        unsigned xs[Q];
-        bool us[Q];
-#pragma unroll
-        for (int q = 0; q < Q; ++q) {
-            xs[q] = x[b + q];
-            us[q] = use[b + q];
-        }
-        cell_queries<Q>(xs, us, l1s, bases, slots, sorted, M, w, t);
-    }
-}
-
-// The labeled query pass over the cell index: the same stream as query_labeled_kernel (every
-// label != +1 is a query against the sorted positives; queried scores checked for finiteness).
-// Returns at once when the builder kept the tree (meta), so it is enqueued unconditionally.
-template <typename LT>
-__global__ __launch_bounds__(kQueryThreads) void query_cells_kernel(const float* __restrict__ s,
-                                                                   const LT* __restrict__ lab, int64_t begin,
-                                                                   int64_t end, const unsigned* __restrict__ meta,
-                                                                   int force, const unsigned* __restrict__ l1g,
-                                                                   const unsigned* __restrict__ baseg,
-                                                                   const uint4* __restrict__ slots,
-                                                                   const unsigned* __restrict__ sorted, int64_t M,
-                                                                   unsigned long long* __restrict__ out,
-                                                                   unsigned long long* __restrict__ nonfinite) {
-    if (!cells_in_use(meta, M, force)) return;
-    extern __shared__ unsigned cells_lds[];
-    unsigned* l1s = cells_lds;
-    unsigned* bases = cells_lds + kTop;
-    {
-        const int nb = static_cast<int>(meta[kMetaCells]) + 2;
-        const uint4* l1v = reinterpret_cast<const uint4*>(l1g);
-        for (int i = threadIdx.x; i < kTop / 4; i += kQueryThreads) reinterpret_cast<uint4*>(l1s)[i] = l1v[i];
-        for (int i = threadIdx.x; i < nb; i += kQueryThreads) bases[i] = baseg[i];
-    }
-    __syncthreads();
-    const unsigned M32 = static_cast<unsigned>(M);
-    unsigned long long w = 0, t = 0;
-    unsigned nf = 0;
-    const int64_t a0 = (begin + 3) & ~int64_t(3);
-    const int64_t head = a0 < end ? a0 : end;
-    const int64_t stride = int64_t(gridDim.x) * kQueryThreads;
-    const int64_t tid = int64_t(blockIdx.x) * kQueryThreads + threadIdx.x;
-    auto one = [&](int64_t i) {
-        if (lab[i] != LT(1)) {
-            nf += !isfinite(s[i]);
-            const unsigned x[1] = {key_of(s[i])};
-            const bool u[1] = {true};
-            cell_queries<1>(x, u, l1s, bases, slots, sorted, M32, w, t);
-        }
-    };
-    for (int64_t i = begin + tid; i < head; i += stride) one(i);
-    const int64_t nvec = end > head ? (end - head) / 4 : 0;
-    const bool aligned = (reinterpret_cast<uintptr_t>(s + head) & 15u) == 0 &&
-                         (reinterpret_cast<uintptr_t>(lab + head) & (4 * sizeof(LT) - 1)) == 0;
-    if (aligned) {
-        constexpr int U = DAUC_CELL_U;
-        f32x4 fc[U], fn[U];
-        LT lc[U][4], ln[U][4];
-        auto load = [&](int64_t v0, f32x4 (&f)[U], LT (&l)[U][4]) {
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int64_t v = v0 + int64_t(u) * stride;
-                if (v < nvec) {
-                    const int64_t i = head + v * 4;
-                    f[u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(s + i));
-                    if constexpr (sizeof(LT) == 1) {
-                        const char4 c = *reinterpret_cast<const char4*>(lab + i);
-                        l[u][0] = c.x;
-                        l[u][1] = c.y;
-                        l[u][2] = c.z;
-                        l[u][3] = c.w;
-                    } else if constexpr (sizeof(LT) == 4) {
-                        const int4 c = *reinterpret_cast<const int4*>(lab + i);
-                        l[u][0] = c.x;
-                        l[u][1] = c.y;
-                        l[u][2] = c.z;
-                        l[u][3] = c.w;
-                    } else {
-                        const longlong2 c0 = reinterpret_cast<const longlong2*>(lab + i)[0];
-                        const longlong2 c1 = reinterpret_cast<const longlong2*>(lab + i)[1];
-                        l[u][0] = c0.x;
-                        l[u][1] = c0.y;
-                        l[u][2] = c1.x;
-                        l[u][3] = c1.y;
-                    }
-                } else {
-                    f[u] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) l[u][q] = LT(1);  // past the end: no query
-                }
-            }
-        };
-        load(tid, fc, lc);
-        for (int64_t v0 = tid; v0 < nvec; v0 += int64_t(U) * stride) {
-            load(v0 + int64_t(U) * stride, fn, ln);
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const float f[4] = {fc[u].x, fc[u].y, fc[u].z, fc[u].w};
-                bool neg[4];
-                unsigned x[4];
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    neg[q] = lc[u][q] != LT(1);
-                    x[q] = key_of(f[q]);
-                    nf += neg[q] && !isfinite(f[q]);
-                }
-                cell_count4<kCellQ>(x, neg, l1s, bases, slots, sorted, M32, w, t);
-            }
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                fc[u] = fn[u];
-#pragma unroll
-                for (int q = 0; q < 4; ++q) lc[u][q] = ln[u][q];
-            }
-        }
-    } else {
-        for (int64_t v = tid; v < nvec; v += stride)
-            for (int q = 0; q < 4; ++q) one(head + v * 4 + q);
-    }
-    for (int64_t i = head + nvec * 4 + tid; i < end; i += stride) one(i);
-    __shared__ unsigned long long red[3][kQueryThreads / kWave];
-    w = wave_sum(w);
-    t = wave_sum(t);
-    const unsigned long long nfw = wave_sum(static_cast<unsigned long long>(nf));
-    const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
-    if (lane == 0) {
-        red[0][wid] = w;
-        red[1][wid] = t;
-        red[2][wid] = nfw;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        unsigned long long bw = 0, bt = 0, bn = 0;
-        for (int i = 0; i < kQueryThreads / kWave; ++i) {
-            bw += red[0][i];
-            bt += red[1][i];
-            bn += red[2][i];
-        }
-        if (bw) atomicAdd(out + 0, bw);
-        if (bt) atomicAdd(out + 1, bt);
-        if (bn && nonfinite) atomicAdd(nonfinite, bn);
-    }
-}
-
-#endif  // DAUC_TUNING
 
 // ---- count index (the default search where it fits: dauc_set_search_mode 0) -----------------
 //
@@ -1441,34 +809,13 @@ __global__ __launch_bounds__(256) void ci_blocks_kernel(const unsigned* __restri
     if (__ballot(skew) != 0ull && (threadIdx.x & (kWave - 1)) == 0) atomicOr(meta + kCiSkew, 1u);
 }
 
-// a 16-byte window of the L2-resident table (DAUC_CI_WIN_NT: with the non-temporal hint)
-#ifndef DAUC_CI_WIN_NT
-#define DAUC_CI_WIN_NT 0
-#endif
-__device__ __forceinline__ uint4 win_load(const unsigned* p) {
-    if (DAUC_CI_WIN_NT) {
-        typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-        const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
-        return uint4{v.x, v.y, v.z, v.w};
-    }
-    return *reinterpret_cast<const uint4*>(p);
-}
-
+// a 16-byte window of the L2-resident table
+__device__ __forceinline__ uint4 win_load(const unsigned* p) { return *reinterpret_cast<const uint4*>(p); }
 
 // Phase 1 of one query: cell, rank_lo, count and (lanes with cnt > 0) the window load
-#ifndef DAUC_CI_ABLATE
-#define DAUC_CI_ABLATE 0  // timing ablations only (wrong counts): 1 no window load, 2 no LDS, 3 neither
-#endif
 __device__ __forceinline__ void ci_locate(unsigned x, const uint2* __restrict__ l1, const uint2* __restrict__ blk,
                                           const unsigned* __restrict__ sorted, unsigned& rl, unsigned& cnt,
                                           uint4& k) {
-    if (DAUC_CI_ABLATE >= 2) {
-        rl = (x * 2654435761u) % 100000u;
-        cnt = (x >> 7) & 1u;
-        k = uint4{kPadKey, kPadKey, kPadKey, kPadKey};
-        if (DAUC_CI_ABLATE == 2 && cnt) k = *reinterpret_cast<const uint4*>(sorted + (rl & ~3u));
-        return;
-    }
     const unsigned c = ci_cell(x, l1[x >> kCiLowBits]);
     const uint2 b = blk[c / kCiBlock];
     const unsigned sh = 4u * (c % kCiBlock);
@@ -1477,7 +824,7 @@ __device__ __forceinline__ void ci_locate(unsigned x, const uint2* __restrict__ 
     rl = b.x + __builtin_amdgcn_sad_u8(bytes, 0u, 0u);
     cnt = __builtin_amdgcn_ubfe(b.y, sh, 4u);
     k = uint4{kPadKey, kPadKey, kPadKey, kPadKey};
-    if (DAUC_CI_ABLATE == 0 && cnt) k = *reinterpret_cast<const uint4*>(sorted + (rl & ~3u));
+    if (cnt) k = *reinterpret_cast<const uint4*>(sorted + (rl & ~3u));
 }
 
 // Phase 2: lb, ub from the window (W += M - ub, T += ub - lb for use); returns whether the cell
@@ -1520,34 +867,6 @@ __device__ __forceinline__ void ci_fix(unsigned x, unsigned rl, unsigned cnt, co
     t += static_cast<unsigned long long>((ub - lb) - (ubf - lbf));
 }
 
-#ifndef DAUC_CI_PIPE
-#define DAUC_CI_PIPE 1  // 1: software-pipelined query loop (LDS lookups overlap the window loads)
-#endif
-#ifndef DAUC_CI_PHASED
-#define DAUC_CI_PHASED 1  // the unpipelined loop: every query's LDS reads of a phase issued together
-#endif
-#ifndef DAUC_CI_U
-#define DAUC_CI_U (DAUC_CI_PIPE ? 1 : 2)  // float4 slots per thread per group (int8 labels)
-#endif
-#ifndef DAUC_CI_ABLATE2
-#define DAUC_CI_ABLATE2 0  // timing ablations only (wrong counts): 1 every window at the table's start,
-                           // 2 the LDS lookups at lane-uniform addresses (same dependency chain), 3 both
-#endif
-#ifndef DAUC_CI_LATEWIN
-#define DAUC_CI_LATEWIN 0  // 1: count the previous group before issuing this group's window loads
-#endif
-#ifndef DAUC_CI_MED3
-#define DAUC_CI_MED3 0  // 1 (with W2): the window counts by v_med3_u32, branch-free
-#endif
-#ifndef DAUC_CI_W2
-#define DAUC_CI_W2 1  // 1: the second window of a cell past its first loaded with the first (no branch)
-#endif
-#ifndef DAUC_CI_COUNT3
-#define DAUC_CI_COUNT3 0  // 1: branch-free window counts by min/max (no compare into SGPRs)
-#endif
-#ifndef DAUC_CI_DEPTH
-#define DAUC_CI_DEPTH 1  // groups of stream loads in flight ahead of the group being located
-#endif
 
 // The labeled query pass over the count index (same stream and checks as query_labeled_kernel);
 // returns at once when the builder kept the tree, so it is enqueued unconditionally. Per
@@ -1569,7 +888,19 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
     const bool in_use = count_index_in_use(meta);
     if (Mp != nullptr) M = static_cast<int64_t>(*Mp);  // the direct build: the table size on the device
     if (verdict != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *verdict = in_use ? 1u : 2u;
-    if (!in_use) return;
+    if (!in_use) {
+        // no positives at all: nothing to count, but the queries are still checked for finiteness
+        // (sklearn raises on a non-finite score before its one-class warning, _ranking.py:868-869)
+        if (M == 0 && nonfinite != nullptr) {
+            unsigned nf = 0;
+            for (int64_t i = begin + int64_t(blockIdx.x) * kQueryThreads + threadIdx.x; i < end;
+                 i += int64_t(gridDim.x) * kQueryThreads)
+                nf += lab[i] != LT(1) && !isfinite(s[i]);
+            const unsigned long long nfw = wave_sum(static_cast<unsigned long long>(nf));
+            if ((threadIdx.x & (kWave - 1)) == 0 && nfw) atomicAdd(nonfinite, nfw);
+        }
+        return;
+    }
     extern __shared__ uint2 ci_lds[];
     const int nb = static_cast<int>(meta[kCiBlocks]);
     uint2* l1 = ci_lds;          // [2048]
@@ -1628,7 +959,6 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
     const int64_t nvec = end > head ? (end - head) / 4 : 0;
     const bool aligned = (reinterpret_cast<uintptr_t>(s + head) & 15u) == 0 &&
                          (reinterpret_cast<uintptr_t>(lab + head) & (4 * sizeof(LT) - 1)) == 0;
-#if DAUC_CI_PIPE
     if (aligned) {
         // Software-pipelined over groups of NQ queries (U float4 slots per thread): the LDS lookups
         // of group g run while group g-1's window loads and group g+1's stream loads are in
@@ -1636,7 +966,7 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
         // issue order: keys(g) [waits for the stream loads issued one group earlier], stream
         // loads of g+1, LDS lookups of g, window loads of g, count of g-1 [waits for the windows
         // issued one group earlier; the younger loads stay in flight: vmcnt retires in order].
-        constexpr int U = sizeof(LT) == 1 ? DAUC_CI_U : 1;
+        constexpr int U = 1;  // one float4 slot per lane per group (more slots spill registers)
         constexpr int NQ = 4 * U;
         const int64_t step = int64_t(U) * stride;
         // two sets of every per-group register (A and B, used alternately by an unrolled pair of
@@ -1665,9 +995,7 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
         struct Group {
             unsigned x[NQ], rc[NQ];
             uint4 k[NQ];
-#if DAUC_CI_W2
             uint4 k2[NQ];  // the next window, for cells that run past the first
-#endif
             unsigned use;
         };
         auto keys = [&](Group& g, const Stream& sg) {
@@ -1690,13 +1018,13 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
         auto locate_lds = [&](Group& g) {
             uint2 e[NQ];
 #pragma unroll
-            for (int q = 0; q < NQ; ++q) e[q] = l1[(DAUC_CI_ABLATE2 & 2) ? (g.x[q] >> 31) : (g.x[q] >> kCiLowBits)];
+            for (int q = 0; q < NQ; ++q) e[q] = l1[g.x[q] >> kCiLowBits];
             unsigned c[NQ];
 #pragma unroll
             for (int q = 0; q < NQ; ++q) c[q] = ci_cell(g.x[q], e[q]);
             uint2 b[NQ];
 #pragma unroll
-            for (int q = 0; q < NQ; ++q) b[q] = blk[(DAUC_CI_ABLATE2 & 2) ? (c[q] & 1u) : (c[q] / kCiBlock)];
+            for (int q = 0; q < NQ; ++q) b[q] = blk[c[q] / kCiBlock];
 #pragma unroll
             for (int q = 0; q < NQ; ++q) {
                 const unsigned sh = 4u * (c[q] % kCiBlock);
@@ -1705,23 +1033,14 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
                 const unsigned rl = b[q].x + __builtin_amdgcn_sad_u8(bytes, 0u, 0u);
                 const unsigned cnt = __builtin_amdgcn_ubfe(b[q].y, sh, 4u);
                 g.rc[q] = rl | (cnt << 28);
-                if (DAUC_CI_ABLATE2 & 2)  // keep ~half the lanes gathering at spread positions
-                    g.rc[q] = ((g.x[q] * 2654435761u) % (M32 + 1u)) | ((((g.x[q] >> 7) & 1u) | (rl >> 31)) << 28);
             }
         };
         auto locate_win = [&](Group& g) {
 #pragma unroll
             for (int q = 0; q < NQ; ++q) {
                 const unsigned rl = g.rc[q] & 0x0fffffffu;
-#if DAUC_CI_COUNT3
-                // every lane loads the window at rank_lo & ~3, an empty cell's too: its keys before
-                // rank_lo are of earlier cells (< x), the others of later cells or padding (> x)
-                g.k[q] = *reinterpret_cast<const uint4*>(sorted + (rl & ~3u));
-#else
-                g.k[q] = win_load(sorted + (((g.rc[q] >> 28) && !(DAUC_CI_ABLATE2 & 1)) ? rl & ~3u : 0u));
-#endif
+                g.k[q] = win_load(sorted + ((g.rc[q] >> 28) ? rl & ~3u : 0u));
             }
-#if DAUC_CI_W2
             // A cell that runs past its first window ((rank_lo & 3) + count > 4: ~7 % of the queries
             // at 1.1 cells per key) also loads the next one here, in the same straight-line issue: as
             // a branch after the count it was waited for with vmcnt(0) -- every load in flight,
@@ -1730,123 +1049,22 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
 #pragma unroll
             for (int q = 0; q < NQ; ++q) {
                 const unsigned rl = g.rc[q] & 0x0fffffffu, cnt = g.rc[q] >> 28;
-                g.k2[q] = win_load(sorted + ((rl & 3u) + cnt > 4u && !(DAUC_CI_ABLATE2 & 1) ? (rl & ~3u) + 4u : 0u));
+                g.k2[q] = win_load(sorted + ((rl & 3u) + cnt > 4u ? (rl & ~3u) + 4u : 0u));
             }
-#endif
         };
         auto locate = [&](Group& g) {
             locate_lds(g);
             locate_win(g);
         };
-#if DAUC_CI_COUNT3
-        // Branch-free counts, no compare results in scalar registers: with med(k, lo, hi) =
-        // min(max(k, lo), hi), med(k, x, x+1) - x = [k > x] and med(k, x-1, x) - (x-1) = [k >= x],
-        // so s1 = sum med(k, x, x+1) = 4x + #(> x), s2 = sum med(k, x-1, x) = 4x - 4 + #(>= x) and
-        // W += M - (a + #(<= x)) = M - 4 - a - 4x + s1, T += #(<= x) - #(< x) = s2 - s1 + 4 (mod 2^32;
-        // a NaN query's key may wrap x +- 1, and a NaN makes the evaluation an error anyway).
-        // Positive-label queries are masked out (m = 0).
         auto count = [&](const Group& g) {
             unsigned wl = 0u, tl = 0u;
             bool more = false;
-#pragma unroll
-            for (int q = 0; q < NQ; ++q) {
-                const unsigned x = g.x[q], xp = x + 1u, xm = x - 1u;
-                const unsigned rl = g.rc[q] & 0x0fffffffu, cnt = g.rc[q] >> 28, a = rl & ~3u;
-                const uint4 k = g.k[q];
-                auto med = [](unsigned v, unsigned lo, unsigned hi) { return min(max(v, lo), hi); };
-                const unsigned s1 = (med(k.x, x, xp) + med(k.y, x, xp)) + (med(k.z, x, xp) + med(k.w, x, xp));
-                const unsigned s2 = (med(k.x, xm, x) + med(k.y, xm, x)) + (med(k.z, xm, x) + med(k.w, xm, x));
-                const unsigned m = 0u - ((g.use >> q) & 1u);
-                wl += (M32 - 4u - a - 4u * x + s1) & m;
-                tl += (s2 - s1 + 4u) & m;
-                more |= ((g.use >> q) & 1u) && (rl & 3u) + cnt > 4u;
-            }
-            w += wl;
-            t += tl;
-            if (more) {
-#pragma unroll
-                for (int q = 0; q < NQ; ++q) {
-                    const unsigned rl = g.rc[q] & 0x0fffffffu, cnt = g.rc[q] >> 28;
-                    if (((g.use >> q) & 1u) && (rl & 3u) + cnt > 4u) ci_fix(g.x[q], rl, cnt, g.k[q], sorted, w, t);
-                }
-            }
-        };
-#elif DAUC_CI_MED3 && DAUC_CI_W2
-        // The counts of both windows by v_med3_u32 (no compare into a scalar register, no hazard
-        // wait, no branch): med3(k, x, x+1) - x = [k > x], med3(k, x-1, x) - (x-1) = [k >= x]
-        // (x +- 1 wraps only for a NaN query's key, and a NaN makes the evaluation an error).
-        // Masks as 0 / ~0 words: m0 the cell holds keys (else window 1 is the table's first, read
-        // as padding: base = rank_lo, no keys counted), m2 the cell runs into window 2, mu a
-        // negative-label query.
-        auto count = [&](const Group& g) {
-            auto med3 = [](unsigned v, unsigned lo, unsigned hi) {
-                unsigned r;
-                asm("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(v), "v"(lo), "v"(hi));
-                return r;
-            };
-            unsigned wl = 0u, tl = 0u;
-            bool more8 = false;
-#pragma unroll
-            for (int q = 0; q < NQ; ++q) {
-                const unsigned x = g.x[q], xp = x + 1u, xm = x - 1u, x4 = x << 2;
-                const unsigned rl = g.rc[q] & 0x0fffffffu, cnt = g.rc[q] >> 28, span = (rl & 3u) + cnt;
-                const uint4 k = g.k[q], k2 = g.k2[q];
-                // #(> x) and #(>= x) of each window
-                const unsigned gt1 = med3(k.x, x, xp) + med3(k.y, x, xp) + med3(k.z, x, xp) + med3(k.w, x, xp) - x4;
-                const unsigned ge1 = med3(k.x, xm, x) + med3(k.y, xm, x) + med3(k.z, xm, x) + med3(k.w, xm, x) - x4 + 4u;
-                const unsigned gt2 = med3(k2.x, x, xp) + med3(k2.y, x, xp) + med3(k2.z, x, xp) + med3(k2.w, x, xp) - x4;
-                const unsigned ge2 = med3(k2.x, xm, x) + med3(k2.y, xm, x) + med3(k2.z, xm, x) + med3(k2.w, xm, x) - x4 + 4u;
-                const unsigned m0 = 0u - min(cnt, 1u);
-                const unsigned m2 = 0u - min((span + 3u) >> 3, 1u);
-                const unsigned mu = 0u - ((g.use >> q) & 1u);
-                // #(<= x) = 4 - gt, #(< x) = 4 - ge; W = M - base - #(<= x), T = #(<= x) - #(< x) = ge - gt
-                const unsigned base = rl - ((rl & 3u) & m0);
-                const unsigned le = ((4u - gt1) & m0) + ((4u - gt2) & m2);
-                const unsigned tie = ((ge1 - gt1) & m0) + ((ge2 - gt2) & m2);
-                wl += (M32 - base - le) & mu;
-                tl += tie & mu;
-                more8 |= ((g.use >> q) & 1u) && span > 8u;
-            }
-            w += wl;
-            t += tl;
-            if (more8) {  // a cell of 6+ keys across both windows: rare (the nibble caps it at 14)
-#pragma unroll
-                for (int q = 0; q < NQ; ++q) {
-                    const unsigned rl = g.rc[q] & 0x0fffffffu, cnt = g.rc[q] >> 28;
-                    if (((g.use >> q) & 1u) && (rl & 3u) + cnt > 8u) {
-                        const unsigned x = g.x[q];
-                        const uint4 k2 = g.k2[q];
-                        w += (k2.x <= x) + (k2.y <= x) + (k2.z <= x) + (k2.w <= x);
-                        t -= ((k2.x <= x) + (k2.y <= x) + (k2.z <= x) + (k2.w <= x)) -
-                             ((k2.x < x) + (k2.y < x) + (k2.z < x) + (k2.w < x));
-                        ci_fix(x, rl, cnt, g.k[q], sorted, w, t);
-                    }
-                }
-            }
-        };
-#else
-        auto count = [&](const Group& g) {
-            unsigned wl = 0u, tl = 0u;
-            bool more = false;
-            if (DAUC_CI_ABLATE2 & 4) {  // timing ablation: the windows consumed, nothing counted
-#pragma unroll
-                for (int q = 0; q < NQ; ++q) {
-                    wl += g.k[q].x ^ g.k[q].w;
-#if DAUC_CI_W2
-                    tl += g.k2[q].y ^ g.k2[q].z;
-#endif
-                }
-                w += wl;
-                t += tl;
-                return;
-            }
 #pragma unroll
             for (int q = 0; q < NQ; ++q) {
                 // an empty cell's lane loaded the table's first window: counted as +inf padding
                 const uint4 k = (g.rc[q] >> 28) ? g.k[q] : uint4{kPadKey, kPadKey, kPadKey, kPadKey};
                 more |= ci_count(g.x[q], (g.use >> q) & 1u, g.rc[q] & 0x0fffffffu, g.rc[q] >> 28, k, M32, wl, tl);
             }
-#if DAUC_CI_W2
             // the second window's keys (those of the cell and of later cells; past the cell they
             // are > x): W -= #(<= x), T += #(<= x) - #(< x); a lane without one adds nothing
             bool more8 = false;
@@ -1880,133 +1098,14 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
                 }
             }
             (void)more;
-#else
-            w += wl;
-            t += tl;
-            if (more) {
-#pragma unroll
-                for (int q = 0; q < NQ; ++q) {
-                    const unsigned rl = g.rc[q] & 0x0fffffffu, cnt = g.rc[q] >> 28;
-                    if (((g.use >> q) & 1u) && (rl & 3u) + cnt > 4u) ci_fix(g.x[q], rl, cnt, g.k[q], sorted, w, t);
-                }
-            }
-#endif
         };
-#endif
-#if DAUC_CI_PIPE == 2
-        // Four stages, each group one stage further per iteration, so that no LDS read or window
-        // load is waited for in the iteration that issues it. Per iteration j, in this order:
-        // D(j-1) the count [its windows were issued 3/4 of an iteration earlier], C(j) the block
-        // word decode + the window loads [block words read 3/4 earlier], B(j+1) the cells + the
-        // block-word reads [l1 entries read 3/4 earlier], A(j+2) the keys + the l1 reads [stream
-        // loads issued D groups earlier]. Every stage reads its input slot before the stage
-        // before it refills the slot: one slot per stage. Groups past the lane's last are
-        // bubbles (their loads re-read slot 0, labels positive).
-        struct SA {
-            unsigned x[NQ], use;
-            uint2 e[NQ];
-        };
-        struct SB {
-            unsigned x[NQ], use, c[NQ];
-            uint2 b[NQ];
-        };
-        struct SC {
-            unsigned x[NQ], use, rc[NQ];
-            uint4 k[NQ];
-        };
-        auto stA = [&](SA& a, const Stream& sg) {
-            Group g;
-            keys(g, sg);
-#pragma unroll
-            for (int q = 0; q < NQ; ++q) {
-                a.x[q] = g.x[q];
-                a.e[q] = l1[(DAUC_CI_ABLATE2 & 2) ? (a.x[q] >> 31) : (a.x[q] >> kCiLowBits)];
-            }
-            a.use = g.use;
-        };
-        auto stB = [&](SB& b, const SA& a) {
-#pragma unroll
-            for (int q = 0; q < NQ; ++q) {
-                b.x[q] = a.x[q];
-                b.c[q] = ci_cell(a.x[q], a.e[q]);
-                b.b[q] = blk[(DAUC_CI_ABLATE2 & 2) ? (b.c[q] & 1u) : (b.c[q] / kCiBlock)];
-            }
-            b.use = a.use;
-        };
-        auto stC = [&](SC& c, const SB& b) {
-#pragma unroll
-            for (int q = 0; q < NQ; ++q) {
-                c.x[q] = b.x[q];
-                const unsigned sh = 4u * (b.c[q] % kCiBlock);
-                const unsigned below = __builtin_amdgcn_ubfe(b.b[q].y, 0u, sh);
-                const unsigned bytes = (below & 0x0f0f0f0fu) + ((below >> 4) & 0x0f0f0f0fu);
-                const unsigned rl = b.b[q].x + __builtin_amdgcn_sad_u8(bytes, 0u, 0u);
-                const unsigned cnt = __builtin_amdgcn_ubfe(b.b[q].y, sh, 4u);
-                c.rc[q] = rl | (cnt << 28);
-            }
-#pragma unroll
-            for (int q = 0; q < NQ; ++q) {
-                const unsigned rl = c.rc[q] & 0x0fffffffu;
-                c.k[q] = *reinterpret_cast<const uint4*>(sorted + (((c.rc[q] >> 28) && !(DAUC_CI_ABLATE2 & 1)) ? rl & ~3u : 0u));
-            }
-            c.use = b.use;
-        };
-        auto stD = [&](const SC& c) {
-            Group g;
-#pragma unroll
-            for (int q = 0; q < NQ; ++q) {
-                g.x[q] = c.x[q];
-                g.rc[q] = c.rc[q];
-                g.k[q] = c.k[q];
-            }
-            g.use = c.use;
-            count(g);
-        };
-        constexpr int D = DAUC_CI_DEPTH;
-        const int64_t ng = nvec > tid ? (nvec - tid + step - 1) / step : 0;  // this lane's groups
-        Stream sbuf[D];
-        SA sa;
-        SB sb;
-        SC sc;
-        auto vof = [&](int64_t g) { return tid + g * step; };
-#pragma unroll
-        for (int g = 0; g < D; ++g) load(sbuf[g], vof(g));
-        // prologue: A(0); B(0) A(1); C(0) B(1) A(2)
-        stA(sa, sbuf[0]);
-        load(sbuf[0], vof(D));
-        asm volatile("" ::: "memory");
-        stB(sb, sa);
-        stA(sa, sbuf[1 % D]);
-        load(sbuf[1 % D], vof(1 + D));
-        asm volatile("" ::: "memory");
-        stC(sc, sb);
-        stB(sb, sa);
-        stA(sa, sbuf[2 % D]);
-        load(sbuf[2 % D], vof(2 + D));
-        asm volatile("" ::: "memory");
-        int64_t j = 1;
-        for (;;) {
-#pragma unroll
-            for (int u = 0; u < D; ++u) {
-                // j = 1 + u (mod D): the stream buffer of group j + 2 is (3 + u) % D
-                if (j > ng) goto ci_stream_done;
-                stD(sc);
-                stC(sc, sb);
-                stB(sb, sa);
-                stA(sa, sbuf[(3 + u) % D]);
-                load(sbuf[(3 + u) % D], vof(j + 2 + D));
-                asm volatile("" ::: "memory");
-                ++j;
-            }
-        }
-#else
         // per group g: keys(g) [its stream loads were issued D groups earlier], stream loads of
         // g + D into the buffer just read, LDS lookups + window loads of g, count of g - 1 [its
         // windows were issued one group earlier; the younger loads stay in flight: vmcnt retires
         // in order]. D stream buffers keep D groups of score/label loads in flight per lane: with
         // one (D = 1) a wave holds 20 B per lane in flight, 5 MB over the chip, which at HBM's
         // loaded latency caps the stream far below the bandwidth.
-        constexpr int D = DAUC_CI_DEPTH;
+        constexpr int D = 1;
         constexpr int L = D % 2 == 0 ? D : 2 * D;  // unroll: every buffer index compile-time
         Stream sbuf[D];
         Group gbuf[2];
@@ -2029,113 +1128,16 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
                 keys(gc, sbuf[(j + 1) % D]);
                 load(sbuf[(j + 1) % D], v + int64_t(D) * step);
                 asm volatile("" ::: "memory");  // the stream loads stay older than this group's windows
-#if DAUC_CI_LATEWIN
-                // the previous group is counted before this group's windows are issued: one group's
-                // windows in registers at a time (they were issued 3/4 of an iteration earlier)
-                locate_lds(gc);
-                count(gp);
-                asm volatile("" ::: "memory");
-                locate_win(gc);
-#else
                 locate(gc);
                 count(gp);
-#endif
                 v += step;
             }
         }
-#endif
     ci_stream_done:;
     } else {
         for (int64_t v = tid; v < nvec; v += stride)
             for (int q = 0; q < 4; ++q) one(head + v * 4 + q);
     }
-#else
-    if (aligned) {
-        constexpr int U = sizeof(LT) == 1 ? DAUC_CI_U : 1;
-        constexpr int NQ = 4 * U;
-        f32x4 fc[U], fn[U];
-        LabelWords<LT> lc[U], ln[U];
-        auto load = [&](int64_t v0, f32x4 (&f)[U], LabelWords<LT> (&l)[U]) {
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int64_t v = v0 + int64_t(u) * stride;
-                if (v < nvec) {
-                    const int64_t i = head + v * 4;
-                    f[u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(s + i));
-                    l[u].load(lab + i);
-                } else {
-                    f[u] = f32x4{0.f, 0.f, 0.f, 0.f};
-                    l[u].set_positive();
-                }
-            }
-        };
-        load(tid, fc, lc);
-        for (int64_t v0 = tid; v0 < nvec; v0 += int64_t(U) * stride) {
-            unsigned x[NQ], rl[NQ], cnt[NQ];
-            bool use[NQ];
-            uint4 k[NQ];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const float f[4] = {fc[u].x, fc[u].y, fc[u].z, fc[u].w};
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    use[4 * u + q] = lc[u].not_positive(q);
-                    x[4 * u + q] = key_fast(f[q]);
-                    nf += use[4 * u + q] && !isfinite(f[q]);
-                }
-            }
-#if DAUC_CI_PHASED
-            {
-                uint2 e[NQ], b[NQ];
-                unsigned c[NQ];
-#pragma unroll
-                for (int q = 0; q < NQ; ++q) e[q] = l1[x[q] >> kCiLowBits];
-#pragma unroll
-                for (int q = 0; q < NQ; ++q) c[q] = ci_cell(x[q], e[q]);
-#pragma unroll
-                for (int q = 0; q < NQ; ++q) b[q] = blk[c[q] / kCiBlock];
-#pragma unroll
-                for (int q = 0; q < NQ; ++q) {
-                    const unsigned sh = 4u * (c[q] % kCiBlock);
-                    const unsigned below = __builtin_amdgcn_ubfe(b[q].y, 0u, sh);
-                    const unsigned bytes = (below & 0x0f0f0f0fu) + ((below >> 4) & 0x0f0f0f0fu);
-                    rl[q] = b[q].x + __builtin_amdgcn_sad_u8(bytes, 0u, 0u);
-                    cnt[q] = __builtin_amdgcn_ubfe(b[q].y, sh, 4u);
-                }
-#pragma unroll
-                for (int q = 0; q < NQ; ++q) {
-                    const uint4 kk = *reinterpret_cast<const uint4*>(sorted + (cnt[q] ? rl[q] & ~3u : 0u));
-                    k[q] = cnt[q] ? kk : uint4{kPadKey, kPadKey, kPadKey, kPadKey};
-                }
-            }
-#else
-#pragma unroll
-            for (int q = 0; q < NQ; ++q) ci_locate(x[q], l1, blk, sorted, rl[q], cnt[q], k[q]);
-#endif
-            asm volatile("" ::: "memory");
-            load(v0 + int64_t(U) * stride, fn, ln);
-            unsigned wl = 0u, tl = 0u;
-            bool more = false;
-#pragma unroll
-            for (int q = 0; q < NQ; ++q) more |= ci_count(x[q], use[q], rl[q], cnt[q], k[q], M32, wl, tl);
-            w += wl;
-            t += tl;
-            if (more) {
-#pragma unroll
-                for (int q = 0; q < NQ; ++q)
-                    if (use[q] && (rl[q] & 3u) + cnt[q] > 4u) ci_fix(x[q], rl[q], cnt[q], k[q], sorted, w, t);
-            }
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                fc[u] = fn[u];
-                lc[u] = ln[u];
-            }
-        }
-    } else {
-        for (int64_t v = tid; v < nvec; v += stride)
-            for (int q = 0; q < 4; ++q) one(head + v * 4 + q);
-    }
-#endif
     for (int64_t i = head + nvec * 4 + tid; i < end; i += stride) one(i);
     __shared__ unsigned long long red[3][kQueryThreads / kWave];
     w = wave_sum(w);
@@ -2368,15 +1370,9 @@ __global__ __launch_bounds__(kQueryThreads) void query_labeled_kernel(const floa
                                                                      const unsigned* __restrict__ sorted,
                                                                      int64_t M, unsigned long long* __restrict__ out,
                                                                      unsigned long long* __restrict__ nonfinite,
-                                                                     const unsigned* __restrict__ meta, int force) {
-    // meta: the slot-cell index's (force = 1, tuning builds) or the count index's (force = 0)
-    // builder verdict
-#ifdef DAUC_TUNING
-    if (meta != nullptr && (force ? cells_in_use(meta, M, 1) : count_index_in_use(meta))) return;
-#else
-    (void)force;
+                                                                     const unsigned* __restrict__ meta) {
+    // meta: the count index's builder verdict (the tree runs only when the index is not used)
     if (meta != nullptr && count_index_in_use(meta)) return;
-#endif
     extern __shared__ TreeNode tree[];
     for (int i = threadIdx.x; i < g.nodes; i += kQueryThreads) tree[i] = gtree[i];
     const TopKeys top = load_top(gtree, g, sorted, k);
@@ -2402,7 +1398,7 @@ __global__ __launch_bounds__(kQueryThreads) void query_labeled_kernel(const floa
         // before this one's walks: each walk is a chain of dependent LDS reads and a bucket load,
         // so without this the stream's HBM latency sits between every two iterations of a wave.
         // slots per iteration (prefetched one iteration ahead): register-bound
-        constexpr int U = sizeof(LT) == 8 ? 2 : (pipelined<K>() ? (sizeof(LT) == 1 ? DAUC_QUERY_PIPE_U : 2) : 4);
+        constexpr int U = sizeof(LT) == 8 ? 2 : 4;
         f32x4 fc[U], fn[U];
         LabelWords<LT> lc[U], ln[U];
         auto load = [&](int64_t v0, f32x4 (&f)[U], LabelWords<LT> (&l)[U]) {
@@ -2430,30 +1426,13 @@ __global__ __launch_bounds__(kQueryThreads) void query_labeled_kernel(const floa
                     nf += neg[q] && !isfinite(f[q]);
                 }
             };
-            if constexpr (pipelined<K>()) {
-                // every slot's walk and bucket load first, THEN the next iteration's stream loads,
-                // then the compares: vmcnt retires loads in issue order, so a wait for a bucket
-                // load issued after a streaming load would also wait out that load's HBM latency
-                bool neg[U][4];
-                unsigned x[U][4], su[U][4], bv[U][4][K > 0 ? K : 1];
+            load(v0 + int64_t(U) * stride, fn, ln);
 #pragma unroll
-                for (int u = 0; u < U; ++u) keys(u, x[u], neg[u]);
-#pragma unroll
-                for (int u = 0; u < U; ++u) walk_and_load<K>(x[u], su[u], bv[u], tree, g, top, sorted);
-                asm volatile("" ::: "memory");
-                load(v0 + int64_t(U) * stride, fn, ln);
-#pragma unroll
-                for (int u = 0; u < U; ++u)
-                    finish_counts<K, true>(x[u], neg[u], su[u], bv[u], tree, g, top, sorted, M, w, t);
-            } else {
-                load(v0 + int64_t(U) * stride, fn, ln);
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    bool neg[4];
-                    unsigned x[4];
-                    keys(u, x, neg);
-                    count4<K, true>(x, neg, tree, g, top, k, sorted, M, w, t);
-                }
+            for (int u = 0; u < U; ++u) {
+                bool neg[4];
+                unsigned x[4];
+                keys(u, x, neg);
+                count4<K, true>(x, neg, tree, g, top, k, sorted, M, w, t);
             }
 #pragma unroll
             for (int u = 0; u < U; ++u) {
@@ -2519,7 +1498,7 @@ int query_grid(int64_t L) {
         }
     }
     int64_t g = (L + 4 * kQueryThreads - 1) / (4 * kQueryThreads);
-    if (g > DAUC_QUERY_BLOCKS_PER_CU * cus) g = DAUC_QUERY_BLOCKS_PER_CU * cus;  // 1024-thread workgroups
+    if (g > 1 * cus) g = 1 * cus;  // 1024-thread workgroups
     if (g < 1) g = 1;
     return static_cast<int>(g);
 }
@@ -2621,41 +1600,6 @@ int radix_sort_keys(const float* neg, int64_t N, const SortWs& w, hipStream_t st
     return DAUC_OK;
 }
 
-CellWs carve_cells(void* p) {
-    char* c = static_cast<char*>(p);
-    CellWs w;
-    w.meta = reinterpret_cast<unsigned*>(c);
-    c += 256;
-    w.l1 = reinterpret_cast<unsigned*>(c);
-    c += size_t(kTop) * 4;
-    w.base = reinterpret_cast<unsigned*>(c);
-    c += ((size_t(kMaxCells) + 2) * 4 + 255) / 256 * 256;
-    w.slots = reinterpret_cast<uint4*>(c);
-    return w;
-}
-
-#ifdef DAUC_TUNING
-// plan + fill of the cell index behind the sort (2 launches; the verdict stays on the device)
-int prepare_cells(const unsigned* sorted, int64_t M, const CellWs& cw, int mu_max, hipStream_t st) {
-    hipLaunchKernelGGL(cell_plan_kernel, dim3(1), dim3(kCellPlanThreads), 0, st, sorted, M, mu_max, cw.l1, cw.meta);
-    hipLaunchKernelGGL(cell_fill_kernel, dim3(static_cast<unsigned>((M + 1 + 255) / 256)), dim3(256), 0, st, sorted, M,
-                       cw.l1, cw.meta, cw.base, cw.slots);
-    return launch_status();
-}
-
-template <typename LT>
-int launch_cells(const float* s, const LT* lab, int64_t begin, int64_t end, const CellWs& cw, int force,
-                 const unsigned* sorted, int64_t M, unsigned long long* out, unsigned long long* nonfinite,
-                 hipStream_t st) {
-    const dim3 grid(query_grid(end - begin)), block(kQueryThreads);
-    const size_t lds = (size_t(kTop) + kMaxCells + 2) * 4;
-    hipLaunchKernelGGL((query_cells_kernel<LT>), grid, block, lds, st, s, lab, begin, end, cw.meta, force, cw.l1,
-                       cw.base, cw.slots, sorted, M, out, nonfinite);
-    return launch_status();
-}
-
-#endif
-
 CountWs carve_count(void* p) {
     char* c = static_cast<char*>(p);
     CountWs w;
@@ -2700,18 +1644,18 @@ char* after_tree_of(void* workspace, int64_t P) {
 }
 
 CountWs count_ws_of(void* workspace, int64_t P) {
-    return carve_count(after_tree_of(workspace, P) + ((kCellBytes + 255) / 256) * 256);
+    return carve_count(after_tree_of(workspace, P) + kGrpBytes);
 }
 
 template <typename LT>
 int launch_labeled(int k, const float* s, const LT* lab, int64_t begin, int64_t end, const TreeNode* tree,
                    const TreeGeom& g, const unsigned* sorted, int64_t M, unsigned long long* out, unsigned long long* nonfinite,
-                   const unsigned* meta, int force, hipStream_t st) {
+                   const unsigned* meta, hipStream_t st) {
     const dim3 grid(query_grid(end - begin)), block(kQueryThreads);
     const size_t lds = size_t(g.nodes) * sizeof(TreeNode);
 #define DAUC_QL(KV)                                                                                              \
     hipLaunchKernelGGL((query_labeled_kernel<KV, LT>), grid, block, lds, st, s, lab, begin, end, tree, g, k, \
-                       sorted, M, out, nonfinite, meta, force)
+                       sorted, M, out, nonfinite, meta)
     switch (k) {
         case 1: DAUC_QL(1); break;
         case 2: DAUC_QL(2); break;
@@ -2765,7 +1709,7 @@ int direct_hist_words() { return kCiTop; }
 
 int64_t direct_hist_offset(int64_t Mcap) {  // carve_count(...).first, relative to the workspace
     return int64_t(((sort_ws_bytes(Mcap) + 255) / 256) * 256 + ((kTreeBytes + 255) / 256) * 256 +
-                   ((kCellBytes + 255) / 256) * 256 + 256);
+                   kGrpBytes + 256);
 }
 
 int build_direct_index(const float* pos, const unsigned long long* Mp, int64_t Mcap, void* workspace,
@@ -2778,7 +1722,7 @@ int build_direct_index(const float* pos, const unsigned long long* Mp, int64_t M
     unsigned* table = w.keys_a;  // Mcap + 64 words: room for the +inf tail
     // the histogram aggregates 8 keys per thread in LDS; the count and scatter passes are chains of
     // dependent loads per key, so they take one key per thread per step (every chain in flight)
-    unsigned* grp = carve_cells(after_tree_of(workspace, Mcap)).l1;  // the slot-cell index is unused here
+    unsigned* grp = reinterpret_cast<unsigned*>(after_tree_of(workspace, Mcap));  // [kDirectMaxGroups]
     const auto blocks = [](int64_t keys, int64_t per, int64_t cap) {
         const int64_t b = (keys + per - 1) / per;
         return dim3(static_cast<unsigned>(b < cap ? b : cap));
@@ -2827,12 +1771,12 @@ using namespace dauc;
 extern "C" {
 
 size_t dauc_sort_workspace_size(int64_t n) {
-    return sort_ws_bytes(n < 1 ? 1 : n) + kTreeBytes + 256 + kCellBytes + 256 + kCountBytes + 256;
+    return sort_ws_bytes(n < 1 ? 1 : n) + kTreeBytes + 256 + kGrpBytes + kCountBytes + 256;
 }
 
 #ifdef DAUC_TUNING
 int dauc_set_search_mode(int mode) {
-    if (mode < 0 || mode > 2) return DAUC_EINVAL;
+    if (mode < 0 || mode > 1) return DAUC_EINVAL;
     g_search_mode = mode;
     return DAUC_OK;
 }
@@ -2898,26 +1842,12 @@ int dauc_auc_counts_sorted_labeled(const float* pos, int64_t P, const float* sco
     int rc = prepare_table(pos, P, workspace, st, &sorted, &tree, &k, &g, count ? nw.first : nullptr);
     if (rc) return rc;
     if (count && (rc = prepare_count(sorted, P, nw, st))) return rc;
-#ifdef DAUC_TUNING
-    const bool slot_cells = mode == 2 && P <= int64_t(kMaxCells) * kCellMuForced;
-    const CellWs cw = carve_cells(after_tree_of(workspace, P));
-    if (slot_cells && (rc = prepare_cells(sorted, P, cw, kCellMuForced, st))) return rc;
-#else
-    constexpr bool slot_cells = false;
-#endif
     const unsigned* meta = count ? nw.meta : nullptr;
     auto run = [&](auto* lab) {
-#ifdef DAUC_TUNING
-        if (slot_cells) {
-            int r = launch_labeled(k, scores, lab, begin, end, tree, g, sorted, P, wins_ties, nonfinite, cw.meta, 1, st);
-            return r ? r : launch_cells(scores, lab, begin, end, cw, 1, sorted, P, wins_ties, nonfinite, st);
-        }
-#endif
-        int r = launch_labeled(k, scores, lab, begin, end, tree, g, sorted, P, wins_ties, nonfinite, meta, 0, st);
+        int r = launch_labeled(k, scores, lab, begin, end, tree, g, sorted, P, wins_ties, nonfinite, meta, st);
         if (r == DAUC_OK && count) r = launch_ci(scores, lab, begin, end, nw, sorted, P, wins_ties, nonfinite, st);
         return r;
     };
-    (void)slot_cells;
     switch (label_dtype) {
         case DAUC_LABEL_I8: return run(static_cast<const int8_t*>(labels));
         case DAUC_LABEL_I32: return run(static_cast<const int32_t*>(labels));

@@ -107,11 +107,11 @@ int compact_positives_zeroing(const float* scores, const void* labels, int label
 // (P), stats[2] (non-finite positives), stats[3] (labels outside {-1, 1}) must be zero on entry
 // and stats[1] must hold `tag` (else no tile reserves or writes anything); block 0 zeroes
 // zero_next[0, 2, 3], sets zero_next[1] = next_tag, and zeroes zero3[0..3) (nullable) and
-// zero_w[0..nzero_w).
+// zero_w[0..nzero_w). At most `cap` positives are stored (stats[0] still counts them all).
 int compact_unordered(const float* scores, const void* labels, int label_dtype, int64_t n, float* pos_out,
                       unsigned long long* stats, unsigned long long tag, unsigned long long* zero_next,
                       unsigned long long next_tag, unsigned long long* zero3, unsigned* zero_w, int nzero_w,
-                      hipStream_t st);
+                      hipStream_t st, int64_t cap = INT64_MAX);
 
 // auc_sort.hip: the count index built straight from the unsorted positives (no radix sort, no
 // tree) and the labeled query pass over scores [begin, end); the table is ordered by cell only.

@@ -30,16 +30,7 @@ constexpr int kVec = 4;                                // elements per float4 sl
 // Geometry from the MI355X sweep (scripts/gpu_sweep_sur.sh, profiles/r01): 8 float4
 // slots per thread and 2 resident blocks per CU stream best (a narrow, deep window;
 // more resident blocks lose DRAM locality).
-#ifndef DAUC_SURROGATE_SLOTS
-#define DAUC_SURROGATE_SLOTS 8
-#endif
-#ifndef DAUC_SURROGATE_BPC
-#define DAUC_SURROGATE_BPC 2
-#endif
-constexpr int kSlots = DAUC_SURROGATE_SLOTS;           // float4 slots per thread per iteration
-#ifndef DAUC_SURROGATE_NTSTORE
-#define DAUC_SURROGATE_NTSTORE 1
-#endif
+constexpr int kSlots = 8;           // float4 slots per thread per iteration
 constexpr int kMaxBlocks = 2048;                       // partial slots in the workspace
 constexpr int kPerBlockIter = kThreads * kVec * kSlots;  // 8192 elements
 constexpr int kNumAcc = 6;                             // fp64 partials per thread / block
@@ -335,8 +326,7 @@ __global__ __launch_bounds__(kThreads) void surrogate_kernel(
                 const f32x4 g = visit4<CLASS_ONLY>(hv[k], yv[k], s, acc);
                 if (write_dh) {
                     f32x4* dst = reinterpret_cast<f32x4*>(dh + base + int64_t(k) * kThreads * kVec);
-                    if (DAUC_SURROGATE_NTSTORE) __builtin_nontemporal_store(g, dst);
-                    else *dst = g;
+                    __builtin_nontemporal_store(g, dst);
                 }
             }
         }
@@ -631,16 +621,8 @@ __device__ __forceinline__ bool wait_row(const unsigned long long* row, unsigned
 __device__ __forceinline__ unsigned long long realtime() { return __builtin_amdgcn_s_memrealtime(); }
 
 // REDUCE = false: the stream with its row stores and nobody reducing (a timing variant).
-// Waves per SIMD the register allocation must allow: the streaming chunk kernel alone runs at 8.
-#ifndef DAUC_TAIL_WAVES
-#define DAUC_TAIL_WAVES 1
-#endif
-// 1: the final reducer loads the other group totals before it waits on its own group
-#ifndef DAUC_TAIL_PREPOLL
-#define DAUC_TAIL_PREPOLL 0
-#endif
 template <typename YT, int S, int R, bool REDUCE, bool STAMPS>
-__global__ __launch_bounds__(kThreads, DAUC_TAIL_WAVES) void surrogate_tail_kernel(
+__global__ __launch_bounds__(kThreads, 1) void surrogate_tail_kernel(
     const float* __restrict__ h, const YT* __restrict__ y, int64_t B, double invB,
     const float* __restrict__ abalpha, const float* __restrict__ p_hat, float* __restrict__ dh, TailWs ws,
     double* __restrict__ out64, float* __restrict__ grad3, float* __restrict__ loss) {
@@ -670,10 +652,6 @@ __global__ __launch_bounds__(kThreads, DAUC_TAIL_WAVES) void surrogate_tail_kern
     const bool holds = final_red && threadIdx.x < nred - 1;  // thread t: group total t
     unsigned long long* st = STAMPS ? ws.stamps + nblocks + 8 * r : nullptr;
     if (STAMPS && threadIdx.x == 0) st[0] = realtime();
-#if DAUC_TAIL_PREPOLL
-    unsigned gp[kGran], gmiss = 0u;
-    if (holds) gmiss = poll_row(ws.gtot + threadIdx.x * kGran, tag, gp);
-#endif
     bool ok = true;
     double tot[kNumAcc];
 #pragma unroll
@@ -712,10 +690,8 @@ __global__ __launch_bounds__(kThreads, DAUC_TAIL_WAVES) void surrogate_tail_kern
 #pragma unroll
     for (int k = 0; k < kNumAcc; ++k) rest[k] = 0.0;
     if (holds) {
-#if !DAUC_TAIL_PREPOLL
         unsigned gp[kGran];
         const unsigned gmiss = poll_row(ws.gtot + threadIdx.x * kGran, tag, gp);
-#endif
         if (wait_row(ws.gtot + threadIdx.x * kGran, tag, gmiss, gp)) add_row(gp, rest);
         else ok = false;
     }
@@ -746,7 +722,7 @@ __global__ __launch_bounds__(kThreads, DAUC_TAIL_WAVES) void surrogate_tail_kern
 // us at 2^26) before the last row: after the last row lands one hop is left. PLAIN: the epoch is
 // read with a plain load (every read of it precedes the final's store; a later call reads it across
 // the kernel boundary). Same granules, epochs, bounded polls and fixed summation order as above.
-template <typename YT, int S, int R, int K, bool PLAIN, bool STAMPS, int WAVES = DAUC_TAIL_WAVES, bool REDUCE = true>
+template <typename YT, int S, int R, int K, bool PLAIN, bool STAMPS, int WAVES = 1, bool REDUCE = true>
 __global__ __launch_bounds__(kThreads, WAVES) void surrogate_tail_x_kernel(
     const float* __restrict__ h, const YT* __restrict__ y, int64_t B, int64_t nblocks, double invB,
     const float* __restrict__ abalpha, const float* __restrict__ p_hat, float* __restrict__ dh, TailWs ws,
@@ -888,7 +864,7 @@ inline TailPlan tail_plan(int64_t nblocks, int64_t L) {
 }
 
 template <typename YT, int S, bool STAMPS>
-__global__ __launch_bounds__(kThreads, DAUC_TAIL_WAVES) void surrogate_tail_early_kernel(
+__global__ __launch_bounds__(kThreads, 1) void surrogate_tail_early_kernel(
     const float* __restrict__ h, const YT* __restrict__ y, int64_t B, double invB,
     const float* __restrict__ abalpha, const float* __restrict__ p_hat, float* __restrict__ dh, TailWs ws,
     TailPlan plan, double* __restrict__ out64, float* __restrict__ grad3, float* __restrict__ loss) {
@@ -975,10 +951,7 @@ __global__ __launch_bounds__(kThreads, DAUC_TAIL_WAVES) void surrogate_tail_earl
 constexpr int kChunkSlots = 4;
 // reducers of the one-launch loss (16 / 32 / 64 / 128 / 256 measured at B = 2^26:
 // profiles/r02/surrogate_ab.jsonl; 64 and 128 tie, 16 is 3 us slower)
-#ifndef DAUC_SURROGATE_TAIL_REDUCERS
-#define DAUC_SURROGATE_TAIL_REDUCERS 64
-#endif
-constexpr int kTailReducers = DAUC_SURROGATE_TAIL_REDUCERS;
+constexpr int kTailReducers = 64;
 // the product's extra-reducer tail (surrogate_tail_x_kernel): 128 reducer workgroups, the final one
 // taking the grid's last 512 rows itself; at B = 2^26 (tuning variants 10-21, profiles/r03/a):
 // 92.3 us vs 94.4 for the 64 streaming reducers above, 88.2 for the stream with its row stores alone
@@ -1019,7 +992,7 @@ int launch_tail(const float* h, const YT* y, int64_t B, const float* abalpha, co
     return launch_status();
 }
 
-template <typename YT, int R, int K, bool PLAIN, bool STAMPS = false, int WAVES = DAUC_TAIL_WAVES, bool REDUCE = true>
+template <typename YT, int R, int K, bool PLAIN, bool STAMPS = false, int WAVES = 1, bool REDUCE = true>
 int launch_tail_x(const float* h, const YT* y, int64_t B, const float* abalpha, const float* p_hat, float* dh,
                   double* out64, float* grad3, float* loss, void* ws, size_t ws_bytes, hipStream_t st) {
     const int64_t nblocks = chunk_blocks(B);
@@ -1033,14 +1006,11 @@ int launch_tail_x(const float* h, const YT* y, int64_t B, const float* abalpha, 
 }
 
 // the lag of the early reducers: 2 x the resident workgroups (8 per CU on 256 CUs)
-#ifndef DAUC_TAIL_LAG
-#define DAUC_TAIL_LAG 4096
-#endif
 
 template <typename YT, bool STAMPS = false>
 int launch_tail_early(const float* h, const YT* y, int64_t B, const float* abalpha, const float* p_hat, float* dh,
                       double* out64, float* grad3, float* loss, void* ws, size_t ws_bytes, hipStream_t st,
-                      int64_t lag = DAUC_TAIL_LAG) {
+                      int64_t lag = 4096) {
     const int64_t nblocks = chunk_blocks(B);
     if (nblocks > 0x7fffffffLL) return DAUC_EINVAL;
     const TailPlan plan = tail_plan(nblocks, lag);
@@ -1087,7 +1057,7 @@ int resident_blocks() {
             (void)hipGetLastError();
             cached = kMaxBlocks;  // no device (e.g. size queries on a build host): upper bound
         } else {
-            per_cu = per_cu < DAUC_SURROGATE_BPC ? per_cu : DAUC_SURROGATE_BPC;
+            per_cu = per_cu < 2 ? per_cu : 2;
             cached = cus * per_cu;
         }
     }
@@ -1146,7 +1116,7 @@ int launch_surrogate(const float* h, int64_t hs, const YT* y, int64_t B, const f
         // stream nothing (one launch); the class sums keep the two-launch form
         if constexpr (!CLASS_ONLY)
             // int8 labels: the register bound of 8 waves per SIMD costs no spill (wider labels would spill)
-            return launch_tail_x<YT, kTailXReducers, kTailFinalRows, true, false, sizeof(YT) == 1 ? 8 : DAUC_TAIL_WAVES>(
+            return launch_tail_x<YT, kTailXReducers, kTailFinalRows, true, false, sizeof(YT) == 1 ? 8 : 1>(
                 h, y, B, abalpha, p_hat, dh, out64, grad3, loss, ws, ws_bytes, st);
         else
             return launch_chunk<YT, true>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, sums4, accumulate, ws,

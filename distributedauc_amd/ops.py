@@ -405,6 +405,46 @@ def auc_eval_enqueue(scores: torch.Tensor, labels: torch.Tensor, part: int, part
     return out
 
 
+def auc_slot_bytes(n: int, parts: int) -> int:
+    """Bytes of one rank's slot of the two-step sharded evaluation (dauc_auc_slot_bytes)."""
+    return int(_lib.load().dauc_auc_slot_bytes(int(n), int(parts)))
+
+
+def auc_eval_compact_part(scores: torch.Tensor, labels: torch.Tensor, part: int, parts: int,
+                          slot: torch.Tensor) -> torch.Tensor:
+    """Step 1 of the two-step sharded evaluation (dauc_auc_eval_compact_part): this rank's slice
+    of the labels compacted into `slot` (a contiguous uint8 tensor of auc_slot_bytes(n, parts)
+    bytes, 256-byte aligned, on the scores' device), enqueued with no host synchronisation."""
+    L, dev, lc, n, st, ws = _eval_args(scores, labels)
+    nb = auc_slot_bytes(n, parts)
+    if (slot.dtype != torch.uint8 or slot.numel() < nb or not slot.is_contiguous() or slot.device != dev
+            or slot.data_ptr() % 256):
+        raise ValueError(f"slot must be a contiguous, 256-byte aligned uint8 tensor of >= {nb} bytes on the scores' device")
+    check(L.dauc_auc_eval_compact_part(scores.data_ptr(), labels.data_ptr(), lc, n, int(part), int(parts),
+                                       slot.data_ptr(), ws.data_ptr(), ws.numel(), st), "dauc_auc_eval_compact_part")
+    return slot
+
+
+def auc_eval_query_part(scores: torch.Tensor, labels: torch.Tensor, part: int, parts: int, slots: torch.Tensor,
+                        out: torch.Tensor | None = None) -> torch.Tensor:
+    """Step 2 (dauc_auc_eval_query_part): the `parts` gathered slots (contiguous, rank order) become
+    the positive table; this rank's query range is counted. Returns the device int64 [8] record of
+    auc_eval_enqueue (verdict 2: every rank runs the blocking sorted path)."""
+    L, dev, lc, n, st, ws = _eval_args(scores, labels)
+    nb = auc_slot_bytes(n, parts)
+    if (slots.dtype != torch.uint8 or slots.numel() < nb * int(parts) or not slots.is_contiguous()
+            or slots.device != dev or slots.data_ptr() % 256):
+        raise ValueError("slots must be the contiguous, 256-byte aligned uint8 gather of every rank's slot")
+    if out is None:
+        out = torch.empty(8, dtype=torch.int64, device=dev)
+    elif out.dtype != torch.int64 or out.numel() < 8 or not out.is_contiguous() or out.device != dev:
+        raise ValueError("out must be a contiguous int64 tensor of >= 8 elements on the scores' device")
+    check(L.dauc_auc_eval_query_part(scores.data_ptr(), labels.data_ptr(), lc, n, int(part), int(parts),
+                                     slots.data_ptr(), out.data_ptr(), ws.data_ptr(), ws.numel(), st),
+          "dauc_auc_eval_query_part")
+    return out
+
+
 def auc_eval_counts_part(scores: torch.Tensor, labels: torch.Tensor, part: int, parts: int,
                          part_counts: torch.Tensor) -> tuple:
     """Part `part` of `parts` of the blocking evaluation (dauc_auc_eval_counts_part): every part
@@ -534,9 +574,8 @@ def sort_keys(scores: torch.Tensor) -> torch.Tensor:
 
 def set_search_mode(mode: int) -> None:
     """Search structure of the sort method (dauc_set_search_mode): 0 automatic (the count index
-    where the table fits it and is not skewed, else the LDS search tree), 1 the tree, 2 the
-    16-key-slot cell index (a measured, slower alternative). Same integers in every mode; for
-    tests and measurements."""
+    where the table fits it and is not skewed, else the LDS search tree), 1 the tree. Same
+    integers in both modes; for tests and measurements (tuning build)."""
     check(_lib.tuning().dauc_set_search_mode(int(mode)), "dauc_set_search_mode")
 
 
@@ -546,4 +585,7 @@ __all__ = [
     "surrogate_logits_fwdbwd", "class_sums_logits",
     "sort_keys", "auc_counts_sorted_labeled", "compact_positives", "mode_code", "workspaces", "set_search_mode",
     "auc_eval_enqueue",
+    "auc_slot_bytes",
+    "auc_eval_compact_part",
+    "auc_eval_query_part",
 ]

@@ -301,6 +301,29 @@ int dauc_auc_eval_counts_part(const float* scores, const void* labels, int label
                               int parts, int64_t* out, int64_t* part_counts, int64_t* pinned, void* workspace,
                               size_t workspace_bytes, dauc_stream_t stream);
 
+/*
+ * The sharded evaluation without a whole-vector compaction on every rank, in two enqueued steps
+ * around the caller's collective (no host synchronisation in either):
+ *   1. dauc_auc_eval_compact_part: the positives of THIS rank's slice of the labels (slices on
+ *      256-label boundaries) compacted, unordered, into `slot` (device, dauc_auc_slot_bytes(n,
+ *      parts) bytes, 256-byte aligned): a header {P_r, #non-finite positives, #labels not in
+ *      {-1, 1}, 0} (int64) at byte 0 and the scores from byte 256;
+ *   -- the caller all-gathers the `parts` slots, rank order, contiguous --
+ *   2. dauc_auc_eval_query_part: the gathered slots become the positive table (headers summed),
+ *      the count index is built from it and scores [part*n/parts, (part+1)*n/parts) are
+ *      counted; part_out (device int64[8]) = dauc_auc_eval_enqueue's record. A slot holds an
+ *      even share of the count index's capacity + 25 %: a slice with more positives (an
+ *      unshuffled test set), like a table the index cannot hold, gives verdict 2 -- the caller
+ *      then runs dauc_auc_eval_counts_part on every rank.
+ * Replaces the reference's rank-0 evaluation (main.py:232-250) with a sharded one.
+ */
+size_t dauc_auc_slot_bytes(int64_t n, int parts);
+int dauc_auc_eval_compact_part(const float* scores, const void* labels, int label_dtype, int64_t n, int part,
+                               int parts, void* slot, void* workspace, size_t workspace_bytes, dauc_stream_t stream);
+int dauc_auc_eval_query_part(const float* scores, const void* labels, int label_dtype, int64_t n, int part, int parts,
+                             const void* slots, int64_t* part_out, void* workspace, size_t workspace_bytes,
+                             dauc_stream_t stream);
+
 /* The radix sort alone: keys_out[0..n) = ascending order-preserving keys of scores (testing). */
 int dauc_sort_keys(const float* scores, int64_t n, unsigned* keys_out, void* workspace,
                    size_t workspace_bytes, dauc_stream_t stream);

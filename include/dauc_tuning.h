@@ -68,9 +68,7 @@ int dauc_pair_count_variant(const float* pos, int64_t P, const float* neg, int64
  *   0: the product's choice -- the count index for tables of up to 219,838 keys, unless the
  *      device finds the table skewed (a cell of 15+ keys, or more than 1.5 keys per cell): then,
  *      and for larger tables, the LDS search tree;
- *   1: the LDS search tree always;
- *   2: a 16-key-slot cell index wherever it fits (tables of up to 573,440 keys): measured slower
- *      than the tree (four lane gathers per query).
+ *   1: the LDS search tree always (the fallback's structure, tested on every table).
  */
 int dauc_set_search_mode(int mode);
 

@@ -1,6 +1,7 @@
 """Search-structure A/B for the sort method: the labeled query pass and the one-call evaluation
 at configs[3] (2^24 @ 1 %) and configs[4] (2^27 @ 0.1 %) in each dauc_set_search_mode
-(0 automatic, 1 tree, 2 cells), HIP events on the launch stream, same counts required.
+(0 automatic, 1 tree), HIP events on the launch stream, same counts required. Every call runs in
+the tuning build, whose search mode the switch sets (the product library ignores it).
 One JSON line per (config, mode)."""
 from __future__ import annotations
 
@@ -11,12 +12,14 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
-from distributedauc_amd import ops  # noqa: E402
+from distributedauc_amd import _lib, ops  # noqa: E402
 from distributedauc_amd.loader import synthetic_scores  # noqa: E402
 
 reps = int(sys.argv[1]) if len(sys.argv) > 1 else 20
-modes = [int(m) for m in (sys.argv[2] if len(sys.argv) > 2 else "1,2,0").split(",")]
+modes = [int(m) for m in (sys.argv[2] if len(sys.argv) > 2 else "1,0").split(",")]
 dev = torch.device("cuda", 0)
+_tuning = _lib.using(_lib.tuning())
+_tuning.__enter__()
 for log2n, pr in ((24, 0.01), (27, 0.001)):
     n = 1 << log2n
     s, y = synthetic_scores(n, pr, dev)
@@ -50,3 +53,4 @@ for log2n, pr in ((24, 0.01), (27, 0.001)):
                "counts": counts, "eval_counts": list(c[:2]), "agree": counts == ref and list(c[:2]) == counts[:2]}
         print(json.dumps(rec), flush=True)
 ops.set_search_mode(0)
+_tuning.__exit__(None, None, None)

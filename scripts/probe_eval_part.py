@@ -59,3 +59,28 @@ for log2n, pr in ((24, 0.01), (27, 0.001)):
         el = wall(lambda: ops.auc_eval_enqueue(s, y, G - 1, G, out=rec).tolist())
         print(json.dumps({"log2n": log2n, "G": G, "fn": "dauc_auc_eval_enqueue + record read", "ms_part0": e0,
                           "ms_last": el, "sum_matches_whole": (W, T) == (whole[0], whole[1])}), flush=True)
+        # round 4: the two-step form -- the rank compacts its slice into its slot, the slots are
+        # all-gathered (a device copy here, one GPU), it counts its query range from the gathered
+        # table; per rank: its own compaction + its query part + the record read (the two
+        # collectives are not on one GPU)
+        n = s.numel()
+        nb = ops.auc_slot_bytes(n, G)
+        slots = torch.empty(nb * G, dtype=torch.uint8, device=dev)
+        mine = torch.empty(nb, dtype=torch.uint8, device=dev)
+        for r in range(G):
+            ops.auc_eval_compact_part(s, y, r, G, mine)
+            slots[r * nb:(r + 1) * nb].copy_(mine)
+        W = T = 0
+        for r in range(G):
+            v = ops.auc_eval_query_part(s, y, r, G, slots, out=rec).tolist()
+            W, T = W + v[0], T + v[1]
+
+        def two_step(r):
+            ops.auc_eval_compact_part(s, y, r, G, mine)
+            return ops.auc_eval_query_part(s, y, r, G, slots, out=rec).tolist()
+
+        t0 = wall(lambda: two_step(0))
+        tl = wall(lambda: two_step(G - 1))
+        print(json.dumps({"log2n": log2n, "G": G, "fn": "two-step: compact_part + query_part + record read",
+                          "ms_part0": t0, "ms_last": tl, "slot_bytes": nb,
+                          "sum_matches_whole": (W, T) == (whole[0], whole[1])}), flush=True)

@@ -168,6 +168,71 @@ def auc_eval_enqueue(scores, labels, part, parts, out=None):
     return rec
 
 
+_INDEX_CAP = 219_838  # 3 / 2 x the count index's cells (auc_sort.hip direct_capacity)
+
+
+def _slot_cap(n, parts):
+    share = -(-n // parts)
+    fair = -(-min(n // 2 + 1, _INDEX_CAP) // parts)
+    return min(share, fair + fair // 4 + 64)
+
+
+def auc_slot_bytes(n, parts):
+    """dauc_auc_slot_bytes' stand-in (same formula)."""
+    return 256 + -(-_slot_cap(n, parts) * 4 // 256) * 256
+
+
+def _slice_lo(n, part, parts):
+    return 0 if part == 0 else (n if part >= parts else (n * part // parts) & ~255)
+
+
+def auc_eval_compact_part(scores, labels, part, parts, slot):
+    """dauc_auc_eval_compact_part's stand-in: header {P_r, #non-finite positives, #other labels, 0}
+    (int64) at byte 0, the slice's positive scores (in order) from byte 256, at most cap of them."""
+    s, y = scores.detach().numpy(), labels.numpy().astype(np.int64)
+    n = s.size
+    lo, hi = _slice_lo(n, part, parts), _slice_lo(n, part + 1, parts)
+    ss, yy = s[lo:hi], y[lo:hi]
+    pos = ss[yy == 1]
+    hdr = np.array([pos.size, int((~np.isfinite(pos)).sum()), int(((yy != 1) & (yy != -1)).sum()), 0], np.int64)
+    slot[:32] = torch.from_numpy(hdr.view(np.uint8).copy())
+    k = min(pos.size, _slot_cap(n, parts))
+    slot[256:256 + 4 * k] = torch.from_numpy(pos[:k].astype(np.float32).view(np.uint8).copy())
+    return slot
+
+
+def auc_eval_query_part(scores, labels, part, parts, slots, out=None):
+    """dauc_auc_eval_query_part's stand-in: the gathered slots' positives (verdict 2 when a slot
+    overflowed or the table exceeds the index), the part's queries counted; the enqueue record."""
+    s, y = scores.detach().numpy(), labels.numpy().astype(np.int64)
+    n = s.size
+    nb, cap = auc_slot_bytes(n, parts), _slot_cap(n, parts)
+    raw = slots.numpy()
+    P = nfpos = other = 0
+    over = False
+    pos = []
+    for r in range(parts):
+        h = raw[r * nb:r * nb + 32].view(np.int64)
+        P, nfpos, other = P + int(h[0]), nfpos + int(h[1]), other + int(h[2])
+        over |= int(h[0]) > cap
+        pos.append(raw[r * nb + 256:r * nb + 256 + 4 * min(int(h[0]), cap)].view(np.float32))
+    pos = np.concatenate(pos) if pos else np.zeros(0, np.float32)
+    lo, hi = n * part // parts, n * (part + 1) // parts
+    rec = torch.zeros(8, dtype=torch.int64) if out is None else out
+    rec.zero_()
+    rec[3], rec[5], rec[6] = P, nfpos, other
+    if hi <= lo:
+        return rec
+    verdict = 1 if (not over and 0 < P <= min(n // 2 + 1, _INDEX_CAP)) else 2
+    rec[7] = verdict
+    q = s[lo:hi][y[lo:hi] != 1]
+    rec[2] = int((~np.isfinite(q)).sum())
+    if verdict == 1 and not nfpos:
+        W, T = coracle_pair_count(pos, q[np.isfinite(q)]) if q.size else (0, 0)
+        rec[0], rec[1] = W, T
+    return rec
+
+
 def split_scores(scores, labels, negatives=True):
     """dauc_split_scores' stand-in: stable (pos, neg) buffers of capacity n and the stats
     {P, N, #non-finite scores, #labels not in {-1, 1}} (N counts every label != 1)."""
@@ -200,7 +265,8 @@ def install(monkeypatch):
 
     for name in ("label_map_phat", "surrogate_fwdbwd", "class_sums", "alpha_from_sums", "coda_finalize",
                  "scale_div", "pd_update", "compact_positives", "auc_counts_sorted_labeled", "auc_eval_counts",
-                 "auc_eval_counts_part", "auc_eval_enqueue", "split_scores", "pair_count"):
+                 "auc_eval_counts_part", "auc_eval_enqueue", "auc_slot_bytes", "auc_eval_compact_part",
+                 "auc_eval_query_part", "split_scores", "pair_count"):
         monkeypatch.setattr(ops, name, globals()[name])
     monkeypatch.setattr(flat, "_check_device", lambda dev: None)
 

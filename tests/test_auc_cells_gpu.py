@@ -5,9 +5,9 @@ The labeled query pass (dauc_auc_counts_sorted_labeled, and through it dauc_auc_
 locates every negative among the sorted positives through one of: the count index (mode 0, the
 default where it fits: top 11 key bits -> bucket, multiply-high -> cell, per-8-cell LDS words of
 base + nibble counts, one 16-byte window for non-empty cells; the device falls back to the tree
-for skewed tables), the LDS search tree (mode 1), or the 16-key-slot cell index (mode 2, a
-measured alternative). Every case here runs in all three modes, so the skewed cases also cover
-mode 0's device-side fallback. Bar: the integers (W, T) bit-exact against oracle/auc_oracle.c (sklearn's
+for skewed tables) or the LDS search tree (mode 1). Every case here runs in both modes, so the
+skewed cases also cover mode 0's device-side fallback. (Round 2's 16-key-slot cell index, a
+measured and slower alternative, was removed in round 4.) Bar: the integers (W, T) bit-exact against oracle/auc_oracle.c (sklearn's
 _binary_clf_curve counts, main.py:79-81) on the same scores.
 """
 from __future__ import annotations
@@ -20,7 +20,7 @@ from oracle import coracle
 
 pytestmark = pytest.mark.gpu
 
-MODES = (0, 1, 2)
+MODES = (0, 1)
 
 
 def T(a, dev):

@@ -1,7 +1,8 @@
-"""The sharded exact-AUC orchestration on CPU (gloo, world 2 and 3): every rank enqueues its
-part (all positives compacted and indexed locally, its slice of the scores streamed through
-the search), one all-gather of the 8-word part records, counts summed on the host, and the
-ranks' records checked to agree (a rank with another test set raises on every rank). Below
+"""The sharded exact-AUC orchestration on CPU (gloo, world 2 and 3): every rank compacts the
+positives of its slice of the labels into a slot, one all-gather of the slots, every rank counts
+its slice of the scores against the gathered table, one all-gather of the 8-word part records,
+counts summed on the host; a slot that overflows (an unshuffled test set) and a table the index
+cannot hold take the sorted path on every rank. Below
 ExactAUC.SHARD_MIN scores every rank evaluates the whole vector instead (same integers, no
 collective); both modes run here. The kernels are served by the oracle (tests/cpu_kernels.py);
 the GPU form runs in bench.py --gpus 2 (tests/test_bench_gpu.py)."""
@@ -51,12 +52,15 @@ def _worker(rank, world, port, q, shard_min):
             raised = True
         assert raised
         if ev.last_mode == "sharded":
-            # ranks holding different vectors: every rank raises (no hang, no mixed counts)
-            y3 = y.copy()
-            if rank == 1:
-                y3[np.flatnonzero(y == -1)[:5]] = 1
-            with pytest.raises(RuntimeError, match="disagree"):
-                ev.counts(torch.from_numpy(y3), torch.from_numpy(s), device="cpu")
+            # (round 4: every rank compacts only its slice, so ranks holding different vectors are
+            # no longer detected -- the caller passes identical vectors, as Evaluator's all-gather
+            # guarantees; the gathered slots give every rank the same P and label counts)
+            # an unshuffled test set: every positive in rank 0's slice overflows its slot -- the
+            # sorted path on every rank, same integers
+            y5 = np.where(np.arange(n) < 8000, 1, -1).astype(np.int8)  # P <= n / 2 + 1: the index could hold it
+            c5 = ev.counts(torch.from_numpy(y5), torch.from_numpy(s), device="cpu")
+            e5 = coracle.auc_counts(y5.astype(np.int64), s)
+            assert (c5["wins"], c5["ties"], c5["P"]) == (e5["wins"], e5["ties"], e5["P"])
             # a table the index cannot hold (positives > n / 2 + 1 here): the sorted path, same integers
             y4 = np.where(rng2.random(n) < 0.7, 1, -1).astype(np.int8)
             c4 = ev.counts(torch.from_numpy(y4), torch.from_numpy(s), device="cpu")

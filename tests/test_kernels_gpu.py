@@ -787,6 +787,68 @@ def test_auc_one_class_rejects_nonfinite(dev):
         assert hits >= 1, fill
 
 
+def _two_step(dev, s, y, G):
+    """The two-step sharded evaluation on one device: every part's slot compacted, the slots
+    concatenated as an all-gather would, then every part's query; returns the G records."""
+    from distributedauc_amd import ops
+
+    n = s.size
+    nb = ops.auc_slot_bytes(n, G)
+    slots = torch.empty(nb * G, dtype=torch.uint8, device=dev)
+    ts, ty = T(s, dev), T(y, dev)
+    for r in range(G):
+        mine = torch.empty(nb, dtype=torch.uint8, device=dev)
+        ops.auc_eval_compact_part(ts, ty, r, G, mine)
+        slots[r * nb:(r + 1) * nb].copy_(mine)
+    return [ops.auc_eval_query_part(ts, ty, r, G, slots).cpu().tolist() for r in range(G)]
+
+
+@pytest.mark.parametrize("ldtype", [np.int8, np.int32, np.int64])
+def test_auc_eval_two_step_parts(dev, ldtype):
+    """dauc_auc_eval_compact_part + dauc_auc_eval_query_part (each rank compacts
+    only its slice; the gathered slots are the table) against the C oracle for G = 1, 2, 3, 8:
+    the parts' (W, T) sum to the oracle's, every record carries the same P and label counts;
+    an unshuffled test set whose positives crowd one slice overflows that slot and every part
+    reports verdict 2 (then the blocking sorted path gives the oracle's integers); a tie-heavy
+    table gives verdict 2; a NaN negative is counted in exactly the part that queries it; a NaN
+    positive is in every record."""
+    from distributedauc_amd import ops
+
+    rng = np.random.default_rng(606)
+    n = 300_007
+    s = (np.floor(rng.random(n) * 5000) / 5000).astype(np.float32)
+    for p in (0.02, 0.2, 0.0005):
+        y = np.where(rng.random(n) < p, 1, -1).astype(ldtype)
+        y[rng.random(n) < 0.001] = 0
+        e = coracle.auc_counts(y.astype(np.int64), s)
+        for G in (1, 2, 3, 8):
+            recs = _two_step(dev, s, y, G)
+            assert {(v[3], v[5], v[6]) for v in recs} == {(e["P"], 0, int((y == 0).sum()))}, (p, G)
+            assert {v[7] for v in recs} == {1}, (p, G, recs)
+            assert (sum(v[0] for v in recs), sum(v[1] for v in recs)) == (e["wins"], e["ties"]), (p, G)
+    # unshuffled: every positive in the first slice
+    y = np.where(np.arange(n) < 30_000, 1, -1).astype(ldtype)  # slice 0 holds 30000 > its slot (23502)
+    e = coracle.auc_counts(y.astype(np.int64), s)
+    recs = _two_step(dev, s, y, 8)
+    assert {v[7] for v in recs} == {2} and {v[3] for v in recs} == {e["P"]}, recs
+    W = Tt = 0
+    for r in range(8):
+        o = ops.auc_eval_counts_part(T(s, dev), T(y, dev), r, 8, torch.zeros(3, dtype=torch.int64, device=dev))
+        W, Tt = W + o[0], Tt + o[1]
+    assert (W, Tt) == (e["wins"], e["ties"])
+    # tie-heavy positives: the index refuses the table
+    y = np.where(rng.random(n) < 0.03, 1, -1).astype(ldtype)
+    s2 = np.where(y == 1, np.float32(0.25), s).astype(np.float32)
+    assert {v[7] for v in _two_step(dev, s2, y, 3)} == {2}
+    # a NaN negative in the last part's query range; a NaN positive in every record
+    s3 = s.copy()
+    s3[int(np.flatnonzero(y == -1)[-2])] = np.nan
+    assert [v[2] for v in _two_step(dev, s3, y, 4)] == [0, 0, 0, 1]
+    s4 = s.copy()
+    s4[int(np.flatnonzero(y == 1)[0])] = np.nan
+    assert {v[5] for v in _two_step(dev, s4, y, 4)} == {1}
+
+
 def test_auc_sort_rejects_nonfinite_negatives(dev):
     """The sort method never materialises the negatives: the query kernel's finiteness count
     must still reject a NaN / inf negative (sklearn _ranking.py:868-869), sharded or not."""
