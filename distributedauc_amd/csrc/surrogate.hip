@@ -541,7 +541,7 @@ constexpr int kGran = 10;                   // granules per row / group total
 constexpr int kMaxPolls = 1 << 22;
 
 struct TailWs {
-    unsigned* epoch;               // header word
+    unsigned* epoch;               // the workspace's epoch word (kEpochOffset, the same for every B)
     unsigned long long* rows;      // [nblocks][kGran]
     unsigned long long* gtot;      // [R][kGran]
     unsigned long long* stamps;    // tuning builds: [nblocks + 8 R] s_memrealtime stamps (nullable)
@@ -553,10 +553,18 @@ inline size_t tail_ws_bytes(int64_t nblocks, int R, bool stamps = false) {
     return kTailHeader + size_t(nblocks + R) * kGran * 8 + (stamps ? size_t(nblocks + 8 * R) * 8 : 0);
 }
 
-inline TailWs tail_ws(void* ws, int64_t nblocks, int R, bool stamps = false) {
-    char* p = static_cast<char*>(ws);
+// The epoch word sits at a FIXED offset of the workspace (in the persistent kernel's counter line,
+// whose other words nothing else uses), not in the B-dependent tail region: a stream alternating
+// two batch sizes then still advances one epoch, and the epoch a call reads is never a word some
+// other B's rows or two-launch region last held.
+constexpr size_t kEpochOffset = 128;
+static_assert(kEpochOffset + sizeof(unsigned) <= kCounterBytes, "the epoch word lives in the counter line");
+
+// ws = the whole workspace; the rows start at `offset` (tail_offset(nblocks) + kTailHeader)
+inline TailWs tail_ws(void* ws, size_t offset, int64_t nblocks, int R, bool stamps = false) {
+    char* p = static_cast<char*>(ws) + offset;
     TailWs w;
-    w.epoch = reinterpret_cast<unsigned*>(p);
+    w.epoch = reinterpret_cast<unsigned*>(static_cast<char*>(ws) + kEpochOffset);
     w.rows = reinterpret_cast<unsigned long long*>(p + kTailHeader);
     w.gtot = w.rows + nblocks * kGran;
     w.stamps = stamps ? w.gtot + int64_t(R) * kGran : nullptr;
@@ -985,7 +993,7 @@ int launch_tail(const float* h, const YT* y, int64_t B, const float* abalpha, co
     const int64_t nblocks = chunk_blocks(B);
     if (nblocks > 0x7fffffffLL) return DAUC_EINVAL;
     if (ws == nullptr || ws_bytes < tail_offset(nblocks) + tail_ws_bytes(nblocks, R, STAMPS)) return DAUC_EINVAL;
-    const TailWs w = tail_ws(static_cast<char*>(ws) + tail_offset(nblocks), nblocks, R, STAMPS);
+    const TailWs w = tail_ws(ws, tail_offset(nblocks), nblocks, R, STAMPS);
     hipLaunchKernelGGL((surrogate_tail_kernel<YT, kChunkSlots, R, REDUCE, STAMPS>), dim3(static_cast<unsigned>(nblocks)),
                        dim3(kThreads), 0, st, h, y, B, 1.0 / static_cast<double>(B), abalpha, p_hat, dh, w, out64,
                        grad3, loss);
@@ -998,7 +1006,7 @@ int launch_tail_x(const float* h, const YT* y, int64_t B, const float* abalpha, 
     const int64_t nblocks = chunk_blocks(B);
     if (nblocks + R > 0x7fffffffLL) return DAUC_EINVAL;
     if (ws == nullptr || ws_bytes < tail_offset(nblocks) + tail_ws_bytes(nblocks, R, STAMPS)) return DAUC_EINVAL;
-    const TailWs w = tail_ws(static_cast<char*>(ws) + tail_offset(nblocks), nblocks, R, STAMPS);
+    const TailWs w = tail_ws(ws, tail_offset(nblocks), nblocks, R, STAMPS);
     hipLaunchKernelGGL((surrogate_tail_x_kernel<YT, kChunkSlots, R, K, PLAIN, STAMPS, WAVES, REDUCE>),
                        dim3(static_cast<unsigned>(nblocks + R)), dim3(kThreads), 0, st, h, y, B, nblocks,
                        1.0 / static_cast<double>(B), abalpha, p_hat, dh, w, out64, grad3, loss);
@@ -1016,7 +1024,7 @@ int launch_tail_early(const float* h, const YT* y, int64_t B, const float* abalp
     const TailPlan plan = tail_plan(nblocks, lag);
     // group totals: ngroups <= 256 granule rows (the workspace holds kTailReducers... size for 256)
     if (ws == nullptr || ws_bytes < tail_offset(nblocks) + tail_ws_bytes(nblocks, 256, STAMPS)) return DAUC_EINVAL;
-    const TailWs w = tail_ws(static_cast<char*>(ws) + tail_offset(nblocks), nblocks, 256, STAMPS);
+    const TailWs w = tail_ws(ws, tail_offset(nblocks), nblocks, 256, STAMPS);
     hipLaunchKernelGGL((surrogate_tail_early_kernel<YT, kChunkSlots, STAMPS>), dim3(static_cast<unsigned>(nblocks)),
                        dim3(kThreads), 0, st, h, y, B, 1.0 / static_cast<double>(B), abalpha, p_hat, dh, w, plan,
                        out64, grad3, loss);

@@ -207,12 +207,12 @@ def test_surrogate_tail_ignores_stale_granules(dev):
     nb = -(-B // 4096)
     chunk = nb * 48 + 256 + -(-nb // 512) * 48
     off = 256 + 2048 * 48 + -(-chunk // 256) * 256
-    words = ws[off: off + 256 + (nb + 128) * 80].view(torch.int64)  # rows + the 128 reducers' totals
-    epoch = int(words[0].item()) & 0xFFFFFFFF
-    gran = words[32:]  # the 256-B header, then the granules
+    gran = ws[off + 256: off + 256 + (nb + 128) * 80].view(torch.int64)  # rows + the 128 reducers' totals
+    ew = ws[128:136].view(torch.int64)  # the epoch word: a fixed offset of the workspace (kEpochOffset)
+    epoch = int(ew.item()) & 0xFFFFFFFF
     rng = torch.Generator(device=dev).manual_seed(5)
     for k in range(3):
-        assert int(words[0].item()) & 0xFFFFFFFF == epoch
+        assert int(ew.item()) & 0xFFFFFFFF == epoch
         garbage = torch.randint(0, 1 << 31, gran.shape, device=dev, generator=rng)
         if k < 2:
             stale_tag = ((epoch - 1) & 0xFFFFFFFF) | 0x80000000
@@ -222,6 +222,45 @@ def test_surrogate_tail_ignores_stale_granules(dev):
             gran.copy_(garbage * (1 << 32) + garbage)  # random tags (bit 31 clear: never current)
         assert np.array_equal(call(), ref), k
         epoch = (epoch + 1) & 0xFFFFFFFF
+
+
+def test_surrogate_tail_alternating_batch_sizes(dev):
+    """The tail kernel's epoch word sits at a fixed offset of the workspace, not in its B-dependent
+    tail region: one stream alternating two batch sizes >= 2^22 on one workspace --
+    each size's rows where the other size's epoch word used to be -- gives every call bit-identical
+    results to its first one, the epoch advances by exactly one per call, and the results match
+    the fp64 closed form."""
+    from distributedauc_amd import _lib, ops
+
+    sizes = (3 * (1 << 22) + 4099, (1 << 22) + 37, 5 * (1 << 22) + 1)
+    g = torch.Generator(device=dev).manual_seed(31)
+    data = {}
+    for B in sizes:
+        h = torch.rand(B, device=dev, generator=g) * 2.0 - 0.5
+        y = torch.where(torch.rand(B, device=dev, generator=g) < 0.2, 1, -1).to(torch.int8)
+        data[B] = (h, y)
+    abap = torch.tensor([0.1, -0.2, 0.3, 0.1], device=dev)
+    ws = ops.workspaces.get(dev, "surrogate", max(_lib.load().dauc_surrogate_workspace_size(B) for B in sizes))
+    ew = ws[128:136].view(torch.int64)
+
+    def call(B):
+        o = torch.zeros(6, dtype=torch.float64, device=dev)
+        ops.surrogate_fwdbwd(*data[B], abap[:3], abap[3:], out64=o)
+        torch.cuda.synchronize()
+        return o.cpu().numpy()
+
+    first = {}
+    for i, B in enumerate(sizes * 4 + sizes[::-1] * 2):
+        e0 = int(ew.item()) & 0xFFFFFFFF
+        got = call(B)
+        assert int(ew.item()) & 0xFFFFFFFF == (e0 + 1) & 0xFFFFFFFF, (i, B)
+        assert np.array_equal(got, first.setdefault(B, got)), (i, B)
+    for B in sizes:
+        hn, yn = data[B][0].cpu().numpy(), data[B][1].cpu().numpy().astype(np.int64)
+        F, _, da, db, dal = R.surrogate_closed_form(hn, yn, 0.1, -0.2, 0.3, float(np.float32(0.1)))
+        sc = _scales(hn, yn, 0.1, -0.2, 0.3, float(np.float32(0.1)))
+        assert np.all(np.abs(first[B][:4] - [F, da, db, dal]) <= 1e-6 * sc + 1e-12), B
+        assert first[B][4] == np.sum(yn == 1) and first[B][5] == np.sum(yn == -1)
 
 
 def test_surrogate_timing_variants_leave_no_current_rows(dev):
