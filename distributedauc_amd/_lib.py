@@ -93,6 +93,7 @@ TUNING_SIGNATURES = {
     "dauc_pd_update_dense_variant": (_int, [_vp, _vp, _vp, _vp, _i64, _f32, _f32, _int, _vp]),
     "dauc_pair_count_variant": (_int, [_vp, _i64, _vp, _i64, _vp, _int, _vp]),
     "dauc_set_search_mode": (_int, [_int]),
+    "dauc_set_direct_fault": (_int, [_int]),
 }
 TUNING_LIB_PATH = Path(os.environ.get("DAUC_TUNING_LIB", PKG_DIR.parent / "tuning" / "libdauc_tuning.so"))
 

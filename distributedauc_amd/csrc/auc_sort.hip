@@ -1712,6 +1712,26 @@ int64_t direct_hist_offset(int64_t Mcap) {  // carve_count(...).first, relative 
                    kGrpBytes + 256);
 }
 
+#ifdef DAUC_TUNING
+// Tuning builds: dauc_set_direct_fault corrupts the direct build between its count and scatter
+// passes, so a test can check that the scatter's index checks turn a producer bug into a verdict-2
+// fallback (include/dauc_tuning.h): 1 = one key's cell past the plan's last cell, 2 = one key moved
+// to the next cell (that cell's counter runs out), 3 = one cell's counter one above its count.
+int g_direct_fault = 0;
+
+__global__ void direct_fault_kernel(int mode, const unsigned long long* __restrict__ Mp,
+                                    const unsigned* __restrict__ meta, unsigned* __restrict__ cnt,
+                                    unsigned* __restrict__ cell) {
+    const int64_t M = static_cast<int64_t>(*Mp);
+    if (threadIdx.x != 0 || meta[kCiOk] == 0u || M == 0) return;
+    const int64_t i = M / 2;
+    const unsigned ncells = meta[kCiCells], c = cell[i];
+    if (mode == 1) cell[i] = ncells + 7u;
+    if (mode == 2) cell[i] = c + 1u < ncells ? c + 1u : 0u;
+    if (mode == 3) cnt[c] += 1u;
+}
+#endif
+
 int build_direct_index(const float* pos, const unsigned long long* Mp, int64_t Mcap, void* workspace,
                        size_t workspace_bytes, hipStream_t st, DirectIndex* ix) {
     if (pos == nullptr || Mp == nullptr || Mcap < 1 || workspace == nullptr || ix == nullptr ||
@@ -1733,6 +1753,11 @@ int build_direct_index(const float* pos, const unsigned long long* Mp, int64_t M
                        Mcap, nw.first, nw.l1, nw.meta, nw.cstart, w.keys_b);
     hipLaunchKernelGGL(direct_blocks_kernel, dim3(kDirectMaxGroups), dim3(kDirectGroup), 0, st, nw.cstart, nw.meta,
                        nw.blk, grp);
+#ifdef DAUC_TUNING
+    if (g_direct_fault != 0)
+        hipLaunchKernelGGL(direct_fault_kernel, dim3(1), dim3(64), 0, st, g_direct_fault, Mp, nw.meta, nw.cstart,
+                           w.keys_b);
+#endif
     hipLaunchKernelGGL(direct_scatter_kernel, blocks(Mcap, kDirectThreads, 1024), dim3(kDirectThreads), 0, st, pos,
                        Mp, nw.blk, grp, nw.meta, nw.cstart, w.keys_b, table);
     *ix = DirectIndex{table, nw.l1, nw.blk, grp, nw.meta};
@@ -1778,6 +1803,12 @@ size_t dauc_sort_workspace_size(int64_t n) {
 int dauc_set_search_mode(int mode) {
     if (mode < 0 || mode > 1) return DAUC_EINVAL;
     g_search_mode = mode;
+    return DAUC_OK;
+}
+
+int dauc_set_direct_fault(int mode) {
+    if (mode < 0 || mode > 3) return DAUC_EINVAL;
+    g_direct_fault = mode;
     return DAUC_OK;
 }
 #endif
@@ -1835,7 +1866,7 @@ int dauc_auc_counts_sorted_labeled(const float* pos, int64_t P, const float* sco
     int k = 1;
     TreeGeom g{};
     // the search structure: mode 0 the count index where the table can use it (the device keeps
-    // the tree for skewed tables), 1 the tree, 2 the slot-cell index (a measured alternative)
+    // the tree for skewed tables), 1 the tree
     const int mode = g_search_mode;
     const bool count = mode == 0 && 2 * P <= 3 * int64_t(kCiMaxCells);
     const CountWs nw = count_ws_of(workspace, P);

@@ -572,6 +572,12 @@ def sort_keys(scores: torch.Tensor) -> torch.Tensor:
     return out
 
 
+def set_direct_fault(mode: int) -> None:
+    """Fault injection into the direct count-index build of the tuning build (dauc_set_direct_fault,
+    include/dauc_tuning.h): 0 none, 1 / 2 / 3 a corrupted cell index or counter. Tests only."""
+    check(_lib.tuning().dauc_set_direct_fault(int(mode)), "dauc_set_direct_fault")
+
+
 def set_search_mode(mode: int) -> None:
     """Search structure of the sort method (dauc_set_search_mode): 0 automatic (the count index
     where the table fits it and is not skewed, else the LDS search tree), 1 the tree. Same
@@ -584,6 +590,7 @@ __all__ = [
     "pd_update_dense", "coda_finalize", "scale_div", "split_scores", "pair_count", "auc_counts_sorted",
     "surrogate_logits_fwdbwd", "class_sums_logits",
     "sort_keys", "auc_counts_sorted_labeled", "compact_positives", "mode_code", "workspaces", "set_search_mode",
+    "set_direct_fault",
     "auc_eval_enqueue",
     "auc_slot_bytes",
     "auc_eval_compact_part",

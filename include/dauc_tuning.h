@@ -72,6 +72,15 @@ int dauc_pair_count_variant(const float* pos, int64_t P, const float* neg, int64
  */
 int dauc_set_search_mode(int mode);
 
+/*
+ * Fault injection into the direct count-index build (process-wide, default 0 = none): between the
+ * build's count and scatter passes, 1 = one key's cell index past the plan's last cell, 2 = one
+ * key moved to the next cell (that cell's counter runs out), 3 = one cell's counter one above its
+ * key count. The scatter's index checks must turn each into verdict 2 (the sorted path), never
+ * into an out-of-bounds store or wrong counts. Tests only.
+ */
+int dauc_set_direct_fault(int mode);
+
 #ifdef __cplusplus
 }
 #endif

@@ -34,8 +34,11 @@ def ops(dev):
     from distributedauc_amd import ops as o
 
     with _lib.using(_lib.tuning()):
-        yield o
-        o.set_search_mode(0)
+        try:
+            yield o
+        finally:
+            o.set_search_mode(0)
+            o.set_direct_fault(0)
 
 
 def _oracle_slice(s, y, begin, end):
@@ -194,3 +197,29 @@ def test_search_mode_rejects_unknown(dev, ops):
 
     with pytest.raises(DaucError):
         ops.set_search_mode(3)
+
+
+@pytest.mark.parametrize("fault", [1, 2, 3])
+def test_direct_build_guards_bad_indices(dev, ops, fault):
+    """The direct count-index build checks every cell index and counter before its scatter stores
+    (auc_sort.hip, direct_scatter_kernel): the tuning build corrupts one key's cell (past the last
+    cell / moved to the next cell) or one cell's counter between the count and scatter passes, and
+    the evaluation reports verdict 2 -- the blocking call then takes the sorted path and returns
+    the oracle's exact counts. Without the fault the same data is counted by the index (verdict 1)."""
+    rng = np.random.default_rng(9 + fault)
+    n = 1 << 21
+    data = [(rng.random(n, dtype=np.float32), _labels(rng, n, p)) for p in (0.01, 0.001)]
+    for s, y in data:
+        e = coracle.auc_counts(y.astype(np.int64), s)
+        ts, ty = T(s, dev), T(y, dev)
+        ops.set_direct_fault(0)
+        rec = ops.auc_eval_enqueue(ts, ty, 0, 1).cpu().tolist()
+        assert rec[7] == 1 and tuple(rec[:2]) == (e["wins"], e["ties"]), rec
+        ops.set_direct_fault(fault)
+        rec = ops.auc_eval_enqueue(ts, ty, 0, 1).cpu().tolist()
+        assert rec[7] == 2, (fault, rec)
+        W, Tt, P, N, bad, other = ops.auc_eval_counts(ts, ty)
+        assert (W, Tt, P, N, bad, other) == (e["wins"], e["ties"], e["P"], e["N"], 0, 0), fault
+        ops.set_direct_fault(0)
+        W, Tt, P, N, bad, other = ops.auc_eval_counts(ts, ty)
+        assert (W, Tt, P, N) == (e["wins"], e["ties"], e["P"], e["N"])
