@@ -514,29 +514,20 @@ __global__ __launch_bounds__(kThreads) void surrogate_rows_reduce_kernel(
     }
 }
 
-// ---- the loss in ONE launch: the stream, its rows reduced by the LAST R workgroups ---------
-// (round 2's product form; since round 3 the tuning build's variants 4 / 5 -- the product takes
-// surrogate_tail_x_kernel below, which shares this section's granules, epochs and polls)
+// ---- the loss in ONE launch: tagged row granules, reduced in-launch -------------------------
 //
-// Every workgroup streams its chunk and publishes its row as tagged 8-byte granules (Guideline
-// 16, R2: the data is the flag; ONE write-through store per granule, no drain, no ticket):
-// granule = {tag (32 bits), payload (32 bits)}, a row = the hi and lo halves of its 4 fp64 sums
-// and its 2 counts = 10 granules. The tag is the call's epoch: every workgroup reads the epoch
-// word of the workspace header at its start, and the final reducer advances it as its very last
-// action (when every row of the call has arrived, so every workgroup has read it). A granule
-// left over from an earlier call -- even one written after that call gave up waiting for it --
-// carries an older tag and is never taken for a current one, and nothing is re-zeroed between
-// calls (tag = epoch | 2^31, so a zeroed workspace holds no valid granule either).
-//
-// The last R workgroups by blockIdx are the reducers: reducer r, after its own chunk and row,
-// takes the rows of group r (a contiguous range of ceil(nblocks / R) rows; one row per thread,
-// only granules not yet current are polled, bounded) and publishes the group total the same way;
-// reducer R-1 (whose group holds the grid's last rows) loads the other R-1 group totals BEFORE
-// waiting on its own group (their trip overlaps its wait), adds them in group order and writes
-// the scalars. A poll that times out makes the outputs NaN (a group reducer then publishes NaN
-// totals), and the epoch still advances. Nothing waits on a workgroup that waits: every row a
-// reducer needs comes from a workgroup that never waits (or from a reducer's own row, stored
-// before it waits). Fixed summation order: bitwise reproducible.
+// Every streaming workgroup publishes its row as tagged 8-byte granules (Guideline 16, R2: the
+// data is the flag; ONE write-through store per granule, no drain, no ticket): granule = {tag (32
+// bits), payload (32 bits)}, a row = the hi and lo halves of its 4 fp64 sums and its 2 counts = 10
+// granules. The tag is the call's epoch: every workgroup reads the epoch word (a fixed word of the
+// workspace) at its start, and the final reducer advances it as its very last action (when every
+// row of the call has arrived, so every workgroup has read it). A granule left over from an earlier
+// call -- even one written after that call gave up waiting for it -- carries an older tag and is
+// never taken for a current one, and nothing is re-zeroed between calls (tag = epoch | 2^31, so a
+// zeroed workspace holds no valid granule either). A poll that times out makes the outputs NaN (a
+// group reducer then publishes NaN totals), and the epoch still advances. Nothing waits on a
+// workgroup that waits: every row a reducer needs comes from a workgroup that never waits.
+// Fixed summation order: bitwise reproducible.
 constexpr int kGran = 10;                   // granules per row / group total
 constexpr int kMaxPolls = 1 << 22;
 
@@ -544,13 +535,12 @@ struct TailWs {
     unsigned* epoch;               // the workspace's epoch word (kEpochOffset, the same for every B)
     unsigned long long* rows;      // [nblocks][kGran]
     unsigned long long* gtot;      // [R][kGran]
-    unsigned long long* stamps;    // tuning builds: [nblocks + 8 R] s_memrealtime stamps (nullable)
 };
 
 constexpr size_t kTailHeader = 256;
 
-inline size_t tail_ws_bytes(int64_t nblocks, int R, bool stamps = false) {
-    return kTailHeader + size_t(nblocks + R) * kGran * 8 + (stamps ? size_t(nblocks + 8 * R) * 8 : 0);
+inline size_t tail_ws_bytes(int64_t nblocks, int R) {
+    return kTailHeader + size_t(nblocks + R) * kGran * 8;
 }
 
 // The epoch word sits at a FIXED offset of the workspace (in the persistent kernel's counter line,
@@ -561,13 +551,12 @@ constexpr size_t kEpochOffset = 128;
 static_assert(kEpochOffset + sizeof(unsigned) <= kCounterBytes, "the epoch word lives in the counter line");
 
 // ws = the whole workspace; the rows start at `offset` (tail_offset(nblocks) + kTailHeader)
-inline TailWs tail_ws(void* ws, size_t offset, int64_t nblocks, int R, bool stamps = false) {
+inline TailWs tail_ws(void* ws, size_t offset, int64_t nblocks) {
     char* p = static_cast<char*>(ws) + offset;
     TailWs w;
     w.epoch = reinterpret_cast<unsigned*>(static_cast<char*>(ws) + kEpochOffset);
     w.rows = reinterpret_cast<unsigned long long*>(p + kTailHeader);
     w.gtot = w.rows + nblocks * kGran;
-    w.stamps = stamps ? w.gtot + int64_t(R) * kGran : nullptr;
     return w;
 }
 
@@ -626,111 +615,20 @@ __device__ __forceinline__ bool wait_row(const unsigned long long* row, unsigned
     return true;
 }
 
-__device__ __forceinline__ unsigned long long realtime() { return __builtin_amdgcn_s_memrealtime(); }
-
-// REDUCE = false: the stream with its row stores and nobody reducing (a timing variant).
-template <typename YT, int S, int R, bool REDUCE, bool STAMPS>
-__global__ __launch_bounds__(kThreads, 1) void surrogate_tail_kernel(
-    const float* __restrict__ h, const YT* __restrict__ y, int64_t B, double invB,
-    const float* __restrict__ abalpha, const float* __restrict__ p_hat, float* __restrict__ dh, TailWs ws,
-    double* __restrict__ out64, float* __restrict__ grad3, float* __restrict__ loss) {
-    const unsigned epoch = __builtin_amdgcn_readfirstlane(
-        __hip_atomic_load((gu32*)ws.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    // a variant that reduces nothing never advances the epoch: its rows carry a tag no call
-    // expects (bit 30 set), so a later call cannot take them for its own
-    const unsigned tag = (epoch | 0x80000000u) ^ (REDUCE ? 0u : 0x40000000u);
-    // uniform scalar inputs (scalar registers); the final reducer rebuilds its fp64 scalars from
-    // them at the end instead of keeping them live through the stream and the reduce
-    const float sa = abalpha[0], sb = abalpha[1], sal = abalpha[2], sp = p_hat[0];
-    const int64_t nblocks = gridDim.x;
-    {
-        const SurrogateScalars s = make_scalars_v(sa, sb, sal, sp, invB);
-        const double v = stream_chunk<YT, false, S>(h, y, B, s, dh, gran_total(threadIdx.x < kGran ? threadIdx.x : 0));
-        publish_granule(ws.rows + int64_t(blockIdx.x) * kGran, tag, v);
-        if (STAMPS && threadIdx.x == 0) ws.stamps[blockIdx.x] = realtime();
-    }
-    const int64_t nred = nblocks < R ? nblocks : R;
-    const int64_t r = int64_t(blockIdx.x) - (nblocks - nred);
-    if (!REDUCE || r < 0) return;
-
-    __shared__ double scratch[kNumAcc * kWaves];
-    const int64_t G = (nblocks + nred - 1) / nred;
-    const int64_t g0 = r * G, g1 = (g0 + G < nblocks) ? g0 + G : nblocks;
-    const bool final_red = r == nred - 1;
-    const bool holds = final_red && threadIdx.x < nred - 1;  // thread t: group total t
-    unsigned long long* st = STAMPS ? ws.stamps + nblocks + 8 * r : nullptr;
-    if (STAMPS && threadIdx.x == 0) st[0] = realtime();
-    bool ok = true;
-    double tot[kNumAcc];
-#pragma unroll
-    for (int k = 0; k < kNumAcc; ++k) tot[k] = 0.0;
-    for (int64_t i = g0 + threadIdx.x; i < g1; i += kThreads) {
-        unsigned p[kGran];
-        const unsigned miss = poll_row(ws.rows + i * kGran, tag, p);
-        if (!wait_row(ws.rows + i * kGran, tag, miss, p)) {
-            ok = false;
-            break;
-        }
-        add_row(p, tot);
-    }
-    if (STAMPS && threadIdx.x == 0) st[1] = realtime();
-    __shared__ int bad;
-    if (threadIdx.x == 0) bad = 0;
-    __syncthreads();
-    if (!ok) bad = 1;
-    block_sum<kNumAcc>(tot, scratch);  // its barriers order the flag
-    ok = bad == 0;
-    if (STAMPS && threadIdx.x == 0) st[2] = realtime();
-    if (!final_red) {
-        if (!ok) {
-#pragma unroll
-            for (int k = 0; k < kNumAcc; ++k) tot[k] = __builtin_nan("");
-        }
-        double v = tot[0];
-#pragma unroll
-        for (int k = 1; k < kNumAcc; ++k)
-            if (threadIdx.x < kGran && gran_total(threadIdx.x) == k) v = tot[k];
-        publish_granule(ws.gtot + r * kGran, tag, v);
-        if (STAMPS && threadIdx.x == 0) st[3] = realtime();
-        return;
-    }
-    double rest[kNumAcc];
-#pragma unroll
-    for (int k = 0; k < kNumAcc; ++k) rest[k] = 0.0;
-    if (holds) {
-        unsigned gp[kGran];
-        const unsigned gmiss = poll_row(ws.gtot + threadIdx.x * kGran, tag, gp);
-        if (wait_row(ws.gtot + threadIdx.x * kGran, tag, gmiss, gp)) add_row(gp, rest);
-        else ok = false;
-    }
-    if (STAMPS && threadIdx.x == 0) st[4] = realtime();
-    if (!ok) bad = 1;
-    block_sum<kNumAcc>(rest, scratch);
-    ok = bad == 0;
-    if (threadIdx.x == 0) {
-#pragma unroll
-        for (int k = 0; k < kNumAcc; ++k) tot[k] = ok ? rest[k] + tot[k] : __builtin_nan("");
-        finalize(tot, make_scalars_v(sa, sb, sal, sp, invB), invB, out64, grad3, loss);
-        // the call's last action: every workgroup has read the epoch (its row has arrived)
-        __hip_atomic_store((gu32*)ws.epoch, epoch + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (STAMPS) st[5] = realtime();
-    }
-}
-
 // ---- the one-launch loss with R EXTRA reducer workgroups that stream nothing (the product) ---
 //
-// The stamps of the kernel above put its tail (6.3-6.6 us after the last row store) in the
-// reducers: they are the last 64 STREAMING workgroups, so every group total waits for its
-// reducer's own chunk, and the groups next to the end hold the grid's last rows -- two hops
-// (row -> group reducer -> final) after the last row, each a write-through store and a poll.
-// Here the grid is nblocks + R: the R reducers come after every streaming workgroup and stream
-// nothing, so they are polling as soon as the last streaming workgroups are dispatched. The
-// final reducer (the grid's last workgroup) takes the last K rows itself (K / 256 per thread) and
-// the R - 1 group totals of rows [0, nblocks - K), which complete K rows' streaming time (~K / 190
-// us at 2^26) before the last row: after the last row lands one hop is left. PLAIN: the epoch is
-// read with a plain load (every read of it precedes the final's store; a later call reads it across
-// the kernel boundary). Same granules, epochs, bounded polls and fixed summation order as above.
-template <typename YT, int S, int R, int K, bool PLAIN, bool STAMPS, int WAVES = 1, bool REDUCE = true>
+// The grid is nblocks + R: the R reducers come after every streaming workgroup and stream nothing,
+// so they are polling as soon as the last streaming workgroups are dispatched (round 2's form, in
+// which the last 64 STREAMING workgroups reduced, put 6.3-6.6 us after the last row store: every
+// group total waited for its reducer's own chunk). Reducer r < R - 1 sums a contiguous group of the
+// rows [0, nblocks - K) (one row per thread, only granules not yet current are polled, bounded) and
+// publishes the group total the same way; the final reducer (the grid's last workgroup) takes the
+// last K rows itself (K / 256 per thread) and the R - 1 group totals, which complete K rows'
+// streaming time (~K / 190 us at 2^26) before the last row: after the last row lands one hop is
+// left. PLAIN: the epoch is read with a plain load (every read of it precedes the final's store; a
+// later call reads it across the kernel boundary). REDUCE = false: the stream with its row stores
+// and nobody reducing (a timing variant; its rows carry a tag no call expects, bit 30 set).
+template <typename YT, int S, int R, int K, bool PLAIN, int WAVES = 1, bool REDUCE = true>
 __global__ __launch_bounds__(kThreads, WAVES) void surrogate_tail_x_kernel(
     const float* __restrict__ h, const YT* __restrict__ y, int64_t B, int64_t nblocks, double invB,
     const float* __restrict__ abalpha, const float* __restrict__ p_hat, float* __restrict__ dh, TailWs ws,
@@ -747,7 +645,6 @@ __global__ __launch_bounds__(kThreads, WAVES) void surrogate_tail_x_kernel(
         const SurrogateScalars s = make_scalars_v(sa, sb, sal, sp, invB);
         const double v = stream_chunk<YT, false, S>(h, y, B, s, dh, gran_total(threadIdx.x < kGran ? threadIdx.x : 0));
         publish_granule(ws.rows + b * kGran, tag, v);
-        if (STAMPS && threadIdx.x == 0) ws.stamps[b] = realtime();
         return;
     }
     if (!REDUCE) return;  // a timing variant: the stream with its row stores, nobody reducing
@@ -758,8 +655,6 @@ __global__ __launch_bounds__(kThreads, WAVES) void surrogate_tail_x_kernel(
     const int64_t G = (k0 + R - 2) / (R - 1);
     __shared__ double scratch[kNumAcc * kWaves];
     __shared__ int bad;
-    unsigned long long* st = STAMPS ? ws.stamps + nblocks + 8 * r : nullptr;
-    if (STAMPS && threadIdx.x == 0) st[0] = realtime();
     if (threadIdx.x == 0) bad = 0;
     bool ok = true;
     double tot[kNumAcc];
@@ -805,12 +700,10 @@ __global__ __launch_bounds__(kThreads, WAVES) void surrogate_tail_x_kernel(
 #pragma unroll
         for (int j = 0; j <= KR; ++j) add_row(p[j], tot);
     }
-    if (STAMPS && threadIdx.x == 0) st[1] = realtime();
     __syncthreads();  // orders bad = 0 before any thread's bad = 1
     if (!ok) bad = 1;
     block_sum<kNumAcc>(tot, scratch);  // its barriers order the flag
     ok = bad == 0;
-    if (STAMPS && threadIdx.x == 0) st[2] = realtime();
     if (!ok) {
 #pragma unroll
         for (int k = 0; k < kNumAcc; ++k) tot[k] = __builtin_nan("");
@@ -821,148 +714,22 @@ __global__ __launch_bounds__(kThreads, WAVES) void surrogate_tail_x_kernel(
         for (int k = 1; k < kNumAcc; ++k)
             if (threadIdx.x < kGran && gran_total(threadIdx.x) == k) v = tot[k];
         publish_granule(ws.gtot + r * kGran, tag, v);
-        if (STAMPS && threadIdx.x == 0) st[3] = realtime();
         return;
     }
     if (threadIdx.x == 0) {
         finalize(tot, make_scalars_v(sa, sb, sal, sp, invB), invB, out64, grad3, loss);
         // the call's last action: every workgroup has read the epoch (its row or total has arrived)
         __hip_atomic_store((gu32*)ws.epoch, epoch + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (STAMPS) st[5] = realtime();
-    }
-}
-
-// ---- the same one-launch loss with EARLY group reducers ------------------------------------
-//
-// The stamps of the kernel above (variant 5, scripts/probe_tail_stamps.py) show its tail after
-// the last row store (6.3 us at B = 2^26): the reducers are the last 64 workgroups, so the last
-// of them START at the very end, stream their own chunk, and only then take their (long finished)
-// group and publish its total (+3.8 us); the final reducer then polls the totals (+4.4) and
-// combines them with a second block sum (+6.3). Here groups of G rows get a reducer dispatched
-// L workgroups AFTER the group's last row (by blockIdx; dispatch runs roughly in blockIdx order,
-// so with L >= the resident workgroups the group is finished when its reducer starts -- speed
-// only: a reducer that starts early waits for rows of workgroups that never wait). Only the
-// groups too close to the end for that (the last L rows) are reduced by the last workgroups, the
-// very last one taking the last group and adding every other group's total to its own rows
-// before ONE block sum (thread t: its rows, then group total t: a fixed order, bitwise
-// reproducible). Same granules, epochs, timeouts and stamps as the kernel above.
-struct TailPlan {
-    int64_t G;        // rows per group (ngroups <= 256: the final reducer's threads hold one total each)
-    int64_t ngroups;
-    int64_t L;        // lag: early reducer of group r = workgroup (r + 1) G - 1 + L
-    int64_t r_late0;  // groups r >= r_late0 are reduced by the last nlate workgroups
-    int64_t nlate;
-};
-
-inline TailPlan tail_plan(int64_t nblocks, int64_t L) {
-    TailPlan p;
-    p.G = (nblocks + 255) / 256 > 256 ? (nblocks + 255) / 256 : 256;
-    p.ngroups = (nblocks + p.G - 1) / p.G;
-    p.L = L;
-    p.r_late0 = p.ngroups - 1;
-    for (int64_t r = 0; r < p.ngroups - 1; ++r) {
-        // the late workgroups of groups r .. ngroups-1 are the last (ngroups - r) of the grid
-        if ((r + 1) * p.G - 1 + L >= nblocks - (p.ngroups - r)) {
-            p.r_late0 = r;
-            break;
-        }
-    }
-    p.nlate = p.ngroups - p.r_late0;
-    return p;
-}
-
-template <typename YT, int S, bool STAMPS>
-__global__ __launch_bounds__(kThreads, 1) void surrogate_tail_early_kernel(
-    const float* __restrict__ h, const YT* __restrict__ y, int64_t B, double invB,
-    const float* __restrict__ abalpha, const float* __restrict__ p_hat, float* __restrict__ dh, TailWs ws,
-    TailPlan plan, double* __restrict__ out64, float* __restrict__ grad3, float* __restrict__ loss) {
-    const unsigned epoch = __builtin_amdgcn_readfirstlane(
-        __hip_atomic_load((gu32*)ws.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    const unsigned tag = epoch | 0x80000000u;
-    const float sa = abalpha[0], sb = abalpha[1], sal = abalpha[2], sp = p_hat[0];
-    const int64_t nblocks = gridDim.x, b = blockIdx.x;
-    {
-        const SurrogateScalars s = make_scalars_v(sa, sb, sal, sp, invB);
-        const double v = stream_chunk<YT, false, S>(h, y, B, s, dh, gran_total(threadIdx.x < kGran ? threadIdx.x : 0));
-        publish_granule(ws.rows + b * kGran, tag, v);
-        if (STAMPS && threadIdx.x == 0) ws.stamps[b] = realtime();
-    }
-    int64_t r = -1;
-    if (b >= nblocks - plan.nlate) {
-        r = plan.r_late0 + (b - (nblocks - plan.nlate));
-    } else {
-        const int64_t e = b + 1 - plan.L;
-        if (e >= plan.G && e % plan.G == 0 && e / plan.G - 1 < plan.r_late0) r = e / plan.G - 1;
-    }
-    if (r < 0) return;
-
-    __shared__ double scratch[kNumAcc * kWaves];
-    __shared__ int bad;
-    const int64_t g0 = r * plan.G, g1 = (g0 + plan.G < nblocks) ? g0 + plan.G : nblocks;
-    const bool final_red = b == nblocks - 1;
-    unsigned long long* st = STAMPS ? ws.stamps + nblocks + 8 * (r < 255 ? r : 255) : nullptr;
-    if (STAMPS && threadIdx.x == 0) st[0] = realtime();
-    if (threadIdx.x == 0) bad = 0;
-    bool ok = true;
-    double tot[kNumAcc];
-#pragma unroll
-    for (int k = 0; k < kNumAcc; ++k) tot[k] = 0.0;
-    for (int64_t i = g0 + threadIdx.x; i < g1; i += kThreads) {
-        unsigned p[kGran];
-        const unsigned miss = poll_row(ws.rows + i * kGran, tag, p);
-        if (!wait_row(ws.rows + i * kGran, tag, miss, p)) {
-            ok = false;
-            break;
-        }
-        add_row(p, tot);
-    }
-    if (STAMPS && threadIdx.x == 0) st[1] = realtime();
-    if (final_red && threadIdx.x < plan.ngroups - 1) {
-        // the other groups' totals, added to this thread's rows (early groups were published long ago)
-        unsigned p[kGran];
-        const unsigned miss = poll_row(ws.gtot + threadIdx.x * kGran, tag, p);
-        if (wait_row(ws.gtot + threadIdx.x * kGran, tag, miss, p)) add_row(p, tot);
-        else ok = false;
-    }
-    if (STAMPS && threadIdx.x == 0) st[4] = realtime();
-    __syncthreads();  // orders bad = 0 before any thread's bad = 1
-    if (!ok) bad = 1;
-    block_sum<kNumAcc>(tot, scratch);  // its barriers order the flag
-    ok = bad == 0;
-    if (STAMPS && threadIdx.x == 0) st[2] = realtime();
-    if (!final_red) {
-        if (!ok) {
-#pragma unroll
-            for (int k = 0; k < kNumAcc; ++k) tot[k] = __builtin_nan("");
-        }
-        double v = tot[0];
-#pragma unroll
-        for (int k = 1; k < kNumAcc; ++k)
-            if (threadIdx.x < kGran && gran_total(threadIdx.x) == k) v = tot[k];
-        publish_granule(ws.gtot + r * kGran, tag, v);
-        if (STAMPS && threadIdx.x == 0) st[3] = realtime();
-        return;
-    }
-    if (threadIdx.x == 0) {
-        if (!ok) {
-#pragma unroll
-            for (int k = 0; k < kNumAcc; ++k) tot[k] = __builtin_nan("");
-        }
-        finalize(tot, make_scalars_v(sa, sb, sal, sp, invB), invB, out64, grad3, loss);
-        // the call's last action: every workgroup has read the epoch (its row has arrived)
-        __hip_atomic_store((gu32*)ws.epoch, epoch + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (STAMPS) st[5] = realtime();
     }
 }
 
 // Default chunk geometry (scripts/micro_kernels.py --which surrogate, profiles/r01-r02).
 constexpr int kChunkSlots = 4;
-// reducers of the one-launch loss (16 / 32 / 64 / 128 / 256 measured at B = 2^26:
-// profiles/r02/surrogate_ab.jsonl; 64 and 128 tie, 16 is 3 us slower)
-constexpr int kTailReducers = 64;
-// the product's extra-reducer tail (surrogate_tail_x_kernel): 128 reducer workgroups, the final one
-// taking the grid's last 512 rows itself; at B = 2^26 (tuning variants 10-21, profiles/r03/a):
-// 92.3 us vs 94.4 for the 64 streaming reducers above, 88.2 for the stream with its row stores alone
+// the one-launch loss's extra-reducer tail (surrogate_tail_x_kernel): 128 reducer workgroups, the
+// final one taking the grid's last 512 rows itself; at B = 2^26 (profiles/r03/a): 92.3 us vs 94.4 for
+// round 2's 64 streaming reducers and 88.2 for the stream with its row stores alone (32 / 64 / 256
+// reducers, 256 / 1024 / 1536 final rows, plain or atomic epoch loads and round 3's early-reducer
+// form were measured there too, and removed in round 4)
 constexpr int kTailXReducers = 128;
 constexpr int kTailFinalRows = 512;
 // Unit-stride batches at least this large take the chunked kernels; smaller ones are
@@ -972,7 +739,7 @@ constexpr int64_t kChunkMinB = int64_t(1) << 22;
 inline int64_t chunk_blocks(int64_t B) { return (B + chunk_elems(kChunkSlots) - 1) / chunk_elems(kChunkSlots); }
 
 // workspace regions after the persistent kernel's: the two-launch form's rows + reduce slots, then
-// the tail kernel's header, granule rows and (tuning builds) stamps
+// the tail kernel's header and granule rows
 inline size_t chunk_region_bytes(int64_t nblocks) {
     return size_t(nblocks) * kRowWords * 8 + kCounterBytes + size_t(reduce_blocks(nblocks)) * kNumAcc * 8;
 }
@@ -981,53 +748,16 @@ inline size_t tail_offset(int64_t nblocks) {
     return kPersistentBytes + (chunk_region_bytes(nblocks) + 255) / 256 * 256;
 }
 
-#ifdef DAUC_TUNING
-constexpr bool kStampRegion = true;
-#else
-constexpr bool kStampRegion = false;
-#endif
-
-template <typename YT, int R, bool REDUCE = true, bool STAMPS = false>
-int launch_tail(const float* h, const YT* y, int64_t B, const float* abalpha, const float* p_hat, float* dh,
-                double* out64, float* grad3, float* loss, void* ws, size_t ws_bytes, hipStream_t st) {
-    const int64_t nblocks = chunk_blocks(B);
-    if (nblocks > 0x7fffffffLL) return DAUC_EINVAL;
-    if (ws == nullptr || ws_bytes < tail_offset(nblocks) + tail_ws_bytes(nblocks, R, STAMPS)) return DAUC_EINVAL;
-    const TailWs w = tail_ws(ws, tail_offset(nblocks), nblocks, R, STAMPS);
-    hipLaunchKernelGGL((surrogate_tail_kernel<YT, kChunkSlots, R, REDUCE, STAMPS>), dim3(static_cast<unsigned>(nblocks)),
-                       dim3(kThreads), 0, st, h, y, B, 1.0 / static_cast<double>(B), abalpha, p_hat, dh, w, out64,
-                       grad3, loss);
-    return launch_status();
-}
-
-template <typename YT, int R, int K, bool PLAIN, bool STAMPS = false, int WAVES = 1, bool REDUCE = true>
+template <typename YT, int R, int K, bool PLAIN, int WAVES = 1, bool REDUCE = true>
 int launch_tail_x(const float* h, const YT* y, int64_t B, const float* abalpha, const float* p_hat, float* dh,
                   double* out64, float* grad3, float* loss, void* ws, size_t ws_bytes, hipStream_t st) {
     const int64_t nblocks = chunk_blocks(B);
     if (nblocks + R > 0x7fffffffLL) return DAUC_EINVAL;
-    if (ws == nullptr || ws_bytes < tail_offset(nblocks) + tail_ws_bytes(nblocks, R, STAMPS)) return DAUC_EINVAL;
-    const TailWs w = tail_ws(ws, tail_offset(nblocks), nblocks, R, STAMPS);
-    hipLaunchKernelGGL((surrogate_tail_x_kernel<YT, kChunkSlots, R, K, PLAIN, STAMPS, WAVES, REDUCE>),
+    if (ws == nullptr || ws_bytes < tail_offset(nblocks) + tail_ws_bytes(nblocks, R)) return DAUC_EINVAL;
+    const TailWs w = tail_ws(ws, tail_offset(nblocks), nblocks);
+    hipLaunchKernelGGL((surrogate_tail_x_kernel<YT, kChunkSlots, R, K, PLAIN, WAVES, REDUCE>),
                        dim3(static_cast<unsigned>(nblocks + R)), dim3(kThreads), 0, st, h, y, B, nblocks,
                        1.0 / static_cast<double>(B), abalpha, p_hat, dh, w, out64, grad3, loss);
-    return launch_status();
-}
-
-// the lag of the early reducers: 2 x the resident workgroups (8 per CU on 256 CUs)
-
-template <typename YT, bool STAMPS = false>
-int launch_tail_early(const float* h, const YT* y, int64_t B, const float* abalpha, const float* p_hat, float* dh,
-                      double* out64, float* grad3, float* loss, void* ws, size_t ws_bytes, hipStream_t st,
-                      int64_t lag = 4096) {
-    const int64_t nblocks = chunk_blocks(B);
-    if (nblocks > 0x7fffffffLL) return DAUC_EINVAL;
-    const TailPlan plan = tail_plan(nblocks, lag);
-    // group totals: ngroups <= 256 granule rows (the workspace holds kTailReducers... size for 256)
-    if (ws == nullptr || ws_bytes < tail_offset(nblocks) + tail_ws_bytes(nblocks, 256, STAMPS)) return DAUC_EINVAL;
-    const TailWs w = tail_ws(ws, tail_offset(nblocks), nblocks, 256, STAMPS);
-    hipLaunchKernelGGL((surrogate_tail_early_kernel<YT, kChunkSlots, STAMPS>), dim3(static_cast<unsigned>(nblocks)),
-                       dim3(kThreads), 0, st, h, y, B, 1.0 / static_cast<double>(B), abalpha, p_hat, dh, w, plan,
-                       out64, grad3, loss);
     return launch_status();
 }
 
@@ -1076,8 +806,8 @@ bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) ==
 
 // variant (tuning builds only; int8 labels with a loss): 0 = default dispatch, 1 = the persistent
 // kernel at any B, 2 = the two-launch form (stream + row-reduce launch), 3 = the streaming kernel
-// alone (no reduce, no scalars), 4 = the one-launch tail kernel's stream with its row stores and
-// nobody reducing, 5 = the tail kernel recording s_memrealtime stamps in the workspace
+// alone (no reduce, no scalars), 20 = the product's one-launch kernel at any unit-stride B, 22 =
+// its stream with the tagged row stores and nobody reducing (the hand-off's cost, by difference)
 template <bool CLASS_ONLY, typename YT>
 int launch_surrogate(const float* h, int64_t hs, const YT* y, int64_t B, const float* abalpha,
                      const float* p_hat, float* dh, int64_t dhs, double* out64, float* grad3,
@@ -1092,25 +822,8 @@ int launch_surrogate(const float* h, int64_t hs, const YT* y, int64_t B, const f
             switch (variant) {
                 case 2: return launch_chunk<YT, false>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, sums4, accumulate, ws, ws_bytes, st);
                 case 3: return launch_chunk<YT, false>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, sums4, accumulate, ws, ws_bytes, st, false);
-                case 4: return launch_tail<YT, kTailReducers, false>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, ws, ws_bytes, st);
-                case 5: return launch_tail<YT, kTailReducers, true, true>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, ws, ws_bytes, st);
-                case 6: return launch_tail_early<YT>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, ws, ws_bytes, st);
-                case 7: return launch_tail_early<YT, true>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, ws, ws_bytes, st);
-                case 8: return launch_tail_early<YT>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, ws, ws_bytes, st, 2048);
-                case 9: return launch_tail_early<YT>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, ws, ws_bytes, st, 8192);
-                case 10: return launch_tail_x<YT, kTailReducers, 512, false>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, ws, ws_bytes, st);
-                case 11: return launch_tail_x<YT, kTailReducers, 512, true>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, ws, ws_bytes, st);
-                case 12: return launch_tail_x<YT, kTailReducers, 256, true>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, ws, ws_bytes, st);
-                case 13: return launch_tail_x<YT, kTailReducers, 1024, true>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, ws, ws_bytes, st);
-                case 14: return launch_tail_x<YT, kTailReducers, 512, true, true>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, ws, ws_bytes, st);
-                case 15: return launch_tail_x<YT, 32, 512, true>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, ws, ws_bytes, st);
-                case 16: return launch_tail_x<YT, 128, 512, true>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, ws, ws_bytes, st);
-                case 17: return launch_tail_x<YT, 128, 1024, true, false, 8>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, ws, ws_bytes, st);
-                case 18: return launch_tail_x<YT, 128, 1536, true, false, 8>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, ws, ws_bytes, st);
-                case 19: return launch_tail_x<YT, 256, 1024, true, false, 8>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, ws, ws_bytes, st);
-                case 20: return launch_tail_x<YT, 128, 512, true, false, 8>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, ws, ws_bytes, st);
-                case 21: return launch_tail_x<YT, 128, 512, true, true>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, ws, ws_bytes, st);
-                case 22: return launch_tail_x<YT, kTailXReducers, kTailFinalRows, true, false, 8, false>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, ws, ws_bytes, st);
+                case 20: return launch_tail_x<YT, kTailXReducers, kTailFinalRows, true, 8>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, ws, ws_bytes, st);
+                case 22: return launch_tail_x<YT, kTailXReducers, kTailFinalRows, true, 8, false>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, ws, ws_bytes, st);
                 default: return DAUC_EINVAL;
             }
         }
@@ -1124,7 +837,7 @@ int launch_surrogate(const float* h, int64_t hs, const YT* y, int64_t B, const f
         // stream nothing (one launch); the class sums keep the two-launch form
         if constexpr (!CLASS_ONLY)
             // int8 labels: the register bound of 8 waves per SIMD costs no spill (wider labels would spill)
-            return launch_tail_x<YT, kTailXReducers, kTailFinalRows, true, false, sizeof(YT) == 1 ? 8 : 1>(
+            return launch_tail_x<YT, kTailXReducers, kTailFinalRows, true, sizeof(YT) == 1 ? 8 : 1>(
                 h, y, B, abalpha, p_hat, dh, out64, grad3, loss, ws, ws_bytes, st);
         else
             return launch_chunk<YT, true>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, sums4, accumulate, ws,
@@ -1286,7 +999,7 @@ size_t dauc_surrogate_workspace_size(int64_t B) {
     const size_t persistent = kCounterBytes + static_cast<size_t>(g) * kNumAcc * sizeof(double);
     // the chunked kernels: the two-launch form's region, then the tail kernel's
     const int64_t nb = chunk_blocks(B);
-    const size_t chunked = tail_offset(nb) + tail_ws_bytes(nb, 256, kStampRegion);  // <= 256 group totals
+    const size_t chunked = tail_offset(nb) + tail_ws_bytes(nb, kTailXReducers);
     return persistent > chunked ? persistent : chunked;
 }
 

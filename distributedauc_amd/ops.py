@@ -135,8 +135,8 @@ def surrogate_fwdbwd(h: torch.Tensor, y: torch.Tensor, abalpha: torch.Tensor, p_
     """Fused loss + gradients of main.py:313-317 (one pass over h and y).
 
     ``variant`` != 0 runs a measured alternative from the tuning build (include/dauc_tuning.h:
-    1 persistent kernel, 2 two-launch form, 3 stream alone, 4 tail stream without its reduce,
-    5 tail kernel with s_memrealtime stamps)."""
+    1 persistent kernel, 2 two-launch form, 3 stream alone, 20 the one-launch kernel at any unit-stride
+    B, 22 its stream with the row stores and no reduce)."""
     B = _check_vec(h, y)
     dev = h.device
     yc = _label_code(y)

@@ -20,23 +20,11 @@ extern "C" {
  * dauc_surrogate_fwdbwd with an explicit kernel: 0 the product's dispatch, 1 the persistent
  * grid-stride kernel (the small-batch path) at any B, 2 the two-launch form (the streaming kernel
  * writes one fp64 row per workgroup, a second launch reduces them), 3 the streaming kernel alone
- * (dh only: no reduce, no scalar outputs), 4 the one-launch tail kernel's stream with its tagged
- * row stores and nobody reducing (no scalar outputs), 5 the one-launch tail kernel recording
- * s_memrealtime stamps in the workspace's stamp region (dauc_surrogate_workspace_size of this
- * build includes it): per workgroup the time its row was stored, per reducer r the start,
- * own-group-done, block-sum-done, publish (group reducers) / group-totals-done, finalize (the final
- * reducer) times; 6 the same one-launch loss with EARLY group reducers (the reducer of a group of
- * rows is the workgroup dispatched 4096 after the group's last row; only the groups too close to
- * the end are reduced by the last workgroups), 7 = 6 with the stamps, 8 / 9 = 6 with a lag of 2048
- * / 8192 workgroups (measured 5 / 3.5 us slower than 0 at B = 2^26: profiles/r03/surrogate_ab.jsonl).
- * 4..9 are round 2's one-launch kernel (64 STREAMING reducers at the grid's end). 10..22 the
- * extra-reducer kernel (the product since round 3: R reducer workgroups after the streaming ones,
- * streaming nothing; the final reducer takes the last K rows itself): 10 R = 64, K = 512 with an
- * atomic epoch load, 11 the same with a plain epoch load, 12 K = 256, 13 K = 1024, 14 = 11 with
- * stamps, 15 R = 32, 16 R = 128, 17 R = 128 K = 1024, 18 R = 128 K = 1536, 19 R = 256 K = 1024
- * (17-19 with an 8-waves-per-SIMD register bound), 20 R = 128 K = 512 with that bound (= the
- * product for int8 labels), 21 = 16 with stamps, 22 = 20 with its reducers returning at once (the
- * stream and its row stores alone). profiles/r03/a: 10 94.7, 11 93.1, 16 92.4, 20 92.3 us vs 4 88.2.
+ * (dh only: no reduce, no scalar outputs), 20 the product's one-launch kernel (128 extra reducer
+ * workgroups, the final one taking the last 512 rows itself) at any unit-stride B, 22 = 20 with its
+ * reducers returning at once (the stream and its tagged row stores alone, no scalar outputs: the
+ * in-launch hand-off's cost by difference). The other numbers of rounds 2-3 (round 2's 64 streaming
+ * reducers, the early-reducer form, other R / K, stamps; profiles/r03/a) were removed in round 4.
  * Variants 2..22 need unit strides, 16-byte aligned h/dh and int8 labels.
  * Every variant returns bitwise-identical dh and counts; the fp64 sums agree to rounding.
  */

@@ -9,3 +9,4 @@ for x in 0 1 2 3; do
   L=$R/tuning/libdauc_x$x.so
   DAUC_LIB=$L timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $D/x$x -o run -- python3 $R/scripts/prof_eval.py 27 0.001 5 > $D/x$x.log 2>&1 || exit 1
 done
+cd $R && timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $D/pytest_gpu.log 2>&1

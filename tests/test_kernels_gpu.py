@@ -127,15 +127,12 @@ def test_surrogate_large_deterministic(dev):
 
 @pytest.mark.parametrize("B", [(1 << 20), (1 << 22), (1 << 22) + 37, 3 * (1 << 22) + 4099, (1 << 24) + 5])
 def test_surrogate_chunked_variants(dev, B):
-    """The one-launch tail kernel (the default for unit-stride B >= 2^22: since round 3 the
-    extra-reducer kernel) and the tuning build's alternatives (include/dauc_tuning.h: 1 persistent,
-    2 two-launch, 3 stream alone, 4 round 2's tail stream without its reduce, 5 round 2's tail with
-    stamps, 6..9 early group reducers, 11 / 16 / 20 extra reducers (R = 64 / 128, 20 = the product's
-    kernel), 21 = 16 with stamps, 22 = the product's stream without its reduce): fp64 closed form
-    within 1e-6 of term scale, dh and counts
-    bitwise equal across variants (dh is per-element; the sums only differ in tree order), bitwise
-    run-to-run, ragged last chunk; the default and the variants interleave on one workspace (the
-    epoch-tagged granules need no cleanup between calls)."""
+    """The one-launch tail kernel (the default for unit-stride B >= 2^22, the extra-reducer kernel)
+    and the tuning build's alternatives (include/dauc_tuning.h: 1 persistent, 2 two-launch, 3
+    stream alone, 20 the product's kernel at any B, 22 its stream without the reduce): fp64 closed
+    form within 1e-6 of term scale, dh and counts bitwise equal across variants (dh is per-element;
+    the sums only differ in tree order), bitwise run-to-run, ragged last chunk; the default and the
+    variants interleave on one workspace (the epoch-tagged granules need no cleanup between calls)."""
     from distributedauc_amd import ops
 
     g = torch.Generator(device=dev).manual_seed(B & 0xFFFF)
@@ -150,7 +147,7 @@ def test_surrogate_chunked_variants(dev, B):
     c = 2.0 / B * (np.abs(hn) + np.abs(k))
     ref_dh = None
     seen = {}
-    for variant in (0, 0, 1, 2, 3, 0, 4, 0, 5, 5, 2, 0, 1, 4, 5, 6, 7, 0, 8, 9, 6, 0, 11, 16, 20, 21, 22, 0, 20):
+    for variant in (0, 0, 1, 2, 3, 0, 22, 0, 20, 20, 2, 0, 1, 22, 22, 20, 3, 0, 20):
         o = torch.zeros(6, dtype=torch.float64, device=dev)
         dh = torch.full((B,), float("nan"), device=dev)
         ops.surrogate_fwdbwd(h, y, abap[:3], abap[3:], dh=dh, out64=o, variant=variant)
@@ -159,17 +156,14 @@ def test_surrogate_chunked_variants(dev, B):
             ref_dh = dhn
         assert np.array_equal(dhn, ref_dh), variant
         assert np.all(np.abs(dhn - dh64) <= 1e-6 * np.maximum(np.abs(dh64), c)), variant
-        if variant in (3, 4, 22):  # the stream without its reduce: no scalar outputs
+        if variant in (3, 22):  # the stream without its reduce: no scalar outputs
             assert not o.any(), variant
             continue
         assert np.all(np.abs(got[:4] - [F, da, db, dal]) <= 1e-6 * sc + 1e-12), (variant, got, F)
         assert got[4] == np.sum(yn == 1) and got[5] == np.sum(yn == -1), variant
-        # fixed summation orders: bitwise run-to-run per kernel (6..9 = the early-reducer kernel:
-        # stamps and the lag change which workgroup reduces, not the order; 21 = 16 with stamps; the
-        # product at B >= 2^22 is variant 20's kernel)
-        key = {7: 6, 8: 6, 9: 6, 21: 16}.get(variant, variant)
-        if variant == 0 and B >= (1 << 22):
-            key = 20
+        # fixed summation orders: bitwise run-to-run per kernel (the product at B >= 2^22 is
+        # variant 20's kernel)
+        key = 20 if variant == 0 and B >= (1 << 22) else variant
         assert np.array_equal(got, seen.setdefault(key, got)), variant
     sums = torch.zeros(4, dtype=torch.float64, device=dev)
     ops.class_sums(h, y, sums, accumulate=False)  # chunked CLASS_ONLY path
@@ -264,7 +258,7 @@ def test_surrogate_tail_alternating_batch_sizes(dev):
 
 
 def test_surrogate_timing_variants_leave_no_current_rows(dev):
-    """The tuning build's stream-only variants of the tail kernels (4, 22) store their rows but
+    """The tuning build's stream-only variant of the tail kernel (22) stores its rows but
     reduce nothing, so the epoch does not advance: their rows carry a tag no call expects. A
     product call on OTHER data right after one is bit-identical to the same call after a product
     call (a stale row taken for a current one would change the sums)."""
@@ -285,7 +279,7 @@ def test_surrogate_timing_variants_leave_no_current_rows(dev):
 
     call(h1, y1)
     ref = call(h2, y2)
-    for v in (22, 4):
+    for v in (22,):
         call(h1, y1, v)
         assert np.array_equal(call(h2, y2), ref), v
 
