@@ -1031,7 +1031,10 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
                 const unsigned below = __builtin_amdgcn_ubfe(b[q].y, 0u, sh);
                 const unsigned bytes = (below & 0x0f0f0f0fu) + ((below >> 4) & 0x0f0f0f0fu);
                 const unsigned rl = b[q].x + __builtin_amdgcn_sad_u8(bytes, 0u, 0u);
-                const unsigned cnt = __builtin_amdgcn_ubfe(b[q].y, sh, 4u);
+                unsigned cnt = __builtin_amdgcn_ubfe(b[q].y, sh, 4u);
+#ifdef DAUC_CI_THIN  // TEMPORARY ablation (wrong counts): fewer window gathers
+                if (g.x[q] & DAUC_CI_THIN) cnt = 0u;
+#endif
                 g.rc[q] = rl | (cnt << 28);
             }
         };
