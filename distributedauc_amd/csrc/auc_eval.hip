@@ -48,7 +48,7 @@ struct EvalWs {
     int64_t* split_stats;         // [4]   the split's stats (sorted fallback)
     void* sws;                    // split workspace
     void* tws;                    // sort + tree + count-index workspace (a table of at most n/2 keys)
-    void* bws;                    // the bucketed count's (auc_bucket.hip): the split queries, tile runs
+    void* bws;                    // the range-slot path's (auc_slots.hip): index, split queries, tile runs
     size_t sws_bytes, tws_bytes, bws_bytes;
 };
 
@@ -71,14 +71,14 @@ EvalWs eval_ws(void* ws, int64_t n) {
     w.tws_bytes = dauc_sort_workspace_size(n / 2 + 1);
     w.tws = p;
     p += align256(w.tws_bytes);
-    w.bws_bytes = bucket_workspace_size(n);
+    w.bws_bytes = slot_index_workspace_size(n);
     w.bws = p;
     return w;
 }
 
 size_t eval_ws_bytes(int64_t n) {
     return kHdr + align256(size_t(n) * 4) + align256(size_t(n / 2 + 1) * 4) + align256(dauc_split_workspace_size(n)) +
-           align256(dauc_sort_workspace_size(n / 2 + 1)) + align256(bucket_workspace_size(n));
+           align256(dauc_sort_workspace_size(n / 2 + 1)) + align256(slot_index_workspace_size(n));
 }
 
 bool valid_args(const float* scores, const void* labels, int label_dtype, int64_t n, int part, int parts,
@@ -106,15 +106,11 @@ int enqueue(const float* scores, const void* labels, int label_dtype, int64_t n,
         // a tuning build forcing another search structure: straight to the sorted path
         return -static_cast<int>(hipMemsetAsync(w.verdict, 2, 1, st));
     }
-#if defined(DAUC_BUCKETED) && DAUC_BUCKETED
-    DirectIndex ix{};
-    if ((rc = build_direct_index(w.pos, w.slot, mcap, w.tws, w.tws_bytes, st, &ix))) return rc;
-    return counts_bucketed(ix, w.slot, scores, labels, label_dtype, qlo, qhi, w.wt, w.wt + 2, w.verdict, w.bws,
-                           w.bws_bytes, st);
-#else
+    if (eval_query_path() == 2)
+        return counts_slotted(w.pos, w.slot, slot_index_capacity(n), scores, labels, label_dtype, qlo, qhi, w.wt,
+                              w.wt + 2, w.verdict, w.bws, w.bws_bytes, st);
     return counts_labeled_direct(w.pos, w.slot, mcap, scores, labels, label_dtype, qlo, qhi, w.wt, w.wt + 2,
                                  w.verdict, w.tws, w.tws_bytes, st);
-#endif
 }
 
 // The sorted path for a verdict-2 evaluation (P, N known): counts of part `part` into w.wt.
@@ -325,8 +321,11 @@ int dauc_auc_eval_query_part(const float* scores, const void* labels, int label_
     const int64_t qlo = n * part / parts, qhi = n * (part + 1) / parts;
     if (qhi > qlo) {
         // the build and the query see m_eff (w.spare[0]): P, or past the index's capacity on overflow
-        rc = counts_labeled_direct(w.pos, w.spare, mcap, scores, labels, label_dtype, qlo, qhi, w.wt, w.wt + 2,
-                                   w.verdict, w.tws, w.tws_bytes, st);
+        rc = eval_query_path() == 2
+                 ? counts_slotted(w.pos, w.spare, mcap, scores, labels, label_dtype, qlo, qhi, w.wt, w.wt + 2,
+                                  w.verdict, w.bws, w.bws_bytes, st)
+                 : counts_labeled_direct(w.pos, w.spare, mcap, scores, labels, label_dtype, qlo, qhi, w.wt, w.wt + 2,
+                                         w.verdict, w.tws, w.tws_bytes, st);
         if (rc) return rc;
     }
     return -static_cast<int>(hipMemcpyAsync(part_out, w.wt, kRecord, hipMemcpyDeviceToDevice, st));

@@ -578,6 +578,13 @@ def set_direct_fault(mode: int) -> None:
     check(_lib.tuning().dauc_set_direct_fault(int(mode)), "dauc_set_direct_fault")
 
 
+def set_query_path(path: int) -> None:
+    """The one-call evaluation's query path in the tuning build (dauc_set_query_path,
+    include/dauc_tuning.h): 1 the count index with per-query window gathers, 2 the range-slot
+    index. Tests and measurements only."""
+    check(_lib.tuning().dauc_set_query_path(int(path)), "dauc_set_query_path")
+
+
 def set_search_mode(mode: int) -> None:
     """Search structure of the sort method (dauc_set_search_mode): 0 automatic (the count index
     where the table fits it and is not skewed, else the LDS search tree), 1 the tree. Same
@@ -590,7 +597,7 @@ __all__ = [
     "pd_update_dense", "coda_finalize", "scale_div", "split_scores", "pair_count", "auc_counts_sorted",
     "surrogate_logits_fwdbwd", "class_sums_logits",
     "sort_keys", "auc_counts_sorted_labeled", "compact_positives", "mode_code", "workspaces", "set_search_mode",
-    "set_direct_fault",
+    "set_direct_fault", "set_query_path",
     "auc_eval_enqueue",
     "auc_slot_bytes",
     "auc_eval_compact_part",
