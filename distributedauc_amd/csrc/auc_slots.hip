@@ -468,12 +468,14 @@ __global__ __launch_bounds__(kSlThreads) void sl_prefix_kernel(const unsigned* _
 
 constexpr int kSlU = 8;  // queries per lane per block (one block = 512 queries of one run)
 
-// One workgroup per chunk of ~kSlChunk queries of one range (the tiles whose run of that range
-// starts in the chunk). The range's slots and the top-bucket table go to LDS; wave w takes the
-// chunk's tiles w, w + 16, ...; a run is read in blocks of 512 queries (8 per lane, all loads in
-// flight together) and the NEXT block's loads -- the same run's or the wave's next run's -- are
-// issued before this block is counted. Workgroup 0 writes the verdict (1 = counted, 2 = the caller
-// takes the sorted path) and any workgroup that meets an inconsistency makes it 2.
+// Persistent: one 1024-thread workgroup per CU takes a contiguous span of the chunks (chunk = the
+// tiles whose run of one range starts in one ~kSlChunk-query stretch of the range's queries;
+// chunks ordered by range), so it loads a range's slots into LDS once per range it meets, not once
+// per chunk. Per chunk, wave w takes the chunk's tiles w, w + 16, ...; a run is read in blocks of
+// 512 queries (8 per lane, all loads in flight together) and the NEXT block's loads -- the same
+// run's or the wave's next run's -- are issued before this block is counted. Workgroup 0 writes
+// the verdict (1 = counted, 2 = the caller takes the sorted path) and any workgroup that meets an
+// inconsistency makes it 2.
 __global__ __launch_bounds__(kSlThreads) void sl_query_kernel(
     const unsigned* __restrict__ out, const unsigned* __restrict__ off, const unsigned* __restrict__ tot,
     const unsigned* __restrict__ cstart, int64_t ntiles, int64_t cstride, const unsigned* __restrict__ meta,
@@ -488,14 +490,14 @@ __global__ __launch_bounds__(kSlThreads) void sl_query_kernel(
     const int G = static_cast<int>(meta[kSmRanges]);
     __shared__ uint2 l1[kCiTop];
     __shared__ uint4 sl[kSlCells];
-    __shared__ int64_t job[3];  // range, first tile, end tile (range < 0: no chunk)
-    __shared__ unsigned rbase;
+    __shared__ unsigned chfirst[kSlMaxRanges + 1];  // the first chunk of every range (+ the total)
+    __shared__ unsigned kfirst[kSlMaxRanges];       // the first table key of every range
     __shared__ unsigned long long red[2][kSlWaves];
     __shared__ int bad_any;
     const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
     if (wid == 0) {
-        // which range and chunk: ranges 2 lane and 2 lane + 1; chunks of range g = ceil(tot_g / K);
-        // and the range's first key in the table (the prefix of the ranges' key counts)
+        // ranges 2 lane and 2 lane + 1: chunks of range g = ceil(tot_g / K); the prefixes of the
+        // chunk counts and of the ranges' key counts
         unsigned ch[2], kt[2];
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
@@ -513,161 +515,164 @@ __global__ __launch_bounds__(kSlThreads) void sl_query_kernel(
                 kincl += ku;
             }
         }
-        const unsigned b = blockIdx.x;
-        if (lane == 0) {
-            job[0] = -1;
-            bad_any = 0;
-        }
-        const unsigned first0 = incl - ch[0] - ch[1];
-        const unsigned kfirst0 = kincl - kt[0] - kt[1];
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const unsigned lo = first0 + (h ? ch[0] : 0u);
-            if (b >= lo && b < lo + ch[h]) {
-                const int g = 2 * lane + h;
-                const unsigned c = b - lo;
-                const unsigned* cs = cstart + int64_t(g) * cstride;
-                job[0] = g;
-                job[1] = cs[c];
-                job[2] = c + 1 < ch[h] ? cs[c + 1] : ntiles;
-                rbase = kfirst0 + (h ? kt[0] : 0u);
-            }
-        }
+        chfirst[2 * lane] = incl - ch[0] - ch[1];
+        chfirst[2 * lane + 1] = incl - ch[1];
+        kfirst[2 * lane] = kincl - kt[0] - kt[1];
+        kfirst[2 * lane + 1] = kincl - kt[1];
+        if (lane == kWave - 1) chfirst[kSlMaxRanges] = incl;
+        if (lane == 0) bad_any = 0;
     }
     __syncthreads();
-    const int64_t g = job[0];
-    if (g < 0) return;
-    {
-        // the tables into LDS with every load of a thread in flight before its first LDS store
-        constexpr int kSlotPer = kSlCells / kSlThreads;  // 8
-        constexpr int kL1Per = kCiTop / kSlThreads;      // 2
-        uint4 sv[kSlotPer];
-        uint2 lv[kL1Per];
-        const uint4* src = slotsg + g * kSlCells;
-#pragma unroll
-        for (int j = 0; j < kSlotPer; ++j) sv[j] = src[j * kSlThreads + threadIdx.x];
-#pragma unroll
-        for (int j = 0; j < kL1Per; ++j) lv[j] = l1g[j * kSlThreads + threadIdx.x];
-#pragma unroll
-        for (int j = 0; j < kSlotPer; ++j) sl[j * kSlThreads + threadIdx.x] = sv[j];
-#pragma unroll
-        for (int j = 0; j < kL1Per; ++j) l1[j * kSlThreads + threadIdx.x] = lv[j];
-    }
-    __syncthreads();
-    const int64_t t1 = job[2];
-    const unsigned cell0 = static_cast<unsigned>(g) << kSlCellBits;
-    const unsigned rb = rbase;
+    const unsigned J = chfirst[kSlMaxRanges];
+    const unsigned jlo = static_cast<unsigned>(uint64_t(blockIdx.x) * J / gridDim.x);
+    const unsigned jhi = static_cast<unsigned>(uint64_t(blockIdx.x + 1) * J / gridDim.x);
     const unsigned M = static_cast<unsigned>(*Mp);
     unsigned long long W = 0, T = 0;
     bool bad = false;
-    // the wave's runs: tiles t0 + wid, + 16, ...; (o, L) of a run = its start in the tile, length
-    struct Run {
-        int64_t t;
-        unsigned o, L;
-    };
-    auto run_of = [&](int64_t t) -> Run {
-        if (t >= t1) return Run{t, 0u, 0u};
-        const unsigned o0 = off[t * kSlOffStride + g], o1 = off[t * kSlOffStride + g + 1];
-        return Run{t, o0, o1 - o0};
-    };
-    auto load_block = [&](unsigned (&x)[kSlU], const Run& r, unsigned j0) {
-        const unsigned* q = out + (r.t < t1 ? r.t : 0) * kSlTile + r.o;
+    int loaded = -1;
+    for (unsigned jc = jlo; jc < jhi; ++jc) {
+        // the chunk's range: the last g with chfirst[g] <= jc (ranges without chunks share their
+        // first chunk index with the next range: the last such g has the chunk)
+        int g = 0;
+        for (int step = kSlMaxRanges / 2; step > 0; step >>= 1)
+            if (g + step < G && chfirst[g + step] <= jc) g += step;
+        const unsigned c = jc - chfirst[g];
+        const unsigned nch = chfirst[g + 1 < G ? g + 1 : kSlMaxRanges] - chfirst[g];
+        const unsigned* cs = cstart + int64_t(g) * cstride;
+        const int64_t t0 = cs[c];
+        const int64_t t1 = c + 1 < nch ? int64_t(cs[c + 1]) : ntiles;
+        if (g != loaded) {
+            __syncthreads();  // every wave is done with the previous range's slots
+            // the tables into LDS with every load of a thread in flight before its first LDS store
+            constexpr int kSlotPer = kSlCells / kSlThreads;  // 8
+            constexpr int kL1Per = kCiTop / kSlThreads;      // 2
+            uint4 sv[kSlotPer];
+            const uint4* src = slotsg + int64_t(g) * kSlCells;
 #pragma unroll
-        for (int u = 0; u < kSlU; ++u) {
-            const unsigned j = j0 + u * kWave + lane;
-            x[u] = q[j < r.L ? j : 0u];  // lanes past the run re-read its first query (counted out below)
+            for (int j = 0; j < kSlotPer; ++j) sv[j] = src[j * kSlThreads + threadIdx.x];
+            if (loaded < 0) {
+                uint2 lv[kL1Per];
+#pragma unroll
+                for (int j = 0; j < kL1Per; ++j) lv[j] = l1g[j * kSlThreads + threadIdx.x];
+#pragma unroll
+                for (int j = 0; j < kL1Per; ++j) l1[j * kSlThreads + threadIdx.x] = lv[j];
+            }
+#pragma unroll
+            for (int j = 0; j < kSlotPer; ++j) sl[j * kSlThreads + threadIdx.x] = sv[j];
+            __syncthreads();
+            loaded = g;
         }
-    };
-    // The block's queries per lane in phases (every LDS read of a phase issued before any is used):
-    // top bucket, slot, counts. A cell of 4+ keys (~0.2 % of the queries at 2 cells per key) reads
-    // the rest of its keys from the table after the block.
-    auto count_block = [&](const unsigned (&x)[kSlU], const Run& r, unsigned j0) {
-        uint2 e[kSlU];
-#pragma unroll
-        for (int u = 0; u < kSlU; ++u) e[u] = l1[x[u] >> kCiLowBits];
-        unsigned cr[kSlU];
-        bool in[kSlU];
-#pragma unroll
-        for (int u = 0; u < kSlU; ++u) {
-            cr[u] = ci_cell(x[u], e[u]) - cell0;  // the cell, relative to the range
-            in[u] = j0 + u * kWave + lane < r.L;
-            bad |= in[u] && cr[u] >= static_cast<unsigned>(kSlCells);
-            in[u] = in[u] && cr[u] < static_cast<unsigned>(kSlCells);
-        }
-        uint4 v[kSlU];
-#pragma unroll
-        for (int u = 0; u < kSlU; ++u) v[u] = sl[in[u] ? cr[u] : 0u];
-        unsigned w32 = 0u, t32 = 0u;
-        bool longer = false;
-#pragma unroll
-        for (int u = 0; u < kSlU; ++u) {
-            const unsigned xv = x[u];
-            // keys past the cell's count are +inf in the slot: above every finite query (and NaN's key)
-            const unsigned lt = (v[u].y < xv) + (v[u].z < xv) + (v[u].w < xv);
-            const unsigned le = (v[u].y <= xv) + (v[u].z <= xv) + (v[u].w <= xv);
-            const unsigned rl = rb + (v[u].x & kSlRankMask);
-            w32 += in[u] ? M - (rl + le) : 0u;
-            t32 += in[u] ? le - lt : 0u;
-            longer |= in[u] && (v[u].x >> 28) > 3u;
-        }
-        if (longer) {
-            // the keys past the first 3 of a longer cell (<= 15: a table with a cell of 16+ keys is
-            // not usable), from the cell-ordered table, counted one by one
+        const unsigned cell0 = static_cast<unsigned>(g) << kSlCellBits;
+        const unsigned rb = kfirst[g];
+        // the wave's runs: tiles t0 + wid, + 16, ...; (o, L) of a run = its start in the tile, length
+        struct Run {
+            int64_t t;
+            unsigned o, L;
+        };
+        auto run_of = [&](int64_t t) -> Run {
+            if (t >= t1) return Run{t, 0u, 0u};
+            const unsigned o0 = off[t * kSlOffStride + g], o1 = off[t * kSlOffStride + g + 1];
+            return Run{t, o0, o1 - o0};
+        };
+        auto load_block = [&](unsigned (&x)[kSlU], const Run& r, unsigned j0) {
+            const unsigned* q = out + (r.t < t1 ? r.t : 0) * kSlTile + r.o;
 #pragma unroll
             for (int u = 0; u < kSlU; ++u) {
-                const unsigned c = v[u].x >> 28;
-                if (!(in[u] && c > 3u)) continue;
-                const unsigned rl = rb + (v[u].x & kSlRankMask);
-                unsigned lt = 0u, le = 0u;
-                for (unsigned q = 3; q < c; ++q) {
-                    const unsigned k = table[rl + q < M ? rl + q : 0u];
-                    lt += k < x[u];
-                    le += k <= x[u];
-                }
-                bad |= rl + c > M;
-                w32 -= le;
-                t32 += le - lt;
+                const unsigned j = j0 + u * kWave + lane;
+                x[u] = q[j < r.L ? j : 0u];  // lanes past the run re-read its first query (counted out below)
             }
+        };
+        // The block's queries per lane in phases (every LDS read of a phase issued before any is
+        // used): top bucket, slot, counts. A cell of 4+ keys (~0.2 % of the queries at 2 cells per
+        // key) reads the rest of its keys from the table after the block.
+        auto count_block = [&](const unsigned (&x)[kSlU], const Run& r, unsigned j0) {
+            uint2 e[kSlU];
+#pragma unroll
+            for (int u = 0; u < kSlU; ++u) e[u] = l1[x[u] >> kCiLowBits];
+            unsigned cr[kSlU];
+            bool in[kSlU];
+#pragma unroll
+            for (int u = 0; u < kSlU; ++u) {
+                cr[u] = ci_cell(x[u], e[u]) - cell0;  // the cell, relative to the range
+                in[u] = j0 + u * kWave + lane < r.L;
+                bad |= in[u] && cr[u] >= static_cast<unsigned>(kSlCells);
+                in[u] = in[u] && cr[u] < static_cast<unsigned>(kSlCells);
+            }
+            uint4 v[kSlU];
+#pragma unroll
+            for (int u = 0; u < kSlU; ++u) v[u] = sl[in[u] ? cr[u] : 0u];
+            unsigned w32 = 0u, t32 = 0u;
+            bool longer = false;
+#pragma unroll
+            for (int u = 0; u < kSlU; ++u) {
+                const unsigned xv = x[u];
+                // keys past the cell's count are +inf in the slot: above every query's key
+                const unsigned lt = (v[u].y < xv) + (v[u].z < xv) + (v[u].w < xv);
+                const unsigned le = (v[u].y <= xv) + (v[u].z <= xv) + (v[u].w <= xv);
+                const unsigned rl = rb + (v[u].x & kSlRankMask);
+                w32 += in[u] ? M - (rl + le) : 0u;
+                t32 += in[u] ? le - lt : 0u;
+                longer |= in[u] && (v[u].x >> 28) > 3u;
+            }
+            if (longer) {
+                // the keys past the first 3 of a longer cell (<= 15: a table with a cell of 16+
+                // keys is not usable), from the cell-ordered table, counted one by one
+#pragma unroll
+                for (int u = 0; u < kSlU; ++u) {
+                    const unsigned cc = v[u].x >> 28;
+                    if (!(in[u] && cc > 3u)) continue;
+                    const unsigned rl = rb + (v[u].x & kSlRankMask);
+                    unsigned lt = 0u, le = 0u;
+                    for (unsigned q = 3; q < cc; ++q) {
+                        const unsigned k = table[rl + q < M ? rl + q : 0u];
+                        lt += k < x[u];
+                        le += k <= x[u];
+                    }
+                    bad |= rl + cc > M;
+                    w32 -= le;
+                    t32 += le - lt;
+                }
+            }
+            W += w32;
+            T += t32;
+        };
+        Run cur = run_of(t0 + wid), nxt = run_of(t0 + wid + kSlWaves);
+        unsigned jb0 = 0;
+        unsigned xa[kSlU], xb[kSlU];
+        load_block(xa, cur, 0);
+        // next block: the same run's, or the next run's first; returns false past the wave's last run
+        auto advance = [&](Run& r, unsigned& j0, Run& n) -> bool {
+            if (j0 + kSlU * kWave < r.L) {
+                j0 += kSlU * kWave;
+                return true;
+            }
+            r = n;
+            j0 = 0;
+            n = run_of(r.t + kSlWaves);
+            return r.t < t1;
+        };
+        while (cur.t < t1) {
+            // A: count xa (block jb0 of cur) while the next block loads into xb
+            Run rb2 = cur, nb = nxt;
+            unsigned jb = jb0;
+            const bool more = advance(rb2, jb, nb);
+            load_block(xb, rb2, jb);  // unconditional (past the end: a valid address, counted out)
+            count_block(xa, cur, jb0);
+            if (!more) break;
+            cur = rb2;
+            nxt = nb;
+            jb0 = jb;
+            // B: the same with the register sets swapped
+            Run ra = cur, na = nxt;
+            unsigned ja = jb0;
+            const bool more2 = advance(ra, ja, na);
+            load_block(xa, ra, ja);
+            count_block(xb, cur, jb0);
+            if (!more2) break;
+            cur = ra;
+            nxt = na;
+            jb0 = ja;
         }
-        W += w32;
-        T += t32;
-    };
-    Run cur = run_of(job[1] + wid), nxt = run_of(job[1] + wid + kSlWaves);
-    unsigned jc = 0;
-    unsigned xa[kSlU], xb[kSlU];
-    load_block(xa, cur, 0);
-    // next block: the same run's, or the next run's first; returns false past the wave's last run
-    auto advance = [&](Run& r, unsigned& j0, Run& n) -> bool {
-        if (j0 + kSlU * kWave < r.L) {
-            j0 += kSlU * kWave;
-            return true;
-        }
-        r = n;
-        j0 = 0;
-        n = run_of(r.t + kSlWaves);
-        return r.t < t1;
-    };
-    while (cur.t < t1) {
-        // A: count xa (block jc of cur) while the next block loads into xb
-        Run rb2 = cur, nb = nxt;
-        unsigned jb = jc;
-        const bool more = advance(rb2, jb, nb);
-        load_block(xb, rb2, jb);  // unconditional (past the end: a valid address, counted out)
-        count_block(xa, cur, jc);
-        if (!more) break;
-        cur = rb2;
-        nxt = nb;
-        jc = jb;
-        // B: the same with the register sets swapped
-        Run ra = cur, na = nxt;
-        unsigned ja = jc;
-        const bool more2 = advance(ra, ja, na);
-        load_block(xa, ra, ja);
-        count_block(xb, cur, jc);
-        if (!more2) break;
-        cur = ra;
-        nxt = na;
-        jc = ja;
     }
     W = wave_sum(W);
     T = wave_sum(T);
@@ -849,10 +854,8 @@ int counts_slotted(const float* pos, const unsigned long long* Mp, int64_t mcap,
     if (rc) return rc;
     hipLaunchKernelGGL(sl_prefix_kernel, dim3(kSlMaxRanges), dim3(kSlThreads), 0, st, w.len, ntiles, sl_cstride(ntiles),
                        w.meta, w.tot, w.cstart);
-    // one workgroup per chunk of ~kSlChunk queries of one range: at most q / kSlChunk + one partial
-    // chunk per range (the surplus workgroups find no chunk and return)
-    const int64_t grid = (q + kSlChunk - 1) / kSlChunk + kSlMaxRanges;
-    hipLaunchKernelGGL(sl_query_kernel, dim3(static_cast<unsigned>(grid)), dim3(kSlThreads), 0, st, w.out, w.off,
+    // persistent: one workgroup per CU, each a contiguous span of the chunks
+    hipLaunchKernelGGL(sl_query_kernel, dim3(static_cast<unsigned>(sl_cu_count())), dim3(kSlThreads), 0, st, w.out, w.off,
                        w.tot, w.cstart, ntiles, sl_cstride(ntiles), w.meta, w.l1, w.slots, w.rtot, w.table, Mp,
                        wins_ties, verdict);
     return launch_status();
