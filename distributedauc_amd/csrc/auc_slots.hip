@@ -279,7 +279,8 @@ struct SlTile {
 // within its range from a returning LDS add on the range's counter (the order inside a run is
 // immaterial: the counts are sums), one wave turns the counters into the runs' starts, the keys go
 // to an LDS stage at their places and the stage is written out with 16-byte stores. off[t][g] = the
-// start of range g's run in the tile (off[t][G] = the tile's query count); len[g][t] = its length.
+// start of range g's run in the tile (off[t][G] = the tile's query count: the runs' lengths are the
+// differences; one contiguous row per tile).
 // Software-pipelined: the next tile's loads are issued before this tile is processed, and the
 // tile's barriers order LDS only, so the stores of a tile are never waited for.
 template <typename LT, bool VEC>
@@ -287,7 +288,7 @@ __global__ __launch_bounds__(kSlThreads) void sl_split_kernel(
     const float* __restrict__ s, const LT* __restrict__ lab, int64_t a0, int64_t begin, int64_t end, int64_t vmax,
     int64_t ntiles, const uint2* __restrict__ l1g, const unsigned* __restrict__ meta,
     const unsigned long long* __restrict__ Mp, unsigned* __restrict__ out, unsigned* __restrict__ off,
-    unsigned* __restrict__ len, unsigned long long* __restrict__ nonfinite) {
+    unsigned long long* __restrict__ nonfinite) {
     // no index: nothing to split, except that with no positives at all (M = 0) the queries are
     // still checked for finiteness (sklearn raises on a non-finite score before its one-class
     // warning, _ranking.py:868-869 / 1191)
@@ -384,14 +385,8 @@ __global__ __launch_bounds__(kSlThreads) void sl_split_kernel(
             const unsigned base0 = incl - c0 - c1, base1 = base0 + c0;
             hist[2 * lane] = base0;
             hist[2 * lane + 1] = base1;
-            if (2 * lane < G) {
-                off[t * kSlOffStride + 2 * lane] = base0;
-                len[int64_t(2 * lane) * ntiles + t] = c0;
-            }
-            if (2 * lane + 1 < G) {
-                off[t * kSlOffStride + 2 * lane + 1] = base1;
-                len[int64_t(2 * lane + 1) * ntiles + t] = c1;
-            }
+            if (2 * lane < G) off[t * kSlOffStride + 2 * lane] = base0;
+            if (2 * lane + 1 < G) off[t * kSlOffStride + 2 * lane + 1] = base1;
             if (lane == kWave - 1) {
                 tile_n = incl;
                 off[t * kSlOffStride + G] = incl;
@@ -434,30 +429,31 @@ __global__ __launch_bounds__(kSlThreads) void sl_split_kernel(
 // with prefix(t - 1) < c K <= prefix(t). A run is shorter than K, so each tile starts at most one
 // chunk; a chunk no tile starts is empty (its queries, if any, are in the last tiles, which the
 // chunk before it runs to the end) and keeps cstart = ntiles.
-__global__ __launch_bounds__(kSlThreads) void sl_prefix_kernel(const unsigned* __restrict__ len, int64_t ntiles,
+__global__ __launch_bounds__(kSlThreads) void sl_prefix_kernel(const unsigned* __restrict__ off, int64_t ntiles,
                                                                int64_t cstride, const unsigned* __restrict__ meta,
                                                                unsigned* __restrict__ tot,
                                                                unsigned* __restrict__ cstart) {
     static_assert(kSlTile < kSlChunk, "a run never spans a chunk");
     if (!sl_usable(meta) || blockIdx.x >= meta[kSmRanges]) return;
     __shared__ unsigned wtot[kSlThreads / kWave];
-    const unsigned* l = len + int64_t(blockIdx.x) * ntiles;
+    const int64_t g = blockIdx.x;
+    auto l = [&](int64_t t) { return off[t * kSlOffStride + g + 1] - off[t * kSlOffStride + g]; };
     unsigned* cs = cstart + int64_t(blockIdx.x) * cstride;
     for (int64_t c = threadIdx.x; c < cstride; c += kSlThreads) cs[c] = static_cast<unsigned>(ntiles);
     const int64_t per = (ntiles + kSlThreads - 1) / kSlThreads;
     const int64_t t0 = int64_t(threadIdx.x) * per;
     const int64_t t1 = t0 + per < ntiles ? t0 + per : ntiles;
     unsigned sum = 0u;
-    for (int64_t t = t0; t < t1; ++t) sum += l[t];
+    for (int64_t t = t0; t < t1; ++t) sum += l(t);
     const unsigned incl = block_incl_scan1024<false>(sum, wtot);  // its barriers order the fill above
     unsigned run = incl - sum;                                     // prefix(t0)
     for (int64_t t = t0; t < t1; ++t) {
-        const unsigned lt = l[t];
+        const unsigned lt = l(t);
         // prefix(t) = run: chunk c = floor(run / K) starts here when prefix(t - 1) < c K
         const uint64_t c = uint64_t(run) / kSlChunk;
         if (t == 0)
             cs[0] = 0u;
-        else if (c * kSlChunk > uint64_t(run) - l[t - 1] && c < uint64_t(cstride))
+        else if (c * kSlChunk > uint64_t(run) - l(t - 1) && c < uint64_t(cstride))
             cs[c] = static_cast<unsigned>(t);
         run += lt;
     }
@@ -723,7 +719,6 @@ struct SlWs {
     unsigned* cell;    // [mcap]
     unsigned* table;   // [mcap + 64]
     unsigned* off;     // [ntiles][kSlOffStride]
-    unsigned* len;     // [kSlMaxRanges][ntiles]
     unsigned* cstart;  // [kSlMaxRanges][cstride]
     unsigned* out;     // [ntiles][kSlTile]
 };
@@ -750,7 +745,6 @@ size_t sl_ws_bytes(int64_t mcap, int64_t q, SlWs* w, void* base) {
     char* cell = take(size_t(mcap) * 4);
     char* table = take(size_t(mcap + 64) * 4);
     char* off = take(size_t(nt) * kSlOffStride * 4);
-    char* len = take(size_t(nt) * kSlMaxRanges * 4);
     char* cst = take(size_t(sl_cstride(nt)) * kSlMaxRanges * 4);
     char* out = take(size_t(nt) * kSlTile * 4);
     if (w != nullptr) {
@@ -764,7 +758,6 @@ size_t sl_ws_bytes(int64_t mcap, int64_t q, SlWs* w, void* base) {
         w->cell = reinterpret_cast<unsigned*>(cell);
         w->table = reinterpret_cast<unsigned*>(table);
         w->off = reinterpret_cast<unsigned*>(off);
-        w->len = reinterpret_cast<unsigned*>(len);
         w->cstart = reinterpret_cast<unsigned*>(cst);
         w->out = reinterpret_cast<unsigned*>(out);
     }
@@ -784,10 +777,10 @@ int launch_sl_split(const float* s, const LT* lab, int64_t begin, int64_t end, c
     if (grid > ntiles) grid = ntiles;
     if (vec)
         hipLaunchKernelGGL((sl_split_kernel<LT, true>), dim3(static_cast<unsigned>(grid)), dim3(kSlThreads), 0, st, s,
-                           lab, a0, begin, end, vmax, ntiles, w.l1, w.meta, Mp, w.out, w.off, w.len, nonfinite);
+                           lab, a0, begin, end, vmax, ntiles, w.l1, w.meta, Mp, w.out, w.off, nonfinite);
     else
         hipLaunchKernelGGL((sl_split_kernel<LT, false>), dim3(static_cast<unsigned>(grid)), dim3(kSlThreads), 0, st, s,
-                           lab, a0, begin, end, vmax, ntiles, w.l1, w.meta, Mp, w.out, w.off, w.len, nonfinite);
+                           lab, a0, begin, end, vmax, ntiles, w.l1, w.meta, Mp, w.out, w.off, nonfinite);
     return launch_status();
 }
 
@@ -852,7 +845,7 @@ int counts_slotted(const float* pos, const unsigned long long* Mp, int64_t mcap,
             return DAUC_EINVAL;
     }
     if (rc) return rc;
-    hipLaunchKernelGGL(sl_prefix_kernel, dim3(kSlMaxRanges), dim3(kSlThreads), 0, st, w.len, ntiles, sl_cstride(ntiles),
+    hipLaunchKernelGGL(sl_prefix_kernel, dim3(kSlMaxRanges), dim3(kSlThreads), 0, st, w.off, ntiles, sl_cstride(ntiles),
                        w.meta, w.tot, w.cstart);
     // persistent: one workgroup per CU, each a contiguous span of the chunks
     hipLaunchKernelGGL(sl_query_kernel, dim3(static_cast<unsigned>(sl_cu_count())), dim3(kSlThreads), 0, st, w.out, w.off,
