@@ -1019,12 +1019,20 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
             uint2 e[NQ];
 #pragma unroll
             for (int q = 0; q < NQ; ++q) e[q] = l1[g.x[q] >> kCiLowBits];
+#if defined(DAUC_CI_ABL) && (DAUC_CI_ABL & 1)  // TEMPORARY ablation (wrong counts): no top-bucket read
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) e[q] = uint2{0u, static_cast<unsigned>(nb) * kCiBlock - 8u};
+#endif
             unsigned c[NQ];
 #pragma unroll
             for (int q = 0; q < NQ; ++q) c[q] = ci_cell(g.x[q], e[q]);
             uint2 b[NQ];
 #pragma unroll
             for (int q = 0; q < NQ; ++q) b[q] = blk[c[q] / kCiBlock];
+#if defined(DAUC_CI_ABL) && (DAUC_CI_ABL & 2)  // TEMPORARY ablation (wrong counts): no block-word read
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) b[q] = uint2{c[q], 0x01010101u};
+#endif
 #pragma unroll
             for (int q = 0; q < NQ; ++q) {
                 const unsigned sh = 4u * (c[q] % kCiBlock);
