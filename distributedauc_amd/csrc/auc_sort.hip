@@ -812,6 +812,19 @@ __global__ __launch_bounds__(256) void ci_blocks_kernel(const unsigned* __restri
 // a 16-byte window of the L2-resident table
 __device__ __forceinline__ uint4 win_load(const unsigned* p) { return *reinterpret_cast<const uint4*>(p); }
 
+#ifdef DAUC_CI_LINEAR
+// TEMPORARY experiment: cells linear in the score VALUE over the used top buckets' span (no
+// top-bucket lookup): cell = clamp(floor((v - lo) * scale), 0, C - 1), monotone in the key
+constexpr int kCiLo = 12, kCiScale = 13;
+__device__ __forceinline__ float key_value(unsigned k) {
+    return __uint_as_float((k & 0x80000000u) ? (k ^ 0x80000000u) : ~k);
+}
+__device__ __forceinline__ unsigned lin_cell(unsigned k, float lo, float scale, float cm1) {
+    const float t = __fmul_rn(__fsub_rn(key_value(k), lo), scale);
+    return static_cast<unsigned>(fminf(fmaxf(t, 0.0f), cm1));
+}
+#endif
+
 // Phase 1 of one query: cell, rank_lo, count and (lanes with cnt > 0) the window load
 __device__ __forceinline__ void ci_locate(unsigned x, const uint2* __restrict__ l1, const uint2* __restrict__ blk,
                                           const unsigned* __restrict__ sorted, unsigned& rl, unsigned& cnt,
@@ -903,6 +916,10 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
     }
     extern __shared__ uint2 ci_lds[];
     const int nb = static_cast<int>(meta[kCiBlocks]);
+#ifdef DAUC_CI_LINEAR
+    const float lin_lo = __uint_as_float(meta[kCiLo]), lin_scale = __uint_as_float(meta[kCiScale]);
+    const float lin_cm1 = static_cast<float>(meta[kCiCells] - 1u);
+#endif
     uint2* l1 = ci_lds;          // [2048]
     uint2* blk = ci_lds + kCiTop;  // [nb]
     {
@@ -1026,6 +1043,10 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
             unsigned c[NQ];
 #pragma unroll
             for (int q = 0; q < NQ; ++q) c[q] = ci_cell(g.x[q], e[q]);
+#ifdef DAUC_CI_LINEAR
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) c[q] = lin_cell(g.x[q], lin_lo, lin_scale, lin_cm1);
+#endif
             uint2 b[NQ];
 #pragma unroll
             for (int q = 0; q < NQ; ++q) b[q] = blk[c[q] / kCiBlock];
@@ -1259,12 +1280,46 @@ __global__ __launch_bounds__(kDirectThreads) void direct_count_kernel(const floa
     const unsigned total = totals[1];
     // usable: at most 1.5 keys per cell, and the table fits the workspace (M <= mcap)
     const bool ok = num > 0 && 3 * num >= 2 * M && total <= static_cast<unsigned>(kCiMaxCells) && M <= mcap;
+#ifdef DAUC_CI_LINEAR
+    // the span of the used top buckets: lo = the first one's lowest value, hi = the last one's highest
+    __shared__ unsigned span[2];
+    {
+        unsigned tmin = 0xffffffffu, tmax = 0u;
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            if (n[j]) {
+                const unsigned t = 8 * threadIdx.x + j;
+                tmin = t < tmin ? t : tmin;
+                tmax = t > tmax ? t : tmax;
+            }
+        const unsigned mn = block_incl_scan1024<true>(tmin, wtot);
+        const unsigned mx = 0xffffffffu - block_incl_scan1024<true>(0xffffffffu - tmax, wtot);
+        if (threadIdx.x == kDirectThreads - 1) {
+            span[0] = mn;
+            span[1] = mx;
+        }
+        __syncthreads();
+    }
+    const unsigned C_lin = static_cast<unsigned>(num + totals[0] - 1 < int64_t(kCiMaxCells) - 1 ? num + totals[0] - 1
+                                                                                                 : int64_t(kCiMaxCells) - 1);
+    const float lin_lo = key_value(span[0] << kCiLowBits), lin_hi = key_value((span[1] << kCiLowBits) | 0x1fffffu);
+    const float lin_scale = static_cast<float>(C_lin) / (lin_hi - lin_lo);
+    const float lin_cm1 = static_cast<float>(C_lin - 1u);
+    const unsigned total_lin = C_lin;
+#endif
     if (blockIdx.x == 0) {
         for (int t = threadIdx.x; t < kCiTop; t += kDirectThreads) l1g[t] = l1[t];
         if (threadIdx.x == 0) {
             meta[kCiOk] = ok ? 1u : 0u;
+#ifdef DAUC_CI_LINEAR
+            meta[kCiCells] = total_lin;
+            meta[kCiBlocks] = (total_lin + 1 + kCiBlock - 1) / kCiBlock;
+            meta[kCiLo] = __float_as_uint(lin_lo);
+            meta[kCiScale] = __float_as_uint(lin_scale);
+#else
             meta[kCiCells] = total;
             meta[kCiBlocks] = (total + 1 + kCiBlock - 1) / kCiBlock;
+#endif
             meta[kCiSkew] = 0u;
         }
     }
@@ -1277,6 +1332,9 @@ __global__ __launch_bounds__(kDirectThreads) void direct_count_kernel(const floa
         if (live) {
             const unsigned x = key_fast(pos[i]);
             c = ci_cell(x, l1[x >> kCiLowBits]);
+#ifdef DAUC_CI_LINEAR
+            c = lin_cell(x, lin_lo, lin_scale, lin_cm1);
+#endif
             cell[i] = c;  // the scatter's cell, so it does not walk pos -> key -> plan again
         }
         const unsigned long long act = __ballot(live);

@@ -7,6 +7,7 @@ R=$GRAFT_REPO_ROOT
 D=$R/gpurun_out/r04y
 mkdir -p $D
 timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $D/t0 -o run -- python3 $R/scripts/prof_eval.py 27 0.001 5 > $D/t0.log 2>&1 || exit 1
+DAUC_LIB=$R/tuning/libdauc_lin.so timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $D/lin -o run -- python3 $R/scripts/prof_eval.py 27 0.001 5 > $D/lin.log 2>&1 || exit 1
 for a in 1 2 3; do
   DAUC_LIB=$R/tuning/libdauc_a$a.so timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $D/a$a -o run -- python3 $R/scripts/prof_eval.py 27 0.001 5 > $D/a$a.log 2>&1 || exit 1
 done
