@@ -1085,10 +1085,17 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
             }
         };
         auto locate = [&](Group& g) {
+#if defined(DAUC_CI_ABL) && (DAUC_CI_ABL & 4)  // TEMPORARY ablation (wrong counts): the stream alone
+            return;
+#endif
             locate_lds(g);
             locate_win(g);
         };
         auto count = [&](const Group& g) {
+#if defined(DAUC_CI_ABL) && (DAUC_CI_ABL & 4)
+            w += g.x[0] + g.use;
+            return;
+#endif
             unsigned wl = 0u, tl = 0u;
             bool more = false;
 #pragma unroll
@@ -1137,7 +1144,11 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
         // in order]. D stream buffers keep D groups of score/label loads in flight per lane: with
         // one (D = 1) a wave holds 20 B per lane in flight, 5 MB over the chip, which at HBM's
         // loaded latency caps the stream far below the bandwidth.
+#ifdef DAUC_CI_D  // TEMPORARY experiment: stream groups in flight per lane
+        constexpr int D = DAUC_CI_D;
+#else
         constexpr int D = 1;
+#endif
         constexpr int L = D % 2 == 0 ? D : 2 * D;  // unroll: every buffer index compile-time
         Stream sbuf[D];
         Group gbuf[2];

@@ -84,3 +84,22 @@ for log2n, pr in ((24, 0.01), (27, 0.001)):
         print(json.dumps({"log2n": log2n, "G": G, "fn": "two-step: compact_part + query_part + record read",
                           "ms_part0": t0, "ms_last": tl, "slot_bytes": nb,
                           "sum_matches_whole": (W, T) == (whole[0], whole[1])}), flush=True)
+
+        # device time per rank (HIP events on the stream around `reps` back-to-back enqueued
+        # sequences, no host read in between): what a rank's GPU spends; the wall times above also
+        # hold the Python binding's calls and the record read
+        def dev_ms(fn):
+            fn()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(reps):
+                fn()
+            e1.record()
+            torch.cuda.synchronize()
+            return e0.elapsed_time(e1) / reps
+
+        d_enq = dev_ms(lambda: ops.auc_eval_enqueue(s, y, 0, G, out=rec))
+        d_two = dev_ms(lambda: (ops.auc_eval_compact_part(s, y, 0, G, mine),
+                                ops.auc_eval_query_part(s, y, 0, G, slots, out=rec)))
+        print(json.dumps({"log2n": log2n, "G": G, "fn": "device time per rank (events)",
+                          "ms_enqueue_form": d_enq, "ms_two_step": d_two}), flush=True)

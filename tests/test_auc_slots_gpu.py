@@ -96,7 +96,7 @@ def test_slots_wide_and_special_values(dev, ops):
     y2[:50] = 1
     s2[:25] = -3.4e38
     s2[25:50] = 3.4e38
-    _check(ops, dev, s2, y2, what="extremes")
+    _check(ops, dev, s2, y2, verdict=2, what="extremes")  # 25 tied positives at each extreme: one cell
     # positives only in the middle: queries below the first and above the last used bucket
     s3 = rng.random(n, dtype=np.float32) * 4.0 - 2.0
     y3 = np.where((np.abs(s3) < 0.25) & (rng.random(n) < 0.3), 1, -1).astype(np.int8)

@@ -857,8 +857,19 @@ def test_auc_eval_two_step_parts(dev, ldtype):
         for G in (1, 2, 3, 8):
             recs = _two_step(dev, s, y, G)
             assert {(v[3], v[5], v[6]) for v in recs} == {(e["P"], 0, int((y == 0).sum()))}, (p, G)
-            assert {v[7] for v in recs} == {1}, (p, G, recs)
-            assert (sum(v[0] for v in recs), sum(v[1] for v in recs)) == (e["wins"], e["ties"]), (p, G)
+            verdicts = {v[7] for v in recs}
+            # 5000 score levels: at p = 0.2 every level holds ~12 positives, so cells of 15+ keys
+            # make the index refuse the table (verdict 2 on every part: the blocking sorted path)
+            assert verdicts == ({2} if p == 0.2 else {1}), (p, G, recs)
+            if verdicts == {1}:
+                assert (sum(v[0] for v in recs), sum(v[1] for v in recs)) == (e["wins"], e["ties"]), (p, G)
+            else:
+                W = Tt = 0
+                for r in range(G):
+                    o = ops.auc_eval_counts_part(T(s, dev), T(y, dev), r, G,
+                                                 torch.zeros(3, dtype=torch.int64, device=dev))
+                    W, Tt = W + o[0], Tt + o[1]
+                assert (W, Tt) == (e["wins"], e["ties"]), (p, G)
     # unshuffled: every positive in the first slice
     y = np.where(np.arange(n) < 30_000, 1, -1).astype(ldtype)  # slice 0 holds 30000 > its slot (23502)
     e = coracle.auc_counts(y.astype(np.int64), s)
