@@ -239,7 +239,11 @@ __global__ __launch_bounds__(kSortThreads) void radix_scatter_kernel(const void*
 // load -- up to M = 160,000 table keys (2^27 scores at 0.1 % positives: M = 134,447 -> k = 4).
 constexpr int kMaxSplit = 40000;
 constexpr size_t kTreeBytes = (size_t(kMaxSplit) + 64) * 4;  // nodes of 4 keys + per-level padding nodes
+#ifdef DAUC_CI_THREADS  // TEMPORARY experiment: query workgroup size
+constexpr int kQueryThreads = DAUC_CI_THREADS;
+#else
 constexpr int kQueryThreads = 1024;
+#endif
 
 // The S splitters are the in-order keys of a perfect 5-ary search tree of height H (5^(H-1) <= S
 // + 1 <= 5^H): a node is 4 keys (16 B, one ds_read_b128) and routes a query to child
@@ -983,7 +987,11 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
         // issue order: keys(g) [waits for the stream loads issued one group earlier], stream
         // loads of g+1, LDS lookups of g, window loads of g, count of g-1 [waits for the windows
         // issued one group earlier; the younger loads stay in flight: vmcnt retires in order].
+#ifdef DAUC_CI_U  // TEMPORARY experiment
+        constexpr int U = DAUC_CI_U;
+#else
         constexpr int U = 1;  // one float4 slot per lane per group (more slots spill registers)
+#endif
         constexpr int NQ = 4 * U;
         const int64_t step = int64_t(U) * stride;
         // two sets of every per-group register (A and B, used alternately by an unrolled pair of

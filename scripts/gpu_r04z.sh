@@ -7,7 +7,7 @@ R=$GRAFT_REPO_ROOT
 D=$R/gpurun_out/r04z
 mkdir -p $D
 timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $D/t0 -o run -- python3 $R/scripts/prof_eval.py 27 0.001 5 > $D/t0.log 2>&1 || exit 1
-for v in s1 s4 d2 d4; do
+for v in s1 s4 d2 d4 w1 w4 w8 wu; do
   DAUC_LIB=$R/tuning/libdauc_$v.so timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $D/$v -o run -- python3 $R/scripts/prof_eval.py 27 0.001 5 > $D/$v.log 2>&1 || exit 1
 done
 cd $R
