@@ -1072,6 +1072,9 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
 #ifdef DAUC_CI_THIN  // TEMPORARY ablation (wrong counts): fewer window gathers
                 if (g.x[q] & DAUC_CI_THIN) cnt = 0u;
 #endif
+#if defined(DAUC_CI_ABL) && (DAUC_CI_ABL & 8)  // TEMPORARY ablation (wrong counts): no gathers at all
+                cnt = 0u;
+#endif
                 g.rc[q] = rl | (cnt << 28);
             }
         };
