@@ -1094,6 +1094,14 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
                 const unsigned rl = g.rc[q] & 0x0fffffffu, cnt = g.rc[q] >> 28;
                 g.k2[q] = win_load(sorted + ((rl & 3u) + cnt > 4u ? (rl & ~3u) + 4u : 0u));
             }
+#if defined(DAUC_CI_ABL) && (DAUC_CI_ABL & 48)  // TEMPORARY ablation (wrong counts): windows from registers
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                const unsigned rl = g.rc[q] & 0x0fffffffu;
+                if (DAUC_CI_ABL & 16) g.k[q] = uint4{rl, rl + 1u, rl + 2u, rl + 3u};
+                g.k2[q] = uint4{rl + 4u, rl + 5u, rl + 6u, rl + 7u};
+            }
+#endif
         };
         auto locate = [&](Group& g) {
 #if defined(DAUC_CI_ABL) && (DAUC_CI_ABL & 4)  // TEMPORARY ablation (wrong counts): the stream alone
