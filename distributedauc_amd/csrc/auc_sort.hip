@@ -816,6 +816,16 @@ __global__ __launch_bounds__(256) void ci_blocks_kernel(const unsigned* __restri
 // a 16-byte window of the L2-resident table
 __device__ __forceinline__ uint4 win_load(const unsigned* p) { return *reinterpret_cast<const uint4*>(p); }
 
+#ifdef DAUC_CI_UNAL
+// TEMPORARY experiment: 4 keys from any 4-byte aligned position (one dwordx4 load)
+typedef unsigned u4a4 __attribute__((ext_vector_type(4), aligned(4)));
+__device__ __forceinline__ uint4 win_load_u(const unsigned* p) {
+    const u4a4 v = *reinterpret_cast<const u4a4*>(p);
+    return uint4{v.x, v.y, v.z, v.w};
+}
+constexpr int kListCap = 64;  // long-cell entries per wave
+#endif
+
 #ifdef DAUC_CI_LINEAR
 // TEMPORARY experiment: cells linear in the score VALUE over the used top buckets' span (no
 // top-bucket lookup): cell = clamp(floor((v - lo) * scale), 0, C - 1), monotone in the key
@@ -1020,9 +1030,34 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
         struct Group {
             unsigned x[NQ], rc[NQ];
             uint4 k[NQ];
+#ifndef DAUC_CI_UNAL
             uint4 k2[NQ];  // the next window, for cells that run past the first
+#endif
             unsigned use;
         };
+#ifdef DAUC_CI_UNAL
+        // the cells of 5+ keys: queued per wave in LDS as {x, rank of the cell's 5th key | the keys
+        // left << 28} and counted from the table when the list fills and after the loop (a load in
+        // the loop's branch would make every later wait a full vmcnt(0))
+        uint2* list = reinterpret_cast<uint2*>(blk + kCiMaxBlocks) + (threadIdx.x / kWave) * kListCap;
+        const unsigned wlane = threadIdx.x & (kWave - 1);
+        unsigned nlist = 0u;
+        auto flush = [&]() {
+            for (unsigned e = wlane; e < nlist; e += kWave) {
+                const uint2 v = list[e];
+                const unsigned r0 = v.y & 0x0fffffffu, c = v.y >> 28;
+                unsigned lt = 0u, le = 0u;
+                for (unsigned q = 0; q < c; ++q) {
+                    const unsigned kk = sorted[r0 + q];
+                    lt += kk < v.x;
+                    le += kk <= v.x;
+                }
+                w -= le;
+                t += le - lt;
+            }
+            nlist = 0u;
+        };
+#endif
         auto keys = [&](Group& g, const Stream& sg) {
             g.use = 0u;
 #pragma unroll
@@ -1079,6 +1114,15 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
             }
         };
         auto locate_win = [&](Group& g) {
+#ifdef DAUC_CI_UNAL
+            // the cell's first 4 keys (lanes without a key read the table's +inf padding)
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                const unsigned rl = g.rc[q] & 0x0fffffffu;
+                g.k[q] = win_load_u(sorted + ((g.rc[q] >> 28) ? rl : M32));
+            }
+            return;
+#endif
 #pragma unroll
             for (int q = 0; q < NQ; ++q) {
                 const unsigned rl = g.rc[q] & 0x0fffffffu;
@@ -1089,11 +1133,13 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
             // a branch after the count it was waited for with vmcnt(0) -- every load in flight,
             // the stream's included -- in nearly every iteration of every wave. Lanes that do not
             // need it load the table's first window (one shared line).
+#ifndef DAUC_CI_UNAL
 #pragma unroll
             for (int q = 0; q < NQ; ++q) {
                 const unsigned rl = g.rc[q] & 0x0fffffffu, cnt = g.rc[q] >> 28;
                 g.k2[q] = win_load(sorted + ((rl & 3u) + cnt > 4u ? (rl & ~3u) + 4u : 0u));
             }
+#endif
 #if defined(DAUC_CI_ABL) && (DAUC_CI_ABL & 48)  // TEMPORARY ablation (wrong counts): windows from registers
 #pragma unroll
             for (int q = 0; q < NQ; ++q) {
@@ -1115,6 +1161,36 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
             w += g.x[0] + g.use;
             return;
 #endif
+#ifdef DAUC_CI_UNAL
+            {
+                unsigned wl = 0u, tl = 0u;
+#pragma unroll
+                for (int q = 0; q < NQ; ++q) {
+                    const unsigned x = g.x[q], rl = g.rc[q] & 0x0fffffffu, cnt = g.rc[q] >> 28;
+                    const bool use = (g.use >> q) & 1u;
+                    const uint4 k = g.k[q];
+                    // keys past the cell are later cells' (> x) or the +inf padding
+                    const unsigned lt = (k.x < x) + (k.y < x) + (k.z < x) + (k.w < x);
+                    const unsigned le = (k.x <= x) + (k.y <= x) + (k.z <= x) + (k.w <= x);
+                    wl += use ? M32 - (rl + le) : 0u;
+                    tl += use ? le - lt : 0u;
+                    const bool lg = use && cnt > 4u;
+                    const unsigned long long m = __ballot(lg);
+                    if (m != 0ull) {
+                        const unsigned nm = static_cast<unsigned>(__popcll(m));
+                        if (nlist + nm > static_cast<unsigned>(kListCap)) flush();
+                        const unsigned below = __builtin_amdgcn_mbcnt_hi(static_cast<unsigned>(m >> 32),
+                                                                        __builtin_amdgcn_mbcnt_lo(static_cast<unsigned>(m), 0u));
+                        if (lg) list[nlist + below] = uint2{x, (rl + 4u) | ((cnt - 4u) << 28)};
+                        nlist += nm;
+                    }
+                }
+                w += wl;
+                t += tl;
+                return;
+            }
+#endif
+#ifndef DAUC_CI_UNAL
             unsigned wl = 0u, tl = 0u;
             bool more = false;
 #pragma unroll
@@ -1156,6 +1232,7 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
                 }
             }
             (void)more;
+#endif
         };
         // per group g: keys(g) [its stream loads were issued D groups earlier], stream loads of
         // g + D into the buffer just read, LDS lookups + window loads of g, count of g - 1 [its
@@ -1196,6 +1273,9 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
             }
         }
     ci_stream_done:;
+#ifdef DAUC_CI_UNAL
+        flush();
+#endif
     } else {
         for (int64_t v = tid; v < nvec; v += stride)
             for (int q = 0; q < 4; ++q) one(head + v * 4 + q);
@@ -1732,7 +1812,11 @@ int launch_ci(const float* s, const LT* lab, int64_t begin, int64_t end, const C
               int64_t M, unsigned long long* out, unsigned long long* nonfinite, hipStream_t st,
               unsigned* verdict = nullptr, const unsigned* grp = nullptr, const unsigned long long* Mp = nullptr) {
     const dim3 grid(query_grid(end - begin)), block(kQueryThreads);
+#ifdef DAUC_CI_UNAL
+    const size_t lds = (size_t(kCiTop) + kCiMaxBlocks) * 8 + size_t(kQueryThreads / kWave) * kListCap * 8;
+#else
     const size_t lds = (size_t(kCiTop) + kCiMaxBlocks) * 8 + (grp ? size_t(kDirectMaxGroups) * 4 : 0);
+#endif
     hipLaunchKernelGGL((query_ci_kernel<LT>), grid, block, lds, st, s, lab, begin, end, cw.meta, cw.l1, cw.blk, sorted,
                        M, out, nonfinite, verdict, grp, Mp);
     return launch_status();
