@@ -1030,6 +1030,10 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
         struct Group {
             unsigned x[NQ], rc[NQ];
             uint4 k[NQ];
+#ifdef DAUC_CI_ILV
+            unsigned c[NQ];  // cells and block words, held across the previous group's count
+            uint2 b[NQ];
+#endif
 #ifndef DAUC_CI_UNAL
             uint4 k2[NQ];  // the next window, for cells that run past the first
 #endif
@@ -1113,6 +1117,28 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
                 g.rc[q] = rl | (cnt << 28);
             }
         };
+#ifdef DAUC_CI_ILV  // TEMPORARY experiment: the block-word reads' latency under the previous count
+        auto locate_issue = [&](Group& g) {
+            uint2 e[NQ];
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) e[q] = l1[g.x[q] >> kCiLowBits];
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) g.c[q] = ci_cell(g.x[q], e[q]);
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) g.b[q] = blk[g.c[q] / kCiBlock];
+        };
+        auto locate_decode = [&](Group& g) {
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                const unsigned sh = 4u * (g.c[q] % kCiBlock);
+                const unsigned below = __builtin_amdgcn_ubfe(g.b[q].y, 0u, sh);
+                const unsigned bytes = (below & 0x0f0f0f0fu) + ((below >> 4) & 0x0f0f0f0fu);
+                const unsigned rl = g.b[q].x + __builtin_amdgcn_sad_u8(bytes, 0u, 0u);
+                const unsigned cnt = __builtin_amdgcn_ubfe(g.b[q].y, sh, 4u);
+                g.rc[q] = rl | (cnt << 28);
+            }
+        };
+#endif
         auto locate_win = [&](Group& g) {
 #ifdef DAUC_CI_UNAL
             // the cell's first 4 keys (lanes without a key read the table's +inf padding)
@@ -1267,8 +1293,15 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
                 keys(gc, sbuf[(j + 1) % D]);
                 load(sbuf[(j + 1) % D], v + int64_t(D) * step);
                 asm volatile("" ::: "memory");  // the stream loads stay older than this group's windows
+#ifdef DAUC_CI_ILV
+                locate_issue(gc);
+                count(gp);
+                locate_decode(gc);
+                locate_win(gc);
+#else
                 locate(gc);
                 count(gp);
+#endif
                 v += step;
             }
         }
