@@ -1124,6 +1124,10 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
             for (int q = 0; q < NQ; ++q) e[q] = l1[g.x[q] >> kCiLowBits];
 #pragma unroll
             for (int q = 0; q < NQ; ++q) g.c[q] = ci_cell(g.x[q], e[q]);
+#ifdef DAUC_CI_LINEAR
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) g.c[q] = lin_cell(g.x[q], lin_lo, lin_scale, lin_cm1);
+#endif
 #pragma unroll
             for (int q = 0; q < NQ; ++q) g.b[q] = blk[g.c[q] / kCiBlock];
         };

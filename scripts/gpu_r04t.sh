@@ -7,7 +7,7 @@ R=$GRAFT_REPO_ROOT
 D=$R/gpurun_out/r04t
 mkdir -p $D
 timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $D/t0 -o run -- python3 $R/scripts/prof_eval.py 27 0.001 5 > $D/t0.log 2>&1 || exit 1
-for v in un ui ui2; do
+for v in un ui ui2 uil; do
   DAUC_LIB=$R/tuning/libdauc_$v.so timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $D/$v -o run -- python3 $R/scripts/prof_eval.py 27 0.001 5 > $D/$v.log 2>&1 || exit 1
 done
 cd $R
