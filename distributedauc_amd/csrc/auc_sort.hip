@@ -1276,6 +1276,41 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
         constexpr int D = 1;
 #endif
         constexpr int L = D % 2 == 0 ? D : 2 * D;  // unroll: every buffer index compile-time
+#ifdef DAUC_CI_P3  // TEMPORARY experiment: windows counted two groups after they are issued
+        Stream sbuf[D];
+        Group gbuf[3];
+#pragma unroll
+        for (int j = 0; j < D; ++j) load(sbuf[j], tid + int64_t(j) * step);
+        keys(gbuf[0], sbuf[0]);
+        load(sbuf[0], tid + int64_t(D) * step);
+        locate(gbuf[0]);
+        keys(gbuf[1], sbuf[1 % D]);
+        load(sbuf[1 % D], tid + int64_t(D + 1) * step);
+        locate(gbuf[1]);
+        int64_t v = tid + 2 * step;
+        constexpr int L3 = D % 3 == 0 ? D : 3 * D;
+        for (;;) {
+#pragma unroll
+            for (int j = 0; j < L3; ++j) {
+                Group& gc = gbuf[(j + 2) % 3];
+                Group& gp = gbuf[(j + 1) % 3];
+                Group& gpp = gbuf[j % 3];
+                if (v >= nvec) {
+                    count(gpp);
+                    count(gp);
+                    goto ci_stream_done;
+                }
+                keys(gc, sbuf[(j + 2) % D]);
+                load(sbuf[(j + 2) % D], v + int64_t(D) * step);
+                asm volatile("" ::: "memory");
+                locate_issue(gc);
+                count(gpp);
+                locate_decode(gc);
+                locate_win(gc);
+                v += step;
+            }
+        }
+#else
         Stream sbuf[D];
         Group gbuf[2];
 #pragma unroll
@@ -1309,6 +1344,7 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
                 v += step;
             }
         }
+#endif
     ci_stream_done:;
 #ifdef DAUC_CI_UNAL
         flush();
