@@ -48,8 +48,11 @@ struct EvalWs {
     int64_t* split_stats;         // [4]   the split's stats (sorted fallback)
     void* sws;                    // split workspace
     void* tws;                    // sort + tree + count-index workspace (a table of at most n/2 keys)
-    void* bws;                    // the range-slot path's (auc_slots.hip): index, split queries, tile runs
-    size_t sws_bytes, tws_bytes, bws_bytes;
+    size_t sws_bytes, tws_bytes;
+#ifdef DAUC_TUNING
+    void* bws;                    // the range-slot path's (tuning_slots.hip): index, split queries, tile runs
+    size_t bws_bytes;
+#endif
 };
 
 EvalWs eval_ws(void* ws, int64_t n) {
@@ -71,14 +74,21 @@ EvalWs eval_ws(void* ws, int64_t n) {
     w.tws_bytes = dauc_sort_workspace_size(n / 2 + 1);
     w.tws = p;
     p += align256(w.tws_bytes);
+#ifdef DAUC_TUNING
     w.bws_bytes = slot_index_workspace_size(n);
     w.bws = p;
+#endif
     return w;
 }
 
 size_t eval_ws_bytes(int64_t n) {
-    return kHdr + align256(size_t(n) * 4) + align256(size_t(n / 2 + 1) * 4) + align256(dauc_split_workspace_size(n)) +
-           align256(dauc_sort_workspace_size(n / 2 + 1)) + align256(slot_index_workspace_size(n));
+    const size_t b = kHdr + align256(size_t(n) * 4) + align256(size_t(n / 2 + 1) * 4) +
+                     align256(dauc_split_workspace_size(n)) + align256(dauc_sort_workspace_size(n / 2 + 1));
+#ifdef DAUC_TUNING
+    return b + align256(slot_index_workspace_size(n));
+#else
+    return b;
+#endif
 }
 
 bool valid_args(const float* scores, const void* labels, int label_dtype, int64_t n, int part, int parts,
@@ -106,9 +116,11 @@ int enqueue(const float* scores, const void* labels, int label_dtype, int64_t n,
         // a tuning build forcing another search structure: straight to the sorted path
         return -static_cast<int>(hipMemsetAsync(w.verdict, 2, 1, st));
     }
+#ifdef DAUC_TUNING
     if (eval_query_path() == 2)
         return counts_slotted(w.pos, w.slot, slot_index_capacity(n), scores, labels, label_dtype, qlo, qhi, w.wt,
                               w.wt + 2, w.verdict, w.bws, w.bws_bytes, st);
+#endif
     return counts_labeled_direct(w.pos, w.slot, mcap, scores, labels, label_dtype, qlo, qhi, w.wt, w.wt + 2,
                                  w.verdict, w.tws, w.tws_bytes, st);
 }
@@ -321,11 +333,14 @@ int dauc_auc_eval_query_part(const float* scores, const void* labels, int label_
     const int64_t qlo = n * part / parts, qhi = n * (part + 1) / parts;
     if (qhi > qlo) {
         // the build and the query see m_eff (w.spare[0]): P, or past the index's capacity on overflow
-        rc = eval_query_path() == 2
-                 ? counts_slotted(w.pos, w.spare, mcap, scores, labels, label_dtype, qlo, qhi, w.wt, w.wt + 2,
-                                  w.verdict, w.bws, w.bws_bytes, st)
-                 : counts_labeled_direct(w.pos, w.spare, mcap, scores, labels, label_dtype, qlo, qhi, w.wt, w.wt + 2,
-                                         w.verdict, w.tws, w.tws_bytes, st);
+#ifdef DAUC_TUNING
+        if (eval_query_path() == 2)
+            rc = counts_slotted(w.pos, w.spare, mcap, scores, labels, label_dtype, qlo, qhi, w.wt, w.wt + 2, w.verdict,
+                                w.bws, w.bws_bytes, st);
+        else
+#endif
+            rc = counts_labeled_direct(w.pos, w.spare, mcap, scores, labels, label_dtype, qlo, qhi, w.wt, w.wt + 2,
+                                       w.verdict, w.tws, w.tws_bytes, st);
         if (rc) return rc;
     }
     return -static_cast<int>(hipMemcpyAsync(part_out, w.wt, kRecord, hipMemcpyDeviceToDevice, st));

@@ -239,11 +239,7 @@ __global__ __launch_bounds__(kSortThreads) void radix_scatter_kernel(const void*
 // load -- up to M = 160,000 table keys (2^27 scores at 0.1 % positives: M = 134,447 -> k = 4).
 constexpr int kMaxSplit = 40000;
 constexpr size_t kTreeBytes = (size_t(kMaxSplit) + 64) * 4;  // nodes of 4 keys + per-level padding nodes
-#ifdef DAUC_CI_THREADS  // TEMPORARY experiment: query workgroup size
-constexpr int kQueryThreads = DAUC_CI_THREADS;
-#else
 constexpr int kQueryThreads = 1024;
-#endif
 
 // The S splitters are the in-order keys of a perfect 5-ary search tree of height H (5^(H-1) <= S
 // + 1 <= 5^H): a node is 4 keys (16 B, one ds_read_b128) and routes a query to child
@@ -816,29 +812,6 @@ __global__ __launch_bounds__(256) void ci_blocks_kernel(const unsigned* __restri
 // a 16-byte window of the L2-resident table
 __device__ __forceinline__ uint4 win_load(const unsigned* p) { return *reinterpret_cast<const uint4*>(p); }
 
-#ifdef DAUC_CI_UNAL
-// TEMPORARY experiment: 4 keys from any 4-byte aligned position (one dwordx4 load)
-typedef unsigned u4a4 __attribute__((ext_vector_type(4), aligned(4)));
-__device__ __forceinline__ uint4 win_load_u(const unsigned* p) {
-    const u4a4 v = *reinterpret_cast<const u4a4*>(p);
-    return uint4{v.x, v.y, v.z, v.w};
-}
-constexpr int kListCap = 64;  // long-cell entries per wave
-#endif
-
-#ifdef DAUC_CI_LINEAR
-// TEMPORARY experiment: cells linear in the score VALUE over the used top buckets' span (no
-// top-bucket lookup): cell = clamp(floor((v - lo) * scale), 0, C - 1), monotone in the key
-constexpr int kCiLo = 12, kCiScale = 13;
-__device__ __forceinline__ float key_value(unsigned k) {
-    return __uint_as_float((k & 0x80000000u) ? (k ^ 0x80000000u) : ~k);
-}
-__device__ __forceinline__ unsigned lin_cell(unsigned k, float lo, float scale, float cm1) {
-    const float t = __fmul_rn(__fsub_rn(key_value(k), lo), scale);
-    return static_cast<unsigned>(fminf(fmaxf(t, 0.0f), cm1));
-}
-#endif
-
 // Phase 1 of one query: cell, rank_lo, count and (lanes with cnt > 0) the window load
 __device__ __forceinline__ void ci_locate(unsigned x, const uint2* __restrict__ l1, const uint2* __restrict__ blk,
                                           const unsigned* __restrict__ sorted, unsigned& rl, unsigned& cnt,
@@ -930,10 +903,6 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
     }
     extern __shared__ uint2 ci_lds[];
     const int nb = static_cast<int>(meta[kCiBlocks]);
-#ifdef DAUC_CI_LINEAR
-    const float lin_lo = __uint_as_float(meta[kCiLo]), lin_scale = __uint_as_float(meta[kCiScale]);
-    const float lin_cm1 = static_cast<float>(meta[kCiCells] - 1u);
-#endif
     uint2* l1 = ci_lds;          // [2048]
     uint2* blk = ci_lds + kCiTop;  // [nb]
     {
@@ -997,11 +966,7 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
         // issue order: keys(g) [waits for the stream loads issued one group earlier], stream
         // loads of g+1, LDS lookups of g, window loads of g, count of g-1 [waits for the windows
         // issued one group earlier; the younger loads stay in flight: vmcnt retires in order].
-#ifdef DAUC_CI_U  // TEMPORARY experiment
-        constexpr int U = DAUC_CI_U;
-#else
         constexpr int U = 1;  // one float4 slot per lane per group (more slots spill registers)
-#endif
         constexpr int NQ = 4 * U;
         const int64_t step = int64_t(U) * stride;
         // two sets of every per-group register (A and B, used alternately by an unrolled pair of
@@ -1030,38 +995,9 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
         struct Group {
             unsigned x[NQ], rc[NQ];
             uint4 k[NQ];
-#ifdef DAUC_CI_ILV
-            unsigned c[NQ];  // cells and block words, held across the previous group's count
-            uint2 b[NQ];
-#endif
-#ifndef DAUC_CI_UNAL
             uint4 k2[NQ];  // the next window, for cells that run past the first
-#endif
             unsigned use;
         };
-#ifdef DAUC_CI_UNAL
-        // the cells of 5+ keys: queued per wave in LDS as {x, rank of the cell's 5th key | the keys
-        // left << 28} and counted from the table when the list fills and after the loop (a load in
-        // the loop's branch would make every later wait a full vmcnt(0))
-        uint2* list = reinterpret_cast<uint2*>(blk + kCiMaxBlocks) + (threadIdx.x / kWave) * kListCap;
-        const unsigned wlane = threadIdx.x & (kWave - 1);
-        unsigned nlist = 0u;
-        auto flush = [&]() {
-            for (unsigned e = wlane; e < nlist; e += kWave) {
-                const uint2 v = list[e];
-                const unsigned r0 = v.y & 0x0fffffffu, c = v.y >> 28;
-                unsigned lt = 0u, le = 0u;
-                for (unsigned q = 0; q < c; ++q) {
-                    const unsigned kk = sorted[r0 + q];
-                    lt += kk < v.x;
-                    le += kk <= v.x;
-                }
-                w -= le;
-                t += le - lt;
-            }
-            nlist = 0u;
-        };
-#endif
         auto keys = [&](Group& g, const Stream& sg) {
             g.use = 0u;
 #pragma unroll
@@ -1083,76 +1019,23 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
             uint2 e[NQ];
 #pragma unroll
             for (int q = 0; q < NQ; ++q) e[q] = l1[g.x[q] >> kCiLowBits];
-#if defined(DAUC_CI_ABL) && (DAUC_CI_ABL & 1)  // TEMPORARY ablation (wrong counts): no top-bucket read
-#pragma unroll
-            for (int q = 0; q < NQ; ++q) e[q] = uint2{0u, static_cast<unsigned>(nb) * kCiBlock - 8u};
-#endif
             unsigned c[NQ];
 #pragma unroll
             for (int q = 0; q < NQ; ++q) c[q] = ci_cell(g.x[q], e[q]);
-#ifdef DAUC_CI_LINEAR
-#pragma unroll
-            for (int q = 0; q < NQ; ++q) c[q] = lin_cell(g.x[q], lin_lo, lin_scale, lin_cm1);
-#endif
             uint2 b[NQ];
 #pragma unroll
             for (int q = 0; q < NQ; ++q) b[q] = blk[c[q] / kCiBlock];
-#if defined(DAUC_CI_ABL) && (DAUC_CI_ABL & 2)  // TEMPORARY ablation (wrong counts): no block-word read
-#pragma unroll
-            for (int q = 0; q < NQ; ++q) b[q] = uint2{c[q], 0x01010101u};
-#endif
 #pragma unroll
             for (int q = 0; q < NQ; ++q) {
                 const unsigned sh = 4u * (c[q] % kCiBlock);
                 const unsigned below = __builtin_amdgcn_ubfe(b[q].y, 0u, sh);
                 const unsigned bytes = (below & 0x0f0f0f0fu) + ((below >> 4) & 0x0f0f0f0fu);
                 const unsigned rl = b[q].x + __builtin_amdgcn_sad_u8(bytes, 0u, 0u);
-                unsigned cnt = __builtin_amdgcn_ubfe(b[q].y, sh, 4u);
-#ifdef DAUC_CI_THIN  // TEMPORARY ablation (wrong counts): fewer window gathers
-                if (g.x[q] & DAUC_CI_THIN) cnt = 0u;
-#endif
-#if defined(DAUC_CI_ABL) && (DAUC_CI_ABL & 8)  // TEMPORARY ablation (wrong counts): no gathers at all
-                cnt = 0u;
-#endif
+                const unsigned cnt = __builtin_amdgcn_ubfe(b[q].y, sh, 4u);
                 g.rc[q] = rl | (cnt << 28);
             }
         };
-#ifdef DAUC_CI_ILV  // TEMPORARY experiment: the block-word reads' latency under the previous count
-        auto locate_issue = [&](Group& g) {
-            uint2 e[NQ];
-#pragma unroll
-            for (int q = 0; q < NQ; ++q) e[q] = l1[g.x[q] >> kCiLowBits];
-#pragma unroll
-            for (int q = 0; q < NQ; ++q) g.c[q] = ci_cell(g.x[q], e[q]);
-#ifdef DAUC_CI_LINEAR
-#pragma unroll
-            for (int q = 0; q < NQ; ++q) g.c[q] = lin_cell(g.x[q], lin_lo, lin_scale, lin_cm1);
-#endif
-#pragma unroll
-            for (int q = 0; q < NQ; ++q) g.b[q] = blk[g.c[q] / kCiBlock];
-        };
-        auto locate_decode = [&](Group& g) {
-#pragma unroll
-            for (int q = 0; q < NQ; ++q) {
-                const unsigned sh = 4u * (g.c[q] % kCiBlock);
-                const unsigned below = __builtin_amdgcn_ubfe(g.b[q].y, 0u, sh);
-                const unsigned bytes = (below & 0x0f0f0f0fu) + ((below >> 4) & 0x0f0f0f0fu);
-                const unsigned rl = g.b[q].x + __builtin_amdgcn_sad_u8(bytes, 0u, 0u);
-                const unsigned cnt = __builtin_amdgcn_ubfe(g.b[q].y, sh, 4u);
-                g.rc[q] = rl | (cnt << 28);
-            }
-        };
-#endif
         auto locate_win = [&](Group& g) {
-#ifdef DAUC_CI_UNAL
-            // the cell's first 4 keys (lanes without a key read the table's +inf padding)
-#pragma unroll
-            for (int q = 0; q < NQ; ++q) {
-                const unsigned rl = g.rc[q] & 0x0fffffffu;
-                g.k[q] = win_load_u(sorted + ((g.rc[q] >> 28) ? rl : M32));
-            }
-            return;
-#endif
 #pragma unroll
             for (int q = 0; q < NQ; ++q) {
                 const unsigned rl = g.rc[q] & 0x0fffffffu;
@@ -1163,64 +1046,17 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
             // a branch after the count it was waited for with vmcnt(0) -- every load in flight,
             // the stream's included -- in nearly every iteration of every wave. Lanes that do not
             // need it load the table's first window (one shared line).
-#ifndef DAUC_CI_UNAL
 #pragma unroll
             for (int q = 0; q < NQ; ++q) {
                 const unsigned rl = g.rc[q] & 0x0fffffffu, cnt = g.rc[q] >> 28;
                 g.k2[q] = win_load(sorted + ((rl & 3u) + cnt > 4u ? (rl & ~3u) + 4u : 0u));
             }
-#endif
-#if defined(DAUC_CI_ABL) && (DAUC_CI_ABL & 48)  // TEMPORARY ablation (wrong counts): windows from registers
-#pragma unroll
-            for (int q = 0; q < NQ; ++q) {
-                const unsigned rl = g.rc[q] & 0x0fffffffu;
-                if (DAUC_CI_ABL & 16) g.k[q] = uint4{rl, rl + 1u, rl + 2u, rl + 3u};
-                g.k2[q] = uint4{rl + 4u, rl + 5u, rl + 6u, rl + 7u};
-            }
-#endif
         };
         auto locate = [&](Group& g) {
-#if defined(DAUC_CI_ABL) && (DAUC_CI_ABL & 4)  // TEMPORARY ablation (wrong counts): the stream alone
-            return;
-#endif
             locate_lds(g);
             locate_win(g);
         };
         auto count = [&](const Group& g) {
-#if defined(DAUC_CI_ABL) && (DAUC_CI_ABL & 4)
-            w += g.x[0] + g.use;
-            return;
-#endif
-#ifdef DAUC_CI_UNAL
-            {
-                unsigned wl = 0u, tl = 0u;
-#pragma unroll
-                for (int q = 0; q < NQ; ++q) {
-                    const unsigned x = g.x[q], rl = g.rc[q] & 0x0fffffffu, cnt = g.rc[q] >> 28;
-                    const bool use = (g.use >> q) & 1u;
-                    const uint4 k = g.k[q];
-                    // keys past the cell are later cells' (> x) or the +inf padding
-                    const unsigned lt = (k.x < x) + (k.y < x) + (k.z < x) + (k.w < x);
-                    const unsigned le = (k.x <= x) + (k.y <= x) + (k.z <= x) + (k.w <= x);
-                    wl += use ? M32 - (rl + le) : 0u;
-                    tl += use ? le - lt : 0u;
-                    const bool lg = use && cnt > 4u;
-                    const unsigned long long m = __ballot(lg);
-                    if (m != 0ull) {
-                        const unsigned nm = static_cast<unsigned>(__popcll(m));
-                        if (nlist + nm > static_cast<unsigned>(kListCap)) flush();
-                        const unsigned below = __builtin_amdgcn_mbcnt_hi(static_cast<unsigned>(m >> 32),
-                                                                        __builtin_amdgcn_mbcnt_lo(static_cast<unsigned>(m), 0u));
-                        if (lg) list[nlist + below] = uint2{x, (rl + 4u) | ((cnt - 4u) << 28)};
-                        nlist += nm;
-                    }
-                }
-                w += wl;
-                t += tl;
-                return;
-            }
-#endif
-#ifndef DAUC_CI_UNAL
             unsigned wl = 0u, tl = 0u;
             bool more = false;
 #pragma unroll
@@ -1262,7 +1098,6 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
                 }
             }
             (void)more;
-#endif
         };
         // per group g: keys(g) [its stream loads were issued D groups earlier], stream loads of
         // g + D into the buffer just read, LDS lookups + window loads of g, count of g - 1 [its
@@ -1270,47 +1105,8 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
         // in order]. D stream buffers keep D groups of score/label loads in flight per lane: with
         // one (D = 1) a wave holds 20 B per lane in flight, 5 MB over the chip, which at HBM's
         // loaded latency caps the stream far below the bandwidth.
-#ifdef DAUC_CI_D  // TEMPORARY experiment: stream groups in flight per lane
-        constexpr int D = DAUC_CI_D;
-#else
         constexpr int D = 1;
-#endif
         constexpr int L = D % 2 == 0 ? D : 2 * D;  // unroll: every buffer index compile-time
-#ifdef DAUC_CI_P3  // TEMPORARY experiment: windows counted two groups after they are issued
-        Stream sbuf[D];
-        Group gbuf[3];
-#pragma unroll
-        for (int j = 0; j < D; ++j) load(sbuf[j], tid + int64_t(j) * step);
-        keys(gbuf[0], sbuf[0]);
-        load(sbuf[0], tid + int64_t(D) * step);
-        locate(gbuf[0]);
-        keys(gbuf[1], sbuf[1 % D]);
-        load(sbuf[1 % D], tid + int64_t(D + 1) * step);
-        locate(gbuf[1]);
-        int64_t v = tid + 2 * step;
-        constexpr int L3 = D % 3 == 0 ? D : 3 * D;
-        for (;;) {
-#pragma unroll
-            for (int j = 0; j < L3; ++j) {
-                Group& gc = gbuf[(j + 2) % 3];
-                Group& gp = gbuf[(j + 1) % 3];
-                Group& gpp = gbuf[j % 3];
-                if (v >= nvec) {
-                    count(gpp);
-                    count(gp);
-                    goto ci_stream_done;
-                }
-                keys(gc, sbuf[(j + 2) % D]);
-                load(sbuf[(j + 2) % D], v + int64_t(D) * step);
-                asm volatile("" ::: "memory");
-                locate_issue(gc);
-                count(gpp);
-                locate_decode(gc);
-                locate_win(gc);
-                v += step;
-            }
-        }
-#else
         Stream sbuf[D];
         Group gbuf[2];
 #pragma unroll
@@ -1332,23 +1128,12 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
                 keys(gc, sbuf[(j + 1) % D]);
                 load(sbuf[(j + 1) % D], v + int64_t(D) * step);
                 asm volatile("" ::: "memory");  // the stream loads stay older than this group's windows
-#ifdef DAUC_CI_ILV
-                locate_issue(gc);
-                count(gp);
-                locate_decode(gc);
-                locate_win(gc);
-#else
                 locate(gc);
                 count(gp);
-#endif
                 v += step;
             }
         }
-#endif
     ci_stream_done:;
-#ifdef DAUC_CI_UNAL
-        flush();
-#endif
     } else {
         for (int64_t v = tid; v < nvec; v += stride)
             for (int q = 0; q < 4; ++q) one(head + v * 4 + q);
@@ -1463,46 +1248,12 @@ __global__ __launch_bounds__(kDirectThreads) void direct_count_kernel(const floa
     const unsigned total = totals[1];
     // usable: at most 1.5 keys per cell, and the table fits the workspace (M <= mcap)
     const bool ok = num > 0 && 3 * num >= 2 * M && total <= static_cast<unsigned>(kCiMaxCells) && M <= mcap;
-#ifdef DAUC_CI_LINEAR
-    // the span of the used top buckets: lo = the first one's lowest value, hi = the last one's highest
-    __shared__ unsigned span[2];
-    {
-        unsigned tmin = 0xffffffffu, tmax = 0u;
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-            if (n[j]) {
-                const unsigned t = 8 * threadIdx.x + j;
-                tmin = t < tmin ? t : tmin;
-                tmax = t > tmax ? t : tmax;
-            }
-        const unsigned mn = block_incl_scan1024<true>(tmin, wtot);
-        const unsigned mx = 0xffffffffu - block_incl_scan1024<true>(0xffffffffu - tmax, wtot);
-        if (threadIdx.x == kDirectThreads - 1) {
-            span[0] = mn;
-            span[1] = mx;
-        }
-        __syncthreads();
-    }
-    const unsigned C_lin = static_cast<unsigned>(num + totals[0] - 1 < int64_t(kCiMaxCells) - 1 ? num + totals[0] - 1
-                                                                                                 : int64_t(kCiMaxCells) - 1);
-    const float lin_lo = key_value(span[0] << kCiLowBits), lin_hi = key_value((span[1] << kCiLowBits) | 0x1fffffu);
-    const float lin_scale = static_cast<float>(C_lin) / (lin_hi - lin_lo);
-    const float lin_cm1 = static_cast<float>(C_lin - 1u);
-    const unsigned total_lin = C_lin;
-#endif
     if (blockIdx.x == 0) {
         for (int t = threadIdx.x; t < kCiTop; t += kDirectThreads) l1g[t] = l1[t];
         if (threadIdx.x == 0) {
             meta[kCiOk] = ok ? 1u : 0u;
-#ifdef DAUC_CI_LINEAR
-            meta[kCiCells] = total_lin;
-            meta[kCiBlocks] = (total_lin + 1 + kCiBlock - 1) / kCiBlock;
-            meta[kCiLo] = __float_as_uint(lin_lo);
-            meta[kCiScale] = __float_as_uint(lin_scale);
-#else
             meta[kCiCells] = total;
             meta[kCiBlocks] = (total + 1 + kCiBlock - 1) / kCiBlock;
-#endif
             meta[kCiSkew] = 0u;
         }
     }
@@ -1515,9 +1266,6 @@ __global__ __launch_bounds__(kDirectThreads) void direct_count_kernel(const floa
         if (live) {
             const unsigned x = key_fast(pos[i]);
             c = ci_cell(x, l1[x >> kCiLowBits]);
-#ifdef DAUC_CI_LINEAR
-            c = lin_cell(x, lin_lo, lin_scale, lin_cm1);
-#endif
             cell[i] = c;  // the scatter's cell, so it does not walk pos -> key -> plan again
         }
         const unsigned long long act = __ballot(live);
@@ -1885,11 +1633,7 @@ int launch_ci(const float* s, const LT* lab, int64_t begin, int64_t end, const C
               int64_t M, unsigned long long* out, unsigned long long* nonfinite, hipStream_t st,
               unsigned* verdict = nullptr, const unsigned* grp = nullptr, const unsigned long long* Mp = nullptr) {
     const dim3 grid(query_grid(end - begin)), block(kQueryThreads);
-#ifdef DAUC_CI_UNAL
-    const size_t lds = (size_t(kCiTop) + kCiMaxBlocks) * 8 + size_t(kQueryThreads / kWave) * kListCap * 8;
-#else
     const size_t lds = (size_t(kCiTop) + kCiMaxBlocks) * 8 + (grp ? size_t(kDirectMaxGroups) * 4 : 0);
-#endif
     hipLaunchKernelGGL((query_ci_kernel<LT>), grid, block, lds, st, s, lab, begin, end, cw.meta, cw.l1, cw.blk, sorted,
                        M, out, nonfinite, verdict, grp, Mp);
     return launch_status();

@@ -33,11 +33,7 @@ constexpr int kCiTopBits = 11;
 constexpr int kCiTop = 1 << kCiTopBits;
 constexpr int kCiLowBits = 32 - kCiTopBits;
 constexpr int kCiBlock = 8;                               // cells per block word
-#ifdef DAUC_CI_UNAL  // TEMPORARY experiment: 8 KB of LDS for the query's long-cell lists
-constexpr int kCiMaxBlocks = 17296;
-#else
 constexpr int kCiMaxBlocks = 18320;                       // 16 KB + 8 B per block + 384 B < 160 KB of LDS
-#endif
 constexpr int kCiMaxCells = kCiMaxBlocks * kCiBlock - 1;  // + the virtual cell past the last
 // meta words: [8] usable, [9] cells, [10] blocks, [11] skewed (or inconsistent: never use)
 constexpr int kCiOk = 8, kCiCells = 9, kCiBlocks = 10, kCiSkew = 11;

@@ -36,6 +36,13 @@
 // Traffic per query: 5 B read + 4 B written (split) + 4 B read (count); the index (~2 cells x 16 B
 // per table key) and the run tables are a few % of that.
 
+// A MEASURED AND REJECTED alternative (round 4): compiled into the tuning build only
+// (tuning/libdauc_tuning.so, -DDAUC_TUNING; selected by dauc_set_query_path(2)). At configs[4]
+// (2^27 @ 0.1 %) the evaluation took 0.86 ms against 0.58 for the count index with gathers, at
+// configs[3] 0.47 vs 0.15 ms (profiles/r04/slots/): the split alone (276 us) moves 9 B per query and
+// the count pass waits on one dependent offset read per 200-250-query run. DESIGN §3.
+#ifdef DAUC_TUNING
+
 #include "count_index.h"
 
 namespace dauc {
@@ -786,12 +793,8 @@ int launch_sl_split(const float* s, const LT* lab, int64_t begin, int64_t end, c
 
 }  // namespace
 
-#ifdef DAUC_TUNING
 int g_query_path = 1;
 int eval_query_path() { return g_query_path; }
-#else
-int eval_query_path() { return 1; }
-#endif
 
 int64_t slot_index_capacity(int64_t n) {
     // 1.5 keys per cell at most, and the smaller class of n scores (a table of n / 2 + 1 keys)
@@ -856,10 +859,10 @@ int counts_slotted(const float* pos, const unsigned long long* Mp, int64_t mcap,
 
 }  // namespace dauc
 
-#ifdef DAUC_TUNING
 extern "C" int dauc_set_query_path(int path) {
     if (path < 1 || path > 2) return DAUC_EINVAL;
     dauc::g_query_path = path;
     return DAUC_OK;
 }
-#endif
+
+#endif  // DAUC_TUNING

@@ -72,8 +72,9 @@ int dauc_set_direct_fault(int mode);
 /*
  * The one-call evaluation's query path in THIS library (process-wide, default 1): 1 = the count
  * index held in LDS whole, each query gathering its cell's keys from the L2-resident table
- * (auc_sort.hip); 2 = the range-slot index (auc_slots.hip): the queries split by range of the
- * table, each range counted from its 16-byte cell slots in LDS with no gather. Same integers.
+ * (auc_sort.hip, the product's); 2 = the range-slot index (tuning_slots.hip, measured slower): the
+ * queries split by range of the table, each range counted from its 16-byte cell slots in LDS with
+ * no gather. Same integers.
  */
 int dauc_set_query_path(int path);
 

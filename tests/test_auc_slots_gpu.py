@@ -1,4 +1,4 @@
-"""The range-slot query path of the one-call evaluation (auc_slots.hip; dauc_set_query_path(2) of
+"""The range-slot query path of the one-call evaluation (tuning_slots.hip; dauc_set_query_path(2) of
 the tuning build, include/dauc_tuning.h) against the C oracle and the count-index path.
 
 The evaluation compacts the positives, builds the range-slot index straight from them (cells of
