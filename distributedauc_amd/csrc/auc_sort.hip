@@ -812,6 +812,19 @@ __global__ __launch_bounds__(256) void ci_blocks_kernel(const unsigned* __restri
 // a 16-byte window of the L2-resident table
 __device__ __forceinline__ uint4 win_load(const unsigned* p) { return *reinterpret_cast<const uint4*>(p); }
 
+// Counting in VGPRs only: gt01(a, b) = min(sat(a - b), 1) is 1 when a > b, else 0. A compare into
+// an SGPR read back by a v_cndmask / v_addc costs the VALU-writes-SGPR hazard's wait states on
+// every key (the round-3 loop issued 110 VALU per query, s_nop-padded, ~75 % of the SIMDs' issue
+// cycles: DESIGN §3).
+__device__ __forceinline__ unsigned gt01(unsigned a, unsigned b) {
+    return min(__builtin_elementwise_sub_sat(a, b), 1u);
+}
+// the window's keys <= x and < x
+__device__ __forceinline__ void win_le_lt(const uint4& k, unsigned x, unsigned& le, unsigned& lt) {
+    le = 4u - (gt01(k.x, x) + gt01(k.y, x) + gt01(k.z, x) + gt01(k.w, x));
+    lt = gt01(x, k.x) + gt01(x, k.y) + gt01(x, k.z) + gt01(x, k.w);
+}
+
 // Phase 1 of one query: cell, rank_lo, count and (lanes with cnt > 0) the window load
 __device__ __forceinline__ void ci_locate(unsigned x, const uint2* __restrict__ l1, const uint2* __restrict__ blk,
                                           const unsigned* __restrict__ sorted, unsigned& rl, unsigned& cnt,
@@ -1035,21 +1048,24 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
                 g.rc[q] = rl | (cnt << 28);
             }
         };
+        // an aligned window of +inf keys (the table is padded with at least 8 past M): the lanes with
+        // no window to gather read it, so their counts need no mask
+        const unsigned padoff = (M32 + 3u) & ~3u;
         auto locate_win = [&](Group& g) {
 #pragma unroll
             for (int q = 0; q < NQ; ++q) {
-                const unsigned rl = g.rc[q] & 0x0fffffffu;
-                g.k[q] = win_load(sorted + ((g.rc[q] >> 28) ? rl & ~3u : 0u));
+                const unsigned rl = g.rc[q] & 0x0fffffffu, cnt = g.rc[q] >> 28;
+                g.k[q] = win_load(sorted + (cnt && ((g.use >> q) & 1u) ? rl & ~3u : padoff));
             }
             // A cell that runs past its first window ((rank_lo & 3) + count > 4: ~7 % of the queries
             // at 1.1 cells per key) also loads the next one here, in the same straight-line issue: as
             // a branch after the count it was waited for with vmcnt(0) -- every load in flight,
             // the stream's included -- in nearly every iteration of every wave. Lanes that do not
-            // need it load the table's first window (one shared line).
+            // need it read the +inf window (one shared line).
 #pragma unroll
             for (int q = 0; q < NQ; ++q) {
                 const unsigned rl = g.rc[q] & 0x0fffffffu, cnt = g.rc[q] >> 28;
-                g.k2[q] = win_load(sorted + ((rl & 3u) + cnt > 4u ? (rl & ~3u) + 4u : 0u));
+                g.k2[q] = win_load(sorted + (((g.use >> q) & 1u) && (rl & 3u) + cnt > 4u ? (rl & ~3u) + 4u : padoff));
             }
         };
         auto locate = [&](Group& g) {
@@ -1058,27 +1074,22 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
         };
         auto count = [&](const Group& g) {
             unsigned wl = 0u, tl = 0u;
-            bool more = false;
-#pragma unroll
-            for (int q = 0; q < NQ; ++q) {
-                // an empty cell's lane loaded the table's first window: counted as +inf padding
-                const uint4 k = (g.rc[q] >> 28) ? g.k[q] : uint4{kPadKey, kPadKey, kPadKey, kPadKey};
-                more |= ci_count(g.x[q], (g.use >> q) & 1u, g.rc[q] & 0x0fffffffu, g.rc[q] >> 28, k, M32, wl, tl);
-            }
-            // the second window's keys (those of the cell and of later cells; past the cell they
-            // are > x): W -= #(<= x), T += #(<= x) - #(< x); a lane without one adds nothing
             bool more8 = false;
 #pragma unroll
             for (int q = 0; q < NQ; ++q) {
+                // lb = base + #(window keys < x), ub = base + #(<= x): the first window's keys before
+                // the cell are < x, after it > x (or the +inf window of a lane without keys); the
+                // second window (the cell's rest and later cells, or +inf) adds its own counts.
+                // W += M - ub, T += ub - lb, for the queries only (um)
                 const unsigned x = g.x[q], rl = g.rc[q] & 0x0fffffffu, cnt = g.rc[q] >> 28;
-                const unsigned span = (rl & 3u) + cnt;
-                const unsigned m = 0u - (((g.use >> q) & 1u) & unsigned(span > 4u));
-                const uint4 k2 = g.k2[q];
-                const unsigned lt = (k2.x < x) + (k2.y < x) + (k2.z < x) + (k2.w < x);
-                const unsigned le = (k2.x <= x) + (k2.y <= x) + (k2.z <= x) + (k2.w <= x);
-                wl -= le & m;
-                tl += (le - lt) & m;
-                more8 |= ((g.use >> q) & 1u) && span > 8u;
+                const unsigned um = 0u - ((g.use >> q) & 1u);
+                const unsigned base = rl & ~(min(cnt, 1u) * 3u);  // rl & ~3 when the cell has keys
+                unsigned le, lt, le2, lt2;
+                win_le_lt(g.k[q], x, le, lt);
+                win_le_lt(g.k2[q], x, le2, lt2);
+                wl += (M32 - (base + le + le2)) & um;
+                tl += ((le - lt) + (le2 - lt2)) & um;
+                more8 |= um && (rl & 3u) + cnt > 8u;
             }
             w += wl;
             t += tl;
@@ -1097,7 +1108,6 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
                     }
                 }
             }
-            (void)more;
         };
         // per group g: keys(g) [its stream loads were issued D groups earlier], stream loads of
         // g + D into the buffer just read, LDS lookups + window loads of g, count of g - 1 [its
