@@ -371,9 +371,10 @@ def _eval_args(scores: torch.Tensor, labels: torch.Tensor):
     if n == 0:
         raise ValueError("empty score vector")
     L = _lib.load()
-    nbytes = _eval_ws_bytes.get(n)
+    # keyed by library too: the tuning build's evaluation workspace also holds its range-slot path
+    nbytes = _eval_ws_bytes.get((id(L), n))
     if nbytes is None:
-        nbytes = _eval_ws_bytes[n] = L.dauc_auc_eval_workspace_size(n)
+        nbytes = _eval_ws_bytes[(id(L), n)] = L.dauc_auc_eval_workspace_size(n)
     st = torch.cuda.current_stream(dev).cuda_stream
     return L, dev, lc, n, st, workspaces.get(dev, "auc_eval", nbytes, st)
 
@@ -464,7 +465,7 @@ def auc_eval_counts_part(scores: torch.Tensor, labels: torch.Tensor, part: int, 
     return tuple(out)
 
 
-_eval_ws_bytes: dict = {}  # dauc_auc_eval_workspace_size per length (a pure function of n)
+_eval_ws_bytes: dict = {}  # dauc_auc_eval_workspace_size per (library, length) (a pure function of n)
 
 
 def compact_positives(scores: torch.Tensor, labels: torch.Tensor):
