@@ -233,8 +233,12 @@ __global__ __launch_bounds__(256) void gather_slots_kernel(const unsigned char* 
                                                            int parts, int64_t cap, int64_t mcap,
                                                            float* __restrict__ table,
                                                            unsigned long long* __restrict__ stats,
-                                                           unsigned long long* __restrict__ m_eff) {
+                                                           unsigned long long* __restrict__ m_eff,
+                                                           unsigned* __restrict__ hist, int nhist) {
     __shared__ unsigned long long off_s;
+    // the direct build's histogram, zeroed here for the build that follows (no memset launch)
+    if (blockIdx.x == 0)
+        for (int i = threadIdx.x; i < nhist; i += 256) hist[i] = 0u;
     auto hdr = [&](int r) { return reinterpret_cast<const unsigned long long*>(slots + size_t(r) * sbytes); };
     if (threadIdx.x < kWave) {
         // wave 0: the prefix of the slots' P before this one, and (workgroup 0) the totals
@@ -324,10 +328,9 @@ int dauc_auc_eval_query_part(const float* scores, const void* labels, int label_
     if ((e = hipMemsetAsync(w.wt, 0, kZeroed, st)) != hipSuccess) return -static_cast<int>(e);
     const int64_t mcap = direct_capacity(n);
     unsigned* hist = reinterpret_cast<unsigned*>(static_cast<char*>(w.tws) + direct_hist_offset(mcap));
-    if ((e = hipMemsetAsync(hist, 0, size_t(direct_hist_words()) * 4, st)) != hipSuccess) return -static_cast<int>(e);
     hipLaunchKernelGGL(gather_slots_kernel, dim3(static_cast<unsigned>(parts)), dim3(256), 0, st,
                        static_cast<const unsigned char*>(slots), slot_bytes(n, parts), parts, slot_cap(n, parts), mcap,
-                       w.pos, w.slot, w.spare);
+                       w.pos, w.slot, w.spare, hist, direct_hist_words());
     int rc = launch_status();
     if (rc) return rc;
     const int64_t qlo = n * part / parts, qhi = n * (part + 1) / parts;

@@ -1742,6 +1742,13 @@ __global__ void direct_fault_kernel(int mode, const unsigned long long* __restri
 }
 #endif
 
+// The count and scatter passes loop over the keys: every workgroup first recomputes the plan (a
+// 2048-bucket scan) or the group prefixes, so fewer, longer workgroups pay that once per CU
+#ifndef DAUC_DIRECT_GRID  // TEMPORARY A/B switch
+#define DAUC_DIRECT_GRID 256
+#endif
+constexpr int64_t kDirectGrid = DAUC_DIRECT_GRID;
+
 int build_direct_index(const float* pos, const unsigned long long* Mp, int64_t Mcap, void* workspace,
                        size_t workspace_bytes, hipStream_t st, DirectIndex* ix) {
     if (pos == nullptr || Mp == nullptr || Mcap < 1 || workspace == nullptr || ix == nullptr ||
@@ -1759,7 +1766,7 @@ int build_direct_index(const float* pos, const unsigned long long* Mp, int64_t M
     };
     hipLaunchKernelGGL(direct_hist_kernel, blocks(Mcap, 256 * kDirectPerThread, 256), dim3(256), 0, st, pos, Mp,
                        nw.first, nw.cstart, kCiCntWords);
-    hipLaunchKernelGGL(direct_count_kernel, blocks(Mcap, kDirectThreads, 1024), dim3(kDirectThreads), 0, st, pos,
+    hipLaunchKernelGGL(direct_count_kernel, blocks(Mcap, kDirectThreads, kDirectGrid), dim3(kDirectThreads), 0, st, pos,
                        Mcap, nw.first, nw.l1, nw.meta, nw.cstart, w.keys_b);
     hipLaunchKernelGGL(direct_blocks_kernel, dim3(kDirectMaxGroups), dim3(kDirectGroup), 0, st, nw.cstart, nw.meta,
                        nw.blk, grp);
@@ -1768,7 +1775,7 @@ int build_direct_index(const float* pos, const unsigned long long* Mp, int64_t M
         hipLaunchKernelGGL(direct_fault_kernel, dim3(1), dim3(64), 0, st, g_direct_fault, Mp, nw.meta, nw.cstart,
                            w.keys_b);
 #endif
-    hipLaunchKernelGGL(direct_scatter_kernel, blocks(Mcap, kDirectThreads, 1024), dim3(kDirectThreads), 0, st, pos,
+    hipLaunchKernelGGL(direct_scatter_kernel, blocks(Mcap, kDirectThreads, kDirectGrid), dim3(kDirectThreads), 0, st, pos,
                        Mp, nw.blk, grp, nw.meta, nw.cstart, w.keys_b, table);
     *ix = DirectIndex{table, nw.l1, nw.blk, grp, nw.meta};
     return launch_status();
