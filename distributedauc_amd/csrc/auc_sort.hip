@@ -1742,12 +1742,9 @@ __global__ void direct_fault_kernel(int mode, const unsigned long long* __restri
 }
 #endif
 
-// The count and scatter passes loop over the keys: every workgroup first recomputes the plan (a
-// 2048-bucket scan) or the group prefixes, so fewer, longer workgroups pay that once per CU
-#ifndef DAUC_DIRECT_GRID  // TEMPORARY A/B switch
-#define DAUC_DIRECT_GRID 256
-#endif
-constexpr int64_t kDirectGrid = DAUC_DIRECT_GRID;
+// The count and scatter passes loop over the keys (up to 1024 workgroups; 256 measured the same:
+// profiles/r04/query_ablations/r04q_*)
+constexpr int64_t kDirectGrid = 1024;
 
 int build_direct_index(const float* pos, const unsigned long long* Mp, int64_t Mcap, void* workspace,
                        size_t workspace_bytes, hipStream_t st, DirectIndex* ix) {
