@@ -226,19 +226,28 @@ int64_t slice_lo(int64_t n, int part, int parts) {
     return part == 0 ? 0 : part >= parts ? n : ((n * part / parts) & ~int64_t(255));
 }
 
-// One workgroup per slot: the slot's keys to table[sum of the earlier slots' P, ...); workgroup 0
-// sums the headers into the evaluation's counters. m_eff = P, or (any slot overflowed) a size the
-// index refuses, so the build reports verdict 2.
+// kGatherBlocks workgroups per slot (blockIdx.y = the slot): the slot's scores to table[sum of the
+// earlier slots' P, ...) (one workgroup per slot copied a 2-rank slot of 67 k scores in ~60 us);
+// workgroup (0, 0) sums the headers into the evaluation's counters and zeroes the query's counts,
+// the verdict and the direct build's histogram (no memset launch). m_eff = P, or (any slot
+// overflowed) a size the index refuses, so the build reports verdict 2.
+constexpr int kGatherBlocks = 32;
 __global__ __launch_bounds__(256) void gather_slots_kernel(const unsigned char* __restrict__ slots, size_t sbytes,
                                                            int parts, int64_t cap, int64_t mcap,
                                                            float* __restrict__ table,
                                                            unsigned long long* __restrict__ stats,
                                                            unsigned long long* __restrict__ m_eff,
-                                                           unsigned* __restrict__ hist, int nhist) {
+                                                           unsigned* __restrict__ hist, int nhist,
+                                                           unsigned long long* __restrict__ wt,
+                                                           unsigned* __restrict__ verdict) {
     __shared__ unsigned long long off_s;
-    // the direct build's histogram, zeroed here for the build that follows (no memset launch)
-    if (blockIdx.x == 0)
+    const int slot = blockIdx.y;
+    const bool first = blockIdx.x == 0 && slot == 0;
+    if (first) {
         for (int i = threadIdx.x; i < nhist; i += 256) hist[i] = 0u;
+        if (threadIdx.x < 3) wt[threadIdx.x] = 0ull;
+        if (threadIdx.x == 0) *reinterpret_cast<unsigned long long*>(verdict) = 0ull;  // record word 7
+    }
     auto hdr = [&](int r) { return reinterpret_cast<const unsigned long long*>(slots + size_t(r) * sbytes); };
     if (threadIdx.x < kWave) {
         // wave 0: the prefix of the slots' P before this one, and (workgroup 0) the totals
@@ -246,7 +255,7 @@ __global__ __launch_bounds__(256) void gather_slots_kernel(const unsigned char* 
         bool over = false;
         for (int r = threadIdx.x; r < parts; r += kWave) {
             const unsigned long long* h = hdr(r);
-            before += r < static_cast<int>(blockIdx.x) ? h[0] : 0ull;
+            before += r < slot ? h[0] : 0ull;
             P += h[0];
             nf += h[2];
             other += h[3];
@@ -259,7 +268,7 @@ __global__ __launch_bounds__(256) void gather_slots_kernel(const unsigned char* 
         over = __ballot(over) != 0ull;
         if (threadIdx.x == 0) {
             off_s = before;
-            if (blockIdx.x == 0) {
+            if (first) {
                 stats[0] = P;
                 stats[1] = 0ull;
                 stats[2] = nf;
@@ -269,11 +278,12 @@ __global__ __launch_bounds__(256) void gather_slots_kernel(const unsigned char* 
         }
     }
     __syncthreads();
-    const unsigned long long Pr = hdr(blockIdx.x)[0];
+    const unsigned long long Pr = hdr(slot)[0];
     const unsigned long long off = off_s;
     if (Pr > static_cast<unsigned long long>(cap) || off + Pr > static_cast<unsigned long long>(mcap)) return;
-    const float* src = reinterpret_cast<const float*>(slots + size_t(blockIdx.x) * sbytes + kSlotHdr);
-    for (unsigned long long i = threadIdx.x; i < Pr; i += 256) table[off + i] = src[i];
+    const float* src = reinterpret_cast<const float*>(slots + size_t(slot) * sbytes + kSlotHdr);
+    for (unsigned long long i = blockIdx.x * 256ull + threadIdx.x; i < Pr; i += 256ull * kGatherBlocks)
+        table[off + i] = src[i];
 }
 
 }  // namespace
@@ -324,13 +334,12 @@ int dauc_auc_eval_query_part(const float* scores, const void* labels, int label_
         return DAUC_EINVAL;
     hipStream_t st = as_hip(stream);
     const EvalWs w = eval_ws(workspace, n);
-    hipError_t e;
-    if ((e = hipMemsetAsync(w.wt, 0, kZeroed, st)) != hipSuccess) return -static_cast<int>(e);
     const int64_t mcap = direct_capacity(n);
     unsigned* hist = reinterpret_cast<unsigned*>(static_cast<char*>(w.tws) + direct_hist_offset(mcap));
-    hipLaunchKernelGGL(gather_slots_kernel, dim3(static_cast<unsigned>(parts)), dim3(256), 0, st,
+    // zeroes the counts, the verdict and the histogram itself (the record's other words are written)
+    hipLaunchKernelGGL(gather_slots_kernel, dim3(kGatherBlocks, static_cast<unsigned>(parts)), dim3(256), 0, st,
                        static_cast<const unsigned char*>(slots), slot_bytes(n, parts), parts, slot_cap(n, parts), mcap,
-                       w.pos, w.slot, w.spare, hist, direct_hist_words());
+                       w.pos, w.slot, w.spare, hist, direct_hist_words(), w.wt, w.verdict);
     int rc = launch_status();
     if (rc) return rc;
     const int64_t qlo = n * part / parts, qhi = n * (part + 1) / parts;
