@@ -20,7 +20,7 @@
 
 #include <type_traits>
 
-#include "dauc_internal.h"
+#include "count_index.h"
 
 namespace dauc {
 namespace {
@@ -537,17 +537,21 @@ __global__ __launch_bounds__(kCmpThreads) void compact_write_kernel(
 // next call's stats) and the first `nzero_w` words of `zero_w`, and zero3[0..3).
 // SLOTS groups of 16 labels per thread: 8 (a 32768-label tile) for small inputs; 32 (131072) for
 // large ones, where the reservation atomics of 4096 tiles on one address serialise (2^27 labels:
-// 65 us at 8 slots).
-template <typename LT, int SLOTS, int THREADS = kCmpThreads>
+// 65 us at 8 slots). HIST: hist_out += the top-bucket histogram of the positives' keys (an LDS
+// histogram per tile, its used buckets added once).
+template <typename LT, int SLOTS, int THREADS = kCmpThreads, bool HIST = false>
 __global__ __launch_bounds__(THREADS) void compact_unordered_kernel(
     const float* __restrict__ s, const LT* __restrict__ lab, int64_t n, int vec, float* __restrict__ pos_out,
     unsigned long long* __restrict__ stats, unsigned long long tag, unsigned long long* __restrict__ zero_next,
     unsigned long long next_tag, unsigned long long* __restrict__ zero3, unsigned* __restrict__ zero_w,
-    int nzero_w, int64_t cap) {
+    int nzero_w, int64_t cap, unsigned* __restrict__ hist_out) {
     constexpr int kW = THREADS / kWave;
     constexpr int64_t kTileU = int64_t(THREADS) * 16 * SLOTS;
     __shared__ int wtot[2][kW];
     __shared__ unsigned long long base_s;
+    __shared__ unsigned hs[HIST ? kCiTop : 1];
+    if constexpr (HIST)
+        for (int i = threadIdx.x; i < kCiTop; i += THREADS) hs[i] = 0u;
     if (blockIdx.x == 0) {
         if (threadIdx.x < 4) zero_next[threadIdx.x] = threadIdx.x == 1 ? next_tag : 0ull;
         else if (threadIdx.x < 7 && zero3 != nullptr) zero3[threadIdx.x - 4] = 0ull;
@@ -636,9 +640,15 @@ __global__ __launch_bounds__(THREADS) void compact_unordered_kernel(
             nf += !isfinite(v);
             if (r < cap) pos_out[r] = v;  // past `cap`: counted in stats[0], not stored (the caller's overflow)
             ++r;
+            if constexpr (HIST) atomicAdd(&hs[key_fast(v) >> kCiLowBits], 1u);
         }
     }
     if (nf) atomicAdd(stats + 2, static_cast<unsigned long long>(nf));
+    if constexpr (HIST) {
+        __syncthreads();
+        for (int i = threadIdx.x; i < kCiTop; i += THREADS)
+            if (hs[i]) atomicAdd(hist_out + i, hs[i]);
+    }
 }
 
 template <typename LT>
@@ -908,7 +918,7 @@ int compact_positives_zeroing(const float* scores, const void* labels, int label
 int compact_unordered(const float* scores, const void* labels, int label_dtype, int64_t n, float* pos_out,
                       unsigned long long* stats, unsigned long long tag, unsigned long long* zero_next,
                       unsigned long long next_tag, unsigned long long* zero3, unsigned* zero_w, int nzero_w,
-                      hipStream_t st, int64_t cap) {
+                      hipStream_t st, int64_t cap, unsigned* hist_out) {
     if (n <= 0 || scores == nullptr || labels == nullptr || pos_out == nullptr || stats == nullptr ||
         zero_next == nullptr)
         return DAUC_EINVAL;
@@ -924,12 +934,19 @@ int compact_unordered(const float* scores, const void* labels, int label_dtype, 
     const dim3 grid(static_cast<unsigned>(nblk)), block(threads);
     auto go = [&](auto* lab) {
         using LT = std::remove_const_t<std::remove_pointer_t<decltype(lab)>>;
-        if (wide)
+        if (wide && hist_out != nullptr)
+            hipLaunchKernelGGL((compact_unordered_kernel<LT, 32, kWideThreads, true>), grid, block, 0, st, scores, lab,
+                               n, vec, pos_out, stats, tag, zero_next, next_tag, zero3, zero_w, nzero_w, cap, hist_out);
+        else if (wide)
             hipLaunchKernelGGL((compact_unordered_kernel<LT, 32, kWideThreads>), grid, block, 0, st, scores, lab, n, vec,
-                               pos_out, stats, tag, zero_next, next_tag, zero3, zero_w, nzero_w, cap);
+                               pos_out, stats, tag, zero_next, next_tag, zero3, zero_w, nzero_w, cap, hist_out);
+        else if (hist_out != nullptr)
+            hipLaunchKernelGGL((compact_unordered_kernel<LT, kCmpSlots, kCmpThreads, true>), grid, block, 0, st, scores,
+                               lab, n, vec, pos_out, stats, tag, zero_next, next_tag, zero3, zero_w, nzero_w, cap,
+                               hist_out);
         else
             hipLaunchKernelGGL((compact_unordered_kernel<LT, kCmpSlots>), grid, block, 0, st, scores, lab, n, vec,
-                               pos_out, stats, tag, zero_next, next_tag, zero3, zero_w, nzero_w, cap);
+                               pos_out, stats, tag, zero_next, next_tag, zero3, zero_w, nzero_w, cap, hist_out);
         return launch_status();
     };
     switch (label_dtype) {

@@ -2,8 +2,8 @@
 //
 // Reference: imagenet/main.py:79-81, AUC(label, scores) = sklearn roc_curve(pos_label=1) + auc,
 // evaluated by rank 0 over the test set (main.py:237-250). The evaluation is:
-//   1. one memset of the 96-byte workspace header (the compaction's counters, the query counts,
-//      the verdict word);
+//   1. one memset of the 64-byte record (the compaction's counters, the query counts, the
+//      verdict word);
 //   2. the one-pass positive compaction: labels read once, the positives' scores gathered (in no
 //      particular order), P counted on the device;
 //   3. the count index built straight from the unsorted positives, sized by the device's P
@@ -12,8 +12,9 @@
 //      counts the non-finite queried scores (sklearn rejects them, _ranking.py:868-869) and writes
 //      the verdict: 1 = counted, 2 = the index cannot hold this table (more than 219,838
 //      positives, or clustered / tie-heavy ones);
-//   4. one 64-byte copy of the header: W, T, #non-finite queried scores, P, #non-finite positives,
-//      #labels outside {-1, 1}, the verdict.
+//   4. the 64-byte record: W, T, #non-finite queried scores, P, #non-finite positives, #labels
+//      outside {-1, 1}, the verdict -- counted straight into the caller's part_out by the enqueued
+//      forms (no copy), into the workspace header by the blocking ones.
 // Nothing in 1-4 waits for the host or allocates: dauc_auc_eval_enqueue is exactly that, and the
 // sharded evaluation all-reduces its counts without a host synchronisation in between. The
 // blocking forms add ONE readback into the caller's page-locked words and, only for verdict 2, the
@@ -35,8 +36,9 @@ inline size_t align256(size_t b) { return (b + 255) / 256 * 256; }
 // workspace header (bytes): [0, 24) W, T, #non-finite queried scores (u64, the query's atomics);
 // [24, 56) the compaction's counters: P, tag (0), #non-finite positives, #labels outside {-1, 1};
 // [56, 60) the verdict; [64, 96) a second counter slot the compaction's block 0 writes (unused).
-// [0, 64) is the result record copied out; [0, 96) is zeroed by the call's one memset.
-constexpr size_t kHdr = 256, kRecord = 64, kZeroed = 96;
+// [0, 64) is the result record (the blocking forms'; the enqueued forms count into the caller's
+// part_out instead), zeroed by the call's one memset.
+constexpr size_t kHdr = 256, kRecord = 64;
 
 struct EvalWs {
     unsigned long long* wt;       // [3]
@@ -99,11 +101,21 @@ bool valid_args(const float* scores, const void* labels, int label_dtype, int64_
            (label_dtype == DAUC_LABEL_I8 || label_dtype == DAUC_LABEL_I32 || label_dtype == DAUC_LABEL_I64);
 }
 
-// Steps 1-3 (no host synchronisation, no allocation).
+// The record words of `w` moved to the caller's part_out (int64[8], 8-byte aligned): the
+// kernels count straight into it, so the enqueued forms end without a record copy.
+EvalWs with_record(EvalWs w, int64_t* rec) {
+    w.wt = reinterpret_cast<unsigned long long*>(rec);
+    w.slot = reinterpret_cast<unsigned long long*>(rec + 3);
+    w.verdict = reinterpret_cast<unsigned*>(rec + 7);
+    return w;
+}
+
+// Steps 1-3 (no host synchronisation, no allocation): the record at w.wt .. w.verdict (the
+// workspace header, or the caller's part_out through with_record).
 int enqueue(const float* scores, const void* labels, int label_dtype, int64_t n, int part, int parts,
             const EvalWs& w, hipStream_t st) {
     hipError_t e;
-    if ((e = hipMemsetAsync(w.wt, 0, kZeroed, st)) != hipSuccess) return -static_cast<int>(e);
+    if ((e = hipMemsetAsync(w.wt, 0, kRecord, st)) != hipSuccess) return -static_cast<int>(e);
     const int64_t mcap = direct_capacity(n);
     unsigned* hist = reinterpret_cast<unsigned*>(static_cast<char*>(w.tws) + direct_hist_offset(mcap));
     // the compaction also zeroes the direct build's histogram (its block 0, ahead of every use)
@@ -201,15 +213,16 @@ int counts_part_blocking(const float* scores, const void* labels, int label_dtyp
 // ---- the sharded evaluation in two steps: each rank compacts only its slice -----------------
 //
 // Step 1 (dauc_auc_eval_compact_part): rank r compacts the positives of ITS slice of the labels
-// into a slot: a 256-byte header {P_r, #non-finite positives, #labels outside {-1, 1}} (u64) and
-// room for `cap` scores. The caller all-gathers the slots (one collective). Step 2
-// (dauc_auc_eval_query_part): the gathered slots are concatenated into the evaluation's positive
-// table on the device (their headers summed), the count index is built from it and the rank's
-// query range is counted; the record is dauc_auc_eval_enqueue's. A slot holds an even share of
+// into a slot: a 256-byte header {P_r, #non-finite positives, #labels outside {-1, 1}} (u64), the
+// top-bucket histogram of its positives' keys (count_index.h, 2048 u32) and room for `cap` scores.
+// The caller all-gathers the slots (one collective). Step 2 (dauc_auc_eval_query_part): the
+// gathered slots are concatenated into the evaluation's positive table on the device (their
+// headers and histograms summed), the count index is built from it -- without its histogram pass
+// -- and the rank's query range is counted; the record is dauc_auc_eval_enqueue's. A slot holds an even share of
 // the index's capacity plus 25 %: a rank whose slice holds more positives (unshuffled test sets)
 // overflows, and the evaluation reports verdict 2 (the caller's blocking sorted path), as it does
 // for tables the index cannot hold.
-constexpr size_t kSlotHdr = 256;
+constexpr size_t kSlotHist = 256, kSlotHdr = kSlotHist + size_t(kCiTop) * 4;
 
 int64_t slot_cap(int64_t n, int parts) {
     const int64_t share = (n + parts - 1) / parts;
@@ -228,26 +241,31 @@ int64_t slice_lo(int64_t n, int part, int parts) {
 
 // kGatherBlocks workgroups per slot (blockIdx.y = the slot): the slot's scores to table[sum of the
 // earlier slots' P, ...) (one workgroup per slot copied a 2-rank slot of 67 k scores in ~60 us);
-// workgroup (0, 0) sums the headers into the evaluation's counters and zeroes the query's counts,
-// the verdict and the direct build's histogram (no memset launch). m_eff = P, or (any slot
-// overflowed) a size the index refuses, so the build reports verdict 2.
+// workgroup (0, 0) sums the headers into the evaluation's counters and zeroes the query's counts
+// and the verdict (no memset launch); the first workgroups sum the slots' histograms into the
+// build's `hist`, and all of them zero its per-cell counters (the histogram pass's other job).
+// m_eff = P, or (any slot overflowed) a size the index refuses, so the build reports verdict 2 (the
+// histogram's bucket 0 gets that size added: its total is the build's M).
 constexpr int kGatherBlocks = 32;
 __global__ __launch_bounds__(256) void gather_slots_kernel(const unsigned char* __restrict__ slots, size_t sbytes,
                                                            int parts, int64_t cap, int64_t mcap,
                                                            float* __restrict__ table,
                                                            unsigned long long* __restrict__ stats,
                                                            unsigned long long* __restrict__ m_eff,
-                                                           unsigned* __restrict__ hist, int nhist,
+                                                           unsigned* __restrict__ hist,
+                                                           unsigned* __restrict__ cnt, int64_t ncnt,
                                                            unsigned long long* __restrict__ wt,
                                                            unsigned* __restrict__ verdict) {
     __shared__ unsigned long long off_s;
+    __shared__ bool over_s;
     const int slot = blockIdx.y;
     const bool first = blockIdx.x == 0 && slot == 0;
     if (first) {
-        for (int i = threadIdx.x; i < nhist; i += 256) hist[i] = 0u;
         if (threadIdx.x < 3) wt[threadIdx.x] = 0ull;
         if (threadIdx.x == 0) *reinterpret_cast<unsigned long long*>(verdict) = 0ull;  // record word 7
     }
+    const int64_t lb = int64_t(slot) * kGatherBlocks + blockIdx.x;
+    for (int64_t i = lb * 256 + threadIdx.x; i < ncnt; i += int64_t(256) * kGatherBlocks * gridDim.y) cnt[i] = 0u;
     auto hdr = [&](int r) { return reinterpret_cast<const unsigned long long*>(slots + size_t(r) * sbytes); };
     if (threadIdx.x < kWave) {
         // wave 0: the prefix of the slots' P before this one, and (workgroup 0) the totals
@@ -268,6 +286,7 @@ __global__ __launch_bounds__(256) void gather_slots_kernel(const unsigned char* 
         over = __ballot(over) != 0ull;
         if (threadIdx.x == 0) {
             off_s = before;
+            over_s = over;
             if (first) {
                 stats[0] = P;
                 stats[1] = 0ull;
@@ -278,6 +297,13 @@ __global__ __launch_bounds__(256) void gather_slots_kernel(const unsigned char* 
         }
     }
     __syncthreads();
+    if (lb * 256 + threadIdx.x < kCiTop) {
+        const int i = static_cast<int>(lb * 256 + threadIdx.x);
+        unsigned h = i == 0 && over_s ? static_cast<unsigned>(mcap) + 1u : 0u;
+        for (int r = 0; r < parts; ++r)
+            h += reinterpret_cast<const unsigned*>(slots + size_t(r) * sbytes + kSlotHist)[i];
+        hist[i] = h;
+    }
     const unsigned long long Pr = hdr(slot)[0];
     const unsigned long long off = off_s;
     if (Pr > static_cast<unsigned long long>(cap) || off + Pr > static_cast<unsigned long long>(mcap)) return;
@@ -299,11 +325,9 @@ int dauc_auc_eval_enqueue(const float* scores, const void* labels, int label_dty
                           int64_t* part_out, void* workspace, size_t workspace_bytes, dauc_stream_t stream) {
     if (part_out == nullptr || !valid_args(scores, labels, label_dtype, n, part, parts, workspace, workspace_bytes))
         return DAUC_EINVAL;
-    hipStream_t st = as_hip(stream);
-    const EvalWs w = eval_ws(workspace, n);
-    const int rc = enqueue(scores, labels, label_dtype, n, part, parts, w, st);
-    if (rc) return rc;
-    return -static_cast<int>(hipMemcpyAsync(part_out, w.wt, kRecord, hipMemcpyDeviceToDevice, st));
+    if ((reinterpret_cast<uintptr_t>(part_out) & 7u) != 0) return DAUC_EINVAL;
+    return enqueue(scores, labels, label_dtype, n, part, parts, with_record(eval_ws(workspace, n), part_out),
+                   as_hip(stream));
 }
 
 size_t dauc_auc_slot_bytes(int64_t n, int parts) { return n < 1 || parts < 1 ? 0 : slot_bytes(n, parts); }
@@ -317,29 +341,33 @@ int dauc_auc_eval_compact_part(const float* scores, const void* labels, int labe
     const EvalWs w = eval_ws(workspace, n);
     auto* hdr = static_cast<unsigned long long*>(slot);
     hipError_t e;
-    if ((e = hipMemsetAsync(hdr, 0, 32, st)) != hipSuccess) return -static_cast<int>(e);
+    if ((e = hipMemsetAsync(hdr, 0, kSlotHdr, st)) != hipSuccess) return -static_cast<int>(e);  // + histogram
     const int64_t lo = slice_lo(n, part, parts), hi = slice_lo(n, part + 1, parts);
     if (hi <= lo) return DAUC_OK;  // an empty slice: P_r = 0
     const size_t lsz = label_dtype == DAUC_LABEL_I8 ? 1 : label_dtype == DAUC_LABEL_I32 ? 4 : 8;
     return compact_unordered(scores + lo, static_cast<const char*>(labels) + size_t(lo) * lsz, label_dtype, hi - lo,
                              reinterpret_cast<float*>(static_cast<char*>(slot) + kSlotHdr), hdr, 0ull, w.spare, 0ull,
-                             nullptr, nullptr, 0, st, slot_cap(n, parts));
+                             nullptr, nullptr, 0, st, slot_cap(n, parts),
+                             reinterpret_cast<unsigned*>(static_cast<char*>(slot) + kSlotHist));
 }
 
 int dauc_auc_eval_query_part(const float* scores, const void* labels, int label_dtype, int64_t n, int part, int parts,
                              const void* slots, int64_t* part_out, void* workspace, size_t workspace_bytes,
                              dauc_stream_t stream) {
     if (slots == nullptr || part_out == nullptr || (reinterpret_cast<uintptr_t>(slots) & 255u) != 0 ||
+        (reinterpret_cast<uintptr_t>(part_out) & 7u) != 0 ||
         !valid_args(scores, labels, label_dtype, n, part, parts, workspace, workspace_bytes))
         return DAUC_EINVAL;
     hipStream_t st = as_hip(stream);
-    const EvalWs w = eval_ws(workspace, n);
+    const EvalWs w = with_record(eval_ws(workspace, n), part_out);
     const int64_t mcap = direct_capacity(n);
     unsigned* hist = reinterpret_cast<unsigned*>(static_cast<char*>(w.tws) + direct_hist_offset(mcap));
-    // zeroes the counts, the verdict and the histogram itself (the record's other words are written)
+    // zeroes the counts and the verdict (the record's other words are written), and hands the
+    // build its histogram and zeroed per-cell counters
+    static_assert(int64_t(kGatherBlocks) * 256 >= kCiTop, "one slot's workgroups cover the histogram");
     hipLaunchKernelGGL(gather_slots_kernel, dim3(kGatherBlocks, static_cast<unsigned>(parts)), dim3(256), 0, st,
                        static_cast<const unsigned char*>(slots), slot_bytes(n, parts), parts, slot_cap(n, parts), mcap,
-                       w.pos, w.slot, w.spare, hist, direct_hist_words(), w.wt, w.verdict);
+                       w.pos, w.slot, w.spare, hist, direct_cnt_ptr(w.tws, mcap), direct_cnt_words(), w.wt, w.verdict);
     int rc = launch_status();
     if (rc) return rc;
     const int64_t qlo = n * part / parts, qhi = n * (part + 1) / parts;
@@ -352,10 +380,10 @@ int dauc_auc_eval_query_part(const float* scores, const void* labels, int label_
         else
 #endif
             rc = counts_labeled_direct(w.pos, w.spare, mcap, scores, labels, label_dtype, qlo, qhi, w.wt, w.wt + 2,
-                                       w.verdict, w.tws, w.tws_bytes, st);
+                                       w.verdict, w.tws, w.tws_bytes, st, true);
         if (rc) return rc;
     }
-    return -static_cast<int>(hipMemcpyAsync(part_out, w.wt, kRecord, hipMemcpyDeviceToDevice, st));
+    return DAUC_OK;
 }
 
 int dauc_auc_eval_counts(const float* scores, const void* labels, int label_dtype, int64_t n, int64_t* out,

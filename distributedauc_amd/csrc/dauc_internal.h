@@ -108,10 +108,12 @@ int compact_positives_zeroing(const float* scores, const void* labels, int label
 // and stats[1] must hold `tag` (else no tile reserves or writes anything); block 0 zeroes
 // zero_next[0, 2, 3], sets zero_next[1] = next_tag, and zeroes zero3[0..3) (nullable) and
 // zero_w[0..nzero_w). At most `cap` positives are stored (stats[0] still counts them all).
+// hist_out (nullable; kCiTop words, zero on entry) += the top-bucket histogram of the positives'
+// keys (count_index.h), so a build from them can skip its histogram pass.
 int compact_unordered(const float* scores, const void* labels, int label_dtype, int64_t n, float* pos_out,
                       unsigned long long* stats, unsigned long long tag, unsigned long long* zero_next,
                       unsigned long long next_tag, unsigned long long* zero3, unsigned* zero_w, int nzero_w,
-                      hipStream_t st, int64_t cap = INT64_MAX);
+                      hipStream_t st, int64_t cap = INT64_MAX, unsigned* hist_out = nullptr);
 
 // auc_sort.hip: the count index built straight from the unsorted positives (no radix sort, no
 // tree) and the labeled query pass over scores [begin, end); the table is ordered by cell only.
@@ -123,10 +125,15 @@ bool direct_enabled();  // the search mode is automatic (always, except in a tun
 int64_t direct_capacity(int64_t n);
 int64_t direct_hist_offset(int64_t Mcap);  // byte offset of `hist` in the sort workspace
 int direct_hist_words();
+// the per-cell counters the count pass adds into (zeroed by the histogram pass, or by the caller
+// when it hands over a ready histogram)
+unsigned* direct_cnt_ptr(void* workspace, int64_t Mcap);
+int64_t direct_cnt_words();
 struct DirectIndex;  // count_index.h
-// the direct build alone (4 launches): fills *ix with the index's device pointers
+// the direct build alone (4 launches; 3 with hist_ready: `hist` already holds the table's top-
+// bucket histogram and the per-cell counters are zero): fills *ix with the index's device pointers
 int build_direct_index(const float* pos, const unsigned long long* Mp, int64_t Mcap, void* workspace,
-                       size_t workspace_bytes, hipStream_t st, DirectIndex* ix);
+                       size_t workspace_bytes, hipStream_t st, DirectIndex* ix, bool hist_ready = false);
 #ifdef DAUC_TUNING
 // tuning_slots.hip (tuning builds only): the labeled queries [begin, end) counted through the range-slot index built
 // straight from the unsorted positives pos[0 .. *Mp) (split + count passes); workspace of
@@ -146,6 +153,6 @@ int eval_query_path();
 int counts_labeled_direct(const float* pos, const unsigned long long* Mp, int64_t Mcap, const float* scores,
                           const void* labels, int label_dtype, int64_t begin, int64_t end,
                           unsigned long long* wins_ties, unsigned long long* nonfinite, unsigned* verdict,
-                          void* workspace, size_t workspace_bytes, hipStream_t st);
+                          void* workspace, size_t workspace_bytes, hipStream_t st, bool hist_ready = false);
 
 }  // namespace dauc

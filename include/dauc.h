@@ -256,12 +256,13 @@ int dauc_auc_counts_sorted_labeled(const float* pos, int64_t P, const float* sco
 /*
  * The exact-AUC evaluation of main.py:79-81 (sklearn roc_curve + auc over one test set), as ONE
  * stream-ordered sequence with no host synchronisation and no allocation: a memset of the
- * workspace header, a one-pass positive compaction (labels read once, P counted on the device),
+ * record, a one-pass positive compaction (labels read once, P counted on the device),
  * the count index built straight from the unsorted positives with the table size read on the
  * device, and the query pass over this part's scores [part*n/parts, (part+1)*n/parts), whose
  * labels are not 1 (every part builds the index over ALL the positives itself: ranks holding the
- * same test set need no collective to share the table). Then one 64-byte device copy:
- *   part_out (DEVICE int64[8]) = { W_part, T_part, #non-finite queried scores of this part,
+ * same test set need no collective to share the table). The kernels count straight into the
+ * record (no copy), so part_out must not overlap the workspace:
+ *   part_out (DEVICE int64[8], 8-byte aligned) = { W_part, T_part, #non-finite queried scores of this part,
  *                                  P, 0, #non-finite positives, #labels not in {-1, 1}, verdict }
  * The first three sum over the parts (the caller's all-reduce); the rest are the same on every
  * part. verdict (low 32 bits): 0 = nothing to query (empty part), 1 = counted, 2 = the count index

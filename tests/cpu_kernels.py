@@ -177,9 +177,20 @@ def _slot_cap(n, parts):
     return min(share, fair + fair // 4 + 64)
 
 
+_SLOT_HIST = 256                  # the slot's top-bucket histogram (2048 u32) after the header
+_SLOT_HDR = _SLOT_HIST + 2048 * 4  # the slot's scores
+
+
 def auc_slot_bytes(n, parts):
     """dauc_auc_slot_bytes' stand-in (same formula)."""
-    return 256 + -(-_slot_cap(n, parts) * 4 // 256) * 256
+    return _SLOT_HDR + -(-_slot_cap(n, parts) * 4 // 256) * 256
+
+
+def _top_buckets(pos):
+    """count_index.h's top-bucket histogram of the scores' order-preserving keys (-0 on +0)."""
+    u = (pos.astype(np.float32) + np.float32(0)).view(np.uint32)
+    key = u ^ np.where(u >> 31 != 0, np.uint32(0xffffffff), np.uint32(0x80000000))
+    return np.bincount(key >> 21, minlength=2048).astype(np.uint32)
 
 
 def _slice_lo(n, part, parts):
@@ -188,7 +199,8 @@ def _slice_lo(n, part, parts):
 
 def auc_eval_compact_part(scores, labels, part, parts, slot):
     """dauc_auc_eval_compact_part's stand-in: header {P_r, #non-finite positives, #other labels, 0}
-    (int64) at byte 0, the slice's positive scores (in order) from byte 256, at most cap of them."""
+    (int64) at byte 0, the positives' top-bucket histogram from byte 256, the slice's positive
+    scores (in order) from byte 8448, at most cap of them."""
     s, y = scores.detach().numpy(), labels.numpy().astype(np.int64)
     n = s.size
     lo, hi = _slice_lo(n, part, parts), _slice_lo(n, part + 1, parts)
@@ -196,8 +208,9 @@ def auc_eval_compact_part(scores, labels, part, parts, slot):
     pos = ss[yy == 1]
     hdr = np.array([pos.size, int((~np.isfinite(pos)).sum()), int(((yy != 1) & (yy != -1)).sum()), 0], np.int64)
     slot[:32] = torch.from_numpy(hdr.view(np.uint8).copy())
+    slot[_SLOT_HIST:_SLOT_HDR] = torch.from_numpy(_top_buckets(pos).view(np.uint8).copy())
     k = min(pos.size, _slot_cap(n, parts))
-    slot[256:256 + 4 * k] = torch.from_numpy(pos[:k].astype(np.float32).view(np.uint8).copy())
+    slot[_SLOT_HDR:_SLOT_HDR + 4 * k] = torch.from_numpy(pos[:k].astype(np.float32).view(np.uint8).copy())
     return slot
 
 
@@ -215,7 +228,7 @@ def auc_eval_query_part(scores, labels, part, parts, slots, out=None):
         h = raw[r * nb:r * nb + 32].view(np.int64)
         P, nfpos, other = P + int(h[0]), nfpos + int(h[1]), other + int(h[2])
         over |= int(h[0]) > cap
-        pos.append(raw[r * nb + 256:r * nb + 256 + 4 * min(int(h[0]), cap)].view(np.float32))
+        pos.append(raw[r * nb + _SLOT_HDR:r * nb + _SLOT_HDR + 4 * min(int(h[0]), cap)].view(np.float32))
     pos = np.concatenate(pos) if pos else np.zeros(0, np.float32)
     lo, hi = n * part // parts, n * (part + 1) // parts
     rec = torch.zeros(8, dtype=torch.int64) if out is None else out

@@ -893,6 +893,37 @@ def test_auc_eval_two_step_parts(dev, ldtype):
     assert {v[5] for v in _two_step(dev, s4, y, 4)} == {1}
 
 
+@pytest.mark.parametrize("n,G", [(300_007, 3), ((1 << 25) + 4097, 1)])
+def test_auc_eval_slot_layout(dev, n, G):
+    """The slot dauc_auc_eval_compact_part writes is the CPU stand-in's (tests/cpu_kernels.py):
+    the header, the top-bucket histogram of the slice's positives (count_index.h keys: -0 on +0,
+    NaN and +-inf included) and the positives themselves (as a multiset: the compaction keeps no
+    order). 2^25 labels in one slice take the wide compaction tiles."""
+    import cpu_kernels
+    from distributedauc_amd import ops
+
+    rng = np.random.default_rng(77)
+    s = (rng.standard_normal(n) * 3).astype(np.float32)
+    y = np.where(rng.random(n) < 0.002, 1, -1).astype(np.int8)
+    pos_idx = np.flatnonzero(y == 1)
+    s[pos_idx[:4]] = np.array([0.0, -0.0, np.inf, np.nan], np.float32)
+    y[5] = 0
+    nb = ops.auc_slot_bytes(n, G)
+    assert nb == cpu_kernels.auc_slot_bytes(n, G)
+    ts, ty = T(s, dev), T(y, dev)
+    for r in range(G):
+        got = torch.full((nb,), 0xAB, dtype=torch.uint8, device=dev)
+        ops.auc_eval_compact_part(ts, ty, r, G, got)
+        want = cpu_kernels.auc_eval_compact_part(torch.from_numpy(s), torch.from_numpy(y), r, G,
+                                                 torch.zeros(nb, dtype=torch.uint8))
+        g, w = got.cpu().numpy(), want.numpy()
+        assert np.array_equal(g[:32], w[:32]), r
+        assert np.array_equal(g[256:8448], w[256:8448]), r
+        k = int(w[:8].view(np.int64)[0])
+        gp, wp = g[8448:8448 + 4 * k].view(np.uint32), w[8448:8448 + 4 * k].view(np.uint32)
+        assert np.array_equal(np.sort(gp), np.sort(wp)), r
+
+
 def test_auc_sort_rejects_nonfinite_negatives(dev):
     """The sort method never materialises the negatives: the query kernel's finiteness count
     must still reject a NaN / inf negative (sklearn _ranking.py:868-869), sharded or not."""
