@@ -915,6 +915,10 @@ int compact_positives_zeroing(const float* scores, const void* labels, int label
             return DAUC_EINVAL;
     }
 }
+#ifdef DAUC_TUNING
+int g_compact_wide_log2 = 25;  // dauc_set_compact_wide (tuning builds)
+#endif
+
 int compact_unordered(const float* scores, const void* labels, int label_dtype, int64_t n, float* pos_out,
                       unsigned long long* stats, unsigned long long tag, unsigned long long* zero_next,
                       unsigned long long next_tag, unsigned long long* zero3, unsigned* zero_w, int nzero_w,
@@ -922,7 +926,11 @@ int compact_unordered(const float* scores, const void* labels, int label_dtype, 
     if (n <= 0 || scores == nullptr || labels == nullptr || pos_out == nullptr || stats == nullptr ||
         zero_next == nullptr)
         return DAUC_EINVAL;
+#ifdef DAUC_TUNING
+    const bool wide = n >= (int64_t(1) << g_compact_wide_log2);
+#else
     const bool wide = n >= (int64_t(1) << 25);
+#endif
     // wide inputs: 1024-thread workgroups of 32 label groups per thread (524,288-label tiles: 256
     // reservations at 2^27 instead of 1024 on the one counter address) -- 256
     constexpr int kWideThreads = 256;
@@ -959,6 +967,14 @@ int compact_unordered(const float* scores, const void* labels, int label_dtype, 
 }  // namespace dauc
 
 extern "C" {
+
+#ifdef DAUC_TUNING
+int dauc_set_compact_wide(int log2n) {
+    if (log2n < 10 || log2n > 40) return DAUC_EINVAL;
+    dauc::g_compact_wide_log2 = log2n;
+    return DAUC_OK;
+}
+#endif
 
 int dauc_compact_positives(const float* scores, const void* labels, int label_dtype, int64_t n,
                            float* pos_out, int64_t* stats, void* workspace, size_t workspace_bytes,

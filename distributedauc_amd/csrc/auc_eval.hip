@@ -213,7 +213,7 @@ int counts_part_blocking(const float* scores, const void* labels, int label_dtyp
 // ---- the sharded evaluation in two steps: each rank compacts only its slice -----------------
 //
 // Step 1 (dauc_auc_eval_compact_part): rank r compacts the positives of ITS slice of the labels
-// into a slot: a 256-byte header {P_r, #non-finite positives, #labels outside {-1, 1}} (u64), the
+// into a slot: a 256-byte header {P_r, 0, #non-finite positives, #labels outside {-1, 1}} (u64), the
 // top-bucket histogram of its positives' keys (count_index.h, 2048 u32) and room for `cap` scores.
 // The caller all-gathers the slots (one collective). Step 2 (dauc_auc_eval_query_part): the
 // gathered slots are concatenated into the evaluation's positive table on the device (their

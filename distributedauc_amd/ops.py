@@ -586,6 +586,13 @@ def set_query_path(path: int) -> None:
     check(_lib.tuning().dauc_set_query_path(int(path)), "dauc_set_query_path")
 
 
+def set_compact_wide(log2n: int) -> None:
+    """The compaction's tile-size threshold in the tuning build (dauc_set_compact_wide,
+    include/dauc_tuning.h): inputs of at least 2^log2n labels take the 131,072-label tiles.
+    Measurements only."""
+    check(_lib.tuning().dauc_set_compact_wide(int(log2n)), "dauc_set_compact_wide")
+
+
 def set_search_mode(mode: int) -> None:
     """Search structure of the sort method (dauc_set_search_mode): 0 automatic (the count index
     where the table fits it and is not skewed, else the LDS search tree), 1 the tree. Same

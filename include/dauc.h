@@ -307,12 +307,14 @@ int dauc_auc_eval_counts_part(const float* scores, const void* labels, int label
  * around the caller's collective (no host synchronisation in either):
  *   1. dauc_auc_eval_compact_part: the positives of THIS rank's slice of the labels (slices on
  *      256-label boundaries) compacted, unordered, into `slot` (device, dauc_auc_slot_bytes(n,
- *      parts) bytes, 256-byte aligned): a header {P_r, #non-finite positives, #labels not in
- *      {-1, 1}, 0} (int64) at byte 0 and the scores from byte 256;
+ *      parts) bytes, 256-byte aligned): a header {P_r, 0, #non-finite positives, #labels not in
+ *      {-1, 1}} (int64) at byte 0, the top-bucket histogram of the positives' order-preserving
+ *      keys (2048 uint32: key >> 21) from byte 256 and the scores from byte 8448;
  *   -- the caller all-gathers the `parts` slots, rank order, contiguous --
- *   2. dauc_auc_eval_query_part: the gathered slots become the positive table (headers summed),
- *      the count index is built from it and scores [part*n/parts, (part+1)*n/parts) are
- *      counted; part_out (device int64[8]) = dauc_auc_eval_enqueue's record. A slot holds an
+ *   2. dauc_auc_eval_query_part: the gathered slots become the positive table (headers and
+ *      histograms summed), the count index is built from it and scores [part*n/parts,
+ *      (part+1)*n/parts) are counted straight into part_out (device int64[8], 8-byte aligned,
+ *      outside the workspace and the slots) = dauc_auc_eval_enqueue's record. A slot holds an
  *      even share of the count index's capacity + 25 %: a slice with more positives (an
  *      unshuffled test set), like a table the index cannot hold, gives verdict 2 -- the caller
  *      then runs dauc_auc_eval_counts_part on every rank.

@@ -78,6 +78,13 @@ int dauc_set_direct_fault(int mode);
  */
 int dauc_set_query_path(int path);
 
+/*
+ * The one-pass unordered compaction's tile size in THIS library (process-wide, default 25): inputs
+ * of at least 2^log2n labels take 131,072-label tiles, smaller ones 32,768-label tiles (the tiles
+ * reserve their output ranges with returning atomics on one address). Measurements only.
+ */
+int dauc_set_compact_wide(int log2n);
+
 #ifdef __cplusplus
 }
 #endif

@@ -198,7 +198,7 @@ def _slice_lo(n, part, parts):
 
 
 def auc_eval_compact_part(scores, labels, part, parts, slot):
-    """dauc_auc_eval_compact_part's stand-in: header {P_r, #non-finite positives, #other labels, 0}
+    """dauc_auc_eval_compact_part's stand-in: header {P_r, 0, #non-finite positives, #other labels}
     (int64) at byte 0, the positives' top-bucket histogram from byte 256, the slice's positive
     scores (in order) from byte 8448, at most cap of them."""
     s, y = scores.detach().numpy(), labels.numpy().astype(np.int64)
@@ -206,7 +206,7 @@ def auc_eval_compact_part(scores, labels, part, parts, slot):
     lo, hi = _slice_lo(n, part, parts), _slice_lo(n, part + 1, parts)
     ss, yy = s[lo:hi], y[lo:hi]
     pos = ss[yy == 1]
-    hdr = np.array([pos.size, int((~np.isfinite(pos)).sum()), int(((yy != 1) & (yy != -1)).sum()), 0], np.int64)
+    hdr = np.array([pos.size, 0, int((~np.isfinite(pos)).sum()), int(((yy != 1) & (yy != -1)).sum())], np.int64)
     slot[:32] = torch.from_numpy(hdr.view(np.uint8).copy())
     slot[_SLOT_HIST:_SLOT_HDR] = torch.from_numpy(_top_buckets(pos).view(np.uint8).copy())
     k = min(pos.size, _slot_cap(n, parts))
@@ -226,7 +226,7 @@ def auc_eval_query_part(scores, labels, part, parts, slots, out=None):
     pos = []
     for r in range(parts):
         h = raw[r * nb:r * nb + 32].view(np.int64)
-        P, nfpos, other = P + int(h[0]), nfpos + int(h[1]), other + int(h[2])
+        P, nfpos, other = P + int(h[0]), nfpos + int(h[2]), other + int(h[3])
         over |= int(h[0]) > cap
         pos.append(raw[r * nb + _SLOT_HDR:r * nb + _SLOT_HDR + 4 * min(int(h[0]), cap)].view(np.float32))
     pos = np.concatenate(pos) if pos else np.zeros(0, np.float32)
