@@ -1,7 +1,7 @@
 """The query pass's fixed cost: rank 0's dauc_auc_eval_query_part at configs[4] (2^27 @ 0.1 %) for
 G = 8 .. 1024 parts (2^24 .. 2^17 queries over the same table), `reps` times each; run under
 `rocprofv3 --kernel-trace` and read query_ci_kernel's duration per G (the gather's grid.y is G).
-    python scripts/probe_query_intercept.py [reps]
+    python scripts/probe_query_intercept.py [reps] [positive fraction]
 """
 from __future__ import annotations
 
@@ -15,8 +15,9 @@ from distributedauc_amd import ops  # noqa: E402
 from distributedauc_amd.loader import synthetic_scores  # noqa: E402
 
 reps = int(sys.argv[1]) if len(sys.argv) > 1 else 10
+pos = float(sys.argv[2]) if len(sys.argv) > 2 else 0.001  # a smaller table: a smaller LDS index
 dev = torch.device("cuda", 0)
-s, y = synthetic_scores(1 << 27, 0.001, dev)
+s, y = synthetic_scores(1 << 27, pos, dev)
 n = s.numel()
 rec = torch.zeros(8, dtype=torch.int64, device=dev)
 for G in (8, 16, 32, 64, 128, 256, 1024):
