@@ -917,6 +917,7 @@ int compact_positives_zeroing(const float* scores, const void* labels, int label
 }
 #ifdef DAUC_TUNING
 int g_compact_wide_log2 = 25;  // dauc_set_compact_wide (tuning builds)
+int g_compact_slots = kCmpSlots;  // dauc_set_compact_slots: the narrow tiles' label groups per thread
 #endif
 
 int compact_unordered(const float* scores, const void* labels, int label_dtype, int64_t n, float* pos_out,
@@ -935,7 +936,12 @@ int compact_unordered(const float* scores, const void* labels, int label_dtype, 
     // reservations at 2^27 instead of 1024 on the one counter address) -- 256
     constexpr int kWideThreads = 256;
     const int threads = wide ? kWideThreads : kCmpThreads;
-    const int64_t tile = int64_t(threads) * 16 * (wide ? 32 : kCmpSlots);
+#ifdef DAUC_TUNING
+    const int slots = wide ? 32 : g_compact_slots;
+#else
+    const int slots = wide ? 32 : kCmpSlots;
+#endif
+    const int64_t tile = int64_t(threads) * 16 * slots;
     const int64_t nblk = (n + tile - 1) / tile;
     if (nblk > 0x7fffffffLL) return DAUC_EINVAL;
     const int vec = (reinterpret_cast<uintptr_t>(labels) & 15u) == 0;
@@ -948,6 +954,22 @@ int compact_unordered(const float* scores, const void* labels, int label_dtype, 
         else if (wide)
             hipLaunchKernelGGL((compact_unordered_kernel<LT, 32, kWideThreads>), grid, block, 0, st, scores, lab, n, vec,
                                pos_out, stats, tag, zero_next, next_tag, zero3, zero_w, nzero_w, cap, hist_out);
+#ifdef DAUC_TUNING
+        else if (slots != kCmpSlots) {
+            auto narrow = [&](auto sl) {
+                constexpr int S = decltype(sl)::value;
+                if (hist_out != nullptr)
+                    hipLaunchKernelGGL((compact_unordered_kernel<LT, S, kCmpThreads, true>), grid, block, 0, st, scores,
+                                       lab, n, vec, pos_out, stats, tag, zero_next, next_tag, zero3, zero_w, nzero_w,
+                                       cap, hist_out);
+                else
+                    hipLaunchKernelGGL((compact_unordered_kernel<LT, S>), grid, block, 0, st, scores, lab, n, vec,
+                                       pos_out, stats, tag, zero_next, next_tag, zero3, zero_w, nzero_w, cap, hist_out);
+            };
+            if (slots == 4) narrow(std::integral_constant<int, 4>{});
+            else narrow(std::integral_constant<int, 16>{});
+        }
+#endif
         else if (hist_out != nullptr)
             hipLaunchKernelGGL((compact_unordered_kernel<LT, kCmpSlots, kCmpThreads, true>), grid, block, 0, st, scores,
                                lab, n, vec, pos_out, stats, tag, zero_next, next_tag, zero3, zero_w, nzero_w, cap,
@@ -972,6 +994,12 @@ extern "C" {
 int dauc_set_compact_wide(int log2n) {
     if (log2n < 10 || log2n > 40) return DAUC_EINVAL;
     dauc::g_compact_wide_log2 = log2n;
+    return DAUC_OK;
+}
+
+int dauc_set_compact_slots(int slots) {
+    if (slots != 4 && slots != 8 && slots != 16) return DAUC_EINVAL;
+    dauc::g_compact_slots = slots;
     return DAUC_OK;
 }
 #endif

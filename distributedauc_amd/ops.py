@@ -593,6 +593,12 @@ def set_compact_wide(log2n: int) -> None:
     check(_lib.tuning().dauc_set_compact_wide(int(log2n)), "dauc_set_compact_wide")
 
 
+def set_compact_slots(slots: int) -> None:
+    """The narrow compaction tiles' label groups per thread in the tuning build
+    (dauc_set_compact_slots, include/dauc_tuning.h): 4, 8 or 16. Measurements only."""
+    check(_lib.tuning().dauc_set_compact_slots(int(slots)), "dauc_set_compact_slots")
+
+
 def set_search_mode(mode: int) -> None:
     """Search structure of the sort method (dauc_set_search_mode): 0 automatic (the count index
     where the table fits it and is not skewed, else the LDS search tree), 1 the tree. Same

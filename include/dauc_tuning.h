@@ -85,6 +85,12 @@ int dauc_set_query_path(int path);
  */
 int dauc_set_compact_wide(int log2n);
 
+/*
+ * The narrow compaction tiles' size in THIS library (process-wide, default 8): 4, 8 or 16 label
+ * groups of 16 per thread (16,384-, 32,768- or 65,536-label tiles). Measurements only.
+ */
+int dauc_set_compact_slots(int slots);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,6 +1,7 @@
 """VALU-issue roofline of the labeled query pass from committed rocprofv3 data.
 
-Inputs (profiles/r02/pmc_count_index/, or the directory given as argv[1]): SQ_INSTS_VALU /
+Inputs (profiles/r02/pmc_count_index/, or the directory given as argv[1], e.g. profiles/r04/pmc_query/
+from scripts/gpu_r04_pmcq.sh over the one-call evaluation): SQ_INSTS_VALU /
 SQ_INSTS_LDS per dispatch (one --pmc pass, scripts/gpu_pmc_ci.sh) and the kernel's average
 duration from a separate --kernel-trace --stats pass over the same command; LDS bank-conflict,
 wait and in-flight counters. The query pass is the count-index kernel (query_ci_kernel) where the
@@ -48,14 +49,18 @@ def avg_us(f):
 
 
 def main():
-    out = {"method": __doc__.split("\n\n")[1].replace("\n", " "), "peak_wave_instr_per_s": PEAK}
+    out = {"method": __doc__.split("\n\n")[1].replace("\n", " "), "peak_wave_instr_per_s": PEAK,
+           "source": str(SRC.resolve().relative_to(REPO)) if SRC.resolve().is_relative_to(REPO) else str(SRC)}
     for tag, n in (("27", 1 << 27), ("24", 1 << 24)):
         c = counters(SRC / f"valu{tag}_counters.csv")
         us = avg_us(SRC / f"trace{tag}_kernel_stats.csv")
         rate = c["SQ_INSTS_VALU"] / (us * 1e-6)
         rec = {"queries": n, "avg_launch_us": us, "valu_wave_instr": c["SQ_INSTS_VALU"],
                "valu_per_query": c["SQ_INSTS_VALU"] * 64 / n, "lds_per_query": c["SQ_INSTS_LDS"] * 64 / n,
-               "achieved_wave_instr_per_s": rate, "frac": rate / PEAK}
+               "achieved_wave_instr_per_s": rate, "frac": rate / PEAK,
+               # the kernel's VALU is integer work: at 4 cycles per wave64 instruction (the no-window
+               # ablation's 351 us for ~100 VALU per query at 2^27 fits it) the ceiling is half
+               "frac_of_4cycle_issue": rate / (PEAK / 2)}
         if tag == "27":
             lds = counters(SRC / "lds27_counters.csv")
             cyc = us * 1e-6 * 2.4e9
