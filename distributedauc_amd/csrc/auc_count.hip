@@ -534,7 +534,7 @@ __global__ __launch_bounds__(kCmpThreads) void compact_write_kernel(
 // for the earlier tiles' counts (no mask pass, no second launch). stats[0] (positives, the
 // reservation counter), stats[2] (non-finite positives) and stats[3] (labels outside {-1, 1})
 // must be zero on entry; stats[1] is not written (N = n - P). Block 0 zeroes `zero_next` (the
-// next call's stats) and the first `nzero_w` words of `zero_w`, and zero3[0..3).
+// next call's stats) and zero3[0..3); the grid zeroes the first `nzero_w` words of `zero_w`.
 // SLOTS groups of 16 labels per thread: 8 (a 32768-label tile) for small inputs; 32 (131072) for
 // large ones, where the reservation atomics of 4096 tiles on one address serialise (2^27 labels:
 // 65 us at 8 slots). HIST: hist_out += the top-bucket histogram of the positives' keys (an LDS
@@ -555,8 +555,9 @@ __global__ __launch_bounds__(THREADS) void compact_unordered_kernel(
     if (blockIdx.x == 0) {
         if (threadIdx.x < 4) zero_next[threadIdx.x] = threadIdx.x == 1 ? next_tag : 0ull;
         else if (threadIdx.x < 7 && zero3 != nullptr) zero3[threadIdx.x - 4] = 0ull;
-        for (int i = threadIdx.x; i < nzero_w; i += THREADS) zero_w[i] = 0u;
     }
+    for (int64_t i = int64_t(blockIdx.x) * THREADS + threadIdx.x; i < nzero_w; i += int64_t(gridDim.x) * THREADS)
+        zero_w[i] = 0u;  // spread over the grid (a later stage's counters: up to 147 k words)
     // the slot's tag (written with the zeroes by the previous call): a workspace whose slot was
     // not left by this thread's previous call holds stale counters, so no tile reserves from it
     // (the caller sees the tag and starts over with zeroed slots)

@@ -3,9 +3,9 @@
 // Reference: imagenet/main.py:79-81, AUC(label, scores) = sklearn roc_curve(pos_label=1) + auc,
 // evaluated by rank 0 over the test set (main.py:237-250). The evaluation is:
 //   1. one memset of the 64-byte record (the compaction's counters, the query counts, the
-//      verdict word);
+//      verdict word) and the top-bucket histogram;
 //   2. the one-pass positive compaction: labels read once, the positives' scores gathered (in no
-//      particular order), P counted on the device;
+//      particular order), P counted on the device, their top-bucket histogram built;
 //   3. the count index built straight from the unsorted positives, sized by the device's P
 //      (auc_sort.hip, direct_*: the grids are sized for the index's capacity and loop), and the
 //      labeled query pass over the scores [part * n / parts, (part + 1) * n / parts), which also
@@ -35,16 +35,18 @@ inline size_t align256(size_t b) { return (b + 255) / 256 * 256; }
 
 // workspace header (bytes): [0, 24) W, T, #non-finite queried scores (u64, the query's atomics);
 // [24, 56) the compaction's counters: P, tag (0), #non-finite positives, #labels outside {-1, 1};
-// [56, 60) the verdict; [64, 96) a second counter slot the compaction's block 0 writes (unused).
-// [0, 64) is the result record (the blocking forms'; the enqueued forms count into the caller's
-// part_out instead), zeroed by the call's one memset.
-constexpr size_t kHdr = 256, kRecord = 64;
+// [56, 60) the verdict; [64, 96) a second counter slot the compaction's block 0 writes (unused);
+// [256, 8448) the top-bucket histogram of the positives (the compaction's, handed to the direct
+// build: no histogram pass). [0, 64) is the result record (the blocking forms'; the enqueued
+// forms count into the caller's part_out instead); record and histogram are zeroed first.
+constexpr size_t kHistOff = 256, kHdr = kHistOff + size_t(kCiTop) * 4, kRecord = 64;
 
 struct EvalWs {
     unsigned long long* wt;       // [3]
     unsigned long long* slot;     // [4]
     unsigned* verdict;
     unsigned long long* spare;    // [4]
+    unsigned* hist;               // [kCiTop]
     float* pos;                   // [n]   positive scores (P <= n)
     float* neg;                   // [n/2] negative scores (only when P > N, so N < n/2)
     int64_t* split_stats;         // [4]   the split's stats (sorted fallback)
@@ -65,6 +67,7 @@ EvalWs eval_ws(void* ws, int64_t n) {
     w.verdict = reinterpret_cast<unsigned*>(p + 56);
     w.spare = reinterpret_cast<unsigned long long*>(p + 64);
     w.split_stats = reinterpret_cast<int64_t*>(p + 128);
+    w.hist = reinterpret_cast<unsigned*>(p + kHistOff);
     p += kHdr;
     w.pos = reinterpret_cast<float*>(p);
     p += align256(size_t(n) * 4);
@@ -115,12 +118,19 @@ EvalWs with_record(EvalWs w, int64_t* rec) {
 int enqueue(const float* scores, const void* labels, int label_dtype, int64_t n, int part, int parts,
             const EvalWs& w, hipStream_t st) {
     hipError_t e;
-    if ((e = hipMemsetAsync(w.wt, 0, kRecord, st)) != hipSuccess) return -static_cast<int>(e);
+    // the record and the histogram: one memset when the record is the workspace header's
+    if (reinterpret_cast<char*>(w.hist) == reinterpret_cast<char*>(w.wt) + kHistOff) {
+        if ((e = hipMemsetAsync(w.wt, 0, kHdr, st)) != hipSuccess) return -static_cast<int>(e);
+    } else if ((e = hipMemsetAsync(w.wt, 0, kRecord, st)) != hipSuccess ||
+               (e = hipMemsetAsync(w.hist, 0, size_t(kCiTop) * 4, st)) != hipSuccess) {
+        return -static_cast<int>(e);
+    }
     const int64_t mcap = direct_capacity(n);
-    unsigned* hist = reinterpret_cast<unsigned*>(static_cast<char*>(w.tws) + direct_hist_offset(mcap));
-    // the compaction also zeroes the direct build's histogram (its block 0, ahead of every use)
-    int rc = compact_unordered(scores, labels, label_dtype, n, w.pos, w.slot, 0ull, w.spare, 0ull, nullptr, hist,
-                               direct_hist_words(), st);
+    // the compaction builds the direct build's histogram and zeroes its per-cell counters (spread
+    // over its grid), so the build skips its histogram pass
+    int rc = compact_unordered(scores, labels, label_dtype, n, w.pos, w.slot, 0ull, w.spare, 0ull, nullptr,
+                               direct_cnt_ptr(w.tws, mcap), static_cast<int>(direct_cnt_words()), st, INT64_MAX,
+                               w.hist);
     if (rc) return rc;
     const int64_t qlo = n * part / parts, qhi = n * (part + 1) / parts;
     if (qhi <= qlo) return DAUC_OK;  // an empty part: verdict 0, counts 0
@@ -134,7 +144,7 @@ int enqueue(const float* scores, const void* labels, int label_dtype, int64_t n,
                               w.wt + 2, w.verdict, w.bws, w.bws_bytes, st);
 #endif
     return counts_labeled_direct(w.pos, w.slot, mcap, scores, labels, label_dtype, qlo, qhi, w.wt, w.wt + 2,
-                                 w.verdict, w.tws, w.tws_bytes, st);
+                                 w.verdict, w.tws, w.tws_bytes, st, w.hist);
 }
 
 // The sorted path for a verdict-2 evaluation (P, N known): counts of part `part` into w.wt.
@@ -380,7 +390,7 @@ int dauc_auc_eval_query_part(const float* scores, const void* labels, int label_
         else
 #endif
             rc = counts_labeled_direct(w.pos, w.spare, mcap, scores, labels, label_dtype, qlo, qhi, w.wt, w.wt + 2,
-                                       w.verdict, w.tws, w.tws_bytes, st, true);
+                                       w.verdict, w.tws, w.tws_bytes, st, hist);
         if (rc) return rc;
     }
     return DAUC_OK;

@@ -1715,8 +1715,6 @@ int64_t direct_capacity(int64_t n) {
     return half < cap ? half : cap;
 }
 
-int direct_hist_words() { return kCiTop; }
-
 unsigned* direct_cnt_ptr(void* workspace, int64_t Mcap) { return count_ws_of(workspace, Mcap).cstart; }
 
 int64_t direct_cnt_words() { return kCiCntWords; }
@@ -1751,7 +1749,7 @@ __global__ void direct_fault_kernel(int mode, const unsigned long long* __restri
 constexpr int64_t kDirectGrid = 1024;
 
 int build_direct_index(const float* pos, const unsigned long long* Mp, int64_t Mcap, void* workspace,
-                       size_t workspace_bytes, hipStream_t st, DirectIndex* ix, bool hist_ready) {
+                       size_t workspace_bytes, hipStream_t st, DirectIndex* ix, const unsigned* ready_hist) {
     if (pos == nullptr || Mp == nullptr || Mcap < 1 || workspace == nullptr || ix == nullptr ||
         workspace_bytes < dauc_sort_workspace_size(Mcap))
         return DAUC_EINVAL;
@@ -1765,11 +1763,11 @@ int build_direct_index(const float* pos, const unsigned long long* Mp, int64_t M
         const int64_t b = (keys + per - 1) / per;
         return dim3(static_cast<unsigned>(b < cap ? b : cap));
     };
-    if (!hist_ready)
+    if (ready_hist == nullptr)
         hipLaunchKernelGGL(direct_hist_kernel, blocks(Mcap, 256 * kDirectPerThread, 256), dim3(256), 0, st, pos, Mp,
                            nw.first, nw.cstart, kCiCntWords);
     hipLaunchKernelGGL(direct_count_kernel, blocks(Mcap, kDirectThreads, kDirectGrid), dim3(kDirectThreads), 0, st, pos,
-                       Mcap, nw.first, nw.l1, nw.meta, nw.cstart, w.keys_b);
+                       Mcap, ready_hist ? ready_hist : nw.first, nw.l1, nw.meta, nw.cstart, w.keys_b);
     hipLaunchKernelGGL(direct_blocks_kernel, dim3(kDirectMaxGroups), dim3(kDirectGroup), 0, st, nw.cstart, nw.meta,
                        nw.blk, grp);
 #ifdef DAUC_TUNING
@@ -1786,13 +1784,13 @@ int build_direct_index(const float* pos, const unsigned long long* Mp, int64_t M
 int counts_labeled_direct(const float* pos, const unsigned long long* Mp, int64_t Mcap, const float* scores,
                           const void* labels, int label_dtype, int64_t begin, int64_t end,
                           unsigned long long* wins_ties, unsigned long long* nonfinite, unsigned* verdict,
-                          void* workspace, size_t workspace_bytes, hipStream_t st, bool hist_ready) {
+                          void* workspace, size_t workspace_bytes, hipStream_t st, const unsigned* ready_hist) {
     if (begin < 0 || end < begin || wins_ties == nullptr || (end > begin && (scores == nullptr || labels == nullptr)))
         return DAUC_EINVAL;
     if (label_dtype != DAUC_LABEL_I8 && label_dtype != DAUC_LABEL_I32 && label_dtype != DAUC_LABEL_I64)
         return DAUC_EINVAL;
     DirectIndex ix{};
-    int rc = build_direct_index(pos, Mp, Mcap, workspace, workspace_bytes, st, &ix, hist_ready);
+    int rc = build_direct_index(pos, Mp, Mcap, workspace, workspace_bytes, st, &ix, ready_hist);
     if (rc || end == begin) return rc;
     const CountWs nw = count_ws_of(workspace, Mcap);
     switch (label_dtype) {

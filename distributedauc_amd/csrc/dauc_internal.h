@@ -106,8 +106,8 @@ int compact_positives_zeroing(const float* scores, const void* labels, int label
 // auc_count.hip: the one-call evaluation's single-pass, unordered positive compaction. stats[0]
 // (P), stats[2] (non-finite positives), stats[3] (labels outside {-1, 1}) must be zero on entry
 // and stats[1] must hold `tag` (else no tile reserves or writes anything); block 0 zeroes
-// zero_next[0, 2, 3], sets zero_next[1] = next_tag, and zeroes zero3[0..3) (nullable) and
-// zero_w[0..nzero_w). At most `cap` positives are stored (stats[0] still counts them all).
+// zero_next[0, 2, 3], sets zero_next[1] = next_tag, and zeroes zero3[0..3) (nullable); the grid
+// zeroes zero_w[0..nzero_w). At most `cap` positives are stored (stats[0] still counts them all).
 // hist_out (nullable; kCiTop words, zero on entry) += the top-bucket histogram of the positives'
 // keys (count_index.h), so a build from them can skip its histogram pass.
 int compact_unordered(const float* scores, const void* labels, int label_dtype, int64_t n, float* pos_out,
@@ -118,22 +118,24 @@ int compact_unordered(const float* scores, const void* labels, int label_dtype, 
 // auc_sort.hip: the count index built straight from the unsorted positives (no radix sort, no
 // tree) and the labeled query pass over scores [begin, end); the table is ordered by cell only.
 // The table size M is read from the device (*Mp, the compaction's count), so nothing waits for the
-// host; the workspace is carved for Mcap = direct_capacity(n) keys. `hist` (kCiTop words at
-// direct_hist_offset(Mcap)) must be zero on entry. *verdict (device) = 1 when the count index held
-// the table, 2 when the caller must run the sorted path (M > Mcap, or a skewed table).
+// host; the workspace is carved for Mcap = direct_capacity(n) keys. Without a ready histogram
+// the build's own `hist` (kCiTop words at direct_hist_offset(Mcap)) must be zero on entry; with
+// one (the table's top-bucket histogram, whose total is the table size), the per-cell counters
+// (direct_cnt_ptr) must be. *verdict (device) = 1 when the count index held the table, 2 when the
+// caller must run the sorted path (M > Mcap, or a skewed table).
 bool direct_enabled();  // the search mode is automatic (always, except in a tuning build's mode 1 / 2)
 int64_t direct_capacity(int64_t n);
 int64_t direct_hist_offset(int64_t Mcap);  // byte offset of `hist` in the sort workspace
-int direct_hist_words();
 // the per-cell counters the count pass adds into (zeroed by the histogram pass, or by the caller
 // when it hands over a ready histogram)
 unsigned* direct_cnt_ptr(void* workspace, int64_t Mcap);
 int64_t direct_cnt_words();
 struct DirectIndex;  // count_index.h
-// the direct build alone (4 launches; 3 with hist_ready: `hist` already holds the table's top-
-// bucket histogram and the per-cell counters are zero): fills *ix with the index's device pointers
+// the direct build alone (4 launches; 3 with a ready histogram: `ready_hist` (kCiTop words, or
+// nullptr) already holds the table's top-bucket histogram and the per-cell counters are zero):
+// fills *ix with the index's device pointers
 int build_direct_index(const float* pos, const unsigned long long* Mp, int64_t Mcap, void* workspace,
-                       size_t workspace_bytes, hipStream_t st, DirectIndex* ix, bool hist_ready = false);
+                       size_t workspace_bytes, hipStream_t st, DirectIndex* ix, const unsigned* ready_hist = nullptr);
 #ifdef DAUC_TUNING
 // tuning_slots.hip (tuning builds only): the labeled queries [begin, end) counted through the range-slot index built
 // straight from the unsorted positives pos[0 .. *Mp) (split + count passes); workspace of
@@ -153,6 +155,7 @@ int eval_query_path();
 int counts_labeled_direct(const float* pos, const unsigned long long* Mp, int64_t Mcap, const float* scores,
                           const void* labels, int label_dtype, int64_t begin, int64_t end,
                           unsigned long long* wins_ties, unsigned long long* nonfinite, unsigned* verdict,
-                          void* workspace, size_t workspace_bytes, hipStream_t st, bool hist_ready = false);
+                          void* workspace, size_t workspace_bytes, hipStream_t st,
+                          const unsigned* ready_hist = nullptr);
 
 }  // namespace dauc

@@ -893,6 +893,38 @@ def test_auc_eval_two_step_parts(dev, ldtype):
     assert {v[5] for v in _two_step(dev, s4, y, 4)} == {1}
 
 
+def test_auc_eval_records_counted_in_place(dev):
+    """The enqueued forms count straight into the caller's part_out (no copy from the workspace):
+    a record holding garbage, or the previous call's counts, comes back exactly the fresh record
+    (the enqueue's memset, the query part's gather zero it first); two parts' records side by side
+    in one buffer do not disturb each other."""
+    from distributedauc_amd import ops
+
+    rng = np.random.default_rng(31)
+    n = 200_003
+    s = rng.random(n, dtype=np.float32)
+    y = np.where(rng.random(n) < 0.01, 1, -1).astype(np.int8)
+    e = coracle.auc_counts(y.astype(np.int64), s)
+    ts, ty = T(s, dev), T(y, dev)
+    G = 2
+    nb = ops.auc_slot_bytes(n, G)
+    slots = torch.empty(nb * G, dtype=torch.uint8, device=dev)
+    for r in range(G):
+        ops.auc_eval_compact_part(ts, ty, r, G, slots[r * nb:(r + 1) * nb])
+    recs = torch.full((8 * G,), -0x0123456789ABCDEF, dtype=torch.int64, device=dev)
+    for rep in range(2):
+        for r in range(G):
+            ops.auc_eval_query_part(ts, ty, r, G, slots, out=recs[8 * r:8 * (r + 1)])
+        v = recs.view(G, 8).cpu().tolist()
+        assert (sum(x[0] for x in v), sum(x[1] for x in v)) == (e["wins"], e["ties"]), rep
+        assert all(x[3] == e["P"] and x[4] == 0 and x[7] == 1 for x in v), (rep, v)
+        recs.fill_(-1)
+        for r in range(G):
+            ops.auc_eval_enqueue(ts, ty, r, G, out=recs[8 * r:8 * (r + 1)])
+        w = recs.view(G, 8).cpu().tolist()
+        assert w == v, (rep, w, v)
+
+
 @pytest.mark.parametrize("n,G", [(300_007, 3), ((1 << 25) + 4097, 1)])
 def test_auc_eval_slot_layout(dev, n, G):
     """The slot dauc_auc_eval_compact_part writes is the CPU stand-in's (tests/cpu_kernels.py):
