@@ -621,56 +621,27 @@ __global__ __launch_bounds__(THREADS) void compact_unordered_kernel(
         tile += wtot[0][w];
     }
     if (seen != tag) return;  // uniform across the workgroup
-    // The reservation's round trip (and its queue on the one address) overlaps the positives'
-    // score gathers: the scores go to a tile-local LDS stage at their in-tile offsets while the
-    // returning atomic is in flight, and are copied out contiguously once the base is known. A
-    // tile of more than kStage positives writes them straight to pos_out after the reservation.
-    constexpr int kStage = 4096;
-    __shared__ float stage[kStage];
-    unsigned long long base_r = 0ull;
     if (threadIdx.x == 0) {
         int other = 0;
 #pragma unroll
         for (int w = 0; w < kW; ++w) other += wtot[1][w];
         if (other) atomicAdd(stats + 3, static_cast<unsigned long long>(other));
-        if (tile) base_r = atomicAdd(stats + 0, static_cast<unsigned long long>(tile));  // waited for below
+        base_s = tile ? atomicAdd(stats + 0, static_cast<unsigned long long>(tile)) : 0ull;
     }
-    if (tile == 0) return;  // uniform
-    const int lo0 = before + incl - np;  // this thread's first positive within the tile
+    __syncthreads();
+    if (tile == 0) return;
+    int64_t r = int64_t(base_s) + before + incl - np;
     int nf = 0;
-    if (tile <= kStage) {
-        int lo = lo0;
 #pragma unroll 1
-        for (int k = 0; k < SLOTS; ++k) {
-            const int64_t i = base + (int64_t(k) * THREADS + threadIdx.x) * 16;
-            const unsigned mk = msk[k][threadIdx.x];  // this thread's own word: no barrier needed
-            for (unsigned b = mk; b != 0u; b &= b - 1u) {
-                const float v = s[i + __ffs(b) - 1];
-                nf += !isfinite(v);
-                stage[lo++] = v;
-                if constexpr (HIST) atomicAdd(&hs[key_fast(v) >> kCiLowBits], 1u);
-            }
-        }
-        if (threadIdx.x == 0) base_s = base_r;
-        __syncthreads();
-        const int64_t b0 = static_cast<int64_t>(base_s);
-        for (int j = threadIdx.x; j < tile; j += THREADS)
-            if (b0 + j < cap) pos_out[b0 + j] = stage[j];  // past `cap`: counted, not stored (the caller's overflow)
-    } else {
-        if (threadIdx.x == 0) base_s = base_r;
-        __syncthreads();
-        int64_t r = static_cast<int64_t>(base_s) + lo0;
-#pragma unroll 1
-        for (int k = 0; k < SLOTS; ++k) {
-            const int64_t i = base + (int64_t(k) * THREADS + threadIdx.x) * 16;
-            const unsigned mk = msk[k][threadIdx.x];
-            for (unsigned b = mk; b != 0u; b &= b - 1u) {
-                const float v = s[i + __ffs(b) - 1];
-                nf += !isfinite(v);
-                if (r < cap) pos_out[r] = v;
-                ++r;
-                if constexpr (HIST) atomicAdd(&hs[key_fast(v) >> kCiLowBits], 1u);
-            }
+    for (int k = 0; k < SLOTS; ++k) {
+        const int64_t i = base + (int64_t(k) * THREADS + threadIdx.x) * 16;
+        const unsigned mk = msk[k][threadIdx.x];  // this thread's own word: no barrier needed
+        for (unsigned b = mk; b != 0u; b &= b - 1u) {
+            const float v = s[i + __ffs(b) - 1];
+            nf += !isfinite(v);
+            if (r < cap) pos_out[r] = v;  // past `cap`: counted in stats[0], not stored (the caller's overflow)
+            ++r;
+            if constexpr (HIST) atomicAdd(&hs[key_fast(v) >> kCiLowBits], 1u);
         }
     }
     if (nf) atomicAdd(stats + 2, static_cast<unsigned long long>(nf));
