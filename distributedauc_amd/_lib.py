@@ -97,6 +97,7 @@ TUNING_SIGNATURES = {
     "dauc_set_query_path": (_int, [_int]),
     "dauc_set_compact_wide": (_int, [_int]),
     "dauc_set_compact_slots": (_int, [_int]),
+    "dauc_set_compact_stage": (_int, [_int]),
 }
 TUNING_LIB_PATH = Path(os.environ.get("DAUC_TUNING_LIB", PKG_DIR.parent / "tuning" / "libdauc_tuning.so"))
 

@@ -599,6 +599,12 @@ def set_compact_slots(slots: int) -> None:
     check(_lib.tuning().dauc_set_compact_slots(int(slots)), "dauc_set_compact_slots")
 
 
+def set_compact_stage(on: int) -> None:
+    """The compaction's staged-score variant in the tuning build (dauc_set_compact_stage,
+    include/dauc_tuning.h): 1 on, 0 off. Measurements only."""
+    check(_lib.tuning().dauc_set_compact_stage(int(on)), "dauc_set_compact_stage")
+
+
 def set_search_mode(mode: int) -> None:
     """Search structure of the sort method (dauc_set_search_mode): 0 automatic (the count index
     where the table fits it and is not skewed, else the LDS search tree), 1 the tree. Same

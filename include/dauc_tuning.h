@@ -91,6 +91,14 @@ int dauc_set_compact_wide(int log2n);
  */
 int dauc_set_compact_slots(int slots);
 
+/*
+ * The one-pass compaction's staged-score variant in THIS library (process-wide, default 0): 1 =
+ * a tile stages its positives' scores in LDS while its reservation atomic is in flight and copies
+ * them out contiguously once the base is known (tiles of up to 4096 positives). Same output.
+ * Measurements only.
+ */
+int dauc_set_compact_stage(int on);
+
 #ifdef __cplusplus
 }
 #endif
