@@ -94,10 +94,6 @@ TUNING_SIGNATURES = {
     "dauc_pair_count_variant": (_int, [_vp, _i64, _vp, _i64, _vp, _int, _vp]),
     "dauc_set_search_mode": (_int, [_int]),
     "dauc_set_direct_fault": (_int, [_int]),
-    "dauc_set_query_path": (_int, [_int]),
-    "dauc_set_compact_wide": (_int, [_int]),
-    "dauc_set_compact_slots": (_int, [_int]),
-    "dauc_set_compact_stage": (_int, [_int]),
 }
 TUNING_LIB_PATH = Path(os.environ.get("DAUC_TUNING_LIB", PKG_DIR.parent / "tuning" / "libdauc_tuning.so"))
 

@@ -539,9 +539,7 @@ __global__ __launch_bounds__(kCmpThreads) void compact_write_kernel(
 // large ones, where the reservation atomics of 4096 tiles on one address serialise (2^27 labels:
 // 65 us at 8 slots). HIST: hist_out += the top-bucket histogram of the positives' keys (an LDS
 // histogram per tile, its used buckets added once).
-// STAGE (tuning builds only, dauc_set_compact_stage): the positives' scores staged in LDS while the
-// tile's reservation atomic is in flight, then copied out contiguously.
-template <typename LT, int SLOTS, int THREADS = kCmpThreads, bool HIST = false, bool STAGE = false>
+template <typename LT, int SLOTS, int THREADS = kCmpThreads, bool HIST = false>
 __global__ __launch_bounds__(THREADS) void compact_unordered_kernel(
     const float* __restrict__ s, const LT* __restrict__ lab, int64_t n, int vec, float* __restrict__ pos_out,
     unsigned long long* __restrict__ stats, unsigned long long tag, unsigned long long* __restrict__ zero_next,
@@ -624,77 +622,26 @@ __global__ __launch_bounds__(THREADS) void compact_unordered_kernel(
     }
     if (seen != tag) return;  // uniform across the workgroup
     int nf = 0;
-    if constexpr (STAGE) {
-        constexpr int kStage = 4096;
-        __shared__ float stage[kStage];
-        unsigned long long base_r = 0ull;
-        if (threadIdx.x == 0) {
-            int other = 0;
+    if (threadIdx.x == 0) {
+        int other = 0;
 #pragma unroll
-            for (int w = 0; w < kW; ++w) other += wtot[1][w];
-            if (other) atomicAdd(stats + 3, static_cast<unsigned long long>(other));
-            if (tile) base_r = atomicAdd(stats + 0, static_cast<unsigned long long>(tile));  // waited for below
-        }
-        if (tile == 0) return;  // uniform
-        const int lo0 = before + incl - np;  // this thread's first positive within the tile
-        const bool staged = tile <= kStage;  // uniform
-        int lo = lo0;
-        if (staged) {
+        for (int w = 0; w < kW; ++w) other += wtot[1][w];
+        if (other) atomicAdd(stats + 3, static_cast<unsigned long long>(other));
+        base_s = tile ? atomicAdd(stats + 0, static_cast<unsigned long long>(tile)) : 0ull;
+    }
+    __syncthreads();
+    if (tile == 0) return;
+    int64_t r = int64_t(base_s) + before + incl - np;
 #pragma unroll 1
-            for (int k = 0; k < SLOTS; ++k) {
-                const int64_t i = base + (int64_t(k) * THREADS + threadIdx.x) * 16;
-                const unsigned mk = msk[k][threadIdx.x];
-                for (unsigned b = mk; b != 0u; b &= b - 1u) {
-                    const float v = s[i + __ffs(b) - 1];
-                    nf += !isfinite(v);
-                    stage[lo++] = v;
-                    if constexpr (HIST) atomicAdd(&hs[key_fast(v) >> kCiLowBits], 1u);
-                }
-            }
-        }
-        if (threadIdx.x == 0) base_s = base_r;
-        __syncthreads();
-        const int64_t b0 = static_cast<int64_t>(base_s);
-        if (staged) {
-            for (int j = threadIdx.x; j < tile; j += THREADS)
-                if (b0 + j < cap) pos_out[b0 + j] = stage[j];
-        } else {
-            int64_t r = b0 + lo0;
-#pragma unroll 1
-            for (int k = 0; k < SLOTS; ++k) {
-                const int64_t i = base + (int64_t(k) * THREADS + threadIdx.x) * 16;
-                const unsigned mk = msk[k][threadIdx.x];
-                for (unsigned b = mk; b != 0u; b &= b - 1u) {
-                    const float v = s[i + __ffs(b) - 1];
-                    nf += !isfinite(v);
-                    if (r < cap) pos_out[r] = v;
-                    ++r;
-                    if constexpr (HIST) atomicAdd(&hs[key_fast(v) >> kCiLowBits], 1u);
-                }
-            }
-        }
-    } else {
-        if (threadIdx.x == 0) {
-            int other = 0;
-#pragma unroll
-            for (int w = 0; w < kW; ++w) other += wtot[1][w];
-            if (other) atomicAdd(stats + 3, static_cast<unsigned long long>(other));
-            base_s = tile ? atomicAdd(stats + 0, static_cast<unsigned long long>(tile)) : 0ull;
-        }
-        __syncthreads();
-        if (tile == 0) return;
-        int64_t r = int64_t(base_s) + before + incl - np;
-#pragma unroll 1
-        for (int k = 0; k < SLOTS; ++k) {
-            const int64_t i = base + (int64_t(k) * THREADS + threadIdx.x) * 16;
-            const unsigned mk = msk[k][threadIdx.x];  // this thread's own word: no barrier needed
-            for (unsigned b = mk; b != 0u; b &= b - 1u) {
-                const float v = s[i + __ffs(b) - 1];
-                nf += !isfinite(v);
-                if (r < cap) pos_out[r] = v;  // past `cap`: counted in stats[0], not stored (the caller's overflow)
-                ++r;
-                if constexpr (HIST) atomicAdd(&hs[key_fast(v) >> kCiLowBits], 1u);
-            }
+    for (int k = 0; k < SLOTS; ++k) {
+        const int64_t i = base + (int64_t(k) * THREADS + threadIdx.x) * 16;
+        const unsigned mk = msk[k][threadIdx.x];  // this thread's own word: no barrier needed
+        for (unsigned b = mk; b != 0u; b &= b - 1u) {
+            const float v = s[i + __ffs(b) - 1];
+            nf += !isfinite(v);
+            if (r < cap) pos_out[r] = v;  // past `cap`: counted in stats[0], not stored (the caller's overflow)
+            ++r;
+            if constexpr (HIST) atomicAdd(&hs[key_fast(v) >> kCiLowBits], 1u);
         }
     }
     if (nf) atomicAdd(stats + 2, static_cast<unsigned long long>(nf));
@@ -969,11 +916,6 @@ int compact_positives_zeroing(const float* scores, const void* labels, int label
             return DAUC_EINVAL;
     }
 }
-#ifdef DAUC_TUNING
-int g_compact_wide_log2 = 25;  // dauc_set_compact_wide (tuning builds)
-int g_compact_slots = kCmpSlots;  // dauc_set_compact_slots: the narrow tiles' label groups per thread
-int g_compact_stage = 0;          // dauc_set_compact_stage: the staged-score variant
-#endif
 
 int compact_unordered(const float* scores, const void* labels, int label_dtype, int64_t n, float* pos_out,
                       unsigned long long* stats, unsigned long long tag, unsigned long long* zero_next,
@@ -982,20 +924,12 @@ int compact_unordered(const float* scores, const void* labels, int label_dtype, 
     if (n <= 0 || scores == nullptr || labels == nullptr || pos_out == nullptr || stats == nullptr ||
         zero_next == nullptr)
         return DAUC_EINVAL;
-#ifdef DAUC_TUNING
-    const bool wide = n >= (int64_t(1) << g_compact_wide_log2);
-#else
     const bool wide = n >= (int64_t(1) << 25);
-#endif
     // wide inputs: 1024-thread workgroups of 32 label groups per thread (524,288-label tiles: 256
     // reservations at 2^27 instead of 1024 on the one counter address) -- 256
     constexpr int kWideThreads = 256;
     const int threads = wide ? kWideThreads : kCmpThreads;
-#ifdef DAUC_TUNING
-    const int slots = wide ? 32 : g_compact_slots;
-#else
     const int slots = wide ? 32 : kCmpSlots;
-#endif
     const int64_t tile = int64_t(threads) * 16 * slots;
     const int64_t nblk = (n + tile - 1) / tile;
     if (nblk > 0x7fffffffLL) return DAUC_EINVAL;
@@ -1003,44 +937,12 @@ int compact_unordered(const float* scores, const void* labels, int label_dtype, 
     const dim3 grid(static_cast<unsigned>(nblk)), block(threads);
     auto go = [&](auto* lab) {
         using LT = std::remove_const_t<std::remove_pointer_t<decltype(lab)>>;
-#ifdef DAUC_TUNING
-        if (g_compact_stage && slots == (wide ? 32 : kCmpSlots)) {
-            auto staged = [&](auto sl, auto hist) {
-                constexpr int S = decltype(sl)::value;
-                constexpr bool H = decltype(hist)::value;
-                hipLaunchKernelGGL((compact_unordered_kernel<LT, S, 256, H, true>), grid, block, 0, st, scores, lab, n,
-                                   vec, pos_out, stats, tag, zero_next, next_tag, zero3, zero_w, nzero_w, cap, hist_out);
-            };
-            static_assert(kCmpThreads == 256, "the staged variants take 256-thread workgroups");
-            if (wide && hist_out != nullptr) staged(std::integral_constant<int, 32>{}, std::true_type{});
-            else if (wide) staged(std::integral_constant<int, 32>{}, std::false_type{});
-            else if (hist_out != nullptr) staged(std::integral_constant<int, kCmpSlots>{}, std::true_type{});
-            else staged(std::integral_constant<int, kCmpSlots>{}, std::false_type{});
-            return launch_status();
-        }
-#endif
         if (wide && hist_out != nullptr)
             hipLaunchKernelGGL((compact_unordered_kernel<LT, 32, kWideThreads, true>), grid, block, 0, st, scores, lab,
                                n, vec, pos_out, stats, tag, zero_next, next_tag, zero3, zero_w, nzero_w, cap, hist_out);
         else if (wide)
             hipLaunchKernelGGL((compact_unordered_kernel<LT, 32, kWideThreads>), grid, block, 0, st, scores, lab, n, vec,
                                pos_out, stats, tag, zero_next, next_tag, zero3, zero_w, nzero_w, cap, hist_out);
-#ifdef DAUC_TUNING
-        else if (slots != kCmpSlots) {
-            auto narrow = [&](auto sl) {
-                constexpr int S = decltype(sl)::value;
-                if (hist_out != nullptr)
-                    hipLaunchKernelGGL((compact_unordered_kernel<LT, S, kCmpThreads, true>), grid, block, 0, st, scores,
-                                       lab, n, vec, pos_out, stats, tag, zero_next, next_tag, zero3, zero_w, nzero_w,
-                                       cap, hist_out);
-                else
-                    hipLaunchKernelGGL((compact_unordered_kernel<LT, S>), grid, block, 0, st, scores, lab, n, vec,
-                                       pos_out, stats, tag, zero_next, next_tag, zero3, zero_w, nzero_w, cap, hist_out);
-            };
-            if (slots == 4) narrow(std::integral_constant<int, 4>{});
-            else narrow(std::integral_constant<int, 16>{});
-        }
-#endif
         else if (hist_out != nullptr)
             hipLaunchKernelGGL((compact_unordered_kernel<LT, kCmpSlots, kCmpThreads, true>), grid, block, 0, st, scores,
                                lab, n, vec, pos_out, stats, tag, zero_next, next_tag, zero3, zero_w, nzero_w, cap,
@@ -1060,26 +962,6 @@ int compact_unordered(const float* scores, const void* labels, int label_dtype, 
 }  // namespace dauc
 
 extern "C" {
-
-#ifdef DAUC_TUNING
-int dauc_set_compact_wide(int log2n) {
-    if (log2n < 10 || log2n > 40) return DAUC_EINVAL;
-    dauc::g_compact_wide_log2 = log2n;
-    return DAUC_OK;
-}
-
-int dauc_set_compact_slots(int slots) {
-    if (slots != 4 && slots != 8 && slots != 16) return DAUC_EINVAL;
-    dauc::g_compact_slots = slots;
-    return DAUC_OK;
-}
-
-int dauc_set_compact_stage(int on) {
-    if (on != 0 && on != 1) return DAUC_EINVAL;
-    dauc::g_compact_stage = on;
-    return DAUC_OK;
-}
-#endif
 
 int dauc_compact_positives(const float* scores, const void* labels, int label_dtype, int64_t n,
                            float* pos_out, int64_t* stats, void* workspace, size_t workspace_bytes,

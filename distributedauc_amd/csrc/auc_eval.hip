@@ -53,10 +53,6 @@ struct EvalWs {
     void* sws;                    // split workspace
     void* tws;                    // sort + tree + count-index workspace (a table of at most n/2 keys)
     size_t sws_bytes, tws_bytes;
-#ifdef DAUC_TUNING
-    void* bws;                    // the range-slot path's (tuning_slots.hip): index, split queries, tile runs
-    size_t bws_bytes;
-#endif
 };
 
 EvalWs eval_ws(void* ws, int64_t n) {
@@ -78,22 +74,12 @@ EvalWs eval_ws(void* ws, int64_t n) {
     p += align256(w.sws_bytes);
     w.tws_bytes = dauc_sort_workspace_size(n / 2 + 1);
     w.tws = p;
-    p += align256(w.tws_bytes);
-#ifdef DAUC_TUNING
-    w.bws_bytes = slot_index_workspace_size(n);
-    w.bws = p;
-#endif
     return w;
 }
 
 size_t eval_ws_bytes(int64_t n) {
-    const size_t b = kHdr + align256(size_t(n) * 4) + align256(size_t(n / 2 + 1) * 4) +
-                     align256(dauc_split_workspace_size(n)) + align256(dauc_sort_workspace_size(n / 2 + 1));
-#ifdef DAUC_TUNING
-    return b + align256(slot_index_workspace_size(n));
-#else
-    return b;
-#endif
+    return kHdr + align256(size_t(n) * 4) + align256(size_t(n / 2 + 1) * 4) + align256(dauc_split_workspace_size(n)) +
+           align256(dauc_sort_workspace_size(n / 2 + 1));
 }
 
 bool valid_args(const float* scores, const void* labels, int label_dtype, int64_t n, int part, int parts,
@@ -138,11 +124,6 @@ int enqueue(const float* scores, const void* labels, int label_dtype, int64_t n,
         // a tuning build forcing another search structure: straight to the sorted path
         return -static_cast<int>(hipMemsetAsync(w.verdict, 2, 1, st));
     }
-#ifdef DAUC_TUNING
-    if (eval_query_path() == 2)
-        return counts_slotted(w.pos, w.slot, slot_index_capacity(n), scores, labels, label_dtype, qlo, qhi, w.wt,
-                              w.wt + 2, w.verdict, w.bws, w.bws_bytes, st);
-#endif
     return counts_labeled_direct(w.pos, w.slot, mcap, scores, labels, label_dtype, qlo, qhi, w.wt, w.wt + 2,
                                  w.verdict, w.tws, w.tws_bytes, st, w.hist);
 }
@@ -383,14 +364,8 @@ int dauc_auc_eval_query_part(const float* scores, const void* labels, int label_
     const int64_t qlo = n * part / parts, qhi = n * (part + 1) / parts;
     if (qhi > qlo) {
         // the build and the query see m_eff (w.spare[0]): P, or past the index's capacity on overflow
-#ifdef DAUC_TUNING
-        if (eval_query_path() == 2)
-            rc = counts_slotted(w.pos, w.spare, mcap, scores, labels, label_dtype, qlo, qhi, w.wt, w.wt + 2, w.verdict,
-                                w.bws, w.bws_bytes, st);
-        else
-#endif
-            rc = counts_labeled_direct(w.pos, w.spare, mcap, scores, labels, label_dtype, qlo, qhi, w.wt, w.wt + 2,
-                                       w.verdict, w.tws, w.tws_bytes, st, hist);
+        rc = counts_labeled_direct(w.pos, w.spare, mcap, scores, labels, label_dtype, qlo, qhi, w.wt, w.wt + 2,
+                                   w.verdict, w.tws, w.tws_bytes, st, hist);
         if (rc) return rc;
     }
     return DAUC_OK;

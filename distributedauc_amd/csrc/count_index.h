@@ -1,5 +1,5 @@
 // The count index of the positive table (auc_sort.hip builds it and counts the queries through
-// it; tuning_slots.hip reuses its cell map). gfx950 only.
+// it). gfx950 only.
 //
 // Keys: an fp32 score maps to a uint32 that orders like the float, with -0 and +0 on one key
 // (fp32 equality semantics). The table's keys are split into CELLS by arithmetic on the key:

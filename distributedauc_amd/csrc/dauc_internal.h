@@ -136,22 +136,6 @@ struct DirectIndex;  // count_index.h
 // fills *ix with the index's device pointers
 int build_direct_index(const float* pos, const unsigned long long* Mp, int64_t Mcap, void* workspace,
                        size_t workspace_bytes, hipStream_t st, DirectIndex* ix, const unsigned* ready_hist = nullptr);
-#ifdef DAUC_TUNING
-// tuning_slots.hip (tuning builds only): the labeled queries [begin, end) counted through the range-slot index built
-// straight from the unsorted positives pos[0 .. *Mp) (split + count passes); workspace of
-// slot_index_workspace_size(n) bytes, 256-B aligned, for Mcap = slot_index_capacity(n) positives.
-// *verdict (zero on entry) = 1 (counted) or 2 (the index cannot hold the table: the caller's sorted
-// path); nonfinite += the non-finite queried scores (also when the table is empty).
-int64_t slot_index_capacity(int64_t n);
-size_t slot_index_workspace_size(int64_t n);
-int counts_slotted(const float* pos, const unsigned long long* Mp, int64_t Mcap, const float* scores,
-                   const void* labels, int label_dtype, int64_t begin, int64_t end, unsigned long long* wins_ties,
-                   unsigned long long* nonfinite, unsigned* verdict, void* workspace, size_t workspace_bytes,
-                   hipStream_t st);
-// the evaluation's query path: 1 = the count index with per-query window gathers (auc_sort.hip),
-// 2 = the range-slot index (tuning_slots.hip); dauc_set_query_path
-int eval_query_path();
-#endif
 int counts_labeled_direct(const float* pos, const unsigned long long* Mp, int64_t Mcap, const float* scores,
                           const void* labels, int label_dtype, int64_t begin, int64_t end,
                           unsigned long long* wins_ties, unsigned long long* nonfinite, unsigned* verdict,

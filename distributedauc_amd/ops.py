@@ -579,32 +579,6 @@ def set_direct_fault(mode: int) -> None:
     check(_lib.tuning().dauc_set_direct_fault(int(mode)), "dauc_set_direct_fault")
 
 
-def set_query_path(path: int) -> None:
-    """The one-call evaluation's query path in the tuning build (dauc_set_query_path,
-    include/dauc_tuning.h): 1 the count index with per-query window gathers, 2 the range-slot
-    index. Tests and measurements only."""
-    check(_lib.tuning().dauc_set_query_path(int(path)), "dauc_set_query_path")
-
-
-def set_compact_wide(log2n: int) -> None:
-    """The compaction's tile-size threshold in the tuning build (dauc_set_compact_wide,
-    include/dauc_tuning.h): inputs of at least 2^log2n labels take the 131,072-label tiles.
-    Measurements only."""
-    check(_lib.tuning().dauc_set_compact_wide(int(log2n)), "dauc_set_compact_wide")
-
-
-def set_compact_slots(slots: int) -> None:
-    """The narrow compaction tiles' label groups per thread in the tuning build
-    (dauc_set_compact_slots, include/dauc_tuning.h): 4, 8 or 16. Measurements only."""
-    check(_lib.tuning().dauc_set_compact_slots(int(slots)), "dauc_set_compact_slots")
-
-
-def set_compact_stage(on: int) -> None:
-    """The compaction's staged-score variant in the tuning build (dauc_set_compact_stage,
-    include/dauc_tuning.h): 1 on, 0 off. Measurements only."""
-    check(_lib.tuning().dauc_set_compact_stage(int(on)), "dauc_set_compact_stage")
-
-
 def set_search_mode(mode: int) -> None:
     """Search structure of the sort method (dauc_set_search_mode): 0 automatic (the count index
     where the table fits it and is not skewed, else the LDS search tree), 1 the tree. Same
@@ -617,7 +591,7 @@ __all__ = [
     "pd_update_dense", "coda_finalize", "scale_div", "split_scores", "pair_count", "auc_counts_sorted",
     "surrogate_logits_fwdbwd", "class_sums_logits",
     "sort_keys", "auc_counts_sorted_labeled", "compact_positives", "mode_code", "workspaces", "set_search_mode",
-    "set_direct_fault", "set_query_path",
+    "set_direct_fault",
     "auc_eval_enqueue",
     "auc_slot_bytes",
     "auc_eval_compact_part",

@@ -69,36 +69,6 @@ int dauc_set_search_mode(int mode);
  */
 int dauc_set_direct_fault(int mode);
 
-/*
- * The one-call evaluation's query path in THIS library (process-wide, default 1): 1 = the count
- * index held in LDS whole, each query gathering its cell's keys from the L2-resident table
- * (auc_sort.hip, the product's); 2 = the range-slot index (tuning_slots.hip, measured slower): the
- * queries split by range of the table, each range counted from its 16-byte cell slots in LDS with
- * no gather. Same integers.
- */
-int dauc_set_query_path(int path);
-
-/*
- * The one-pass unordered compaction's tile size in THIS library (process-wide, default 25): inputs
- * of at least 2^log2n labels take 131,072-label tiles, smaller ones 32,768-label tiles (the tiles
- * reserve their output ranges with returning atomics on one address). Measurements only.
- */
-int dauc_set_compact_wide(int log2n);
-
-/*
- * The narrow compaction tiles' size in THIS library (process-wide, default 8): 4, 8 or 16 label
- * groups of 16 per thread (16,384-, 32,768- or 65,536-label tiles). Measurements only.
- */
-int dauc_set_compact_slots(int slots);
-
-/*
- * The one-pass compaction's staged-score variant in THIS library (process-wide, default 0): 1 =
- * a tile stages its positives' scores in LDS while its reservation atomic is in flight and copies
- * them out contiguously once the base is known (tiles of up to 4096 positives). Same output.
- * Measurements only.
- */
-int dauc_set_compact_stage(int on);
-
 #ifdef __cplusplus
 }
 #endif

@@ -1,6 +1,6 @@
 """A short exact-AUC run for profilers: `reps` one-call evaluations of 2^log2n synthetic scores
 (the bench's generator) after one warm call.
-    [DAUC_QUERY_PATH=1|2] python scripts/prof_eval.py [log2n] [pos] [reps]
+    python scripts/prof_eval.py [log2n] [pos] [reps]
 """
 from __future__ import annotations
 
@@ -10,14 +10,8 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
-from distributedauc_amd import _lib, ops  # noqa: E402
 from distributedauc_amd.auc import ExactAUC  # noqa: E402
 from distributedauc_amd.loader import synthetic_scores  # noqa: E402
-
-# DAUC_QUERY_PATH (tuning build): 1 the count index with window gathers, 2 the range-slot index
-if os.environ.get("DAUC_QUERY_PATH"):
-    _lib._lib = _lib.tuning()
-    ops.set_query_path(int(os.environ["DAUC_QUERY_PATH"]))
 
 log2n = int(sys.argv[1]) if len(sys.argv) > 1 else 27
 pos = float(sys.argv[2]) if len(sys.argv) > 2 else 0.001
