@@ -99,7 +99,10 @@ def parse(argv=None):
     p.add_argument("--sur-log2b", type=int, default=26, help="surrogate kernel leg: batch of 2^k scores")
     p.add_argument("--sur-reps", type=int, default=100)
     p.add_argument("--variant", type=int, default=0, help="pair-count kernel variant")
-    p.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL; gloo for rehearsals)")
+    p.add_argument("--backend", default=None,
+                   help="torch.distributed backend: nccl (= RCCL; the default at --gpus > 1) or gloo (shared-GPU "
+                        "rehearsals). Given at --gpus 1, a one-rank process group of that backend is started through "
+                        "torch.distributed.run and every collective of the N > 1 path runs on it (the RCCL rehearsal)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-workers", type=int, default=4, help="configs[0] CPU leg: gloo worker processes")
     p.add_argument("--cpu-steps", type=int, default=8, help="configs[0] CPU leg: timed steps (one round at I=8)")
@@ -183,8 +186,13 @@ class KernelTimer:
         return float(np.mean([a.elapsed_time(b) for a, b in self.pairs])) if self.pairs else float("nan")
 
 
+def grouped() -> bool:
+    """A process group is up: the N > 1 path (and its collectives) runs, at any world size."""
+    return dist.is_available() and dist.is_initialized()
+
+
 def max_over_ranks(x: float, world: int) -> float:
-    if world == 1:
+    if not grouped():
         return x
     t = torch.tensor([x], dtype=torch.float64, device="cuda")
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -194,7 +202,7 @@ def max_over_ranks(x: float, world: int) -> float:
 def timed_steps(coda, it, steps: int, world: int) -> float:
     """Exactly `steps` CoDA steps between barrier + synchronize on both sides; max over ranks (s)."""
     torch.cuda.synchronize()
-    if world > 1:
+    if grouped():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -202,7 +210,7 @@ def timed_steps(coda, it, steps: int, world: int) -> float:
         x, y = next(it)
         coda.train_step(x, y)
     torch.cuda.synchronize()
-    if world > 1:
+    if grouped():
         dist.barrier()
     torch.cuda.synchronize()
     return max_over_ranks(time.perf_counter() - t0, world)
@@ -223,7 +231,7 @@ def make_coda(arch, batch, image_size, I, pos_ratio, pool, world, rank, device, 
     net = build_backbone(arch, num_classes=2).to(device).to(memory_format=torch.channels_last)
     net.set_fused_bn(bool(fused_bn)).set_gemm_conv1x1(bool(gemm_conv1x1))
     coda = CoDA(net, lr=lr, gamma=2000.0, T0=10 ** 9, I=I, split_index=split, world=world, rank=rank,
-                autocast_dtype=torch.bfloat16, device=device)
+                autocast_dtype=torch.bfloat16, device=device, collective=grouped())
     it = iter(loader)
     coda.average_all()            # main.py:141-142
     coda.begin_stage(1, it)       # alpha estimate + anchors (untimed)
@@ -258,7 +266,7 @@ def bench_train(args, world, rank, device):
     }
     if args.sweep_I:
         out["period_sweep"] = bench_period_sweep(coda, it, args, world)
-    if world > 1:
+    if grouped():
         out["coda_round"] = bench_coda_round(coda, world)
     if args.eval_images > 0:
         out["training_eval"] = bench_training_eval(coda, args, world, rank, device)
@@ -309,11 +317,11 @@ def bench_training_eval(coda, args, world, rank, device, reps=3):
     batches = [next(it) for _ in range((n + tb - 1) // tb)]
 
     def timed(split):
-        ev = Evaluator(batches, n, 499, device, None, world, rank, None, split=split)
+        ev = Evaluator(batches, n, 499, device, None, world, rank, None, split=split, collective=grouped())
         ev(coda)  # warm (workspaces, MIOpen eval-mode kernels)
         ts, aucs = [], []
         for _ in range(reps):
-            if world > 1:
+            if grouped():
                 dist.barrier()
             torch.cuda.synchronize()
             t0 = time.perf_counter()
@@ -326,10 +334,10 @@ def bench_training_eval(coda, args, world, rank, device, reps=3):
     rec = {"workload": f"{n} test images {args.image_size}^2 scored by {args.arch} (eval mode, bf16 autocast), "
                        f"test batch {tb}, then the exact AUC; {world} rank(s)",
            "ms": ms_split * 1e3, "imgs_per_sec": n / ms_split, "auc": aucs[-1], "auc_reps": aucs,
-           "method": "split" if world > 1 else "one rank",
+           "method": "split" if grouped() else "one rank",
            "auc_note": "AUCs are reported, not asserted equal: MIOpen's fast solvers change low bits between "
                        "scorings (bit-identity needs --deterministic_eval, tested in tests/test_main_gpu.py)"}
-    if world > 1:
+    if grouped():
         ms0, aucs0 = timed(False)
         rec.update({"ms_rank0_scoring": ms0 * 1e3, "speedup_vs_rank0_scoring": ms0 / ms_split,
                     "auc_rank0_scoring": aucs0[-1],
@@ -356,11 +364,17 @@ def bench_coda_round(coda, world, reps=5):
     e1.synchronize()
     ms = max_over_ranks(e0.elapsed_time(e1) / reps, world)
     bus = 2 * (world - 1) / world * nbytes / (ms / 1e3) / 1e9
-    return {"workload": f"all-reduce of {nbytes} B (params + a, b, alpha + class counts) + finalise, {world} ranks",
-            "ms_per_round": ms, "payload_bytes": nbytes, "rounds_per_step": 1.0 / coda.I,
-            "backend": dist.get_backend(),
-            "roofline": {"bound": "xgmi", "achieved": bus, "peak": XGMI_PEAK_GBS, "unit": "GB/s (bus)",
-                         "frac": bus / XGMI_PEAK_GBS}}
+    rec = {"workload": f"all-reduce of {nbytes} B (params + a, b, alpha + class counts) + finalise, {world} ranks",
+           "ms_per_round": ms, "payload_bytes": nbytes, "rounds_per_step": 1.0 / coda.I,
+           "backend": dist.get_backend(),
+           "roofline": {"bound": "xgmi", "achieved": bus, "peak": XGMI_PEAK_GBS, "unit": "GB/s (bus)",
+                        "frac": bus / XGMI_PEAK_GBS}}
+    if world == 1:
+        # the one-rank rehearsal: no bus traffic (the collective is a local copy), so no xGMI figure
+        rec["roofline"] = None
+        rec["note"] = ("one-rank process group (RCCL rehearsal): the all-reduce moves no bytes over xGMI; "
+                       "this times the collective's launch + local copy and the finalise launch")
+    return rec
 
 
 def bench_r18(args, world, rank, device):
@@ -402,16 +416,17 @@ def bench_auc(args, world, rank, device, log2n=None, pos=None, pair_reps=None):
     # (dauc_auc_eval_compact_part), one all-gather of the slots, each counts its query range
     # (dauc_auc_eval_query_part, timed here), one all-gather of the records and one host read
     shard_min = ExactAUC.SHARD_MIN if args.auc_shard_min is None else args.auc_shard_min
-    sort_fn = "dauc_auc_eval_counts" if world == 1 or n < shard_min else "dauc_auc_eval_query_part"
+    sort_fn = "dauc_auc_eval_counts" if not grouped() or n < shard_min else "dauc_auc_eval_query_part"
     for method, fn in (("sort", sort_fn), ("pairs", "dauc_pair_count")):
-        ev = ExactAUC(world=world, rank=rank, variant=args.variant, method=method, shard_min=shard_min)
+        ev = ExactAUC(world=world, rank=rank, variant=args.variant, method=method, shard_min=shard_min,
+                      collective=grouped())
         kt = KernelTimer(_lib.load(), fn)
         cold = None
         if method == "sort":
             # the first call ever on this device and stream: the evaluator's workspace and the
             # page-locked readback words are allocated inside it
             torch.cuda.synchronize()
-            if world > 1:
+            if grouped():
                 dist.barrier()
             t0 = time.perf_counter()
             ev.counts(y, s)
@@ -424,7 +439,7 @@ def bench_auc(args, world, rank, device, log2n=None, pos=None, pair_reps=None):
         times = []
         for _ in range(reps):
             torch.cuda.synchronize()
-            if world > 1:
+            if grouped():
                 dist.barrier()
             t0 = time.perf_counter()
             c = ev.counts(y, s)
@@ -432,7 +447,7 @@ def bench_auc(args, world, rank, device, log2n=None, pos=None, pair_reps=None):
             times.append(time.perf_counter() - t0)
         kt.enabled = True
         for _ in range(reps):
-            if world > 1:
+            if grouped():
                 dist.barrier()
             ev.counts(y, s)
         kt.enabled = False
@@ -449,7 +464,7 @@ def bench_auc(args, world, rank, device, log2n=None, pos=None, pair_reps=None):
             alt = []
             for k in range(reps):
                 torch.cuda.synchronize()
-                if world > 1:
+                if grouped():
                     dist.barrier()
                 t0 = time.perf_counter()
                 ev.counts(y2, s2) if k % 2 == 0 else ev.counts(y, s)
@@ -795,13 +810,13 @@ def cpu_baseline_auc(auc_res, max_log2n=None, oracle_check=False):
 def self_launch(args) -> int | None:
     """--gpus N without a launcher: start N ranks as a torch.distributed.run child process (this
     process has not touched the GPU) and return its exit code."""
-    if args.cpu_coda_worker or "WORLD_SIZE" in os.environ or args.gpus <= 1:
+    if args.cpu_coda_worker or "WORLD_SIZE" in os.environ or (args.gpus <= 1 and args.backend is None):
         return None
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
            "--master-addr=127.0.0.1", f"--master-port={free_port()}", str(Path(__file__).resolve()), *sys.argv[1:]]
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-    log(f"launching {args.gpus} ranks: {' '.join(cmd[1:5])} ...")
+    log(f"launching {args.gpus} rank(s): {' '.join(cmd[1:5])} ...")
     return subprocess.call(cmd, env=env)
 
 
@@ -826,18 +841,22 @@ def main():
         print(f"error: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks", file=sys.stderr)
         sys.exit(2)
     ndev = torch.cuda.device_count()
-    if args.backend == "nccl" and world > 1 and ndev < local_world:
+    backend = args.backend or "nccl"
+    use_group = world > 1 or args.backend is not None
+    if backend == "nccl" and world > 1 and ndev < local_world:
         print(f"error: the nccl (RCCL) backend needs one GPU per rank: {local_world} ranks on this node, "
               f"{ndev} GPU(s) visible (use --backend gloo for a shared-GPU rehearsal)", file=sys.stderr)
         sys.exit(3)
     device = torch.device("cuda", local % max(ndev, 1))  # ranks share a device only in gloo rehearsals
     torch.cuda.set_device(device)
     quiet = None
-    if world > 1:
-        if args.backend == "nccl":
+    if use_group:
+        if "MASTER_ADDR" not in os.environ:  # a --backend run at --gpus 1 outside a launcher
+            os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()), RANK="0", WORLD_SIZE="1")
+        if backend == "nccl":
             dist.init_process_group("nccl", device_id=device)
         else:
-            dist.init_process_group(args.backend)
+            dist.init_process_group(backend)
         if dist.get_world_size() != args.gpus:
             print(f"error: process group has {dist.get_world_size()} ranks, --gpus {args.gpus}", file=sys.stderr)
             sys.exit(2)
@@ -882,8 +901,8 @@ def main():
                 out["coda_round"] = res["coda_round"]
             if "training_eval" in res:
                 out["training_eval"] = res["training_eval"]
-        out["process_group"] = {"world_size": dist.get_world_size() if world > 1 else 1,
-                                "backend": dist.get_backend() if world > 1 else None,
+        out["process_group"] = {"world_size": dist.get_world_size() if grouped() else 1,
+                                "backend": dist.get_backend() if grouped() else None,
                                 "rccl_version": ".".join(map(str, torch.cuda.nccl.version()))
                                 if torch.cuda.is_available() and hasattr(torch.cuda, "nccl") else None,
                                 "devices_visible": torch.cuda.device_count()}
@@ -916,7 +935,7 @@ def main():
             out["cpu_baseline"] = None
         sys.stdout.flush()
         os.write(json_fd, (json.dumps(_finite(out)) + "\n").encode())
-    if world > 1:
+    if grouped():
         dist.barrier(group=quiet)
         dist.destroy_process_group()
 

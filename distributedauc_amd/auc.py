@@ -9,20 +9,24 @@ float is within a few ulp of sklearn's trapezoid sum.
 
 Two exact methods give the same integers: ``method="pairs"`` runs the LDS-tiled
 pair-count kernel (O(P*N), the north-star kernel) and ``method="sort"`` (default)
-radix-sorts the smaller class and locates every score of the larger class in it
-through an LDS search tree (O(M log M + L log M)).
+compacts the positives, builds an LDS count index straight from them (cells of the
+score's order-preserving key, no sort) and locates every other score in it
+(O(n + P)); tables the index cannot hold (clustered or more than
+219,838 positives) take a radix sort + LDS search tree instead.
 
 Sharding (north star): every rank holds the same score vector. The
 pair-count method gives rank r the positives [r*P/G, (r+1)*P/G) of the stable
-split against ALL negatives, then one int64 [3] all-reduce sums (W, T, non-finite);
-the sort method has every rank compact the positives of its slice of the labels
-into a slot, all-gathers the slots (every rank then holds the whole positive
-table), builds the count index from them, counts its index slice of the scores,
-and all-gathers the parts' 8-word records (two collectives, one host read, no host
-synchronisation before the read). The result does not depend on G. The gathered
-records' label counts (P, non-finite positives, labels outside {-1, 1}) and
-verdicts must agree, and a mismatch raises on every rank together; the scores
-themselves are not compared across ranks.
+split against ALL negatives, then one all-gather of every rank's 6-word record
+(W, T, P, N, non-finite, other): the split's figures must agree. The sort method has
+every rank compact the positives of its slice of the labels into a slot,
+all-gathers the slots (every rank then holds the whole positive table), builds the
+count index from them, counts the next rank's slice of the scores, and all-gathers
+the parts' 8-word records (two collectives, one host read, no host synchronisation
+before the read); each record carries a check of the queried slice's labels and
+positive scores against the slot the next rank compacted from it, and of the
+length every slot was built for. The result does not depend on G. A mismatch raises
+RuntimeError on every rank together, after the collective; the negatives' scores are
+not compared across ranks.
 
 Error behaviour mirrors sklearn: non-finite scores raise ValueError; labels
 with more than two distinct values raise ValueError; a single class returns NaN
@@ -67,18 +71,21 @@ class ExactAUC:
     """Exact AUC evaluator; sharded over a process group when world > 1."""
 
     # Below this many scores the sort method does not shard: every rank evaluates the whole vector
-    # (same integers, no collective). Sharding saves (G-1)/G of the query pass (~7 ns per score on
-    # one GPU: 113 us at 2^24) and costs one int64 [3] all-reduce and its readback; every rank
-    # still compacts and sorts all the positives (~90 us at 2^24), so it pays from ~2^24 scores.
+    # (same integers, no collective). Sharding saves (G-1)/G of the compaction and of the query pass
+    # (0.15 ms on one GPU at 2^24) but every rank still builds the count index from all the gathered
+    # positives (~30 us) and pays two all-gathers and their launches, so it pays from ~2^24 scores.
     SHARD_MIN = 1 << 24
 
     def __init__(self, group=None, world: int = 1, rank: int = 0, variant: int = 0, reduce: bool = True,
-                 method: str = "sort", shard_min: int | None = None):
+                 method: str = "sort", shard_min: int | None = None, collective: bool | None = None):
         if method not in ("sort", "pairs"):
             raise ValueError("method must be 'sort' (radix sort + search) or 'pairs' (pair-count kernel)")
         self.group = group
         self.world = world
         self.rank = rank
+        # collective: take the sharded path with its collectives (default: world > 1). True at world
+        # 1 is the RCCL rehearsal: the world > 1 code path on a one-rank process group
+        self.collective = world > 1 if collective is None else bool(collective)
         self.variant = variant
         self.reduce = reduce  # False: return only this rank's share (no collective)
         self.method = method
@@ -101,7 +108,7 @@ class ExactAUC:
             raise ValueError(f"Found input variables with inconsistent numbers of samples: {[y.numel(), s.numel()]}")
         if self.method == "sort":
             return self._counts_sort(y, s)
-        self.last_mode = "sharded" if self.world > 1 else "single"
+        self.last_mode = "sharded" if self.collective else "single"
         # the pair-count method: a stable split, so every rank sees the positives in the same order
         # and positive blocks shard
         pos, neg, stats = ops.split_scores(s, y)
@@ -111,7 +118,7 @@ class ExactAUC:
             lo, hi = self.rank * P // self.world, (self.rank + 1) * P // self.world
             if hi > lo:
                 ops.pair_count(pos[lo:hi], neg[:N], wt, variant=self.variant)
-        if self.world > 1 and self.reduce:
+        if self.collective and self.reduce:
             # one all-gather of every rank's (W, T, P, N, non-finite, other): the split's figures
             # must agree (ranks holding different test sets raise together), and no rank raises
             # before the collective, so a bad input cannot leave the others waiting in it
@@ -140,13 +147,18 @@ class ExactAUC:
         whole: same integers, no collective): ONE blocking C call (dauc_auc_eval_counts). Over
         ranks: every rank compacts its slice of the labels into a slot (dauc_auc_eval_compact_part),
         one all-gather of the slots, every rank builds the index from the gathered positives and
-        counts its index slice of the scores (dauc_auc_eval_query_part), one all-gather of the
-        parts' 8-word records, and ONE host read of the gathered records: the counts are summed
-        on the host, and the label counts and the verdict must agree on every rank (ranks whose
-        label counts differ raise together instead of mixing counts; the scores are not compared).
-        With reduce=False each rank evaluates its part against all the positives itself."""
-        if self.world == 1 or (self.reduce and s.numel() < self.shard_min):
-            self.last_mode = "single" if self.world == 1 else "replicated"
+        counts the NEXT rank's slice of the scores (dauc_auc_eval_query_part), one all-gather of the
+        parts' 8-word records, and ONE host read of the gathered records. P and the label counts
+        come from the gathered slots, so they are the same on every rank by construction; what the
+        ranks could disagree on is checked through record word 4 instead: every rank's query pass
+        compares its own labels (and its positives' scores, by a key sum) over the next rank's slice
+        with the slot that rank compacted from it, and every gather compares the length each slot
+        was built for. A mismatch raises RuntimeError on every rank together, after the collective
+        (the slot size does not depend on n, so differing lengths cannot desynchronise the gather).
+        The negatives' scores are not compared across ranks. With reduce=False each rank evaluates
+        its part against all the positives itself (no collective, no check)."""
+        if not self.collective or (self.reduce and s.numel() < self.shard_min):
+            self.last_mode = "single" if not self.collective else "replicated"
             W, T, P, N, nonfinite, other = ops.auc_eval_counts(s, y)
             if nonfinite:
                 raise ValueError("Input y_score contains NaN or infinity.")
@@ -173,19 +185,23 @@ class ExactAUC:
             ops.auc_eval_query_part(s, y, self.rank, self.world, slots[1][: nb * self.world], out=mine)
             dist.all_gather_into_tensor(gathered, mine, group=self.group)
             vals = gathered.view(self.world, 8).tolist()  # the one host synchronisation
-        shared = {(v[3], v[5], v[6]) for v in vals}
+            check = [v[4] & 0xFFFFFFFFFFFFFFFF for v in vals]
+            if any(c >> 32 for c in check):
+                raise RuntimeError("ExactAUC: the ranks passed test sets of different lengths: every rank must "
+                                   "pass the same scores and labels")
+            if any(c & 0xFFFFFFFF for c in check):
+                raise RuntimeError("ExactAUC: the ranks' parts disagree on the test set (labels or positive scores "
+                                   "of a slice differ between the rank that compacted it and the rank that queried "
+                                   "it): every rank must pass the same scores and labels")
+        P, nonfinite, other = vals[0][3], vals[0][5], vals[0][6]
         verdicts = {v[7] for v in vals} - {0}
-        if len(shared) != 1 or len(verdicts) > 1:
-            raise RuntimeError("ExactAUC: the ranks' parts disagree on the test set (positives, non-finite or "
-                               "label counts): every rank must pass the same scores and labels")
-        P, nonfinite, other = shared.pop()
         N = n - P
         if nonfinite or sum(v[2] for v in vals):
             raise ValueError("Input y_score contains NaN or infinity.")
         self._check_labels(other, y)
         if P == 0 or N == 0:
             return {"wins": 0, "ties": 0, "P": P, "N": N}
-        if verdicts == {2}:
+        if 2 in verdicts:
             return self._counts_sort_sorted_path(y, s)
         return {"wins": sum(v[0] for v in vals), "ties": sum(v[1] for v in vals), "P": P, "N": N}
 
@@ -203,13 +219,20 @@ class ExactAUC:
 
     def _counts_sort_sorted_path(self, y: torch.Tensor, s: torch.Tensor) -> dict:
         """A table the count index cannot hold (more than 219,838 positives, or clustered ones):
-        every rank runs the blocking part (the sorted path) and one int64 [3] all-reduce sums the
-        parts' counts. Every rank reached here with the same verdict, so all take this branch."""
-        wt = torch.zeros(3, dtype=torch.int64, device=s.device)
+        every rank runs the blocking part (the sorted path, its own whole compaction) and one
+        all-gather of the parts' (W, T, #non-finite queried, P) sums the counts; the parts' P must
+        agree. Every rank reached here with the same verdicts, so all take this branch."""
+        wt = torch.zeros(4, dtype=torch.int64, device=s.device)
         W, T, P, N, nonfinite, other, qbad = ops.auc_eval_counts_part(s, y, self.rank, self.world, wt)
         if self.reduce:
-            dist.all_reduce(wt, op=dist.ReduceOp.SUM, group=self.group)
-            W, T, qbad = (int(v) for v in wt.tolist())
+            wt[3] = P
+            got = torch.empty(4 * self.world, dtype=torch.int64, device=s.device)
+            dist.all_gather_into_tensor(got, wt, group=self.group)
+            vals = got.view(self.world, 4).tolist()
+            if len({v[3] for v in vals}) != 1:
+                raise RuntimeError("ExactAUC: the ranks' parts disagree on the test set (positives): every rank "
+                                   "must pass the same scores and labels")
+            W, T, qbad = sum(v[0] for v in vals), sum(v[1] for v in vals), sum(v[2] for v in vals)
         if qbad:
             raise ValueError("Input y_score contains NaN or infinity.")
         return {"wins": W, "ties": T, "P": P, "N": N}

@@ -37,7 +37,7 @@ class CoDA:
     def __init__(self, model: nn.Module, *, lr: float = 0.1, gamma: float = 2000.0, T0: int = 5000,
                  I: int = 2, split_index: int = 4, mode: str = "reference", world: int = 1, rank: int = 0,
                  group=None, autocast_dtype: torch.dtype | None = None, device=None,
-                 max_exact_count: int = 1 << 24, head: str = "softmax"):
+                 max_exact_count: int = 1 << 24, head: str = "softmax", collective: bool | None = None):
         if I < 1:
             raise ValueError("averaging period I must be >= 1")
         ops.mode_code(mode)  # validates
@@ -56,6 +56,11 @@ class CoDA:
         self.world = int(world)
         self.rank = int(rank)
         self.group = group
+        # collective: issue the averaging and alpha all-reduces (default: world > 1). True at world
+        # 1 is the RCCL rehearsal: the world > 1 code path on a one-rank process group
+        self.collective = self.world > 1 if collective is None else bool(collective)
+        if collective and not (dist.is_available() and dist.is_initialized()):
+            raise RuntimeError("CoDA(collective=True) needs an initialised torch.distributed process group")
         self.autocast_dtype = autocast_dtype
         self.max_exact_count = max_exact_count
         self.t_total = 0
@@ -95,7 +100,7 @@ class CoDA:
     def average_all(self):
         """One CoDA round: main.py:40-54 (world > 1) / 297-299 (world == 1), then 300-301."""
         st = self.state
-        if self.world > 1:
+        if self.collective:
             dist.all_reduce(st.flat[: st.n_reduce], op=dist.ReduceOp.SUM, group=self.group)
         ops.coda_finalize(st.flat, st.n_avg, self.world, st.lcounts, st.gcounts)
 
@@ -120,7 +125,7 @@ class CoDA:
                 else:
                     ops.class_sums(self.scores(x), y8, self._sums4, accumulate=True)
             self.model.train()
-            if self.world > 1:
+            if self.collective:
                 dist.all_reduce(self._sums4, op=dist.ReduceOp.SUM, group=self.group)  # main.py:192-195
             ops.alpha_from_sums(self._sums4, st.alpha)  # main.py:197
             st.snapshot_anchor()                        # main.py:154 + 199-201
@@ -308,5 +313,6 @@ class CoDA:
     def __repr__(self):
         n = self.state.numel()
         return (f"CoDA(params={n}, I={self.I}, T0={self.T0}, lr0={self.lr0}, gamma={self.gamma}, "
-                f"mode={self.mode}, world={self.world}, rank={self.rank}, flat_MB={4 * n / 2**20:.1f})")
+                f"mode={self.mode}, world={self.world}, rank={self.rank}, collective={self.collective}, "
+                f"flat_MB={4 * n / 2**20:.1f})")
 

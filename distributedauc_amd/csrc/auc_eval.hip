@@ -2,8 +2,9 @@
 //
 // Reference: imagenet/main.py:79-81, AUC(label, scores) = sklearn roc_curve(pos_label=1) + auc,
 // evaluated by rank 0 over the test set (main.py:237-250). The evaluation is:
-//   1. one memset of the 64-byte record (the compaction's counters, the query counts, the
-//      verdict word) and the top-bucket histogram;
+//   1. memsets of the 64-byte record (the compaction's counters, the query counts, the verdict
+//      word) and the top-bucket histogram: one when the record is the workspace header (the
+//      blocking forms), two when it is the caller's part_out (the enqueued form);
 //   2. the one-pass positive compaction: labels read once, the positives' scores gathered (in no
 //      particular order), P counted on the device, their top-bucket histogram built;
 //   3. the count index built straight from the unsorted positives, sized by the device's P
@@ -88,6 +89,12 @@ bool valid_args(const float* scores, const void* labels, int label_dtype, int64_
            workspace_bytes >= eval_ws_bytes(n) && (reinterpret_cast<uintptr_t>(workspace) & 255u) == 0 &&
            parts >= 1 && part >= 0 && part < parts &&
            (label_dtype == DAUC_LABEL_I8 || label_dtype == DAUC_LABEL_I32 || label_dtype == DAUC_LABEL_I64);
+}
+
+// [a, a + an) and [b, b + bn) overlap (byte ranges)
+bool overlaps(const void* a, size_t an, const void* b, size_t bn) {
+    const uintptr_t x = reinterpret_cast<uintptr_t>(a), y = reinterpret_cast<uintptr_t>(b);
+    return x < y + bn && y < x + an;
 }
 
 // The record words of `w` moved to the caller's part_out (int64[8], 8-byte aligned): the
@@ -204,25 +211,29 @@ int counts_part_blocking(const float* scores, const void* labels, int label_dtyp
 // ---- the sharded evaluation in two steps: each rank compacts only its slice -----------------
 //
 // Step 1 (dauc_auc_eval_compact_part): rank r compacts the positives of ITS slice of the labels
-// into a slot: a 256-byte header {P_r, 0, #non-finite positives, #labels outside {-1, 1}} (u64), the
-// top-bucket histogram of its positives' keys (count_index.h, 2048 u32) and room for `cap` scores.
-// The caller all-gathers the slots (one collective). Step 2 (dauc_auc_eval_query_part): the
-// gathered slots are concatenated into the evaluation's positive table on the device (their
-// headers and histograms summed), the count index is built from it -- without its histogram pass
-// -- and the rank's query range is counted; the record is dauc_auc_eval_enqueue's. A slot holds an even share of
-// the index's capacity plus 25 %: a rank whose slice holds more positives (unshuffled test sets)
-// overflows, and the evaluation reports verdict 2 (the caller's blocking sorted path), as it does
-// for tables the index cannot hold.
+// into a slot: a 256-byte header {P_r, 0, #non-finite positives, #labels outside {-1, 1}, n, the
+// positives' keys summed mod 2^32} (u64 words), the top-bucket histogram of its positives' keys
+// (count_index.h, 2048 u32) and room for `cap` scores. The caller all-gathers the slots (one
+// collective). Step 2 (dauc_auc_eval_query_part): the gathered slots are concatenated into the
+// evaluation's positive table on the device (their headers and histograms summed), the count index
+// is built from it -- without its histogram pass -- and the scores of the NEXT rank's slice are
+// counted (rank r queries slice (r + 1) % parts): the record is dauc_auc_eval_enqueue's, with word 4
+// a consistency check -- this rank's labels over that slice against the slot the next rank
+// compacted from it (low 32 bits: (P + key sum) of that slot - (positives + their key sum) seen by
+// this rank's query pass, mod 2^32; high 32 bits: the number of slots built for another n). A slot
+// holds an even share of the index's capacity plus 25 %, whatever n (so ranks called with different
+// n still gather equal sizes and report the mismatch instead of hanging in the collective): a rank
+// whose slice holds more positives (unshuffled test sets) overflows, and the evaluation reports
+// verdict 2 (the caller's blocking sorted path), as it does for tables the index cannot hold.
 constexpr size_t kSlotHist = 256, kSlotHdr = kSlotHist + size_t(kCiTop) * 4;
+constexpr int kSlotN = 4, kSlotKeySum = 5;  // header words
 
-int64_t slot_cap(int64_t n, int parts) {
-    const int64_t share = (n + parts - 1) / parts;
-    const int64_t fair = (direct_capacity(n) + parts - 1) / parts;
-    const int64_t c = fair + fair / 4 + 64;
-    return share < c ? share : c;
+int64_t slot_cap(int parts) {
+    const int64_t fair = (direct_capacity(INT64_MAX / 4) + parts - 1) / parts;
+    return fair + fair / 4 + 64;
 }
 
-size_t slot_bytes(int64_t n, int parts) { return kSlotHdr + align256(size_t(slot_cap(n, parts)) * 4); }
+size_t slot_bytes(int parts) { return kSlotHdr + align256(size_t(slot_cap(parts)) * 4); }
 
 // the slice of the labels rank `part` compacts: boundaries on 256-label multiples (int8 label
 // loads stay 16-byte aligned for every slice of an aligned array)
@@ -230,16 +241,26 @@ int64_t slice_lo(int64_t n, int part, int parts) {
     return part == 0 ? 0 : part >= parts ? n : ((n * part / parts) & ~int64_t(255));
 }
 
+// the slice queried by part `part`: the next part's slice (the consistency check of the record)
+int64_t query_lo(int64_t n, int part, int parts) { return slice_lo(n, (part + 1) % parts, parts); }
+int64_t query_hi(int64_t n, int part, int parts) {
+    const int q = (part + 1) % parts;
+    return slice_lo(n, q + 1, parts);
+}
+
 // kGatherBlocks workgroups per slot (blockIdx.y = the slot): the slot's scores to table[sum of the
 // earlier slots' P, ...) (one workgroup per slot copied a 2-rank slot of 67 k scores in ~60 us);
-// workgroup (0, 0) sums the headers into the evaluation's counters and zeroes the query's counts
-// and the verdict (no memset launch); the first workgroups sum the slots' histograms into the
-// build's `hist`, and all of them zero its per-cell counters (the histogram pass's other job).
-// m_eff = P, or (any slot overflowed) a size the index refuses, so the build reports verdict 2 (the
-// histogram's bucket 0 gets that size added: its total is the build's M).
+// workgroup (0, 0) sums the headers into the evaluation's counters, zeroes the query's counts and
+// the verdict (no memset launch) and sets the record's check word (the queried slot's P + key sum
+// - the slice length, which the query pass brings back to zero; the slots built for another n in
+// its high half); the first workgroups sum the slots' histograms into the build's `hist`, and all
+// of them zero its per-cell counters (the histogram pass's other job). m_eff = P, or (any slot
+// overflowed) a size the index refuses, so the build reports verdict 2 (the histogram's bucket 0
+// gets that size added: its total is the build's M).
 constexpr int kGatherBlocks = 32;
 __global__ __launch_bounds__(256) void gather_slots_kernel(const unsigned char* __restrict__ slots, size_t sbytes,
-                                                           int parts, int64_t cap, int64_t mcap,
+                                                           int parts, int part, int64_t n, int64_t qlen,
+                                                           int64_t cap, int64_t mcap,
                                                            float* __restrict__ table,
                                                            unsigned long long* __restrict__ stats,
                                                            unsigned long long* __restrict__ m_eff,
@@ -254,6 +275,18 @@ __global__ __launch_bounds__(256) void gather_slots_kernel(const unsigned char* 
     if (first) {
         if (threadIdx.x < 3) wt[threadIdx.x] = 0ull;
         if (threadIdx.x == 0) *reinterpret_cast<unsigned long long*>(verdict) = 0ull;  // record word 7
+    }
+    auto hdr0 = [&](int r) { return reinterpret_cast<const unsigned long long*>(slots + size_t(r) * sbytes); };
+    if (first && threadIdx.x == 64) {
+        // record word 4 (stats + 1): low half = the queried slot's P + key sum - the slice length
+        // (mod 2^32; the query pass adds its queries and subtracts its positives' keys), high half =
+        // the slots written for a length other than this call's n
+        const unsigned long long* q = hdr0((part + 1) % parts);
+        unsigned mism = 0u;
+        for (int r = 0; r < parts; ++r) mism += hdr0(r)[kSlotN] != static_cast<unsigned long long>(n);
+        const unsigned lo = static_cast<unsigned>(q[0]) + static_cast<unsigned>(q[kSlotKeySum]) -
+                            static_cast<unsigned>(qlen);
+        stats[1] = (static_cast<unsigned long long>(mism) << 32) | lo;
     }
     const int64_t lb = int64_t(slot) * kGatherBlocks + blockIdx.x;
     for (int64_t i = lb * 256 + threadIdx.x; i < ncnt; i += int64_t(256) * kGatherBlocks * gridDim.y) cnt[i] = 0u;
@@ -280,7 +313,6 @@ __global__ __launch_bounds__(256) void gather_slots_kernel(const unsigned char* 
             over_s = over;
             if (first) {
                 stats[0] = P;
-                stats[1] = 0ull;
                 stats[2] = nf;
                 stats[3] = other;
                 *m_eff = over ? static_cast<unsigned long long>(mcap) + 1ull : P;
@@ -316,17 +348,20 @@ int dauc_auc_eval_enqueue(const float* scores, const void* labels, int label_dty
                           int64_t* part_out, void* workspace, size_t workspace_bytes, dauc_stream_t stream) {
     if (part_out == nullptr || !valid_args(scores, labels, label_dtype, n, part, parts, workspace, workspace_bytes))
         return DAUC_EINVAL;
-    if ((reinterpret_cast<uintptr_t>(part_out) & 7u) != 0) return DAUC_EINVAL;
+    // the kernels count straight into part_out: it must not lie in the workspace they also write
+    if ((reinterpret_cast<uintptr_t>(part_out) & 7u) != 0 || overlaps(part_out, kRecord, workspace, workspace_bytes))
+        return DAUC_EINVAL;
     return enqueue(scores, labels, label_dtype, n, part, parts, with_record(eval_ws(workspace, n), part_out),
                    as_hip(stream));
 }
 
-size_t dauc_auc_slot_bytes(int64_t n, int parts) { return n < 1 || parts < 1 ? 0 : slot_bytes(n, parts); }
+size_t dauc_auc_slot_bytes(int64_t n, int parts) { return n < 1 || parts < 1 ? 0 : slot_bytes(parts); }
 
 int dauc_auc_eval_compact_part(const float* scores, const void* labels, int label_dtype, int64_t n, int part,
                                int parts, void* slot, void* workspace, size_t workspace_bytes, dauc_stream_t stream) {
     if (slot == nullptr || (reinterpret_cast<uintptr_t>(slot) & 255u) != 0 ||
-        !valid_args(scores, labels, label_dtype, n, part, parts, workspace, workspace_bytes))
+        !valid_args(scores, labels, label_dtype, n, part, parts, workspace, workspace_bytes) ||
+        overlaps(slot, slot_bytes(parts), workspace, workspace_bytes))
         return DAUC_EINVAL;
     hipStream_t st = as_hip(stream);
     const EvalWs w = eval_ws(workspace, n);
@@ -334,12 +369,22 @@ int dauc_auc_eval_compact_part(const float* scores, const void* labels, int labe
     hipError_t e;
     if ((e = hipMemsetAsync(hdr, 0, kSlotHdr, st)) != hipSuccess) return -static_cast<int>(e);  // + histogram
     const int64_t lo = slice_lo(n, part, parts), hi = slice_lo(n, part + 1, parts);
-    if (hi <= lo) return DAUC_OK;  // an empty slice: P_r = 0
+    if (hi <= lo) {
+        // an empty slice: P_r = 0, the length word still set (its two halves)
+        auto* nw = reinterpret_cast<unsigned*>(hdr + kSlotN);
+        const unsigned long long nv = static_cast<unsigned long long>(n);
+        if ((e = hipMemsetD32Async(nw, static_cast<int>(nv & 0xffffffffull), 1, st)) != hipSuccess ||
+            (e = hipMemsetD32Async(nw + 1, static_cast<int>(nv >> 32), 1, st)) != hipSuccess)
+            return -static_cast<int>(e);
+        return DAUC_OK;
+    }
     const size_t lsz = label_dtype == DAUC_LABEL_I8 ? 1 : label_dtype == DAUC_LABEL_I32 ? 4 : 8;
     return compact_unordered(scores + lo, static_cast<const char*>(labels) + size_t(lo) * lsz, label_dtype, hi - lo,
                              reinterpret_cast<float*>(static_cast<char*>(slot) + kSlotHdr), hdr, 0ull, w.spare, 0ull,
-                             nullptr, nullptr, 0, st, slot_cap(n, parts),
-                             reinterpret_cast<unsigned*>(static_cast<char*>(slot) + kSlotHist));
+                             nullptr, nullptr, 0, st, slot_cap(parts),
+                             reinterpret_cast<unsigned*>(static_cast<char*>(slot) + kSlotHist),
+                             reinterpret_cast<unsigned*>(hdr + kSlotKeySum), hdr + kSlotN,
+                             static_cast<unsigned long long>(n));
 }
 
 int dauc_auc_eval_query_part(const float* scores, const void* labels, int label_dtype, int64_t n, int part, int parts,
@@ -349,6 +394,11 @@ int dauc_auc_eval_query_part(const float* scores, const void* labels, int label_
         (reinterpret_cast<uintptr_t>(part_out) & 7u) != 0 ||
         !valid_args(scores, labels, label_dtype, n, part, parts, workspace, workspace_bytes))
         return DAUC_EINVAL;
+    // the record, the gathered slots and the workspace: written / read by the same launches
+    const size_t sall = slot_bytes(parts) * size_t(parts);
+    if (overlaps(part_out, kRecord, workspace, workspace_bytes) || overlaps(part_out, kRecord, slots, sall) ||
+        overlaps(slots, sall, workspace, workspace_bytes))
+        return DAUC_EINVAL;
     hipStream_t st = as_hip(stream);
     const EvalWs w = with_record(eval_ws(workspace, n), part_out);
     const int64_t mcap = direct_capacity(n);
@@ -356,16 +406,19 @@ int dauc_auc_eval_query_part(const float* scores, const void* labels, int label_
     // zeroes the counts and the verdict (the record's other words are written), and hands the
     // build its histogram and zeroed per-cell counters
     static_assert(int64_t(kGatherBlocks) * 256 >= kCiTop, "one slot's workgroups cover the histogram");
+    const int64_t qlo = query_lo(n, part, parts), qhi = query_hi(n, part, parts);
     hipLaunchKernelGGL(gather_slots_kernel, dim3(kGatherBlocks, static_cast<unsigned>(parts)), dim3(256), 0, st,
-                       static_cast<const unsigned char*>(slots), slot_bytes(n, parts), parts, slot_cap(n, parts), mcap,
-                       w.pos, w.slot, w.spare, hist, direct_cnt_ptr(w.tws, mcap), direct_cnt_words(), w.wt, w.verdict);
+                       static_cast<const unsigned char*>(slots), slot_bytes(parts), parts, part, n, qhi - qlo,
+                       slot_cap(parts), mcap, w.pos, w.slot, w.spare, hist, direct_cnt_ptr(w.tws, mcap),
+                       direct_cnt_words(), w.wt, w.verdict);
     int rc = launch_status();
     if (rc) return rc;
-    const int64_t qlo = n * part / parts, qhi = n * (part + 1) / parts;
     if (qhi > qlo) {
-        // the build and the query see m_eff (w.spare[0]): P, or past the index's capacity on overflow
+        // the build and the query see m_eff (w.spare[0]): P, or past the index's capacity on overflow;
+        // the query pass brings the record's check word (its low half) back to zero
         rc = counts_labeled_direct(w.pos, w.spare, mcap, scores, labels, label_dtype, qlo, qhi, w.wt, w.wt + 2,
-                                   w.verdict, w.tws, w.tws_bytes, st, hist);
+                                   w.verdict, w.tws, w.tws_bytes, st, hist,
+                                   reinterpret_cast<unsigned*>(part_out + 4));
         if (rc) return rc;
     }
     return DAUC_OK;

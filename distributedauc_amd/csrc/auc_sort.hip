@@ -885,8 +885,11 @@ __device__ __forceinline__ void ci_fix(unsigned x, unsigned rl, unsigned cnt, co
 // returns at once when the builder kept the tree, so it is enqueued unconditionally. Per
 // iteration every slot's window loads are issued BEFORE the next iteration's stream loads:
 // vmcnt retires loads in issue order, so a wait for a window would otherwise also wait out a
-// streaming load's HBM latency.
-template <typename LT>
+// streaming load's HBM latency. CHECK (the two-step evaluation): *check += #queries - the sum of
+// the keys of the scores labeled 1, mod 2^32, over [begin, end) -- also when the index is not used
+// (the pass then only reads the range for it) -- so the caller can compare the range's positives
+// with the ones another rank compacted from it.
+template <typename LT, bool CHECK = false>
 __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __restrict__ s,
                                                                 const LT* __restrict__ lab, int64_t begin,
                                                                 int64_t end, const unsigned* __restrict__ meta,
@@ -897,11 +900,33 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
                                                                 unsigned long long* __restrict__ nonfinite,
                                                                 unsigned* __restrict__ verdict,
                                                                 const unsigned* __restrict__ grp,
-                                                                const unsigned long long* __restrict__ Mp) {
+                                                                const unsigned long long* __restrict__ Mp,
+                                                                unsigned* __restrict__ check) {
     const bool in_use = count_index_in_use(meta);
     if (Mp != nullptr) M = static_cast<int64_t>(*Mp);  // the direct build: the table size on the device
     if (verdict != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *verdict = in_use ? 1u : 2u;
     if (!in_use) {
+        if constexpr (CHECK) {
+            // the consistency word and the finiteness of every query, whatever the table
+            unsigned nf = 0u, chk = 0u;
+            for (int64_t i = begin + int64_t(blockIdx.x) * kQueryThreads + threadIdx.x; i < end;
+                 i += int64_t(gridDim.x) * kQueryThreads) {
+                const float v = s[i];
+                if (lab[i] != LT(1)) {
+                    nf += !isfinite(v);
+                    chk += 1u;
+                } else {
+                    chk -= key_fast(v);
+                }
+            }
+            const unsigned long long nfw = wave_sum(static_cast<unsigned long long>(nf));
+            const unsigned ck = static_cast<unsigned>(wave_sum(static_cast<unsigned long long>(chk)));
+            if ((threadIdx.x & (kWave - 1)) == 0) {
+                if (nfw && nonfinite != nullptr) atomicAdd(nonfinite, nfw);
+                if (ck) atomicAdd(check, ck);
+            }
+            return;
+        }
         // no positives at all: nothing to count, but the queries are still checked for finiteness
         // (sklearn raises on a non-finite score before its one-class warning, _ranking.py:868-869)
         if (M == 0 && nonfinite != nullptr) {
@@ -951,11 +976,13 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
     const unsigned M32 = static_cast<unsigned>(M);
     unsigned long long w = 0, t = 0;
     unsigned nf = 0;
+    unsigned chk = 0u;  // CHECK: #queries - sum of the positives' keys (mod 2^32)
     const int64_t a0 = (begin + 3) & ~int64_t(3);
     const int64_t head = a0 < end ? a0 : end;
     const int64_t stride = int64_t(gridDim.x) * kQueryThreads;
     const int64_t tid = int64_t(blockIdx.x) * kQueryThreads + threadIdx.x;
     auto one = [&](int64_t i) {
+        if constexpr (CHECK) chk += lab[i] != LT(1) ? 1u : 0u - key_fast(s[i]);
         if (lab[i] != LT(1)) {
             nf += !isfinite(s[i]);
             const unsigned x = key_fast(s[i]);
@@ -988,6 +1015,7 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
         struct Stream {
             f32x4 f[U];
             LabelWords<LT> l[U];
+            unsigned valid;  // CHECK: bit u = slot u is in range
         };
         // Every load of the loop is issued unconditionally (out-of-range slots re-read slot 0 and are
         // masked; a lane without a window reads the table's first one): a load under a branch
@@ -1001,6 +1029,10 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
                 sg.f[u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(s + i));
                 sg.l[u].load(lab + i);
                 if (v >= nvec) sg.l[u].set_positive();
+                if constexpr (CHECK) {
+                    if (u == 0) sg.valid = 0u;
+                    sg.valid |= unsigned(v < nvec) << u;
+                }
             }
         };
         // one group in flight: its keys, rank_lo | count << 28 (rank_lo < 2^28: M <= 2^27 here),
@@ -1022,8 +1054,11 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
                     g.use |= unsigned(use) << (4 * u + q);
                     g.x[4 * u + q] = key_fast(f[q]);
                     nf += use && !isfinite(f[q]);
+                    if constexpr (CHECK)
+                        chk -= !use && ((sg.valid >> u) & 1u) ? g.x[4 * u + q] : 0u;
                 }
             }
+            if constexpr (CHECK) chk += __builtin_popcount(g.use);
         };
         // phase by phase over the group, so that every query's LDS read of a phase is issued before
         // the first wait (a per-query chain with its conditional window load in between keeps the
@@ -1154,6 +1189,10 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
     t = wave_sum(t);
     const unsigned long long nfw = wave_sum(static_cast<unsigned long long>(nf));
     const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+    if constexpr (CHECK) {
+        const unsigned ck = static_cast<unsigned>(wave_sum(static_cast<unsigned long long>(chk)));
+        if (lane == 0 && ck) atomicAdd(check, ck);
+    }
     if (lane == 0) {
         red[0][wid] = w;
         red[1][wid] = t;
@@ -1641,11 +1680,16 @@ int prepare_count(const unsigned* sorted, int64_t M, const CountWs& cw, hipStrea
 template <typename LT>
 int launch_ci(const float* s, const LT* lab, int64_t begin, int64_t end, const CountWs& cw, const unsigned* sorted,
               int64_t M, unsigned long long* out, unsigned long long* nonfinite, hipStream_t st,
-              unsigned* verdict = nullptr, const unsigned* grp = nullptr, const unsigned long long* Mp = nullptr) {
+              unsigned* verdict = nullptr, const unsigned* grp = nullptr, const unsigned long long* Mp = nullptr,
+              unsigned* check = nullptr) {
     const dim3 grid(query_grid(end - begin)), block(kQueryThreads);
     const size_t lds = (size_t(kCiTop) + kCiMaxBlocks) * 8 + (grp ? size_t(kDirectMaxGroups) * 4 : 0);
-    hipLaunchKernelGGL((query_ci_kernel<LT>), grid, block, lds, st, s, lab, begin, end, cw.meta, cw.l1, cw.blk, sorted,
-                       M, out, nonfinite, verdict, grp, Mp);
+    if (check != nullptr)
+        hipLaunchKernelGGL((query_ci_kernel<LT, true>), grid, block, lds, st, s, lab, begin, end, cw.meta, cw.l1,
+                           cw.blk, sorted, M, out, nonfinite, verdict, grp, Mp, check);
+    else
+        hipLaunchKernelGGL((query_ci_kernel<LT>), grid, block, lds, st, s, lab, begin, end, cw.meta, cw.l1, cw.blk,
+                           sorted, M, out, nonfinite, verdict, grp, Mp, check);
     return launch_status();
 }
 
@@ -1784,7 +1828,8 @@ int build_direct_index(const float* pos, const unsigned long long* Mp, int64_t M
 int counts_labeled_direct(const float* pos, const unsigned long long* Mp, int64_t Mcap, const float* scores,
                           const void* labels, int label_dtype, int64_t begin, int64_t end,
                           unsigned long long* wins_ties, unsigned long long* nonfinite, unsigned* verdict,
-                          void* workspace, size_t workspace_bytes, hipStream_t st, const unsigned* ready_hist) {
+                          void* workspace, size_t workspace_bytes, hipStream_t st, const unsigned* ready_hist,
+                          unsigned* check) {
     if (begin < 0 || end < begin || wins_ties == nullptr || (end > begin && (scores == nullptr || labels == nullptr)))
         return DAUC_EINVAL;
     if (label_dtype != DAUC_LABEL_I8 && label_dtype != DAUC_LABEL_I32 && label_dtype != DAUC_LABEL_I64)
@@ -1796,13 +1841,13 @@ int counts_labeled_direct(const float* pos, const unsigned long long* Mp, int64_
     switch (label_dtype) {
         case DAUC_LABEL_I8:
             return launch_ci(scores, static_cast<const int8_t*>(labels), begin, end, nw, ix.table, 0, wins_ties,
-                             nonfinite, st, verdict, ix.grp, Mp);
+                             nonfinite, st, verdict, ix.grp, Mp, check);
         case DAUC_LABEL_I32:
             return launch_ci(scores, static_cast<const int32_t*>(labels), begin, end, nw, ix.table, 0, wins_ties,
-                             nonfinite, st, verdict, ix.grp, Mp);
+                             nonfinite, st, verdict, ix.grp, Mp, check);
         default:
             return launch_ci(scores, static_cast<const int64_t*>(labels), begin, end, nw, ix.table, 0, wins_ties,
-                             nonfinite, st, verdict, ix.grp, Mp);
+                             nonfinite, st, verdict, ix.grp, Mp, check);
     }
 }
 

@@ -141,15 +141,19 @@ class Evaluator:
     reference's rank-0 scoring."""
 
     def __init__(self, test_batches, n_test: int, split_index: int, device, group, world: int, rank: int,
-                 history_path: str | None = None, split: bool = True, deterministic: bool = False):
+                 history_path: str | None = None, split: bool = True, deterministic: bool = False,
+                 collective: bool | None = None):
         self.batches = test_batches
         self.n = n_test
         self.split = split_index
-        self.split_scoring = bool(split) and world > 1
+        # collective (default world > 1): True at world 1 rehearses the split path's broadcast and
+        # all-gather on a one-rank process group
+        self.collective = world > 1 if collective is None else bool(collective)
+        self.split_scoring = bool(split) and self.collective
         self.deterministic = bool(deterministic)
         self.device = device
         self.world, self.rank = world, rank
-        self.auc = ExactAUC(group, world, rank)
+        self.auc = ExactAUC(group, world, rank, collective=self.collective)
         self.group = group
         self.history_path = history_path
         self.rows: list[tuple[int, float, float]] = []
@@ -227,7 +231,7 @@ class Evaluator:
             scores = torch.empty(self.n, dtype=torch.float32, device=self.device)
             if self.rank == 0:
                 self._score(coda, 0, len(self.batches), scores)
-            if self.world > 1:
+            if self.collective:
                 dist.broadcast(scores, 0, group=self.group)
         auc = self.auc(labels, scores)
         if self.rank == 0:

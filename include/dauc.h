@@ -255,13 +255,13 @@ int dauc_auc_counts_sorted_labeled(const float* pos, int64_t P, const float* sco
 
 /*
  * The exact-AUC evaluation of main.py:79-81 (sklearn roc_curve + auc over one test set), as ONE
- * stream-ordered sequence with no host synchronisation and no allocation: a memset of the
- * record, a one-pass positive compaction (labels read once, P counted on the device),
+ * stream-ordered sequence with no host synchronisation and no allocation: two memsets (the
+ * record, the workspace's top-bucket histogram), a one-pass positive compaction (labels read once, P counted on the device),
  * the count index built straight from the unsorted positives with the table size read on the
  * device, and the query pass over this part's scores [part*n/parts, (part+1)*n/parts), whose
  * labels are not 1 (every part builds the index over ALL the positives itself: ranks holding the
  * same test set need no collective to share the table). The kernels count straight into the
- * record (no copy), so part_out must not overlap the workspace:
+ * record (no copy), so part_out must not overlap the workspace (DAUC_EINVAL if it does):
  *   part_out (DEVICE int64[8], 8-byte aligned) = { W_part, T_part, #non-finite queried scores of this part,
  *                                  P, 0, #non-finite positives, #labels not in {-1, 1}, verdict }
  * The first three sum over the parts (the caller's all-reduce); the rest are the same on every
@@ -304,20 +304,26 @@ int dauc_auc_eval_counts_part(const float* scores, const void* labels, int label
 
 /*
  * The sharded evaluation without a whole-vector compaction on every rank, in two enqueued steps
- * around the caller's collective (no host synchronisation in either):
- *   1. dauc_auc_eval_compact_part: the positives of THIS rank's slice of the labels (slices on
- *      256-label boundaries) compacted, unordered, into `slot` (device, dauc_auc_slot_bytes(n,
- *      parts) bytes, 256-byte aligned): a header {P_r, 0, #non-finite positives, #labels not in
- *      {-1, 1}} (int64) at byte 0, the top-bucket histogram of the positives' order-preserving
- *      keys (2048 uint32: key >> 21) from byte 256 and the scores from byte 8448;
+ * around the caller's collective (no host synchronisation in either). Slice r of n labels is
+ * [lo(r), lo(r+1)) with lo(0) = 0, lo(parts) = n and lo(r) = (r*n/parts) rounded down to a multiple
+ * of 256.
+ *   1. dauc_auc_eval_compact_part: the positives of THIS rank's slice compacted, unordered, into
+ *      `slot` (device, dauc_auc_slot_bytes(n, parts) bytes -- the same for every n --, 256-byte
+ *      aligned, outside the workspace): a header of int64 words {P_r, 0, #non-finite positives,
+ *      #labels not in {-1, 1}, n, the positives' order-preserving keys summed mod 2^32} at byte 0,
+ *      the top-bucket histogram of those keys (2048 uint32: key >> 21) from byte 256 and the scores
+ *      from byte 8448;
  *   -- the caller all-gathers the `parts` slots, rank order, contiguous --
  *   2. dauc_auc_eval_query_part: the gathered slots become the positive table (headers and
- *      histograms summed), the count index is built from it and scores [part*n/parts,
- *      (part+1)*n/parts) are counted straight into part_out (device int64[8], 8-byte aligned,
- *      outside the workspace and the slots) = dauc_auc_eval_enqueue's record. A slot holds an
- *      even share of the count index's capacity + 25 %: a slice with more positives (an
- *      unshuffled test set), like a table the index cannot hold, gives verdict 2 -- the caller
- *      then runs dauc_auc_eval_counts_part on every rank.
+ *      histograms summed), the count index is built from it and the scores of the NEXT rank's
+ *      slice, (part + 1) % parts, are counted straight into part_out (device int64[8], 8-byte
+ *      aligned, outside the workspace and the slots; DAUC_EINVAL otherwise) =
+ *      dauc_auc_eval_enqueue's record, except word 4, a consistency check that is 0 when the ranks
+ *      agree: low 32 bits = (P + key sum) of the queried slice's slot - (positives + their key sum)
+ *      this rank's labels and scores give over that slice, mod 2^32; high 32 bits = the number of
+ *      slots built for another n. A slot holds an even share of the count index's capacity + 25 %:
+ *      a slice with more positives (an unshuffled test set), like a table the index cannot hold,
+ *      gives verdict 2 -- the caller then runs dauc_auc_eval_counts_part on every rank.
  * Replaces the reference's rank-0 evaluation (main.py:232-250) with a sharded one.
  */
 size_t dauc_auc_slot_bytes(int64_t n, int parts);

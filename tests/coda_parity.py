@@ -31,7 +31,8 @@ def close(got, ref, what, rtol=RTOL, atol=ATOL):
                              f"ref {ref.reshape(-1)[i]!r}")
 
 
-def run_rank(fixture: dict, rank: int, world: int, device, group=None, head: str = "softmax", graph: bool = False):
+def run_rank(fixture: dict, rank: int, world: int, device, group=None, head: str = "softmax", graph: bool = False,
+             collective: bool | None = None):
     from distributedauc_amd.coda import CoDA
 
     cfg = json.loads(str(fixture["config"]))
@@ -42,7 +43,7 @@ def run_rank(fixture: dict, rank: int, world: int, device, group=None, head: str
         net.softmax = torch.nn.Identity()
     net = net.to(device)
     coda = CoDA(net, lr=cfg["lr"], gamma=cfg["gamma"], T0=cfg["T0"], I=cfg["I"], split_index=cfg["split_index"],
-                world=world, rank=rank, group=group, device=device, head=head)
+                world=world, rank=rank, group=group, device=device, head=head, collective=collective)
     coda.use_graph(graph)
     xs, ys = fixture[f"r{rank}_x"], fixture[f"r{rank}_y"]
 

@@ -171,10 +171,10 @@ def auc_eval_enqueue(scores, labels, part, parts, out=None):
 _INDEX_CAP = 219_838  # 3 / 2 x the count index's cells (auc_sort.hip direct_capacity)
 
 
-def _slot_cap(n, parts):
-    share = -(-n // parts)
-    fair = -(-min(n // 2 + 1, _INDEX_CAP) // parts)
-    return min(share, fair + fair // 4 + 64)
+def _slot_cap(parts):
+    """auc_eval.hip slot_cap: an even share of the index's capacity + 25 % + 64, whatever n."""
+    fair = -(-_INDEX_CAP // parts)
+    return fair + fair // 4 + 64
 
 
 _SLOT_HIST = 256                  # the slot's top-bucket histogram (2048 u32) after the header
@@ -182,63 +182,85 @@ _SLOT_HDR = _SLOT_HIST + 2048 * 4  # the slot's scores
 
 
 def auc_slot_bytes(n, parts):
-    """dauc_auc_slot_bytes' stand-in (same formula)."""
-    return _SLOT_HDR + -(-_slot_cap(n, parts) * 4 // 256) * 256
+    """dauc_auc_slot_bytes' stand-in (same formula; n only has to be >= 1)."""
+    return _SLOT_HDR + -(-_slot_cap(parts) * 4 // 256) * 256
+
+
+def _keys(v):
+    """count_index.h key_fast: the order-preserving uint32 key (-0 on +0)."""
+    u = (np.asarray(v, np.float32) + np.float32(0)).view(np.uint32)
+    return u ^ np.where(u >> 31 != 0, np.uint32(0xffffffff), np.uint32(0x80000000))
 
 
 def _top_buckets(pos):
     """count_index.h's top-bucket histogram of the scores' order-preserving keys (-0 on +0)."""
-    u = (pos.astype(np.float32) + np.float32(0)).view(np.uint32)
-    key = u ^ np.where(u >> 31 != 0, np.uint32(0xffffffff), np.uint32(0x80000000))
-    return np.bincount(key >> 21, minlength=2048).astype(np.uint32)
+    return np.bincount(_keys(pos) >> 21, minlength=2048).astype(np.uint32)
 
 
 def _slice_lo(n, part, parts):
     return 0 if part == 0 else (n if part >= parts else (n * part // parts) & ~255)
 
 
+def _query_range(n, part, parts):
+    """auc_eval.hip query_lo / query_hi: part r counts the NEXT part's slice."""
+    q = (part + 1) % parts
+    return _slice_lo(n, q, parts), _slice_lo(n, q + 1, parts)
+
+
 def auc_eval_compact_part(scores, labels, part, parts, slot):
-    """dauc_auc_eval_compact_part's stand-in: header {P_r, 0, #non-finite positives, #other labels}
-    (int64) at byte 0, the positives' top-bucket histogram from byte 256, the slice's positive
-    scores (in order) from byte 8448, at most cap of them."""
+    """dauc_auc_eval_compact_part's stand-in: header {P_r, 0, #non-finite positives, #other labels,
+    n, the positives' keys summed mod 2^32} (int64) at byte 0, the positives' top-bucket histogram
+    from byte 256, the slice's positive scores (in order) from byte 8448, at most cap of them."""
     s, y = scores.detach().numpy(), labels.numpy().astype(np.int64)
     n = s.size
     lo, hi = _slice_lo(n, part, parts), _slice_lo(n, part + 1, parts)
     ss, yy = s[lo:hi], y[lo:hi]
     pos = ss[yy == 1]
-    hdr = np.array([pos.size, 0, int((~np.isfinite(pos)).sum()), int(((yy != 1) & (yy != -1)).sum())], np.int64)
-    slot[:32] = torch.from_numpy(hdr.view(np.uint8).copy())
+    ksum = int(_keys(pos).astype(np.uint64).sum()) & 0xFFFFFFFF
+    hdr = np.array([pos.size, 0, int((~np.isfinite(pos)).sum()), int(((yy != 1) & (yy != -1)).sum()), n, ksum],
+                   np.int64)
+    slot[:48] = torch.from_numpy(hdr.view(np.uint8).copy())
     slot[_SLOT_HIST:_SLOT_HDR] = torch.from_numpy(_top_buckets(pos).view(np.uint8).copy())
-    k = min(pos.size, _slot_cap(n, parts))
+    k = min(pos.size, _slot_cap(parts))
     slot[_SLOT_HDR:_SLOT_HDR + 4 * k] = torch.from_numpy(pos[:k].astype(np.float32).view(np.uint8).copy())
     return slot
 
 
 def auc_eval_query_part(scores, labels, part, parts, slots, out=None):
     """dauc_auc_eval_query_part's stand-in: the gathered slots' positives (verdict 2 when a slot
-    overflowed or the table exceeds the index), the part's queries counted; the enqueue record."""
+    overflowed or the table exceeds the index), the next part's slice counted, the record's check
+    word (low half: the queried slot's P + key sum - this rank's positives + key sum over that slice,
+    mod 2^32; high half: slots built for another n); the enqueue record otherwise."""
     s, y = scores.detach().numpy(), labels.numpy().astype(np.int64)
     n = s.size
-    nb, cap = auc_slot_bytes(n, parts), _slot_cap(n, parts)
+    nb, cap = auc_slot_bytes(n, parts), _slot_cap(parts)
     raw = slots.numpy()
     P = nfpos = other = 0
     over = False
     pos = []
+    hdrs = []
     for r in range(parts):
-        h = raw[r * nb:r * nb + 32].view(np.int64)
+        h = raw[r * nb:r * nb + 48].view(np.int64)
+        hdrs.append(h)
         P, nfpos, other = P + int(h[0]), nfpos + int(h[2]), other + int(h[3])
         over |= int(h[0]) > cap
         pos.append(raw[r * nb + _SLOT_HDR:r * nb + _SLOT_HDR + 4 * min(int(h[0]), cap)].view(np.float32))
     pos = np.concatenate(pos) if pos else np.zeros(0, np.float32)
-    lo, hi = n * part // parts, n * (part + 1) // parts
+    lo, hi = _query_range(n, part, parts)
     rec = torch.zeros(8, dtype=torch.int64) if out is None else out
     rec.zero_()
     rec[3], rec[5], rec[6] = P, nfpos, other
+    qh = hdrs[(part + 1) % parts]
+    mism = sum(int(h[4]) != n for h in hdrs)
+    yq, sq = y[lo:hi], s[lo:hi]
+    seen_pos = yq == 1
+    low = (int(qh[0]) + int(qh[5]) - int(seen_pos.sum()) - int(_keys(sq[seen_pos]).astype(np.uint64).sum())) & 0xFFFFFFFF
+    rec[4] = (mism << 32) | low
     if hi <= lo:
         return rec
     verdict = 1 if (not over and 0 < P <= min(n // 2 + 1, _INDEX_CAP)) else 2
     rec[7] = verdict
-    q = s[lo:hi][y[lo:hi] != 1]
+    q = sq[yq != 1]
     rec[2] = int((~np.isfinite(q)).sum())
     if verdict == 1 and not nfpos:
         W, T = coracle_pair_count(pos, q[np.isfinite(q)]) if q.size else (0, 0)

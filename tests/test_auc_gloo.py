@@ -1,8 +1,9 @@
 """The sharded exact-AUC orchestration on CPU (gloo, world 2 and 3): every rank compacts the
 positives of its slice of the labels into a slot, one all-gather of the slots, every rank counts
-its slice of the scores against the gathered table, one all-gather of the 8-word part records,
-counts summed on the host; a slot that overflows (an unshuffled test set) and a table the index
-cannot hold take the sorted path on every rank. Below
+the next rank's slice of the scores against the gathered table, one all-gather of the 8-word part
+records, counts summed on the host; ranks whose labels, positive scores or lengths differ raise
+together; a slot that overflows (an unshuffled test set) and a table the index cannot hold take
+the sorted path on every rank. Below
 ExactAUC.SHARD_MIN scores every rank evaluates the whole vector instead (same integers, no
 collective); both modes run here. The kernels are served by the oracle (tests/cpu_kernels.py);
 the GPU form runs in bench.py --gpus 2 (tests/test_bench_gpu.py)."""
@@ -52,9 +53,32 @@ def _worker(rank, world, port, q, shard_min):
             raised = True
         assert raised
         if ev.last_mode == "sharded":
-            # (round 4: every rank compacts only its slice, so ranks holding different vectors are
-            # no longer detected -- the caller passes identical vectors, as Evaluator's all-gather
-            # guarantees; the gathered slots give every rank the same P and label counts)
+            # ranks holding different labels: every rank checks its own labels over the
+            # next rank's slice against the slot that rank compacted from it -- all raise together.
+            # (Labels a rank holds but never reads -- outside its own and the next slice -- cannot
+            # change the result and are not checked.) Indices 10000-13000: rank 1's own slice at
+            # world 2 and 3, queried by rank 0.
+            y3 = y.copy()
+            if rank == 1:
+                neg = np.flatnonzero(y == -1)
+                y3[neg[(neg > 10_000) & (neg < 13_000)][:4]] = 1
+            with pytest.raises(RuntimeError, match="disagree"):
+                ev.counts(torch.from_numpy(y3), torch.from_numpy(s), device="cpu")
+            # a positive's score differs on one rank (same labels): the slot's key sum catches it
+            s3 = s.copy()
+            if rank == world - 1:
+                j = int(np.flatnonzero(y == 1)[-1])
+                s3[j] = np.float32(s3[j] + 0.5)
+            with pytest.raises(RuntimeError, match="disagree"):
+                ev.counts(torch.from_numpy(y), torch.from_numpy(s3), device="cpu")
+            # ranks called with different lengths: equal slot sizes, so the gather completes and
+            # every rank raises
+            m = n if rank == 0 else n - 300
+            with pytest.raises(RuntimeError, match="different lengths"):
+                ev.counts(torch.from_numpy(y[:m].copy()), torch.from_numpy(s[:m].copy()), device="cpu")
+            # the group is still usable: the same exact counts
+            c2 = ev.counts(torch.from_numpy(y), torch.from_numpy(s), device="cpu")
+            assert c2 == c, (c2, c)
             # an unshuffled test set: every positive in rank 0's slice overflows its slot -- the
             # sorted path on every rank, same integers
             y5 = np.where(np.arange(n) < 8000, 1, -1).astype(np.int8)  # P <= n / 2 + 1: the index could hold it
