@@ -80,6 +80,11 @@ def parse(argv=None):
                         "oracle loop too: profiles/r04/direction/), so the in-training AUC is meaningless there. "
                         "0.01 learns the synthetic signal. The step's kernels and bytes do not depend on lr")
     p.add_argument("--pool", type=int, default=4, help="distinct resident input batches cycled")
+    p.add_argument("--signal-flip", type=float, default=0.2,
+                   help="fraction of the synthetic images (training and test) carrying the other class's sign "
+                        "(loader.py): the best achievable test AUC is 1 - flip, so the in-training AUC can land "
+                        "between chance and that ceiling instead of saturating at 1.0 (VERDICT r04 #7); shapes "
+                        "and bytes of every step are unchanged")
     p.add_argument("--sweep-I", default="1,8,16,32", help="configs[2] averaging periods ('' = off)")
     p.add_argument("--sweep-steps", type=int, default=32, help="timed steps per period (a multiple of every I)")
     p.add_argument("--eval-images", type=int, default=8192,
@@ -218,7 +223,7 @@ def timed_steps(coda, it, steps: int, world: int) -> float:
 
 # ----------------------------------------------------------------------------- training legs
 def make_coda(arch, batch, image_size, I, pos_ratio, pool, world, rank, device, fused_bn=True, gemm_conv1x1=True,
-              graph=False, lr=0.1):
+              graph=False, lr=0.1, flip=0.0):
     from distributedauc_amd.backbone import build_backbone
     from distributedauc_amd.coda import CoDA
     from distributedauc_amd.loader import DeviceLoader, SyntheticImageNet, imagenet_like_labels
@@ -227,7 +232,8 @@ def make_coda(arch, batch, image_size, I, pos_ratio, pool, world, rank, device, 
     split = 499
     labels = imagenet_like_labels(1 << 16, 1000, split, pos_ratio=pos_ratio, seed=123 + rank)
     ds = SyntheticImageNet(labels, image_size, split)
-    loader = DeviceLoader(ds, np.arange(len(labels)), batch, device, seed=1234 + rank, channels_last=True, pool=pool)
+    loader = DeviceLoader(ds, np.arange(len(labels)), batch, device, seed=1234 + rank, channels_last=True, pool=pool,
+                          flip=flip)
     net = build_backbone(arch, num_classes=2).to(device).to(memory_format=torch.channels_last)
     net.set_fused_bn(bool(fused_bn)).set_gemm_conv1x1(bool(gemm_conv1x1))
     coda = CoDA(net, lr=lr, gamma=2000.0, T0=10 ** 9, I=I, split_index=split, world=world, rank=rank,
@@ -243,7 +249,7 @@ def bench_train(args, world, rank, device):
     from distributedauc_amd import _lib
 
     coda, it = make_coda(args.arch, args.batch, args.image_size, args.I, args.pos_ratio, args.pool, world, rank,
-                         device, args.fused_bn, args.gemm_conv1x1, lr=args.lr)
+                         device, args.fused_bn, args.gemm_conv1x1, lr=args.lr, flip=args.signal_flip)
     log(f"rank {rank}: model + data ready, first steps compile/tune MIOpen kernels")
     lib = _lib.load()
     upd = KernelTimer(lib, "dauc_pd_update")
@@ -306,14 +312,15 @@ def bench_training_eval(coda, args, world, rank, device, reps=3):
     So the AUCs of every repetition and of both scoring modes are REPORTED (with their largest
     difference), never asserted equal; tests/test_main_gpu.py checks bit-identity under
     deterministic solvers."""
-    from distributedauc_amd.loader import DeviceLoader, SyntheticImageNet, imagenet_like_labels
+    from distributedauc_amd.loader import DeviceLoader, SyntheticImageNet, imagenet_like_labels, signal_auc_ceiling
     from distributedauc_amd.main import Evaluator
 
     n = args.eval_images
     tb = args.batch
     labels = imagenet_like_labels(n, 1000, 499, pos_ratio=args.pos_ratio, seed=777)  # same on every rank
     ds = SyntheticImageNet(labels, args.image_size, 499)
-    it = iter(DeviceLoader(ds, np.arange(n), tb, device, seed=777, shuffle=False, channels_last=True))
+    it = iter(DeviceLoader(ds, np.arange(n), tb, device, seed=777, shuffle=False, channels_last=True,
+                           flip=args.signal_flip))
     batches = [next(it) for _ in range((n + tb - 1) // tb)]
 
     def timed(split):
@@ -337,12 +344,41 @@ def bench_training_eval(coda, args, world, rank, device, reps=3):
            "method": "split" if grouped() else "one rank",
            "auc_note": "AUCs are reported, not asserted equal: MIOpen's fast solvers change low bits between "
                        "scorings (bit-identity needs --deterministic_eval, tested in tests/test_main_gpu.py)"}
+    rec["band"] = auc_band(args, n, labels, aucs[-1])
     if grouped():
         ms0, aucs0 = timed(False)
         rec.update({"ms_rank0_scoring": ms0 * 1e3, "speedup_vs_rank0_scoring": ms0 / ms_split,
                     "auc_rank0_scoring": aucs0[-1],
                     "auc_max_abs_diff_split_vs_rank0": max(abs(a - b) for a in aucs for b in aucs0)})
     log(f"rank {rank}: in-training eval of {n} images {ms_split * 1e3:.1f} ms, auc {aucs[-1]:.4f}")
+    return rec
+
+
+def auc_band(args, n, labels, auc):
+    """Where the in-training AUC should land: above chance, at most the test set's
+    exact Bayes ceiling (the AUC of the sign each image carries, 1 - flip in expectation), next to
+    the CPU oracle loop's test AUC on the same workload (scripts/oracle_auc_band.py, committed under
+    profiles/r05/; it applies when its configuration is this run's)."""
+    from distributedauc_amd.loader import signal_auc_ceiling
+
+    steps_trained = args.warmup + args.steps + (len([v for v in args.sweep_I.split(",") if v.strip()]) * args.sweep_steps
+                                                if args.sweep_I else 0)
+    ceiling = signal_auc_ceiling(np.arange(n), labels, 499, args.signal_flip)
+    rec = {"chance": 0.5, "bayes_ceiling_test_set": ceiling, "flip": args.signal_flip,
+           "steps_trained": steps_trained, "cpu_oracle_loop": None}
+    f = REPO / "profiles" / "r05" / "oracle_auc_band.json"
+    if f.exists():
+        o = json.loads(f.read_text())
+        c = o.get("config", {})
+        same = (c.get("arch"), c.get("batch"), c.get("image_size"), c.get("pool"), c.get("steps"), c.get("lr"),
+                c.get("flip"), c.get("test_images")) == (args.arch, args.batch, args.image_size, args.pool,
+                                                         steps_trained, args.lr, args.signal_flip, n)
+        rec["cpu_oracle_loop"] = {"band": o.get("band"), "same_config": same,
+                                  "source": "profiles/r05/oracle_auc_band.json (scripts/oracle_auc_band.py, "
+                                            "fp32 torch CPU; not this run)"}
+    lo = 0.5 + 0.05  # clearly above chance
+    rec["in_band"] = bool(lo <= auc <= ceiling + 0.02)  # + the test set's sampling slack
+    rec["band_rule"] = "0.55 <= auc <= bayes_ceiling_test_set + 0.02"
     return rec
 
 
@@ -586,6 +622,8 @@ def bench_surrogate(args, device):
     kt.enabled = False
     kt.restore()
     per_call_ms = kt.mean_ms()
+    # every reduction of the leg completed (a timed-out one would have returned NaN: VERDICT r04 #4)
+    status = ops.surrogate_status(device, raise_on_error=True)
     nbytes = 9 * B
     gbs = nbytes / (ms / 1e3) / 1e9
     sgbs = nbytes / (stream_ms / 1e3) / 1e9
@@ -593,7 +631,7 @@ def bench_surrogate(args, device):
             "B": B, "avg_launch_us": ms * 1e3, "per_call_events_us": per_call_ms * 1e3,
             "timing": f"HIP events around {args.sur_reps} back-to-back calls on the launch stream, divided by the "
                       "call count (per_call_events_us: an event pair around every call instead)",
-            "loss": loss,
+            "loss": loss, "reduction_status": status,
             "roofline": {"kernel": "dauc_surrogate_fwdbwd (whole call)", "launches": "surrogate_tail_x_kernel: the stream "
                          "and its fp64 row reduce (by 128 extra workgroups that stream nothing, the last one taking "
                          "the grid's last 512 rows itself; epoch-tagged granules) in ONE launch",
@@ -885,7 +923,7 @@ def main():
                                        f"{' (1x1 convs as GEMMs)' if args.gemm_conv1x1 else ''}, fp32 AUC kernels "
                                        "(BASELINE configs[1])",
                            "global_batch": args.batch * world, "image_size": args.image_size, "I": args.I,
-                           "lr": args.lr, "gamma": 2000.0,
+                           "lr": args.lr, "gamma": 2000.0, "signal_flip": args.signal_flip,
                            "pos_ratio": args.pos_ratio, "parallelism": f"dp{world}", "params": res["n_params"]},
                 "roofline": {"kernel": "dauc_pd_update (fused dppd_sg + running average)", "bound": "hbm",
                              "achieved": upd_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -48,6 +48,7 @@ SIGNATURES = {
     "dauc_surrogate_fwdbwd": (_int, [_vp, _i64, _vp, _int, _i64, _vp, _vp, _vp, _i64, _vp, _vp, _vp,
                                      _vp, _sz, _vp]),
     "dauc_class_sums": (_int, [_vp, _i64, _vp, _int, _i64, _vp, _int, _vp, _sz, _vp]),
+    "dauc_surrogate_status": (_int, [_vp, _sz, _vp, _int, _vp]),
     "dauc_alpha_from_sums": (_int, [_vp, _vp, _vp]),
     "dauc_surrogate_logits_fwdbwd": (_int, [_vp, _int, _i64, _vp, _int, _i64, _vp, _vp, _vp, _i64, _vp, _vp,
                                             _vp, _vp, _vp, _sz, _vp]),

@@ -525,14 +525,16 @@ __global__ __launch_bounds__(kThreads) void surrogate_rows_reduce_kernel(
 // call -- even one written after that call gave up waiting for it -- carries an older tag and is
 // never taken for a current one, and nothing is re-zeroed between calls (tag = epoch | 2^31, so a
 // zeroed workspace holds no valid granule either). A poll that times out makes the outputs NaN (a
-// group reducer then publishes NaN totals), and the epoch still advances. Nothing waits on a
-// workgroup that waits: every row a reducer needs comes from a workgroup that never waits.
+// group reducer then publishes NaN totals) and sets bit 0 of the workspace's sticky status word
+// (dauc_surrogate_status reads it), and the epoch still advances. Nothing waits on a workgroup
+// that waits: every row a reducer needs comes from a workgroup that never waits.
 // Fixed summation order: bitwise reproducible.
 constexpr int kGran = 10;                   // granules per row / group total
 constexpr int kMaxPolls = 1 << 22;
 
 struct TailWs {
     unsigned* epoch;               // the workspace's epoch word (kEpochOffset, the same for every B)
+    unsigned* status;              // the sticky status word (kStatusOffset): bit 0 = a poll timed out
     unsigned long long* rows;      // [nblocks][kGran]
     unsigned long long* gtot;      // [R][kGran]
 };
@@ -549,12 +551,18 @@ inline size_t tail_ws_bytes(int64_t nblocks, int R) {
 // other B's rows or two-launch region last held.
 constexpr size_t kEpochOffset = 128;
 static_assert(kEpochOffset + sizeof(unsigned) <= kCounterBytes, "the epoch word lives in the counter line");
+// the sticky status word, next to it: set by a reducer that gave up waiting, cleared only by the
+// caller (dauc_surrogate_status)
+constexpr size_t kStatusOffset = 132;
+constexpr unsigned kStatusTimeout = 1u;
+static_assert(kStatusOffset + sizeof(unsigned) <= kCounterBytes, "the status word lives in the counter line");
 
 // ws = the whole workspace; the rows start at `offset` (tail_offset(nblocks) + kTailHeader)
 inline TailWs tail_ws(void* ws, size_t offset, int64_t nblocks) {
     char* p = static_cast<char*>(ws) + offset;
     TailWs w;
     w.epoch = reinterpret_cast<unsigned*>(static_cast<char*>(ws) + kEpochOffset);
+    w.status = reinterpret_cast<unsigned*>(static_cast<char*>(ws) + kStatusOffset);
     w.rows = reinterpret_cast<unsigned long long*>(p + kTailHeader);
     w.gtot = w.rows + nblocks * kGran;
     return w;
@@ -627,8 +635,10 @@ __device__ __forceinline__ bool wait_row(const unsigned long long* row, unsigned
 // streaming time (~K / 190 us at 2^26) before the last row: after the last row lands one hop is
 // left. PLAIN: the epoch is read with a plain load (every read of it precedes the final's store; a
 // later call reads it across the kernel boundary). REDUCE = false: the stream with its row stores
-// and nobody reducing (a timing variant; its rows carry a tag no call expects, bit 30 set).
-template <typename YT, int S, int R, int K, bool PLAIN, int WAVES = 1, bool REDUCE = true>
+// and nobody reducing (a timing variant; its rows carry a tag no call expects, bit 30 set). FAULT
+// (tuning builds' variant 23, a test of the timeout path): streaming workgroup nblocks / 2 does not
+// publish its row.
+template <typename YT, int S, int R, int K, bool PLAIN, int WAVES = 1, bool REDUCE = true, bool FAULT = false>
 __global__ __launch_bounds__(kThreads, WAVES) void surrogate_tail_x_kernel(
     const float* __restrict__ h, const YT* __restrict__ y, int64_t B, int64_t nblocks, double invB,
     const float* __restrict__ abalpha, const float* __restrict__ p_hat, float* __restrict__ dh, TailWs ws,
@@ -644,6 +654,7 @@ __global__ __launch_bounds__(kThreads, WAVES) void surrogate_tail_x_kernel(
     if (b < nblocks) {
         const SurrogateScalars s = make_scalars_v(sa, sb, sal, sp, invB);
         const double v = stream_chunk<YT, false, S>(h, y, B, s, dh, gran_total(threadIdx.x < kGran ? threadIdx.x : 0));
+        if (FAULT && b == nblocks / 2) return;
         publish_granule(ws.rows + b * kGran, tag, v);
         return;
     }
@@ -707,6 +718,8 @@ __global__ __launch_bounds__(kThreads, WAVES) void surrogate_tail_x_kernel(
     if (!ok) {
 #pragma unroll
         for (int k = 0; k < kNumAcc; ++k) tot[k] = __builtin_nan("");
+        // reported, not only NaN: the caller tells a timed-out reduction from a diverged loss
+        if (threadIdx.x == 0) atomicOr(ws.status, kStatusTimeout);
     }
     if (!final_red) {
         double v = tot[0];
@@ -748,14 +761,14 @@ inline size_t tail_offset(int64_t nblocks) {
     return kPersistentBytes + (chunk_region_bytes(nblocks) + 255) / 256 * 256;
 }
 
-template <typename YT, int R, int K, bool PLAIN, int WAVES = 1, bool REDUCE = true>
+template <typename YT, int R, int K, bool PLAIN, int WAVES = 1, bool REDUCE = true, bool FAULT = false>
 int launch_tail_x(const float* h, const YT* y, int64_t B, const float* abalpha, const float* p_hat, float* dh,
                   double* out64, float* grad3, float* loss, void* ws, size_t ws_bytes, hipStream_t st) {
     const int64_t nblocks = chunk_blocks(B);
     if (nblocks + R > 0x7fffffffLL) return DAUC_EINVAL;
     if (ws == nullptr || ws_bytes < tail_offset(nblocks) + tail_ws_bytes(nblocks, R)) return DAUC_EINVAL;
     const TailWs w = tail_ws(ws, tail_offset(nblocks), nblocks);
-    hipLaunchKernelGGL((surrogate_tail_x_kernel<YT, kChunkSlots, R, K, PLAIN, WAVES, REDUCE>),
+    hipLaunchKernelGGL((surrogate_tail_x_kernel<YT, kChunkSlots, R, K, PLAIN, WAVES, REDUCE, FAULT>),
                        dim3(static_cast<unsigned>(nblocks + R)), dim3(kThreads), 0, st, h, y, B, nblocks,
                        1.0 / static_cast<double>(B), abalpha, p_hat, dh, w, out64, grad3, loss);
     return launch_status();
@@ -824,6 +837,7 @@ int launch_surrogate(const float* h, int64_t hs, const YT* y, int64_t B, const f
                 case 3: return launch_chunk<YT, false>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, sums4, accumulate, ws, ws_bytes, st, false);
                 case 20: return launch_tail_x<YT, kTailXReducers, kTailFinalRows, true, 8>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, ws, ws_bytes, st);
                 case 22: return launch_tail_x<YT, kTailXReducers, kTailFinalRows, true, 8, false>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, ws, ws_bytes, st);
+                case 23: return launch_tail_x<YT, kTailXReducers, kTailFinalRows, true, 8, true, true>(h, y, B, abalpha, p_hat, dh, out64, grad3, loss, ws, ws_bytes, st);
                 default: return DAUC_EINVAL;
             }
         }
@@ -1021,13 +1035,28 @@ int dauc_surrogate_fwdbwd_variant(const float* h, int64_t h_stride, const void* 
                                   double* out64, float* grad3, float* loss, void* workspace,
                                   size_t workspace_bytes, int variant, dauc_stream_t stream) {
     if (B <= 0 || h == nullptr || y == nullptr || abalpha == nullptr || p_hat == nullptr ||
-        h_stride <= 0 || (dh != nullptr && dh_stride <= 0) || variant < 0 || variant > 22)
+        h_stride <= 0 || (dh != nullptr && dh_stride <= 0) || variant < 0 || variant > 23)
         return DAUC_EINVAL;
     return dispatch_labels<false>(h, h_stride, y, y_dtype, B, abalpha, p_hat, dh, dh_stride, out64,
                                   grad3, loss, nullptr, 0, workspace, workspace_bytes,
                                   as_hip(stream), variant);
 }
 #endif
+
+int dauc_surrogate_status(void* workspace, size_t workspace_bytes, unsigned* status_out, int clear,
+                          dauc_stream_t stream) {
+    if (workspace == nullptr || status_out == nullptr || workspace_bytes < kStatusOffset + sizeof(unsigned))
+        return DAUC_EINVAL;
+    hipStream_t st = as_hip(stream);
+    unsigned* word = reinterpret_cast<unsigned*>(static_cast<char*>(workspace) + kStatusOffset);
+    hipError_t e;
+    if ((e = hipMemcpyAsync(status_out, word, sizeof(unsigned), hipMemcpyDeviceToHost, st)) != hipSuccess ||
+        (e = hipStreamSynchronize(st)) != hipSuccess)
+        return -static_cast<int>(e);
+    if (clear && *status_out != 0u && (e = hipMemsetAsync(word, 0, sizeof(unsigned), st)) != hipSuccess)
+        return -static_cast<int>(e);
+    return DAUC_OK;
+}
 
 int dauc_class_sums(const float* h, int64_t h_stride, const void* y, int y_dtype, int64_t B,
                     double* sums4, int accumulate, void* workspace, size_t workspace_bytes,

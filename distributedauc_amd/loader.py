@@ -7,6 +7,12 @@ ImageNet's shape: a label per sample index (class 0..num_classes-1) and
 images generated directly in HBM (N(0,1) noise plus a small class-dependent
 signal, so the AUC actually moves). Only the int64 label indices cross PCIe,
 through pinned memory and non-blocking copies.
+
+The signal is +-``signal`` on channel 0 by class. With ``flip`` > 0 a fixed fraction of the
+samples (chosen by a hash of the sample index, so an image keeps its sign in every epoch and on
+every rank) carries the OTHER class's sign: no model can see through it, so the best achievable
+test AUC is 1 - flip (a score that only reads the sign) instead of 1, and a trained model's AUC
+lands between chance and that ceiling (bench.py's in-training evaluation).
 """
 from __future__ import annotations
 
@@ -42,6 +48,29 @@ def imagenet_like_labels(n: int = IMAGENET_LEN, num_classes: int = 1000, split_i
     return np.where(is_pos, pos_cls, neg_cls).astype(np.int64)
 
 
+def flipped(indices: np.ndarray, flip: float) -> np.ndarray:
+    """Which samples carry the other class's sign: a multiplicative hash of the sample index
+    (Knuth's 2654435761), below ``flip`` * 2^32 -- a fixed fraction ``flip`` of the indices."""
+    if flip <= 0:
+        return np.zeros(len(indices), bool)
+    h = (np.asarray(indices, dtype=np.uint64) * np.uint64(2654435761)) & np.uint64(0xFFFFFFFF)
+    return h < np.uint64(int(flip * 2 ** 32))
+
+
+def signal_auc_ceiling(indices: np.ndarray, labels: np.ndarray, split_index: int, flip: float) -> float:
+    """The exact AUC of the best possible score on these samples -- the sign each image carries
+    (1 for +, 0 for -, ties counted half as sklearn does): 1 - flip in expectation."""
+    pos = np.asarray(labels)[np.asarray(indices)] > split_index
+    plus = pos ^ flipped(indices, flip)
+    P, N = int(pos.sum()), int((~pos).sum())
+    if P == 0 or N == 0:
+        return float("nan")
+    a, b = int((plus & pos).sum()), int((plus & ~pos).sum())  # + signs among positives / negatives
+    wins = a * (N - b)
+    ties = a * b + (P - a) * (N - b)
+    return (2 * wins + ties) / (2 * P * N)
+
+
 class SyntheticImageNet:
     """Index -> (image spec, class label). Images are materialised per batch on the device."""
 
@@ -68,7 +97,7 @@ class DeviceLoader:
 
     def __init__(self, dataset: SyntheticImageNet, indices: Sequence[int], batch_size: int, device,
                  seed: int = 0, shuffle: bool = True, channels_last: bool = True, signal: float = 0.25,
-                 pool: int = 0, drop_last: bool = False):
+                 pool: int = 0, drop_last: bool = False, flip: float = 0.0):
         self.ds = dataset
         self.indices = np.asarray(indices, dtype=np.int64)
         if self.indices.size == 0:
@@ -79,6 +108,7 @@ class DeviceLoader:
         self.shuffle = shuffle
         self.channels_last = channels_last
         self.signal = signal
+        self.flip = float(flip)
         self.drop_last = drop_last
         self.gen = torch.Generator(device=self.device)
         self.gen.manual_seed(seed)
@@ -100,11 +130,17 @@ class DeviceLoader:
 
     def _make(self, idx: np.ndarray):
         R = self.ds.image_size
-        lab_host = torch.from_numpy(self.ds.labels[idx]).pin_memory()
+        lab_host = torch.from_numpy(self.ds.labels[idx])
+        if self.device.type == "cuda":
+            lab_host = lab_host.pin_memory()
         labels = lab_host.to(self.device, non_blocking=True)
         x = torch.randn((len(idx), 3, R, R), generator=self.gen, device=self.device, dtype=torch.float32)
         if self.signal:
-            sign = torch.where(labels > self.ds.split_index, 1.0, -1.0).to(torch.float32)
+            if self.flip > 0:
+                plus = (self.ds.labels[idx] > self.ds.split_index) ^ flipped(idx, self.flip)
+                sign = torch.from_numpy(np.where(plus, 1.0, -1.0).astype(np.float32)).to(self.device)
+            else:
+                sign = torch.where(labels > self.ds.split_index, 1.0, -1.0).to(torch.float32)
             x[:, 0].add_(sign.view(-1, 1, 1), alpha=self.signal)
         if self.channels_last:
             x = x.contiguous(memory_format=torch.channels_last)

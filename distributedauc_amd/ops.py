@@ -136,7 +136,8 @@ def surrogate_fwdbwd(h: torch.Tensor, y: torch.Tensor, abalpha: torch.Tensor, p_
 
     ``variant`` != 0 runs a measured alternative from the tuning build (include/dauc_tuning.h:
     1 persistent kernel, 2 two-launch form, 3 stream alone, 20 the one-launch kernel at any unit-stride
-    B, 22 its stream with the row stores and no reduce)."""
+    B, 22 its stream with the row stores and no reduce, 23 variant 20 with one row never published:
+    the timeout path, for tests). ``surrogate_status`` reports a timed-out reduction."""
     B = _check_vec(h, y)
     dev = h.device
     yc = _label_code(y)
@@ -173,6 +174,30 @@ def surrogate_fwdbwd(h: torch.Tensor, y: torch.Tensor, abalpha: torch.Tensor, p_
                                              _ptr(dh), dh_stride, _ptr(out64), _ptr(grad3), _ptr(loss), _ptr(ws),
                                              ws.numel(), int(variant), _stream(dev))
     check(rc, "dauc_surrogate_fwdbwd")
+
+
+SURROGATE_TIMEOUT = 1  # dauc_surrogate_status bit 0
+
+
+def surrogate_status(device, *, clear: bool = True, variant: int = 0, raise_on_error: bool = False) -> int:
+    """The sticky status word of this stream's loss workspace (dauc_surrogate_status: a BLOCKING
+    read). 0 = every loss call since the last clear completed its reduction; bit 0 = a reducer of
+    the one-launch loss (B >= 2^22) timed out and that call returned NaN -- a failed reduction, not
+    a diverged loss. ``raise_on_error`` raises DaucError instead of returning a nonzero word."""
+    dev = torch.device(device)
+    L = _lib.load() if variant == 0 else _lib.tuning()
+    key = (dev.index, torch.cuda.current_stream(dev).cuda_stream, threading.get_ident(),
+           "surrogate" if variant == 0 else "surrogate_tuning")
+    ws = workspaces._ws.get(key)
+    if ws is None:
+        return 0  # no loss call on this stream yet
+    out = ctypes.c_uint(0)
+    check(L.dauc_surrogate_status(_ptr(ws), ws.numel(), ctypes.byref(out), int(bool(clear)), _stream(dev)),
+          "dauc_surrogate_status")
+    if raise_on_error and out.value:
+        raise _lib.DaucError(f"dauc_surrogate_fwdbwd: a reducer of the one-launch loss timed out (status "
+                             f"{out.value:#x}); the affected call's loss and gradients are NaN")
+    return out.value
 
 
 def class_sums(h: torch.Tensor, y: torch.Tensor, sums4: torch.Tensor, accumulate: bool = True) -> None:
@@ -589,7 +614,7 @@ def set_search_mode(mode: int) -> None:
 __all__ = [
     "GradSeg", "label_map_phat", "surrogate_fwdbwd", "class_sums", "alpha_from_sums", "pd_update",
     "pd_update_dense", "coda_finalize", "scale_div", "split_scores", "pair_count", "auc_counts_sorted",
-    "surrogate_logits_fwdbwd", "class_sums_logits",
+    "surrogate_logits_fwdbwd", "class_sums_logits", "surrogate_status",
     "sort_keys", "auc_counts_sorted_labeled", "compact_positives", "mode_code", "workspaces", "set_search_mode",
     "set_direct_fault",
     "auc_eval_enqueue",

@@ -99,6 +99,16 @@ int dauc_surrogate_fwdbwd(const float* h, int64_t h_stride, const void* y, int y
                           size_t workspace_bytes, dauc_stream_t stream);
 
 /*
+ * The sticky status of a surrogate workspace (a BLOCKING call: it synchronises `stream` and reads
+ * one word into the HOST *status_out): 0 = every dauc_surrogate_fwdbwd on this workspace since the
+ * last clear completed its reduction; bit 0 set = a reducer of the one-launch loss (unit-stride
+ * batches of 2^22 or more) gave up waiting for a row, and that call's F and gradients are NaN --
+ * a failed reduction, not a diverged loss. clear != 0 resets the word (the library never does).
+ */
+int dauc_surrogate_status(void* workspace, size_t workspace_bytes, unsigned* status_out, int clear,
+                          dauc_stream_t stream);
+
+/*
  * Replaces the stage-start alpha estimate of main.py:166-188 (per batch):
  *   sums4 (+)= { sum h[y=-1], #{y=-1}, sum h[y=1], #{y=1} }       (fp64 [4])
  * accumulate != 0 adds into sums4, otherwise overwrites it.

@@ -23,10 +23,12 @@ extern "C" {
  * (dh only: no reduce, no scalar outputs), 20 the product's one-launch kernel (128 extra reducer
  * workgroups, the final one taking the last 512 rows itself) at any unit-stride B, 22 = 20 with its
  * reducers returning at once (the stream and its tagged row stores alone, no scalar outputs: the
- * in-launch hand-off's cost by difference). The other numbers of rounds 2-3 (round 2's 64 streaming
+ * in-launch hand-off's cost by difference), 23 = 20 with streaming workgroup nblocks / 2 never
+ * publishing its row (the reducers' bounded wait times out: NaN outputs and the workspace's status
+ * bit, dauc_surrogate_status; seconds of polling -- a test of the timeout path only). The other numbers of rounds 2-3 (round 2's 64 streaming
  * reducers, the early-reducer form, other R / K, stamps; profiles/r03/a) were removed in round 4.
- * Variants 2..22 need unit strides, 16-byte aligned h/dh and int8 labels.
- * Every variant returns bitwise-identical dh and counts; the fp64 sums agree to rounding.
+ * Variants 2..23 need unit strides, 16-byte aligned h/dh and int8 labels.
+ * Every variant but 23 returns bitwise-identical dh and counts; the fp64 sums agree to rounding.
  */
 int dauc_surrogate_fwdbwd_variant(const float* h, int64_t h_stride, const void* y, int y_dtype, int64_t B,
                                   const float* abalpha, const float* p_hat, float* dh, int64_t dh_stride,

@@ -257,6 +257,43 @@ def test_surrogate_tail_alternating_batch_sizes(dev):
         assert first[B][4] == np.sum(yn == 1) and first[B][5] == np.sum(yn == -1)
 
 
+@pytest.mark.timeout(120)
+def test_surrogate_timeout_reports_status(dev):
+    """a reducer of the one-launch loss that gives up waiting (tuning variant 23:
+    one streaming workgroup never publishes its row; the bounded poll takes seconds) makes that
+    call's outputs NaN AND sets the workspace's sticky status bit, which dauc_surrogate_status
+    reports (ops.surrogate_status: the value, or DaucError with raise_on_error) and clears; a good
+    call on the same workspace before and after is exact with status 0."""
+    from distributedauc_amd import _lib, ops
+
+    B = 1 << 22
+    g = torch.Generator(device=dev).manual_seed(11)
+    h = torch.rand(B, device=dev, generator=g)
+    y = torch.where(torch.rand(B, device=dev, generator=g) < 0.1, 1, -1).to(torch.int8)
+    ab, p = torch.tensor([0.1, -0.2, 0.3], device=dev), torch.tensor([0.1], device=dev)
+
+    def call(variant):
+        out64 = torch.zeros(6, dtype=torch.float64, device=dev)
+        dh = torch.empty(B, device=dev)
+        ops.surrogate_fwdbwd(h, y, ab, p, dh=dh, out64=out64, variant=variant)
+        return out64.cpu().numpy(), dh
+
+    good, dh0 = call(20)
+    assert np.isfinite(good).all() and ops.surrogate_status(dev, variant=20) == 0
+    bad, _ = call(23)
+    assert np.isnan(bad[:4]).all(), bad
+    assert ops.surrogate_status(dev, variant=20, clear=False) == ops.SURROGATE_TIMEOUT  # sticky
+    with pytest.raises(_lib.DaucError, match="timed out"):
+        ops.surrogate_status(dev, variant=20, raise_on_error=True)  # reads and clears
+    assert ops.surrogate_status(dev, variant=20) == 0
+    again, dh1 = call(20)
+    assert np.array_equal(again, good) and torch.equal(dh0, dh1)
+    assert ops.surrogate_status(dev, variant=20) == 0
+    # the product library's own workspace: a clean run reports 0
+    ops.surrogate_fwdbwd(h, y, ab, p, out64=torch.zeros(6, dtype=torch.float64, device=dev))
+    assert ops.surrogate_status(dev, raise_on_error=True) == 0
+
+
 def test_surrogate_timing_variants_leave_no_current_rows(dev):
     """The tuning build's stream-only variant of the tail kernel (22) stores its rows but
     reduce nothing, so the epoch does not advance: their rows carry a tag no call expects. A
@@ -746,13 +783,12 @@ def test_auc_eval_enqueue_records(dev):
 
 @pytest.mark.parametrize("ldtype", [np.int8, np.int32, np.int64])
 def test_auc_eval_bucketed_ranges(dev, ldtype):
-    """The range-bucketed count (auc_bucket.hip: plan -> split -> prefix -> count) against the C
-    oracle where its bookkeeping is stressed: one range (few positives) and the most ranges the
-    index allows (~220 k positives, 18+ ranges); every query in ONE range (negatives packed into a
-    narrow interval: one range's runs carry all the work, many count chunks of one range); queries
-    in top buckets with no positive at all (their cell is the next used bucket's first); queries
-    below / above every positive; a misaligned score slice (scalar split path) and misaligned
-    labels; parts with ragged bounds (G = 3, 7)."""
+    """The count-index evaluation against the C oracle on distributions that once stressed round
+    3's range-bucketed count (removed; the cases stay for the count index and its cell map): few
+    positives and ~220 k positives (near the index's capacity); every query in one narrow
+    interval; queries in top buckets with no positive at all (their cell is the next used bucket's
+    first); queries below / above every positive; a misaligned score slice and misaligned labels;
+    parts with ragged bounds (G = 3, 7)."""
     from distributedauc_amd import ops
 
     rng = np.random.default_rng(404)
