@@ -22,11 +22,10 @@ every rank compact the positives of its slice of the labels into a slot,
 all-gathers the slots (every rank then holds the whole positive table), builds the
 count index from them, counts the next rank's slice of the scores, and all-gathers
 the parts' 8-word records (two collectives, one host read, no host synchronisation
-before the read); each record carries a check of the queried slice's labels and
-positive scores against the slot the next rank compacted from it, and of the
-length every slot was built for. The result does not depend on G. A mismatch raises
-RuntimeError on every rank together, after the collective; the negatives' scores are
-not compared across ranks.
+before the read); each record carries a check of the queried slice's labels
+against the slot the next rank compacted from it, and of the length every slot was
+built for. The result does not depend on G. A mismatch raises RuntimeError on every
+rank together, after the collective; the scores are not compared across ranks.
 
 Error behaviour mirrors sklearn: non-finite scores raise ValueError; labels
 with more than two distinct values raise ValueError; a single class returns NaN
@@ -151,11 +150,10 @@ class ExactAUC:
         parts' 8-word records, and ONE host read of the gathered records. P and the label counts
         come from the gathered slots, so they are the same on every rank by construction; what the
         ranks could disagree on is checked through record word 4 instead: every rank's query pass
-        compares its own labels (and its positives' scores, by a key sum) over the next rank's slice
-        with the slot that rank compacted from it, and every gather compares the length each slot
-        was built for. A mismatch raises RuntimeError on every rank together, after the collective
+        compares the positives its own labels give over the next rank's slice with the slot that
+        rank compacted from it, and every build compares the length each slot was built for. A mismatch raises RuntimeError on every rank together, after the collective
         (the slot size does not depend on n, so differing lengths cannot desynchronise the gather).
-        The negatives' scores are not compared across ranks. With reduce=False each rank evaluates
+        The scores are not compared across ranks (that would take a second pass over them). With reduce=False each rank evaluates
         its part against all the positives itself (no collective, no check)."""
         if not self.collective or (self.reduce and s.numel() < self.shard_min):
             self.last_mode = "single" if not self.collective else "replicated"
@@ -190,9 +188,9 @@ class ExactAUC:
                 raise RuntimeError("ExactAUC: the ranks passed test sets of different lengths: every rank must "
                                    "pass the same scores and labels")
             if any(c & 0xFFFFFFFF for c in check):
-                raise RuntimeError("ExactAUC: the ranks' parts disagree on the test set (labels or positive scores "
-                                   "of a slice differ between the rank that compacted it and the rank that queried "
-                                   "it): every rank must pass the same scores and labels")
+                raise RuntimeError("ExactAUC: the ranks' parts disagree on the test set (the labels of a slice "
+                                   "differ between the rank that compacted it and the rank that queried it): every "
+                                   "rank must pass the same scores and labels")
         P, nonfinite, other = vals[0][3], vals[0][5], vals[0][6]
         verdicts = {v[7] for v in vals} - {0}
         N = n - P

@@ -538,16 +538,15 @@ __global__ __launch_bounds__(kCmpThreads) void compact_write_kernel(
 // SLOTS groups of 16 labels per thread: 8 (a 32768-label tile) for small inputs; 32 (131072) for
 // large ones, where the reservation atomics of 4096 tiles on one address serialise (2^27 labels:
 // 65 us at 8 slots). HIST: hist_out += the top-bucket histogram of the positives' keys (an LDS
-// histogram per tile, its used buckets added once). The two-step evaluation's slots (HIST) also
-// take ksum (nullable, one u32) += the positives' keys mod 2^32, and block 0 writes put_val to
-// *put (nullable): the slot header's length word.
+// histogram per tile, its used buckets added once). Block 0 writes put_val to *put (nullable: the
+// two-step evaluation's slot header length word).
 template <typename LT, int SLOTS, int THREADS = kCmpThreads, bool HIST = false>
 __global__ __launch_bounds__(THREADS) void compact_unordered_kernel(
     const float* __restrict__ s, const LT* __restrict__ lab, int64_t n, int vec, float* __restrict__ pos_out,
     unsigned long long* __restrict__ stats, unsigned long long tag, unsigned long long* __restrict__ zero_next,
     unsigned long long next_tag, unsigned long long* __restrict__ zero3, unsigned* __restrict__ zero_w,
-    int nzero_w, int64_t cap, unsigned* __restrict__ hist_out, unsigned* __restrict__ ksum,
-    unsigned long long* __restrict__ put, unsigned long long put_val) {
+    int nzero_w, int64_t cap, unsigned* __restrict__ hist_out, unsigned long long* __restrict__ put,
+    unsigned long long put_val) {
     constexpr int kW = THREADS / kWave;
     constexpr int64_t kTileU = int64_t(THREADS) * 16 * SLOTS;
     __shared__ int wtot[2][kW];
@@ -636,7 +635,6 @@ __global__ __launch_bounds__(THREADS) void compact_unordered_kernel(
     __syncthreads();
     if (tile == 0) return;
     int64_t r = int64_t(base_s) + before + incl - np;
-    unsigned ks = 0u;
 #pragma unroll 1
     for (int k = 0; k < SLOTS; ++k) {
         const int64_t i = base + (int64_t(k) * THREADS + threadIdx.x) * 16;
@@ -646,20 +644,10 @@ __global__ __launch_bounds__(THREADS) void compact_unordered_kernel(
             nf += !isfinite(v);
             if (r < cap) pos_out[r] = v;  // past `cap`: counted in stats[0], not stored (the caller's overflow)
             ++r;
-            if constexpr (HIST) {
-                const unsigned x = key_fast(v);
-                ks += x;
-                atomicAdd(&hs[x >> kCiLowBits], 1u);
-            }
+            if constexpr (HIST) atomicAdd(&hs[key_fast(v) >> kCiLowBits], 1u);
         }
     }
     if (nf) atomicAdd(stats + 2, static_cast<unsigned long long>(nf));
-    if constexpr (HIST) {
-        if (ksum != nullptr) {
-            ks = static_cast<unsigned>(wave_sum(static_cast<unsigned long long>(ks)));
-            if ((threadIdx.x & (kWave - 1)) == 0 && ks) atomicAdd(ksum, ks);
-        }
-    }
     if constexpr (HIST) {
         __syncthreads();
         for (int i = threadIdx.x; i < kCiTop; i += THREADS)
@@ -935,7 +923,7 @@ int compact_positives_zeroing(const float* scores, const void* labels, int label
 int compact_unordered(const float* scores, const void* labels, int label_dtype, int64_t n, float* pos_out,
                       unsigned long long* stats, unsigned long long tag, unsigned long long* zero_next,
                       unsigned long long next_tag, unsigned long long* zero3, unsigned* zero_w, int nzero_w,
-                      hipStream_t st, int64_t cap, unsigned* hist_out, unsigned* ksum, unsigned long long* put,
+                      hipStream_t st, int64_t cap, unsigned* hist_out, unsigned long long* put,
                       unsigned long long put_val) {
     if (n <= 0 || scores == nullptr || labels == nullptr || pos_out == nullptr || stats == nullptr ||
         zero_next == nullptr)
@@ -955,18 +943,17 @@ int compact_unordered(const float* scores, const void* labels, int label_dtype, 
         using LT = std::remove_const_t<std::remove_pointer_t<decltype(lab)>>;
         if (wide && hist_out != nullptr)
             hipLaunchKernelGGL((compact_unordered_kernel<LT, 32, kWideThreads, true>), grid, block, 0, st, scores, lab,
-                               n, vec, pos_out, stats, tag, zero_next, next_tag, zero3, zero_w, nzero_w, cap, hist_out, ksum, put,
-                               put_val);
+                               n, vec, pos_out, stats, tag, zero_next, next_tag, zero3, zero_w, nzero_w, cap, hist_out, put, put_val);
         else if (wide)
             hipLaunchKernelGGL((compact_unordered_kernel<LT, 32, kWideThreads>), grid, block, 0, st, scores, lab, n, vec,
-                               pos_out, stats, tag, zero_next, next_tag, zero3, zero_w, nzero_w, cap, hist_out, ksum, put, put_val);
+                               pos_out, stats, tag, zero_next, next_tag, zero3, zero_w, nzero_w, cap, hist_out, put, put_val);
         else if (hist_out != nullptr)
             hipLaunchKernelGGL((compact_unordered_kernel<LT, kCmpSlots, kCmpThreads, true>), grid, block, 0, st, scores,
                                lab, n, vec, pos_out, stats, tag, zero_next, next_tag, zero3, zero_w, nzero_w, cap,
-                               hist_out, ksum, put, put_val);
+                               hist_out, put, put_val);
         else
             hipLaunchKernelGGL((compact_unordered_kernel<LT, kCmpSlots>), grid, block, 0, st, scores, lab, n, vec,
-                               pos_out, stats, tag, zero_next, next_tag, zero3, zero_w, nzero_w, cap, hist_out, ksum, put, put_val);
+                               pos_out, stats, tag, zero_next, next_tag, zero3, zero_w, nzero_w, cap, hist_out, put, put_val);
         return launch_status();
     };
     switch (label_dtype) {

@@ -211,22 +211,23 @@ int counts_part_blocking(const float* scores, const void* labels, int label_dtyp
 // ---- the sharded evaluation in two steps: each rank compacts only its slice -----------------
 //
 // Step 1 (dauc_auc_eval_compact_part): rank r compacts the positives of ITS slice of the labels
-// into a slot: a 256-byte header {P_r, 0, #non-finite positives, #labels outside {-1, 1}, n, the
-// positives' keys summed mod 2^32} (u64 words), the top-bucket histogram of its positives' keys
-// (count_index.h, 2048 u32) and room for `cap` scores. The caller all-gathers the slots (one
-// collective). Step 2 (dauc_auc_eval_query_part): the gathered slots are concatenated into the
-// evaluation's positive table on the device (their headers and histograms summed), the count index
-// is built from it -- without its histogram pass -- and the scores of the NEXT rank's slice are
-// counted (rank r queries slice (r + 1) % parts): the record is dauc_auc_eval_enqueue's, with word 4
-// a consistency check -- this rank's labels over that slice against the slot the next rank
-// compacted from it (low 32 bits: (P + key sum) of that slot - (positives + their key sum) seen by
-// this rank's query pass, mod 2^32; high 32 bits: the number of slots built for another n). A slot
+// (and zeroes the per-cell counters of step 2's build in its workspace) into a slot: a 256-byte
+// header {P_r, 0, #non-finite positives, #labels outside {-1, 1}, n} (u64 words), the top-bucket
+// histogram of its positives' keys (count_index.h, 2048 u32) and room for `cap` scores. The caller
+// all-gathers the slots (one collective). Step 2 (dauc_auc_eval_query_part): the count index is
+// built from the gathered slots read in place (the count pass sums their headers and histograms --
+// no histogram pass -- and copies each key to the table's position array as it counts it: no
+// gather launch), and the scores of the NEXT rank's slice are counted (rank r queries slice
+// (r + 1) % parts): the record is dauc_auc_eval_enqueue's, with word 4 a consistency check -- this
+// rank's labels over that slice against the slot the next rank compacted from it (low 32 bits: the
+// P of that slot - the positives this rank's labels give over it, mod 2^32; high 32 bits: the
+// number of slots built for another n). A slot
 // holds an even share of the index's capacity plus 25 %, whatever n (so ranks called with different
 // n still gather equal sizes and report the mismatch instead of hanging in the collective): a rank
 // whose slice holds more positives (unshuffled test sets) overflows, and the evaluation reports
 // verdict 2 (the caller's blocking sorted path), as it does for tables the index cannot hold.
 constexpr size_t kSlotHist = 256, kSlotHdr = kSlotHist + size_t(kCiTop) * 4;
-constexpr int kSlotN = 4, kSlotKeySum = 5;  // header words
+constexpr int kSlotN = 4;  // header word: the n the slot was built for
 
 int64_t slot_cap(int parts) {
     const int64_t fair = (direct_capacity(INT64_MAX / 4) + parts - 1) / parts;
@@ -246,93 +247,6 @@ int64_t query_lo(int64_t n, int part, int parts) { return slice_lo(n, (part + 1)
 int64_t query_hi(int64_t n, int part, int parts) {
     const int q = (part + 1) % parts;
     return slice_lo(n, q + 1, parts);
-}
-
-// kGatherBlocks workgroups per slot (blockIdx.y = the slot): the slot's scores to table[sum of the
-// earlier slots' P, ...) (one workgroup per slot copied a 2-rank slot of 67 k scores in ~60 us);
-// workgroup (0, 0) sums the headers into the evaluation's counters, zeroes the query's counts and
-// the verdict (no memset launch) and sets the record's check word (the queried slot's P + key sum
-// - the slice length, which the query pass brings back to zero; the slots built for another n in
-// its high half); the first workgroups sum the slots' histograms into the build's `hist`, and all
-// of them zero its per-cell counters (the histogram pass's other job). m_eff = P, or (any slot
-// overflowed) a size the index refuses, so the build reports verdict 2 (the histogram's bucket 0
-// gets that size added: its total is the build's M).
-constexpr int kGatherBlocks = 32;
-__global__ __launch_bounds__(256) void gather_slots_kernel(const unsigned char* __restrict__ slots, size_t sbytes,
-                                                           int parts, int part, int64_t n, int64_t qlen,
-                                                           int64_t cap, int64_t mcap,
-                                                           float* __restrict__ table,
-                                                           unsigned long long* __restrict__ stats,
-                                                           unsigned long long* __restrict__ m_eff,
-                                                           unsigned* __restrict__ hist,
-                                                           unsigned* __restrict__ cnt, int64_t ncnt,
-                                                           unsigned long long* __restrict__ wt,
-                                                           unsigned* __restrict__ verdict) {
-    __shared__ unsigned long long off_s;
-    __shared__ bool over_s;
-    const int slot = blockIdx.y;
-    const bool first = blockIdx.x == 0 && slot == 0;
-    if (first) {
-        if (threadIdx.x < 3) wt[threadIdx.x] = 0ull;
-        if (threadIdx.x == 0) *reinterpret_cast<unsigned long long*>(verdict) = 0ull;  // record word 7
-    }
-    auto hdr0 = [&](int r) { return reinterpret_cast<const unsigned long long*>(slots + size_t(r) * sbytes); };
-    if (first && threadIdx.x == 64) {
-        // record word 4 (stats + 1): low half = the queried slot's P + key sum - the slice length
-        // (mod 2^32; the query pass adds its queries and subtracts its positives' keys), high half =
-        // the slots written for a length other than this call's n
-        const unsigned long long* q = hdr0((part + 1) % parts);
-        unsigned mism = 0u;
-        for (int r = 0; r < parts; ++r) mism += hdr0(r)[kSlotN] != static_cast<unsigned long long>(n);
-        const unsigned lo = static_cast<unsigned>(q[0]) + static_cast<unsigned>(q[kSlotKeySum]) -
-                            static_cast<unsigned>(qlen);
-        stats[1] = (static_cast<unsigned long long>(mism) << 32) | lo;
-    }
-    const int64_t lb = int64_t(slot) * kGatherBlocks + blockIdx.x;
-    for (int64_t i = lb * 256 + threadIdx.x; i < ncnt; i += int64_t(256) * kGatherBlocks * gridDim.y) cnt[i] = 0u;
-    auto hdr = [&](int r) { return reinterpret_cast<const unsigned long long*>(slots + size_t(r) * sbytes); };
-    if (threadIdx.x < kWave) {
-        // wave 0: the prefix of the slots' P before this one, and (workgroup 0) the totals
-        unsigned long long before = 0, P = 0, nf = 0, other = 0;
-        bool over = false;
-        for (int r = threadIdx.x; r < parts; r += kWave) {
-            const unsigned long long* h = hdr(r);
-            before += r < slot ? h[0] : 0ull;
-            P += h[0];
-            nf += h[2];
-            other += h[3];
-            over |= h[0] > static_cast<unsigned long long>(cap);
-        }
-        before = wave_sum(before);
-        P = wave_sum(P);
-        nf = wave_sum(nf);
-        other = wave_sum(other);
-        over = __ballot(over) != 0ull;
-        if (threadIdx.x == 0) {
-            off_s = before;
-            over_s = over;
-            if (first) {
-                stats[0] = P;
-                stats[2] = nf;
-                stats[3] = other;
-                *m_eff = over ? static_cast<unsigned long long>(mcap) + 1ull : P;
-            }
-        }
-    }
-    __syncthreads();
-    if (lb * 256 + threadIdx.x < kCiTop) {
-        const int i = static_cast<int>(lb * 256 + threadIdx.x);
-        unsigned h = i == 0 && over_s ? static_cast<unsigned>(mcap) + 1u : 0u;
-        for (int r = 0; r < parts; ++r)
-            h += reinterpret_cast<const unsigned*>(slots + size_t(r) * sbytes + kSlotHist)[i];
-        hist[i] = h;
-    }
-    const unsigned long long Pr = hdr(slot)[0];
-    const unsigned long long off = off_s;
-    if (Pr > static_cast<unsigned long long>(cap) || off + Pr > static_cast<unsigned long long>(mcap)) return;
-    const float* src = reinterpret_cast<const float*>(slots + size_t(slot) * sbytes + kSlotHdr);
-    for (unsigned long long i = blockIdx.x * 256ull + threadIdx.x; i < Pr; i += 256ull * kGatherBlocks)
-        table[off + i] = src[i];
 }
 
 }  // namespace
@@ -370,20 +284,23 @@ int dauc_auc_eval_compact_part(const float* scores, const void* labels, int labe
     if ((e = hipMemsetAsync(hdr, 0, kSlotHdr, st)) != hipSuccess) return -static_cast<int>(e);  // + histogram
     const int64_t lo = slice_lo(n, part, parts), hi = slice_lo(n, part + 1, parts);
     if (hi <= lo) {
-        // an empty slice: P_r = 0, the length word still set (its two halves)
+        // an empty slice: P_r = 0, the length word still set (its two halves), and the query step's
+        // per-cell counters zeroed (the compaction's job otherwise)
         auto* nw = reinterpret_cast<unsigned*>(hdr + kSlotN);
         const unsigned long long nv = static_cast<unsigned long long>(n);
         if ((e = hipMemsetD32Async(nw, static_cast<int>(nv & 0xffffffffull), 1, st)) != hipSuccess ||
-            (e = hipMemsetD32Async(nw + 1, static_cast<int>(nv >> 32), 1, st)) != hipSuccess)
+            (e = hipMemsetD32Async(nw + 1, static_cast<int>(nv >> 32), 1, st)) != hipSuccess ||
+            (e = hipMemsetAsync(direct_cnt_ptr(w.tws, direct_capacity(n)), 0, size_t(direct_cnt_words()) * 4, st)) !=
+                hipSuccess)
             return -static_cast<int>(e);
         return DAUC_OK;
     }
     const size_t lsz = label_dtype == DAUC_LABEL_I8 ? 1 : label_dtype == DAUC_LABEL_I32 ? 4 : 8;
     return compact_unordered(scores + lo, static_cast<const char*>(labels) + size_t(lo) * lsz, label_dtype, hi - lo,
                              reinterpret_cast<float*>(static_cast<char*>(slot) + kSlotHdr), hdr, 0ull, w.spare, 0ull,
-                             nullptr, nullptr, 0, st, slot_cap(parts),
-                             reinterpret_cast<unsigned*>(static_cast<char*>(slot) + kSlotHist),
-                             reinterpret_cast<unsigned*>(hdr + kSlotKeySum), hdr + kSlotN,
+                             nullptr, direct_cnt_ptr(w.tws, direct_capacity(n)), static_cast<int>(direct_cnt_words()),
+                             st, slot_cap(parts),
+                             reinterpret_cast<unsigned*>(static_cast<char*>(slot) + kSlotHist), hdr + kSlotN,
                              static_cast<unsigned long long>(n));
 }
 
@@ -402,26 +319,16 @@ int dauc_auc_eval_query_part(const float* scores, const void* labels, int label_
     hipStream_t st = as_hip(stream);
     const EvalWs w = with_record(eval_ws(workspace, n), part_out);
     const int64_t mcap = direct_capacity(n);
-    unsigned* hist = reinterpret_cast<unsigned*>(static_cast<char*>(w.tws) + direct_hist_offset(mcap));
-    // zeroes the counts and the verdict (the record's other words are written), and hands the
-    // build its histogram and zeroed per-cell counters
-    static_assert(int64_t(kGatherBlocks) * 256 >= kCiTop, "one slot's workgroups cover the histogram");
     const int64_t qlo = query_lo(n, part, parts), qhi = query_hi(n, part, parts);
-    hipLaunchKernelGGL(gather_slots_kernel, dim3(kGatherBlocks, static_cast<unsigned>(parts)), dim3(256), 0, st,
-                       static_cast<const unsigned char*>(slots), slot_bytes(parts), parts, part, n, qhi - qlo,
-                       slot_cap(parts), mcap, w.pos, w.slot, w.spare, hist, direct_cnt_ptr(w.tws, mcap),
-                       direct_cnt_words(), w.wt, w.verdict);
-    int rc = launch_status();
-    if (rc) return rc;
-    if (qhi > qlo) {
-        // the build and the query see m_eff (w.spare[0]): P, or past the index's capacity on overflow;
-        // the query pass brings the record's check word (its low half) back to zero
-        rc = counts_labeled_direct(w.pos, w.spare, mcap, scores, labels, label_dtype, qlo, qhi, w.wt, w.wt + 2,
-                                   w.verdict, w.tws, w.tws_bytes, st, hist,
-                                   reinterpret_cast<unsigned*>(part_out + 4));
-        if (rc) return rc;
-    }
-    return DAUC_OK;
+    // the build reads the gathered slots in place (no gather copy): its count pass sums their
+    // headers and histograms, writes this part's record (counts zeroed, P, the check word, the
+    // label counts) and m_eff (w.spare[0]: P, or past the index's capacity on an overflow); the
+    // query pass brings the check word's low half back to zero
+    SlotSource src{static_cast<const unsigned char*>(slots), slot_bytes(parts), kSlotHist, kSlotHdr, parts, part,
+                   slot_cap(parts), n, qhi - qlo, w.wt, w.slot, reinterpret_cast<unsigned long long*>(w.verdict),
+                   w.spare};
+    return counts_labeled_direct_slots(src, w.pos, mcap, scores, labels, label_dtype, qlo, qhi, w.wt, w.wt + 2,
+                                       w.verdict, w.tws, w.tws_bytes, st, reinterpret_cast<unsigned*>(part_out + 4));
 }
 
 int dauc_auc_eval_counts(const float* scores, const void* labels, int label_dtype, int64_t n, int64_t* out,

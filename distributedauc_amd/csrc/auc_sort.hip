@@ -885,10 +885,11 @@ __device__ __forceinline__ void ci_fix(unsigned x, unsigned rl, unsigned cnt, co
 // returns at once when the builder kept the tree, so it is enqueued unconditionally. Per
 // iteration every slot's window loads are issued BEFORE the next iteration's stream loads:
 // vmcnt retires loads in issue order, so a wait for a window would otherwise also wait out a
-// streaming load's HBM latency. CHECK (the two-step evaluation): *check += #queries - the sum of
-// the keys of the scores labeled 1, mod 2^32, over [begin, end) -- also when the index is not used
-// (the pass then only reads the range for it) -- so the caller can compare the range's positives
-// with the ones another rank compacted from it.
+// streaming load's HBM latency. CHECK (the two-step evaluation): *check += #queries over [begin,
+// end) (mod 2^32) -- also when the index is not used (the pass then only reads the range for it) --
+// so the caller can compare the range's positives with the ones another rank compacted from it.
+// The loop runs at the 128-VGPR bound of 4 waves per SIMD, so the query count rides in the high
+// half of the non-finite counter (per lane both stay far below 2^16): no extra register.
 template <typename LT, bool CHECK = false>
 __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __restrict__ s,
                                                                 const LT* __restrict__ lab, int64_t begin,
@@ -911,19 +912,28 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
             unsigned nf = 0u, chk = 0u;
             for (int64_t i = begin + int64_t(blockIdx.x) * kQueryThreads + threadIdx.x; i < end;
                  i += int64_t(gridDim.x) * kQueryThreads) {
-                const float v = s[i];
                 if (lab[i] != LT(1)) {
-                    nf += !isfinite(v);
+                    nf += !isfinite(s[i]);
                     chk += 1u;
-                } else {
-                    chk -= key_fast(v);
                 }
             }
+            // one atomic per workgroup and word (per-wave atomics on one address serialise)
+            __shared__ unsigned long long red2[2][kQueryThreads / kWave];
             const unsigned long long nfw = wave_sum(static_cast<unsigned long long>(nf));
-            const unsigned ck = static_cast<unsigned>(wave_sum(static_cast<unsigned long long>(chk)));
+            const unsigned long long ckw = wave_sum(static_cast<unsigned long long>(chk));
             if ((threadIdx.x & (kWave - 1)) == 0) {
-                if (nfw && nonfinite != nullptr) atomicAdd(nonfinite, nfw);
-                if (ck) atomicAdd(check, ck);
+                red2[0][threadIdx.x / kWave] = nfw;
+                red2[1][threadIdx.x / kWave] = ckw;
+            }
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                unsigned long long bn = 0, bc = 0;
+                for (int i = 0; i < kQueryThreads / kWave; ++i) {
+                    bn += red2[0][i];
+                    bc += red2[1][i];
+                }
+                if (bn && nonfinite != nullptr) atomicAdd(nonfinite, bn);
+                if (bc) atomicAdd(check, static_cast<unsigned>(bc));
             }
             return;
         }
@@ -975,16 +985,14 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
     __syncthreads();
     const unsigned M32 = static_cast<unsigned>(M);
     unsigned long long w = 0, t = 0;
-    unsigned nf = 0;
-    unsigned chk = 0u;  // CHECK: #queries - sum of the positives' keys (mod 2^32)
+    unsigned nf = 0;  // CHECK: + #queries << 16
     const int64_t a0 = (begin + 3) & ~int64_t(3);
     const int64_t head = a0 < end ? a0 : end;
     const int64_t stride = int64_t(gridDim.x) * kQueryThreads;
     const int64_t tid = int64_t(blockIdx.x) * kQueryThreads + threadIdx.x;
     auto one = [&](int64_t i) {
-        if constexpr (CHECK) chk += lab[i] != LT(1) ? 1u : 0u - key_fast(s[i]);
         if (lab[i] != LT(1)) {
-            nf += !isfinite(s[i]);
+            nf += !isfinite(s[i]) + (CHECK ? 0x10000u : 0u);
             const unsigned x = key_fast(s[i]);
             unsigned rl, cnt, wl = 0u, tl = 0u;
             uint4 k;
@@ -1015,7 +1023,6 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
         struct Stream {
             f32x4 f[U];
             LabelWords<LT> l[U];
-            unsigned valid;  // CHECK: bit u = slot u is in range
         };
         // Every load of the loop is issued unconditionally (out-of-range slots re-read slot 0 and are
         // masked; a lane without a window reads the table's first one): a load under a branch
@@ -1029,10 +1036,6 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
                 sg.f[u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(s + i));
                 sg.l[u].load(lab + i);
                 if (v >= nvec) sg.l[u].set_positive();
-                if constexpr (CHECK) {
-                    if (u == 0) sg.valid = 0u;
-                    sg.valid |= unsigned(v < nvec) << u;
-                }
             }
         };
         // one group in flight: its keys, rank_lo | count << 28 (rank_lo < 2^28: M <= 2^27 here),
@@ -1054,11 +1057,10 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
                     g.use |= unsigned(use) << (4 * u + q);
                     g.x[4 * u + q] = key_fast(f[q]);
                     nf += use && !isfinite(f[q]);
-                    if constexpr (CHECK)
-                        chk -= !use && ((sg.valid >> u) & 1u) ? g.x[4 * u + q] : 0u;
                 }
             }
-            if constexpr (CHECK) chk += __builtin_popcount(g.use);
+            // (a slot past the end loads as positive: no use bit, so it counts no query)
+            if constexpr (CHECK) nf += static_cast<unsigned>(__builtin_popcount(g.use)) << 16;
         };
         // phase by phase over the group, so that every query's LDS read of a phase is issued before
         // the first wait (a per-query chain with its conditional window load in between keeps the
@@ -1184,31 +1186,37 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
             for (int q = 0; q < 4; ++q) one(head + v * 4 + q);
     }
     for (int64_t i = head + nvec * 4 + tid; i < end; i += stride) one(i);
-    __shared__ unsigned long long red[3][kQueryThreads / kWave];
+    // one atomic per workgroup and word: per-wave atomics on one address serialise across the
+    // XCDs (~15 ns each: 4096 of them cost ~60 us)
+    __shared__ unsigned long long red[CHECK ? 4 : 3][kQueryThreads / kWave];
     w = wave_sum(w);
     t = wave_sum(t);
-    const unsigned long long nfw = wave_sum(static_cast<unsigned long long>(nf));
     const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+    unsigned long long ckw = 0;
     if constexpr (CHECK) {
-        const unsigned ck = static_cast<unsigned>(wave_sum(static_cast<unsigned long long>(chk)));
-        if (lane == 0 && ck) atomicAdd(check, ck);
+        ckw = wave_sum(static_cast<unsigned long long>(nf >> 16));
+        nf &= 0xffffu;
     }
+    const unsigned long long nfw = wave_sum(static_cast<unsigned long long>(nf));
     if (lane == 0) {
         red[0][wid] = w;
         red[1][wid] = t;
         red[2][wid] = nfw;
+        if constexpr (CHECK) red[CHECK ? 3 : 0][wid] = ckw;
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-        unsigned long long bw = 0, bt = 0, bn = 0;
+        unsigned long long bw = 0, bt = 0, bn = 0, bc = 0;
         for (int i = 0; i < kQueryThreads / kWave; ++i) {
             bw += red[0][i];
             bt += red[1][i];
             bn += red[2][i];
+            if constexpr (CHECK) bc += red[CHECK ? 3 : 0][i];
         }
         if (bw) atomicAdd(out + 0, bw);
         if (bt) atomicAdd(out + 1, bt);
         if (bn && nonfinite) atomicAdd(nonfinite, bn);
+        if (CHECK && bc) atomicAdd(check, static_cast<unsigned>(bc));
     }
 }
 
@@ -1329,6 +1337,155 @@ __global__ __launch_bounds__(kDirectThreads) void direct_count_kernel(const floa
     }
 }
 
+// The two-step evaluation's count pass straight from the gathered slots (the gather copy folded
+// in): every workgroup sums the slots' headers (wave 0: the stored scores' prefix per slot) and
+// their histograms (two top buckets per thread), computes the plan as direct_count_kernel does,
+// and counts its keys -- each key read from its slot, copied to the table position array `pos`
+// (the scatter's input) with its cell. Workgroup 0 also writes the plan, the verdict words, the
+// part's record (counts zeroed, P, the check word, the label counts) and m_eff (P, or past the
+// index's capacity when a slot overflowed, so the plan refuses the table: verdict 2).
+constexpr int kSlotCountThreads = 1024;
+__global__ __launch_bounds__(kSlotCountThreads) void direct_count_slots_kernel(SlotSource src, int64_t mcap,
+                                                                              uint2* __restrict__ l1g,
+                                                                              unsigned* __restrict__ meta,
+                                                                              unsigned* __restrict__ cnt,
+                                                                              unsigned* __restrict__ cell,
+                                                                              float* __restrict__ pos) {
+    static_assert(kCiTop == 2 * kSlotCountThreads, "two top buckets per thread");
+    __shared__ uint2 l1[kCiTop];
+    __shared__ unsigned wtot[kSlotCountThreads / kWave];
+    __shared__ unsigned totals[3];
+    __shared__ unsigned long long off[kMaxSlotParts + 1];  // stored scores before slot r
+    __shared__ unsigned long long hs[5];                   // P, #non-finite, #other, overflow, check
+    const int parts = src.parts;
+    const int lane = threadIdx.x & (kWave - 1);
+    auto hdr = [&](int r) { return reinterpret_cast<const unsigned long long*>(src.slots + size_t(r) * src.sbytes); };
+    const unsigned long long cap = static_cast<unsigned long long>(src.cap);
+    if (threadIdx.x < kWave) {
+        unsigned long long run = 0, P = 0, nf = 0, other = 0, mism = 0;
+        bool over = false;
+        for (int r0 = 0; r0 < parts; r0 += kWave) {
+            const int r = r0 + lane;
+            unsigned long long stored = 0;
+            if (r < parts) {
+                const unsigned long long* h = hdr(r);
+                const unsigned long long pr = h[0];
+                P += pr;
+                nf += h[2];
+                other += h[3];
+                mism += h[4] != static_cast<unsigned long long>(src.n);
+                over |= pr > cap;
+                stored = pr < cap ? pr : cap;
+            }
+            unsigned long long inc = stored;
+#pragma unroll
+            for (int d = 1; d < kWave; d <<= 1) {
+                const unsigned long long t = __shfl_up(inc, d, kWave);
+                if (lane >= d) inc += t;
+            }
+            if (r < parts) off[r] = run + inc - stored;
+            run += __shfl(inc, kWave - 1, kWave);
+        }
+        P = wave_sum(P);
+        nf = wave_sum(nf);
+        other = wave_sum(other);
+        mism = wave_sum(mism);
+        over = __ballot(over) != 0ull;
+        if (lane == 0) {
+            off[parts] = run;
+            hs[0] = P;
+            hs[1] = nf;
+            hs[2] = other;
+            hs[3] = over ? 1ull : 0ull;
+            // the check word: the queried slot's P - the range length (low half, mod 2^32; the
+            // query pass adds its queries), the slots built for another n (high half)
+            const unsigned long long* q = hdr((src.part + 1) % parts);
+            const unsigned lo = static_cast<unsigned>(q[0]) - static_cast<unsigned>(src.qlen);
+            hs[4] = (mism << 32) | lo;
+        }
+    }
+    // the summed histogram: buckets 2t, 2t + 1 (an overflow adds past-capacity keys to bucket 0)
+    unsigned n0 = 0u, n1 = 0u;
+    for (int r = 0; r < parts; ++r) {
+        const uint2 v = reinterpret_cast<const uint2*>(src.slots + size_t(r) * src.sbytes + src.hist_off)[threadIdx.x];
+        n0 += v.x;
+        n1 += v.y;
+    }
+    __syncthreads();
+    const bool over = hs[3] != 0ull;
+    if (threadIdx.x == 0 && over) n0 += static_cast<unsigned>(mcap) + 1u;
+    unsigned used = (n0 != 0u) + (n1 != 0u);
+    used = block_incl_scan1024<false>(used, wtot);
+    if (threadIdx.x == kSlotCountThreads - 1) totals[0] = used;
+    const unsigned keys = block_incl_scan1024<false>(n0 + n1, wtot);
+    if (threadIdx.x == kSlotCountThreads - 1) totals[2] = keys;
+    __syncthreads();
+    const int64_t M = totals[2];
+    const int64_t avail = int64_t(kCiMaxCells) - int64_t(totals[0]);
+    const int64_t num = avail < 2 * M ? avail : 2 * M;
+    const unsigned C0 = n0 ? static_cast<unsigned>((int64_t(n0) * num + M - 1) / M) : 0u;
+    const unsigned C1 = n1 ? static_cast<unsigned>((int64_t(n1) * num + M - 1) / M) : 0u;
+    const unsigned incl = block_incl_scan1024<false>(C0 + C1, wtot);
+    if (threadIdx.x == kSlotCountThreads - 1) totals[1] = incl;
+    const unsigned run = incl - (C0 + C1);
+    l1[2 * threadIdx.x] = uint2{run, C0};
+    l1[2 * threadIdx.x + 1] = uint2{run + C0, C1};
+    __syncthreads();
+    const unsigned total = totals[1];
+    const bool ok = num > 0 && 3 * num >= 2 * M && total <= static_cast<unsigned>(kCiMaxCells) && M <= mcap;
+    const unsigned long long P = hs[0];
+    if (blockIdx.x == 0) {
+        l1g[2 * threadIdx.x] = l1[2 * threadIdx.x];
+        l1g[2 * threadIdx.x + 1] = l1[2 * threadIdx.x + 1];
+        if (threadIdx.x == 0) {
+            meta[kCiOk] = ok ? 1u : 0u;
+            meta[kCiCells] = total;
+            meta[kCiBlocks] = (total + 1 + kCiBlock - 1) / kCiBlock;
+            meta[kCiSkew] = 0u;
+            *src.m_eff = over ? static_cast<unsigned long long>(mcap) + 1ull : P;
+        } else if (threadIdx.x < 4) {
+            src.wt[threadIdx.x - 1] = 0ull;
+        } else if (threadIdx.x == 4) {
+            *src.verdict = 0ull;
+        } else if (threadIdx.x < 9) {
+            const int k = threadIdx.x - 5;  // stats: P, check, #non-finite, #other
+            src.stats[k] = k == 0 ? P : k == 1 ? hs[4] : hs[k];
+        }
+    }
+    if (!ok) return;
+    const int64_t Mk = static_cast<int64_t>(P);  // no overflow here: every positive is stored
+    for (int64_t i0 = int64_t(blockIdx.x) * kSlotCountThreads; i0 < Mk;
+         i0 += int64_t(gridDim.x) * kSlotCountThreads) {
+        const int64_t i = i0 + threadIdx.x;
+        const bool live = i < Mk;
+        unsigned c = 0u;
+        if (live) {
+            // the slot holding key i: the last r with off[r] <= i (binary search over the prefix)
+            int lo = 0, hi = parts;  // off[lo] <= i < off[hi]
+            while (hi - lo > 1) {
+                const int mid = (lo + hi) >> 1;
+                if (off[mid] <= static_cast<unsigned long long>(i)) lo = mid;
+                else hi = mid;
+            }
+            const float v = reinterpret_cast<const float*>(src.slots + size_t(lo) * src.sbytes + src.data_off)
+                [i - static_cast<int64_t>(off[lo])];
+            pos[i] = v;
+            const unsigned x = key_fast(v);
+            c = ci_cell(x, l1[x >> kCiLowBits]);
+            cell[i] = c;
+        }
+        const unsigned long long act = __ballot(live);
+        if (act == 0ull) continue;
+        const int first = __ffsll(static_cast<long long>(act)) - 1;
+        const unsigned cf = __shfl(c, first, kWave);
+        if (__ballot(live && c == cf) == act) {
+            if (lane == first) atomicAdd(cnt + cf, static_cast<unsigned>(__popcll(act)));
+        } else if (live) {
+            atomicAdd(cnt + c, 1u);
+        }
+    }
+}
+
 // One thread per block of 8 cells, one workgroup per group of 256 blocks: blk[b] = {the table
 // keys before block b within its group, the 8 cells' counts as nibbles}, grp[g] = the group's
 // keys; a count of 15 or more marks the table skewed. The consumers add the groups' prefix
@@ -1368,8 +1525,17 @@ __global__ __launch_bounds__(kDirectThreads) void direct_scatter_kernel(const fl
                                                                         unsigned* __restrict__ meta,
                                                                         unsigned* __restrict__ cnt,
                                                                         const unsigned* __restrict__ cell,
-                                                                        unsigned* __restrict__ table) {
-    if (meta[kCiOk] == 0u || meta[kCiSkew] != 0u) return;
+                                                                        unsigned* __restrict__ table,
+                                                                        int64_t ncnt) {
+    if (meta[kCiOk] == 0u) return;  // nothing was counted: the counters are still zero
+    if (meta[kCiSkew] != 0u) {
+        // a skewed table: no scatter, but the counters go back to zero for the next build (the
+        // scatter of a good build counts them down to zero itself)
+        for (int64_t i = int64_t(blockIdx.x) * kDirectThreads + threadIdx.x; i < ncnt;
+             i += int64_t(gridDim.x) * kDirectThreads)
+            cnt[i] = 0u;
+        return;
+    }
     const int64_t M = static_cast<int64_t>(*Mp);
     __shared__ unsigned pre[kDirectMaxGroups];
     group_prefix(grp, (static_cast<int>(meta[kCiBlocks]) + kDirectGroup - 1) / kDirectGroup, pre);
@@ -1820,9 +1986,48 @@ int build_direct_index(const float* pos, const unsigned long long* Mp, int64_t M
                            w.keys_b);
 #endif
     hipLaunchKernelGGL(direct_scatter_kernel, blocks(Mcap, kDirectThreads, kDirectGrid), dim3(kDirectThreads), 0, st, pos,
-                       Mp, nw.blk, grp, nw.meta, nw.cstart, w.keys_b, table);
+                       Mp, nw.blk, grp, nw.meta, nw.cstart, w.keys_b, table, kCiCntWords);
     *ix = DirectIndex{table, nw.l1, nw.blk, grp, nw.meta};
     return launch_status();
+}
+
+int counts_labeled_direct_slots(const SlotSource& src, float* pos, int64_t Mcap, const float* scores,
+                                const void* labels, int label_dtype, int64_t begin, int64_t end,
+                                unsigned long long* wins_ties, unsigned long long* nonfinite, unsigned* verdict,
+                                void* workspace, size_t workspace_bytes, hipStream_t st, unsigned* check) {
+    if (begin < 0 || end < begin || wins_ties == nullptr || pos == nullptr || src.slots == nullptr ||
+        src.parts < 1 || src.parts > kMaxSlotParts || (end > begin && (scores == nullptr || labels == nullptr)) ||
+        workspace == nullptr || Mcap < 1 || workspace_bytes < dauc_sort_workspace_size(Mcap))
+        return DAUC_EINVAL;
+    if (label_dtype != DAUC_LABEL_I8 && label_dtype != DAUC_LABEL_I32 && label_dtype != DAUC_LABEL_I64)
+        return DAUC_EINVAL;
+    const SortWs w = carve(workspace, Mcap);
+    const CountWs nw = count_ws_of(workspace, Mcap);
+    unsigned* table = w.keys_a;
+    unsigned* grp = reinterpret_cast<unsigned*>(after_tree_of(workspace, Mcap));
+    const int64_t gk = (Mcap + kSlotCountThreads - 1) / kSlotCountThreads;
+    hipLaunchKernelGGL(direct_count_slots_kernel, dim3(static_cast<unsigned>(gk)), dim3(kSlotCountThreads), 0, st, src,
+                       Mcap, nw.l1, nw.meta, nw.cstart, w.keys_b, pos);
+    hipLaunchKernelGGL(direct_blocks_kernel, dim3(kDirectMaxGroups), dim3(kDirectGroup), 0, st, nw.cstart, nw.meta,
+                       nw.blk, grp);
+    const int64_t gs = (Mcap + kDirectThreads - 1) / kDirectThreads;
+    hipLaunchKernelGGL(direct_scatter_kernel, dim3(static_cast<unsigned>(gs < kDirectGrid ? gs : kDirectGrid)),
+                       dim3(kDirectThreads), 0, st, pos, src.m_eff, nw.blk, grp, nw.meta, nw.cstart, w.keys_b, table,
+                       kCiCntWords);
+    int rc = launch_status();
+    if (rc || end == begin) return rc;
+    const unsigned long long* Mp = src.m_eff;
+    switch (label_dtype) {
+        case DAUC_LABEL_I8:
+            return launch_ci(scores, static_cast<const int8_t*>(labels), begin, end, nw, table, 0, wins_ties,
+                             nonfinite, st, verdict, grp, Mp, check);
+        case DAUC_LABEL_I32:
+            return launch_ci(scores, static_cast<const int32_t*>(labels), begin, end, nw, table, 0, wins_ties,
+                             nonfinite, st, verdict, grp, Mp, check);
+        default:
+            return launch_ci(scores, static_cast<const int64_t*>(labels), begin, end, nw, table, 0, wins_ties,
+                             nonfinite, st, verdict, grp, Mp, check);
+    }
 }
 
 int counts_labeled_direct(const float* pos, const unsigned long long* Mp, int64_t Mcap, const float* scores,

@@ -130,6 +130,23 @@ struct LabelWords<int8_t> {
     __device__ __forceinline__ bool not_positive(int q) const { return ((w >> (8 * q)) & 0xffu) != 1u; }
 };
 
+// The two-step sharded evaluation's gathered slots (auc_eval.hip), read in place by the direct
+// build (auc_sort.hip, direct_count_slots_kernel): slot r at slots + r * sbytes holds a header of
+// u64 words {P_r, 0, #non-finite positives, #labels outside {-1, 1}, n}, the
+// top-bucket histogram of its positives (kCiTop u32) at hist_off and at most cap scores at
+// data_off. The build's first workgroup also writes the record of the part it serves.
+struct SlotSource {
+    const unsigned char* slots;
+    size_t sbytes, hist_off, data_off;
+    int parts, part;
+    int64_t cap, n, qlen;              // qlen: the part's query range length (the check word)
+    unsigned long long* wt;            // record words 0..2: zeroed
+    unsigned long long* stats;         // record words 3..6: P, the check word, #non-finite, #other
+    unsigned long long* verdict;       // record word 7: zeroed (the query pass writes it)
+    unsigned long long* m_eff;         // the table size the scatter and the query read
+};
+constexpr int kMaxSlotParts = 1024;
+
 // The count index built straight from the unsorted positives (auc_sort.hip, build_direct_index):
 // device pointers into the caller's sort workspace.
 struct DirectIndex {

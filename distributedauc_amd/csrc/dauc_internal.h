@@ -109,12 +109,12 @@ int compact_positives_zeroing(const float* scores, const void* labels, int label
 // zero_next[0, 2, 3], sets zero_next[1] = next_tag, and zeroes zero3[0..3) (nullable); the grid
 // zeroes zero_w[0..nzero_w). At most `cap` positives are stored (stats[0] still counts them all).
 // hist_out (nullable; kCiTop words, zero on entry) += the top-bucket histogram of the positives'
-// keys (count_index.h), so a build from them can skip its histogram pass. With hist_out: ksum
-// (nullable, one u32) += the positives' keys mod 2^32; *put = put_val (put nullable, block 0).
+// keys (count_index.h), so a build from them can skip its histogram pass. *put = put_val (put
+// nullable; block 0).
 int compact_unordered(const float* scores, const void* labels, int label_dtype, int64_t n, float* pos_out,
                       unsigned long long* stats, unsigned long long tag, unsigned long long* zero_next,
                       unsigned long long next_tag, unsigned long long* zero3, unsigned* zero_w, int nzero_w,
-                      hipStream_t st, int64_t cap = INT64_MAX, unsigned* hist_out = nullptr, unsigned* ksum = nullptr,
+                      hipStream_t st, int64_t cap = INT64_MAX, unsigned* hist_out = nullptr,
                       unsigned long long* put = nullptr, unsigned long long put_val = 0ull);
 
 // auc_sort.hip: the count index built straight from the unsorted positives (no radix sort, no
@@ -139,12 +139,23 @@ struct DirectIndex;  // count_index.h
 int build_direct_index(const float* pos, const unsigned long long* Mp, int64_t Mcap, void* workspace,
                        size_t workspace_bytes, hipStream_t st, DirectIndex* ix, const unsigned* ready_hist = nullptr);
 // check (nullable, one u32; the two-step evaluation's consistency word): += #queried scores
-// (labels != 1) - sum of the keys of the scores whose label is 1, mod 2^32, over [begin, end) --
-// counted by the query pass whether or not the index held the table.
+// (labels != 1) over [begin, end), mod 2^32 -- counted by the query pass whether or not the index
+// held the table.
 int counts_labeled_direct(const float* pos, const unsigned long long* Mp, int64_t Mcap, const float* scores,
                           const void* labels, int label_dtype, int64_t begin, int64_t end,
                           unsigned long long* wins_ties, unsigned long long* nonfinite, unsigned* verdict,
                           void* workspace, size_t workspace_bytes, hipStream_t st,
                           const unsigned* ready_hist = nullptr, unsigned* check = nullptr);
+
+// the two-step evaluation's build + query straight from the gathered slots (no gather copy):
+// the count pass reads the slots in place (and writes the part's record header, count_index.h
+// SlotSource), then blocks, scatter and the labeled query over [begin, end) as above. The per-cell
+// counters must be zero on entry (dauc_auc_eval_compact_part zeroes them; a build leaves them
+// zero again).
+struct SlotSource;
+int counts_labeled_direct_slots(const SlotSource& src, float* pos, int64_t Mcap, const float* scores,
+                                const void* labels, int label_dtype, int64_t begin, int64_t end,
+                                unsigned long long* wins_ties, unsigned long long* nonfinite, unsigned* verdict,
+                                void* workspace, size_t workspace_bytes, hipStream_t st, unsigned* check);
 
 }  // namespace dauc

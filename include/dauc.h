@@ -319,19 +319,19 @@ int dauc_auc_eval_counts_part(const float* scores, const void* labels, int label
  * of 256.
  *   1. dauc_auc_eval_compact_part: the positives of THIS rank's slice compacted, unordered, into
  *      `slot` (device, dauc_auc_slot_bytes(n, parts) bytes -- the same for every n --, 256-byte
- *      aligned, outside the workspace): a header of int64 words {P_r, 0, #non-finite positives,
- *      #labels not in {-1, 1}, n, the positives' order-preserving keys summed mod 2^32} at byte 0,
- *      the top-bucket histogram of those keys (2048 uint32: key >> 21) from byte 256 and the scores
- *      from byte 8448;
+ *      aligned, outside the workspace; the per-cell counters of step 2 in `workspace` are zeroed,
+ *      so step 2 must use the same workspace): a header of int64 words {P_r, 0, #non-finite
+ *      positives, #labels not in {-1, 1}, n} at byte 0, the top-bucket histogram of the positives'
+ *      order-preserving keys (2048 uint32: key >> 21) from byte 256 and the scores from byte 8448;
  *   -- the caller all-gathers the `parts` slots, rank order, contiguous --
- *   2. dauc_auc_eval_query_part: the gathered slots become the positive table (headers and
- *      histograms summed), the count index is built from it and the scores of the NEXT rank's
- *      slice, (part + 1) % parts, are counted straight into part_out (device int64[8], 8-byte
- *      aligned, outside the workspace and the slots; DAUC_EINVAL otherwise) =
- *      dauc_auc_eval_enqueue's record, except word 4, a consistency check that is 0 when the ranks
- *      agree: low 32 bits = (P + key sum) of the queried slice's slot - (positives + their key sum)
- *      this rank's labels and scores give over that slice, mod 2^32; high 32 bits = the number of
- *      slots built for another n. A slot holds an even share of the count index's capacity + 25 %:
+ *   2. dauc_auc_eval_query_part: the count index is built from the gathered slots read in place
+ *      (headers and histograms summed) and the scores of the NEXT rank's slice, (part + 1) %
+ *      parts, are counted straight into part_out (device int64[8], 8-byte aligned, outside the
+ *      workspace and the slots; DAUC_EINVAL otherwise) = dauc_auc_eval_enqueue's record, except
+ *      word 4, a consistency check that is 0 when the ranks agree: low 32 bits = the P of the
+ *      queried slice's slot - the positives this rank's labels give over that slice, mod 2^32;
+ *      high 32 bits = the number of slots built for another n (parts <= 1024). A slot holds an
+ *      even share of the count index's capacity + 25 %:
  *      a slice with more positives (an unshuffled test set), like a table the index cannot hold,
  *      gives verdict 2 -- the caller then runs dauc_auc_eval_counts_part on every rank.
  * Replaces the reference's rank-0 evaluation (main.py:232-250) with a sharded one.

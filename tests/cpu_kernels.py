@@ -209,17 +209,15 @@ def _query_range(n, part, parts):
 
 def auc_eval_compact_part(scores, labels, part, parts, slot):
     """dauc_auc_eval_compact_part's stand-in: header {P_r, 0, #non-finite positives, #other labels,
-    n, the positives' keys summed mod 2^32} (int64) at byte 0, the positives' top-bucket histogram
-    from byte 256, the slice's positive scores (in order) from byte 8448, at most cap of them."""
+    n} (int64) at byte 0, the positives' top-bucket histogram from byte 256, the slice's positive
+    scores (in order) from byte 8448, at most cap of them."""
     s, y = scores.detach().numpy(), labels.numpy().astype(np.int64)
     n = s.size
     lo, hi = _slice_lo(n, part, parts), _slice_lo(n, part + 1, parts)
     ss, yy = s[lo:hi], y[lo:hi]
     pos = ss[yy == 1]
-    ksum = int(_keys(pos).astype(np.uint64).sum()) & 0xFFFFFFFF
-    hdr = np.array([pos.size, 0, int((~np.isfinite(pos)).sum()), int(((yy != 1) & (yy != -1)).sum()), n, ksum],
-                   np.int64)
-    slot[:48] = torch.from_numpy(hdr.view(np.uint8).copy())
+    hdr = np.array([pos.size, 0, int((~np.isfinite(pos)).sum()), int(((yy != 1) & (yy != -1)).sum()), n], np.int64)
+    slot[:40] = torch.from_numpy(hdr.view(np.uint8).copy())
     slot[_SLOT_HIST:_SLOT_HDR] = torch.from_numpy(_top_buckets(pos).view(np.uint8).copy())
     k = min(pos.size, _slot_cap(parts))
     slot[_SLOT_HDR:_SLOT_HDR + 4 * k] = torch.from_numpy(pos[:k].astype(np.float32).view(np.uint8).copy())
@@ -229,8 +227,8 @@ def auc_eval_compact_part(scores, labels, part, parts, slot):
 def auc_eval_query_part(scores, labels, part, parts, slots, out=None):
     """dauc_auc_eval_query_part's stand-in: the gathered slots' positives (verdict 2 when a slot
     overflowed or the table exceeds the index), the next part's slice counted, the record's check
-    word (low half: the queried slot's P + key sum - this rank's positives + key sum over that slice,
-    mod 2^32; high half: slots built for another n); the enqueue record otherwise."""
+    word (low half: the queried slot's P - this rank's positives over that slice, mod 2^32; high
+    half: slots built for another n); the enqueue record otherwise."""
     s, y = scores.detach().numpy(), labels.numpy().astype(np.int64)
     n = s.size
     nb, cap = auc_slot_bytes(n, parts), _slot_cap(parts)
@@ -240,7 +238,7 @@ def auc_eval_query_part(scores, labels, part, parts, slots, out=None):
     pos = []
     hdrs = []
     for r in range(parts):
-        h = raw[r * nb:r * nb + 48].view(np.int64)
+        h = raw[r * nb:r * nb + 40].view(np.int64)
         hdrs.append(h)
         P, nfpos, other = P + int(h[0]), nfpos + int(h[2]), other + int(h[3])
         over |= int(h[0]) > cap
@@ -253,8 +251,7 @@ def auc_eval_query_part(scores, labels, part, parts, slots, out=None):
     qh = hdrs[(part + 1) % parts]
     mism = sum(int(h[4]) != n for h in hdrs)
     yq, sq = y[lo:hi], s[lo:hi]
-    seen_pos = yq == 1
-    low = (int(qh[0]) + int(qh[5]) - int(seen_pos.sum()) - int(_keys(sq[seen_pos]).astype(np.uint64).sum())) & 0xFFFFFFFF
+    low = (int(qh[0]) - int((yq == 1).sum())) & 0xFFFFFFFF
     rec[4] = (mism << 32) | low
     if hi <= lo:
         return rec

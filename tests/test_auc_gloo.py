@@ -64,13 +64,6 @@ def _worker(rank, world, port, q, shard_min):
                 y3[neg[(neg > 10_000) & (neg < 13_000)][:4]] = 1
             with pytest.raises(RuntimeError, match="disagree"):
                 ev.counts(torch.from_numpy(y3), torch.from_numpy(s), device="cpu")
-            # a positive's score differs on one rank (same labels): the slot's key sum catches it
-            s3 = s.copy()
-            if rank == world - 1:
-                j = int(np.flatnonzero(y == 1)[-1])
-                s3[j] = np.float32(s3[j] + 0.5)
-            with pytest.raises(RuntimeError, match="disagree"):
-                ev.counts(torch.from_numpy(y), torch.from_numpy(s3), device="cpu")
             # ranks called with different lengths: equal slot sizes, so the gather completes and
             # every rank raises
             m = n if rank == 0 else n - 300

@@ -989,7 +989,7 @@ def test_auc_eval_slot_layout(dev, n, G):
         want = cpu_kernels.auc_eval_compact_part(torch.from_numpy(s), torch.from_numpy(y), r, G,
                                                  torch.zeros(nb, dtype=torch.uint8))
         g, w = got.cpu().numpy(), want.numpy()
-        assert np.array_equal(g[:48], w[:48]), r  # P, 0, non-finite, other, n, key sum
+        assert np.array_equal(g[:40], w[:40]), r  # P, 0, non-finite, other, n
         assert np.array_equal(g[256:8448], w[256:8448]), r
         k = int(w[:8].view(np.int64)[0])
         gp, wp = g[8448:8448 + 4 * k].view(np.uint32), w[8448:8448 + 4 * k].view(np.uint32)
