@@ -905,6 +905,9 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
                                                                 unsigned* __restrict__ check) {
     const bool in_use = count_index_in_use(meta);
     if (Mp != nullptr) M = static_cast<int64_t>(*Mp);  // the direct build: the table size on the device
+    // the end-of-kernel reduction's rows (W, T, #non-finite, CHECK: #queries); static LDS on top of
+    // the index's 163,232 dynamic bytes: the 160 KB limit leaves room for 4 rows, no more
+    __shared__ unsigned long long red[CHECK ? 4 : 3][kQueryThreads / kWave];
     if (verdict != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *verdict = in_use ? 1u : 2u;
     if (!in_use) {
         if constexpr (CHECK) {
@@ -918,19 +921,18 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
                 }
             }
             // one atomic per workgroup and word (per-wave atomics on one address serialise)
-            __shared__ unsigned long long red2[2][kQueryThreads / kWave];
             const unsigned long long nfw = wave_sum(static_cast<unsigned long long>(nf));
             const unsigned long long ckw = wave_sum(static_cast<unsigned long long>(chk));
             if ((threadIdx.x & (kWave - 1)) == 0) {
-                red2[0][threadIdx.x / kWave] = nfw;
-                red2[1][threadIdx.x / kWave] = ckw;
+                red[0][threadIdx.x / kWave] = nfw;
+                red[1][threadIdx.x / kWave] = ckw;
             }
             __syncthreads();
             if (threadIdx.x == 0) {
                 unsigned long long bn = 0, bc = 0;
                 for (int i = 0; i < kQueryThreads / kWave; ++i) {
-                    bn += red2[0][i];
-                    bc += red2[1][i];
+                    bn += red[0][i];
+                    bc += red[1][i];
                 }
                 if (bn && nonfinite != nullptr) atomicAdd(nonfinite, bn);
                 if (bc) atomicAdd(check, static_cast<unsigned>(bc));
@@ -1188,7 +1190,6 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
     for (int64_t i = head + nvec * 4 + tid; i < end; i += stride) one(i);
     // one atomic per workgroup and word: per-wave atomics on one address serialise across the
     // XCDs (~15 ns each: 4096 of them cost ~60 us)
-    __shared__ unsigned long long red[CHECK ? 4 : 3][kQueryThreads / kWave];
     w = wave_sum(w);
     t = wave_sum(t);
     const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
@@ -1850,6 +1851,11 @@ int launch_ci(const float* s, const LT* lab, int64_t begin, int64_t end, const C
               unsigned* check = nullptr) {
     const dim3 grid(query_grid(end - begin)), block(kQueryThreads);
     const size_t lds = (size_t(kCiTop) + kCiMaxBlocks) * 8 + (grp ? size_t(kDirectMaxGroups) * 4 : 0);
+    // dynamic + the kernel's static reduction rows must fit the CU's 160 KB of LDS (a launch past it
+    // aborts the queue: HSA_STATUS_ERROR_INVALID_ALLOCATION)
+    static_assert((size_t(kCiTop) + kCiMaxBlocks) * 8 + size_t(kDirectMaxGroups) * 4 +
+                          4 * (kQueryThreads / kWave) * 8 <= 160 * 1024,
+                  "the count-index query's LDS");
     if (check != nullptr)
         hipLaunchKernelGGL((query_ci_kernel<LT, true>), grid, block, lds, st, s, lab, begin, end, cw.meta, cw.l1,
                            cw.blk, sorted, M, out, nonfinite, verdict, grp, Mp, check);
