@@ -1450,7 +1450,7 @@ __global__ __launch_bounds__(kSlotCountThreads) void direct_count_slots_kernel(S
             *src.verdict = 0ull;
         } else if (threadIdx.x < 9) {
             const int k = threadIdx.x - 5;  // stats: P, check, #non-finite, #other
-            src.stats[k] = k == 0 ? P : k == 1 ? hs[4] : hs[k];
+            src.stats[k] = k == 0 ? P : k == 1 ? hs[4] : hs[k - 1];  // hs: P, #non-finite, #other, .., check
         }
     }
     if (!ok) return;
