@@ -1362,6 +1362,29 @@ __global__ __launch_bounds__(kSlotCountThreads) void direct_count_slots_kernel(S
     const int lane = threadIdx.x & (kWave - 1);
     auto hdr = [&](int r) { return reinterpret_cast<const unsigned long long*>(src.slots + size_t(r) * src.sbytes); };
     const unsigned long long cap = static_cast<unsigned long long>(src.cap);
+    // the summed histogram: buckets 2t, 2t + 1 -- every slot's load issued before the header work
+    // (8 loads in flight per thread: one L2 round trip, not one per slot)
+    unsigned n0 = 0u, n1 = 0u;
+    {
+        const uint2* hp = reinterpret_cast<const uint2*>(src.slots + src.hist_off) + threadIdx.x;
+        const size_t sw = src.sbytes / sizeof(uint2);
+        int r = 0;
+        for (; r + 8 <= parts; r += 8) {
+            uint2 v[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = hp[size_t(r + j) * sw];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                n0 += v[j].x;
+                n1 += v[j].y;
+            }
+        }
+        for (; r < parts; ++r) {
+            const uint2 v = hp[size_t(r) * sw];
+            n0 += v.x;
+            n1 += v.y;
+        }
+    }
     if (threadIdx.x < kWave) {
         unsigned long long run = 0, P = 0, nf = 0, other = 0, mism = 0;
         bool over = false;
@@ -1405,14 +1428,7 @@ __global__ __launch_bounds__(kSlotCountThreads) void direct_count_slots_kernel(S
             hs[4] = (mism << 32) | lo;
         }
     }
-    // the summed histogram: buckets 2t, 2t + 1 (an overflow adds past-capacity keys to bucket 0)
-    unsigned n0 = 0u, n1 = 0u;
-    for (int r = 0; r < parts; ++r) {
-        const uint2 v = reinterpret_cast<const uint2*>(src.slots + size_t(r) * src.sbytes + src.hist_off)[threadIdx.x];
-        n0 += v.x;
-        n1 += v.y;
-    }
-    __syncthreads();
+    __syncthreads();  // (an overflow adds past-capacity keys to bucket 0)
     const bool over = hs[3] != 0ull;
     if (threadIdx.x == 0 && over) n0 += static_cast<unsigned>(mcap) + 1u;
     unsigned used = (n0 != 0u) + (n1 != 0u);
