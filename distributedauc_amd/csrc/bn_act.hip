@@ -291,39 +291,24 @@ __device__ __forceinline__ void sum_partials(const float* __restrict__ partials,
     const int c = cbase + cq * 4;
     double a1[4] = {0, 0, 0, 0}, a2[4] = {0, 0, 0, 0};
     if (c < C) {
-        // kFinGroup row blocks' loads in flight per step (a load-then-add loop waited out one L2
-        // round trip per row block); the additions keep the order rb = j, j + 64, j + 128, ...
-        constexpr int kFinGroup = 4;
-        for (int rb0 = j; rb0 < nrb; rb0 += kFinGroup * kFinSubsets) {
-            f32x4 p1[kFinGroup], p2[kFinGroup], pk[kFinGroup];
+        for (int rb = j; rb < nrb; rb += kFinSubsets) {
+            const f32x4 p1 = *reinterpret_cast<const f32x4*>(partials + (int64_t(rb) * NP) * C + c);
+            const f32x4 p2 = *reinterpret_cast<const f32x4*>(partials + (int64_t(rb) * NP + 1) * C + c);
+            if (STATS) {
+                const f32x4 pk = *reinterpret_cast<const f32x4*>(partials + (int64_t(rb) * NP + 2) * C + c);
+                const int64_t r0 = int64_t(rb) * rows;
+                const double nb = double((M - r0) < rows ? (M - r0) : rows);
 #pragma unroll
-            for (int q = 0; q < kFinGroup; ++q) {
-                const int rb = rb0 + q * kFinSubsets;
-                if (rb < nrb) {
-                    p1[q] = *reinterpret_cast<const f32x4*>(partials + (int64_t(rb) * NP) * C + c);
-                    p2[q] = *reinterpret_cast<const f32x4*>(partials + (int64_t(rb) * NP + 1) * C + c);
-                    if (STATS) pk[q] = *reinterpret_cast<const f32x4*>(partials + (int64_t(rb) * NP + 2) * C + c);
+                for (int i = 0; i < 4; ++i) {
+                    const double k = pk[i], s1 = p1[i];
+                    a1[i] += s1 + nb * k;
+                    a2[i] += double(p2[i]) + 2.0 * k * s1 + nb * k * k;
                 }
-            }
+            } else {
 #pragma unroll
-            for (int q = 0; q < kFinGroup; ++q) {
-                const int rb = rb0 + q * kFinSubsets;
-                if (rb >= nrb) break;
-                if (STATS) {
-                    const int64_t r0 = int64_t(rb) * rows;
-                    const double nb = double((M - r0) < rows ? (M - r0) : rows);
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        const double k = pk[q][i], s1 = p1[q][i];
-                        a1[i] += s1 + nb * k;
-                        a2[i] += double(p2[q][i]) + 2.0 * k * s1 + nb * k * k;
-                    }
-                } else {
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        a1[i] += p1[q][i];
-                        a2[i] += p2[q][i];
-                    }
+                for (int i = 0; i < 4; ++i) {
+                    a1[i] += p1[i];
+                    a2[i] += p2[i];
                 }
             }
         }
