@@ -76,9 +76,9 @@ SIGNATURES = {
     "dauc_sort_keys": (_int, [_vp, _i64, _vp, _vp, _sz, _vp]),
     "dauc_bn_workspace_size": (_sz, [_i64, _int]),
     "dauc_bn_act_forward": (_int, [_vp, _int, _i64, _int, _vp, _int, _vp, _vp, _vp, _vp, _f32, _f32, _vp, _vp, _vp,
-                                   _vp, _sz, _vp]),
-    "dauc_bn_act_backward": (_int, [_vp, _vp, _vp, _int, _i64, _int, _int, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
-                                    _sz, _vp]),
+                                   _vp, _vp, _sz, _vp]),
+    "dauc_bn_act_backward": (_int, [_vp, _vp, _vp, _vp, _int, _i64, _int, _int, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                    _vp, _sz, _vp]),
     "dauc_maxpool2d_forward": (_int, [_vp, _int, _i64, _int, _int, _int, _int, _int, _int, _vp, _vp, _int, _int,
                                       _vp]),
     "dauc_slab_sum": (_int, [_vp, _i64, _i64, _vp, _vp]),

@@ -14,6 +14,11 @@
 // accumulated in fp32 per thread (shifted by a sample of the channel), combined in
 // fp64 in a fixed order: results are bitwise reproducible run to run.
 //
+// ReLU mask (round 5): a forward with ReLU can also write one bit per element, y > 0 as stored
+// (one byte per 16-byte vector), and the backward then reads that bit instead of the whole y for the
+// ReLU's gradient mask: 0.125 B instead of 2 (bf16) per element in both backward passes -- the BN
+// backward is HBM-bound, so this is ~2 B less traffic per element and pass.
+//
 // Geometry: a thread owns one 16-byte vector of channels (8 bf16 or 4 fp32) of
 // a channel tile of CT channels; TPR = CT / vec threads cover a row, RPB = 256 /
 // TPR rows are in flight per pass, and a workgroup walks a contiguous block of
@@ -125,6 +130,32 @@ __device__ __forceinline__ void store_vec(float* p, const float (&v)[4]) {
     *reinterpret_cast<f32x4*>(p) = u;
 }
 
+// store_vec + the ReLU mask of what was stored: bit i = (stored element i > 0), i.e. exactly the
+// backward's `y > 0` on the stored y (positive nonzero, +inf included, NaN excluded)
+__device__ __forceinline__ unsigned store_vec_mask(__hip_bfloat16* p, const float (&v)[8]) {
+    unsigned b[8], m = 0u;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        b[i] = bf16_bits(v[i]);
+        m |= unsigned(b[i] - 1u < 0x7f80u) << i;  // 1 .. 0x7f80: +denormal .. +inf
+    }
+    uint4 u;
+    u.x = b[0] | (b[1] << 16);
+    u.y = b[2] | (b[3] << 16);
+    u.z = b[4] | (b[5] << 16);
+    u.w = b[6] | (b[7] << 16);
+    *reinterpret_cast<uint4*>(p) = u;
+    return m;
+}
+
+__device__ __forceinline__ unsigned store_vec_mask(float* p, const float (&v)[4]) {
+    unsigned m = 0u;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) m |= unsigned(__float_as_uint(v[i]) - 1u < 0x7f800000u) << i;
+    store_vec(p, v);
+    return m;
+}
+
 struct Geometry {
     int N;        // elements per 16-byte vector
     int CT;       // channels per tile
@@ -161,10 +192,13 @@ int make_geometry(int64_t M, int C, int elem_bytes, Geometry& g, int threads = k
 // factor is (mean - k)^2 / var = O(1)); k is written as a third partial row.
 // Backward: g = dy * [y > 0] (RELU) or dy; s1 = sum g, s2 = sum g * (x - mean); g is
 // written to dz (the residual branch's gradient) when dz != nullptr.
-template <typename T, bool STATS, bool RELU, int TH>
+// MASK (backward with RELU): the ReLU mask comes from `mask` (one byte per 16-byte vector) instead
+// of y.
+template <typename T, bool STATS, bool RELU, int TH, bool MASK = false>
 __global__ __launch_bounds__(TH) void bn_partial_kernel(
     const T* __restrict__ x, const T* __restrict__ dy, const T* __restrict__ y, T* __restrict__ dz, int64_t M,
-    int C, int CT, int64_t rows_per_block, const float* __restrict__ center, float* __restrict__ partials) {
+    int C, int CT, int64_t rows_per_block, const float* __restrict__ center, float* __restrict__ partials,
+    const unsigned char* __restrict__ mask) {
     constexpr int N = VecT<T>::N;
     __shared__ float red[2 * TH * N];
     const int TPR = CT / N;
@@ -198,7 +232,11 @@ __global__ __launch_bounds__(TH) void bn_partial_kernel(
         } else {
             float gv[N];
             load_vec(dy + off, gv);
-            if (RELU) {
+            if (RELU && MASK) {
+                const unsigned m = mask[off / N];
+#pragma unroll
+                for (int i = 0; i < N; ++i) gv[i] = (m >> i) & 1u ? gv[i] : 0.f;
+            } else if (RELU) {
                 float yv[N];
                 load_vec(y + off, yv);
 #pragma unroll
@@ -218,12 +256,14 @@ __global__ __launch_bounds__(TH) void bn_partial_kernel(
     const int64_t step = int64_t(RPB) * U;
     for (; r + step - RPB < re; r += step) {
         RawT<T> xr[U], gr[U], yr[U];
+        unsigned mr[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int64_t off = (r + int64_t(u) * RPB) * C + c0;
             xr[u] = load_raw(x + off);
             if (!STATS) gr[u] = load_raw(dy + off);
-            if (!STATS && RELU) yr[u] = load_raw(y + off);
+            if (!STATS && RELU && MASK) mr[u] = mask[off / N];
+            else if (!STATS && RELU) yr[u] = load_raw(y + off);
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -239,7 +279,10 @@ __global__ __launch_bounds__(TH) void bn_partial_kernel(
             } else {
                 float gv[N];
                 cvt(gr[u], gv);
-                if (RELU) {
+                if (RELU && MASK) {
+#pragma unroll
+                    for (int i = 0; i < N; ++i) gv[i] = (mr[u] >> i) & 1u ? gv[i] : 0.f;
+                } else if (RELU) {
                     float yv[N];
                     cvt(yr[u], yv);
 #pragma unroll
@@ -385,11 +428,13 @@ __global__ __launch_bounds__(kFinThreads) void bn_bwd_finalize_kernel(
 // Forward apply: y = act((x - mean) * scale + beta [+ res]). Backward: dx = a*g + b*(x - mean) + c,
 // g = dz (GMODE 2), dy * [y > 0] (GMODE 1) or dy (GMODE 0).
 // HOIST: the vector count per row divides 256, so a thread's channels never change.
-template <typename T, bool BWD, int GMODE, bool RELU, bool RES, bool HOIST>
+// MASK: forward with RELU writes the ReLU mask byte of every vector; backward GMODE 1 reads it
+// instead of y (aux).
+template <typename T, bool BWD, int GMODE, bool RELU, bool RES, bool HOIST, bool MASK = false>
 __global__ __launch_bounds__(kBnThreads) void bn_elementwise_kernel(
     const T* __restrict__ x, const T* __restrict__ g_in, const T* __restrict__ aux, T* __restrict__ out,
     int64_t nvec, int CV, const float* __restrict__ p0, const float* __restrict__ p1, const float* __restrict__ p2,
-    const float* __restrict__ p3) {
+    const float* __restrict__ p3, unsigned char* __restrict__ mask) {
     constexpr int N = VecT<T>::N;
     // forward: p0 = scale, p1 = beta, aux = residual. backward: p0..p2 = a, b, c, aux = y. p3 = mean
     auto body = [&](int64_t v, const float* P0, const float* P1, const float* P2, const float* P3) {
@@ -409,7 +454,11 @@ __global__ __launch_bounds__(kBnThreads) void bn_elementwise_kernel(
         } else {
             float gv[N];
             load_vec(g_in + off, gv);
-            if (GMODE == 1) {
+            if (GMODE == 1 && MASK) {
+                const unsigned m = mask[v];
+#pragma unroll
+                for (int i = 0; i < N; ++i) gv[i] = (m >> i) & 1u ? gv[i] : 0.f;
+            } else if (GMODE == 1) {
                 float yv[N];
                 load_vec(aux + off, yv);
 #pragma unroll
@@ -418,7 +467,10 @@ __global__ __launch_bounds__(kBnThreads) void bn_elementwise_kernel(
 #pragma unroll
             for (int i = 0; i < N; ++i) o[i] = P0[i] * gv[i] + P1[i] * (xv[i] - P3[i]) + P2[i];
         }
-        store_vec(out + off, o);
+        if constexpr (!BWD && RELU && MASK)
+            mask[v] = static_cast<unsigned char>(store_vec_mask(out + off, o));
+        else
+            store_vec(out + off, o);
     };
     auto params = [&](int cv, float (&q0)[N], float (&q1)[N], float (&q2)[N], float (&q3)[N]) {
 #pragma unroll
@@ -475,9 +527,10 @@ BnWs carve(void* ws, int C) {
 
 bool aligned16p(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
-template <typename T, bool BWD, int GMODE, bool RELU, bool RES>
+template <typename T, bool BWD, int GMODE, bool RELU, bool RES, bool MASK = false>
 int launch_elementwise(const T* x, const T* g_in, const T* aux, T* out, int64_t M, int C, const float* p0,
-                       const float* p1, const float* p2, const float* p3, hipStream_t st) {
+                       const float* p1, const float* p2, const float* p3, hipStream_t st,
+                       unsigned char* mask = nullptr) {
     constexpr int N = VecT<T>::N;
     const int CV = C / N;
     const int64_t nvec = M * CV;
@@ -485,33 +538,33 @@ int launch_elementwise(const T* x, const T* g_in, const T* aux, T* out, int64_t 
     const int64_t grid = (nvec + per_block - 1) / per_block;
     if (grid > 0x7fffffffLL) return DAUC_EINVAL;
     if (kBnThreads % CV == 0)
-        hipLaunchKernelGGL((bn_elementwise_kernel<T, BWD, GMODE, RELU, RES, true>), dim3(unsigned(grid)),
-                           dim3(kBnThreads), 0, st, x, g_in, aux, out, nvec, CV, p0, p1, p2, p3);
+        hipLaunchKernelGGL((bn_elementwise_kernel<T, BWD, GMODE, RELU, RES, true, MASK>), dim3(unsigned(grid)),
+                           dim3(kBnThreads), 0, st, x, g_in, aux, out, nvec, CV, p0, p1, p2, p3, mask);
     else
-        hipLaunchKernelGGL((bn_elementwise_kernel<T, BWD, GMODE, RELU, RES, false>), dim3(unsigned(grid)),
-                           dim3(kBnThreads), 0, st, x, g_in, aux, out, nvec, CV, p0, p1, p2, p3);
+        hipLaunchKernelGGL((bn_elementwise_kernel<T, BWD, GMODE, RELU, RES, false, MASK>), dim3(unsigned(grid)),
+                           dim3(kBnThreads), 0, st, x, g_in, aux, out, nvec, CV, p0, p1, p2, p3, mask);
     return launch_status();
 }
 
-template <typename T, bool STATS, bool RELU>
+template <typename T, bool STATS, bool RELU, bool MASK = false>
 void launch_partial(int th, const Geometry& g, const T* x, const T* dy, const T* y, T* dz, int64_t M, int C,
-                    const float* center, float* partials, hipStream_t st) {
+                    const float* center, float* partials, hipStream_t st, const unsigned char* mask = nullptr) {
     const dim3 grid(g.nrb, g.ctiles);
     if (th == 1024)
-        hipLaunchKernelGGL((bn_partial_kernel<T, STATS, RELU, 1024>), grid, dim3(1024), 0, st, x, dy, y, dz, M, C,
-                           g.CT, g.rows, center, partials);
+        hipLaunchKernelGGL((bn_partial_kernel<T, STATS, RELU, 1024, MASK>), grid, dim3(1024), 0, st, x, dy, y, dz, M,
+                           C, g.CT, g.rows, center, partials, mask);
     else if (th == 512)
-        hipLaunchKernelGGL((bn_partial_kernel<T, STATS, RELU, 512>), grid, dim3(512), 0, st, x, dy, y, dz, M, C,
-                           g.CT, g.rows, center, partials);
+        hipLaunchKernelGGL((bn_partial_kernel<T, STATS, RELU, 512, MASK>), grid, dim3(512), 0, st, x, dy, y, dz, M,
+                           C, g.CT, g.rows, center, partials, mask);
     else
-        hipLaunchKernelGGL((bn_partial_kernel<T, STATS, RELU, 256>), grid, dim3(256), 0, st, x, dy, y, dz, M, C,
-                           g.CT, g.rows, center, partials);
+        hipLaunchKernelGGL((bn_partial_kernel<T, STATS, RELU, 256, MASK>), grid, dim3(256), 0, st, x, dy, y, dz, M,
+                           C, g.CT, g.rows, center, partials, mask);
 }
 
 template <typename T>
 int bn_forward_t(const T* x, int64_t M, int C, const T* res, int relu, const float* gamma, const float* beta,
-                 float* running_mean, float* running_var, float momentum, float eps, T* y, float* save_mean,
-                 float* save_invstd, void* ws, size_t ws_bytes, hipStream_t st) {
+                 float* running_mean, float* running_var, float momentum, float eps, T* y, unsigned char* mask,
+                 float* save_mean, float* save_invstd, void* ws, size_t ws_bytes, hipStream_t st) {
     Geometry g;
     const int th = part_threads();
     if (make_geometry(M, C, sizeof(T), g, th) != DAUC_OK) return DAUC_EINVAL;
@@ -523,6 +576,12 @@ int bn_forward_t(const T* x, int64_t M, int C, const T* res, int relu, const flo
                        g.rows, M, C, gamma, beta, running_mean, running_var, momentum, eps, save_mean, save_invstd, w.c0, w.c1, w.c3);
     int rc = launch_status();
     if (rc != DAUC_OK) return rc;
+    if (relu && mask && res)
+        return launch_elementwise<T, false, 0, true, true, true>(x, nullptr, res, y, M, C, w.c0, w.c1, nullptr, w.c3, st,
+                                                                mask);
+    if (relu && mask)
+        return launch_elementwise<T, false, 0, true, false, true>(x, nullptr, nullptr, y, M, C, w.c0, w.c1, nullptr,
+                                                                 w.c3, st, mask);
     if (relu && res)
         return launch_elementwise<T, false, 0, true, true>(x, nullptr, res, y, M, C, w.c0, w.c1, nullptr, w.c3, st);
     if (relu) return launch_elementwise<T, false, 0, true, false>(x, nullptr, nullptr, y, M, C, w.c0, w.c1, nullptr, w.c3, st);
@@ -531,16 +590,18 @@ int bn_forward_t(const T* x, int64_t M, int C, const T* res, int relu, const flo
 }
 
 template <typename T>
-int bn_backward_t(const T* dy, const T* y, const T* x, int64_t M, int C, int relu, const float* gamma,
-                  const float* save_mean, const float* save_invstd, T* dres, T* dx, float* dgamma, float* dbeta,
-                  void* ws, size_t ws_bytes, hipStream_t st) {
+int bn_backward_t(const T* dy, const T* y, const unsigned char* mask, const T* x, int64_t M, int C, int relu,
+                  const float* gamma, const float* save_mean, const float* save_invstd, T* dres, T* dx, float* dgamma,
+                  float* dbeta, void* ws, size_t ws_bytes, hipStream_t st) {
     Geometry g;
     const int th = part_threads();
     if (make_geometry(M, C, sizeof(T), g, th) != DAUC_OK) return DAUC_EINVAL;
     if (ws == nullptr || ws_bytes < ws_bytes_for(C) || !aligned16p(ws)) return DAUC_EINVAL;
-    if (relu && y == nullptr) return DAUC_EINVAL;
+    if (relu && y == nullptr && mask == nullptr) return DAUC_EINVAL;
     const BnWs w = carve(ws, C);
-    if (relu)
+    if (relu && mask)
+        launch_partial<T, false, true, true>(th, g, x, dy, nullptr, dres, M, C, save_mean, w.partials, st, mask);
+    else if (relu)
         launch_partial<T, false, true>(th, g, x, dy, y, dres, M, C, save_mean, w.partials, st);
     else
         launch_partial<T, false, false>(th, g, x, dy, nullptr, dres, M, C, save_mean, w.partials, st);
@@ -550,6 +611,9 @@ int bn_backward_t(const T* dy, const T* y, const T* x, int64_t M, int C, int rel
     if (rc != DAUC_OK) return rc;
     if (dres)  // the masked gradient was written once; read it back instead of dy and y
         return launch_elementwise<T, true, 2, false, false>(x, dres, nullptr, dx, M, C, w.c0, w.c1, w.c2, w.c3, st);
+    if (relu && mask)
+        return launch_elementwise<T, true, 1, false, false, true>(x, dy, nullptr, dx, M, C, w.c0, w.c1, w.c2, w.c3, st,
+                                                                 const_cast<unsigned char*>(mask));
     if (relu) return launch_elementwise<T, true, 1, false, false>(x, dy, y, dx, M, C, w.c0, w.c1, w.c2, w.c3, st);
     return launch_elementwise<T, true, 0, false, false>(x, dy, nullptr, dx, M, C, w.c0, w.c1, w.c2, w.c3, st);
 }
@@ -574,37 +638,39 @@ size_t dauc_bn_workspace_size(int64_t M, int C) {
 
 int dauc_bn_act_forward(const void* x, int dtype, int64_t M, int C, const void* residual, int relu,
                         const float* gamma, const float* beta, float* running_mean, float* running_var,
-                        float momentum, float eps, void* y, float* save_mean, float* save_invstd, void* workspace,
-                        size_t workspace_bytes, dauc_stream_t stream) {
+                        float momentum, float eps, void* y, uint8_t* relu_mask, float* save_mean, float* save_invstd,
+                        void* workspace, size_t workspace_bytes, dauc_stream_t stream) {
     if (x == nullptr || y == nullptr || save_mean == nullptr || save_invstd == nullptr) return DAUC_EINVAL;
     if (!all_aligned({x, residual, y})) return DAUC_EINVAL;
+    if (relu_mask != nullptr && !relu) return DAUC_EINVAL;
     hipStream_t st = as_hip(stream);
     if (dtype == DAUC_DTYPE_BF16)
         return bn_forward_t(static_cast<const __hip_bfloat16*>(x), M, C, static_cast<const __hip_bfloat16*>(residual),
                             relu, gamma, beta, running_mean, running_var, momentum, eps,
-                            static_cast<__hip_bfloat16*>(y), save_mean, save_invstd, workspace, workspace_bytes, st);
+                            static_cast<__hip_bfloat16*>(y), relu_mask, save_mean, save_invstd, workspace,
+                            workspace_bytes, st);
     if (dtype == DAUC_DTYPE_F32)
         return bn_forward_t(static_cast<const float*>(x), M, C, static_cast<const float*>(residual), relu, gamma,
-                            beta, running_mean, running_var, momentum, eps, static_cast<float*>(y), save_mean,
-                            save_invstd, workspace, workspace_bytes, st);
+                            beta, running_mean, running_var, momentum, eps, static_cast<float*>(y), relu_mask,
+                            save_mean, save_invstd, workspace, workspace_bytes, st);
     return DAUC_EINVAL;
 }
 
-int dauc_bn_act_backward(const void* dy, const void* y, const void* x, int dtype, int64_t M, int C, int relu,
-                         const float* gamma, const float* save_mean, const float* save_invstd, void* dres, void* dx,
-                         float* dgamma, float* dbeta, void* workspace, size_t workspace_bytes,
+int dauc_bn_act_backward(const void* dy, const void* y, const uint8_t* relu_mask, const void* x, int dtype, int64_t M,
+                         int C, int relu, const float* gamma, const float* save_mean, const float* save_invstd,
+                         void* dres, void* dx, float* dgamma, float* dbeta, void* workspace, size_t workspace_bytes,
                          dauc_stream_t stream) {
     if (dy == nullptr || x == nullptr || dx == nullptr || save_mean == nullptr || save_invstd == nullptr)
         return DAUC_EINVAL;
     if (!all_aligned({dy, y, x, dres, dx})) return DAUC_EINVAL;
     hipStream_t st = as_hip(stream);
     if (dtype == DAUC_DTYPE_BF16)
-        return bn_backward_t(static_cast<const __hip_bfloat16*>(dy), static_cast<const __hip_bfloat16*>(y),
+        return bn_backward_t(static_cast<const __hip_bfloat16*>(dy), static_cast<const __hip_bfloat16*>(y), relu_mask,
                              static_cast<const __hip_bfloat16*>(x), M, C, relu, gamma, save_mean, save_invstd,
                              static_cast<__hip_bfloat16*>(dres), static_cast<__hip_bfloat16*>(dx), dgamma, dbeta,
                              workspace, workspace_bytes, st);
     if (dtype == DAUC_DTYPE_F32)
-        return bn_backward_t(static_cast<const float*>(dy), static_cast<const float*>(y),
+        return bn_backward_t(static_cast<const float*>(dy), static_cast<const float*>(y), relu_mask,
                              static_cast<const float*>(x), M, C, relu, gamma, save_mean, save_invstd,
                              static_cast<float*>(dres), static_cast<float*>(dx), dgamma, dbeta, workspace,
                              workspace_bytes, st);

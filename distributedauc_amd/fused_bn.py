@@ -4,7 +4,9 @@ The reference's blocks (resnet.py:47-64, 87-108, stem 203-206) run bn, the resid
 relu as separate passes; under torch each is its own HBM round trip (MIOpen's three BN
 kernels forward, three backward, plus the elementwise add and relu both ways). Here one
 autograd node per BN layer calls ``dauc_bn_act_forward`` / ``dauc_bn_act_backward``
-(csrc/bn_act.hip): two passes over the activation forward, two backward.
+(csrc/bn_act.hip): two passes over the activation forward, two backward. With ReLU the forward
+also writes a 1-bit-per-element mask of y > 0 and the backward reads it instead of y (both
+backward passes are HBM-bound: 2 B less per element and pass in bf16).
 
 Semantics are torch's ``F.batch_norm(training=True)`` followed by ``+ residual`` and
 ``relu``: batch mean and biased variance for the normalisation, running statistics
@@ -52,6 +54,8 @@ class BnActFunction(torch.autograd.Function):
         dev = x.device
         L = _lib.load()
         y = torch.empty_like(x, memory_format=torch.channels_last)
+        # the ReLU mask: one byte per 16-byte vector of y
+        mask = torch.empty(M * C * x.element_size() // 16, dtype=torch.uint8, device=dev) if relu else None
         mean = torch.empty(C, dtype=torch.float32, device=dev)
         invstd = torch.empty(C, dtype=torch.float32, device=dev)
         ws = workspaces.get(dev, "bn", L.dauc_bn_workspace_size(M, C))
@@ -61,9 +65,9 @@ class BnActFunction(torch.autograd.Function):
             residual = residual.contiguous(memory_format=torch.channels_last)
         check(L.dauc_bn_act_forward(_ptr(x), _DTYPES[x.dtype], M, C, _ptr(residual), int(relu), _ptr(weight),
                                     _ptr(bias), _ptr(running_mean), _ptr(running_var), float(momentum), float(eps),
-                                    _ptr(y), _ptr(mean), _ptr(invstd), _ptr(ws), ws.numel(), _stream(dev)),
+                                    _ptr(y), _ptr(mask), _ptr(mean), _ptr(invstd), _ptr(ws), ws.numel(), _stream(dev)),
               "dauc_bn_act_forward")
-        ctx.save_for_backward(x, y if relu else None, weight, mean, invstd)
+        ctx.save_for_backward(x, mask, weight, mean, invstd)
         ctx.relu = bool(relu)
         ctx.has_residual = residual is not None
         ctx.has_bias = bias is not None
@@ -71,7 +75,7 @@ class BnActFunction(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
-        x, y, weight, mean, invstd = ctx.saved_tensors
+        x, mask, weight, mean, invstd = ctx.saved_tensors
         N, C, H, W = x.shape
         M = N * H * W
         dev = x.device
@@ -84,7 +88,7 @@ class BnActFunction(torch.autograd.Function):
         dgamma = torch.empty(C, dtype=torch.float32, device=dev) if weight is not None else None
         dbeta = torch.empty(C, dtype=torch.float32, device=dev) if ctx.has_bias else None
         ws = workspaces.get(dev, "bn", L.dauc_bn_workspace_size(M, C))
-        check(L.dauc_bn_act_backward(_ptr(dy), _ptr(y), _ptr(x), _DTYPES[x.dtype], M, C, int(ctx.relu),
+        check(L.dauc_bn_act_backward(_ptr(dy), None, _ptr(mask), _ptr(x), _DTYPES[x.dtype], M, C, int(ctx.relu),
                                      _ptr(weight), _ptr(mean), _ptr(invstd), _ptr(dres), _ptr(dx), _ptr(dgamma),
                                      _ptr(dbeta), _ptr(ws), ws.numel(), _stream(dev)),
               "dauc_bn_act_backward")

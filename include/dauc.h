@@ -359,23 +359,26 @@ int dauc_sort_keys(const float* scores, int64_t n, unsigned* keys_out, void* wor
  * running statistics updated as torch does (unbiased variance, momentum). gamma,
  * beta, running_* are fp32 [C] (nullable: affine off / no running stats);
  * save_mean, save_invstd fp32 [C] receive the batch statistics for the backward.
+ * relu_mask (nullable; relu only): one byte per 16-byte vector of y ([M * C * elem / 16] bytes),
+ * bit i = (stored element i of the vector > 0): the backward's ReLU mask in 1/16 (bf16) of y's bytes.
  * Workspace: dauc_bn_workspace_size(M, C) bytes, 16-byte aligned, no zeroing needed.
  */
 size_t dauc_bn_workspace_size(int64_t M, int C);
 int dauc_bn_act_forward(const void* x, int dtype, int64_t M, int C, const void* residual, int relu,
                         const float* gamma, const float* beta, float* running_mean, float* running_var,
-                        float momentum, float eps, void* y, float* save_mean, float* save_invstd, void* workspace,
-                        size_t workspace_bytes, dauc_stream_t stream);
+                        float momentum, float eps, void* y, uint8_t* relu_mask, float* save_mean, float* save_invstd,
+                        void* workspace, size_t workspace_bytes, dauc_stream_t stream);
 
 /*
- * Backward of dauc_bn_act_forward. g = dy * [y > 0] (relu; y = the forward output) or dy.
+ * Backward of dauc_bn_act_forward. g = dy * [y > 0] (relu; y = the forward output, or relu_mask --
+ * the forward's mask bytes, read instead of y when non-null) or dy.
  *   dres (nullable) <- g: the gradient of the residual input;
  *   dx <- gamma*invstd*(g - mean(g) - xhat*mean(g*xhat)); dgamma <- sum g*xhat; dbeta <- sum g
  * (dgamma / dbeta fp32 [C], nullable).
  */
-int dauc_bn_act_backward(const void* dy, const void* y, const void* x, int dtype, int64_t M, int C, int relu,
-                         const float* gamma, const float* save_mean, const float* save_invstd, void* dres, void* dx,
-                         float* dgamma, float* dbeta, void* workspace, size_t workspace_bytes,
+int dauc_bn_act_backward(const void* dy, const void* y, const uint8_t* relu_mask, const void* x, int dtype, int64_t M,
+                         int C, int relu, const float* gamma, const float* save_mean, const float* save_invstd,
+                         void* dres, void* dx, float* dgamma, float* dbeta, void* workspace, size_t workspace_bytes,
                          dauc_stream_t stream);
 
 /* ------------------------------------------------ backbone: stem max-pool */

@@ -148,3 +148,58 @@ def test_resnet_fused_counts_batches_once(dev):
     net.eval()
     net(x)
     assert {int(b) for n, b in net.named_buffers() if n.endswith("num_batches_tracked")} == {2}
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("residual", [False, True])
+def test_bn_relu_mask_matches_y_path(dev, dtype, residual):
+    """Round 5: the forward's 1-bit ReLU mask (one byte per 16-byte vector) is exactly `y > 0` on the
+    stored y -- zeros, negative zeros, values whose bf16 rounding lands on a denormal or on zero,
+    +inf and NaN included -- and the backward that reads it gives dx, dres, dgamma and dbeta bit for
+    bit as the backward that reads y (the layout: element i of vector v is bit i of mask byte v)."""
+    from distributedauc_amd import _lib
+    from distributedauc_amd.fused_bn import _DTYPES
+    from distributedauc_amd.ops import _ptr, _stream, check, workspaces
+
+    g = torch.Generator(device=dev).manual_seed(21)
+    N, C, H, W = 4, 64, 6, 5
+    x = torch.randn(N, C, H, W, device=dev, generator=g).to(dtype).contiguous(memory_format=torch.channels_last)
+    flat = x.permute(0, 2, 3, 1).reshape(-1)  # channels-last order
+    flat[::97] = 0.0
+    flat[5::211] = float("nan")
+    flat[7::223] = float("inf")
+    res = torch.randn(N, C, H, W, device=dev, generator=g).to(dtype).contiguous(memory_format=torch.channels_last)
+    # shift/scale so that many outputs sit just above / below zero, some in the denormal range
+    gamma = torch.full((C,), 1e-38, device=dev)
+    gamma[: C // 2] = 1.0
+    beta = torch.zeros(C, device=dev)
+    M = N * H * W
+    L = _lib.load()
+    ws = workspaces.get(dev, "bn_mask_test", L.dauc_bn_workspace_size(M, C))
+    y = torch.empty_like(x)
+    mask = torch.full((M * C * x.element_size() // 16,), 0xAA, dtype=torch.uint8, device=dev)
+    mean, invstd = torch.empty(C, device=dev), torch.empty(C, device=dev)
+    rp = res if residual else None
+    check(L.dauc_bn_act_forward(_ptr(x), _DTYPES[dtype], M, C, _ptr(rp), 1, _ptr(gamma), _ptr(beta), None, None,
+                                0.1, 1e-5, _ptr(y), _ptr(mask), _ptr(mean), _ptr(invstd), _ptr(ws), ws.numel(),
+                                _stream(dev)), "forward")
+    yv = y.permute(0, 2, 3, 1).reshape(-1).float()
+    vec = 16 // x.element_size()
+    bits = (yv > 0).view(-1, vec).to(torch.int32)
+    want = (bits << torch.arange(vec, device=dev, dtype=torch.int32)).sum(1).to(torch.uint8)
+    assert torch.equal(mask, want)
+    assert bool((yv > 0).any()) and bool((yv == 0).any())
+    dy = torch.randn(N, C, H, W, device=dev, generator=g).to(dtype).contiguous(memory_format=torch.channels_last)
+    outs = []
+    for use_mask in (False, True):
+        dx = torch.empty_like(x)
+        dres = torch.empty_like(x) if residual else None
+        dgamma, dbeta = torch.empty(C, device=dev), torch.empty(C, device=dev)
+        check(L.dauc_bn_act_backward(_ptr(dy), None if use_mask else _ptr(y), _ptr(mask) if use_mask else None,
+                                     _ptr(x), _DTYPES[dtype], M, C, 1, _ptr(gamma), _ptr(mean), _ptr(invstd),
+                                     _ptr(dres), _ptr(dx), _ptr(dgamma), _ptr(dbeta), _ptr(ws), ws.numel(),
+                                     _stream(dev)), "backward")
+        outs.append([t.view(torch.int16 if t.dtype == torch.bfloat16 else torch.int32).clone()
+                     for t in (dx, dgamma, dbeta) + ((dres,) if residual else ())])
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
