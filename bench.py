@@ -117,6 +117,8 @@ def parse(argv=None):
     p.add_argument("--no-train", action="store_true")
     p.add_argument("--no-surrogate", action="store_true")
     p.add_argument("--fused-bn", type=int, default=1, help="fused BN+add+ReLU HIP kernels in the backbone (1/0)")
+    p.add_argument("--weight-shadow", type=int, default=1,
+                   help="bf16 conv weights from one shadow cast per forward (1) or autocast's cast per conv (0)")
     p.add_argument("--gemm-conv1x1", type=int, default=1,
                    help="stride-1 1x1 convs as hipBLASLt GEMMs where faster (per-shape timing; 1/0)")
     # internal: one process of the configs[0] CPU baseline (never touches the GPU)
@@ -223,7 +225,7 @@ def timed_steps(coda, it, steps: int, world: int) -> float:
 
 # ----------------------------------------------------------------------------- training legs
 def make_coda(arch, batch, image_size, I, pos_ratio, pool, world, rank, device, fused_bn=True, gemm_conv1x1=True,
-              graph=False, lr=0.1, flip=0.0):
+              graph=False, lr=0.1, flip=0.0, weight_shadow=None):
     from distributedauc_amd.backbone import build_backbone
     from distributedauc_amd.coda import CoDA
     from distributedauc_amd.loader import DeviceLoader, SyntheticImageNet, imagenet_like_labels
@@ -237,7 +239,7 @@ def make_coda(arch, batch, image_size, I, pos_ratio, pool, world, rank, device, 
     net = build_backbone(arch, num_classes=2).to(device).to(memory_format=torch.channels_last)
     net.set_fused_bn(bool(fused_bn)).set_gemm_conv1x1(bool(gemm_conv1x1))
     coda = CoDA(net, lr=lr, gamma=2000.0, T0=10 ** 9, I=I, split_index=split, world=world, rank=rank,
-                autocast_dtype=torch.bfloat16, device=device, collective=grouped())
+                autocast_dtype=torch.bfloat16, device=device, collective=grouped(), weight_shadow=weight_shadow)
     it = iter(loader)
     coda.average_all()            # main.py:141-142
     coda.begin_stage(1, it)       # alpha estimate + anchors (untimed)
@@ -249,7 +251,8 @@ def bench_train(args, world, rank, device):
     from distributedauc_amd import _lib
 
     coda, it = make_coda(args.arch, args.batch, args.image_size, args.I, args.pos_ratio, args.pool, world, rank,
-                         device, args.fused_bn, args.gemm_conv1x1, lr=args.lr, flip=args.signal_flip)
+                         device, args.fused_bn, args.gemm_conv1x1, lr=args.lr, flip=args.signal_flip,
+                         weight_shadow=bool(args.weight_shadow))
     log(f"rank {rank}: model + data ready, first steps compile/tune MIOpen kernels")
     lib = _lib.load()
     upd = KernelTimer(lib, "dauc_pd_update")

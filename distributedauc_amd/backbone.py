@@ -38,6 +38,110 @@ def _bn_act(fused: bool, bn: nn.BatchNorm2d, x: torch.Tensor, relu: bool = True,
     return F.relu(y, inplace=True) if relu else y
 
 
+# ---- bf16 weight shadow ---------------------------------------------------------------------
+# Under bf16 autocast every convolution casts its fp32 master weight to bf16 on every forward: one
+# small cast launch per conv (ResNet-50: 53 launches, ~0.3 ms of a 26 ms step, each a few us of
+# launch latency for a few hundred KB). With the shadow on, ONE cast launch per forward writes bf16
+# copies of all parameters (the FlatState buffer is contiguous) and the convolutions read their
+# bf16 weight from it: the same conversion (round to nearest even), so the same bits.
+_shadow_live: list = []  # the shadow of the forward in flight (set by ResNet.features)
+
+
+class WeightShadow:
+    """bf16 copies of a FlatState's parameters at the same offsets (views per conv weight)."""
+
+    def __init__(self, model: nn.Module):
+        flat = getattr(model, "_dauc_flat", None)
+        if flat is None:
+            raise RuntimeError("the weight shadow mirrors the FlatState buffer: build CoDA / FlatState first")
+        self.src = flat.params
+        self.buf = torch.empty(self.src.numel(), dtype=torch.bfloat16, device=self.src.device)
+        self.views: dict[int, torch.Tensor] = {}
+        convs = {id(m.weight) for m in model.modules() if isinstance(m, nn.Conv2d)}
+        for _, p, off, _n in flat.entries:
+            if id(p) in convs:
+                self.views[id(p)] = torch.as_strided(self.buf, p.shape, p.stride(), off)
+
+    def refresh(self) -> None:
+        """One cast launch: bf16(params) -> the shadow (stream-ordered after the last update)."""
+        self.buf.copy_(self.src)
+
+    def weight(self, p: torch.Tensor) -> torch.Tensor | None:
+        return self.views.get(id(p))
+
+
+def shadow_weight(p: torch.Tensor, dtype: torch.dtype) -> torch.Tensor | None:
+    """The bf16 shadow of conv weight ``p`` for the forward in flight, or None (cast it yourself)."""
+    if not _shadow_live or dtype != torch.bfloat16:
+        return None
+    return _shadow_live[-1].weight(p)
+
+
+class _ShadowConv(torch.autograd.Function):
+    """conv2d(x, w_bf16) with the weight read from the shadow; the gradient goes to the fp32 master
+    weight exactly as autocast's graph sends it (aten.convolution_backward in bf16, then the
+    bf16 -> fp32 copy of ToCopyBackward)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, wb, stride, padding, dilation, groups):
+        with torch.autocast("cuda", enabled=False):
+            y = F.conv2d(x, wb, None, stride, padding, dilation, groups)
+        ctx.save_for_backward(x, wb)
+        ctx.conf = (list(stride), list(padding), list(dilation), groups)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, wb = ctx.saved_tensors
+        stride, padding, dilation, groups = ctx.conf
+        nx, nw = bool(ctx.needs_input_grad[0]), bool(ctx.needs_input_grad[1])
+        dx, dw, _ = torch.ops.aten.convolution_backward(gy, x, wb, None, stride, padding, dilation, False, [0, 0],
+                                                         groups, [nx, nw, False])
+        return dx, (dw.float() if nw else None), None, None, None, None, None
+
+
+def _cw(conv: nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
+    """``conv(x)`` (a k x k convolution), reading its weight from the bf16 shadow when one is live."""
+    wb = shadow_weight(conv.weight, torch.bfloat16) if x.is_cuda else None
+    if (wb is None or conv.bias is not None or conv.padding_mode != "zeros" or isinstance(conv.padding, str)
+            or not torch.is_autocast_enabled("cuda")):
+        return conv(x)
+    if x.dtype == torch.float32:
+        x = x.to(torch.bfloat16)  # autocast's input cast
+    if x.dtype != torch.bfloat16:
+        return conv(x)
+    return _ShadowConv.apply(x, conv.weight, wb, conv.stride, conv.padding, conv.dilation, conv.groups)
+
+
+class _GlobalAvgPoolCL(torch.autograd.Function):
+    """adaptive_avg_pool2d(x, 1) of a channels-last activation with its gradient produced straight
+    in channels-last. torch's backward (MeanBackward: grad.expand(x.shape) / (H*W)) writes an NCHW
+    tensor that the fused BN backward then copies into channels-last: ResNet-50 b256, 2 passes over
+    25.7 M elements, 0.11 ms per step, the transposing copy alone 85 us. Here the same division
+    (the same elementwise op on the [N, C, 1, 1] gradient, so the same bits) is broadcast into a
+    channels-last tensor by one copy."""
+
+    @staticmethod
+    def forward(ctx, x):
+        ctx.shape = x.shape
+        return F.adaptive_avg_pool2d(x, 1)
+
+    @staticmethod
+    def backward(ctx, g):
+        N, C, H, W = ctx.shape
+        gs = g / (H * W)
+        out = torch.empty((N, C, H, W), dtype=gs.dtype, device=gs.device, memory_format=torch.channels_last)
+        out.copy_(gs.expand(N, C, H, W))
+        return out
+
+
+def _global_pool(pool: nn.Module, x: torch.Tensor) -> torch.Tensor:
+    if (x.is_cuda and x.dim() == 4 and x.is_contiguous(memory_format=torch.channels_last)
+            and isinstance(pool, nn.AdaptiveAvgPool2d) and pool.output_size in (1, (1, 1)) and torch.is_grad_enabled()):
+        return _GlobalAvgPoolCL.apply(x)
+    return pool(x)
+
+
 def _c1(gemm: bool, conv: nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
     """A 1x1 conv: through conv1x1.py (GEMM or MIOpen, timed per shape) when ``gemm``, else the module."""
     if gemm:
@@ -72,8 +176,8 @@ class BasicBlock(nn.Module):
         skip = x if self.downsample is None else _bn_act(f, self.downsample[1], _c1(self.gemm_conv1x1,
                                                                                   self.downsample[0], x),
                                                          relu=False)
-        y = _bn_act(f, self.bn1, self.conv1(x))
-        return _bn_act(f, self.bn2, self.conv2(y), residual=skip)
+        y = _bn_act(f, self.bn1, _cw(self.conv1, x))
+        return _bn_act(f, self.bn2, _cw(self.conv2, y), residual=skip)
 
 
 class Bottleneck(nn.Module):
@@ -108,7 +212,7 @@ class Bottleneck(nn.Module):
         if down is not None:
             skip = _bn_act(f, self.downsample[1], skip, relu=False)
         y = _bn_act(f, self.bn1, h)
-        y = _bn_act(f, self.bn2, self.conv2(y))
+        y = _bn_act(f, self.bn2, _cw(self.conv2, y))
         return _bn_act(f, self.bn3, _c1(g, self.conv3, y), residual=skip)
 
 
@@ -160,6 +264,14 @@ class ResNet(nn.Module):
 
     fused_bn = False
     _counted_bns: list = []
+    _wshadow: WeightShadow | None = None
+
+    def set_weight_shadow(self, enabled: bool = True) -> "ResNet":
+        """Read every convolution's bf16 weight from one shadow buffer refreshed by a single cast
+        launch per forward, instead of autocast's cast per convolution (bf16 autocast only; the
+        parameters must already live in a FlatState, i.e. after CoDA(model))."""
+        self._wshadow = WeightShadow(self) if enabled else None
+        return self
 
     def set_fused_bn(self, enabled: bool = True) -> "ResNet":
         """Route every training-mode bn (+ add) + relu through the fused HIP kernels (channels-last
@@ -189,15 +301,24 @@ class ResNet(nn.Module):
     def features(self, x):
         if self.fused_bn and self.training and x.is_cuda and self._counted_bns:
             torch._foreach_add_([m.num_batches_tracked for m in self._counted_bns], 1)
-        x = _bn_act(self.fused_bn, self.bn1, self.conv1(x))
-        if self.fused_bn and x.is_cuda:  # the stem max-pool with int8 indices (pool.py)
-            from .pool import max_pool2d
+        live = (self._wshadow is not None and x.is_cuda and torch.is_autocast_enabled("cuda")
+                and torch.get_autocast_dtype("cuda") == torch.bfloat16)
+        if live:
+            self._wshadow.refresh()
+            _shadow_live.append(self._wshadow)
+        try:
+            x = _bn_act(self.fused_bn, self.bn1, _cw(self.conv1, x))
+            if self.fused_bn and x.is_cuda:  # the stem max-pool with int8 indices (pool.py)
+                from .pool import max_pool2d
 
-            x = max_pool2d(x, self.maxpool)
-        else:
-            x = self.maxpool(x)
-        x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
-        return torch.flatten(self.avgpool(x), 1)
+                x = max_pool2d(x, self.maxpool)
+            else:
+                x = self.maxpool(x)
+            x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
+        finally:
+            if live:
+                _shadow_live.pop()
+        return torch.flatten(_global_pool(self.avgpool, x), 1)
 
     def forward(self, x):
         return self.softmax(self.fc(self.features(x)))

@@ -37,7 +37,8 @@ class CoDA:
     def __init__(self, model: nn.Module, *, lr: float = 0.1, gamma: float = 2000.0, T0: int = 5000,
                  I: int = 2, split_index: int = 4, mode: str = "reference", world: int = 1, rank: int = 0,
                  group=None, autocast_dtype: torch.dtype | None = None, device=None,
-                 max_exact_count: int = 1 << 24, head: str = "softmax", collective: bool | None = None):
+                 max_exact_count: int = 1 << 24, head: str = "softmax", collective: bool | None = None,
+                 weight_shadow: bool | None = None):
         if I < 1:
             raise ValueError("averaging period I must be >= 1")
         ops.mode_code(mode)  # validates
@@ -62,6 +63,12 @@ class CoDA:
         if collective and not (dist.is_available() and dist.is_initialized()):
             raise RuntimeError("CoDA(collective=True) needs an initialised torch.distributed process group")
         self.autocast_dtype = autocast_dtype
+        # bf16 autocast: the backbone's convolutions read their bf16 weights from one shadow buffer
+        # cast once per forward (backbone.WeightShadow) instead of one cast launch per convolution
+        if weight_shadow is None:
+            weight_shadow = autocast_dtype == torch.bfloat16 and hasattr(model, "set_weight_shadow")
+        if weight_shadow:
+            model.set_weight_shadow(True)
         self.max_exact_count = max_exact_count
         self.t_total = 0
         self.stage = 0

@@ -143,12 +143,21 @@ def _wgrad_gemm(g2, x2, slabs):
     return out
 
 
+def _low(weight, dtype):
+    """The weight in the activations' dtype: the backbone's bf16 shadow when one is live (one cast
+    launch per forward for every conv), else a cast of its own."""
+    from .backbone import shadow_weight
+
+    wb = shadow_weight(weight, dtype)
+    return wb.detach() if wb is not None else weight.detach().to(dtype)
+
+
 def _fwd(x, weight):
     """y = conv1x1(x, weight) (bf16 operands as x, fp32 accumulation), engine timed per shape."""
     N, cin, H, W = x.shape
     cout = weight.shape[0]
     M = N * H * W
-    wc = weight.detach().reshape(cout, cin).to(x.dtype)
+    wc = _low(weight, x.dtype).reshape(cout, cin)
     x2 = x.permute(0, 2, 3, 1).reshape(M, cin)  # a view: x is channels-last contiguous
     with torch.autocast("cuda", enabled=False):
         key = (M, cin, cout, x.dtype, "fwd")
@@ -269,7 +278,7 @@ class Conv1x1SkipFunction(torch.autograd.Function):
         elif down_stride == 1:
             skip, wcd = _fwd(x, wd)
         else:
-            wcd = wd.detach().reshape(wd.shape[0], wd.shape[1]).to(x.dtype)
+            wcd = _low(wd, x.dtype).reshape(wd.shape[0], wd.shape[1])
             with torch.autocast("cuda", enabled=False):
                 skip = F.conv2d(x, wcd.view(*wd.shape), stride=down_stride).contiguous(
                     memory_format=torch.channels_last)

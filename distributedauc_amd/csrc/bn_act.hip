@@ -330,30 +330,50 @@ __device__ __forceinline__ void sum_partials(const float* __restrict__ partials,
                                              int C, int cbase, double (*red)[kFinSubsets][64], double& t1,
                                              double& t2) {
     constexpr int NP = STATS ? 3 : 2;
+    constexpr int FU = 4;  // row subsets' loads in flight per thread before any fold
     const int cq = threadIdx.x % 16, j = threadIdx.x / 16;
     const int c = cbase + cq * 4;
     double a1[4] = {0, 0, 0, 0}, a2[4] = {0, 0, 0, 0};
-    if (c < C) {
-        for (int rb = j; rb < nrb; rb += kFinSubsets) {
-            const f32x4 p1 = *reinterpret_cast<const f32x4*>(partials + (int64_t(rb) * NP) * C + c);
-            const f32x4 p2 = *reinterpret_cast<const f32x4*>(partials + (int64_t(rb) * NP + 1) * C + c);
-            if (STATS) {
-                const f32x4 pk = *reinterpret_cast<const f32x4*>(partials + (int64_t(rb) * NP + 2) * C + c);
-                const int64_t r0 = int64_t(rb) * rows;
-                const double nb = double((M - r0) < rows ? (M - r0) : rows);
+    auto fold = [&](int rb, const f32x4& p1, const f32x4& p2, const f32x4& pk) {
+        if (STATS) {
+            const int64_t r0 = int64_t(rb) * rows;
+            const double nb = double((M - r0) < rows ? (M - r0) : rows);
 #pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const double k = pk[i], s1 = p1[i];
-                    a1[i] += s1 + nb * k;
-                    a2[i] += double(p2[i]) + 2.0 * k * s1 + nb * k * k;
-                }
-            } else {
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    a1[i] += p1[i];
-                    a2[i] += p2[i];
-                }
+            for (int i = 0; i < 4; ++i) {
+                const double k = pk[i], s1 = p1[i];
+                a1[i] += s1 + nb * k;
+                a2[i] += double(p2[i]) + 2.0 * k * s1 + nb * k * k;
             }
+        } else {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                a1[i] += p1[i];
+                a2[i] += p2[i];
+            }
+        }
+    };
+    auto ld = [&](int rb, int q) {
+        return *reinterpret_cast<const f32x4*>(partials + (int64_t(rb) * NP + q) * C + c);
+    };
+    if (c < C) {
+        // rows rb = j, j + S, j + 2S, ... folded in that order; FU rows' loads issued together
+        int rb = j;
+        for (; rb + (FU - 1) * kFinSubsets < nrb; rb += FU * kFinSubsets) {
+            f32x4 p1[FU], p2[FU], pk[FU];
+#pragma unroll
+            for (int u = 0; u < FU; ++u) {
+                p1[u] = ld(rb + u * kFinSubsets, 0);
+                p2[u] = ld(rb + u * kFinSubsets, 1);
+                if (STATS) pk[u] = ld(rb + u * kFinSubsets, 2);
+            }
+#pragma unroll
+            for (int u = 0; u < FU; ++u) fold(rb + u * kFinSubsets, p1[u], p2[u], pk[u]);
+        }
+        for (; rb < nrb; rb += kFinSubsets) {
+            const f32x4 p1 = ld(rb, 0), p2 = ld(rb, 1);
+            f32x4 pk;
+            if (STATS) pk = ld(rb, 2);
+            fold(rb, p1, p2, pk);
         }
     }
 #pragma unroll
@@ -362,13 +382,23 @@ __device__ __forceinline__ void sum_partials(const float* __restrict__ partials,
         red[1][j][cq * 4 + i] = a2[i];
     }
     __syncthreads();
+    // pairwise tree over the row subsets (a fixed order: bitwise reproducible)
+#pragma unroll
+    for (int s = kFinSubsets / 2; s >= 1; s >>= 1) {
+        if (j < s) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                red[0][j][cq * 4 + i] += red[0][j + s][cq * 4 + i];
+                red[1][j][cq * 4 + i] += red[1][j + s][cq * 4 + i];
+            }
+        }
+        __syncthreads();
+    }
     t1 = 0.0;
     t2 = 0.0;
     if (threadIdx.x < 64) {
-        for (int q = 0; q < kFinSubsets; ++q) {
-            t1 += red[0][q][threadIdx.x];
-            t2 += red[1][q][threadIdx.x];
-        }
+        t1 = red[0][0][threadIdx.x];
+        t2 = red[1][0][threadIdx.x];
     }
 }
 

@@ -194,6 +194,131 @@ __global__ __launch_bounds__(kPoolThreads) void maxpool_bwd_kernel(const T* __re
     *reinterpret_cast<Raw*>(dx + pix * g.C + c) = pack(acc);
 }
 
+// ---- the ResNet stem's shape (k = 3): every load of a window issued before any compare ------
+// Forward: the 9 window loads of the generic kernel sit in a clipped loop (one load latency per
+// element); here they are unrolled with per-element predicates (same comparisons, same order).
+template <typename T>
+__global__ __launch_bounds__(kPoolThreads) void maxpool_fwd_k3_kernel(const T* __restrict__ x, PoolGeom g,
+                                                                      T* __restrict__ y, int8_t* __restrict__ idx) {
+    constexpr int V = PoolVec<T>::N;
+    typedef typename PoolVec<T>::Raw Raw;
+    typedef typename PoolVec<T>::Idx Idx;
+    const int cv = g.C / V;
+    const int t = blockIdx.x * kPoolThreads + threadIdx.x;
+    if (t >= g.Ho * g.Wo * cv) return;
+    const int c = (t % cv) * V;
+    const int q = t / cv;
+    const int ow = q % g.Wo;
+    const int oh = q / g.Wo;
+    const int64_t n = blockIdx.y;
+    const int64_t pix = n * g.Ho * g.Wo + q;
+    const int hs = oh * g.s - g.p, ws = ow * g.s - g.p;
+    const T* __restrict__ xn = x + n * g.H * g.W * g.C + c;
+    Raw r[9];
+    bool in[9];
+#pragma unroll
+    for (int e = 0; e < 9; ++e) {
+        const int ih = hs + e / 3, iw = ws + e % 3;
+        in[e] = ih >= 0 && ih < g.H && iw >= 0 && iw < g.W;
+        if (in[e]) r[e] = *reinterpret_cast<const Raw*>(xn + (int64_t(ih) * g.W + iw) * g.C);
+    }
+    float m[V];
+    int id[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+        m[v] = -__builtin_huge_valf();
+        id[v] = -1;
+    }
+#pragma unroll
+    for (int e = 0; e < 9; ++e) {
+        if (!in[e]) continue;
+        float val[V];
+        unpack(r[e], val);
+#pragma unroll
+        for (int v = 0; v < V; ++v) {
+            if (val[v] > m[v] || val[v] != val[v]) {
+                m[v] = val[v];
+                id[v] = e;
+            }
+        }
+    }
+    *reinterpret_cast<Raw*>(y + pix * g.C + c) = pack(m);
+    *reinterpret_cast<Idx*>(idx + pix * g.C + c) = pack_idx(id);
+}
+
+// Backward for k = 3, s = 2, p = 1: a thread owns the 2 x 2 input pixels (2a + di, 2b + dj) of one
+// channel vector. Their windows are exactly (a + i, b + j), i, j in {0, 1} (row 2a lies only in
+// window row a, row 2a + 1 in rows a and a + 1; columns alike), so the thread loads those four
+// windows' dy and indices once, all before any add -- every dy / index element is read by one
+// thread (the generic kernel reads each 2.25 times on average, one window after another). Each
+// input element adds the windows naming it in torch's order (window rows, then columns,
+// ascending) in fp32 and rounds once: bit-identical to the generic kernel.
+template <typename T>
+__global__ __launch_bounds__(kPoolThreads) void maxpool_bwd_k3s2_kernel(const T* __restrict__ dy,
+                                                                        const int8_t* __restrict__ idx, PoolGeom g,
+                                                                        T* __restrict__ dx) {
+    constexpr int V = PoolVec<T>::N;
+    typedef typename PoolVec<T>::Raw Raw;
+    typedef typename PoolVec<T>::Idx Idx;
+    const int cv = g.C / V;
+    const int Hb = (g.H + 1) / 2, Wb = (g.W + 1) / 2;
+    const int t = blockIdx.x * kPoolThreads + threadIdx.x;
+    if (t >= Hb * Wb * cv) return;
+    const int c = (t % cv) * V;
+    const int q = t / cv;
+    const int b = q % Wb;
+    const int a = q / Wb;
+    const int64_t n = blockIdx.y;
+    const int64_t obase = n * g.Ho * g.Wo;
+    Raw d[2][2];
+    Idx ix[2][2];
+    bool win[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            win[i][j] = a + i < g.Ho && b + j < g.Wo;
+            if (win[i][j]) {
+                const int64_t o = (obase + int64_t(a + i) * g.Wo + (b + j)) * g.C + c;
+                ix[i][j] = *reinterpret_cast<const Idx*>(idx + o);
+                d[i][j] = *reinterpret_cast<const Raw*>(dy + o);
+            }
+        }
+#pragma unroll
+    for (int di = 0; di < 2; ++di) {
+        const int ih = 2 * a + di;
+        if (ih >= g.H) continue;
+#pragma unroll
+        for (int dj = 0; dj < 2; ++dj) {
+            const int iw = 2 * b + dj;
+            if (iw >= g.W) continue;
+            const bool origin = (ih == 0 && iw == 0);
+            float acc[V];
+#pragma unroll
+            for (int v = 0; v < V; ++v) acc[v] = 0.0f;
+            // window (a + i, b + j) covers this pixel when i <= di and j <= dj; the pixel's
+            // position in it: row di + 1 - 2i, column dj + 1 - 2j
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                if (i > di) continue;
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    if (j > dj || !win[i][j]) continue;
+                    const int rel = (di + 1 - 2 * i) * 3 + (dj + 1 - 2 * j);
+                    int id[V];
+                    unpack_idx(ix[i][j], id);
+                    float dv[V];
+                    unpack(d[i][j], dv);
+#pragma unroll
+                    for (int v = 0; v < V; ++v)
+                        if (id[v] == rel || (origin && id[v] == -1)) acc[v] += dv[v];
+                }
+            }
+            *reinterpret_cast<Raw*>(dx + ((n * g.H + ih) * int64_t(g.W) + iw) * g.C + c) = pack(acc);
+        }
+    }
+}
+
 bool pool_args_ok(const void* a, const void* b, const void* c, int dtype, int64_t N, int H, int W, int C, int k,
                   int s, int p, int Ho, int Wo) {
     if (a == nullptr || b == nullptr || c == nullptr) return false;
@@ -230,6 +355,15 @@ int dauc_maxpool2d_forward(const void* x, int dtype, int64_t N, int H, int W, in
     dim3 grid;
     if (pool_grid(int64_t(Ho) * Wo * (C / V), N, &grid)) return DAUC_EINVAL;
     hipStream_t st = as_hip(stream);
+    if (kernel == 3) {
+        if (dtype == DAUC_DTYPE_BF16)
+            hipLaunchKernelGGL(maxpool_fwd_k3_kernel<__hip_bfloat16>, grid, dim3(kPoolThreads), 0, st,
+                               static_cast<const __hip_bfloat16*>(x), g, static_cast<__hip_bfloat16*>(y), argmax);
+        else
+            hipLaunchKernelGGL(maxpool_fwd_k3_kernel<float>, grid, dim3(kPoolThreads), 0, st,
+                               static_cast<const float*>(x), g, static_cast<float*>(y), argmax);
+        return launch_status();
+    }
     if (dtype == DAUC_DTYPE_BF16)
         hipLaunchKernelGGL(maxpool_fwd_kernel<__hip_bfloat16>, grid, dim3(kPoolThreads), 0, st,
                            static_cast<const __hip_bfloat16*>(x), g, static_cast<__hip_bfloat16*>(y), argmax);
@@ -245,8 +379,18 @@ int dauc_maxpool2d_backward(const void* dy, const int8_t* argmax, int dtype, int
     const PoolGeom g{N, H, W, C, kernel, stride, pad, Ho, Wo};
     const int V = dtype == DAUC_DTYPE_BF16 ? 8 : 4;
     dim3 grid;
-    if (pool_grid(int64_t(H) * W * (C / V), N, &grid)) return DAUC_EINVAL;
     hipStream_t st = as_hip(stream);
+    if (kernel == 3 && stride == 2 && pad == 1) {
+        if (pool_grid(int64_t((H + 1) / 2) * ((W + 1) / 2) * (C / V), N, &grid)) return DAUC_EINVAL;
+        if (dtype == DAUC_DTYPE_BF16)
+            hipLaunchKernelGGL(maxpool_bwd_k3s2_kernel<__hip_bfloat16>, grid, dim3(kPoolThreads), 0, st,
+                               static_cast<const __hip_bfloat16*>(dy), argmax, g, static_cast<__hip_bfloat16*>(dx));
+        else
+            hipLaunchKernelGGL(maxpool_bwd_k3s2_kernel<float>, grid, dim3(kPoolThreads), 0, st,
+                               static_cast<const float*>(dy), argmax, g, static_cast<float*>(dx));
+        return launch_status();
+    }
+    if (pool_grid(int64_t(H) * W * (C / V), N, &grid)) return DAUC_EINVAL;
     if (dtype == DAUC_DTYPE_BF16)
         hipLaunchKernelGGL(maxpool_bwd_kernel<__hip_bfloat16>, grid, dim3(kPoolThreads), 0, st,
                            static_cast<const __hip_bfloat16*>(dy), argmax, g, static_cast<__hip_bfloat16*>(dx));

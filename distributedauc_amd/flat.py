@@ -52,6 +52,15 @@ def _dense_layout(t: torch.Tensor) -> bool:
     return True
 
 
+def _same_order(g: torch.Tensor, p: torch.Tensor) -> bool:
+    """g's elements sit where p's do: equal strides on every dimension longer than 1 (a 1x1 conv
+    weight's gradient [Cout, Cin, 1, 1] is the same memory whether its unit dimensions carry
+    contiguous or channels-last strides -- autograd's layout contract ignores them too)."""
+    if g.shape != p.shape or not _dense_layout(g):
+        return False
+    return all(n == 1 or gs == ps for n, gs, ps in zip(p.shape, g.stride(), p.stride()))
+
+
 class FlatState:
     """One rank's CoDA state in four device buffers (see module docstring)."""
 
@@ -115,7 +124,7 @@ class FlatState:
                 raise RuntimeError(f"parameter {name} has no gradient; run backward first")
             if g.dtype != torch.float32 or g.device != self.device:
                 raise TypeError(f"gradient of {name} must be fp32 on {self.device}")
-            if g.stride() != p.stride() and n > 1:
+            if n > 1 and not _same_order(g, p):
                 g = torch.empty_like(p).copy_(g)  # same physical order as the parameter
                 keep.append(g)
             seg = self._segs[i]

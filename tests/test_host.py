@@ -9,7 +9,7 @@ import pytest
 import torch
 
 from distributedauc_amd import backbone, data_partitioner, loader, parameters
-from distributedauc_amd.flat import ALIGN, FlatState, _dense_layout
+from distributedauc_amd.flat import ALIGN, FlatState, _dense_layout, _same_order
 
 
 def test_reference_flags_and_defaults():
@@ -83,6 +83,19 @@ def test_dense_layout_and_flat_requires_gpu():
     with pytest.raises(RuntimeError, match="GPU memory"):
         FlatState(torch.nn.Linear(3, 2))
     assert ALIGN * 4 == 256
+
+
+def test_gradient_memory_order_check():
+    """FlatState.grad_segments copies a gradient only when its memory order differs from the
+    parameter's: a 1x1 conv weight's contiguous gradient is the channels-last parameter's order."""
+    p1 = torch.empty_strided((8, 4, 1, 1), (4, 1, 4, 4))  # what model.to(channels_last) leaves
+    assert p1.stride() != torch.zeros(8, 4, 1, 1).stride()
+    assert _same_order(torch.zeros(8, 4, 1, 1), p1)
+    p3 = torch.zeros(8, 4, 3, 3).contiguous(memory_format=torch.channels_last)
+    assert not _same_order(torch.zeros(8, 4, 3, 3), p3)
+    assert _same_order(torch.zeros(8, 4, 3, 3).contiguous(memory_format=torch.channels_last), p3)
+    assert not _same_order(torch.zeros(8, 8)[:, ::2], torch.zeros(8, 4))
+    assert not _same_order(torch.zeros(4, 8).t(), torch.zeros(8, 4))
 
 
 def test_run_label_format():

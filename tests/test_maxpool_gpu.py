@@ -109,3 +109,24 @@ def test_maxpool_refuses_unsupported(dev):
     with pytest.raises(ValueError):
         max_pool2d(torch.randn((2, 16, 8, 8), device=dev).contiguous(memory_format=torch.channels_last),
                    nn.MaxPool2d(3, 2, 1, ceil_mode=True))
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("shape", [(256, 2048, 7, 7), (3, 16, 5, 4), (2, 8, 1, 1)])
+def test_global_avgpool_channels_last_grad_matches_torch(dev, dtype, shape):
+    """backbone._GlobalAvgPoolCL (the head's average pool, resnet.py:210): the same output and the
+    same input-gradient bits as torch's AdaptiveAvgPool2d(1), the gradient channels-last."""
+    from distributedauc_amd.backbone import _GlobalAvgPoolCL
+
+    g = torch.Generator(device=dev).manual_seed(21)
+    x = torch.randn(shape, device=dev, generator=g).to(dtype).contiguous(memory_format=torch.channels_last)
+    dy = torch.randn(shape[:2], device=dev, generator=g).to(dtype)
+    xa = x.clone(memory_format=torch.channels_last).requires_grad_(True)
+    ya = torch.flatten(nn.AdaptiveAvgPool2d(1)(xa), 1)
+    ya.backward(dy)
+    xb = x.clone(memory_format=torch.channels_last).requires_grad_(True)
+    yb = torch.flatten(_GlobalAvgPoolCL.apply(xb), 1)
+    yb.backward(dy)
+    assert torch.equal(_bits(yb), _bits(ya))
+    assert xb.grad.is_contiguous(memory_format=torch.channels_last)
+    assert torch.equal(_bits(xb.grad), _bits(xa.grad))

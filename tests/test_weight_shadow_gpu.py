@@ -1,0 +1,71 @@
+"""The bf16 weight shadow (backbone.WeightShadow): one cast launch per forward instead of autocast's
+cast per convolution must change no bit of the step.
+
+Reference: the same backbone under torch's bf16 autocast (main.py:311-326's forward/backward, the
+autocast the trainer adds), where each conv casts its fp32 weight itself. Same model, same input,
+deterministic MIOpen solvers and the GEMM engine fixed for the 1x1 convolutions (engine timing must
+not pick different numerics for the two runs): scores, every parameter gradient and the loss after
+a CoDA step are bit-identical with and without the shadow, and a parameter change between
+forwards is seen by the next forward (the shadow is refreshed per forward).
+"""
+from __future__ import annotations
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _bits(t):
+    t = t.detach().contiguous()
+    return t.view(torch.int16 if t.element_size() == 2 else torch.int32).cpu()
+
+
+def _run(dev, arch, shadow, size):
+    from distributedauc_amd import conv1x1
+    from distributedauc_amd.backbone import build_backbone
+    from distributedauc_amd.coda import CoDA
+
+    torch.manual_seed(7)
+    net = build_backbone(arch, num_classes=2).to(dev).to(memory_format=torch.channels_last)
+    net.set_fused_bn(True).set_gemm_conv1x1(True).train()
+    coda = CoDA(net, lr=0.01, split_index=4, autocast_dtype=torch.bfloat16, device=dev, weight_shadow=shadow)
+    assert (net._wshadow is not None) == shadow
+    g = torch.Generator(device=dev).manual_seed(11)
+    x = torch.randn((8, 3, size, size), device=dev, generator=g).contiguous(memory_format=torch.channels_last)
+    y = torch.tensor([9, 0, 7, 1, 5, 3, 8, 2], device=dev)
+    with conv1x1.fixed_engine("gemm"):
+        h = coda.scores(x)
+        h.float().pow(2).sum().backward()
+        grads = [p.grad.detach().clone() for p in net.parameters()]
+        net.zero_grad(set_to_none=True)
+        loss = coda.train_step(x, y)  # forward, surrogate, backward, update
+        coda.state.params.mul_(0.5)   # parameters change between forwards: the shadow must follow
+        h2 = coda.scores(x)
+    return h.detach().clone(), grads, float(loss), h2.detach().clone(), coda.state.flat.clone()
+
+
+@pytest.mark.parametrize("arch,size", [("resnet18", 64), ("resnet50", 64)])
+def test_weight_shadow_bit_identical(dev, arch, size):
+    det = torch.backends.cudnn.deterministic
+    torch.backends.cudnn.deterministic = True
+    try:
+        a = _run(dev, arch, False, size)
+        b = _run(dev, arch, True, size)
+    finally:
+        torch.backends.cudnn.deterministic = det
+    assert torch.equal(_bits(a[0]), _bits(b[0])), "scores differ"
+    assert len(a[1]) == len(b[1])
+    for i, (ga, gb) in enumerate(zip(a[1], b[1])):
+        assert torch.equal(_bits(ga), _bits(gb)), f"gradient {i} differs"
+    assert a[2] == b[2] or (a[2] != a[2] and b[2] != b[2]), "loss differs"
+    assert torch.equal(_bits(a[3]), _bits(b[3])), "scores after a parameter change differ"
+    assert torch.equal(_bits(a[4]), _bits(b[4])), "state after the step differs"
+
+
+def test_weight_shadow_needs_flat_state(dev):
+    from distributedauc_amd.backbone import resnet18
+
+    net = resnet18().to(dev)
+    with pytest.raises(RuntimeError, match="FlatState"):
+        net.set_weight_shadow(True)
