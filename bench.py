@@ -117,8 +117,12 @@ def parse(argv=None):
     p.add_argument("--no-train", action="store_true")
     p.add_argument("--no-surrogate", action="store_true")
     p.add_argument("--fused-bn", type=int, default=1, help="fused BN+add+ReLU HIP kernels in the backbone (1/0)")
-    p.add_argument("--weight-shadow", type=int, default=1,
-                   help="bf16 conv weights from one shadow cast per forward (1) or autocast's cast per conv (0)")
+    p.add_argument("--graph", type=int, default=0,
+                   help="headline step: replay label map -> forward -> surrogate -> backward from one HIP graph, "
+                        "the update launched eagerly after each replay (1) or everything eager (0)")
+    p.add_argument("--weight-shadow", type=int, default=2,
+                   help="bf16 conv weights from one shadow cast per forward (1), + the stride-1 3x3 input "
+                        "gradients as forward convolutions with flipped weights (2), or autocast's cast per conv (0)")
     p.add_argument("--gemm-conv1x1", type=int, default=1,
                    help="stride-1 1x1 convs as hipBLASLt GEMMs where faster (per-shape timing; 1/0)")
     # internal: one process of the configs[0] CPU baseline (never touches the GPU)
@@ -239,7 +243,10 @@ def make_coda(arch, batch, image_size, I, pos_ratio, pool, world, rank, device, 
     net = build_backbone(arch, num_classes=2).to(device).to(memory_format=torch.channels_last)
     net.set_fused_bn(bool(fused_bn)).set_gemm_conv1x1(bool(gemm_conv1x1))
     coda = CoDA(net, lr=lr, gamma=2000.0, T0=10 ** 9, I=I, split_index=split, world=world, rank=rank,
-                autocast_dtype=torch.bfloat16, device=device, collective=grouped(), weight_shadow=weight_shadow)
+                autocast_dtype=torch.bfloat16, device=device, collective=grouped(),
+                weight_shadow=None if weight_shadow is None else bool(weight_shadow))
+    if weight_shadow == 1:
+        net.set_weight_shadow(True, dgrad_fwd=False)
     it = iter(loader)
     coda.average_all()            # main.py:141-142
     coda.begin_stage(1, it)       # alpha estimate + anchors (untimed)
@@ -252,7 +259,9 @@ def bench_train(args, world, rank, device):
 
     coda, it = make_coda(args.arch, args.batch, args.image_size, args.I, args.pos_ratio, args.pool, world, rank,
                          device, args.fused_bn, args.gemm_conv1x1, lr=args.lr, flip=args.signal_flip,
-                         weight_shadow=bool(args.weight_shadow))
+                         weight_shadow=int(args.weight_shadow))
+    if args.graph:
+        coda.use_graph(True, eager_update=True)
     log(f"rank {rank}: model + data ready, first steps compile/tune MIOpen kernels")
     lib = _lib.load()
     upd = KernelTimer(lib, "dauc_pd_update")
@@ -271,7 +280,9 @@ def bench_train(args, world, rank, device):
     out = {
         "dt": dt, "imgs": world * args.batch * args.steps, "loss": loss, "n_params": coda.state.numel(),
         "update_ms": upd.mean_ms(), "update_bytes": coda.state.bytes_per_update(True),
-        "surrogate_us": sur.mean_ms() * 1e3, "payload_bytes": coda.state.n_reduce * 4,
+        "surrogate_us": (sur.mean_ms() * 1e3) if sur.pairs else None,  # inside the graph: not timed
+        "payload_bytes": coda.state.n_reduce * 4, "graph": bool(coda._graph_on),
+        "graph_captures": coda.graph_captures,
     }
     if args.sweep_I:
         out["period_sweep"] = bench_period_sweep(coda, it, args, world)
@@ -937,6 +948,10 @@ def main():
                              "frac": upd_gbs / HBM_PEAK_GBS, "traffic": load_traffic("pd_update"),
                              "bytes_per_launch": res["update_bytes"], "avg_launch_us": res["update_ms"] * 1e3},
                 "surrogate_us_per_call": res["surrogate_us"],
+                "step_graph": {"replayed": res["graph"], "captures": res["graph_captures"],
+                               "what": "label map -> forward -> surrogate -> backward replayed from one HIP graph; "
+                                       "the update launched eagerly after each replay (timed by events)"
+                               if res["graph"] else "every step launched eagerly"},
                 "final_loss": res["loss"],
             })
             if "period_sweep" in res:

@@ -48,26 +48,61 @@ _shadow_live: list = []  # the shadow of the forward in flight (set by ResNet.fe
 
 
 class WeightShadow:
-    """bf16 copies of a FlatState's parameters at the same offsets (views per conv weight)."""
+    """bf16 copies of a FlatState's parameters at the same offsets (views per conv weight), and,
+    with ``dgrad_fwd``, each stride-1 'same' k x k convolution's weight flipped and transposed
+    (W'[ci, co, kh, kw] = W[co, ci, k-1-kh, k-1-kw], channels-last) for its input gradient."""
 
-    def __init__(self, model: nn.Module):
+    def __init__(self, model: nn.Module, dgrad_fwd: bool = False):
         flat = getattr(model, "_dauc_flat", None)
         if flat is None:
             raise RuntimeError("the weight shadow mirrors the FlatState buffer: build CoDA / FlatState first")
         self.src = flat.params
-        self.buf = torch.empty(self.src.numel(), dtype=torch.bfloat16, device=self.src.device)
+        dev = self.src.device
+        self.buf = torch.empty(self.src.numel(), dtype=torch.bfloat16, device=dev)
         self.views: dict[int, torch.Tensor] = {}
-        convs = {id(m.weight) for m in model.modules() if isinstance(m, nn.Conv2d)}
+        self.flips: dict[int, torch.Tensor] = {}
+        convs = {id(m.weight): m for m in model.modules() if isinstance(m, nn.Conv2d)}
+        idx, foff = [], 0
         for _, p, off, _n in flat.entries:
-            if id(p) in convs:
-                self.views[id(p)] = torch.as_strided(self.buf, p.shape, p.stride(), off)
+            m = convs.get(id(p))
+            if m is None:
+                continue
+            self.views[id(p)] = torch.as_strided(self.buf, p.shape, p.stride(), off)
+            if dgrad_fwd and _dgrad_as_fwd_ok(m):
+                co, ci, k, _ = p.shape
+                s0, s1, s2, s3 = p.stride()
+                r = torch.arange(k)
+                src = (off + torch.arange(co).view(1, co, 1, 1) * s0 + torch.arange(ci).view(ci, 1, 1, 1) * s1
+                       + (k - 1 - r).view(1, 1, k, 1) * s2 + (k - 1 - r).view(1, 1, 1, k) * s3)  # [ci, co, kh, kw]
+                idx.append(src.permute(0, 2, 3, 1).reshape(-1))  # channels-last storage order (ci, kh, kw, co)
+                self.flips[id(p)] = (foff, (ci, co, k, k), (k * k * co, 1, k * co, co))
+                foff += p.numel()
+        self.fbuf = torch.empty(foff, dtype=torch.bfloat16, device=dev) if foff else None
+        self.fidx = torch.cat(idx).to(device=dev, dtype=torch.int64) if idx else None
+        for key, (o, shape, stride) in list(self.flips.items()):
+            self.flips[key] = torch.as_strided(self.fbuf, shape, stride, o)
 
-    def refresh(self) -> None:
-        """One cast launch: bf16(params) -> the shadow (stream-ordered after the last update)."""
+    def refresh(self, flips: bool = True) -> None:
+        """One cast launch: bf16(params) -> the shadow (stream-ordered after the last update); with
+        the flipped weights, one gather launch more."""
         self.buf.copy_(self.src)
+        if flips and self.fbuf is not None:
+            torch.index_select(self.buf, 0, self.fidx, out=self.fbuf)
 
     def weight(self, p: torch.Tensor) -> torch.Tensor | None:
         return self.views.get(id(p))
+
+    def flipped(self, p: torch.Tensor) -> torch.Tensor | None:
+        return self.flips.get(id(p))
+
+
+def _dgrad_as_fwd_ok(m: nn.Conv2d) -> bool:
+    """A stride-1, 'same'-padded, odd square k x k convolution (k > 1, one group): its input
+    gradient is the forward convolution of dy with the flipped, transposed weight."""
+    k = m.kernel_size
+    return (k[0] == k[1] and k[0] % 2 == 1 and k[0] > 1 and m.stride == (1, 1) and m.dilation == (1, 1)
+            and m.groups == 1 and not isinstance(m.padding, str) and tuple(m.padding) == (k[0] // 2, k[0] // 2)
+            and m.padding_mode == "zeros")
 
 
 def shadow_weight(p: torch.Tensor, dtype: torch.dtype) -> torch.Tensor | None:
@@ -78,26 +113,35 @@ def shadow_weight(p: torch.Tensor, dtype: torch.dtype) -> torch.Tensor | None:
 
 
 class _ShadowConv(torch.autograd.Function):
-    """conv2d(x, w_bf16) with the weight read from the shadow; the gradient goes to the fp32 master
-    weight exactly as autocast's graph sends it (aten.convolution_backward in bf16, then the
-    bf16 -> fp32 copy of ToCopyBackward)."""
+    """conv2d(x, w_bf16) with the weight read from the shadow; the weight gradient goes to the fp32
+    master weight exactly as autocast's graph sends it (aten.convolution_backward in bf16, then the
+    bf16 -> fp32 copy of ToCopyBackward). The input gradient is torch's too, unless ``wf`` (the
+    flipped weight) is given: then dx = conv2d(dy, wf) -- a FORWARD convolution of the same shape
+    as this one (C_in = C_out for the bottlenecks' 3x3), which runs on the forward solvers (CK,
+    no output zero-fill) instead of MIOpen's backward-data kernel and its zero-fill. Same
+    products, fp32 accumulation in another order: the bits of dx differ from torch's."""
 
     @staticmethod
-    def forward(ctx, x, weight, wb, stride, padding, dilation, groups):
+    def forward(ctx, x, weight, wb, wf, stride, padding, dilation, groups):
         with torch.autocast("cuda", enabled=False):
             y = F.conv2d(x, wb, None, stride, padding, dilation, groups)
-        ctx.save_for_backward(x, wb)
+        ctx.save_for_backward(x, wb, wf)
         ctx.conf = (list(stride), list(padding), list(dilation), groups)
         return y
 
     @staticmethod
     def backward(ctx, gy):
-        x, wb = ctx.saved_tensors
+        x, wb, wf = ctx.saved_tensors
         stride, padding, dilation, groups = ctx.conf
         nx, nw = bool(ctx.needs_input_grad[0]), bool(ctx.needs_input_grad[1])
-        dx, dw, _ = torch.ops.aten.convolution_backward(gy, x, wb, None, stride, padding, dilation, False, [0, 0],
-                                                         groups, [nx, nw, False])
-        return dx, (dw.float() if nw else None), None, None, None, None, None
+        if wf is not None and nx:
+            dx = F.conv2d(gy.contiguous(memory_format=torch.channels_last), wf, None, 1, padding, 1, 1)
+            dw = (torch.ops.aten.convolution_backward(gy, x, wb, None, stride, padding, dilation, False, [0, 0],
+                                                      groups, [False, True, False])[1] if nw else None)
+        else:
+            dx, dw, _ = torch.ops.aten.convolution_backward(gy, x, wb, None, stride, padding, dilation, False,
+                                                             [0, 0], groups, [nx, nw, False])
+        return dx, (dw.float() if nw else None), None, None, None, None, None, None
 
 
 def _cw(conv: nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
@@ -110,7 +154,8 @@ def _cw(conv: nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
         x = x.to(torch.bfloat16)  # autocast's input cast
     if x.dtype != torch.bfloat16:
         return conv(x)
-    return _ShadowConv.apply(x, conv.weight, wb, conv.stride, conv.padding, conv.dilation, conv.groups)
+    wf = _shadow_live[-1].flipped(conv.weight) if torch.is_grad_enabled() else None
+    return _ShadowConv.apply(x, conv.weight, wb, wf, conv.stride, conv.padding, conv.dilation, conv.groups)
 
 
 class _GlobalAvgPoolCL(torch.autograd.Function):
@@ -266,11 +311,13 @@ class ResNet(nn.Module):
     _counted_bns: list = []
     _wshadow: WeightShadow | None = None
 
-    def set_weight_shadow(self, enabled: bool = True) -> "ResNet":
+    def set_weight_shadow(self, enabled: bool = True, dgrad_fwd: bool = True) -> "ResNet":
         """Read every convolution's bf16 weight from one shadow buffer refreshed by a single cast
         launch per forward, instead of autocast's cast per convolution (bf16 autocast only; the
-        parameters must already live in a FlatState, i.e. after CoDA(model))."""
-        self._wshadow = WeightShadow(self) if enabled else None
+        parameters must already live in a FlatState, i.e. after CoDA(model)). ``dgrad_fwd``: the
+        stride-1 3x3 convolutions' input gradients as forward convolutions with flipped weights
+        (_ShadowConv)."""
+        self._wshadow = WeightShadow(self, dgrad_fwd=dgrad_fwd) if enabled else None
         return self
 
     def set_fused_bn(self, enabled: bool = True) -> "ResNet":
@@ -304,7 +351,7 @@ class ResNet(nn.Module):
         live = (self._wshadow is not None and x.is_cuda and torch.is_autocast_enabled("cuda")
                 and torch.get_autocast_dtype("cuda") == torch.bfloat16)
         if live:
-            self._wshadow.refresh()
+            self._wshadow.refresh(flips=torch.is_grad_enabled())
             _shadow_live.append(self._wshadow)
         try:
             x = _bn_act(self.fused_bn, self.bn1, _cw(self.conv1, x))

@@ -81,6 +81,8 @@ class CoDA:
         self._ab_stage = torch.zeros(2, dtype=torch.float32, device=self.device)
         self.last_loss: torch.Tensor | None = None
         self._graph_on = False
+        self._graph_eager_update = False
+        self._graph_grads = False  # p.grad holds a graph's static gradient buffers
         self._graph = None
         self._graph_key = None
         self.graph_captures = 0
@@ -164,6 +166,16 @@ class CoDA:
         """main.py:303-334 without the round trigger: label map + p_hat, forward, surrogate,
         backward, pd_update, zero_grad. Stream-ordered with no host sync, so it can be
         captured in a HIP graph (the lr it bakes in changes only at a stage start)."""
+        if self._graph_grads:  # leave graph mode: the next backward must not add into its buffers
+            self.model.zero_grad(set_to_none=True)
+            self._graph_grads = False
+        loss = self._forward_backward(x, labels)
+        self.state.update(self.lr, self.gamma, self.mode)
+        self.model.zero_grad(set_to_none=True)
+        return loss
+
+    def _forward_backward(self, x: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
+        """main.py:303-326: label map + p_hat, forward, surrogate, backward (gradients in p.grad)."""
         st = self.state
         y8 = st.y8(labels.numel())
         ops.label_map_phat(labels, self.split_index, y8, st.lcounts, st.gcounts, st.p_hat)
@@ -172,30 +184,41 @@ class CoDA:
         else:
             loss = auc_surrogate(self.scores(x), y8, st.abalpha, st.p_hat, st.grad3)
         loss.backward(unit_seed(loss.device))  # no ones_like fill, no dF/dh * 1 pass
-        st.update(self.lr, self.gamma, self.mode)
-        self.model.zero_grad(set_to_none=True)
         return loss.detach()
 
     # ---------------------------------------------------------------- HIP graph replay
-    def use_graph(self, enable: bool = True) -> "CoDA":
+    def use_graph(self, enable: bool = True, eager_update: bool = False) -> "CoDA":
         """Replay step_body (label map, forward, surrogate, backward, pd_update, zero_grad) as ONE
         HIP graph: a small batch's step is bound by the ~200 kernel launches of the backbone, not
         by the GPU. The averaging round stays outside the graph (RCCL, every I steps), so the
         schedule is the reference's. The graph is captured at the first step of each (input
         shape, dtype, lr) — lr changes only at a stage start — after two warm-up bodies on a
         side stream whose effect on the state is undone; every replay reads the batch from the
-        graph's own input buffers, so the caller's tensors are copied in first."""
+        graph's own input buffers, so the caller's tensors are copied in first.
+
+        ``eager_update``: the graph holds label map -> forward -> surrogate -> backward only, and
+        the update (dppd_sg + running average, ONE launch) runs eagerly after each replay from
+        the gradients the replay left in the parameters' (static) .grad buffers. The update is
+        then an ordinary launch on the stream -- timed by events like in eager mode -- and lr is
+        not baked into the graph (no re-capture at a stage start)."""
         self._graph_on = bool(enable)
+        self._graph_eager_update = bool(enable and eager_update)
         self._graph = self._graph_key = None
+        if self._graph_grads:
+            self.model.zero_grad(set_to_none=True)
+            self._graph_grads = False
         return self
 
     def _graphed_body(self, x: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
-        key = (tuple(x.shape), x.dtype, x.stride(), tuple(labels.shape), labels.dtype, self.lr)
+        key = (tuple(x.shape), x.dtype, x.stride(), tuple(labels.shape), labels.dtype,
+               None if self._graph_eager_update else self.lr)
         if self._graph is None or self._graph_key != key:
             self._capture(x, labels, key)
         self._gx.copy_(x)
         self._gy.copy_(labels)
         self._graph.replay()
+        if self._graph_eager_update:
+            self.state.update(self.lr, self.gamma, self.mode)  # reads the replay's static .grad buffers
         # the graph's loss buffer is overwritten by the next replay: hand out a copy, as eager does
         return self._gloss.clone()
 
@@ -219,8 +242,16 @@ class CoDA:
         graph = torch.cuda.CUDAGraph()
         # thread_local: a communicator's helper threads (RCCL's proxy) may touch the runtime while
         # this thread captures; only this thread's calls must be capturable
+        if self._graph_grads:
+            self.model.zero_grad(set_to_none=True)
+            self._graph_grads = False
         with torch.cuda.graph(graph, capture_error_mode="thread_local"):
-            self._gloss = self.step_body(self._gx, self._gy)
+            if self._graph_eager_update:
+                # the backward's gradient tensors become p.grad (static: every replay rewrites them)
+                self._gloss = self._forward_backward(self._gx, self._gy)
+            else:
+                self._gloss = self.step_body(self._gx, self._gy)
+        self._graph_grads = self._graph_eager_update
         self._graph, self._graph_key = graph, key
         self.graph_captures += 1
 

@@ -32,7 +32,7 @@ def close(got, ref, what, rtol=RTOL, atol=ATOL):
 
 
 def run_rank(fixture: dict, rank: int, world: int, device, group=None, head: str = "softmax", graph: bool = False,
-             collective: bool | None = None):
+             collective: bool | None = None, eager_update: bool = False):
     from distributedauc_amd.coda import CoDA
 
     cfg = json.loads(str(fixture["config"]))
@@ -44,7 +44,7 @@ def run_rank(fixture: dict, rank: int, world: int, device, group=None, head: str
     net = net.to(device)
     coda = CoDA(net, lr=cfg["lr"], gamma=cfg["gamma"], T0=cfg["T0"], I=cfg["I"], split_index=cfg["split_index"],
                 world=world, rank=rank, group=group, device=device, head=head, collective=collective)
-    coda.use_graph(graph)
+    coda.use_graph(graph, eager_update=eager_update)
     xs, ys = fixture[f"r{rank}_x"], fixture[f"r{rank}_y"]
 
     def batches():

@@ -107,6 +107,24 @@ def test_coda_graph_replay_matches_eager_and_reference(dev, golden):
     coda_parity.compare(fx, 0, graphed)
 
 
+def test_coda_graph_eager_update_matches_eager_and_reference(dev, golden):
+    """use_graph(eager_update=True) (the bench's headline mode): label map -> forward -> surrogate
+    -> backward replayed from one graph, the update launched eagerly from the replay's static
+    gradient buffers. Same trajectory as eager, bit for bit, over 2 stages (lr not baked in: ONE
+    capture), and the reference's; switching back to eager steps afterwards stays exact."""
+    fx = _load(golden, 1)
+    eager, _ = coda_parity.run_rank(fx, 0, 1, dev)
+    graphed, coda = coda_parity.run_rank(fx, 0, 1, dev, graph=True, eager_update=True)
+    assert coda._graph is not None and coda.graph_captures == 1
+    for k in eager:
+        assert np.array_equal(eager[k], graphed[k]), k
+    coda_parity.compare(fx, 0, graphed)
+    # leaving graph mode: the static gradient buffers are dropped, eager backward starts from None
+    assert all(p.grad is not None for p in coda.model.parameters())
+    coda.use_graph(False)
+    assert all(p.grad is None for p in coda.model.parameters())
+
+
 def test_step_body_hip_graph_bitwise(dev, golden):
     """CoDA.step_body (label map, forward, surrogate, backward, pd_update, zero_grad) captured in a
     HIP graph and replayed 3 times from a saved state gives the same parameters, running average,

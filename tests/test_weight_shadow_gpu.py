@@ -1,5 +1,6 @@
 """The bf16 weight shadow (backbone.WeightShadow): one cast launch per forward instead of autocast's
-cast per convolution must change no bit of the step.
+cast per convolution must change no bit of the step; the 3x3 input gradients as forward
+convolutions with flipped weights (dgrad_fwd) change only the summation order.
 
 Reference: the same backbone under torch's bf16 autocast (main.py:311-326's forward/backward, the
 autocast the trainer adds), where each conv casts its fp32 weight itself. Same model, same input,
@@ -21,7 +22,7 @@ def _bits(t):
     return t.view(torch.int16 if t.element_size() == 2 else torch.int32).cpu()
 
 
-def _run(dev, arch, shadow, size):
+def _run(dev, arch, shadow, size, dgrad_fwd=False):
     from distributedauc_amd import conv1x1
     from distributedauc_amd.backbone import build_backbone
     from distributedauc_amd.coda import CoDA
@@ -31,6 +32,8 @@ def _run(dev, arch, shadow, size):
     net.set_fused_bn(True).set_gemm_conv1x1(True).train()
     coda = CoDA(net, lr=0.01, split_index=4, autocast_dtype=torch.bfloat16, device=dev, weight_shadow=shadow)
     assert (net._wshadow is not None) == shadow
+    if shadow and not dgrad_fwd:
+        net.set_weight_shadow(True, dgrad_fwd=False)  # torch's backward-data: bit-identical
     g = torch.Generator(device=dev).manual_seed(11)
     x = torch.randn((8, 3, size, size), device=dev, generator=g).contiguous(memory_format=torch.channels_last)
     y = torch.tensor([9, 0, 7, 1, 5, 3, 8, 2], device=dev)
@@ -69,3 +72,51 @@ def test_weight_shadow_needs_flat_state(dev):
     net = resnet18().to(dev)
     with pytest.raises(RuntimeError, match="FlatState"):
         net.set_weight_shadow(True)
+
+
+@pytest.mark.parametrize("shape", [(4, 64, 56, 56), (4, 128, 28, 28), (8, 512, 7, 7), (2, 24, 9, 13)])
+def test_dgrad_as_forward_conv(dev, shape):
+    """_ShadowConv with the flipped weight: dx = conv2d(dy, W') against torch's convolution backward
+    on the same bf16 operands: within one bf16 rounding of the fp64 result (both accumulate in fp32),
+    and the weight gradient bit-identical (same call)."""
+    from distributedauc_amd.backbone import _ShadowConv
+
+    N, C, H, W = shape
+    g = torch.Generator(device=dev).manual_seed(5)
+    x = torch.randn(shape, device=dev, generator=g).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    w = (torch.randn((C, C, 3, 3), device=dev, generator=g) / (3 * C ** 0.5)).to(torch.bfloat16)
+    w = w.contiguous(memory_format=torch.channels_last)
+    wf = w.flip(2, 3).transpose(0, 1).contiguous(memory_format=torch.channels_last)
+    gy = torch.randn(shape, device=dev, generator=g).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    p = torch.zeros((C, C, 3, 3), device=dev, requires_grad=True)
+    xa = x.clone().requires_grad_(True)
+    ya = _ShadowConv.apply(xa, p, w, wf, (1, 1), (1, 1), (1, 1), 1)
+    ya.backward(gy)
+    xb = x.clone().requires_grad_(True)
+    pb = torch.zeros((C, C, 3, 3), device=dev, requires_grad=True)
+    yb = _ShadowConv.apply(xb, pb, w, None, (1, 1), (1, 1), (1, 1), 1)
+    yb.backward(gy)
+    assert torch.equal(ya, yb)
+    assert xa.grad.is_contiguous(memory_format=torch.channels_last)
+    ref = torch.nn.functional.conv2d(gy.double(), wf.double(), padding=1)
+    scale = ref.abs().max()
+    for got in (xa.grad, xb.grad):
+        err = (got.double() - ref).abs()
+        assert float((err - ref.abs() * 2 ** -8).max()) <= float(scale) * 1e-5, float(err.max())
+    assert torch.equal(p.grad, pb.grad)
+
+
+def test_weight_shadow_dgrad_fwd_step_close(dev):
+    """The whole ResNet-50 step with dgrad_fwd against torch's backward-data: scores identical (the
+    forward is untouched), every gradient within bf16 summation-order noise of the other."""
+    det = torch.backends.cudnn.deterministic
+    torch.backends.cudnn.deterministic = True
+    try:
+        a = _run(dev, "resnet50", True, 64, dgrad_fwd=False)
+        b = _run(dev, "resnet50", True, 64, dgrad_fwd=True)
+    finally:
+        torch.backends.cudnn.deterministic = det
+    assert torch.equal(_bits(a[0]), _bits(b[0]))
+    for i, (ga, gb) in enumerate(zip(a[1], b[1])):
+        scale = float(ga.abs().max().clamp_min(1e-30))
+        assert float((ga - gb).abs().max()) <= 0.05 * scale, (i, float((ga - gb).abs().max()), scale)
