@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 O=gpurun_out/r05g
 mkdir -p $O
-timeout -k 10 500 python -u -m pytest tests/test_weight_shadow_gpu.py tests/test_maxpool_gpu.py tests/test_coda_gpu.py \
+timeout -k 10 500 python -u -m pytest tests/test_weight_shadow_gpu.py \
     -q --timeout 200 --timeout-method thread > $O/pytest_new.log 2>&1
 rc=$?; echo "tests rc=$rc"; tail -3 $O/pytest_new.log
 [ $rc -eq 0 ] || exit $rc

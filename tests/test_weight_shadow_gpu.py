@@ -11,6 +11,7 @@ forwards is seen by the next forward (the shadow is refreshed per forward).
 """
 from __future__ import annotations
 
+import numpy as np
 import pytest
 import torch
 
@@ -22,7 +23,7 @@ def _bits(t):
     return t.view(torch.int16 if t.element_size() == 2 else torch.int32).cpu()
 
 
-def _run(dev, arch, shadow, size, dgrad_fwd=False):
+def _run(dev, arch, shadow, size, dgrad_fwd=False, autocast=True):
     from distributedauc_amd import conv1x1
     from distributedauc_amd.backbone import build_backbone
     from distributedauc_amd.coda import CoDA
@@ -30,7 +31,8 @@ def _run(dev, arch, shadow, size, dgrad_fwd=False):
     torch.manual_seed(7)
     net = build_backbone(arch, num_classes=2).to(dev).to(memory_format=torch.channels_last)
     net.set_fused_bn(True).set_gemm_conv1x1(True).train()
-    coda = CoDA(net, lr=0.01, split_index=4, autocast_dtype=torch.bfloat16, device=dev, weight_shadow=shadow)
+    coda = CoDA(net, lr=0.01, split_index=4, autocast_dtype=torch.bfloat16 if autocast else None, device=dev,
+                weight_shadow=shadow)
     assert (net._wshadow is not None) == shadow
     if shadow and not dgrad_fwd:
         net.set_weight_shadow(True, dgrad_fwd=False)  # torch's backward-data: bit-identical
@@ -74,49 +76,69 @@ def test_weight_shadow_needs_flat_state(dev):
         net.set_weight_shadow(True)
 
 
+def _rel_excess(got, ref):
+    """max over elements of (|got - ref| - |ref| * 2^-8) / max|ref|: <= ~0 when got is ref rounded
+    once to bf16 (an fp32-accumulated sum rounded once)."""
+    err = (got.double() - ref).abs()
+    return float((err - ref.abs() * 2 ** -8).max() / ref.abs().max())
+
+
 @pytest.mark.parametrize("shape", [(4, 64, 56, 56), (4, 128, 28, 28), (8, 512, 7, 7), (2, 24, 9, 13)])
 def test_dgrad_as_forward_conv(dev, shape):
-    """_ShadowConv with the flipped weight: dx = conv2d(dy, W') against torch's convolution backward
-    on the same bf16 operands: within one bf16 rounding of the fp64 result (both accumulate in fp32),
-    and the weight gradient bit-identical (same call)."""
+    """_ShadowConv with the flipped weight: dx = conv2d(dy, W') against the fp64 result of the same
+    bf16 operands: one bf16 rounding of an fp32 sum (the forward solvers accumulate in fp32). torch's
+    backward-data on the same operands is reported beside it (MIOpen's split accumulation may round
+    more than once). Forward output and weight gradient: the same calls, bit-identical under
+    deterministic solvers."""
     from distributedauc_amd.backbone import _ShadowConv
 
-    N, C, H, W = shape
-    g = torch.Generator(device=dev).manual_seed(5)
-    x = torch.randn(shape, device=dev, generator=g).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
-    w = (torch.randn((C, C, 3, 3), device=dev, generator=g) / (3 * C ** 0.5)).to(torch.bfloat16)
-    w = w.contiguous(memory_format=torch.channels_last)
-    wf = w.flip(2, 3).transpose(0, 1).contiguous(memory_format=torch.channels_last)
-    gy = torch.randn(shape, device=dev, generator=g).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
-    p = torch.zeros((C, C, 3, 3), device=dev, requires_grad=True)
-    xa = x.clone().requires_grad_(True)
-    ya = _ShadowConv.apply(xa, p, w, wf, (1, 1), (1, 1), (1, 1), 1)
-    ya.backward(gy)
-    xb = x.clone().requires_grad_(True)
-    pb = torch.zeros((C, C, 3, 3), device=dev, requires_grad=True)
-    yb = _ShadowConv.apply(xb, pb, w, None, (1, 1), (1, 1), (1, 1), 1)
-    yb.backward(gy)
-    assert torch.equal(ya, yb)
-    assert xa.grad.is_contiguous(memory_format=torch.channels_last)
-    ref = torch.nn.functional.conv2d(gy.double(), wf.double(), padding=1)
-    scale = ref.abs().max()
-    for got in (xa.grad, xb.grad):
-        err = (got.double() - ref).abs()
-        assert float((err - ref.abs() * 2 ** -8).max()) <= float(scale) * 1e-5, float(err.max())
-    assert torch.equal(p.grad, pb.grad)
-
-
-def test_weight_shadow_dgrad_fwd_step_close(dev):
-    """The whole ResNet-50 step with dgrad_fwd against torch's backward-data: scores identical (the
-    forward is untouched), every gradient within bf16 summation-order noise of the other."""
     det = torch.backends.cudnn.deterministic
     torch.backends.cudnn.deterministic = True
     try:
+        N, C, H, W = shape
+        g = torch.Generator(device=dev).manual_seed(5)
+        x = torch.randn(shape, device=dev, generator=g).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        w = (torch.randn((C, C, 3, 3), device=dev, generator=g) / (3 * C ** 0.5)).to(torch.bfloat16)
+        w = w.contiguous(memory_format=torch.channels_last)
+        wf = w.flip(2, 3).transpose(0, 1).contiguous(memory_format=torch.channels_last)
+        gy = torch.randn(shape, device=dev, generator=g).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        p = torch.zeros((C, C, 3, 3), device=dev, requires_grad=True)
+        xa = x.clone().requires_grad_(True)
+        ya = _ShadowConv.apply(xa, p, w, wf, (1, 1), (1, 1), (1, 1), 1)
+        ya.backward(gy)
+        xb = x.clone().requires_grad_(True)
+        pb = torch.zeros((C, C, 3, 3), device=dev, requires_grad=True)
+        yb = _ShadowConv.apply(xb, pb, w, None, (1, 1), (1, 1), (1, 1), 1)
+        yb.backward(gy)
+    finally:
+        torch.backends.cudnn.deterministic = det
+    assert torch.equal(ya, yb)
+    assert torch.equal(p.grad, pb.grad)
+    assert xa.grad.is_contiguous(memory_format=torch.channels_last)
+    ref = torch.nn.functional.conv2d(gy.double(), wf.double(), padding=1)
+    ours, theirs = _rel_excess(xa.grad, ref), _rel_excess(xb.grad, ref)
+    assert ours <= 1e-5, (ours, theirs)
+
+
+def test_weight_shadow_dgrad_fwd_step_close(dev):
+    """The whole ResNet-50 step with dgrad_fwd against torch's backward-data, both against the fp32
+    step (no autocast): the forward is untouched (scores identical) and every gradient is as close
+    to fp32 as torch's bf16 step is (bf16 rounding differences propagate through 50 layers, so
+    the two bf16 steps differ from each other by about as much as each differs from fp32)."""
+    det = torch.backends.cudnn.deterministic
+    torch.backends.cudnn.deterministic = True
+    try:
+        ref = _run(dev, "resnet50", False, 64, autocast=False)
         a = _run(dev, "resnet50", True, 64, dgrad_fwd=False)
         b = _run(dev, "resnet50", True, 64, dgrad_fwd=True)
     finally:
         torch.backends.cudnn.deterministic = det
     assert torch.equal(_bits(a[0]), _bits(b[0]))
-    for i, (ga, gb) in enumerate(zip(a[1], b[1])):
-        scale = float(ga.abs().max().clamp_min(1e-30))
-        assert float((ga - gb).abs().max()) <= 0.05 * scale, (i, float((ga - gb).abs().max()), scale)
+    ea, eb = [], []
+    for g32, ga, gb in zip(ref[1], a[1], b[1]):
+        scale = float(g32.abs().max().clamp_min(1e-30))
+        ea.append(float((ga - g32).abs().max()) / scale)
+        eb.append(float((gb - g32).abs().max()) / scale)
+    ea, eb = np.array(ea), np.array(eb)
+    assert np.median(eb) <= 1.5 * np.median(ea) + 1e-3, (np.median(eb), np.median(ea))
+    assert eb.max() <= 2.0 * ea.max() + 1e-2, (eb.max(), ea.max())
