@@ -182,6 +182,14 @@ def _conv_dgrad(gy, x, wc):
                                                False, [0, 0], 1, [True, False, False])[0]
 
 
+def _fconv_dgrad(gy, wc):
+    """dx = dy @ W as a FORWARD 1x1 convolution of dy with W^T (C_in' = cout, C_out' = cin): the
+    forward solvers (CK, no output zero-fill) instead of MIOpen's backward-data kernel, which zeroes
+    its output first (ResNet-50 layer1 256 -> 64: 102 + 25 us against a ~42 us forward)."""
+    cout, cin = wc.shape
+    return F.conv2d(gy, wc.t().contiguous().view(cin, cout, 1, 1)).contiguous(memory_format=torch.channels_last)
+
+
 def _dgrad(gy, g2, x, wc):
     """dx = dy @ W (a new channels-last tensor)."""
     N, cin, H, W = x.shape
@@ -189,9 +197,12 @@ def _dgrad(gy, g2, x, wc):
     M = N * H * W
     with torch.autocast("cuda", enabled=False):
         eng = _choose((M, cin, cout, x.dtype, "dgrad"),
-                      {"gemm": lambda: torch.mm(g2, wc), "conv": lambda: _conv_dgrad(gy, x, wc)})
+                      {"gemm": lambda: torch.mm(g2, wc), "conv": lambda: _conv_dgrad(gy, x, wc),
+                       "fconv": lambda: _fconv_dgrad(gy, wc)})
         if eng == "gemm":
             return torch.mm(g2, wc).view(N, H, W, cin).permute(0, 3, 1, 2)
+        if eng == "fconv":
+            return _fconv_dgrad(gy, wc)
         return _conv_dgrad(gy, x, wc).contiguous(memory_format=torch.channels_last)
 
 
@@ -213,15 +224,18 @@ def _dgrad_acc(base, gy, g2, x, wc):
             _loaded.append(True)
         eng = None if _fixed else plans.get(key)
         if eng is None and _fixed:
-            eng = _choose(key, {"gemm": None, "conv": None})  # fixed_engine(): named, never timed
+            eng = _choose(key, {"gemm": None, "conv": None, "fconv": None})  # fixed_engine(): never timed
         elif eng is None:
             scratch = base.clone(memory_format=torch.channels_last)
             s2 = scratch.permute(0, 2, 3, 1).reshape(M, cin)
             eng = _choose(key, {"gemm": lambda: s2.addmm_(g2, wc),
-                                "conv": lambda: scratch.add_(_conv_dgrad(gy, x, wc))})
+                                "conv": lambda: scratch.add_(_conv_dgrad(gy, x, wc)),
+                                "fconv": lambda: scratch.add_(_fconv_dgrad(gy, wc))})
             del scratch, s2
         if eng == "gemm":
             b2.addmm_(g2, wc)
+        elif eng == "fconv":
+            base.add_(_fconv_dgrad(gy, wc))
         else:
             base.add_(_conv_dgrad(gy, x, wc))
     return base

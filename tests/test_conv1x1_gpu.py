@@ -21,7 +21,8 @@ def _err(got, ref):
 
 
 @pytest.mark.parametrize("shape", [(4, 64, 256, 14), (2, 256, 64, 28), (8, 512, 2048, 7), (3, 128, 96, 5)])
-@pytest.mark.parametrize("engines", [("gemm", "gemm", "gemm32"), ("conv", "conv", "conv"), ("gemm", "conv", "gemm8")])
+@pytest.mark.parametrize("engines", [("gemm", "gemm", "gemm32"), ("conv", "conv", "conv"), ("gemm", "conv", "gemm8"),
+                                     ("conv", "fconv", "gemm8")])
 def test_conv1x1_engines(dev, shape, engines):
     from distributedauc_amd import conv1x1 as C
 
@@ -82,10 +83,11 @@ def test_resnet_fast_paths_at_bench_shape(dev):
 
 @pytest.mark.parametrize("down", [0, 1, 2])
 @pytest.mark.parametrize("owned", [False, True])
-@pytest.mark.parametrize("acc_engine", ["gemm", "conv"])
+@pytest.mark.parametrize("acc_engine", ["gemm", "conv", "fconv"])
 def test_conv1x1_skip_fuses_branch_gradient(dev, down, owned, acc_engine):
     """(conv1(x), skip) in one node: dx = dgrad(conv1) + d(skip), the sum accumulated by the GEMM
-    (beta = 1, in place) or by an add after MIOpen's dgrad; skip = identity (down 0) or a 1x1
+    (beta = 1, in place) or by an add after MIOpen's dgrad (or the forward convolution with W^T);
+    skip = identity (down 0) or a 1x1
     downsample of stride 1 (GEMM) / 2 (MIOpen); vs fp64 autograd of the two branches.
     Also: the incoming skip gradient is left untouched unless the caller marked it as owned."""
     from distributedauc_amd import conv1x1 as C
