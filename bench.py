@@ -120,9 +120,10 @@ def parse(argv=None):
     p.add_argument("--graph", type=int, default=0,
                    help="headline step: replay label map -> forward -> surrogate -> backward from one HIP graph, "
                         "the update launched eagerly after each replay (1) or everything eager (0)")
-    p.add_argument("--weight-shadow", type=int, default=2,
+    p.add_argument("--weight-shadow", type=int, default=3,
                    help="bf16 conv weights from one shadow cast per forward (1), + the stride-1 3x3 input "
-                        "gradients as forward convolutions with flipped weights (2), or autocast's cast per conv (0)")
+                        "gradients as forward convolutions with flipped weights (2), + the 3x3 weight gradients "
+                        "from the HIP MFMA kernel (3), or autocast's cast per conv (0)")
     p.add_argument("--gemm-conv1x1", type=int, default=1,
                    help="stride-1 1x1 convs as hipBLASLt GEMMs where faster (per-shape timing; 1/0)")
     # internal: one process of the configs[0] CPU baseline (never touches the GPU)
@@ -245,8 +246,8 @@ def make_coda(arch, batch, image_size, I, pos_ratio, pool, world, rank, device, 
     coda = CoDA(net, lr=lr, gamma=2000.0, T0=10 ** 9, I=I, split_index=split, world=world, rank=rank,
                 autocast_dtype=torch.bfloat16, device=device, collective=grouped(),
                 weight_shadow=None if weight_shadow is None else bool(weight_shadow))
-    if weight_shadow == 1:
-        net.set_weight_shadow(True, dgrad_fwd=False)
+    if weight_shadow in (1, 2):
+        net.set_weight_shadow(True, dgrad_fwd=weight_shadow == 2, wgrad_hip=False)
     it = iter(loader)
     coda.average_all()            # main.py:141-142
     coda.begin_stage(1, it)       # alpha estimate + anchors (untimed)

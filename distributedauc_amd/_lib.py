@@ -82,6 +82,9 @@ SIGNATURES = {
     "dauc_maxpool2d_forward": (_int, [_vp, _int, _i64, _int, _int, _int, _int, _int, _int, _vp, _vp, _int, _int,
                                       _vp]),
     "dauc_slab_sum": (_int, [_vp, _i64, _i64, _vp, _vp]),
+    "dauc_conv3x3_wgrad_workspace_size": (_sz, [_i64, _int, _int, _int, _int]),
+    "dauc_conv3x3_wgrad": (_int, [_vp, _vp, _int, _i64, _int, _int, _int, _int, _int, _int, _int, _vp, _vp, _sz,
+                                  _vp]),
     "dauc_maxpool2d_backward": (_int, [_vp, _vp, _int, _i64, _int, _int, _int, _int, _int, _int, _int, _int, _vp,
                                        _vp]),
 }
@@ -95,6 +98,7 @@ TUNING_SIGNATURES = {
     "dauc_pair_count_variant": (_int, [_vp, _i64, _vp, _i64, _vp, _int, _vp]),
     "dauc_set_search_mode": (_int, [_int]),
     "dauc_set_direct_fault": (_int, [_int]),
+    "dauc_probe_tr16": (_int, [_vp, _vp]),
 }
 TUNING_LIB_PATH = Path(os.environ.get("DAUC_TUNING_LIB", PKG_DIR.parent / "tuning" / "libdauc_tuning.so"))
 

@@ -52,11 +52,12 @@ class WeightShadow:
     with ``dgrad_fwd``, each stride-1 'same' k x k convolution's weight flipped and transposed
     (W'[ci, co, kh, kw] = W[co, ci, k-1-kh, k-1-kw], channels-last) for its input gradient."""
 
-    def __init__(self, model: nn.Module, dgrad_fwd: bool = False):
+    def __init__(self, model: nn.Module, dgrad_fwd: bool = False, wgrad_hip: bool = False):
         flat = getattr(model, "_dauc_flat", None)
         if flat is None:
             raise RuntimeError("the weight shadow mirrors the FlatState buffer: build CoDA / FlatState first")
         self.src = flat.params
+        self.wgrad_hip = bool(wgrad_hip)
         dev = self.src.device
         self.buf = torch.empty(self.src.numel(), dtype=torch.bfloat16, device=dev)
         self.views: dict[int, torch.Tensor] = {}
@@ -122,11 +123,12 @@ class _ShadowConv(torch.autograd.Function):
     products, fp32 accumulation in another order: the bits of dx differ from torch's."""
 
     @staticmethod
-    def forward(ctx, x, weight, wb, wf, stride, padding, dilation, groups):
+    def forward(ctx, x, weight, wb, wf, stride, padding, dilation, groups, wgrad_hip=False):
         with torch.autocast("cuda", enabled=False):
             y = F.conv2d(x, wb, None, stride, padding, dilation, groups)
         ctx.save_for_backward(x, wb, wf)
         ctx.conf = (list(stride), list(padding), list(dilation), groups)
+        ctx.wgrad_hip = bool(wgrad_hip)
         return y
 
     @staticmethod
@@ -134,14 +136,26 @@ class _ShadowConv(torch.autograd.Function):
         x, wb, wf = ctx.saved_tensors
         stride, padding, dilation, groups = ctx.conf
         nx, nw = bool(ctx.needs_input_grad[0]), bool(ctx.needs_input_grad[1])
+        dx = dw = None
+        if nw and ctx.wgrad_hip and wb.shape[2:] == (3, 3):
+            from . import ops
+
+            gyc = gy.contiguous(memory_format=torch.channels_last)
+            if ops.conv3x3_wgrad_supported(x, gyc, stride, padding, dilation, groups):
+                # the fp32 master gradient straight from csrc/conv_wgrad.hip (no bf16 round trip)
+                dw = ops.conv3x3_wgrad(x, gyc, stride[0])
+        mw = nw and dw is None
         if wf is not None and nx:
             dx = F.conv2d(gy.contiguous(memory_format=torch.channels_last), wf, None, 1, padding, 1, 1)
-            dw = (torch.ops.aten.convolution_backward(gy, x, wb, None, stride, padding, dilation, False, [0, 0],
-                                                      groups, [False, True, False])[1] if nw else None)
-        else:
-            dx, dw, _ = torch.ops.aten.convolution_backward(gy, x, wb, None, stride, padding, dilation, False,
-                                                             [0, 0], groups, [nx, nw, False])
-        return dx, (dw.float() if nw else None), None, None, None, None, None, None
+            if mw:
+                dw = torch.ops.aten.convolution_backward(gy, x, wb, None, stride, padding, dilation, False, [0, 0],
+                                                         groups, [False, True, False])[1].float()
+        elif nx or mw:
+            dx, dwb, _ = torch.ops.aten.convolution_backward(gy, x, wb, None, stride, padding, dilation, False,
+                                                              [0, 0], groups, [nx, mw, False])
+            if mw:
+                dw = dwb.float()
+        return dx, dw, None, None, None, None, None, None, None
 
 
 def _cw(conv: nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
@@ -154,8 +168,10 @@ def _cw(conv: nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
         x = x.to(torch.bfloat16)  # autocast's input cast
     if x.dtype != torch.bfloat16:
         return conv(x)
-    wf = _shadow_live[-1].flipped(conv.weight) if torch.is_grad_enabled() else None
-    return _ShadowConv.apply(x, conv.weight, wb, wf, conv.stride, conv.padding, conv.dilation, conv.groups)
+    sh = _shadow_live[-1]
+    wf = sh.flipped(conv.weight) if torch.is_grad_enabled() else None
+    return _ShadowConv.apply(x, conv.weight, wb, wf, conv.stride, conv.padding, conv.dilation, conv.groups,
+                             sh.wgrad_hip)
 
 
 class _GlobalAvgPoolCL(torch.autograd.Function):
@@ -311,13 +327,14 @@ class ResNet(nn.Module):
     _counted_bns: list = []
     _wshadow: WeightShadow | None = None
 
-    def set_weight_shadow(self, enabled: bool = True, dgrad_fwd: bool = True) -> "ResNet":
+    def set_weight_shadow(self, enabled: bool = True, dgrad_fwd: bool = True, wgrad_hip: bool = True) -> "ResNet":
         """Read every convolution's bf16 weight from one shadow buffer refreshed by a single cast
         launch per forward, instead of autocast's cast per convolution (bf16 autocast only; the
         parameters must already live in a FlatState, i.e. after CoDA(model)). ``dgrad_fwd``: the
         stride-1 3x3 convolutions' input gradients as forward convolutions with flipped weights
-        (_ShadowConv)."""
-        self._wshadow = WeightShadow(self, dgrad_fwd=dgrad_fwd) if enabled else None
+        (_ShadowConv). ``wgrad_hip``: the 3x3 weight gradients from csrc/conv_wgrad.hip (fp32, MFMA)
+        instead of MIOpen's backward-weights + the bf16 -> fp32 cast."""
+        self._wshadow = WeightShadow(self, dgrad_fwd=dgrad_fwd, wgrad_hip=wgrad_hip) if enabled else None
         return self
 
     def set_fused_bn(self, enabled: bool = True) -> "ResNet":

@@ -1,0 +1,266 @@
+// Weight gradient of the backbone's 3x3 convolutions (pad 1, stride 1 or 2), channels-last bf16,
+// as a split-K MFMA implicit GEMM with an fp32 result.
+//
+// Reference: the ResNet blocks' 3x3 convolutions (imagenet/resnet.py:72-85 conv3x3, Bottleneck.conv2
+// resnet.py:87-108) trained by main.py:326 (loss.backward). torch under bf16 autocast runs MIOpen's
+// backward-weights kernel, which zero-fills an fp32 workspace, accumulates into it with atomics,
+// casts the result to bf16, and autograd then casts it back to the fp32 master weight's dtype:
+// ResNet-50 b256, 16 launches of 115-160 us at ~15 % of the bf16 MFMA peak, plus a zero-fill and
+// two casts each, and a bf16-rounded gradient.
+//
+//   dW[co][kh][kw][ci] = sum over output pixels q = (n, ho, wo) of
+//                        dy[q][co] * x[n][ho*s - 1 + kh][wo*s - 1 + kw][ci]   (0 outside the image)
+//
+// is a GEMM C[M = Co][N = 9 * Ci] = A[M][K] * B[K][N] with K = the N*Ho*Wo output pixels. Both
+// operands are stored K-major (pixel rows of channels), so they are staged into LDS as loaded (one
+// 16-byte vector per thread and row) and read with gfx950's transposing LDS read
+// (ds_read_b64_tr_b16: 4 pixel rows x 16 channels -> each lane gets one channel's 4 consecutive
+// pixels), which is exactly the k-run the 16x16x32 bf16 MFMA fragments take.
+//
+// A workgroup (8 waves) owns a 64-output-channel x (9 taps x 64 input-channel) tile of C and a
+// contiguous range of 64-pixel K chunks (split-K); per chunk it stages dy's 64 x 64 tile and the 9
+// taps' 64 x 64 gathers of x (halo rows -> zeros), then every wave runs 18 MFMAs per 32-pixel k-step
+// (2 output-channel tiles x 9 (tap, input-channel) tiles of 16 x 16). The next chunk's global loads
+// are issued before the current chunk's MFMAs (register double buffering). Each split writes its
+// fp32 partial C to a slab; dauc_slab_sum adds the slabs in split order (no atomics): bitwise
+// reproducible, one fp32 rounding per product sum instead of MIOpen's bf16 rounding.
+
+#include <hip/hip_bf16.h>
+
+#include "dauc_internal.h"
+
+namespace dauc {
+namespace {
+
+typedef short v4s __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4s lds_v4s;
+
+constexpr int kWgThreads = 512;  // 8 waves
+constexpr int kBM = 64;          // output channels per tile
+constexpr int kBC = 64;          // input channels per tile (per tap)
+constexpr int kKT = 64;          // output pixels per K chunk
+constexpr int kRow = 72;         // LDS row stride in bf16 elements (64 + 8: 144-byte rows)
+constexpr int kTaps = 9;
+constexpr int kTile = kKT * kRow;  // one staged [pixel][channel] tile, elements
+
+struct WgradGeom {
+    int N, H, W, Ci, Ho, Wo, Co, stride;
+    int64_t P;        // output pixels N * Ho * Wo
+    int64_t chunks;   // ceil(P / kKT)
+    int64_t cps;      // chunks per split
+    int ctiles;       // Ci / kBC
+};
+
+// one lane's half fragment: rows r0 .. r0 + 3 of a staged [pixel][channel] tile, channels
+// c0 .. c0 + 15 across the lane's 16-lane group -> 4 consecutive pixels of channel c0 + (lane & 15)
+__device__ __forceinline__ v4s tr_read(const short* tile, int r0, int c0, int lane) {
+    const int i = lane & 15;
+    const short* p = tile + (r0 + (i >> 2)) * kRow + c0 + 4 * (i & 3);
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)p);
+}
+
+// the 16x16x32 operand fragment of k-step ks (32 pixels) for channel block c0: lane group
+// g = lane >> 4 holds pixels 32 ks + 8 g + (0 .. 7)
+__device__ __forceinline__ bf16x8 frag(const short* tile, int ks, int c0, int lane) {
+    const int r0 = 32 * ks + 8 * (lane >> 4);
+    const v4s lo = tr_read(tile, r0, c0, lane);
+    const v4s hi = tr_read(tile, r0 + 4, c0, lane);
+    const v4s f[2] = {lo, hi};
+    return *reinterpret_cast<const bf16x8*>(f);
+}
+
+// one thread's share of a chunk's staging: the dy vector and the 9 taps' x vectors of one pixel row,
+// with the in-image bits (bit t: tap t's pixel exists; bit 9: the output pixel exists)
+struct Staging {
+    uint4 a, b[kTaps];
+    unsigned ok;
+};
+
+// every load is issued unconditionally (a clamped in-bounds address; out-of-range rows are zeroed
+// when staged, after the loads have long landed): a branch or select right behind each load would
+// make the compiler wait for each one in turn
+__device__ __forceinline__ void load_chunk(Staging& s, const __hip_bfloat16* __restrict__ x,
+                                           const __hip_bfloat16* __restrict__ dy, const WgradGeom& g,
+                                           int64_t chunk, int pr, int v, int co0, int ci0) {
+    const int64_t q0 = chunk * kKT + pr;
+    const bool qok = q0 < g.P;
+    const unsigned q = static_cast<unsigned>(qok ? q0 : g.P - 1);  // P < 2^31 (host check)
+    s.a = *reinterpret_cast<const uint4*>(dy + int64_t(q) * g.Co + co0 + 8 * v);
+    const unsigned hw = static_cast<unsigned>(g.Ho * g.Wo);
+    const unsigned n = q / hw, r = q - n * hw;
+    const int ho = static_cast<int>(r / static_cast<unsigned>(g.Wo));
+    const int wo = static_cast<int>(r) - ho * g.Wo;
+    const int ih0 = ho * g.stride - 1, iw0 = wo * g.stride - 1;
+    const __hip_bfloat16* xn = x + int64_t(n) * g.H * g.W * g.Ci + ci0 + 8 * v;
+    unsigned m = qok ? (1u << kTaps) : 0u;
+#pragma unroll
+    for (int t = 0; t < kTaps; ++t) {
+        const int ih = ih0 + t / 3, iw = iw0 + t % 3;
+        const bool in = qok & (ih >= 0) & (ih < g.H) & (iw >= 0) & (iw < g.W);
+        m |= in ? (1u << t) : 0u;
+        const int ihc = min(max(ih, 0), g.H - 1), iwc = min(max(iw, 0), g.W - 1);
+        s.b[t] = *reinterpret_cast<const uint4*>(xn + (int64_t(ihc) * g.W + iwc) * g.Ci);
+    }
+    s.ok = m;
+}
+
+// the in-image bit as an AND mask (a select of the two values would become a select of their
+// addresses, i.e. the staging registers spilled to scratch)
+__device__ __forceinline__ uint4 masked(uint4 u, unsigned ok, int bit) {
+    const unsigned m = 0u - ((ok >> bit) & 1u);
+    u.x &= m;
+    u.y &= m;
+    u.z &= m;
+    u.w &= m;
+    return u;
+}
+
+__device__ __forceinline__ void stage_chunk(const Staging& s, short* lds, int pr, int v) {
+    *reinterpret_cast<uint4*>(lds + pr * kRow + 8 * v) = masked(s.a, s.ok, kTaps);
+#pragma unroll
+    for (int t = 0; t < kTaps; ++t)
+        *reinterpret_cast<uint4*>(lds + (1 + t) * kTile + pr * kRow + 8 * v) = masked(s.b[t], s.ok, t);
+}
+
+__global__ __launch_bounds__(kWgThreads) void wgrad3x3_kernel(const __hip_bfloat16* __restrict__ x,
+                                                              const __hip_bfloat16* __restrict__ dy,
+                                                              WgradGeom g, float* __restrict__ out) {
+    __shared__ short lds[(1 + kTaps) * kTile];  // A tile, then the 9 taps' B tiles
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int co0 = (blockIdx.x / g.ctiles) * kBM, ci0 = (blockIdx.x % g.ctiles) * kBC;
+    const int64_t c_begin = int64_t(blockIdx.y) * g.cps;
+    const int64_t c_end = c_begin + g.cps < g.chunks ? c_begin + g.cps : g.chunks;
+
+    // staging: thread -> (pixel row pr, 16-byte vector v) of every tile
+    const int pr = tid >> 3, v = tid & 7;
+    Staging cur;
+    load_chunk(cur, x, dy, g, c_begin, pr, v, co0, ci0);
+
+    // wave tiles: output-channel tiles 2 (wave & 1) + a, a < 2; (tap, input-channel) tiles
+    // 9 (wave >> 1) + b, b < 9 -> tap = tile >> 2, channel block 16 (tile & 3)
+    f32x4v acc[2][9];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 9; ++b) acc[a][b] = f32x4v{0.f, 0.f, 0.f, 0.f};
+    const int mt0 = 2 * (wave & 1), nt0 = 9 * (wave >> 1);
+
+    // every split owns >= 1 chunk (host); the loads are unconditional (the last chunk's "next" is
+    // itself again): a branch around them would force the loaded registers through copies that
+    // wait for each load
+    for (int64_t c = c_begin; c < c_end; ++c) {
+        __syncthreads();  // the previous chunk's fragment reads are done
+        stage_chunk(cur, lds, pr, v);
+        __syncthreads();
+        load_chunk(cur, x, dy, g, c + 1 < c_end ? c + 1 : c, pr, v, co0, ci0);  // in flight during the MFMAs
+        __builtin_amdgcn_sched_barrier(0);  // keep the loads ahead of the MFMAs (the scheduler sinks them)
+#pragma unroll
+        for (int ks = 0; ks < kKT / 32; ++ks) {
+            bf16x8 fa[2];
+#pragma unroll
+            for (int a = 0; a < 2; ++a) fa[a] = frag(lds, ks, 16 * (mt0 + a), lane);
+#pragma unroll
+            for (int b = 0; b < 9; ++b) {
+                const int t = nt0 + b;
+                const bf16x8 fb = frag(lds + (1 + (t >> 2)) * kTile, ks, 16 * (t & 3), lane);
+#pragma unroll
+                for (int a = 0; a < 2; ++a) acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[a], fb, acc[a][b], 0, 0, 0);
+            }
+        }
+    }
+    // C[row = output channel][col = (tap, input channel)]: col = lane & 15, row = 4 (lane >> 4) + r
+    float* o = out + int64_t(blockIdx.y) * int64_t(g.Co) * kTaps * g.Ci;
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 9; ++b) {
+            const int t = nt0 + b, tap = t >> 2;
+            const int ci = ci0 + 16 * (t & 3) + (lane & 15);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int co = co0 + 16 * (mt0 + a) + 4 * (lane >> 4) + r;
+                o[(int64_t(co) * kTaps + tap) * g.Ci + ci] = acc[a][b][r];
+            }
+        }
+}
+
+#ifdef DAUC_TUNING
+// the transposing LDS read's lane map, for the tests: LDS holds element value = row * 64 + col of a
+// [16][64] tile (row stride kRow); lane l reads frag(tile, 0, c0 = 16 * (l >> 6 ... 0), l)
+__global__ void probe_tr16_kernel(short* out) {
+    __shared__ short t[32 * kRow];
+    for (int i = threadIdx.x; i < 32 * kRow; i += 64) t[i] = static_cast<short>((i / kRow) * 64 + i % kRow);
+    __syncthreads();
+    const bf16x8 f = frag(t, 0, 16, threadIdx.x);
+    const short* s = reinterpret_cast<const short*>(&f);
+    for (int j = 0; j < 8; ++j) out[threadIdx.x * 8 + j] = s[j];
+}
+#endif
+
+}  // namespace
+}  // namespace dauc
+
+using namespace dauc;
+
+extern "C" {
+
+size_t dauc_conv3x3_wgrad_workspace_size(int64_t N, int Ho, int Wo, int Ci, int Co) {
+    if (N < 1 || Ho < 1 || Wo < 1 || Ci < kBC || Co < kBM || Ci % kBC || Co % kBM) return 0;
+    const int64_t tiles = int64_t(Co / kBM) * (Ci / kBC);
+    const int64_t chunks = (N * Ho * Wo + kKT - 1) / kKT;
+    int64_t S = (256 + tiles - 1) / tiles;
+    if (S > chunks) S = chunks;
+    if (S <= 1) return 0;
+    return size_t(S) * size_t(Co) * kTaps * size_t(Ci) * sizeof(float);
+}
+
+int dauc_conv3x3_wgrad(const void* x, const void* dy, int dtype, int64_t N, int H, int W, int Ci, int Ho, int Wo,
+                       int Co, int stride, float* dw, void* workspace, size_t workspace_bytes, dauc_stream_t stream) {
+    if (x == nullptr || dy == nullptr || dw == nullptr || dtype != DAUC_DTYPE_BF16) return DAUC_EINVAL;
+    if (N < 1 || H < 1 || W < 1 || Ho < 1 || Wo < 1 || Ci < kBC || Co < kBM || Ci % kBC || Co % kBM) return DAUC_EINVAL;
+    if (stride != 1 && stride != 2) return DAUC_EINVAL;
+    if (Ho != (H + 2 - 3) / stride + 1 || Wo != (W + 2 - 3) / stride + 1) return DAUC_EINVAL;  // pad 1
+    if ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(dy) | reinterpret_cast<uintptr_t>(dw)) & 15u)
+        return DAUC_EINVAL;
+    if (N * int64_t(H) * W > (int64_t(1) << 31) || N * int64_t(Ho) * Wo > (int64_t(1) << 31)) return DAUC_EINVAL;
+    WgradGeom g;
+    g.N = static_cast<int>(N);
+    g.H = H;
+    g.W = W;
+    g.Ci = Ci;
+    g.Ho = Ho;
+    g.Wo = Wo;
+    g.Co = Co;
+    g.stride = stride;
+    g.P = N * Ho * Wo;
+    g.chunks = (g.P + kKT - 1) / kKT;
+    g.ctiles = Ci / kBC;
+    const int64_t tiles = int64_t(Co / kBM) * g.ctiles;
+    const size_t need = dauc_conv3x3_wgrad_workspace_size(N, Ho, Wo, Ci, Co);
+    const int64_t S = need ? int64_t(need / (size_t(Co) * kTaps * size_t(Ci) * sizeof(float))) : 1;
+    if (need && (workspace == nullptr || workspace_bytes < need || (reinterpret_cast<uintptr_t>(workspace) & 15u)))
+        return DAUC_EINVAL;
+    g.cps = (g.chunks + S - 1) / S;
+    const int64_t splits = (g.chunks + g.cps - 1) / g.cps;  // every split owns at least one chunk
+    if (tiles > 0x7fffffffLL || splits > 65535) return DAUC_EINVAL;
+    hipStream_t st = as_hip(stream);
+    float* target = splits > 1 ? static_cast<float*>(workspace) : dw;
+    hipLaunchKernelGGL(wgrad3x3_kernel, dim3(static_cast<unsigned>(tiles), static_cast<unsigned>(splits)),
+                       dim3(kWgThreads), 0, st, static_cast<const __hip_bfloat16*>(x),
+                       static_cast<const __hip_bfloat16*>(dy), g, target);
+    int rc = launch_status();
+    if (rc != DAUC_OK || splits == 1) return rc;
+    return dauc_slab_sum(target, splits, int64_t(Co) * kTaps * Ci, dw, stream);
+}
+
+#ifdef DAUC_TUNING
+int dauc_probe_tr16(short* out, dauc_stream_t stream) {
+    if (out == nullptr) return DAUC_EINVAL;
+    hipLaunchKernelGGL(probe_tr16_kernel, dim3(1), dim3(64), 0, as_hip(stream), out);
+    return launch_status();
+}
+#endif
+
+}  // extern "C"

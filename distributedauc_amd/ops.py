@@ -598,6 +598,53 @@ def sort_keys(scores: torch.Tensor) -> torch.Tensor:
     return out
 
 
+def conv3x3_wgrad(x: torch.Tensor, dy: torch.Tensor, stride: int, out: torch.Tensor | None = None) -> torch.Tensor:
+    """The fp32 weight gradient of a 3x3 / pad 1 / stride 1|2 convolution from its channels-last
+    bf16 input x [N, Ci, H, W] and output gradient dy [N, Co, Ho, Wo] (dauc_conv3x3_wgrad):
+    a [Co, Ci, 3, 3] fp32 tensor in channels-last memory order (the backbone's parameter layout)."""
+    _require(x, "x", torch.bfloat16)
+    _require(dy, "dy", torch.bfloat16, x.device)
+    if x.dim() != 4 or dy.dim() != 4 or x.shape[0] != dy.shape[0]:
+        raise ValueError(f"x and dy must be [N, C, H, W] of one batch, got {tuple(x.shape)} and {tuple(dy.shape)}")
+    for t, name in ((x, "x"), (dy, "dy")):
+        if not t.is_contiguous(memory_format=torch.channels_last):
+            raise ValueError(f"{name} must be channels-last contiguous")
+    N, Ci, H, W = x.shape
+    Co, Ho, Wo = dy.shape[1], dy.shape[2], dy.shape[3]
+    dev = x.device
+    if out is None:
+        out = torch.empty((Co, Ci, 3, 3), dtype=torch.float32, device=dev, memory_format=torch.channels_last)
+    elif (out.dtype != torch.float32 or tuple(out.shape) != (Co, Ci, 3, 3)
+          or not out.is_contiguous(memory_format=torch.channels_last)):
+        raise ValueError("out must be a channels-last fp32 [Co, Ci, 3, 3] tensor")
+    L = _lib.load()
+    nbytes = L.dauc_conv3x3_wgrad_workspace_size(N, Ho, Wo, Ci, Co)
+    ws = workspaces.get(dev, "wgrad3x3", nbytes) if nbytes else None
+    check(L.dauc_conv3x3_wgrad(_ptr(x), _ptr(dy), _lib.DTYPE_BF16, N, H, W, Ci, Ho, Wo, Co, int(stride), _ptr(out),
+                               _ptr(ws), 0 if ws is None else ws.numel(), _stream(dev)), "dauc_conv3x3_wgrad")
+    return out
+
+
+def conv3x3_wgrad_supported(x: torch.Tensor, dy: torch.Tensor, stride, padding, dilation, groups) -> bool:
+    """The shapes dauc_conv3x3_wgrad takes (the ResNet bottlenecks' and basic blocks' 3x3 convolutions)."""
+    s = tuple(stride) if isinstance(stride, (tuple, list)) else (stride, stride)
+    p = tuple(padding) if isinstance(padding, (tuple, list)) else (padding, padding)
+    d = tuple(dilation) if isinstance(dilation, (tuple, list)) else (dilation, dilation)
+    return (x.dtype == torch.bfloat16 and dy.dtype == torch.bfloat16 and x.is_cuda and groups == 1
+            and s[0] == s[1] and s[0] in (1, 2) and p == (1, 1) and d == (1, 1)
+            and x.shape[1] % 64 == 0 and dy.shape[1] % 64 == 0
+            and x.is_contiguous(memory_format=torch.channels_last)
+            and dy.is_contiguous(memory_format=torch.channels_last)
+            and x.shape[0] * x.shape[2] * x.shape[3] < 2 ** 31)
+
+
+def probe_tr16() -> torch.Tensor:
+    """The wgrad kernel's transposing-read lane map (tuning build): [64 lanes, 8] int16."""
+    out = torch.zeros((64, 8), dtype=torch.int16, device="cuda")
+    check(_lib.tuning().dauc_probe_tr16(_ptr(out), _stream(out.device)), "dauc_probe_tr16")
+    return out
+
+
 def set_direct_fault(mode: int) -> None:
     """Fault injection into the direct count-index build of the tuning build (dauc_set_direct_fault,
     include/dauc_tuning.h): 0 none, 1 / 2 / 3 a corrupted cell index or counter. Tests only."""
@@ -616,7 +663,7 @@ __all__ = [
     "pd_update_dense", "coda_finalize", "scale_div", "split_scores", "pair_count", "auc_counts_sorted",
     "surrogate_logits_fwdbwd", "class_sums_logits", "surrogate_status",
     "sort_keys", "auc_counts_sorted_labeled", "compact_positives", "mode_code", "workspaces", "set_search_mode",
-    "set_direct_fault",
+    "set_direct_fault", "conv3x3_wgrad", "conv3x3_wgrad_supported",
     "auc_eval_enqueue",
     "auc_slot_bytes",
     "auc_eval_compact_part",

@@ -409,6 +409,23 @@ int dauc_maxpool2d_backward(const void* dy, const int8_t* argmax, int dtype, int
  */
 int dauc_slab_sum(const float* part, int64_t S, int64_t n, float* out, dauc_stream_t stream);
 
+/* ---------------------------------- backbone: 3x3 convolution weight gradient */
+
+/*
+ * dw[co][kh][kw][ci] (fp32, the channels-last [Co, Ci, 3, 3] weight's memory order) <-
+ *   sum over output pixels (n, ho, wo) of dy[n][ho][wo][co] * x[n][ho*stride - 1 + kh][wo*stride - 1 + kw][ci]
+ * for a 3x3 convolution with padding 1 and stride 1 or 2: x [N, H, W, Ci] and dy [N, Ho, Wo, Co]
+ * channels-last bf16 (dtype DAUC_DTYPE_BF16 only), Ci and Co multiples of 64, 16-byte aligned
+ * pointers, N*H*W and N*Ho*Wo < 2^31. A split-K MFMA implicit GEMM with fp32 accumulation; the
+ * splits' fp32 partials go to `workspace` (dauc_conv3x3_wgrad_workspace_size bytes; 0 = none
+ * needed) and are summed in split order (dauc_slab_sum): bitwise reproducible. Replaces MIOpen's
+ * backward-weights call of the ResNet 3x3 convolutions under bf16 autocast (resnet.py:72-108,
+ * main.py:326) and autograd's bf16 -> fp32 cast of its result.
+ */
+size_t dauc_conv3x3_wgrad_workspace_size(int64_t N, int Ho, int Wo, int Ci, int Co);
+int dauc_conv3x3_wgrad(const void* x, const void* dy, int dtype, int64_t N, int H, int W, int Ci, int Ho, int Wo,
+                       int Co, int stride, float* dw, void* workspace, size_t workspace_bytes, dauc_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -71,6 +71,11 @@ int dauc_set_search_mode(int mode);
  */
 int dauc_set_direct_fault(int mode);
 
+/* The transposing LDS read of the 3x3 weight gradient (csrc/conv_wgrad.hip), for its lane-map test:
+ * out[64 lanes][8] <- the 16x16x32 operand fragment (k-step 0, channel block 16) of a [32][64]
+ * tile whose element (row, col) holds row * 64 + col. */
+int dauc_probe_tr16(short* out, dauc_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -86,7 +86,7 @@ def test_shipped_conv1x1_plans_load():
         assert len(C.plans) >= 30
         key = (200704, 512, 128, __import__("torch").bfloat16, "dgrad_acc")  # ResNet-50 layer1 conv1 + skip
         assert key in C.plans
-        assert all(v in ("gemm", "conv") or v.startswith("gemm") for v in C.plans.values())
+        assert all(v in ("gemm", "conv", "fconv") or v.startswith("gemm") for v in C.plans.values())
     finally:
         C.plans.clear()
         C.plans.update(saved)

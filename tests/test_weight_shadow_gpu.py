@@ -35,7 +35,7 @@ def _run(dev, arch, shadow, size, dgrad_fwd=False, autocast=True):
                 weight_shadow=shadow)
     assert (net._wshadow is not None) == shadow
     if shadow and not dgrad_fwd:
-        net.set_weight_shadow(True, dgrad_fwd=False)  # torch's backward-data: bit-identical
+        net.set_weight_shadow(True, dgrad_fwd=False, wgrad_hip=False)  # torch's backward: bit-identical
     g = torch.Generator(device=dev).manual_seed(11)
     x = torch.randn((8, 3, size, size), device=dev, generator=g).contiguous(memory_format=torch.channels_last)
     y = torch.tensor([9, 0, 7, 1, 5, 3, 8, 2], device=dev)
