@@ -27,6 +27,8 @@
 
 #include <hip/hip_bf16.h>
 
+#include <cstdlib>
+
 #include "dauc_internal.h"
 
 namespace dauc {
@@ -186,6 +188,175 @@ __global__ __launch_bounds__(kWgThreads) void wgrad3x3_kernel(const __hip_bfloat
         }
 }
 
+// ---- the window form (every ResNet-50 3x3 shape: Wo <= 64) ----------------------------------
+// The 9 taps' B tiles above are 9 gathers of mostly the same x pixels: 80 KB of L2 traffic per
+// 64-pixel chunk, which bounds that kernel (0.21 of the MFMA peak at 110 us a launch). Here a chunk
+// is R whole output rows (R = 64 / Wo, KP = R * Wo <= 64 pixels) and the workgroup stages, per
+// output row, the 3 input rows its taps read, W + 2 positions wide with the zero halo: R * 3 *
+// (W + 2) positions of 64 channels (ResNet-50: 174 - 432 positions, 22 - 54 KB instead of 72 KB),
+// and every tap's B fragment reads the window in place -- the transposing read takes a per-lane
+// row address, so lane (q, p) of a group points at pixel k's window position + kh (W + 2) + kw.
+// The pixel -> position map is the same for every chunk, so each lane computes its 4 positions
+// once. Two LDS buffers: the next chunk is staged while this one is multiplied, one barrier per
+// chunk. Pixels k >= KP (a chunk's padding) have zero dy rows (A), so their B values (pixel 0's)
+// add nothing.
+constexpr int kMaxWinVec = 8;  // window vectors per thread: <= 512 positions of 8 vectors
+
+struct WinGeom {
+    int N, H, W, Ci, Ho, Wo, Co, stride;
+    int R, Wd, npos, KP, nvec;
+    int64_t GR;      // output rows N * Ho
+    int64_t chunks;  // ceil(GR / R)
+    int64_t cps;
+    int ctiles;
+};
+
+inline size_t win_lds_bytes(const struct WinGeom& g);
+
+struct WinStaging {
+    uint4 a, w[kMaxWinVec];
+    unsigned ok;  // bit j: window vector j in the image; bit kMaxWinVec: the dy row exists
+};
+
+template <int NV>
+__device__ __forceinline__ void load_win(WinStaging& s, const __hip_bfloat16* __restrict__ x,
+                                         const __hip_bfloat16* __restrict__ dy, const WinGeom& g, int64_t chunk,
+                                         const int (&wpos)[kMaxWinVec], int pr, int v, int co0, int ci0) {
+    const int64_t gr0 = chunk * g.R;
+    // dy: pixel k = pr of the chunk
+    {
+        const int rr = pr / g.Wo, wo = pr - rr * g.Wo;
+        const int64_t gr = gr0 + rr;
+        const bool ok = (pr < g.KP) & (gr < g.GR);
+        const int64_t q = ok ? gr * g.Wo + wo : 0;
+        s.a = *reinterpret_cast<const uint4*>(dy + q * g.Co + co0 + 8 * v);
+        s.ok = ok ? (1u << kMaxWinVec) : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+        const int pk = wpos[j];  // rr | kh << 8 | w' << 16, bit 31: a position of the window
+        const int rr = pk & 0xff, kh = (pk >> 8) & 0xff, wc = (pk >> 16) & 0x7fff;
+        const int64_t gr = gr0 + rr;
+        const int grc = static_cast<int>(gr < g.GR ? gr : g.GR - 1);
+        const int n = grc / g.Ho, ho = grc - n * g.Ho;
+        const int ih = ho * g.stride - 1 + kh, iw = wc - 1;
+        const bool ok = (pk < 0) & (gr < g.GR) & (ih >= 0) & (ih < g.H) & (iw >= 0) & (iw < g.W);
+        const int ihc = min(max(ih, 0), g.H - 1), iwc = min(max(iw, 0), g.W - 1);
+        const int vv = (threadIdx.x + kWgThreads * j) & 7;
+        s.w[j] = *reinterpret_cast<const uint4*>(x + ((int64_t(n) * g.H + ihc) * g.W + iwc) * g.Ci + ci0 + 8 * vv);
+        s.ok |= ok ? (1u << j) : 0u;
+    }
+}
+
+template <int NV>
+__device__ __forceinline__ void stage_win(const WinStaging& s, short* buf, const WinGeom& g, int pr, int v) {
+    *reinterpret_cast<uint4*>(buf + pr * kRow + 8 * v) = masked(s.a, s.ok, kMaxWinVec);
+    short* win = buf + kKT * kRow;
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+        const int idx = threadIdx.x + kWgThreads * j;
+        const int pos = idx >> 3;
+        if (pos < g.npos) *reinterpret_cast<uint4*>(win + pos * kRow + 8 * (idx & 7)) = masked(s.w[j], s.ok, j);
+    }
+}
+
+inline size_t win_lds_bytes(const WinGeom& g) { return size_t(2) * (kKT + g.npos) * kRow * sizeof(short); }
+
+__device__ __forceinline__ v4s tr_read_at(const short* base, int row, int c0, int lane) {
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(base + row * kRow + c0 + 4 * (lane & 3)));
+}
+
+template <int NV>
+__global__ __launch_bounds__(kWgThreads) void wgrad3x3_win_kernel(const __hip_bfloat16* __restrict__ x,
+                                                                  const __hip_bfloat16* __restrict__ dy,
+                                                                  WinGeom g, float* __restrict__ out) {
+    extern __shared__ short lds_dyn[];
+    const int buf_elems = (kKT + g.npos) * kRow;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int co0 = (blockIdx.x / g.ctiles) * kBM, ci0 = (blockIdx.x % g.ctiles) * kBC;
+    const int64_t c_begin = int64_t(blockIdx.y) * g.cps;
+    const int64_t c_end = c_begin + g.cps < g.chunks ? c_begin + g.cps : g.chunks;
+    const int pr = tid >> 3, v = tid & 7;
+
+    // this thread's window vectors (the same positions in every chunk)
+    int wpos[kMaxWinVec];
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+        const int pos = (tid + kWgThreads * j) >> 3;
+        const int per_row = 3 * g.Wd;
+        const int rr = pos / per_row, rem = pos - rr * per_row;
+        const int kh = rem / g.Wd, wc = rem - kh * g.Wd;
+        wpos[j] = (pos < g.npos ? int(0x80000000u) : 0) | rr | (kh << 8) | (wc << 16);
+    }
+    // this lane's B-fragment rows: pixel k = 32 ks + 8 (lane >> 4) + 4 h + ((lane & 15) >> 2) ->
+    // its window position for tap (0, 0)
+    int bpos[2][2];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int k = 32 * ks + 8 * (lane >> 4) + 4 * h + ((lane & 15) >> 2);
+            const int rr = k / g.Wo, cc = k - rr * g.Wo;
+            bpos[ks][h] = k < g.KP ? rr * 3 * g.Wd + cc * g.stride : 0;
+        }
+
+    f32x4v acc[2][9];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 9; ++b) acc[a][b] = f32x4v{0.f, 0.f, 0.f, 0.f};
+    const int mt0 = 2 * (wave & 1), nt0 = 9 * (wave >> 1);
+
+    WinStaging st;
+    load_win<NV>(st, x, dy, g, c_begin, wpos, pr, v, co0, ci0);
+    stage_win<NV>(st, lds_dyn, g, pr, v);
+    load_win<NV>(st, x, dy, g, c_begin + 1 < c_end ? c_begin + 1 : c_begin, wpos, pr, v, co0, ci0);
+    __syncthreads();
+    for (int64_t c = c_begin; c < c_end; ++c) {
+        const int b = static_cast<int>(c - c_begin) & 1;
+        short* cur = lds_dyn + b * buf_elems;
+        // chunk c + 1 into the other buffer (read last by chunk c - 1, before the barrier below
+        // ended that iteration); on the last chunk this stages a clamped copy nobody reads
+        stage_win<NV>(st, lds_dyn + (b ^ 1) * buf_elems, g, pr, v);
+        load_win<NV>(st, x, dy, g, c + 2 < c_end ? c + 2 : c_end - 1, wpos, pr, v, co0, ci0);
+        __builtin_amdgcn_sched_barrier(0);  // the loads ahead of the MFMAs
+        const short* win = cur + kKT * kRow;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            bf16x8 fa[2];
+#pragma unroll
+            for (int a = 0; a < 2; ++a) fa[a] = frag(cur, ks, 16 * (mt0 + a), lane);
+#pragma unroll
+            for (int bb = 0; bb < 9; ++bb) {
+                const int t = nt0 + bb, tap = t >> 2;
+                const int toff = (tap / 3) * g.Wd + tap % 3;
+                const int c0 = 16 * (t & 3);
+                const v4s lo = tr_read_at(win, bpos[ks][0] + toff, c0, lane);
+                const v4s hi = tr_read_at(win, bpos[ks][1] + toff, c0, lane);
+                const v4s f2[2] = {lo, hi};
+                const bf16x8 fb = *reinterpret_cast<const bf16x8*>(f2);
+#pragma unroll
+                for (int a = 0; a < 2; ++a)
+                    acc[a][bb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[a], fb, acc[a][bb], 0, 0, 0);
+            }
+        }
+        __syncthreads();
+    }
+    float* o = out + int64_t(blockIdx.y) * int64_t(g.Co) * kTaps * g.Ci;
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int bb = 0; bb < 9; ++bb) {
+            const int t = nt0 + bb, tap = t >> 2;
+            const int ci = ci0 + 16 * (t & 3) + (lane & 15);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int co = co0 + 16 * (mt0 + a) + 4 * (lane >> 4) + r;
+                o[(int64_t(co) * kTaps + tap) * g.Ci + ci] = acc[a][bb][r];
+            }
+        }
+}
+
 #ifdef DAUC_TUNING
 // the transposing LDS read's lane map, for the tests: LDS holds element value = row * 64 + col of a
 // [16][64] tile (row stride kRow); lane l reads frag(tile, 0, c0 = 16 * (l >> 6 ... 0), l)
@@ -206,12 +377,42 @@ using namespace dauc;
 
 extern "C" {
 
+namespace {
+// the window form's geometry (returns false when the shape needs the gather form)
+bool win_geom(int64_t N, int H, int W, int Ci, int Ho, int Wo, int Co, int stride, WinGeom& g) {
+    if (Wo > kKT || std::getenv("DAUC_WGRAD_GATHER") != nullptr) return false;
+    g.N = static_cast<int>(N);
+    g.H = H;
+    g.W = W;
+    g.Ci = Ci;
+    g.Ho = Ho;
+    g.Wo = Wo;
+    g.Co = Co;
+    g.stride = stride;
+    g.R = kKT / Wo;
+    g.KP = g.R * Wo;
+    g.Wd = W + 2;
+    g.npos = g.R * 3 * g.Wd;
+    g.nvec = (g.npos * 8 + kWgThreads - 1) / kWgThreads;
+    if (g.nvec > kMaxWinVec || win_lds_bytes(g) > 160 * 1024) return false;
+    g.GR = N * Ho;
+    g.chunks = (g.GR + g.R - 1) / g.R;
+    g.ctiles = Ci / kBC;
+    return true;
+}
+
+int64_t split_count(int64_t tiles, int64_t chunks) {
+    int64_t S = (256 + tiles - 1) / tiles;
+    return S > chunks ? chunks : S;
+}
+}  // namespace
+
 size_t dauc_conv3x3_wgrad_workspace_size(int64_t N, int Ho, int Wo, int Ci, int Co) {
     if (N < 1 || Ho < 1 || Wo < 1 || Ci < kBC || Co < kBM || Ci % kBC || Co % kBM) return 0;
     const int64_t tiles = int64_t(Co / kBM) * (Ci / kBC);
+    // the larger of the two forms' chunk counts bounds the splits of either
     const int64_t chunks = (N * Ho * Wo + kKT - 1) / kKT;
-    int64_t S = (256 + tiles - 1) / tiles;
-    if (S > chunks) S = chunks;
+    const int64_t S = split_count(tiles, chunks > N * Ho ? chunks : N * Ho);
     if (S <= 1) return 0;
     return size_t(S) * size_t(Co) * kTaps * size_t(Ci) * sizeof(float);
 }
@@ -225,31 +426,62 @@ int dauc_conv3x3_wgrad(const void* x, const void* dy, int dtype, int64_t N, int 
     if ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(dy) | reinterpret_cast<uintptr_t>(dw)) & 15u)
         return DAUC_EINVAL;
     if (N * int64_t(H) * W > (int64_t(1) << 31) || N * int64_t(Ho) * Wo > (int64_t(1) << 31)) return DAUC_EINVAL;
-    WgradGeom g;
-    g.N = static_cast<int>(N);
-    g.H = H;
-    g.W = W;
-    g.Ci = Ci;
-    g.Ho = Ho;
-    g.Wo = Wo;
-    g.Co = Co;
-    g.stride = stride;
-    g.P = N * Ho * Wo;
-    g.chunks = (g.P + kKT - 1) / kKT;
-    g.ctiles = Ci / kBC;
-    const int64_t tiles = int64_t(Co / kBM) * g.ctiles;
+    const int64_t tiles = int64_t(Co / kBM) * (Ci / kBC);
     const size_t need = dauc_conv3x3_wgrad_workspace_size(N, Ho, Wo, Ci, Co);
-    const int64_t S = need ? int64_t(need / (size_t(Co) * kTaps * size_t(Ci) * sizeof(float))) : 1;
+    const int64_t Smax = need ? int64_t(need / (size_t(Co) * kTaps * size_t(Ci) * sizeof(float))) : 1;
     if (need && (workspace == nullptr || workspace_bytes < need || (reinterpret_cast<uintptr_t>(workspace) & 15u)))
         return DAUC_EINVAL;
-    g.cps = (g.chunks + S - 1) / S;
-    const int64_t splits = (g.chunks + g.cps - 1) / g.cps;  // every split owns at least one chunk
-    if (tiles > 0x7fffffffLL || splits > 65535) return DAUC_EINVAL;
+    if (tiles > 0x7fffffffLL) return DAUC_EINVAL;
     hipStream_t st = as_hip(stream);
-    float* target = splits > 1 ? static_cast<float*>(workspace) : dw;
-    hipLaunchKernelGGL(wgrad3x3_kernel, dim3(static_cast<unsigned>(tiles), static_cast<unsigned>(splits)),
-                       dim3(kWgThreads), 0, st, static_cast<const __hip_bfloat16*>(x),
-                       static_cast<const __hip_bfloat16*>(dy), g, target);
+    WinGeom wg;
+    int64_t splits;
+    float* target;
+    if (win_geom(N, H, W, Ci, Ho, Wo, Co, stride, wg)) {
+        const int64_t S = split_count(tiles, wg.chunks) < Smax ? split_count(tiles, wg.chunks) : Smax;
+        wg.cps = (wg.chunks + S - 1) / S;
+        splits = (wg.chunks + wg.cps - 1) / wg.cps;  // every split owns at least one chunk
+        if (splits > 65535) return DAUC_EINVAL;
+        target = splits > 1 ? static_cast<float*>(workspace) : dw;
+        const dim3 grid(static_cast<unsigned>(tiles), static_cast<unsigned>(splits));
+        const size_t lds = win_lds_bytes(wg);
+        const __hip_bfloat16* xb = static_cast<const __hip_bfloat16*>(x);
+        const __hip_bfloat16* db = static_cast<const __hip_bfloat16*>(dy);
+        switch (wg.nvec) {
+#define DAUC_WIN_CASE(NV) \
+    case NV: hipLaunchKernelGGL(wgrad3x3_win_kernel<NV>, grid, dim3(kWgThreads), lds, st, xb, db, wg, target); break;
+            DAUC_WIN_CASE(1)
+            DAUC_WIN_CASE(2)
+            DAUC_WIN_CASE(3)
+            DAUC_WIN_CASE(4)
+            DAUC_WIN_CASE(5)
+            DAUC_WIN_CASE(6)
+            DAUC_WIN_CASE(7)
+            DAUC_WIN_CASE(8)
+#undef DAUC_WIN_CASE
+            default: return DAUC_EINVAL;
+        }
+    } else {
+        WgradGeom g;
+        g.N = static_cast<int>(N);
+        g.H = H;
+        g.W = W;
+        g.Ci = Ci;
+        g.Ho = Ho;
+        g.Wo = Wo;
+        g.Co = Co;
+        g.stride = stride;
+        g.P = N * Ho * Wo;
+        g.chunks = (g.P + kKT - 1) / kKT;
+        g.ctiles = Ci / kBC;
+        const int64_t S = split_count(tiles, g.chunks) < Smax ? split_count(tiles, g.chunks) : Smax;
+        g.cps = (g.chunks + S - 1) / S;
+        splits = (g.chunks + g.cps - 1) / g.cps;
+        if (splits > 65535) return DAUC_EINVAL;
+        target = splits > 1 ? static_cast<float*>(workspace) : dw;
+        hipLaunchKernelGGL(wgrad3x3_kernel, dim3(static_cast<unsigned>(tiles), static_cast<unsigned>(splits)),
+                           dim3(kWgThreads), 0, st, static_cast<const __hip_bfloat16*>(x),
+                           static_cast<const __hip_bfloat16*>(dy), g, target);
+    }
     int rc = launch_status();
     if (rc != DAUC_OK || splits == 1) return rc;
     return dauc_slab_sum(target, splits, int64_t(Co) * kTaps * Ci, dw, stream);

@@ -38,11 +38,19 @@ def _ref_wgrad(x, dy, stride):
                                                [False, True, False])[1]
 
 
+@pytest.mark.parametrize("form", ["window", "gather"])
 @pytest.mark.parametrize("N,Ci,Co,H,W,stride", [
     (2, 64, 64, 9, 11, 1), (3, 128, 64, 14, 14, 2), (1, 64, 192, 7, 5, 1), (4, 64, 128, 15, 13, 2),
-    (2, 256, 256, 14, 14, 1), (5, 512, 512, 7, 7, 1), (1, 64, 64, 1, 1, 1), (2, 64, 64, 2, 3, 2)])
-def test_conv3x3_wgrad_matches_fp64(dev, N, Ci, Co, H, W, stride):
+    (2, 256, 256, 14, 14, 1), (5, 512, 512, 7, 7, 1), (1, 64, 64, 1, 1, 1), (2, 64, 64, 2, 3, 2),
+    (3, 64, 64, 70, 9, 1), (2, 64, 128, 131, 5, 2), (1, 64, 64, 3, 70, 1), (2, 64, 64, 5, 131, 2)])
+def test_conv3x3_wgrad_matches_fp64(dev, monkeypatch, form, N, Ci, Co, H, W, stride):
+    """Both forms of the kernel: the window form (whole output rows per chunk, the taps read one
+    staged input window; every shape with Wo <= 64) and the gather form (64-pixel chunks, one
+    gathered tile per tap; wider images, or DAUC_WGRAD_GATHER=1)."""
     from distributedauc_amd import ops
+
+    if form == "gather":
+        monkeypatch.setenv("DAUC_WGRAD_GATHER", "1")
 
     g = torch.Generator(device=dev).manual_seed(N * 1000 + Ci + Co + H)
     x = torch.randn((N, Ci, H, W), device=dev, generator=g).to(torch.bfloat16)
@@ -61,7 +69,7 @@ def test_conv3x3_wgrad_matches_fp64(dev, N, Ci, Co, H, W, stride):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("C,H,stride", [(64, 56, 1), (128, 56, 2), (512, 7, 1)])
+@pytest.mark.parametrize("C,H,stride", [(64, 56, 1), (128, 56, 2), (256, 28, 2), (512, 14, 2), (512, 7, 1)])
 def test_conv3x3_wgrad_resnet50_b256(dev, C, H, stride):
     """The bench's shapes (ResNet-50 b256 224^2: layer1 conv2, layer2.0 conv2, layer4 conv2) against
     torch's fp32 convolution backward on the GPU (fp32 operands from the same bf16 values)."""
