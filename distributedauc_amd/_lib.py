@@ -99,6 +99,7 @@ TUNING_SIGNATURES = {
     "dauc_set_search_mode": (_int, [_int]),
     "dauc_set_direct_fault": (_int, [_int]),
     "dauc_probe_tr16": (_int, [_vp, _vp]),
+    "dauc_set_wgrad_form": (_int, [_int]),
 }
 TUNING_LIB_PATH = Path(os.environ.get("DAUC_TUNING_LIB", PKG_DIR.parent / "tuning" / "libdauc_tuning.so"))
 

@@ -27,8 +27,6 @@
 
 #include <hip/hip_bf16.h>
 
-#include <cstdlib>
-
 #include "dauc_internal.h"
 
 namespace dauc {
@@ -198,9 +196,10 @@ __global__ __launch_bounds__(kWgThreads) void wgrad3x3_kernel(const __hip_bfloat
 // row address, so lane (q, p) of a group points at pixel k's window position + kh (W + 2) + kw.
 // The pixel -> position map is the same for every chunk, so each lane computes its 4 positions
 // once. Two LDS buffers: the next chunk is staged while this one is multiplied, one barrier per
-// chunk. Pixels k >= KP (a chunk's padding) have zero dy rows (A), so their B values (pixel 0's)
+// chunk; two staging register sets: a chunk's loads are issued two chunks ahead. Pixels k >= KP (a chunk's padding) have zero dy rows (A), so their B values (pixel 0's)
 // add nothing.
 constexpr int kMaxWinVec = 8;  // window vectors per thread: <= 512 positions of 8 vectors
+constexpr int kWinVecFast = 6;  // the most the two staging register sets hold without spilling much
 
 struct WinGeom {
     int N, H, W, Ci, Ho, Wo, Co, stride;
@@ -213,13 +212,14 @@ struct WinGeom {
 
 inline size_t win_lds_bytes(const struct WinGeom& g);
 
+template <int NV>
 struct WinStaging {
-    uint4 a, w[kMaxWinVec];
+    uint4 a, w[NV];
     unsigned ok;  // bit j: window vector j in the image; bit kMaxWinVec: the dy row exists
 };
 
 template <int NV>
-__device__ __forceinline__ void load_win(WinStaging& s, const __hip_bfloat16* __restrict__ x,
+__device__ __forceinline__ void load_win(WinStaging<NV>& s, const __hip_bfloat16* __restrict__ x,
                                          const __hip_bfloat16* __restrict__ dy, const WinGeom& g, int64_t chunk,
                                          const int (&wpos)[kMaxWinVec], int pr, int v, int co0, int ci0) {
     const int64_t gr0 = chunk * g.R;
@@ -249,7 +249,7 @@ __device__ __forceinline__ void load_win(WinStaging& s, const __hip_bfloat16* __
 }
 
 template <int NV>
-__device__ __forceinline__ void stage_win(const WinStaging& s, short* buf, const WinGeom& g, int pr, int v) {
+__device__ __forceinline__ void stage_win(const WinStaging<NV>& s, short* buf, const WinGeom& g, int pr, int v) {
     *reinterpret_cast<uint4*>(buf + pr * kRow + 8 * v) = masked(s.a, s.ok, kMaxWinVec);
     short* win = buf + kKT * kRow;
 #pragma unroll
@@ -264,6 +264,30 @@ inline size_t win_lds_bytes(const WinGeom& g) { return size_t(2) * (kKT + g.npos
 
 __device__ __forceinline__ v4s tr_read_at(const short* base, int row, int c0, int lane) {
     return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(base + row * kRow + c0 + 4 * (lane & 3)));
+}
+
+// one wave's 36 MFMAs of a chunk staged in `cur` (A rows, then the window)
+__device__ __forceinline__ void win_multiply(f32x4v (&acc)[2][9], const short* cur, const WinGeom& g,
+                                             const int (&bpos)[2][2], int mt0, int nt0, int lane) {
+    const short* win = cur + kKT * kRow;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+        bf16x8 fa[2];
+#pragma unroll
+        for (int a = 0; a < 2; ++a) fa[a] = frag(cur, ks, 16 * (mt0 + a), lane);
+#pragma unroll
+        for (int bb = 0; bb < 9; ++bb) {
+            const int t = nt0 + bb, tap = t >> 2;
+            const int toff = (tap / 3) * g.Wd + tap % 3;
+            const v4s lo = tr_read_at(win, bpos[ks][0] + toff, 16 * (t & 3), lane);
+            const v4s hi = tr_read_at(win, bpos[ks][1] + toff, 16 * (t & 3), lane);
+            const v4s f2[2] = {lo, hi};
+            const bf16x8 fb = *reinterpret_cast<const bf16x8*>(f2);
+#pragma unroll
+            for (int a = 0; a < 2; ++a)
+                acc[a][bb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[a], fb, acc[a][bb], 0, 0, 0);
+        }
+    }
 }
 
 template <int NV>
@@ -307,40 +331,28 @@ __global__ __launch_bounds__(kWgThreads) void wgrad3x3_win_kernel(const __hip_bf
         for (int b = 0; b < 9; ++b) acc[a][b] = f32x4v{0.f, 0.f, 0.f, 0.f};
     const int mt0 = 2 * (wave & 1), nt0 = 9 * (wave >> 1);
 
-    WinStaging st;
-    load_win<NV>(st, x, dy, g, c_begin, wpos, pr, v, co0, ci0);
-    stage_win<NV>(st, lds_dyn, g, pr, v);
-    load_win<NV>(st, x, dy, g, c_begin + 1 < c_end ? c_begin + 1 : c_begin, wpos, pr, v, co0, ci0);
+    // Two register sets: a chunk's global loads are issued two chunks before it is staged, so
+    // their latency (mostly HBM: a window is read by one workgroup) has two chunks' MFMAs to hide
+    // behind instead of one. s0 / s1 alternate; every load is unconditional (clamped chunk).
+    short* buf0 = lds_dyn;
+    short* buf1 = lds_dyn + buf_elems;
+    WinStaging<NV> s0, s1;
+    load_win<NV>(s0, x, dy, g, c_begin, wpos, pr, v, co0, ci0);
+    stage_win<NV>(s0, buf0, g, pr, v);
+    load_win<NV>(s0, x, dy, g, min(c_begin + 1, c_end - 1), wpos, pr, v, co0, ci0);
+    load_win<NV>(s1, x, dy, g, min(c_begin + 2, c_end - 1), wpos, pr, v, co0, ci0);
     __syncthreads();
     for (int64_t c = c_begin; c < c_end; ++c) {
+        // chunk c on buffer (c - c_begin) & 1; s0 holds chunk c + 1, s1 chunk c + 2
         const int b = static_cast<int>(c - c_begin) & 1;
-        short* cur = lds_dyn + b * buf_elems;
-        // chunk c + 1 into the other buffer (read last by chunk c - 1, before the barrier below
-        // ended that iteration); on the last chunk this stages a clamped copy nobody reads
-        stage_win<NV>(st, lds_dyn + (b ^ 1) * buf_elems, g, pr, v);
-        load_win<NV>(st, x, dy, g, c + 2 < c_end ? c + 2 : c_end - 1, wpos, pr, v, co0, ci0);
+        stage_win<NV>(s0, b ? buf0 : buf1, g, pr, v);
+        load_win<NV>(s0, x, dy, g, min(c + 3, c_end - 1), wpos, pr, v, co0, ci0);
         __builtin_amdgcn_sched_barrier(0);  // the loads ahead of the MFMAs
-        const short* win = cur + kKT * kRow;
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-            bf16x8 fa[2];
-#pragma unroll
-            for (int a = 0; a < 2; ++a) fa[a] = frag(cur, ks, 16 * (mt0 + a), lane);
-#pragma unroll
-            for (int bb = 0; bb < 9; ++bb) {
-                const int t = nt0 + bb, tap = t >> 2;
-                const int toff = (tap / 3) * g.Wd + tap % 3;
-                const int c0 = 16 * (t & 3);
-                const v4s lo = tr_read_at(win, bpos[ks][0] + toff, c0, lane);
-                const v4s hi = tr_read_at(win, bpos[ks][1] + toff, c0, lane);
-                const v4s f2[2] = {lo, hi};
-                const bf16x8 fb = *reinterpret_cast<const bf16x8*>(f2);
-#pragma unroll
-                for (int a = 0; a < 2; ++a)
-                    acc[a][bb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[a], fb, acc[a][bb], 0, 0, 0);
-            }
-        }
+        win_multiply(acc, b ? buf1 : buf0, g, bpos, mt0, nt0, lane);
         __syncthreads();
+        const WinStaging<NV> t = s0;  // rotate the ring: s0 <- chunk c + 2, s1 <- chunk c + 3
+        s0 = s1;
+        s1 = t;
     }
     float* o = out + int64_t(blockIdx.y) * int64_t(g.Co) * kTaps * g.Ci;
 #pragma unroll
@@ -379,8 +391,15 @@ extern "C" {
 
 namespace {
 // the window form's geometry (returns false when the shape needs the gather form)
+#ifdef DAUC_TUNING
+int g_wgrad_form = 0;  // dauc_set_wgrad_form: 0 automatic, 1 the gather form (tests, A/B runs)
+#endif
+
 bool win_geom(int64_t N, int H, int W, int Ci, int Ho, int Wo, int Co, int stride, WinGeom& g) {
-    if (Wo > kKT || std::getenv("DAUC_WGRAD_GATHER") != nullptr) return false;
+    if (Wo > kKT) return false;
+#ifdef DAUC_TUNING
+    if (g_wgrad_form == 1) return false;
+#endif
     g.N = static_cast<int>(N);
     g.H = H;
     g.W = W;
@@ -389,11 +408,20 @@ bool win_geom(int64_t N, int H, int W, int Ci, int Ho, int Wo, int Co, int strid
     g.Wo = Wo;
     g.Co = Co;
     g.stride = stride;
-    g.R = kKT / Wo;
-    g.KP = g.R * Wo;
     g.Wd = W + 2;
-    g.npos = g.R * 3 * g.Wd;
-    g.nvec = (g.npos * 8 + kWgThreads - 1) / kWgThreads;
+    // as many whole output rows as fit 64 pixels, fewer when the window would need more than 6
+    // vectors per thread (two staging sets of more spill beside the accumulators)
+    for (g.R = kKT / Wo; g.R >= 1; --g.R) {
+        g.npos = g.R * 3 * g.Wd;
+        g.nvec = (g.npos * 8 + kWgThreads - 1) / kWgThreads;
+        if (g.nvec <= kWinVecFast) break;
+    }
+    if (g.R < 1) {
+        g.R = 1;
+        g.npos = 3 * g.Wd;
+        g.nvec = (g.npos * 8 + kWgThreads - 1) / kWgThreads;
+    }
+    g.KP = g.R * Wo;
     if (g.nvec > kMaxWinVec || win_lds_bytes(g) > 160 * 1024) return false;
     g.GR = N * Ho;
     g.chunks = (g.GR + g.R - 1) / g.R;
@@ -488,6 +516,12 @@ int dauc_conv3x3_wgrad(const void* x, const void* dy, int dtype, int64_t N, int 
 }
 
 #ifdef DAUC_TUNING
+int dauc_set_wgrad_form(int form) {
+    if (form != 0 && form != 1) return DAUC_EINVAL;
+    g_wgrad_form = form;
+    return DAUC_OK;
+}
+
 int dauc_probe_tr16(short* out, dauc_stream_t stream) {
     if (out == nullptr) return DAUC_EINVAL;
     hipLaunchKernelGGL(probe_tr16_kernel, dim3(1), dim3(64), 0, as_hip(stream), out);

@@ -638,6 +638,11 @@ def conv3x3_wgrad_supported(x: torch.Tensor, dy: torch.Tensor, stride, padding, 
             and x.shape[0] * x.shape[2] * x.shape[3] < 2 ** 31)
 
 
+def set_wgrad_form(form: int) -> None:
+    """The tuning build's 3x3 weight-gradient form (dauc_set_wgrad_form): 0 automatic, 1 gather."""
+    check(_lib.tuning().dauc_set_wgrad_form(int(form)), "dauc_set_wgrad_form")
+
+
 def probe_tr16() -> torch.Tensor:
     """The wgrad kernel's transposing-read lane map (tuning build): [64 lanes, 8] int16."""
     out = torch.zeros((64, 8), dtype=torch.int16, device="cuda")

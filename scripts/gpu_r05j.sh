@@ -1,6 +1,7 @@
 #!/bin/bash
 # round 5: the window form of the 3x3 weight-gradient kernel. Tests, then training-only runs
-# (DAUC_WGRAD_GATHER=1 forces the previous gather form) interleaved, then a kernel trace.
+# (DAUC_WGRAD_GATHER=1 forced the gather form in that build; later builds: the tuning build's
+# dauc_set_wgrad_form) interleaved, then a kernel trace.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 O=gpurun_out/r05j

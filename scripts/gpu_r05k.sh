@@ -1,12 +1,12 @@
 #!/bin/bash
-# round 5: the window wgrad kernel reading a k-step's 11 fragments before its MFMAs (and at most 6
-# window vectors per thread). Tests, then training-only runs against the previous build
+# round 5: the window wgrad kernel with two staging register sets (loads two chunks ahead) and at
+# most 6 window vectors per thread. Tests, then training-only runs against the previous build
 # (tuning/ab/libdauc_win1.so) interleaved, then a kernel trace.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-O=gpurun_out/r05k
+O=gpurun_out/r05l
 mkdir -p $O
-timeout -k 10 300 python -u -m pytest tests/test_conv_wgrad_gpu.py -x -q --timeout 240 --timeout-method thread \
+timeout -k 10 400 python -u -m pytest tests/test_conv_wgrad_gpu.py tests/test_weight_shadow_gpu.py -x -q --timeout 240 --timeout-method thread \
     > $O/pytest_wgrad.log 2>&1
 rc=$?; echo "wgrad tests rc=$rc"; tail -2 $O/pytest_wgrad.log
 [ $rc -eq 0 ] || exit $rc

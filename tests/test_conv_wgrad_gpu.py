@@ -43,14 +43,25 @@ def _ref_wgrad(x, dy, stride):
     (2, 64, 64, 9, 11, 1), (3, 128, 64, 14, 14, 2), (1, 64, 192, 7, 5, 1), (4, 64, 128, 15, 13, 2),
     (2, 256, 256, 14, 14, 1), (5, 512, 512, 7, 7, 1), (1, 64, 64, 1, 1, 1), (2, 64, 64, 2, 3, 2),
     (3, 64, 64, 70, 9, 1), (2, 64, 128, 131, 5, 2), (1, 64, 64, 3, 70, 1), (2, 64, 64, 5, 131, 2)])
-def test_conv3x3_wgrad_matches_fp64(dev, monkeypatch, form, N, Ci, Co, H, W, stride):
+def test_conv3x3_wgrad_matches_fp64(dev, form, N, Ci, Co, H, W, stride):
     """Both forms of the kernel: the window form (whole output rows per chunk, the taps read one
     staged input window; every shape with Wo <= 64) and the gather form (64-pixel chunks, one
-    gathered tile per tap; wider images, or DAUC_WGRAD_GATHER=1)."""
-    from distributedauc_amd import ops
+    gathered tile per tap; wider images; everywhere under the tuning build's dauc_set_wgrad_form(1))."""
+    from distributedauc_amd import _lib, ops
 
-    if form == "gather":
-        monkeypatch.setenv("DAUC_WGRAD_GATHER", "1")
+    if form == "window":
+        _check_wgrad(dev, N, Ci, Co, H, W, stride)
+        return
+    ops.set_wgrad_form(1)
+    try:
+        with _lib.using(_lib.tuning()):
+            _check_wgrad(dev, N, Ci, Co, H, W, stride)
+    finally:
+        ops.set_wgrad_form(0)
+
+
+def _check_wgrad(dev, N, Ci, Co, H, W, stride):
+    from distributedauc_amd import ops
 
     g = torch.Generator(device=dev).manual_seed(N * 1000 + Ci + Co + H)
     x = torch.randn((N, Ci, H, W), device=dev, generator=g).to(torch.bfloat16)
