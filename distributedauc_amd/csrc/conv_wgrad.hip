@@ -196,10 +196,10 @@ __global__ __launch_bounds__(kWgThreads) void wgrad3x3_kernel(const __hip_bfloat
 // row address, so lane (q, p) of a group points at pixel k's window position + kh (W + 2) + kw.
 // The pixel -> position map is the same for every chunk, so each lane computes its 4 positions
 // once. Two LDS buffers: the next chunk is staged while this one is multiplied, one barrier per
-// chunk; two staging register sets: a chunk's loads are issued two chunks ahead. Pixels k >= KP (a chunk's padding) have zero dy rows (A), so their B values (pixel 0's)
+// chunk. Pixels k >= KP (a chunk's padding) have zero dy rows (A), so their B values (pixel 0's)
 // add nothing.
 constexpr int kMaxWinVec = 8;  // window vectors per thread: <= 512 positions of 8 vectors
-constexpr int kWinVecFast = 6;  // the most the two staging register sets hold without spilling much
+constexpr int kWinVecFast = 8;  // window vectors per thread that fit beside the accumulators unspilled
 
 struct WinGeom {
     int N, H, W, Ci, Ho, Wo, Co, stride;
@@ -218,70 +218,82 @@ struct WinStaging {
     unsigned ok;  // bit j: window vector j in the image; bit kMaxWinVec: the dy row exists
 };
 
+// 32-bit element offsets throughout (host: N * H * W * Ci and N * Ho * Wo * Co < 2^31): 64-bit
+// address arithmetic per load was most of the loop's VALU work
 template <int NV>
 __device__ __forceinline__ void load_win(WinStaging<NV>& s, const __hip_bfloat16* __restrict__ x,
-                                         const __hip_bfloat16* __restrict__ dy, const WinGeom& g, int64_t chunk,
+                                         const __hip_bfloat16* __restrict__ dy, const WinGeom& g, int chunk,
                                          const int (&wpos)[kMaxWinVec], int pr, int v, int co0, int ci0) {
-    const int64_t gr0 = chunk * g.R;
-    // dy: pixel k = pr of the chunk
-    {
+    const int gr0 = chunk * g.R;
+    const int GR = static_cast<int>(g.GR);
+    {  // dy: pixel k = pr of the chunk
         const int rr = pr / g.Wo, wo = pr - rr * g.Wo;
-        const int64_t gr = gr0 + rr;
-        const bool ok = (pr < g.KP) & (gr < g.GR);
-        const int64_t q = ok ? gr * g.Wo + wo : 0;
-        s.a = *reinterpret_cast<const uint4*>(dy + q * g.Co + co0 + 8 * v);
+        const int gr = gr0 + rr;
+        const bool ok = (pr < g.KP) & (gr < GR);
+        const int q = ok ? gr * g.Wo + wo : 0;
+        s.a = *reinterpret_cast<const uint4*>(dy + (q * g.Co + co0 + 8 * v));
         s.ok = ok ? (1u << kMaxWinVec) : 0u;
     }
 #pragma unroll
     for (int j = 0; j < NV; ++j) {
         const int pk = wpos[j];  // rr | kh << 8 | w' << 16, bit 31: a position of the window
         const int rr = pk & 0xff, kh = (pk >> 8) & 0xff, wc = (pk >> 16) & 0x7fff;
-        const int64_t gr = gr0 + rr;
-        const int grc = static_cast<int>(gr < g.GR ? gr : g.GR - 1);
+        const int gr = gr0 + rr;
+        const int grc = gr < GR ? gr : GR - 1;
         const int n = grc / g.Ho, ho = grc - n * g.Ho;
         const int ih = ho * g.stride - 1 + kh, iw = wc - 1;
-        const bool ok = (pk < 0) & (gr < g.GR) & (ih >= 0) & (ih < g.H) & (iw >= 0) & (iw < g.W);
+        const bool ok = (pk < 0) & (gr < GR) & (ih >= 0) & (ih < g.H) & (iw >= 0) & (iw < g.W);
         const int ihc = min(max(ih, 0), g.H - 1), iwc = min(max(iw, 0), g.W - 1);
         const int vv = (threadIdx.x + kWgThreads * j) & 7;
-        s.w[j] = *reinterpret_cast<const uint4*>(x + ((int64_t(n) * g.H + ihc) * g.W + iwc) * g.Ci + ci0 + 8 * vv);
+        s.w[j] = *reinterpret_cast<const uint4*>(x + (((n * g.H + ihc) * g.W + iwc) * g.Ci + ci0 + 8 * vv));
         s.ok |= ok ? (1u << j) : 0u;
     }
 }
 
+typedef __attribute__((address_space(3))) short lds_short;
+typedef unsigned v4u __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4u lds_v4u;
+
+__device__ __forceinline__ void st_lds(lds_short* p, const uint4& u) { *(lds_v4u*)p = v4u{u.x, u.y, u.z, u.w}; }
+
 template <int NV>
-__device__ __forceinline__ void stage_win(const WinStaging<NV>& s, short* buf, const WinGeom& g, int pr, int v) {
-    *reinterpret_cast<uint4*>(buf + pr * kRow + 8 * v) = masked(s.a, s.ok, kMaxWinVec);
-    short* win = buf + kKT * kRow;
+__device__ __forceinline__ void stage_win(const WinStaging<NV>& s, lds_short* buf, const WinGeom& g, int pr, int v) {
+    st_lds(buf + (pr * kRow + 8 * v), masked(s.a, s.ok, kMaxWinVec));
+    lds_short* win = buf + kKT * kRow;
 #pragma unroll
     for (int j = 0; j < NV; ++j) {
         const int idx = threadIdx.x + kWgThreads * j;
         const int pos = idx >> 3;
-        if (pos < g.npos) *reinterpret_cast<uint4*>(win + pos * kRow + 8 * (idx & 7)) = masked(s.w[j], s.ok, j);
+        if (pos < g.npos)
+            st_lds(win + (pos * kRow + 8 * (idx & 7)), masked(s.w[j], s.ok, j));
     }
 }
 
 inline size_t win_lds_bytes(const WinGeom& g) { return size_t(2) * (kKT + g.npos) * kRow * sizeof(short); }
 
-__device__ __forceinline__ v4s tr_read_at(const short* base, int row, int c0, int lane) {
-    return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(base + row * kRow + c0 + 4 * (lane & 3)));
+__device__ __forceinline__ v4s tr_at(const lds_short* p) {
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)p);
 }
 
-// one wave's 36 MFMAs of a chunk staged in `cur` (A rows, then the window)
-__device__ __forceinline__ void win_multiply(f32x4v (&acc)[2][9], const short* cur, const WinGeom& g,
-                                             const int (&bpos)[2][2], int mt0, int nt0, int lane) {
-    const short* win = cur + kKT * kRow;
+// one wave's 36 MFMAs of a chunk staged at `cur` (A rows, then the window). aoff / boff: this
+// lane's element offsets of its A rows / window positions (k-step, half); toff: each tap's window
+// offset (wave-uniform)
+__device__ __forceinline__ void win_multiply(f32x4v (&acc)[2][9], const lds_short* cur, const int (&aoff)[2][2],
+                                             const int (&boff)[2][2], const int (&toff)[9], int mt0, int nt0) {
+    const lds_short* win = cur + kKT * kRow;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
         bf16x8 fa[2];
 #pragma unroll
-        for (int a = 0; a < 2; ++a) fa[a] = frag(cur, ks, 16 * (mt0 + a), lane);
+        for (int a = 0; a < 2; ++a) {
+            const int c0 = 16 * (mt0 + a);
+            const v4s f2[2] = {tr_at(cur + (aoff[ks][0] + c0)), tr_at(cur + (aoff[ks][1] + c0))};
+            fa[a] = *reinterpret_cast<const bf16x8*>(f2);
+        }
 #pragma unroll
         for (int bb = 0; bb < 9; ++bb) {
-            const int t = nt0 + bb, tap = t >> 2;
-            const int toff = (tap / 3) * g.Wd + tap % 3;
-            const v4s lo = tr_read_at(win, bpos[ks][0] + toff, 16 * (t & 3), lane);
-            const v4s hi = tr_read_at(win, bpos[ks][1] + toff, 16 * (t & 3), lane);
-            const v4s f2[2] = {lo, hi};
+            const int o = toff[bb];
+            const v4s f2[2] = {tr_at(win + (boff[ks][0] + o)), tr_at(win + (boff[ks][1] + o))};
             const bf16x8 fb = *reinterpret_cast<const bf16x8*>(f2);
 #pragma unroll
             for (int a = 0; a < 2; ++a)
@@ -295,11 +307,12 @@ __global__ __launch_bounds__(kWgThreads) void wgrad3x3_win_kernel(const __hip_bf
                                                                   const __hip_bfloat16* __restrict__ dy,
                                                                   WinGeom g, float* __restrict__ out) {
     extern __shared__ short lds_dyn[];
+    lds_short* L = (lds_short*)lds_dyn;
     const int buf_elems = (kKT + g.npos) * kRow;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int co0 = (blockIdx.x / g.ctiles) * kBM, ci0 = (blockIdx.x % g.ctiles) * kBC;
-    const int64_t c_begin = int64_t(blockIdx.y) * g.cps;
-    const int64_t c_end = c_begin + g.cps < g.chunks ? c_begin + g.cps : g.chunks;
+    const int c_begin = static_cast<int>(blockIdx.y * g.cps);
+    const int c_end = static_cast<int>(c_begin + g.cps < g.chunks ? c_begin + g.cps : g.chunks);
     const int pr = tid >> 3, v = tid & 7;
 
     // this thread's window vectors (the same positions in every chunk)
@@ -312,47 +325,47 @@ __global__ __launch_bounds__(kWgThreads) void wgrad3x3_win_kernel(const __hip_bf
         const int kh = rem / g.Wd, wc = rem - kh * g.Wd;
         wpos[j] = (pos < g.npos ? int(0x80000000u) : 0) | rr | (kh << 8) | (wc << 16);
     }
-    // this lane's B-fragment rows: pixel k = 32 ks + 8 (lane >> 4) + 4 h + ((lane & 15) >> 2) ->
-    // its window position for tap (0, 0)
-    int bpos[2][2];
+    // this lane's fragment rows: pixel k = 32 ks + 8 (lane >> 4) + 4 h + ((lane & 15) >> 2); A row
+    // k, window position of k for tap (0, 0); + the lane's 4 channels 4 (lane & 3)
+    int aoff[2][2], boff[2][2];
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             const int k = 32 * ks + 8 * (lane >> 4) + 4 * h + ((lane & 15) >> 2);
             const int rr = k / g.Wo, cc = k - rr * g.Wo;
-            bpos[ks][h] = k < g.KP ? rr * 3 * g.Wd + cc * g.stride : 0;
+            const int pos = k < g.KP ? rr * 3 * g.Wd + cc * g.stride : 0;
+            aoff[ks][h] = k * kRow + 4 * (lane & 3);
+            boff[ks][h] = pos * kRow + 4 * (lane & 3);
         }
+    const int mt0 = 2 * (wave & 1), nt0 = 9 * (wave >> 1);
+    int toff[9];  // (tap, 16-channel block) tile nt0 + bb: tap window offset + channel block
+#pragma unroll
+    for (int bb = 0; bb < 9; ++bb) {
+        const int t = nt0 + bb, tap = t >> 2;
+        toff[bb] = ((tap / 3) * g.Wd + tap % 3) * kRow + 16 * (t & 3);
+    }
 
     f32x4v acc[2][9];
 #pragma unroll
     for (int a = 0; a < 2; ++a)
 #pragma unroll
         for (int b = 0; b < 9; ++b) acc[a][b] = f32x4v{0.f, 0.f, 0.f, 0.f};
-    const int mt0 = 2 * (wave & 1), nt0 = 9 * (wave >> 1);
 
-    // Two register sets: a chunk's global loads are issued two chunks before it is staged, so
-    // their latency (mostly HBM: a window is read by one workgroup) has two chunks' MFMAs to hide
-    // behind instead of one. s0 / s1 alternate; every load is unconditional (clamped chunk).
-    short* buf0 = lds_dyn;
-    short* buf1 = lds_dyn + buf_elems;
-    WinStaging<NV> s0, s1;
-    load_win<NV>(s0, x, dy, g, c_begin, wpos, pr, v, co0, ci0);
-    stage_win<NV>(s0, buf0, g, pr, v);
-    load_win<NV>(s0, x, dy, g, min(c_begin + 1, c_end - 1), wpos, pr, v, co0, ci0);
-    load_win<NV>(s1, x, dy, g, min(c_begin + 2, c_end - 1), wpos, pr, v, co0, ci0);
+    WinStaging<NV> st;
+    load_win<NV>(st, x, dy, g, c_begin, wpos, pr, v, co0, ci0);
+    stage_win<NV>(st, L, g, pr, v);
+    load_win<NV>(st, x, dy, g, c_begin + 1 < c_end ? c_begin + 1 : c_begin, wpos, pr, v, co0, ci0);
     __syncthreads();
-    for (int64_t c = c_begin; c < c_end; ++c) {
-        // chunk c on buffer (c - c_begin) & 1; s0 holds chunk c + 1, s1 chunk c + 2
-        const int b = static_cast<int>(c - c_begin) & 1;
-        stage_win<NV>(s0, b ? buf0 : buf1, g, pr, v);
-        load_win<NV>(s0, x, dy, g, min(c + 3, c_end - 1), wpos, pr, v, co0, ci0);
+    for (int c = c_begin; c < c_end; ++c) {
+        const int b = (c - c_begin) & 1;
+        // chunk c + 1 into the other buffer (read last by chunk c - 1, before the barrier below
+        // ended that iteration); on the last chunk this stages a clamped copy nobody reads
+        stage_win<NV>(st, L + (b ^ 1) * buf_elems, g, pr, v);
+        load_win<NV>(st, x, dy, g, c + 2 < c_end ? c + 2 : c_end - 1, wpos, pr, v, co0, ci0);
         __builtin_amdgcn_sched_barrier(0);  // the loads ahead of the MFMAs
-        win_multiply(acc, b ? buf1 : buf0, g, bpos, mt0, nt0, lane);
+        win_multiply(acc, L + b * buf_elems, aoff, boff, toff, mt0, nt0);
         __syncthreads();
-        const WinStaging<NV> t = s0;  // rotate the ring: s0 <- chunk c + 2, s1 <- chunk c + 3
-        s0 = s1;
-        s1 = t;
     }
     float* o = out + int64_t(blockIdx.y) * int64_t(g.Co) * kTaps * g.Ci;
 #pragma unroll
@@ -397,6 +410,8 @@ int g_wgrad_form = 0;  // dauc_set_wgrad_form: 0 automatic, 1 the gather form (t
 
 bool win_geom(int64_t N, int H, int W, int Ci, int Ho, int Wo, int Co, int stride, WinGeom& g) {
     if (Wo > kKT) return false;
+    // the window kernel indexes x and dy with 32-bit element offsets
+    if (N * H * int64_t(W) * Ci >= (int64_t(1) << 31) || N * Ho * int64_t(Wo) * Co >= (int64_t(1) << 31)) return false;
 #ifdef DAUC_TUNING
     if (g_wgrad_form == 1) return false;
 #endif
@@ -409,8 +424,8 @@ bool win_geom(int64_t N, int H, int W, int Ci, int Ho, int Wo, int Co, int strid
     g.Co = Co;
     g.stride = stride;
     g.Wd = W + 2;
-    // as many whole output rows as fit 64 pixels, fewer when the window would need more than 6
-    // vectors per thread (two staging sets of more spill beside the accumulators)
+    // as many whole output rows as fit 64 pixels (fewer if the window needs more vectors per thread
+    // than kWinVecFast)
     for (g.R = kKT / Wo; g.R >= 1; --g.R) {
         g.npos = g.R * 3 * g.Wd;
         g.nvec = (g.npos * 8 + kWgThreads - 1) / kWgThreads;

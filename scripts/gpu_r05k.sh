@@ -1,10 +1,10 @@
 #!/bin/bash
-# round 5: the window wgrad kernel with two staging register sets (loads two chunks ahead) and at
-# most 6 window vectors per thread. Tests, then training-only runs against the previous build
+# round 5: the window wgrad kernel with 32-bit LDS and global offsets (the 64-bit address math was
+# most of its loop VALU). Tests, then training-only runs against the previous build
 # (tuning/ab/libdauc_win1.so) interleaved, then a kernel trace.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-O=gpurun_out/r05l
+O=gpurun_out/r05m
 mkdir -p $O
 timeout -k 10 400 python -u -m pytest tests/test_conv_wgrad_gpu.py tests/test_weight_shadow_gpu.py -x -q --timeout 240 --timeout-method thread \
     > $O/pytest_wgrad.log 2>&1
