@@ -200,9 +200,16 @@ __global__ __launch_bounds__(kWgThreads) void wgrad3x3_kernel(const __hip_bfloat
 // add nothing.
 constexpr int kMaxWinVec = 8;  // window vectors per thread: <= 512 positions of 8 vectors
 constexpr int kWinVecFast = 8;  // window vectors per thread that fit beside the accumulators unspilled
+// LDS row strides (bf16 elements) of the window kernel. A transposing read serves 32 lanes per
+// pass, 8 rows of 8 bytes; the k order below puts 8 consecutive pixels in one pass, so 80-element
+// (40-bank) rows land them on 8 disjoint bank octets: conflict-free for the dy tile and a stride-1
+// window, where 72 (36 banks) conflicts 2-way. A stride-2 window steps 2 rows per pixel: 72 there.
+constexpr int kARow = 80;
 
 struct WinGeom {
     int N, H, W, Ci, Ho, Wo, Co, stride;
+    int KT;    // pixel rows of the staged dy tile: 64 or 128 (2 or 4 k-steps per chunk)
+    int wrow;  // LDS row stride of the window: 80 (stride 1) or 72 (stride 2)
     int R, Wd, npos, KP, nvec;
     int64_t GR;      // output rows N * Ho
     int64_t chunks;  // ceil(GR / R)
@@ -212,27 +219,30 @@ struct WinGeom {
 
 inline size_t win_lds_bytes(const struct WinGeom& g);
 
-template <int NV>
+template <int NV, int KS>
 struct WinStaging {
-    uint4 a, w[NV];
+    uint4 a[KS / 2], w[NV];
     unsigned ok;  // bit j: window vector j in the image; bit kMaxWinVec: the dy row exists
 };
 
 // 32-bit element offsets throughout (host: N * H * W * Ci and N * Ho * Wo * Co < 2^31): 64-bit
 // address arithmetic per load was most of the loop's VALU work
-template <int NV>
-__device__ __forceinline__ void load_win(WinStaging<NV>& s, const __hip_bfloat16* __restrict__ x,
+template <int NV, int KS>
+__device__ __forceinline__ void load_win(WinStaging<NV, KS>& s, const __hip_bfloat16* __restrict__ x,
                                          const __hip_bfloat16* __restrict__ dy, const WinGeom& g, int chunk,
                                          const int (&wpos)[kMaxWinVec], int pr, int v, int co0, int ci0) {
     const int gr0 = chunk * g.R;
     const int GR = static_cast<int>(g.GR);
-    {  // dy: pixel k = pr of the chunk
-        const int rr = pr / g.Wo, wo = pr - rr * g.Wo;
+    s.ok = 0u;
+#pragma unroll
+    for (int i = 0; i < KS / 2; ++i) {  // dy: pixels k = pr + 64 i of the chunk
+        const int k = pr + 64 * i;
+        const int rr = k / g.Wo, wo = k - rr * g.Wo;
         const int gr = gr0 + rr;
-        const bool ok = (pr < g.KP) & (gr < GR);
+        const bool ok = (k < g.KP) & (gr < GR);
         const int q = ok ? gr * g.Wo + wo : 0;
-        s.a = *reinterpret_cast<const uint4*>(dy + (q * g.Co + co0 + 8 * v));
-        s.ok = ok ? (1u << kMaxWinVec) : 0u;
+        s.a[i] = *reinterpret_cast<const uint4*>(dy + (q * g.Co + co0 + 8 * v));
+        s.ok |= ok ? (1u << (kMaxWinVec + i)) : 0u;
     }
 #pragma unroll
     for (int j = 0; j < NV; ++j) {
@@ -256,20 +266,24 @@ typedef __attribute__((address_space(3))) v4u lds_v4u;
 
 __device__ __forceinline__ void st_lds(lds_short* p, const uint4& u) { *(lds_v4u*)p = v4u{u.x, u.y, u.z, u.w}; }
 
-template <int NV>
-__device__ __forceinline__ void stage_win(const WinStaging<NV>& s, lds_short* buf, const WinGeom& g, int pr, int v) {
-    st_lds(buf + (pr * kRow + 8 * v), masked(s.a, s.ok, kMaxWinVec));
-    lds_short* win = buf + kKT * kRow;
+template <int NV, int KS>
+__device__ __forceinline__ void stage_win(const WinStaging<NV, KS>& s, lds_short* buf, const WinGeom& g, int pr,
+                                          int v) {
+#pragma unroll
+    for (int i = 0; i < KS / 2; ++i) st_lds(buf + ((pr + 64 * i) * kARow + 8 * v), masked(s.a[i], s.ok, kMaxWinVec + i));
+    lds_short* win = buf + 32 * KS * kARow;
 #pragma unroll
     for (int j = 0; j < NV; ++j) {
         const int idx = threadIdx.x + kWgThreads * j;
         const int pos = idx >> 3;
         if (pos < g.npos)
-            st_lds(win + (pos * kRow + 8 * (idx & 7)), masked(s.w[j], s.ok, j));
+            st_lds(win + (pos * g.wrow + 8 * (idx & 7)), masked(s.w[j], s.ok, j));
     }
 }
 
-inline size_t win_lds_bytes(const WinGeom& g) { return size_t(2) * (kKT + g.npos) * kRow * sizeof(short); }
+inline size_t win_lds_bytes(const WinGeom& g) {
+    return size_t(2) * (size_t(g.KT) * kARow + size_t(g.npos) * g.wrow) * sizeof(short);
+}
 
 __device__ __forceinline__ v4s tr_at(const lds_short* p) {
     return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)p);
@@ -278,11 +292,12 @@ __device__ __forceinline__ v4s tr_at(const lds_short* p) {
 // one wave's 36 MFMAs of a chunk staged at `cur` (A rows, then the window). aoff / boff: this
 // lane's element offsets of its A rows / window positions (k-step, half); toff: each tap's window
 // offset (wave-uniform)
-__device__ __forceinline__ void win_multiply(f32x4v (&acc)[2][9], const lds_short* cur, const int (&aoff)[2][2],
-                                             const int (&boff)[2][2], const int (&toff)[9], int mt0, int nt0) {
-    const lds_short* win = cur + kKT * kRow;
+template <int KS>
+__device__ __forceinline__ void win_multiply(f32x4v (&acc)[2][9], const lds_short* cur, const int (&aoff)[KS][2],
+                                             const int (&boff)[KS][2], const int (&toff)[9], int mt0, int nt0) {
+    const lds_short* win = cur + 32 * KS * kARow;
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
+    for (int ks = 0; ks < KS; ++ks) {
         bf16x8 fa[2];
 #pragma unroll
         for (int a = 0; a < 2; ++a) {
@@ -302,13 +317,13 @@ __device__ __forceinline__ void win_multiply(f32x4v (&acc)[2][9], const lds_shor
     }
 }
 
-template <int NV>
+template <int NV, int KS>
 __global__ __launch_bounds__(kWgThreads) void wgrad3x3_win_kernel(const __hip_bfloat16* __restrict__ x,
                                                                   const __hip_bfloat16* __restrict__ dy,
                                                                   WinGeom g, float* __restrict__ out) {
     extern __shared__ short lds_dyn[];
     lds_short* L = (lds_short*)lds_dyn;
-    const int buf_elems = (kKT + g.npos) * kRow;
+    const int buf_elems = 32 * KS * kARow + g.npos * g.wrow;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int co0 = (blockIdx.x / g.ctiles) * kBM, ci0 = (blockIdx.x % g.ctiles) * kBC;
     const int c_begin = static_cast<int>(blockIdx.y * g.cps);
@@ -325,25 +340,27 @@ __global__ __launch_bounds__(kWgThreads) void wgrad3x3_win_kernel(const __hip_bf
         const int kh = rem / g.Wd, wc = rem - kh * g.Wd;
         wpos[j] = (pos < g.npos ? int(0x80000000u) : 0) | rr | (kh << 8) | (wc << 16);
     }
-    // this lane's fragment rows: pixel k = 32 ks + 8 (lane >> 4) + 4 h + ((lane & 15) >> 2); A row
-    // k, window position of k for tap (0, 0); + the lane's 4 channels 4 (lane & 3)
-    int aoff[2][2], boff[2][2];
+    // this lane's fragment rows: pixel k = 32 ks + 16 h + 4 (lane >> 4) + ((lane & 15) >> 2) (any
+    // order of the 32 pixels of a k-step sums the same products; this one gives each 32-lane pass
+    // of read h 8 consecutive pixels); A row k, window position of k for tap (0, 0); + the lane's 4
+    // channels 4 (lane & 3)
+    int aoff[KS][2], boff[KS][2];
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
+    for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-            const int k = 32 * ks + 8 * (lane >> 4) + 4 * h + ((lane & 15) >> 2);
+            const int k = 32 * ks + 16 * h + 4 * (lane >> 4) + ((lane & 15) >> 2);
             const int rr = k / g.Wo, cc = k - rr * g.Wo;
             const int pos = k < g.KP ? rr * 3 * g.Wd + cc * g.stride : 0;
-            aoff[ks][h] = k * kRow + 4 * (lane & 3);
-            boff[ks][h] = pos * kRow + 4 * (lane & 3);
+            aoff[ks][h] = k * kARow + 4 * (lane & 3);
+            boff[ks][h] = pos * g.wrow + 4 * (lane & 3);
         }
     const int mt0 = 2 * (wave & 1), nt0 = 9 * (wave >> 1);
     int toff[9];  // (tap, 16-channel block) tile nt0 + bb: tap window offset + channel block
 #pragma unroll
     for (int bb = 0; bb < 9; ++bb) {
         const int t = nt0 + bb, tap = t >> 2;
-        toff[bb] = ((tap / 3) * g.Wd + tap % 3) * kRow + 16 * (t & 3);
+        toff[bb] = ((tap / 3) * g.Wd + tap % 3) * g.wrow + 16 * (t & 3);
     }
 
     f32x4v acc[2][9];
@@ -352,19 +369,19 @@ __global__ __launch_bounds__(kWgThreads) void wgrad3x3_win_kernel(const __hip_bf
 #pragma unroll
         for (int b = 0; b < 9; ++b) acc[a][b] = f32x4v{0.f, 0.f, 0.f, 0.f};
 
-    WinStaging<NV> st;
-    load_win<NV>(st, x, dy, g, c_begin, wpos, pr, v, co0, ci0);
-    stage_win<NV>(st, L, g, pr, v);
-    load_win<NV>(st, x, dy, g, c_begin + 1 < c_end ? c_begin + 1 : c_begin, wpos, pr, v, co0, ci0);
+    WinStaging<NV, KS> st;
+    load_win<NV, KS>(st, x, dy, g, c_begin, wpos, pr, v, co0, ci0);
+    stage_win<NV, KS>(st, L, g, pr, v);
+    load_win<NV, KS>(st, x, dy, g, c_begin + 1 < c_end ? c_begin + 1 : c_begin, wpos, pr, v, co0, ci0);
     __syncthreads();
     for (int c = c_begin; c < c_end; ++c) {
         const int b = (c - c_begin) & 1;
         // chunk c + 1 into the other buffer (read last by chunk c - 1, before the barrier below
         // ended that iteration); on the last chunk this stages a clamped copy nobody reads
-        stage_win<NV>(st, L + (b ^ 1) * buf_elems, g, pr, v);
-        load_win<NV>(st, x, dy, g, c + 2 < c_end ? c + 2 : c_end - 1, wpos, pr, v, co0, ci0);
+        stage_win<NV, KS>(st, L + (b ^ 1) * buf_elems, g, pr, v);
+        load_win<NV, KS>(st, x, dy, g, c + 2 < c_end ? c + 2 : c_end - 1, wpos, pr, v, co0, ci0);
         __builtin_amdgcn_sched_barrier(0);  // the loads ahead of the MFMAs
-        win_multiply(acc, L + b * buf_elems, aoff, boff, toff, mt0, nt0);
+        win_multiply<KS>(acc, L + b * buf_elems, aoff, boff, toff, mt0, nt0);
         __syncthreads();
     }
     float* o = out + int64_t(blockIdx.y) * int64_t(g.Co) * kTaps * g.Ci;
@@ -404,17 +421,39 @@ extern "C" {
 
 namespace {
 // the window form's geometry (returns false when the shape needs the gather form)
+// one chunk layout: R whole output rows of a KT-row dy tile and their windows (false: does not fit)
+bool win_layout(int W, int Wo, int KT, WinGeom& g) {
+    if (Wo > KT) return false;
+    g.KT = KT;
+    g.wrow = g.stride == 1 ? kARow : kRow;
+    g.Wd = W + 2;
+    // as many whole output rows as fit the tile (fewer if the window needs more vectors per thread
+    // than kWinVecFast or more LDS than a CU has)
+    for (g.R = KT / Wo; g.R >= 1; --g.R) {
+        g.npos = g.R * 3 * g.Wd;
+        g.nvec = (g.npos * 8 + kWgThreads - 1) / kWgThreads;
+        if (g.nvec <= kWinVecFast && win_lds_bytes(g) <= 160 * 1024) break;
+    }
+    if (g.R < 1) return false;
+    g.KP = g.R * Wo;
+    return true;
+}
+
 #ifdef DAUC_TUNING
-int g_wgrad_form = 0;  // dauc_set_wgrad_form: 0 automatic, 1 the gather form (tests, A/B runs)
+int g_wgrad_form = 0;  // dauc_set_wgrad_form: 0 automatic, 1 the gather form, 2 / 3 window KT 64 / 128
 #endif
 
 bool win_geom(int64_t N, int H, int W, int Ci, int Ho, int Wo, int Co, int stride, WinGeom& g) {
-    if (Wo > kKT) return false;
     // the window kernel indexes x and dy with 32-bit element offsets
     if (N * H * int64_t(W) * Ci >= (int64_t(1) << 31) || N * Ho * int64_t(Wo) * Co >= (int64_t(1) << 31)) return false;
+    int form = 0;
 #ifdef DAUC_TUNING
-    if (g_wgrad_form == 1) return false;
+    form = g_wgrad_form;
+    if (form == 1) return false;
 #endif
+    // stride 2: the gather form (ResNet-50 layer2.0 at b256: 123 us against the window form's 133;
+    // profiles/r05/wgrad3x3_korder)
+    if (form == 0 && stride != 1) return false;
     g.N = static_cast<int>(N);
     g.H = H;
     g.W = W;
@@ -423,21 +462,14 @@ bool win_geom(int64_t N, int H, int W, int Ci, int Ho, int Wo, int Co, int strid
     g.Wo = Wo;
     g.Co = Co;
     g.stride = stride;
-    g.Wd = W + 2;
-    // as many whole output rows as fit 64 pixels (fewer if the window needs more vectors per thread
-    // than kWinVecFast)
-    for (g.R = kKT / Wo; g.R >= 1; --g.R) {
-        g.npos = g.R * 3 * g.Wd;
-        g.nvec = (g.npos * 8 + kWgThreads - 1) / kWgThreads;
-        if (g.nvec <= kWinVecFast) break;
-    }
-    if (g.R < 1) {
-        g.R = 1;
-        g.npos = 3 * g.Wd;
-        g.nvec = (g.npos * 8 + kWgThreads - 1) / kWgThreads;
-    }
-    g.KP = g.R * Wo;
-    if (g.nvec > kMaxWinVec || win_lds_bytes(g) > 160 * 1024) return false;
+    // a 128-pixel chunk (4 k-steps: half the barriers and staging waits per MFMA) when its rows
+    // fill at least 7/8 of it, else 64 pixels
+    WinGeom g64 = g, g128 = g;
+    const bool ok64 = win_layout(W, Wo, 64, g64);
+    const bool ok128 = win_layout(W, Wo, 128, g128);
+    if (form == 2 ? !ok64 : form == 3 ? !ok128 : !(ok64 || ok128)) return false;
+    const bool use128 = form == 3 || (form == 0 && ok128 && (!ok64 || 8 * g128.KP >= 7 * 128));
+    g = use128 ? g128 : g64;
     g.GR = N * Ho;
     g.chunks = (g.GR + g.R - 1) / g.R;
     g.ctiles = Ci / kBC;
@@ -489,17 +521,26 @@ int dauc_conv3x3_wgrad(const void* x, const void* dy, int dtype, int64_t N, int 
         const size_t lds = win_lds_bytes(wg);
         const __hip_bfloat16* xb = static_cast<const __hip_bfloat16*>(x);
         const __hip_bfloat16* db = static_cast<const __hip_bfloat16*>(dy);
-        switch (wg.nvec) {
-#define DAUC_WIN_CASE(NV) \
-    case NV: hipLaunchKernelGGL(wgrad3x3_win_kernel<NV>, grid, dim3(kWgThreads), lds, st, xb, db, wg, target); break;
-            DAUC_WIN_CASE(1)
-            DAUC_WIN_CASE(2)
-            DAUC_WIN_CASE(3)
-            DAUC_WIN_CASE(4)
-            DAUC_WIN_CASE(5)
-            DAUC_WIN_CASE(6)
-            DAUC_WIN_CASE(7)
-            DAUC_WIN_CASE(8)
+        switch (wg.nvec * 8 + wg.KT / 32) {
+#define DAUC_WIN_CASE(NV, KS) \
+    case NV * 8 + KS:         \
+        hipLaunchKernelGGL((wgrad3x3_win_kernel<NV, KS>), grid, dim3(kWgThreads), lds, st, xb, db, wg, target); break;
+            DAUC_WIN_CASE(1, 2)
+            DAUC_WIN_CASE(2, 2)
+            DAUC_WIN_CASE(3, 2)
+            DAUC_WIN_CASE(4, 2)
+            DAUC_WIN_CASE(5, 2)
+            DAUC_WIN_CASE(6, 2)
+            DAUC_WIN_CASE(7, 2)
+            DAUC_WIN_CASE(8, 2)
+            DAUC_WIN_CASE(1, 4)
+            DAUC_WIN_CASE(2, 4)
+            DAUC_WIN_CASE(3, 4)
+            DAUC_WIN_CASE(4, 4)
+            DAUC_WIN_CASE(5, 4)
+            DAUC_WIN_CASE(6, 4)
+            DAUC_WIN_CASE(7, 4)
+            DAUC_WIN_CASE(8, 4)
 #undef DAUC_WIN_CASE
             default: return DAUC_EINVAL;
         }
@@ -532,7 +573,7 @@ int dauc_conv3x3_wgrad(const void* x, const void* dy, int dtype, int64_t N, int 
 
 #ifdef DAUC_TUNING
 int dauc_set_wgrad_form(int form) {
-    if (form != 0 && form != 1) return DAUC_EINVAL;
+    if (form < 0 || form > 3) return DAUC_EINVAL;
     g_wgrad_form = form;
     return DAUC_OK;
 }

@@ -639,7 +639,7 @@ def conv3x3_wgrad_supported(x: torch.Tensor, dy: torch.Tensor, stride, padding, 
 
 
 def set_wgrad_form(form: int) -> None:
-    """The tuning build's 3x3 weight-gradient form (dauc_set_wgrad_form): 0 automatic, 1 gather."""
+    """The tuning build's 3x3 weight-gradient form (dauc_set_wgrad_form): 0 automatic, 1 gather, 2 / 3 window with 64- / 128-pixel chunks."""
     check(_lib.tuning().dauc_set_wgrad_form(int(form)), "dauc_set_wgrad_form")
 
 

@@ -2,7 +2,9 @@
 shapes, for kernel traces and PMC passes: each shape's call repeated `reps` times, HIP-event time per
 call printed as one JSON line per shape.
 
-    python scripts/probe_wgrad.py [reps]
+    python scripts/probe_wgrad.py [reps] [form]
+
+form (tuning build's dauc_set_wgrad_form): 1 gather, 2 / 3 window with 64- / 128-pixel chunks.
 """
 from __future__ import annotations
 
@@ -13,9 +15,13 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
-from distributedauc_amd import ops  # noqa: E402
+from distributedauc_amd import _lib, ops  # noqa: E402
 
 reps = int(sys.argv[1]) if len(sys.argv) > 1 else 20
+if len(sys.argv) > 2:
+    ops.set_wgrad_form(int(sys.argv[2]))
+    _ctx = _lib.using(_lib.tuning())  # held for the whole run: its exit restores the product build
+    _ctx.__enter__()
 dev = torch.device("cuda", 0)
 for C, H, stride in ((64, 56, 1), (128, 28, 1), (256, 14, 1), (512, 7, 1), (128, 56, 2)):
     g = torch.Generator(device=dev).manual_seed(C + H)
@@ -32,4 +38,4 @@ for C, H, stride in ((64, 56, 1), (128, 28, 1), (256, 14, 1), (512, 7, 1), (128,
     torch.cuda.synchronize()
     us = e0.elapsed_time(e1) / reps * 1e3
     flop = 2 * 256 * Ho * Ho * C * 9 * C
-    print(json.dumps({"C": C, "H": H, "stride": stride, "us_per_call": us, "tflops": flop / us / 1e6}), flush=True)
+    print(json.dumps({"form": sys.argv[2] if len(sys.argv) > 2 else "auto", "C": C, "H": H, "stride": stride, "us_per_call": us, "tflops": flop / us / 1e6}), flush=True)
