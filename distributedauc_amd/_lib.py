@@ -87,6 +87,9 @@ SIGNATURES = {
                                   _vp]),
     "dauc_maxpool2d_backward": (_int, [_vp, _vp, _int, _i64, _int, _int, _int, _int, _int, _int, _int, _int, _vp,
                                        _vp]),
+    "dauc_conv7x7s2_stem_forward": (_int, [_vp, _vp, _int, _i64, _int, _int, _int, _int, _vp, _vp]),
+    "dauc_conv7x7s2_stem_wgrad_workspace_size": (_sz, [_i64, _int, _int]),
+    "dauc_conv7x7s2_stem_wgrad": (_int, [_vp, _vp, _int, _i64, _int, _int, _int, _int, _vp, _vp, _sz, _vp]),
 }
 
 # tuning builds only (tuning/libdauc_tuning.so, -DDAUC_TUNING; include/dauc_tuning.h): measured

@@ -121,12 +121,22 @@ class _ShadowConv(torch.autograd.Function):
     flipped weight) is given: then dx = conv2d(dy, wf) -- a FORWARD convolution of the same shape
     as this one (C_in = C_out for the bottlenecks' 3x3), which runs on the forward solvers (CK,
     no output zero-fill) instead of MIOpen's backward-data kernel and its zero-fill. Same
-    products, fp32 accumulation in another order: the bits of dx differ from torch's."""
+    products, fp32 accumulation in another order: the bits of dx differ from torch's. With
+    ``wgrad_hip`` the 3x3 weight gradients come from csrc/conv_wgrad.hip and the 7x7 stem's forward
+    and weight gradient from csrc/conv_stem.hip (fp32 gradients, no bf16 round trip)."""
 
     @staticmethod
     def forward(ctx, x, weight, wb, wf, stride, padding, dilation, groups, wgrad_hip=False):
-        with torch.autocast("cuda", enabled=False):
-            y = F.conv2d(x, wb, None, stride, padding, dilation, groups)
+        ctx.stem = False
+        if wgrad_hip:
+            from . import ops
+
+            ctx.stem = ops.stem_conv_supported(x, wb, stride, padding, dilation, groups)
+        if ctx.stem:  # the 7x7 stem on csrc/conv_stem.hip (MIOpen: ~6x the HBM-bound time)
+            y = ops.stem_conv_forward(x, wb)
+        else:
+            with torch.autocast("cuda", enabled=False):
+                y = F.conv2d(x, wb, None, stride, padding, dilation, groups)
         ctx.save_for_backward(x, wb, wf)
         ctx.conf = (list(stride), list(padding), list(dilation), groups)
         ctx.wgrad_hip = bool(wgrad_hip)
@@ -138,7 +148,11 @@ class _ShadowConv(torch.autograd.Function):
         stride, padding, dilation, groups = ctx.conf
         nx, nw = bool(ctx.needs_input_grad[0]), bool(ctx.needs_input_grad[1])
         dx = dw = None
-        if nw and ctx.wgrad_hip and wb.shape[2:] == (3, 3):
+        if nw and ctx.stem:
+            from . import ops
+
+            dw = ops.stem_conv_wgrad(x, gy.contiguous(memory_format=torch.channels_last))
+        elif nw and ctx.wgrad_hip and wb.shape[2:] == (3, 3):
             from . import ops
 
             gyc = gy.contiguous(memory_format=torch.channels_last)
@@ -334,7 +348,8 @@ class ResNet(nn.Module):
         parameters must already live in a FlatState, i.e. after CoDA(model)). ``dgrad_fwd``: the
         stride-1 3x3 convolutions' input gradients as forward convolutions with flipped weights
         (_ShadowConv). ``wgrad_hip``: the 3x3 weight gradients from csrc/conv_wgrad.hip (fp32, MFMA)
-        instead of MIOpen's backward-weights + the bf16 -> fp32 cast."""
+        instead of MIOpen's backward-weights + the bf16 -> fp32 cast, and the 7x7 stem's forward
+        and weight gradient from csrc/conv_stem.hip."""
         self._wshadow = WeightShadow(self, dgrad_fwd=dgrad_fwd, wgrad_hip=wgrad_hip) if enabled else None
         return self
 

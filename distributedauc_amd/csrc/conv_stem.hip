@@ -1,0 +1,391 @@
+// The backbone stem: the 7x7 / stride 2 / pad 3 convolution of the 3-channel image into 64
+// channels, forward and weight gradient, channels-last bf16 on MFMA with fp32 accumulation.
+//
+// Reference: imagenet/resnet.py:145 (conv1 = Conv2d(3, 64, kernel_size=7, stride=2, padding=3)),
+// trained by main.py:311-326. torch under bf16 autocast runs MIOpen's implicit-GEMM kernels for it:
+// ResNet-50 b256, forward ~360 us and backward-weights ~350 us (+ a zero-fill and two casts) for
+// 60 GFLOP each, because a 3-channel, 147-deep reduction fits neither kernel's tiling. Both are
+// bound here by HBM (the 411 MB activation written / read once), not by the MFMA.
+//
+// Layout: x [N][H][W][3], y / dy [N][Ho][Wo][64], weight [64][7][7][3] (the channels-last memory
+// order of [64, 3, 7, 7]). For output pixel (n, oh, ow) and kernel row kh, the 21 inputs
+// (kw, ci) are CONTIGUOUS in x: x[n][2oh - 3 + kh][2ow - 3 + kw][ci] = row_kh[6 ow + 3 kw + ci]
+// of the staged input row. So the reduction index is k' = 24 kh + j (j = 3 kw + ci < 21; 21..23
+// and kh = 7 carry zero weights): K' = 192 = 6 MFMA k-steps, and a lane's 8 consecutive k' of one
+// pixel are 8 consecutive bf16 of one staged row (4-byte aligned: 12 ow bytes).
+//
+// A task is one output row segment (n, oh, ow0 .. ow0 + 127): its 7 input rows (+ a zero row)
+// are staged into LDS (zeros outside the image), then
+//   forward: D[co][px] = W'[co][k'] * P[k'][px]: the weights as A fragments in registers (loaded
+//            once per workgroup), the patches as B fragments read straight from the rows; the
+//            64 x 128 bf16 result goes through an LDS tile to 16-byte coalesced stores.
+//   wgrad:   D[co][k'] = dy^T[co][px] * P[px][k']: dy's [px][co] tile read with the transposing
+//            LDS read (ds_read_b64_tr_b16), the patches gathered 2 bytes per pixel; each
+//            workgroup accumulates its tasks in registers and writes one fp32 slab, summed in
+//            workgroup order by dauc_slab_sum: bitwise reproducible.
+// Workgroups are persistent (a fixed grid striding over the tasks); the next task's input rows
+// (and dy tile) are loaded into registers while the current one computes.
+
+#include <hip/hip_bf16.h>
+
+#include "dauc_internal.h"
+
+namespace dauc {
+namespace {
+
+typedef short v4s __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) short lds_short;
+typedef __attribute__((address_space(3))) v4s lds_v4s;
+typedef __attribute__((address_space(3))) unsigned lds_u32;
+typedef __attribute__((address_space(3))) u32x4 lds_u32x4;
+
+constexpr int kThreads = 256;             // 4 waves
+constexpr int kSeg = 128;                 // output pixels per task
+constexpr int kInRow = 800;               // staged input row, bf16 elements (>= 3 * (2 * 127 + 7) = 783 and
+                                          // >= 6 * 127 + 23 + 1 read by the last pixel's last k-step)
+constexpr int kInElems = 8 * kInRow;      // 7 kernel rows + a zero row
+constexpr int kInPer = kInElems / kThreads;  // 25 staged elements per thread
+constexpr int kKp = 192;                  // padded reduction length of the forward
+constexpr int kOutRow = 72;               // forward output tile row (64 channels + 8)
+constexpr int kDyRow = 80;                // wgrad dy tile row (64 channels + 16: conflict-free transposing reads)
+constexpr int kWElems = 64 * 147;         // weight / gradient elements
+static_assert(kInElems % kThreads == 0, "input staging");
+
+struct StemGeom {
+    int N, H, W, Ho, Wo;
+    int segs;     // ceil(Wo / kSeg)
+    int tasks;    // N * Ho * segs
+};
+
+__device__ __forceinline__ void task_coords(const StemGeom& g, int t, int& n, int& oh, int& ow0) {
+    const int row = t / g.segs;
+    ow0 = (t - row * g.segs) * kSeg;
+    n = row / g.Ho;
+    oh = row - n * g.Ho;
+}
+
+// this thread's 25 elements of task t's staged rows: element i = tid + 256 u of the [8][kInRow] image.
+// Each element arrives as the aligned 4-byte word that holds it (a word holding a valid element
+// cannot leave the allocation); which half it is and whether it lies in the image go to bit masks
+// applied when the values are stored to LDS. Any select, zero-extension or packing of the loaded
+// values here would make the wave wait for the loads now instead of across the current task's MFMAs.
+struct RowStage {
+    unsigned r[kInPer];
+    unsigned ok, hi;  // bit u: element u is in the image / is the upper half of its word
+};
+
+__device__ __forceinline__ void load_rows(RowStage& st, const unsigned short* __restrict__ x, const StemGeom& g,
+                                          int t) {
+    int n, oh, ow0;
+    task_coords(g, t, n, oh, ow0);
+    const int c0 = 3 * (2 * ow0 - 3);  // element of the row where the staged run starts
+    const int rowlen = 3 * g.W;
+    const unsigned* xw = reinterpret_cast<const unsigned*>(x);
+    unsigned okm = 0u, him = 0u;
+#pragma unroll
+    for (int u = 0; u < kInPer; ++u) {
+        // i = tid + 256 u lies in staged row klo or klo + 1 (compile-time bounds: no division)
+        const int i = threadIdx.x + kThreads * u;
+        const int klo = (kThreads * u) / kInRow;
+        const int kh = klo + (i >= kInRow * (klo + 1) ? 1 : 0);
+        const int e = i - kInRow * kh;
+        const int ih = 2 * oh - 3 + kh;
+        const int col = c0 + e;  // the run of a row is contiguous in x: (iw, ci) -> 3 iw + ci
+        const bool ok = (kh < 7) & (ih >= 0) & (ih < g.H) & (col >= 0) & (col < rowlen);
+        const int ihc = min(max(ih, 0), g.H - 1);
+        const int q = (n * g.H + ihc) * rowlen + min(max(col, 0), rowlen - 1);
+        st.r[u] = xw[q >> 1];
+        okm |= ok ? (1u << u) : 0u;
+        him |= static_cast<unsigned>(q & 1) << u;
+    }
+    st.ok = okm;
+    st.hi = him;
+}
+
+__device__ __forceinline__ void store_rows(const RowStage& st, lds_short* in) {
+#pragma unroll
+    for (int u = 0; u < kInPer; ++u) {
+        const unsigned v = (st.r[u] >> (((st.hi >> u) & 1u) * 16)) & 0xffffu;
+        in[threadIdx.x + kThreads * u] = static_cast<short>(((st.ok >> u) & 1u) ? v : 0u);
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// forward
+
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) void stem_fwd_kernel(const unsigned short* __restrict__ x,
+                                                            const unsigned short* __restrict__ w, StemGeom g,
+                                                            unsigned short* __restrict__ y) {
+    __shared__ short in_s[kInElems];
+    __shared__ short out_s[kSeg * kOutRow];
+    __shared__ short w_s[64 * kKp];
+    lds_short* in = (lds_short*)in_s;
+    lds_short* out = (lds_short*)out_s;
+    lds_short* wl = (lds_short*)w_s;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int grp = lane >> 4, col = lane & 15;
+
+    // the padded weight W'[co][k'] (zeros at j >= 21 and kh = 7), once per workgroup
+    for (int i = tid; i < 64 * kKp; i += kThreads) {
+        const int co = i / kKp, kp = i - co * kKp;
+        const int kh = kp / 24, j = kp - kh * 24;
+        wl[i] = (kh < 7 && j < 21) ? static_cast<short>(w[co * 147 + kh * 21 + j]) : short(0);
+    }
+    int t = blockIdx.x;
+    RowStage st;
+    if (t < g.tasks) load_rows(st, x, g, t);
+    __syncthreads();
+    // A fragments: lane (grp, col) holds W'[16 ct + col][32 s + 8 grp .. + 7]
+    bf16x8 wa[4][6];
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct)
+#pragma unroll
+        for (int s = 0; s < 6; ++s)
+            wa[ct][s] = __builtin_bit_cast(bf16x8, *(const lds_u32x4*)(wl + ((16 * ct + col) * kKp + 32 * s + 8 * grp)));
+    // this lane's k' offset into the staged rows per k-step: row kh, element j0 of the pixel's run
+    int koff[6];
+#pragma unroll
+    for (int s = 0; s < 6; ++s) {
+        const int kp0 = 32 * s + 8 * grp;
+        koff[s] = (kp0 / 24) * kInRow + kp0 % 24;
+    }
+
+    for (; t < g.tasks; t += gridDim.x) {
+        int n, oh, ow0;
+        task_coords(g, t, n, oh, ow0);
+        const int count = g.Wo - ow0 < kSeg ? g.Wo - ow0 : kSeg;
+        __syncthreads();  // the previous task's reads of in / out are done
+        store_rows(st, in);
+        __syncthreads();
+        if (t + static_cast<int>(gridDim.x) < g.tasks) load_rows(st, x, g, t + gridDim.x);  // in flight meanwhile
+#pragma unroll
+        for (int pi = 0; pi < 2; ++pi) {
+            const int pt = wave + 4 * pi;  // pixel tile (wave-uniform)
+            if (16 * pt >= count) break;
+            const int px = 16 * pt + col;
+            f32x4v acc[4];
+#pragma unroll
+            for (int ct = 0; ct < 4; ++ct) acc[ct] = f32x4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int s = 0; s < 6; ++s) {
+                const lds_u32* p = (const lds_u32*)(in + (koff[s] + 6 * px));  // 4-byte aligned
+                const u32x4 v = {p[0], p[1], p[2], p[3]};
+                const bf16x8 b = __builtin_bit_cast(bf16x8, v);
+#pragma unroll
+                for (int ct = 0; ct < 4; ++ct) acc[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[ct][s], b, acc[ct], 0, 0, 0);
+            }
+            // D[co = 16 ct + 4 grp + i][px = col] -> bf16 (round to nearest even), 8 bytes per lane
+#pragma unroll
+            for (int ct = 0; ct < 4; ++ct) {
+                v4s o;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) o[i] = __bfloat16_as_short(__float2bfloat16(acc[ct][i]));
+                *(lds_v4s*)(out + (px * kOutRow + 16 * ct + 4 * grp)) = o;
+            }
+        }
+        __syncthreads();
+        // the segment's [count][64] bf16 rows are contiguous in y: 16-byte stores
+        unsigned short* yrow = y + (static_cast<int64_t>(n * g.Ho + oh) * g.Wo + ow0) * 64;
+#pragma unroll
+        for (int u = 0; u < kSeg * 8 / kThreads; ++u) {
+            const int q = tid + kThreads * u, p = q >> 3, v = q & 7;
+            if (p < count)
+                *reinterpret_cast<u32x4*>(yrow + (p * 64 + 8 * v)) = *(const lds_u32x4*)(out + (p * kOutRow + 8 * v));
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// weight gradient
+
+__device__ __forceinline__ v4s tr_at(const lds_short* p) { return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)p); }
+
+// this thread's 4 16-byte vectors of task t's dy tile [128 px][64 co] (bit u of the result: vector u
+// lies before the row's end; the others are stored as zeros)
+__device__ __forceinline__ unsigned load_dy(u32x4 (&d)[4], const unsigned short* __restrict__ dy, const StemGeom& g,
+                                            int t) {
+    int n, oh, ow0;
+    task_coords(g, t, n, oh, ow0);
+    const int count = g.Wo - ow0 < kSeg ? g.Wo - ow0 : kSeg;
+    const unsigned short* row = dy + (static_cast<int64_t>(n * g.Ho + oh) * g.Wo + ow0) * 64;
+    unsigned okm = 0u;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int q = threadIdx.x + kThreads * u, p = q >> 3, v = q & 7;
+        const bool ok = p < count;
+        d[u] = *reinterpret_cast<const u32x4*>(row + ((ok ? p : 0) * 64 + 8 * v));
+        okm |= ok ? (1u << u) : 0u;
+    }
+    return okm;
+}
+
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) void stem_wgrad_kernel(const unsigned short* __restrict__ x,
+                                                              const unsigned short* __restrict__ dy, StemGeom g,
+                                                              float* __restrict__ slabs) {
+    __shared__ short in_s[kInElems];
+    __shared__ short dy_s[kSeg * kDyRow];
+    lds_short* in = (lds_short*)in_s;
+    lds_short* dyl = (lds_short*)dy_s;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int grp = lane >> 4, col = lane & 15;
+
+    // pixel order of a k-step (any order sums the same products): lane group grp's 8 values are
+    // pixels 4 grp + 0..3 (transposing read h = 0) and 16 + 4 grp + 0..3 (h = 1)
+    int aoff[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) aoff[h] = (16 * h + 4 * grp + ((lane & 15) >> 2)) * kDyRow + 4 * (lane & 3);
+    // this wave's k' tiles nt = wave, wave + 4, wave + 8 (< 11: k' < 176 covers kh <= 6), lane column k'
+    int boff[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const int kp = 16 * (wave + 4 * i) + col;
+        boff[i] = (kp / 24) * kInRow + kp % 24 + 6 * 4 * grp;
+    }
+    const int ntiles = wave + 8 < 11 ? 3 : 2;
+
+    f32x4v acc[4][3];
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct)
+#pragma unroll
+        for (int i = 0; i < 3; ++i) acc[ct][i] = f32x4v{0.f, 0.f, 0.f, 0.f};
+
+    int t = blockIdx.x;
+    RowStage st;
+    u32x4 d[4];
+    unsigned dm = 0u;
+    if (t < g.tasks) {
+        load_rows(st, x, g, t);
+        dm = load_dy(d, dy, g, t);
+    }
+    for (; t < g.tasks; t += gridDim.x) {
+        int n, oh, ow0;
+        task_coords(g, t, n, oh, ow0);
+        const int count = g.Wo - ow0 < kSeg ? g.Wo - ow0 : kSeg;
+        __syncthreads();
+        store_rows(st, in);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int q = tid + kThreads * u;
+            const unsigned m = ((dm >> u) & 1u) ? ~0u : 0u;
+            *(lds_u32x4*)(dyl + ((q >> 3) * kDyRow + 8 * (q & 7))) = u32x4{d[u][0] & m, d[u][1] & m, d[u][2] & m, d[u][3] & m};
+        }
+        __syncthreads();
+        if (t + static_cast<int>(gridDim.x) < g.tasks) {
+            load_rows(st, x, g, t + gridDim.x);
+            dm = load_dy(d, dy, g, t + gridDim.x);
+        }
+        for (int s = 0; 32 * s < count; ++s) {
+            bf16x8 fa[4];
+#pragma unroll
+            for (int ct = 0; ct < 4; ++ct) {
+                const v4s f2[2] = {tr_at(dyl + (aoff[0] + 32 * s * kDyRow + 16 * ct)),
+                                   tr_at(dyl + (aoff[1] + 32 * s * kDyRow + 16 * ct))};
+                fa[ct] = *reinterpret_cast<const bf16x8*>(f2);
+            }
+#pragma unroll
+            for (int i = 0; i < 3; ++i) {
+                if (i == 2 && ntiles == 2) break;
+                // B[px][k']: pixels 32 s + {4 grp + 0..3, 16 + 4 grp + 0..3}, 6 elements apart
+                const lds_short* p = in + (boff[i] + 6 * 32 * s);
+                s16x8 b;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    b[j] = p[6 * j];
+                    b[4 + j] = p[6 * (16 + j)];
+                }
+                const bf16x8 fb = __builtin_bit_cast(bf16x8, b);
+#pragma unroll
+                for (int ct = 0; ct < 4; ++ct)
+                    acc[ct][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[ct], fb, acc[ct][i], 0, 0, 0);
+            }
+        }
+    }
+    // D[co = 16 ct + 4 grp + e][k' = 16 nt + col] -> this workgroup's slab [co][kh][kw][ci]
+    float* slab = slabs + static_cast<int64_t>(blockIdx.x) * kWElems;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        if (i == 2 && ntiles == 2) break;
+        const int kp = 16 * (wave + 4 * i) + col;
+        const int kh = kp / 24, j = kp - kh * 24;
+        if (kh < 7 && j < 21) {
+#pragma unroll
+            for (int ct = 0; ct < 4; ++ct)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) slab[(16 * ct + 4 * grp + e) * 147 + kh * 21 + j] = acc[ct][i][e];
+        }
+    }
+}
+
+bool stem_geom(int64_t N, int H, int W, int Ho, int Wo, StemGeom& g) {
+    if (N < 1 || H < 1 || W < 1 || Ho != (H - 1) / 2 + 1 || Wo != (W - 1) / 2 + 1) return false;
+    // 32-bit element offsets: N * H * W * 3 and N * Ho * Wo * 64 (+ a segment) < 2^31
+    if (N * H * int64_t(W) * 3 >= (int64_t(1) << 31) || (N * Ho * int64_t(Wo) + kSeg) * 64 >= (int64_t(1) << 31))
+        return false;
+    g.N = static_cast<int>(N);
+    g.H = H;
+    g.W = W;
+    g.Ho = Ho;
+    g.Wo = Wo;
+    g.segs = (Wo + kSeg - 1) / kSeg;
+    const int64_t tasks = N * Ho * int64_t(g.segs);
+    if (tasks >= (int64_t(1) << 31)) return false;
+    g.tasks = static_cast<int>(tasks);
+    return true;
+}
+
+// persistent grids: 2 workgroups per CU (forward: LDS 54 KB; wgrad: 33 KB)
+constexpr int kFwdGrid = 512;
+constexpr int kWgradGrid = 512;
+
+}  // namespace
+}  // namespace dauc
+
+using namespace dauc;
+
+extern "C" {
+
+int dauc_conv7x7s2_stem_forward(const void* x, const void* w, int dtype, int64_t N, int H, int W, int Ho, int Wo,
+                                void* y, dauc_stream_t stream) {
+    if (x == nullptr || w == nullptr || y == nullptr || dtype != DAUC_DTYPE_BF16) return DAUC_EINVAL;
+    if ((reinterpret_cast<uintptr_t>(y) & 15u) || (reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(w)) & 1u)
+        return DAUC_EINVAL;
+    StemGeom g;
+    if (!stem_geom(N, H, W, Ho, Wo, g)) return DAUC_EINVAL;
+    const int grid = g.tasks < kFwdGrid ? g.tasks : kFwdGrid;
+    hipLaunchKernelGGL(stem_fwd_kernel, dim3(grid), dim3(kThreads), 0, as_hip(stream),
+                       static_cast<const unsigned short*>(x), static_cast<const unsigned short*>(w), g,
+                       static_cast<unsigned short*>(y));
+    return launch_status();
+}
+
+size_t dauc_conv7x7s2_stem_wgrad_workspace_size(int64_t N, int Ho, int Wo) {
+    if (N < 1 || Ho < 1 || Wo < 1) return 0;
+    const int64_t tasks = N * Ho * ((Wo + kSeg - 1) / kSeg);
+    const int64_t grid = tasks < kWgradGrid ? tasks : kWgradGrid;
+    return grid > 1 ? size_t(grid) * kWElems * sizeof(float) : 0;
+}
+
+int dauc_conv7x7s2_stem_wgrad(const void* x, const void* dy, int dtype, int64_t N, int H, int W, int Ho, int Wo,
+                              float* dw, void* workspace, size_t workspace_bytes, dauc_stream_t stream) {
+    if (x == nullptr || dy == nullptr || dw == nullptr || dtype != DAUC_DTYPE_BF16) return DAUC_EINVAL;
+    if ((reinterpret_cast<uintptr_t>(dy) | reinterpret_cast<uintptr_t>(dw)) & 15u || (reinterpret_cast<uintptr_t>(x) & 1u))
+        return DAUC_EINVAL;
+    StemGeom g;
+    if (!stem_geom(N, H, W, Ho, Wo, g)) return DAUC_EINVAL;
+    const int grid = g.tasks < kWgradGrid ? g.tasks : kWgradGrid;
+    const size_t need = dauc_conv7x7s2_stem_wgrad_workspace_size(N, Ho, Wo);
+    if (need && (workspace == nullptr || workspace_bytes < need || (reinterpret_cast<uintptr_t>(workspace) & 15u)))
+        return DAUC_EINVAL;
+    float* target = grid > 1 ? static_cast<float*>(workspace) : dw;
+    hipLaunchKernelGGL(stem_wgrad_kernel, dim3(grid), dim3(kThreads), 0, as_hip(stream),
+                       static_cast<const unsigned short*>(x), static_cast<const unsigned short*>(dy), g, target);
+    const int rc = launch_status();
+    if (rc != DAUC_OK || grid == 1) return rc;
+    return dauc_slab_sum(target, grid, kWElems, dw, stream);
+}
+
+}  // extern "C"

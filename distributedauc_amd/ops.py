@@ -638,6 +638,67 @@ def conv3x3_wgrad_supported(x: torch.Tensor, dy: torch.Tensor, stride, padding, 
             and x.shape[0] * x.shape[2] * x.shape[3] < 2 ** 31)
 
 
+def _stem_shapes(x: torch.Tensor):
+    _require(x, "x", torch.bfloat16)
+    if x.dim() != 4 or x.shape[1] != 3 or not x.is_contiguous(memory_format=torch.channels_last):
+        raise ValueError(f"x must be a channels-last [N, 3, H, W] bf16 tensor, got {tuple(x.shape)}")
+    N, _, H, W = x.shape
+    return N, H, W, (H - 1) // 2 + 1, (W - 1) // 2 + 1
+
+
+def stem_conv_forward(x: torch.Tensor, weight: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """conv2d(x, weight, stride=2, padding=3) for the 7x7 stem (resnet.py:145) on channels-last bf16
+    (dauc_conv7x7s2_stem_forward): x [N, 3, H, W], weight [64, 3, 7, 7] bf16 in channels-last
+    memory order; returns a channels-last bf16 [N, 64, Ho, Wo]."""
+    N, H, W, Ho, Wo = _stem_shapes(x)
+    _require(weight, "weight", torch.bfloat16, x.device)
+    if tuple(weight.shape) != (64, 3, 7, 7) or not weight.is_contiguous(memory_format=torch.channels_last):
+        raise ValueError("weight must be a channels-last bf16 [64, 3, 7, 7] tensor")
+    if out is None:
+        out = torch.empty((N, 64, Ho, Wo), dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
+    elif (out.dtype != torch.bfloat16 or tuple(out.shape) != (N, 64, Ho, Wo)
+          or not out.is_contiguous(memory_format=torch.channels_last)):
+        raise ValueError("out must be a channels-last bf16 [N, 64, Ho, Wo] tensor")
+    check(_lib.load().dauc_conv7x7s2_stem_forward(_ptr(x), _ptr(weight), _lib.DTYPE_BF16, N, H, W, Ho, Wo, _ptr(out),
+                                                  _stream(x.device)), "dauc_conv7x7s2_stem_forward")
+    return out
+
+
+def stem_conv_wgrad(x: torch.Tensor, dy: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """The fp32 weight gradient of the 7x7 / stride-2 / pad-3 stem from its channels-last bf16 input
+    x [N, 3, H, W] and output gradient dy [N, 64, Ho, Wo] (dauc_conv7x7s2_stem_wgrad): a [64, 3, 7, 7]
+    fp32 tensor in channels-last memory order (the backbone's parameter layout)."""
+    N, H, W, Ho, Wo = _stem_shapes(x)
+    _require(dy, "dy", torch.bfloat16, x.device)
+    if tuple(dy.shape) != (N, 64, Ho, Wo) or not dy.is_contiguous(memory_format=torch.channels_last):
+        raise ValueError(f"dy must be a channels-last bf16 [{N}, 64, {Ho}, {Wo}] tensor, got {tuple(dy.shape)}")
+    dev = x.device
+    if out is None:
+        out = torch.empty((64, 3, 7, 7), dtype=torch.float32, device=dev, memory_format=torch.channels_last)
+    elif (out.dtype != torch.float32 or tuple(out.shape) != (64, 3, 7, 7)
+          or not out.is_contiguous(memory_format=torch.channels_last)):
+        raise ValueError("out must be a channels-last fp32 [64, 3, 7, 7] tensor")
+    L = _lib.load()
+    nbytes = L.dauc_conv7x7s2_stem_wgrad_workspace_size(N, Ho, Wo)
+    ws = workspaces.get(dev, "wgrad_stem", nbytes) if nbytes else None
+    check(L.dauc_conv7x7s2_stem_wgrad(_ptr(x), _ptr(dy), _lib.DTYPE_BF16, N, H, W, Ho, Wo, _ptr(out), _ptr(ws),
+                                      0 if ws is None else ws.numel(), _stream(dev)), "dauc_conv7x7s2_stem_wgrad")
+    return out
+
+
+def stem_conv_supported(x: torch.Tensor, weight: torch.Tensor, stride, padding, dilation, groups) -> bool:
+    """The convolutions dauc_conv7x7s2_stem_* take: the ResNet stem on a channels-last bf16 image."""
+    s = tuple(stride) if isinstance(stride, (tuple, list)) else (stride, stride)
+    p = tuple(padding) if isinstance(padding, (tuple, list)) else (padding, padding)
+    d = tuple(dilation) if isinstance(dilation, (tuple, list)) else (dilation, dilation)
+    if not (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4 and x.shape[1] == 3 and groups == 1
+            and tuple(weight.shape) == (64, 3, 7, 7) and s == (2, 2) and p == (3, 3) and d == (1, 1)
+            and x.is_contiguous(memory_format=torch.channels_last)):
+        return False
+    N, _, H, W = x.shape
+    return N * H * W * 3 < 2 ** 31 and (N * ((H - 1) // 2 + 1) * ((W - 1) // 2 + 1) + 128) * 64 < 2 ** 31
+
+
 def set_wgrad_form(form: int) -> None:
     """The tuning build's 3x3 weight-gradient form (dauc_set_wgrad_form): 0 automatic, 1 gather, 2 / 3 window with 64- / 128-pixel chunks."""
     check(_lib.tuning().dauc_set_wgrad_form(int(form)), "dauc_set_wgrad_form")
@@ -668,7 +729,8 @@ __all__ = [
     "pd_update_dense", "coda_finalize", "scale_div", "split_scores", "pair_count", "auc_counts_sorted",
     "surrogate_logits_fwdbwd", "class_sums_logits", "surrogate_status",
     "sort_keys", "auc_counts_sorted_labeled", "compact_positives", "mode_code", "workspaces", "set_search_mode",
-    "set_direct_fault", "conv3x3_wgrad", "conv3x3_wgrad_supported",
+    "set_direct_fault", "conv3x3_wgrad", "conv3x3_wgrad_supported", "stem_conv_forward", "stem_conv_wgrad",
+    "stem_conv_supported",
     "auc_eval_enqueue",
     "auc_slot_bytes",
     "auc_eval_compact_part",

@@ -426,6 +426,25 @@ size_t dauc_conv3x3_wgrad_workspace_size(int64_t N, int Ho, int Wo, int Ci, int 
 int dauc_conv3x3_wgrad(const void* x, const void* dy, int dtype, int64_t N, int H, int W, int Ci, int Ho, int Wo,
                        int Co, int stride, float* dw, void* workspace, size_t workspace_bytes, dauc_stream_t stream);
 
+/* ---------------------------------- backbone: the 7x7 / stride-2 stem convolution */
+
+/*
+ * The stem convolution conv1 = Conv2d(3, 64, 7, stride 2, padding 3, no bias) (imagenet/resnet.py:145)
+ * on channels-last bf16 (dtype DAUC_DTYPE_BF16 only): x [N, H, W, 3], weight [64][7][7][3] (the
+ * channels-last memory order of [64, 3, 7, 7]), y / dy [N, Ho, Wo, 64] with Ho = (H - 1) / 2 + 1,
+ * Wo = (W - 1) / 2 + 1; y and dy 16-byte aligned, N*H*W*3 and N*Ho*Wo*64 < 2^31. MFMA with fp32
+ * accumulation: forward y = bf16(sum) rounded once; weight gradient dw (fp32, [64][7][7][3])
+ * through per-workgroup slabs in `workspace` (dauc_conv7x7s2_stem_wgrad_workspace_size bytes)
+ * summed in workgroup order (dauc_slab_sum): bitwise reproducible. Replaces MIOpen's forward and
+ * backward-weights calls for the stem under bf16 autocast (main.py:311-326) and autograd's
+ * bf16 -> fp32 cast of the gradient. The stem's input gradient is never needed (the image).
+ */
+int dauc_conv7x7s2_stem_forward(const void* x, const void* w, int dtype, int64_t N, int H, int W, int Ho, int Wo,
+                                void* y, dauc_stream_t stream);
+size_t dauc_conv7x7s2_stem_wgrad_workspace_size(int64_t N, int Ho, int Wo);
+int dauc_conv7x7s2_stem_wgrad(const void* x, const void* dy, int dtype, int64_t N, int H, int W, int Ho, int Wo,
+                              float* dw, void* workspace, size_t workspace_bytes, dauc_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

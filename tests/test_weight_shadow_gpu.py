@@ -121,10 +121,11 @@ def test_dgrad_as_forward_conv(dev, shape):
 
 
 def test_weight_shadow_dgrad_fwd_step_close(dev):
-    """The whole ResNet-50 step with dgrad_fwd against torch's backward-data, both against the fp32
-    step (no autocast): the forward is untouched (scores identical) and every gradient is as close
-    to fp32 as torch's bf16 step is (bf16 rounding differences propagate through 50 layers, so
-    the two bf16 steps differ from each other by about as much as each differs from fp32)."""
+    """The whole ResNet-50 step with the HIP convolution paths (dgrad_fwd, the 3x3 weight gradients,
+    the 7x7 stem's forward and weight gradient) against torch's, both against the fp32 step (no
+    autocast): scores and every gradient are as close to fp32 as torch's bf16 step is (bf16
+    rounding differences propagate through 50 layers, so the two bf16 steps differ from each other
+    by about as much as each differs from fp32)."""
     det = torch.backends.cudnn.deterministic
     torch.backends.cudnn.deterministic = True
     try:
@@ -133,7 +134,8 @@ def test_weight_shadow_dgrad_fwd_step_close(dev):
         b = _run(dev, "resnet50", True, 64, dgrad_fwd=True)
     finally:
         torch.backends.cudnn.deterministic = det
-    assert torch.equal(_bits(a[0]), _bits(b[0]))
+    sa, sb = float((a[0].float() - ref[0].float()).abs().max()), float((b[0].float() - ref[0].float()).abs().max())
+    assert sb <= 2.0 * sa + 1e-2, (sb, sa)
     ea, eb = [], []
     for g32, ga, gb in zip(ref[1], a[1], b[1]):
         scale = float(g32.abs().max().clamp_min(1e-30))
