@@ -12,7 +12,7 @@
 // (kw, ci) are CONTIGUOUS in x: x[n][2oh - 3 + kh][2ow - 3 + kw][ci] = row_kh[6 ow + 3 kw + ci]
 // of the staged input row. So the reduction index is k' = 24 kh + j (j = 3 kw + ci < 21; 21..23
 // and kh = 7 carry zero weights): K' = 192 = 6 MFMA k-steps, and a lane's 8 consecutive k' of one
-// pixel are 8 consecutive bf16 of one staged row (4-byte aligned: 12 ow bytes).
+// pixel are 8 consecutive bf16 of one staged row (read as 5 aligned words and realigned).
 //
 // A task is one output row segment (n, oh, ow0 .. ow0 + 127): its 7 input rows (+ a zero row)
 // are staged into LDS (zeros outside the image), then
@@ -48,7 +48,8 @@ constexpr int kSeg = 128;                 // output pixels per task
 constexpr int kInRow = 800;               // staged input row, bf16 elements (>= 3 * (2 * 127 + 7) = 783 and
                                           // >= 6 * 127 + 23 + 1 read by the last pixel's last k-step)
 constexpr int kInElems = 8 * kInRow;      // 7 kernel rows + a zero row
-constexpr int kInPer = kInElems / kThreads;  // 25 staged elements per thread
+constexpr int kChunks = kInElems / 8;    // 16-byte chunks per staged task (100 per row)
+constexpr int kChunkPer = (kChunks + kThreads - 1) / kThreads;  // 4 per thread
 constexpr int kKp = 192;                  // padded reduction length of the forward
 constexpr int kOutRow = 72;               // forward output tile row (64 channels + 8)
 constexpr int kDyRow = 80;                // wgrad dy tile row (64 channels + 16: conflict-free transposing reads)
@@ -68,49 +69,61 @@ __device__ __forceinline__ void task_coords(const StemGeom& g, int t, int& n, in
     oh = row - n * g.Ho;
 }
 
-// this thread's 25 elements of task t's staged rows: element i = tid + 256 u of the [8][kInRow] image.
-// Each element arrives as the aligned 4-byte word that holds it (a word holding a valid element
-// cannot leave the allocation); which half it is and whether it lies in the image go to bit masks
-// applied when the values are stored to LDS. Any select, zero-extension or packing of the loaded
-// values here would make the wave wait for the loads now instead of across the current task's MFMAs.
+// Staged row kh holds input row ih = 2 oh - 3 + kh from the 16-byte-aligned chunk at or below the
+// run's first element g0 = (n H + ih) 3W + 3 (2 ow0 - 3): position p of the LDS row is element
+// (g0 & ~7) + p of x, so the run starts at position sh(kh) = g0 & 7 and every chunk lands whole
+// (one 16-byte load, one 16-byte LDS store; x 16-byte aligned). Elements outside the image row are
+// zeroed at the store. A chunk holding a valid element cannot leave x's allocation (an aligned
+// 16-byte block around a valid byte); a chunk with none is not used (its load reads chunk 0).
+__device__ __forceinline__ int row_shift(const StemGeom& g, int n, int oh, int ow0, int kh) {
+    return ((n * g.H + 2 * oh - 3 + kh) * 3 * g.W + 3 * (2 * ow0 - 3)) & 7;
+}
+
 struct RowStage {
-    unsigned r[kInPer];
-    unsigned ok, hi;  // bit u: element u is in the image / is the upper half of its word
+    u32x4 c[kChunkPer];
+    unsigned lohi;  // per chunk u, bits 8u .. 8u + 7: the valid element range [lo, hi) (4 bits each)
 };
 
+// this thread's chunks u: chunk index q = tid + 256 u of the task's [8 rows][100 chunks]. The loads
+// are unconditional and their validity goes to `lohi`, applied when the chunks are stored to LDS: a
+// select right after a load would make the wave wait for it here instead of across the MFMAs.
 __device__ __forceinline__ void load_rows(RowStage& st, const unsigned short* __restrict__ x, const StemGeom& g,
                                           int t) {
     int n, oh, ow0;
     task_coords(g, t, n, oh, ow0);
-    const int c0 = 3 * (2 * ow0 - 3);  // element of the row where the staged run starts
     const int rowlen = 3 * g.W;
-    const unsigned* xw = reinterpret_cast<const unsigned*>(x);
-    unsigned okm = 0u, him = 0u;
+    unsigned lohi = 0u;
 #pragma unroll
-    for (int u = 0; u < kInPer; ++u) {
-        // i = tid + 256 u lies in staged row klo or klo + 1 (compile-time bounds: no division)
-        const int i = threadIdx.x + kThreads * u;
-        const int klo = (kThreads * u) / kInRow;
-        const int kh = klo + (i >= kInRow * (klo + 1) ? 1 : 0);
-        const int e = i - kInRow * kh;
+    for (int u = 0; u < kChunkPer; ++u) {
+        const int q = threadIdx.x + kThreads * u;
+        const int kh = q / (kInRow / 8), k = q - kh * (kInRow / 8);
         const int ih = 2 * oh - 3 + kh;
-        const int col = c0 + e;  // the run of a row is contiguous in x: (iw, ci) -> 3 iw + ci
-        const bool ok = (kh < 7) & (ih >= 0) & (ih < g.H) & (col >= 0) & (col < rowlen);
-        const int ihc = min(max(ih, 0), g.H - 1);
-        const int q = (n * g.H + ihc) * rowlen + min(max(col, 0), rowlen - 1);
-        st.r[u] = xw[q >> 1];
-        okm |= ok ? (1u << u) : 0u;
-        him |= static_cast<unsigned>(q & 1) << u;
+        const int rs = (n * g.H + ih) * rowlen;                      // element of (n, ih, 0, 0)
+        const int cb = ((rs + 3 * (2 * ow0 - 3)) & ~7) + 8 * k;        // this chunk's first element
+        const bool row_ok = (q < kChunks) & (kh < 7) & (ih >= 0) & (ih < g.H);
+        const int lo = min(max(rs - cb, 0), 8), hi = min(max(rs + rowlen - cb, 0), 8);
+        const bool any = row_ok & (lo < hi);
+        st.c[u] = *reinterpret_cast<const u32x4*>(x + (any ? cb : 0));
+        lohi |= static_cast<unsigned>(any ? (lo | (hi << 4)) : 0) << (8 * u);
     }
-    st.ok = okm;
-    st.hi = him;
+    st.lohi = lohi;
 }
 
 __device__ __forceinline__ void store_rows(const RowStage& st, lds_short* in) {
 #pragma unroll
-    for (int u = 0; u < kInPer; ++u) {
-        const unsigned v = (st.r[u] >> (((st.hi >> u) & 1u) * 16)) & 0xffffu;
-        in[threadIdx.x + kThreads * u] = static_cast<short>(((st.ok >> u) & 1u) ? v : 0u);
+    for (int u = 0; u < kChunkPer; ++u) {
+        const int q = threadIdx.x + kThreads * u;
+        if (q >= kChunks) break;
+        const int lo = (st.lohi >> (8 * u)) & 15, hi = (st.lohi >> (8 * u + 4)) & 15;
+        u32x4 v;
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+            const unsigned m = (((2 * d >= lo) & (2 * d < hi)) ? 0x0000ffffu : 0u) |
+                               (((2 * d + 1 >= lo) & (2 * d + 1 < hi)) ? 0xffff0000u : 0u);
+            v[d] = st.c[u][d] & m;
+        }
+        const int kh = q / (kInRow / 8), k = q - kh * (kInRow / 8);
+        *(lds_u32x4*)(in + (kh * kInRow + 8 * k)) = v;
     }
 }
 
@@ -147,6 +160,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
         for (int s = 0; s < 6; ++s)
             wa[ct][s] = __builtin_bit_cast(bf16x8, *(const lds_u32x4*)(wl + ((16 * ct + col) * kKp + 32 * s + 8 * grp)));
     // this lane's k' offset into the staged rows per k-step: row kh, element j0 of the pixel's run
+    // (+ the row's shift, per task)
     int koff[6];
 #pragma unroll
     for (int s = 0; s < 6; ++s) {
@@ -158,6 +172,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
         int n, oh, ow0;
         task_coords(g, t, n, oh, ow0);
         const int count = g.Wo - ow0 < kSeg ? g.Wo - ow0 : kSeg;
+        int kofs[6];
+#pragma unroll
+        for (int s = 0; s < 6; ++s) kofs[s] = koff[s] + row_shift(g, n, oh, ow0, (32 * s + 8 * grp) / 24);
         __syncthreads();  // the previous task's reads of in / out are done
         store_rows(st, in);
         __syncthreads();
@@ -172,8 +189,13 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
             for (int ct = 0; ct < 4; ++ct) acc[ct] = f32x4v{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int s = 0; s < 6; ++s) {
-                const lds_u32* p = (const lds_u32*)(in + (koff[s] + 6 * px));  // 4-byte aligned
-                const u32x4 v = {p[0], p[1], p[2], p[3]};
+                // 8 bf16 at any 2-byte offset: 5 aligned words, realigned by 0 or 2 bytes
+                const int e = kofs[s] + 6 * px;
+                const lds_u32* p = (const lds_u32*)(in + (e & ~1));
+                const unsigned sb = (e & 1) * 16;
+                const unsigned w0 = p[0], w1 = p[1], w2 = p[2], w3 = p[3], w4 = p[4];
+                const u32x4 v = {__builtin_amdgcn_alignbit(w1, w0, sb), __builtin_amdgcn_alignbit(w2, w1, sb),
+                                 __builtin_amdgcn_alignbit(w3, w2, sb), __builtin_amdgcn_alignbit(w4, w3, sb)};
                 const bf16x8 b = __builtin_bit_cast(bf16x8, v);
 #pragma unroll
                 for (int ct = 0; ct < 4; ++ct) acc[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[ct][s], b, acc[ct], 0, 0, 0);
@@ -265,6 +287,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
         int n, oh, ow0;
         task_coords(g, t, n, oh, ow0);
         const int count = g.Wo - ow0 < kSeg ? g.Wo - ow0 : kSeg;
+        int bofs[3];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) bofs[i] = boff[i] + row_shift(g, n, oh, ow0, (16 * (wave + 4 * i) + col) / 24);
         __syncthreads();
         store_rows(st, in);
 #pragma unroll
@@ -290,7 +315,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
             for (int i = 0; i < 3; ++i) {
                 if (i == 2 && ntiles == 2) break;
                 // B[px][k']: pixels 32 s + {4 grp + 0..3, 16 + 4 grp + 0..3}, 6 elements apart
-                const lds_short* p = in + (boff[i] + 6 * 32 * s);
+                const lds_short* p = in + (bofs[i] + 6 * 32 * s);
                 s16x8 b;
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
@@ -337,9 +362,9 @@ bool stem_geom(int64_t N, int H, int W, int Ho, int Wo, StemGeom& g) {
     return true;
 }
 
-// persistent grids: 2 workgroups per CU (forward: LDS 54 KB; wgrad: 33 KB)
+// persistent grids: workgroups per CU as registers allow (forward 196 VGPRs: 2; wgrad 155: 3)
 constexpr int kFwdGrid = 512;
-constexpr int kWgradGrid = 512;
+constexpr int kWgradGrid = 768;
 
 }  // namespace
 }  // namespace dauc
@@ -351,7 +376,7 @@ extern "C" {
 int dauc_conv7x7s2_stem_forward(const void* x, const void* w, int dtype, int64_t N, int H, int W, int Ho, int Wo,
                                 void* y, dauc_stream_t stream) {
     if (x == nullptr || w == nullptr || y == nullptr || dtype != DAUC_DTYPE_BF16) return DAUC_EINVAL;
-    if ((reinterpret_cast<uintptr_t>(y) & 15u) || (reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(w)) & 1u)
+    if (((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y)) & 15u) || (reinterpret_cast<uintptr_t>(w) & 1u))
         return DAUC_EINVAL;
     StemGeom g;
     if (!stem_geom(N, H, W, Ho, Wo, g)) return DAUC_EINVAL;
@@ -372,7 +397,7 @@ size_t dauc_conv7x7s2_stem_wgrad_workspace_size(int64_t N, int Ho, int Wo) {
 int dauc_conv7x7s2_stem_wgrad(const void* x, const void* dy, int dtype, int64_t N, int H, int W, int Ho, int Wo,
                               float* dw, void* workspace, size_t workspace_bytes, dauc_stream_t stream) {
     if (x == nullptr || dy == nullptr || dw == nullptr || dtype != DAUC_DTYPE_BF16) return DAUC_EINVAL;
-    if ((reinterpret_cast<uintptr_t>(dy) | reinterpret_cast<uintptr_t>(dw)) & 15u || (reinterpret_cast<uintptr_t>(x) & 1u))
+    if ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(dy) | reinterpret_cast<uintptr_t>(dw)) & 15u)
         return DAUC_EINVAL;
     StemGeom g;
     if (!stem_geom(N, H, W, Ho, Wo, g)) return DAUC_EINVAL;

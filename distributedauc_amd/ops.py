@@ -642,6 +642,8 @@ def _stem_shapes(x: torch.Tensor):
     _require(x, "x", torch.bfloat16)
     if x.dim() != 4 or x.shape[1] != 3 or not x.is_contiguous(memory_format=torch.channels_last):
         raise ValueError(f"x must be a channels-last [N, 3, H, W] bf16 tensor, got {tuple(x.shape)}")
+    if x.data_ptr() % 16:
+        raise ValueError("x must be 16-byte aligned")
     N, _, H, W = x.shape
     return N, H, W, (H - 1) // 2 + 1, (W - 1) // 2 + 1
 
@@ -696,7 +698,8 @@ def stem_conv_supported(x: torch.Tensor, weight: torch.Tensor, stride, padding, 
             and x.is_contiguous(memory_format=torch.channels_last)):
         return False
     N, _, H, W = x.shape
-    return N * H * W * 3 < 2 ** 31 and (N * ((H - 1) // 2 + 1) * ((W - 1) // 2 + 1) + 128) * 64 < 2 ** 31
+    return (x.data_ptr() % 16 == 0 and N * H * W * 3 < 2 ** 31
+            and (N * ((H - 1) // 2 + 1) * ((W - 1) // 2 + 1) + 128) * 64 < 2 ** 31)
 
 
 def set_wgrad_form(form: int) -> None:

@@ -432,7 +432,7 @@ int dauc_conv3x3_wgrad(const void* x, const void* dy, int dtype, int64_t N, int 
  * The stem convolution conv1 = Conv2d(3, 64, 7, stride 2, padding 3, no bias) (imagenet/resnet.py:145)
  * on channels-last bf16 (dtype DAUC_DTYPE_BF16 only): x [N, H, W, 3], weight [64][7][7][3] (the
  * channels-last memory order of [64, 3, 7, 7]), y / dy [N, Ho, Wo, 64] with Ho = (H - 1) / 2 + 1,
- * Wo = (W - 1) / 2 + 1; y and dy 16-byte aligned, N*H*W*3 and N*Ho*Wo*64 < 2^31. MFMA with fp32
+ * Wo = (W - 1) / 2 + 1; x, y and dy 16-byte aligned, N*H*W*3 and N*Ho*Wo*64 < 2^31. MFMA with fp32
  * accumulation: forward y = bf16(sum) rounded once; weight gradient dw (fp32, [64][7][7][3])
  * through per-workgroup slabs in `workspace` (dauc_conv7x7s2_stem_wgrad_workspace_size bytes)
  * summed in workgroup order (dauc_slab_sum): bitwise reproducible. Replaces MIOpen's forward and
