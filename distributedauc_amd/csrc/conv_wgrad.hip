@@ -226,36 +226,43 @@ struct WinStaging {
 };
 
 // 32-bit element offsets throughout (host: N * H * W * Ci and N * Ho * Wo * Co < 2^31): 64-bit
-// address arithmetic per load was most of the loop's VALU work
+// address arithmetic per load was most of the loop's VALU work. What does not change from chunk to
+// chunk is decoded once per thread (apk / wpos); per chunk one division finds the chunk's first
+// output row (n0, ho0), and each vector's row follows by at most a few wrap steps, not a division.
 template <int NV, int KS>
 __device__ __forceinline__ void load_win(WinStaging<NV, KS>& s, const __hip_bfloat16* __restrict__ x,
                                          const __hip_bfloat16* __restrict__ dy, const WinGeom& g, int chunk,
-                                         const int (&wpos)[kMaxWinVec], int pr, int v, int co0, int ci0) {
+                                         const int (&apk)[KS / 2], const int (&wpos)[kMaxWinVec], int v, int co0,
+                                         int ci0) {
     const int gr0 = chunk * g.R;
     const int GR = static_cast<int>(g.GR);
+    const int n0 = gr0 / g.Ho, ho0 = gr0 - n0 * g.Ho;
     s.ok = 0u;
 #pragma unroll
-    for (int i = 0; i < KS / 2; ++i) {  // dy: pixels k = pr + 64 i of the chunk
-        const int k = pr + 64 * i;
-        const int rr = k / g.Wo, wo = k - rr * g.Wo;
+    for (int i = 0; i < KS / 2; ++i) {  // dy: pixel k = pr + 64 i of the chunk (rr | wo << 8, bit 31: k < KP)
+        const int rr = apk[i] & 0xff, wo = (apk[i] >> 8) & 0x7fffff;
         const int gr = gr0 + rr;
-        const bool ok = (k < g.KP) & (gr < GR);
+        const bool ok = (apk[i] < 0) & (gr < GR);
         const int q = ok ? gr * g.Wo + wo : 0;
         s.a[i] = *reinterpret_cast<const uint4*>(dy + (q * g.Co + co0 + 8 * v));
         s.ok |= ok ? (1u << (kMaxWinVec + i)) : 0u;
     }
 #pragma unroll
     for (int j = 0; j < NV; ++j) {
-        const int pk = wpos[j];  // rr | kh << 8 | w' << 16, bit 31: a position of the window
-        const int rr = pk & 0xff, kh = (pk >> 8) & 0xff, wc = (pk >> 16) & 0x7fff;
+        // rr | kh << 8 | iwc << 10 (the clamped input column), bit 31: a window position in the image's columns
+        const int pk = wpos[j];
+        const int rr = pk & 0xff, kh = (pk >> 8) & 3, iwc = (pk >> 10) & 0x1fffff;
         const int gr = gr0 + rr;
-        const int grc = gr < GR ? gr : GR - 1;
-        const int n = grc / g.Ho, ho = grc - n * g.Ho;
-        const int ih = ho * g.stride - 1 + kh, iw = wc - 1;
-        const bool ok = (pk < 0) & (gr < GR) & (ih >= 0) & (ih < g.H) & (iw >= 0) & (iw < g.W);
-        const int ihc = min(max(ih, 0), g.H - 1), iwc = min(max(iw, 0), g.W - 1);
-        const int vv = (threadIdx.x + kWgThreads * j) & 7;
-        s.w[j] = *reinterpret_cast<const uint4*>(x + (((n * g.H + ihc) * g.W + iwc) * g.Ci + ci0 + 8 * vv));
+        int ho = ho0 + rr, n = n0;
+        while (ho >= g.Ho) {  // rr < R: a few steps at most for the shapes the window form takes
+            ho -= g.Ho;
+            ++n;
+        }
+        const int ih = ho * g.stride - 1 + kh;
+        const bool ok = (pk < 0) & (gr < GR) & (ih >= 0) & (ih < g.H);
+        const int ihc = min(max(ih, 0), g.H - 1);
+        const int nc = gr < GR ? n : 0;
+        s.w[j] = *reinterpret_cast<const uint4*>(x + (((nc * g.H + ihc) * g.W + iwc) * g.Ci + ci0 + 8 * v));
         s.ok |= ok ? (1u << j) : 0u;
     }
 }
@@ -330,7 +337,8 @@ __global__ __launch_bounds__(kWgThreads) void wgrad3x3_win_kernel(const __hip_bf
     const int c_end = static_cast<int>(c_begin + g.cps < g.chunks ? c_begin + g.cps : g.chunks);
     const int pr = tid >> 3, v = tid & 7;
 
-    // this thread's window vectors (the same positions in every chunk)
+    // this thread's window vectors (the same positions in every chunk; the vector's channel block
+    // is v = tid & 7 for every j) and dy rows
     int wpos[kMaxWinVec];
 #pragma unroll
     for (int j = 0; j < NV; ++j) {
@@ -338,7 +346,16 @@ __global__ __launch_bounds__(kWgThreads) void wgrad3x3_win_kernel(const __hip_bf
         const int per_row = 3 * g.Wd;
         const int rr = pos / per_row, rem = pos - rr * per_row;
         const int kh = rem / g.Wd, wc = rem - kh * g.Wd;
-        wpos[j] = (pos < g.npos ? int(0x80000000u) : 0) | rr | (kh << 8) | (wc << 16);
+        const int iw = wc - 1;
+        const bool ok = (pos < g.npos) & (iw >= 0) & (iw < g.W);
+        wpos[j] = (ok ? int(0x80000000u) : 0) | rr | (kh << 8) | (min(max(iw, 0), g.W - 1) << 10);
+    }
+    int apk[KS / 2];
+#pragma unroll
+    for (int i = 0; i < KS / 2; ++i) {
+        const int k = pr + 64 * i;
+        const int rr = k / g.Wo, wo = k - rr * g.Wo;
+        apk[i] = (k < g.KP ? int(0x80000000u) : 0) | (k < g.KP ? rr | (wo << 8) : 0);
     }
     // this lane's fragment rows: pixel k = 32 ks + 16 h + 4 (lane >> 4) + ((lane & 15) >> 2) (any
     // order of the 32 pixels of a k-step sums the same products; this one gives each 32-lane pass
@@ -370,16 +387,16 @@ __global__ __launch_bounds__(kWgThreads) void wgrad3x3_win_kernel(const __hip_bf
         for (int b = 0; b < 9; ++b) acc[a][b] = f32x4v{0.f, 0.f, 0.f, 0.f};
 
     WinStaging<NV, KS> st;
-    load_win<NV, KS>(st, x, dy, g, c_begin, wpos, pr, v, co0, ci0);
+    load_win<NV, KS>(st, x, dy, g, c_begin, apk, wpos, v, co0, ci0);
     stage_win<NV, KS>(st, L, g, pr, v);
-    load_win<NV, KS>(st, x, dy, g, c_begin + 1 < c_end ? c_begin + 1 : c_begin, wpos, pr, v, co0, ci0);
+    load_win<NV, KS>(st, x, dy, g, c_begin + 1 < c_end ? c_begin + 1 : c_begin, apk, wpos, v, co0, ci0);
     __syncthreads();
     for (int c = c_begin; c < c_end; ++c) {
         const int b = (c - c_begin) & 1;
         // chunk c + 1 into the other buffer (read last by chunk c - 1, before the barrier below
         // ended that iteration); on the last chunk this stages a clamped copy nobody reads
         stage_win<NV, KS>(st, L + (b ^ 1) * buf_elems, g, pr, v);
-        load_win<NV, KS>(st, x, dy, g, c + 2 < c_end ? c + 2 : c_end - 1, wpos, pr, v, co0, ci0);
+        load_win<NV, KS>(st, x, dy, g, c + 2 < c_end ? c + 2 : c_end - 1, apk, wpos, v, co0, ci0);
         __builtin_amdgcn_sched_barrier(0);  // the loads ahead of the MFMAs
         win_multiply<KS>(acc, L + b * buf_elems, aoff, boff, toff, mt0, nt0);
         __syncthreads();
@@ -444,8 +461,9 @@ int g_wgrad_form = 0;  // dauc_set_wgrad_form: 0 automatic, 1 the gather form, 2
 #endif
 
 bool win_geom(int64_t N, int H, int W, int Ci, int Ho, int Wo, int Co, int stride, WinGeom& g) {
-    // the window kernel indexes x and dy with 32-bit element offsets
+    // the window kernel indexes x and dy with 32-bit element offsets (and packs a column in 21 bits)
     if (N * H * int64_t(W) * Ci >= (int64_t(1) << 31) || N * Ho * int64_t(Wo) * Co >= (int64_t(1) << 31)) return false;
+    if (W >= (1 << 21)) return false;
     int form = 0;
 #ifdef DAUC_TUNING
     form = g_wgrad_form;

@@ -1,0 +1,33 @@
+#!/bin/bash
+# round 5: window wgrad staging with the per-chunk row found once (no division per vector) and the
+# static part of every vector's address decoded once. wgrad tests, micro-benchmark of both builds,
+# training-only runs against the previous build ($PREV) interleaved.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+O=gpurun_out/${1:-r05u}
+PREV=${PREV:-tuning/ab/libdauc_v3.so}
+mkdir -p $O
+timeout -k 10 400 python -u -m pytest tests/test_conv_wgrad_gpu.py -x -q --timeout 240 --timeout-method thread \
+    > $O/pytest_wgrad.log 2>&1
+rc=$?; echo "wgrad tests rc=$rc"; tail -2 $O/pytest_wgrad.log
+[ $rc -eq 0 ] || exit $rc
+DAUC_LIB=$PREV timeout -k 10 120 python3 scripts/probe_wgrad.py 20 > $O/probe_prev.jsonl 2> $O/probe_prev.err || exit $?
+timeout -k 10 120 python3 scripts/probe_wgrad.py 20 > $O/probe_new.jsonl 2> $O/probe_new.err || exit $?
+python3 - $O <<'PY'
+import json, sys
+o = sys.argv[1]
+a = [json.loads(l) for l in open(f"{o}/probe_prev.jsonl")]; b = [json.loads(l) for l in open(f"{o}/probe_new.jsonl")]
+for x, y in zip(a, b):
+    print(x["C"], x["H"], x["stride"], round(x["us_per_call"], 1), "->", round(y["us_per_call"], 1))
+PY
+run() {  # name, env...
+    local name=$1; shift
+    env "$@" timeout -k 10 300 python3 bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-auc --no-surrogate \
+        --r18-steps 0 --sweep-I "" --eval-images 0 > $O/$name.json 2> $O/$name.err || return $?
+    python3 -c "import json;d=json.load(open('$O/$name.json'));print('$name', round(d['ms_per_step'],3), round(d['value'],1))"
+}
+run prev1 DAUC_LIB=$PREV || exit $?
+run new1 || exit $?
+run prev2 DAUC_LIB=$PREV || exit $?
+run new2 || exit $?
+echo done
