@@ -1,6 +1,8 @@
 """Per-training-step GPU time by kernel family from a rocprofv3 kernel trace of bench.py.
 
-The window is the last N steps before the final update launch (one dauc_pd_update per step).
+The window is the last N steps before the final update launch (one dauc_pd_update per step) of
+the largest model in the trace (the update launches with the largest grid: the default bench also
+trains ResNet-18 for its N = 2 leg).
 
     python scripts/step_breakdown.py gpurun_out/prof_r01/bench_kernel_trace.csv [N]
 """
@@ -29,7 +31,10 @@ def family(name: str) -> str:
 
 def main(path: str, nsteps: int = 5) -> None:
     rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
-    ups = [i for i, r in enumerate(rows) if "pd_update_kernel" in r["Kernel_Name"]]
+    grid = lambda r: int(r.get("Grid_Size_X") or r.get("Grid_Size") or 0)  # noqa: E731
+    upd = [(i, grid(r)) for i, r in enumerate(rows) if "pd_update_kernel" in r["Kernel_Name"]]
+    gmax = max(gs for _, gs in upd)
+    ups = [i for i, gs in upd if gs == gmax]
     i0, i1 = ups[-1 - nsteps], ups[-1]
     agg: dict = collections.defaultdict(lambda: [0.0, 0])
     busy = 0.0
