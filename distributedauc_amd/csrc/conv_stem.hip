@@ -60,6 +60,7 @@ struct StemGeom {
     int N, H, W, Ho, Wo;
     int segs;     // ceil(Wo / kSeg)
     int tasks;    // N * Ho * segs
+    int sgroups;  // wgrad: slab groups of the two-level slab sum (1: one level)
 };
 
 __device__ __forceinline__ void task_coords(const StemGeom& g, int t, int& n, int& oh, int& ow0) {
@@ -330,7 +331,11 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
         }
     }
     // D[co = 16 ct + 4 grp + e][k' = 16 nt + col] -> this workgroup's slab [co][kh][kw][ci]
-    float* slab = slabs + static_cast<int64_t>(blockIdx.x) * kWElems;
+    // two-level sum: workgroup b's slab is row b % G1 of group b / G1, stored [G1][groups] so the
+    // first level is one slab sum of G1 slabs of groups x 9,408 floats (a wide grid)
+    const int b = blockIdx.x, groups = static_cast<int>(gridDim.x) / g.sgroups;
+    const int slot = g.sgroups > 1 ? (b % g.sgroups) * groups + b / g.sgroups : b;
+    float* slab = slabs + static_cast<int64_t>(slot) * kWElems;
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
         if (i == 2 && ntiles == 2) break;
@@ -359,12 +364,14 @@ bool stem_geom(int64_t N, int H, int W, int Ho, int Wo, StemGeom& g) {
     const int64_t tasks = N * Ho * int64_t(g.segs);
     if (tasks >= (int64_t(1) << 31)) return false;
     g.tasks = static_cast<int>(tasks);
+    g.sgroups = 1;
     return true;
 }
 
 // persistent grids: workgroups per CU as registers allow (forward 196 VGPRs: 2; wgrad 155: 3)
 constexpr int kFwdGrid = 512;
 constexpr int kWgradGrid = 768;
+constexpr int kSlabGroups = 32;  // first level of the weight-gradient slab sum: 32 slabs of 24 x 9,408 floats
 
 }  // namespace
 }  // namespace dauc
@@ -391,7 +398,8 @@ size_t dauc_conv7x7s2_stem_wgrad_workspace_size(int64_t N, int Ho, int Wo) {
     if (N < 1 || Ho < 1 || Wo < 1) return 0;
     const int64_t tasks = N * Ho * ((Wo + kSeg - 1) / kSeg);
     const int64_t grid = tasks < kWgradGrid ? tasks : kWgradGrid;
-    return grid > 1 ? size_t(grid) * kWElems * sizeof(float) : 0;
+    const int64_t second = grid == kWgradGrid ? grid / kSlabGroups : 0;  // the first level's output
+    return grid > 1 ? size_t(grid + second) * kWElems * sizeof(float) : 0;
 }
 
 int dauc_conv7x7s2_stem_wgrad(const void* x, const void* dy, int dtype, int64_t N, int H, int W, int Ho, int Wo,
@@ -405,12 +413,18 @@ int dauc_conv7x7s2_stem_wgrad(const void* x, const void* dy, int dtype, int64_t 
     const size_t need = dauc_conv7x7s2_stem_wgrad_workspace_size(N, Ho, Wo);
     if (need && (workspace == nullptr || workspace_bytes < need || (reinterpret_cast<uintptr_t>(workspace) & 15u)))
         return DAUC_EINVAL;
+    g.sgroups = grid == kWgradGrid ? kSlabGroups : 1;
     float* target = grid > 1 ? static_cast<float*>(workspace) : dw;
     hipLaunchKernelGGL(stem_wgrad_kernel, dim3(grid), dim3(kThreads), 0, as_hip(stream),
                        static_cast<const unsigned short*>(x), static_cast<const unsigned short*>(dy), g, target);
-    const int rc = launch_status();
+    int rc = launch_status();
     if (rc != DAUC_OK || grid == 1) return rc;
-    return dauc_slab_sum(target, grid, kWElems, dw, stream);
+    if (g.sgroups == 1) return dauc_slab_sum(target, grid, kWElems, dw, stream);
+    const int groups = grid / g.sgroups;
+    float* level1 = target + int64_t(grid) * kWElems;
+    rc = dauc_slab_sum(target, g.sgroups, int64_t(groups) * kWElems, level1, stream);
+    if (rc != DAUC_OK) return rc;
+    return dauc_slab_sum(level1, groups, kWElems, dw, stream);
 }
 
 }  // extern "C"

@@ -4,7 +4,8 @@ Reference: imagenet/resnet.py:145 (conv1) under main.py:311-326's forward / back
 same convolution in fp64 on the CPU (torch.nn.functional.conv2d on the bf16 operands widened to
 fp64). Tolerances: the forward is one bf16 rounding of an fp32 sum, so |y - ref| <= |ref| 2^-8 +
 (fp32 accumulation, 1e-5 of the largest output); the weight gradient is an fp32 sum over every
-output pixel (per-workgroup slabs summed in a fixed order), within 2e-5 of its largest entry.
+output pixel (per-workgroup slabs summed in a fixed order, in two levels on the full grid), within
+2e-5 of its largest entry.
 Both are bitwise reproducible run to run.
 """
 from __future__ import annotations
@@ -15,7 +16,8 @@ import torch.nn.functional as F
 
 pytestmark = pytest.mark.gpu
 
-SHAPES = [(2, 224, 224), (1, 17, 23), (3, 40, 300), (1, 1, 1), (5, 8, 9), (2, 2, 257)]
+# (7, 224, 64): 784 row tasks >= the 768-workgroup grid, so the weight gradient's two-level slab sum
+SHAPES = [(2, 224, 224), (1, 17, 23), (3, 40, 300), (1, 1, 1), (5, 8, 9), (2, 2, 257), (7, 224, 64)]
 
 
 def _inputs(dev, N, H, W, seed):
