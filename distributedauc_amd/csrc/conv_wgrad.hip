@@ -211,6 +211,10 @@ struct WinGeom {
     int KT;    // pixel rows of the staged dy tile: 64 or 128 (2 or 4 k-steps per chunk)
     int wrow;  // LDS row stride of the window: 80 (stride 1) or 72 (stride 2)
     int R, Wd, npos, KP, nvec;
+    // shared rows (stride 1, R | Ho or Ho | R): the chunk's output rows read consecutive input rows,
+    // so its window is the R + 2 input rows they span (per image: Ho + 2) instead of 3 per output
+    // row; window slot s is image n0 + s / (Ho + 2), input row ho0 - 1 + s % (Ho + 2)
+    int shared;
     int64_t GR;      // output rows N * Ho
     int64_t chunks;  // ceil(GR / R)
     int64_t cps;
@@ -249,19 +253,32 @@ __device__ __forceinline__ void load_win(WinStaging<NV, KS>& s, const __hip_bflo
     }
 #pragma unroll
     for (int j = 0; j < NV; ++j) {
-        // rr | kh << 8 | iwc << 10 (the clamped input column), bit 31: a window position in the image's columns
+        // rr | kh << 8 | iwc << 10 (the clamped input column), or with shared rows sg | u << 8 |
+        // iwc << 16 (slot sg (Ho + 2) + u); bit 31: a window position in the image's columns
         const int pk = wpos[j];
-        const int rr = pk & 0xff, kh = (pk >> 8) & 3, iwc = (pk >> 10) & 0x1fffff;
-        const int gr = gr0 + rr;
-        int ho = ho0 + rr, n = n0;
-        while (ho >= g.Ho) {  // rr < R: a few steps at most for the shapes the window form takes
-            ho -= g.Ho;
-            ++n;
+        int n, ih, iwc;
+        bool ok;
+        if (g.shared) {  // image n0 + sg, input row ho0 - 1 + u (a wave-uniform branch)
+            const int sg = pk & 0xff, u = (pk >> 8) & 0xff;
+            iwc = (pk >> 16) & 0x7fff;
+            n = n0 + sg;
+            ih = ho0 - 1 + u;
+            ok = (pk < 0) & (n < g.N) & (ih >= 0) & (ih < g.H);
+        } else {
+            const int rr = pk & 0xff, kh = (pk >> 8) & 3;
+            iwc = (pk >> 10) & 0x1fffff;
+            const int gr = gr0 + rr;
+            int ho = ho0 + rr;
+            n = n0;
+            while (ho >= g.Ho) {  // rr < R: a few steps at most for the shapes the window form takes
+                ho -= g.Ho;
+                ++n;
+            }
+            ih = ho * g.stride - 1 + kh;
+            ok = (pk < 0) & (gr < GR) & (ih >= 0) & (ih < g.H);
         }
-        const int ih = ho * g.stride - 1 + kh;
-        const bool ok = (pk < 0) & (gr < GR) & (ih >= 0) & (ih < g.H);
         const int ihc = min(max(ih, 0), g.H - 1);
-        const int nc = gr < GR ? n : 0;
+        const int nc = n < g.N ? n : 0;
         s.w[j] = *reinterpret_cast<const uint4*>(x + (((nc * g.H + ihc) * g.W + iwc) * g.Ci + ci0 + 8 * v));
         s.ok |= ok ? (1u << j) : 0u;
     }
@@ -343,12 +360,20 @@ __global__ __launch_bounds__(kWgThreads) void wgrad3x3_win_kernel(const __hip_bf
 #pragma unroll
     for (int j = 0; j < NV; ++j) {
         const int pos = (tid + kWgThreads * j) >> 3;
-        const int per_row = 3 * g.Wd;
-        const int rr = pos / per_row, rem = pos - rr * per_row;
-        const int kh = rem / g.Wd, wc = rem - kh * g.Wd;
-        const int iw = wc - 1;
-        const bool ok = (pos < g.npos) & (iw >= 0) & (iw < g.W);
-        wpos[j] = (ok ? int(0x80000000u) : 0) | rr | (kh << 8) | (min(max(iw, 0), g.W - 1) << 10);
+        if (g.shared) {
+            const int sl = pos / g.Wd, wc = pos - sl * g.Wd;
+            const int sg = sl / (g.Ho + 2), u = sl - sg * (g.Ho + 2);
+            const int iw = wc - 1;
+            const bool ok = (pos < g.npos) & (iw >= 0) & (iw < g.W);
+            wpos[j] = (ok ? int(0x80000000u) : 0) | sg | (u << 8) | (min(max(iw, 0), g.W - 1) << 16);
+        } else {
+            const int per_row = 3 * g.Wd;
+            const int rr = pos / per_row, rem = pos - rr * per_row;
+            const int kh = rem / g.Wd, wc = rem - kh * g.Wd;
+            const int iw = wc - 1;
+            const bool ok = (pos < g.npos) & (iw >= 0) & (iw < g.W);
+            wpos[j] = (ok ? int(0x80000000u) : 0) | rr | (kh << 8) | (min(max(iw, 0), g.W - 1) << 10);
+        }
     }
     int apk[KS / 2];
 #pragma unroll
@@ -368,7 +393,9 @@ __global__ __launch_bounds__(kWgThreads) void wgrad3x3_win_kernel(const __hip_bf
         for (int h = 0; h < 2; ++h) {
             const int k = 32 * ks + 16 * h + 4 * (lane >> 4) + ((lane & 15) >> 2);
             const int rr = k / g.Wo, cc = k - rr * g.Wo;
-            const int pos = k < g.KP ? rr * 3 * g.Wd + cc * g.stride : 0;
+            // the window position of pixel k's tap (0, 0): its output row's first window row
+            const int row0 = g.shared ? rr + 2 * (rr / g.Ho) : 3 * rr;
+            const int pos = k < g.KP ? row0 * g.Wd + cc * g.stride : 0;
             aoff[ks][h] = k * kARow + 4 * (lane & 3);
             boff[ks][h] = pos * g.wrow + 4 * (lane & 3);
         }
@@ -439,15 +466,25 @@ extern "C" {
 namespace {
 // the window form's geometry (returns false when the shape needs the gather form)
 // one chunk layout: R whole output rows of a KT-row dy tile and their windows (false: does not fit)
-bool win_layout(int W, int Wo, int KT, WinGeom& g) {
+bool win_layout(int W, int Wo, int KT, bool shared, WinGeom& g) {
     if (Wo > KT) return false;
+    if (shared && (g.stride != 1 || W >= (1 << 15))) return false;
     g.KT = KT;
+    g.shared = shared ? 1 : 0;
     g.wrow = g.stride == 1 ? kARow : kRow;
     g.Wd = W + 2;
     // as many whole output rows as fit the tile (fewer if the window needs more vectors per thread
-    // than kWinVecFast or more LDS than a CU has)
+    // than kWinVecFast or more LDS than a CU has; with shared rows, R divides Ho or Ho divides R,
+    // so no chunk holds part of an image beside another image's rows)
     for (g.R = KT / Wo; g.R >= 1; --g.R) {
-        g.npos = g.R * 3 * g.Wd;
+        if (shared) {
+            if (g.Ho % g.R != 0 && g.R % g.Ho != 0) continue;
+            const int images = g.R >= g.Ho ? g.R / g.Ho : 1, rows = g.R >= g.Ho ? g.Ho + 2 : g.R + 2;
+            if (images > 255 || rows > 255) continue;  // packed in 8 bits each
+            g.npos = images * rows * g.Wd;
+        } else {
+            g.npos = g.R * 3 * g.Wd;
+        }
         g.nvec = (g.npos * 8 + kWgThreads - 1) / kWgThreads;
         if (g.nvec <= kWinVecFast && win_lds_bytes(g) <= 160 * 1024) break;
     }
@@ -456,8 +493,18 @@ bool win_layout(int W, int Wo, int KT, WinGeom& g) {
     return true;
 }
 
+// relative cost of a layout: per chunk, its k-steps' MFMAs (a SIMD's 2 waves x 18 x 16 cycles per
+// k-step), the staging of its window (about 4.4 SIMD cycles per position: 8 vectors' loads,
+// address VALU and LDS stores) and a fixed ~1,000 cycles (barrier, exposed load latency), times
+// the chunk count. Measured at ResNet-50 b256 (profiles/r05/wgrad3x3_shared/): it picks shared rows
+// with 128-pixel chunks for every stride-1 shape, the fastest of the four layouts there.
+double win_cost(const WinGeom& g) {
+    const double chunks = double((g.GR + g.R - 1) / g.R);
+    return chunks * (576.0 * (g.KT / 32) + 4.4 * g.npos + 1000.0);
+}
+
 #ifdef DAUC_TUNING
-int g_wgrad_form = 0;  // dauc_set_wgrad_form: 0 automatic, 1 the gather form, 2 / 3 window KT 64 / 128
+int g_wgrad_form = 0;  // dauc_set_wgrad_form: 0 automatic, 1 gather, 2 / 3 window KT 64 / 128, 4 / 5 shared rows
 #endif
 
 bool win_geom(int64_t N, int H, int W, int Ci, int Ho, int Wo, int Co, int stride, WinGeom& g) {
@@ -480,15 +527,22 @@ bool win_geom(int64_t N, int H, int W, int Ci, int Ho, int Wo, int Co, int strid
     g.Wo = Wo;
     g.Co = Co;
     g.stride = stride;
-    // a 128-pixel chunk (4 k-steps: half the barriers and staging waits per MFMA) when its rows
-    // fill at least 7/8 of it, else 64 pixels
-    WinGeom g64 = g, g128 = g;
-    const bool ok64 = win_layout(W, Wo, 64, g64);
-    const bool ok128 = win_layout(W, Wo, 128, g128);
-    if (form == 2 ? !ok64 : form == 3 ? !ok128 : !(ok64 || ok128)) return false;
-    const bool use128 = form == 3 || (form == 0 && ok128 && (!ok64 || 8 * g128.KP >= 7 * 128));
-    g = use128 ? g128 : g64;
     g.GR = N * Ho;
+    // 64- or 128-pixel chunks (2 or 4 k-steps per barrier and staging wait), per-output-row or
+    // shared window rows: the layout of least estimated cost (tuning forms 2 / 3: per-row windows
+    // with 64 / 128-pixel chunks; 4 / 5: shared rows with 64 / 128-pixel chunks)
+    WinGeom cand[4] = {g, g, g, g};
+    bool ok[4];
+    for (int i = 0; i < 4; ++i) ok[i] = win_layout(W, Wo, (i & 1) ? 128 : 64, i >= 2, cand[i]);
+    int pick = -1;
+    if (form >= 2 && form <= 5) {
+        pick = form - 2;
+    } else {
+        for (int i = 0; i < 4; ++i)
+            if (ok[i] && (pick < 0 || win_cost(cand[i]) < win_cost(cand[pick]))) pick = i;
+    }
+    if (pick < 0 || !ok[pick]) return false;
+    g = cand[pick];
     g.chunks = (g.GR + g.R - 1) / g.R;
     g.ctiles = Ci / kBC;
     return true;
@@ -591,7 +645,7 @@ int dauc_conv3x3_wgrad(const void* x, const void* dy, int dtype, int64_t N, int 
 
 #ifdef DAUC_TUNING
 int dauc_set_wgrad_form(int form) {
-    if (form < 0 || form > 3) return DAUC_EINVAL;
+    if (form < 0 || form > 5) return DAUC_EINVAL;
     g_wgrad_form = form;
     return DAUC_OK;
 }

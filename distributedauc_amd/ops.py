@@ -703,7 +703,8 @@ def stem_conv_supported(x: torch.Tensor, weight: torch.Tensor, stride, padding, 
 
 
 def set_wgrad_form(form: int) -> None:
-    """The tuning build's 3x3 weight-gradient form (dauc_set_wgrad_form): 0 automatic, 1 gather, 2 / 3 window with 64- / 128-pixel chunks."""
+    """The tuning build's 3x3 weight-gradient form (dauc_set_wgrad_form): 0 automatic, 1 gather, 2 / 3 window with 64- / 128-pixel chunks,
+    4 / 5 the same with shared window rows."""
     check(_lib.tuning().dauc_set_wgrad_form(int(form)), "dauc_set_wgrad_form")
 
 

@@ -76,9 +76,10 @@ int dauc_set_direct_fault(int mode);
  * tile whose element (row, col) holds row * 64 + col. */
 int dauc_probe_tr16(short* out, dauc_stream_t stream);
 
-/* The 3x3 weight gradient's form: 0 automatic (stride 1: the window form wherever it fits, with 128-pixel
- * chunks where their rows fill 7/8 of them), 1 the gather form everywhere, 2 / 3 the window form
- * with 64 / 128-pixel chunks where it fits (tests, A/B runs). Process-global; tuning builds only. */
+/* The 3x3 weight gradient's form: 0 automatic (stride 1: the window layout of least estimated cost
+ * wherever one fits; stride 2: gather), 1 the gather form everywhere, 2 / 3 the window form with
+ * per-output-row windows and 64 / 128-pixel chunks, 4 / 5 with shared window rows (stride 1) and
+ * 64 / 128-pixel chunks, where they fit (tests, A/B runs). Process-global; tuning builds only. */
 int dauc_set_wgrad_form(int form);
 
 #ifdef __cplusplus

@@ -38,7 +38,7 @@ def _ref_wgrad(x, dy, stride):
                                                [False, True, False])[1]
 
 
-@pytest.mark.parametrize("form", ["auto", "gather", "window64", "window128"])
+@pytest.mark.parametrize("form", ["auto", "gather", "window64", "window128", "shared64", "shared128"])
 @pytest.mark.parametrize("N,Ci,Co,H,W,stride", [
     (2, 64, 64, 9, 11, 1), (3, 128, 64, 14, 14, 2), (1, 64, 192, 7, 5, 1), (4, 64, 128, 15, 13, 2),
     (2, 256, 256, 14, 14, 1), (5, 512, 512, 7, 7, 1), (1, 64, 64, 1, 1, 1), (2, 64, 64, 2, 3, 2),
@@ -47,14 +47,16 @@ def test_conv3x3_wgrad_matches_fp64(dev, form, N, Ci, Co, H, W, stride):
     """Every form of the kernel: the window form (whole output rows per chunk, the taps read one
     staged input window) with 64- or 128-pixel chunks (Wo <= 64 / 128; the automatic choice takes
     128 where its rows fill 7/8 of the chunk), and the gather form (64-pixel chunks, one gathered
-    tile per tap; wider images). The tuning build's dauc_set_wgrad_form(1 / 2 / 3) forces one form
-    (a window form that does not fit falls back to the gather form)."""
+    tile per tap; wider images), and the window form with shared rows (stride 1: a chunk's output
+    rows read its R + 2 input rows, per image Ho + 2, when R divides Ho or Ho divides R). The tuning
+    build's dauc_set_wgrad_form(1 .. 5) forces one form (a window form that does not fit falls back
+    to the gather form)."""
     from distributedauc_amd import _lib, ops
 
     if form == "auto":
         _check_wgrad(dev, N, Ci, Co, H, W, stride)
         return
-    ops.set_wgrad_form({"gather": 1, "window64": 2, "window128": 3}[form])
+    ops.set_wgrad_form({"gather": 1, "window64": 2, "window128": 3, "shared64": 4, "shared128": 5}[form])
     try:
         with _lib.using(_lib.tuning()):
             _check_wgrad(dev, N, Ci, Co, H, W, stride)
