@@ -211,9 +211,10 @@ struct WinGeom {
     int KT;    // pixel rows of the staged dy tile: 64 or 128 (2 or 4 k-steps per chunk)
     int wrow;  // LDS row stride of the window: 80 (stride 1) or 72 (stride 2)
     int R, Wd, npos, KP, nvec;
-    // shared rows (stride 1, R | Ho or Ho | R): the chunk's output rows read consecutive input rows,
-    // so its window is the R + 2 input rows they span (per image: Ho + 2) instead of 3 per output
-    // row; window slot s is image n0 + s / (Ho + 2), input row ho0 - 1 + s % (Ho + 2)
+    // shared rows (R | Ho or Ho | R): the chunk's output rows read overlapping input rows, so its
+    // window is the stride R + 3 - stride input rows they span (per image: IR = stride Ho + 3 -
+    // stride) instead of 3 per output row; window slot s is image n0 + s / IR, input row
+    // stride ho0 - 1 + s % IR
     int shared;
     int64_t GR;      // output rows N * Ho
     int64_t chunks;  // ceil(GR / R)
@@ -254,15 +255,15 @@ __device__ __forceinline__ void load_win(WinStaging<NV, KS>& s, const __hip_bflo
 #pragma unroll
     for (int j = 0; j < NV; ++j) {
         // rr | kh << 8 | iwc << 10 (the clamped input column), or with shared rows sg | u << 8 |
-        // iwc << 16 (slot sg (Ho + 2) + u); bit 31: a window position in the image's columns
+        // iwc << 16 (slot sg IR + u); bit 31: a window position in the image's columns
         const int pk = wpos[j];
         int n, ih, iwc;
         bool ok;
-        if (g.shared) {  // image n0 + sg, input row ho0 - 1 + u (a wave-uniform branch)
+        if (g.shared) {  // image n0 + sg, input row stride ho0 - 1 + u (a wave-uniform branch)
             const int sg = pk & 0xff, u = (pk >> 8) & 0xff;
             iwc = (pk >> 16) & 0x7fff;
             n = n0 + sg;
-            ih = ho0 - 1 + u;
+            ih = ho0 * g.stride - 1 + u;
             ok = (pk < 0) & (n < g.N) & (ih >= 0) & (ih < g.H);
         } else {
             const int rr = pk & 0xff, kh = (pk >> 8) & 3;
@@ -361,8 +362,9 @@ __global__ __launch_bounds__(kWgThreads) void wgrad3x3_win_kernel(const __hip_bf
     for (int j = 0; j < NV; ++j) {
         const int pos = (tid + kWgThreads * j) >> 3;
         if (g.shared) {
+            const int ir = g.stride * g.Ho + 3 - g.stride;  // input rows per image
             const int sl = pos / g.Wd, wc = pos - sl * g.Wd;
-            const int sg = sl / (g.Ho + 2), u = sl - sg * (g.Ho + 2);
+            const int sg = sl / ir, u = sl - sg * ir;
             const int iw = wc - 1;
             const bool ok = (pos < g.npos) & (iw >= 0) & (iw < g.W);
             wpos[j] = (ok ? int(0x80000000u) : 0) | sg | (u << 8) | (min(max(iw, 0), g.W - 1) << 16);
@@ -394,7 +396,7 @@ __global__ __launch_bounds__(kWgThreads) void wgrad3x3_win_kernel(const __hip_bf
             const int k = 32 * ks + 16 * h + 4 * (lane >> 4) + ((lane & 15) >> 2);
             const int rr = k / g.Wo, cc = k - rr * g.Wo;
             // the window position of pixel k's tap (0, 0): its output row's first window row
-            const int row0 = g.shared ? rr + 2 * (rr / g.Ho) : 3 * rr;
+            const int row0 = g.shared ? g.stride * rr + (3 - g.stride) * (rr / g.Ho) : 3 * rr;
             const int pos = k < g.KP ? row0 * g.Wd + cc * g.stride : 0;
             aoff[ks][h] = k * kARow + 4 * (lane & 3);
             boff[ks][h] = pos * g.wrow + 4 * (lane & 3);
@@ -468,7 +470,7 @@ namespace {
 // one chunk layout: R whole output rows of a KT-row dy tile and their windows (false: does not fit)
 bool win_layout(int W, int Wo, int KT, bool shared, WinGeom& g) {
     if (Wo > KT) return false;
-    if (shared && (g.stride != 1 || W >= (1 << 15))) return false;
+    if (shared && W >= (1 << 15)) return false;
     g.KT = KT;
     g.shared = shared ? 1 : 0;
     g.wrow = g.stride == 1 ? kARow : kRow;
@@ -479,7 +481,9 @@ bool win_layout(int W, int Wo, int KT, bool shared, WinGeom& g) {
     for (g.R = KT / Wo; g.R >= 1; --g.R) {
         if (shared) {
             if (g.Ho % g.R != 0 && g.R % g.Ho != 0) continue;
-            const int images = g.R >= g.Ho ? g.R / g.Ho : 1, rows = g.R >= g.Ho ? g.Ho + 2 : g.R + 2;
+            const int s = g.stride;
+            const int images = g.R >= g.Ho ? g.R / g.Ho : 1;
+            const int rows = (g.R >= g.Ho ? s * g.Ho : s * g.R) + 3 - s;
             if (images > 255 || rows > 255) continue;  // packed in 8 bits each
             g.npos = images * rows * g.Wd;
         } else {
@@ -516,9 +520,11 @@ bool win_geom(int64_t N, int H, int W, int Ci, int Ho, int Wo, int Co, int strid
     form = g_wgrad_form;
     if (form == 1) return false;
 #endif
-    // stride 2: the gather form (ResNet-50 layer2.0 at b256: 123 us against the window form's 133;
-    // profiles/r05/wgrad3x3_korder)
-    if (form == 0 && stride != 1) return false;
+    // stride 2: the gather form unless a shared-row window fits with its rows filling at least half
+    // of the chunk (ResNet-50 b256: layer2.0 gather 123 us, shared 118; layer4.0 119 / 117;
+    // layer3.0's shared layout fills 28 of 64 pixels: 177 against the gather form's 120;
+    // profiles/r05/wgrad3x3_shared)
+    const bool s2_shared_only = form == 0 && stride != 1;
     g.N = static_cast<int>(N);
     g.H = H;
     g.W = W;
@@ -538,8 +544,10 @@ bool win_geom(int64_t N, int H, int W, int Ci, int Ho, int Wo, int Co, int strid
     if (form >= 2 && form <= 5) {
         pick = form - 2;
     } else {
-        for (int i = 0; i < 4; ++i)
-            if (ok[i] && (pick < 0 || win_cost(cand[i]) < win_cost(cand[pick]))) pick = i;
+        for (int i = s2_shared_only ? 2 : 0; i < 4; ++i)
+            if (ok[i] && !(s2_shared_only && 2 * cand[i].KP < cand[i].KT) &&
+                (pick < 0 || win_cost(cand[i]) < win_cost(cand[pick])))
+                pick = i;
     }
     if (pick < 0 || !ok[pick]) return false;
     g = cand[pick];

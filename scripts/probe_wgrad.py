@@ -23,7 +23,7 @@ if len(sys.argv) > 2:
     _ctx = _lib.using(_lib.tuning())  # held for the whole run: its exit restores the product build
     _ctx.__enter__()
 dev = torch.device("cuda", 0)
-for C, H, stride in ((64, 56, 1), (128, 28, 1), (256, 14, 1), (512, 7, 1), (128, 56, 2)):
+for C, H, stride in ((64, 56, 1), (128, 28, 1), (256, 14, 1), (512, 7, 1), (128, 56, 2), (256, 28, 2), (512, 14, 2)):
     g = torch.Generator(device=dev).manual_seed(C + H)
     x = torch.randn((256, C, H, H), device=dev, generator=g).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
     Ho = (H - 1) // stride + 1
