@@ -32,6 +32,9 @@ plans: dict = {}  # (M, Cin, Cout, dtype, direction) -> engine
 # 224^2, bf16 channels-last; scripts/gpu_conv1x1_plans.sh): shapes listed here are never timed at
 # run time, so every rank (and every run) uses the same engines and the same numerics. Shapes
 # not listed are timed on first use; DAUC_CONV1X1_PLANS names another file ("" = none).
+# the strided downsample's backward: "gemm" (GEMMs on x[:, :, ::s, ::s]) or "miopen" (one
+# convolution_backward call; kept as the A/B reference, DAUC_DOWNSAMPLE_BWD=miopen)
+_DOWNSAMPLE_BWD = os.environ.get("DAUC_DOWNSAMPLE_BWD", "gemm")
 PLANS_FILE = os.environ.get("DAUC_CONV1X1_PLANS", os.path.join(os.path.dirname(__file__), "conv1x1_plans.json"))
 
 
@@ -282,10 +285,17 @@ class Conv1x1Function(torch.autograd.Function):
 
 class Conv1x1SkipFunction(torch.autograd.Function):
     """(conv1(x), skip) for a bottleneck block's input x: skip = x (identity) or the 1x1 downsample
-    conv of x (resnet.py:87-108; stride 1 as a GEMM, stride 2 through MIOpen). Backward: dx = d(skip)
-    + dgrad(conv1), the conv1 dgrad GEMM accumulating into the skip term in place (beta = 1), so the
-    branch-point gradient sum that autograd would run as a separate add kernel over the block input
-    (ResNet-50 b256: up to 3 x 411 MB per block) disappears."""
+    conv of x (resnet.py:87-108; stride 1 as a GEMM, stride 2 forward through MIOpen). Backward:
+    dx = d(skip) + dgrad(conv1), the conv1 dgrad GEMM accumulating into the skip term in place
+    (beta = 1), so the branch-point gradient sum that autograd would run as a separate add kernel
+    over the block input (ResNet-50 b256: up to 3 x 411 MB per block) disappears.
+
+    The strided downsample's backward runs as GEMMs on xs = x[:, :, ::s, ::s] (one strided copy of a
+    quarter of x): dWd = dy^T xs (the split-K fp32 engine) and dxs = dy Wd, added at the strided
+    positions of the conv1 dgrad's output. MIOpen's backward-data zero-fills the whole input
+    gradient and its backward-weights a workspace, then casts (ResNet-50 b256 layer2.0: ~105 us +
+    fill, ~120 us + fill + cast). Its forward stays on the convolution solvers, which beat the
+    strided copy + GEMM (profiles/r05/downsample_gemm/)."""
 
     @staticmethod
     def forward(ctx, x, w1, wd, skip_grad_owned, down_stride=1):
@@ -313,17 +323,20 @@ class Conv1x1SkipFunction(torch.autograd.Function):
         if g1 is not None:
             gy1, g21 = _prep_grad(g1, x, wc1.shape[0])
         strided = wcd is not None and ctx.down_stride != 1
-        if gs is not None and wcd is not None and not strided:
-            gyd, g2d = _prep_grad(gs, x, wcd.shape[0])
-        dx_down = None
-        if gs is not None and strided:
-            # the strided downsample through MIOpen: input and weight grads in one call
+        s = ctx.down_stride
+        xd = x  # the downsample GEMMs' input
+        dx_down = dwd_s = None
+        if gs is not None and strided and _DOWNSAMPLE_BWD == "miopen":  # A/B reference only
             gsd = gs.to(x.dtype).contiguous(memory_format=torch.channels_last)
             cout, cin = wcd.shape
             with torch.autocast("cuda", enabled=False):
                 dx_down, dwd_s, _ = torch.ops.aten.convolution_backward(
-                    gsd, x, wcd.view(cout, cin, 1, 1), None, [ctx.down_stride] * 2, [0, 0], [1, 1], False, [0, 0], 1,
+                    gsd, x, wcd.view(cout, cin, 1, 1), None, [s, s], [0, 0], [1, 1], False, [0, 0], 1,
                     [bool(ctx.needs_input_grad[0]), bool(ctx.needs_input_grad[2]), False])
+        elif gs is not None and wcd is not None:
+            if strided:
+                xd = x[:, :, ::s, ::s].contiguous(memory_format=torch.channels_last)
+            gyd, g2d = _prep_grad(gs, xd, wcd.shape[0])
         if ctx.needs_input_grad[0]:
             if gs is None:
                 base = None
@@ -335,7 +348,7 @@ class Conv1x1SkipFunction(torch.autograd.Function):
                 if base is gs and not ctx.skip_grad_owned:
                     base = base.clone(memory_format=torch.channels_last)
             elif strided:
-                base = dx_down.contiguous(memory_format=torch.channels_last)
+                base = None if dx_down is None else dx_down.contiguous(memory_format=torch.channels_last)
             else:
                 base = _dgrad(gyd, g2d, x, wcd)
             if g1 is None:
@@ -344,13 +357,17 @@ class Conv1x1SkipFunction(torch.autograd.Function):
                 dx = _dgrad(gy1, g21, x, wc1)
             else:
                 dx = _dgrad_acc(base, gy1, g21, x, wc1)
+            if strided and gs is not None and dx_down is None:
+                if dx is None:
+                    dx = torch.zeros_like(x, memory_format=torch.channels_last)
+                dx[:, :, ::s, ::s].add_(_dgrad(gyd, g2d, xd, wcd))
         if ctx.needs_input_grad[1] and g1 is not None:
             dw1 = _wgrad(gy1, g21, x, wc1, ctx.wdtypes[0])
         if wcd is not None and ctx.needs_input_grad[2] and gs is not None:
-            if strided:
-                dwd = dwd_s.to(ctx.wdtypes[1]).view(cout, cin, 1, 1)
+            if dwd_s is not None:
+                dwd = dwd_s.to(ctx.wdtypes[1]).view(wcd.shape[0], wcd.shape[1], 1, 1)
             else:
-                dwd = _wgrad(gyd, g2d, x, wcd, ctx.wdtypes[1])
+                dwd = _wgrad(gyd, g2d, xd, wcd, ctx.wdtypes[1])
         return dx, dw1, dwd, None, None
 
 

@@ -88,12 +88,13 @@ def test_conv1x1_skip_fuses_branch_gradient(dev, down, owned, acc_engine):
     """(conv1(x), skip) in one node: dx = dgrad(conv1) + d(skip), the sum accumulated by the GEMM
     (beta = 1, in place) or by an add after MIOpen's dgrad (or the forward convolution with W^T);
     skip = identity (down 0) or a 1x1
-    downsample of stride 1 (GEMM) / 2 (MIOpen); vs fp64 autograd of the two branches.
+    downsample of stride 1 (GEMM) / 2 (MIOpen forward, backward as GEMMs on x[:, :, ::2, ::2] with the
+    input gradient added at the strided positions; an odd H once); vs fp64 autograd of the two branches.
     Also: the incoming skip gradient is left untouched unless the caller marked it as owned."""
     from distributedauc_amd import conv1x1 as C
 
     torch.manual_seed(7 + down + 2 * owned)
-    N, cin, width, H = 4, 256, 64, 14
+    N, cin, width, H = 4, 256, 64, (13 if down == 2 and acc_engine == "fconv" else 14)
     conv = nn.Conv2d(cin, width, 1, bias=False).to(dev).to(memory_format=torch.channels_last)
     dconv = (nn.Conv2d(cin, 4 * width, 1, stride=down, bias=False).to(dev).to(memory_format=torch.channels_last)
              if down else None)
