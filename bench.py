@@ -239,8 +239,9 @@ def make_coda(arch, batch, image_size, I, pos_ratio, pool, world, rank, device, 
     split = 499
     labels = imagenet_like_labels(1 << 16, 1000, split, pos_ratio=pos_ratio, seed=123 + rank)
     ds = SyntheticImageNet(labels, image_size, split)
+    # bf16 images: the values autocast would cast them to before the stem, cast once per pooled batch
     loader = DeviceLoader(ds, np.arange(len(labels)), batch, device, seed=1234 + rank, channels_last=True, pool=pool,
-                          flip=flip)
+                          flip=flip, dtype=torch.bfloat16)
     net = build_backbone(arch, num_classes=2).to(device).to(memory_format=torch.channels_last)
     net.set_fused_bn(bool(fused_bn)).set_gemm_conv1x1(bool(gemm_conv1x1))
     coda = CoDA(net, lr=lr, gamma=2000.0, T0=10 ** 9, I=I, split_index=split, world=world, rank=rank,

@@ -92,12 +92,14 @@ class DeviceLoader:
     Epochs reshuffle ``indices`` (like DataLoader(shuffle=True)) with a seeded RNG;
     a final partial batch is kept (drop_last=False, the DataLoader default).
     ``pool`` > 0 pre-generates that many batches once and cycles them, so a timed
-    loop reads inputs already resident in HBM.
+    loop reads inputs already resident in HBM. ``dtype``: the images' dtype (bf16 for a bf16
+    autocast model: the values its first convolution would cast them to, cast once here instead
+    of every step).
     """
 
     def __init__(self, dataset: SyntheticImageNet, indices: Sequence[int], batch_size: int, device,
                  seed: int = 0, shuffle: bool = True, channels_last: bool = True, signal: float = 0.25,
-                 pool: int = 0, drop_last: bool = False, flip: float = 0.0):
+                 pool: int = 0, drop_last: bool = False, flip: float = 0.0, dtype: torch.dtype = torch.float32):
         self.ds = dataset
         self.indices = np.asarray(indices, dtype=np.int64)
         if self.indices.size == 0:
@@ -110,6 +112,7 @@ class DeviceLoader:
         self.signal = signal
         self.flip = float(flip)
         self.drop_last = drop_last
+        self.dtype = dtype
         self.gen = torch.Generator(device=self.device)
         self.gen.manual_seed(seed)
         self._pool = [self._make(b) for b in self._index_batches(pool)] if pool else None
@@ -144,6 +147,8 @@ class DeviceLoader:
             x[:, 0].add_(sign.view(-1, 1, 1), alpha=self.signal)
         if self.channels_last:
             x = x.contiguous(memory_format=torch.channels_last)
+        if self.dtype != torch.float32:
+            x = x.to(self.dtype)  # preserves the memory format
         return x, labels
 
     def __iter__(self):
