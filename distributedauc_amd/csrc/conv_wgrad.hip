@@ -33,6 +33,7 @@ namespace dauc {
 namespace {
 
 typedef short v4s __attribute__((ext_vector_type(4)));
+typedef unsigned v4u __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4v __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) v4s lds_v4s;
@@ -203,13 +204,14 @@ constexpr int kWinVecFast = 8;  // window vectors per thread that fit beside the
 // LDS row strides (bf16 elements) of the window kernel. A transposing read serves 32 lanes per
 // pass, 8 rows of 8 bytes; the k order below puts 8 consecutive pixels in one pass, so 80-element
 // (40-bank) rows land them on 8 disjoint bank octets: conflict-free for the dy tile and a stride-1
-// window, where 72 (36 banks) conflicts 2-way. A stride-2 window steps 2 rows per pixel: 72 there.
+// window, where 72 (36 banks) conflicts 2-way. (A stride-2 window steps 2 rows per pixel, 2-way at
+// 80; it keeps 80 so that every tap's offset is one compile-time multiple of the row.)
 constexpr int kARow = 80;
 
 struct WinGeom {
     int N, H, W, Ci, Ho, Wo, Co, stride;
     int KT;    // pixel rows of the staged dy tile: 64 or 128 (2 or 4 k-steps per chunk)
-    int wrow;  // LDS row stride of the window: 80 (stride 1) or 72 (stride 2)
+    int wrow;  // LDS row stride of the window (kARow: fixed, so every tap's offset is an immediate)
     int R, Wd, npos, KP, nvec;
     // shared rows (R | Ho or Ho | R): the chunk's output rows read overlapping input rows, so its
     // window is the stride R + 3 - stride input rows they span (per image: IR = stride Ho + 3 -
@@ -226,31 +228,39 @@ inline size_t win_lds_bytes(const struct WinGeom& g);
 
 template <int NV, int KS>
 struct WinStaging {
-    uint4 a[KS / 2], w[NV];
-    unsigned ok;  // bit j: window vector j in the image; bit kMaxWinVec: the dy row exists
+    v4u a[KS / 2], w[NV];  // zeros where the vector lies outside the image / past the chunk's rows
 };
+
+// Buffer descriptors of x and dy: the range check returns zeros for an offset past the buffer, so
+// a vector outside the image or past the last output row is loaded from offset `bytes` and arrives
+// as zeros -- no validity bits, no masking at the LDS store, 32-bit offsets (no 64-bit address math)
+struct WinSrc {
+    __amdgpu_buffer_rsrc_t x, dy;
+    unsigned xbytes, dybytes;
+};
+
+__device__ __forceinline__ v4u load16(__amdgpu_buffer_rsrc_t r, unsigned off) {
+    return __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(r, static_cast<int>(off), 0, 0));
+}
 
 // 32-bit element offsets throughout (host: N * H * W * Ci and N * Ho * Wo * Co < 2^31): 64-bit
 // address arithmetic per load was most of the loop's VALU work. What does not change from chunk to
 // chunk is decoded once per thread (apk / wpos); per chunk one division finds the chunk's first
 // output row (n0, ho0), and each vector's row follows by at most a few wrap steps, not a division.
 template <int NV, int KS>
-__device__ __forceinline__ void load_win(WinStaging<NV, KS>& s, const __hip_bfloat16* __restrict__ x,
-                                         const __hip_bfloat16* __restrict__ dy, const WinGeom& g, int chunk,
+__device__ __forceinline__ void load_win(WinStaging<NV, KS>& s, const WinSrc& src, const WinGeom& g, int chunk,
                                          const int (&apk)[KS / 2], const int (&wpos)[kMaxWinVec], int v, int co0,
                                          int ci0) {
     const int gr0 = chunk * g.R;
     const int GR = static_cast<int>(g.GR);
     const int n0 = gr0 / g.Ho, ho0 = gr0 - n0 * g.Ho;
-    s.ok = 0u;
 #pragma unroll
     for (int i = 0; i < KS / 2; ++i) {  // dy: pixel k = pr + 64 i of the chunk (rr | wo << 8, bit 31: k < KP)
         const int rr = apk[i] & 0xff, wo = (apk[i] >> 8) & 0x7fffff;
         const int gr = gr0 + rr;
         const bool ok = (apk[i] < 0) & (gr < GR);
-        const int q = ok ? gr * g.Wo + wo : 0;
-        s.a[i] = *reinterpret_cast<const uint4*>(dy + (q * g.Co + co0 + 8 * v));
-        s.ok |= ok ? (1u << (kMaxWinVec + i)) : 0u;
+        const unsigned off = 2u * static_cast<unsigned>((gr * g.Wo + wo) * g.Co + co0 + 8 * v);
+        s.a[i] = load16(src.dy, ok ? off : src.dybytes);
     }
 #pragma unroll
     for (int j = 0; j < NV; ++j) {
@@ -278,31 +288,28 @@ __device__ __forceinline__ void load_win(WinStaging<NV, KS>& s, const __hip_bflo
             ih = ho * g.stride - 1 + kh;
             ok = (pk < 0) & (gr < GR) & (ih >= 0) & (ih < g.H);
         }
-        const int ihc = min(max(ih, 0), g.H - 1);
-        const int nc = n < g.N ? n : 0;
-        s.w[j] = *reinterpret_cast<const uint4*>(x + (((nc * g.H + ihc) * g.W + iwc) * g.Ci + ci0 + 8 * v));
-        s.ok |= ok ? (1u << j) : 0u;
+        const unsigned off = 2u * static_cast<unsigned>(((n * g.H + ih) * g.W + iwc) * g.Ci + ci0 + 8 * v);
+        s.w[j] = load16(src.x, ok ? off : src.xbytes);
     }
 }
 
 typedef __attribute__((address_space(3))) short lds_short;
-typedef unsigned v4u __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) v4u lds_v4u;
 
-__device__ __forceinline__ void st_lds(lds_short* p, const uint4& u) { *(lds_v4u*)p = v4u{u.x, u.y, u.z, u.w}; }
+__device__ __forceinline__ void st_lds(lds_short* p, const v4u& u) { *(lds_v4u*)p = u; }
 
 template <int NV, int KS>
 __device__ __forceinline__ void stage_win(const WinStaging<NV, KS>& s, lds_short* buf, const WinGeom& g, int pr,
                                           int v) {
 #pragma unroll
-    for (int i = 0; i < KS / 2; ++i) st_lds(buf + ((pr + 64 * i) * kARow + 8 * v), masked(s.a[i], s.ok, kMaxWinVec + i));
+    for (int i = 0; i < KS / 2; ++i) st_lds(buf + ((pr + 64 * i) * kARow + 8 * v), s.a[i]);
     lds_short* win = buf + 32 * KS * kARow;
 #pragma unroll
     for (int j = 0; j < NV; ++j) {
         const int idx = threadIdx.x + kWgThreads * j;
         const int pos = idx >> 3;
         if (pos < g.npos)
-            st_lds(win + (pos * g.wrow + 8 * (idx & 7)), masked(s.w[j], s.ok, j));
+            st_lds(win + (pos * g.wrow + 8 * (idx & 7)), s.w[j]);
     }
 }
 
@@ -314,30 +321,35 @@ __device__ __forceinline__ v4s tr_at(const lds_short* p) {
     return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)p);
 }
 
-// one wave's 36 MFMAs of a chunk staged at `cur` (A rows, then the window). aoff / boff: this
-// lane's element offsets of its A rows / window positions (k-step, half); toff: each tap's window
-// offset (wave-uniform)
+// one wave's 72 MFMAs of a chunk staged at `cur` (A rows, then the window): its 2 output-channel
+// tiles x the 9 taps of its 16-input-channel block. aoff / boff: this lane's element offsets of its
+// A rows / window positions (k-step, half), the wave's channel blocks included; wd_row: one window
+// row (Wd positions). Each k-step reads tap (kh, kw) at boff + kh wd_row + kw kARow: two adds per
+// (k-step, half), the rest immediate offsets.
 template <int KS>
 __device__ __forceinline__ void win_multiply(f32x4v (&acc)[2][9], const lds_short* cur, const int (&aoff)[KS][2],
-                                             const int (&boff)[KS][2], const int (&toff)[9], int mt0, int nt0) {
+                                             const int (&boff)[KS][2], int wd_row) {
     const lds_short* win = cur + 32 * KS * kARow;
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
         bf16x8 fa[2];
 #pragma unroll
         for (int a = 0; a < 2; ++a) {
-            const int c0 = 16 * (mt0 + a);
-            const v4s f2[2] = {tr_at(cur + (aoff[ks][0] + c0)), tr_at(cur + (aoff[ks][1] + c0))};
+            const v4s f2[2] = {tr_at(cur + (aoff[ks][0] + 16 * a)), tr_at(cur + (aoff[ks][1] + 16 * a))};
             fa[a] = *reinterpret_cast<const bf16x8*>(f2);
         }
 #pragma unroll
-        for (int bb = 0; bb < 9; ++bb) {
-            const int o = toff[bb];
-            const v4s f2[2] = {tr_at(win + (boff[ks][0] + o)), tr_at(win + (boff[ks][1] + o))};
-            const bf16x8 fb = *reinterpret_cast<const bf16x8*>(f2);
+        for (int kh = 0; kh < 3; ++kh) {
+            const lds_short* r0 = win + (boff[ks][0] + kh * wd_row);
+            const lds_short* r1 = win + (boff[ks][1] + kh * wd_row);
 #pragma unroll
-            for (int a = 0; a < 2; ++a)
-                acc[a][bb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[a], fb, acc[a][bb], 0, 0, 0);
+            for (int kw = 0; kw < 3; ++kw) {
+                const v4s f2[2] = {tr_at(r0 + kw * kARow), tr_at(r1 + kw * kARow)};
+                const bf16x8 fb = *reinterpret_cast<const bf16x8*>(f2);
+#pragma unroll
+                for (int a = 0; a < 2; ++a)
+                    acc[a][3 * kh + kw] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[a], fb, acc[a][3 * kh + kw], 0, 0, 0);
+            }
         }
     }
 }
@@ -349,11 +361,17 @@ __global__ __launch_bounds__(kWgThreads) void wgrad3x3_win_kernel(const __hip_bf
     extern __shared__ short lds_dyn[];
     lds_short* L = (lds_short*)lds_dyn;
     const int buf_elems = 32 * KS * kARow + g.npos * g.wrow;
+    WinSrc src;  // host: both buffers hold < 2^31 - 64 elements, so bytes + 16 < 2^32
+    src.xbytes = static_cast<unsigned>(int64_t(g.N) * g.H * g.W * g.Ci * 2);
+    src.dybytes = static_cast<unsigned>(g.GR * g.Wo * g.Co * 2);
+    src.x = __builtin_amdgcn_make_buffer_rsrc(const_cast<__hip_bfloat16*>(x), 0, static_cast<int>(src.xbytes), 0x00020000);
+    src.dy = __builtin_amdgcn_make_buffer_rsrc(const_cast<__hip_bfloat16*>(dy), 0, static_cast<int>(src.dybytes), 0x00020000);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int co0 = (blockIdx.x / g.ctiles) * kBM, ci0 = (blockIdx.x % g.ctiles) * kBC;
     const int c_begin = static_cast<int>(blockIdx.y * g.cps);
     const int c_end = static_cast<int>(c_begin + g.cps < g.chunks ? c_begin + g.cps : g.chunks);
     const int pr = tid >> 3, v = tid & 7;
+    const int mt0 = 2 * (wave & 1), cb = wave >> 1;  // this wave's output-channel tiles, input-channel block
 
     // this thread's window vectors (the same positions in every chunk; the vector's channel block
     // is v = tid & 7 for every j) and dy rows
@@ -398,16 +416,11 @@ __global__ __launch_bounds__(kWgThreads) void wgrad3x3_win_kernel(const __hip_bf
             // the window position of pixel k's tap (0, 0): its output row's first window row
             const int row0 = g.shared ? g.stride * rr + (3 - g.stride) * (rr / g.Ho) : 3 * rr;
             const int pos = k < g.KP ? row0 * g.Wd + cc * g.stride : 0;
-            aoff[ks][h] = k * kARow + 4 * (lane & 3);
-            boff[ks][h] = pos * g.wrow + 4 * (lane & 3);
+            // the wave's tiles: output channels 16 (mt0 + a), input channel block cb, all 9 taps
+            aoff[ks][h] = k * kARow + 4 * (lane & 3) + 16 * mt0;
+            boff[ks][h] = pos * kARow + 4 * (lane & 3) + 16 * cb;
         }
-    const int mt0 = 2 * (wave & 1), nt0 = 9 * (wave >> 1);
-    int toff[9];  // (tap, 16-channel block) tile nt0 + bb: tap window offset + channel block
-#pragma unroll
-    for (int bb = 0; bb < 9; ++bb) {
-        const int t = nt0 + bb, tap = t >> 2;
-        toff[bb] = ((tap / 3) * g.Wd + tap % 3) * g.wrow + 16 * (t & 3);
-    }
+    const int wd_row = g.Wd * kARow;
 
     f32x4v acc[2][9];
 #pragma unroll
@@ -416,31 +429,30 @@ __global__ __launch_bounds__(kWgThreads) void wgrad3x3_win_kernel(const __hip_bf
         for (int b = 0; b < 9; ++b) acc[a][b] = f32x4v{0.f, 0.f, 0.f, 0.f};
 
     WinStaging<NV, KS> st;
-    load_win<NV, KS>(st, x, dy, g, c_begin, apk, wpos, v, co0, ci0);
+    load_win<NV, KS>(st, src, g, c_begin, apk, wpos, v, co0, ci0);
     stage_win<NV, KS>(st, L, g, pr, v);
-    load_win<NV, KS>(st, x, dy, g, c_begin + 1 < c_end ? c_begin + 1 : c_begin, apk, wpos, v, co0, ci0);
+    load_win<NV, KS>(st, src, g, c_begin + 1 < c_end ? c_begin + 1 : c_begin, apk, wpos, v, co0, ci0);
     __syncthreads();
     for (int c = c_begin; c < c_end; ++c) {
         const int b = (c - c_begin) & 1;
         // chunk c + 1 into the other buffer (read last by chunk c - 1, before the barrier below
         // ended that iteration); on the last chunk this stages a clamped copy nobody reads
         stage_win<NV, KS>(st, L + (b ^ 1) * buf_elems, g, pr, v);
-        load_win<NV, KS>(st, x, dy, g, c + 2 < c_end ? c + 2 : c_end - 1, apk, wpos, v, co0, ci0);
+        load_win<NV, KS>(st, src, g, c + 2 < c_end ? c + 2 : c_end - 1, apk, wpos, v, co0, ci0);
         __builtin_amdgcn_sched_barrier(0);  // the loads ahead of the MFMAs
-        win_multiply<KS>(acc, L + b * buf_elems, aoff, boff, toff, mt0, nt0);
+        win_multiply<KS>(acc, L + b * buf_elems, aoff, boff, wd_row);
         __syncthreads();
     }
     float* o = out + int64_t(blockIdx.y) * int64_t(g.Co) * kTaps * g.Ci;
 #pragma unroll
     for (int a = 0; a < 2; ++a)
 #pragma unroll
-        for (int bb = 0; bb < 9; ++bb) {
-            const int t = nt0 + bb, tap = t >> 2;
-            const int ci = ci0 + 16 * (t & 3) + (lane & 15);
+        for (int tap = 0; tap < 9; ++tap) {
+            const int ci = ci0 + 16 * cb + (lane & 15);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int co = co0 + 16 * (mt0 + a) + 4 * (lane >> 4) + r;
-                o[(int64_t(co) * kTaps + tap) * g.Ci + ci] = acc[a][bb][r];
+                o[(int64_t(co) * kTaps + tap) * g.Ci + ci] = acc[a][tap][r];
             }
         }
 }
@@ -473,7 +485,7 @@ bool win_layout(int W, int Wo, int KT, bool shared, WinGeom& g) {
     if (shared && W >= (1 << 15)) return false;
     g.KT = KT;
     g.shared = shared ? 1 : 0;
-    g.wrow = g.stride == 1 ? kARow : kRow;
+    g.wrow = kARow;
     g.Wd = W + 2;
     // as many whole output rows as fit the tile (fewer if the window needs more vectors per thread
     // than kWinVecFast or more LDS than a CU has; with shared rows, R divides Ho or Ho divides R,
@@ -512,8 +524,10 @@ int g_wgrad_form = 0;  // dauc_set_wgrad_form: 0 automatic, 1 gather, 2 / 3 wind
 #endif
 
 bool win_geom(int64_t N, int H, int W, int Ci, int Ho, int Wo, int Co, int stride, WinGeom& g) {
-    // the window kernel indexes x and dy with 32-bit element offsets (and packs a column in 21 bits)
-    if (N * H * int64_t(W) * Ci >= (int64_t(1) << 31) || N * Ho * int64_t(Wo) * Co >= (int64_t(1) << 31)) return false;
+    // the window kernel reads x and dy through buffer descriptors with 32-bit byte offsets (an
+    // offset of `bytes` returns zeros, so bytes + 16 must not wrap) and packs a column in 21 bits
+    if (N * H * int64_t(W) * Ci >= (int64_t(1) << 31) - 64 || N * Ho * int64_t(Wo) * Co >= (int64_t(1) << 31) - 64)
+        return false;
     if (W >= (1 << 21)) return false;
     int form = 0;
 #ifdef DAUC_TUNING
