@@ -1,0 +1,24 @@
+#!/bin/bash
+# round 5: weight gradients on a side stream joined at the end of backward (wgrad_stream.py).
+# Bit-identity tests, the step / CoDA / graph tests, training-only runs with the side stream off
+# (DAUC_WGRAD_STREAM=0) and on, interleaved, and a kernel trace with it on.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+O=gpurun_out/${1:-r05ac}
+mkdir -p $O
+timeout -k 10 600 python -u -m pytest tests/test_wgrad_stream_gpu.py tests/test_weight_shadow_gpu.py tests/test_coda_gpu.py tests/test_conv1x1_gpu.py -x -q --timeout 300 --timeout-method thread \
+    > $O/pytest.log 2>&1
+rc=$?; echo "tests rc=$rc"; tail -2 $O/pytest.log
+[ $rc -eq 0 ] || exit $rc
+run() {  # name, env...
+    local name=$1; shift
+    env "$@" timeout -k 10 300 python3 bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-auc --no-surrogate \
+        --r18-steps 0 --sweep-I "" --eval-images 0 > $O/$name.json 2> $O/$name.err || return $?
+    python3 -c "import json;d=json.load(open('$O/$name.json'));print('$name', round(d['ms_per_step'],3), round(d['value'],1))"
+}
+run off1 DAUC_WGRAD_STREAM=0 || exit $?
+run on1 || exit $?
+run off2 DAUC_WGRAD_STREAM=0 || exit $?
+run on2 || exit $?
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o bench -- python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-auc --no-surrogate --r18-steps 0 --sweep-I "" --eval-images 0 > $O/bench_trace.log 2>&1 || exit $?
+echo done
