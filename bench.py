@@ -878,6 +878,23 @@ def self_launch(args) -> int | None:
     return subprocess.call(cmd, env=env)
 
 
+def gemm_selections(path: str) -> None:
+    """Read-only TunableOp selections for the 1x1 convolutions' GEMMs (scripts/tune_gemms.py: tuned
+    with every candidate checked against the default solution; the shipped file
+    distributedauc_amd/tunableop_gfx950.csv, profiles/r05/tunableop/); no tuning at run time, so every
+    rank and run uses the same solutions. DAUC_TUNABLEOP=0 (or a missing file): the default solutions.
+    The file's validators (torch, HIP, hipBLASLt, rocBLAS versions, gfx950) must match, else torch
+    ignores its entries."""
+    if not path or path == "0" or not os.path.exists(path):
+        return
+    import torch.cuda.tunable as tunable
+
+    tunable.enable(True)
+    tunable.tuning_enable(False)
+    tunable.set_filename(path)
+    tunable.read_file(path)
+
+
 def main():
     args = parse()
     if args.cpu_coda_worker:
@@ -907,6 +924,8 @@ def main():
         sys.exit(3)
     device = torch.device("cuda", local % max(ndev, 1))  # ranks share a device only in gloo rehearsals
     torch.cuda.set_device(device)
+    gemm_selections(os.environ.get("DAUC_TUNABLEOP", os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                                                    "distributedauc_amd", "tunableop_gfx950.csv")))
     quiet = None
     if use_group:
         if "MASTER_ADDR" not in os.environ:  # a --backend run at --gpus 1 outside a launcher
