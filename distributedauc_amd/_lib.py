@@ -90,6 +90,9 @@ SIGNATURES = {
     "dauc_conv7x7s2_stem_forward": (_int, [_vp, _vp, _int, _i64, _int, _int, _int, _int, _vp, _vp]),
     "dauc_conv7x7s2_stem_wgrad_workspace_size": (_sz, [_i64, _int, _int]),
     "dauc_conv7x7s2_stem_wgrad": (_int, [_vp, _vp, _int, _i64, _int, _int, _int, _int, _vp, _vp, _sz, _vp]),
+    "dauc_strided_pick": (_int, [_vp, _int, _i64, _int, _int, _int, _int, _vp, _vp]),
+    "dauc_strided_add": (_int, [_vp, _int, _i64, _int, _int, _int, _int, _vp, _vp]),
+    "dauc_broadcast_hw": (_int, [_vp, _int, _i64, _i64, _int, _vp, _vp]),
 }
 
 # tuning builds only (tuning/libdauc_tuning.so, -DDAUC_TUNING; include/dauc_tuning.h): measured

@@ -22,7 +22,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import _lib
-from .ops import _ptr, _stream, check
+from .ops import _ptr, _stream, check, strided_add_, strided_pick
 
 __all__ = ["conv1x1", "conv1x1_skip", "Conv1x1Function", "Conv1x1SkipFunction", "plans", "dump_plans"]
 
@@ -266,6 +266,27 @@ def _wgrad(gy, g2, x, wc, wdtype):
     return dw.view(cout, cin, 1, 1)
 
 
+def _cl_ok(t: torch.Tensor) -> bool:
+    return (t.is_cuda and t.dtype == torch.bfloat16 and t.dim() == 4 and t.shape[1] % 8 == 0
+            and t.is_contiguous(memory_format=torch.channels_last) and t.data_ptr() % 16 == 0)
+
+
+def _pick(x: torch.Tensor, s: int) -> torch.Tensor:
+    """x[:, :, ::s, ::s] as a channels-last tensor (csrc/strided.hip at HBM rate; torch's strided copy
+    ran at 2.9 TB/s)."""
+    if _cl_ok(x):
+        return strided_pick(x, s)
+    return x[:, :, ::s, ::s].contiguous(memory_format=torch.channels_last)
+
+
+def _add_strided(dx: torch.Tensor, src: torch.Tensor, s: int) -> None:
+    """dx[:, :, ::s, ::s] += src (csrc/strided.hip; the bits of torch's add_)."""
+    if _cl_ok(dx) and _cl_ok(src):
+        strided_add_(dx, src, s)
+    else:
+        dx[:, :, ::s, ::s].add_(src)
+
+
 class Conv1x1Function(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight):
@@ -335,7 +356,7 @@ class Conv1x1SkipFunction(torch.autograd.Function):
                     [bool(ctx.needs_input_grad[0]), bool(ctx.needs_input_grad[2]), False])
         elif gs is not None and wcd is not None:
             if strided:
-                xd = x[:, :, ::s, ::s].contiguous(memory_format=torch.channels_last)
+                xd = _pick(x, s)
             gyd, g2d = _prep_grad(gs, xd, wcd.shape[0])
         if ctx.needs_input_grad[0]:
             if gs is None:
@@ -360,7 +381,7 @@ class Conv1x1SkipFunction(torch.autograd.Function):
             if strided and gs is not None and dx_down is None:
                 if dx is None:
                     dx = torch.zeros_like(x, memory_format=torch.channels_last)
-                dx[:, :, ::s, ::s].add_(_dgrad(gyd, g2d, xd, wcd))
+                _add_strided(dx, _dgrad(gyd, g2d, xd, wcd), s)
         if ctx.needs_input_grad[1] and g1 is not None:
             dw1 = _wgrad(gy1, g21, x, wc1, ctx.wdtypes[0])
         if wcd is not None and ctx.needs_input_grad[2] and gs is not None:

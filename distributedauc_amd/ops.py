@@ -702,6 +702,48 @@ def stem_conv_supported(x: torch.Tensor, weight: torch.Tensor, stride, padding, 
             and (N * ((H - 1) // 2 + 1) * ((W - 1) // 2 + 1) + 128) * 64 < 2 ** 31)
 
 
+def _cl_bf16(t: torch.Tensor, name: str) -> None:
+    _require(t, name, torch.bfloat16)
+    if t.dim() != 4 or not t.is_contiguous(memory_format=torch.channels_last) or t.shape[1] % 8 or t.data_ptr() % 16:
+        raise ValueError(f"{name} must be a 16-byte aligned channels-last bf16 [N, C, H, W] tensor with C % 8 == 0")
+
+
+def strided_pick(x: torch.Tensor, stride: int) -> torch.Tensor:
+    """x[:, :, ::stride, ::stride] as a new channels-last tensor (dauc_strided_pick)."""
+    _cl_bf16(x, "x")
+    N, C, H, W = x.shape
+    out = torch.empty((N, C, (H - 1) // stride + 1, (W - 1) // stride + 1), dtype=x.dtype, device=x.device,
+                      memory_format=torch.channels_last)
+    check(_lib.load().dauc_strided_pick(_ptr(x), _lib.DTYPE_BF16, N, H, W, C, int(stride), _ptr(out),
+                                        _stream(x.device)), "dauc_strided_pick")
+    return out
+
+
+def strided_add_(dx: torch.Tensor, src: torch.Tensor, stride: int) -> torch.Tensor:
+    """dx[:, :, ::stride, ::stride] += src in place (dauc_strided_add; the bits of torch's add_)."""
+    _cl_bf16(dx, "dx")
+    _cl_bf16(src, "src")
+    N, C, H, W = dx.shape
+    if tuple(src.shape) != (N, C, (H - 1) // stride + 1, (W - 1) // stride + 1) or src.device != dx.device:
+        raise ValueError(f"src must be {[N, C, (H - 1) // stride + 1, (W - 1) // stride + 1]} on {dx.device}")
+    check(_lib.load().dauc_strided_add(_ptr(dx), _lib.DTYPE_BF16, N, H, W, C, int(stride), _ptr(src),
+                                       _stream(dx.device)), "dauc_strided_add")
+    return dx
+
+
+def broadcast_hw(g: torch.Tensor, H: int, W: int) -> torch.Tensor:
+    """g [N, C] (or [N, C, 1, 1]) broadcast to a channels-last [N, C, H, W] tensor (dauc_broadcast_hw)."""
+    _require(g, "g", torch.bfloat16)
+    N, C = g.shape[0], g.shape[1]
+    g2 = g.reshape(N, C).contiguous()
+    if C % 8 or g2.data_ptr() % 16:
+        raise ValueError("g must have C % 8 == 0")
+    out = torch.empty((N, C, H, W), dtype=g.dtype, device=g.device, memory_format=torch.channels_last)
+    check(_lib.load().dauc_broadcast_hw(_ptr(g2), _lib.DTYPE_BF16, N, H * W, C, _ptr(out), _stream(g.device)),
+          "dauc_broadcast_hw")
+    return out
+
+
 def set_wgrad_form(form: int) -> None:
     """The tuning build's 3x3 weight-gradient form (dauc_set_wgrad_form): 0 automatic, 1 gather, 2 / 3 window with 64- / 128-pixel chunks,
     4 / 5 the same with shared window rows."""
@@ -734,7 +776,7 @@ __all__ = [
     "surrogate_logits_fwdbwd", "class_sums_logits", "surrogate_status",
     "sort_keys", "auc_counts_sorted_labeled", "compact_positives", "mode_code", "workspaces", "set_search_mode",
     "set_direct_fault", "conv3x3_wgrad", "conv3x3_wgrad_supported", "stem_conv_forward", "stem_conv_wgrad",
-    "stem_conv_supported",
+    "stem_conv_supported", "strided_pick", "strided_add_", "broadcast_hw",
     "auc_eval_enqueue",
     "auc_slot_bytes",
     "auc_eval_compact_part",

@@ -445,6 +445,23 @@ size_t dauc_conv7x7s2_stem_wgrad_workspace_size(int64_t N, int Ho, int Wo);
 int dauc_conv7x7s2_stem_wgrad(const void* x, const void* dy, int dtype, int64_t N, int H, int W, int Ho, int Wo,
                               float* dw, void* workspace, size_t workspace_bytes, dauc_stream_t stream);
 
+/* ---------------------------------- backbone: strided and broadcast copies (channels-last bf16) */
+
+/*
+ * The strided 1x1 downsample's backward (conv1x1.py; resnet.py:87-108) and the average pool's
+ * gradient (resnet.py:214), bf16 (DAUC_DTYPE_BF16) channels-last, C a multiple of 8, 16-byte
+ * aligned pointers. Ho = (H - 1) / stride + 1, Wo = (W - 1) / stride + 1.
+ *   dauc_strided_pick:  out[n][i][j][:] = x[n][stride i][stride j][:]   (x [N, H, W, C], out [N, Ho, Wo, C])
+ *   dauc_strided_add:   dx[n][stride i][stride j][:] += src[n][i][j][:] (fp32 sum rounded to bf16,
+ *                       bit-identical to torch's add_ on the strided view)
+ *   dauc_broadcast_hw:  out[n][p][:] = g[n][:] for p < HW           (g [N, C], out [N, HW, C])
+ */
+int dauc_strided_pick(const void* x, int dtype, int64_t N, int H, int W, int C, int stride, void* out,
+                      dauc_stream_t stream);
+int dauc_strided_add(void* dx, int dtype, int64_t N, int H, int W, int C, int stride, const void* src,
+                     dauc_stream_t stream);
+int dauc_broadcast_hw(const void* g, int dtype, int64_t N, int64_t HW, int C, void* out, dauc_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif
