@@ -110,18 +110,24 @@ __device__ __forceinline__ void load_rows(RowStage& st, const unsigned short* __
     st.lohi = lohi;
 }
 
+// FAST: skip the masks when every lane's chunk lies wholly inside the image (a wave-uniform test;
+// the weight-gradient kernel: 181.5 -> 177.4 us; the forward measured slower with it)
+template <bool FAST>
 __device__ __forceinline__ void store_rows(const RowStage& st, lds_short* in) {
 #pragma unroll
     for (int u = 0; u < kChunkPer; ++u) {
         const int q = threadIdx.x + kThreads * u;
         if (q >= kChunks) break;
-        const int lo = (st.lohi >> (8 * u)) & 15, hi = (st.lohi >> (8 * u + 4)) & 15;
-        u32x4 v;
+        const unsigned lh = (st.lohi >> (8 * u)) & 0xff;
+        u32x4 v = st.c[u];
+        if (!FAST || !__all(lh == 0x80u)) {  // some lane's chunk is not wholly inside the image
+            const int lo = lh & 15, hi = lh >> 4;
 #pragma unroll
-        for (int d = 0; d < 4; ++d) {
-            const unsigned m = (((2 * d >= lo) & (2 * d < hi)) ? 0x0000ffffu : 0u) |
-                               (((2 * d + 1 >= lo) & (2 * d + 1 < hi)) ? 0xffff0000u : 0u);
-            v[d] = st.c[u][d] & m;
+            for (int d = 0; d < 4; ++d) {
+                const unsigned m = (((2 * d >= lo) & (2 * d < hi)) ? 0x0000ffffu : 0u) |
+                                   (((2 * d + 1 >= lo) & (2 * d + 1 < hi)) ? 0xffff0000u : 0u);
+                v[d] &= m;
+            }
         }
         const int kh = q / (kInRow / 8), k = q - kh * (kInRow / 8);
         *(lds_u32x4*)(in + (kh * kInRow + 8 * k)) = v;
@@ -177,7 +183,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
 #pragma unroll
         for (int s = 0; s < 6; ++s) kofs[s] = koff[s] + row_shift(g, n, oh, ow0, (32 * s + 8 * grp) / 24);
         __syncthreads();  // the previous task's reads of in / out are done
-        store_rows(st, in);
+        store_rows<false>(st, in);
         __syncthreads();
         if (t + static_cast<int>(gridDim.x) < g.tasks) load_rows(st, x, g, t + gridDim.x);  // in flight meanwhile
 #pragma unroll
@@ -292,7 +298,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
 #pragma unroll
         for (int i = 0; i < 3; ++i) bofs[i] = boff[i] + row_shift(g, n, oh, ow0, (16 * (wave + 4 * i) + col) / 24);
         __syncthreads();
-        store_rows(st, in);
+        store_rows<true>(st, in);
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const int q = tid + kThreads * u;
