@@ -63,6 +63,25 @@ struct StemGeom {
     int sgroups;  // wgrad: slab groups of the two-level slab sum (1: one level)
 };
 
+// this workgroup's tasks t = first, first + step, ... < end. Workgroups go to the 8 XCDs round
+// robin (blockIdx.x % 8), each with its own L2: XCD x takes the x-th eighth of the tasks, so the
+// tasks running at once on one XCD are consecutive output rows and share their input rows in that
+// L2 (a grid-stride order spread them over all 8: ~3.5 fetches of every input row from beyond L2)
+__device__ __forceinline__ void task_range(const StemGeom& g, int& first, int& end, int& step) {
+    const int G = static_cast<int>(gridDim.x), b = static_cast<int>(blockIdx.x);
+    if (G % 8 != 0) {
+        first = b;
+        end = g.tasks;
+        step = G;
+        return;
+    }
+    const int xcd = b % 8, per = G / 8;
+    const int lo = static_cast<int>(int64_t(g.tasks) * xcd / 8), hi = static_cast<int>(int64_t(g.tasks) * (xcd + 1) / 8);
+    first = lo + b / 8;
+    end = hi;
+    step = per;
+}
+
 __device__ __forceinline__ void task_coords(const StemGeom& g, int t, int& n, int& oh, int& ow0) {
     const int row = t / g.segs;
     ow0 = (t - row * g.segs) * kSeg;
@@ -155,9 +174,10 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
         const int kh = kp / 24, j = kp - kh * 24;
         wl[i] = (kh < 7 && j < 21) ? static_cast<short>(w[co * 147 + kh * 21 + j]) : short(0);
     }
-    int t = blockIdx.x;
+    int t, t_end, t_step;
+    task_range(g, t, t_end, t_step);
     RowStage st;
-    if (t < g.tasks) load_rows(st, x, g, t);
+    if (t < t_end) load_rows(st, x, g, t);
     __syncthreads();
     // A fragments: lane (grp, col) holds W'[16 ct + col][32 s + 8 grp .. + 7]
     bf16x8 wa[4][6];
@@ -175,7 +195,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
         koff[s] = (kp0 / 24) * kInRow + kp0 % 24;
     }
 
-    for (; t < g.tasks; t += gridDim.x) {
+    for (; t < t_end; t += t_step) {
         int n, oh, ow0;
         task_coords(g, t, n, oh, ow0);
         const int count = g.Wo - ow0 < kSeg ? g.Wo - ow0 : kSeg;
@@ -185,7 +205,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
         __syncthreads();  // the previous task's reads of in / out are done
         store_rows<false>(st, in);
         __syncthreads();
-        if (t + static_cast<int>(gridDim.x) < g.tasks) load_rows(st, x, g, t + gridDim.x);  // in flight meanwhile
+        if (t + t_step < t_end) load_rows(st, x, g, t + t_step);  // in flight meanwhile
 #pragma unroll
         for (int pi = 0; pi < 2; ++pi) {
             const int pt = wave + 4 * pi;  // pixel tile (wave-uniform)
@@ -282,15 +302,16 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
 #pragma unroll
         for (int i = 0; i < 3; ++i) acc[ct][i] = f32x4v{0.f, 0.f, 0.f, 0.f};
 
-    int t = blockIdx.x;
+    int t, t_end, t_step;
+    task_range(g, t, t_end, t_step);
     RowStage st;
     u32x4 d[4];
     unsigned dm = 0u;
-    if (t < g.tasks) {
+    if (t < t_end) {
         load_rows(st, x, g, t);
         dm = load_dy(d, dy, g, t);
     }
-    for (; t < g.tasks; t += gridDim.x) {
+    for (; t < t_end; t += t_step) {
         int n, oh, ow0;
         task_coords(g, t, n, oh, ow0);
         const int count = g.Wo - ow0 < kSeg ? g.Wo - ow0 : kSeg;
@@ -306,9 +327,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
             *(lds_u32x4*)(dyl + ((q >> 3) * kDyRow + 8 * (q & 7))) = u32x4{d[u][0] & m, d[u][1] & m, d[u][2] & m, d[u][3] & m};
         }
         __syncthreads();
-        if (t + static_cast<int>(gridDim.x) < g.tasks) {
-            load_rows(st, x, g, t + gridDim.x);
-            dm = load_dy(d, dy, g, t + gridDim.x);
+        if (t + t_step < t_end) {
+            load_rows(st, x, g, t + t_step);
+            dm = load_dy(d, dy, g, t + t_step);
         }
         for (int s = 0; 32 * s < count; ++s) {
             bf16x8 fa[4];
