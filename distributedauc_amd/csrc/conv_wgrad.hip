@@ -208,6 +208,21 @@ constexpr int kWinVecFast = 8;  // window vectors per thread that fit beside the
 // 80; it keeps 80 so that every tap's offset is one compile-time multiple of the row.)
 constexpr int kARow = 80;
 
+// (tile, split) of this workgroup. Workgroups go to the 8 XCDs round robin by linear id, each XCD
+// with its own L2; the tiles of one split read the same dy rows (same output-channel tile) or the
+// same input window (same input-channel tile), so when the split count allows, a split's tiles are
+// placed on one XCD (XCD x runs splits x, x + 8, ...) and share those reads in its L2.
+__device__ __forceinline__ void tile_split(int& tile, int& split) {
+    const int tiles = static_cast<int>(gridDim.x), splits = static_cast<int>(gridDim.y);
+    tile = static_cast<int>(blockIdx.x);
+    split = static_cast<int>(blockIdx.y);
+    if (tiles > 1 && splits % 8 == 0) {
+        const int b = tile + tiles * split, k = b / 8;
+        tile = k % tiles;
+        split = (k / tiles) * 8 + b % 8;
+    }
+}
+
 struct WinGeom {
     int N, H, W, Ci, Ho, Wo, Co, stride;
     int KT;    // pixel rows of the staged dy tile: 64 or 128 (2 or 4 k-steps per chunk)
@@ -367,8 +382,10 @@ __global__ __launch_bounds__(kWgThreads) void wgrad3x3_win_kernel(const __hip_bf
     src.x = __builtin_amdgcn_make_buffer_rsrc(const_cast<__hip_bfloat16*>(x), 0, static_cast<int>(src.xbytes), 0x00020000);
     src.dy = __builtin_amdgcn_make_buffer_rsrc(const_cast<__hip_bfloat16*>(dy), 0, static_cast<int>(src.dybytes), 0x00020000);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int co0 = (blockIdx.x / g.ctiles) * kBM, ci0 = (blockIdx.x % g.ctiles) * kBC;
-    const int c_begin = static_cast<int>(blockIdx.y * g.cps);
+    int tile, split;
+    tile_split(tile, split);
+    const int co0 = (tile / g.ctiles) * kBM, ci0 = (tile % g.ctiles) * kBC;
+    const int c_begin = static_cast<int>(split * g.cps);
     const int c_end = static_cast<int>(c_begin + g.cps < g.chunks ? c_begin + g.cps : g.chunks);
     const int pr = tid >> 3, v = tid & 7;
     const int mt0 = 2 * (wave & 1), cb = wave >> 1;  // this wave's output-channel tiles, input-channel block
@@ -443,7 +460,7 @@ __global__ __launch_bounds__(kWgThreads) void wgrad3x3_win_kernel(const __hip_bf
         win_multiply<KS>(acc, L + b * buf_elems, aoff, boff, wd_row);
         __syncthreads();
     }
-    float* o = out + int64_t(blockIdx.y) * int64_t(g.Co) * kTaps * g.Ci;
+    float* o = out + int64_t(split) * int64_t(g.Co) * kTaps * g.Ci;
 #pragma unroll
     for (int a = 0; a < 2; ++a)
 #pragma unroll
