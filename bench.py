@@ -53,6 +53,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+MFMA_BF16_PEAK_TFS = 2500.0  # MI355X_MICROARCH.md: ~2.5 PF bf16 dense MFMA (no sparsity)
 # VALU ceilings of the pair count (pairs/s per GPU). Vector fp32 rate = 256 CU x 4 SIMD x 32
 # lanes x 2.4 GHz = 7.86e13 lane-ops/s (157.3 TF / 2).
 #   packed: the cheapest exact sequence on gfx950, 3 fp32 lane-ops per pair (v_pk_add_f32,
@@ -124,6 +125,8 @@ def parse(argv=None):
                    help="bf16 conv weights from one shadow cast per forward (1), + the stride-1 3x3 input "
                         "gradients as forward convolutions with flipped weights (2), + the 3x3 weight gradients "
                         "from the HIP MFMA kernel (3), or autocast's cast per conv (0)")
+    p.add_argument("--bn-steps", type=int, default=3,
+                   help="last warm-up steps with HIP events around every fused BN call (step_roofline.bn; 0 = off)")
     p.add_argument("--gemm-conv1x1", type=int, default=1,
                    help="stride-1 1x1 convs as hipBLASLt GEMMs where faster (per-shape timing; 1/0)")
     # internal: one process of the configs[0] CPU baseline (never touches the GPU)
@@ -170,10 +173,11 @@ class KernelTimer:
     is the last parameter of every dauc_* entry point.
     """
 
-    def __init__(self, lib, name):
+    def __init__(self, lib, name, nbytes=None):
         self.lib, self.name = lib, name
         self.fn = getattr(lib, name)
         self.pairs = []
+        self.bytes = 0  # algorithmic bytes of the timed calls (nbytes(args) per call), when given
         self.enabled = False
         fn = self.fn
 
@@ -186,6 +190,8 @@ class KernelTimer:
             r = fn(*a)
             e1.record(s)
             self.pairs.append((e0, e1))
+            if nbytes is not None:
+                self.bytes += nbytes(a)
             return r
 
         setattr(lib, name, wrapped)
@@ -196,6 +202,71 @@ class KernelTimer:
     def mean_ms(self):
         torch.cuda.synchronize()
         return float(np.mean([a.elapsed_time(b) for a, b in self.pairs])) if self.pairs else float("nan")
+
+    def total_ms(self):
+        torch.cuda.synchronize()
+        return float(np.sum([a.elapsed_time(b) for a, b in self.pairs]))
+
+
+# ----------------------------------------------------------------------------- step roofline
+def _ival(v):
+    return int(getattr(v, "value", v) or 0)
+
+
+def _esize(dtype_code):
+    return 2 if _ival(dtype_code) == 2 else 4  # DAUC_DTYPE_BF16 = 2, DAUC_DTYPE_F32 = 1
+
+
+def bn_forward_bytes(a):
+    """Algorithmic HBM bytes of one dauc_bn_act_forward call (csrc/bn_act.hip's two passes): the
+    stats pass reads x; the apply pass reads x (+ residual) and writes y (+ the 1-bit ReLU mask, one
+    byte per 16-byte vector). Per-channel vectors are negligible. Args: include/dauc.h order."""
+    e, M, C = _esize(a[1]), _ival(a[2]), _ival(a[3])
+    act = M * C * e
+    residual, mask = _ival(a[4]) != 0, _ival(a[13]) != 0
+    return act + act + (act if residual else 0) + act + (act // 16 if mask else 0)
+
+
+def bn_backward_bytes(a):
+    """One dauc_bn_act_backward call: the reduce pass reads dy, the ReLU mask (or y) and x (and writes
+    dz = the residual's gradient when there is one); the dx pass reads dy + mask (or dz) and x and
+    writes dx."""
+    e, M, C = _esize(a[4]), _ival(a[5]), _ival(a[6])
+    act = M * C * e
+    relu, has_mask, has_y, dres = _ival(a[7]) != 0, _ival(a[2]) != 0, _ival(a[1]) != 0, _ival(a[11]) != 0
+    g_src = (act // 16 if has_mask else act if has_y else 0) if relu else 0  # what the ReLU mask costs
+    reduce = act + g_src + act + (act if dres else 0)
+    dx = (act if dres else act + g_src) + act + act
+    return reduce + dx
+
+
+def backbone_flops(arch: str, image_size: int, batch: int) -> dict:
+    """FLOP of one training step's convolutions and fc from the layer shapes (a forward on the meta
+    device with hooks): forward 2 MAC, weight gradient 2 MAC, input gradient 2 MAC except for the
+    stem (its input, the image, needs none). BN, pooling and the AUC kernels are not counted (they
+    are bandwidth work: bn_roofline / the update and loss kernels' rooflines)."""
+    from distributedauc_amd.backbone import build_backbone
+
+    with torch.device("meta"):
+        net = build_backbone(arch, num_classes=2)
+    macs = []
+
+    def hook(m, inp, out):
+        if isinstance(m, torch.nn.Conv2d):
+            kh, kw = m.kernel_size
+            macs.append((m is net.conv1, out.numel() * (m.in_channels // m.groups) * kh * kw))
+        elif isinstance(m, torch.nn.Linear):
+            macs.append((False, out.numel() * m.in_features))
+
+    hs = [m.register_forward_hook(hook) for m in net.modules() if isinstance(m, (torch.nn.Conv2d, torch.nn.Linear))]
+    with torch.no_grad():
+        net(torch.empty((batch, 3, image_size, image_size), device="meta"))
+    for h in hs:
+        h.remove()
+    fwd = sum(m for _, m in macs)
+    stem = sum(m for first, m in macs if first)
+    flop = 2 * fwd + 2 * fwd + 2 * (fwd - stem)
+    return {"forward_gmac": fwd / 1e9, "flop_per_step": flop, "layers": len(macs)}
 
 
 def grouped() -> bool:
@@ -268,10 +339,27 @@ def bench_train(args, world, rank, device):
     lib = _lib.load()
     upd = KernelTimer(lib, "dauc_pd_update")
     sur = KernelTimer(lib, "dauc_surrogate_fwdbwd")
-    for _ in range(args.warmup):
+    # the step's BN kernels (csrc/bn_act.hip) timed by HIP events around every call during the last
+    # warm-up steps (an event pair per call is host work the timed steps must not pay; the first
+    # warm-up step compiles and tunes, so it is never in the window)
+    nbn = min(args.bn_steps, max(args.warmup - 1, 0)) if (args.fused_bn and not args.graph) else 0
+    bnf = KernelTimer(lib, "dauc_bn_act_forward", bn_forward_bytes)
+    bnb = KernelTimer(lib, "dauc_bn_act_backward", bn_backward_bytes)
+    for i in range(args.warmup):
+        if i == args.warmup - nbn:
+            torch.cuda.synchronize()
+            bnf.enabled = bnb.enabled = True
         x, y = next(it)
         coda.train_step(x, y)
+    bnf.enabled = bnb.enabled = False
+    bnf.restore()
+    bnb.restore()
     torch.cuda.synchronize()
+    bn = None
+    if nbn > 0:
+        bn = {"steps": nbn, "fwd_ms": bnf.total_ms() / nbn, "bwd_ms": bnb.total_ms() / nbn,
+              "calls_per_step": (len(bnf.pairs) + len(bnb.pairs)) / nbn,
+              "bytes_per_step": (bnf.bytes + bnb.bytes) / nbn}
     log(f"rank {rank}: warm-up done")
     upd.enabled = sur.enabled = True
     dt = timed_steps(coda, it, args.steps, world)
@@ -284,7 +372,7 @@ def bench_train(args, world, rank, device):
         "update_ms": upd.mean_ms(), "update_bytes": coda.state.bytes_per_update(True),
         "surrogate_us": (sur.mean_ms() * 1e3) if sur.pairs else None,  # inside the graph: not timed
         "payload_bytes": coda.state.n_reduce * 4, "graph": bool(coda._graph_on),
-        "graph_captures": coda.graph_captures,
+        "graph_captures": coda.graph_captures, "bn": bn,
     }
     if args.sweep_I:
         out["period_sweep"] = bench_period_sweep(coda, it, args, world)
@@ -558,7 +646,13 @@ def auc_record(auc, world, config_name):
                     "range, one all-gather of the 8-word part records; replicated = every rank evaluates the whole "
                     "vector, below 2^24 scores); pair count: positive blocks, int64 all-reduce",
         "sort_mode": sk["mode"],
-        "pairs_per_sec": npairs / sk["t_eval"],
+        # north_star's pair-compare throughput: the pair-count kernel, which compares every
+        # positive with every negative (its roofline below)
+        "pair_compare_per_sec": pc_rate,
+        # the sort method enumerates no pairs: P*N / its wall time is an EFFECTIVE rate only
+        "effective_pairs_per_sec": npairs / sk["t_eval"],
+        "effective_pairs_what": "P*N / the sort method's evaluation wall time: it locates each negative among the "
+                                "positives and compares no pairs, so this exceeds any pair-compare ceiling",
         "method": "sort (default evaluator: compact the positives reading labels only, build the LDS count index "
                   "straight from them with the table size read on the device (cell-ordered table, no sort), locate "
                   "every negative, read in place, through it -- all enqueued with no host sync; one readback per "
@@ -667,6 +761,37 @@ def bench_surrogate(args, device):
                                 "once (variant 22)",
             "row_reduce_us": (ms - tail_stream_ms) * 1e3,
             "row_reduce_what": "whole call - variant 22: the in-launch hand-off chain after the last row lands"}
+
+
+def step_roofline(args, res) -> dict:
+    """The roofline of what `value` measures: the whole training step against the bf16 dense MFMA
+    peak (convolution + fc FLOP from the layer shapes), and its BN passes against HBM (bytes per call
+    from bn_forward_bytes / bn_backward_bytes, time by HIP events around every BN call in
+    res["bn"]'s window of warm-up steps) -- VERDICT r05 #2."""
+    ms = res["dt"] / args.steps * 1e3
+    fl = backbone_flops(args.arch, args.image_size, args.batch)
+    tf = fl["flop_per_step"] / (ms / 1e3) / 1e12
+    rec = {"bound": "mfma", "flop_per_step": fl["flop_per_step"], "forward_gmac": fl["forward_gmac"],
+           "achieved": tf, "peak": MFMA_BF16_PEAK_TFS, "unit": "TFLOP/s", "frac": tf / MFMA_BF16_PEAK_TFS,
+           "per_rank": True,
+           "what": f"{args.arch} b{args.batch} {args.image_size}^2 per rank: conv + fc FLOP (forward 2 MAC, weight "
+                   "gradient 2 MAC, input gradient 2 MAC except the stem's) / ms_per_step, against the bf16 dense "
+                   "MFMA peak (MI355X_MICROARCH.md); the step also runs BN, pooling and the AUC kernels, which are "
+                   "HBM work (bn below; roofline = the update kernel)"}
+    bn = res.get("bn")
+    if bn:
+        bms = bn["fwd_ms"] + bn["bwd_ms"]
+        gbs = bn["bytes_per_step"] / (bms / 1e3) / 1e9 if bms > 0 else float("nan")
+        rec["bn"] = {"bound": "hbm", "bytes_per_step": bn["bytes_per_step"], "ms_per_step": bms,
+                     "fwd_ms": bn["fwd_ms"], "bwd_ms": bn["bwd_ms"], "calls_per_step": bn["calls_per_step"],
+                     "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
+                     "share_of_step": bms / ms, "steps_timed": bn["steps"],
+                     "what": "fused BN + add + ReLU (csrc/bn_act.hip): algorithmic bytes of its two passes each way "
+                             "(forward: stats read x, apply read x [+ residual] write y [+ 1-bit mask]; backward: reduce "
+                             "read dy + mask + x [write dz], dx read dy + mask | dz + x write dx) / the summed HIP-event "
+                             "time of every BN call (all its launches, finalizes included), in a window of "
+                             f"the last {bn['steps']} warm-up steps (untimed)"}
+    return rec
 
 
 # ----------------------------------------------------------------------------- CPU baselines
@@ -956,7 +1081,10 @@ def main():
             out.update({
                 "value": res["imgs"] / res["dt"], "unit": "imgs/sec", "n_gpus": world, "steps": args.steps,
                 "warmup": args.warmup, "ms_per_step": res["dt"] / args.steps * 1e3, "higher_is_better": True,
-                "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+                "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "auc_kernels_dtype": "f32",
+                "dtype_what": "bf16 = the backbone's arithmetic (autocast convolutions / GEMMs, fp32 accumulation, "
+                              "fp32 master weights); the AUC loss, update and exact-AUC kernels compute in fp32",
+                "data": "synthetic",
                 "config": {"workload": f"{args.arch} CoDA, bf16 autocast backbone"
                                        f"{' (fused BN+add+ReLU kernels)' if args.fused_bn else ''}"
                                        f"{' (1x1 convs as GEMMs)' if args.gemm_conv1x1 else ''}, fp32 AUC kernels "
@@ -968,6 +1096,7 @@ def main():
                              "achieved": upd_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                              "frac": upd_gbs / HBM_PEAK_GBS, "traffic": load_traffic("pd_update"),
                              "bytes_per_launch": res["update_bytes"], "avg_launch_us": res["update_ms"] * 1e3},
+                "step_roofline": step_roofline(args, res),
                 "surrogate_us_per_call": res["surrogate_us"],
                 "step_graph": {"replayed": res["graph"], "captures": res["graph_captures"],
                                "what": "label map -> forward -> surrogate -> backward replayed from one HIP graph; "

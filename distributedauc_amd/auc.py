@@ -27,9 +27,13 @@ against the slot the next rank compacted from it, and of the length every slot w
 built for. The result does not depend on G. A mismatch raises RuntimeError on every
 rank together, after the collective; the scores are not compared across ranks.
 
-Error behaviour mirrors sklearn: non-finite scores raise ValueError; labels
-with more than two distinct values raise ValueError; a single class returns NaN
-with a warning.
+Error behaviour mirrors sklearn 1.7.2's roc_curve(pos_label=1): non-finite scores
+raise ValueError; every label other than 1 is a negative, whatever the number of
+distinct label values (sklearn accepts a "multiclass" y_true when pos_label is
+given: {-1, 0, 1} scores as {negative, negative, positive}); non-integer float
+labels raise ValueError ("continuous format is not supported"); a single class
+returns NaN with a warning. The kernels count the labels outside {-1, 1}
+("other"), which is reported, not an error.
 """
 from __future__ import annotations
 
@@ -61,6 +65,9 @@ def _as_device_pair(label, scores, device):
         y = label.detach().to(dev).reshape(-1)
     else:
         y = torch.as_tensor(np.asarray(label).reshape(-1), device=dev)
+    if y.dtype.is_floating_point and y.numel() and not bool((y == y.round()).all()):
+        # sklearn's type_of_target: non-integer float labels are "continuous" (_ranking.py:826's check)
+        raise ValueError("continuous format is not supported")
     if y.dtype not in (torch.int8, torch.int32, torch.int64):
         y = y.to(torch.int64)
     return y.contiguous(), s
@@ -133,13 +140,7 @@ class ExactAUC:
             W, T, _ = (int(v) for v in wt.tolist())
         if nonfinite:
             raise ValueError("Input y_score contains NaN or infinity.")
-        self._check_labels(other, y)
-        return {"wins": W, "ties": T, "P": P, "N": N}
-
-    @staticmethod
-    def _check_labels(other: int, y: torch.Tensor) -> None:
-        if other and torch.unique(y).numel() > 2:
-            raise ValueError("multiclass format is not supported")
+        return {"wins": W, "ties": T, "P": P, "N": N, "other": other}
 
     def _counts_sort(self, y: torch.Tensor, s: torch.Tensor) -> dict:
         """The sort method. One GPU (or a vector below ``shard_min``, which every rank evaluates
@@ -160,8 +161,7 @@ class ExactAUC:
             W, T, P, N, nonfinite, other = ops.auc_eval_counts(s, y)
             if nonfinite:
                 raise ValueError("Input y_score contains NaN or infinity.")
-            self._check_labels(other, y)
-            return {"wins": W, "ties": T, "P": P, "N": N}
+            return {"wins": W, "ties": T, "P": P, "N": N, "other": other}
         self.last_mode = "sharded"
         n = s.numel()
         rec = self._part_counts.get(s.device)
@@ -193,15 +193,16 @@ class ExactAUC:
                                    "rank must pass the same scores and labels")
         P, nonfinite, other = vals[0][3], vals[0][5], vals[0][6]
         verdicts = {v[7] for v in vals} - {0}
+        # every label other than 1 is a negative (pos_label=1), and word 4 above has checked that
+        # every rank holds this n and these labels: N = n - P on every rank
         N = n - P
         if nonfinite or sum(v[2] for v in vals):
             raise ValueError("Input y_score contains NaN or infinity.")
-        self._check_labels(other, y)
         if P == 0 or N == 0:
-            return {"wins": 0, "ties": 0, "P": P, "N": N}
+            return {"wins": 0, "ties": 0, "P": P, "N": N, "other": other}
         if 2 in verdicts:
-            return self._counts_sort_sorted_path(y, s)
-        return {"wins": sum(v[0] for v in vals), "ties": sum(v[1] for v in vals), "P": P, "N": N}
+            return dict(self._counts_sort_sorted_path(y, s), other=other)
+        return {"wins": sum(v[0] for v in vals), "ties": sum(v[1] for v in vals), "P": P, "N": N, "other": other}
 
     def _slots_of(self, device, n: int):
         """(this rank's slot, the gathered slots) for n scores: uint8 device buffers, 256-byte

@@ -14,6 +14,8 @@ state_dict path.
 """
 from __future__ import annotations
 
+import weakref
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
@@ -50,25 +52,29 @@ _shadow_live: list = []  # the shadow of the forward in flight (set by ResNet.fe
 class WeightShadow:
     """bf16 copies of a FlatState's parameters at the same offsets (views per conv weight), and,
     with ``dgrad_fwd``, each stride-1 'same' k x k convolution's weight flipped and transposed
-    (W'[ci, co, kh, kw] = W[co, ci, k-1-kh, k-1-kw], channels-last) for its input gradient."""
+    (W'[ci, co, kh, kw] = W[co, ci, k-1-kh, k-1-kw], channels-last) for its input gradient.
+
+    Two buffer sets, used by alternate forwards: the convolutions save views of the shadow for
+    their backward, so refreshing the set a pending backward still holds would trip autograd's
+    in-place check. With two, two grad-enabled forwards may precede one backward (summed losses
+    over two micro-batches or two views); a third forward before that backward reuses the first
+    set and autograd raises (never silently stale weights)."""
 
     def __init__(self, model: nn.Module, dgrad_fwd: bool = False, wgrad_hip: bool = False):
         flat = getattr(model, "_dauc_flat", None)
         if flat is None:
             raise RuntimeError("the weight shadow mirrors the FlatState buffer: build CoDA / FlatState first")
         self.src = flat.params
+        self._model = weakref.ref(model)
         self.wgrad_hip = bool(wgrad_hip)
         dev = self.src.device
-        self.buf = torch.empty(self.src.numel(), dtype=torch.bfloat16, device=dev)
-        self.views: dict[int, torch.Tensor] = {}
-        self.flips: dict[int, torch.Tensor] = {}
         convs = {id(m.weight): m for m in model.modules() if isinstance(m, nn.Conv2d)}
-        idx, foff = [], 0
+        idx, foff, vspec, fspec = [], 0, {}, {}
         for _, p, off, _n in flat.entries:
             m = convs.get(id(p))
             if m is None:
                 continue
-            self.views[id(p)] = torch.as_strided(self.buf, p.shape, p.stride(), off)
+            vspec[id(p)] = (p.shape, p.stride(), off)
             if dgrad_fwd and _dgrad_as_fwd_ok(m):
                 co, ci, k, _ = p.shape
                 s0, s1, s2, s3 = p.stride()
@@ -76,17 +82,32 @@ class WeightShadow:
                 src = (off + torch.arange(co).view(1, co, 1, 1) * s0 + torch.arange(ci).view(ci, 1, 1, 1) * s1
                        + (k - 1 - r).view(1, 1, k, 1) * s2 + (k - 1 - r).view(1, 1, 1, k) * s3)  # [ci, co, kh, kw]
                 idx.append(src.permute(0, 2, 3, 1).reshape(-1))  # channels-last storage order (ci, kh, kw, co)
-                self.flips[id(p)] = (foff, (ci, co, k, k), (k * k * co, 1, k * co, co))
+                fspec[id(p)] = ((ci, co, k, k), (k * k * co, 1, k * co, co), foff)
                 foff += p.numel()
-        self.fbuf = torch.empty(foff, dtype=torch.bfloat16, device=dev) if foff else None
         # int32 gather indices (ResNet-50: 11 M of them; int64 would double the bytes read per refresh)
         self.fidx = torch.cat(idx).to(device=dev, dtype=torch.int32) if idx else None
-        for key, (o, shape, stride) in list(self.flips.items()):
-            self.flips[key] = torch.as_strided(self.fbuf, shape, stride, o)
+        self._sets = []
+        for _ in range(2):
+            buf = torch.empty(self.src.numel(), dtype=torch.bfloat16, device=dev)
+            fbuf = torch.empty(foff, dtype=torch.bfloat16, device=dev) if foff else None
+            views = {k: torch.as_strided(buf, sh, st, o) for k, (sh, st, o) in vspec.items()}
+            flips = {k: torch.as_strided(fbuf, sh, st, o) for k, (sh, st, o) in fspec.items()}
+            self._sets.append((buf, fbuf, views, flips))
+        self._cur = 1
+        self.buf, self.fbuf, self.views, self.flips = self._sets[0]
 
     def refresh(self, flips: bool = True) -> None:
-        """One cast launch: bf16(params) -> the shadow (stream-ordered after the last update); with
-        the flipped weights, one gather launch more."""
+        """Switch to the other buffer set, then one cast launch: bf16(params) -> the shadow
+        (stream-ordered after the last update); with the flipped weights, one gather launch more."""
+        m = self._model()
+        flat = getattr(m, "_dauc_flat", None) if m is not None else None
+        if flat is None or flat.params is not self.src:
+            # a later FlatState moved the parameters into another buffer: this shadow would mirror
+            # the old one and every bf16 forward would read stale weights (ADVICE r05)
+            raise RuntimeError("weight shadow is stale: the model's parameters moved to a new FlatState; call "
+                               "model.set_weight_shadow(...) again after building it (CoDA does)")
+        self._cur ^= 1
+        self.buf, self.fbuf, self.views, self.flips = self._sets[self._cur]
         self.buf.copy_(self.src)
         if flips and self.fbuf is not None:
             torch.index_select(self.buf, 0, self.fidx, out=self.fbuf)
@@ -148,7 +169,7 @@ class _ShadowConv(torch.autograd.Function):
         stride, padding, dilation, groups = ctx.conf
         nx, nw = bool(ctx.needs_input_grad[0]), bool(ctx.needs_input_grad[1])
         dx = dw = None
-        if nw and ctx.stem:
+        if nw and ctx.stem and gy.dtype == torch.bfloat16:
             from . import ops
 
             dw = ops.stem_conv_wgrad(x, gy.contiguous(memory_format=torch.channels_last))

@@ -67,8 +67,10 @@ class CoDA:
         # cast once per forward (backbone.WeightShadow) instead of one cast launch per convolution
         if weight_shadow is None:
             weight_shadow = autocast_dtype == torch.bfloat16 and hasattr(model, "set_weight_shadow")
-        if weight_shadow:
-            model.set_weight_shadow(True)
+        if hasattr(model, "set_weight_shadow"):
+            # always (re)set: this FlatState moved the parameters into a new buffer, so a shadow
+            # left by an earlier CoDA / FlatState would mirror the old one
+            model.set_weight_shadow(bool(weight_shadow))
         self.max_exact_count = max_exact_count
         self.t_total = 0
         self.stage = 0

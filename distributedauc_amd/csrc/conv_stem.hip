@@ -189,10 +189,16 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
     // this lane's k' offset into the staged rows per k-step: row kh, element j0 of the pixel's run
     // (+ the row's shift, per task)
     int koff[6];
+    // bit s: this lane's 8 k' of k-step s are j = 16 .. 23 of a row, whose last three (j >= 21) are
+    // the input column just right of the 7-wide window. Their weights are zero, but 0 x Inf is NaN:
+    // those B elements are zeroed so a non-finite neighbour cannot reach the output (torch's 7x7
+    // conv never reads it)
+    unsigned jtail = 0u;
 #pragma unroll
     for (int s = 0; s < 6; ++s) {
         const int kp0 = 32 * s + 8 * grp;
         koff[s] = (kp0 / 24) * kInRow + kp0 % 24;
+        jtail |= (kp0 % 24 == 16 ? 1u : 0u) << s;
     }
 
     for (; t < t_end; t += t_step) {
@@ -221,8 +227,10 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
                 const lds_u32* p = (const lds_u32*)(in + (e & ~1));
                 const unsigned sb = (e & 1) * 16;
                 const unsigned w0 = p[0], w1 = p[1], w2 = p[2], w3 = p[3], w4 = p[4];
+                const bool tail = (jtail >> s) & 1u;
                 const u32x4 v = {__builtin_amdgcn_alignbit(w1, w0, sb), __builtin_amdgcn_alignbit(w2, w1, sb),
-                                 __builtin_amdgcn_alignbit(w3, w2, sb), __builtin_amdgcn_alignbit(w4, w3, sb)};
+                                 __builtin_amdgcn_alignbit(w3, w2, sb) & (tail ? 0x0000ffffu : 0xffffffffu),
+                                 tail ? 0u : __builtin_amdgcn_alignbit(w4, w3, sb)};
                 const bf16x8 b = __builtin_bit_cast(bf16x8, v);
 #pragma unroll
                 for (int ct = 0; ct < 4; ++ct) acc[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[ct][s], b, acc[ct], 0, 0, 0);

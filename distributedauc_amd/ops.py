@@ -695,7 +695,10 @@ def stem_conv_supported(x: torch.Tensor, weight: torch.Tensor, stride, padding, 
     d = tuple(dilation) if isinstance(dilation, (tuple, list)) else (dilation, dilation)
     if not (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4 and x.shape[1] == 3 and groups == 1
             and tuple(weight.shape) == (64, 3, 7, 7) and s == (2, 2) and p == (3, 3) and d == (1, 1)
-            and x.is_contiguous(memory_format=torch.channels_last)):
+            and x.is_contiguous(memory_format=torch.channels_last)
+            # the kernels read a channels-last bf16 weight; an NCHW model (build_backbone's default)
+            # fed channels-last images takes F.conv2d instead
+            and weight.dtype == torch.bfloat16 and weight.is_contiguous(memory_format=torch.channels_last)):
         return False
     N, _, H, W = x.shape
     return (x.data_ptr() % 16 == 0 and N * H * W * 3 < 2 ** 31

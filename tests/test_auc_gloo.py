@@ -43,6 +43,19 @@ def _worker(rank, world, port, q, shard_min):
         assert ev.last_mode == ("sharded" if n >= shard_min else "replicated"), ev.last_mode
         e = coracle.auc_counts(y.astype(np.int64), s)
         assert (c["wins"], c["ties"], c["P"], c["N"]) == (e["wins"], e["ties"], e["P"], e["N"]), (c, e)
+        # labels beyond {-1, 1}: sklearn's roc_curve(pos_label=1) takes every label other than 1 as a
+        # negative ("multiclass" y_true is accepted when pos_label is given), so the counts, and the
+        # AUC, are sklearn's; "other" reports how many labels lay outside {-1, 1}
+        ym = y.astype(np.int32)
+        ym[::7] = 0
+        ym[3::11] = 2
+        cm = ev.counts(torch.from_numpy(ym), torch.from_numpy(s), device="cpu")
+        em = coracle.auc_counts(ym.astype(np.int64), s)
+        assert (cm["wins"], cm["ties"], cm["P"], cm["N"]) == (em["wins"], em["ties"], em["P"], em["N"]), (cm, em)
+        assert cm["other"] == int(((ym != 1) & (ym != -1)).sum())
+        from oracle import reference_cpu as R
+
+        assert abs(ExactAUC.from_counts(cm) - R.auc_sklearn(ym, s)) <= 1e-12
         # a non-finite negative in one rank's slice is seen by every rank after the reduce
         s2 = s.copy()
         s2[np.flatnonzero(y == -1)[-3]] = np.nan

@@ -90,3 +90,29 @@ def test_shipped_conv1x1_plans_load():
     finally:
         C.plans.clear()
         C.plans.update(saved)
+
+
+def test_step_roofline_helpers():
+    """the step's FLOP from the layer shapes (ResNet-50 b256 224^2: 4.09 GMAC per image
+    forward; 3 x 2 MAC per step except the stem's input gradient) and the fused BN calls' bytes."""
+    import ctypes
+
+    import bench
+
+    f = bench.backbone_flops("resnet50", 224, 256)
+    assert abs(f["forward_gmac"] / 256 - 4.087) < 0.01
+    stem = 256 * 112 * 112 * 64 * 3 * 49
+    assert f["flop_per_step"] == 6 * int(f["forward_gmac"] * 1e9 + 0.5) - 2 * stem
+    vp = ctypes.c_void_p
+    M, C = 1000, 64
+    act = M * C * 2
+    # forward: x (stats) + x, residual, y (apply) + mask
+    fwd = [vp(1), 2, M, C, vp(1), 1, vp(1), vp(1), vp(1), vp(1), 0.1, 1e-5, vp(1), vp(1), vp(1), vp(1), vp(1), 0, vp(1)]
+    assert bench.bn_forward_bytes(fwd) == 4 * act + act // 16
+    fwd[4], fwd[13] = vp(0), vp(0)  # no residual, no mask
+    assert bench.bn_forward_bytes(fwd) == 3 * act
+    # backward with the mask and a residual gradient: reduce dy + mask + x + dz, dx pass dz + x + dx
+    bwd = [vp(1), vp(0), vp(1), vp(1), 2, M, C, 1, vp(1), vp(1), vp(1), vp(1), vp(1), vp(1), vp(1), vp(1), 0, vp(1)]
+    assert bench.bn_backward_bytes(bwd) == (3 * act + act // 16) + 3 * act
+    bwd[11] = vp(0)  # no residual: both passes read dy + mask + x, the second writes dx
+    assert bench.bn_backward_bytes(bwd) == 2 * (2 * act + act // 16) + act

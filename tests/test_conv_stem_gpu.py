@@ -110,3 +110,28 @@ def test_stem_rejects_unsupported(dev):
     assert ops.stem_conv_supported(x, w, 2, 3, 1, 1)
     assert not ops.stem_conv_supported(x, w, 1, 3, 1, 1)
     assert not ops.stem_conv_supported(x.contiguous(), w, 2, 3, 1, 1)
+    assert not ops.stem_conv_supported(x, w.contiguous(), 2, 3, 1, 1)  # NCHW weight
+    assert not ops.stem_conv_supported(x, w.float().contiguous(memory_format=torch.channels_last), 2, 3, 1, 1)
+
+
+@pytest.mark.parametrize("col", [4, 12, 13, 31])
+@pytest.mark.parametrize("val", [float("inf"), float("-inf"), float("nan")])
+def test_stem_forward_nonfinite_neighbour(dev, col, val):
+    """the forward pads each row's 21 window elements to 24 with zero weights; the
+    three padded lanes hold the input column just right of the window (2 ow + 4). A non-finite
+    value there must not reach that output (0 x Inf = NaN), as in torch's convolution: the set of
+    non-finite outputs equals the fp64 reference's, and the finite ones match it as in
+    test_stem_forward_matches_fp64. Every channel of the column and the image's last column."""
+    from distributedauc_amd import ops
+
+    x, w, _ = _inputs(dev, 2, 32, 32, 17 + col)
+    for ch in range(3):
+        x[1, ch, 5 + 7 * ch, col] = val
+    y = ops.stem_conv_forward(x, w)
+    ref = F.conv2d(x.cpu().double(), w.cpu().double(), stride=2, padding=3)
+    yc = y.cpu().double()
+    assert torch.equal(torch.isfinite(yc), torch.isfinite(ref))
+    assert int((~torch.isfinite(ref)).sum()) > 0
+    fin = torch.isfinite(ref)
+    err = (yc[fin] - ref[fin]).abs()
+    assert float((err - ref[fin].abs() * 2 ** -8).max()) <= 1e-5 * float(ref[fin].abs().max())

@@ -144,3 +144,87 @@ def test_weight_shadow_dgrad_fwd_step_close(dev):
     ea, eb = np.array(ea), np.array(eb)
     assert np.median(eb) <= 1.5 * np.median(ea) + 1e-3, (np.median(eb), np.median(ea))
     assert eb.max() <= 2.0 * ea.max() + 1e-2, (eb.max(), ea.max())
+
+
+def test_nchw_model_channels_last_input_default_coda(dev):
+    """an NCHW model (build_backbone's default) fed channels-last images under default
+    CoDA (bf16 autocast: the shadow and the HIP weight-gradient paths on) trains: the stem kernels
+    take only a channels-last bf16 weight, so the stem falls back to F.conv2d instead of raising."""
+    from distributedauc_amd import ops
+    from distributedauc_amd.backbone import build_backbone
+    from distributedauc_amd.coda import CoDA
+
+    torch.manual_seed(3)
+    net = build_backbone("resnet18", num_classes=2).to(dev).set_fused_bn(True).train()
+    coda = CoDA(net, lr=0.01, split_index=4, autocast_dtype=torch.bfloat16, device=dev)
+    assert net._wshadow is not None and net._wshadow.wgrad_hip
+    wb = net._wshadow.weight(net.conv1.weight)
+    assert not ops.stem_conv_supported(torch.zeros((2, 3, 32, 32), device=dev, dtype=torch.bfloat16).contiguous(
+        memory_format=torch.channels_last), wb, (2, 2), (3, 3), (1, 1), 1)
+    g = torch.Generator(device=dev).manual_seed(2)
+    x = torch.randn((8, 3, 32, 32), device=dev, generator=g).contiguous(memory_format=torch.channels_last)
+    y = torch.tensor([9, 0, 7, 1, 5, 3, 8, 2], device=dev)
+    loss = coda.train_step(x, y)
+    loss2 = coda.train_step(x, y)
+    torch.cuda.synchronize()
+    assert np.isfinite(float(loss)) and np.isfinite(float(loss2))
+    assert bool(torch.isfinite(coda.state.flat).all())
+
+
+def test_shadow_follows_new_flat_state(dev):
+    """a second CoDA on the same model moves the parameters into a new FlatState; its
+    weight_shadow=False must turn the old shadow off, and a shadow left mirroring an old buffer
+    raises at the next forward instead of reading stale weights."""
+    from distributedauc_amd.backbone import build_backbone
+    from distributedauc_amd.coda import CoDA
+    from distributedauc_amd.flat import FlatState
+
+    torch.manual_seed(4)
+    net = build_backbone("resnet18", num_classes=2).to(dev).to(memory_format=torch.channels_last)
+    net.set_fused_bn(True).train()
+    CoDA(net, lr=0.01, split_index=4, autocast_dtype=torch.bfloat16, device=dev)
+    assert net._wshadow is not None
+    CoDA(net, lr=0.01, split_index=4, autocast_dtype=torch.bfloat16, device=dev, weight_shadow=False)
+    assert net._wshadow is None
+    coda = CoDA(net, lr=0.01, split_index=4, autocast_dtype=torch.bfloat16, device=dev)
+    assert net._wshadow is not None and net._wshadow.src is coda.state.params
+    FlatState(net, dev)  # parameters move again, the shadow is not rebuilt
+    x = torch.randn((4, 3, 32, 32), device=dev).contiguous(memory_format=torch.channels_last)
+    with pytest.raises(RuntimeError, match="stale"):
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            net(x)
+
+
+def test_two_forwards_one_backward(dev):
+    """two grad-enabled forwards before one backward (a loss summed over two
+    micro-batches) work with the shadow on -- each forward refreshes the other buffer set, so the
+    views the first forward saved are intact -- and give the same gradients, bit for bit, as the
+    same two forwards without the shadow (torch's backward: dgrad_fwd and wgrad_hip off,
+    deterministic solvers, the GEMM engine fixed)."""
+    from distributedauc_amd import conv1x1
+    from distributedauc_amd.backbone import build_backbone
+    from distributedauc_amd.coda import CoDA
+
+    def run(shadow):
+        torch.manual_seed(8)
+        net = build_backbone("resnet18", num_classes=2).to(dev).to(memory_format=torch.channels_last)
+        net.set_fused_bn(True).set_gemm_conv1x1(True).train()
+        coda = CoDA(net, lr=0.01, split_index=4, autocast_dtype=torch.bfloat16, device=dev, weight_shadow=shadow)
+        if shadow:
+            net.set_weight_shadow(True, dgrad_fwd=False, wgrad_hip=False)
+        g = torch.Generator(device=dev).manual_seed(12)
+        x1 = torch.randn((4, 3, 32, 32), device=dev, generator=g).contiguous(memory_format=torch.channels_last)
+        x2 = torch.randn((4, 3, 32, 32), device=dev, generator=g).contiguous(memory_format=torch.channels_last)
+        with conv1x1.fixed_engine("gemm"):
+            loss = coda.scores(x1).pow(2).sum() + coda.scores(x2).sum()
+            loss.backward()
+        return [p.grad.detach().clone() for p in net.parameters()]
+
+    det = torch.backends.cudnn.deterministic
+    torch.backends.cudnn.deterministic = True
+    try:
+        a, b = run(False), run(True)
+    finally:
+        torch.backends.cudnn.deterministic = det
+    for i, (ga, gb) in enumerate(zip(a, b)):
+        assert torch.equal(_bits(ga), _bits(gb)), f"gradient {i} differs"
