@@ -1049,8 +1049,18 @@ def main():
         sys.exit(3)
     device = torch.device("cuda", local % max(ndev, 1))  # ranks share a device only in gloo rehearsals
     torch.cuda.set_device(device)
-    gemm_selections(os.environ.get("DAUC_TUNABLEOP", os.path.join(os.path.dirname(os.path.abspath(__file__)),
-                                                                    "distributedauc_amd", "tunableop_gfx950.csv")))
+    shared = local_world > max(ndev, 1)  # gloo rehearsal: several ranks on one GPU
+    gemm_sel = "off: ranks share a GPU" if shared else (
+        "off: DAUC_TUNABLEOP=0" if os.environ.get("DAUC_TUNABLEOP") == "0" else "shipped TunableOp selections")
+    if shared:
+        # the selections were tuned and checked with one process owning the GPU; the first 8-rank
+        # shared-GPU rehearsal with them on (round 6) aborted in one rank with an illegal-instruction
+        # fault in a hipBLASLt GEMM (profiles/r06/n8_gloo_fault/README.txt) -- a shared GPU takes the
+        # default solutions; one rank per GPU (the driver's N > 1 run, and N = 1) keeps them
+        log(f"rank {rank}: {local_world} ranks share {ndev} GPU(s): TunableOp selections off (default GEMM solutions)")
+    else:
+        gemm_selections(os.environ.get("DAUC_TUNABLEOP", os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                                                        "distributedauc_amd", "tunableop_gfx950.csv")))
     quiet = None
     if use_group:
         if "MASTER_ADDR" not in os.environ:  # a --backend run at --gpus 1 outside a launcher
@@ -1117,6 +1127,7 @@ def main():
                                 if torch.cuda.is_available() and hasattr(torch.cuda, "nccl") else None,
                                 "devices_visible": torch.cuda.device_count()}
         out["host"] = host
+        out["gemm_selections"] = gemm_sel
         if sur is not None:
             out["surrogate_kernel"] = sur
         if r18 is not None:
