@@ -112,6 +112,8 @@ def parse(argv=None):
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-workers", type=int, default=4, help="configs[0] CPU leg: gloo worker processes")
     p.add_argument("--cpu-steps", type=int, default=8, help="configs[0] CPU leg: timed steps (one round at I=8)")
+    p.add_argument("--cpu-max-s", type=float, default=90.0,
+                   help="all-core CPU baseline of configs[1]: skipped when its warm-up projects a longer timed step")
     p.add_argument("--cpu-sklearn-full", type=int, default=1,
                    help="time sklearn on the full configs[4] vector (1) or its first 2^24 scores (0)")
     p.add_argument("--no-auc", action="store_true")
@@ -161,7 +163,22 @@ def host_info() -> dict:
         omp = None
     budget = min(affinity, int(omp)) if omp and omp.isdigit() and int(omp) > 0 else min(affinity, 16)
     return {"nproc": os.cpu_count(), "affinity_cpus": affinity, "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
-            "cpu_budget": budget}
+            "cpu_budget": budget, "cgroup_cpu_quota": cgroup_cpus()}
+
+
+def cgroup_cpus():
+    """The cgroup CPU quota in CPUs (cpu.max / cfs_quota_us), or None when unlimited / unreadable."""
+    try:
+        q, per = Path("/sys/fs/cgroup/cpu.max").read_text().split()[:2]
+        return None if q == "max" else int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    try:
+        q = int(Path("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read_text())
+        per = int(Path("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read_text())
+        return None if q < 0 else q / per
+    except (OSError, ValueError):
+        return None
 
 
 # ----------------------------------------------------------------------------- timing helpers
@@ -795,7 +812,23 @@ def step_roofline(args, res) -> dict:
 
 
 # ----------------------------------------------------------------------------- CPU baselines
-def cpu_baseline_train(args, threads):
+def cpu_baseline_train_cores(args, host):
+    """configs[1]'s CPU path at the thread budget (OMP_NUM_THREADS, the box's CPU share) and at every
+    CPU of the affinity mask; `value` is the faster. A run whose warm-up projects
+    more than --cpu-max-s seconds for the timed step is skipped and says so (a bounded sample)."""
+    runs = [cpu_baseline_train(args, host["cpu_budget"])]
+    if host["affinity_cpus"] > host["cpu_budget"]:
+        runs.append(cpu_baseline_train(args, host["affinity_cpus"], max_s=args.cpu_max_s))
+    torch.set_num_threads(host["cpu_budget"])
+    done = [r for r in runs if "value" in r]
+    best = dict(max(done, key=lambda r: r["value"]))
+    best["by_threads"] = runs
+    best["cores_note"] = (f"timed at {host['cpu_budget']} threads (the budget) and at all {host['affinity_cpus']} CPUs of "
+                          f"the affinity mask (cgroup quota: {host.get('cgroup_cpu_quota')} CPUs); value = the faster")
+    return best
+
+
+def cpu_baseline_train(args, threads, max_s=None):
     """The reference's CPU path for the headline config: torch-CPU ResNet-50 fwd at the GPU's batch
     (256, 224^2), verbatim loss (main.py:313-317), autograd, per-tensor dppd_sg (main.py:56-64)
     + running average (main.py:333-334). One warm-up step at batch 32, one timed step at 256."""
@@ -823,11 +856,16 @@ def cpu_baseline_train(args, threads):
                 prm.data = R.pd_step(prm.data, prm.grad.data, net0[name], 0.1, 2000.0)
                 avg[name] = avg[name] + prm.data
 
+    t0 = time.perf_counter()
     step(32)  # warm-up
+    t32 = time.perf_counter() - t0
+    if max_s is not None and t32 * B / 32 > max_s:
+        return {"cores": threads, "skipped": f"warm-up at batch 32 took {t32:.1f} s: the batch-{B} step would take "
+                                             f"~{t32 * B / 32:.0f} s > {max_s} s", "warmup_s": t32}
     t0 = time.perf_counter()
     step(B)
     dt = time.perf_counter() - t0
-    return {"value": B / dt, "unit": "imgs/sec", "cores": threads, "kind": "port",
+    return {"value": B / dt, "unit": "imgs/sec", "cores": threads, "kind": "port", "warmup_s": t32,
             "sample": f"{args.arch} {args.image_size}x{args.image_size}, one timed step at batch {B} (the GPU's "
                       "batch; warm-up at 32): fwd + reference loss + backward + per-tensor dppd_sg + running "
                       f"average, torch CPU fp32, {threads} threads", "seconds": dt}
@@ -914,12 +952,12 @@ _LAUNCH_VARS = ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_R
                 "ROLE_RANK", "ROLE_WORLD_SIZE", "ROLE_NAME", "MASTER_ADDR", "MASTER_PORT")
 
 
-def cpu_baseline_configs0(args, host):
+def cpu_baseline_configs0(args, host, threads_total=None, timeout=600):
     """configs[0]: 4 gloo CPU worker processes x (budget / 4) threads, ResNet-18 b32 224^2, I = 8
     ("4 processes x nproc/4 threads"). Child processes of this one (they never touch
     the GPU); their rank 0 reports the max-over-ranks time of exactly --cpu-steps steps."""
     W = args.cpu_workers
-    threads = max(1, host["cpu_budget"] // W)
+    threads = max(1, (threads_total or host["cpu_budget"]) // W)
     port = free_port()
     with tempfile.TemporaryDirectory() as td:
         out = Path(td) / "cw.json"
@@ -936,7 +974,10 @@ def cpu_baseline_configs0(args, host):
                                    "--pos-ratio", str(args.pos_ratio)], env=env)
                  for r in range(W)]
         try:
-            rcs = [p.wait(timeout=600) for p in procs]
+            rcs = [p.wait(timeout=timeout) for p in procs]
+        except subprocess.TimeoutExpired:
+            return {"cores": W * threads, "workers": W, "threads_per_worker": threads,
+                    "skipped": f"not done within {timeout} s (a bounded sample)"}
         finally:
             for p in procs:
                 if p.poll() is None:
@@ -1140,10 +1181,15 @@ def main():
             threads = host["cpu_budget"]
             if res is not None:
                 log("cpu baseline: resnet50 step")
-                out["cpu_baseline"] = cpu_baseline_train(args, threads)
+                out["cpu_baseline"] = cpu_baseline_train_cores(args, host)
             if r18 is not None and args.cpu_workers > 0:
                 log("cpu baseline: configs[0] gloo workers")
-                out.setdefault("configs0", {})["cpu"] = cpu_baseline_configs0(args, host)
+                c0 = cpu_baseline_configs0(args, host)
+                if host["affinity_cpus"] > host["cpu_budget"] and "value" in c0:
+                    log("cpu baseline: configs[0] gloo workers on every CPU of the affinity mask")
+                    c0["all_cores"] = cpu_baseline_configs0(args, host, threads_total=host["affinity_cpus"],
+                                                            timeout=args.cpu_max_s * 2)
+                out.setdefault("configs0", {})["cpu"] = c0
             torch.set_num_threads(threads)
             if auc is not None:
                 log("cpu baseline: sklearn configs[3]")

@@ -4,8 +4,13 @@ A drop-in for the data-parallel AUC path of ZhishuaiGuo/DistributedAUC
 (imagenet/main.py): the min-max square-loss surrogate, the proximal
 primal-dual update over the flattened model, CoDA periodic averaging over
 RCCL, and exact AUC evaluation. The AUC-specific work runs in hand-written
-gfx950 HIP kernels behind the C ABI of include/dauc.h (libdauc.so); the ResNet
-backbone stays on PyTorch-ROCm.
+gfx950 HIP kernels behind the C ABI of include/dauc.h (libdauc.so). The ResNet
+backbone runs on PyTorch-ROCm (MIOpen / CK convolutions, hipBLASLt GEMMs) with
+some of its passes on the same library's HIP kernels when switched on
+(backbone.py: fused BN + add + ReLU, the stem max-pool, the bf16 weight shadow
+with the 3x3 and 7x7-stem weight-gradient and stem-forward MFMA kernels, the
+strided / broadcast copies; CoDA turns them on under bf16 autocast and bench.py
+uses them); each is parity-tested against an fp64 / torch reference of its op.
 """
 import os
 

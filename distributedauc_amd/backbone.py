@@ -5,8 +5,15 @@ The reference scores images with a torchvision-style ResNet whose head is
 the AUC score is column 1 of that softmax. This module builds the same
 architectures (ResNet-18/34/50/101/152, ResNeXt-50/101, Wide-ResNet-50/101)
 with the same parameter names, so a reference state_dict loads unchanged. The
-backbone runs on PyTorch-ROCm (MIOpen convolutions, bf16 autocast in the
-trainer); only the AUC-specific work is in the HIP library.
+convolutions run on PyTorch-ROCm (MIOpen / CK, hipBLASLt for the 1x1 GEMMs, bf16
+autocast in the trainer). Switches put other passes on libdauc.so's HIP kernels:
+set_fused_bn (bn + add + ReLU, csrc/bn_act.hip; the stem max-pool, csrc/maxpool.hip),
+set_gemm_conv1x1 (conv1x1.py) and set_weight_shadow (one bf16 cast of all weights per
+forward; the stride-1 3x3 input gradients as forward convolutions; the 3x3 weight
+gradients, csrc/conv_wgrad.hip, and the 7x7 stem's forward and weight gradient,
+csrc/conv_stem.hip, on MFMA kernels). Parity bars: BN vs fp64 torch (fp32 2e-5, bf16
+2^-7 of scale), max-pool bit-identical to torch, weight gradients vs fp64 within 2e-5
+of scale, the stem forward one bf16 rounding of the fp64 result (tests/test_*_gpu.py).
 
 Pretrained weights are a network download in the reference (resnet.py:15-25,
 228-237); this build has no network, so ``pretrained=True`` requires a local

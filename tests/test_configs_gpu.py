@@ -10,7 +10,9 @@ For a few real steps (an averaging round included) each test checks:
     update (main.py:58-59, 64) against the oracle's restatement;
   * the class counts exact (main.py:307-308, 49-50) against the labels actually drawn;
   * a finite loss, and the all-reduced payload size (parameters + a, b, alpha + 2 counts).
-The backbone itself is PyTorch-ROCm (not compared to a CPU run: different conv kernels)."""
+The backbone (PyTorch-ROCm convolutions plus the HIP BN / max-pool / weight-gradient / stem kernels,
+each parity-tested on its own in tests/test_{fused_bn,maxpool,conv_wgrad,conv_stem,weight_shadow}_gpu.py)
+is not compared to a CPU run as a whole: different conv kernels."""
 from __future__ import annotations
 
 import sys
