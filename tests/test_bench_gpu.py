@@ -46,7 +46,7 @@ def test_bench_full_two_ranks_gloo(tmp_path):
            "--arch", "resnet18", "--batch", "32", "--image-size", "64", "--steps", "4", "--warmup", "2",
            "--sweep-I", "1,2", "--sweep-steps", "2", "--eval-images", "256", "--r18-steps", "8",
            "--auc-log2n", "20", "--auc2-log2n", "21", "--auc-reps", "1", "--auc-shard-min", "0", "--sur-log2b", "16", "--sur-reps", "5",
-           "--cpu-workers", "2", "--cpu-steps", "2", "--cpu-sklearn-full", "0"]
+           "--cpu-workers", "2", "--cpu-steps", "2", "--cpu-sklearn-full", "0", "--cpu-max-s", "20"]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=840)
     (tmp_path / "stderr.log").write_text(r.stderr)
     assert r.returncode == 0, r.stderr[-4000:]
@@ -69,6 +69,40 @@ def test_bench_full_two_ranks_gloo(tmp_path):
     assert out["configs0"]["gpu"]["n_gpus"] == 2 and out["configs0"]["cpu"]["params_finite"]
     assert out["surrogate_kernel"]["roofline"]["achieved"] > 0
     assert out["cpu_baseline"]["value"] > 0
+
+
+@pytest.mark.timeout(600)
+def test_bench_default_sizes_two_ranks_gloo(tmp_path):
+    """the driver's N > 1 bench at the BASELINE sizes -- ResNet-50 b256 224^2 bf16 at
+    I = 16 with the HIP backbone kernels, the period sweep with real averaging rounds, configs[3]
+    (2^24 @ 1 %) and configs[4] (2^27 @ 0.1 %) sharded over the ranks -- as 2 gloo ranks on cuda:0.
+    Fewer steps than the driver's (and no CPU baselines, which profiles/r06/n8_gloo/ covers at 8
+    ranks) so the test stays short; every leg and every size is the default one."""
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    cmd = [sys.executable, str(REPO / "bench.py"), "--gpus", "2", "--backend", "gloo", "--steps", "4", "--warmup", "3",
+           "--sweep-I", "1,8,16", "--sweep-steps", "16", "--eval-images", "1024", "--r18-steps", "8", "--auc-reps", "1",
+           "--sur-reps", "10", "--no-cpu-baseline"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=560)
+    (tmp_path / "stderr.log").write_text(r.stderr)
+    assert r.returncode == 0, r.stderr[-4000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout[-3000:]
+    out = json.loads(lines[0])
+    out_dir = os.environ.get("DAUC_BENCH_RECORD_DIR")
+    if out_dir:
+        Path(out_dir).mkdir(parents=True, exist_ok=True)
+        (Path(out_dir) / "bench_n2_gloo_default_sizes.json").write_text(lines[0] + "\n")
+    assert out["n_gpus"] == 2 and out["process_group"]["world_size"] == 2
+    assert out["config"]["global_batch"] == 512 and out["config"]["image_size"] == 224 and out["config"]["I"] == 16
+    assert out["config"]["params"] == 23_512_130 and out["value"] > 0
+    assert out["coda_round"]["payload_bytes"] == 94_048_788 and out["coda_round"]["ms_per_round"] > 0
+    assert [rec["I"] for rec in out["period_sweep"]["records"]] == [1, 8, 16]
+    for k, P in (("auc_eval", 168478), ("auc_eval_extreme", 134447)):
+        assert out[k]["methods_agree"] and out[k]["sort_mode"] == "sharded", k
+        assert out[k]["P"] == P  # the bench's synthetic_scores at 2^24 @ 1 % and 2^27 @ 0.1 %
+    assert out["step_roofline"]["flop_per_step"] > 6e12 and out["step_roofline"]["bn"]["bytes_per_step"] > 0
 
 
 @pytest.mark.timeout(300)
