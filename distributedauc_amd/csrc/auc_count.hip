@@ -539,14 +539,16 @@ __global__ __launch_bounds__(kCmpThreads) void compact_write_kernel(
 // large ones, where the reservation atomics of 4096 tiles on one address serialise (2^27 labels:
 // 65 us at 8 slots). HIST: hist_out += the top-bucket histogram of the positives' keys (an LDS
 // histogram per tile, its used buckets added once). Block 0 writes put_val to *put (nullable: the
-// two-step evaluation's slot header length word).
+// two-step evaluation's slot header length word). fill_w (nullable): the grid also fills nfill16
+// 16-byte words there with all-ones (the two-step's slotted table: +inf keys), by extra workgroups
+// past the tiles (blockIdx.x >= ntiles), which do only that and the zeroing.
 template <typename LT, int SLOTS, int THREADS = kCmpThreads, bool HIST = false>
 __global__ __launch_bounds__(THREADS) void compact_unordered_kernel(
     const float* __restrict__ s, const LT* __restrict__ lab, int64_t n, int vec, float* __restrict__ pos_out,
     unsigned long long* __restrict__ stats, unsigned long long tag, unsigned long long* __restrict__ zero_next,
     unsigned long long next_tag, unsigned long long* __restrict__ zero3, unsigned* __restrict__ zero_w,
     int nzero_w, int64_t cap, unsigned* __restrict__ hist_out, unsigned long long* __restrict__ put,
-    unsigned long long put_val) {
+    unsigned long long put_val, uint4* __restrict__ fill_w, int64_t nfill16, int64_t ntiles) {
     constexpr int kW = THREADS / kWave;
     constexpr int64_t kTileU = int64_t(THREADS) * 16 * SLOTS;
     __shared__ int wtot[2][kW];
@@ -561,6 +563,9 @@ __global__ __launch_bounds__(THREADS) void compact_unordered_kernel(
     }
     for (int64_t i = int64_t(blockIdx.x) * THREADS + threadIdx.x; i < nzero_w; i += int64_t(gridDim.x) * THREADS)
         zero_w[i] = 0u;  // spread over the grid (a later stage's counters: up to 147 k words)
+    for (int64_t i = int64_t(blockIdx.x) * THREADS + threadIdx.x; i < nfill16; i += int64_t(gridDim.x) * THREADS)
+        fill_w[i] = uint4{~0u, ~0u, ~0u, ~0u};
+    if (blockIdx.x >= ntiles) return;  // a fill-only workgroup (uniform)
     // the slot's tag (written with the zeroes by the previous call): a workspace whose slot was
     // not left by this thread's previous call holds stale counters, so no tile reserves from it
     // (the caller sees the tag and starts over with zeroed slots)
@@ -924,7 +929,7 @@ int compact_unordered(const float* scores, const void* labels, int label_dtype, 
                       unsigned long long* stats, unsigned long long tag, unsigned long long* zero_next,
                       unsigned long long next_tag, unsigned long long* zero3, unsigned* zero_w, int nzero_w,
                       hipStream_t st, int64_t cap, unsigned* hist_out, unsigned long long* put,
-                      unsigned long long put_val) {
+                      unsigned long long put_val, unsigned* fill_w, int64_t nfill16) {
     if (n <= 0 || scores == nullptr || labels == nullptr || pos_out == nullptr || stats == nullptr ||
         zero_next == nullptr)
         return DAUC_EINVAL;
@@ -938,22 +943,30 @@ int compact_unordered(const float* scores, const void* labels, int label_dtype, 
     const int64_t nblk = (n + tile - 1) / tile;
     if (nblk > 0x7fffffffLL) return DAUC_EINVAL;
     const int vec = (reinterpret_cast<uintptr_t>(labels) & 15u) == 0;
-    const dim3 grid(static_cast<unsigned>(nblk)), block(threads);
+    // fill-only workgroups past the tiles: 4 16-byte stores per thread (the tiles' CUs stay theirs)
+    const int64_t nfill = fill_w != nullptr ? nfill16 : 0;
+    const int64_t extra = (nfill + int64_t(threads) * 4 - 1) / (int64_t(threads) * 4);
+    if (nblk + extra > 0x7fffffffLL) return DAUC_EINVAL;
+    const dim3 grid(static_cast<unsigned>(nblk + extra)), block(threads);
+    uint4* fw = reinterpret_cast<uint4*>(fill_w);
     auto go = [&](auto* lab) {
         using LT = std::remove_const_t<std::remove_pointer_t<decltype(lab)>>;
         if (wide && hist_out != nullptr)
             hipLaunchKernelGGL((compact_unordered_kernel<LT, 32, kWideThreads, true>), grid, block, 0, st, scores, lab,
-                               n, vec, pos_out, stats, tag, zero_next, next_tag, zero3, zero_w, nzero_w, cap, hist_out, put, put_val);
+                               n, vec, pos_out, stats, tag, zero_next, next_tag, zero3, zero_w, nzero_w, cap, hist_out, put, put_val, fw,
+                               nfill, nblk);
         else if (wide)
             hipLaunchKernelGGL((compact_unordered_kernel<LT, 32, kWideThreads>), grid, block, 0, st, scores, lab, n, vec,
-                               pos_out, stats, tag, zero_next, next_tag, zero3, zero_w, nzero_w, cap, hist_out, put, put_val);
+                               pos_out, stats, tag, zero_next, next_tag, zero3, zero_w, nzero_w, cap, hist_out, put, put_val, fw,
+                               nfill, nblk);
         else if (hist_out != nullptr)
             hipLaunchKernelGGL((compact_unordered_kernel<LT, kCmpSlots, kCmpThreads, true>), grid, block, 0, st, scores,
                                lab, n, vec, pos_out, stats, tag, zero_next, next_tag, zero3, zero_w, nzero_w, cap,
-                               hist_out, put, put_val);
+                               hist_out, put, put_val, fw, nfill, nblk);
         else
             hipLaunchKernelGGL((compact_unordered_kernel<LT, kCmpSlots>), grid, block, 0, st, scores, lab, n, vec,
-                               pos_out, stats, tag, zero_next, next_tag, zero3, zero_w, nzero_w, cap, hist_out, put, put_val);
+                               pos_out, stats, tag, zero_next, next_tag, zero3, zero_w, nzero_w, cap, hist_out, put, put_val, fw,
+                               nfill, nblk);
         return launch_status();
     };
     switch (label_dtype) {

@@ -54,6 +54,7 @@ struct EvalWs {
     void* sws;                    // split workspace
     void* tws;                    // sort + tree + count-index workspace (a table of at most n/2 keys)
     size_t sws_bytes, tws_bytes;
+    unsigned* stab;               // the two-step evaluation's cell-slotted table (+inf filled by step 1)
 };
 
 EvalWs eval_ws(void* ws, int64_t n) {
@@ -75,12 +76,14 @@ EvalWs eval_ws(void* ws, int64_t n) {
     p += align256(w.sws_bytes);
     w.tws_bytes = dauc_sort_workspace_size(n / 2 + 1);
     w.tws = p;
+    p += align256(w.tws_bytes);
+    w.stab = reinterpret_cast<unsigned*>(p);
     return w;
 }
 
 size_t eval_ws_bytes(int64_t n) {
     return kHdr + align256(size_t(n) * 4) + align256(size_t(n / 2 + 1) * 4) + align256(dauc_split_workspace_size(n)) +
-           align256(dauc_sort_workspace_size(n / 2 + 1));
+           align256(dauc_sort_workspace_size(n / 2 + 1)) + align256(slotted_table_bytes(direct_capacity(n)));
 }
 
 bool valid_args(const float* scores, const void* labels, int label_dtype, int64_t n, int part, int parts,
@@ -229,6 +232,14 @@ int counts_part_blocking(const float* scores, const void* labels, int label_dtyp
 constexpr size_t kSlotHist = 256, kSlotHdr = kSlotHist + size_t(kCiTop) * 4;
 constexpr int kSlotN = 4;  // header word: the n the slot was built for
 
+#ifdef DAUC_TUNING
+// tuning builds: the two-step's step-2 build (dauc_set_two_step_form): 0 the slotted table (the
+// product's), 1 round 5's direct build (count, blocks, scatter passes into the cell-ordered table)
+int g_two_step_form = 0;
+#else
+constexpr int g_two_step_form = 0;
+#endif
+
 int64_t slot_cap(int parts) {
     const int64_t fair = (direct_capacity(INT64_MAX / 4) + parts - 1) / parts;
     return fair + fair / 4 + 64;
@@ -283,25 +294,34 @@ int dauc_auc_eval_compact_part(const float* scores, const void* labels, int labe
     hipError_t e;
     if ((e = hipMemsetAsync(hdr, 0, kSlotHdr, st)) != hipSuccess) return -static_cast<int>(e);  // + histogram
     const int64_t lo = slice_lo(n, part, parts), hi = slice_lo(n, part + 1, parts);
+    // step 2's slotted build state, reset here (the compaction's grid does it on the side): the
+    // packed per-cell byte counters zeroed, the slotted table +inf, meta words 8..13 (the skew
+    // word among them, which step 2's count pass sets from any workgroup) zeroed
+    const int64_t mcap = direct_capacity(n);
+    unsigned* cnt = direct_cnt_ptr(w.tws, mcap);
+    auto* meta8 = reinterpret_cast<unsigned long long*>(slotted_meta_ptr(w.tws, mcap) + 8);
+    // (form 1, tuning builds: round 5's direct build counts into one u32 per cell and fills nothing)
+    const size_t tab = g_two_step_form == 0 ? slotted_fill_bytes(mcap) : 0;
+    const int64_t ncnt = g_two_step_form == 0 ? slotted_cnt_words() : direct_cnt_words();
     if (hi <= lo) {
-        // an empty slice: P_r = 0, the length word still set (its two halves), and the query step's
-        // per-cell counters zeroed (the compaction's job otherwise)
+        // an empty slice: P_r = 0, the length word still set (its two halves), and step 2's state
+        // reset by memsets (the compaction's job otherwise)
         auto* nw = reinterpret_cast<unsigned*>(hdr + kSlotN);
         const unsigned long long nv = static_cast<unsigned long long>(n);
         if ((e = hipMemsetD32Async(nw, static_cast<int>(nv & 0xffffffffull), 1, st)) != hipSuccess ||
             (e = hipMemsetD32Async(nw + 1, static_cast<int>(nv >> 32), 1, st)) != hipSuccess ||
-            (e = hipMemsetAsync(direct_cnt_ptr(w.tws, direct_capacity(n)), 0, size_t(direct_cnt_words()) * 4, st)) !=
-                hipSuccess)
+            (e = hipMemsetAsync(cnt, 0, size_t(ncnt) * 4, st)) != hipSuccess ||
+            (e = hipMemsetAsync(meta8, 0, 24, st)) != hipSuccess ||
+            (tab && (e = hipMemsetD32Async(w.stab, -1, tab / 4, st)) != hipSuccess))
             return -static_cast<int>(e);
         return DAUC_OK;
     }
     const size_t lsz = label_dtype == DAUC_LABEL_I8 ? 1 : label_dtype == DAUC_LABEL_I32 ? 4 : 8;
     return compact_unordered(scores + lo, static_cast<const char*>(labels) + size_t(lo) * lsz, label_dtype, hi - lo,
                              reinterpret_cast<float*>(static_cast<char*>(slot) + kSlotHdr), hdr, 0ull, w.spare, 0ull,
-                             nullptr, direct_cnt_ptr(w.tws, direct_capacity(n)), static_cast<int>(direct_cnt_words()),
-                             st, slot_cap(parts),
+                             meta8, cnt, static_cast<int>(ncnt), st, slot_cap(parts),
                              reinterpret_cast<unsigned*>(static_cast<char*>(slot) + kSlotHist), hdr + kSlotN,
-                             static_cast<unsigned long long>(n));
+                             static_cast<unsigned long long>(n), w.stab, static_cast<int64_t>(tab / 16));
 }
 
 int dauc_auc_eval_query_part(const float* scores, const void* labels, int label_dtype, int64_t n, int part, int parts,
@@ -327,8 +347,11 @@ int dauc_auc_eval_query_part(const float* scores, const void* labels, int label_
     SlotSource src{static_cast<const unsigned char*>(slots), slot_bytes(parts), kSlotHist, kSlotHdr, parts, part,
                    slot_cap(parts), n, qhi - qlo, w.wt, w.slot, reinterpret_cast<unsigned long long*>(w.verdict),
                    w.spare};
-    return counts_labeled_direct_slots(src, w.pos, mcap, scores, labels, label_dtype, qlo, qhi, w.wt, w.wt + 2,
-                                       w.verdict, w.tws, w.tws_bytes, st, reinterpret_cast<unsigned*>(part_out + 4));
+    if (g_two_step_form == 1)
+        return counts_labeled_direct_slots(src, w.pos, mcap, scores, labels, label_dtype, qlo, qhi, w.wt, w.wt + 2,
+                                           w.verdict, w.tws, w.tws_bytes, st, reinterpret_cast<unsigned*>(part_out + 4));
+    return counts_labeled_slotted(src, w.stab, mcap, scores, labels, label_dtype, qlo, qhi, w.wt, w.wt + 2, w.verdict,
+                                  w.tws, w.tws_bytes, st, reinterpret_cast<unsigned*>(part_out + 4));
 }
 
 int dauc_auc_eval_counts(const float* scores, const void* labels, int label_dtype, int64_t n, int64_t* out,
@@ -348,5 +371,13 @@ int dauc_auc_eval_counts_part(const float* scores, const void* labels, int label
     return counts_part_blocking(scores, labels, label_dtype, n, part, parts, out, part_counts, pinned, workspace,
                                 workspace_bytes, as_hip(stream));
 }
+
+#ifdef DAUC_TUNING
+int dauc_set_two_step_form(int form) {
+    if (form < 0 || form > 1) return DAUC_EINVAL;
+    g_two_step_form = form;
+    return DAUC_OK;
+}
+#endif
 
 }  // extern "C"

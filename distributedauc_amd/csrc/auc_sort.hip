@@ -880,6 +880,17 @@ __device__ __forceinline__ void ci_fix(unsigned x, unsigned rl, unsigned cnt, co
     t += static_cast<unsigned long long>((ub - lb) - (ubf - lbf));
 }
 
+// SLOT: keys 8 .. cnt - 1 of cell c (its tertiary run), counted one by one after the two windows
+// counted the first 8: W += M - ub loses the run's keys <= x, T gains its keys == x
+__device__ __forceinline__ void slot_tertiary(unsigned x, unsigned c, unsigned cnt, const unsigned* __restrict__ tab,
+                                              unsigned cells, unsigned long long& w, unsigned long long& t) {
+    const unsigned* r = tab + slot_ter(cells, c);
+    for (unsigned j = 0; j + 8u < cnt; ++j) {
+        const unsigned v = r[j];
+        w -= v <= x;
+        t += (v <= x) - (v < x);
+    }
+}
 
 // The labeled query pass over the count index (same stream and checks as query_labeled_kernel);
 // returns at once when the builder kept the tree, so it is enqueued unconditionally. Per
@@ -890,10 +901,17 @@ __device__ __forceinline__ void ci_fix(unsigned x, unsigned rl, unsigned cnt, co
 // so the caller can compare the range's positives with the ones another rank compacted from it.
 // The loop runs at the 128-VGPR bound of 4 waves per SIMD, so the query count rides in the high
 // half of the non-finite counter (per lane both stay far below 2^16): no extra register.
-template <typename LT, bool CHECK = false>
+//
+// SLOT (round 6): the cell-slotted table of direct_count_slots_kernel<true> (count_index.h). `blkg`
+// is then the raw per-cell byte counts (8 per block: the block words' size), turned into block words
+// in LDS by the workgroup itself (each thread sums its run of 18 blocks, one workgroup scan, written
+// back in place); `sorted` is the slotted table of `slot_cells` cells. A cell's keys are its primary
+// window (+inf past its count), its secondary window past 4 keys and, past 8 (rare), its tertiary
+// run: W += M - (rank_lo + #keys <= x), T += #(== x); no straddling windows.
+template <typename LT, bool CHECK = false, bool SLOT = false>
 __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __restrict__ s,
                                                                 const LT* __restrict__ lab, int64_t begin,
-                                                                int64_t end, const unsigned* __restrict__ meta,
+                                                                int64_t end, unsigned* __restrict__ meta,
                                                                 const uint2* __restrict__ l1g,
                                                                 const uint2* __restrict__ blkg,
                                                                 const unsigned* __restrict__ sorted, int64_t M,
@@ -902,9 +920,14 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
                                                                 unsigned* __restrict__ verdict,
                                                                 const unsigned* __restrict__ grp,
                                                                 const unsigned long long* __restrict__ Mp,
-                                                                unsigned* __restrict__ check) {
+                                                                unsigned* __restrict__ check, unsigned slot_cells = 0u) {
+    const unsigned pad_word = 4u * slot_cells;  // SLOT: the all-+inf primary slot past the last cell
     const bool in_use = count_index_in_use(meta);
     if (Mp != nullptr) M = static_cast<int64_t>(*Mp);  // the direct build: the table size on the device
+    if constexpr (SLOT) {
+        // the slotted state is consumed (read after every count-pass workgroup finished: stream order)
+        if (blockIdx.x == 0 && threadIdx.x == 0) meta[kCiConsumed] = 1u;
+    }
     // the end-of-kernel reduction's rows (W, T, #non-finite, CHECK: #queries); static LDS on top of
     // the index's 163,232 dynamic bytes: the 160 KB limit leaves room for 4 rows, no more
     __shared__ unsigned long long red[CHECK ? 4 : 3][kQueryThreads / kWave];
@@ -984,6 +1007,35 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
             if (i < nb) blk[i] = v[j];
         }
     }
+    if constexpr (SLOT) {
+        // byte counts -> block words {keys before the block, the 8 counts as nibbles}, in place:
+        // thread t owns blocks [18 t, 18 t + 18); its run total, one workgroup scan, then each
+        // block rewritten with its exclusive prefix (counts <= 8: a skewed table never gets here)
+        constexpr int kOwn = (kCiMaxBlocks + kQueryThreads - 1) / kQueryThreads;  // 18
+        __syncthreads();
+        const int b0 = threadIdx.x * kOwn;
+        unsigned run = 0u;
+#pragma unroll
+        for (int j = 0; j < kOwn; ++j) {
+            if (b0 + j < nb) {
+                const uint2 r = blk[b0 + j];
+                run += __builtin_amdgcn_sad_u8(r.x, 0u, 0u) + __builtin_amdgcn_sad_u8(r.y, 0u, 0u);
+            }
+        }
+        unsigned before = block_incl_scan1024<false>(run, reinterpret_cast<unsigned*>(&red[0][0])) - run;
+#pragma unroll
+        for (int j = 0; j < kOwn; ++j) {
+            if (b0 + j < nb) {
+                const uint2 r = blk[b0 + j];
+                // bytes b0..b3 (each <= 8) -> nibbles: 0x0b3b2b1b0 per half
+                const unsigned tl = (r.x & 0x000f000fu) | ((r.x >> 4) & 0x00f000f0u);
+                const unsigned th = (r.y & 0x000f000fu) | ((r.y >> 4) & 0x00f000f0u);
+                const unsigned nib = (tl & 0xffu) | ((tl >> 8) & 0xff00u) | ((th & 0xffu) << 16) | ((th >> 8) & 0xff00u) << 16;
+                blk[b0 + j] = uint2{before, nib};
+                before += __builtin_amdgcn_sad_u8(r.x, 0u, 0u) + __builtin_amdgcn_sad_u8(r.y, 0u, 0u);
+            }
+        }
+    }
     __syncthreads();
     const unsigned M32 = static_cast<unsigned>(M);
     unsigned long long w = 0, t = 0;
@@ -996,13 +1048,27 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
         if (lab[i] != LT(1)) {
             nf += !isfinite(s[i]) + (CHECK ? 0x10000u : 0u);
             const unsigned x = key_fast(s[i]);
-            unsigned rl, cnt, wl = 0u, tl = 0u;
-            uint4 k;
-            ci_locate(x, l1, blk, sorted, rl, cnt, k);
-            const bool more = ci_count(x, true, rl, cnt, k, M32, wl, tl);
-            w += wl;
-            t += tl;
-            if (more) ci_fix(x, rl, cnt, k, sorted, w, t);
+            if constexpr (SLOT) {
+                const unsigned c = ci_cell(x, l1[x >> kCiLowBits]);
+                unsigned rl, cnt;
+                ci_decode(c, blk[c / kCiBlock], rl, cnt);
+                const uint4 k = win_load(sorted + (cnt ? 4u * c : pad_word));
+                const uint4 k2 = win_load(sorted + (cnt > 4u ? slot_sec(slot_cells, c) : pad_word));
+                unsigned le, lt, le2, lt2;
+                win_le_lt(k, x, le, lt);
+                win_le_lt(k2, x, le2, lt2);
+                w += M32 - (rl + le + le2);
+                t += (le - lt) + (le2 - lt2);
+                if (cnt > 8u) slot_tertiary(x, c, cnt, sorted, slot_cells, w, t);
+            } else {
+                unsigned rl, cnt, wl = 0u, tl = 0u;
+                uint4 k;
+                ci_locate(x, l1, blk, sorted, rl, cnt, k);
+                const bool more = ci_count(x, true, rl, cnt, k, M32, wl, tl);
+                w += wl;
+                t += tl;
+                if (more) ci_fix(x, rl, cnt, k, sorted, w, t);
+            }
         }
     };
     for (int64_t i = begin + tid; i < head; i += stride) one(i);
@@ -1067,11 +1133,10 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
         // phase by phase over the group, so that every query's LDS read of a phase is issued before
         // the first wait (a per-query chain with its conditional window load in between keeps the
         // compiler from interleaving the queries: one LDS round trip per read per query)
-        auto locate_lds = [&](Group& g) {
+        auto locate_lds = [&](Group& g, unsigned (&c)[NQ]) {
             uint2 e[NQ];
 #pragma unroll
             for (int q = 0; q < NQ; ++q) e[q] = l1[g.x[q] >> kCiLowBits];
-            unsigned c[NQ];
 #pragma unroll
             for (int q = 0; q < NQ; ++q) c[q] = ci_cell(g.x[q], e[q]);
             uint2 b[NQ];
@@ -1089,8 +1154,22 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
         };
         // an aligned window of +inf keys (the table is padded with at least 8 past M): the lanes with
         // no window to gather read it, so their counts need no mask
-        const unsigned padoff = (M32 + 3u) & ~3u;
-        auto locate_win = [&](Group& g) {
+        const unsigned padoff = SLOT ? pad_word : (M32 + 3u) & ~3u;
+        auto locate_win = [&](Group& g, const unsigned (&c)[NQ]) {
+            if constexpr (SLOT) {
+                // the cell's primary window (its first 4 keys), and its secondary one past 4 keys
+#pragma unroll
+                for (int q = 0; q < NQ; ++q) {
+                    const unsigned cnt = g.rc[q] >> 28;
+                    g.k[q] = win_load(sorted + (cnt && ((g.use >> q) & 1u) ? 4u * c[q] : padoff));
+                }
+#pragma unroll
+                for (int q = 0; q < NQ; ++q) {
+                    const unsigned cnt = g.rc[q] >> 28;
+                    g.k2[q] = win_load(sorted + (((g.use >> q) & 1u) && cnt > 4u ? slot_sec(slot_cells, c[q]) : padoff));
+                }
+                return;
+            }
 #pragma unroll
             for (int q = 0; q < NQ; ++q) {
                 const unsigned rl = g.rc[q] & 0x0fffffffu, cnt = g.rc[q] >> 28;
@@ -1108,8 +1187,9 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
             }
         };
         auto locate = [&](Group& g) {
-            locate_lds(g);
-            locate_win(g);
+            unsigned c[NQ];
+            locate_lds(g, c);
+            locate_win(g, c);
         };
         auto count = [&](const Group& g) {
             unsigned wl = 0u, tl = 0u;
@@ -1122,17 +1202,30 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
                 // W += M - ub, T += ub - lb, for the queries only (um)
                 const unsigned x = g.x[q], rl = g.rc[q] & 0x0fffffffu, cnt = g.rc[q] >> 28;
                 const unsigned um = 0u - ((g.use >> q) & 1u);
-                const unsigned base = rl & ~(min(cnt, 1u) * 3u);  // rl & ~3 when the cell has keys
+                // rl & ~3 when the cell has keys (its window starts at the aligned rank); SLOT: the
+                // window holds exactly the cell's keys, then +inf
+                const unsigned base = SLOT ? rl : rl & ~(min(cnt, 1u) * 3u);
                 unsigned le, lt, le2, lt2;
                 win_le_lt(g.k[q], x, le, lt);
                 win_le_lt(g.k2[q], x, le2, lt2);
                 wl += (M32 - (base + le + le2)) & um;
                 tl += ((le - lt) + (le2 - lt2)) & um;
-                more8 |= um && (rl & 3u) + cnt > 8u;
+                more8 |= um && (SLOT ? cnt : (rl & 3u) + cnt) > 8u;
             }
             w += wl;
             t += tl;
             if (more8) {  // a cell of 6+ keys across both windows: rare (the nibble caps it at 14)
+                if constexpr (SLOT) {  // a cell of 9+ keys: its tertiary run, key by key
+#pragma unroll
+                    for (int q = 0; q < NQ; ++q) {
+                        const unsigned cnt = g.rc[q] >> 28;
+                        if (((g.use >> q) & 1u) && cnt > 8u) {
+                            const unsigned x = g.x[q];
+                            slot_tertiary(x, ci_cell(x, l1[x >> kCiLowBits]), cnt, sorted, slot_cells, w, t);
+                        }
+                    }
+                    return;
+                }
 #pragma unroll
                 for (int q = 0; q < NQ; ++q) {
                     const unsigned rl = g.rc[q] & 0x0fffffffu, cnt = g.rc[q] >> 28;
@@ -1345,13 +1438,25 @@ __global__ __launch_bounds__(kDirectThreads) void direct_count_kernel(const floa
 // (the scatter's input) with its cell. Workgroup 0 also writes the plan, the verdict words, the
 // part's record (counts zeroed, P, the check word, the label counts) and m_eff (P, or past the
 // index's capacity when a slot overflowed, so the plan refuses the table: verdict 2).
+//
+// SLOT (round 6, the two-step evaluation's default): the cell-slotted table instead (count_index.h:
+// primary / secondary windows +inf filled by the compaction of step 1, a tertiary run), the per-cell
+// counters bytes packed four to a word (zeroed by that compaction too), and each key inserted
+// straight into its cell: its rank in the cell is the byte its returning atomic add found. No
+// position array, no cell array, no block pass and no scatter: the query pass turns the byte counts
+// into the block words itself (query_ci_kernel<.., SLOT>). A cell of 15+ keys marks the index skewed
+// (verdict 2: the caller's sorted path), as in the direct build; meta[kCiSkew] was zeroed by the
+// compaction, because this pass's workgroups set it while workgroup 0 writes the other meta words.
 constexpr int kSlotCountThreads = 1024;
+template <bool SLOT = false>
 __global__ __launch_bounds__(kSlotCountThreads) void direct_count_slots_kernel(SlotSource src, int64_t mcap,
                                                                               uint2* __restrict__ l1g,
                                                                               unsigned* __restrict__ meta,
                                                                               unsigned* __restrict__ cnt,
                                                                               unsigned* __restrict__ cell,
-                                                                              float* __restrict__ pos) {
+                                                                              float* __restrict__ pos,
+                                                                              unsigned* __restrict__ stab,
+                                                                              unsigned slot_cells) {
     static_assert(kCiTop == 2 * kSlotCountThreads, "two top buckets per thread");
     __shared__ uint2 l1[kCiTop];
     __shared__ unsigned wtot[kSlotCountThreads / kWave];
@@ -1429,6 +1534,22 @@ __global__ __launch_bounds__(kSlotCountThreads) void direct_count_slots_kernel(S
         }
     }
     __syncthreads();  // (an overflow adds past-capacity keys to bucket 0)
+    // SLOT: this thread's first key is loaded now, so its latency overlaps the plan's three scans
+    // (one key per thread: the grid covers the index's capacity)
+    const int64_t i_first = int64_t(blockIdx.x) * kSlotCountThreads + threadIdx.x;
+    float v_first = 0.0f;
+    if constexpr (SLOT) {
+        if (hs[3] == 0ull && i_first < static_cast<int64_t>(hs[0])) {
+            int lo = 0, hi = parts;
+            while (hi - lo > 1) {
+                const int mid = (lo + hi) >> 1;
+                if (off[mid] <= static_cast<unsigned long long>(i_first)) lo = mid;
+                else hi = mid;
+            }
+            v_first = reinterpret_cast<const float*>(src.slots + size_t(lo) * src.sbytes + src.data_off)
+                [i_first - static_cast<int64_t>(off[lo])];
+        }
+    }
     const bool over = hs[3] != 0ull;
     if (threadIdx.x == 0 && over) n0 += static_cast<unsigned>(mcap) + 1u;
     unsigned used = (n0 != 0u) + (n1 != 0u);
@@ -1458,7 +1579,7 @@ __global__ __launch_bounds__(kSlotCountThreads) void direct_count_slots_kernel(S
             meta[kCiOk] = ok ? 1u : 0u;
             meta[kCiCells] = total;
             meta[kCiBlocks] = (total + 1 + kCiBlock - 1) / kCiBlock;
-            meta[kCiSkew] = 0u;
+            if constexpr (!SLOT) meta[kCiSkew] = 0u;  // SLOT: zeroed by the compaction (see above)
             *src.m_eff = over ? static_cast<unsigned long long>(mcap) + 1ull : P;
         } else if (threadIdx.x < 4) {
             src.wt[threadIdx.x - 1] = 0ull;
@@ -1471,6 +1592,63 @@ __global__ __launch_bounds__(kSlotCountThreads) void direct_count_slots_kernel(S
     }
     if (!ok) return;
     const int64_t Mk = static_cast<int64_t>(P);  // no overflow here: every positive is stored
+    if constexpr (SLOT) {
+        // step 2 again on the same step-1 state: the counters and slots already hold the keys, so
+        // inserting them twice would double every count -- refuse the index instead (verdict 2:
+        // the caller's sorted path gives the exact integers)
+        if (meta[kCiConsumed] != 0u) {
+            if (threadIdx.x == 0) atomicOr(meta + kCiSkew, 1u);
+            return;
+        }
+        bool skew = false;
+        for (int64_t i0 = int64_t(blockIdx.x) * kSlotCountThreads; i0 < Mk;
+             i0 += int64_t(gridDim.x) * kSlotCountThreads) {
+            const int64_t i = i0 + threadIdx.x;
+            const bool live = i < Mk;
+            unsigned x = 0u, c = 0u;
+            if (live) {
+                float v = v_first;
+                if (i != i_first) {  // past the first key (a grid smaller than the table)
+                    int lo = 0, hi = parts;
+                    while (hi - lo > 1) {
+                        const int mid = (lo + hi) >> 1;
+                        if (off[mid] <= static_cast<unsigned long long>(i)) lo = mid;
+                        else hi = mid;
+                    }
+                    v = reinterpret_cast<const float*>(src.slots + size_t(lo) * src.sbytes + src.data_off)
+                        [i - static_cast<int64_t>(off[lo])];
+                }
+                x = key_fast(v);
+                c = ci_cell(x, l1[x >> kCiLowBits]);
+            }
+            const unsigned long long act = __ballot(live);
+            if (act == 0ull) continue;
+            const int first = __ffsll(static_cast<long long>(act)) - 1;
+            const unsigned cf = __shfl(c, first, kWave);
+            unsigned rank = 0u;
+            if (__ballot(live && c == cf) == act) {
+                // every key of the wave in one cell (tie-heavy tables): one add for all of them
+                unsigned old = 0u;
+                if (lane == first)
+                    old = atomicAdd(cnt + (cf >> 2), static_cast<unsigned>(__popcll(act)) << (8u * (cf & 3u)));
+                old = __shfl(old, first, kWave);
+                const unsigned below = static_cast<unsigned>(
+                    __popcll(act & ((lane == 0 ? 0ull : (~0ull >> (kWave - lane))))));
+                rank = ((old >> (8u * (cf & 3u))) & 0xffu) + below;
+            } else if (live) {
+                const unsigned old = atomicAdd(cnt + (c >> 2), 1u << (8u * (c & 3u)));
+                rank = (old >> (8u * (c & 3u))) & 0xffu;
+            }
+            if (live) {
+                if (rank < 4u) stab[4u * c + rank] = x;
+                else if (rank < 8u) stab[slot_sec(slot_cells, c) + rank - 4u] = x;
+                else if (rank < kSlotMaxKeys) stab[slot_ter(slot_cells, c) + rank - 8u] = x;
+                else skew = true;  // (a byte past 255 also carries into the next cell: skewed anyway)
+            }
+        }
+        if (__ballot(skew) != 0ull && lane == 0) atomicOr(meta + kCiSkew, 1u);
+        return;
+    }
     for (int64_t i0 = int64_t(blockIdx.x) * kSlotCountThreads; i0 < Mk;
          i0 += int64_t(gridDim.x) * kSlotCountThreads) {
         const int64_t i = i0 + threadIdx.x;
@@ -1864,7 +2042,7 @@ template <typename LT>
 int launch_ci(const float* s, const LT* lab, int64_t begin, int64_t end, const CountWs& cw, const unsigned* sorted,
               int64_t M, unsigned long long* out, unsigned long long* nonfinite, hipStream_t st,
               unsigned* verdict = nullptr, const unsigned* grp = nullptr, const unsigned long long* Mp = nullptr,
-              unsigned* check = nullptr) {
+              unsigned* check = nullptr, const uint2* slot_counts = nullptr, unsigned slot_cells = 0u) {
     const dim3 grid(query_grid(end - begin)), block(kQueryThreads);
     const size_t lds = (size_t(kCiTop) + kCiMaxBlocks) * 8 + (grp ? size_t(kDirectMaxGroups) * 4 : 0);
     // dynamic + the kernel's static reduction rows must fit the CU's 160 KB of LDS (a launch past it
@@ -1872,12 +2050,15 @@ int launch_ci(const float* s, const LT* lab, int64_t begin, int64_t end, const C
     static_assert((size_t(kCiTop) + kCiMaxBlocks) * 8 + size_t(kDirectMaxGroups) * 4 +
                           4 * (kQueryThreads / kWave) * 8 <= 160 * 1024,
                   "the count-index query's LDS");
-    if (check != nullptr)
+    if (slot_counts != nullptr && check != nullptr)
+        hipLaunchKernelGGL((query_ci_kernel<LT, true, true>), grid, block, lds, st, s, lab, begin, end, cw.meta, cw.l1,
+                           slot_counts, sorted, M, out, nonfinite, verdict, nullptr, Mp, check, slot_cells);
+    else if (check != nullptr)
         hipLaunchKernelGGL((query_ci_kernel<LT, true>), grid, block, lds, st, s, lab, begin, end, cw.meta, cw.l1,
-                           cw.blk, sorted, M, out, nonfinite, verdict, grp, Mp, check);
+                           cw.blk, sorted, M, out, nonfinite, verdict, grp, Mp, check, 0u);
     else
         hipLaunchKernelGGL((query_ci_kernel<LT>), grid, block, lds, st, s, lab, begin, end, cw.meta, cw.l1, cw.blk,
-                           sorted, M, out, nonfinite, verdict, grp, Mp, check);
+                           sorted, M, out, nonfinite, verdict, grp, Mp, check, 0u);
     return launch_status();
 }
 
@@ -2028,8 +2209,8 @@ int counts_labeled_direct_slots(const SlotSource& src, float* pos, int64_t Mcap,
     unsigned* table = w.keys_a;
     unsigned* grp = reinterpret_cast<unsigned*>(after_tree_of(workspace, Mcap));
     const int64_t gk = (Mcap + kSlotCountThreads - 1) / kSlotCountThreads;
-    hipLaunchKernelGGL(direct_count_slots_kernel, dim3(static_cast<unsigned>(gk)), dim3(kSlotCountThreads), 0, st, src,
-                       Mcap, nw.l1, nw.meta, nw.cstart, w.keys_b, pos);
+    hipLaunchKernelGGL(direct_count_slots_kernel<false>, dim3(static_cast<unsigned>(gk)), dim3(kSlotCountThreads), 0,
+                       st, src, Mcap, nw.l1, nw.meta, nw.cstart, w.keys_b, pos, nullptr, 0u);
     hipLaunchKernelGGL(direct_blocks_kernel, dim3(kDirectMaxGroups), dim3(kDirectGroup), 0, st, nw.cstart, nw.meta,
                        nw.blk, grp);
     const int64_t gs = (Mcap + kDirectThreads - 1) / kDirectThreads;
@@ -2049,6 +2230,54 @@ int counts_labeled_direct_slots(const SlotSource& src, float* pos, int64_t Mcap,
         default:
             return launch_ci(scores, static_cast<const int64_t*>(labels), begin, end, nw, table, 0, wins_ties,
                              nonfinite, st, verdict, grp, Mp, check);
+    }
+}
+
+int64_t slotted_cells(int64_t Mcap) {
+    // the plan uses at most min(kCiMaxCells, 2 M + one per used bucket) cells
+    const int64_t c = 2 * Mcap + kCiTop;
+    return c < kCiMaxCells ? c : kCiMaxCells;
+}
+
+size_t slotted_table_bytes(int64_t Mcap) {  // primary + secondary + tertiary
+    return size_t(slotted_cells(Mcap) + 1) * 8 * 4 + size_t(slotted_cells(Mcap)) * 8 * 4;
+}
+
+size_t slotted_fill_bytes(int64_t Mcap) { return size_t(slotted_cells(Mcap) + 1) * 8 * 4; }  // the +inf part
+
+int64_t slotted_cnt_words() { return (int64_t(kCiMaxBlocks) * kCiBlock) / 4; }
+
+unsigned* slotted_meta_ptr(void* workspace, int64_t Mcap) { return count_ws_of(workspace, Mcap).meta; }
+
+int counts_labeled_slotted(const SlotSource& src, unsigned* stab, int64_t Mcap, const float* scores, const void* labels,
+                           int label_dtype, int64_t begin, int64_t end, unsigned long long* wins_ties,
+                           unsigned long long* nonfinite, unsigned* verdict, void* workspace, size_t workspace_bytes,
+                           hipStream_t st, unsigned* check) {
+    if (begin < 0 || end < begin || wins_ties == nullptr || stab == nullptr || src.slots == nullptr ||
+        src.parts < 1 || src.parts > kMaxSlotParts || (end > begin && (scores == nullptr || labels == nullptr)) ||
+        workspace == nullptr || Mcap < 1 || workspace_bytes < dauc_sort_workspace_size(Mcap) || check == nullptr)
+        return DAUC_EINVAL;
+    if (label_dtype != DAUC_LABEL_I8 && label_dtype != DAUC_LABEL_I32 && label_dtype != DAUC_LABEL_I64)
+        return DAUC_EINVAL;
+    const CountWs nw = count_ws_of(workspace, Mcap);
+    const int64_t gk = (Mcap + kSlotCountThreads - 1) / kSlotCountThreads;
+    const unsigned cells = static_cast<unsigned>(slotted_cells(Mcap));
+    hipLaunchKernelGGL(direct_count_slots_kernel<true>, dim3(static_cast<unsigned>(gk)), dim3(kSlotCountThreads), 0,
+                       st, src, Mcap, nw.l1, nw.meta, nw.cstart, nullptr, nullptr, stab, cells);
+    int rc = launch_status();
+    if (rc || end == begin) return rc;
+    const unsigned long long* Mp = src.m_eff;
+    const uint2* counts = reinterpret_cast<const uint2*>(nw.cstart);
+    switch (label_dtype) {
+        case DAUC_LABEL_I8:
+            return launch_ci(scores, static_cast<const int8_t*>(labels), begin, end, nw, stab, 0, wins_ties, nonfinite,
+                             st, verdict, nullptr, Mp, check, counts, cells);
+        case DAUC_LABEL_I32:
+            return launch_ci(scores, static_cast<const int32_t*>(labels), begin, end, nw, stab, 0, wins_ties, nonfinite,
+                             st, verdict, nullptr, Mp, check, counts, cells);
+        default:
+            return launch_ci(scores, static_cast<const int64_t*>(labels), begin, end, nw, stab, 0, wins_ties, nonfinite,
+                             st, verdict, nullptr, Mp, check, counts, cells);
     }
 }
 

@@ -35,8 +35,17 @@ constexpr int kCiLowBits = 32 - kCiTopBits;
 constexpr int kCiBlock = 8;                               // cells per block word
 constexpr int kCiMaxBlocks = 18320;                       // 16 KB + 8 B per block + 384 B < 160 KB of LDS
 constexpr int kCiMaxCells = kCiMaxBlocks * kCiBlock - 1;  // + the virtual cell past the last
-// meta words: [8] usable, [9] cells, [10] blocks, [11] skewed (or inconsistent: never use)
-constexpr int kCiOk = 8, kCiCells = 9, kCiBlocks = 10, kCiSkew = 11;
+// The slotted table (the two-step evaluation, round 6), for `cells` cells: a cell's keys by rank,
+// 0-3 in its PRIMARY window (4 words at 4c), 4-7 in its SECONDARY window (4 (cells + 1) + 4c), 8-14
+// in its TERTIARY run (8 (cells + 1) + 8c); the primary and secondary regions are +inf filled
+// (windows past a cell's count read +inf) and primary slot `cells` is the all-+inf pad window. The
+// primary region (16 B per cell, 2.3 MB at most) is the one nearly every query gathers from.
+__host__ __device__ __forceinline__ unsigned slot_sec(unsigned cells, unsigned c) { return 4u * (cells + 1u) + 4u * c; }
+__host__ __device__ __forceinline__ unsigned slot_ter(unsigned cells, unsigned c) { return 8u * (cells + 1u) + 8u * c; }
+constexpr unsigned kSlotMaxKeys = 14;  // the nibble's bound: a cell of 15+ keys marks the table skewed
+// meta words: [8] usable, [9] cells, [10] blocks, [11] skewed (or inconsistent: never use),
+// [13] the slotted build's state was consumed by a query pass (a second step 2 without a new step 1)
+constexpr int kCiOk = 8, kCiCells = 9, kCiBlocks = 10, kCiSkew = 11, kCiConsumed = 13;
 
 __device__ __forceinline__ unsigned ci_cell(unsigned key, uint2 e) { return e.x + __umulhi(key << kCiTopBits, e.y); }
 

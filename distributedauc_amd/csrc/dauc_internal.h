@@ -115,7 +115,8 @@ int compact_unordered(const float* scores, const void* labels, int label_dtype, 
                       unsigned long long* stats, unsigned long long tag, unsigned long long* zero_next,
                       unsigned long long next_tag, unsigned long long* zero3, unsigned* zero_w, int nzero_w,
                       hipStream_t st, int64_t cap = INT64_MAX, unsigned* hist_out = nullptr,
-                      unsigned long long* put = nullptr, unsigned long long put_val = 0ull);
+                      unsigned long long* put = nullptr, unsigned long long put_val = 0ull,
+                      unsigned* fill_w = nullptr, int64_t nfill16 = 0);
 
 // auc_sort.hip: the count index built straight from the unsorted positives (no radix sort, no
 // tree) and the labeled query pass over scores [begin, end); the table is ordered by cell only.
@@ -157,5 +158,19 @@ int counts_labeled_direct_slots(const SlotSource& src, float* pos, int64_t Mcap,
                                 const void* labels, int label_dtype, int64_t begin, int64_t end,
                                 unsigned long long* wins_ties, unsigned long long* nonfinite, unsigned* verdict,
                                 void* workspace, size_t workspace_bytes, hipStream_t st, unsigned* check);
+
+// the cell-slotted form of the same (round 6; the two-step evaluation's default): one count pass
+// inserts every key into its cell's 8-word slot of `stab` (filled with +inf, and the packed byte
+// counters and meta's skew word zeroed, by the compaction of step 1), then the query pass, which
+// builds the block words from the byte counts itself: two launches instead of four.
+int64_t slotted_cells(int64_t Mcap);
+size_t slotted_table_bytes(int64_t Mcap);   // primary + secondary + tertiary regions (count_index.h)
+size_t slotted_fill_bytes(int64_t Mcap);    // the +inf part: primary + secondary
+int64_t slotted_cnt_words();                // the packed byte counters (words) the compaction zeroes
+unsigned* slotted_meta_ptr(void* workspace, int64_t Mcap);
+int counts_labeled_slotted(const SlotSource& src, unsigned* stab, int64_t Mcap, const float* scores,
+                           const void* labels, int label_dtype, int64_t begin, int64_t end,
+                           unsigned long long* wins_ties, unsigned long long* nonfinite, unsigned* verdict,
+                           void* workspace, size_t workspace_bytes, hipStream_t st, unsigned* check);
 
 }  // namespace dauc

@@ -1,17 +1,21 @@
-"""Per-rank device time of the two-step sharded evaluation (VERDICT r04 #3), on ONE GPU.
+"""Per-rank device time of the two-step sharded evaluation (VERDICT r04 #3, r05 #4), on ONE GPU.
 
 One rank of a G-GPU job runs dauc_auc_eval_compact_part over its slice, the slot all-gather, and
 dauc_auc_eval_query_part over the next slice. Here the G slots are gathered by a device copy once,
 and the rank's two calls are timed back to back (HIP events on the stream around `reps` sequences,
-no host read in between: the GPU time a rank spends; the collectives are not on one GPU). Parts 0
-and G-1 at configs[3] (2^24 @ 1 %) and configs[4] (2^27 @ 0.1 %), G = 2, 4, 8; the parts' counts
-are checked against the one-call evaluation. One JSON line per (n, G). With --trace only the G = 8
-sequences run (for a rocprofv3 kernel trace of one rank's chain).
+no host read in between: the GPU time a rank spends; the collectives are not on one GPU). Step 2
+consumes the build state its step 1 prepares in the workspace, so every timed step 2 follows its
+step 1 (the step-2 figure is the pair minus step 1 alone). Parts 0 and G-1 at configs[3] (2^24 @
+1 %) and configs[4] (2^27 @ 0.1 %), G = 2, 4, 8; the parts' counts are checked against the one-call
+evaluation. --ab: the tuning build, step 2's two forms interleaved (dauc_set_two_step_form: 0 the
+slotted build = the product's, 1 round 5's direct build). One JSON line per (n, G, form). With
+--trace only the G = 8 sequences run (for a rocprofv3 kernel trace of one rank's chain).
 
-    python scripts/probe_two_step.py [reps] [--trace]
+    python scripts/probe_two_step.py [reps] [--trace] [--ab]
 """
 from __future__ import annotations
 
+import contextlib
 import json
 import os
 import sys
@@ -19,12 +23,13 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
-from distributedauc_amd import ops  # noqa: E402
+from distributedauc_amd import _lib, ops  # noqa: E402
 from distributedauc_amd.loader import synthetic_scores  # noqa: E402
 
 args = [a for a in sys.argv[1:] if not a.startswith("--")]
 reps = int(args[0]) if args else 50
 trace = "--trace" in sys.argv
+ab = "--ab" in sys.argv
 dev = torch.device("cuda", 0)
 
 
@@ -41,29 +46,38 @@ def dev_ms(fn):
     return e0.elapsed_time(e1) / reps
 
 
-for log2n, pr in ((24, 0.01), (27, 0.001)):
-    s, y = synthetic_scores(1 << log2n, pr, dev)
-    n = s.numel()
-    whole = ops.auc_eval_counts(s, y)
-    for G in ((8,) if trace else (2, 4, 8)):
-        nb = ops.auc_slot_bytes(n, G)
-        slots = torch.empty(nb * G, dtype=torch.uint8, device=dev)
-        mine = torch.empty(nb, dtype=torch.uint8, device=dev)
-        rec = torch.zeros(8, dtype=torch.int64, device=dev)
-        for r in range(G):
-            ops.auc_eval_compact_part(s, y, r, G, slots[r * nb:(r + 1) * nb])
-        W = T = 0
-        for r in range(G):
-            v = ops.auc_eval_query_part(s, y, r, G, slots, out=rec).tolist()
-            assert v[4] == 0 and v[7] == 1, v
-            W, T = W + v[0], T + v[1]
-        out = {"log2n": log2n, "G": G, "slot_bytes": nb, "sum_matches_whole": (W, T) == whole[:2]}
-        for r in (0, G - 1):
-            out[f"ms_part{r}"] = dev_ms(lambda: (ops.auc_eval_compact_part(s, y, r, G, mine),
-                                                 ops.auc_eval_query_part(s, y, r, G, slots, out=rec)))
-            out[f"ms_compact_part{r}"] = dev_ms(lambda: ops.auc_eval_compact_part(s, y, r, G, mine))
-            out[f"ms_query_part{r}"] = dev_ms(lambda: ops.auc_eval_query_part(s, y, r, G, slots, out=rec))
-        out["ms_whole_one_call_events"] = dev_ms(lambda: ops.auc_eval_enqueue(s, y, 0, 1, out=rec))
-        print(json.dumps(out), flush=True)
-    del s, y
-    torch.cuda.empty_cache()
+ctx = _lib.using(_lib.tuning()) if ab else contextlib.nullcontext()
+with ctx:
+    for log2n, pr in ((24, 0.01), (27, 0.001)):
+        s, y = synthetic_scores(1 << log2n, pr, dev)
+        n = s.numel()
+        whole = ops.auc_eval_counts(s, y)
+        for G in ((8,) if trace else (2, 4, 8)):
+            for form in ((1, 0, 1, 0) if ab else (None,)):
+                if form is not None:
+                    ops.set_two_step_form(form)
+                nb = ops.auc_slot_bytes(n, G)
+                slots = torch.empty(nb * G, dtype=torch.uint8, device=dev)
+                mine = torch.empty(nb, dtype=torch.uint8, device=dev)
+                rec = torch.zeros(8, dtype=torch.int64, device=dev)
+                for r in range(G):
+                    ops.auc_eval_compact_part(s, y, r, G, slots[r * nb:(r + 1) * nb])
+                W = T = 0
+                for r in range(G):
+                    ops.auc_eval_compact_part(s, y, r, G, mine)
+                    v = ops.auc_eval_query_part(s, y, r, G, slots, out=rec).tolist()
+                    assert v[4] == 0 and v[7] == 1, v
+                    W, T = W + v[0], T + v[1]
+                out = {"log2n": log2n, "G": G, "form": form, "slot_bytes": nb, "sum_matches_whole": (W, T) == whole[:2]}
+                for r in (0, G - 1):
+                    out[f"ms_part{r}"] = dev_ms(lambda: (ops.auc_eval_compact_part(s, y, r, G, mine),
+                                                         ops.auc_eval_query_part(s, y, r, G, slots, out=rec)))
+                    out[f"ms_compact_part{r}"] = dev_ms(lambda: ops.auc_eval_compact_part(s, y, r, G, mine))
+                    out[f"ms_query_part{r}"] = out[f"ms_part{r}"] - out[f"ms_compact_part{r}"]
+                if not ab:
+                    out["ms_whole_one_call_events"] = dev_ms(lambda: ops.auc_eval_enqueue(s, y, 0, 1, out=rec))
+                print(json.dumps(out), flush=True)
+        del s, y
+        torch.cuda.empty_cache()
+    if ab:
+        ops.set_two_step_form(0)

@@ -532,8 +532,14 @@ def test_auc_errors_like_sklearn(dev):
         AUC(torch.tensor([1, -1, 1], device=dev), torch.tensor([0.1, float("nan"), 0.3], device=dev))
     with pytest.raises(ValueError):
         AUC(torch.tensor([1, -1, 1], device=dev), torch.tensor([0.1, float("inf"), 0.3], device=dev))
-    with pytest.raises(ValueError):
-        AUC(torch.tensor([1, -1, 0], device=dev), torch.tensor([0.1, 0.2, 0.3], device=dev))
+    # three label values: sklearn 1.7.2's roc_curve(pos_label=1) accepts a "multiclass" y_true when
+    # pos_label is given and takes every label other than 1 as a negative (0.0 here, like sklearn)
+    assert AUC(torch.tensor([1, -1, 0], device=dev), torch.tensor([0.1, 0.2, 0.3], device=dev)) == 0.0
+    assert AUC(torch.tensor([1, -1, 0, 1, 2], device=dev), torch.tensor([0.9, 0.1, 0.5, 0.4, 0.3], device=dev)) == (
+        pytest.approx(R.auc_sklearn(np.array([1, -1, 0, 1, 2]), np.array([0.9, 0.1, 0.5, 0.4, 0.3], np.float32)),
+                      rel=1e-12))
+    with pytest.raises(ValueError):  # non-integer float labels: "continuous" for sklearn
+        AUC(np.array([1.0, 0.5, 0.0]), np.array([0.1, 0.2, 0.3], np.float32))
     with warnings.catch_warnings(record=True) as rec:
         warnings.simplefilter("always")
         v = AUC(torch.tensor([1, 1, 1], device=dev), torch.tensor([0.1, 0.2, 0.3], device=dev))
@@ -869,7 +875,13 @@ def _two_step(dev, s, y, G):
         mine = torch.empty(nb, dtype=torch.uint8, device=dev)
         ops.auc_eval_compact_part(ts, ty, r, G, mine)
         slots[r * nb:(r + 1) * nb].copy_(mine)
-    return [ops.auc_eval_query_part(ts, ty, r, G, slots).cpu().tolist() for r in range(G)]
+    recs = []
+    for r in range(G):
+        # rank r's own step 1 just before its step 2 (the simulated ranks share one workspace, and
+        # step 2 consumes the build state step 1 prepares there)
+        ops.auc_eval_compact_part(ts, ty, r, G, mine)
+        recs.append(ops.auc_eval_query_part(ts, ty, r, G, slots).cpu().tolist())
+    return recs
 
 
 @pytest.mark.parametrize("ldtype", [np.int8, np.int32, np.int64])
@@ -949,8 +961,10 @@ def test_auc_eval_records_counted_in_place(dev):
     for r in range(G):
         ops.auc_eval_compact_part(ts, ty, r, G, slots[r * nb:(r + 1) * nb])
     recs = torch.full((8 * G,), -0x0123456789ABCDEF, dtype=torch.int64, device=dev)
+    mine = torch.empty(nb, dtype=torch.uint8, device=dev)
     for rep in range(2):
         for r in range(G):
+            ops.auc_eval_compact_part(ts, ty, r, G, mine)  # rank r's step 1 (the build state step 2 consumes)
             ops.auc_eval_query_part(ts, ty, r, G, slots, out=recs[8 * r:8 * (r + 1)])
         v = recs.view(G, 8).cpu().tolist()
         assert (sum(x[0] for x in v), sum(x[1] for x in v)) == (e["wins"], e["ties"]), rep

@@ -32,7 +32,17 @@ def _two_step(dev, ts, ty, G):
     slots = torch.empty(nb * G, dtype=torch.uint8, device=dev)
     for r in range(G):
         ops.auc_eval_compact_part(ts, ty, r, G, slots[r * nb:(r + 1) * nb])
-    return [ops.auc_eval_query_part(ts, ty, r, G, slots).cpu().tolist() for r in range(G)]
+    return [_query(dev, ts, ty, r, G, slots) for r in range(G)]
+
+
+def _query(dev, ts, ty, r, G, slots, out=None):
+    """Rank r's step 2 as a rank runs it: its own step 1 just before (the G simulated ranks share
+    one workspace here, and step 2 consumes the build state step 1 prepares there)."""
+    from distributedauc_amd import ops
+
+    nb = ops.auc_slot_bytes(ts.numel(), G)
+    ops.auc_eval_compact_part(ts, ty, r, G, torch.empty(nb, dtype=torch.uint8, device=dev))
+    return ops.auc_eval_query_part(ts, ty, r, G, slots, out=out).cpu().tolist()
 
 
 def _sorted_parts(dev, ts, ty, G):
@@ -135,7 +145,7 @@ def test_two_step_rejects_overlapping_buffers(dev):
         ops.auc_eval_enqueue(ts, ty, 0, G, out=ws[2048:2112].view(torch.int64))
     # the slots are untouched by the refused calls: the evaluation still gives the oracle's counts
     e = _oracle(ts, ty)
-    recs = [ops.auc_eval_query_part(ts, ty, r, G, slots).cpu().tolist() for r in range(G)]
+    recs = [_query(dev, ts, ty, r, G, slots) for r in range(G)]
     assert (sum(v[0] for v in recs), sum(v[1] for v in recs)) == (e["wins"], e["ties"])
 
 
@@ -208,3 +218,67 @@ def test_exact_auc_sharded_two_gloo_ranks_2e24():
     errs = [e for _, e in res if e]
     assert not errs, "\n".join(errs)
     assert sorted(r for r, _ in res) == list(range(world))
+
+
+@pytest.mark.parametrize("mults", [(5, 6, 8), (9, 12, 14), (15,)])
+def test_two_step_slotted_cells_of_many_keys(dev, mults):
+    """The slotted build (round 6): a cell's keys 0-3 in its primary window, 4-7 in its secondary
+    window, 8-14 in its tertiary run; a cell of 15+ keys refuses the index (verdict 2, as the direct
+    build's nibble did). Positives repeating one score value `m` times put m keys in one cell; the
+    negatives include that value (ties) and its neighbours. Bit-exact against the C oracle for G = 2,
+    3 (verdict 1 below 15 keys; verdict 2, then the sorted path, at 15)."""
+    from distributedauc_amd import ops
+
+    rng = np.random.default_rng(77 + sum(mults))
+    n = 400_003
+    # random scores below 0.25, the repeated values at 0.3 / 0.4 / 0.5: their top buckets hold
+    # nothing else, so each value's cell holds exactly its m keys
+    s = (rng.random(n, dtype=np.float32) * np.float32(0.25)).astype(np.float32)
+    y = np.where(rng.random(n) < 0.05, 1, -1).astype(np.int8)
+    pos = np.flatnonzero(y == 1)
+    neg = np.flatnonzero(y == -1)
+    at = 0
+    for j, m in enumerate(mults):
+        v = np.float32(0.3 + 0.1 * j)
+        s[pos[at:at + m]] = v
+        at += m
+        s[neg[100 * j:100 * j + 7]] = v                                     # ties
+        s[neg[100 * j + 7:100 * j + 9]] = np.nextafter(v, np.float32(1))     # just above
+        s[neg[100 * j + 9:100 * j + 11]] = np.nextafter(v, np.float32(0))    # just below
+    ts, ty = torch.from_numpy(s).to(dev), torch.from_numpy(y).to(dev)
+    e = _oracle(ts, ty)
+    for G in (2, 3):
+        recs = _two_step(dev, ts, ty, G)
+        verdicts = {v[7] for v in recs}
+        if max(mults) >= 15:
+            assert verdicts == {2}, recs
+            assert _sorted_parts(dev, ts, ty, G) == (e["wins"], e["ties"])
+        else:
+            assert verdicts == {1}, recs
+            assert (sum(v[0] for v in recs), sum(v[1] for v in recs)) == (e["wins"], e["ties"]), (G, recs)
+
+
+def test_two_step_second_query_without_step1(dev):
+    """Step 2 consumes the build state step 1 prepared in the workspace: a second
+    dauc_auc_eval_query_part without a new dauc_auc_eval_compact_part must not count the keys twice --
+    it reports verdict 2, and the blocking sorted path gives the exact integers."""
+    from distributedauc_amd import ops
+
+    n, G = 300_007, 2
+    g = torch.Generator(device=dev).manual_seed(9)
+    ts = torch.rand(n, generator=g, device=dev)
+    ty = torch.where(torch.rand(n, generator=g, device=dev) < 0.02, 1, -1).to(torch.int8)
+    e = _oracle(ts, ty)
+    nb = ops.auc_slot_bytes(n, G)
+    slots = torch.empty(nb * G, dtype=torch.uint8, device=dev)
+    for r in range(G):
+        ops.auc_eval_compact_part(ts, ty, r, G, slots[r * nb:(r + 1) * nb])
+    first = ops.auc_eval_query_part(ts, ty, G - 1, G, slots).cpu().tolist()
+    again = ops.auc_eval_query_part(ts, ty, G - 1, G, slots).cpu().tolist()
+    assert first[7] == 1 and again[7] == 2, (first, again)
+    assert again[3] == first[3] == e["P"] and again[4] == 0
+    assert _sorted_parts(dev, ts, ty, G) == (e["wins"], e["ties"])
+    # a fresh step 1 re-arms it
+    recs = _two_step(dev, ts, ty, G)
+    assert {v[7] for v in recs} == {1}
+    assert (sum(v[0] for v in recs), sum(v[1] for v in recs)) == (e["wins"], e["ties"])
