@@ -943,9 +943,19 @@ int compact_unordered(const float* scores, const void* labels, int label_dtype, 
     const int64_t nblk = (n + tile - 1) / tile;
     if (nblk > 0x7fffffffLL) return DAUC_EINVAL;
     const int vec = (reinterpret_cast<uintptr_t>(labels) & 15u) == 0;
-    // fill-only workgroups past the tiles: 4 16-byte stores per thread (the tiles' CUs stay theirs)
+    // fill-only workgroups past the tiles: `per` 16-byte stores per thread (the tiles' CUs stay theirs)
+#ifdef DAUC_TUNING
+    static int per = 0;  // tuning builds: DAUC_FILL_PER_THREAD
+    if (per == 0) {
+        const char* e = getenv("DAUC_FILL_PER_THREAD");
+        per = e ? atoi(e) : 4;
+        if (per < 1 || per > 4096) per = 4;
+    }
+#else
+    constexpr int per = 4;
+#endif
     const int64_t nfill = fill_w != nullptr ? nfill16 : 0;
-    const int64_t extra = (nfill + int64_t(threads) * 4 - 1) / (int64_t(threads) * 4);
+    const int64_t extra = (nfill + int64_t(threads) * per - 1) / (int64_t(threads) * per);
     if (nblk + extra > 0x7fffffffLL) return DAUC_EINVAL;
     const dim3 grid(static_cast<unsigned>(nblk + extra)), block(threads);
     uint4* fw = reinterpret_cast<uint4*>(fill_w);

@@ -27,6 +27,7 @@
 //   per-block integer sums, one 64-bit atomic each.
 //   table = positives: W += M - ub(x), T += ub - lb;  table = negatives: W += lb(x), T += ub - lb.
 
+#include <stdlib.h>
 #include <type_traits>
 
 #include "count_index.h"
@@ -908,6 +909,12 @@ __device__ __forceinline__ void slot_tertiary(unsigned x, unsigned c, unsigned c
 // back in place); `sorted` is the slotted table of `slot_cells` cells. A cell's keys are its primary
 // window (+inf past its count), its secondary window past 4 keys and, past 8 (rare), its tertiary
 // run: W += M - (rank_lo + #keys <= x), T += #(== x); no straddling windows.
+#ifdef DAUC_TUNING
+// tuning builds: DAUC_QUERY_ABL (timing ablations of the SLOT query pass; WRONG counts): 1 = no
+// query loop (the prologue and the reduction only), 2 = the block words zeroed instead of loaded
+// and converted (every cell empty: the loop's windows all read the +inf pad window)
+__device__ int g_query_abl = 0;
+#endif
 template <typename LT, bool CHECK = false, bool SLOT = false>
 __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __restrict__ s,
                                                                 const LT* __restrict__ lab, int64_t begin,
@@ -986,10 +993,15 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
         uint2 a[kL1Per], v[kBlkPer];
 #pragma unroll
         for (int j = 0; j < kL1Per; ++j) a[j] = l1g[j * kQueryThreads + threadIdx.x];
+#ifdef DAUC_TUNING
+        const bool abl2 = SLOT && g_query_abl == 2;
+#else
+        constexpr bool abl2 = false;
+#endif
 #pragma unroll
         for (int j = 0; j < kBlkPer; ++j) {
             const int i = j * kQueryThreads + threadIdx.x;
-            v[j] = i < nb ? blkg[i] : uint2{0u, 0u};
+            v[j] = i < nb && !abl2 ? blkg[i] : uint2{0u, 0u};
         }
         if (grp != nullptr) {
             // the direct build's block words hold prefixes within groups of 256 blocks: add the groups'
@@ -1010,7 +1022,7 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
     if constexpr (SLOT) {
         // byte counts -> block words {keys before the block, the 8 counts as nibbles}, in place:
         // thread t owns blocks [18 t, 18 t + 18); its run total, one workgroup scan, then each
-        // block rewritten with its exclusive prefix (counts <= 8: a skewed table never gets here)
+        // block rewritten with its exclusive prefix (counts <= 14: a skewed table never gets here)
         constexpr int kOwn = (kCiMaxBlocks + kQueryThreads - 1) / kQueryThreads;  // 18
         __syncthreads();
         const int b0 = threadIdx.x * kOwn;
@@ -1027,7 +1039,7 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
         for (int j = 0; j < kOwn; ++j) {
             if (b0 + j < nb) {
                 const uint2 r = blk[b0 + j];
-                // bytes b0..b3 (each <= 8) -> nibbles: 0x0b3b2b1b0 per half
+                // bytes b0..b3 (each <= 14) -> nibbles: 0x0b3b2b1b0 per half
                 const unsigned tl = (r.x & 0x000f000fu) | ((r.x >> 4) & 0x00f000f0u);
                 const unsigned th = (r.y & 0x000f000fu) | ((r.y >> 4) & 0x00f000f0u);
                 const unsigned nib = (tl & 0xffu) | ((tl >> 8) & 0xff00u) | ((th & 0xffu) << 16) | ((th >> 8) & 0xff00u) << 16;
@@ -1040,6 +1052,9 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
     const unsigned M32 = static_cast<unsigned>(M);
     unsigned long long w = 0, t = 0;
     unsigned nf = 0;  // CHECK: + #queries << 16
+#ifdef DAUC_TUNING
+    if (SLOT && g_query_abl == 1) end = begin;  // no queries: the prologue and the reduction only
+#endif
     const int64_t a0 = (begin + 3) & ~int64_t(3);
     const int64_t head = a0 < end ? a0 : end;
     const int64_t stride = int64_t(gridDim.x) * kQueryThreads;
@@ -1907,7 +1922,18 @@ int query_grid(int64_t L) {
             cus = 256;
         }
     }
-    int64_t g = (L + 4 * kQueryThreads - 1) / (4 * kQueryThreads);
+#ifdef DAUC_TUNING
+    // tuning builds: DAUC_QUERY_QPT = the queries per thread the grid aims at (default 4)
+    static int qpt = 0;
+    if (qpt == 0) {
+        const char* e = getenv("DAUC_QUERY_QPT");
+        qpt = e ? atoi(e) : 4;
+        if (qpt < 1 || qpt > 1024) qpt = 4;
+    }
+#else
+    constexpr int qpt = 4;
+#endif
+    int64_t g = (L + int64_t(qpt) * kQueryThreads - 1) / (int64_t(qpt) * kQueryThreads);
     if (g > 1 * cus) g = 1 * cus;  // 1024-thread workgroups
     if (g < 1) g = 1;
     return static_cast<int>(g);
@@ -2045,6 +2071,16 @@ int launch_ci(const float* s, const LT* lab, int64_t begin, int64_t end, const C
               unsigned* check = nullptr, const uint2* slot_counts = nullptr, unsigned slot_cells = 0u) {
     const dim3 grid(query_grid(end - begin)), block(kQueryThreads);
     const size_t lds = (size_t(kCiTop) + kCiMaxBlocks) * 8 + (grp ? size_t(kDirectMaxGroups) * 4 : 0);
+#ifdef DAUC_TUNING
+    {
+        static int abl = -1;
+        if (abl < 0) {
+            const char* e = getenv("DAUC_QUERY_ABL");
+            abl = e ? atoi(e) : 0;
+            if (hipMemcpyToSymbol(HIP_SYMBOL(g_query_abl), &abl, sizeof(int)) != hipSuccess) return DAUC_EINVAL;
+        }
+    }
+#endif
     // dynamic + the kernel's static reduction rows must fit the CU's 160 KB of LDS (a launch past it
     // aborts the queue: HSA_STATUS_ERROR_INVALID_ALLOCATION)
     static_assert((size_t(kCiTop) + kCiMaxBlocks) * 8 + size_t(kDirectMaxGroups) * 4 +

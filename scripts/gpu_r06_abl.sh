@@ -1,0 +1,13 @@
+#!/bin/bash
+# round 6: where the slotted query pass's fixed cost goes (tuning build, DAUC_QUERY_ABL timing
+# ablations; wrong counts by design, so only timed): 0 normal, 1 no query loop, 2 no block words
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+O=gpurun_out/r06abl
+mkdir -p $O
+for rep in 1 2; do
+for abl in 0 1 2; do
+  DAUC_QUERY_ABL=$abl timeout -k 10 120 python -u scripts/probe_query_abl.py 30 >> $O/abl.jsonl 2>> $O/abl.err || exit $?
+done
+done
+echo done

@@ -11,7 +11,7 @@ evaluation. --ab: the tuning build, step 2's two forms interleaved (dauc_set_two
 slotted build = the product's, 1 round 5's direct build). One JSON line per (n, G, form). With
 --trace only the G = 8 sequences run (for a rocprofv3 kernel trace of one rank's chain).
 
-    python scripts/probe_two_step.py [reps] [--trace] [--ab]
+    python scripts/probe_two_step.py [reps] [--trace] [--ab | --tuning]
 """
 from __future__ import annotations
 
@@ -30,6 +30,7 @@ args = [a for a in sys.argv[1:] if not a.startswith("--")]
 reps = int(args[0]) if args else 50
 trace = "--trace" in sys.argv
 ab = "--ab" in sys.argv
+tun = ab or "--tuning" in sys.argv  # --tuning: the tuning build, product form (its DAUC_* env knobs)
 dev = torch.device("cuda", 0)
 
 
@@ -46,14 +47,14 @@ def dev_ms(fn):
     return e0.elapsed_time(e1) / reps
 
 
-ctx = _lib.using(_lib.tuning()) if ab else contextlib.nullcontext()
+ctx = _lib.using(_lib.tuning()) if tun else contextlib.nullcontext()
 with ctx:
     for log2n, pr in ((24, 0.01), (27, 0.001)):
         s, y = synthetic_scores(1 << log2n, pr, dev)
         n = s.numel()
         whole = ops.auc_eval_counts(s, y)
         for G in ((8,) if trace else (2, 4, 8)):
-            for form in ((1, 0, 1, 0) if ab else (None,)):
+            for form in ((1, 0, 1, 0) if ab else (0,) if tun else (None,)):
                 if form is not None:
                     ops.set_two_step_form(form)
                 nb = ops.auc_slot_bytes(n, G)
@@ -74,10 +75,11 @@ with ctx:
                                                          ops.auc_eval_query_part(s, y, r, G, slots, out=rec)))
                     out[f"ms_compact_part{r}"] = dev_ms(lambda: ops.auc_eval_compact_part(s, y, r, G, mine))
                     out[f"ms_query_part{r}"] = out[f"ms_part{r}"] - out[f"ms_compact_part{r}"]
+                out["env"] = {k: v for k, v in os.environ.items() if k.startswith("DAUC_")}
                 if not ab:
                     out["ms_whole_one_call_events"] = dev_ms(lambda: ops.auc_eval_enqueue(s, y, 0, 1, out=rec))
                 print(json.dumps(out), flush=True)
         del s, y
         torch.cuda.empty_cache()
-    if ab:
+    if tun:
         ops.set_two_step_form(0)
