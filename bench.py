@@ -133,6 +133,7 @@ def parse(argv=None):
                    help="stride-1 1x1 convs as hipBLASLt GEMMs where faster (per-shape timing; 1/0)")
     # internal: one process of the configs[0] CPU baseline (never touches the GPU)
     p.add_argument("--cpu-coda-worker", action="store_true", help=argparse.SUPPRESS)
+    p.add_argument("--cpu-train-worker", action="store_true", help=argparse.SUPPRESS)
     p.add_argument("--cw-rank", type=int, default=0, help=argparse.SUPPRESS)
     p.add_argument("--cw-port", type=int, default=0, help=argparse.SUPPRESS)
     p.add_argument("--cw-threads", type=int, default=1, help=argparse.SUPPRESS)
@@ -140,8 +141,29 @@ def parse(argv=None):
     return p.parse_args(argv)
 
 
+_last_log = ["start", time.time()]
+
+
 def log(msg: str):
+    _last_log[:] = [msg, time.time()]
     print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
+def start_heartbeat(period: float = 45.0) -> None:
+    """A line on stderr whenever `period` seconds pass without one (long CPU-baseline legs, first
+    MIOpen searches): a watchdog that reads silence as a hang sees the run alive."""
+    import threading
+
+    def beat():
+        while True:
+            time.sleep(period / 3)
+            msg, t = _last_log
+            if time.time() - t >= period:
+                print(f"[bench {time.strftime('%H:%M:%S')}] still running: {msg} (+{time.time() - t:.0f} s)",
+                      file=sys.stderr, flush=True)
+                _last_log[1] = time.time()
+
+    threading.Thread(target=beat, daemon=True).start()
 
 
 def free_port() -> int:
@@ -162,8 +184,10 @@ def host_info() -> dict:
         # baselines run on rank 0 alone while the other ranks wait, so use the default share
         omp = None
     budget = min(affinity, int(omp)) if omp and omp.isdigit() and int(omp) > 0 else min(affinity, 16)
+    quota = cgroup_cpus()
+    usable = min(affinity, int(quota)) if quota else affinity  # CPUs of time the process can get
     return {"nproc": os.cpu_count(), "affinity_cpus": affinity, "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
-            "cpu_budget": budget, "cgroup_cpu_quota": cgroup_cpus()}
+            "cpu_budget": budget, "cgroup_cpu_quota": quota, "usable_cpus": max(usable, 1)}
 
 
 def cgroup_cpus():
@@ -814,18 +838,61 @@ def step_roofline(args, res) -> dict:
 # ----------------------------------------------------------------------------- CPU baselines
 def cpu_baseline_train_cores(args, host):
     """configs[1]'s CPU path at the thread budget (OMP_NUM_THREADS, the box's CPU share) and at every
-    CPU of the affinity mask; `value` is the faster. A run whose warm-up projects
-    more than --cpu-max-s seconds for the timed step is skipped and says so (a bounded sample)."""
+    CPU of the affinity mask; `value` is the faster. The all-CPU leg runs in a child
+    process that never touches the GPU, killed after 2 x --cpu-max-s (a bounded sample: on a host
+    whose cgroup quota is below the affinity mask, that many threads oversubscribe the quota)."""
     runs = [cpu_baseline_train(args, host["cpu_budget"])]
-    if host["affinity_cpus"] > host["cpu_budget"]:
-        runs.append(cpu_baseline_train(args, host["affinity_cpus"], max_s=args.cpu_max_s))
+    more = all_cores_leg(host)
+    if isinstance(more, int):
+        log(f"cpu baseline: {args.arch} step at {more} threads (every usable CPU; child process)")
+        runs.append(cpu_train_child(args, more, timeout=2 * args.cpu_max_s))
+    else:
+        runs.append({"cores": host["affinity_cpus"], "skipped": more})
     torch.set_num_threads(host["cpu_budget"])
     done = [r for r in runs if "value" in r]
     best = dict(max(done, key=lambda r: r["value"]))
     best["by_threads"] = runs
-    best["cores_note"] = (f"timed at {host['cpu_budget']} threads (the budget) and at all {host['affinity_cpus']} CPUs of "
-                          f"the affinity mask (cgroup quota: {host.get('cgroup_cpu_quota')} CPUs); value = the faster")
+    best["cores_note"] = (f"timed at {host['cpu_budget']} threads (the budget); nproc {host['nproc']}, affinity mask "
+                          f"{host['affinity_cpus']} CPUs, cgroup quota {host.get('cgroup_cpu_quota')} CPUs; value = the "
+                          "fastest leg")
     return best
+
+
+def all_cores_leg(host):
+    """Threads for the every-CPU leg of the CPU baselines, or why it is not run: the
+    CPUs of time the process can get are the affinity mask capped by the cgroup quota. On the GPU box
+    the quota is 16 CPUs under a 256-CPU mask, and threads past it oversubscribe the quota: ResNet-50
+    b32 took 2.0x as long at 64 threads as at 16, and at 256 threads did not finish one step in 180 s
+    (profiles/r06/host_cores/)."""
+    usable = host.get("usable_cpus", host["affinity_cpus"])
+    if usable > host["cpu_budget"]:
+        return usable
+    return (f"not run: the cgroup quota ({host.get('cgroup_cpu_quota')} CPUs) caps this process below its "
+            f"{host['affinity_cpus']}-CPU affinity mask, so the budget of {host['cpu_budget']} threads is every CPU it "
+            "can use; more threads oversubscribe the quota (64 threads: 2.0x slower than 16, 256 threads: no "
+            "ResNet-50 step in 180 s, profiles/r06/host_cores/)")
+
+
+def cpu_train_child(args, threads, timeout):
+    """cpu_baseline_train(args, threads) in a child process (HIP hidden: it never touches the GPU),
+    killed after `timeout` seconds; its record, or why there is none."""
+    with tempfile.TemporaryDirectory() as td:
+        out = Path(td) / "cpu_train.json"
+        env = {k: v for k, v in os.environ.items() if not (k.startswith("TORCHELASTIC_") or k in _LAUNCH_VARS)}
+        env.update(HIP_VISIBLE_DEVICES="", CUDA_VISIBLE_DEVICES="", ROCR_VISIBLE_DEVICES="", OMP_NUM_THREADS=str(threads))
+        cmd = [sys.executable, str(Path(__file__).resolve()), "--cpu-train-worker", "--cw-threads", str(threads),
+               "--cw-out", str(out), "--arch", args.arch, "--batch", str(args.batch), "--image-size",
+               str(args.image_size), "--pos-ratio", str(args.pos_ratio), "--cpu-max-s", str(args.cpu_max_s)]
+        proc = subprocess.Popen(cmd, env=env)
+        try:
+            rc = proc.wait(timeout=timeout)
+        except subprocess.TimeoutExpired:
+            proc.kill()
+            proc.wait()
+            return {"cores": threads, "skipped": f"not done within {timeout:.0f} s (a bounded sample)"}
+        if rc != 0 or not out.exists():
+            return {"cores": threads, "skipped": f"child exited with {rc}"}
+        return json.loads(out.read_text())
 
 
 def cpu_baseline_train(args, threads, max_s=None):
@@ -1034,7 +1101,8 @@ def cpu_baseline_auc(auc_res, max_log2n=None, oracle_check=False):
 def self_launch(args) -> int | None:
     """--gpus N without a launcher: start N ranks as a torch.distributed.run child process (this
     process has not touched the GPU) and return its exit code."""
-    if args.cpu_coda_worker or "WORLD_SIZE" in os.environ or (args.gpus <= 1 and args.backend is None):
+    if args.cpu_coda_worker or args.cpu_train_worker or "WORLD_SIZE" in os.environ or (
+            args.gpus <= 1 and args.backend is None):
         return None
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
            "--master-addr=127.0.0.1", f"--master-port={free_port()}", str(Path(__file__).resolve()), *sys.argv[1:]]
@@ -1066,9 +1134,14 @@ def main():
     if args.cpu_coda_worker:
         cpu_coda_worker(args)
         return
+    if args.cpu_train_worker:  # one CPU baseline leg in a child process (cpu_train_child)
+        Path(args.cw_out).write_text(json.dumps(cpu_baseline_train(args, args.cw_threads, max_s=args.cpu_max_s)))
+        return
     rc = self_launch(args)
     if rc is not None:
         sys.exit(rc)
+    if int(os.environ.get("RANK", "0")) == 0:
+        start_heartbeat()
     # Only the JSON record goes to stdout: everything else written to fd 1 (gloo's C++ connection
     # messages, CPU worker children, library chatter) is sent to stderr for the rest of the run.
     json_fd = os.dup(1)
@@ -1185,10 +1258,12 @@ def main():
             if r18 is not None and args.cpu_workers > 0:
                 log("cpu baseline: configs[0] gloo workers")
                 c0 = cpu_baseline_configs0(args, host)
-                if host["affinity_cpus"] > host["cpu_budget"] and "value" in c0:
-                    log("cpu baseline: configs[0] gloo workers on every CPU of the affinity mask")
-                    c0["all_cores"] = cpu_baseline_configs0(args, host, threads_total=host["affinity_cpus"],
-                                                            timeout=args.cpu_max_s * 2)
+                more = all_cores_leg(host)
+                if isinstance(more, int) and "value" in c0:
+                    log(f"cpu baseline: configs[0] gloo workers on {more} threads (every usable CPU)")
+                    c0["all_cores"] = cpu_baseline_configs0(args, host, threads_total=more, timeout=args.cpu_max_s * 2)
+                elif not isinstance(more, int):
+                    c0["all_cores"] = {"cores": host["affinity_cpus"], "skipped": more}
                 out.setdefault("configs0", {})["cpu"] = c0
             torch.set_num_threads(threads)
             if auc is not None:

@@ -104,7 +104,7 @@ TUNING_SIGNATURES = {
     "dauc_pair_count_variant": (_int, [_vp, _i64, _vp, _i64, _vp, _int, _vp]),
     "dauc_set_search_mode": (_int, [_int]),
     "dauc_set_direct_fault": (_int, [_int]),
-    "dauc_set_two_step_form": (_int, [_int]),
+    "dauc_set_index_form": (_int, [_int]),
     "dauc_probe_tr16": (_int, [_vp, _vp]),
     "dauc_set_wgrad_form": (_int, [_int]),
 }

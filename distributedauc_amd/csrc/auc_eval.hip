@@ -109,6 +109,15 @@ EvalWs with_record(EvalWs w, int64_t* rec) {
     return w;
 }
 
+#ifdef DAUC_TUNING
+// tuning builds: the count index's build (dauc_set_index_form), in the one-call and the two-step
+// evaluation alike: 0 the slotted table (the product's), 1 round 5's direct build (count, blocks,
+// scatter passes into the cell-ordered table)
+int g_index_form = 0;
+#else
+constexpr int g_index_form = 0;
+#endif
+
 // Steps 1-3 (no host synchronisation, no allocation): the record at w.wt .. w.verdict (the
 // workspace header, or the caller's part_out through with_record).
 int enqueue(const float* scores, const void* labels, int label_dtype, int64_t n, int part, int parts,
@@ -122,11 +131,17 @@ int enqueue(const float* scores, const void* labels, int label_dtype, int64_t n,
         return -static_cast<int>(e);
     }
     const int64_t mcap = direct_capacity(n);
-    // the compaction builds the direct build's histogram and zeroes its per-cell counters (spread
-    // over its grid), so the build skips its histogram pass
-    int rc = compact_unordered(scores, labels, label_dtype, n, w.pos, w.slot, 0ull, w.spare, 0ull, nullptr,
-                               direct_cnt_ptr(w.tws, mcap), static_cast<int>(direct_cnt_words()), st, INT64_MAX,
-                               w.hist);
+    // the compaction builds the index build's histogram and prepares its state (spread over its
+    // grid): the per-cell counters zeroed, so the build skips its histogram pass; for the slotted
+    // build (round 6) also the slotted table's +inf fill and meta words 8..13
+    const bool slot = g_index_form == 0;
+    unsigned* cnt = direct_cnt_ptr(w.tws, mcap);
+    auto* meta8 = reinterpret_cast<unsigned long long*>(slotted_meta_ptr(w.tws, mcap) + 8);
+    int rc = compact_unordered(scores, labels, label_dtype, n, w.pos, w.slot, 0ull, w.spare, 0ull,
+                               slot ? meta8 : nullptr, cnt,
+                               static_cast<int>(slot ? slotted_cnt_words() : direct_cnt_words()), st, INT64_MAX,
+                               w.hist, nullptr, 0ull, slot ? w.stab : nullptr,
+                               slot ? static_cast<int64_t>(slotted_fill_bytes(mcap) / 16) : 0);
     if (rc) return rc;
     const int64_t qlo = n * part / parts, qhi = n * (part + 1) / parts;
     if (qhi <= qlo) return DAUC_OK;  // an empty part: verdict 0, counts 0
@@ -134,6 +149,9 @@ int enqueue(const float* scores, const void* labels, int label_dtype, int64_t n,
         // a tuning build forcing another search structure: straight to the sorted path
         return -static_cast<int>(hipMemsetAsync(w.verdict, 2, 1, st));
     }
+    if (slot)
+        return counts_labeled_direct_slotted(w.pos, w.slot, mcap, w.stab, scores, labels, label_dtype, qlo, qhi, w.wt,
+                                             w.wt + 2, w.verdict, w.tws, w.tws_bytes, st, w.hist);
     return counts_labeled_direct(w.pos, w.slot, mcap, scores, labels, label_dtype, qlo, qhi, w.wt, w.wt + 2,
                                  w.verdict, w.tws, w.tws_bytes, st, w.hist);
 }
@@ -232,13 +250,6 @@ int counts_part_blocking(const float* scores, const void* labels, int label_dtyp
 constexpr size_t kSlotHist = 256, kSlotHdr = kSlotHist + size_t(kCiTop) * 4;
 constexpr int kSlotN = 4;  // header word: the n the slot was built for
 
-#ifdef DAUC_TUNING
-// tuning builds: the two-step's step-2 build (dauc_set_two_step_form): 0 the slotted table (the
-// product's), 1 round 5's direct build (count, blocks, scatter passes into the cell-ordered table)
-int g_two_step_form = 0;
-#else
-constexpr int g_two_step_form = 0;
-#endif
 
 int64_t slot_cap(int parts) {
     const int64_t fair = (direct_capacity(INT64_MAX / 4) + parts - 1) / parts;
@@ -301,8 +312,8 @@ int dauc_auc_eval_compact_part(const float* scores, const void* labels, int labe
     unsigned* cnt = direct_cnt_ptr(w.tws, mcap);
     auto* meta8 = reinterpret_cast<unsigned long long*>(slotted_meta_ptr(w.tws, mcap) + 8);
     // (form 1, tuning builds: round 5's direct build counts into one u32 per cell and fills nothing)
-    const size_t tab = g_two_step_form == 0 ? slotted_fill_bytes(mcap) : 0;
-    const int64_t ncnt = g_two_step_form == 0 ? slotted_cnt_words() : direct_cnt_words();
+    const size_t tab = g_index_form == 0 ? slotted_fill_bytes(mcap) : 0;
+    const int64_t ncnt = g_index_form == 0 ? slotted_cnt_words() : direct_cnt_words();
     if (hi <= lo) {
         // an empty slice: P_r = 0, the length word still set (its two halves), and step 2's state
         // reset by memsets (the compaction's job otherwise)
@@ -347,7 +358,7 @@ int dauc_auc_eval_query_part(const float* scores, const void* labels, int label_
     SlotSource src{static_cast<const unsigned char*>(slots), slot_bytes(parts), kSlotHist, kSlotHdr, parts, part,
                    slot_cap(parts), n, qhi - qlo, w.wt, w.slot, reinterpret_cast<unsigned long long*>(w.verdict),
                    w.spare};
-    if (g_two_step_form == 1)
+    if (g_index_form == 1)
         return counts_labeled_direct_slots(src, w.pos, mcap, scores, labels, label_dtype, qlo, qhi, w.wt, w.wt + 2,
                                            w.verdict, w.tws, w.tws_bytes, st, reinterpret_cast<unsigned*>(part_out + 4));
     return counts_labeled_slotted(src, w.stab, mcap, scores, labels, label_dtype, qlo, qhi, w.wt, w.wt + 2, w.verdict,
@@ -373,9 +384,9 @@ int dauc_auc_eval_counts_part(const float* scores, const void* labels, int label
 }
 
 #ifdef DAUC_TUNING
-int dauc_set_two_step_form(int form) {
+int dauc_set_index_form(int form) {
     if (form < 0 || form > 1) return DAUC_EINVAL;
-    g_two_step_form = form;
+    g_index_form = form;
     return DAUC_OK;
 }
 #endif

@@ -1362,6 +1362,37 @@ __global__ __launch_bounds__(256) void direct_hist_kernel(const float* __restric
         if (h[i]) atomicAdd(hist + i, h[i]);
 }
 
+// The slotted build's insertion (count_index.h), one key per live lane; every lane of the wave
+// calls it. The key's rank in its cell is the byte its returning add on the cell's packed counter
+// found (a wave whose keys all fall in one cell -- tie-heavy tables -- adds once and ranks its lanes
+// itself); ranks 0-3 go to the primary window, 4-7 to the secondary, 8-13 to the tertiary run.
+// Returns true for a key past 14 in its cell (the caller marks the index skewed; a byte past 255
+// also carries into the next cell's counter: skewed anyway).
+__device__ __forceinline__ bool slot_insert(unsigned x, unsigned c, bool live, unsigned* __restrict__ cnt,
+                                            unsigned* __restrict__ stab, unsigned cells, int lane) {
+    const unsigned long long act = __ballot(live);
+    if (act == 0ull) return false;
+    const int first = __ffsll(static_cast<long long>(act)) - 1;
+    const unsigned cf = __shfl(c, first, kWave);
+    unsigned rank = 0u;
+    if (__ballot(live && c == cf) == act) {
+        unsigned old = 0u;
+        if (lane == first) old = atomicAdd(cnt + (cf >> 2), static_cast<unsigned>(__popcll(act)) << (8u * (cf & 3u)));
+        old = __shfl(old, first, kWave);
+        const unsigned below = static_cast<unsigned>(__popcll(act & (lane == 0 ? 0ull : (~0ull >> (kWave - lane)))));
+        rank = ((old >> (8u * (cf & 3u))) & 0xffu) + below;
+    } else if (live) {
+        const unsigned old = atomicAdd(cnt + (c >> 2), 1u << (8u * (c & 3u)));
+        rank = (old >> (8u * (c & 3u))) & 0xffu;
+    }
+    if (!live) return false;
+    if (rank < 4u) stab[4u * c + rank] = x;
+    else if (rank < 8u) stab[slot_sec(cells, c) + rank - 4u] = x;
+    else if (rank < kSlotMaxKeys) stab[slot_ter(cells, c) + rank - 8u] = x;
+    else return true;
+    return false;
+}
+
 // The plan of ci_plan_kernel from the bucket sizes themselves, computed by EVERY workgroup of the
 // count pass in LDS (2048 buckets, 8 per thread: cheaper than a one-workgroup launch between the
 // histogram and the counts): C_t = ceil(n_t * num / M) cells per used bucket, num = min(cells left
@@ -1369,12 +1400,17 @@ __global__ __launch_bounds__(256) void direct_hist_kernel(const float* __restric
 // writes the plan and the verdict words for the later passes. Then the per-cell key counts (a wave
 // whose keys all fall in one cell adds once: tie-heavy tables) and every key's cell.
 
+// SLOT (round 6, the one-call evaluation's default): every key inserted into the cell-slotted
+// table instead (slot_insert; the compaction prepared the table, the packed counters and meta).
+template <bool SLOT = false>
 __global__ __launch_bounds__(kDirectThreads) void direct_count_kernel(const float* __restrict__ pos, int64_t mcap,
                                                                       const unsigned* __restrict__ hist,
                                                                       uint2* __restrict__ l1g,
                                                                       unsigned* __restrict__ meta,
                                                                       unsigned* __restrict__ cnt,
-                                                                      unsigned* __restrict__ cell) {
+                                                                      unsigned* __restrict__ cell,
+                                                                      unsigned* __restrict__ stab = nullptr,
+                                                                      unsigned slot_cells = 0u) {
     static_assert(kCiTop == 8 * kDirectThreads, "eight top buckets per thread");
     __shared__ uint2 l1[kCiTop];
     __shared__ unsigned wtot[kDirectThreads / kWave];
@@ -1420,11 +1456,26 @@ __global__ __launch_bounds__(kDirectThreads) void direct_count_kernel(const floa
             meta[kCiOk] = ok ? 1u : 0u;
             meta[kCiCells] = total;
             meta[kCiBlocks] = (total + 1 + kCiBlock - 1) / kCiBlock;
-            meta[kCiSkew] = 0u;
+            if constexpr (!SLOT) meta[kCiSkew] = 0u;  // SLOT: zeroed by the compaction (set by any workgroup)
         }
     }
     if (!ok) return;
     const int lane = threadIdx.x & (kWave - 1);
+    if constexpr (SLOT) {
+        bool skew = false;
+        for (int64_t i0 = int64_t(blockIdx.x) * kDirectThreads; i0 < M; i0 += int64_t(gridDim.x) * kDirectThreads) {
+            const int64_t i = i0 + threadIdx.x;
+            const bool live = i < M;
+            unsigned x = 0u, c = 0u;
+            if (live) {
+                x = key_fast(pos[i]);
+                c = ci_cell(x, l1[x >> kCiLowBits]);
+            }
+            skew |= slot_insert(x, c, live, cnt, stab, slot_cells, lane);
+        }
+        if (__ballot(skew) != 0ull && lane == 0) atomicOr(meta + kCiSkew, 1u);
+        return;
+    }
     for (int64_t i0 = int64_t(blockIdx.x) * kDirectThreads; i0 < M; i0 += int64_t(gridDim.x) * kDirectThreads) {
         const int64_t i = i0 + threadIdx.x;
         const bool live = i < M;
@@ -1636,30 +1687,7 @@ __global__ __launch_bounds__(kSlotCountThreads) void direct_count_slots_kernel(S
                 x = key_fast(v);
                 c = ci_cell(x, l1[x >> kCiLowBits]);
             }
-            const unsigned long long act = __ballot(live);
-            if (act == 0ull) continue;
-            const int first = __ffsll(static_cast<long long>(act)) - 1;
-            const unsigned cf = __shfl(c, first, kWave);
-            unsigned rank = 0u;
-            if (__ballot(live && c == cf) == act) {
-                // every key of the wave in one cell (tie-heavy tables): one add for all of them
-                unsigned old = 0u;
-                if (lane == first)
-                    old = atomicAdd(cnt + (cf >> 2), static_cast<unsigned>(__popcll(act)) << (8u * (cf & 3u)));
-                old = __shfl(old, first, kWave);
-                const unsigned below = static_cast<unsigned>(
-                    __popcll(act & ((lane == 0 ? 0ull : (~0ull >> (kWave - lane))))));
-                rank = ((old >> (8u * (cf & 3u))) & 0xffu) + below;
-            } else if (live) {
-                const unsigned old = atomicAdd(cnt + (c >> 2), 1u << (8u * (c & 3u)));
-                rank = (old >> (8u * (c & 3u))) & 0xffu;
-            }
-            if (live) {
-                if (rank < 4u) stab[4u * c + rank] = x;
-                else if (rank < 8u) stab[slot_sec(slot_cells, c) + rank - 4u] = x;
-                else if (rank < kSlotMaxKeys) stab[slot_ter(slot_cells, c) + rank - 8u] = x;
-                else skew = true;  // (a byte past 255 also carries into the next cell: skewed anyway)
-            }
+            skew |= slot_insert(x, c, live, cnt, stab, slot_cells, lane);
         }
         if (__ballot(skew) != 0ull && lane == 0) atomicOr(meta + kCiSkew, 1u);
         return;
@@ -2089,6 +2117,9 @@ int launch_ci(const float* s, const LT* lab, int64_t begin, int64_t end, const C
     if (slot_counts != nullptr && check != nullptr)
         hipLaunchKernelGGL((query_ci_kernel<LT, true, true>), grid, block, lds, st, s, lab, begin, end, cw.meta, cw.l1,
                            slot_counts, sorted, M, out, nonfinite, verdict, nullptr, Mp, check, slot_cells);
+    else if (slot_counts != nullptr)
+        hipLaunchKernelGGL((query_ci_kernel<LT, false, true>), grid, block, lds, st, s, lab, begin, end, cw.meta,
+                           cw.l1, slot_counts, sorted, M, out, nonfinite, verdict, nullptr, Mp, nullptr, slot_cells);
     else if (check != nullptr)
         hipLaunchKernelGGL((query_ci_kernel<LT, true>), grid, block, lds, st, s, lab, begin, end, cw.meta, cw.l1,
                            cw.blk, sorted, M, out, nonfinite, verdict, grp, Mp, check, 0u);
@@ -2215,8 +2246,9 @@ int build_direct_index(const float* pos, const unsigned long long* Mp, int64_t M
     if (ready_hist == nullptr)
         hipLaunchKernelGGL(direct_hist_kernel, blocks(Mcap, 256 * kDirectPerThread, 256), dim3(256), 0, st, pos, Mp,
                            nw.first, nw.cstart, kCiCntWords);
-    hipLaunchKernelGGL(direct_count_kernel, blocks(Mcap, kDirectThreads, kDirectGrid), dim3(kDirectThreads), 0, st, pos,
-                       Mcap, ready_hist ? ready_hist : nw.first, nw.l1, nw.meta, nw.cstart, w.keys_b);
+    hipLaunchKernelGGL(direct_count_kernel<false>, blocks(Mcap, kDirectThreads, kDirectGrid), dim3(kDirectThreads), 0,
+                       st, pos, Mcap, ready_hist ? ready_hist : nw.first, nw.l1, nw.meta, nw.cstart, w.keys_b,
+                       nullptr, 0u);
     hipLaunchKernelGGL(direct_blocks_kernel, dim3(kDirectMaxGroups), dim3(kDirectGroup), 0, st, nw.cstart, nw.meta,
                        nw.blk, grp);
 #ifdef DAUC_TUNING
@@ -2314,6 +2346,39 @@ int counts_labeled_slotted(const SlotSource& src, unsigned* stab, int64_t Mcap, 
         default:
             return launch_ci(scores, static_cast<const int64_t*>(labels), begin, end, nw, stab, 0, wins_ties, nonfinite,
                              st, verdict, nullptr, Mp, check, counts, cells);
+    }
+}
+
+int counts_labeled_direct_slotted(const float* pos, const unsigned long long* Mp, int64_t Mcap, unsigned* stab,
+                                  const float* scores, const void* labels, int label_dtype, int64_t begin,
+                                  int64_t end, unsigned long long* wins_ties, unsigned long long* nonfinite,
+                                  unsigned* verdict, void* workspace, size_t workspace_bytes, hipStream_t st,
+                                  const unsigned* ready_hist) {
+    if (begin < 0 || end < begin || wins_ties == nullptr || pos == nullptr || Mp == nullptr || stab == nullptr ||
+        ready_hist == nullptr || Mcap < 1 || workspace == nullptr || workspace_bytes < dauc_sort_workspace_size(Mcap) ||
+        (end > begin && (scores == nullptr || labels == nullptr)))
+        return DAUC_EINVAL;
+    if (label_dtype != DAUC_LABEL_I8 && label_dtype != DAUC_LABEL_I32 && label_dtype != DAUC_LABEL_I64)
+        return DAUC_EINVAL;
+    const CountWs nw = count_ws_of(workspace, Mcap);
+    const unsigned cells = static_cast<unsigned>(slotted_cells(Mcap));
+    const int64_t gb = (Mcap + kDirectThreads - 1) / kDirectThreads;
+    hipLaunchKernelGGL(direct_count_kernel<true>, dim3(static_cast<unsigned>(gb < kDirectGrid ? gb : kDirectGrid)),
+                       dim3(kDirectThreads), 0, st, pos, Mcap, ready_hist, nw.l1, nw.meta, nw.cstart, nullptr, stab,
+                       cells);
+    int rc = launch_status();
+    if (rc || end == begin) return rc;
+    const uint2* counts = reinterpret_cast<const uint2*>(nw.cstart);
+    switch (label_dtype) {
+        case DAUC_LABEL_I8:
+            return launch_ci(scores, static_cast<const int8_t*>(labels), begin, end, nw, stab, 0, wins_ties, nonfinite,
+                             st, verdict, nullptr, Mp, nullptr, counts, cells);
+        case DAUC_LABEL_I32:
+            return launch_ci(scores, static_cast<const int32_t*>(labels), begin, end, nw, stab, 0, wins_ties, nonfinite,
+                             st, verdict, nullptr, Mp, nullptr, counts, cells);
+        default:
+            return launch_ci(scores, static_cast<const int64_t*>(labels), begin, end, nw, stab, 0, wins_ties, nonfinite,
+                             st, verdict, nullptr, Mp, nullptr, counts, cells);
     }
 }
 

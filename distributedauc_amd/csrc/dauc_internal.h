@@ -168,6 +168,14 @@ size_t slotted_table_bytes(int64_t Mcap);   // primary + secondary + tertiary re
 size_t slotted_fill_bytes(int64_t Mcap);    // the +inf part: primary + secondary
 int64_t slotted_cnt_words();                // the packed byte counters (words) the compaction zeroes
 unsigned* slotted_meta_ptr(void* workspace, int64_t Mcap);
+// the one-call evaluation's slotted form: the same insertion from the compacted positives `pos`
+// (P on the device at *Mp, the top-bucket histogram ready), then the query pass (two launches
+// instead of three after the compaction)
+int counts_labeled_direct_slotted(const float* pos, const unsigned long long* Mp, int64_t Mcap, unsigned* stab,
+                                  const float* scores, const void* labels, int label_dtype, int64_t begin,
+                                  int64_t end, unsigned long long* wins_ties, unsigned long long* nonfinite,
+                                  unsigned* verdict, void* workspace, size_t workspace_bytes, hipStream_t st,
+                                  const unsigned* ready_hist);
 int counts_labeled_slotted(const SlotSource& src, unsigned* stab, int64_t Mcap, const float* scores,
                            const void* labels, int label_dtype, int64_t begin, int64_t end,
                            unsigned long long* wins_ties, unsigned long long* nonfinite, unsigned* verdict,

@@ -766,11 +766,12 @@ def set_direct_fault(mode: int) -> None:
     check(_lib.tuning().dauc_set_direct_fault(int(mode)), "dauc_set_direct_fault")
 
 
-def set_two_step_form(form: int) -> None:
-    """Step 2 of the two-step sharded evaluation in the tuning build (dauc_set_two_step_form): 0 the
-    product's cell-slotted build, 1 round 5's direct build. Same integers; for A/B measurements and
-    tests. Set it before step 1."""
-    check(_lib.tuning().dauc_set_two_step_form(int(form)), "dauc_set_two_step_form")
+def set_index_form(form: int) -> None:
+    """The count index's build in the exact-AUC evaluations of the tuning build (dauc_set_index_form;
+    the one-call and the two-step forms): 0 the product's cell-slotted build, 1 round 5's direct
+    build (count, blocks, scatter). Same integers; for A/B measurements and tests. Set it before the
+    compaction."""
+    check(_lib.tuning().dauc_set_index_form(int(form)), "dauc_set_index_form")
 
 
 def set_search_mode(mode: int) -> None:
@@ -785,7 +786,7 @@ __all__ = [
     "pd_update_dense", "coda_finalize", "scale_div", "split_scores", "pair_count", "auc_counts_sorted",
     "surrogate_logits_fwdbwd", "class_sums_logits", "surrogate_status",
     "sort_keys", "auc_counts_sorted_labeled", "compact_positives", "mode_code", "workspaces", "set_search_mode",
-    "set_direct_fault", "set_two_step_form", "conv3x3_wgrad", "conv3x3_wgrad_supported", "stem_conv_forward", "stem_conv_wgrad",
+    "set_direct_fault", "set_index_form", "conv3x3_wgrad", "conv3x3_wgrad_supported", "stem_conv_forward", "stem_conv_wgrad",
     "stem_conv_supported", "strided_pick", "strided_add_", "broadcast_hw",
     "auc_eval_enqueue",
     "auc_slot_bytes",

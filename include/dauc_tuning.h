@@ -72,13 +72,14 @@ int dauc_set_search_mode(int mode);
 int dauc_set_direct_fault(int mode);
 
 /*
- * Step 2 of the two-step sharded evaluation (dauc_auc_eval_compact_part / _query_part; process-wide,
- * default 0): 0 the product's cell-slotted build (one count pass inserting every key into its cell's
- * 8-key slot, then the query pass, which turns the byte counts into block words itself), 1 round
- * 5's direct build (count, block and scatter passes into the cell-ordered table, then the query).
- * Same integers; set it before step 1 (the compaction prepares the chosen form's state).
+ * The count index's build in the exact-AUC evaluations (dauc_auc_eval_counts / _enqueue / _counts_part
+ * and the two-step dauc_auc_eval_compact_part / _query_part; process-wide, default 0): 0 the
+ * product's cell-slotted build (one count pass inserting every key into its cell's slots, then the
+ * query pass, which turns the byte counts into block words itself), 1 round 5's direct build (count,
+ * block and scatter passes into the cell-ordered table, then the query; dauc_set_direct_fault acts on
+ * it). Same integers; set it before the compaction (which prepares the chosen form's state).
  */
-int dauc_set_two_step_form(int form);
+int dauc_set_index_form(int form);
 
 /* The transposing LDS read of the 3x3 weight gradient (csrc/conv_wgrad.hip), for its lane-map test:
  * out[64 lanes][8] <- the 16x16x32 operand fragment (k-step 0, channel block 16) of a [32][64]

@@ -56,6 +56,7 @@ def main():
     aff = len(os.sched_getaffinity(0))
     rec = {"nproc": os.cpu_count(), "affinity_cpus": aff, "cgroup": cgroup_quota(),
            "omp_num_threads": os.environ.get("OMP_NUM_THREADS"), "runs": []}
+    print(json.dumps({k: v for k, v in rec.items() if k != "runs"}), file=sys.stderr, flush=True)
     for th in [int(v) for v in (sys.argv[1] if len(sys.argv) > 1 else "16,64,256").split(",")]:
         th = min(th, aff)
         ts = step_time(th, 32)

@@ -32,7 +32,7 @@ def dev_ms(fn):
 
 
 with _lib.using(_lib.tuning()):
-    ops.set_two_step_form(0)
+    ops.set_index_form(0)
     G = 8
     for log2n, pr in ((24, 0.01), (27, 0.001)):
         s, y = synthetic_scores(1 << log2n, pr, dev)

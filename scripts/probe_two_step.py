@@ -7,7 +7,7 @@ no host read in between: the GPU time a rank spends; the collectives are not on 
 consumes the build state its step 1 prepares in the workspace, so every timed step 2 follows its
 step 1 (the step-2 figure is the pair minus step 1 alone). Parts 0 and G-1 at configs[3] (2^24 @
 1 %) and configs[4] (2^27 @ 0.1 %), G = 2, 4, 8; the parts' counts are checked against the one-call
-evaluation. --ab: the tuning build, step 2's two forms interleaved (dauc_set_two_step_form: 0 the
+evaluation. --ab: the tuning build, step 2's two forms interleaved (dauc_set_index_form: 0 the
 slotted build = the product's, 1 round 5's direct build). One JSON line per (n, G, form). With
 --trace only the G = 8 sequences run (for a rocprofv3 kernel trace of one rank's chain).
 
@@ -56,7 +56,7 @@ with ctx:
         for G in ((8,) if trace else (2, 4, 8)):
             for form in ((1, 0, 1, 0) if ab else (0,) if tun else (None,)):
                 if form is not None:
-                    ops.set_two_step_form(form)
+                    ops.set_index_form(form)
                 nb = ops.auc_slot_bytes(n, G)
                 slots = torch.empty(nb * G, dtype=torch.uint8, device=dev)
                 mine = torch.empty(nb, dtype=torch.uint8, device=dev)
@@ -76,10 +76,11 @@ with ctx:
                     out[f"ms_compact_part{r}"] = dev_ms(lambda: ops.auc_eval_compact_part(s, y, r, G, mine))
                     out[f"ms_query_part{r}"] = out[f"ms_part{r}"] - out[f"ms_compact_part{r}"]
                 out["env"] = {k: v for k, v in os.environ.items() if k.startswith("DAUC_")}
-                if not ab:
+                if G == 8:  # the one-call evaluation (enqueue, part 0 of 1) on the same data, this form
                     out["ms_whole_one_call_events"] = dev_ms(lambda: ops.auc_eval_enqueue(s, y, 0, 1, out=rec))
+                    assert tuple(rec.tolist()[:2]) == whole[:2] and rec.tolist()[7] == 1
                 print(json.dumps(out), flush=True)
         del s, y
         torch.cuda.empty_cache()
     if tun:
-        ops.set_two_step_form(0)
+        ops.set_index_form(0)

@@ -39,6 +39,7 @@ def ops(dev):
         finally:
             o.set_search_mode(0)
             o.set_direct_fault(0)
+            o.set_index_form(0)
 
 
 def _oracle_slice(s, y, begin, end):
@@ -206,6 +207,7 @@ def test_direct_build_guards_bad_indices(dev, ops, fault):
     cell / moved to the next cell) or one cell's counter between the count and scatter passes, and
     the evaluation reports verdict 2 -- the blocking call then takes the sorted path and returns
     the oracle's exact counts. Without the fault the same data is counted by the index (verdict 1)."""
+    ops.set_index_form(1)  # round 5's direct build (the slotted build has no scatter to guard)
     rng = np.random.default_rng(9 + fault)
     n = 1 << 21
     data = [(rng.random(n, dtype=np.float32), _labels(rng, n, p)) for p in (0.01, 0.001)]
@@ -223,3 +225,41 @@ def test_direct_build_guards_bad_indices(dev, ops, fault):
         ops.set_direct_fault(0)
         W, Tt, P, N, bad, other = ops.auc_eval_counts(ts, ty)
         assert (W, Tt, P, N) == (e["wins"], e["ties"], e["P"], e["N"])
+
+
+@pytest.mark.parametrize("case", ["uniform", "ties", "cells_5_14", "cell_15", "p_over_half"])
+def test_index_forms_agree_one_call(dev, ops, case):
+    """The one-call evaluation (dauc_auc_eval_enqueue / _counts) with the count index built by round 5's
+    direct build (form 1: count, blocks, scatter) and by round 6's slotted build (form 0, the
+    product's): the same record, word for word, and the C oracle's counts. Cases: uniform scores;
+    tie-heavy quantised scores; positives repeated 5..14 times in one cell (the secondary window and
+    the tertiary run); a cell of 15 (both forms refuse the index: verdict 2, then the sorted path);
+    more positives than negatives."""
+    rng = np.random.default_rng({"uniform": 1, "ties": 2, "cells_5_14": 3, "cell_15": 4, "p_over_half": 5}[case])
+    n = 1_000_003
+    s = rng.random(n, dtype=np.float32)
+    p = 0.6 if case == "p_over_half" else 0.02
+    y = np.where(rng.random(n) < p, 1, -1).astype(np.int8)
+    if case == "ties":
+        s = (np.floor(s * 20000) / 20000).astype(np.float32)
+    if case in ("cells_5_14", "cell_15"):
+        s = (s * np.float32(0.25)).astype(np.float32)
+        pos, neg = np.flatnonzero(y == 1), np.flatnonzero(y == -1)
+        at = 0
+        for j, m in enumerate((5, 8, 9, 14) if case == "cells_5_14" else (15,)):
+            v = np.float32(0.3 + 0.1 * j)
+            s[pos[at:at + m]] = v
+            at += m
+            s[neg[50 * j:50 * j + 9]] = v
+            s[neg[50 * j + 9:50 * j + 12]] = np.nextafter(v, np.float32(1))
+    e = coracle.auc_counts(y.astype(np.int64), s)
+    ts, ty = T(s, dev), T(y, dev)
+    recs = {}
+    for form in (1, 0):
+        ops.set_index_form(form)
+        recs[form] = ops.auc_eval_enqueue(ts, ty, 0, 1).cpu().tolist()
+        W, Tt, P, N, bad, other = ops.auc_eval_counts(ts, ty)
+        assert (W, Tt, P, N, bad) == (e["wins"], e["ties"], e["P"], e["N"], 0), (case, form)
+    assert recs[0] == recs[1], (case, recs)
+    want = 2 if case in ("cell_15", "p_over_half") else 1
+    assert recs[0][7] == want, (case, recs[0])
