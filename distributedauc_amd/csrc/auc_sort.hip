@@ -1262,6 +1262,7 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
         // in order]. D stream buffers keep D groups of score/label loads in flight per lane: with
         // one (D = 1) a wave holds 20 B per lane in flight, 5 MB over the chip, which at HBM's
         // loaded latency caps the stream far below the bandwidth.
+        // (round 6: D = 2 for the slotted form needs 128 VGPRs + 144-200 B of scratch per lane)
         constexpr int D = 1;
         constexpr int L = D % 2 == 0 ? D : 2 * D;  // unroll: every buffer index compile-time
         Stream sbuf[D];

@@ -319,8 +319,10 @@ int dauc_auc_eval_counts_part(const float* scores, const void* labels, int label
  * of 256.
  *   1. dauc_auc_eval_compact_part: the positives of THIS rank's slice compacted, unordered, into
  *      `slot` (device, dauc_auc_slot_bytes(n, parts) bytes -- the same for every n --, 256-byte
- *      aligned, outside the workspace; the per-cell counters of step 2 in `workspace` are zeroed,
- *      so step 2 must use the same workspace): a header of int64 words {P_r, 0, #non-finite
+ *      aligned, outside the workspace; step 2's index-build state in `workspace` is prepared --
+ *      per-cell counters zeroed, the cell-slotted table filled with +inf --, so step 2 must use the
+ *      same workspace, and each step 2 needs its own step 1: a second step 2 on the same state
+ *      reports verdict 2 instead of counting twice): a header of int64 words {P_r, 0, #non-finite
  *      positives, #labels not in {-1, 1}, n} at byte 0, the top-bucket histogram of the positives'
  *      order-preserving keys (2048 uint32: key >> 21) from byte 256 and the scores from byte 8448;
  *   -- the caller all-gathers the `parts` slots, rank order, contiguous --
