@@ -915,7 +915,12 @@ __device__ __forceinline__ void slot_tertiary(unsigned x, unsigned c, unsigned c
 // and converted (every cell empty: the loop's windows all read the +inf pad window)
 __device__ int g_query_abl = 0;
 #endif
-template <typename LT, bool CHECK = false, bool SLOT = false>
+// SEC (SLOT only; round 6): a lane carries ONE pending secondary window from one group's count to the
+// next instead of loading a second window for each of its 4 queries: cells of 5+ keys are ~0.6 % of
+// the queries, so per group a lane loads one secondary window (the +inf pad when nothing is pending)
+// and counts it one group later; a second pending query in the same group (~2e-4 of lane-groups) is
+// counted at once. 26 fewer live VGPRs and ~69 fewer VALU per group of 4 queries.
+template <typename LT, bool CHECK = false, bool SLOT = false, bool SEC = true>
 __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __restrict__ s,
                                                                 const LT* __restrict__ lab, int64_t begin,
                                                                 int64_t end, unsigned* __restrict__ meta,
@@ -1123,10 +1128,11 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
         };
         // one group in flight: its keys, rank_lo | count << 28 (rank_lo < 2^28: M <= 2^27 here),
         // window and query mask
+        constexpr bool CARRY = SLOT && SEC;  // one carried secondary window per lane (see SEC)
         struct Group {
             unsigned x[NQ], rc[NQ];
             uint4 k[NQ];
-            uint4 k2[NQ];  // the next window, for cells that run past the first
+            uint4 k2[CARRY ? 1 : NQ];  // the next window, for cells that run past the first (unused: CARRY)
             unsigned use;
         };
         auto keys = [&](Group& g, const Stream& sg) {
@@ -1178,10 +1184,12 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
                     const unsigned cnt = g.rc[q] >> 28;
                     g.k[q] = win_load(sorted + (cnt && ((g.use >> q) & 1u) ? 4u * c[q] : padoff));
                 }
+                if constexpr (!CARRY) {
 #pragma unroll
-                for (int q = 0; q < NQ; ++q) {
-                    const unsigned cnt = g.rc[q] >> 28;
-                    g.k2[q] = win_load(sorted + (((g.use >> q) & 1u) && cnt > 4u ? slot_sec(slot_cells, c[q]) : padoff));
+                    for (int q = 0; q < NQ; ++q) {
+                        const unsigned cnt = g.rc[q] >> 28;
+                        g.k2[q] = win_load(sorted + (((g.use >> q) & 1u) && cnt > 4u ? slot_sec(slot_cells, c[q]) : padoff));
+                    }
                 }
                 return;
             }
@@ -1206,9 +1214,48 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
             locate_lds(g, c);
             locate_win(g, c);
         };
+        // CARRY: the pending secondary window (issued by the previous count, or the pad window) and its
+        // query's key; hs = 1 when one is pending
+        uint4 ks = uint4{kPadKey, kPadKey, kPadKey, kPadKey};
+        unsigned xs = 0u, hs = 0u;
+        auto count_carry = [&](const Group& g) {
+            // the previous group's pending query: its secondary window's keys <= x were not in its ub
+            unsigned les, lts;
+            win_le_lt(ks, xs, les, lts);
+            const unsigned hm = 0u - hs;
+            w -= static_cast<unsigned long long>(les & hm);
+            t += (les - lts) & hm;
+            // this group's: the first query with 5+ keys in its cell is carried, any further one
+            // (rare) counted now from its secondary window
+            unsigned pend = 0u;
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) pend |= unsigned(((g.use >> q) & 1u) && (g.rc[q] >> 28) > 4u) << q;
+            unsigned xn = 0u;
+#pragma unroll
+            for (int q = NQ - 1; q >= 0; --q) xn = (pend >> q) & 1u ? g.x[q] : xn;  // the lowest pending q
+            const unsigned rest = pend & (pend - 1u);
+            if (__ballot(rest != 0u) != 0ull) {
+#pragma unroll
+                for (int q = 0; q < NQ; ++q) {
+                    if ((rest >> q) & 1u) {
+                        const unsigned x = g.x[q];
+                        const uint4 k2 = win_load(sorted + slot_sec(slot_cells, ci_cell(x, l1[x >> kCiLowBits])));
+                        unsigned le2, lt2;
+                        win_le_lt(k2, x, le2, lt2);
+                        w -= le2;
+                        t += le2 - lt2;
+                    }
+                }
+            }
+            xs = xn;
+            hs = pend != 0u;
+            const unsigned cs = ci_cell(xs, l1[xs >> kCiLowBits]);
+            ks = win_load(sorted + (hs ? slot_sec(slot_cells, cs) : padoff));
+        };
         auto count = [&](const Group& g) {
             unsigned wl = 0u, tl = 0u;
             bool more8 = false;
+            if constexpr (CARRY) count_carry(g);
 #pragma unroll
             for (int q = 0; q < NQ; ++q) {
                 // lb = base + #(window keys < x), ub = base + #(<= x): the first window's keys before
@@ -1220,9 +1267,9 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
                 // rl & ~3 when the cell has keys (its window starts at the aligned rank); SLOT: the
                 // window holds exactly the cell's keys, then +inf
                 const unsigned base = SLOT ? rl : rl & ~(min(cnt, 1u) * 3u);
-                unsigned le, lt, le2, lt2;
+                unsigned le, lt, le2 = 0u, lt2 = 0u;
                 win_le_lt(g.k[q], x, le, lt);
-                win_le_lt(g.k2[q], x, le2, lt2);
+                if constexpr (!CARRY) win_le_lt(g.k2[q], x, le2, lt2);
                 wl += (M32 - (base + le + le2)) & um;
                 tl += ((le - lt) + (le2 - lt2)) & um;
                 more8 |= um && (SLOT ? cnt : (rl & 3u) + cnt) > 8u;
@@ -1247,7 +1294,7 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
                     if (((g.use >> q) & 1u) && (rl & 3u) + cnt > 8u) {
                         // undo the two windows' counts, then count the cell key by key (ci_fix)
                         const unsigned x = g.x[q];
-                        const uint4 k2 = g.k2[q];
+                        const uint4 k2 = g.k2[0 * CARRY + q * !CARRY];
                         w += (k2.x <= x) + (k2.y <= x) + (k2.z <= x) + (k2.w <= x);
                         t -= ((k2.x <= x) + (k2.y <= x) + (k2.z <= x) + (k2.w <= x)) -
                              ((k2.x < x) + (k2.y < x) + (k2.z < x) + (k2.w < x));
@@ -1262,7 +1309,9 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
         // in order]. D stream buffers keep D groups of score/label loads in flight per lane: with
         // one (D = 1) a wave holds 20 B per lane in flight, 5 MB over the chip, which at HBM's
         // loaded latency caps the stream far below the bandwidth.
-        // (round 6: D = 2 for the slotted form needs 128 VGPRs + 144-200 B of scratch per lane)
+        // (round 6: D = 2 for the slotted form with a secondary window per query needs 128 VGPRs +
+        // 144-200 B of scratch per lane; the carried form (SEC) fits it in 119-123 VGPRs for 1- and
+        // 4-byte labels, but runs 0.3-0.5 % slower at 2^27 and the same at 2^24: dropped)
         constexpr int D = 1;
         constexpr int L = D % 2 == 0 ? D : 2 * D;  // unroll: every buffer index compile-time
         Stream sbuf[D];
@@ -1292,6 +1341,13 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
             }
         }
     ci_stream_done:;
+        if constexpr (CARRY) {  // the last group's pending secondary window
+            unsigned les, lts;
+            win_le_lt(ks, xs, les, lts);
+            const unsigned hm = 0u - hs;
+            w -= static_cast<unsigned long long>(les & hm);
+            t += (les - lts) & hm;
+        }
     } else {
         for (int64_t v = tid; v < nvec; v += stride)
             for (int q = 0; q < 4; ++q) one(head + v * 4 + q);
@@ -2100,6 +2156,7 @@ int launch_ci(const float* s, const LT* lab, int64_t begin, int64_t end, const C
               unsigned* check = nullptr, const uint2* slot_counts = nullptr, unsigned slot_cells = 0u) {
     const dim3 grid(query_grid(end - begin)), block(kQueryThreads);
     const size_t lds = (size_t(kCiTop) + kCiMaxBlocks) * 8 + (grp ? size_t(kDirectMaxGroups) * 4 : 0);
+    bool sec = true;  // the carried secondary window (query_ci_kernel's SEC)
 #ifdef DAUC_TUNING
     {
         static int abl = -1;
@@ -2108,6 +2165,8 @@ int launch_ci(const float* s, const LT* lab, int64_t begin, int64_t end, const C
             abl = e ? atoi(e) : 0;
             if (hipMemcpyToSymbol(HIP_SYMBOL(g_query_abl), &abl, sizeof(int)) != hipSuccess) return DAUC_EINVAL;
         }
+        const char* e = getenv("DAUC_QUERY_SEC");  // 0: a secondary window per query (the round-6 form)
+        sec = !(e && atoi(e) == 0);
     }
 #endif
     // dynamic + the kernel's static reduction rows must fit the CU's 160 KB of LDS (a launch past it
@@ -2115,12 +2174,21 @@ int launch_ci(const float* s, const LT* lab, int64_t begin, int64_t end, const C
     static_assert((size_t(kCiTop) + kCiMaxBlocks) * 8 + size_t(kDirectMaxGroups) * 4 +
                           4 * (kQueryThreads / kWave) * 8 <= 160 * 1024,
                   "the count-index query's LDS");
-    if (slot_counts != nullptr && check != nullptr)
-        hipLaunchKernelGGL((query_ci_kernel<LT, true, true>), grid, block, lds, st, s, lab, begin, end, cw.meta, cw.l1,
-                           slot_counts, sorted, M, out, nonfinite, verdict, nullptr, Mp, check, slot_cells);
-    else if (slot_counts != nullptr)
-        hipLaunchKernelGGL((query_ci_kernel<LT, false, true>), grid, block, lds, st, s, lab, begin, end, cw.meta,
+    if (slot_counts != nullptr && check != nullptr && sec)
+        hipLaunchKernelGGL((query_ci_kernel<LT, true, true, true>), grid, block, lds, st, s, lab, begin, end, cw.meta,
+                           cw.l1, slot_counts, sorted, M, out, nonfinite, verdict, nullptr, Mp, check, slot_cells);
+    else if (slot_counts != nullptr && sec)
+        hipLaunchKernelGGL((query_ci_kernel<LT, false, true, true>), grid, block, lds, st, s, lab, begin, end, cw.meta,
                            cw.l1, slot_counts, sorted, M, out, nonfinite, verdict, nullptr, Mp, nullptr, slot_cells);
+#ifdef DAUC_TUNING
+    else if (slot_counts != nullptr && check != nullptr)
+        hipLaunchKernelGGL((query_ci_kernel<LT, true, true, false>), grid, block, lds, st, s, lab, begin, end, cw.meta,
+                           cw.l1, slot_counts, sorted, M, out, nonfinite, verdict, nullptr, Mp, check, slot_cells);
+    else if (slot_counts != nullptr)
+        hipLaunchKernelGGL((query_ci_kernel<LT, false, true, false>), grid, block, lds, st, s, lab, begin, end,
+                           cw.meta, cw.l1, slot_counts, sorted, M, out, nonfinite, verdict, nullptr, Mp, nullptr,
+                           slot_cells);
+#endif
     else if (check != nullptr)
         hipLaunchKernelGGL((query_ci_kernel<LT, true>), grid, block, lds, st, s, lab, begin, end, cw.meta, cw.l1,
                            cw.blk, sorted, M, out, nonfinite, verdict, grp, Mp, check, 0u);
