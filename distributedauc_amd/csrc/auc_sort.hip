@@ -915,11 +915,11 @@ __device__ __forceinline__ void slot_tertiary(unsigned x, unsigned c, unsigned c
 // and converted (every cell empty: the loop's windows all read the +inf pad window)
 __device__ int g_query_abl = 0;
 #endif
-// SEC (SLOT only; round 6): a lane carries ONE pending secondary window from one group's count to the
-// next instead of loading a second window for each of its 4 queries: cells of 5+ keys are ~0.6 % of
-// the queries, so per group a lane loads one secondary window (the +inf pad when nothing is pending)
-// and counts it one group later; a second pending query in the same group (~2e-4 of lane-groups) is
-// counted at once. 26 fewer live VGPRs and ~69 fewer VALU per group of 4 queries.
+// SEC (SLOT only; round 6): ONE secondary window per lane per group of 4 queries instead of one per
+// query: cells of 5+ keys are ~0.6 % of the queries, so a lane loads the secondary window of its
+// group's first such query (the +inf pad when there is none) with the group's primaries, and counts
+// it with them; a second such query in the same group (~2e-4 of lane-groups) is counted at once.
+// 12 fewer live VGPRs per group and ~69 fewer VALU per group.
 template <typename LT, bool CHECK = false, bool SLOT = false, bool SEC = true>
 __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __restrict__ s,
                                                                 const LT* __restrict__ lab, int64_t begin,
@@ -1128,12 +1128,13 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
         };
         // one group in flight: its keys, rank_lo | count << 28 (rank_lo < 2^28: M <= 2^27 here),
         // window and query mask
-        constexpr bool CARRY = SLOT && SEC;  // one carried secondary window per lane (see SEC)
+        constexpr bool ONE2 = SLOT && SEC;  // one secondary window per lane per group (see SEC)
         struct Group {
             unsigned x[NQ], rc[NQ];
             uint4 k[NQ];
-            uint4 k2[CARRY ? 1 : NQ];  // the next window, for cells that run past the first (unused: CARRY)
-            unsigned use;
+            uint4 k2[ONE2 ? 1 : NQ];  // the next window, for cells that run past the first
+            unsigned xs;              // ONE2: the key of the query k2[0] belongs to
+            unsigned use;             // bit q: query q counts; ONE2: bit 8 + q: q's cell has 5+ keys
         };
         auto keys = [&](Group& g, const Stream& sg) {
             g.use = 0u;
@@ -1184,7 +1185,20 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
                     const unsigned cnt = g.rc[q] >> 28;
                     g.k[q] = win_load(sorted + (cnt && ((g.use >> q) & 1u) ? 4u * c[q] : padoff));
                 }
-                if constexpr (!CARRY) {
+                if constexpr (ONE2) {
+                    unsigned pend = 0u;
+#pragma unroll
+                    for (int q = 0; q < NQ; ++q) pend |= unsigned(((g.use >> q) & 1u) && (g.rc[q] >> 28) > 4u) << q;
+                    unsigned xs = 0u, cs = 0u;
+#pragma unroll
+                    for (int q = NQ - 1; q >= 0; --q) {  // the lowest such query
+                        xs = (pend >> q) & 1u ? g.x[q] : xs;
+                        cs = (pend >> q) & 1u ? c[q] : cs;
+                    }
+                    g.xs = xs;
+                    g.use |= pend << 8;
+                    g.k2[0] = win_load(sorted + (pend ? slot_sec(slot_cells, cs) : padoff));
+                } else {
 #pragma unroll
                     for (int q = 0; q < NQ; ++q) {
                         const unsigned cnt = g.rc[q] >> 28;
@@ -1214,25 +1228,16 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
             locate_lds(g, c);
             locate_win(g, c);
         };
-        // CARRY: the pending secondary window (issued by the previous count, or the pad window) and its
-        // query's key; hs = 1 when one is pending
-        uint4 ks = uint4{kPadKey, kPadKey, kPadKey, kPadKey};
-        unsigned xs = 0u, hs = 0u;
-        auto count_carry = [&](const Group& g) {
-            // the previous group's pending query: its secondary window's keys <= x were not in its ub
+        // ONE2: the group's secondary window, for its first query whose cell has 5+ keys (whose
+        // primary window's count lacks the keys past the 4th); any further such query of the group
+        // (rare) gets its secondary window now
+        auto count_sec = [&](const Group& g) {
+            const unsigned pend = (g.use >> 8) & 0xfu;
             unsigned les, lts;
-            win_le_lt(ks, xs, les, lts);
-            const unsigned hm = 0u - hs;
+            win_le_lt(g.k2[0], g.xs, les, lts);
+            const unsigned hm = 0u - min(pend, 1u);
             w -= static_cast<unsigned long long>(les & hm);
             t += (les - lts) & hm;
-            // this group's: the first query with 5+ keys in its cell is carried, any further one
-            // (rare) counted now from its secondary window
-            unsigned pend = 0u;
-#pragma unroll
-            for (int q = 0; q < NQ; ++q) pend |= unsigned(((g.use >> q) & 1u) && (g.rc[q] >> 28) > 4u) << q;
-            unsigned xn = 0u;
-#pragma unroll
-            for (int q = NQ - 1; q >= 0; --q) xn = (pend >> q) & 1u ? g.x[q] : xn;  // the lowest pending q
             const unsigned rest = pend & (pend - 1u);
             if (__ballot(rest != 0u) != 0ull) {
 #pragma unroll
@@ -1247,15 +1252,11 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
                     }
                 }
             }
-            xs = xn;
-            hs = pend != 0u;
-            const unsigned cs = ci_cell(xs, l1[xs >> kCiLowBits]);
-            ks = win_load(sorted + (hs ? slot_sec(slot_cells, cs) : padoff));
         };
         auto count = [&](const Group& g) {
             unsigned wl = 0u, tl = 0u;
             bool more8 = false;
-            if constexpr (CARRY) count_carry(g);
+            if constexpr (ONE2) count_sec(g);
 #pragma unroll
             for (int q = 0; q < NQ; ++q) {
                 // lb = base + #(window keys < x), ub = base + #(<= x): the first window's keys before
@@ -1269,7 +1270,7 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
                 const unsigned base = SLOT ? rl : rl & ~(min(cnt, 1u) * 3u);
                 unsigned le, lt, le2 = 0u, lt2 = 0u;
                 win_le_lt(g.k[q], x, le, lt);
-                if constexpr (!CARRY) win_le_lt(g.k2[q], x, le2, lt2);
+                if constexpr (!ONE2) win_le_lt(g.k2[q], x, le2, lt2);
                 wl += (M32 - (base + le + le2)) & um;
                 tl += ((le - lt) + (le2 - lt2)) & um;
                 more8 |= um && (SLOT ? cnt : (rl & 3u) + cnt) > 8u;
@@ -1294,7 +1295,7 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
                     if (((g.use >> q) & 1u) && (rl & 3u) + cnt > 8u) {
                         // undo the two windows' counts, then count the cell key by key (ci_fix)
                         const unsigned x = g.x[q];
-                        const uint4 k2 = g.k2[0 * CARRY + q * !CARRY];
+                        const uint4 k2 = g.k2[ONE2 ? 0 : q];
                         w += (k2.x <= x) + (k2.y <= x) + (k2.z <= x) + (k2.w <= x);
                         t -= ((k2.x <= x) + (k2.y <= x) + (k2.z <= x) + (k2.w <= x)) -
                              ((k2.x < x) + (k2.y < x) + (k2.z < x) + (k2.w < x));
@@ -1310,30 +1311,38 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
         // one (D = 1) a wave holds 20 B per lane in flight, 5 MB over the chip, which at HBM's
         // loaded latency caps the stream far below the bandwidth.
         // (round 6: D = 2 for the slotted form with a secondary window per query needs 128 VGPRs +
-        // 144-200 B of scratch per lane; the carried form (SEC) fits it in 119-123 VGPRs for 1- and
-        // 4-byte labels, but runs 0.3-0.5 % slower at 2^27 and the same at 2^24: dropped)
+        // 144-200 B of scratch per lane; with SEC's one secondary window per group it fits in 119-123
+        // VGPRs for 1- and 4-byte labels, but ran 0.3-0.5 % slower at 2^27 and the same at 2^24)
         constexpr int D = 1;
-        constexpr int L = D % 2 == 0 ? D : 2 * D;  // unroll: every buffer index compile-time
+        // groups in flight (windows issued GD - 1 groups before their count; round 6 measured 3 with
+        // SEC: 127-128 VGPRs, the same time as 2 -- more loads in flight do not help)
+        constexpr int GD = 2;
+        static_assert(GD == 2 || (GD == 3 && D == 1), "the pipeline's unroll");
+        constexpr int L = GD == 3 ? 3 : D % 2 == 0 ? D : 2 * D;  // unroll: every buffer index compile-time
         Stream sbuf[D];
-        Group gbuf[2];
+        Group gbuf[GD];
 #pragma unroll
         for (int j = 0; j < D; ++j) load(sbuf[j], tid + int64_t(j) * step);
-        keys(gbuf[0], sbuf[0]);
-        load(sbuf[0], tid + int64_t(D) * step);
-        locate(gbuf[0]);
-        int64_t v = tid + step;
+#pragma unroll
+        for (int p = 0; p < GD - 1; ++p) {  // groups 0 .. GD - 2 located (a group past the end counts nothing)
+            keys(gbuf[p], sbuf[p % D]);
+            load(sbuf[p % D], tid + int64_t(p + D) * step);
+            locate(gbuf[p]);
+        }
+        int64_t v = tid + int64_t(GD - 1) * step;
         for (;;) {
 #pragma unroll
             for (int j = 0; j < L; ++j) {
-                // group v sits in stream buffer (j + 1) % D and group slot (j + 1) % 2
-                Group& gc = gbuf[(j + 1) % 2];
-                Group& gp = gbuf[j % 2];
+                // group v sits in stream buffer (j + GD - 1) % D and group slot (j + GD - 1) % GD
+                Group& gc = gbuf[(j + GD - 1) % GD];
+                Group& gp = gbuf[j % GD];
                 if (v >= nvec) {
-                    count(gp);
+#pragma unroll
+                    for (int p = 0; p < GD - 1; ++p) count(gbuf[(j + p) % GD]);
                     goto ci_stream_done;
                 }
-                keys(gc, sbuf[(j + 1) % D]);
-                load(sbuf[(j + 1) % D], v + int64_t(D) * step);
+                keys(gc, sbuf[(j + GD - 1) % D]);
+                load(sbuf[(j + GD - 1) % D], v + int64_t(D) * step);
                 asm volatile("" ::: "memory");  // the stream loads stay older than this group's windows
                 locate(gc);
                 count(gp);
@@ -1341,13 +1350,6 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
             }
         }
     ci_stream_done:;
-        if constexpr (CARRY) {  // the last group's pending secondary window
-            unsigned les, lts;
-            win_le_lt(ks, xs, les, lts);
-            const unsigned hm = 0u - hs;
-            w -= static_cast<unsigned long long>(les & hm);
-            t += (les - lts) & hm;
-        }
     } else {
         for (int64_t v = tid; v < nvec; v += stride)
             for (int q = 0; q < 4; ++q) one(head + v * 4 + q);

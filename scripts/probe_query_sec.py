@@ -1,7 +1,8 @@
 """A/B of the slotted query's secondary-window forms (tuning build, DAUC_QUERY_SEC read per launch):
-1 = one carried secondary window per lane per group (the product's), 0 = one per query (round 6's
-first form); DAUC_QUERY_D=2: the carried form with two stream buffers. Interleaved (1, D1), (0, D1),
-(1, D2), three times, on the same data: the one-call evaluation (enqueue, HIP
+1 = one secondary window per lane per group (the product's), 0 = one per query (round 6's first
+form); DAUC_QUERY_GD=3: form 1 with three groups in flight (windows issued two groups before their
+count; measured, then dropped: the knob no longer selects anything). Interleaved (1, GD 2), (0, GD 2),
+(1, GD 3), three times, on the same data: the one-call evaluation (enqueue, HIP
 events around `reps` back-to-back calls) and rank 0's step 1 + step 2 at G = 8, at configs[3]
 (2^24 @ 1 %) and configs[4] (2^27 @ 0.1 %); every form's counts are checked against round 5's
 direct build (index form 1). One JSON line per (n, form, rep).
@@ -52,10 +53,8 @@ with _lib.using(_lib.tuning()):
         for r in range(G):
             ops.auc_eval_compact_part(s, y, r, G, slots[r * nb:(r + 1) * nb])
         for rep in range(3):
-            for sec, d in (("1", "1"), ("0", "1"), ("1", "2")):
-                # (DAUC_QUERY_D=2 selected a two-stream-buffer build of the carried form while it was
-                # measured; dropped since, the knob now changes nothing)
-                os.environ["DAUC_QUERY_SEC"], os.environ["DAUC_QUERY_D"] = sec, d
+            for sec, gd in (("1", "2"), ("0", "2"), ("1", "3")):
+                os.environ["DAUC_QUERY_SEC"], os.environ["DAUC_QUERY_GD"] = sec, gd
                 whole = ops.auc_eval_counts(s, y)
                 W = T = 0
                 for r in range(G):
@@ -63,7 +62,7 @@ with _lib.using(_lib.tuning()):
                     v = ops.auc_eval_query_part(s, y, r, G, slots, out=rec).tolist()
                     assert v[4] == 0 and v[7] == 1, v
                     W, T = W + v[0], T + v[1]
-                out = {"log2n": log2n, "sec": int(sec), "D": int(d), "rep": rep, "whole_matches": whole[:2] == ref[:2],
+                out = {"log2n": log2n, "sec": int(sec), "GD": int(gd), "rep": rep, "whole_matches": whole[:2] == ref[:2],
                        "parts_match": (W, T) == ref[:2]}
                 out["ms_one_call"] = dev_ms(lambda: ops.auc_eval_enqueue(s, y, 0, 1, out=rec))
                 pair = dev_ms(lambda: (ops.auc_eval_compact_part(s, y, 0, G, mine),
@@ -72,6 +71,6 @@ with _lib.using(_lib.tuning()):
                 out.update(ms_part0=pair, ms_compact_part0=comp, ms_query_part0=pair - comp)
                 print(json.dumps(out), flush=True)
         os.environ.pop("DAUC_QUERY_SEC", None)
-        os.environ.pop("DAUC_QUERY_D", None)
+        os.environ.pop("DAUC_QUERY_GD", None)
         del s, y
         torch.cuda.empty_cache()
