@@ -166,8 +166,9 @@ int sorted_path(const float* scores, const void* labels, int label_dtype, int64_
         // the positives are the table; every other score of the part is a query read in place
         const int64_t qlo = n * part / parts, qhi = n * (part + 1) / parts;
         if (qhi <= qlo) return DAUC_OK;
-        return dauc_auc_counts_sorted_labeled(w.pos, P, scores, labels, label_dtype, qlo, qhi, w.wt, w.wt + 2, w.tws,
-                                              w.tws_bytes, ds);
+        // (the count index refused this table: its plan over the sorted copy would too)
+        return counts_sorted_labeled(w.pos, P, scores, labels, label_dtype, qlo, qhi, w.wt, w.wt + 2, w.tws,
+                                     w.tws_bytes, st, false);
     }
     // the negatives are the smaller class: materialise both (the split also checks every score)
     int rc = dauc_split_scores(scores, labels, label_dtype, n, w.pos, w.neg, w.split_stats, w.sws, w.sws_bytes, ds);

@@ -651,8 +651,9 @@ __device__ __forceinline__ void label4(const LT* __restrict__ lab, int64_t i, bo
 // Region of the sort workspace that holds the direct build's 72 group totals (grp)
 constexpr size_t kGrpBytes = 512;
 
-// search structure: 0 automatic (the count index where it holds the table, else the tree); the
-// tuning build can force the tree (dauc_set_search_mode(1)) to test it on any table
+// search structure: 0 automatic (the count index where it holds the table, else the distinct-key
+// index where it holds it, else the tree); the tuning build can force the tree
+// (dauc_set_search_mode(1)) or the distinct-key index (2) to test them on any table
 #ifdef DAUC_TUNING
 int g_search_mode = 0;
 #else
@@ -692,6 +693,28 @@ struct CountWs {
 constexpr size_t kCountBytes = 256 + 3 * size_t(kCiTop) * 4 + ((size_t(kCiMaxCells) + 2) * 4 + 255) / 256 * 256 +
                                size_t(kCiMaxBlocks) * 8 + 256;
 
+// the distinct-key index of tie-heavy tables (dk_*_kernel below)
+constexpr int kDkMax = 8192;
+constexpr int kDkMaxCells = 2 * kDkMax + kCiTop;  // the plan's cells: <= 2 per distinct key + 1 per used bucket
+constexpr int kDkTile = 1024;                     // table keys per tile of the mark / write passes (4 per thread)
+constexpr int kDkUse = 0, kDkD = 1;              // meta words; kCiOk, kCiCells, kCiBlocks: the plan's
+constexpr int kDkScanThreads = 1024;
+static_assert(kDkMax < 65536, "cell words hold 16-bit indices and counts");
+
+struct DkWs {
+    unsigned* meta;    // [16]
+    uint2* l1;         // [kCiTop]
+    unsigned* cstart;  // [kDkMaxCells + 2] the first distinct key of every cell
+    unsigned* kd;      // [kDkMax] the distinct keys, ascending
+    unsigned* cd;      // [kDkMax] #(table keys <= kd[i])
+    unsigned* tcnt;    // [tiles] distinct keys whose last copy is in the tile -> their exclusive prefix
+};
+
+__device__ __forceinline__ bool dk_ci_in_use(const unsigned* __restrict__ ci_meta) {
+    return ci_meta != nullptr && count_index_in_use(ci_meta);
+}
+
+
 
 
 // first[t] = the first table index of top bucket t, for the buckets holding keys (first[] was set
@@ -708,13 +731,11 @@ __global__ __launch_bounds__(256) void ci_first_kernel(const unsigned* __restric
 // 2046 - 2i: descending, so the suffix minima are prefix minima over the threads), the cells per
 // bucket C_t = ceil(n_t * num / M), num = min(cells left after one per used bucket, 2 M) (so
 // sum C_t fits), and the first cell of every bucket (prefix sum).
-__global__ __launch_bounds__(kCiPlanThreads) void ci_plan_kernel(int64_t M, const unsigned* __restrict__ first,
-                                                                 uint2* __restrict__ l1,
-                                                                 unsigned* __restrict__ meta) {
+// (the body is shared with the distinct-key index's plan: dk_index_kernel; `first` and `l1` may be
+// LDS or global, `max_cells` the cells the consumer's LDS holds)
+__device__ __forceinline__ void ci_plan_body(int64_t M, const unsigned* first, uint2* l1, unsigned* __restrict__ meta,
+                                             int64_t max_cells, unsigned* wtot, unsigned* incl_min, unsigned* totals) {
     static_assert(kCiTop == 2 * kCiPlanThreads, "two top buckets per thread");
-    __shared__ unsigned wtot[kCiPlanThreads / kWave];
-    __shared__ unsigned incl_min[kCiPlanThreads];
-    __shared__ unsigned totals[2];
     const unsigned m32 = static_cast<unsigned>(M);
     int tj[2];
     unsigned st[2], run = ~0u;
@@ -742,7 +763,7 @@ __global__ __launch_bounds__(kCiPlanThreads) void ci_plan_kernel(int64_t M, cons
     const unsigned used = block_incl_scan1024<false>((n[0] != 0u) + (n[1] != 0u), wtot);
     if (threadIdx.x == kCiPlanThreads - 1) totals[0] = used;
     __syncthreads();
-    const int64_t avail = int64_t(kCiMaxCells) - int64_t(totals[0]);
+    const int64_t avail = max_cells - int64_t(totals[0]);
     const int64_t num = avail < 2 * M ? avail : 2 * M;
     unsigned C[2];
 #pragma unroll
@@ -759,11 +780,20 @@ __global__ __launch_bounds__(kCiPlanThreads) void ci_plan_kernel(int64_t M, cons
         l1[tj[j]] = uint2{total - upto, C[j]};
     }
     if (threadIdx.x == 0) {
-        meta[kCiOk] = (3 * num >= 2 * M && total <= static_cast<unsigned>(kCiMaxCells)) ? 1u : 0u;  // <= 1.5 keys/cell
+        meta[kCiOk] = (3 * num >= 2 * M && total <= static_cast<unsigned>(max_cells)) ? 1u : 0u;  // <= 1.5 keys/cell
         meta[kCiCells] = total;
         meta[kCiBlocks] = (total + 1 + kCiBlock - 1) / kCiBlock;
         meta[kCiSkew] = 0u;
     }
+}
+
+__global__ __launch_bounds__(kCiPlanThreads) void ci_plan_kernel(int64_t M, const unsigned* __restrict__ first,
+                                                                 uint2* __restrict__ l1,
+                                                                 unsigned* __restrict__ meta) {
+    __shared__ unsigned wtot[kCiPlanThreads / kWave];
+    __shared__ unsigned incl_min[kCiPlanThreads];
+    __shared__ unsigned totals[2];
+    ci_plan_body(M, first, l1, meta, kCiMaxCells, wtot, incl_min, totals);
 }
 
 // One thread per table index i in [0, M] (i = M: past the last cell): cells (c(i-1), c(i)] start at i
@@ -1882,9 +1912,12 @@ __global__ __launch_bounds__(kQueryThreads) void query_labeled_kernel(const floa
                                                                      const unsigned* __restrict__ sorted,
                                                                      int64_t M, unsigned long long* __restrict__ out,
                                                                      unsigned long long* __restrict__ nonfinite,
-                                                                     const unsigned* __restrict__ meta) {
-    // meta: the count index's builder verdict (the tree runs only when the index is not used)
+                                                                     const unsigned* __restrict__ meta,
+                                                                     const unsigned* __restrict__ dk_meta) {
+    // meta: the count index's builder verdict, dk_meta the distinct-key index's (the tree runs only
+    // when neither is used)
     if (meta != nullptr && count_index_in_use(meta)) return;
+    if (dk_meta != nullptr && dk_meta[kDkUse] != 0u) return;
     extern __shared__ TreeNode tree[];
     for (int i = threadIdx.x; i < g.nodes; i += kQueryThreads) tree[i] = gtree[i];
     const TopKeys top = load_top(gtree, g, sorted, k);
@@ -1998,6 +2031,306 @@ __global__ __launch_bounds__(kQueryThreads) void query_labeled_kernel(const floa
         if (bn && nonfinite) atomicAdd(nonfinite, bn);
     }
 }
+
+// ---- distinct-key index: tie-heavy tables (round 6) ---------------------------------------------
+//
+// The count index refuses a table whose cells hold 15+ keys. In practice that is a table of FEW
+// DISTINCT values -- rounded scores, or the probabilities of a bf16 model (2^27 @ 0.1 % rounded to
+// bf16: 134,447 positives on 1,329 values) -- whose equal keys no cell split can separate, and the
+// tree it fell back to ran 1.05 ms at 2^27 (vs 0.47 ms for the index on spread scores). Its distinct
+// keys, each with the number of table keys <= it (cum), answer a query exactly: #(table <= x) = the
+// cum of the last distinct key <= x, #(== x) = that cum minus the previous one when the key IS x.
+// Up to kDkMax distinct keys the whole structure fits the query's LDS: the count index's top-bucket
+// plan over the distinct keys (l1, 16 KB), one word per cell {first distinct key, distinct keys in
+// the cell} (2 cells per distinct key: <= 72 KB), and {key, cum} per distinct key (<= 64 KB). A
+// query is then 3 dependent LDS reads -- l1, its cell word, the two entries at the cell's start --
+// and no table gather at all; a cell of 2+ distinct keys (rare) adds a binary search over them.
+// Built behind prepare_count from the sorted table in 4 small launches (mark, scan, write, index),
+// every one deciding on the device (the count index in use: they return at once; more than kDkMax
+// distinct keys: the tree runs), so the sorted path still needs no host readback. Round 6.
+// the tile's 4 keys per thread and whether each is the LAST copy of its key (the table is +inf
+// padded past M, and no finite key is +inf's)
+__device__ __forceinline__ unsigned dk_flags(const unsigned* __restrict__ sorted, int64_t M, int64_t i0,
+                                             unsigned (&k)[4]) {
+    unsigned f = 0u;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) k[j] = i0 + j < M ? sorted[i0 + j] : kPadKey;
+    const unsigned nxt = i0 + 4 < M ? sorted[i0 + 4] : kPadKey;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const unsigned after = j < 3 ? k[j + 1] : nxt;
+        f |= unsigned(i0 + j < M && k[j] != after) << j;
+    }
+    return f;
+}
+
+__global__ __launch_bounds__(kDkTile / 4) void dk_mark_kernel(const unsigned* __restrict__ sorted, int64_t M,
+                                                              const unsigned* __restrict__ ci_meta,
+                                                              unsigned* __restrict__ tcnt) {
+    if (dk_ci_in_use(ci_meta)) return;
+    __shared__ unsigned wsum[kDkTile / 4 / kWave];
+    unsigned k[4];
+    const unsigned f = dk_flags(sorted, M, int64_t(blockIdx.x) * kDkTile + 4 * int64_t(threadIdx.x), k);
+    unsigned c = static_cast<unsigned>(__popc(f));
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off, kWave);
+    if ((threadIdx.x & (kWave - 1)) == 0) wsum[threadIdx.x / kWave] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) tcnt[blockIdx.x] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+}
+
+// one workgroup: the tiles' exclusive prefix in place, D, and whether the index is used
+__global__ __launch_bounds__(kDkScanThreads) void dk_scan_kernel(const unsigned* __restrict__ ci_meta, DkWs dk,
+                                                                 int64_t ntiles) {
+    if (dk_ci_in_use(ci_meta)) return;
+    __shared__ unsigned wtot[kDkScanThreads / kWave];
+    const int64_t per = (ntiles + kDkScanThreads - 1) / kDkScanThreads;
+    const int64_t t0 = int64_t(threadIdx.x) * per, t1 = t0 + per < ntiles ? t0 + per : ntiles;
+    unsigned long long mine = 0;
+    for (int64_t t = t0; t < t1; ++t) mine += dk.tcnt[t];
+    // a thread's run past kDkMax: saturated (the total is then past it too, and nothing else is read)
+    const unsigned m = mine > unsigned(kDkMax) ? unsigned(kDkMax) + 1u : static_cast<unsigned>(mine);
+    const unsigned incl = block_incl_scan1024<false>(m, wtot);
+    unsigned run = incl - m;
+    for (int64_t t = t0; t < t1; ++t) {
+        const unsigned c = dk.tcnt[t];
+        dk.tcnt[t] = run;
+        run += c;
+    }
+    if (threadIdx.x == kDkScanThreads - 1) {
+        dk.meta[kDkD] = incl;
+        dk.meta[kDkUse] = (incl >= 1u && incl <= static_cast<unsigned>(kDkMax)) ? 1u : 0u;
+    }
+}
+
+// the distinct keys and their cums: the last copy of key kd[d] is table index cd[d] - 1
+__global__ __launch_bounds__(kDkTile / 4) void dk_write_kernel(const unsigned* __restrict__ sorted, int64_t M,
+                                                               const unsigned* __restrict__ ci_meta, DkWs dk) {
+    if (dk_ci_in_use(ci_meta) || dk.meta[kDkUse] == 0u) return;
+    __shared__ unsigned wsum[kDkTile / 4 / kWave];
+    unsigned k[4];
+    const int64_t i0 = int64_t(blockIdx.x) * kDkTile + 4 * int64_t(threadIdx.x);
+    const unsigned f = dk_flags(sorted, M, i0, k);
+    const unsigned c = static_cast<unsigned>(__popc(f));
+    const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+    unsigned incl = c;
+#pragma unroll
+    for (int off = 1; off < kWave; off <<= 1) {
+        const unsigned t = __shfl_up(incl, off, kWave);
+        if (lane >= off) incl += t;
+    }
+    if (lane == kWave - 1) wsum[wid] = incl;
+    __syncthreads();
+    unsigned d = dk.tcnt[blockIdx.x] + incl - c;
+    for (int w = 0; w < wid; ++w) d += wsum[w];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        if ((f >> j) & 1u) {
+            dk.kd[d] = k[j];
+            dk.cd[d] = static_cast<unsigned>(i0 + j + 1);
+            ++d;
+        }
+    }
+}
+
+// one workgroup: the plan over the distinct keys (the count index's, ci_plan_body) and the first
+// distinct key of every cell (cells (c(d-1), c(d)] start at d; d = D: up to the virtual last cell)
+__global__ __launch_bounds__(kCiPlanThreads) void dk_index_kernel(const unsigned* __restrict__ ci_meta, DkWs dk) {
+    if (dk_ci_in_use(ci_meta) || dk.meta[kDkUse] == 0u) return;
+    __shared__ unsigned first[kCiTop];
+    __shared__ uint2 l1[kCiTop];
+    __shared__ unsigned wtot[kCiPlanThreads / kWave];
+    __shared__ unsigned incl_min[kCiPlanThreads];
+    __shared__ unsigned totals[2];
+    const unsigned D = dk.meta[kDkD];
+    for (int t = threadIdx.x; t < kCiTop; t += kCiPlanThreads) first[t] = D;
+    __syncthreads();
+    for (unsigned d = threadIdx.x; d < D; d += kCiPlanThreads) {
+        const unsigned t = dk.kd[d] >> kCiLowBits;
+        if (d == 0 || (dk.kd[d - 1] >> kCiLowBits) != t) first[t] = d;
+    }
+    __syncthreads();
+    ci_plan_body(D, first, l1, dk.meta, kDkMaxCells, wtot, incl_min, totals);
+    __syncthreads();
+    for (int t = threadIdx.x; t < kCiTop; t += kCiPlanThreads) dk.l1[t] = l1[t];
+    const unsigned cells = totals[1];
+    auto cell = [&](unsigned d) -> int64_t {
+        const unsigned key = dk.kd[d];
+        return ci_cell(key, l1[key >> kCiLowBits]);
+    };
+    for (unsigned d = threadIdx.x; d <= D; d += kCiPlanThreads) {
+        const int64_t cd = d < D ? cell(d) : int64_t(cells) + 1;
+        const int64_t cp = d > 0 ? cell(d - 1) : -1;
+        for (int64_t c = cp + 1; c <= cd; ++c) dk.cstart[c] = d;
+    }
+}
+
+// NQ queries of one lane: W += M - #(table <= x), T += #(table == x) for the queries in `use`
+template <int NQ>
+__device__ __forceinline__ void dk_count(const unsigned (&x)[NQ], unsigned use, const uint2* l1, const unsigned* cw,
+                                         const uint2* kc, unsigned long long M, unsigned long long& w,
+                                         unsigned long long& t) {
+    unsigned s0[NQ], n[NQ];
+    uint2 e[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) e[q] = l1[x[q] >> kCiLowBits];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+        const unsigned v = cw[ci_cell(x[q], e[q])];
+        s0[q] = v & 0xffffu;
+        n[q] = v >> 16;
+    }
+    bool many = false;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) many |= n[q] > 1u;
+    if (many) {  // a cell of 2+ distinct keys: s0 <- the last one <= x (n = 1), or none (n = 0)
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            if (n[q] > 1u) {
+                unsigned lo = s0[q], cnt = n[q];
+                while (cnt > 0u) {
+                    const unsigned h = cnt >> 1;
+                    if (kc[lo + h + 1].x <= x[q]) {
+                        lo += h + 1;
+                        cnt -= h + 1;
+                    } else {
+                        cnt = h;
+                    }
+                }
+                n[q] = lo > s0[q] ? 1u : 0u;
+                s0[q] = lo > s0[q] ? lo - 1 : s0[q];
+            }
+        }
+    }
+    // kc[s0] = the distinct key before the cell's (or {0, 0}), kc[s0 + 1] = the cell's first one
+    uint2 a[NQ], b[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+        a[q] = kc[s0[q]];
+        b[q] = kc[s0[q] + 1];
+    }
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+        const bool in = n[q] != 0u && b[q].x <= x[q];
+        const bool eq = in && b[q].x == x[q];
+        const unsigned le = in ? b[q].y : a[q].y;
+        const unsigned lt = eq ? a[q].y : le;
+        if ((use >> q) & 1u) {
+            w += M - le;
+            t += le - lt;
+        }
+    }
+}
+
+// The labeled query pass over the distinct-key index (the stream and checks of query_labeled_kernel);
+// returns at once unless the count index is not in use and the distinct-key index is
+template <typename LT, int U = 2>
+__global__ __launch_bounds__(kQueryThreads) void dk_query_kernel(const float* __restrict__ s, const LT* __restrict__ lab,
+                                                                 int64_t begin, int64_t end,
+                                                                 const unsigned* __restrict__ ci_meta, DkWs dk,
+                                                                 int64_t M, unsigned long long* __restrict__ out,
+                                                                 unsigned long long* __restrict__ nonfinite) {
+    if (dk_ci_in_use(ci_meta) || dk.meta[kDkUse] == 0u) return;
+    extern __shared__ uint2 dk_lds[];
+    uint2* l1 = dk_lds;                                                         // [kCiTop]
+    uint2* kc = dk_lds + kCiTop;                                                // [D + 2]
+    unsigned* cw = reinterpret_cast<unsigned*>(dk_lds + kCiTop + kDkMax + 2);  // [cells + 1]
+    const unsigned D = dk.meta[kDkD], cells = dk.meta[kCiCells];
+    const unsigned long long MM = static_cast<unsigned long long>(M);
+    for (int i = threadIdx.x; i < kCiTop; i += kQueryThreads) l1[i] = dk.l1[i];
+    // {0, 0}, {key, cum} of every distinct key, then {+inf, M} (read, never counted, past the last)
+    for (unsigned i = threadIdx.x; i < D + 2; i += kQueryThreads)
+        kc[i] = i == 0 ? uint2{0u, 0u}
+                       : (i <= D ? uint2{dk.kd[i - 1], dk.cd[i - 1]} : uint2{kPadKey, static_cast<unsigned>(M)});
+    for (unsigned c = threadIdx.x; c <= cells; c += kQueryThreads) {
+        const unsigned a = dk.cstart[c], b = dk.cstart[c + 1];
+        cw[c] = a | ((b - a) << 16);
+    }
+    __syncthreads();
+    unsigned long long w = 0, t = 0;
+    unsigned nf = 0;
+    auto one = [&](int64_t i) {
+        if (lab[i] != LT(1)) {
+            const float f = s[i];
+            nf += !isfinite(f);
+            const unsigned x[1] = {key_fast(f)};
+            dk_count<1>(x, 1u, l1, cw, kc, MM, w, t);
+        }
+    };
+    const int64_t a0 = (begin + 3) & ~int64_t(3);
+    const int64_t head = a0 < end ? a0 : end;
+    const int64_t stride = int64_t(gridDim.x) * kQueryThreads;
+    const int64_t tid = int64_t(blockIdx.x) * kQueryThreads + threadIdx.x;
+    for (int64_t i = begin + tid; i < head; i += stride) one(i);
+    const int64_t nvec = end > head ? (end - head) / 4 : 0;
+    const bool aligned = (reinterpret_cast<uintptr_t>(s + head) & 15u) == 0 &&
+                         (reinterpret_cast<uintptr_t>(lab + head) & (4 * sizeof(LT) - 1)) == 0;
+    if (aligned && nvec > 0) {
+        // U float4 slots per iteration, the next iteration's loaded before this one's lookups
+        constexpr int NQ = 4 * U;
+        f32x4 fc[U], fn[U];
+        LabelWords<LT> lc[U], ln[U];
+        auto load = [&](int64_t v0, f32x4 (&f)[U], LabelWords<LT> (&l)[U]) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int64_t v = v0 + int64_t(u) * stride;
+                const int64_t i = head + (v < nvec ? v : 0) * 4;
+                f[u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(s + i));
+                l[u].load(lab + i);
+                if (v >= nvec) l[u].set_positive();  // past the end: no query
+            }
+        };
+        load(tid, fc, lc);
+        for (int64_t v0 = tid; v0 < nvec; v0 += int64_t(U) * stride) {
+            load(v0 + int64_t(U) * stride, fn, ln);
+            unsigned x[NQ], use = 0u;
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const float f[4] = {fc[u].x, fc[u].y, fc[u].z, fc[u].w};
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const bool neg = lc[u].not_positive(q);
+                    use |= unsigned(neg) << (4 * u + q);
+                    x[4 * u + q] = key_fast(f[q]);
+                    nf += neg && !isfinite(f[q]);
+                }
+            }
+            dk_count<NQ>(x, use, l1, cw, kc, MM, w, t);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                fc[u] = fn[u];
+                lc[u] = ln[u];
+            }
+        }
+    } else if (!aligned) {
+        for (int64_t i = head + tid; i < head + nvec * 4; i += stride) one(i);
+    }
+    for (int64_t i = head + nvec * 4 + tid; i < end; i += stride) one(i);
+    __shared__ unsigned long long red[3][kQueryThreads / kWave];
+    w = wave_sum(w);
+    t = wave_sum(t);
+    const unsigned long long nfw = wave_sum(static_cast<unsigned long long>(nf));
+    const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+    if (lane == 0) {
+        red[0][wid] = w;
+        red[1][wid] = t;
+        red[2][wid] = nfw;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long bw = 0, bt = 0, bn = 0;
+        for (int i = 0; i < kQueryThreads / kWave; ++i) {
+            bw += red[0][i];
+            bt += red[1][i];
+            bn += red[2][i];
+        }
+        if (bw) atomicAdd(out + 0, bw);
+        if (bt) atomicAdd(out + 1, bt);
+        if (bn && nonfinite) atomicAdd(nonfinite, bn);
+    }
+}
+constexpr size_t kDkQueryLds = (size_t(kCiTop) + kDkMax + 2) * 8 + (size_t(kDkMaxCells) + 1) * 4;
+static_assert(kDkQueryLds + 3 * (kQueryThreads / kWave) * 8 <= 160 * 1024, "the distinct-key query's LDS");
 
 int query_grid(int64_t L) {
     static int cus = 0;
@@ -2208,15 +2541,69 @@ CountWs count_ws_of(void* workspace, int64_t P) {
     return carve_count(after_tree_of(workspace, P) + kGrpBytes);
 }
 
+int64_t dk_tiles(int64_t M) { return (M + kDkTile - 1) / kDkTile; }
+
+size_t dk_ws_bytes(int64_t M) {  // (+ 256: the count region's end rounded up to 256 bytes)
+    return 256 + 256 + size_t(kCiTop) * 8 + (size_t(kDkMaxCells) + 2 + 63) / 64 * 256 + 2 * size_t(kDkMax) * 4 +
+           (size_t(dk_tiles(M < 1 ? 1 : M)) * 4 + 255) / 256 * 256;
+}
+
+// the distinct-key index's region: past the count index's
+DkWs dk_ws_of(void* workspace, int64_t P) {
+    char* c = after_tree_of(workspace, P) + kGrpBytes + (kCountBytes + 255) / 256 * 256;
+    DkWs w;
+    w.meta = reinterpret_cast<unsigned*>(c);
+    c += 256;
+    w.l1 = reinterpret_cast<uint2*>(c);
+    c += size_t(kCiTop) * 8;
+    w.cstart = reinterpret_cast<unsigned*>(c);
+    c += (size_t(kDkMaxCells) + 2 + 63) / 64 * 256;
+    w.kd = reinterpret_cast<unsigned*>(c);
+    c += size_t(kDkMax) * 4;
+    w.cd = reinterpret_cast<unsigned*>(c);
+    c += size_t(kDkMax) * 4;
+    w.tcnt = reinterpret_cast<unsigned*>(c);
+    return w;
+}
+
+// the distinct-key index behind prepare_count (ci_meta: the count index's verdict, or nullptr when
+// it was not built): 4 small launches, each returning at once when the index is not needed / not used
+int prepare_dk(const unsigned* sorted, int64_t M, const unsigned* ci_meta, const DkWs& dk, hipStream_t st) {
+    const int64_t nt = dk_tiles(M);
+    hipLaunchKernelGGL(dk_mark_kernel, dim3(static_cast<unsigned>(nt)), dim3(kDkTile / 4), 0, st, sorted, M, ci_meta,
+                       dk.tcnt);
+    hipLaunchKernelGGL(dk_scan_kernel, dim3(1), dim3(kDkScanThreads), 0, st, ci_meta, dk, nt);
+    hipLaunchKernelGGL(dk_write_kernel, dim3(static_cast<unsigned>(nt)), dim3(kDkTile / 4), 0, st, sorted, M, ci_meta,
+                       dk);
+    hipLaunchKernelGGL(dk_index_kernel, dim3(1), dim3(kCiPlanThreads), 0, st, ci_meta, dk);
+    return launch_status();
+}
+
+template <typename LT>
+int launch_dk(const float* s, const LT* lab, int64_t begin, int64_t end, const unsigned* ci_meta, const DkWs& dk,
+              int64_t M, unsigned long long* out, unsigned long long* nonfinite, hipStream_t st) {
+#ifdef DAUC_TUNING
+    const char* e = getenv("DAUC_DK_U");  // tuning builds: 4 float4 slots per iteration instead of 2
+    if (e && atoi(e) == 4) {
+        hipLaunchKernelGGL((dk_query_kernel<LT, 4>), dim3(query_grid(end - begin)), dim3(kQueryThreads), kDkQueryLds,
+                           st, s, lab, begin, end, ci_meta, dk, M, out, nonfinite);
+        return launch_status();
+    }
+#endif
+    hipLaunchKernelGGL((dk_query_kernel<LT>), dim3(query_grid(end - begin)), dim3(kQueryThreads), kDkQueryLds, st, s,
+                       lab, begin, end, ci_meta, dk, M, out, nonfinite);
+    return launch_status();
+}
+
 template <typename LT>
 int launch_labeled(int k, const float* s, const LT* lab, int64_t begin, int64_t end, const TreeNode* tree,
                    const TreeGeom& g, const unsigned* sorted, int64_t M, unsigned long long* out, unsigned long long* nonfinite,
-                   const unsigned* meta, hipStream_t st) {
+                   const unsigned* meta, hipStream_t st, const unsigned* dk_meta = nullptr) {
     const dim3 grid(query_grid(end - begin)), block(kQueryThreads);
     const size_t lds = size_t(g.nodes) * sizeof(TreeNode);
 #define DAUC_QL(KV)                                                                                              \
     hipLaunchKernelGGL((query_labeled_kernel<KV, LT>), grid, block, lds, st, s, lab, begin, end, tree, g, k, \
-                       sorted, M, out, nonfinite, meta)
+                       sorted, M, out, nonfinite, meta, dk_meta)
     switch (k) {
         case 1: DAUC_QL(1); break;
         case 2: DAUC_QL(2); break;
@@ -2479,6 +2866,47 @@ int counts_labeled_direct(const float* pos, const unsigned long long* Mp, int64_
     }
 }
 
+int counts_sorted_labeled(const float* pos, int64_t P, const float* scores, const void* labels, int label_dtype,
+                          int64_t begin, int64_t end, unsigned long long* wins_ties, unsigned long long* nonfinite,
+                          void* workspace, size_t workspace_bytes, hipStream_t st, bool count_index) {
+    if (P < 0 || begin < 0 || end < begin || wins_ties == nullptr || (P > 0 && pos == nullptr) ||
+        (end > begin && (scores == nullptr || labels == nullptr)))
+        return DAUC_EINVAL;
+    if (label_dtype != DAUC_LABEL_I8 && label_dtype != DAUC_LABEL_I32 && label_dtype != DAUC_LABEL_I64)
+        return DAUC_EINVAL;
+    if (P == 0 || end == begin) return DAUC_OK;
+    if (workspace == nullptr || workspace_bytes < dauc_sort_workspace_size(P) || P > 0xffffffffLL) return DAUC_EINVAL;
+    const unsigned* sorted = nullptr;
+    TreeNode* tree = nullptr;
+    int k = 1;
+    TreeGeom g{};
+    // the search structure: mode 0 the count index where the table can use it, else the
+    // distinct-key index where it holds the table, else the tree (every choice made on the device);
+    // 1 the tree; 2 the distinct-key index, else the tree
+    const int mode = g_search_mode;
+    const bool count = count_index && mode == 0 && 2 * P <= 3 * int64_t(kCiMaxCells);
+    const bool distinct = mode == 0 || mode == 2;  // the distinct-key index where the count index is not used
+    const CountWs nw = count_ws_of(workspace, P);
+    const DkWs dk = dk_ws_of(workspace, P);
+    int rc = prepare_table(pos, P, workspace, st, &sorted, &tree, &k, &g, count ? nw.first : nullptr);
+    if (rc) return rc;
+    if (count && (rc = prepare_count(sorted, P, nw, st))) return rc;
+    const unsigned* meta = count ? nw.meta : nullptr;
+    if (distinct && (rc = prepare_dk(sorted, P, meta, dk, st))) return rc;
+    auto run = [&](auto* lab) {
+        int r = launch_labeled(k, scores, lab, begin, end, tree, g, sorted, P, wins_ties, nonfinite, meta, st,
+                               distinct ? dk.meta : nullptr);
+        if (r == DAUC_OK && count) r = launch_ci(scores, lab, begin, end, nw, sorted, P, wins_ties, nonfinite, st);
+        if (r == DAUC_OK && distinct) r = launch_dk(scores, lab, begin, end, meta, dk, P, wins_ties, nonfinite, st);
+        return r;
+    };
+    switch (label_dtype) {
+        case DAUC_LABEL_I8: return run(static_cast<const int8_t*>(labels));
+        case DAUC_LABEL_I32: return run(static_cast<const int32_t*>(labels));
+        default: return run(static_cast<const int64_t*>(labels));
+    }
+}
+
 }  // namespace dauc
 
 using namespace dauc;
@@ -2486,12 +2914,12 @@ using namespace dauc;
 extern "C" {
 
 size_t dauc_sort_workspace_size(int64_t n) {
-    return sort_ws_bytes(n < 1 ? 1 : n) + kTreeBytes + 256 + kGrpBytes + kCountBytes + 256;
+    return sort_ws_bytes(n < 1 ? 1 : n) + kTreeBytes + 256 + kGrpBytes + kCountBytes + 256 + dk_ws_bytes(n);
 }
 
 #ifdef DAUC_TUNING
 int dauc_set_search_mode(int mode) {
-    if (mode < 0 || mode > 1) return DAUC_EINVAL;
+    if (mode < 0 || mode > 2) return DAUC_EINVAL;
     g_search_mode = mode;
     return DAUC_OK;
 }
@@ -2543,37 +2971,8 @@ int dauc_auc_counts_sorted_labeled(const float* pos, int64_t P, const float* sco
                                    int label_dtype, int64_t begin, int64_t end, unsigned long long* wins_ties,
                                    unsigned long long* nonfinite, void* workspace, size_t workspace_bytes,
                                    dauc_stream_t stream) {
-    if (P < 0 || begin < 0 || end < begin || wins_ties == nullptr || (P > 0 && pos == nullptr) ||
-        (end > begin && (scores == nullptr || labels == nullptr)))
-        return DAUC_EINVAL;
-    if (label_dtype != DAUC_LABEL_I8 && label_dtype != DAUC_LABEL_I32 && label_dtype != DAUC_LABEL_I64)
-        return DAUC_EINVAL;
-    if (P == 0 || end == begin) return DAUC_OK;
-    if (workspace == nullptr || workspace_bytes < dauc_sort_workspace_size(P) || P > 0xffffffffLL) return DAUC_EINVAL;
-    hipStream_t st = as_hip(stream);
-    const unsigned* sorted = nullptr;
-    TreeNode* tree = nullptr;
-    int k = 1;
-    TreeGeom g{};
-    // the search structure: mode 0 the count index where the table can use it (the device keeps
-    // the tree for skewed tables), 1 the tree
-    const int mode = g_search_mode;
-    const bool count = mode == 0 && 2 * P <= 3 * int64_t(kCiMaxCells);
-    const CountWs nw = count_ws_of(workspace, P);
-    int rc = prepare_table(pos, P, workspace, st, &sorted, &tree, &k, &g, count ? nw.first : nullptr);
-    if (rc) return rc;
-    if (count && (rc = prepare_count(sorted, P, nw, st))) return rc;
-    const unsigned* meta = count ? nw.meta : nullptr;
-    auto run = [&](auto* lab) {
-        int r = launch_labeled(k, scores, lab, begin, end, tree, g, sorted, P, wins_ties, nonfinite, meta, st);
-        if (r == DAUC_OK && count) r = launch_ci(scores, lab, begin, end, nw, sorted, P, wins_ties, nonfinite, st);
-        return r;
-    };
-    switch (label_dtype) {
-        case DAUC_LABEL_I8: return run(static_cast<const int8_t*>(labels));
-        case DAUC_LABEL_I32: return run(static_cast<const int32_t*>(labels));
-        default: return run(static_cast<const int64_t*>(labels));
-    }
+    return counts_sorted_labeled(pos, P, scores, labels, label_dtype, begin, end, wins_ties, nonfinite, workspace,
+                                 workspace_bytes, as_hip(stream), true);
 }
 
 }  // extern "C"

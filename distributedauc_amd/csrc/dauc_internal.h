@@ -180,5 +180,12 @@ int counts_labeled_slotted(const SlotSource& src, unsigned* stab, int64_t Mcap, 
                            const void* labels, int label_dtype, int64_t begin, int64_t end,
                            unsigned long long* wins_ties, unsigned long long* nonfinite, unsigned* verdict,
                            void* workspace, size_t workspace_bytes, hipStream_t st, unsigned* check);
+// dauc_auc_counts_sorted_labeled with the count index optional: the evaluation's sorted path runs
+// only after the count index refused the table (verdict 2), and the sorted table has the same keys
+// and the same plan, so it skips that build (count_index = false) and goes to the distinct-key
+// index or the tree at once
+int counts_sorted_labeled(const float* pos, int64_t P, const float* scores, const void* labels, int label_dtype,
+                          int64_t begin, int64_t end, unsigned long long* wins_ties, unsigned long long* nonfinite,
+                          void* workspace, size_t workspace_bytes, hipStream_t st, bool count_index);
 
 }  // namespace dauc
