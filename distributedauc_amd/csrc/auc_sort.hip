@@ -2786,8 +2786,15 @@ int counts_labeled_slotted(const SlotSource& src, unsigned* stab, int64_t Mcap, 
     if (label_dtype != DAUC_LABEL_I8 && label_dtype != DAUC_LABEL_I32 && label_dtype != DAUC_LABEL_I64)
         return DAUC_EINVAL;
     const CountWs nw = count_ws_of(workspace, Mcap);
-    const int64_t gk = (Mcap + kSlotCountThreads - 1) / kSlotCountThreads;
+    const int64_t gk0 = (Mcap + kSlotCountThreads - 1) / kSlotCountThreads;
     const unsigned cells = static_cast<unsigned>(slotted_cells(Mcap));
+#ifdef DAUC_TUNING
+    // tuning builds: DAUC_SLOT_COUNT_WGS = this many count workgroups instead (each loops over keys)
+    int64_t gk = gk0;
+    if (const char* e = getenv("DAUC_SLOT_COUNT_WGS"); e && atoi(e) > 0 && atoi(e) <= 4096) gk = atoi(e);
+#else
+    const int64_t gk = gk0;
+#endif
     hipLaunchKernelGGL(direct_count_slots_kernel<true>, dim3(static_cast<unsigned>(gk)), dim3(kSlotCountThreads), 0,
                        st, src, Mcap, nw.l1, nw.meta, nw.cstart, nullptr, nullptr, stab, cells);
     int rc = launch_status();
