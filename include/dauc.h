@@ -256,7 +256,11 @@ int dauc_auc_counts_sorted(const float* pos, int64_t P, const float* neg, int64_
  * whose label is not 1 (the full arrays, as given to dauc_compact_positives). Same
  * accumulation into wins_ties; nonfinite (device uint64 [1], nullable) += the number of
  * queried scores that are NaN or +-inf (the only check the negatives get: sklearn's
- * _ranking.py:868-869 rejects them). workspace >= dauc_sort_workspace_size(P).
+ * _ranking.py:868-869 rejects them). workspace >= dauc_sort_workspace_size(P). The search
+ * structure behind the sort is chosen on the device: the LDS count index (one 16-byte window
+ * gather per query) where it holds the table; else, for a table of at most 8,192 DISTINCT keys
+ * (tie-heavy: rounded scores, a bf16 model's probabilities), the LDS distinct-key index (no
+ * gather); else the LDS search tree. Same integers whichever runs.
  */
 int dauc_auc_counts_sorted_labeled(const float* pos, int64_t P, const float* scores, const void* labels,
                                    int label_dtype, int64_t begin, int64_t end, unsigned long long* wins_ties,
@@ -290,8 +294,9 @@ int dauc_auc_eval_enqueue(const float* scores, const void* labels, int label_dty
  * host call too): the sequence above, ONE readback of its record into `pinned` (caller-owned
  * page-locked host memory of >= 8 int64, e.g. hipHostMalloc; the call writes and reads it) and a
  * synchronisation of `stream`; for verdict 2 the sorted path (radix sort of the positives + the
- * LDS search tree or the count index; or, when the negatives are the smaller class, both classes
- * split and the negatives sorted) and one more readback. Stateless: same inputs, same work.
+ * LDS distinct-key index for tie-heavy tables, or the search tree; or, when the negatives are the
+ * smaller class, both classes split and the negatives sorted) and one more readback. Stateless:
+ * same inputs, same work.
  *   out[6] (HOST int64) = { W, T, P, N, #non-finite scores, #labels not in {-1, 1} }
  *   (W = T = 0 when a class is empty or a score is non-finite: the caller raises like sklearn)
  */
