@@ -233,6 +233,27 @@ __global__ __launch_bounds__(kSortThreads) void radix_scatter_kernel(const void*
     }
 }
 
+// the distinct-key index of tie-heavy tables (dk_*_kernel below)
+constexpr int kDkMax = 8192;
+constexpr int kDkMaxCells = 2 * kDkMax + kCiTop;  // the plan's cells: <= 2 per distinct key + 1 per used bucket
+constexpr int kDkTile = 1024;                     // table keys per tile of the mark / write passes (4 per thread)
+constexpr int kDkUse = 0, kDkD = 1;              // meta words; kCiOk, kCiCells, kCiBlocks: the plan's
+constexpr int kDkScanThreads = 1024;
+static_assert(kDkMax < 65536, "cell words hold 16-bit indices and counts");
+
+struct DkWs {
+    unsigned* meta;    // [16]
+    uint2* l1;         // [kCiTop]
+    unsigned* cstart;  // [kDkMaxCells + 2] the first distinct key of every cell
+    unsigned* kd;      // [kDkMax] the distinct keys, ascending
+    unsigned* cd;      // [kDkMax] #(table keys <= kd[i])
+    unsigned* tcnt;    // [tiles] distinct keys whose last copy is in the tile -> their exclusive prefix
+};
+
+__device__ __forceinline__ bool dk_ci_in_use(const unsigned* __restrict__ ci_meta) {
+    return ci_meta != nullptr && count_index_in_use(ci_meta);
+}
+
 // ---- search ---------------------------------------------------------------------------
 
 // Splitters (every k-th sorted key, k a power of two) kept in LDS: at most kMaxSplit of them
@@ -587,7 +608,9 @@ template <int K, bool TABLE_POS>
 __global__ __launch_bounds__(kQueryThreads) void query_count_kernel(const float* __restrict__ q, int64_t L,
                                                                    const TreeNode* __restrict__ gtree, TreeGeom g,
                                                                    int k, const unsigned* __restrict__ sorted,
-                                                                   int64_t M, unsigned long long* __restrict__ out) {
+                                                                   int64_t M, unsigned long long* __restrict__ out,
+                                                                   const unsigned* __restrict__ dk_meta) {
+    if (dk_meta != nullptr && dk_meta[kDkUse] != 0u) return;  // the distinct-key index counts instead
     extern __shared__ TreeNode tree[];
     for (int i = threadIdx.x; i < g.nodes; i += kQueryThreads) tree[i] = gtree[i];
     const TopKeys top = load_top(gtree, g, sorted, k);
@@ -693,26 +716,6 @@ struct CountWs {
 constexpr size_t kCountBytes = 256 + 3 * size_t(kCiTop) * 4 + ((size_t(kCiMaxCells) + 2) * 4 + 255) / 256 * 256 +
                                size_t(kCiMaxBlocks) * 8 + 256;
 
-// the distinct-key index of tie-heavy tables (dk_*_kernel below)
-constexpr int kDkMax = 8192;
-constexpr int kDkMaxCells = 2 * kDkMax + kCiTop;  // the plan's cells: <= 2 per distinct key + 1 per used bucket
-constexpr int kDkTile = 1024;                     // table keys per tile of the mark / write passes (4 per thread)
-constexpr int kDkUse = 0, kDkD = 1;              // meta words; kCiOk, kCiCells, kCiBlocks: the plan's
-constexpr int kDkScanThreads = 1024;
-static_assert(kDkMax < 65536, "cell words hold 16-bit indices and counts");
-
-struct DkWs {
-    unsigned* meta;    // [16]
-    uint2* l1;         // [kCiTop]
-    unsigned* cstart;  // [kDkMaxCells + 2] the first distinct key of every cell
-    unsigned* kd;      // [kDkMax] the distinct keys, ascending
-    unsigned* cd;      // [kDkMax] #(table keys <= kd[i])
-    unsigned* tcnt;    // [tiles] distinct keys whose last copy is in the tile -> their exclusive prefix
-};
-
-__device__ __forceinline__ bool dk_ci_in_use(const unsigned* __restrict__ ci_meta) {
-    return ci_meta != nullptr && count_index_in_use(ci_meta);
-}
 
 
 
@@ -2166,7 +2169,8 @@ __global__ __launch_bounds__(kCiPlanThreads) void dk_index_kernel(const unsigned
 }
 
 // NQ queries of one lane: W += M - #(table <= x), T += #(table == x) for the queries in `use`
-template <int NQ>
+// (TABLE_POS false: the table is the negatives and the queries positives, W += #(table < x))
+template <int NQ, bool TABLE_POS = true>
 __device__ __forceinline__ void dk_count(const unsigned (&x)[NQ], unsigned use, const uint2* l1, const unsigned* cw,
                                          const uint2* kc, unsigned long long M, unsigned long long& w,
                                          unsigned long long& t) {
@@ -2216,7 +2220,7 @@ __device__ __forceinline__ void dk_count(const unsigned (&x)[NQ], unsigned use, 
         const unsigned le = in ? b[q].y : a[q].y;
         const unsigned lt = eq ? a[q].y : le;
         if ((use >> q) & 1u) {
-            w += M - le;
+            w += TABLE_POS ? M - le : lt;
             t += le - lt;
         }
     }
@@ -2224,6 +2228,104 @@ __device__ __forceinline__ void dk_count(const unsigned (&x)[NQ], unsigned use, 
 
 // The labeled query pass over the distinct-key index (the stream and checks of query_labeled_kernel);
 // returns at once unless the count index is not in use and the distinct-key index is
+// the query kernels' LDS: l1, then {0, 0}, {key, cum} of every distinct key, {+inf, M} (read, never
+// counted, past the last), then the cell words {first distinct key | keys in the cell << 16}
+struct DkLds {
+    uint2* l1;
+    uint2* kc;
+    unsigned* cw;
+};
+__device__ __forceinline__ DkLds dk_load_lds(uint2* lds, const DkWs& dk, int64_t M) {
+    DkLds r{lds, lds + kCiTop, reinterpret_cast<unsigned*>(lds + kCiTop + kDkMax + 2)};
+    const unsigned D = dk.meta[kDkD], cells = dk.meta[kCiCells];
+    for (int i = threadIdx.x; i < kCiTop; i += blockDim.x) r.l1[i] = dk.l1[i];
+    for (unsigned i = threadIdx.x; i < D + 2; i += blockDim.x)
+        r.kc[i] = i == 0 ? uint2{0u, 0u}
+                         : (i <= D ? uint2{dk.kd[i - 1], dk.cd[i - 1]} : uint2{kPadKey, static_cast<unsigned>(M)});
+    for (unsigned c = threadIdx.x; c <= cells; c += blockDim.x) {
+        const unsigned a = dk.cstart[c], b = dk.cstart[c + 1];
+        r.cw[c] = a | ((b - a) << 16);
+    }
+    __syncthreads();
+    return r;
+}
+
+// the block's W, T (and non-finite count) into out[0..1] (and *nonfinite)
+__device__ __forceinline__ void dk_reduce(unsigned long long w, unsigned long long t, unsigned nf,
+                                          unsigned long long* __restrict__ out,
+                                          unsigned long long* __restrict__ nonfinite) {
+    __shared__ unsigned long long red[3][kQueryThreads / kWave];
+    w = wave_sum(w);
+    t = wave_sum(t);
+    const unsigned long long nfw = wave_sum(static_cast<unsigned long long>(nf));
+    const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+    if (lane == 0) {
+        red[0][wid] = w;
+        red[1][wid] = t;
+        red[2][wid] = nfw;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long bw = 0, bt = 0, bn = 0;
+        for (int i = 0; i < kQueryThreads / kWave; ++i) {
+            bw += red[0][i];
+            bt += red[1][i];
+            bn += red[2][i];
+        }
+        if (bw) atomicAdd(out + 0, bw);
+        if (bt) atomicAdd(out + 1, bt);
+        if (bn && nonfinite) atomicAdd(nonfinite, bn);
+    }
+}
+
+// dauc_auc_counts_sorted's form: every element of q[0, L) is a query (no labels); the table is the
+// positives (TABLE_POS) or the negatives
+template <bool TABLE_POS>
+__global__ __launch_bounds__(kQueryThreads) void dk_plain_kernel(const float* __restrict__ q, int64_t L, DkWs dk,
+                                                                 int64_t M, unsigned long long* __restrict__ out) {
+    if (dk.meta[kDkUse] == 0u) return;
+    extern __shared__ uint2 dk_lds[];
+    const DkLds ld = dk_load_lds(dk_lds, dk, M);
+    const unsigned long long MM = static_cast<unsigned long long>(M);
+    unsigned long long w = 0, t = 0;
+    const bool vec = (reinterpret_cast<uintptr_t>(q) & 15u) == 0;
+    const int64_t nvec = vec ? L / 4 : 0;
+    const int64_t stride = int64_t(gridDim.x) * kQueryThreads;
+    const int64_t tid = int64_t(blockIdx.x) * kQueryThreads + threadIdx.x;
+    if (nvec > 0) {
+        constexpr int U = 2, NQ = 4 * U;
+        f32x4 fc[U], fn[U];
+        auto load = [&](int64_t v0, f32x4 (&f)[U]) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int64_t v = v0 + int64_t(u) * stride;
+                f[u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(q) + (v < nvec ? v : 0));
+            }
+        };
+        load(tid, fc);
+        for (int64_t v0 = tid; v0 < nvec; v0 += int64_t(U) * stride) {
+            load(v0 + int64_t(U) * stride, fn);
+            unsigned x[NQ], use = 0u;
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const float f[4] = {fc[u].x, fc[u].y, fc[u].z, fc[u].w};
+                const unsigned in = v0 + int64_t(u) * stride < nvec ? 0xfu : 0u;
+                use |= in << (4 * u);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) x[4 * u + j] = key_fast(f[j]);
+            }
+            dk_count<NQ, TABLE_POS>(x, use, ld.l1, ld.cw, ld.kc, MM, w, t);
+#pragma unroll
+            for (int u = 0; u < U; ++u) fc[u] = fn[u];
+        }
+    }
+    for (int64_t i = nvec * 4 + tid; i < L; i += stride) {
+        const unsigned x[1] = {key_fast(q[i])};
+        dk_count<1, TABLE_POS>(x, 1u, ld.l1, ld.cw, ld.kc, MM, w, t);
+    }
+    dk_reduce(w, t, 0u, out, nullptr);
+}
+
 template <typename LT, int U = 2>
 __global__ __launch_bounds__(kQueryThreads) void dk_query_kernel(const float* __restrict__ s, const LT* __restrict__ lab,
                                                                  int64_t begin, int64_t end,
@@ -2232,21 +2334,11 @@ __global__ __launch_bounds__(kQueryThreads) void dk_query_kernel(const float* __
                                                                  unsigned long long* __restrict__ nonfinite) {
     if (dk_ci_in_use(ci_meta) || dk.meta[kDkUse] == 0u) return;
     extern __shared__ uint2 dk_lds[];
-    uint2* l1 = dk_lds;                                                         // [kCiTop]
-    uint2* kc = dk_lds + kCiTop;                                                // [D + 2]
-    unsigned* cw = reinterpret_cast<unsigned*>(dk_lds + kCiTop + kDkMax + 2);  // [cells + 1]
-    const unsigned D = dk.meta[kDkD], cells = dk.meta[kCiCells];
+    const DkLds ld = dk_load_lds(dk_lds, dk, M);
+    const uint2* l1 = ld.l1;
+    const uint2* kc = ld.kc;
+    const unsigned* cw = ld.cw;
     const unsigned long long MM = static_cast<unsigned long long>(M);
-    for (int i = threadIdx.x; i < kCiTop; i += kQueryThreads) l1[i] = dk.l1[i];
-    // {0, 0}, {key, cum} of every distinct key, then {+inf, M} (read, never counted, past the last)
-    for (unsigned i = threadIdx.x; i < D + 2; i += kQueryThreads)
-        kc[i] = i == 0 ? uint2{0u, 0u}
-                       : (i <= D ? uint2{dk.kd[i - 1], dk.cd[i - 1]} : uint2{kPadKey, static_cast<unsigned>(M)});
-    for (unsigned c = threadIdx.x; c <= cells; c += kQueryThreads) {
-        const unsigned a = dk.cstart[c], b = dk.cstart[c + 1];
-        cw[c] = a | ((b - a) << 16);
-    }
-    __syncthreads();
     unsigned long long w = 0, t = 0;
     unsigned nf = 0;
     auto one = [&](int64_t i) {
@@ -2306,28 +2398,7 @@ __global__ __launch_bounds__(kQueryThreads) void dk_query_kernel(const float* __
         for (int64_t i = head + tid; i < head + nvec * 4; i += stride) one(i);
     }
     for (int64_t i = head + nvec * 4 + tid; i < end; i += stride) one(i);
-    __shared__ unsigned long long red[3][kQueryThreads / kWave];
-    w = wave_sum(w);
-    t = wave_sum(t);
-    const unsigned long long nfw = wave_sum(static_cast<unsigned long long>(nf));
-    const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
-    if (lane == 0) {
-        red[0][wid] = w;
-        red[1][wid] = t;
-        red[2][wid] = nfw;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        unsigned long long bw = 0, bt = 0, bn = 0;
-        for (int i = 0; i < kQueryThreads / kWave; ++i) {
-            bw += red[0][i];
-            bt += red[1][i];
-            bn += red[2][i];
-        }
-        if (bw) atomicAdd(out + 0, bw);
-        if (bt) atomicAdd(out + 1, bt);
-        if (bn && nonfinite) atomicAdd(nonfinite, bn);
-    }
+    dk_reduce(w, t, nf, out, nonfinite);
 }
 constexpr size_t kDkQueryLds = (size_t(kCiTop) + kDkMax + 2) * 8 + (size_t(kDkMaxCells) + 1) * 4;
 static_assert(kDkQueryLds + 3 * (kQueryThreads / kWave) * 8 <= 160 * 1024, "the distinct-key query's LDS");
@@ -2361,11 +2432,12 @@ int query_grid(int64_t L) {
 
 template <bool TABLE_POS>
 int launch_query(int k, const float* q, int64_t L, const TreeNode* tree, const TreeGeom& g, const unsigned* sorted,
-                 int64_t M, unsigned long long* out, hipStream_t st) {
+                 int64_t M, unsigned long long* out, hipStream_t st, const unsigned* dk_meta = nullptr) {
     const dim3 grid(query_grid(L)), block(kQueryThreads);
     const size_t lds = size_t(g.nodes) * sizeof(TreeNode);
 #define DAUC_QC(KV) \
-    hipLaunchKernelGGL((query_count_kernel<KV, TABLE_POS>), grid, block, lds, st, q, L, tree, g, k, sorted, M, out)
+    hipLaunchKernelGGL((query_count_kernel<KV, TABLE_POS>), grid, block, lds, st, q, L, tree, g, k, sorted, M, out, \
+                       dk_meta)
     switch (k) {
         case 1: DAUC_QC(1); break;
         case 2: DAUC_QC(2); break;
@@ -2576,6 +2648,13 @@ int prepare_dk(const unsigned* sorted, int64_t M, const unsigned* ci_meta, const
     hipLaunchKernelGGL(dk_write_kernel, dim3(static_cast<unsigned>(nt)), dim3(kDkTile / 4), 0, st, sorted, M, ci_meta,
                        dk);
     hipLaunchKernelGGL(dk_index_kernel, dim3(1), dim3(kCiPlanThreads), 0, st, ci_meta, dk);
+    return launch_status();
+}
+
+template <bool TABLE_POS>
+int launch_dk_plain(const float* q, int64_t L, const DkWs& dk, int64_t M, unsigned long long* out, hipStream_t st) {
+    hipLaunchKernelGGL((dk_plain_kernel<TABLE_POS>), dim3(query_grid(L)), dim3(kQueryThreads), kDkQueryLds, st, q, L,
+                       dk, M, out);
     return launch_status();
 }
 
@@ -2970,8 +3049,16 @@ int dauc_auc_counts_sorted(const float* pos, int64_t P, const float* neg, int64_
     int rc = prepare_table(table_pos ? pos : neg, M, workspace, st, &sorted, &tree, &k, &g);
     if (rc) return rc;
     const float* q = table_pos ? neg : pos;
-    return table_pos ? launch_query<true>(k, q, L, tree, g, sorted, M, wins_ties, st)
-                     : launch_query<false>(k, q, L, tree, g, sorted, M, wins_ties, st);
+    // the distinct-key index where it holds the table (tie-heavy), else the tree: chosen on the device
+    const bool distinct = g_search_mode != 1;
+    const DkWs dk = dk_ws_of(workspace, M);
+    if (distinct && (rc = prepare_dk(sorted, M, nullptr, dk, st))) return rc;
+    const unsigned* dkm = distinct ? dk.meta : nullptr;
+    rc = table_pos ? launch_query<true>(k, q, L, tree, g, sorted, M, wins_ties, st, dkm)
+                   : launch_query<false>(k, q, L, tree, g, sorted, M, wins_ties, st, dkm);
+    if (rc || !distinct) return rc;
+    return table_pos ? launch_dk_plain<true>(q, L, dk, M, wins_ties, st)
+                     : launch_dk_plain<false>(q, L, dk, M, wins_ties, st);
 }
 
 int dauc_auc_counts_sorted_labeled(const float* pos, int64_t P, const float* scores, const void* labels,
