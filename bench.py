@@ -658,6 +658,29 @@ def bench_auc(args, world, rank, device, log2n=None, pos=None, pair_reps=None):
             out["m_sort"]["t_cold"] = cold
             out["m_sort"]["t_alternating"] = max_over_ranks(float(np.median(alt)), world)
             del s2, y2
+            # the same scores rounded to bf16 (a bf16 model's scores: few distinct values, many
+            # positives on each): the count index refuses the table and the evaluation runs the
+            # sorted path's distinct-key index; checked against one pair-count evaluation of them
+            sb = s.bfloat16().float()
+            cb = ev.counts(y, sb)
+            tb = []
+            for _ in range(reps):
+                torch.cuda.synchronize()
+                if grouped():
+                    dist.barrier()
+                t0 = time.perf_counter()
+                ev.counts(y, sb)
+                torch.cuda.synchronize()
+                tb.append(time.perf_counter() - t0)
+            pb = ExactAUC(world=world, rank=rank, variant=args.variant, method="pairs", shard_min=shard_min,
+                          collective=grouped()).counts(y, sb)
+            out["m_sort"]["tie_heavy"] = {
+                "t_eval": max_over_ranks(float(np.median(tb)), world),
+                "distinct_positive_values": int(torch.unique(sb[y == 1]).numel()),
+                "counts_match_pair_count": (cb["wins"], cb["ties"]) == (pb["wins"], pb["ties"])}
+            if not out["m_sort"]["tie_heavy"]["counts_match_pair_count"]:
+                raise RuntimeError(f"exact AUC methods disagree on bf16-rounded scores: {cb} vs {pb}")
+            del sb
         log(f"rank {rank}: auc 2^{log2n} {method} eval {out['m_' + method]['t_eval'] * 1e3:.2f} ms")
     a, b = out["m_sort"]["counts"], out["m_pairs"]["counts"]
     if (a["wins"], a["ties"]) != (b["wins"], b["ties"]):
@@ -703,6 +726,12 @@ def auc_record(auc, world, config_name):
         "eval_ms_cold": sk["t_cold"] * 1e3,
         "eval_ms_cold_what": "the first call on this device/stream: workspace + page-locked readback words allocated",
         "eval_ms_other_data": sk["t_alternating"] * 1e3,
+        "eval_ms_tie_heavy": sk["tie_heavy"]["t_eval"] * 1e3,
+        "eval_tie_heavy_what": (f"the same scores rounded to bf16 ({sk['tie_heavy']['distinct_positive_values']} "
+                                "distinct positive values; a bf16 model's scores): the count index refuses the "
+                                "table, the blocking call runs the sorted path's LDS distinct-key index; counts "
+                                "equal the pair count's on the same scores: "
+                                f"{sk['tie_heavy']['counts_match_pair_count']}"),
         "eval_ms_other_data_what": "median over calls alternating with another test set of the same length and a "
                                    "different P (no state between calls: no speculation, no miss path)",
         "sort_count_what": f"HIP events around every {sk['count_fn']} call"
