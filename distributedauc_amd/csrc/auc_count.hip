@@ -938,7 +938,12 @@ int compact_unordered(const float* scores, const void* labels, int label_dtype, 
     // reservations at 2^27 instead of 1024 on the one counter address) -- 256
     constexpr int kWideThreads = 256;
     const int threads = wide ? kWideThreads : kCmpThreads;
-    const int slots = wide ? 32 : kCmpSlots;
+    int slots = wide ? 32 : kCmpSlots;
+#ifdef DAUC_TUNING
+    // tuning builds: DAUC_CMP_SLOTS (8, 16, 32) = label groups per thread whatever n
+    if (const char* e = getenv("DAUC_CMP_SLOTS"); e && (atoi(e) == 8 || atoi(e) == 16 || atoi(e) == 32))
+        slots = atoi(e);
+#endif
     const int64_t tile = int64_t(threads) * 16 * slots;
     const int64_t nblk = (n + tile - 1) / tile;
     if (nblk > 0x7fffffffLL) return DAUC_EINVAL;
@@ -961,6 +966,38 @@ int compact_unordered(const float* scores, const void* labels, int label_dtype, 
     uint4* fw = reinterpret_cast<uint4*>(fill_w);
     auto go = [&](auto* lab) {
         using LT = std::remove_const_t<std::remove_pointer_t<decltype(lab)>>;
+#ifdef DAUC_TUNING
+        if (slots == 16) {
+            if (hist_out != nullptr)
+                hipLaunchKernelGGL((compact_unordered_kernel<LT, 16, kCmpThreads, true>), grid, block, 0, st, scores,
+                                   lab, n, vec, pos_out, stats, tag, zero_next, next_tag, zero3, zero_w, nzero_w, cap,
+                                   hist_out, put, put_val, fw, nfill, nblk);
+            else
+                hipLaunchKernelGGL((compact_unordered_kernel<LT, 16, kCmpThreads>), grid, block, 0, st, scores, lab, n,
+                                   vec, pos_out, stats, tag, zero_next, next_tag, zero3, zero_w, nzero_w, cap, hist_out,
+                                   put, put_val, fw, nfill, nblk);
+            return launch_status();
+        }
+        if ((slots == 32) != wide) {  // the other of the two product shapes
+            if (slots == 32 && hist_out != nullptr)
+                hipLaunchKernelGGL((compact_unordered_kernel<LT, 32, kWideThreads, true>), grid, block, 0, st, scores,
+                                   lab, n, vec, pos_out, stats, tag, zero_next, next_tag, zero3, zero_w, nzero_w, cap,
+                                   hist_out, put, put_val, fw, nfill, nblk);
+            else if (slots == 32)
+                hipLaunchKernelGGL((compact_unordered_kernel<LT, 32, kWideThreads>), grid, block, 0, st, scores, lab, n,
+                                   vec, pos_out, stats, tag, zero_next, next_tag, zero3, zero_w, nzero_w, cap, hist_out,
+                                   put, put_val, fw, nfill, nblk);
+            else if (hist_out != nullptr)
+                hipLaunchKernelGGL((compact_unordered_kernel<LT, kCmpSlots, kCmpThreads, true>), grid, block, 0, st,
+                                   scores, lab, n, vec, pos_out, stats, tag, zero_next, next_tag, zero3, zero_w, nzero_w,
+                                   cap, hist_out, put, put_val, fw, nfill, nblk);
+            else
+                hipLaunchKernelGGL((compact_unordered_kernel<LT, kCmpSlots>), grid, block, 0, st, scores, lab, n, vec,
+                                   pos_out, stats, tag, zero_next, next_tag, zero3, zero_w, nzero_w, cap, hist_out, put,
+                                   put_val, fw, nfill, nblk);
+            return launch_status();
+        }
+#endif
         if (wide && hist_out != nullptr)
             hipLaunchKernelGGL((compact_unordered_kernel<LT, 32, kWideThreads, true>), grid, block, 0, st, scores, lab,
                                n, vec, pos_out, stats, tag, zero_next, next_tag, zero3, zero_w, nzero_w, cap, hist_out, put, put_val, fw,
