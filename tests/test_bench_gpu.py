@@ -38,7 +38,8 @@ def test_bench_full_two_ranks_gloo(tmp_path):
     """Every leg the driver's N > 1 run takes, at reduced sizes, as 2 gloo ranks on cuda:0 (VERDICT
     r03 #2): training + the period sweep, coda_round, the split in-training evaluation, the
     configs[0] GPU leg, both exact-AUC legs (sharded sort method and pair count), the loss kernel
-    leg and the CPU baselines. One JSON line on stdout, world size 2."""
+    leg and (--cpu-baseline-any-n: the contract times them at N = 1 only) the CPU baselines. One JSON
+    line on stdout, world size 2."""
     env = dict(os.environ)
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
         env.pop(k, None)
@@ -46,7 +47,8 @@ def test_bench_full_two_ranks_gloo(tmp_path):
            "--arch", "resnet18", "--batch", "32", "--image-size", "64", "--steps", "4", "--warmup", "2",
            "--sweep-I", "1,2", "--sweep-steps", "2", "--eval-images", "256", "--r18-steps", "8",
            "--auc-log2n", "20", "--auc2-log2n", "21", "--auc-reps", "1", "--auc-shard-min", "0", "--sur-log2b", "16", "--sur-reps", "5",
-           "--cpu-workers", "2", "--cpu-steps", "2", "--cpu-sklearn-full", "0", "--cpu-max-s", "20"]
+           "--cpu-workers", "2", "--cpu-steps", "2", "--cpu-sklearn-full", "0", "--cpu-max-s", "20",
+           "--cpu-baseline-any-n"]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=840)
     (tmp_path / "stderr.log").write_text(r.stderr)
     assert r.returncode == 0, r.stderr[-4000:]
@@ -76,14 +78,14 @@ def test_bench_default_sizes_two_ranks_gloo(tmp_path):
     """the driver's N > 1 bench at the BASELINE sizes -- ResNet-50 b256 224^2 bf16 at
     I = 16 with the HIP backbone kernels, the period sweep with real averaging rounds, configs[3]
     (2^24 @ 1 %) and configs[4] (2^27 @ 0.1 %) sharded over the ranks -- as 2 gloo ranks on cuda:0.
-    Fewer steps than the driver's (and no CPU baselines, which profiles/r06/n8_gloo/ covers at 8
-    ranks) so the test stays short; every leg and every size is the default one."""
+    Fewer steps than the driver's so the test stays short; every leg and every size is the default
+    one, and, as in the driver's N > 1 runs, no CPU baseline (timed at N = 1 only)."""
     env = dict(os.environ)
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
         env.pop(k, None)
     cmd = [sys.executable, str(REPO / "bench.py"), "--gpus", "2", "--backend", "gloo", "--steps", "4", "--warmup", "3",
            "--sweep-I", "1,8,16", "--sweep-steps", "16", "--eval-images", "1024", "--r18-steps", "8", "--auc-reps", "1",
-           "--sur-reps", "10", "--no-cpu-baseline"]
+           "--sur-reps", "10"]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=560)
     (tmp_path / "stderr.log").write_text(r.stderr)
     assert r.returncode == 0, r.stderr[-4000:]
@@ -103,6 +105,7 @@ def test_bench_default_sizes_two_ranks_gloo(tmp_path):
         assert out[k]["methods_agree"] and out[k]["sort_mode"] == "sharded", k
         assert out[k]["P"] == P  # the bench's synthetic_scores at 2^24 @ 1 % and 2^27 @ 0.1 %
     assert out["step_roofline"]["flop_per_step"] > 6e12 and out["step_roofline"]["bn"]["bytes_per_step"] > 0
+    assert out["cpu_baseline"] is None and "N = 1 only" in out["cpu_baseline_note"]
 
 
 @pytest.mark.timeout(300)
