@@ -729,7 +729,7 @@ def auc_record(auc, world, config_name):
                   "straight from them with the table size read on the device (cell-ordered table, no sort), locate "
                   "every negative, read in place, through it -- all enqueued with no host sync; one readback per "
                   "call; for tables the index does not fit or finds skewed, the radix sort and behind it the LDS "
-                  "distinct-key index (tie-heavy tables, up to 8,192 distinct keys) or the LDS search tree)",
+                  "distinct-key index (tie-heavy tables, up to 14,000 distinct keys) or the LDS search tree)",
         "eval_ms": sk["t_eval"] * 1e3, "sort_count_ms": sk["t_count"] * 1e3,
         "eval_ms_cold": sk["t_cold"] * 1e3,
         "eval_ms_cold_what": "the first call on this device/stream: workspace + page-locked readback words allocated",

@@ -234,12 +234,13 @@ __global__ __launch_bounds__(kSortThreads) void radix_scatter_kernel(const void*
 }
 
 // the distinct-key index of tie-heavy tables (dk_*_kernel below)
-constexpr int kDkMax = 8192;
-constexpr int kDkMaxCells = 2 * kDkMax + kCiTop;  // the plan's cells: <= 2 per distinct key + 1 per used bucket
+constexpr int kDkMax = 14000;
+// the plan's cells: 4 per distinct key (up to 3,500 of them), fewer but at least 1 past that, + 1 per used bucket
+constexpr int kDkMaxCells = kDkMax + kCiTop;
 constexpr int kDkTile = 1024;                     // table keys per tile of the mark / write passes (4 per thread)
 constexpr int kDkUse = 0, kDkD = 1;              // meta words; kCiOk, kCiCells, kCiBlocks: the plan's
 constexpr int kDkScanThreads = 1024;
-static_assert(kDkMax < 65536, "cell words hold 16-bit indices and counts");
+static_assert(kDkMax < 16384, "the query's LDS holds a cell's first distinct key in 14 bits");
 
 struct DkWs {
     unsigned* meta;    // [16]
@@ -737,7 +738,8 @@ __global__ __launch_bounds__(256) void ci_first_kernel(const unsigned* __restric
 // (the body is shared with the distinct-key index's plan: dk_index_kernel; `first` and `l1` may be
 // LDS or global, `max_cells` the cells the consumer's LDS holds)
 __device__ __forceinline__ void ci_plan_body(int64_t M, const unsigned* first, uint2* l1, unsigned* __restrict__ meta,
-                                             int64_t max_cells, unsigned* wtot, unsigned* incl_min, unsigned* totals) {
+                                             int64_t max_cells, unsigned* wtot, unsigned* incl_min, unsigned* totals,
+                                             int per_key = 2) {
     static_assert(kCiTop == 2 * kCiPlanThreads, "two top buckets per thread");
     const unsigned m32 = static_cast<unsigned>(M);
     int tj[2];
@@ -767,7 +769,7 @@ __device__ __forceinline__ void ci_plan_body(int64_t M, const unsigned* first, u
     if (threadIdx.x == kCiPlanThreads - 1) totals[0] = used;
     __syncthreads();
     const int64_t avail = max_cells - int64_t(totals[0]);
-    const int64_t num = avail < 2 * M ? avail : 2 * M;
+    const int64_t num = avail < per_key * M ? avail : per_key * M;
     unsigned C[2];
 #pragma unroll
     for (int j = 0; j < 2; ++j) C[j] = n[j] ? static_cast<unsigned>((int64_t(n[j]) * num + M - 1) / M) : 0u;
@@ -2153,7 +2155,8 @@ __global__ __launch_bounds__(kCiPlanThreads) void dk_index_kernel(const unsigned
         if (d == 0 || (dk.kd[d - 1] >> kCiLowBits) != t) first[t] = d;
     }
     __syncthreads();
-    ci_plan_body(D, first, l1, dk.meta, kDkMaxCells, wtot, incl_min, totals);
+    // up to 4 cells per distinct key while the LDS holds them (fewer cells of 2+ keys: less searching)
+    ci_plan_body(D, first, l1, dk.meta, kDkMaxCells, wtot, incl_min, totals, 4);
     __syncthreads();
     for (int t = threadIdx.x; t < kCiTop; t += kCiPlanThreads) dk.l1[t] = l1[t];
     const unsigned cells = totals[1];
@@ -2171,18 +2174,20 @@ __global__ __launch_bounds__(kCiPlanThreads) void dk_index_kernel(const unsigned
 // NQ queries of one lane: W += M - #(table <= x), T += #(table == x) for the queries in `use`
 // (TABLE_POS false: the table is the negatives and the queries positives, W += #(table < x))
 template <int NQ, bool TABLE_POS = true>
-__device__ __forceinline__ void dk_count(const unsigned (&x)[NQ], unsigned use, const uint2* l1, const unsigned* cw,
-                                         const uint2* kc, unsigned long long M, unsigned long long& w,
-                                         unsigned long long& t) {
+__device__ __forceinline__ void dk_count(const unsigned (&x)[NQ], unsigned use, const uint2* l1,
+                                         const unsigned short* st, const uint2* kc, unsigned long long M,
+                                         unsigned long long& w, unsigned long long& t) {
     unsigned s0[NQ], n[NQ];
     uint2 e[NQ];
 #pragma unroll
     for (int q = 0; q < NQ; ++q) e[q] = l1[x[q] >> kCiLowBits];
+unsigned c[NQ];
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
-        const unsigned v = cw[ci_cell(x[q], e[q])];
-        s0[q] = v & 0xffffu;
-        n[q] = v >> 16;
+        c[q] = ci_cell(x[q], e[q]);
+        const unsigned v = st[c[q]];
+        s0[q] = v & 0x3fffu;
+        n[q] = v >> 14;
     }
     bool many = false;
 #pragma unroll
@@ -2191,7 +2196,7 @@ __device__ __forceinline__ void dk_count(const unsigned (&x)[NQ], unsigned use, 
 #pragma unroll
         for (int q = 0; q < NQ; ++q) {
             if (n[q] > 1u) {
-                unsigned lo = s0[q], cnt = n[q];
+                unsigned lo = s0[q], cnt = n[q] < 3u ? n[q] : (st[c[q] + 1] & 0x3fffu) - s0[q];
                 while (cnt > 0u) {
                     const unsigned h = cnt >> 1;
                     if (kc[lo + h + 1].x <= x[q]) {
@@ -2229,22 +2234,23 @@ __device__ __forceinline__ void dk_count(const unsigned (&x)[NQ], unsigned use, 
 // The labeled query pass over the distinct-key index (the stream and checks of query_labeled_kernel);
 // returns at once unless the count index is not in use and the distinct-key index is
 // the query kernels' LDS: l1, then {0, 0}, {key, cum} of every distinct key, {+inf, M} (read, never
-// counted, past the last), then the cell words {first distinct key | keys in the cell << 16}
+// counted, past the last), then per cell 16 bits: its first distinct key (14 bits) and how many it
+// holds, saturated at 3 (the next cell's first key then gives the count: rare)
 struct DkLds {
     uint2* l1;
     uint2* kc;
-    unsigned* cw;
+    unsigned short* st;
 };
 __device__ __forceinline__ DkLds dk_load_lds(uint2* lds, const DkWs& dk, int64_t M) {
-    DkLds r{lds, lds + kCiTop, reinterpret_cast<unsigned*>(lds + kCiTop + kDkMax + 2)};
+    DkLds r{lds, lds + kCiTop, reinterpret_cast<unsigned short*>(lds + kCiTop + kDkMax + 2)};
     const unsigned D = dk.meta[kDkD], cells = dk.meta[kCiCells];
     for (int i = threadIdx.x; i < kCiTop; i += blockDim.x) r.l1[i] = dk.l1[i];
     for (unsigned i = threadIdx.x; i < D + 2; i += blockDim.x)
         r.kc[i] = i == 0 ? uint2{0u, 0u}
                          : (i <= D ? uint2{dk.kd[i - 1], dk.cd[i - 1]} : uint2{kPadKey, static_cast<unsigned>(M)});
-    for (unsigned c = threadIdx.x; c <= cells; c += blockDim.x) {
-        const unsigned a = dk.cstart[c], b = dk.cstart[c + 1];
-        r.cw[c] = a | ((b - a) << 16);
+    for (unsigned c = threadIdx.x; c <= cells + 1; c += blockDim.x) {
+        const unsigned a = dk.cstart[c], n = c <= cells ? dk.cstart[c + 1] - a : 0u;
+        r.st[c] = static_cast<unsigned short>(a | (min(n, 3u) << 14));
     }
     __syncthreads();
     return r;
@@ -2314,14 +2320,14 @@ __global__ __launch_bounds__(kQueryThreads) void dk_plain_kernel(const float* __
 #pragma unroll
                 for (int j = 0; j < 4; ++j) x[4 * u + j] = key_fast(f[j]);
             }
-            dk_count<NQ, TABLE_POS>(x, use, ld.l1, ld.cw, ld.kc, MM, w, t);
+            dk_count<NQ, TABLE_POS>(x, use, ld.l1, ld.st, ld.kc, MM, w, t);
 #pragma unroll
             for (int u = 0; u < U; ++u) fc[u] = fn[u];
         }
     }
     for (int64_t i = nvec * 4 + tid; i < L; i += stride) {
         const unsigned x[1] = {key_fast(q[i])};
-        dk_count<1, TABLE_POS>(x, 1u, ld.l1, ld.cw, ld.kc, MM, w, t);
+        dk_count<1, TABLE_POS>(x, 1u, ld.l1, ld.st, ld.kc, MM, w, t);
     }
     dk_reduce(w, t, 0u, out, nullptr);
 }
@@ -2337,7 +2343,7 @@ __global__ __launch_bounds__(kQueryThreads) void dk_query_kernel(const float* __
     const DkLds ld = dk_load_lds(dk_lds, dk, M);
     const uint2* l1 = ld.l1;
     const uint2* kc = ld.kc;
-    const unsigned* cw = ld.cw;
+    const unsigned short* st = ld.st;
     const unsigned long long MM = static_cast<unsigned long long>(M);
     unsigned long long w = 0, t = 0;
     unsigned nf = 0;
@@ -2346,7 +2352,7 @@ __global__ __launch_bounds__(kQueryThreads) void dk_query_kernel(const float* __
             const float f = s[i];
             nf += !isfinite(f);
             const unsigned x[1] = {key_fast(f)};
-            dk_count<1>(x, 1u, l1, cw, kc, MM, w, t);
+            dk_count<1>(x, 1u, l1, st, kc, MM, w, t);
         }
     };
     const int64_t a0 = (begin + 3) & ~int64_t(3);
@@ -2387,7 +2393,7 @@ __global__ __launch_bounds__(kQueryThreads) void dk_query_kernel(const float* __
                     nf += neg && !isfinite(f[q]);
                 }
             }
-            dk_count<NQ>(x, use, l1, cw, kc, MM, w, t);
+            dk_count<NQ>(x, use, l1, st, kc, MM, w, t);
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 fc[u] = fn[u];
@@ -2400,7 +2406,7 @@ __global__ __launch_bounds__(kQueryThreads) void dk_query_kernel(const float* __
     for (int64_t i = head + nvec * 4 + tid; i < end; i += stride) one(i);
     dk_reduce(w, t, nf, out, nonfinite);
 }
-constexpr size_t kDkQueryLds = (size_t(kCiTop) + kDkMax + 2) * 8 + (size_t(kDkMaxCells) + 1) * 4;
+constexpr size_t kDkQueryLds = (size_t(kCiTop) + kDkMax + 2) * 8 + (size_t(kDkMaxCells) + 2) * 2;
 static_assert(kDkQueryLds + 3 * (kQueryThreads / kWave) * 8 <= 160 * 1024, "the distinct-key query's LDS");
 
 int query_grid(int64_t L) {
@@ -2661,14 +2667,6 @@ int launch_dk_plain(const float* q, int64_t L, const DkWs& dk, int64_t M, unsign
 template <typename LT>
 int launch_dk(const float* s, const LT* lab, int64_t begin, int64_t end, const unsigned* ci_meta, const DkWs& dk,
               int64_t M, unsigned long long* out, unsigned long long* nonfinite, hipStream_t st) {
-#ifdef DAUC_TUNING
-    const char* e = getenv("DAUC_DK_U");  // tuning builds: 4 float4 slots per iteration instead of 2
-    if (e && atoi(e) == 4) {
-        hipLaunchKernelGGL((dk_query_kernel<LT, 4>), dim3(query_grid(end - begin)), dim3(kQueryThreads), kDkQueryLds,
-                           st, s, lab, begin, end, ci_meta, dk, M, out, nonfinite);
-        return launch_status();
-    }
-#endif
     hipLaunchKernelGGL((dk_query_kernel<LT>), dim3(query_grid(end - begin)), dim3(kQueryThreads), kDkQueryLds, st, s,
                        lab, begin, end, ci_meta, dk, M, out, nonfinite);
     return launch_status();

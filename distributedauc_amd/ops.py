@@ -777,7 +777,7 @@ def set_index_form(form: int) -> None:
 def set_search_mode(mode: int) -> None:
     """Search structure of the sort method (dauc_set_search_mode): 0 automatic (the count index
     where the table fits it and is not skewed, else the distinct-key index where the table holds
-    at most 8,192 distinct keys, else the LDS search tree), 1 the tree, 2 the distinct-key index
+    at most 14,000 distinct keys, else the LDS search tree), 1 the tree, 2 the distinct-key index
     wherever it holds the table. Same integers in every mode; for tests and measurements (tuning
     build)."""
     check(_lib.tuning().dauc_set_search_mode(int(mode)), "dauc_set_search_mode")

@@ -258,7 +258,7 @@ int dauc_auc_counts_sorted(const float* pos, int64_t P, const float* neg, int64_
  * queried scores that are NaN or +-inf (the only check the negatives get: sklearn's
  * _ranking.py:868-869 rejects them). workspace >= dauc_sort_workspace_size(P). The search
  * structure behind the sort is chosen on the device: the LDS count index (one 16-byte window
- * gather per query) where it holds the table; else, for a table of at most 8,192 DISTINCT keys
+ * gather per query) where it holds the table; else, for a table of at most 14,000 DISTINCT keys
  * (tie-heavy: rounded scores, a bf16 model's probabilities), the LDS distinct-key index (no
  * gather); else the LDS search tree. Same integers whichever runs.
  */

@@ -57,10 +57,10 @@ int dauc_pair_count_variant(const float* pos, int64_t P, const float* neg, int64
  * Same integers in every mode.
  *   0: the product's choice -- the count index for tables of up to 219,838 keys, unless the
  *      device finds the table skewed (a cell of 15+ keys, or more than 1.5 keys per cell): then,
- *      and for larger tables, the distinct-key index when the table holds at most 8,192 distinct
+ *      and for larger tables, the distinct-key index when the table holds at most 14,000 distinct
  *      keys (tie-heavy tables, round 6), else the LDS search tree;
  *   1: the LDS search tree always (the fallback's structure, tested on every table);
- *   2: the distinct-key index whenever the table holds at most 8,192 distinct keys (the count
+ *   2: the distinct-key index whenever the table holds at most 14,000 distinct keys (the count
  *      index is not built), else the tree -- to test it on any table.
  * Modes 1 and 2 also send dauc_auc_eval_* straight to the sorted path (no count index first).
  */

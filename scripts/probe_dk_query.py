@@ -1,7 +1,9 @@
 """The distinct-key query pass alone (tuning build, search mode 2: the sorted path builds the
 distinct-key index, the tree and count-index passes return at once), HIP events around `reps`
 back-to-back dauc_auc_counts_sorted_labeled calls on bf16-rounded scores at 2^24 @ 1 % and
-2^27 @ 0.1 %; DAUC_DK_U (2, 4) interleaved: the float4 slots per iteration. Counts checked equal.
+2^27 @ 0.1 %. (It interleaved DAUC_DK_U = 2 and 4 float4 slots per iteration while that knob existed:
+4 spills and was removed; the second leg of each pair now runs the product's 2 again.) Counts
+checked equal.
 
     python scripts/probe_dk_query.py [reps]
 """

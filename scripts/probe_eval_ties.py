@@ -2,7 +2,7 @@
 enqueued evaluation reports (1: the count index held the table; 2: it refused it, and the blocking
 call re-runs the sorted path) and the wall time of the blocking call (dauc_auc_eval_counts, host
 read included, mean of `reps` after a warm call). Distributions at 2^24 @ 1 % and 2^27 @ 0.1 %:
-U(0,1) (the bench's), U(0,1) rounded to bf16, to 1e-3 and to 1e-5, and sigmoid of N(0, 2) logits
+U(0,1) (the bench's), U(0,1) rounded to bf16, to 1e-3, 1e-4 and 1e-5, and sigmoid of N(0, 2) logits
 rounded to bf16 (a bf16 model's probabilities).
 
     python scripts/probe_eval_ties.py [reps] [--only DIST LOG2N]   (--only: one case, for a kernel trace)
@@ -33,6 +33,7 @@ def dists(s):
     yield "uniform", s
     yield "bf16", s.bfloat16().float()
     yield "round1e-3", torch.round(s * 1e3) / 1e3
+    yield "round1e-4", torch.round(s * 1e4) / 1e4
     yield "round1e-5", torch.round(s * 1e5) / 1e5
     z = torch.randn(s.numel(), generator=g, device=dev) * 2.0
     yield "sigmoid_bf16_logits", torch.sigmoid(z.bfloat16().float())

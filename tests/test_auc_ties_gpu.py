@@ -2,7 +2,7 @@
 
 The count index refuses a table with a cell of 15+ keys; tie-heavy positive tables (rounded scores,
 the probabilities of a bf16 model) are exactly that. The sorted path then counts every query from
-the table's DISTINCT keys with the number of table keys <= each, held in LDS (up to 8,192 distinct
+the table's DISTINCT keys with the number of table keys <= each, held in LDS (up to 14,000 distinct
 keys), instead of the LDS search tree. Every case runs in search mode 0 (the product's choice), 1
 (the tree) and 2 (the distinct-key index wherever it holds the table: include/dauc_tuning.h), so
 the three structures are checked against each other and against the oracle. Bar: (W, T) bit-exact
@@ -128,10 +128,10 @@ def test_distinct_index_label_widths(dev, ops, dtype):
     _check(ops, dev, s, y.astype(dtype), 1, 299_999, what=str(dtype) + " ragged")
 
 
-@pytest.mark.parametrize("D", [1, 2, 8191, 8192, 8193, 20_000])
+@pytest.mark.parametrize("D", [1, 2, 8192, 13_999, 14_000, 14_001, 20_000])
 def test_distinct_index_capacity(dev, ops, D):
     """Exactly D distinct positive values, 16 copies each (a cell of the count index holds 15+:
-    refused), queries on, between, below and above them. Up to 8,192 the distinct-key index holds
+    refused), queries on, between, below and above them. Up to 14,000 the distinct-key index holds
     the table; past it the tree counts (mode 2 then falls back too)."""
     rng = np.random.default_rng(D)
     vals = np.unique(rng.random(4 * D + 16, dtype=np.float32))[:D]
