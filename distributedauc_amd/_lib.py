@@ -72,6 +72,7 @@ SIGNATURES = {
     "dauc_auc_slot_bytes": (_sz, [_i64, _int]),
     "dauc_auc_eval_compact_part": (_int, [_vp, _vp, _int, _i64, _int, _int, _vp, _vp, _sz, _vp]),
     "dauc_auc_eval_query_part": (_int, [_vp, _vp, _int, _i64, _int, _int, _vp, _vp, _vp, _sz, _vp]),
+    "dauc_auc_eval_query_part_sorted": (_int, [_vp, _vp, _int, _i64, _int, _int, _vp, _i64, _vp, _vp, _sz, _vp]),
     "dauc_compact_positives": (_int, [_vp, _vp, _int, _i64, _vp, _vp, _vp, _sz, _vp]),
     "dauc_sort_keys": (_int, [_vp, _i64, _vp, _vp, _sz, _vp]),
     "dauc_bn_workspace_size": (_sz, [_i64, _int]),

@@ -201,6 +201,18 @@ class ExactAUC:
         if P == 0 or N == 0:
             return {"wins": 0, "ties": 0, "P": P, "N": N, "other": other}
         if 2 in verdicts:
+            if self.reduce and P <= N:
+                # the gathered slots still hold every positive (unless a slot overflowed): each rank
+                # sorts them and counts its own slice (tie-heavy tables: the distinct-key index), one
+                # more all-gather of the records -- no whole-vector compaction on any rank
+                ops.auc_eval_query_part_sorted(s, y, self.rank, self.world, slots[1][: nb * self.world], P, out=mine)
+                dist.all_gather_into_tensor(gathered, mine, group=self.group)
+                vals2 = gathered.view(self.world, 8).tolist()
+                if all(v[7] == 1 for v in vals2):
+                    if sum(v[2] for v in vals2):
+                        raise ValueError("Input y_score contains NaN or infinity.")
+                    return {"wins": sum(v[0] for v in vals2), "ties": sum(v[1] for v in vals2), "P": P, "N": N,
+                            "other": other}
             return dict(self._counts_sort_sorted_path(y, s), other=other)
         return {"wins": sum(v[0] for v in vals), "ties": sum(v[1] for v in vals), "P": P, "N": N, "other": other}
 

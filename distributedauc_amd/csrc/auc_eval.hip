@@ -272,6 +272,48 @@ int64_t query_hi(int64_t n, int part, int parts) {
     return slice_lo(n, q + 1, parts);
 }
 
+// The two-step evaluation's sorted fallback (dauc_auc_eval_query_part_sorted): the gathered slots'
+// positives copied into one contiguous table at their rank-order offsets; bad[0] = 1 when a slot
+// overflowed (its positives are not all there) or the slots' total is not the caller's P.
+__global__ __launch_bounds__(256) void slot_gather_kernel(const unsigned char* __restrict__ slots, size_t sbytes,
+                                                          int parts, int64_t cap, int64_t P, float* __restrict__ pos,
+                                                          unsigned* __restrict__ bad) {
+    const int r = blockIdx.y;
+    auto count = [&](int j) {
+        return reinterpret_cast<const unsigned long long*>(slots + size_t(j) * sbytes)[0];
+    };
+    __shared__ unsigned long long off;
+    if (threadIdx.x == 0) {
+        unsigned long long before = 0, total = 0;
+        bool over = false;
+        for (int j = 0; j < parts; ++j) {
+            const unsigned long long pj = count(j);
+            before += j < r ? pj : 0ull;
+            total += pj;
+            over |= pj > static_cast<unsigned long long>(cap);
+        }
+        off = before;
+        if (blockIdx.x == 0 && r == 0 && (over || total != static_cast<unsigned long long>(P))) bad[0] = 1u;
+    }
+    __syncthreads();
+    const unsigned long long pr = count(r);
+    if (pr > static_cast<unsigned long long>(cap)) return;  // overflowed: bad, nothing to copy
+    const float* src = reinterpret_cast<const float*>(slots + size_t(r) * sbytes + kSlotHdr);
+    for (unsigned long long i = uint64_t(blockIdx.x) * 256 + threadIdx.x; i < pr; i += uint64_t(gridDim.x) * 256) {
+        const unsigned long long d = off + i;
+        if (d < static_cast<unsigned long long>(P)) pos[d] = src[i];
+    }
+}
+
+// record word 3 = P, word 7 = the verdict (1 counted, 2 the slots could not serve: the caller's
+// whole-vector fallback)
+__global__ void sorted_part_verdict_kernel(const unsigned* __restrict__ bad, int64_t P, int64_t* __restrict__ rec) {
+    if (threadIdx.x == 0) {
+        rec[3] = P;
+        rec[7] = bad[0] ? 2 : 1;
+    }
+}
+
 }  // namespace
 }  // namespace dauc
 
@@ -364,6 +406,48 @@ int dauc_auc_eval_query_part(const float* scores, const void* labels, int label_
                                            w.verdict, w.tws, w.tws_bytes, st, reinterpret_cast<unsigned*>(part_out + 4));
     return counts_labeled_slotted(src, w.stab, mcap, scores, labels, label_dtype, qlo, qhi, w.wt, w.wt + 2, w.verdict,
                                   w.tws, w.tws_bytes, st, reinterpret_cast<unsigned*>(part_out + 4));
+}
+
+int dauc_auc_eval_query_part_sorted(const float* scores, const void* labels, int label_dtype, int64_t n, int part,
+                                    int parts, const void* slots, int64_t P, int64_t* part_out, void* workspace,
+                                    size_t workspace_bytes, dauc_stream_t stream) {
+    if (slots == nullptr || part_out == nullptr || (reinterpret_cast<uintptr_t>(slots) & 255u) != 0 ||
+        (reinterpret_cast<uintptr_t>(part_out) & 7u) != 0 || P < 1 ||
+        !valid_args(scores, labels, label_dtype, n, part, parts, workspace, workspace_bytes))
+        return DAUC_EINVAL;
+    const size_t sall = slot_bytes(parts) * size_t(parts);
+    if (overlaps(part_out, kRecord, workspace, workspace_bytes) || overlaps(part_out, kRecord, slots, sall) ||
+        overlaps(slots, sall, workspace, workspace_bytes))
+        return DAUC_EINVAL;
+    hipStream_t st = as_hip(stream);
+    const EvalWs w = eval_ws(workspace, n);
+    hipError_t e;
+    auto* bad = reinterpret_cast<unsigned*>(w.spare);
+    if ((e = hipMemsetAsync(part_out, 0, kRecord, st)) != hipSuccess ||
+        (e = hipMemsetAsync(bad, 0, 4, st)) != hipSuccess)
+        return -static_cast<int>(e);
+    if (P > n - P) {
+        // the negatives are the smaller class: the slots hold the wrong one (the caller's fallback)
+        if ((e = hipMemsetAsync(bad, 1, 1, st)) != hipSuccess) return -static_cast<int>(e);
+    } else {
+        const int64_t cap = slot_cap(parts);
+        const int64_t bx = (cap + 1023) / 1024 < 64 ? (cap + 1023) / 1024 : 64;
+        hipLaunchKernelGGL(slot_gather_kernel, dim3(static_cast<unsigned>(bx), static_cast<unsigned>(parts)), dim3(256),
+                           0, st, static_cast<const unsigned char*>(slots), slot_bytes(parts), parts, cap, P, w.pos, bad);
+        int rc = launch_status();
+        if (rc) return rc;
+        // this rank's own slice of the scores against the sorted table (the count index would refuse
+        // it again: the distinct-key index for tie-heavy tables, else the tree); on a bad gather the
+        // counts are discarded with the verdict
+        const int64_t qlo = slice_lo(n, part, parts), qhi = slice_lo(n, part + 1, parts);
+        auto* rec = reinterpret_cast<unsigned long long*>(part_out);
+        if (qhi > qlo &&
+            (rc = counts_sorted_labeled(w.pos, P, scores, labels, label_dtype, qlo, qhi, rec, rec + 2, w.tws,
+                                        w.tws_bytes, st, false)))
+            return rc;
+    }
+    hipLaunchKernelGGL(sorted_part_verdict_kernel, dim3(1), dim3(64), 0, st, bad, P, part_out);
+    return launch_status();
 }
 
 int dauc_auc_eval_counts(const float* scores, const void* labels, int label_dtype, int64_t n, int64_t* out,

@@ -471,6 +471,28 @@ def auc_eval_query_part(scores: torch.Tensor, labels: torch.Tensor, part: int, p
     return out
 
 
+def auc_eval_query_part_sorted(scores: torch.Tensor, labels: torch.Tensor, part: int, parts: int,
+                               slots: torch.Tensor, P: int, out: torch.Tensor | None = None) -> torch.Tensor:
+    """The two-step evaluation's verdict-2 path (dauc_auc_eval_query_part_sorted): the gathered
+    slots' P positives sorted into one table (the distinct-key index for tie-heavy tables, else the
+    LDS tree), this rank's own slice counted. Returns the device int64 [8] record {W, T, #non-finite
+    queried, P, 0, 0, 0, verdict}; verdict 2: a slot overflowed (or P > n - P) -- run
+    auc_eval_counts_part instead."""
+    L, dev, lc, n, st, ws = _eval_args(scores, labels)
+    nb = auc_slot_bytes(n, parts)
+    if (slots.dtype != torch.uint8 or slots.numel() < nb * int(parts) or not slots.is_contiguous()
+            or slots.device != dev or slots.data_ptr() % 256):
+        raise ValueError("slots must be the contiguous, 256-byte aligned uint8 gather of every rank's slot")
+    if out is None:
+        out = torch.empty(8, dtype=torch.int64, device=dev)
+    elif out.dtype != torch.int64 or out.numel() < 8 or not out.is_contiguous() or out.device != dev:
+        raise ValueError("out must be a contiguous int64 tensor of >= 8 elements on the scores' device")
+    check(L.dauc_auc_eval_query_part_sorted(scores.data_ptr(), labels.data_ptr(), lc, n, int(part), int(parts),
+                                            slots.data_ptr(), int(P), out.data_ptr(), ws.data_ptr(), ws.numel(), st),
+          "dauc_auc_eval_query_part_sorted")
+    return out
+
+
 def auc_eval_counts_part(scores: torch.Tensor, labels: torch.Tensor, part: int, parts: int,
                          part_counts: torch.Tensor) -> tuple:
     """Part `part` of `parts` of the blocking evaluation (dauc_auc_eval_counts_part): every part
@@ -794,4 +816,5 @@ __all__ = [
     "auc_slot_bytes",
     "auc_eval_compact_part",
     "auc_eval_query_part",
+    "auc_eval_query_part_sorted",
 ]

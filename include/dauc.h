@@ -340,7 +340,15 @@ int dauc_auc_eval_counts_part(const float* scores, const void* labels, int label
  *      high 32 bits = the number of slots built for another n (parts <= 1024). A slot holds an
  *      even share of the count index's capacity + 25 %:
  *      a slice with more positives (an unshuffled test set), like a table the index cannot hold,
- *      gives verdict 2 -- the caller then runs dauc_auc_eval_counts_part on every rank.
+ *      gives verdict 2 -- the caller then runs dauc_auc_eval_query_part_sorted on every rank, and
+ *      where that reports verdict 2 too, dauc_auc_eval_counts_part.
+ *   dauc_auc_eval_query_part_sorted (verdict-2 path, after the caller has read the records): the
+ *      gathered slots' positives (P of them, the records' word 3) are copied into one table, which
+ *      is sorted and searched (the distinct-key index for tie-heavy tables, else the LDS tree), and
+ *      THIS rank's own slice of the scores is counted into part_out (zeroed first): {W_part,
+ *      T_part, #non-finite queried scores, P, 0, 0, 0, verdict}; verdict 2 when a slot overflowed,
+ *      the slots do not hold P positives, or P > n - P -- then dauc_auc_eval_counts_part. No host
+ *      synchronisation; the same workspace, slots and alignment rules as step 2.
  * Replaces the reference's rank-0 evaluation (main.py:232-250) with a sharded one.
  */
 size_t dauc_auc_slot_bytes(int64_t n, int parts);
@@ -349,6 +357,9 @@ int dauc_auc_eval_compact_part(const float* scores, const void* labels, int labe
 int dauc_auc_eval_query_part(const float* scores, const void* labels, int label_dtype, int64_t n, int part, int parts,
                              const void* slots, int64_t* part_out, void* workspace, size_t workspace_bytes,
                              dauc_stream_t stream);
+int dauc_auc_eval_query_part_sorted(const float* scores, const void* labels, int label_dtype, int64_t n, int part,
+                                    int parts, const void* slots, int64_t P, int64_t* part_out, void* workspace,
+                                    size_t workspace_bytes, dauc_stream_t stream);
 
 /* The radix sort alone: keys_out[0..n) = ascending order-preserving keys of scores (testing). */
 int dauc_sort_keys(const float* scores, int64_t n, unsigned* keys_out, void* workspace,

@@ -102,6 +102,11 @@ def _sharded_worker(rank, world, port, q):
         y5 = torch.where(torch.arange(1 << 24, device=dev) < 200_000, 1, -1).to(torch.int8)
         e5 = coracle.auc_counts(y5.cpu().numpy().astype(np.int64), s)
         assert auc(y5, ts) == _area(e5)
+        # tie-heavy scores (bf16-rounded): verdict 2, then dauc_auc_eval_query_part_sorted over the
+        # gathered slots on both ranks (the distinct-key index), the oracle's integers
+        tb = ts.bfloat16().float()
+        eb = coracle.auc_counts(y, tb.cpu().numpy())
+        assert auc(ty, tb) == _area(eb)
         assert auc(ty, ts) == _area(e)  # the group is still usable
         dist.destroy_process_group()
         q.put((rank, None))
@@ -113,7 +118,8 @@ def _sharded_worker(rank, world, port, q):
 def test_integration_stub_sharded_two_gloo_ranks_2e24():
     """INTEGRATION.md §2's AUC_sharded, verbatim, as 2 processes on cuda:0 over gloo at 2^24 scores
     and 1 % positives (configs[3]): the oracle's counts; multi-valued labels as sklearn; differing
-    labels, lengths and a non-finite score raise on both ranks; the verdict-2 sorted path."""
+    labels, lengths and a non-finite score raise on both ranks; the verdict-2 paths (tie-heavy
+    scores through the sorted two-step fallback, an unshuffled set through the whole-vector one)."""
     import torch.multiprocessing as mp
 
     world = 2

@@ -104,6 +104,68 @@ def test_two_step_unshuffled_overflow_2e24(dev):
     assert _sorted_parts(dev, ts, ty, G) == (e["wins"], e["ties"])
 
 
+def _gathered(dev, ts, ty, G):
+    """The G slots side by side (the all-gather) and every part's step-2 record."""
+    from distributedauc_amd import ops
+
+    n = ts.numel()
+    nb = ops.auc_slot_bytes(n, G)
+    slots = torch.empty(nb * G, dtype=torch.uint8, device=dev)
+    for r in range(G):
+        ops.auc_eval_compact_part(ts, ty, r, G, slots[r * nb:(r + 1) * nb])
+    return slots, [_query(dev, ts, ty, r, G, slots) for r in range(G)]
+
+
+def _sorted_fallback(dev, ts, ty, G, slots, P):
+    """Every part's dauc_auc_eval_query_part_sorted record."""
+    from distributedauc_amd import ops
+
+    return [ops.auc_eval_query_part_sorted(ts, ty, r, G, slots, P).cpu().tolist() for r in range(G)]
+
+
+@pytest.mark.parametrize("G", [2, 8])
+@pytest.mark.timeout(300)
+def test_two_step_sorted_fallback_tie_heavy(dev, G):
+    """configs[3]'s scores rounded to bf16 (1,377 distinct positive values: the slotted index
+    refuses the table, verdict 2 on every part): dauc_auc_eval_query_part_sorted sorts the gathered
+    slots' positives and counts each part's own slice through the distinct-key index -- verdict 1
+    everywhere, the parts' (W, T) sum to the oracle's, no whole-vector compaction."""
+    from distributedauc_amd.loader import synthetic_scores
+
+    ts, ty = synthetic_scores(1 << 24, 0.01, dev)
+    ts = ts.bfloat16().float()
+    e = _oracle(ts, ty)
+    slots, recs = _gathered(dev, ts, ty, G)
+    assert {(v[3], v[7]) for v in recs} == {(e["P"], 2)}, recs
+    got = _sorted_fallback(dev, ts, ty, G, slots, e["P"])
+    assert {(v[2], v[3], v[7]) for v in got} == {(0, e["P"], 1)}, got
+    assert (sum(v[0] for v in got), sum(v[1] for v in got)) == (e["wins"], e["ties"])
+
+
+@pytest.mark.timeout(300)
+def test_two_step_sorted_fallback_refuses_what_slots_cannot_serve(dev):
+    """The sorted two-step fallback reports verdict 2 (the caller's whole-vector path) when a slot
+    overflowed (an unshuffled test set), when P exceeds the slots' total, and when the positives are
+    the larger class."""
+    from distributedauc_amd.loader import synthetic_scores
+
+    G = 8
+    ts, _ = synthetic_scores(1 << 22, 0.01, dev)
+    P = (1 << 22) // 20
+    ty = torch.where(torch.arange(1 << 22, device=dev) < P, 1, -1).to(torch.int8)
+    slots, _ = _gathered(dev, ts, ty, G)
+    assert {v[7] for v in _sorted_fallback(dev, ts, ty, G, slots, P)} == {2}
+    ts2, ty2 = synthetic_scores(1 << 20, 0.01, dev, seed=5)
+    e2 = _oracle(ts2, ty2)
+    slots2, _ = _gathered(dev, ts2, ty2, G)
+    assert {v[7] for v in _sorted_fallback(dev, ts2, ty2, G, slots2, e2["P"] + 1)} == {2}
+    assert {v[7] for v in _sorted_fallback(dev, ts2, ty2, G, slots2, e2["P"])} == {1}
+    ts3, ty3 = synthetic_scores(400_000, 0.55, dev, seed=99)
+    e3 = _oracle(ts3, ty3)
+    slots3, _ = _gathered(dev, ts3, ty3, G)
+    assert {v[7] for v in _sorted_fallback(dev, ts3, ty3, G, slots3, e3["P"])} == {2}
+
+
 @pytest.mark.parametrize("n,p", [(400_000, 0.55), (1 << 19, 0.45)])
 @pytest.mark.timeout(300)
 def test_two_step_table_past_index_capacity(dev, n, p):
@@ -187,6 +249,12 @@ def _rank_worker(rank, world, port, q):
         with pytest.raises(RuntimeError, match="different lengths"):
             ExactAUC(world=world, rank=rank, shard_min=0).counts(ty[:m], ts[:m])
         assert ev.counts(ty, ts) == c  # the group is still usable
+        # tie-heavy scores (bf16-rounded): verdict 2, then the sorted two-step fallback over the
+        # gathered slots (the distinct-key index) on both ranks
+        tb = ts.bfloat16().float()
+        eb = _oracle(tb, ty)
+        cb = ev.counts(ty, tb)
+        assert (cb["wins"], cb["ties"], cb["P"], cb["N"]) == (eb["wins"], eb["ties"], eb["P"], eb["N"]), (cb, eb)
         dist.destroy_process_group()
         q.put((rank, None))
     except BaseException:
