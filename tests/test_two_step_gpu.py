@@ -185,7 +185,8 @@ def test_two_step_table_past_index_capacity(dev, n, p):
 
 def test_two_step_rejects_overlapping_buffers(dev):
     """a record inside the evaluation workspace or the gathered slots is refused
-    (DAUC_EINVAL) instead of being zeroed or overwritten mid-evaluation."""
+    (DAUC_EINVAL) instead of being zeroed or overwritten mid-evaluation (step 2 and the sorted slot
+    fallback alike; the fallback also refuses P < 1)."""
     from distributedauc_amd import _lib, ops
 
     n, G = 100_003, 2
@@ -205,6 +206,13 @@ def test_two_step_rejects_overlapping_buffers(dev):
         ops.auc_eval_query_part(ts, ty, 0, G, slots, out=slots[256:320].view(torch.int64))
     with pytest.raises(_lib.DaucError):
         ops.auc_eval_enqueue(ts, ty, 0, G, out=ws[2048:2112].view(torch.int64))
+    # the sorted slot fallback: the same rules, and a table of at least one positive
+    with pytest.raises(_lib.DaucError):
+        ops.auc_eval_query_part_sorted(ts, ty, 0, G, slots, 100, out=ws[1024:1088].view(torch.int64))
+    with pytest.raises(_lib.DaucError):
+        ops.auc_eval_query_part_sorted(ts, ty, 0, G, slots, 100, out=slots[256:320].view(torch.int64))
+    with pytest.raises(_lib.DaucError):
+        ops.auc_eval_query_part_sorted(ts, ty, 0, G, slots, 0)
     # the slots are untouched by the refused calls: the evaluation still gives the oracle's counts
     e = _oracle(ts, ty)
     recs = [_query(dev, ts, ty, r, G, slots) for r in range(G)]
