@@ -2171,23 +2171,67 @@ __global__ __launch_bounds__(kCiPlanThreads) void dk_index_kernel(const unsigned
     }
 }
 
+// Two LDS layouts of the index; the kernel built for the other one returns at once. Up to
+// kDkSmall distinct keys (4 cells each) a cell word is 8 bytes {the cum before the cell, its first
+// distinct key | its count << 16}: a query reads its cell word and, in a cell that holds keys, the
+// cell's first {key, cum} -- 2 random LDS reads. Past it, to kDkMax, a cell word is 16 bits {first
+// distinct key (14 bits), count saturated at 3} and a query reads the two entries at the cell's
+// start -- 3 random reads. (The pass is bound by the LDS bank conflicts of those reads.)
+constexpr int kDkSmall = 3200;
+constexpr int kDkSmallCells = 4 * kDkSmall + kCiTop;
+
+// the query kernels' LDS: l1, then {0, 0}, {key, cum} of every distinct key, {+inf, M} (read, never
+// counted, past the last), then the cell words
+template <bool SMALL>
+struct DkLds {
+    uint2* l1;
+    uint2* kc;
+    std::conditional_t<SMALL, uint2*, unsigned short*> cw;
+};
+template <bool SMALL>
+__device__ __forceinline__ DkLds<SMALL> dk_load_lds(uint2* lds, const DkWs& dk, int64_t M) {
+    constexpr int kMax = SMALL ? kDkSmall : kDkMax;
+    using CW = std::conditional_t<SMALL, uint2*, unsigned short*>;
+    DkLds<SMALL> r{lds, lds + kCiTop, reinterpret_cast<CW>(lds + kCiTop + kMax + 2)};
+    const unsigned D = dk.meta[kDkD], cells = dk.meta[kCiCells];
+    for (int i = threadIdx.x; i < kCiTop; i += blockDim.x) r.l1[i] = dk.l1[i];
+    for (unsigned i = threadIdx.x; i < D + 2; i += blockDim.x)
+        r.kc[i] = i == 0 ? uint2{0u, 0u}
+                         : (i <= D ? uint2{dk.kd[i - 1], dk.cd[i - 1]} : uint2{kPadKey, static_cast<unsigned>(M)});
+    for (unsigned c = threadIdx.x; c <= cells + (SMALL ? 0u : 1u); c += blockDim.x) {
+        const unsigned a = dk.cstart[c], n = c <= cells ? dk.cstart[c + 1] - a : 0u;
+        if constexpr (SMALL)
+            r.cw[c] = uint2{a ? dk.cd[a - 1] : 0u, a | (n << 16)};
+        else
+            r.cw[c] = static_cast<unsigned short>(a | (min(n, 3u) << 14));
+    }
+    __syncthreads();
+    return r;
+}
+
 // NQ queries of one lane: W += M - #(table <= x), T += #(table == x) for the queries in `use`
 // (TABLE_POS false: the table is the negatives and the queries positives, W += #(table < x))
-template <int NQ, bool TABLE_POS = true>
-__device__ __forceinline__ void dk_count(const unsigned (&x)[NQ], unsigned use, const uint2* l1,
-                                         const unsigned short* st, const uint2* kc, unsigned long long M,
-                                         unsigned long long& w, unsigned long long& t) {
-    unsigned s0[NQ], n[NQ];
+template <int NQ, bool TABLE_POS = true, bool SMALL = false>
+__device__ __forceinline__ void dk_count(const unsigned (&x)[NQ], unsigned use, const DkLds<SMALL>& ld,
+                                         unsigned long long M, unsigned long long& w, unsigned long long& t) {
+    const uint2* kc = ld.kc;
+    unsigned s0[NQ], n[NQ], cb[NQ], c[NQ];  // cb: the cum before s0 (SMALL)
     uint2 e[NQ];
 #pragma unroll
-    for (int q = 0; q < NQ; ++q) e[q] = l1[x[q] >> kCiLowBits];
-unsigned c[NQ];
+    for (int q = 0; q < NQ; ++q) e[q] = ld.l1[x[q] >> kCiLowBits];
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
         c[q] = ci_cell(x[q], e[q]);
-        const unsigned v = st[c[q]];
-        s0[q] = v & 0x3fffu;
-        n[q] = v >> 14;
+        if constexpr (SMALL) {
+            const uint2 v = ld.cw[c[q]];
+            cb[q] = v.x;
+            s0[q] = v.y & 0xffffu;
+            n[q] = v.y >> 16;
+        } else {
+            const unsigned v = ld.cw[c[q]];
+            s0[q] = v & 0x3fffu;
+            n[q] = v >> 14;
+        }
     }
     bool many = false;
 #pragma unroll
@@ -2196,7 +2240,8 @@ unsigned c[NQ];
 #pragma unroll
         for (int q = 0; q < NQ; ++q) {
             if (n[q] > 1u) {
-                unsigned lo = s0[q], cnt = n[q] < 3u ? n[q] : (st[c[q] + 1] & 0x3fffu) - s0[q];
+                unsigned lo = s0[q], cnt = n[q];
+                if constexpr (!SMALL) cnt = n[q] < 3u ? n[q] : (ld.cw[c[q] + 1] & 0x3fffu) - s0[q];
                 while (cnt > 0u) {
                     const unsigned h = cnt >> 1;
                     if (kc[lo + h + 1].x <= x[q]) {
@@ -2205,6 +2250,9 @@ unsigned c[NQ];
                     } else {
                         cnt = h;
                     }
+                }
+                if constexpr (SMALL) {  // the cum before the last key <= x, when that is not the cell's first
+                    if (lo > s0[q] + 1) cb[q] = kc[lo - 1].y;
                 }
                 n[q] = lo > s0[q] ? 1u : 0u;
                 s0[q] = lo > s0[q] ? lo - 1 : s0[q];
@@ -2215,8 +2263,14 @@ unsigned c[NQ];
     uint2 a[NQ], b[NQ];
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
-        a[q] = kc[s0[q]];
-        b[q] = kc[s0[q] + 1];
+        if constexpr (SMALL) {
+            a[q] = uint2{0u, cb[q]};
+            b[q] = uint2{kPadKey, 0u};
+            if (n[q]) b[q] = kc[s0[q] + 1];  // only the lanes whose cell holds keys read it
+        } else {
+            a[q] = kc[s0[q]];
+            b[q] = kc[s0[q] + 1];
+        }
     }
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
@@ -2229,31 +2283,6 @@ unsigned c[NQ];
             t += le - lt;
         }
     }
-}
-
-// The labeled query pass over the distinct-key index (the stream and checks of query_labeled_kernel);
-// returns at once unless the count index is not in use and the distinct-key index is
-// the query kernels' LDS: l1, then {0, 0}, {key, cum} of every distinct key, {+inf, M} (read, never
-// counted, past the last), then per cell 16 bits: its first distinct key (14 bits) and how many it
-// holds, saturated at 3 (the next cell's first key then gives the count: rare)
-struct DkLds {
-    uint2* l1;
-    uint2* kc;
-    unsigned short* st;
-};
-__device__ __forceinline__ DkLds dk_load_lds(uint2* lds, const DkWs& dk, int64_t M) {
-    DkLds r{lds, lds + kCiTop, reinterpret_cast<unsigned short*>(lds + kCiTop + kDkMax + 2)};
-    const unsigned D = dk.meta[kDkD], cells = dk.meta[kCiCells];
-    for (int i = threadIdx.x; i < kCiTop; i += blockDim.x) r.l1[i] = dk.l1[i];
-    for (unsigned i = threadIdx.x; i < D + 2; i += blockDim.x)
-        r.kc[i] = i == 0 ? uint2{0u, 0u}
-                         : (i <= D ? uint2{dk.kd[i - 1], dk.cd[i - 1]} : uint2{kPadKey, static_cast<unsigned>(M)});
-    for (unsigned c = threadIdx.x; c <= cells + 1; c += blockDim.x) {
-        const unsigned a = dk.cstart[c], n = c <= cells ? dk.cstart[c + 1] - a : 0u;
-        r.st[c] = static_cast<unsigned short>(a | (min(n, 3u) << 14));
-    }
-    __syncthreads();
-    return r;
 }
 
 // the block's W, T (and non-finite count) into out[0..1] (and *nonfinite)
@@ -2286,12 +2315,12 @@ __device__ __forceinline__ void dk_reduce(unsigned long long w, unsigned long lo
 
 // dauc_auc_counts_sorted's form: every element of q[0, L) is a query (no labels); the table is the
 // positives (TABLE_POS) or the negatives
-template <bool TABLE_POS>
+template <bool TABLE_POS, bool SMALL>
 __global__ __launch_bounds__(kQueryThreads) void dk_plain_kernel(const float* __restrict__ q, int64_t L, DkWs dk,
                                                                  int64_t M, unsigned long long* __restrict__ out) {
-    if (dk.meta[kDkUse] == 0u) return;
+    if (dk.meta[kDkUse] == 0u || (dk.meta[kDkD] <= unsigned(kDkSmall)) != SMALL) return;
     extern __shared__ uint2 dk_lds[];
-    const DkLds ld = dk_load_lds(dk_lds, dk, M);
+    const DkLds<SMALL> ld = dk_load_lds<SMALL>(dk_lds, dk, M);
     const unsigned long long MM = static_cast<unsigned long long>(M);
     unsigned long long w = 0, t = 0;
     const bool vec = (reinterpret_cast<uintptr_t>(q) & 15u) == 0;
@@ -2320,30 +2349,29 @@ __global__ __launch_bounds__(kQueryThreads) void dk_plain_kernel(const float* __
 #pragma unroll
                 for (int j = 0; j < 4; ++j) x[4 * u + j] = key_fast(f[j]);
             }
-            dk_count<NQ, TABLE_POS>(x, use, ld.l1, ld.st, ld.kc, MM, w, t);
+            dk_count<NQ, TABLE_POS, SMALL>(x, use, ld, MM, w, t);
 #pragma unroll
             for (int u = 0; u < U; ++u) fc[u] = fn[u];
         }
     }
     for (int64_t i = nvec * 4 + tid; i < L; i += stride) {
         const unsigned x[1] = {key_fast(q[i])};
-        dk_count<1, TABLE_POS>(x, 1u, ld.l1, ld.st, ld.kc, MM, w, t);
+        dk_count<1, TABLE_POS, SMALL>(x, 1u, ld, MM, w, t);
     }
     dk_reduce(w, t, 0u, out, nullptr);
 }
 
-template <typename LT, int U = 2>
+// The labeled query pass over the distinct-key index (the stream and checks of query_labeled_kernel);
+// returns at once unless the count index is not in use and the distinct-key index is, in this layout
+template <typename LT, bool SMALL, int U = 2>
 __global__ __launch_bounds__(kQueryThreads) void dk_query_kernel(const float* __restrict__ s, const LT* __restrict__ lab,
                                                                  int64_t begin, int64_t end,
                                                                  const unsigned* __restrict__ ci_meta, DkWs dk,
                                                                  int64_t M, unsigned long long* __restrict__ out,
                                                                  unsigned long long* __restrict__ nonfinite) {
-    if (dk_ci_in_use(ci_meta) || dk.meta[kDkUse] == 0u) return;
+    if (dk_ci_in_use(ci_meta) || dk.meta[kDkUse] == 0u || (dk.meta[kDkD] <= unsigned(kDkSmall)) != SMALL) return;
     extern __shared__ uint2 dk_lds[];
-    const DkLds ld = dk_load_lds(dk_lds, dk, M);
-    const uint2* l1 = ld.l1;
-    const uint2* kc = ld.kc;
-    const unsigned short* st = ld.st;
+    const DkLds<SMALL> ld = dk_load_lds<SMALL>(dk_lds, dk, M);
     const unsigned long long MM = static_cast<unsigned long long>(M);
     unsigned long long w = 0, t = 0;
     unsigned nf = 0;
@@ -2352,7 +2380,7 @@ __global__ __launch_bounds__(kQueryThreads) void dk_query_kernel(const float* __
             const float f = s[i];
             nf += !isfinite(f);
             const unsigned x[1] = {key_fast(f)};
-            dk_count<1>(x, 1u, l1, st, kc, MM, w, t);
+            dk_count<1, true, SMALL>(x, 1u, ld, MM, w, t);
         }
     };
     const int64_t a0 = (begin + 3) & ~int64_t(3);
@@ -2393,7 +2421,7 @@ __global__ __launch_bounds__(kQueryThreads) void dk_query_kernel(const float* __
                     nf += neg && !isfinite(f[q]);
                 }
             }
-            dk_count<NQ>(x, use, l1, st, kc, MM, w, t);
+            dk_count<NQ, true, SMALL>(x, use, ld, MM, w, t);
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 fc[u] = fn[u];
@@ -2407,7 +2435,9 @@ __global__ __launch_bounds__(kQueryThreads) void dk_query_kernel(const float* __
     dk_reduce(w, t, nf, out, nonfinite);
 }
 constexpr size_t kDkQueryLds = (size_t(kCiTop) + kDkMax + 2) * 8 + (size_t(kDkMaxCells) + 2) * 2;
+constexpr size_t kDkQueryLdsSmall = (size_t(kCiTop) + kDkSmall + 2) * 8 + (size_t(kDkSmallCells) + 1) * 8;
 static_assert(kDkQueryLds + 3 * (kQueryThreads / kWave) * 8 <= 160 * 1024, "the distinct-key query's LDS");
+static_assert(kDkQueryLdsSmall + 3 * (kQueryThreads / kWave) * 8 <= 160 * 1024, "the distinct-key query's LDS");
 
 int query_grid(int64_t L) {
     static int cus = 0;
@@ -2659,16 +2689,23 @@ int prepare_dk(const unsigned* sorted, int64_t M, const unsigned* ci_meta, const
 
 template <bool TABLE_POS>
 int launch_dk_plain(const float* q, int64_t L, const DkWs& dk, int64_t M, unsigned long long* out, hipStream_t st) {
-    hipLaunchKernelGGL((dk_plain_kernel<TABLE_POS>), dim3(query_grid(L)), dim3(kQueryThreads), kDkQueryLds, st, q, L,
-                       dk, M, out);
+    // both layouts enqueued: the one the device's distinct count does not select returns at once
+    hipLaunchKernelGGL((dk_plain_kernel<TABLE_POS, true>), dim3(query_grid(L)), dim3(kQueryThreads), kDkQueryLdsSmall,
+                       st, q, L, dk, M, out);
+    hipLaunchKernelGGL((dk_plain_kernel<TABLE_POS, false>), dim3(query_grid(L)), dim3(kQueryThreads), kDkQueryLds, st,
+                       q, L, dk, M, out);
     return launch_status();
 }
 
 template <typename LT>
 int launch_dk(const float* s, const LT* lab, int64_t begin, int64_t end, const unsigned* ci_meta, const DkWs& dk,
               int64_t M, unsigned long long* out, unsigned long long* nonfinite, hipStream_t st) {
-    hipLaunchKernelGGL((dk_query_kernel<LT>), dim3(query_grid(end - begin)), dim3(kQueryThreads), kDkQueryLds, st, s,
-                       lab, begin, end, ci_meta, dk, M, out, nonfinite);
+    // both layouts enqueued: the one the device's distinct count does not select returns at once
+    const dim3 grid(query_grid(end - begin));
+    hipLaunchKernelGGL((dk_query_kernel<LT, true>), grid, dim3(kQueryThreads), kDkQueryLdsSmall, st, s, lab, begin,
+                       end, ci_meta, dk, M, out, nonfinite);
+    hipLaunchKernelGGL((dk_query_kernel<LT, false>), grid, dim3(kQueryThreads), kDkQueryLds, st, s, lab, begin, end,
+                       ci_meta, dk, M, out, nonfinite);
     return launch_status();
 }
 

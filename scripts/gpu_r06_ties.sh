@@ -3,7 +3,7 @@
 # the one-call timings per score distribution, and a kernel trace of the bf16-rounded 2^27 case
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-O=${O:-gpurun_out/r06ties7}
+O=${O:-gpurun_out/r06ties8}
 mkdir -p $O
 timeout -k 10 500 python -u -m pytest -x -v --timeout 120 --timeout-method thread -m gpu \
   tests/test_auc_ties_gpu.py tests/test_auc_cells_gpu.py tests/test_kernels_gpu.py tests/test_two_step_gpu.py > $O/tests.log 2>&1 &&

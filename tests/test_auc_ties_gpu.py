@@ -128,7 +128,7 @@ def test_distinct_index_label_widths(dev, ops, dtype):
     _check(ops, dev, s, y.astype(dtype), 1, 299_999, what=str(dtype) + " ragged")
 
 
-@pytest.mark.parametrize("D", [1, 2, 8192, 13_999, 14_000, 14_001, 20_000])
+@pytest.mark.parametrize("D", [1, 2, 3_200, 3_201, 8192, 13_999, 14_000, 14_001, 20_000])
 def test_distinct_index_capacity(dev, ops, D):
     """Exactly D distinct positive values, 16 copies each (a cell of the count index holds 15+:
     refused), queries on, between, below and above them. Up to 14,000 the distinct-key index holds
