@@ -116,3 +116,15 @@ def test_step_roofline_helpers():
     assert bench.bn_backward_bytes(bwd) == (3 * act + act // 16) + 3 * act
     bwd[11] = vp(0)  # no residual: both passes read dy + mask + x, the second writes dx
     assert bench.bn_backward_bytes(bwd) == 2 * (2 * act + act // 16) + act
+
+
+def test_cpu_baselines_at_one_gpu_only():
+    """The bench contract times the CPU baselines on rank 0 at N = 1 only; --cpu-baseline-any-n
+    keeps them for rehearsals, --no-cpu-baseline drops them everywhere."""
+    b = _bench()
+    assert b.cpu_baseline_on(b.parse([]), 1)
+    assert not b.cpu_baseline_on(b.parse([]), 2)
+    assert not b.cpu_baseline_on(b.parse([]), 8)
+    assert b.cpu_baseline_on(b.parse(["--cpu-baseline-any-n"]), 8)
+    assert not b.cpu_baseline_on(b.parse(["--no-cpu-baseline"]), 1)
+    assert not b.cpu_baseline_on(b.parse(["--no-cpu-baseline", "--cpu-baseline-any-n"]), 4)
