@@ -940,8 +940,9 @@ int compact_unordered(const float* scores, const void* labels, int label_dtype, 
     const int threads = wide ? kWideThreads : kCmpThreads;
     int slots = wide ? 32 : kCmpSlots;
 #ifdef DAUC_TUNING
-    // tuning builds: DAUC_CMP_SLOTS (8, 16, 32) = label groups per thread whatever n
-    if (const char* e = getenv("DAUC_CMP_SLOTS"); e && (atoi(e) == 8 || atoi(e) == 16 || atoi(e) == 32))
+    // tuning builds: DAUC_CMP_SLOTS (8, 16, 32, 64) = label groups per thread whatever n
+    if (const char* e = getenv("DAUC_CMP_SLOTS");
+        e && (atoi(e) == 8 || atoi(e) == 16 || atoi(e) == 32 || atoi(e) == 64))
         slots = atoi(e);
 #endif
     const int64_t tile = int64_t(threads) * 16 * slots;
@@ -967,6 +968,17 @@ int compact_unordered(const float* scores, const void* labels, int label_dtype, 
     auto go = [&](auto* lab) {
         using LT = std::remove_const_t<std::remove_pointer_t<decltype(lab)>>;
 #ifdef DAUC_TUNING
+        if (slots == 64) {
+            if (hist_out != nullptr)
+                hipLaunchKernelGGL((compact_unordered_kernel<LT, 64, kCmpThreads, true>), grid, block, 0, st, scores,
+                                   lab, n, vec, pos_out, stats, tag, zero_next, next_tag, zero3, zero_w, nzero_w, cap,
+                                   hist_out, put, put_val, fw, nfill, nblk);
+            else
+                hipLaunchKernelGGL((compact_unordered_kernel<LT, 64, kCmpThreads>), grid, block, 0, st, scores, lab, n,
+                                   vec, pos_out, stats, tag, zero_next, next_tag, zero3, zero_w, nzero_w, cap, hist_out,
+                                   put, put_val, fw, nfill, nblk);
+            return launch_status();
+        }
         if (slots == 16) {
             if (hist_out != nullptr)
                 hipLaunchKernelGGL((compact_unordered_kernel<LT, 16, kCmpThreads, true>), grid, block, 0, st, scores,

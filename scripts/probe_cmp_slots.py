@@ -1,5 +1,5 @@
 """The unordered compaction's tile size (tuning build, DAUC_CMP_SLOTS: label groups of 16 per thread
-of a 256-thread workgroup, 8 / 16 / 32; the product takes 32 from 2^25 labels, else 8): one rank's
+of a 256-thread workgroup, 8 / 16 / 32 / 64; the product takes 32 from 2^25 labels, else 8): one rank's
 step 1 at G = 8 (dauc_auc_eval_compact_part over a 2^21 / 2^24-label slice) and the one-call
 evaluation (enqueue) at 2^24 @ 1 % and 2^27 @ 0.1 %, HIP events around `reps` back-to-back calls,
 the sizes interleaved three times; the one-call counts checked against the product's.
@@ -45,7 +45,7 @@ with _lib.using(_lib.tuning()):
         mine = torch.empty(nb, dtype=torch.uint8, device=dev)
         rec = torch.zeros(8, dtype=torch.int64, device=dev)
         for rep in range(3):
-            for sl in ("0", "8", "16", "32"):
+            for sl in ("0", "8", "16", "32", "64"):
                 os.environ["DAUC_CMP_SLOTS"] = sl
                 ops.auc_eval_enqueue(s, y, 0, 1, out=rec)
                 ok = tuple(rec.tolist()[:2]) == whole[:2]
