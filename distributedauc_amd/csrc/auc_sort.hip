@@ -947,7 +947,8 @@ __device__ __forceinline__ void slot_tertiary(unsigned x, unsigned c, unsigned c
 #ifdef DAUC_TUNING
 // tuning builds: DAUC_QUERY_ABL (timing ablations of the SLOT query pass; WRONG counts): 1 = no
 // query loop (the prologue and the reduction only), 2 = the block words zeroed instead of loaded
-// and converted (every cell empty: the loop's windows all read the +inf pad window)
+// and converted (every cell empty: the loop's windows all read the +inf pad window), 3 = no
+// end-of-kernel atomics, 4 = 1 + 3 (the prologue only)
 __device__ int g_query_abl = 0;
 #endif
 // SEC (SLOT only; round 6): ONE secondary window per lane per group of 4 queries instead of one per
@@ -967,7 +968,8 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
                                                                 unsigned* __restrict__ verdict,
                                                                 const unsigned* __restrict__ grp,
                                                                 const unsigned long long* __restrict__ Mp,
-                                                                unsigned* __restrict__ check, unsigned slot_cells = 0u) {
+                                                                unsigned* __restrict__ check, unsigned slot_cells = 0u,
+                                                                unsigned long long* __restrict__ red8 = nullptr) {
     const unsigned pad_word = 4u * slot_cells;  // SLOT: the all-+inf primary slot past the last cell
     const bool in_use = count_index_in_use(meta);
     if (Mp != nullptr) M = static_cast<int64_t>(*Mp);  // the direct build: the table size on the device
@@ -1093,7 +1095,7 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
     unsigned long long w = 0, t = 0;
     unsigned nf = 0;  // CHECK: + #queries << 16
 #ifdef DAUC_TUNING
-    if (SLOT && g_query_abl == 1) end = begin;  // no queries: the prologue and the reduction only
+    if (SLOT && (g_query_abl == 1 || g_query_abl == 4)) end = begin;  // no queries: the prologue (+ reduction)
 #endif
     const int64_t a0 = (begin + 3) & ~int64_t(3);
     const int64_t head = a0 < end ? a0 : end;
@@ -1408,6 +1410,9 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
         if constexpr (CHECK) red[CHECK ? 3 : 0][wid] = ckw;
     }
     __syncthreads();
+#ifdef DAUC_TUNING
+    if (SLOT && g_query_abl >= 3) return;  // no end-of-kernel atomics
+#endif
     if (threadIdx.x == 0) {
         unsigned long long bw = 0, bt = 0, bn = 0, bc = 0;
         for (int i = 0; i < kQueryThreads / kWave; ++i) {
@@ -1416,10 +1421,41 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
             bn += red[2][i];
             if constexpr (CHECK) bc += red[CHECK ? 3 : 0][i];
         }
-        if (bw) atomicAdd(out + 0, bw);
-        if (bt) atomicAdd(out + 1, bt);
-        if (bn && nonfinite) atomicAdd(nonfinite, bn);
-        if (CHECK && bc) atomicAdd(check, static_cast<unsigned>(bc));
+        if (red8 == nullptr) {
+            if (bw) atomicAdd(out + 0, bw);
+            if (bt) atomicAdd(out + 1, bt);
+            if (bn && nonfinite) atomicAdd(nonfinite, bn);
+            if (CHECK && bc) atomicAdd(check, static_cast<unsigned>(bc));
+        } else {
+            // round 6 (the two-step's query pass): its workgroups finish together, and 3-4 atomics
+            // each on the record's one line serialise (~8 us at 256 workgroups and 2^21 queries,
+            // DAUC_QUERY_ABL 3; the one-call pass, 8x the queries per workgroup, measured 1 us
+            // slower with the groups and keeps the plain atomics). Group g = blockIdx % 8 adds into
+            // its own line of red8 (256 B apart; zeroed by the count pass before this launch), takes
+            // the group's ticket after its adds are acknowledged, and the group's last arriver adds
+            // the group's sums to the record: <= 8 atomics per record word, 8 chains in parallel
+            const unsigned g = blockIdx.x & 7u;
+            unsigned long long* L = red8 + 32u * g;
+            if (bw) atomicAdd(L + 0, bw);
+            if (bt) atomicAdd(L + 1, bt);
+            if (bn) atomicAdd(L + 2, bn);
+            if (CHECK && bc) atomicAdd(L + 3, bc);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const unsigned members = (gridDim.x - g + 7u) / 8u;
+            const unsigned tk = __hip_atomic_fetch_add(reinterpret_cast<unsigned*>(L + 4), 1u, __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT);
+            if (tk == members - 1u) {
+                const unsigned long long gw = __hip_atomic_load(L + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const unsigned long long gt = __hip_atomic_load(L + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const unsigned long long gn = __hip_atomic_load(L + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const unsigned long long gc =
+                    CHECK ? __hip_atomic_load(L + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+                if (gw) atomicAdd(out + 0, gw);
+                if (gt) atomicAdd(out + 1, gt);
+                if (gn && nonfinite) atomicAdd(nonfinite, gn);
+                if (CHECK && gc) atomicAdd(check, static_cast<unsigned>(gc));
+            }
+        }
     }
 }
 
@@ -1546,6 +1582,10 @@ __global__ __launch_bounds__(kDirectThreads) void direct_count_kernel(const floa
     const bool ok = num > 0 && 3 * num >= 2 * M && total <= static_cast<unsigned>(kCiMaxCells) && M <= mcap;
     if (blockIdx.x == 0) {
         for (int t = threadIdx.x; t < kCiTop; t += kDirectThreads) l1g[t] = l1[t];
+        // SLOT: `cell` is unused as such; it holds the query pass's 8 group lines (query_ci_kernel's
+        // red8: 2 KB), zeroed here, before that launch
+        if (SLOT && cell != nullptr && threadIdx.x < 256)
+            reinterpret_cast<unsigned long long*>(cell)[threadIdx.x] = 0ull;
         if (threadIdx.x == 0) {
             meta[kCiOk] = ok ? 1u : 0u;
             meta[kCiCells] = total;
@@ -1735,6 +1775,9 @@ __global__ __launch_bounds__(kSlotCountThreads) void direct_count_slots_kernel(S
     if (blockIdx.x == 0) {
         l1g[2 * threadIdx.x] = l1[2 * threadIdx.x];
         l1g[2 * threadIdx.x + 1] = l1[2 * threadIdx.x + 1];
+        // SLOT: `cell` holds the query pass's 8 group lines (query_ci_kernel's red8), zeroed here
+        if (SLOT && cell != nullptr && threadIdx.x < 256)
+            reinterpret_cast<unsigned long long*>(cell)[threadIdx.x] = 0ull;
         if (threadIdx.x == 0) {
             meta[kCiOk] = ok ? 1u : 0u;
             meta[kCiCells] = total;
@@ -2596,7 +2639,8 @@ template <typename LT>
 int launch_ci(const float* s, const LT* lab, int64_t begin, int64_t end, const CountWs& cw, const unsigned* sorted,
               int64_t M, unsigned long long* out, unsigned long long* nonfinite, hipStream_t st,
               unsigned* verdict = nullptr, const unsigned* grp = nullptr, const unsigned long long* Mp = nullptr,
-              unsigned* check = nullptr, const uint2* slot_counts = nullptr, unsigned slot_cells = 0u) {
+              unsigned* check = nullptr, const uint2* slot_counts = nullptr, unsigned slot_cells = 0u,
+              unsigned long long* red8 = nullptr) {
     const dim3 grid(query_grid(end - begin)), block(kQueryThreads);
     const size_t lds = (size_t(kCiTop) + kCiMaxBlocks) * 8 + (grp ? size_t(kDirectMaxGroups) * 4 : 0);
     bool sec = true;  // the carried secondary window (query_ci_kernel's SEC)
@@ -2619,18 +2663,18 @@ int launch_ci(const float* s, const LT* lab, int64_t begin, int64_t end, const C
                   "the count-index query's LDS");
     if (slot_counts != nullptr && check != nullptr && sec)
         hipLaunchKernelGGL((query_ci_kernel<LT, true, true, true>), grid, block, lds, st, s, lab, begin, end, cw.meta,
-                           cw.l1, slot_counts, sorted, M, out, nonfinite, verdict, nullptr, Mp, check, slot_cells);
+                           cw.l1, slot_counts, sorted, M, out, nonfinite, verdict, nullptr, Mp, check, slot_cells, red8);
     else if (slot_counts != nullptr && sec)
         hipLaunchKernelGGL((query_ci_kernel<LT, false, true, true>), grid, block, lds, st, s, lab, begin, end, cw.meta,
-                           cw.l1, slot_counts, sorted, M, out, nonfinite, verdict, nullptr, Mp, nullptr, slot_cells);
+                           cw.l1, slot_counts, sorted, M, out, nonfinite, verdict, nullptr, Mp, nullptr, slot_cells, red8);
 #ifdef DAUC_TUNING
     else if (slot_counts != nullptr && check != nullptr)
         hipLaunchKernelGGL((query_ci_kernel<LT, true, true, false>), grid, block, lds, st, s, lab, begin, end, cw.meta,
-                           cw.l1, slot_counts, sorted, M, out, nonfinite, verdict, nullptr, Mp, check, slot_cells);
+                           cw.l1, slot_counts, sorted, M, out, nonfinite, verdict, nullptr, Mp, check, slot_cells, red8);
     else if (slot_counts != nullptr)
         hipLaunchKernelGGL((query_ci_kernel<LT, false, true, false>), grid, block, lds, st, s, lab, begin, end,
                            cw.meta, cw.l1, slot_counts, sorted, M, out, nonfinite, verdict, nullptr, Mp, nullptr,
-                           slot_cells);
+                           slot_cells, red8);
 #endif
     else if (check != nullptr)
         hipLaunchKernelGGL((query_ci_kernel<LT, true>), grid, block, lds, st, s, lab, begin, end, cw.meta, cw.l1,
@@ -2910,7 +2954,7 @@ int counts_labeled_slotted(const SlotSource& src, unsigned* stab, int64_t Mcap, 
     const int64_t gk = gk0;
 #endif
     hipLaunchKernelGGL(direct_count_slots_kernel<true>, dim3(static_cast<unsigned>(gk)), dim3(kSlotCountThreads), 0,
-                       st, src, Mcap, nw.l1, nw.meta, nw.cstart, nullptr, nullptr, stab, cells);
+                       st, src, Mcap, nw.l1, nw.meta, nw.cstart, nw.first, nullptr, stab, cells);  // (SLOT: see above)
     int rc = launch_status();
     if (rc || end == begin) return rc;
     const unsigned long long* Mp = src.m_eff;
@@ -2918,13 +2962,16 @@ int counts_labeled_slotted(const SlotSource& src, unsigned* stab, int64_t Mcap, 
     switch (label_dtype) {
         case DAUC_LABEL_I8:
             return launch_ci(scores, static_cast<const int8_t*>(labels), begin, end, nw, stab, 0, wins_ties, nonfinite,
-                             st, verdict, nullptr, Mp, check, counts, cells);
+                             st, verdict, nullptr, Mp, check, counts, cells,
+                             reinterpret_cast<unsigned long long*>(nw.first));
         case DAUC_LABEL_I32:
             return launch_ci(scores, static_cast<const int32_t*>(labels), begin, end, nw, stab, 0, wins_ties, nonfinite,
-                             st, verdict, nullptr, Mp, check, counts, cells);
+                             st, verdict, nullptr, Mp, check, counts, cells,
+                             reinterpret_cast<unsigned long long*>(nw.first));
         default:
             return launch_ci(scores, static_cast<const int64_t*>(labels), begin, end, nw, stab, 0, wins_ties, nonfinite,
-                             st, verdict, nullptr, Mp, check, counts, cells);
+                             st, verdict, nullptr, Mp, check, counts, cells,
+                             reinterpret_cast<unsigned long long*>(nw.first));
     }
 }
 
