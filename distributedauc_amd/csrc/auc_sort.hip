@@ -971,6 +971,21 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
                                                                 unsigned* __restrict__ check, unsigned slot_cells = 0u,
                                                                 unsigned long long* __restrict__ red8 = nullptr) {
     const unsigned pad_word = 4u * slot_cells;  // SLOT: the all-+inf primary slot past the last cell
+    // SLOT: the index's loads (the l1 plan, the byte counts of every block the workspace holds) are
+    // issued BEFORE the meta words are read, so the prologue waits one round trip, not two (meta ->
+    // block count -> loads); blocks past the count are loaded and never stored
+    constexpr int kL1Per = kCiTop / kQueryThreads;                                 // 2
+    constexpr int kBlkPer = (kCiMaxBlocks + kQueryThreads - 1) / kQueryThreads;  // 18
+    uint2 pre_a[SLOT ? kL1Per : 1], pre_v[SLOT ? kBlkPer : 1];
+    if constexpr (SLOT) {
+#pragma unroll
+        for (int j = 0; j < kL1Per; ++j) pre_a[j] = l1g[j * kQueryThreads + threadIdx.x];
+#pragma unroll
+        for (int j = 0; j < kBlkPer; ++j) {
+            const int i = j * kQueryThreads + threadIdx.x;
+            pre_v[j] = i < kCiMaxBlocks ? blkg[i] : uint2{0u, 0u};
+        }
+    }
     const bool in_use = count_index_in_use(meta);
     if (Mp != nullptr) M = static_cast<int64_t>(*Mp);  // the direct build: the table size on the device
     if constexpr (SLOT) {
@@ -1030,20 +1045,25 @@ __global__ __launch_bounds__(kQueryThreads) void query_ci_kernel(const float* __
     {
         // the index into LDS with every load of a thread in flight before its first LDS store (a
         // load-store loop waits out one L2 round trip per iteration: 18 of them per thread)
-        constexpr int kL1Per = kCiTop / kQueryThreads;                                 // 2
-        constexpr int kBlkPer = (kCiMaxBlocks + kQueryThreads - 1) / kQueryThreads;  // 18
         uint2 a[kL1Per], v[kBlkPer];
-#pragma unroll
-        for (int j = 0; j < kL1Per; ++j) a[j] = l1g[j * kQueryThreads + threadIdx.x];
 #ifdef DAUC_TUNING
         const bool abl2 = SLOT && g_query_abl == 2;
 #else
         constexpr bool abl2 = false;
 #endif
+        if constexpr (SLOT) {  // (loaded above)
 #pragma unroll
-        for (int j = 0; j < kBlkPer; ++j) {
-            const int i = j * kQueryThreads + threadIdx.x;
-            v[j] = i < nb && !abl2 ? blkg[i] : uint2{0u, 0u};
+            for (int j = 0; j < kL1Per; ++j) a[j] = pre_a[j];
+#pragma unroll
+            for (int j = 0; j < kBlkPer; ++j) v[j] = abl2 ? uint2{0u, 0u} : pre_v[j];
+        } else {
+#pragma unroll
+            for (int j = 0; j < kL1Per; ++j) a[j] = l1g[j * kQueryThreads + threadIdx.x];
+#pragma unroll
+            for (int j = 0; j < kBlkPer; ++j) {
+                const int i = j * kQueryThreads + threadIdx.x;
+                v[j] = i < nb && !abl2 ? blkg[i] : uint2{0u, 0u};
+            }
         }
         if (grp != nullptr) {
             // the direct build's block words hold prefixes within groups of 256 blocks: add the groups'
