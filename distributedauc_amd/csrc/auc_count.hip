@@ -542,6 +542,11 @@ __global__ __launch_bounds__(kCmpThreads) void compact_write_kernel(
 // two-step evaluation's slot header length word). fill_w (nullable): the grid also fills nfill16
 // 16-byte words there with all-ones (the two-step's slotted table: +inf keys), by extra workgroups
 // past the tiles (blockIdx.x >= ntiles), which do only that and the zeroing.
+#ifdef DAUC_TUNING
+// tuning builds: DAUC_CMP_ABL = 1, a timing ablation of the tiles' reservation (WRONG output): every
+// tile writes from position 0 without its returning atomic on the one counter
+__device__ int g_cmp_abl = 0;
+#endif
 template <typename LT, int SLOTS, int THREADS = kCmpThreads, bool HIST = false>
 __global__ __launch_bounds__(THREADS) void compact_unordered_kernel(
     const float* __restrict__ s, const LT* __restrict__ lab, int64_t n, int vec, float* __restrict__ pos_out,
@@ -635,6 +640,10 @@ __global__ __launch_bounds__(THREADS) void compact_unordered_kernel(
 #pragma unroll
         for (int w = 0; w < kW; ++w) other += wtot[1][w];
         if (other) atomicAdd(stats + 3, static_cast<unsigned long long>(other));
+#ifdef DAUC_TUNING
+        if (g_cmp_abl == 1) base_s = 0ull;
+        else
+#endif
         base_s = tile ? atomicAdd(stats + 0, static_cast<unsigned long long>(tile)) : 0ull;
     }
     __syncthreads();
@@ -944,6 +953,16 @@ int compact_unordered(const float* scores, const void* labels, int label_dtype, 
     if (const char* e = getenv("DAUC_CMP_SLOTS");
         e && (atoi(e) == 8 || atoi(e) == 16 || atoi(e) == 32 || atoi(e) == 64))
         slots = atoi(e);
+#endif
+#ifdef DAUC_TUNING
+    {
+        static int abl = -1;
+        if (abl < 0) {
+            const char* e = getenv("DAUC_CMP_ABL");
+            abl = e ? atoi(e) : 0;
+            if (hipMemcpyToSymbol(HIP_SYMBOL(g_cmp_abl), &abl, sizeof(int)) != hipSuccess) return DAUC_EINVAL;
+        }
+    }
 #endif
     const int64_t tile = int64_t(threads) * 16 * slots;
     const int64_t nblk = (n + tile - 1) / tile;
