@@ -269,8 +269,8 @@ int dauc_auc_counts_sorted_labeled(const float* pos, int64_t P, const float* sco
 
 /*
  * The exact-AUC evaluation of main.py:79-81 (sklearn roc_curve + auc over one test set), as ONE
- * stream-ordered sequence with no host synchronisation and no allocation: two memsets (the
- * record, the workspace's top-bucket histogram), a one-pass positive compaction (labels read once, P counted on the device),
+ * stream-ordered sequence with no host synchronisation and no allocation: one zeroing launch (the
+ * record and the workspace's top-bucket histogram), a one-pass positive compaction (labels read once, P counted on the device),
  * the count index built straight from the unsorted positives with the table size read on the
  * device, and the query pass over this part's scores [part*n/parts, (part+1)*n/parts), whose
  * labels are not 1 (every part builds the index over ALL the positives itself: ranks holding the
