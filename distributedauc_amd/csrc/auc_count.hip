@@ -946,13 +946,25 @@ int compact_unordered(const float* scores, const void* labels, int label_dtype, 
     // wide inputs: 1024-thread workgroups of 32 label groups per thread (524,288-label tiles: 256
     // reservations at 2^27 instead of 1024 on the one counter address) -- 256
     constexpr int kWideThreads = 256;
-    const int threads = wide ? kWideThreads : kCmpThreads;
     int slots = wide ? 32 : kCmpSlots;
 #ifdef DAUC_TUNING
     // tuning builds: DAUC_CMP_SLOTS (8, 16, 32, 64) = label groups per thread whatever n
     if (const char* e = getenv("DAUC_CMP_SLOTS");
         e && (atoi(e) == 8 || atoi(e) == 16 || atoi(e) == 32 || atoi(e) == 64))
         slots = atoi(e);
+#endif
+    // round 6: 512-thread tiles (8 groups per thread, the histogram form) from 2^23 labels below the
+    // wide shape: half the tiles, so half the reservations on the one counter, which serialise
+    // (the two-step's 2^24-label slice: 512 -> 256 tiles, step 1 17.9 -> 14.9 us; the one-call
+    // evaluation of 2^24 labels 114.9 -> 110.1 us; the 2^21-label slice keeps 256: 12.2 vs 12.8 us)
+    constexpr int kMidThreads = 512;
+    const bool mid_ok = !wide && hist_out != nullptr && slots == kCmpSlots;
+    int threads = wide ? kWideThreads : mid_ok && n >= (int64_t(1) << 23) ? kMidThreads : kCmpThreads;
+#ifdef DAUC_TUNING
+    // tuning builds: DAUC_CMP_THREADS (256, 512, 1024) = threads per tile of that form whatever n
+    if (const char* e = getenv("DAUC_CMP_THREADS");
+        mid_ok && e && (atoi(e) == 256 || atoi(e) == 512 || atoi(e) == 1024))
+        threads = atoi(e);
 #endif
 #ifdef DAUC_TUNING
     {
@@ -986,7 +998,19 @@ int compact_unordered(const float* scores, const void* labels, int label_dtype, 
     uint4* fw = reinterpret_cast<uint4*>(fill_w);
     auto go = [&](auto* lab) {
         using LT = std::remove_const_t<std::remove_pointer_t<decltype(lab)>>;
+        if (mid_ok && threads == kMidThreads) {
+            hipLaunchKernelGGL((compact_unordered_kernel<LT, kCmpSlots, kMidThreads, true>), grid, block, 0, st, scores,
+                               lab, n, vec, pos_out, stats, tag, zero_next, next_tag, zero3, zero_w, nzero_w, cap,
+                               hist_out, put, put_val, fw, nfill, nblk);
+            return launch_status();
+        }
 #ifdef DAUC_TUNING
+        if (mid_ok && threads == 1024) {
+            hipLaunchKernelGGL((compact_unordered_kernel<LT, kCmpSlots, 1024, true>), grid, block, 0, st, scores, lab,
+                               n, vec, pos_out, stats, tag, zero_next, next_tag, zero3, zero_w, nzero_w, cap, hist_out,
+                               put, put_val, fw, nfill, nblk);
+            return launch_status();
+        }
         if (slots == 64) {
             if (hist_out != nullptr)
                 hipLaunchKernelGGL((compact_unordered_kernel<LT, 64, kCmpThreads, true>), grid, block, 0, st, scores,
