@@ -1,5 +1,5 @@
 #!/bin/bash
-# round 6 (end): kernel trace of one rank's two-step chain at G = 8 after the grouped reduction, the hoisted prologue loads and the zeroing launch, both sizes
+# round 6 (end): kernel trace of one rank's two-step chain at G = 8 with the shipped kernels (grouped reduction, hoisted prologue loads, zeroing launch, 512-thread compaction tiles), both sizes
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 O=gpurun_out/r06trace3
