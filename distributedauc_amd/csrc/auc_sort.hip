@@ -1772,14 +1772,22 @@ __global__ __launch_bounds__(kSlotCountThreads) void direct_count_slots_kernel(S
     }
     const bool over = hs[3] != 0ull;
     if (threadIdx.x == 0 && over) n0 += static_cast<unsigned>(mcap) + 1u;
-    unsigned used = (n0 != 0u) + (n1 != 0u);
-    used = block_incl_scan1024<false>(used, wtot);
-    if (threadIdx.x == kSlotCountThreads - 1) totals[0] = used;
-    const unsigned keys = block_incl_scan1024<false>(n0 + n1, wtot);
-    if (threadIdx.x == kSlotCountThreads - 1) totals[2] = keys;
+    // round 6: only the totals of the used buckets and of the keys are needed, not their scans: the
+    // used buckets by two ballots per wave and one LDS sum, and the keys = the slots' P (every
+    // positive is in its slot's histogram, stored or not; an overflow adds the past-capacity count,
+    // as the overflow bucket did, so the plan refuses the table) -- two workgroup scans fewer
+    {
+        const int wid = threadIdx.x / kWave;
+        const unsigned wu = static_cast<unsigned>(__popcll(__ballot(n0 != 0u)) + __popcll(__ballot(n1 != 0u)));
+        if (lane == 0) wtot[wid] = wu;
+    }
     __syncthreads();
-    const int64_t M = totals[2];
-    const int64_t avail = int64_t(kCiMaxCells) - int64_t(totals[0]);
+    unsigned used_total = 0u;
+#pragma unroll
+    for (int w = 0; w < kSlotCountThreads / kWave; ++w) used_total += wtot[w];
+    __syncthreads();  // (wtot is the next scan's)
+    const int64_t M = static_cast<int64_t>(hs[0]) + (over ? mcap + 1 : 0);
+    const int64_t avail = int64_t(kCiMaxCells) - int64_t(used_total);
     const int64_t num = avail < 2 * M ? avail : 2 * M;
     const unsigned C0 = n0 ? static_cast<unsigned>((int64_t(n0) * num + M - 1) / M) : 0u;
     const unsigned C1 = n1 ? static_cast<unsigned>((int64_t(n1) * num + M - 1) / M) : 0u;
