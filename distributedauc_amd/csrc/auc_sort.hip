@@ -1560,27 +1560,50 @@ __global__ __launch_bounds__(kDirectThreads) void direct_count_kernel(const floa
                                                                       unsigned* __restrict__ cnt,
                                                                       unsigned* __restrict__ cell,
                                                                       unsigned* __restrict__ stab = nullptr,
-                                                                      unsigned slot_cells = 0u) {
+                                                                      unsigned slot_cells = 0u,
+                                                                      const unsigned long long* __restrict__ Mp =
+                                                                          nullptr) {
     static_assert(kCiTop == 8 * kDirectThreads, "eight top buckets per thread");
     __shared__ uint2 l1[kCiTop];
     __shared__ unsigned wtot[kDirectThreads / kWave];
     __shared__ unsigned totals[3];
+    // Mp (round 6, the slotted one-call form): the compaction's P, which is the histogram's total
+    // (every positive is in it) -- loaded with the histogram, so only the used buckets are summed
+    // (eight ballots per wave, one LDS sum) and the plan needs one workgroup scan instead of three
+    const unsigned long long Mdev = Mp != nullptr ? *Mp : 0ull;
     const uint4 h0 = reinterpret_cast<const uint4*>(hist)[2 * threadIdx.x];
     const uint4 h1 = reinterpret_cast<const uint4*>(hist)[2 * threadIdx.x + 1];
     const unsigned n[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
-    unsigned used = 0u, keys = 0u;
+    int64_t M, used_total;
+    if (Mp != nullptr) {  // (uniform)
+        const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+        unsigned wu = 0u;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-        used += n[j] != 0u;
-        keys += n[j];
+        for (int j = 0; j < 8; ++j) wu += static_cast<unsigned>(__popcll(__ballot(n[j] != 0u)));
+        if (lane == 0) wtot[wid] = wu;
+        __syncthreads();
+        unsigned u = 0u;
+#pragma unroll
+        for (int w = 0; w < kDirectThreads / kWave; ++w) u += wtot[w];
+        __syncthreads();  // (wtot is the next scan's)
+        M = static_cast<int64_t>(Mdev);
+        used_total = u;
+    } else {
+        unsigned used = 0u, keys = 0u;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            used += n[j] != 0u;
+            keys += n[j];
+        }
+        used = block_incl_scan1024<false>(used, wtot);
+        if (threadIdx.x == kDirectThreads - 1) totals[0] = used;
+        keys = block_incl_scan1024<false>(keys, wtot);  // M = the histogram's total (< 2^32: M <= n / 2)
+        if (threadIdx.x == kDirectThreads - 1) totals[2] = keys;
+        __syncthreads();
+        M = totals[2];
+        used_total = totals[0];
     }
-    used = block_incl_scan1024<false>(used, wtot);
-    if (threadIdx.x == kDirectThreads - 1) totals[0] = used;
-    keys = block_incl_scan1024<false>(keys, wtot);  // M = the histogram's total (< 2^32: M <= n / 2)
-    if (threadIdx.x == kDirectThreads - 1) totals[2] = keys;
-    __syncthreads();
-    const int64_t M = totals[2];
-    const int64_t avail = int64_t(kCiMaxCells) - int64_t(totals[0]);
+    const int64_t avail = int64_t(kCiMaxCells) - used_total;
     const int64_t num = avail < 2 * M ? avail : 2 * M;
     unsigned C[8], csum = 0u;
 #pragma unroll
@@ -3019,7 +3042,7 @@ int counts_labeled_direct_slotted(const float* pos, const unsigned long long* Mp
     const int64_t gb = (Mcap + kDirectThreads - 1) / kDirectThreads;
     hipLaunchKernelGGL(direct_count_kernel<true>, dim3(static_cast<unsigned>(gb < kDirectGrid ? gb : kDirectGrid)),
                        dim3(kDirectThreads), 0, st, pos, Mcap, ready_hist, nw.l1, nw.meta, nw.cstart, nullptr, stab,
-                       cells);
+                       cells, Mp);
     int rc = launch_status();
     if (rc || end == begin) return rc;
     const uint2* counts = reinterpret_cast<const uint2*>(nw.cstart);
